@@ -1,0 +1,208 @@
+#!/usr/bin/env python3
+"""Headline benchmark: agent-env-steps/s of the vectorised grid-world step (BASELINE.json).
+
+A "step" = one batched CustomMAEnv.step (custom/ma_customenv.py:217-334) over every env of
+this rank: scripted policy + random RL policy drawn on device, FeAR counterfactuals
+(custom/Responsibility.py:135-210), world update, rewards, the rollout reward/score arithmetic
+(maddpg/agent.py:124-173), auto-reset, float32 observations for every RL agent and the
+per-block statistics; with --gpus N > 1 also the per-step RCCL reduction of those statistics
+(episode returns) across ranks.  Inputs are resident in HBM before the timed region.
+
+Default workload = BASELINE config 3 (the north-star shape): 4-agent 32x32 grid, 65536 envs
+per GPU, FeAR on with weight -5 (configs/custom_fear_5.yaml).  value = all ranks' envs x N
+agents x steps / max-over-ranks wall time.
+
+  python bench.py [--gpus N --steps K --warmup W] [--config c3|c2|c4|c1] [--no-cpu-baseline]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "marl-responsible-nav_amd")
+for _p in (REPO, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+METRIC = "agent-env-steps/sec at 64k envs × 4 agents, 1/2/4/8 MI355X; HBM BW fraction"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+CONFIGS = {
+    "c3": dict(scenario="grid32", envs=65536, fear=True, fear_weight=-5.0,
+               workload="BASELINE config 3: 4-agent (2 RL) 32x32 Level-3-like grid, 65536 envs/GPU, "
+                        "FeAR on (weight -5, configs/custom_fear_5.yaml), random RL policy"),
+    "c2": dict(scenario="grid32", envs=4096, fear=False, fear_weight=-2.0,
+               workload="BASELINE config 2: 4-agent 32x32 grid, 4096 envs, MLP obs, FeAR off"),
+    "c4": dict(scenario="grid64_n8", envs=65536, fear=False, fear_weight=-5.0,
+               workload="BASELINE config 4: 8-agent 64x64 grid, 65536 envs, FeAR off"),
+    "c4f": dict(scenario="grid64_n8", envs=65536, fear=True, fear_weight=-5.0,
+                workload="8-agent 64x64 grid, 65536 envs, FeAR on"),
+    "c1": dict(scenario="level3", envs=1, fear=False, fear_weight=-2.0,
+               workload="BASELINE config 1: Level 3 (10x16), 1 env, random policy"),
+}
+
+
+def algorithmic_bytes(N: int, K: int, HW: int):
+    """Bytes per env-step each kernel must move at minimum:
+    step_kernel: state read+write (pos 4N, flags 4, t 4, prev 4K, score 8, fear_score 8; x2)
+                 + episode 4 read + outputs (reward/fear/shaped 24K, term/trunc 2K, mask 2K,
+                 done 1, crashes 4, apples 4, ep_return 8, ep_fear 8, ep_len 4)
+                 + obs descriptor 20 written;
+    obs_kernel:  obs 4*K*HW written + descriptor 20 read."""
+    state = 2 * (4 * N + 4 + 4 + 4 * K + 8 + 8) + 4
+    outputs = 24 * K + 2 * K + 2 * K + 1 + 4 + 4 + 8 + 8 + 4
+    step_b = state + outputs + 20
+    obs_b = 4 * K * HW + 20
+    return step_b, obs_b
+
+
+def cpu_baseline(cfg, seconds: float = 12.0):
+    """The C restatement (oracle/, test infrastructure) on the host cores: same scenario,
+    same step semantics, native-RNG mode, OpenMP over envs.  Bounded sample."""
+    import numpy as np
+    from marlnav import scenario as S
+    from oracle import oracle as O
+
+    sc = S.builtin(cfg["scenario"])
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    threads = max(1, min(threads, 16))
+    E = 4096 if cfg["fear"] else 16384
+    orc = O.OracleEnvs(sc, E, fear=cfg["fear"], fear_weight=cfg["fear_weight"], seed=42, reset=False)
+    obs = np.zeros((sc.K, E, sc.HW), np.float32)
+    orc.reset_all(obs=obs, nthreads=threads)
+    orc.vec_step(None, obs=obs, nthreads=threads)  # warm
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        orc.vec_step(None, obs=obs, nthreads=threads)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or steps >= 2000:
+            break
+    value = E * sc.N * steps / el
+    return {"value": value, "unit": "agent-env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{E} envs x {steps} steps of {cfg['scenario']} (fear={'on' if cfg['fear'] else 'off'}, "
+                      f"obs written) in {el:.1f}s by oracle/gw_oracle.c (bit-exact C restatement of the "
+                      f"reference step), {threads} OpenMP threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--envs", type=int, default=0, help="override envs per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from marlnav.vec_env import VecGridEnv
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    cfg = dict(CONFIGS[args.config])
+    if args.envs:
+        cfg["envs"] = args.envs
+    E = cfg["envs"]
+    env = VecGridEnv(cfg["scenario"], num_envs=E, fear=cfg["fear"], fear_weight=cfg["fear_weight"],
+                     max_steps=150, auto_reset=True, seed=42, env_offset=rank * E, stats=True)
+    N, K, HW = env.N, env.K, env.H * env.W
+    stream = torch.cuda.current_stream()
+    stats_acc = torch.zeros_like(env.out["stats"][0])
+
+    def one_step(i):
+        r = env.step()
+        if world > 1:
+            # per-step RCCL reduction of the episode-return statistics across the shards
+            dist.all_reduce(r.stats, op=dist.ReduceOp.SUM)
+        return r
+
+    env.reset()
+    for i in range(args.warmup):
+        one_step(i)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+    env.profile(True)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for i in range(args.steps):
+        r = one_step(i)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    env.profile(False)
+    (ms_step, ms_obs), nprof = env.profile_read()
+    gpu_ms = ev0.elapsed_time(ev1)
+
+    t_local = torch.tensor([wall], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t_local, op=dist.ReduceOp.MAX)
+    t_max = float(t_local.item())
+    stats = r.stats.sum(0).cpu().tolist()
+
+    if rank == 0:
+        step_b, obs_b = algorithmic_bytes(N, K, HW)
+        avg_step_ms, avg_obs_ms = ms_step / max(nprof, 1), ms_obs / max(nprof, 1)
+        if avg_obs_ms >= avg_step_ms:
+            dom, bytes_per_launch, dur = "obs_kernel", obs_b * E, avg_obs_ms
+        else:
+            dom, bytes_per_launch, dur = "step_kernel", step_b * E, avg_step_ms
+        achieved = bytes_per_launch / (dur * 1e-3) / 1e9
+        total_units = world * E * N * args.steps
+        line = {
+            "metric": METRIC,
+            "value": total_units / t_max,
+            "unit": "agent-env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": t_max * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic (device Philox spawns / scripted policy / random RL policy)",
+            "config": {"workload": cfg["workload"], "scenario": cfg["scenario"], "envs_per_gpu": E,
+                       "global_envs": world * E, "agents": N, "rl_agents": K, "grid": [env.H, env.W],
+                       "fear": cfg["fear"], "parallelism": f"env-sharded dp{world}"},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "bytes_per_launch": bytes_per_launch, "avg_launch_ms": dur},
+            "kernels_ms": {"step_kernel": avg_step_ms, "obs_kernel": avg_obs_ms,
+                           "stream_ms_per_step": gpu_ms / args.steps},
+            "last_step_episodes": {"completed": stats[1], "mean_return": stats[0] / max(stats[1], 1.0),
+                         "mean_len": stats[6] / max(stats[1], 1.0)},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,152 @@
+/*
+ * gridenv.h — C ABI of the MI355X-native vectorised grid world (libgridenv.so).
+ *
+ * Drop-in boundary for the reference's hot path (Henweiz/MARL-Responsible-Nav):
+ *   CustomMAEnv.__init__/reset/step   custom/ma_customenv.py:74-108, 169-215, 217-334
+ *   GWorld.UpdateGWorld               custom/grid_world.py:424-563
+ *   Responsibility.FeAR_4_one_actor   custom/Responsibility.py:135-210
+ *   MADDPGAgent.train per-step reward/score arithmetic   maddpg/agent.py:120-173, 226-243
+ * The reference has no FFI of its own (pure Python); these entry points are what its
+ * PettingZoo surface binds to through the ctypes layer in marlnav/_lib.py.
+ *
+ * One handle = E independent envs resident in HBM (structure of arrays).  All device
+ * pointers are plain HIP device addresses (e.g. torch.Tensor.data_ptr()); `stream` is a
+ * hipStream_t passed as void*.  Calls only enqueue work on `stream`; there is no implicit
+ * host synchronisation.  Statuses are negative on error; gw_last_error() explains.
+ * Layout: obs are agent-major [K][E][H*W] float32 (each RL agent's actor reads one
+ * contiguous [E, H*W] matrix); per-env per-agent outputs are [E][K].
+ */
+#ifndef GRIDENV_H
+#define GRIDENV_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GW_MAX_AGENTS 8
+#define GW_N_ACTIONS 9
+
+typedef enum gw_status {
+    GW_OK = 0,
+    GW_ERR_ARG = -1,    /* invalid argument / scenario                        */
+    GW_ERR_HIP = -2,    /* HIP runtime error                                  */
+    GW_ERR_ALLOC = -3,  /* device allocation failed                           */
+    GW_ERR_STATE = -4   /* call order (e.g. gw_step before the first reset)   */
+} gw_status;
+
+/* Static scenario tables (host pointers, copied by gw_create).
+ * Replaces LoadJsonScenario + CustomMAEnv.setup_env's map build
+ * (custom/grid_world.py:621-674, custom/ma_customenv.py:338-365, 422). */
+typedef struct gw_scenario {
+    int32_t H, W;               /* grid rows, columns (H*W <= 4096, W >= 2)             */
+    const uint8_t *region;      /* [H*W] 1 active road, 0 inactive                      */
+    const uint8_t *policy_id;   /* [H*W] policy index                                   */
+    int32_t n_policies;
+    const double *policy_cdf;   /* [n_policies][2][9] choice CDFs; [.][1] = the 25 %
+                                   uniform-direction branch (ma_customenv.py:441-443)   */
+    const uint8_t *mdr;         /* [H*W] MdR action per cell                            */
+    const int32_t *apples;      /* [K] apple cell of RL agent k                         */
+} gw_scenario;
+
+typedef struct gw_config {
+    int32_t N;                  /* world agents  (Scenario N_Agents)          1..8      */
+    int32_t K;                  /* RL agents     (N_INTELLIGENT_AGENTS)       1..N      */
+    int64_t num_envs;           /* E, envs owned by this handle                          */
+    int64_t env_offset;         /* global id of local env 0 (RNG counter; sharding)      */
+    int32_t fear;               /* CustomMAEnv(fear=...)                                 */
+    double fear_weight;         /* INIT_HP["FeAR_weight"] (maddpg/agent.py:125)          */
+    int32_t max_steps;          /* TRAIN_STEPS episode cap; 0 = none                     */
+    int32_t auto_reset;         /* reset done envs inside gw_step                        */
+    uint64_t seed;              /* Philox key (spawns, scripted policy, random RL policy)*/
+} gw_config;
+
+/* Per-step outputs: device pointers, any may be NULL (not written). */
+typedef struct gw_step_out {
+    float *obs;          /* [K][E][H*W] obs after the step (reset obs if auto-reset)  */
+    float *final_obs;    /* [K][E][H*W] terminal obs; rows written only for done envs */
+    double *reward;      /* [E][K] env reward                (ma_customenv.py:258-302) */
+    double *fear;        /* [E][K] info["fear"]              (ma_customenv.py:245-252) */
+    double *shaped;      /* [E][K] FeAR_weight*FeAR + reward (maddpg/agent.py:130)     */
+    uint8_t *term;       /* [E][K] terminations                                         */
+    uint8_t *trunc;      /* [E][K] truncations                                          */
+    uint8_t *done;       /* [E]   all(term) | all(trunc) | t >= max_steps               */
+    uint16_t *mask;      /* [E][K] 9-bit action mask of the returned obs                */
+    int32_t *crashes;    /* [E]   info["agent_crashes"]                                 */
+    int32_t *apples;     /* [E]   info["apples_caught"]                                 */
+    double *ep_return;   /* [E]   episode score incl. this step (maddpg/agent.py:173)   */
+    double *ep_fear;     /* [E]   episode fear_score (maddpg/agent.py:141)              */
+    int32_t *ep_len;     /* [E]   steps in the episode incl. this one                   */
+    int32_t *actions;    /* [E][N] joint action applied (env.Action4Agents)             */
+    int32_t *mdr;        /* [E][N] MdR4Agents                                           */
+    int32_t *final_pos;  /* [E][N] positions after the move, before any auto-reset      */
+    uint8_t *crash_bits; /* [E]   bit n: agent n crashed (UpdateGWorld agent_crashes)   */
+    uint8_t *restr_bits; /* [E]   bit n: restricted move                                */
+    double *stats;       /* [gw_stats_rows()][GW_STATS] per-block partial sums of this step:
+                            completed-episode returns, episodes completed, FeAR, crashes,
+                            apples caught, shaped rewards, completed-episode lengths, envs.
+                            Deterministic (fixed reduction tree); fed to the RCCL
+                            reduction of the multi-GPU rollout.                          */
+} gw_step_out;
+
+#define GW_STATS 8
+
+/* Env state (device arrays owned by the handle), structure of arrays. */
+typedef struct gw_state {
+    int32_t *pos;        /* [N][E] cell r*W+c of agent n            (World.AgentLocations) */
+    uint32_t *flags;     /* [E] bits 0-7 apples present, 8-15 terminations, 16-23 truncations */
+    int32_t *t;          /* [E] moves in the episode                 (num_moves)          */
+    uint32_t *episode;   /* [E] episode counter (RNG)                                     */
+    int32_t *prev_dist;  /* [K][E] previous distance to own apple, -1 = None              */
+    double *score;       /* [E] running episode score                                     */
+    double *fear_score;  /* [E] running episode fear score                                */
+} gw_state;
+
+/* CustomMAEnv(render=False, fear=cfg->fear, seed=cfg->seed) x E  (ma_customenv.py:74-108).
+ * Allocates the state on `device`.  The envs are unusable until gw_reset. */
+gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, void **out_env);
+
+/* CustomMAEnv.reset (ma_customenv.py:169-215) for every env with env_mask[e] != 0
+ * (env_mask NULL = all).  spawn_cells: [E][N] sorted road cells (replay) or NULL (Philox
+ * spawn).  obs [K][E][H*W] and mask [E][K] are written for the reset envs (either may be
+ * NULL). */
+gw_status gw_reset(void *env, const uint8_t *env_mask, const int32_t *spawn_cells, float *obs,
+                   uint16_t *mask, void *stream);
+
+/* CustomMAEnv.step (ma_customenv.py:217-334) on all E envs at once.
+ *   rl_actions [E][K] int32 in 0..8, or NULL = uniform random RL policy (Philox)
+ *   scripted   [E][N-K] int32 actions of the scripted agents (replay), or NULL = the
+ *              scenario policy sampled on device (ma_customenv.py:432-452)
+ *   spawn      [E][N] spawn cells for envs that auto-reset (replay), or NULL = Philox */
+gw_status gw_step(void *env, const int32_t *rl_actions, const int32_t *scripted,
+                  const int32_t *spawn, const gw_step_out *out, void *stream);
+
+/* Device pointers of the state arrays (valid until gw_destroy). */
+gw_status gw_state_view(void *env, gw_state *out);
+
+/* Copy the whole state to (to_env = 0) or from (to_env = 1) caller buffers with the
+ * gw_state layout (device or pinned host memory), enqueued on stream. */
+gw_status gw_copy_state(void *env, const gw_state *buf, int to_env, void *stream);
+
+/* Per-launch timing: while enabled, gw_step records HIP events on its stream around each of
+ * its two kernels (step_kernel, obs_kernel).  gw_profile_read synchronises on those events,
+ * returns the summed elapsed milliseconds per kernel and the number of gw_step calls timed,
+ * and clears them.  Used by bench.py for the live roofline. */
+gw_status gw_profile(void *env, int enable);
+gw_status gw_profile_read(void *env, double out_ms[2], int64_t *n_steps);
+
+/* Rows of the gw_step_out.stats buffer (one per step_kernel block). */
+int64_t gw_stats_rows(void *env);
+
+/* Sizes: H, W, N, K, E (out[0..4]). */
+gw_status gw_dims(void *env, int64_t out[5]);
+
+/* Thread-local description of the last error. */
+const char *gw_last_error(void);
+
+void gw_destroy(void *env);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GRIDENV_H */

@@ -1,0 +1,1362 @@
+// gridenv.hip — MI355X (gfx950) implementation of the vectorised grid world behind
+// include/gridenv.h.
+//
+// Per gw_step, two launches on the caller's stream:
+//   1. step_kernel   — everything that is per env: scripted policy (Philox), RL override,
+//                      the FeAR counterfactual sims (custom/Responsibility.py:135-210), the
+//                      world update (custom/grid_world.py:424-563), rewards/dones
+//                      (custom/ma_customenv.py:258-302), the rollout arithmetic
+//                      (maddpg/agent.py:124-173), auto-reset and a 48-byte obs descriptor.
+//                      Integer/VALU work; with fear on, one block owns BE envs, turns their
+//                      counterfactuals into a de-duplicated task list in LDS and lets all
+//                      256 lanes run one sim each (no lane idles on a far agent).
+//   2. obs_kernel    — writes the K x H*W float32 observation of every env
+//                      (custom/ma_customenv.py:303-322) from the descriptors: a pure HBM
+//                      store stream, 16 B per lane, coalesced, static map staged in LDS.
+// Everything is exact integer logic; the only floating point is the f64 reward arithmetic,
+// compiled with -ffp-contract=off and written with explicit _rn intrinsics in the order
+// numpy/Python evaluate it.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "gridenv.h"
+
+namespace gw {
+
+constexpr int NA = GW_N_ACTIONS;
+constexpr int MAXN = GW_MAX_AGENTS;
+constexpr int NDESC = 12;  // u32 words per obs descriptor
+
+// desc[4] flag bits
+constexpr uint32_t D_RESET = 1u;      // obs uses the reset encoding (0.5 agents, no relabel)
+constexpr uint32_t D_WRITE = 2u;      // write obs for this env
+constexpr uint32_t D_FINAL = 4u;      // write final_obs for this env (terminal encoding)
+
+struct Tables {
+    const uint8_t *okmask;    // [HW] bit d: unit move d (0 U,1 D,2 L,3 R) allowed
+    const uint8_t *policy;    // [HW]
+    const double *cdf;        // [P][2][9]
+    const uint8_t *mdr;       // [HW]
+    const uint16_t *amask;    // [HW]
+    const int32_t *free_cells;// [F]
+    const float *base;        // [HW] 0 road / -1 inactive
+    const double *resp;       // [10][10] clip((vm-va)/(vm+EPS),-1,1)
+};
+
+struct State {
+    int32_t *pos;
+    uint32_t *flags;
+    int32_t *t;
+    uint32_t *episode;
+    int32_t *prev;
+    double *score;
+    double *fscore;
+};
+
+struct Params {
+    Tables tb;
+    State st;
+    gw_step_out out;
+    uint32_t *desc;           // [E][NDESC]
+    const int32_t *rl;        // [E][K] or null
+    const int32_t *scripted;  // [E][N-K] or null
+    const int32_t *spawn;     // [E][N] or null
+    const uint8_t *rmask;     // reset mask or null
+    int64_t E, env_offset;
+    double fear_weight;
+    int H, W, HW, N, K, F;
+    int max_steps, auto_reset;
+    uint32_t key0, key1;
+    uint32_t w_magic;         // ceil(2^32 / W)  (exact /W for cells < 2^16)
+    int apples[MAXN];
+};
+
+// ---------------------------------------------------------------------------------------
+// Philox4x32-10 (counter-based; every draw is keyed by global env id, episode, step, tag)
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                        uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        if (r > 0) {
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    }
+    return make_uint4(c0, c1, c2, c3);
+}
+
+__device__ __forceinline__ int div_w(const Params &p, int cell) {
+    return (int)__umulhi((uint32_t)cell, p.w_magic);
+}
+
+__device__ __forceinline__ int manhattan(const Params &p, int a, int b) {
+    const int ra = div_w(p, a), rb = div_w(p, b);
+    const int ca = a - ra * p.W, cb = b - rb * p.W;
+    return abs(ra - rb) + abs(ca - cb);
+}
+
+// ---------------------------------------------------------------------------------------
+// One world update (GWorld.UpdateGWorld, custom/grid_world.py:424-563) in registers.
+// Floor/ceil sub-path indices of (s+1)*len/4 and the overhang terms are compile-time per
+// (len, s): len 1 -> f {0,0,0,1} c {1,1,1,1}; len 2 -> f {0,1,1,2} c {1,1,2,2}.
+// ---------------------------------------------------------------------------------------
+template <int S> struct SubStep;
+template <> struct SubStep<0> { static constexpr int f1 = 0, c1 = 1, f2 = 0, c2 = 1, ohf1 = 3, ohc1 = 1, ohf2 = 2, ohc2 = 2; };
+template <> struct SubStep<1> { static constexpr int f1 = 0, c1 = 1, f2 = 1, c2 = 1, ohf1 = 2, ohc1 = 2, ohf2 = 0, ohc2 = 0; };
+template <> struct SubStep<2> { static constexpr int f1 = 0, c1 = 1, f2 = 1, c2 = 2, ohf1 = 1, ohc1 = 3, ohf2 = 2, ohc2 = 2; };
+template <> struct SubStep<3> { static constexpr int f1 = 1, c1 = 1, f2 = 2, c2 = 2, ohf1 = 0, ohc1 = 0, ohf2 = 0, ohc2 = 0; };
+
+template <int N>
+struct World {
+    int nal[N][5];
+    int loc[N];
+    int delta[N];
+    uint32_t two, mv, dir0, dir1;   // bit masks: 2-step action, moving action, direction bits
+    uint32_t crash, restr;
+
+    __device__ __forceinline__ void init(const int (&l)[N], const int (&a)[N], int W) {
+        two = mv = dir0 = dir1 = crash = restr = 0;
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            loc[i] = l[i];
+            nal[i][0] = l[i];
+            const int act = a[i];
+            const int d = (act - 1) & 3;  // 0 U, 1 D, 2 L, 3 R
+            two |= (uint32_t)(act >= 5) << i;
+            mv |= (uint32_t)(act != 0) << i;
+            dir0 |= (uint32_t)(d & 1) << i;
+            dir1 |= (uint32_t)(d >> 1) << i;
+            delta[i] = (d == 0) ? -W : (d == 1) ? W : (d == 2) ? -1 : 1;
+        }
+    }
+
+    __device__ __forceinline__ int dir_of(int i) const {
+        return (int)(((dir0 >> i) & 1u) | (((dir1 >> i) & 1u) << 1));
+    }
+
+    // values, not a conditional lvalue: a select between two element addresses would keep
+    // the sub-paths in scratch instead of registers
+    template <int S>
+    __device__ __forceinline__ int fl(int i) const {
+        const int a2 = nal[i][SubStep<S>::f2], a1 = nal[i][SubStep<S>::f1];
+        return ((two >> i) & 1u) ? a2 : a1;
+    }
+    template <int S>
+    __device__ __forceinline__ int ce(int i) const {
+        const int a2 = nal[i][SubStep<S>::c2], a1 = nal[i][SubStep<S>::c1];
+        return ((two >> i) & 1u) ? a2 : a1;
+    }
+
+    template <int S>
+    __device__ __forceinline__ void move(const uint8_t *__restrict__ okm) {  // :462-518
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            const int old = nal[i][S];
+            int nw = old;
+            const bool active_sub = (S == 0) || (S == 1 && ((two >> i) & 1u));
+            const bool moving = active_sub && ((mv >> i) & 1u) && !((crash >> i) & 1u);
+            if (moving) {
+                const bool ok = (okm[old] >> dir_of(i)) & 1u;
+                nw = ok ? old + delta[i] : old;
+                restr |= (uint32_t)(!ok) << i;
+            }
+            nal[i][S + 1] = nw;
+        }
+    }
+
+    template <int S>
+    __device__ __forceinline__ void resolve() {  // collision_checks_and_resolution :233-405
+        for (int pass = 0; pass < 2 * N; ++pass) {
+            uint32_t hit = 0;
+            int cnt = 0;
+#pragma unroll
+            for (int ii = 0; ii < N - 1; ++ii) {
+                const int Af = fl<S>(ii), Ac = ce<S>(ii);
+                const bool t_i = (two >> ii) & 1u;
+                const int ohf_i = t_i ? SubStep<S>::ohf2 : SubStep<S>::ohf1;
+                const int ohc_i = t_i ? SubStep<S>::ohc2 : SubStep<S>::ohc1;
+#pragma unroll
+                for (int jj = ii + 1; jj < N; ++jj) {
+                    const int Bf = fl<S>(jj), Bc = ce<S>(jj);
+                    const bool t_j = (two >> jj) & 1u;
+                    const int ohf_j = t_j ? SubStep<S>::ohf2 : SubStep<S>::ohf1;
+                    const int ohc_j = t_j ? SubStep<S>::ohc2 : SubStep<S>::ohc1;
+                    const bool same_dir = (Ac - Af) == (Bc - Bf);
+                    bool coll;
+                    if (Af == Bf || Ac == Bc) {
+                        coll = true;                                    // :276-278
+                    } else if (Af == Bc && Ac == Bf) {
+                        coll = true;                                    // :291-294
+                    } else if (Af == Bc) {
+                        coll = !((ohf_i + ohc_j) <= 4 && same_dir);     // :307-337
+                    } else if (Ac == Bf) {
+                        coll = !((ohf_j + ohc_i) <= 4 && same_dir);     // :339-368
+                    } else {
+                        const int Li = loc[ii], Lj = loc[jj];           // :371-378
+                        coll = (Af == Lj && Li == Bf) || (Ac == Lj && Li == Bc) ||
+                               (Af == Lj && Li == Bc) || (Ac == Lj && Li == Bf);
+                    }
+                    if (coll) {
+                        ++cnt;
+                        hit |= (1u << ii) | (1u << jj);
+                    }
+                }
+            }
+            crash |= hit;
+            // revertStepsWithCollisions :190-209 (all crashed agents, every pass)
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                if ((crash >> i) & 1u) {
+                    const int f = ((two >> i) & 1u) ? SubStep<S>::f2 : SubStep<S>::f1;
+#pragma unroll
+                    for (int k = 0; k <= S + 1; ++k)
+                        if (k >= f) nal[i][k] = loc[i];
+                }
+            }
+            if (cnt == 0) break;
+        }
+    }
+
+    template <int S>
+    __device__ __forceinline__ int cf(int i) const {  // NewAgentLocations_CurrentFloor
+        return (N == 1) ? loc[i] : fl<S>(i);
+    }
+};
+
+template <int N, bool APPLES>
+__device__ __forceinline__ void simulate(World<N> &w, const uint8_t *__restrict__ okm, int K,
+                                         const int (&apple)[MAXN], uint32_t &caught, int (&fin)[N]) {
+    caught = 0;
+    w.template move<0>(okm);
+    w.template resolve<0>();
+    if (APPLES) {
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+            if (k < K && w.template cf<0>(k) == apple[k]) caught |= 1u << k;
+    }
+    w.template move<1>(okm);
+    w.template resolve<1>();
+    if (APPLES) {
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+            if (k < K && w.template cf<1>(k) == apple[k]) caught |= 1u << k;
+    }
+    w.template move<2>(okm);
+    w.template resolve<2>();
+    if (APPLES) {
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+            if (k < K && w.template cf<2>(k) == apple[k]) caught |= 1u << k;
+    }
+    w.template move<3>(okm);
+    w.template resolve<3>();
+#pragma unroll
+    for (int i = 0; i < N; ++i) fin[i] = w.template cf<3>(i);
+    if (APPLES) {
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+            if (k < K && fin[k] == apple[k]) caught |= 1u << k;
+    }
+}
+
+// numpy float64 sum (0.0 + pairwise_sum) of an N*N matrix whose only non-zero row is `row`
+// (np.sum(FeAR_vals), custom/ma_customenv.py:252).  Zeros never change a partial sum here
+// (no -0.0 can occur), so only the row's terms are accumulated, in numpy's order.
+template <int N>
+__device__ __forceinline__ double np_sum_row(const double (&v)[N], int row) {
+    constexpr int n = N * N;
+    if (n < 8) {
+        double res = 0.0;
+#pragma unroll
+        for (int j = 0; j < N; ++j) res = __dadd_rn(res, v[j]);
+        return __dadd_rn(0.0, res);
+    } else {
+        static_assert(N * N <= 128, "N <= 11");
+        double r[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) r[q] = 0.0;
+        constexpr int main_end = n - (n % 8);
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            const int idx = row * N + j;
+            if (idx < main_end) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    if ((idx & 7) == q) r[q] = __dadd_rn(r[q], v[j]);
+            }
+        }
+        double res = __dadd_rn(__dadd_rn(__dadd_rn(r[0], r[1]), __dadd_rn(r[2], r[3])),
+                               __dadd_rn(__dadd_rn(r[4], r[5]), __dadd_rn(r[6], r[7])));
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            const int idx = row * N + j;
+            if (idx >= main_end) res = __dadd_rn(res, v[j]);
+        }
+        return __dadd_rn(0.0, res);
+    }
+}
+
+// numpy sum of a short 1-D f64 vector (n <= 8): scores += np.sum(rewards) (agent.py:173).
+__device__ __forceinline__ double np_sum_small(const double (&a)[MAXN], int n) {
+    if (n < 8) {
+        double res = 0.0;
+#pragma unroll
+        for (int i = 0; i < MAXN; ++i)
+            if (i < n) res = __dadd_rn(res, a[i]);
+        return __dadd_rn(0.0, res);
+    }
+    double res = __dadd_rn(__dadd_rn(__dadd_rn(a[0], a[1]), __dadd_rn(a[2], a[3])),
+                           __dadd_rn(__dadd_rn(a[4], a[5]), __dadd_rn(a[6], a[7])));
+    return __dadd_rn(0.0, res);
+}
+
+// ---------------------------------------------------------------------------------------
+// per-env helpers
+// ---------------------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ void load_state(const Params &p, int64_t e, int (&pos)[N]) {
+#pragma unroll
+    for (int n = 0; n < N; ++n) pos[n] = p.st.pos[(int64_t)n * p.E + e];
+}
+
+// setup_step (ma_customenv.py:432-452) + the RL override (:239-242)
+template <int N>
+__device__ __forceinline__ void select_actions(const Params &p, int64_t e, uint32_t episode, int t,
+                                               const int (&pos)[N], int (&act)[N]) {
+    const uint32_t gid = (uint32_t)(p.env_offset + e);
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+        if (n < p.K) {
+            if (p.rl) {
+                act[n] = p.rl[e * p.K + n];
+            } else {
+                const uint4 r = philox(gid, episode, (uint32_t)t, (2u << 24) | (uint32_t)n, p.key0, p.key1);
+                act[n] = (int)(((uint64_t)r.x * 9u) >> 32);
+            }
+        } else if (p.scripted) {
+            act[n] = p.scripted[e * (p.N - p.K) + (n - p.K)];
+        } else {
+            const uint4 r = philox(gid, episode, (uint32_t)t, (1u << 24) | (uint32_t)n, p.key0, p.key1);
+            const int uni = r.x < 0x40000000u;  // random.random() < 0.25 (:441)
+            const double u = ((double)(r.y >> 5) * 67108864.0 + (double)(r.z >> 6)) * (1.0 / 9007199254740992.0);
+            const double *cdf = p.tb.cdf + ((int)p.tb.policy[pos[n]] * 2 + uni) * NA;
+            int a = NA - 1;
+#pragma unroll
+            for (int q = NA - 2; q >= 0; --q)
+                if (u < cdf[q]) a = q;  // searchsorted(cdf, u, 'right')
+            act[n] = a;
+        }
+        act[n] = ((unsigned)act[n] < (unsigned)NA) ? act[n] : 0;
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void spawn_cells(const Params &p, int64_t e, uint32_t episode, int (&pos)[N]) {
+    if (p.spawn) {
+#pragma unroll
+        for (int n = 0; n < N; ++n) pos[n] = p.spawn[e * N + n];
+        return;
+    }
+    // Floyd's uniform N-subset of the road cells, then sorted (ma_customenv.py:373-380).
+    const uint32_t gid = (uint32_t)(p.env_offset + e);
+    int S[N];
+    uint4 r = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int d = 0; d < N; ++d) {
+        if ((d & 3) == 0) r = philox(gid, episode, 0xFFFFFFFFu, (3u << 24) | (uint32_t)(d >> 2), p.key0, p.key1);
+        const uint32_t word = ((d & 3) == 0) ? r.x : ((d & 3) == 1) ? r.y : ((d & 3) == 2) ? r.z : r.w;
+        const uint32_t j = (uint32_t)(p.F - N + d);
+        const int cand = (int)(((uint64_t)word * (uint64_t)(j + 1)) >> 32);
+        bool dup = false;
+#pragma unroll
+        for (int q = 0; q < d; ++q) dup |= (S[q] == cand);
+        S[d] = dup ? (int)j : cand;
+    }
+    // sorting network (insertion, unrolled)
+#pragma unroll
+    for (int a = 1; a < N; ++a) {
+#pragma unroll
+        for (int b = a; b > 0; --b) {
+            const int x = S[b - 1], y = S[b];
+            S[b - 1] = min(x, y);
+            S[b] = max(x, y);
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < N; ++n) pos[n] = p.tb.free_cells[S[n]];
+}
+
+__device__ __forceinline__ uint32_t all_bits(int K) { return (K >= 32) ? 0xFFFFFFFFu : ((1u << K) - 1u); }
+
+template <int N>
+__device__ __forceinline__ void write_desc_pos(uint32_t *d, const int (&pos)[N]) {
+    uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int n = 0; n < N; ++n) w[n >> 1] |= ((uint32_t)pos[n] & 0xFFFFu) << (16 * (n & 1));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) d[q] = w[q];
+}
+
+template <int N>
+__device__ __forceinline__ void reset_env(const Params &p, int64_t e, uint32_t episode, int (&pos)[N]) {
+    spawn_cells<N>(p, e, episode, pos);
+#pragma unroll
+    for (int n = 0; n < N; ++n) p.st.pos[(int64_t)n * p.E + e] = pos[n];
+    p.st.flags[e] = all_bits(p.K);
+    p.st.t[e] = 0;
+    p.st.episode[e] = episode;
+    for (int k = 0; k < p.K; ++k) p.st.prev[(int64_t)k * p.E + e] = -1;
+    p.st.score[e] = 0.0;
+    p.st.fscore[e] = 0.0;
+}
+
+// Rewards, dones, rollout arithmetic, state update, auto-reset, outputs, obs descriptor.
+// custom/ma_customenv.py:254-334, maddpg/agent.py:124-173,226-243
+struct Contrib {  // this env's share of gw_step_out.stats
+    double v[GW_STATS];
+};
+
+__device__ __forceinline__ void contrib_zero(Contrib &c) {
+#pragma unroll
+    for (int i = 0; i < GW_STATS; ++i) c.v[i] = 0.0;
+}
+
+// deterministic wave64 butterfly sum of every field
+__device__ __forceinline__ void wave_sum(Contrib &c) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+        for (int i = 0; i < GW_STATS; ++i) c.v[i] = __dadd_rn(c.v[i], __shfl_xor(c.v[i], off, 64));
+}
+
+template <int N>
+__device__ __forceinline__ void finish_env(const Params &p, int64_t e, const int (&pos0)[N],
+                                           const int (&act)[N], const int (&mdr)[N],
+                                           const double (&fear)[MAXN], uint32_t crash,
+                                           uint32_t restr, int (&fin)[N], uint32_t caught,
+                                           Contrib &ct) {
+    const int K = p.K;
+    uint32_t flags = p.st.flags[e];
+    uint32_t apples = flags & 0xFFu, term = (flags >> 8) & 0xFFu, trunc = (flags >> 16) & 0xFFu;
+    const uint32_t allk = all_bits(K);
+    int t = p.st.t[e] + 1;
+    int rew[MAXN];
+#pragma unroll
+    for (int k = 0; k < MAXN; ++k) rew[k] = 0;
+    // apples (:258-275): own apple, once; all eaten -> +20 to all, truncation
+    const uint32_t popped = caught & apples;
+    apples &= ~popped;
+    int apple_rewarded = __popc(popped);
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+        if ((popped >> k) & 1u) rew[k] += 20;
+    if (popped && apples == 0) {
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+            if (k < K) rew[k] += 20;
+        trunc = allk;
+    }
+    int crash_count = 0;
+    double shaped[MAXN];
+    double fsum_in[MAXN];
+#pragma unroll
+    for (int k = 0; k < MAXN; ++k) shaped[k] = fsum_in[k] = 0.0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        if (k >= K) continue;
+        if ((crash >> k) & 1u) {  // :281-285
+            rew[k] -= 10;
+            ++crash_count;
+            trunc = allk;
+            term |= 1u << k;
+        }
+        const int d = ((apples >> k) & 1u) ? manhattan(p, fin[k], p.apples[k]) : -1;  // :287-294
+        const int64_t pi = (int64_t)k * p.E + e;
+        const int prev = p.st.prev[pi];
+        if (prev >= 0 && d >= 0 && prev > d) rew[k] += 1;  // :296-300
+        p.st.prev[pi] = d;
+        shaped[k] = __dadd_rn(__dmul_rn(p.fear_weight, fear[k]), (double)rew[k]);  // agent.py:130
+        fsum_in[k] = fear[k];
+    }
+    const double score = __dadd_rn(p.st.score[e], np_sum_small(shaped, K));       // agent.py:173
+    const double fscore = __dadd_rn(p.st.fscore[e], np_sum_small(fsum_in, K));     // agent.py:141
+    const bool done = ((term & allk) == allk) || ((trunc & allk) == allk) ||
+                      (p.max_steps > 0 && t >= p.max_steps);                       // agent.py:241-243
+
+    const gw_step_out &o = p.out;
+    ct.v[0] = done ? score : 0.0;
+    ct.v[1] = done ? 1.0 : 0.0;
+    ct.v[2] = np_sum_small(fsum_in, K);
+    ct.v[3] = (double)crash_count;
+    ct.v[4] = (double)apple_rewarded;
+    ct.v[5] = np_sum_small(shaped, K);
+    ct.v[6] = done ? (double)t : 0.0;
+    ct.v[7] = 1.0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        if (k >= K) continue;
+        const int64_t ek = e * K + k;
+        if (o.reward) o.reward[ek] = (double)rew[k];
+        if (o.fear) o.fear[ek] = fear[k];
+        if (o.shaped) o.shaped[ek] = shaped[k];
+        if (o.term) o.term[ek] = (uint8_t)((term >> k) & 1u);
+        if (o.trunc) o.trunc[ek] = (uint8_t)((trunc >> k) & 1u);
+    }
+    if (o.done) o.done[e] = done;
+    if (o.crashes) o.crashes[e] = crash_count;
+    if (o.apples) o.apples[e] = apple_rewarded;
+    if (o.ep_return) o.ep_return[e] = score;
+    if (o.ep_fear) o.ep_fear[e] = fscore;
+    if (o.ep_len) o.ep_len[e] = t;
+    if (o.crash_bits) o.crash_bits[e] = (uint8_t)crash;
+    if (o.restr_bits) o.restr_bits[e] = (uint8_t)restr;
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+        if (o.actions) o.actions[e * N + n] = act[n];
+        if (o.mdr) o.mdr[e * N + n] = mdr[n];
+        if (o.final_pos) o.final_pos[e * N + n] = fin[n];
+    }
+
+    uint32_t *d = p.desc + e * NDESC;
+    if (done && p.auto_reset) {
+        // terminal obs -> final_obs, then CustomMAEnv.reset for the next episode
+        write_desc_pos<N>(d + 8, fin);
+        const uint32_t ep = p.st.episode[e] + 1;
+        int np_[N];
+        reset_env<N>(p, e, ep, np_);
+        write_desc_pos<N>(d, np_);
+        d[4] = D_RESET | D_WRITE | (o.final_obs ? D_FINAL : 0u) | (all_bits(K) << 8) | (apples << 16);
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+            if (k < K && o.mask) o.mask[e * K + k] = p.tb.amask[np_[k]];
+    } else {
+#pragma unroll
+        for (int n = 0; n < N; ++n) p.st.pos[(int64_t)n * p.E + e] = fin[n];
+        p.st.flags[e] = apples | (term << 8) | (trunc << 16);
+        p.st.t[e] = t;
+        p.st.score[e] = score;
+        p.st.fscore[e] = fscore;
+        write_desc_pos<N>(d, fin);
+        d[4] = D_WRITE | (apples << 8);
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+            if (k < K && o.mask) o.mask[e * K + k] = p.tb.amask[fin[k]];
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// step kernel, fear off: one thread per env
+// ---------------------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ void step_env_nofear(const Params &p, int64_t e, const uint8_t *s_ok, Contrib &ct) {
+    int pos[N], act[N], mdr[N], fin[N];
+    load_state<N>(p, e, pos);
+    const uint32_t episode = p.st.episode[e];
+    const int t = p.st.t[e];
+    select_actions<N>(p, e, episode, t, pos, act);
+#pragma unroll
+    for (int n = 0; n < N; ++n) mdr[n] = p.tb.mdr[pos[n]];
+    const uint32_t flags = p.st.flags[e];
+    int apple[MAXN];
+#pragma unroll
+    for (int k = 0; k < MAXN; ++k) apple[k] = (k < p.K && ((flags >> k) & 1u)) ? p.apples[k] : -1;
+    World<N> w;
+    w.init(pos, act, p.W);
+    uint32_t caught;
+    simulate<N, true>(w, s_ok, p.K, apple, caught, fin);
+    double fear[MAXN];
+#pragma unroll
+    for (int k = 0; k < MAXN; ++k) fear[k] = 0.0;
+    finish_env<N>(p, e, pos, act, mdr, fear, w.crash, w.restr, fin, caught, ct);
+}
+
+template <int N>
+__global__ void __launch_bounds__(256) step_kernel_nofear(Params p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_ok[];
+    for (int c = threadIdx.x; c < p.HW; c += blockDim.x) s_ok[c] = p.tb.okmask[c];
+    __syncthreads();
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    Contrib ct;
+    contrib_zero(ct);
+    if (e < p.E) step_env_nofear<N>(p, e, s_ok, ct);
+    if (p.out.stats) {
+        __shared__ double s_red[4][GW_STATS];
+        wave_sum(ct);
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        if (lane == 0)
+            for (int i = 0; i < GW_STATS; ++i) s_red[wv][i] = ct.v[i];
+        __syncthreads();
+        if (threadIdx.x < GW_STATS) {
+            const int i = threadIdx.x;
+            p.out.stats[(int64_t)blockIdx.x * GW_STATS + i] =
+                __dadd_rn(__dadd_rn(s_red[0][i], s_red[1][i]), __dadd_rn(s_red[2][i], s_red[3][i]));
+        }
+    }
+}
+
+
+// ---------------------------------------------------------------------------------------
+// step kernel, fear on: BE envs per 256-thread block, counterfactual sims as LDS tasks.
+//   FeAR_4_one_actor(actor k): for every affected j != k,
+//     V_x(j) = #{b : sim(joint_x with a_j := b if j close else a_j = stay).valid(j)}
+//   x in {MdR_k, a_k}.  Far j (not in close_agents) ignore b, so all 9 sims equal the
+//   "base" sim of x (j stays) -> one sim serves every far j.  For close j the b = a_j sim is
+//   the base sim too.  Tasks per (env, k) with a_k != MdR_k: 2 base + 2*8 per close j;
+//   a_k == MdR_k gives V_mdr == V_act -> Resp = 0 exactly, no task.
+// ---------------------------------------------------------------------------------------
+template <int N, int KMAX> struct FearCfg {
+    // envs per block, sized so that the task list + sim results stay under ~48 KB of LDS
+    static constexpr int BE = KMAX <= 2 ? (N <= 4 ? 64 : 32) : (N <= 4 ? 32 : 8);
+    static constexpr int MAXT = BE * (1 + KMAX * (2 + 16 * (N - 1)));
+};
+
+enum : uint32_t { T_MAIN = 0, T_BASE = 1, T_CJ = 2 };
+
+__device__ __forceinline__ uint32_t enc(uint32_t e, uint32_t k, uint32_t j, uint32_t var, uint32_t b, uint32_t kind) {
+    return e | (k << 6) | (j << 9) | (var << 12) | (b << 13) | (kind << 17);
+}
+
+template <int N, int KMAX>
+__global__ void __launch_bounds__(256) step_kernel_fear(Params p) {
+    constexpr int BE = FearCfg<N, KMAX>::BE;
+    constexpr int MAXT = FearCfg<N, KMAX>::MAXT;
+    __shared__ __attribute__((aligned(16))) uint8_t s_ok[4096];
+    __shared__ int s_pos[BE][N];
+    __shared__ int8_t s_act[BE][N];
+    __shared__ int8_t s_mdr[BE][N];
+    __shared__ uint8_t s_close[BE][KMAX];
+    __shared__ uint32_t s_tasks[MAXT];
+    __shared__ uint8_t s_base[BE][KMAX][2];
+    __shared__ uint8_t s_cj[BE][KMAX][N][2][NA];
+    __shared__ int s_fin[BE][N];
+    __shared__ uint32_t s_bits[BE];  // crash | restr << 8 | caught << 16
+    __shared__ int s_apple[BE][KMAX];
+    __shared__ int s_ntask;
+
+    const int tid = threadIdx.x;
+    for (int c = tid; c < p.HW; c += blockDim.x) s_ok[c] = p.tb.okmask[c];
+    if (tid == 0) s_ntask = BE;
+    __syncthreads();
+
+    const int64_t e0 = (int64_t)blockIdx.x * BE;
+    const int nenv = (int)min((int64_t)BE, p.E - e0);
+    const int K = p.K;
+
+    // ---- phase A: per env: actions, MdR, close sets, task list ----
+    if (tid < nenv) {
+        const int64_t e = e0 + tid;
+        int pos[N], act[N];
+        load_state<N>(p, e, pos);
+        select_actions<N>(p, e, p.st.episode[e], p.st.t[e], pos, act);
+        const uint32_t flags = p.st.flags[e];
+#pragma unroll
+        for (int n = 0; n < N; ++n) {
+            s_pos[tid][n] = pos[n];
+            s_act[tid][n] = (int8_t)act[n];
+            s_mdr[tid][n] = (int8_t)p.tb.mdr[pos[n]];
+        }
+        int ntask = 0;
+        uint32_t close[KMAX];
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) {
+            close[k] = 0;
+            s_apple[tid][k] = (k < K && ((flags >> k) & 1u)) ? p.apples[k] : -1;
+            if (k >= K) continue;
+#pragma unroll
+            for (int n = 0; n < N; ++n)
+                if (n == k || manhattan(p, pos[k], pos[n]) <= 5) close[k] |= 1u << n;  // :456-464
+            s_close[tid][k] = (uint8_t)close[k];
+            if (act[k] != (int)p.tb.mdr[pos[k]]) ntask += 2 + 16 * (__popc(close[k]) - 1);
+        }
+        s_tasks[tid] = enc(tid, 0, 0, 0, 0, T_MAIN);
+        if (ntask) {
+            int slot = atomicAdd(&s_ntask, ntask);
+#pragma unroll
+            for (int k = 0; k < KMAX; ++k) {
+                if (k >= K || act[k] == (int)p.tb.mdr[pos[k]]) continue;
+                s_tasks[slot++] = enc(tid, k, 0, 0, 15, T_BASE);
+                s_tasks[slot++] = enc(tid, k, 0, 1, 15, T_BASE);
+#pragma unroll
+                for (int j = 0; j < N; ++j) {
+                    if (j == k || !((close[k] >> j) & 1u)) continue;
+#pragma unroll
+                    for (int var = 0; var < 2; ++var)
+                        for (int b = 0; b < NA; ++b)
+                            if (b != act[j]) s_tasks[slot++] = enc(tid, k, j, var, b, T_CJ);
+                }
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- phase B: every lane runs one world update per task ----
+    const int ntask = s_ntask;
+    for (int ti = tid; ti < ntask; ti += blockDim.x) {
+        if (ti < BE && ti >= nenv) continue;  // main-sim slot of a missing env
+        const uint32_t tk = s_tasks[ti];
+        const int el = tk & 63, k = (tk >> 6) & 7, j = (tk >> 9) & 7, var = (tk >> 12) & 1,
+                  b = (tk >> 13) & 15, kind = (tk >> 17) & 3;
+        int pos[N], joint[N], fin[N];
+#pragma unroll
+        for (int n = 0; n < N; ++n) pos[n] = s_pos[el][n];
+        if (kind == T_MAIN) {
+#pragma unroll
+            for (int n = 0; n < N; ++n) joint[n] = s_act[el][n];
+            int apple[MAXN];
+#pragma unroll
+            for (int q = 0; q < MAXN; ++q) apple[q] = -1;
+#pragma unroll
+            for (int q = 0; q < KMAX; ++q) apple[q] = s_apple[el][q];
+            World<N> w;
+            w.init(pos, joint, p.W);
+            uint32_t caught;
+            simulate<N, true>(w, s_ok, K, apple, caught, fin);
+#pragma unroll
+            for (int n = 0; n < N; ++n) s_fin[el][n] = fin[n];
+            s_bits[el] = w.crash | (w.restr << 8) | (caught << 16);
+        } else {
+            const uint32_t cl = s_close[el][k];
+#pragma unroll
+            for (int n = 0; n < N; ++n) joint[n] = ((cl >> n) & 1u) ? (int)s_act[el][n] : 0;
+#pragma unroll
+            for (int n = 0; n < N; ++n)
+                if (n == k && var == 0) joint[n] = s_mdr[el][n];
+            if (kind == T_CJ) {
+#pragma unroll
+                for (int n = 0; n < N; ++n)
+                    if (n == j) joint[n] = b;
+            }
+            World<N> w;
+            w.init(pos, joint, p.W);
+            uint32_t caught;
+            int no_apple[MAXN];
+#pragma unroll
+            for (int q = 0; q < MAXN; ++q) no_apple[q] = -1;
+            simulate<N, true>(w, s_ok, 0, no_apple, caught, fin);  // one sim body in the loop
+            const uint32_t valid = ~(w.crash | w.restr) & ((1u << N) - 1u);
+            if (kind == T_BASE) {
+                s_base[el][k][var] = (uint8_t)valid;
+            } else {
+                s_cj[el][k][j][var][b] = (uint8_t)((valid >> j) & 1u);
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- phase C: FeAR sums, rewards, outputs ----
+    Contrib ct;
+    contrib_zero(ct);
+    if (tid < nenv) {
+        const int64_t e = e0 + tid;
+        int pos[N], act[N], mdr[N], fin[N];
+#pragma unroll
+        for (int n = 0; n < N; ++n) {
+            pos[n] = s_pos[tid][n];
+            act[n] = s_act[tid][n];
+            mdr[n] = s_mdr[tid][n];
+            fin[n] = s_fin[tid][n];
+        }
+        double fear[MAXN];
+#pragma unroll
+        for (int k = 0; k < MAXN; ++k) fear[k] = 0.0;
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) {
+            if (k >= K || act[k] == mdr[k]) continue;
+            const uint32_t cl = s_close[tid][k];
+            const uint32_t b0 = s_base[tid][k][0], b1 = s_base[tid][k][1];
+            double resp[N];
+#pragma unroll
+            for (int jj = 0; jj < N; ++jj) {
+                resp[jj] = 0.0;
+                if (jj == k) continue;
+                int vm, va;
+                if ((cl >> jj) & 1u) {
+                    vm = 0;
+                    va = 0;
+                    for (int b = 0; b < NA; ++b) {
+                        vm += (b == act[jj]) ? (int)((b0 >> jj) & 1u) : (int)s_cj[tid][k][jj][0][b];
+                        va += (b == act[jj]) ? (int)((b1 >> jj) & 1u) : (int)s_cj[tid][k][jj][1][b];
+                    }
+                } else {
+                    vm = 9 * (int)((b0 >> jj) & 1u);
+                    va = 9 * (int)((b1 >> jj) & 1u);
+                }
+                resp[jj] = p.tb.resp[vm * 10 + va];
+            }
+            fear[k] = np_sum_row<N>(resp, k);
+        }
+        const uint32_t bits = s_bits[tid];
+        finish_env<N>(p, e, pos, act, mdr, fear, bits & 0xFFu, (bits >> 8) & 0xFFu, fin, (bits >> 16) & 0xFFu, ct);
+    }
+    if (p.out.stats && tid < 64) {  // BE <= 64: every env of the block sits in wave 0
+        wave_sum(ct);
+        if (tid < GW_STATS) p.out.stats[(int64_t)blockIdx.x * GW_STATS + tid] = ct.v[tid];
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// reset kernel (CustomMAEnv.reset for masked envs)
+// ---------------------------------------------------------------------------------------
+template <int N>
+__global__ void __launch_bounds__(256) reset_kernel(Params p) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= p.E) return;
+    uint32_t *d = p.desc + e * NDESC;
+    if (p.rmask && !p.rmask[e]) {
+        d[4] = 0;
+        return;
+    }
+    int pos[N];
+    reset_env<N>(p, e, p.st.episode[e] + 1u, pos);
+    write_desc_pos<N>(d, pos);
+    d[4] = D_RESET | D_WRITE | (all_bits(p.K) << 8);
+    if (p.out.mask)
+        for (int k = 0; k < p.K; ++k) p.out.mask[e * p.K + k] = p.tb.amask[pos[k]];
+}
+
+// ---------------------------------------------------------------------------------------
+// obs kernel: obs[k][e][cell] float32 from the descriptors.
+//   step obs  (ma_customenv.py:303-322): map, agent n -> n+1, +9 own apple, relabel
+//   reset obs (ma_customenv.py:197-209): map, 0.5 at agents, +9 own apple
+// Each (env, k) has at most N+1 non-map cells ("patches"), computed once per block in LDS;
+// the store loop is then map float4 + <= N+1 compares per 16-byte store.
+// ---------------------------------------------------------------------------------------
+constexpr int OBS_BE = 8;      // envs per block
+constexpr int OBS_THREADS = 256;
+
+__device__ __forceinline__ float agent_value(bool reset, int n, int k, bool on_apple) {
+    if (reset) return on_apple ? 9.5f : 0.5f;
+    if (on_apple) return (float)(n + 1 + 9);
+    int v = n + 1;
+    if (v >= 1 && v <= 4 && v != k + 1) v = 5;   // other ids -> 5 (all_ids = [1,2,3,4], :314)
+    if (v == k + 1) v = 1;                        // my id -> 1 (:321)
+    return (float)v;
+}
+
+template <bool VEC4>
+__global__ void __launch_bounds__(OBS_THREADS) obs_kernel(Params p, float *__restrict__ obs,
+                                                          float *__restrict__ final_obs) {
+    __shared__ __attribute__((aligned(16))) float s_base[4096];  // [HW] static map
+    __shared__ int s_pc[2][OBS_BE][MAXN][MAXN + 1];    // [which][env][k][patch] cell (-1 none)
+    __shared__ float s_pv[2][OBS_BE][MAXN][MAXN + 1];
+    __shared__ uint32_t s_flag[OBS_BE];
+    const int tid = threadIdx.x;
+    const int HW = p.HW, N = p.N, K = p.K;
+    const int64_t e0 = (int64_t)blockIdx.x * OBS_BE;
+    const int nenv = (int)min((int64_t)OBS_BE, p.E - e0);
+    for (int c = tid; c < HW; c += OBS_THREADS) s_base[c] = p.tb.base[c];
+    // patches: one thread per (which, env, k)
+    if (tid < 2 * OBS_BE * MAXN) {
+        const int which = tid / (OBS_BE * MAXN), el = (tid / MAXN) % OBS_BE, k = tid % MAXN;
+        if (el < nenv && k < K) {
+            const uint32_t *d = p.desc + (e0 + el) * NDESC;
+            const uint32_t f = d[4];
+            if (k == 0 && which == 0) s_flag[el] = f;
+            const bool reset = (which == 0) && (f & D_RESET);
+            const uint32_t apples = which == 0 ? (f >> 8) & 0xFFu : (f >> 16) & 0xFFu;
+            const uint32_t *pw = d + (which == 0 ? 0 : 8);
+            const int ac = ((apples >> k) & 1u) ? p.apples[k] : -1;
+            int np = 0;
+            if (ac >= 0) {  // apple first, agents override it
+                float av = p.tb.base[ac] + 9.0f;
+                if (!reset && av == (float)(k + 1)) av = 1.0f;  // relabel of :321 (apple on a wall, K = 8)
+                s_pc[which][el][k][np] = ac;
+                s_pv[which][el][k][np] = av;
+                ++np;
+            }
+            for (int n = 0; n < N; ++n) {
+                const int c = (int)((pw[n >> 1] >> (16 * (n & 1))) & 0xFFFFu);
+                s_pc[which][el][k][np] = c;
+                s_pv[which][el][k][np] = agent_value(reset, n, k, c == ac);
+                ++np;
+            }
+            for (; np <= MAXN; ++np) s_pc[which][el][k][np] = -1;
+        }
+    }
+    if (tid < OBS_BE && tid >= nenv) s_flag[tid] = 0;
+    __syncthreads();
+
+    const int npatch = N + 1;
+    for (int which = 0; which < 2; ++which) {
+        float *dst = which == 0 ? obs : final_obs;
+        if (!dst) continue;
+        const uint32_t need = which == 0 ? D_WRITE : D_FINAL;
+        if (VEC4) {
+            const int HW4 = HW >> 2;
+            const int total4 = nenv * HW4;
+            for (int k = 0; k < K; ++k) {
+                float4 *out4 = reinterpret_cast<float4 *>(dst + ((int64_t)k * p.E + e0) * HW);
+                for (int i4 = tid; i4 < total4; i4 += OBS_THREADS) {
+                    const int el = i4 / HW4;
+                    if (!(s_flag[el] & need)) continue;
+                    const int c0 = (i4 - el * HW4) << 2;
+                    float4 v = *reinterpret_cast<const float4 *>(&s_base[c0]);
+                    for (int q = 0; q < npatch; ++q) {
+                        const int dd = s_pc[which][el][k][q] - c0;
+                        if ((unsigned)dd < 4u) {
+                            const float pv = s_pv[which][el][k][q];
+                            if (dd == 0) v.x = pv;
+                            else if (dd == 1) v.y = pv;
+                            else if (dd == 2) v.z = pv;
+                            else v.w = pv;
+                        }
+                    }
+                    out4[i4] = v;
+                }
+            }
+        } else {
+            const int total = nenv * HW;
+            for (int k = 0; k < K; ++k) {
+                float *o = dst + ((int64_t)k * p.E + e0) * HW;
+                for (int i = tid; i < total; i += OBS_THREADS) {
+                    const int el = i / HW;
+                    if (!(s_flag[el] & need)) continue;
+                    const int c = i - el * HW;
+                    float v = s_base[c];
+                    for (int q = 0; q < npatch; ++q)
+                        if (s_pc[which][el][k][q] == c) v = s_pv[which][el][k][q];
+                    o[i] = v;
+                }
+            }
+        }
+    }
+}
+
+}  // namespace gw
+
+// =========================================================================================
+// C ABI
+// =========================================================================================
+namespace {
+
+thread_local std::string g_err;
+
+gw_status fail(gw_status s, const std::string &msg) {
+    g_err = msg;
+    return s;
+}
+
+#define HIP_TRY(expr)                                                                      \
+    do {                                                                                   \
+        hipError_t _e = (expr);                                                            \
+        if (_e != hipSuccess) return fail(GW_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+struct Env {
+    int device = 0;
+    int H = 0, W = 0, HW = 0, N = 0, K = 0, F = 0, P = 0;
+    int64_t E = 0, env_offset = 0;
+    int fear = 0, max_steps = 0, auto_reset = 1;
+    double fear_weight = 0.0;
+    uint64_t seed = 0;
+    int apples[GW_MAX_AGENTS] = {0};
+    bool initialized = false;
+    // tables
+    uint8_t *okmask = nullptr, *policy = nullptr, *mdr = nullptr;
+    double *cdf = nullptr, *resp = nullptr;
+    uint16_t *amask = nullptr;
+    int32_t *free_cells = nullptr;
+    float *base = nullptr;
+    // state
+    int32_t *pos = nullptr, *t = nullptr, *prev = nullptr;
+    uint32_t *flags = nullptr, *episode = nullptr, *desc = nullptr;
+    double *score = nullptr, *fscore = nullptr;
+    std::vector<void *> allocs;
+    // per-launch profiling events (gw_profile)
+    bool profiling = false;
+    std::vector<hipEvent_t> ev_pool;   // 3 events per timed gw_step
+    size_t ev_used = 0;
+};
+
+hipEvent_t next_event(Env *env) {
+    if (env->ev_used == env->ev_pool.size()) {
+        hipEvent_t e = nullptr;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        env->ev_pool.push_back(e);
+    }
+    return env->ev_pool[env->ev_used++];
+}
+
+template <typename T>
+gw_status dalloc(Env *env, T **ptr, size_t count) {
+    void *p = nullptr;
+    hipError_t e = hipMalloc(&p, sizeof(T) * (count ? count : 1));
+    if (e != hipSuccess) return fail(GW_ERR_ALLOC, std::string("hipMalloc: ") + hipGetErrorString(e));
+    env->allocs.push_back(p);
+    *ptr = static_cast<T *>(p);
+    return GW_OK;
+}
+
+#define GW_TRY(expr)                   \
+    do {                               \
+        gw_status _s = (expr);         \
+        if (_s != GW_OK) return _s;    \
+    } while (0)
+
+gw::Params make_params(const Env *env) {
+    gw::Params p;
+    std::memset(&p, 0, sizeof(p));
+    p.tb.okmask = env->okmask;
+    p.tb.policy = env->policy;
+    p.tb.cdf = env->cdf;
+    p.tb.mdr = env->mdr;
+    p.tb.amask = env->amask;
+    p.tb.free_cells = env->free_cells;
+    p.tb.base = env->base;
+    p.tb.resp = env->resp;
+    p.st.pos = env->pos;
+    p.st.flags = env->flags;
+    p.st.t = env->t;
+    p.st.episode = env->episode;
+    p.st.prev = env->prev;
+    p.st.score = env->score;
+    p.st.fscore = env->fscore;
+    p.desc = env->desc;
+    p.E = env->E;
+    p.env_offset = env->env_offset;
+    p.fear_weight = env->fear_weight;
+    p.H = env->H;
+    p.W = env->W;
+    p.HW = env->HW;
+    p.N = env->N;
+    p.K = env->K;
+    p.F = env->F;
+    p.max_steps = env->max_steps;
+    p.auto_reset = env->auto_reset;
+    p.key0 = (uint32_t)env->seed;
+    p.key1 = (uint32_t)(env->seed >> 32);
+    p.w_magic = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)env->W - 1) / (uint64_t)env->W);
+    for (int k = 0; k < GW_MAX_AGENTS; ++k) p.apples[k] = env->apples[k];
+    return p;
+}
+
+template <int N>
+hipError_t launch_step(const Env *env, const gw::Params &p, hipStream_t s) {
+    if (env->fear) {
+        if (env->K <= 2) {
+            constexpr int BE = gw::FearCfg<N, 2>::BE;
+            const unsigned grid = (unsigned)((env->E + BE - 1) / BE);
+            hipLaunchKernelGGL((gw::step_kernel_fear<N, 2>), dim3(grid), dim3(256), 0, s, p);
+        } else {
+            constexpr int BE = gw::FearCfg<N, N>::BE;
+            const unsigned grid = (unsigned)((env->E + BE - 1) / BE);
+            hipLaunchKernelGGL((gw::step_kernel_fear<N, N>), dim3(grid), dim3(256), 0, s, p);
+        }
+    } else {
+        const unsigned grid = (unsigned)((env->E + 255) / 256);
+        hipLaunchKernelGGL((gw::step_kernel_nofear<N>), dim3(grid), dim3(256), env->HW, s, p);
+    }
+    return hipGetLastError();
+}
+
+template <int N>
+hipError_t launch_reset(const Env *env, const gw::Params &p, hipStream_t s) {
+    const unsigned grid = (unsigned)((env->E + 255) / 256);
+    hipLaunchKernelGGL((gw::reset_kernel<N>), dim3(grid), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t dispatch_step(const Env *env, const gw::Params &p, hipStream_t s) {
+    switch (env->N) {
+        case 1: return launch_step<1>(env, p, s);
+        case 2: return launch_step<2>(env, p, s);
+        case 3: return launch_step<3>(env, p, s);
+        case 4: return launch_step<4>(env, p, s);
+        case 5: return launch_step<5>(env, p, s);
+        case 6: return launch_step<6>(env, p, s);
+        case 7: return launch_step<7>(env, p, s);
+        case 8: return launch_step<8>(env, p, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+hipError_t dispatch_reset(const Env *env, const gw::Params &p, hipStream_t s) {
+    switch (env->N) {
+        case 1: return launch_reset<1>(env, p, s);
+        case 2: return launch_reset<2>(env, p, s);
+        case 3: return launch_reset<3>(env, p, s);
+        case 4: return launch_reset<4>(env, p, s);
+        case 5: return launch_reset<5>(env, p, s);
+        case 6: return launch_reset<6>(env, p, s);
+        case 7: return launch_reset<7>(env, p, s);
+        case 8: return launch_reset<8>(env, p, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_obs(const Env *env, const gw::Params &p, float *obs, float *final_obs, hipStream_t s) {
+    if (!obs && !final_obs) return hipSuccess;
+    const unsigned grid = (unsigned)((env->E + gw::OBS_BE - 1) / gw::OBS_BE);
+    if (env->HW % 4 == 0)
+        hipLaunchKernelGGL((gw::obs_kernel<true>), dim3(grid), dim3(gw::OBS_THREADS), 0, s, p, obs, final_obs);
+    else
+        hipLaunchKernelGGL((gw::obs_kernel<false>), dim3(grid), dim3(gw::OBS_THREADS), 0, s, p, obs, final_obs);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+namespace {
+template <int N>
+int64_t stats_rows_n(const Env *env) {
+    if (!env->fear) return (env->E + 255) / 256;
+    const int be = env->K <= 2 ? gw::FearCfg<N, 2>::BE : gw::FearCfg<N, N>::BE;
+    return (env->E + be - 1) / be;
+}
+}  // namespace
+
+extern "C" {
+
+const char *gw_last_error(void) { return g_err.c_str(); }
+
+gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, void **out_env) {
+    if (!sc || !cfg || !out_env) return fail(GW_ERR_ARG, "null argument");
+    *out_env = nullptr;
+    const int H = sc->H, W = sc->W, N = cfg->N, K = cfg->K;
+    if (H < 1 || W < 2 || (int64_t)H * W > 4096) return fail(GW_ERR_ARG, "need W >= 2 and H*W <= 4096");
+    if (N < 1 || N > GW_MAX_AGENTS || K < 1 || K > N) return fail(GW_ERR_ARG, "need 1 <= K <= N <= 8");
+    if (cfg->num_envs < 1) return fail(GW_ERR_ARG, "num_envs must be >= 1");
+    if (cfg->env_offset < 0 || cfg->env_offset + cfg->num_envs > ((int64_t)1 << 32))
+        return fail(GW_ERR_ARG, "global env ids must fit in 32 bits");
+    if (!sc->region || !sc->policy_id || !sc->policy_cdf || !sc->mdr || !sc->apples || sc->n_policies < 1)
+        return fail(GW_ERR_ARG, "incomplete scenario tables");
+    const int HW = H * W;
+    std::vector<uint8_t> ok(HW), mdr(HW), pol(HW);
+    std::vector<uint16_t> am(HW);
+    std::vector<float> base(HW);
+    std::vector<int32_t> freec;
+    for (int c = 0; c < HW; ++c) {
+        const int r = c / W, q = c % W;
+        const auto road = [&](int rr, int cc) { return rr >= 0 && rr < H && cc >= 0 && cc < W && sc->region[rr * W + cc] != 0; };
+        ok[c] = (uint8_t)(road(r - 1, q) | (road(r + 1, q) << 1) | (road(r, q - 1) << 2) | (road(r, q + 1) << 3));
+        // get_action_mask, custom/ma_customenv.py:467-506
+        uint16_t m = 0x1FF;
+        if (!road(r - 1, q)) m &= ~(1u << 1);
+        if (!road(r + 1, q)) m &= ~(1u << 2);
+        if (!road(r, q - 1)) m &= ~(1u << 3);
+        if (!road(r, q + 1)) m &= ~(1u << 4);
+        if (!road(r - 2, q)) m &= ~(1u << 5);
+        if (!road(r + 2, q)) m &= ~(1u << 6);
+        if (!road(r, q - 2)) m &= ~(1u << 7);
+        if (!road(r, q + 2)) m &= ~(1u << 8);
+        am[c] = m;
+        base[c] = sc->region[c] ? 0.0f : -1.0f;
+        if (sc->region[c]) freec.push_back(c);
+        if (sc->mdr[c] >= GW_N_ACTIONS) return fail(GW_ERR_ARG, "MdR action out of range");
+        if (sc->policy_id[c] >= sc->n_policies) return fail(GW_ERR_ARG, "policy id out of range");
+        mdr[c] = sc->mdr[c];
+        pol[c] = sc->policy_id[c];
+    }
+    if ((int)freec.size() < N) return fail(GW_ERR_ARG, "fewer road cells than agents");
+    for (int k = 0; k < K; ++k)
+        if (sc->apples[k] < 0 || sc->apples[k] >= HW) return fail(GW_ERR_ARG, "apple outside the grid");
+    // Resp table: Responsibility.py:194-198 evaluated in IEEE f64 exactly as numpy does
+    std::vector<double> resp(100);
+    for (int vm = 0; vm < 10; ++vm)
+        for (int va = 0; va < 10; ++va) {
+            volatile double num = (double)vm - (double)va;
+            volatile double den = (double)vm + 0.000001;
+            double r = num / den;
+            r = r < -1.0 ? -1.0 : (r > 1.0 ? 1.0 : r);
+            resp[vm * 10 + va] = r;
+        }
+
+    Env *env = new (std::nothrow) Env();
+    if (!env) return fail(GW_ERR_ALLOC, "host allocation failed");
+    env->device = device;
+    env->H = H; env->W = W; env->HW = HW; env->N = N; env->K = K;
+    env->F = (int)freec.size();
+    env->P = sc->n_policies;
+    env->E = cfg->num_envs;
+    env->env_offset = cfg->env_offset;
+    env->fear = cfg->fear ? 1 : 0;
+    env->fear_weight = cfg->fear_weight;
+    env->max_steps = cfg->max_steps;
+    env->auto_reset = cfg->auto_reset ? 1 : 0;
+    env->seed = cfg->seed;
+    for (int k = 0; k < K; ++k) env->apples[k] = sc->apples[k];
+
+    auto cleanup = [&](gw_status s) {
+        for (void *p : env->allocs) (void)hipFree(p);
+        delete env;
+        return s;
+    };
+    if (hipSetDevice(device) != hipSuccess) return cleanup(fail(GW_ERR_HIP, "hipSetDevice failed"));
+    const size_t E = (size_t)env->E;
+    gw_status st = GW_OK;
+    if ((st = dalloc(env, &env->okmask, HW)) || (st = dalloc(env, &env->policy, HW)) ||
+        (st = dalloc(env, &env->mdr, HW)) || (st = dalloc(env, &env->cdf, (size_t)env->P * 2 * 9)) ||
+        (st = dalloc(env, &env->resp, 100)) || (st = dalloc(env, &env->amask, HW)) ||
+        (st = dalloc(env, &env->free_cells, freec.size())) || (st = dalloc(env, &env->base, HW)) ||
+        (st = dalloc(env, &env->pos, (size_t)N * E)) || (st = dalloc(env, &env->t, E)) ||
+        (st = dalloc(env, &env->prev, (size_t)K * E)) || (st = dalloc(env, &env->flags, E)) ||
+        (st = dalloc(env, &env->episode, E)) || (st = dalloc(env, &env->desc, E * gw::NDESC)) ||
+        (st = dalloc(env, &env->score, E)) || (st = dalloc(env, &env->fscore, E)))
+        return cleanup(st);
+    hipError_t he = hipSuccess;
+#define CP(dst, src, n) if (he == hipSuccess) he = hipMemcpy(dst, src, n, hipMemcpyHostToDevice)
+    CP(env->okmask, ok.data(), HW);
+    CP(env->policy, pol.data(), HW);
+    CP(env->mdr, mdr.data(), HW);
+    CP(env->cdf, sc->policy_cdf, sizeof(double) * env->P * 2 * 9);
+    CP(env->resp, resp.data(), sizeof(double) * 100);
+    CP(env->amask, am.data(), sizeof(uint16_t) * HW);
+    CP(env->free_cells, freec.data(), sizeof(int32_t) * freec.size());
+    CP(env->base, base.data(), sizeof(float) * HW);
+#undef CP
+    if (he == hipSuccess) he = hipMemset(env->episode, 0xFF, sizeof(uint32_t) * E);  // first reset -> 0
+    if (he == hipSuccess) he = hipMemset(env->desc, 0, sizeof(uint32_t) * E * gw::NDESC);
+    if (he == hipSuccess) he = hipDeviceSynchronize();
+    if (he != hipSuccess) return cleanup(fail(GW_ERR_HIP, std::string("init: ") + hipGetErrorString(he)));
+    *out_env = env;
+    return GW_OK;
+}
+
+gw_status gw_reset(void *handle, const uint8_t *env_mask, const int32_t *spawn_cells, float *obs,
+                   uint16_t *mask, void *stream) {
+    Env *env = static_cast<Env *>(handle);
+    if (!env) return fail(GW_ERR_ARG, "null env");
+    gw::Params p = make_params(env);
+    p.rmask = env_mask;
+    p.spawn = spawn_cells;
+    p.out.mask = mask;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    HIP_TRY(dispatch_reset(env, p, s));
+    HIP_TRY(launch_obs(env, p, obs, nullptr, s));
+    env->initialized = true;
+    return GW_OK;
+}
+
+gw_status gw_step(void *handle, const int32_t *rl_actions, const int32_t *scripted,
+                  const int32_t *spawn, const gw_step_out *out, void *stream) {
+    Env *env = static_cast<Env *>(handle);
+    if (!env) return fail(GW_ERR_ARG, "null env");
+    if (!env->initialized) return fail(GW_ERR_STATE, "gw_step before gw_reset");
+    gw::Params p = make_params(env);
+    p.rl = rl_actions;
+    p.scripted = scripted;
+    p.spawn = spawn;
+    if (out) p.out = *out;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    if (env->profiling)
+        for (int i = 0; i < 3; ++i)
+            if (!(ev[i] = next_event(env))) return fail(GW_ERR_HIP, "hipEventCreate failed");
+    if (ev[0]) HIP_TRY(hipEventRecord(ev[0], s));
+    HIP_TRY(dispatch_step(env, p, s));
+    if (ev[1]) HIP_TRY(hipEventRecord(ev[1], s));
+    HIP_TRY(launch_obs(env, p, p.out.obs, p.out.final_obs, s));
+    if (ev[2]) HIP_TRY(hipEventRecord(ev[2], s));
+    return GW_OK;
+}
+
+gw_status gw_profile(void *handle, int enable) {
+    Env *env = static_cast<Env *>(handle);
+    if (!env) return fail(GW_ERR_ARG, "null env");
+    env->profiling = enable != 0;
+    return GW_OK;
+}
+
+gw_status gw_profile_read(void *handle, double out_ms[2], int64_t *n_steps) {
+    Env *env = static_cast<Env *>(handle);
+    if (!env || !out_ms) return fail(GW_ERR_ARG, "null argument");
+    out_ms[0] = out_ms[1] = 0.0;
+    const size_t n = env->ev_used / 3;
+    for (size_t i = 0; i < n; ++i) {
+        hipEvent_t *e = &env->ev_pool[3 * i];
+        HIP_TRY(hipEventSynchronize(e[2]));
+        float a = 0.f, b = 0.f;
+        HIP_TRY(hipEventElapsedTime(&a, e[0], e[1]));
+        HIP_TRY(hipEventElapsedTime(&b, e[1], e[2]));
+        out_ms[0] += a;
+        out_ms[1] += b;
+    }
+    if (n_steps) *n_steps = (int64_t)n;
+    env->ev_used = 0;
+    return GW_OK;
+}
+
+gw_status gw_state_view(void *handle, gw_state *out) {
+    Env *env = static_cast<Env *>(handle);
+    if (!env || !out) return fail(GW_ERR_ARG, "null argument");
+    out->pos = env->pos;
+    out->flags = env->flags;
+    out->t = env->t;
+    out->episode = env->episode;
+    out->prev_dist = env->prev;
+    out->score = env->score;
+    out->fear_score = env->fscore;
+    return GW_OK;
+}
+
+gw_status gw_copy_state(void *handle, const gw_state *buf, int to_env, void *stream) {
+    Env *env = static_cast<Env *>(handle);
+    if (!env || !buf) return fail(GW_ERR_ARG, "null argument");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const size_t E = (size_t)env->E;
+    struct Item { void *mine; void *theirs; size_t bytes; } items[] = {
+        {env->pos, buf->pos, sizeof(int32_t) * env->N * E},
+        {env->flags, buf->flags, sizeof(uint32_t) * E},
+        {env->t, buf->t, sizeof(int32_t) * E},
+        {env->episode, buf->episode, sizeof(uint32_t) * E},
+        {env->prev, buf->prev_dist, sizeof(int32_t) * env->K * E},
+        {env->score, buf->score, sizeof(double) * E},
+        {env->fscore, buf->fear_score, sizeof(double) * E},
+    };
+    for (const Item &it : items) {
+        if (!it.theirs) continue;
+        if (to_env)
+            HIP_TRY(hipMemcpyAsync(it.mine, it.theirs, it.bytes, hipMemcpyDefault, s));
+        else
+            HIP_TRY(hipMemcpyAsync(it.theirs, it.mine, it.bytes, hipMemcpyDefault, s));
+    }
+    if (to_env) env->initialized = true;
+    return GW_OK;
+}
+
+
+int64_t gw_stats_rows(void *handle) {
+    const Env *env = static_cast<const Env *>(handle);
+    if (!env) return -1;
+    switch (env->N) {
+        case 1: return stats_rows_n<1>(env);
+        case 2: return stats_rows_n<2>(env);
+        case 3: return stats_rows_n<3>(env);
+        case 4: return stats_rows_n<4>(env);
+        case 5: return stats_rows_n<5>(env);
+        case 6: return stats_rows_n<6>(env);
+        case 7: return stats_rows_n<7>(env);
+        case 8: return stats_rows_n<8>(env);
+    }
+    return -1;
+}
+
+gw_status gw_dims(void *handle, int64_t out[5]) {
+    Env *env = static_cast<Env *>(handle);
+    if (!env || !out) return fail(GW_ERR_ARG, "null argument");
+    out[0] = env->H; out[1] = env->W; out[2] = env->N; out[3] = env->K; out[4] = env->E;
+    return GW_OK;
+}
+
+void gw_destroy(void *handle) {
+    Env *env = static_cast<Env *>(handle);
+    if (!env) return;
+    (void)hipSetDevice(env->device);
+    (void)hipDeviceSynchronize();
+    for (hipEvent_t e : env->ev_pool) (void)hipEventDestroy(e);
+    for (void *p : env->allocs) (void)hipFree(p);
+    delete env;
+}
+
+}  // extern "C"

@@ -1,0 +1,154 @@
+"""ctypes binding of libgridenv.so (include/gridenv.h) and its in-tree build.
+
+The library is built in-tree for gfx950 (``hipcc --offload-arch=gfx950``) so that the .so
+travels with the repository snapshot.  torch must be imported before the library is loaded:
+both then share torch's HIP runtime (same soname), and the device pointers / streams torch
+hands out are valid for our kernels.  There is no CPU fallback: if the library cannot be
+built or loaded, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(HERE)
+REPO_ROOT = os.path.dirname(PKG_ROOT)
+CSRC = os.path.join(PKG_ROOT, "csrc")
+INCLUDE = os.path.join(REPO_ROOT, "include")
+LIB_PATH = os.path.join(CSRC, "libgridenv.so")
+SOURCES = [os.path.join(CSRC, "gridenv.hip"), os.path.join(INCLUDE, "gridenv.h")]
+ARCH = os.environ.get("MARLNAV_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+HIPCC_FLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared",
+               "-ffp-contract=off", "-fno-fast-math", "-Wall"]
+
+GW_MAX_AGENTS = 8
+_lock = threading.Lock()
+_lib = None
+
+
+class GwError(RuntimeError):
+    pass
+
+
+STAMP_PATH = LIB_PATH + ".sha256"
+
+
+def source_hash() -> str:
+    """Content hash of the sources + compile flags (mtimes change when the tree is copied)."""
+    import hashlib
+    h = hashlib.sha256(" ".join(HIPCC_FLAGS).encode())
+    for src in SOURCES:
+        with open(src, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def needs_build() -> bool:
+    if not os.path.exists(LIB_PATH) or not os.path.exists(STAMP_PATH):
+        return True
+    with open(STAMP_PATH) as f:
+        return f.read().strip() != source_hash()
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile csrc/gridenv.hip -> csrc/libgridenv.so for gfx950 (cross-compiles without a GPU)."""
+    if not force and not needs_build():
+        return LIB_PATH
+    tmp = LIB_PATH + f".tmp{os.getpid()}"
+    cmd = [HIPCC, *HIPCC_FLAGS, f"-I{INCLUDE}", SOURCES[0], "-o", tmp]
+    if verbose:
+        print(" ".join(cmd))
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise GwError(f"hipcc failed ({r.returncode}):\n{r.stderr[-4000:]}")
+    os.replace(tmp, LIB_PATH)
+    with open(STAMP_PATH, "w") as f:
+        f.write(source_hash())
+    return LIB_PATH
+
+
+class GwScenario(C.Structure):
+    _fields_ = [("H", C.c_int32), ("W", C.c_int32), ("region", C.c_void_p),
+                ("policy_id", C.c_void_p), ("n_policies", C.c_int32), ("policy_cdf", C.c_void_p),
+                ("mdr", C.c_void_p), ("apples", C.c_void_p)]
+
+
+class GwConfig(C.Structure):
+    _fields_ = [("N", C.c_int32), ("K", C.c_int32), ("num_envs", C.c_int64),
+                ("env_offset", C.c_int64), ("fear", C.c_int32), ("fear_weight", C.c_double),
+                ("max_steps", C.c_int32), ("auto_reset", C.c_int32), ("seed", C.c_uint64)]
+
+
+STEP_OUT_FIELDS = ["obs", "final_obs", "reward", "fear", "shaped", "term", "trunc", "done", "mask",
+                   "crashes", "apples", "ep_return", "ep_fear", "ep_len", "actions", "mdr",
+                   "final_pos", "crash_bits", "restr_bits", "stats"]
+GW_STATS = 8
+STATS_NAMES = ["done_return", "episodes", "fear", "crashes", "apples", "shaped", "done_len", "env_steps"]
+
+
+class GwStepOut(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in STEP_OUT_FIELDS]
+
+
+STATE_FIELDS = ["pos", "flags", "t", "episode", "prev_dist", "score", "fear_score"]
+
+
+class GwState(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in STATE_FIELDS]
+
+
+EXPORTS = ["gw_create", "gw_reset", "gw_step", "gw_state_view", "gw_copy_state", "gw_profile",
+           "gw_profile_read", "gw_stats_rows", "gw_dims", "gw_last_error", "gw_destroy"]
+
+
+def _declare(L):
+    p = C.c_void_p
+    L.gw_create.argtypes = [C.POINTER(GwScenario), C.POINTER(GwConfig), C.c_int, C.POINTER(C.c_void_p)]
+    L.gw_create.restype = C.c_int
+    L.gw_reset.argtypes = [p, p, p, p, p, p]
+    L.gw_reset.restype = C.c_int
+    L.gw_step.argtypes = [p, p, p, p, C.POINTER(GwStepOut), p]
+    L.gw_step.restype = C.c_int
+    L.gw_state_view.argtypes = [p, C.POINTER(GwState)]
+    L.gw_state_view.restype = C.c_int
+    L.gw_copy_state.argtypes = [p, C.POINTER(GwState), C.c_int, p]
+    L.gw_copy_state.restype = C.c_int
+    L.gw_profile.argtypes = [p, C.c_int]
+    L.gw_profile.restype = C.c_int
+    L.gw_profile_read.argtypes = [p, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
+    L.gw_profile_read.restype = C.c_int
+    L.gw_stats_rows.argtypes = [p]
+    L.gw_stats_rows.restype = C.c_int64
+    L.gw_dims.argtypes = [p, C.POINTER(C.c_int64)]
+    L.gw_dims.restype = C.c_int
+    L.gw_last_error.argtypes = []
+    L.gw_last_error.restype = C.c_char_p
+    L.gw_destroy.argtypes = [p]
+    L.gw_destroy.restype = None
+    return L
+
+
+def load(build_if_needed: bool = True):
+    """Load libgridenv.so (building it first if stale).  Imports torch first on purpose."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        import torch  # noqa: F401  (bind to torch's HIP runtime)
+        if build_if_needed and needs_build():
+            build()
+        if not os.path.exists(LIB_PATH):
+            raise GwError(f"{LIB_PATH} is missing; run __graft_entry__.build()")
+        _lib = _declare(C.CDLL(LIB_PATH))
+        return _lib
+
+
+def check(status: int, what: str):
+    if status != 0:
+        msg = load().gw_last_error().decode(errors="replace")
+        raise GwError(f"{what} failed (status {status}): {msg}")

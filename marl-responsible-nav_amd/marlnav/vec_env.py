@@ -1,0 +1,205 @@
+"""VecGridEnv: E independent CustomMAEnv episodes resident on one MI355X.
+
+Tensor API over libgridenv (include/gridenv.h).  One ``step`` is the reference's
+``CustomMAEnv.step`` (custom/ma_customenv.py:217-334) applied to all E envs at once, plus the
+per-step reward/score arithmetic of ``MADDPGAgent.train`` (maddpg/agent.py:124-173) and an
+optional auto-reset (the ``break`` + ``env.reset()`` of maddpg/agent.py:241 / main_custom.py:129).
+
+Layouts (device tensors, owned by the env and overwritten by the next call):
+  obs        [K, E, H, W] float32   agent-major: obs[k] is RL agent k's actor input batch
+  reward, fear, shaped      [E, K] float64
+  term, trunc               [E, K] uint8;  done [E] uint8
+  mask       [E, K] int16 (9-bit action mask, bit a = action a allowed)
+  crashes, apples, ep_len   [E] int32;  ep_return, ep_fear [E] float64
+  debug outputs (debug=True): actions/mdr/final_pos [E, N] int32, crash_bits/restr_bits [E] uint8
+  stats (stats=True): [rows, 8] float64 per-block partial sums of the step (_lib.STATS_NAMES)
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+from .scenario import CompiledScenario, builtin
+
+
+@dataclass
+class StepResult:
+    obs: torch.Tensor
+    reward: torch.Tensor
+    fear: torch.Tensor
+    shaped: torch.Tensor
+    term: torch.Tensor
+    trunc: torch.Tensor
+    done: torch.Tensor
+    mask: torch.Tensor
+    crashes: torch.Tensor
+    apples: torch.Tensor
+    ep_return: torch.Tensor
+    ep_fear: torch.Tensor
+    ep_len: torch.Tensor
+    final_obs: torch.Tensor | None = None
+    actions: torch.Tensor | None = None
+    mdr: torch.Tensor | None = None
+    final_pos: torch.Tensor | None = None
+    crash_bits: torch.Tensor | None = None
+    restr_bits: torch.Tensor | None = None
+    stats: torch.Tensor | None = None   # [rows, 8] per-block partial sums (_lib.STATS_NAMES)
+
+
+def _ptr(t: torch.Tensor | None):
+    if t is None:
+        return None
+    assert t.is_cuda and t.is_contiguous()
+    return t.data_ptr()
+
+
+class VecGridEnv:
+    def __init__(self, scenario: CompiledScenario | str = "level3", num_envs: int = 1, fear: bool = True,
+                 fear_weight: float = -5.0, max_steps: int = 150, auto_reset: bool = True, seed: int = 42,
+                 device: torch.device | int | None = None, env_offset: int = 0, final_obs: bool = False,
+                 debug: bool = False, obs: bool = True, stats: bool = False):
+        if not torch.cuda.is_available():
+            raise _lib.GwError("VecGridEnv needs a HIP device (no CPU fallback by design)")
+        sc = builtin(scenario) if isinstance(scenario, str) else scenario
+        self.sc = sc
+        self.E = int(num_envs)
+        self.N, self.K, self.H, self.W = sc.N, sc.K, sc.H, sc.W
+        self.fear_enabled = bool(fear)
+        self.fear_weight = float(fear_weight)
+        self.max_steps = int(max_steps)
+        self.auto_reset = bool(auto_reset)
+        self.seed = int(seed)
+        self.env_offset = int(env_offset)
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else
+                                   (device if isinstance(device, int) else device.index or 0))
+        self.lib = _lib.load()
+
+        keep = dict(region=np.ascontiguousarray(sc.region, np.uint8),
+                    policy_id=np.ascontiguousarray(sc.policy_id, np.uint8),
+                    cdf=np.ascontiguousarray(sc.policy_cdf, np.float64),
+                    mdr=np.ascontiguousarray(sc.mdr, np.uint8),
+                    apples=np.ascontiguousarray(sc.apples, np.int32))
+        scn = _lib.GwScenario(sc.H, sc.W, keep["region"].ctypes.data, keep["policy_id"].ctypes.data,
+                              int(sc.policy_cdf.shape[0]), keep["cdf"].ctypes.data, keep["mdr"].ctypes.data,
+                              keep["apples"].ctypes.data)
+        cfg = _lib.GwConfig(self.N, self.K, self.E, self.env_offset, int(self.fear_enabled), self.fear_weight,
+                            self.max_steps, int(self.auto_reset), self.seed & 0xFFFFFFFFFFFFFFFF)
+        h = C.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.gw_create(C.byref(scn), C.byref(cfg), self.device.index, C.byref(h)), "gw_create")
+        self.handle = h
+
+        dev, E, K, N = self.device, self.E, self.K, self.N
+        f64 = dict(dtype=torch.float64, device=dev)
+        self.out = dict(
+            obs=torch.empty((K, E, sc.H, sc.W), dtype=torch.float32, device=dev) if obs else None,
+            final_obs=torch.full((K, E, sc.H, sc.W), float("nan"), dtype=torch.float32, device=dev) if final_obs else None,
+            reward=torch.zeros((E, K), **f64), fear=torch.zeros((E, K), **f64), shaped=torch.zeros((E, K), **f64),
+            term=torch.zeros((E, K), dtype=torch.uint8, device=dev),
+            trunc=torch.zeros((E, K), dtype=torch.uint8, device=dev),
+            done=torch.zeros(E, dtype=torch.uint8, device=dev),
+            mask=torch.zeros((E, K), dtype=torch.int16, device=dev),
+            crashes=torch.zeros(E, dtype=torch.int32, device=dev),
+            apples=torch.zeros(E, dtype=torch.int32, device=dev),
+            ep_return=torch.zeros(E, **f64), ep_fear=torch.zeros(E, **f64),
+            ep_len=torch.zeros(E, dtype=torch.int32, device=dev),
+            actions=torch.zeros((E, N), dtype=torch.int32, device=dev) if debug else None,
+            mdr=torch.zeros((E, N), dtype=torch.int32, device=dev) if debug else None,
+            final_pos=torch.zeros((E, N), dtype=torch.int32, device=dev) if debug else None,
+            crash_bits=torch.zeros(E, dtype=torch.uint8, device=dev) if debug else None,
+            restr_bits=torch.zeros(E, dtype=torch.uint8, device=dev) if debug else None,
+            stats=torch.zeros((int(self.lib.gw_stats_rows(self.handle)), _lib.GW_STATS), **f64) if stats else None,
+        )
+        self._step_out = _lib.GwStepOut(*[_ptr(self.out[n]) for n in _lib.STEP_OUT_FIELDS])
+        self._closed = False
+
+    # ------------------------------------------------------------------------------------
+    def _stream(self):
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def reset(self, spawn: torch.Tensor | None = None, env_mask: torch.Tensor | None = None):
+        """CustomMAEnv.reset for all envs (or those with env_mask != 0).
+        spawn: [E, N] int32 sorted road cells (replay) or None (device RNG)."""
+        spawn = self._as_i32(spawn, (self.E, self.N))
+        if env_mask is not None:
+            env_mask = env_mask.to(device=self.device, dtype=torch.uint8).contiguous()
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.gw_reset(self.handle, _ptr(env_mask), _ptr(spawn), _ptr(self.out["obs"]),
+                                         _ptr(self.out["mask"]), self._stream()), "gw_reset")
+        return self.out["obs"], self.out["mask"]
+
+    def step(self, rl_actions: torch.Tensor | None = None, scripted: torch.Tensor | None = None,
+             spawn: torch.Tensor | None = None) -> StepResult:
+        """rl_actions [E, K] int32 (None = uniform random RL policy on device);
+        scripted [E, N-K] (replay) or None (scenario policy on device);
+        spawn [E, N] spawns for auto-resetting envs (replay) or None."""
+        rl = self._as_i32(rl_actions, (self.E, self.K))
+        sa = self._as_i32(scripted, (self.E, self.N - self.K))
+        sp = self._as_i32(spawn, (self.E, self.N))
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.gw_step(self.handle, _ptr(rl), _ptr(sa), _ptr(sp), C.byref(self._step_out),
+                                        self._stream()), "gw_step")
+        return StepResult(**self.out)
+
+    def _as_i32(self, t, shape):
+        if t is None:
+            return None
+        if not isinstance(t, torch.Tensor):
+            t = torch.as_tensor(np.asarray(t))
+        t = t.to(device=self.device, dtype=torch.int32).contiguous()
+        if tuple(t.shape) != tuple(shape):
+            t = t.reshape(shape)
+        return t
+
+    # ------------------------------------------------------------------------------------
+    def state(self) -> dict:
+        """Copy of the env state (device tensors): pos [N, E] cells, flags, t, episode,
+        prev_dist [K, E], score, fear_score."""
+        E, N, K, dev = self.E, self.N, self.K, self.device
+        st = dict(pos=torch.empty((N, E), dtype=torch.int32, device=dev),
+                  flags=torch.empty(E, dtype=torch.int32, device=dev),
+                  t=torch.empty(E, dtype=torch.int32, device=dev),
+                  episode=torch.empty(E, dtype=torch.int32, device=dev),
+                  prev_dist=torch.empty((K, E), dtype=torch.int32, device=dev),
+                  score=torch.empty(E, dtype=torch.float64, device=dev),
+                  fear_score=torch.empty(E, dtype=torch.float64, device=dev))
+        gs = _lib.GwState(*[_ptr(st[n]) for n in _lib.STATE_FIELDS])
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.gw_copy_state(self.handle, C.byref(gs), 0, self._stream()), "gw_copy_state")
+        return st
+
+    def set_state(self, st: dict):
+        gs = _lib.GwState(*[_ptr(st[n].contiguous()) if st.get(n) is not None else None
+                            for n in _lib.STATE_FIELDS])
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.gw_copy_state(self.handle, C.byref(gs), 1, self._stream()), "gw_copy_state")
+
+    def profile(self, enable: bool = True):
+        """Record HIP events around each gw_step kernel (see gw_profile)."""
+        _lib.check(self.lib.gw_profile(self.handle, int(enable)), "gw_profile")
+
+    def profile_read(self):
+        """-> (ms summed over timed steps [step_kernel, obs_kernel], number of timed steps)."""
+        ms = (C.c_double * 2)()
+        n = C.c_int64()
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.gw_profile_read(self.handle, ms, C.byref(n)), "gw_profile_read")
+        return (ms[0], ms[1]), n.value
+
+    def positions(self) -> torch.Tensor:
+        return self.state()["pos"].t().contiguous()
+
+    def close(self):
+        if not self._closed and getattr(self, "handle", None):
+            self.lib.gw_destroy(self.handle)
+            self._closed = True
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
