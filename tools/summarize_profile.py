@@ -1,0 +1,68 @@
+"""Summarise a tools/gpu_profile.sh run (rocprofv3 kernel stats + FETCH_SIZE/WRITE_SIZE passes)
+into profiles/<tag>/SUMMARY.md and copy the raw CSVs next to it.
+
+gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports half the bytes of a wide
+coalesced stream -> x2; WRITE_SIZE is exact for 16-B/lane stores.  Both are in KiB."""
+import csv
+import json
+import os
+import shutil
+import sys
+
+
+def main(src, dst):
+    os.makedirs(dst, exist_ok=True)
+    stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
+    pmc = {}
+    for which, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+        path = os.path.join(src, which, "run_counter_collection.csv")
+        if not os.path.exists(path):
+            continue
+        for r in csv.DictReader(open(path)):
+            if r["Counter_Name"] != ctr:
+                continue
+            pmc.setdefault(r["Kernel_Name"], {}).setdefault(ctr, []).append(float(r["Counter_Value"]))
+    lines = [f"# rocprofv3 summary ({os.path.basename(dst)})", "",
+             "| kernel | calls | avg us | min us | max us | % time | FETCH MB/launch (x2 corr.) | WRITE MB/launch | HBM MB/launch |",
+             "|---|---|---|---|---|---|---|---|---|"]
+    out = {}
+    for r in stats:
+        name = r["Name"]
+        p = pmc.get(name, {})
+        f = p.get("FETCH_SIZE")
+        w = p.get("WRITE_SIZE")
+        fmb = (sum(f) / len(f)) * 1024 * 2 / 1e6 if f else None
+        wmb = (sum(w) / len(w)) * 1024 / 1e6 if w else None
+        tot = (fmb or 0) + (wmb or 0) if (f or w) else None
+        short = name.split("(")[0].replace("void ", "")
+        lines.append(f"| `{short}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.2f} | {float(r['MinNs'])/1e3:.2f} | "
+                     f"{float(r['MaxNs'])/1e3:.2f} | {float(r['Percentage']):.1f} | "
+                     f"{'' if fmb is None else f'{fmb:.2f}'} | {'' if wmb is None else f'{wmb:.2f}'} | "
+                     f"{'' if tot is None else f'{tot:.2f}'} |")
+        out[short] = dict(calls=int(r["Calls"]), avg_us=float(r["AverageNs"]) / 1e3, fetch_mb=fmb, write_mb=wmb,
+                          hbm_mb=tot)
+    for log in ("trace.log", "fetch.log", "write.log"):
+        p = os.path.join(src, log)
+        if os.path.exists(p):
+            for l in open(p):
+                if l.startswith("{"):
+                    j = json.loads(l)
+                    lines += ["", f"bench line under `{log}`: value {j['value']:.4g} {j['unit']}, "
+                              f"{j['ms_per_step']:.4f} ms/step, kernels_ms {j.get('kernels_ms')}"]
+    open(os.path.join(dst, "SUMMARY.md"), "w").write("\n".join(lines) + "\n")
+    json.dump(out, open(os.path.join(dst, "summary.json"), "w"), indent=1)
+    for sub in ("trace", "fetch", "write"):
+        for fn in ("run_kernel_stats.csv", "run_counter_collection.csv"):
+            p = os.path.join(src, sub, fn)
+            if os.path.exists(p):
+                shutil.copy(p, os.path.join(dst, f"{sub}_{fn}"))
+    for log in ("trace.log", "fetch.log", "write.log"):
+        p = os.path.join(src, log)
+        if os.path.exists(p):
+            with open(p) as fi, open(os.path.join(dst, log), "w") as fo:
+                fo.writelines(l for l in fi if l.startswith("{"))
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
