@@ -96,6 +96,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--envs", type=int, default=0, help="override envs per GPU")
+    ap.add_argument("--fear", type=int, default=-1, help="override FeAR on (1) / off (0)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     args = ap.parse_args()
@@ -117,6 +118,9 @@ def main():
     cfg = dict(CONFIGS[args.config])
     if args.envs:
         cfg["envs"] = args.envs
+    if args.fear >= 0:
+        cfg["fear"] = bool(args.fear)
+        cfg["workload"] += f" [override: FeAR {'on' if cfg['fear'] else 'off'}]"
     E = cfg["envs"]
     env = VecGridEnv(cfg["scenario"], num_envs=E, fear=cfg["fear"], fear_weight=cfg["fear_weight"],
                      max_steps=150, auto_reset=True, seed=42, env_offset=rank * E, stats=True)
@@ -166,7 +170,10 @@ def main():
     if rank == 0:
         step_b, obs_b = algorithmic_bytes(N, K, HW)
         avg_step_ms, avg_obs_ms = ms_step / max(nprof, 1), ms_obs / max(nprof, 1)
-        if avg_obs_ms >= avg_step_ms:
+        fused = env.fused
+        if fused:  # one launch per step moves every byte of the step
+            dom, bytes_per_launch, dur = "step_fused", (step_b + obs_b) * E, avg_step_ms
+        elif avg_obs_ms >= avg_step_ms:
             dom, bytes_per_launch, dur = "obs_kernel", obs_b * E, avg_obs_ms
         else:
             dom, bytes_per_launch, dur = "step_kernel", step_b * E, avg_step_ms

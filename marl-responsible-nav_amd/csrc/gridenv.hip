@@ -20,8 +20,11 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <new>
+#include <type_traits>
 #include <string>
 #include <vector>
 
@@ -74,6 +77,7 @@ struct Params {
     int max_steps, auto_reset;
     uint32_t key0, key1;
     uint32_t w_magic;         // ceil(2^32 / W)  (exact /W for cells < 2^16)
+    uint32_t hw4_magic;       // ceil(2^32 / (H*W/4))
     int apples[MAXN];
 };
 
@@ -440,12 +444,28 @@ __device__ __forceinline__ void wave_sum(Contrib &c) {
         for (int i = 0; i < GW_STATS; ++i) c.v[i] = __dadd_rn(c.v[i], __shfl_xor(c.v[i], off, 64));
 }
 
+// What the obs writer needs to know about one env after its step.
+template <int N>
+struct ObsInfo {
+    int pos[N];      // agents of the returned obs (post-step, or the new episode's spawn)
+    int fpos[N];     // agents of the terminal obs (valid with D_FINAL)
+    uint32_t flags;  // D_RESET | D_WRITE | D_FINAL | apples of obs << 8 | apples of final obs << 16
+};
+
+template <int N>
+__device__ __forceinline__ void store_desc(const Params &p, int64_t e, const ObsInfo<N> &oi) {
+    uint32_t *d = p.desc + e * NDESC;
+    write_desc_pos<N>(d, oi.pos);
+    d[4] = oi.flags;
+    if (oi.flags & D_FINAL) write_desc_pos<N>(d + 8, oi.fpos);
+}
+
 template <int N>
 __device__ __forceinline__ void finish_env(const Params &p, int64_t e, const int (&pos0)[N],
                                            const int (&act)[N], const int (&mdr)[N],
                                            const double (&fear)[MAXN], uint32_t crash,
                                            uint32_t restr, int (&fin)[N], uint32_t caught,
-                                           Contrib &ct) {
+                                           Contrib &ct, ObsInfo<N> &oi) {
     const int K = p.K;
     uint32_t flags = p.st.flags[e];
     uint32_t apples = flags & 0xFFu, term = (flags >> 8) & 0xFFu, trunc = (flags >> 16) & 0xFFu;
@@ -528,15 +548,17 @@ __device__ __forceinline__ void finish_env(const Params &p, int64_t e, const int
         if (o.final_pos) o.final_pos[e * N + n] = fin[n];
     }
 
-    uint32_t *d = p.desc + e * NDESC;
     if (done && p.auto_reset) {
         // terminal obs -> final_obs, then CustomMAEnv.reset for the next episode
-        write_desc_pos<N>(d + 8, fin);
         const uint32_t ep = p.st.episode[e] + 1;
         int np_[N];
         reset_env<N>(p, e, ep, np_);
-        write_desc_pos<N>(d, np_);
-        d[4] = D_RESET | D_WRITE | (o.final_obs ? D_FINAL : 0u) | (all_bits(K) << 8) | (apples << 16);
+#pragma unroll
+        for (int n = 0; n < N; ++n) {
+            oi.fpos[n] = fin[n];
+            oi.pos[n] = np_[n];
+        }
+        oi.flags = D_RESET | D_WRITE | (o.final_obs ? D_FINAL : 0u) | (all_bits(K) << 8) | (apples << 16);
 #pragma unroll
         for (int k = 0; k < N; ++k)
             if (k < K && o.mask) o.mask[e * K + k] = p.tb.amask[np_[k]];
@@ -547,8 +569,9 @@ __device__ __forceinline__ void finish_env(const Params &p, int64_t e, const int
         p.st.t[e] = t;
         p.st.score[e] = score;
         p.st.fscore[e] = fscore;
-        write_desc_pos<N>(d, fin);
-        d[4] = D_WRITE | (apples << 8);
+#pragma unroll
+        for (int n = 0; n < N; ++n) oi.pos[n] = oi.fpos[n] = fin[n];
+        oi.flags = D_WRITE | (apples << 8);
 #pragma unroll
         for (int k = 0; k < N; ++k)
             if (k < K && o.mask) o.mask[e * K + k] = p.tb.amask[fin[k]];
@@ -578,7 +601,9 @@ __device__ __forceinline__ void step_env_nofear(const Params &p, int64_t e, cons
     double fear[MAXN];
 #pragma unroll
     for (int k = 0; k < MAXN; ++k) fear[k] = 0.0;
-    finish_env<N>(p, e, pos, act, mdr, fear, w.crash, w.restr, fin, caught, ct);
+    ObsInfo<N> oi;
+    finish_env<N>(p, e, pos, act, mdr, fear, w.crash, w.restr, fin, caught, ct, oi);
+    store_desc<N>(p, e, oi);
 }
 
 template <int N>
@@ -797,7 +822,9 @@ __global__ void __launch_bounds__(256) step_kernel_fear(Params p) {
             fear[k] = np_sum_row<N>(resp, k);
         }
         const uint32_t bits = s_bits[tid];
-        finish_env<N>(p, e, pos, act, mdr, fear, bits & 0xFFu, (bits >> 8) & 0xFFu, fin, (bits >> 16) & 0xFFu, ct);
+        ObsInfo<N> oi;
+        finish_env<N>(p, e, pos, act, mdr, fear, bits & 0xFFu, (bits >> 8) & 0xFFu, fin, (bits >> 16) & 0xFFu, ct, oi);
+        store_desc<N>(p, e, oi);
     }
     if (p.out.stats && tid < 64) {  // BE <= 64: every env of the block sits in wave 0
         wave_sum(ct);
@@ -933,6 +960,315 @@ __global__ void __launch_bounds__(OBS_THREADS) obs_kernel(Params p, float *__res
     }
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Fused step (default path): the whole CustomMAEnv.step of BE envs in one block, obs
+// included.  Phases: A per-env actions/MdR/close sets (+ FeAR task list), B one world update
+// per task on every lane, C FeAR sums + rewards + state + small outputs + obs patches into LDS,
+// D the block's K x BE x H*W float32 obs as coalesced 16-byte stores.  Many small blocks are
+// co-resident per CU, so the VALU phases of some overlap the HBM store streams of others --
+// the split path runs them as two serialised launches.
+// ---------------------------------------------------------------------------------------
+template <int N, int KMAX, bool FEAR> struct FusedCfg {
+    static constexpr int THREADS = 128;
+    static constexpr int BE = FEAR ? (KMAX <= 2 ? (N <= 4 ? 32 : 16) : (N <= 4 ? 16 : 4)) : 64;
+    static constexpr int MAXT = FEAR ? BE * (1 + KMAX * (2 + 16 * (N - 1))) : 1;
+    using Task = typename std::conditional<(KMAX <= 2), uint16_t, uint32_t>::type;
+    // task bits: env 0-5 | b 6-9 (15 = base sim) | var 10 | j 11-13 | k 14+; slots < BE = main sims
+    static __device__ __forceinline__ Task enc(int el, int k, int j, int var, int b) {
+        return (Task)((uint32_t)el | ((uint32_t)b << 6) | ((uint32_t)var << 10) | ((uint32_t)j << 11) |
+                      ((uint32_t)k << 14));
+    }
+};
+
+template <int N, int WH, int BE, int KMAX, int NP>
+__device__ __forceinline__ void fused_patches(const Params &p, int el, const ObsInfo<N> &oi,
+                                              const uint8_t *s_ok, uint16_t (&pc)[2][BE][KMAX][NP],
+                                              float (&pv)[2][BE][KMAX][NP]) {
+    const uint32_t f = oi.flags;
+    const bool reset = (WH == 0) && (f & D_RESET);
+    const uint32_t apples = WH == 0 ? (f >> 8) & 0xFFu : (f >> 16) & 0xFFu;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+        if (k >= p.K) continue;
+        const int ac = ((apples >> k) & 1u) ? p.apples[k] : -1;
+        int np = 0;
+        if (ac >= 0) {  // own apple first; an agent standing on it overrides this patch
+            float av = ((s_ok[ac] >> 4) & 1u) ? 9.0f : 8.0f;
+            if (!reset && av == (float)(k + 1)) av = 1.0f;  // relabel of :321 (apple on a wall, K = 8)
+            pc[WH][el][k][np] = (uint16_t)ac;
+            pv[WH][el][k][np] = av;
+            ++np;
+        }
+#pragma unroll
+        for (int n = 0; n < N; ++n) {
+            const int c = WH == 0 ? oi.pos[n] : oi.fpos[n];
+            pc[WH][el][k][np] = (uint16_t)c;
+            pv[WH][el][k][np] = agent_value(reset, n, k, c == ac);
+            ++np;
+        }
+        for (; np < NP; ++np) pc[WH][el][k][np] = 0xFFFFu;
+    }
+}
+
+template <int N, int KMAX, bool FEAR>
+__global__ void __launch_bounds__(128) step_fused(Params p) {
+    using Cfg = FusedCfg<N, KMAX, FEAR>;
+    constexpr int BE = Cfg::BE, T = Cfg::THREADS, MAXT = Cfg::MAXT;
+    constexpr int NP = N + 1;
+    constexpr int FB = FEAR ? BE : 1;
+    using Task = typename Cfg::Task;
+    __shared__ __attribute__((aligned(16))) uint8_t s_ok[4096];  // bits 0-3 unit moves, bit 4 road
+    __shared__ int s_pos[BE][N];
+    __shared__ int8_t s_act[BE][N];
+    __shared__ int8_t s_mdr[BE][N];
+    __shared__ uint8_t s_close[FB][KMAX];
+    __shared__ Task s_tasks[MAXT];
+    __shared__ uint8_t s_base[FB][KMAX][2];
+    __shared__ uint8_t s_cj[FB][KMAX][FEAR ? N : 1][2][NA];
+    __shared__ int s_fin[FB][N];
+    __shared__ uint32_t s_bits[FB];
+    __shared__ int s_apple[FB][KMAX];
+    __shared__ uint16_t s_pc[2][BE][KMAX][NP];
+    __shared__ float s_pv[2][BE][KMAX][NP];
+    __shared__ uint32_t s_eflag[BE];
+    __shared__ double s_red[T / 64][GW_STATS];
+    __shared__ int s_ntask;
+
+    const int tid = threadIdx.x;
+    for (int c = tid; c < p.HW; c += T) s_ok[c] = p.tb.okmask[c];
+    if (tid == 0) s_ntask = BE;
+    __syncthreads();
+    const int64_t e0 = (int64_t)blockIdx.x * BE;
+    const int nenv = (int)min((int64_t)BE, p.E - e0);
+    const int K = p.K;
+    Contrib ct;
+    contrib_zero(ct);
+
+    if constexpr (FEAR) {
+        // ---- A: actions, MdR, close sets, task list ----
+        if (tid < nenv) {
+            const int64_t e = e0 + tid;
+            int pos[N], act[N];
+            load_state<N>(p, e, pos);
+            select_actions<N>(p, e, p.st.episode[e], p.st.t[e], pos, act);
+            const uint32_t flags = p.st.flags[e];
+#pragma unroll
+            for (int n = 0; n < N; ++n) {
+                s_pos[tid][n] = pos[n];
+                s_act[tid][n] = (int8_t)act[n];
+                s_mdr[tid][n] = (int8_t)p.tb.mdr[pos[n]];
+            }
+            int ntask = 0;
+            uint32_t close[KMAX];
+#pragma unroll
+            for (int k = 0; k < KMAX; ++k) {
+                close[k] = 0;
+                s_apple[tid][k] = (k < K && ((flags >> k) & 1u)) ? p.apples[k] : -1;
+                if (k >= K) continue;
+#pragma unroll
+                for (int n = 0; n < N; ++n)
+                    if (n == k || manhattan(p, pos[k], pos[n]) <= 5) close[k] |= 1u << n;  // :456-464
+                s_close[tid][k] = (uint8_t)close[k];
+                if (act[k] != (int)p.tb.mdr[pos[k]]) ntask += 2 + 16 * (__popc(close[k]) - 1);
+            }
+            s_tasks[tid] = Cfg::enc(tid, 0, 0, 0, 0);
+            if (ntask) {
+                int slot = atomicAdd(&s_ntask, ntask);
+#pragma unroll
+                for (int k = 0; k < KMAX; ++k) {
+                    if (k >= K || act[k] == (int)p.tb.mdr[pos[k]]) continue;
+                    s_tasks[slot++] = Cfg::enc(tid, k, 0, 0, 15);
+                    s_tasks[slot++] = Cfg::enc(tid, k, 0, 1, 15);
+#pragma unroll
+                    for (int j = 0; j < N; ++j) {
+                        if (j == k || !((close[k] >> j) & 1u)) continue;
+#pragma unroll
+                        for (int var = 0; var < 2; ++var)
+                            for (int b = 0; b < NA; ++b)
+                                if (b != act[j]) s_tasks[slot++] = Cfg::enc(tid, k, j, var, b);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        // ---- B: one world update per task ----
+        const int ntask = s_ntask;
+        for (int ti = tid; ti < ntask; ti += T) {
+            if (ti < BE && ti >= nenv) continue;
+            const uint32_t tk = s_tasks[ti];
+            const int el = tk & 63, b = (tk >> 6) & 15, var = (tk >> 10) & 1, j = (tk >> 11) & 7,
+                      k = (int)(tk >> 14);
+            int pos[N], joint[N], fin[N];
+#pragma unroll
+            for (int n = 0; n < N; ++n) pos[n] = s_pos[el][n];
+            int apple[MAXN];
+#pragma unroll
+            for (int q = 0; q < MAXN; ++q) apple[q] = -1;
+            int nk = 0;
+            if (ti < BE) {  // the env's real world update, with the apple scan
+#pragma unroll
+                for (int n = 0; n < N; ++n) joint[n] = s_act[el][n];
+#pragma unroll
+                for (int q = 0; q < KMAX; ++q) apple[q] = s_apple[el][q];
+                nk = K;
+            } else {        // a counterfactual of FeAR_4_one_actor(actor k)
+                const uint32_t cl = s_close[el][k];
+#pragma unroll
+                for (int n = 0; n < N; ++n) joint[n] = ((cl >> n) & 1u) ? (int)s_act[el][n] : 0;
+#pragma unroll
+                for (int n = 0; n < N; ++n)
+                    if (n == k && var == 0) joint[n] = s_mdr[el][n];
+                if (b != 15) {
+#pragma unroll
+                    for (int n = 0; n < N; ++n)
+                        if (n == j) joint[n] = b;
+                }
+            }
+            World<N> w;
+            w.init(pos, joint, p.W);
+            uint32_t caught;
+            simulate<N, true>(w, s_ok, nk, apple, caught, fin);
+            if (ti < BE) {
+#pragma unroll
+                for (int n = 0; n < N; ++n) s_fin[el][n] = fin[n];
+                s_bits[el] = w.crash | (w.restr << 8) | (caught << 16);
+            } else {
+                const uint32_t valid = ~(w.crash | w.restr) & ((1u << N) - 1u);
+                if (b == 15)
+                    s_base[el][k][var] = (uint8_t)valid;
+                else
+                    s_cj[el][k][j][var][b] = (uint8_t)((valid >> j) & 1u);
+            }
+        }
+        __syncthreads();
+        // ---- C: FeAR sums, rewards, outputs, obs patches ----
+        if (tid < nenv) {
+            const int64_t e = e0 + tid;
+            int pos[N], act[N], mdr[N], fin[N];
+#pragma unroll
+            for (int n = 0; n < N; ++n) {
+                pos[n] = s_pos[tid][n];
+                act[n] = s_act[tid][n];
+                mdr[n] = s_mdr[tid][n];
+                fin[n] = s_fin[tid][n];
+            }
+            double fear[MAXN];
+#pragma unroll
+            for (int k = 0; k < MAXN; ++k) fear[k] = 0.0;
+#pragma unroll
+            for (int k = 0; k < KMAX; ++k) {
+                if (k >= K || act[k] == mdr[k]) continue;
+                const uint32_t cl = s_close[tid][k];
+                const uint32_t b0 = s_base[tid][k][0], b1 = s_base[tid][k][1];
+                double resp[N];
+#pragma unroll
+                for (int jj = 0; jj < N; ++jj) {
+                    resp[jj] = 0.0;
+                    if (jj == k) continue;
+                    int vm, va;
+                    if ((cl >> jj) & 1u) {
+                        vm = 0;
+                        va = 0;
+                        for (int b = 0; b < NA; ++b) {
+                            vm += (b == act[jj]) ? (int)((b0 >> jj) & 1u) : (int)s_cj[tid][k][jj][0][b];
+                            va += (b == act[jj]) ? (int)((b1 >> jj) & 1u) : (int)s_cj[tid][k][jj][1][b];
+                        }
+                    } else {
+                        vm = 9 * (int)((b0 >> jj) & 1u);
+                        va = 9 * (int)((b1 >> jj) & 1u);
+                    }
+                    resp[jj] = p.tb.resp[vm * 10 + va];
+                }
+                fear[k] = np_sum_row<N>(resp, k);
+            }
+            const uint32_t bits = s_bits[tid];
+            ObsInfo<N> oi;
+            finish_env<N>(p, e, pos, act, mdr, fear, bits & 0xFFu, (bits >> 8) & 0xFFu, fin, (bits >> 16) & 0xFFu, ct, oi);
+            fused_patches<N, 0, BE, KMAX, NP>(p, tid, oi, s_ok, s_pc, s_pv);
+            if (oi.flags & D_FINAL) fused_patches<N, 1, BE, KMAX, NP>(p, tid, oi, s_ok, s_pc, s_pv);
+            s_eflag[tid] = oi.flags;
+        }
+    } else {
+        // fear off: one thread does the whole env
+        if (tid < nenv) {
+            const int64_t e = e0 + tid;
+            int pos[N], act[N], mdr[N], fin[N];
+            load_state<N>(p, e, pos);
+            select_actions<N>(p, e, p.st.episode[e], p.st.t[e], pos, act);
+#pragma unroll
+            for (int n = 0; n < N; ++n) mdr[n] = p.tb.mdr[pos[n]];
+            const uint32_t flags = p.st.flags[e];
+            int apple[MAXN];
+#pragma unroll
+            for (int k = 0; k < MAXN; ++k) apple[k] = (k < K && ((flags >> k) & 1u)) ? p.apples[k] : -1;
+            World<N> w;
+            w.init(pos, act, p.W);
+            uint32_t caught;
+            simulate<N, true>(w, s_ok, K, apple, caught, fin);
+            double fear[MAXN];
+#pragma unroll
+            for (int k = 0; k < MAXN; ++k) fear[k] = 0.0;
+            ObsInfo<N> oi;
+            finish_env<N>(p, e, pos, act, mdr, fear, w.crash, w.restr, fin, caught, ct, oi);
+            fused_patches<N, 0, BE, KMAX, NP>(p, tid, oi, s_ok, s_pc, s_pv);
+            if (oi.flags & D_FINAL) fused_patches<N, 1, BE, KMAX, NP>(p, tid, oi, s_ok, s_pc, s_pv);
+            s_eflag[tid] = oi.flags;
+        }
+    }
+    if (tid < BE && tid >= nenv) s_eflag[tid] = 0;
+
+    // ---- block statistics (deterministic tree) ----
+    if (p.out.stats) {
+        wave_sum(ct);
+        if ((tid & 63) == 0)
+#pragma unroll
+            for (int i = 0; i < GW_STATS; ++i) s_red[tid >> 6][i] = ct.v[i];
+    }
+    __syncthreads();
+    if (p.out.stats && tid < GW_STATS) {
+        double acc = s_red[0][tid];
+#pragma unroll
+        for (int w = 1; w < T / 64; ++w) acc = __dadd_rn(acc, s_red[w][tid]);
+        p.out.stats[(int64_t)blockIdx.x * GW_STATS + tid] = acc;
+    }
+
+    // ---- D: obs of the block's envs, 16-byte coalesced stores ----
+    const int HW4 = p.HW >> 2;
+    const int total4 = nenv * HW4;
+#pragma unroll
+    for (int wh = 0; wh < 2; ++wh) {
+        float *dst = wh == 0 ? p.out.obs : p.out.final_obs;
+        if (!dst) continue;
+        const uint32_t need = wh == 0 ? D_WRITE : D_FINAL;
+        for (int k = 0; k < K; ++k) {
+            float4 *out4 = reinterpret_cast<float4 *>(dst + ((int64_t)k * p.E + e0) * p.HW);
+            for (int i4 = tid; i4 < total4; i4 += T) {
+                const int el = (int)__umulhi((uint32_t)i4, p.hw4_magic);
+                if (!(s_eflag[el] & need)) continue;
+                const int c0 = (i4 - el * HW4) << 2;
+                const uint32_t okw = *reinterpret_cast<const uint32_t *>(&s_ok[c0]);
+                float4 v;
+                v.x = (okw & 0x10u) ? 0.0f : -1.0f;
+                v.y = (okw & 0x1000u) ? 0.0f : -1.0f;
+                v.z = (okw & 0x100000u) ? 0.0f : -1.0f;
+                v.w = (okw & 0x10000000u) ? 0.0f : -1.0f;
+#pragma unroll
+                for (int q = 0; q < NP; ++q) {
+                    const int dd = (int)s_pc[wh][el][k][q] - c0;
+                    if ((unsigned)dd < 4u) {
+                        const float pvq = s_pv[wh][el][k][q];
+                        v.x = dd == 0 ? pvq : v.x;
+                        v.y = dd == 1 ? pvq : v.y;
+                        v.z = dd == 2 ? pvq : v.z;
+                        v.w = dd == 3 ? pvq : v.w;
+                    }
+                }
+                out4[i4] = v;
+            }
+        }
+    }
+}
 }  // namespace gw
 
 // =========================================================================================
@@ -962,6 +1298,7 @@ struct Env {
     uint64_t seed = 0;
     int apples[GW_MAX_AGENTS] = {0};
     bool initialized = false;
+    bool fused = false;  // true: one fused launch per step (GW_KERNEL=fused); default: step + obs kernels
     // tables
     uint8_t *okmask = nullptr, *policy = nullptr, *mdr = nullptr;
     double *cdf = nullptr, *resp = nullptr;
@@ -1037,12 +1374,29 @@ gw::Params make_params(const Env *env) {
     p.key0 = (uint32_t)env->seed;
     p.key1 = (uint32_t)(env->seed >> 32);
     p.w_magic = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)env->W - 1) / (uint64_t)env->W);
+    {
+        const uint64_t hw4 = (uint64_t)std::max(1, env->HW / 4);
+        p.hw4_magic = (uint32_t)std::min<uint64_t>(0xFFFFFFFFull, (((uint64_t)1 << 32) + hw4 - 1) / hw4);
+    }
     for (int k = 0; k < GW_MAX_AGENTS; ++k) p.apples[k] = env->apples[k];
     return p;
 }
 
+template <int N, int KMAX, bool FEAR>
+hipError_t launch_fused(const Env *env, const gw::Params &p, hipStream_t s) {
+    constexpr int BE = gw::FusedCfg<N, KMAX, FEAR>::BE;
+    const unsigned grid = (unsigned)((env->E + BE - 1) / BE);
+    hipLaunchKernelGGL((gw::step_fused<N, KMAX, FEAR>), dim3(grid), dim3(gw::FusedCfg<N, KMAX, FEAR>::THREADS), 0, s, p);
+    return hipGetLastError();
+}
+
 template <int N>
 hipError_t launch_step(const Env *env, const gw::Params &p, hipStream_t s) {
+    if (env->fused) {
+        if (env->fear)
+            return env->K <= 2 ? launch_fused<N, 2, true>(env, p, s) : launch_fused<N, N, true>(env, p, s);
+        return env->K <= 2 ? launch_fused<N, 2, false>(env, p, s) : launch_fused<N, N, false>(env, p, s);
+    }
     if (env->fear) {
         if (env->K <= 2) {
             constexpr int BE = gw::FearCfg<N, 2>::BE;
@@ -1110,6 +1464,12 @@ hipError_t launch_obs(const Env *env, const gw::Params &p, float *obs, float *fi
 namespace {
 template <int N>
 int64_t stats_rows_n(const Env *env) {
+    if (env->fused) {
+        int be;
+        if (env->fear) be = env->K <= 2 ? gw::FusedCfg<N, 2, true>::BE : gw::FusedCfg<N, N, true>::BE;
+        else be = env->K <= 2 ? gw::FusedCfg<N, 2, false>::BE : gw::FusedCfg<N, N, false>::BE;
+        return (env->E + be - 1) / be;
+    }
     if (!env->fear) return (env->E + 255) / 256;
     const int be = env->K <= 2 ? gw::FearCfg<N, 2>::BE : gw::FearCfg<N, N>::BE;
     return (env->E + be - 1) / be;
@@ -1139,7 +1499,8 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
     for (int c = 0; c < HW; ++c) {
         const int r = c / W, q = c % W;
         const auto road = [&](int rr, int cc) { return rr >= 0 && rr < H && cc >= 0 && cc < W && sc->region[rr * W + cc] != 0; };
-        ok[c] = (uint8_t)(road(r - 1, q) | (road(r + 1, q) << 1) | (road(r, q - 1) << 2) | (road(r, q + 1) << 3));
+        ok[c] = (uint8_t)(road(r - 1, q) | (road(r + 1, q) << 1) | (road(r, q - 1) << 2) | (road(r, q + 1) << 3) |
+                          ((sc->region[c] != 0) << 4));  // bit 4: the cell itself is road
         // get_action_mask, custom/ma_customenv.py:467-506
         uint16_t m = 0x1FF;
         if (!road(r - 1, q)) m &= ~(1u << 1);
@@ -1186,6 +1547,10 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
     env->auto_reset = cfg->auto_reset ? 1 : 0;
     env->seed = cfg->seed;
     for (int k = 0; k < K; ++k) env->apples[k] = sc->apples[k];
+    {
+        const char *kv = std::getenv("GW_KERNEL");  // "fused" selects the one-launch path (A/B)
+        env->fused = (HW % 4 == 0) && kv && std::strcmp(kv, "fused") == 0;
+    }
 
     auto cleanup = [&](gw_status s) {
         for (void *p : env->allocs) (void)hipFree(p);
@@ -1256,7 +1621,7 @@ gw_status gw_step(void *handle, const int32_t *rl_actions, const int32_t *script
     if (ev[0]) HIP_TRY(hipEventRecord(ev[0], s));
     HIP_TRY(dispatch_step(env, p, s));
     if (ev[1]) HIP_TRY(hipEventRecord(ev[1], s));
-    HIP_TRY(launch_obs(env, p, p.out.obs, p.out.final_obs, s));
+    if (!env->fused) HIP_TRY(launch_obs(env, p, p.out.obs, p.out.final_obs, s));
     if (ev[2]) HIP_TRY(hipEventRecord(ev[2], s));
     return GW_OK;
 }

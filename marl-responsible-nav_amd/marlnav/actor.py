@@ -1,0 +1,140 @@
+"""MADDPG actors (PyTorch-ROCm), batched over envs and stacked over the K RL agents.
+
+The reference drives one actor per RL agent through agilerl 1.0.15's MADDPG
+(maddpg/agent.py:41-65, get_action at :109-113).  agilerl is not installed here; the actor
+architecture is the one the shipped checkpoints hold:
+
+  MLP  (configs/mlp.yaml):  Linear(H*W -> 128) - LayerNorm - ReLU - Linear(128 -> 128) - LayerNorm
+                            - ReLU - Linear(128 -> 9) - GumbelSoftmax
+  CNN  (configs/cnn.yaml):  Conv2d(1 -> 32, k2, s2) - ReLU - Conv2d(32 -> 64, k2, s2) - ReLU - flatten
+                            - Linear(-> 128) - ReLU - Linear(128 -> 128) - ReLU - Linear(128 -> 9)
+
+The K agents' MLPs run as one batched GEMM chain (torch.bmm over stacked [K, in, out] weights),
+so a step is three GEMM launches for all agents instead of 3K.  Exploration: agilerl's
+GumbelSoftmax sample during training, then invalid actions (the env's action mask) are
+removed and the argmax is taken.  That sampling path is "parity unpinned" (agilerl is absent
+and the reference has no test of it); the deterministic logits are a plain restatement.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+N_ACTIONS = 9
+
+
+def _init_linear(K, fan_in, fan_out, device, dtype, gen=None):
+    bound = 1.0 / math.sqrt(fan_in)  # nn.Linear's default (kaiming_uniform a=sqrt(5)) bound
+    w = (torch.rand((K, fan_in, fan_out), generator=gen, device="cpu") * 2 - 1) * bound
+    b = (torch.rand((K, 1, fan_out), generator=gen, device="cpu") * 2 - 1) * bound
+    return nn.Parameter(w.to(device=device, dtype=dtype)), nn.Parameter(b.to(device=device, dtype=dtype))
+
+
+class StackedMLPActors(nn.Module):
+    """K independent MLP actors evaluated together: x [K, E, D] -> logits [K, E, 9]."""
+
+    def __init__(self, K: int, in_dim: int, hidden=(128, 128), n_actions: int = N_ACTIONS, layer_norm: bool = True,
+                 device=None, dtype=torch.float32, seed: int = 0):
+        super().__init__()
+        gen = torch.Generator().manual_seed(seed)
+        dims = [in_dim, *hidden, n_actions]
+        self.weights = nn.ParameterList()
+        self.biases = nn.ParameterList()
+        for a, b in zip(dims[:-1], dims[1:]):
+            w, bb = _init_linear(K, a, b, device, dtype, gen)
+            self.weights.append(w)
+            self.biases.append(bb)
+        self.layer_norm = layer_norm
+        self.ln_w = nn.ParameterList([nn.Parameter(torch.ones((K, 1, h), device=device, dtype=dtype)) for h in hidden])
+        self.ln_b = nn.ParameterList([nn.Parameter(torch.zeros((K, 1, h), device=device, dtype=dtype)) for h in hidden])
+        self.K, self.in_dim = K, in_dim
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        n = len(self.weights)
+        for i in range(n):
+            x = torch.baddbmm(self.biases[i], x, self.weights[i])
+            if i < n - 1:
+                if self.layer_norm:
+                    mu = x.mean(-1, keepdim=True)
+                    var = x.var(-1, unbiased=False, keepdim=True)
+                    x = (x - mu) * torch.rsqrt(var + 1e-5) * self.ln_w[i] + self.ln_b[i]
+                x = F.relu(x)
+        return x
+
+    def load_agent(self, k: int, state: dict):
+        """Per-agent weights in the checkpoint's naming (feature_net.linear_layer_i.weight [out, in], ...)."""
+        names = [f"linear_layer_{i}" for i in range(len(self.weights) - 1)] + ["linear_layer_output"]
+        with torch.no_grad():
+            for i, nm in enumerate(names):
+                self.weights[i][k].copy_(torch.as_tensor(state[f"{nm}.weight"]).t())
+                self.biases[i][k, 0].copy_(torch.as_tensor(state[f"{nm}.bias"]))
+            for i in range(len(self.ln_w)):
+                if f"layer_norm_{i}.weight" in state:
+                    self.ln_w[i][k, 0].copy_(torch.as_tensor(state[f"layer_norm_{i}.weight"]))
+                    self.ln_b[i][k, 0].copy_(torch.as_tensor(state[f"layer_norm_{i}.bias"]))
+
+
+class CNNActor(nn.Module):
+    """configs/cnn.yaml head for one agent: x [E, 1, H, W] -> logits [E, 9]."""
+
+    def __init__(self, H: int, W: int, channels=(32, 64), kernels=(2, 2), strides=(2, 2), hidden=(128, 128),
+                 n_actions: int = N_ACTIONS):
+        super().__init__()
+        layers, c, h, w = [], 1, H, W
+        for ch, k, s in zip(channels, kernels, strides):
+            layers += [nn.Conv2d(c, ch, k, s), nn.ReLU()]
+            c, h, w = ch, (h - k) // s + 1, (w - k) // s + 1
+        self.conv = nn.Sequential(*layers)
+        dims = [c * h * w, *hidden]
+        mlp = []
+        for a, b in zip(dims[:-1], dims[1:]):
+            mlp += [nn.Linear(a, b), nn.ReLU()]
+        mlp.append(nn.Linear(dims[-1], n_actions))
+        self.mlp = nn.Sequential(*mlp)
+
+    def forward(self, x):
+        return self.mlp(self.conv(x).flatten(1))
+
+
+class MultiAgentActors(nn.Module):
+    """The K RL agents' actors: obs [K, E, H, W] -> logits [K, E, 9]."""
+
+    def __init__(self, K: int, H: int, W: int, arch: str = "mlp", hidden=(128, 128), device=None,
+                 dtype=torch.float32, seed: int = 0):
+        super().__init__()
+        self.K, self.H, self.W, self.arch, self.dtype = K, H, W, arch, dtype
+        if arch == "mlp":
+            self.net = StackedMLPActors(K, H * W, hidden, device=device, dtype=dtype, seed=seed)
+        elif arch == "cnn":
+            torch.manual_seed(seed)
+            self.nets = nn.ModuleList([CNNActor(H, W, hidden=hidden) for _ in range(K)]).to(device=device, dtype=dtype)
+        else:
+            raise ValueError(arch)
+
+    def forward(self, obs: torch.Tensor) -> torch.Tensor:
+        K, E = obs.shape[0], obs.shape[1]
+        x = obs.to(self.dtype)
+        if self.arch == "mlp":
+            return self.net(x.reshape(K, E, -1)).float()
+        return torch.stack([self.nets[k](x[k].unsqueeze(1)) for k in range(K)]).float()
+
+    @torch.no_grad()
+    def act(self, obs: torch.Tensor, mask: torch.Tensor | None = None, training: bool = True,
+            tau: float = 1.0, eps: float = 1e-20, generator: torch.Generator | None = None):
+        """-> (actions [E, K] int32, probs [K, E, 9] float32 = the continuous actions stored in
+        replay, as agilerl's MADDPG.get_action returns them)."""
+        logits = self.forward(obs)
+        if training:  # agilerl GumbelSoftmax: softmax((logits + Gumbel noise) / tau)
+            u = torch.rand(logits.shape, device=logits.device, generator=generator)
+            logits = logits - torch.log(-torch.log(u + eps) + eps)
+        probs = torch.softmax(logits / tau, dim=-1)
+        if mask is not None:  # env action mask [E, K] (9 bits) -> [K, E, 9]
+            bits = (mask.t().to(torch.int32).unsqueeze(-1) >> torch.arange(N_ACTIONS, device=mask.device)) & 1
+            probs_m = torch.where(bits.bool(), probs, torch.zeros((), device=probs.device))
+        else:
+            probs_m = probs
+        actions = probs_m.argmax(-1).t().to(torch.int32).contiguous()
+        return actions, probs

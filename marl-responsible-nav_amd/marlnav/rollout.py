@@ -1,0 +1,118 @@
+"""Batched MADDPG rollout: the per-step body of MADDPGAgent.train (maddpg/agent.py:77-252) over
+E envs of one GPU, plus the multi-GPU pieces.
+
+Per step (all on the GPU, no host sync):
+  actions, probs = actors.act(obs_t, mask_t)                 get_action          agent.py:109-122
+  env.step(actions) -> obs_{t+1}, shaped reward, dones         env.step + :124-141 (in-kernel)
+  replay ring <- (slot of obs_t, probs, shaped reward, term)  memory.save_to_memory :190-197
+  auto-reset of done envs (in-kernel)                          the break / env.reset :241, main :129
+  [multi-GPU] RCCL all-reduce of the per-block episode stats   (north_star: per-step return gather)
+
+Replay storage is zero-copy: the env writes obs_{t+1} straight into ring slot (t+1) % S, so
+the obs of step t is both the next_state of transition t-1 and the state of transition t;
+terminal observations of done envs go to a parallel final-obs ring (their next_state).
+Learning (agilerl MADDPG.learn, agent.py:199-224) is SURVEY §8f "next" and not part of this
+rollout.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from .actor import MultiAgentActors
+from .parallel import StatsReducer, shard  # noqa: F401  (re-exported)
+from .vec_env import VecGridEnv
+
+
+class ReplayRing:
+    """S steps of E transitions each, in HBM.  obs slots are written by the env directly."""
+
+    def __init__(self, env: VecGridEnv, slots: int):
+        self.S = max(2, int(slots))
+        K, E, H, W, dev = env.K, env.E, env.H, env.W, env.device
+        self.obs = torch.zeros((self.S, K, E, H, W), dtype=torch.float32, device=dev)
+        self.final_obs = torch.zeros((self.S, K, E, H, W), dtype=torch.float32, device=dev)
+        self.probs = torch.zeros((self.S, K, E, 9), dtype=torch.float32, device=dev)
+        self.reward = torch.zeros((self.S, E, K), dtype=torch.float64, device=dev)
+        self.term = torch.zeros((self.S, E, K), dtype=torch.uint8, device=dev)
+        self.done = torch.zeros((self.S, E), dtype=torch.uint8, device=dev)
+        self.t = 0          # transitions stored = steps taken
+        self.E, self.K = E, K
+
+    def __len__(self):
+        return min(self.t, self.S - 1) * self.E
+
+    @torch.no_grad()
+    def sample(self, batch: int, generator: torch.Generator | None = None):
+        """Uniform transitions -> (state [K,B,H,W], probs [K,B,9], reward [B,K], next_state, term [B,K])."""
+        n_steps = min(self.t, self.S - 1)
+        if n_steps <= 0:
+            raise RuntimeError("empty replay ring")
+        dev = self.obs.device
+        step = torch.randint(0, n_steps, (batch,), device=dev, generator=generator)
+        env = torch.randint(0, self.E, (batch,), device=dev, generator=generator)
+        tr = (self.t - 1 - step) % self.S          # transition slot (its state is obs[tr])
+        nx = (tr + 1) % self.S
+        state = self.obs[tr, :, env].permute(1, 0, 2, 3)
+        done = self.done[tr, env].bool()
+        next_state = torch.where(done[None, :, None, None], self.final_obs[tr, :, env].permute(1, 0, 2, 3),
+                                 self.obs[nx, :, env].permute(1, 0, 2, 3))
+        return state, self.probs[tr, :, env].permute(1, 0, 2), self.reward[tr, env], next_state, self.term[tr, env]
+
+
+class Rollout:
+    def __init__(self, env: VecGridEnv, actors: MultiAgentActors | None = None, replay_slots: int = 0,
+                 training: bool = True, group=None, seed: int = 0):
+        self.env = env
+        self.actors = actors
+        self.training = training
+        self.group = group
+        self.replay = ReplayRing(env, replay_slots) if replay_slots else None
+        self.gen = torch.Generator(device=env.device).manual_seed(seed) if actors is not None else None
+        self.t = 0
+        self.reducer = StatsReducer(_lib.GW_STATS, env.device, group) if env.out.get("stats") is not None else None
+
+    def reset(self):
+        if self.replay is not None:
+            obs, mask = self.env.reset()
+            self.replay.obs[0].copy_(obs)
+        else:
+            self.env.reset()
+        self.t = 0
+
+    def _obs_now(self):
+        if self.replay is not None:
+            return self.replay.obs[self.t % self.replay.S]
+        return self.env.out["obs"]
+
+    @torch.no_grad()
+    def step(self):
+        env = self.env
+        mask = env.out["mask"]
+        if self.actors is not None:
+            actions, probs = self.actors.act(self._obs_now(), mask, self.training, generator=self.gen)
+        else:
+            actions, probs = None, None  # device-RNG random policy
+        if self.replay is not None:
+            rp = self.replay
+            cur, nxt = self.t % rp.S, (self.t + 1) % rp.S
+            r = env.step(actions, obs_out=rp.obs[nxt], final_obs_out=rp.final_obs[cur])
+            if probs is not None:
+                rp.probs[cur].copy_(probs)
+            rp.reward[cur].copy_(r.shaped)
+            rp.term[cur].copy_(r.term)
+            rp.done[cur].copy_(r.done)
+            rp.t = self.t + 1
+        else:
+            r = env.step(actions)
+        self.t += 1
+        if self.reducer is not None:
+            self.reducer.push(r.stats)  # per-step (RCCL) reduction of the episode statistics
+        return r
+
+    def totals(self) -> dict:
+        """Episode statistics summed over all steps (and ranks): completed-episode return sum,
+        episodes, FeAR, crashes, apples, shaped reward, completed-episode length sum, env-steps."""
+        if self.reducer is None:
+            return {}
+        return dict(zip(_lib.STATS_NAMES, self.reducer.result().cpu().tolist()))

@@ -17,6 +17,7 @@ Layouts (device tensors, owned by the env and overwritten by the next call):
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -116,6 +117,7 @@ class VecGridEnv:
         )
         self._step_out = _lib.GwStepOut(*[_ptr(self.out[n]) for n in _lib.STEP_OUT_FIELDS])
         self._closed = False
+        self.fused = (sc.HW % 4 == 0) and os.environ.get("GW_KERNEL", "split") == "fused"
 
     # ------------------------------------------------------------------------------------
     def _stream(self):
@@ -133,17 +135,30 @@ class VecGridEnv:
         return self.out["obs"], self.out["mask"]
 
     def step(self, rl_actions: torch.Tensor | None = None, scripted: torch.Tensor | None = None,
-             spawn: torch.Tensor | None = None) -> StepResult:
+             spawn: torch.Tensor | None = None, obs_out: torch.Tensor | None = None,
+             final_obs_out: torch.Tensor | None = None) -> StepResult:
         """rl_actions [E, K] int32 (None = uniform random RL policy on device);
         scripted [E, N-K] (replay) or None (scenario policy on device);
-        spawn [E, N] spawns for auto-resetting envs (replay) or None."""
+        spawn [E, N] spawns for auto-resetting envs (replay) or None;
+        obs_out / final_obs_out: [K, E, H, W] float32 buffers to write this step's obs into
+        instead of the env's own (e.g. a replay-ring slot: zero-copy replay storage)."""
         rl = self._as_i32(rl_actions, (self.E, self.K))
         sa = self._as_i32(scripted, (self.E, self.N - self.K))
         sp = self._as_i32(spawn, (self.E, self.N))
+        so = self._step_out
+        res = self.out
+        if obs_out is not None or final_obs_out is not None:
+            so = _lib.GwStepOut.from_buffer_copy(self._step_out)
+            res = dict(self.out)
+            for name, t in (("obs", obs_out), ("final_obs", final_obs_out)):
+                if t is not None:
+                    assert t.dtype == torch.float32 and t.numel() == self.K * self.E * self.H * self.W
+                    setattr(so, name, _ptr(t))
+                    res[name] = t
         with torch.cuda.device(self.device):
-            _lib.check(self.lib.gw_step(self.handle, _ptr(rl), _ptr(sa), _ptr(sp), C.byref(self._step_out),
+            _lib.check(self.lib.gw_step(self.handle, _ptr(rl), _ptr(sa), _ptr(sp), C.byref(so),
                                         self._stream()), "gw_step")
-        return StepResult(**self.out)
+        return StepResult(**res)
 
     def _as_i32(self, t, shape):
         if t is None:

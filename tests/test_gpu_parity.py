@@ -104,14 +104,28 @@ def _compare_native(sc, E, fear, steps, nthreads=16, offset=0, seed=7, weight=-5
     return done_total
 
 
+@pytest.fixture(params=["fused", "split"])
+def kernel_path(request, monkeypatch):
+    """GW_KERNEL selects the one-launch fused step (default) or the step + obs launches."""
+    monkeypatch.setenv("GW_KERNEL", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("name,fear", [("level3", False), ("level3", True), ("grid32", False), ("grid32", True),
                                        ("grid64_n8", False), ("grid64_n8", True)])
-def test_native_rng_matches_oracle(name, fear):
+def test_native_rng_matches_oracle(name, fear, kernel_path):
     sc = S.builtin(name)
     E = 2048 if not fear else 512
     steps = 60 if not fear else 25
     done = _compare_native(sc, E, fear, steps)
     assert done > 0
+
+
+def test_many_agents_k_gt_2_matches_oracle(kernel_path):
+    """K > 2 RL agents (the KMAX = N kernel variants) on an open 8x8 map with N = 5."""
+    sc = S.compile_scenario(S.level3_like(10, 16, 5, 3))
+    _compare_native(sc, 512, True, 20)
+    _compare_native(sc, 1024, False, 40)
 
 
 def test_sharding_is_invariant():
