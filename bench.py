@@ -199,7 +199,8 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "bytes_per_launch": bytes_per_launch, "avg_launch_ms": dur},
             "kernels_ms": {"step_kernel": avg_step_ms, "obs_kernel": avg_obs_ms,
-                           "stream_ms_per_step": gpu_ms / args.steps},
+                           "stream_ms_per_step": gpu_ms / args.steps,
+                           "pipeline_chunks": int(os.environ.get("GW_CHUNKS", "4")) if not env.fused else 1},
             "last_step_episodes": {"completed": stats[1], "mean_return": stats[0] / max(stats[1], 1.0),
                          "mean_len": stats[6] / max(stats[1], 1.0)},
         }

@@ -33,6 +33,12 @@
 namespace gw {
 
 constexpr int NA = GW_N_ACTIONS;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void store_nt(float4 *dst, const float4 &v) {
+    const f32x4 x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<f32x4 *>(dst));
+}
 constexpr int MAXN = GW_MAX_AGENTS;
 constexpr int NDESC = 12;  // u32 words per obs descriptor
 
@@ -50,6 +56,8 @@ struct Tables {
     const int32_t *free_cells;// [F]
     const float *base;        // [HW] 0 road / -1 inactive
     const double *resp;       // [10][10] clip((vm-va)/(vm+EPS),-1,1)
+    const uint32_t *celltab;  // [HW] policy | MdR<<8 | action mask<<12 | unit moves<<21 | road<<25
+    const uint32_t *roadbits; // [ceil(HW/32)] bit c: cell c is road
 };
 
 struct State {
@@ -78,6 +86,9 @@ struct Params {
     uint32_t key0, key1;
     uint32_t w_magic;         // ceil(2^32 / W)  (exact /W for cells < 2^16)
     uint32_t hw4_magic;       // ceil(2^32 / (H*W/4))
+    int lds_cdf, n_cdf, ctab_off;  // step_v2 dynamic LDS: [cdf n_cdf f64 if lds_cdf][cell table]
+    int obs_be;               // envs per obs_kernel block (<= OBS_BE)
+    int64_t e_begin, e_end;   // env range of this launch (step_v2 / obs_kernel chunks)
     int apples[MAXN];
 };
 
@@ -121,6 +132,17 @@ template <> struct SubStep<1> { static constexpr int f1 = 0, c1 = 1, f2 = 1, c2 
 template <> struct SubStep<2> { static constexpr int f1 = 0, c1 = 1, f2 = 1, c2 = 2, ohf1 = 1, ohc1 = 3, ohf2 = 2, ohc2 = 2; };
 template <> struct SubStep<3> { static constexpr int f1 = 1, c1 = 1, f2 = 2, c2 = 2, ohf1 = 0, ohc1 = 0, ohf2 = 0, ohc2 = 0; };
 
+// unit-move bit tables seen by the world update: a byte table (v1 kernels) or the u32 cell
+// table of step_v2 (bits CT_OK..CT_OK+3)
+struct ByteOk {
+    const uint8_t *t;
+    __device__ __forceinline__ uint32_t operator()(int c) const { return t[c]; }
+};
+struct CtabOk {
+    const uint32_t *t;
+    __device__ __forceinline__ uint32_t operator()(int c) const { return t[c] >> 21; }
+};
+
 template <int N>
 struct World {
     int nal[N][5];
@@ -128,9 +150,29 @@ struct World {
     int delta[N];
     uint32_t two, mv, dir0, dir1;   // bit masks: 2-step action, moving action, direction bits
     uint32_t crash, restr;
+    uint32_t near;                  // bit pair(ii, jj): start cells within Manhattan 4
+    // A pair whose start cells are more than 4 apart can never trigger a rule of
+    // collision_checks_and_resolution: every sub-path entry stays within 2 of its own start
+    // (reverts go back to the start), so equal / crossing cells need distance <= 4.  Such
+    // pairs are skipped; with no near pair at all the resolution loop is skipped.
 
-    __device__ __forceinline__ void init(const int (&l)[N], const int (&a)[N], int W) {
-        two = mv = dir0 = dir1 = crash = restr = 0;
+    __device__ __forceinline__ static constexpr int pair_bit(int ii, int jj) {
+        return ii * (2 * N - ii - 1) / 2 + (jj - ii - 1);
+    }
+
+    __device__ __forceinline__ void init(const int (&l)[N], const int (&a)[N], int W, uint32_t w_magic) {
+        two = mv = dir0 = dir1 = crash = restr = near = 0;
+        int rr[N], cc[N];
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            rr[i] = (int)__umulhi((uint32_t)l[i], w_magic);
+            cc[i] = l[i] - rr[i] * W;
+        }
+#pragma unroll
+        for (int ii = 0; ii < N - 1; ++ii)
+#pragma unroll
+            for (int jj = ii + 1; jj < N; ++jj)
+                near |= (uint32_t)(abs(rr[ii] - rr[jj]) + abs(cc[ii] - cc[jj]) <= 4) << pair_bit(ii, jj);
 #pragma unroll
         for (int i = 0; i < N; ++i) {
             loc[i] = l[i];
@@ -162,8 +204,8 @@ struct World {
         return ((two >> i) & 1u) ? a2 : a1;
     }
 
-    template <int S>
-    __device__ __forceinline__ void move(const uint8_t *__restrict__ okm) {  // :462-518
+    template <int S, class OK>
+    __device__ __forceinline__ void move(const OK &okm) {  // :462-518
 #pragma unroll
         for (int i = 0; i < N; ++i) {
             const int old = nal[i][S];
@@ -171,7 +213,7 @@ struct World {
             const bool active_sub = (S == 0) || (S == 1 && ((two >> i) & 1u));
             const bool moving = active_sub && ((mv >> i) & 1u) && !((crash >> i) & 1u);
             if (moving) {
-                const bool ok = (okm[old] >> dir_of(i)) & 1u;
+                const bool ok = (okm(old) >> dir_of(i)) & 1u;
                 nw = ok ? old + delta[i] : old;
                 restr |= (uint32_t)(!ok) << i;
             }
@@ -181,6 +223,7 @@ struct World {
 
     template <int S>
     __device__ __forceinline__ void resolve() {  // collision_checks_and_resolution :233-405
+        if (near == 0) return;  // no pair can collide: every pass counts 0 (crash stays 0)
         for (int pass = 0; pass < 2 * N; ++pass) {
             uint32_t hit = 0;
             int cnt = 0;
@@ -192,6 +235,7 @@ struct World {
                 const int ohc_i = t_i ? SubStep<S>::ohc2 : SubStep<S>::ohc1;
 #pragma unroll
                 for (int jj = ii + 1; jj < N; ++jj) {
+                    if (!((near >> pair_bit(ii, jj)) & 1u)) continue;
                     const int Bf = fl<S>(jj), Bc = ce<S>(jj);
                     const bool t_j = (two >> jj) & 1u;
                     const int ohf_j = t_j ? SubStep<S>::ohf2 : SubStep<S>::ohf1;
@@ -238,32 +282,32 @@ struct World {
     }
 };
 
-template <int N, bool APPLES>
-__device__ __forceinline__ void simulate(World<N> &w, const uint8_t *__restrict__ okm, int K,
+template <int N, bool APPLES, class OK>
+__device__ __forceinline__ void simulate(World<N> &w, const OK &okm, int K,
                                          const int (&apple)[MAXN], uint32_t &caught, int (&fin)[N]) {
     caught = 0;
-    w.template move<0>(okm);
+    w.template move<0, OK>(okm);
     w.template resolve<0>();
     if (APPLES) {
 #pragma unroll
         for (int k = 0; k < N; ++k)
             if (k < K && w.template cf<0>(k) == apple[k]) caught |= 1u << k;
     }
-    w.template move<1>(okm);
+    w.template move<1, OK>(okm);
     w.template resolve<1>();
     if (APPLES) {
 #pragma unroll
         for (int k = 0; k < N; ++k)
             if (k < K && w.template cf<1>(k) == apple[k]) caught |= 1u << k;
     }
-    w.template move<2>(okm);
+    w.template move<2, OK>(okm);
     w.template resolve<2>();
     if (APPLES) {
 #pragma unroll
         for (int k = 0; k < N; ++k)
             if (k < K && w.template cf<2>(k) == apple[k]) caught |= 1u << k;
     }
-    w.template move<3>(okm);
+    w.template move<3, OK>(okm);
     w.template resolve<3>();
 #pragma unroll
     for (int i = 0; i < N; ++i) fin[i] = w.template cf<3>(i);
@@ -444,6 +488,29 @@ __device__ __forceinline__ void wave_sum(Contrib &c) {
         for (int i = 0; i < GW_STATS; ++i) c.v[i] = __dadd_rn(c.v[i], __shfl_xor(c.v[i], off, 64));
 }
 
+// One env's state, loaded once (prefetched before the counterfactual phase in step_v2).
+template <int N>
+struct EnvState {
+    int pos[N];
+    uint32_t flags, episode;
+    int t;
+    int prev[N];
+    double score, fscore;
+};
+
+template <int N>
+__device__ __forceinline__ void load_env(const Params &p, int64_t e, EnvState<N> &s) {
+#pragma unroll
+    for (int n = 0; n < N; ++n) s.pos[n] = p.st.pos[(int64_t)n * p.E + e];
+    s.flags = p.st.flags[e];
+    s.episode = p.st.episode[e];
+    s.t = p.st.t[e];
+#pragma unroll
+    for (int k = 0; k < N; ++k) s.prev[k] = (k < p.K) ? p.st.prev[(int64_t)k * p.E + e] : -1;
+    s.score = p.st.score[e];
+    s.fscore = p.st.fscore[e];
+}
+
 // What the obs writer needs to know about one env after its step.
 template <int N>
 struct ObsInfo {
@@ -461,16 +528,16 @@ __device__ __forceinline__ void store_desc(const Params &p, int64_t e, const Obs
 }
 
 template <int N>
-__device__ __forceinline__ void finish_env(const Params &p, int64_t e, const int (&pos0)[N],
+__device__ __forceinline__ void finish_env(const Params &p, int64_t e, const EnvState<N> &es,
                                            const int (&act)[N], const int (&mdr)[N],
                                            const double (&fear)[MAXN], uint32_t crash,
                                            uint32_t restr, int (&fin)[N], uint32_t caught,
                                            Contrib &ct, ObsInfo<N> &oi) {
     const int K = p.K;
-    uint32_t flags = p.st.flags[e];
+    const uint32_t flags = es.flags;
     uint32_t apples = flags & 0xFFu, term = (flags >> 8) & 0xFFu, trunc = (flags >> 16) & 0xFFu;
     const uint32_t allk = all_bits(K);
-    int t = p.st.t[e] + 1;
+    int t = es.t + 1;
     int rew[MAXN];
 #pragma unroll
     for (int k = 0; k < MAXN; ++k) rew[k] = 0;
@@ -503,14 +570,14 @@ __device__ __forceinline__ void finish_env(const Params &p, int64_t e, const int
         }
         const int d = ((apples >> k) & 1u) ? manhattan(p, fin[k], p.apples[k]) : -1;  // :287-294
         const int64_t pi = (int64_t)k * p.E + e;
-        const int prev = p.st.prev[pi];
+        const int prev = es.prev[k];
         if (prev >= 0 && d >= 0 && prev > d) rew[k] += 1;  // :296-300
         p.st.prev[pi] = d;
         shaped[k] = __dadd_rn(__dmul_rn(p.fear_weight, fear[k]), (double)rew[k]);  // agent.py:130
         fsum_in[k] = fear[k];
     }
-    const double score = __dadd_rn(p.st.score[e], np_sum_small(shaped, K));       // agent.py:173
-    const double fscore = __dadd_rn(p.st.fscore[e], np_sum_small(fsum_in, K));     // agent.py:141
+    const double score = __dadd_rn(es.score, np_sum_small(shaped, K));            // agent.py:173
+    const double fscore = __dadd_rn(es.fscore, np_sum_small(fsum_in, K));          // agent.py:141
     const bool done = ((term & allk) == allk) || ((trunc & allk) == allk) ||
                       (p.max_steps > 0 && t >= p.max_steps);                       // agent.py:241-243
 
@@ -550,7 +617,7 @@ __device__ __forceinline__ void finish_env(const Params &p, int64_t e, const int
 
     if (done && p.auto_reset) {
         // terminal obs -> final_obs, then CustomMAEnv.reset for the next episode
-        const uint32_t ep = p.st.episode[e] + 1;
+        const uint32_t ep = es.episode + 1;
         int np_[N];
         reset_env<N>(p, e, ep, np_);
 #pragma unroll
@@ -584,25 +651,26 @@ __device__ __forceinline__ void finish_env(const Params &p, int64_t e, const int
 template <int N>
 __device__ __forceinline__ void step_env_nofear(const Params &p, int64_t e, const uint8_t *s_ok, Contrib &ct) {
     int pos[N], act[N], mdr[N], fin[N];
-    load_state<N>(p, e, pos);
-    const uint32_t episode = p.st.episode[e];
-    const int t = p.st.t[e];
-    select_actions<N>(p, e, episode, t, pos, act);
+    EnvState<N> es;
+    load_env<N>(p, e, es);
+#pragma unroll
+    for (int n = 0; n < N; ++n) pos[n] = es.pos[n];
+    select_actions<N>(p, e, es.episode, es.t, pos, act);
 #pragma unroll
     for (int n = 0; n < N; ++n) mdr[n] = p.tb.mdr[pos[n]];
-    const uint32_t flags = p.st.flags[e];
+    const uint32_t flags = es.flags;
     int apple[MAXN];
 #pragma unroll
     for (int k = 0; k < MAXN; ++k) apple[k] = (k < p.K && ((flags >> k) & 1u)) ? p.apples[k] : -1;
     World<N> w;
-    w.init(pos, act, p.W);
+    w.init(pos, act, p.W, p.w_magic);
     uint32_t caught;
-    simulate<N, true>(w, s_ok, p.K, apple, caught, fin);
+    simulate<N, true>(w, ByteOk{s_ok}, p.K, apple, caught, fin);
     double fear[MAXN];
 #pragma unroll
     for (int k = 0; k < MAXN; ++k) fear[k] = 0.0;
     ObsInfo<N> oi;
-    finish_env<N>(p, e, pos, act, mdr, fear, w.crash, w.restr, fin, caught, ct, oi);
+    finish_env<N>(p, e, es, act, mdr, fear, w.crash, w.restr, fin, caught, ct, oi);
     store_desc<N>(p, e, oi);
 }
 
@@ -744,9 +812,9 @@ __global__ void __launch_bounds__(256) step_kernel_fear(Params p) {
 #pragma unroll
             for (int q = 0; q < KMAX; ++q) apple[q] = s_apple[el][q];
             World<N> w;
-            w.init(pos, joint, p.W);
+            w.init(pos, joint, p.W, p.w_magic);
             uint32_t caught;
-            simulate<N, true>(w, s_ok, K, apple, caught, fin);
+            simulate<N, true>(w, ByteOk{s_ok}, K, apple, caught, fin);
 #pragma unroll
             for (int n = 0; n < N; ++n) s_fin[el][n] = fin[n];
             s_bits[el] = w.crash | (w.restr << 8) | (caught << 16);
@@ -763,12 +831,12 @@ __global__ void __launch_bounds__(256) step_kernel_fear(Params p) {
                     if (n == j) joint[n] = b;
             }
             World<N> w;
-            w.init(pos, joint, p.W);
+            w.init(pos, joint, p.W, p.w_magic);
             uint32_t caught;
             int no_apple[MAXN];
 #pragma unroll
             for (int q = 0; q < MAXN; ++q) no_apple[q] = -1;
-            simulate<N, true>(w, s_ok, 0, no_apple, caught, fin);  // one sim body in the loop
+            simulate<N, true>(w, ByteOk{s_ok}, 0, no_apple, caught, fin);  // one sim body in the loop
             const uint32_t valid = ~(w.crash | w.restr) & ((1u << N) - 1u);
             if (kind == T_BASE) {
                 s_base[el][k][var] = (uint8_t)valid;
@@ -822,8 +890,10 @@ __global__ void __launch_bounds__(256) step_kernel_fear(Params p) {
             fear[k] = np_sum_row<N>(resp, k);
         }
         const uint32_t bits = s_bits[tid];
+        EnvState<N> es;
+        load_env<N>(p, e, es);
         ObsInfo<N> oi;
-        finish_env<N>(p, e, pos, act, mdr, fear, bits & 0xFFu, (bits >> 8) & 0xFFu, fin, (bits >> 16) & 0xFFu, ct, oi);
+        finish_env<N>(p, e, es, act, mdr, fear, bits & 0xFFu, (bits >> 8) & 0xFFu, fin, (bits >> 16) & 0xFFu, ct, oi);
         store_desc<N>(p, e, oi);
     }
     if (p.out.stats && tid < 64) {  // BE <= 64: every env of the block sits in wave 0
@@ -871,18 +941,19 @@ __device__ __forceinline__ float agent_value(bool reset, int n, int k, bool on_a
     return (float)v;
 }
 
-template <bool VEC4>
+template <bool VEC4, bool NT>
 __global__ void __launch_bounds__(OBS_THREADS) obs_kernel(Params p, float *__restrict__ obs,
                                                           float *__restrict__ final_obs) {
-    __shared__ __attribute__((aligned(16))) float s_base[4096];  // [HW] static map
+    __shared__ uint32_t s_road[128];                   // road bitmask of the map (HW <= 4096)
     __shared__ int s_pc[2][OBS_BE][MAXN][MAXN + 1];    // [which][env][k][patch] cell (-1 none)
     __shared__ float s_pv[2][OBS_BE][MAXN][MAXN + 1];
     __shared__ uint32_t s_flag[OBS_BE];
     const int tid = threadIdx.x;
     const int HW = p.HW, N = p.N, K = p.K;
-    const int64_t e0 = (int64_t)blockIdx.x * OBS_BE;
-    const int nenv = (int)min((int64_t)OBS_BE, p.E - e0);
-    for (int c = tid; c < HW; c += OBS_THREADS) s_base[c] = p.tb.base[c];
+    const int64_t e0 = p.e_begin + (int64_t)blockIdx.x * p.obs_be;
+    if (e0 >= p.e_end) return;  // uniform per block
+    const int nenv = (int)min((int64_t)p.obs_be, p.e_end - e0);
+    for (int w = tid; w < (HW + 31) / 32; w += OBS_THREADS) s_road[w] = p.tb.roadbits[w];
     // patches: one thread per (which, env, k)
     if (tid < 2 * OBS_BE * MAXN) {
         const int which = tid / (OBS_BE * MAXN), el = (tid / MAXN) % OBS_BE, k = tid % MAXN;
@@ -925,21 +996,29 @@ __global__ void __launch_bounds__(OBS_THREADS) obs_kernel(Params p, float *__res
             for (int k = 0; k < K; ++k) {
                 float4 *out4 = reinterpret_cast<float4 *>(dst + ((int64_t)k * p.E + e0) * HW);
                 for (int i4 = tid; i4 < total4; i4 += OBS_THREADS) {
-                    const int el = i4 / HW4;
+                    const int el = HW4 == 1 ? i4 : (int)__umulhi((uint32_t)i4, p.hw4_magic);
                     if (!(s_flag[el] & need)) continue;
                     const int c0 = (i4 - el * HW4) << 2;
-                    float4 v = *reinterpret_cast<const float4 *>(&s_base[c0]);
+                    const uint32_t rb = s_road[c0 >> 5] >> (c0 & 31);  // 4 cells share one word
+                    float4 v;
+                    v.x = (rb & 1u) ? 0.0f : -1.0f;
+                    v.y = (rb & 2u) ? 0.0f : -1.0f;
+                    v.z = (rb & 4u) ? 0.0f : -1.0f;
+                    v.w = (rb & 8u) ? 0.0f : -1.0f;
                     for (int q = 0; q < npatch; ++q) {
                         const int dd = s_pc[which][el][k][q] - c0;
                         if ((unsigned)dd < 4u) {
                             const float pv = s_pv[which][el][k][q];
-                            if (dd == 0) v.x = pv;
-                            else if (dd == 1) v.y = pv;
-                            else if (dd == 2) v.z = pv;
-                            else v.w = pv;
+                            v.x = dd == 0 ? pv : v.x;
+                            v.y = dd == 1 ? pv : v.y;
+                            v.z = dd == 2 ? pv : v.z;
+                            v.w = dd == 3 ? pv : v.w;
                         }
                     }
-                    out4[i4] = v;
+                    if (NT)
+                        store_nt(&out4[i4], v);
+                    else
+                        out4[i4] = v;
                 }
             }
         } else {
@@ -950,7 +1029,7 @@ __global__ void __launch_bounds__(OBS_THREADS) obs_kernel(Params p, float *__res
                     const int el = i / HW;
                     if (!(s_flag[el] & need)) continue;
                     const int c = i - el * HW;
-                    float v = s_base[c];
+                    float v = ((s_road[c >> 5] >> (c & 31)) & 1u) ? 0.0f : -1.0f;
                     for (int q = 0; q < npatch; ++q)
                         if (s_pc[which][el][k][q] == c) v = s_pv[which][el][k][q];
                     o[i] = v;
@@ -960,18 +1039,23 @@ __global__ void __launch_bounds__(OBS_THREADS) obs_kernel(Params p, float *__res
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// step_v2 (default): CustomMAEnv.step of BE envs per 128-thread block.
+//   A  per env (tid < BE): state loaded once into registers, scripted policy + RL override,
+//      MdR, close sets, and the de-duplicated FeAR task list (see FeAR note above)
+//   B  every lane: one world update per task (the env's real update = the first BE slots)
+//   C  per env: FeAR sums in numpy order, rewards, dones, state, outputs, obs descriptor
+//   D  (OBS = true, GW_KERNEL=fused) the block's float32 obs, 16-byte coalesced stores
+// All per-cell tables live in one u32 LDS table (policy | MdR | action mask | unit moves |
+// road), the policy CDFs in LDS too, so no lane walks a dependent chain of global loads.
+// Small blocks (2 waves) keep ~9 blocks per CU resident so their latency-bound phases overlap.
+// ---------------------------------------------------------------------------------------
+// cell table bits
+constexpr uint32_t CT_POL = 0, CT_MDR = 8, CT_AMASK = 12, CT_OK = 21, CT_ROAD = 25;
 
-// ---------------------------------------------------------------------------------------
-// Fused step (default path): the whole CustomMAEnv.step of BE envs in one block, obs
-// included.  Phases: A per-env actions/MdR/close sets (+ FeAR task list), B one world update
-// per task on every lane, C FeAR sums + rewards + state + small outputs + obs patches into LDS,
-// D the block's K x BE x H*W float32 obs as coalesced 16-byte stores.  Many small blocks are
-// co-resident per CU, so the VALU phases of some overlap the HBM store streams of others --
-// the split path runs them as two serialised launches.
-// ---------------------------------------------------------------------------------------
-template <int N, int KMAX, bool FEAR> struct FusedCfg {
+template <int N, int KMAX, bool FEAR> struct V2Cfg {
     static constexpr int THREADS = 128;
-    static constexpr int BE = FEAR ? (KMAX <= 2 ? (N <= 4 ? 32 : 16) : (N <= 4 ? 16 : 4)) : 64;
+    static constexpr int BE = FEAR ? (KMAX <= 2 ? (N <= 4 ? 32 : 16) : (N <= 4 ? 16 : 4)) : (KMAX <= 2 ? 128 : 32);
     static constexpr int MAXT = FEAR ? BE * (1 + KMAX * (2 + 16 * (N - 1))) : 1;
     using Task = typename std::conditional<(KMAX <= 2), uint16_t, uint32_t>::type;
     // task bits: env 0-5 | b 6-9 (15 = base sim) | var 10 | j 11-13 | k 14+; slots < BE = main sims
@@ -981,10 +1065,62 @@ template <int N, int KMAX, bool FEAR> struct FusedCfg {
     }
 };
 
-template <int N, int WH, int BE, int KMAX, int NP>
-__device__ __forceinline__ void fused_patches(const Params &p, int el, const ObsInfo<N> &oi,
-                                              const uint8_t *s_ok, uint16_t (&pc)[2][BE][KMAX][NP],
-                                              float (&pv)[2][BE][KMAX][NP]) {
+template <int N, int KMAX, bool FEAR, bool OBS>
+struct alignas(16) V2Shared {
+    using Cfg = V2Cfg<N, KMAX, FEAR>;
+    static constexpr int BE = Cfg::BE, FB = FEAR ? BE : 1, OB = OBS ? BE : 1, NP = N + 1;
+    double red[Cfg::THREADS / 64][GW_STATS];
+    typename Cfg::Task tasks[Cfg::MAXT];
+    int pos[FB][N];
+    int fin[FB][N];
+    int apple[FB][KMAX];
+    uint32_t bits[FB];
+    int8_t act[FB][N];
+    int8_t mdr[FB][N];
+    uint8_t close[FB][KMAX];
+    uint8_t base[FB][KMAX][2];
+    uint8_t cj[FB][KMAX][FEAR ? N : 1][2][NA];
+    uint16_t pc[2][OB][KMAX][NP];
+    float pv[2][OB][KMAX][NP];
+    uint32_t eflag[OB];
+    int ntask;
+};
+
+// setup_step (ma_customenv.py:432-452) + RL override (:239-242) from the LDS tables
+template <int N>
+__device__ __forceinline__ void select_actions_v2(const Params &p, int64_t e, const EnvState<N> &es,
+                                                  const uint32_t *ctab, const double *cdf_s, int (&act)[N]) {
+    const uint32_t gid = (uint32_t)(p.env_offset + e);
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+        if (n < p.K) {
+            if (p.rl) {
+                act[n] = p.rl[e * p.K + n];
+            } else {
+                const uint4 r = philox(gid, es.episode, (uint32_t)es.t, (2u << 24) | (uint32_t)n, p.key0, p.key1);
+                act[n] = (int)(((uint64_t)r.x * 9u) >> 32);
+            }
+        } else if (p.scripted) {
+            act[n] = p.scripted[e * (p.N - p.K) + (n - p.K)];
+        } else {
+            const uint4 r = philox(gid, es.episode, (uint32_t)es.t, (1u << 24) | (uint32_t)n, p.key0, p.key1);
+            const int uni = r.x < 0x40000000u;  // random.random() < 0.25 (:441)
+            const double u = ((double)(r.y >> 5) * 67108864.0 + (double)(r.z >> 6)) * (1.0 / 9007199254740992.0);
+            const int pid = (int)((ctab[es.pos[n]] >> CT_POL) & 0xFFu);
+            const double *cdf = (cdf_s ? cdf_s : p.tb.cdf) + (pid * 2 + uni) * NA;
+            int a = NA - 1;
+#pragma unroll
+            for (int q = NA - 2; q >= 0; --q)
+                if (u < cdf[q]) a = q;  // searchsorted(cdf, u, 'right')
+            act[n] = a;
+        }
+        act[n] = ((unsigned)act[n] < (unsigned)NA) ? act[n] : 0;
+    }
+}
+
+template <int N, int WH, int OB, int KMAX, int NP>
+__device__ __forceinline__ void v2_patches(const Params &p, int el, const ObsInfo<N> &oi, const uint32_t *ctab,
+                                           uint16_t (&pc)[2][OB][KMAX][NP], float (&pv)[2][OB][KMAX][NP]) {
     const uint32_t f = oi.flags;
     const bool reset = (WH == 0) && (f & D_RESET);
     const uint32_t apples = WH == 0 ? (f >> 8) & 0xFFu : (f >> 16) & 0xFFu;
@@ -994,7 +1130,7 @@ __device__ __forceinline__ void fused_patches(const Params &p, int el, const Obs
         const int ac = ((apples >> k) & 1u) ? p.apples[k] : -1;
         int np = 0;
         if (ac >= 0) {  // own apple first; an agent standing on it overrides this patch
-            float av = ((s_ok[ac] >> 4) & 1u) ? 9.0f : 8.0f;
+            float av = ((ctab[ac] >> CT_ROAD) & 1u) ? 9.0f : 8.0f;
             if (!reset && av == (float)(k + 1)) av = 1.0f;  // relabel of :321 (apple on a wall, K = 8)
             pc[WH][el][k][np] = (uint16_t)ac;
             pv[WH][el][k][np] = av;
@@ -1011,114 +1147,105 @@ __device__ __forceinline__ void fused_patches(const Params &p, int el, const Obs
     }
 }
 
-template <int N, int KMAX, bool FEAR>
-__global__ void __launch_bounds__(128) step_fused(Params p) {
-    using Cfg = FusedCfg<N, KMAX, FEAR>;
-    constexpr int BE = Cfg::BE, T = Cfg::THREADS, MAXT = Cfg::MAXT;
-    constexpr int NP = N + 1;
-    constexpr int FB = FEAR ? BE : 1;
-    using Task = typename Cfg::Task;
-    __shared__ __attribute__((aligned(16))) uint8_t s_ok[4096];  // bits 0-3 unit moves, bit 4 road
-    __shared__ int s_pos[BE][N];
-    __shared__ int8_t s_act[BE][N];
-    __shared__ int8_t s_mdr[BE][N];
-    __shared__ uint8_t s_close[FB][KMAX];
-    __shared__ Task s_tasks[MAXT];
-    __shared__ uint8_t s_base[FB][KMAX][2];
-    __shared__ uint8_t s_cj[FB][KMAX][FEAR ? N : 1][2][NA];
-    __shared__ int s_fin[FB][N];
-    __shared__ uint32_t s_bits[FB];
-    __shared__ int s_apple[FB][KMAX];
-    __shared__ uint16_t s_pc[2][BE][KMAX][NP];
-    __shared__ float s_pv[2][BE][KMAX][NP];
-    __shared__ uint32_t s_eflag[BE];
-    __shared__ double s_red[T / 64][GW_STATS];
-    __shared__ int s_ntask;
+template <int N, int KMAX, bool FEAR, bool OBS>
+__global__ void __launch_bounds__(128) step_v2(Params p) {
+    using Cfg = V2Cfg<N, KMAX, FEAR>;
+    using Sh = V2Shared<N, KMAX, FEAR, OBS>;
+    constexpr int BE = Cfg::BE, T = Cfg::THREADS, NP = N + 1, OB = Sh::OB;
+    __shared__ Sh sh;
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];  // [cdf P*18 f64][cell table HW u32]
+    const double *cdf_s = p.lds_cdf ? reinterpret_cast<const double *>(dyn) : nullptr;
+    uint32_t *ctab = reinterpret_cast<uint32_t *>(dyn + p.ctab_off);
+    const uint8_t *okb = nullptr;  // sims read the unit-move bits through ctab (see OkView)
+    (void)okb;
 
     const int tid = threadIdx.x;
-    for (int c = tid; c < p.HW; c += T) s_ok[c] = p.tb.okmask[c];
-    if (tid == 0) s_ntask = BE;
+    if (p.e_begin + (int64_t)blockIdx.x * BE >= p.e_end) return;  // uniform per block
+    for (int c = tid; c < p.HW; c += T) ctab[c] = p.tb.celltab[c];
+    if (p.lds_cdf)
+        for (int i = tid; i < p.n_cdf; i += T) reinterpret_cast<double *>(dyn)[i] = p.tb.cdf[i];
+    if (tid == 0) sh.ntask = BE;
     __syncthreads();
-    const int64_t e0 = (int64_t)blockIdx.x * BE;
-    const int nenv = (int)min((int64_t)BE, p.E - e0);
+    const int64_t e0 = p.e_begin + (int64_t)blockIdx.x * BE;
+    const int nenv = (int)min((int64_t)BE, p.e_end - e0);
     const int K = p.K;
     Contrib ct;
     contrib_zero(ct);
+    EnvState<N> es;
+    const CtabOk okv{ctab};
 
     if constexpr (FEAR) {
-        // ---- A: actions, MdR, close sets, task list ----
+        // ---- A ----
         if (tid < nenv) {
             const int64_t e = e0 + tid;
-            int pos[N], act[N];
-            load_state<N>(p, e, pos);
-            select_actions<N>(p, e, p.st.episode[e], p.st.t[e], pos, act);
-            const uint32_t flags = p.st.flags[e];
+            load_env<N>(p, e, es);
+            int act[N];
+            select_actions_v2<N>(p, e, es, ctab, cdf_s, act);
 #pragma unroll
             for (int n = 0; n < N; ++n) {
-                s_pos[tid][n] = pos[n];
-                s_act[tid][n] = (int8_t)act[n];
-                s_mdr[tid][n] = (int8_t)p.tb.mdr[pos[n]];
+                sh.pos[tid][n] = es.pos[n];
+                sh.act[tid][n] = (int8_t)act[n];
+                sh.mdr[tid][n] = (int8_t)((ctab[es.pos[n]] >> CT_MDR) & 0xFu);
             }
             int ntask = 0;
             uint32_t close[KMAX];
 #pragma unroll
             for (int k = 0; k < KMAX; ++k) {
                 close[k] = 0;
-                s_apple[tid][k] = (k < K && ((flags >> k) & 1u)) ? p.apples[k] : -1;
+                sh.apple[tid][k] = (k < K && ((es.flags >> k) & 1u)) ? p.apples[k] : -1;
                 if (k >= K) continue;
 #pragma unroll
                 for (int n = 0; n < N; ++n)
-                    if (n == k || manhattan(p, pos[k], pos[n]) <= 5) close[k] |= 1u << n;  // :456-464
-                s_close[tid][k] = (uint8_t)close[k];
-                if (act[k] != (int)p.tb.mdr[pos[k]]) ntask += 2 + 16 * (__popc(close[k]) - 1);
+                    if (n == k || manhattan(p, es.pos[k], es.pos[n]) <= 5) close[k] |= 1u << n;  // :456-464
+                sh.close[tid][k] = (uint8_t)close[k];
+                if (act[k] != (int)sh.mdr[tid][k]) ntask += 2 + 16 * (__popc(close[k]) - 1);
             }
-            s_tasks[tid] = Cfg::enc(tid, 0, 0, 0, 0);
+            sh.tasks[tid] = Cfg::enc(tid, 0, 0, 0, 0);
             if (ntask) {
-                int slot = atomicAdd(&s_ntask, ntask);
+                int slot = atomicAdd(&sh.ntask, ntask);
 #pragma unroll
                 for (int k = 0; k < KMAX; ++k) {
-                    if (k >= K || act[k] == (int)p.tb.mdr[pos[k]]) continue;
-                    s_tasks[slot++] = Cfg::enc(tid, k, 0, 0, 15);
-                    s_tasks[slot++] = Cfg::enc(tid, k, 0, 1, 15);
+                    if (k >= K || act[k] == (int)sh.mdr[tid][k]) continue;
+                    sh.tasks[slot++] = Cfg::enc(tid, k, 0, 0, 15);
+                    sh.tasks[slot++] = Cfg::enc(tid, k, 0, 1, 15);
 #pragma unroll
                     for (int j = 0; j < N; ++j) {
                         if (j == k || !((close[k] >> j) & 1u)) continue;
 #pragma unroll
                         for (int var = 0; var < 2; ++var)
                             for (int b = 0; b < NA; ++b)
-                                if (b != act[j]) s_tasks[slot++] = Cfg::enc(tid, k, j, var, b);
+                                if (b != act[j]) sh.tasks[slot++] = Cfg::enc(tid, k, j, var, b);
                     }
                 }
             }
         }
         __syncthreads();
-        // ---- B: one world update per task ----
-        const int ntask = s_ntask;
+        // ---- B ----
+        const int ntask = sh.ntask;
         for (int ti = tid; ti < ntask; ti += T) {
             if (ti < BE && ti >= nenv) continue;
-            const uint32_t tk = s_tasks[ti];
-            const int el = tk & 63, b = (tk >> 6) & 15, var = (tk >> 10) & 1, j = (tk >> 11) & 7,
-                      k = (int)(tk >> 14);
+            const uint32_t tk = sh.tasks[ti];
+            const int el = tk & 63, b = (tk >> 6) & 15, var = (tk >> 10) & 1, j = (tk >> 11) & 7, k = (int)(tk >> 14);
             int pos[N], joint[N], fin[N];
 #pragma unroll
-            for (int n = 0; n < N; ++n) pos[n] = s_pos[el][n];
+            for (int n = 0; n < N; ++n) pos[n] = sh.pos[el][n];
             int apple[MAXN];
 #pragma unroll
             for (int q = 0; q < MAXN; ++q) apple[q] = -1;
             int nk = 0;
-            if (ti < BE) {  // the env's real world update, with the apple scan
+            if (ti < BE) {
 #pragma unroll
-                for (int n = 0; n < N; ++n) joint[n] = s_act[el][n];
+                for (int n = 0; n < N; ++n) joint[n] = sh.act[el][n];
 #pragma unroll
-                for (int q = 0; q < KMAX; ++q) apple[q] = s_apple[el][q];
+                for (int q = 0; q < KMAX; ++q) apple[q] = sh.apple[el][q];
                 nk = K;
-            } else {        // a counterfactual of FeAR_4_one_actor(actor k)
-                const uint32_t cl = s_close[el][k];
+            } else {
+                const uint32_t cl = sh.close[el][k];
 #pragma unroll
-                for (int n = 0; n < N; ++n) joint[n] = ((cl >> n) & 1u) ? (int)s_act[el][n] : 0;
+                for (int n = 0; n < N; ++n) joint[n] = ((cl >> n) & 1u) ? (int)sh.act[el][n] : 0;
 #pragma unroll
                 for (int n = 0; n < N; ++n)
-                    if (n == k && var == 0) joint[n] = s_mdr[el][n];
+                    if (n == k && var == 0) joint[n] = sh.mdr[el][n];
                 if (b != 15) {
 #pragma unroll
                     for (int n = 0; n < N; ++n)
@@ -1126,32 +1253,31 @@ __global__ void __launch_bounds__(128) step_fused(Params p) {
                 }
             }
             World<N> w;
-            w.init(pos, joint, p.W);
+            w.init(pos, joint, p.W, p.w_magic);
             uint32_t caught;
-            simulate<N, true>(w, s_ok, nk, apple, caught, fin);
+            simulate<N, true>(w, okv, nk, apple, caught, fin);
             if (ti < BE) {
 #pragma unroll
-                for (int n = 0; n < N; ++n) s_fin[el][n] = fin[n];
-                s_bits[el] = w.crash | (w.restr << 8) | (caught << 16);
+                for (int n = 0; n < N; ++n) sh.fin[el][n] = fin[n];
+                sh.bits[el] = w.crash | (w.restr << 8) | (caught << 16);
             } else {
                 const uint32_t valid = ~(w.crash | w.restr) & ((1u << N) - 1u);
                 if (b == 15)
-                    s_base[el][k][var] = (uint8_t)valid;
+                    sh.base[el][k][var] = (uint8_t)valid;
                 else
-                    s_cj[el][k][j][var][b] = (uint8_t)((valid >> j) & 1u);
+                    sh.cj[el][k][j][var][b] = (uint8_t)((valid >> j) & 1u);
             }
         }
         __syncthreads();
-        // ---- C: FeAR sums, rewards, outputs, obs patches ----
+        // ---- C ----
         if (tid < nenv) {
             const int64_t e = e0 + tid;
-            int pos[N], act[N], mdr[N], fin[N];
+            int act[N], mdr[N], fin[N];
 #pragma unroll
             for (int n = 0; n < N; ++n) {
-                pos[n] = s_pos[tid][n];
-                act[n] = s_act[tid][n];
-                mdr[n] = s_mdr[tid][n];
-                fin[n] = s_fin[tid][n];
+                act[n] = sh.act[tid][n];
+                mdr[n] = sh.mdr[tid][n];
+                fin[n] = sh.fin[tid][n];
             }
             double fear[MAXN];
 #pragma unroll
@@ -1159,8 +1285,8 @@ __global__ void __launch_bounds__(128) step_fused(Params p) {
 #pragma unroll
             for (int k = 0; k < KMAX; ++k) {
                 if (k >= K || act[k] == mdr[k]) continue;
-                const uint32_t cl = s_close[tid][k];
-                const uint32_t b0 = s_base[tid][k][0], b1 = s_base[tid][k][1];
+                const uint32_t cl = sh.close[tid][k];
+                const uint32_t b0 = sh.base[tid][k][0], b1 = sh.base[tid][k][1];
                 double resp[N];
 #pragma unroll
                 for (int jj = 0; jj < N; ++jj) {
@@ -1171,8 +1297,8 @@ __global__ void __launch_bounds__(128) step_fused(Params p) {
                         vm = 0;
                         va = 0;
                         for (int b = 0; b < NA; ++b) {
-                            vm += (b == act[jj]) ? (int)((b0 >> jj) & 1u) : (int)s_cj[tid][k][jj][0][b];
-                            va += (b == act[jj]) ? (int)((b1 >> jj) & 1u) : (int)s_cj[tid][k][jj][1][b];
+                            vm += (b == act[jj]) ? (int)((b0 >> jj) & 1u) : (int)sh.cj[tid][k][jj][0][b];
+                            va += (b == act[jj]) ? (int)((b1 >> jj) & 1u) : (int)sh.cj[tid][k][jj][1][b];
                         }
                     } else {
                         vm = 9 * (int)((b0 >> jj) & 1u);
@@ -1182,93 +1308,107 @@ __global__ void __launch_bounds__(128) step_fused(Params p) {
                 }
                 fear[k] = np_sum_row<N>(resp, k);
             }
-            const uint32_t bits = s_bits[tid];
+            const uint32_t bits = sh.bits[tid];
             ObsInfo<N> oi;
-            finish_env<N>(p, e, pos, act, mdr, fear, bits & 0xFFu, (bits >> 8) & 0xFFu, fin, (bits >> 16) & 0xFFu, ct, oi);
-            fused_patches<N, 0, BE, KMAX, NP>(p, tid, oi, s_ok, s_pc, s_pv);
-            if (oi.flags & D_FINAL) fused_patches<N, 1, BE, KMAX, NP>(p, tid, oi, s_ok, s_pc, s_pv);
-            s_eflag[tid] = oi.flags;
+            finish_env<N>(p, e, es, act, mdr, fear, bits & 0xFFu, (bits >> 8) & 0xFFu, fin, (bits >> 16) & 0xFFu, ct, oi);
+            if constexpr (OBS) {
+                v2_patches<N, 0, OB, KMAX, NP>(p, tid, oi, ctab, sh.pc, sh.pv);
+                if (oi.flags & D_FINAL) v2_patches<N, 1, OB, KMAX, NP>(p, tid, oi, ctab, sh.pc, sh.pv);
+                sh.eflag[tid] = oi.flags;
+            } else {
+                store_desc<N>(p, e, oi);
+            }
         }
     } else {
-        // fear off: one thread does the whole env
-        if (tid < nenv) {
+        if (tid < nenv) {  // fear off: one thread does the whole env
             const int64_t e = e0 + tid;
-            int pos[N], act[N], mdr[N], fin[N];
-            load_state<N>(p, e, pos);
-            select_actions<N>(p, e, p.st.episode[e], p.st.t[e], pos, act);
+            load_env<N>(p, e, es);
+            int act[N], mdr[N], fin[N], pos[N];
+            select_actions_v2<N>(p, e, es, ctab, cdf_s, act);
 #pragma unroll
-            for (int n = 0; n < N; ++n) mdr[n] = p.tb.mdr[pos[n]];
-            const uint32_t flags = p.st.flags[e];
+            for (int n = 0; n < N; ++n) {
+                pos[n] = es.pos[n];
+                mdr[n] = (int)((ctab[pos[n]] >> CT_MDR) & 0xFu);
+            }
             int apple[MAXN];
 #pragma unroll
-            for (int k = 0; k < MAXN; ++k) apple[k] = (k < K && ((flags >> k) & 1u)) ? p.apples[k] : -1;
+            for (int k = 0; k < MAXN; ++k) apple[k] = (k < K && ((es.flags >> k) & 1u)) ? p.apples[k] : -1;
             World<N> w;
-            w.init(pos, act, p.W);
+            w.init(pos, act, p.W, p.w_magic);
             uint32_t caught;
-            simulate<N, true>(w, s_ok, K, apple, caught, fin);
+            simulate<N, true>(w, okv, K, apple, caught, fin);
             double fear[MAXN];
 #pragma unroll
             for (int k = 0; k < MAXN; ++k) fear[k] = 0.0;
             ObsInfo<N> oi;
-            finish_env<N>(p, e, pos, act, mdr, fear, w.crash, w.restr, fin, caught, ct, oi);
-            fused_patches<N, 0, BE, KMAX, NP>(p, tid, oi, s_ok, s_pc, s_pv);
-            if (oi.flags & D_FINAL) fused_patches<N, 1, BE, KMAX, NP>(p, tid, oi, s_ok, s_pc, s_pv);
-            s_eflag[tid] = oi.flags;
+            finish_env<N>(p, e, es, act, mdr, fear, w.crash, w.restr, fin, caught, ct, oi);
+            if constexpr (OBS) {
+                v2_patches<N, 0, OB, KMAX, NP>(p, tid, oi, ctab, sh.pc, sh.pv);
+                if (oi.flags & D_FINAL) v2_patches<N, 1, OB, KMAX, NP>(p, tid, oi, ctab, sh.pc, sh.pv);
+                sh.eflag[tid] = oi.flags;
+            } else {
+                store_desc<N>(p, e, oi);
+            }
         }
     }
-    if (tid < BE && tid >= nenv) s_eflag[tid] = 0;
+    if constexpr (OBS) {
+        if (tid < BE && tid >= nenv) sh.eflag[tid] = 0;
+    }
 
     // ---- block statistics (deterministic tree) ----
     if (p.out.stats) {
         wave_sum(ct);
         if ((tid & 63) == 0)
 #pragma unroll
-            for (int i = 0; i < GW_STATS; ++i) s_red[tid >> 6][i] = ct.v[i];
+            for (int i = 0; i < GW_STATS; ++i) sh.red[tid >> 6][i] = ct.v[i];
     }
     __syncthreads();
     if (p.out.stats && tid < GW_STATS) {
-        double acc = s_red[0][tid];
+        double acc = sh.red[0][tid];
 #pragma unroll
-        for (int w = 1; w < T / 64; ++w) acc = __dadd_rn(acc, s_red[w][tid]);
-        p.out.stats[(int64_t)blockIdx.x * GW_STATS + tid] = acc;
+        for (int w = 1; w < T / 64; ++w) acc = __dadd_rn(acc, sh.red[w][tid]);
+        p.out.stats[(e0 / BE) * GW_STATS + tid] = acc;
     }
 
-    // ---- D: obs of the block's envs, 16-byte coalesced stores ----
-    const int HW4 = p.HW >> 2;
-    const int total4 = nenv * HW4;
+    if constexpr (OBS) {
+        // ---- D: obs of the block's envs, 16-byte coalesced stores ----
+        const int HW4 = p.HW >> 2;
+        const int total4 = nenv * HW4;
 #pragma unroll
-    for (int wh = 0; wh < 2; ++wh) {
-        float *dst = wh == 0 ? p.out.obs : p.out.final_obs;
-        if (!dst) continue;
-        const uint32_t need = wh == 0 ? D_WRITE : D_FINAL;
-        for (int k = 0; k < K; ++k) {
-            float4 *out4 = reinterpret_cast<float4 *>(dst + ((int64_t)k * p.E + e0) * p.HW);
-            for (int i4 = tid; i4 < total4; i4 += T) {
-                const int el = (int)__umulhi((uint32_t)i4, p.hw4_magic);
-                if (!(s_eflag[el] & need)) continue;
-                const int c0 = (i4 - el * HW4) << 2;
-                const uint32_t okw = *reinterpret_cast<const uint32_t *>(&s_ok[c0]);
-                float4 v;
-                v.x = (okw & 0x10u) ? 0.0f : -1.0f;
-                v.y = (okw & 0x1000u) ? 0.0f : -1.0f;
-                v.z = (okw & 0x100000u) ? 0.0f : -1.0f;
-                v.w = (okw & 0x10000000u) ? 0.0f : -1.0f;
+        for (int wh = 0; wh < 2; ++wh) {
+            float *dst = wh == 0 ? p.out.obs : p.out.final_obs;
+            if (!dst) continue;
+            const uint32_t need = wh == 0 ? D_WRITE : D_FINAL;
+            for (int k = 0; k < K; ++k) {
+                float4 *out4 = reinterpret_cast<float4 *>(dst + ((int64_t)k * p.E + e0) * p.HW);
+                for (int i4 = tid; i4 < total4; i4 += T) {
+                    const int el = HW4 == 1 ? i4 : (int)__umulhi((uint32_t)i4, p.hw4_magic);
+                    if (!(sh.eflag[el] & need)) continue;
+                    const int c0 = (i4 - el * HW4) << 2;
+                    const uint4 cw = *reinterpret_cast<const uint4 *>(&ctab[c0]);
+                    float4 v;
+                    v.x = ((cw.x >> CT_ROAD) & 1u) ? 0.0f : -1.0f;
+                    v.y = ((cw.y >> CT_ROAD) & 1u) ? 0.0f : -1.0f;
+                    v.z = ((cw.z >> CT_ROAD) & 1u) ? 0.0f : -1.0f;
+                    v.w = ((cw.w >> CT_ROAD) & 1u) ? 0.0f : -1.0f;
 #pragma unroll
-                for (int q = 0; q < NP; ++q) {
-                    const int dd = (int)s_pc[wh][el][k][q] - c0;
-                    if ((unsigned)dd < 4u) {
-                        const float pvq = s_pv[wh][el][k][q];
-                        v.x = dd == 0 ? pvq : v.x;
-                        v.y = dd == 1 ? pvq : v.y;
-                        v.z = dd == 2 ? pvq : v.z;
-                        v.w = dd == 3 ? pvq : v.w;
+                    for (int q = 0; q < NP; ++q) {
+                        const int dd = (int)sh.pc[wh][el][k][q] - c0;
+                        if ((unsigned)dd < 4u) {
+                            const float pvq = sh.pv[wh][el][k][q];
+                            v.x = dd == 0 ? pvq : v.x;
+                            v.y = dd == 1 ? pvq : v.y;
+                            v.z = dd == 2 ? pvq : v.z;
+                            v.w = dd == 3 ? pvq : v.w;
+                        }
                     }
+                    store_nt(&out4[i4], v);
                 }
-                out4[i4] = v;
             }
         }
     }
 }
+
 }  // namespace gw
 
 // =========================================================================================
@@ -1298,7 +1438,14 @@ struct Env {
     uint64_t seed = 0;
     int apples[GW_MAX_AGENTS] = {0};
     bool initialized = false;
-    bool fused = false;  // true: one fused launch per step (GW_KERNEL=fused); default: step + obs kernels
+    int mode = 1;        // GW_KERNEL: 0 "v1" (first kernels), 1 "split" step_v2 + obs_kernel (default), 2 "fused"
+    int obs_be = 4;      // GW_OBS_BE: envs per obs_kernel block (4 measured best, 32x32 and 64x64)
+    bool obs_nt = true;  // GW_OBS_NT=0: plain instead of nontemporal obs stores
+    uint32_t *celltab = nullptr;
+    uint32_t *roadbits = nullptr;
+    int chunks = 4;                 // GW_CHUNKS: step/obs pipeline depth (split path)
+    hipStream_t aux = nullptr;      // second stream of the pipeline (created on first use)
+    std::vector<hipEvent_t> sync_ev;  // fork/chunk/join events (timing disabled)
     // tables
     uint8_t *okmask = nullptr, *policy = nullptr, *mdr = nullptr;
     double *cdf = nullptr, *resp = nullptr;
@@ -1312,8 +1459,11 @@ struct Env {
     std::vector<void *> allocs;
     // per-launch profiling events (gw_profile)
     bool profiling = false;
-    std::vector<hipEvent_t> ev_pool;   // 3 events per timed gw_step
+    std::vector<hipEvent_t> ev_pool;   // timing events, reused across calls
     size_t ev_used = 0;
+    struct Span { size_t b, e; int kind; };  // kind 0 = step kernel(s), 1 = obs kernel(s)
+    std::vector<Span> spans;
+    int64_t steps_timed = 0;
 };
 
 hipEvent_t next_event(Env *env) {
@@ -1352,6 +1502,14 @@ gw::Params make_params(const Env *env) {
     p.tb.free_cells = env->free_cells;
     p.tb.base = env->base;
     p.tb.resp = env->resp;
+    p.tb.celltab = env->celltab;
+    p.n_cdf = env->P * 2 * 9;
+    p.lds_cdf = env->P <= 64 ? 1 : 0;
+    p.ctab_off = p.lds_cdf ? ((p.n_cdf * 8 + 15) / 16) * 16 : 0;
+    p.obs_be = env->obs_be;
+    p.e_begin = 0;
+    p.e_end = env->E;
+    p.tb.roadbits = env->roadbits;
     p.st.pos = env->pos;
     p.st.flags = env->flags;
     p.st.t = env->t;
@@ -1382,21 +1540,28 @@ gw::Params make_params(const Env *env) {
     return p;
 }
 
-template <int N, int KMAX, bool FEAR>
-hipError_t launch_fused(const Env *env, const gw::Params &p, hipStream_t s) {
-    constexpr int BE = gw::FusedCfg<N, KMAX, FEAR>::BE;
-    const unsigned grid = (unsigned)((env->E + BE - 1) / BE);
-    hipLaunchKernelGGL((gw::step_fused<N, KMAX, FEAR>), dim3(grid), dim3(gw::FusedCfg<N, KMAX, FEAR>::THREADS), 0, s, p);
+template <int N, int KMAX, bool FEAR, bool OBS>
+hipError_t launch_v2(const Env *env, const gw::Params &p, hipStream_t s) {
+    constexpr int BE = gw::V2Cfg<N, KMAX, FEAR>::BE;
+    const int64_t n = p.e_end - p.e_begin;  // this launch's env range (a pipeline chunk or all)
+    if (n <= 0) return hipSuccess;
+    const unsigned grid = (unsigned)((n + BE - 1) / BE);
+    const size_t dyn = (size_t)p.ctab_off + sizeof(uint32_t) * (size_t)env->HW;
+    hipLaunchKernelGGL((gw::step_v2<N, KMAX, FEAR, OBS>), dim3(grid), dim3(gw::V2Cfg<N, KMAX, FEAR>::THREADS), dyn, s, p);
     return hipGetLastError();
+}
+
+template <int N, bool OBS>
+hipError_t launch_v2_k(const Env *env, const gw::Params &p, hipStream_t s) {
+    if (env->fear)
+        return env->K <= 2 ? launch_v2<N, 2, true, OBS>(env, p, s) : launch_v2<N, N, true, OBS>(env, p, s);
+    return env->K <= 2 ? launch_v2<N, 2, false, OBS>(env, p, s) : launch_v2<N, N, false, OBS>(env, p, s);
 }
 
 template <int N>
 hipError_t launch_step(const Env *env, const gw::Params &p, hipStream_t s) {
-    if (env->fused) {
-        if (env->fear)
-            return env->K <= 2 ? launch_fused<N, 2, true>(env, p, s) : launch_fused<N, N, true>(env, p, s);
-        return env->K <= 2 ? launch_fused<N, 2, false>(env, p, s) : launch_fused<N, N, false>(env, p, s);
-    }
+    if (env->mode == 2) return launch_v2_k<N, true>(env, p, s);
+    if (env->mode == 1) return launch_v2_k<N, false>(env, p, s);
     if (env->fear) {
         if (env->K <= 2) {
             constexpr int BE = gw::FearCfg<N, 2>::BE;
@@ -1451,11 +1616,17 @@ hipError_t dispatch_reset(const Env *env, const gw::Params &p, hipStream_t s) {
 
 hipError_t launch_obs(const Env *env, const gw::Params &p, float *obs, float *final_obs, hipStream_t s) {
     if (!obs && !final_obs) return hipSuccess;
-    const unsigned grid = (unsigned)((env->E + gw::OBS_BE - 1) / gw::OBS_BE);
-    if (env->HW % 4 == 0)
-        hipLaunchKernelGGL((gw::obs_kernel<true>), dim3(grid), dim3(gw::OBS_THREADS), 0, s, p, obs, final_obs);
-    else
-        hipLaunchKernelGGL((gw::obs_kernel<false>), dim3(grid), dim3(gw::OBS_THREADS), 0, s, p, obs, final_obs);
+    const int64_t n = p.e_end - p.e_begin;
+    if (n <= 0) return hipSuccess;
+    const unsigned grid = (unsigned)((n + env->obs_be - 1) / env->obs_be);
+    if (env->HW % 4 == 0) {
+        if (env->obs_nt)
+            hipLaunchKernelGGL((gw::obs_kernel<true, true>), dim3(grid), dim3(gw::OBS_THREADS), 0, s, p, obs, final_obs);
+        else
+            hipLaunchKernelGGL((gw::obs_kernel<true, false>), dim3(grid), dim3(gw::OBS_THREADS), 0, s, p, obs, final_obs);
+    } else {
+        hipLaunchKernelGGL((gw::obs_kernel<false, false>), dim3(grid), dim3(gw::OBS_THREADS), 0, s, p, obs, final_obs);
+    }
     return hipGetLastError();
 }
 
@@ -1464,14 +1635,15 @@ hipError_t launch_obs(const Env *env, const gw::Params &p, float *obs, float *fi
 namespace {
 template <int N>
 int64_t stats_rows_n(const Env *env) {
-    if (env->fused) {
-        int be;
-        if (env->fear) be = env->K <= 2 ? gw::FusedCfg<N, 2, true>::BE : gw::FusedCfg<N, N, true>::BE;
-        else be = env->K <= 2 ? gw::FusedCfg<N, 2, false>::BE : gw::FusedCfg<N, N, false>::BE;
-        return (env->E + be - 1) / be;
+    int be;
+    if (env->mode >= 1) {
+        if (env->fear) be = env->K <= 2 ? gw::V2Cfg<N, 2, true>::BE : gw::V2Cfg<N, N, true>::BE;
+        else be = env->K <= 2 ? gw::V2Cfg<N, 2, false>::BE : gw::V2Cfg<N, N, false>::BE;
+    } else if (!env->fear) {
+        be = 256;
+    } else {
+        be = env->K <= 2 ? gw::FearCfg<N, 2>::BE : gw::FearCfg<N, N>::BE;
     }
-    if (!env->fear) return (env->E + 255) / 256;
-    const int be = env->K <= 2 ? gw::FearCfg<N, 2>::BE : gw::FearCfg<N, N>::BE;
     return (env->E + be - 1) / be;
 }
 }  // namespace
@@ -1495,6 +1667,8 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
     std::vector<uint8_t> ok(HW), mdr(HW), pol(HW);
     std::vector<uint16_t> am(HW);
     std::vector<float> base(HW);
+    std::vector<uint32_t> ctab(HW);
+    std::vector<uint32_t> rbits((HW + 31) / 32, 0u);
     std::vector<int32_t> freec;
     for (int c = 0; c < HW; ++c) {
         const int r = c / W, q = c % W;
@@ -1518,6 +1692,9 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
         if (sc->policy_id[c] >= sc->n_policies) return fail(GW_ERR_ARG, "policy id out of range");
         mdr[c] = sc->mdr[c];
         pol[c] = sc->policy_id[c];
+        ctab[c] = (uint32_t)pol[c] | ((uint32_t)mdr[c] << 8) | ((uint32_t)m << 12) | ((uint32_t)(ok[c] & 0xFu) << 21) |
+                  ((uint32_t)(sc->region[c] != 0) << 25);
+        if (sc->region[c]) rbits[c >> 5] |= 1u << (c & 31);
     }
     if ((int)freec.size() < N) return fail(GW_ERR_ARG, "fewer road cells than agents");
     for (int k = 0; k < K; ++k)
@@ -1548,8 +1725,16 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
     env->seed = cfg->seed;
     for (int k = 0; k < K; ++k) env->apples[k] = sc->apples[k];
     {
-        const char *kv = std::getenv("GW_KERNEL");  // "fused" selects the one-launch path (A/B)
-        env->fused = (HW % 4 == 0) && kv && std::strcmp(kv, "fused") == 0;
+        const char *kv = std::getenv("GW_KERNEL");  // kernel path for A/B measurements
+        env->mode = 1;
+        if (kv && std::strcmp(kv, "v1") == 0) env->mode = 0;
+        if (kv && std::strcmp(kv, "fused") == 0 && HW % 4 == 0) env->mode = 2;
+        const char *be = std::getenv("GW_OBS_BE");
+        if (be) env->obs_be = std::max(1, std::min(gw::OBS_BE, std::atoi(be)));
+        const char *nt = std::getenv("GW_OBS_NT");
+        if (nt) env->obs_nt = std::atoi(nt) != 0;
+        const char *ch = std::getenv("GW_CHUNKS");
+        if (ch) env->chunks = std::max(1, std::min(16, std::atoi(ch)));
     }
 
     auto cleanup = [&](gw_status s) {
@@ -1567,7 +1752,8 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
         (st = dalloc(env, &env->pos, (size_t)N * E)) || (st = dalloc(env, &env->t, E)) ||
         (st = dalloc(env, &env->prev, (size_t)K * E)) || (st = dalloc(env, &env->flags, E)) ||
         (st = dalloc(env, &env->episode, E)) || (st = dalloc(env, &env->desc, E * gw::NDESC)) ||
-        (st = dalloc(env, &env->score, E)) || (st = dalloc(env, &env->fscore, E)))
+        (st = dalloc(env, &env->score, E)) || (st = dalloc(env, &env->fscore, E)) ||
+        (st = dalloc(env, &env->celltab, HW)) || (st = dalloc(env, &env->roadbits, rbits.size())))
         return cleanup(st);
     hipError_t he = hipSuccess;
 #define CP(dst, src, n) if (he == hipSuccess) he = hipMemcpy(dst, src, n, hipMemcpyHostToDevice)
@@ -1579,6 +1765,8 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
     CP(env->amask, am.data(), sizeof(uint16_t) * HW);
     CP(env->free_cells, freec.data(), sizeof(int32_t) * freec.size());
     CP(env->base, base.data(), sizeof(float) * HW);
+    CP(env->celltab, ctab.data(), sizeof(uint32_t) * HW);
+    CP(env->roadbits, rbits.data(), sizeof(uint32_t) * rbits.size());
 #undef CP
     if (he == hipSuccess) he = hipMemset(env->episode, 0xFF, sizeof(uint32_t) * E);  // first reset -> 0
     if (he == hipSuccess) he = hipMemset(env->desc, 0, sizeof(uint32_t) * E * gw::NDESC);
@@ -1614,15 +1802,67 @@ gw_status gw_step(void *handle, const int32_t *rl_actions, const int32_t *script
     p.spawn = spawn;
     if (out) p.out = *out;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-    if (env->profiling)
-        for (int i = 0; i < 3; ++i)
-            if (!(ev[i] = next_event(env))) return fail(GW_ERR_HIP, "hipEventCreate failed");
-    if (ev[0]) HIP_TRY(hipEventRecord(ev[0], s));
-    HIP_TRY(dispatch_step(env, p, s));
-    if (ev[1]) HIP_TRY(hipEventRecord(ev[1], s));
-    if (!env->fused) HIP_TRY(launch_obs(env, p, p.out.obs, p.out.final_obs, s));
-    if (ev[2]) HIP_TRY(hipEventRecord(ev[2], s));
+    const bool want_obs = p.out.obs || p.out.final_obs;
+    if (env->profiling) env->steps_timed++;
+    auto span_begin = [&](hipStream_t st, size_t &idx) -> gw_status {
+        idx = env->profiling ? env->ev_used : 0;
+        if (!env->profiling) return GW_OK;
+        hipEvent_t e = next_event(env);
+        if (!e) return fail(GW_ERR_HIP, "hipEventCreate failed");
+        HIP_TRY(hipEventRecord(e, st));
+        return GW_OK;
+    };
+    auto span_end = [&](hipStream_t st, size_t b, int kind) -> gw_status {
+        if (!env->profiling) return GW_OK;
+        hipEvent_t e = next_event(env);
+        if (!e) return fail(GW_ERR_HIP, "hipEventCreate failed");
+        HIP_TRY(hipEventRecord(e, st));
+        env->spans.push_back({b, env->ev_used - 1, kind});
+        return GW_OK;
+    };
+    // chunk size: a multiple of every block size in play (v2 BE, obs_be) so blocks never straddle
+    const int64_t unit = 128;  // multiple of every step_v2 BE (<= 128) and obs_be (<= 8)
+    const int nch = (env->mode == 1 && want_obs && env->chunks > 1 && env->E >= unit * env->chunks) ? env->chunks : 1;
+    if (nch == 1) {
+        size_t b;
+        GW_TRY(span_begin(s, b));
+        HIP_TRY(dispatch_step(env, p, s));
+        GW_TRY(span_end(s, b, 0));
+        if (env->mode != 2 && want_obs) {
+            GW_TRY(span_begin(s, b));
+            HIP_TRY(launch_obs(env, p, p.out.obs, p.out.final_obs, s));
+            GW_TRY(span_end(s, b, 1));
+        }
+        return GW_OK;
+    }
+    // Pipeline over env chunks: step_v2(chunk c) on `s`, obs_kernel(chunk c) on the aux stream
+    // after an event; VALU-bound step chunks run concurrently with HBM-bound obs chunks.
+    if (!env->aux) HIP_TRY(hipStreamCreateWithFlags(&env->aux, hipStreamNonBlocking));
+    while ((int)env->sync_ev.size() < nch + 2) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        env->sync_ev.push_back(e);
+    }
+    HIP_TRY(hipEventRecord(env->sync_ev[0], s));           // fork: aux waits for prior work on s
+    HIP_TRY(hipStreamWaitEvent(env->aux, env->sync_ev[0], 0));
+    const int64_t per = ((env->E / nch + unit - 1) / unit) * unit;
+    for (int c = 0; c < nch; ++c) {
+        gw::Params q = p;
+        q.e_begin = std::min<int64_t>(env->E, c * per);
+        q.e_end = std::min<int64_t>(env->E, (c + 1) * per);
+        if (q.e_begin >= q.e_end) break;
+        size_t b;
+        GW_TRY(span_begin(s, b));
+        HIP_TRY(dispatch_step(env, q, s));
+        GW_TRY(span_end(s, b, 0));
+        HIP_TRY(hipEventRecord(env->sync_ev[1 + c], s));
+        HIP_TRY(hipStreamWaitEvent(env->aux, env->sync_ev[1 + c], 0));
+        GW_TRY(span_begin(env->aux, b));
+        HIP_TRY(launch_obs(env, q, q.out.obs, q.out.final_obs, env->aux));
+        GW_TRY(span_end(env->aux, b, 1));
+    }
+    HIP_TRY(hipEventRecord(env->sync_ev[nch + 1], env->aux));  // join
+    HIP_TRY(hipStreamWaitEvent(s, env->sync_ev[nch + 1], 0));
     return GW_OK;
 }
 
@@ -1637,18 +1877,16 @@ gw_status gw_profile_read(void *handle, double out_ms[2], int64_t *n_steps) {
     Env *env = static_cast<Env *>(handle);
     if (!env || !out_ms) return fail(GW_ERR_ARG, "null argument");
     out_ms[0] = out_ms[1] = 0.0;
-    const size_t n = env->ev_used / 3;
-    for (size_t i = 0; i < n; ++i) {
-        hipEvent_t *e = &env->ev_pool[3 * i];
-        HIP_TRY(hipEventSynchronize(e[2]));
-        float a = 0.f, b = 0.f;
-        HIP_TRY(hipEventElapsedTime(&a, e[0], e[1]));
-        HIP_TRY(hipEventElapsedTime(&b, e[1], e[2]));
-        out_ms[0] += a;
-        out_ms[1] += b;
+    for (const Env::Span &sp : env->spans) {
+        HIP_TRY(hipEventSynchronize(env->ev_pool[sp.e]));
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, env->ev_pool[sp.b], env->ev_pool[sp.e]));
+        out_ms[sp.kind] += ms;
     }
-    if (n_steps) *n_steps = (int64_t)n;
+    if (n_steps) *n_steps = env->steps_timed;
+    env->spans.clear();
     env->ev_used = 0;
+    env->steps_timed = 0;
     return GW_OK;
 }
 
@@ -1720,6 +1958,8 @@ void gw_destroy(void *handle) {
     (void)hipSetDevice(env->device);
     (void)hipDeviceSynchronize();
     for (hipEvent_t e : env->ev_pool) (void)hipEventDestroy(e);
+    for (hipEvent_t e : env->sync_ev) (void)hipEventDestroy(e);
+    if (env->aux) (void)hipStreamDestroy(env->aux);
     for (void *p : env->allocs) (void)hipFree(p);
     delete env;
 }

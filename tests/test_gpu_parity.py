@@ -71,7 +71,8 @@ def test_gpu_replays_reference_trajectory(fname, seed):
 def _compare_native(sc, E, fear, steps, nthreads=16, offset=0, seed=7, weight=-5.0):
     """GPU native-RNG rollout == C oracle rollout, every output, every step (bit-exact)."""
     env = VecGridEnv(sc, num_envs=E, fear=fear, fear_weight=weight, max_steps=150, auto_reset=True,
-                     seed=seed, env_offset=offset, final_obs=True, debug=True)
+                     seed=seed, env_offset=offset, final_obs=True, debug=True, stats=True)
+    guard = torch.full((1 << 16,), 7.0, dtype=torch.float64, device=env.device)  # canary after stats
     orc = O.OracleEnvs(sc, E, fear=fear, fear_weight=weight, max_steps=150, seed=seed, env_offset=offset,
                        reset=False)
     obs_o = np.zeros((sc.K, E, sc.HW), np.float32)
@@ -99,15 +100,32 @@ def _compare_native(sc, E, fear, steps, nthreads=16, offset=0, seed=7, weight=-5
         np.testing.assert_array_equal(r.ep_return.cpu().numpy(), np.array([outs[e].ep_return for e in range(E)]), err_msg=f"t={t} ret")
         np.testing.assert_array_equal(r.mask.cpu().numpy().astype(np.uint16), get("mask", K), err_msg=f"t={t} mask")
         np.testing.assert_array_equal(r.obs.reshape(K, E, -1).cpu().numpy(), obs_o, err_msg=f"t={t} obs")
+        # per-block statistics == the same sums over the oracle's outputs
+        st = r.stats.sum(0).cpu().numpy()
+        assert st[7] == E and st[1] == dn.sum()
+        assert st[3] == sum(outs[e].crashes for e in range(E))
+        np.testing.assert_allclose(st[0], sum(outs[e].ep_return for e in range(E) if outs[e].done), rtol=1e-12, atol=1e-9)
         done_total += int(dn.sum())
+    assert bool((guard == 7.0).all()), "write past the stats buffer"
     env.close()
     return done_total
 
 
-@pytest.fixture(params=["fused", "split"])
+KERNEL_PATHS = {
+    "split": {"GW_KERNEL": "split"},                          # default: chunked 2-stream pipeline
+    "split1": {"GW_KERNEL": "split", "GW_CHUNKS": "1"},       # step_v2 then obs_kernel, one stream
+    "split_plain": {"GW_KERNEL": "split", "GW_OBS_NT": "0", "GW_OBS_BE": "8"},
+    "fused": {"GW_KERNEL": "fused"},                          # obs stores inside step_v2
+    "v1": {"GW_KERNEL": "v1"},                                # the first kernels
+}
+
+
+@pytest.fixture(params=sorted(KERNEL_PATHS))
 def kernel_path(request, monkeypatch):
-    """GW_KERNEL selects the one-launch fused step (default) or the step + obs launches."""
-    monkeypatch.setenv("GW_KERNEL", request.param)
+    """Every kernel path must pass the same bit-exact checks (selected by env vars read at
+    gw_create)."""
+    for k, v in KERNEL_PATHS[request.param].items():
+        monkeypatch.setenv(k, v)
     return request.param
 
 
@@ -147,3 +165,38 @@ def test_sharding_is_invariant():
         assert torch.equal(rf.obs.cpu(), torch.cat([ra.obs.cpu(), rb.obs.cpu()], dim=1))
     for env in (full, a, b):
         env.close()
+
+
+@pytest.mark.parametrize("name,E", [("grid32", 65536), ("grid64_n8", 65536)])
+def test_full_size_properties(name, E, kernel_path):
+    """BASELINE sizes: size-independent invariants on every env + a bit-exact slice vs the oracle."""
+    if kernel_path in ("v1", "split_plain"):
+        pytest.skip("full-size run only for the default and fused paths")
+    sc = S.builtin(name)
+    env = VecGridEnv(sc, num_envs=E, fear=True, fear_weight=-5.0, seed=9, stats=True, debug=True)
+    sl0, sl = 4096 + 128, 256  # a slice that straddles pipeline chunks and blocks
+    orc = O.OracleEnvs(sc, sl, fear=True, fear_weight=-5.0, seed=9, env_offset=sl0, reset=False)
+    obs_o = np.zeros((sc.K, sl, sc.HW), np.float32)
+    orc.reset_all(obs=obs_o)
+    env.reset()
+    outs = (O.StepOut * sl)()
+    road = torch.as_tensor(sc.region.astype(bool), device=env.device)
+    for t in range(12):
+        r = env.step()
+        orc.vec_step(None, obs=obs_o, outs=outs, nthreads=16)
+        pos = env.positions()                                        # [E, N] after any auto-reset
+        srt = pos.sort(1).values
+        assert bool((srt[:, 1:] != srt[:, :-1]).all()), "two agents share a cell"
+        assert bool(road[pos.long()].all()), "agent off the road"
+        # obs encodes exactly the agents: N cells per agent-obs carry agent values
+        o = r.obs.reshape(sc.K, E, -1)
+        agents_in_obs = ((o != 0) & (o != -1) & (o != 9)).sum(-1)
+        assert bool((agents_in_obs == sc.N).all())
+        st = r.stats.sum(0)
+        assert float(st[7]) == E and float(st[1]) == float(r.done.sum())
+        np.testing.assert_array_equal(r.final_pos[sl0:sl0 + sl].cpu().numpy(),
+                                      np.array([list(outs[e].final_pos)[:sc.N] for e in range(sl)]))
+        np.testing.assert_array_equal(r.ep_return[sl0:sl0 + sl].cpu().numpy(),
+                                      np.array([outs[e].ep_return for e in range(sl)]))
+        np.testing.assert_array_equal(o[:, sl0:sl0 + sl].cpu().numpy(), obs_o)
+    env.close()

@@ -1,0 +1,105 @@
+"""GPU tests of the host-side pieces around the kernels: the CustomMAEnv facade, the actors and
+the batched rollout with the zero-copy replay ring."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from marlnav import scenario as S
+from marlnav.actor import MultiAgentActors
+from marlnav.rollout import Rollout
+from marlnav.vec_env import VecGridEnv
+
+pytestmark = pytest.mark.gpu
+
+
+def test_facade_matches_oracle_native_mode():
+    """CustomMAEnv (reference dict API, E = 1, no auto-reset, no step cap) == the oracle."""
+    from custom.ma_customenv import CustomMAEnv
+    sc = S.builtin("level3")
+    env = CustomMAEnv(render=False, fear=True, seed=123)
+    orc = O.OracleEnvs(sc, 1, fear=True, fear_weight=0.0, max_steps=0, seed=123, reset=False)
+    obs, info = env.reset()
+    o_obs, o_mask = orc.reset_one(0, episode=0)
+    assert set(obs) == {"agent_0", "agent_1"} and info["fear"] == 0.0
+    for k in range(2):
+        np.testing.assert_array_equal(obs[f"agent_{k}"], o_obs[k].reshape(10, 16).astype(np.float64))
+        assert obs[f"agent_{k}"].dtype == np.float64
+        m = info[f"agent_{k}"]["action_mask"]
+        assert m.dtype == np.int8 and int(np.dot(m, 1 << np.arange(9))) == int(o_mask[k])
+    rng = np.random.default_rng(0)
+    for t in range(60):
+        a = tuple(int(x) for x in rng.integers(0, 9, 2))
+        obs, rew, term, trunc, info = env.step(a)
+        o_obs, _, out = orc.step_one(0, rl_act=np.array(a, np.int32), auto_reset=False)
+        assert rew == {f"agent_{k}": int(out.reward[k]) for k in range(2)}
+        assert all(isinstance(v, int) for v in rew.values())
+        assert term == {f"agent_{k}": bool(out.term[k]) for k in range(2)}
+        assert trunc == {f"agent_{k}": bool(out.trunc[k]) for k in range(2)}
+        assert info["fear"] == {f"agent_{k}": out.fear[k] for k in range(2)}
+        assert info["agent_crashes"] == out.crashes and info["apples_caught"] == out.apples_caught
+        assert [x[1] for x in env.Action4Agents] == list(out.actions)[:4]
+        for k in range(2):
+            np.testing.assert_array_equal(obs[f"agent_{k}"], o_obs[k].reshape(10, 16))
+    assert env.step(()) == ({}, {}, {}, {}, {})
+    assert env.action_space.n == 9 and env.num_agents == 2
+    assert env.observation_space("agent_0").shape == (10, 16)
+
+
+def test_stacked_actor_matches_plain_pytorch_fp32():
+    """The batched K-agent MLP == K independent nn.Sequential fp32 actors."""
+    torch.manual_seed(0)
+    K, H, W, E = 2, 32, 32, 512
+    actors = MultiAgentActors(K, H, W, "mlp", device="cuda", seed=3)
+    x = torch.randint(-1, 6, (K, E, H, W), device="cuda").float()
+    got = actors(x)
+    net = actors.net
+    for k in range(K):
+        ref = torch.nn.Sequential(
+            torch.nn.Linear(H * W, 128), torch.nn.LayerNorm(128), torch.nn.ReLU(),
+            torch.nn.Linear(128, 128), torch.nn.LayerNorm(128), torch.nn.ReLU(),
+            torch.nn.Linear(128, 9)).cuda()
+        with torch.no_grad():
+            for li, lin in enumerate([ref[0], ref[3], ref[6]]):
+                lin.weight.copy_(net.weights[li][k].t())
+                lin.bias.copy_(net.biases[li][k, 0])
+            for li, ln in enumerate([ref[1], ref[4]]):
+                ln.weight.copy_(net.ln_w[li][k, 0])
+                ln.bias.copy_(net.ln_b[li][k, 0])
+            want = ref(x[k].reshape(E, -1))
+        torch.testing.assert_close(got[k], want, rtol=1e-4, atol=1e-4)
+
+
+def test_rollout_with_actor_and_replay_ring():
+    sc = S.builtin("grid32")
+    E = 2048
+    env = VecGridEnv(sc, num_envs=E, fear=True, fear_weight=-5.0, stats=True, final_obs=False, debug=True)
+    actors = MultiAgentActors(sc.K, sc.H, sc.W, "mlp", device=env.device, seed=1)
+    ro = Rollout(env, actors, replay_slots=4, training=True, seed=2)
+    ro.reset()
+    shaped_sum = 0.0
+    for t in range(40):
+        mask = env.out["mask"].clone()
+        r = ro.step()
+        # actions respect the action mask of the obs they were chosen from
+        a = r.actions[:, : sc.K].long()
+        allowed = (mask.long() >> a) & 1
+        assert bool(allowed.all())
+        cur = t % ro.replay.S
+        assert torch.equal(ro.replay.reward[cur], r.shaped)
+        shaped_sum += float(r.shaped.sum())
+    tot = ro.totals()
+    assert tot["env_steps"] == 40 * E
+    assert abs(tot["shaped"] - shaped_sum) < 1e-6 * max(1.0, abs(shaped_sum))
+    state, probs, rew, nxt, term = ro.replay.sample(256)
+    assert state.shape == (sc.K, 256, sc.H, sc.W) and nxt.shape == state.shape
+    assert probs.shape == (sc.K, 256, 9) and rew.shape == (256, sc.K)
+    torch.testing.assert_close(probs.sum(-1), torch.ones_like(probs.sum(-1)))
+    env.close()
+
+
+def test_cnn_actor_runs():
+    actors = MultiAgentActors(2, 64, 64, "cnn", device="cuda")
+    x = torch.zeros((2, 16, 64, 64), device="cuda")
+    a, p = actors.act(x, None, training=False)
+    assert a.shape == (16, 2) and p.shape == (2, 16, 9)
