@@ -178,6 +178,15 @@ def main():
         else:
             dom, bytes_per_launch, dur = "step_kernel", step_b * E, avg_step_ms
         achieved = bytes_per_launch / (dur * 1e-3) / 1e9
+        traffic, traffic_src = None, None
+        try:  # HBM bytes measured by the PMC passes committed under profiles/ for this workload
+            with open(os.path.join(REPO, "profiles", "latest.json")) as f:
+                prof = json.load(f)
+            if prof.get("config") == args.config and not args.envs and args.fear < 0 and not fused:
+                traffic = prof["kernels"][dom]["hbm_bytes_per_launch"]
+                traffic_src = prof["source"]
+        except (OSError, KeyError, ValueError):
+            pass
         total_units = world * E * N * args.steps
         line = {
             "metric": METRIC,
@@ -196,11 +205,12 @@ def main():
                        "global_envs": world * E, "agents": N, "rl_agents": K, "grid": [env.H, env.W],
                        "fear": cfg["fear"], "parallelism": f"env-sharded dp{world}"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "bytes_per_launch": bytes_per_launch, "avg_launch_ms": dur},
             "kernels_ms": {"step_kernel": avg_step_ms, "obs_kernel": avg_obs_ms,
                            "stream_ms_per_step": gpu_ms / args.steps,
-                           "pipeline_chunks": int(os.environ.get("GW_CHUNKS", "4")) if not env.fused else 1},
+                           "pipeline_chunks": int(os.environ.get("GW_CHUNKS", "1")) if not env.fused else 1},
             "last_step_episodes": {"completed": stats[1], "mean_return": stats[0] / max(stats[1], 1.0),
                          "mean_len": stats[6] / max(stats[1], 1.0)},
         }

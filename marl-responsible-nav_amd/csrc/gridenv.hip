@@ -86,7 +86,7 @@ struct Params {
     uint32_t key0, key1;
     uint32_t w_magic;         // ceil(2^32 / W)  (exact /W for cells < 2^16)
     uint32_t hw4_magic;       // ceil(2^32 / (H*W/4))
-    int lds_cdf, n_cdf, ctab_off;  // step_v2 dynamic LDS: [cdf n_cdf f64 if lds_cdf][cell table]
+    int lds_cdf, n_cdf, ctab_off, resp_off;  // step_v2 dynamic LDS: [cdf][cell table][Resp 100 f64]
     int obs_be;               // envs per obs_kernel block (<= OBS_BE)
     int64_t e_begin, e_end;   // env range of this launch (step_v2 / obs_kernel chunks)
     int apples[MAXN];
@@ -209,70 +209,69 @@ struct World {
 #pragma unroll
         for (int i = 0; i < N; ++i) {
             const int old = nal[i][S];
-            int nw = old;
-            const bool active_sub = (S == 0) || (S == 1 && ((two >> i) & 1u));
-            const bool moving = active_sub && ((mv >> i) & 1u) && !((crash >> i) & 1u);
-            if (moving) {
-                const bool ok = (okm(old) >> dir_of(i)) & 1u;
-                nw = ok ? old + delta[i] : old;
-                restr |= (uint32_t)(!ok) << i;
+            if (S >= 2) {  // every action has at most 2 sub-moves: (0, 0) from here on
+                nal[i][S + 1] = old;
+                continue;
             }
-            nal[i][S + 1] = nw;
+            const bool active_sub = (S == 0) || ((two >> i) & 1u);
+            const bool moving = active_sub & (bool)((mv >> i) & 1u) & !((crash >> i) & 1u);
+            const bool ok = (okm(old) >> dir_of(i)) & 1u;  // clip + WorldState[new] >= 0
+            nal[i][S + 1] = (moving & ok) ? old + delta[i] : old;
+            restr |= (uint32_t)(moving & !ok) << i;
         }
+    }
+
+    // overhang test of :310-312 / :341-343 in quarter steps, per (len_i, len_j) at sub-step S
+    template <int S>
+    __device__ __forceinline__ static bool overhang_ok(bool two_a, bool two_b) {
+        // (4*ceil_a - q_a) + (q_b - 4*floor_b) <= 4
+        constexpr bool c11 = SubStep<S>::ohf1 + SubStep<S>::ohc1 <= 4;
+        constexpr bool c12 = SubStep<S>::ohf1 + SubStep<S>::ohc2 <= 4;
+        constexpr bool c21 = SubStep<S>::ohf2 + SubStep<S>::ohc1 <= 4;
+        constexpr bool c22 = SubStep<S>::ohf2 + SubStep<S>::ohc2 <= 4;
+        return two_a ? (two_b ? c22 : c21) : (two_b ? c12 : c11);
     }
 
     template <int S>
     __device__ __forceinline__ void resolve() {  // collision_checks_and_resolution :233-405
         if (near == 0) return;  // no pair can collide: every pass counts 0 (crash stays 0)
         for (int pass = 0; pass < 2 * N; ++pass) {
+            int Af[N], Ac[N];
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                Af[i] = fl<S>(i);
+                Ac[i] = ce<S>(i);
+            }
             uint32_t hit = 0;
-            int cnt = 0;
 #pragma unroll
             for (int ii = 0; ii < N - 1; ++ii) {
-                const int Af = fl<S>(ii), Ac = ce<S>(ii);
                 const bool t_i = (two >> ii) & 1u;
-                const int ohf_i = t_i ? SubStep<S>::ohf2 : SubStep<S>::ohf1;
-                const int ohc_i = t_i ? SubStep<S>::ohc2 : SubStep<S>::ohc1;
 #pragma unroll
                 for (int jj = ii + 1; jj < N; ++jj) {
-                    if (!((near >> pair_bit(ii, jj)) & 1u)) continue;
-                    const int Bf = fl<S>(jj), Bc = ce<S>(jj);
                     const bool t_j = (two >> jj) & 1u;
-                    const int ohf_j = t_j ? SubStep<S>::ohf2 : SubStep<S>::ohf1;
-                    const int ohc_j = t_j ? SubStep<S>::ohc2 : SubStep<S>::ohc1;
-                    const bool same_dir = (Ac - Af) == (Bc - Bf);
-                    bool coll;
-                    if (Af == Bf || Ac == Bc) {
-                        coll = true;                                    // :276-278
-                    } else if (Af == Bc && Ac == Bf) {
-                        coll = true;                                    // :291-294
-                    } else if (Af == Bc) {
-                        coll = !((ohf_i + ohc_j) <= 4 && same_dir);     // :307-337
-                    } else if (Ac == Bf) {
-                        coll = !((ohf_j + ohc_i) <= 4 && same_dir);     // :339-368
-                    } else {
-                        const int Li = loc[ii], Lj = loc[jj];           // :371-378
-                        coll = (Af == Lj && Li == Bf) || (Ac == Lj && Li == Bc) ||
-                               (Af == Lj && Li == Bc) || (Ac == Lj && Li == Bf);
-                    }
-                    if (coll) {
-                        ++cnt;
-                        hit |= (1u << ii) | (1u << jj);
-                    }
+                    const int af = Af[ii], ac = Ac[ii], bf = Af[jj], bc = Ac[jj];
+                    const int li = loc[ii], lj = loc[jj];
+                    const bool eqFF = af == bf, eqCC = ac == bc, eqFC = af == bc, eqCF = ac == bf;
+                    const bool sd = (ac - af) == (bc - bf);
+                    const bool slide_fc = overhang_ok<S>(t_i, t_j) & sd;   // :307-337
+                    const bool slide_cf = overhang_ok<S>(t_j, t_i) & sd;   // :339-368
+                    const bool old_x = ((af == lj) | (ac == lj)) & ((li == bf) | (li == bc));  // :371-378
+                    // the elif chain of :276-384, branch-free
+                    const bool coll = eqFF | eqCC | (eqFC ? (eqCF | !slide_fc) : (eqCF ? !slide_cf : old_x));
+                    const bool nb = (near >> pair_bit(ii, jj)) & 1u;
+                    hit |= (coll & nb) ? ((1u << ii) | (1u << jj)) : 0u;
                 }
             }
             crash |= hit;
             // revertStepsWithCollisions :190-209 (all crashed agents, every pass)
 #pragma unroll
             for (int i = 0; i < N; ++i) {
-                if ((crash >> i) & 1u) {
-                    const int f = ((two >> i) & 1u) ? SubStep<S>::f2 : SubStep<S>::f1;
+                const bool cr = (crash >> i) & 1u;
+                const int f = ((two >> i) & 1u) ? SubStep<S>::f2 : SubStep<S>::f1;
 #pragma unroll
-                    for (int k = 0; k <= S + 1; ++k)
-                        if (k >= f) nal[i][k] = loc[i];
-                }
+                for (int k = 0; k <= S + 1; ++k) nal[i][k] = (cr & (k >= f)) ? loc[i] : nal[i][k];
             }
-            if (cnt == 0) break;
+            if (hit == 0) break;
         }
     }
 
@@ -532,7 +531,7 @@ __device__ __forceinline__ void finish_env(const Params &p, int64_t e, const Env
                                            const int (&act)[N], const int (&mdr)[N],
                                            const double (&fear)[MAXN], uint32_t crash,
                                            uint32_t restr, int (&fin)[N], uint32_t caught,
-                                           Contrib &ct, ObsInfo<N> &oi) {
+                                           Contrib &ct, ObsInfo<N> &oi, const uint32_t *ctab = nullptr) {
     const int K = p.K;
     const uint32_t flags = es.flags;
     uint32_t apples = flags & 0xFFu, term = (flags >> 8) & 0xFFu, trunc = (flags >> 16) & 0xFFu;
@@ -628,7 +627,7 @@ __device__ __forceinline__ void finish_env(const Params &p, int64_t e, const Env
         oi.flags = D_RESET | D_WRITE | (o.final_obs ? D_FINAL : 0u) | (all_bits(K) << 8) | (apples << 16);
 #pragma unroll
         for (int k = 0; k < N; ++k)
-            if (k < K && o.mask) o.mask[e * K + k] = p.tb.amask[np_[k]];
+            if (k < K && o.mask) o.mask[e * K + k] = ctab ? (uint16_t)((ctab[np_[k]] >> 12) & 0x1FFu) : p.tb.amask[np_[k]];
     } else {
 #pragma unroll
         for (int n = 0; n < N; ++n) p.st.pos[(int64_t)n * p.E + e] = fin[n];
@@ -641,7 +640,7 @@ __device__ __forceinline__ void finish_env(const Params &p, int64_t e, const Env
         oi.flags = D_WRITE | (apples << 8);
 #pragma unroll
         for (int k = 0; k < N; ++k)
-            if (k < K && o.mask) o.mask[e * K + k] = p.tb.amask[fin[k]];
+            if (k < K && o.mask) o.mask[e * K + k] = ctab ? (uint16_t)((ctab[fin[k]] >> 12) & 0x1FFu) : p.tb.amask[fin[k]];
     }
 }
 
@@ -1147,6 +1146,29 @@ __device__ __forceinline__ void v2_patches(const Params &p, int el, const ObsInf
     }
 }
 
+// Copy n 32-bit words global -> LDS with 16-byte accesses, all loads of a lane issued before
+// its stores (a plain element loop serialises one L2 round trip per iteration).
+template <int T>
+__device__ __forceinline__ void lds_fill(uint32_t *dst, const uint32_t *__restrict__ src, int n, int tid) {
+    const int n4 = n >> 2;
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+    uint4 *d4 = reinterpret_cast<uint4 *>(dst);
+    constexpr int U = 4;
+    for (int base = 0; n4 > 0 && base < n4; base += U * T) {
+        uint4 v0, v1, v2, v3;  // named registers: loads clamped in range, stores predicated
+        const int i0 = base + tid, i1 = i0 + T, i2 = i1 + T, i3 = i2 + T;
+        v0 = s4[min(i0, n4 - 1)];
+        v1 = s4[min(i1, n4 - 1)];
+        v2 = s4[min(i2, n4 - 1)];
+        v3 = s4[min(i3, n4 - 1)];
+        if (i0 < n4) d4[i0] = v0;
+        if (i1 < n4) d4[i1] = v1;
+        if (i2 < n4) d4[i2] = v2;
+        if (i3 < n4) d4[i3] = v3;
+    }
+    for (int i = (n4 << 2) + tid; i < n; i += T) dst[i] = src[i];
+}
+
 template <int N, int KMAX, bool FEAR, bool OBS>
 __global__ void __launch_bounds__(128) step_v2(Params p) {
     using Cfg = V2Cfg<N, KMAX, FEAR>;
@@ -1156,29 +1178,32 @@ __global__ void __launch_bounds__(128) step_v2(Params p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];  // [cdf P*18 f64][cell table HW u32]
     const double *cdf_s = p.lds_cdf ? reinterpret_cast<const double *>(dyn) : nullptr;
     uint32_t *ctab = reinterpret_cast<uint32_t *>(dyn + p.ctab_off);
+    double *resp_s = reinterpret_cast<double *>(dyn + p.resp_off);  // [10][10] Resp table
     const uint8_t *okb = nullptr;  // sims read the unit-move bits through ctab (see OkView)
     (void)okb;
 
     const int tid = threadIdx.x;
     if (p.e_begin + (int64_t)blockIdx.x * BE >= p.e_end) return;  // uniform per block
-    for (int c = tid; c < p.HW; c += T) ctab[c] = p.tb.celltab[c];
-    if (p.lds_cdf)
-        for (int i = tid; i < p.n_cdf; i += T) reinterpret_cast<double *>(dyn)[i] = p.tb.cdf[i];
-    if (tid == 0) sh.ntask = BE;
-    __syncthreads();
     const int64_t e0 = p.e_begin + (int64_t)blockIdx.x * BE;
     const int nenv = (int)min((int64_t)BE, p.e_end - e0);
     const int K = p.K;
     Contrib ct;
     contrib_zero(ct);
     EnvState<N> es;
+    // the env's state loads are issued first so that their latency overlaps the table fill
+    if (tid < nenv) load_env<N>(p, e0 + tid, es);
+    lds_fill<T>(ctab, p.tb.celltab, p.HW, tid);
+    if (p.lds_cdf)
+        lds_fill<T>(reinterpret_cast<uint32_t *>(dyn), reinterpret_cast<const uint32_t *>(p.tb.cdf), 2 * p.n_cdf, tid);
+    if (FEAR) lds_fill<T>(reinterpret_cast<uint32_t *>(resp_s), reinterpret_cast<const uint32_t *>(p.tb.resp), 200, tid);
+    if (tid == 0) sh.ntask = BE;
+    __syncthreads();
     const CtabOk okv{ctab};
 
     if constexpr (FEAR) {
         // ---- A ----
         if (tid < nenv) {
             const int64_t e = e0 + tid;
-            load_env<N>(p, e, es);
             int act[N];
             select_actions_v2<N>(p, e, es, ctab, cdf_s, act);
 #pragma unroll
@@ -1304,13 +1329,13 @@ __global__ void __launch_bounds__(128) step_v2(Params p) {
                         vm = 9 * (int)((b0 >> jj) & 1u);
                         va = 9 * (int)((b1 >> jj) & 1u);
                     }
-                    resp[jj] = p.tb.resp[vm * 10 + va];
+                    resp[jj] = resp_s[vm * 10 + va];
                 }
                 fear[k] = np_sum_row<N>(resp, k);
             }
             const uint32_t bits = sh.bits[tid];
             ObsInfo<N> oi;
-            finish_env<N>(p, e, es, act, mdr, fear, bits & 0xFFu, (bits >> 8) & 0xFFu, fin, (bits >> 16) & 0xFFu, ct, oi);
+            finish_env<N>(p, e, es, act, mdr, fear, bits & 0xFFu, (bits >> 8) & 0xFFu, fin, (bits >> 16) & 0xFFu, ct, oi, ctab);
             if constexpr (OBS) {
                 v2_patches<N, 0, OB, KMAX, NP>(p, tid, oi, ctab, sh.pc, sh.pv);
                 if (oi.flags & D_FINAL) v2_patches<N, 1, OB, KMAX, NP>(p, tid, oi, ctab, sh.pc, sh.pv);
@@ -1322,7 +1347,6 @@ __global__ void __launch_bounds__(128) step_v2(Params p) {
     } else {
         if (tid < nenv) {  // fear off: one thread does the whole env
             const int64_t e = e0 + tid;
-            load_env<N>(p, e, es);
             int act[N], mdr[N], fin[N], pos[N];
             select_actions_v2<N>(p, e, es, ctab, cdf_s, act);
 #pragma unroll
@@ -1341,7 +1365,7 @@ __global__ void __launch_bounds__(128) step_v2(Params p) {
 #pragma unroll
             for (int k = 0; k < MAXN; ++k) fear[k] = 0.0;
             ObsInfo<N> oi;
-            finish_env<N>(p, e, es, act, mdr, fear, w.crash, w.restr, fin, caught, ct, oi);
+            finish_env<N>(p, e, es, act, mdr, fear, w.crash, w.restr, fin, caught, ct, oi, ctab);
             if constexpr (OBS) {
                 v2_patches<N, 0, OB, KMAX, NP>(p, tid, oi, ctab, sh.pc, sh.pv);
                 if (oi.flags & D_FINAL) v2_patches<N, 1, OB, KMAX, NP>(p, tid, oi, ctab, sh.pc, sh.pv);
@@ -1439,11 +1463,11 @@ struct Env {
     int apples[GW_MAX_AGENTS] = {0};
     bool initialized = false;
     int mode = 1;        // GW_KERNEL: 0 "v1" (first kernels), 1 "split" step_v2 + obs_kernel (default), 2 "fused"
-    int obs_be = 4;      // GW_OBS_BE: envs per obs_kernel block (4 measured best, 32x32 and 64x64)
+    int obs_be = 2;      // GW_OBS_BE: envs per obs_kernel block (2 measured best, 32x32 and 64x64)
     bool obs_nt = true;  // GW_OBS_NT=0: plain instead of nontemporal obs stores
     uint32_t *celltab = nullptr;
     uint32_t *roadbits = nullptr;
-    int chunks = 4;                 // GW_CHUNKS: step/obs pipeline depth (split path)
+    int chunks = 1;                 // GW_CHUNKS: step/obs pipeline depth (split path; 1 = off, measured best)
     hipStream_t aux = nullptr;      // second stream of the pipeline (created on first use)
     std::vector<hipEvent_t> sync_ev;  // fork/chunk/join events (timing disabled)
     // tables
@@ -1506,6 +1530,7 @@ gw::Params make_params(const Env *env) {
     p.n_cdf = env->P * 2 * 9;
     p.lds_cdf = env->P <= 64 ? 1 : 0;
     p.ctab_off = p.lds_cdf ? ((p.n_cdf * 8 + 15) / 16) * 16 : 0;
+    p.resp_off = p.ctab_off + ((env->HW * 4 + 15) / 16) * 16;
     p.obs_be = env->obs_be;
     p.e_begin = 0;
     p.e_end = env->E;
@@ -1546,7 +1571,7 @@ hipError_t launch_v2(const Env *env, const gw::Params &p, hipStream_t s) {
     const int64_t n = p.e_end - p.e_begin;  // this launch's env range (a pipeline chunk or all)
     if (n <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((n + BE - 1) / BE);
-    const size_t dyn = (size_t)p.ctab_off + sizeof(uint32_t) * (size_t)env->HW;
+    const size_t dyn = (size_t)p.resp_off + (FEAR ? 100 * sizeof(double) : 0);
     hipLaunchKernelGGL((gw::step_v2<N, KMAX, FEAR, OBS>), dim3(grid), dim3(gw::V2Cfg<N, KMAX, FEAR>::THREADS), dyn, s, p);
     return hipGetLastError();
 }
