@@ -214,64 +214,65 @@ struct World {
                 continue;
             }
             const bool active_sub = (S == 0) || ((two >> i) & 1u);
-            const bool moving = active_sub & (bool)((mv >> i) & 1u) & !((crash >> i) & 1u);
-            const bool ok = (okm(old) >> dir_of(i)) & 1u;  // clip + WorldState[new] >= 0
-            nal[i][S + 1] = (moving & ok) ? old + delta[i] : old;
-            restr |= (uint32_t)(moving & !ok) << i;
+            const bool moving = active_sub && ((mv >> i) & 1u) && !((crash >> i) & 1u);
+            int nw = old;
+            if (moving) {
+                const bool ok = (okm(old) >> dir_of(i)) & 1u;  // clip + WorldState[new] >= 0
+                nw = ok ? old + delta[i] : old;
+                restr |= (uint32_t)(!ok) << i;
+            }
+            nal[i][S + 1] = nw;
         }
-    }
-
-    // overhang test of :310-312 / :341-343 in quarter steps, per (len_i, len_j) at sub-step S
-    template <int S>
-    __device__ __forceinline__ static bool overhang_ok(bool two_a, bool two_b) {
-        // (4*ceil_a - q_a) + (q_b - 4*floor_b) <= 4
-        constexpr bool c11 = SubStep<S>::ohf1 + SubStep<S>::ohc1 <= 4;
-        constexpr bool c12 = SubStep<S>::ohf1 + SubStep<S>::ohc2 <= 4;
-        constexpr bool c21 = SubStep<S>::ohf2 + SubStep<S>::ohc1 <= 4;
-        constexpr bool c22 = SubStep<S>::ohf2 + SubStep<S>::ohc2 <= 4;
-        return two_a ? (two_b ? c22 : c21) : (two_b ? c12 : c11);
     }
 
     template <int S>
     __device__ __forceinline__ void resolve() {  // collision_checks_and_resolution :233-405
         if (near == 0) return;  // no pair can collide: every pass counts 0 (crash stays 0)
         for (int pass = 0; pass < 2 * N; ++pass) {
-            int Af[N], Ac[N];
-#pragma unroll
-            for (int i = 0; i < N; ++i) {
-                Af[i] = fl<S>(i);
-                Ac[i] = ce<S>(i);
-            }
             uint32_t hit = 0;
 #pragma unroll
             for (int ii = 0; ii < N - 1; ++ii) {
+                const int Af = fl<S>(ii), Ac = ce<S>(ii);
                 const bool t_i = (two >> ii) & 1u;
+                const int ohf_i = t_i ? SubStep<S>::ohf2 : SubStep<S>::ohf1;
+                const int ohc_i = t_i ? SubStep<S>::ohc2 : SubStep<S>::ohc1;
 #pragma unroll
                 for (int jj = ii + 1; jj < N; ++jj) {
+                    if (!((near >> pair_bit(ii, jj)) & 1u)) continue;
+                    const int Bf = fl<S>(jj), Bc = ce<S>(jj);
                     const bool t_j = (two >> jj) & 1u;
-                    const int af = Af[ii], ac = Ac[ii], bf = Af[jj], bc = Ac[jj];
-                    const int li = loc[ii], lj = loc[jj];
-                    const bool eqFF = af == bf, eqCC = ac == bc, eqFC = af == bc, eqCF = ac == bf;
-                    const bool sd = (ac - af) == (bc - bf);
-                    const bool slide_fc = overhang_ok<S>(t_i, t_j) & sd;   // :307-337
-                    const bool slide_cf = overhang_ok<S>(t_j, t_i) & sd;   // :339-368
-                    const bool old_x = ((af == lj) | (ac == lj)) & ((li == bf) | (li == bc));  // :371-378
-                    // the elif chain of :276-384, branch-free
-                    const bool coll = eqFF | eqCC | (eqFC ? (eqCF | !slide_fc) : (eqCF ? !slide_cf : old_x));
-                    const bool nb = (near >> pair_bit(ii, jj)) & 1u;
-                    hit |= (coll & nb) ? ((1u << ii) | (1u << jj)) : 0u;
+                    const int ohf_j = t_j ? SubStep<S>::ohf2 : SubStep<S>::ohf1;
+                    const int ohc_j = t_j ? SubStep<S>::ohc2 : SubStep<S>::ohc1;
+                    const bool same_dir = (Ac - Af) == (Bc - Bf);
+                    bool coll;
+                    if (Af == Bf || Ac == Bc) {
+                        coll = true;                                    // :276-278
+                    } else if (Af == Bc && Ac == Bf) {
+                        coll = true;                                    // :291-294
+                    } else if (Af == Bc) {
+                        coll = !((ohf_i + ohc_j) <= 4 && same_dir);     // :307-337
+                    } else if (Ac == Bf) {
+                        coll = !((ohf_j + ohc_i) <= 4 && same_dir);     // :339-368
+                    } else {
+                        const int Li = loc[ii], Lj = loc[jj];           // :371-378
+                        coll = (Af == Lj && Li == Bf) || (Ac == Lj && Li == Bc) ||
+                               (Af == Lj && Li == Bc) || (Ac == Lj && Li == Bf);
+                    }
+                    if (coll) hit |= (1u << ii) | (1u << jj);
                 }
             }
             crash |= hit;
             // revertStepsWithCollisions :190-209 (all crashed agents, every pass)
 #pragma unroll
             for (int i = 0; i < N; ++i) {
-                const bool cr = (crash >> i) & 1u;
-                const int f = ((two >> i) & 1u) ? SubStep<S>::f2 : SubStep<S>::f1;
+                if ((crash >> i) & 1u) {
+                    const int f = ((two >> i) & 1u) ? SubStep<S>::f2 : SubStep<S>::f1;
 #pragma unroll
-                for (int k = 0; k <= S + 1; ++k) nal[i][k] = (cr & (k >= f)) ? loc[i] : nal[i][k];
+                    for (int k = 0; k <= S + 1; ++k)
+                        if (k >= f) nal[i][k] = loc[i];
+                }
             }
-            if (hit == 0) break;
+            if (hit == 0) break;  // this pass recorded no collision (CollisionCount == 0)
         }
     }
 

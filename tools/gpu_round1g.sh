@@ -1,0 +1,11 @@
+mkdir -p gpurun_out/v6; rm -f gpurun_out/v6/*.log
+echo "== pytest gpu" && timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/v6/pytest_gpu.log 2>&1; rc=$?; tail -5 gpurun_out/v6/pytest_gpu.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+B="python bench.py --steps 200 --warmup 20 --no-cpu-baseline"
+run() { tag=$1; shift; env "$@" timeout -k 10 200 $B $EXTRA > gpurun_out/v6/$tag.log 2>&1; python3 -c "
+import json; l=[x for x in open('gpurun_out/v6/$tag.log') if x.startswith('{')][-1]; j=json.loads(l); print('$tag', round(j['ms_per_step'],4), {k: round(v,4) for k,v in j['kernels_ms'].items()}, j['roofline']['kernel'], round(j['roofline']['achieved']))" || tail -3 gpurun_out/v6/$tag.log; }
+EXTRA=""; run def
+EXTRA="--envs 8192"; run e8192
+EXTRA="--fear 0"; run f0
+EXTRA="--config c4f"; run c4f
+EXTRA="--config c2"; run c2
