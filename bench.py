@@ -98,6 +98,9 @@ def main():
     ap.add_argument("--envs", type=int, default=0, help="override envs per GPU")
     ap.add_argument("--fear", type=int, default=-1, help="override FeAR on (1) / off (0)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-every", type=int, default=8,
+                    help="bracket every n-th timed step's kernels with HIP events (0 = none); the "
+                         "events themselves cost ~2-3 us per kernel boundary, so not every step")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     args = ap.parse_args()
 
@@ -142,14 +145,16 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
 
-    env.profile(True)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ev0.record(stream)
+    pe = args.profile_every
     for i in range(args.steps):
+        if pe > 0:
+            env.profile(i % pe == 0)
         r = one_step(i)
     ev1.record(stream)
     torch.cuda.synchronize()
@@ -158,7 +163,7 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     env.profile(False)
-    (ms_step, ms_obs), nprof = env.profile_read()
+    (ms_step, ms_obs, ms_fear), nprof = env.profile_read()
     gpu_ms = ev0.elapsed_time(ev1)
 
     t_local = torch.tensor([wall], dtype=torch.float64, device="cuda")
@@ -170,6 +175,7 @@ def main():
     if rank == 0:
         step_b, obs_b = algorithmic_bytes(N, K, HW)
         avg_step_ms, avg_obs_ms = ms_step / max(nprof, 1), ms_obs / max(nprof, 1)
+        avg_fear_ms = ms_fear / max(nprof, 1)
         fused = env.fused
         if fused:  # one launch per step moves every byte of the step
             dom, bytes_per_launch, dur = "step_fused", (step_b + obs_b) * E, avg_step_ms
@@ -177,7 +183,7 @@ def main():
             dom, bytes_per_launch, dur = "obs_kernel", obs_b * E, avg_obs_ms
         else:
             dom, bytes_per_launch, dur = "step_kernel", step_b * E, avg_step_ms
-        achieved = bytes_per_launch / (dur * 1e-3) / 1e9
+        achieved = bytes_per_launch / (dur * 1e-3) / 1e9 if dur > 0 else None
         traffic, traffic_src = None, None
         try:  # HBM bytes measured by the PMC passes committed under profiles/ for this workload
             with open(os.path.join(REPO, "profiles", "latest.json")) as f:
@@ -205,10 +211,11 @@ def main():
                        "global_envs": world * E, "agents": N, "rl_agents": K, "grid": [env.H, env.W],
                        "fear": cfg["fear"], "parallelism": f"env-sharded dp{world}"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
                          "traffic_source": traffic_src,
                          "bytes_per_launch": bytes_per_launch, "avg_launch_ms": dur},
-            "kernels_ms": {"step_kernel": avg_step_ms, "obs_kernel": avg_obs_ms,
+            "kernels_ms": {"profiled_steps": nprof, "step_kernel": avg_step_ms, "obs_kernel": avg_obs_ms, "fear_kernel": avg_fear_ms,
+                           "kernel_path": os.environ.get("GW_KERNEL", "defer"),
                            "stream_ms_per_step": gpu_ms / args.steps,
                            "pipeline_chunks": int(os.environ.get("GW_CHUNKS", "1")) if not env.fused else 1},
             "last_step_episodes": {"completed": stats[1], "mean_return": stats[0] / max(stats[1], 1.0),

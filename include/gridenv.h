@@ -128,14 +128,17 @@ gw_status gw_state_view(void *env, gw_state *out);
  * gw_state layout (device or pinned host memory), enqueued on stream. */
 gw_status gw_copy_state(void *env, const gw_state *buf, int to_env, void *stream);
 
-/* Per-launch timing: while enabled, gw_step records HIP events on its stream around each of
- * its two kernels (step_kernel, obs_kernel).  gw_profile_read synchronises on those events,
- * returns the summed elapsed milliseconds per kernel and the number of gw_step calls timed,
- * and clears them.  Used by bench.py for the live roofline. */
+/* Per-launch timing: while enabled, gw_step records HIP events around each of its kernels on
+ * the stream each is launched on: [0] the world-update kernel (step_v2), [1] the obs writer
+ * (obs_kernel), [2] the deferred FeAR kernel (fear_v2, GW_KERNEL=defer only; it runs on a second
+ * stream concurrently with [1]).  gw_profile_read synchronises on those events, returns the
+ * summed elapsed milliseconds per kernel and the number of gw_step calls timed, and clears
+ * them.  Used by bench.py for the live roofline. */
 gw_status gw_profile(void *env, int enable);
-gw_status gw_profile_read(void *env, double out_ms[2], int64_t *n_steps);
+gw_status gw_profile_read(void *env, double out_ms[3], int64_t *n_steps);
 
-/* Rows of the gw_step_out.stats buffer (one per step_kernel block). */
+/* Rows of the gw_step_out.stats buffer (one per kernel block; GW_KERNEL=defer: the world-update
+ * kernel's rows then fear_v2's rows, each kernel filling the fields it owns, zeros elsewhere). */
 int64_t gw_stats_rows(void *env);
 
 /* Sizes: H, W, N, K, E (out[0..4]). */

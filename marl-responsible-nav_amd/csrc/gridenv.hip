@@ -89,6 +89,8 @@ struct Params {
     int lds_cdf, n_cdf, ctab_off, resp_off;  // step_v2 dynamic LDS: [cdf][cell table][Resp 100 f64]
     int obs_be;               // envs per obs_kernel block (<= OBS_BE)
     int64_t e_begin, e_end;   // env range of this launch (step_v2 / obs_kernel chunks)
+    uint4 *fwork;             // [E][FearRec<N>::R4] deferred-FeAR records (GW_KERNEL=defer)
+    int64_t stats_row0;       // first gw_step_out.stats row this launch writes
     int apples[MAXN];
 };
 
@@ -456,7 +458,7 @@ __device__ __forceinline__ void write_desc_pos(uint32_t *d, const int (&pos)[N])
     for (int q = 0; q < 4; ++q) d[q] = w[q];
 }
 
-template <int N>
+template <int N, bool ZERO_SCORE = true>
 __device__ __forceinline__ void reset_env(const Params &p, int64_t e, uint32_t episode, int (&pos)[N]) {
     spawn_cells<N>(p, e, episode, pos);
 #pragma unroll
@@ -465,8 +467,61 @@ __device__ __forceinline__ void reset_env(const Params &p, int64_t e, uint32_t e
     p.st.t[e] = 0;
     p.st.episode[e] = episode;
     for (int k = 0; k < p.K; ++k) p.st.prev[(int64_t)k * p.E + e] = -1;
-    p.st.score[e] = 0.0;
-    p.st.fscore[e] = 0.0;
+    if (ZERO_SCORE) {  // with deferred FeAR the fear kernel owns score / fear_score
+        p.st.score[e] = 0.0;
+        p.st.fscore[e] = 0.0;
+    }
+}
+
+// Deferred-FeAR record of one env step (GW_KERNEL=defer): what fear_v2 needs to finish the
+// step after step_v2 has moved the world on.  R4 uint4 words per env, AoS for 16-byte
+// coalesced access:  u16 pre-step cells [N] | u8 actions [N] (bit 7 of byte 0 = done) | i8 env
+// rewards [K].  N <= 4: words 0-1 | 2 | 3;  N <= 8: words 0-3 | 4-5 | 6-7.
+template <int N>
+struct FearRec {
+    static constexpr int R4 = N <= 4 ? 1 : 2, PW = 2 * R4, AW = PW, RW = PW + R4;
+    uint32_t w[4 * R4];
+};
+
+template <int N>
+__device__ __forceinline__ void store_fear_rec(const Params &p, int64_t e, const int (&pos)[N], const int (&act)[N],
+                                               const int (&rew)[MAXN], bool done) {
+    using R = FearRec<N>;
+    R r;
+#pragma unroll
+    for (int i = 0; i < 4 * R::R4; ++i) r.w[i] = 0u;
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+        r.w[n >> 1] |= ((uint32_t)pos[n] & 0xFFFFu) << (16 * (n & 1));
+        r.w[R::AW + (n >> 2)] |= ((uint32_t)act[n] & 0x7Fu) << (8 * (n & 3));
+        if (n < p.K) r.w[R::RW + (n >> 2)] |= ((uint32_t)rew[n] & 0xFFu) << (8 * (n & 3));
+    }
+    r.w[R::AW] |= (uint32_t)done << 7;
+    uint4 *dst = p.fwork + e * R::R4;
+#pragma unroll
+    for (int q = 0; q < R::R4; ++q) dst[q] = make_uint4(r.w[4 * q], r.w[4 * q + 1], r.w[4 * q + 2], r.w[4 * q + 3]);
+}
+
+template <int N>
+__device__ __forceinline__ void load_fear_rec(const Params &p, int64_t e, int (&pos)[N], int (&act)[N],
+                                              int (&rew)[MAXN], bool &done) {
+    using R = FearRec<N>;
+    R r;
+    const uint4 *src = p.fwork + e * R::R4;
+#pragma unroll
+    for (int q = 0; q < R::R4; ++q) {
+        const uint4 v = src[q];
+        r.w[4 * q] = v.x; r.w[4 * q + 1] = v.y; r.w[4 * q + 2] = v.z; r.w[4 * q + 3] = v.w;
+    }
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+        pos[n] = (int)((r.w[n >> 1] >> (16 * (n & 1))) & 0xFFFFu);
+        act[n] = (int)((r.w[R::AW + (n >> 2)] >> (8 * (n & 3))) & 0x7Fu);
+    }
+#pragma unroll
+    for (int k = 0; k < MAXN; ++k)
+        rew[k] = (k < N) ? (int)(int8_t)((r.w[R::RW + (k >> 2)] >> (8 * (k & 3))) & 0xFFu) : 0;
+    done = (r.w[R::AW] >> 7) & 1u;
 }
 
 // Rewards, dones, rollout arithmetic, state update, auto-reset, outputs, obs descriptor.
@@ -527,7 +582,10 @@ __device__ __forceinline__ void store_desc(const Params &p, int64_t e, const Obs
     if (oi.flags & D_FINAL) write_desc_pos<N>(d + 8, oi.fpos);
 }
 
-template <int N>
+// DEFER (GW_KERNEL=defer, FeAR on): everything FeAR touches -- fear, shaped reward, score,
+// fear_score, ep_return / ep_fear and stats fields 0, 2, 5 -- is left to fear_v2, which gets a
+// FearRec; the rest (positions, dones, env rewards, auto-reset, obs descriptor) is final here.
+template <int N, bool DEFER = false>
 __device__ __forceinline__ void finish_env(const Params &p, int64_t e, const EnvState<N> &es,
                                            const int (&act)[N], const int (&mdr)[N],
                                            const double (&fear)[MAXN], uint32_t crash,
@@ -576,18 +634,18 @@ __device__ __forceinline__ void finish_env(const Params &p, int64_t e, const Env
         shaped[k] = __dadd_rn(__dmul_rn(p.fear_weight, fear[k]), (double)rew[k]);  // agent.py:130
         fsum_in[k] = fear[k];
     }
-    const double score = __dadd_rn(es.score, np_sum_small(shaped, K));            // agent.py:173
-    const double fscore = __dadd_rn(es.fscore, np_sum_small(fsum_in, K));          // agent.py:141
+    const double score = DEFER ? 0.0 : __dadd_rn(es.score, np_sum_small(shaped, K));    // agent.py:173
+    const double fscore = DEFER ? 0.0 : __dadd_rn(es.fscore, np_sum_small(fsum_in, K));  // agent.py:141
     const bool done = ((term & allk) == allk) || ((trunc & allk) == allk) ||
                       (p.max_steps > 0 && t >= p.max_steps);                       // agent.py:241-243
 
     const gw_step_out &o = p.out;
-    ct.v[0] = done ? score : 0.0;
+    ct.v[0] = (done && !DEFER) ? score : 0.0;
     ct.v[1] = done ? 1.0 : 0.0;
-    ct.v[2] = np_sum_small(fsum_in, K);
+    ct.v[2] = DEFER ? 0.0 : np_sum_small(fsum_in, K);
     ct.v[3] = (double)crash_count;
     ct.v[4] = (double)apple_rewarded;
-    ct.v[5] = np_sum_small(shaped, K);
+    ct.v[5] = DEFER ? 0.0 : np_sum_small(shaped, K);
     ct.v[6] = done ? (double)t : 0.0;
     ct.v[7] = 1.0;
 #pragma unroll
@@ -595,17 +653,18 @@ __device__ __forceinline__ void finish_env(const Params &p, int64_t e, const Env
         if (k >= K) continue;
         const int64_t ek = e * K + k;
         if (o.reward) o.reward[ek] = (double)rew[k];
-        if (o.fear) o.fear[ek] = fear[k];
-        if (o.shaped) o.shaped[ek] = shaped[k];
+        if (!DEFER && o.fear) o.fear[ek] = fear[k];
+        if (!DEFER && o.shaped) o.shaped[ek] = shaped[k];
         if (o.term) o.term[ek] = (uint8_t)((term >> k) & 1u);
         if (o.trunc) o.trunc[ek] = (uint8_t)((trunc >> k) & 1u);
     }
     if (o.done) o.done[e] = done;
     if (o.crashes) o.crashes[e] = crash_count;
     if (o.apples) o.apples[e] = apple_rewarded;
-    if (o.ep_return) o.ep_return[e] = score;
-    if (o.ep_fear) o.ep_fear[e] = fscore;
+    if (!DEFER && o.ep_return) o.ep_return[e] = score;
+    if (!DEFER && o.ep_fear) o.ep_fear[e] = fscore;
     if (o.ep_len) o.ep_len[e] = t;
+    if (DEFER) store_fear_rec<N>(p, e, es.pos, act, rew, done);
     if (o.crash_bits) o.crash_bits[e] = (uint8_t)crash;
     if (o.restr_bits) o.restr_bits[e] = (uint8_t)restr;
 #pragma unroll
@@ -619,7 +678,7 @@ __device__ __forceinline__ void finish_env(const Params &p, int64_t e, const Env
         // terminal obs -> final_obs, then CustomMAEnv.reset for the next episode
         const uint32_t ep = es.episode + 1;
         int np_[N];
-        reset_env<N>(p, e, ep, np_);
+        reset_env<N, !DEFER>(p, e, ep, np_);
 #pragma unroll
         for (int n = 0; n < N; ++n) {
             oi.fpos[n] = fin[n];
@@ -634,8 +693,10 @@ __device__ __forceinline__ void finish_env(const Params &p, int64_t e, const Env
         for (int n = 0; n < N; ++n) p.st.pos[(int64_t)n * p.E + e] = fin[n];
         p.st.flags[e] = apples | (term << 8) | (trunc << 16);
         p.st.t[e] = t;
-        p.st.score[e] = score;
-        p.st.fscore[e] = fscore;
+        if (!DEFER) {
+            p.st.score[e] = score;
+            p.st.fscore[e] = fscore;
+        }
 #pragma unroll
         for (int n = 0; n < N; ++n) oi.pos[n] = oi.fpos[n] = fin[n];
         oi.flags = D_WRITE | (apples << 8);
@@ -1170,7 +1231,126 @@ __device__ __forceinline__ void lds_fill(uint32_t *dst, const uint32_t *__restri
     for (int i = (n4 << 2) + tid; i < n; i += T) dst[i] = src[i];
 }
 
-template <int N, int KMAX, bool FEAR, bool OBS>
+// FeAR phase A of one env (custom/ma_customenv.py:247-251, Responsibility.py:135-210): close sets
+// (:456-464) into sh.close and the de-duplicated counterfactual task list appended to sh.tasks.
+// Expects sh.pos / sh.act / sh.mdr of the env filled.
+template <int N, int KMAX, class Sh>
+__device__ __forceinline__ void fear_plan(const Params &p, Sh &sh, int el, const int (&pos)[N], const int (&act)[N]) {
+    using Cfg = typename Sh::Cfg;
+    const int K = p.K;
+    int ntask = 0;
+    uint32_t close[KMAX];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+        close[k] = 0;
+        if (k >= K) continue;
+#pragma unroll
+        for (int n = 0; n < N; ++n)
+            if (n == k || manhattan(p, pos[k], pos[n]) <= 5) close[k] |= 1u << n;
+        sh.close[el][k] = (uint8_t)close[k];
+        if (act[k] != (int)sh.mdr[el][k]) ntask += 2 + 16 * (__popc(close[k]) - 1);
+    }
+    if (!ntask) return;
+    int slot = atomicAdd(&sh.ntask, ntask);
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+        if (k >= K || act[k] == (int)sh.mdr[el][k]) continue;
+        sh.tasks[slot++] = Cfg::enc(el, k, 0, 0, 15);
+        sh.tasks[slot++] = Cfg::enc(el, k, 0, 1, 15);
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            if (j == k || !((close[k] >> j) & 1u)) continue;
+#pragma unroll
+            for (int var = 0; var < 2; ++var)
+                for (int b = 0; b < NA; ++b)
+                    if (b != act[j]) sh.tasks[slot++] = Cfg::enc(el, k, j, var, b);
+        }
+    }
+}
+
+// FeAR phase B, one counterfactual world update (task bits: see V2Cfg::enc): the joint action
+// with actor k's action (var 0: MdR, var 1: its own) and agent j's alternative b (15 = none);
+// agents outside k's close set stay.  Records which agents end valid (no crash, no restriction).
+template <int N, int KMAX, class Sh, class OK>
+__device__ __forceinline__ void fear_task(const Params &p, Sh &sh, uint32_t tk, const OK &okv) {
+    const int el = tk & 63, b = (tk >> 6) & 15, var = (tk >> 10) & 1, j = (tk >> 11) & 7, k = (int)(tk >> 14);
+    int pos[N], joint[N], fin[N];
+    const uint32_t cl = sh.close[el][k];
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+        pos[n] = sh.pos[el][n];
+        joint[n] = ((cl >> n) & 1u) ? (int)sh.act[el][n] : 0;
+        if (n == k && var == 0) joint[n] = sh.mdr[el][n];
+        if (n == j && b != 15) joint[n] = b;
+    }
+    int apple[MAXN];
+#pragma unroll
+    for (int q = 0; q < MAXN; ++q) apple[q] = -1;
+    World<N> w;
+    w.init(pos, joint, p.W, p.w_magic);
+    uint32_t caught;
+    simulate<N, true>(w, okv, 0, apple, caught, fin);
+    const uint32_t valid = ~(w.crash | w.restr) & ((1u << N) - 1u);
+    if (b == 15)
+        sh.base[el][k][var] = (uint8_t)valid;
+    else
+        sh.cj[el][k][j][var][b] = (uint8_t)((valid >> j) & 1u);
+}
+
+// FeAR phase C of one env: V counts -> Resp table -> np.sum of the Resp row in numpy's order.
+template <int N, int KMAX, class Sh>
+__device__ __forceinline__ void fear_values(const Params &p, const Sh &sh, int el, const int (&act)[N],
+                                            const int (&mdr)[N], const double *resp_s, double (&fear)[MAXN]) {
+#pragma unroll
+    for (int k = 0; k < MAXN; ++k) fear[k] = 0.0;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+        if (k >= p.K || act[k] == mdr[k]) continue;
+        const uint32_t cl = sh.close[el][k];
+        const uint32_t b0 = sh.base[el][k][0], b1 = sh.base[el][k][1];
+        double resp[N];
+#pragma unroll
+        for (int jj = 0; jj < N; ++jj) {
+            resp[jj] = 0.0;
+            if (jj == k) continue;
+            int vm, va;
+            if ((cl >> jj) & 1u) {
+                vm = 0;
+                va = 0;
+                for (int b = 0; b < NA; ++b) {
+                    vm += (b == act[jj]) ? (int)((b0 >> jj) & 1u) : (int)sh.cj[el][k][jj][0][b];
+                    va += (b == act[jj]) ? (int)((b1 >> jj) & 1u) : (int)sh.cj[el][k][jj][1][b];
+                }
+            } else {
+                vm = 9 * (int)((b0 >> jj) & 1u);
+                va = 9 * (int)((b1 >> jj) & 1u);
+            }
+            resp[jj] = resp_s[vm * 10 + va];
+        }
+        fear[k] = np_sum_row<N>(resp, k);
+    }
+}
+
+// Block statistics: deterministic wave butterfly + fixed-order cross-wave sum, one row per block.
+template <int T>
+__device__ __forceinline__ void block_stats(const Params &p, Contrib &ct, double (&red)[T / 64][GW_STATS], int tid,
+                                            int64_t row) {
+    if (p.out.stats) {
+        wave_sum(ct);
+        if ((tid & 63) == 0)
+#pragma unroll
+            for (int i = 0; i < GW_STATS; ++i) red[tid >> 6][i] = ct.v[i];
+    }
+    __syncthreads();
+    if (p.out.stats && tid < GW_STATS) {
+        double acc = red[0][tid];
+#pragma unroll
+        for (int w = 1; w < T / 64; ++w) acc = __dadd_rn(acc, red[w][tid]);
+        p.out.stats[row * GW_STATS + tid] = acc;
+    }
+}
+
+template <int N, int KMAX, bool FEAR, bool OBS, bool DEFER = false>
 __global__ void __launch_bounds__(128) step_v2(Params p) {
     using Cfg = V2Cfg<N, KMAX, FEAR>;
     using Sh = V2Shared<N, KMAX, FEAR, OBS>;
@@ -1213,37 +1393,10 @@ __global__ void __launch_bounds__(128) step_v2(Params p) {
                 sh.act[tid][n] = (int8_t)act[n];
                 sh.mdr[tid][n] = (int8_t)((ctab[es.pos[n]] >> CT_MDR) & 0xFu);
             }
-            int ntask = 0;
-            uint32_t close[KMAX];
 #pragma unroll
-            for (int k = 0; k < KMAX; ++k) {
-                close[k] = 0;
-                sh.apple[tid][k] = (k < K && ((es.flags >> k) & 1u)) ? p.apples[k] : -1;
-                if (k >= K) continue;
-#pragma unroll
-                for (int n = 0; n < N; ++n)
-                    if (n == k || manhattan(p, es.pos[k], es.pos[n]) <= 5) close[k] |= 1u << n;  // :456-464
-                sh.close[tid][k] = (uint8_t)close[k];
-                if (act[k] != (int)sh.mdr[tid][k]) ntask += 2 + 16 * (__popc(close[k]) - 1);
-            }
+            for (int k = 0; k < KMAX; ++k) sh.apple[tid][k] = (k < K && ((es.flags >> k) & 1u)) ? p.apples[k] : -1;
             sh.tasks[tid] = Cfg::enc(tid, 0, 0, 0, 0);
-            if (ntask) {
-                int slot = atomicAdd(&sh.ntask, ntask);
-#pragma unroll
-                for (int k = 0; k < KMAX; ++k) {
-                    if (k >= K || act[k] == (int)sh.mdr[tid][k]) continue;
-                    sh.tasks[slot++] = Cfg::enc(tid, k, 0, 0, 15);
-                    sh.tasks[slot++] = Cfg::enc(tid, k, 0, 1, 15);
-#pragma unroll
-                    for (int j = 0; j < N; ++j) {
-                        if (j == k || !((close[k] >> j) & 1u)) continue;
-#pragma unroll
-                        for (int var = 0; var < 2; ++var)
-                            for (int b = 0; b < NA; ++b)
-                                if (b != act[j]) sh.tasks[slot++] = Cfg::enc(tid, k, j, var, b);
-                    }
-                }
-            }
+            fear_plan<N, KMAX>(p, sh, tid, es.pos, act);
         }
         __syncthreads();
         // ---- B ----
@@ -1306,34 +1459,7 @@ __global__ void __launch_bounds__(128) step_v2(Params p) {
                 fin[n] = sh.fin[tid][n];
             }
             double fear[MAXN];
-#pragma unroll
-            for (int k = 0; k < MAXN; ++k) fear[k] = 0.0;
-#pragma unroll
-            for (int k = 0; k < KMAX; ++k) {
-                if (k >= K || act[k] == mdr[k]) continue;
-                const uint32_t cl = sh.close[tid][k];
-                const uint32_t b0 = sh.base[tid][k][0], b1 = sh.base[tid][k][1];
-                double resp[N];
-#pragma unroll
-                for (int jj = 0; jj < N; ++jj) {
-                    resp[jj] = 0.0;
-                    if (jj == k) continue;
-                    int vm, va;
-                    if ((cl >> jj) & 1u) {
-                        vm = 0;
-                        va = 0;
-                        for (int b = 0; b < NA; ++b) {
-                            vm += (b == act[jj]) ? (int)((b0 >> jj) & 1u) : (int)sh.cj[tid][k][jj][0][b];
-                            va += (b == act[jj]) ? (int)((b1 >> jj) & 1u) : (int)sh.cj[tid][k][jj][1][b];
-                        }
-                    } else {
-                        vm = 9 * (int)((b0 >> jj) & 1u);
-                        va = 9 * (int)((b1 >> jj) & 1u);
-                    }
-                    resp[jj] = resp_s[vm * 10 + va];
-                }
-                fear[k] = np_sum_row<N>(resp, k);
-            }
+            fear_values<N, KMAX>(p, sh, tid, act, mdr, resp_s, fear);
             const uint32_t bits = sh.bits[tid];
             ObsInfo<N> oi;
             finish_env<N>(p, e, es, act, mdr, fear, bits & 0xFFu, (bits >> 8) & 0xFFu, fin, (bits >> 16) & 0xFFu, ct, oi, ctab);
@@ -1366,7 +1492,7 @@ __global__ void __launch_bounds__(128) step_v2(Params p) {
 #pragma unroll
             for (int k = 0; k < MAXN; ++k) fear[k] = 0.0;
             ObsInfo<N> oi;
-            finish_env<N>(p, e, es, act, mdr, fear, w.crash, w.restr, fin, caught, ct, oi, ctab);
+            finish_env<N, DEFER>(p, e, es, act, mdr, fear, w.crash, w.restr, fin, caught, ct, oi, ctab);
             if constexpr (OBS) {
                 v2_patches<N, 0, OB, KMAX, NP>(p, tid, oi, ctab, sh.pc, sh.pv);
                 if (oi.flags & D_FINAL) v2_patches<N, 1, OB, KMAX, NP>(p, tid, oi, ctab, sh.pc, sh.pv);
@@ -1381,19 +1507,7 @@ __global__ void __launch_bounds__(128) step_v2(Params p) {
     }
 
     // ---- block statistics (deterministic tree) ----
-    if (p.out.stats) {
-        wave_sum(ct);
-        if ((tid & 63) == 0)
-#pragma unroll
-            for (int i = 0; i < GW_STATS; ++i) sh.red[tid >> 6][i] = ct.v[i];
-    }
-    __syncthreads();
-    if (p.out.stats && tid < GW_STATS) {
-        double acc = sh.red[0][tid];
-#pragma unroll
-        for (int w = 1; w < T / 64; ++w) acc = __dadd_rn(acc, sh.red[w][tid]);
-        p.out.stats[(e0 / BE) * GW_STATS + tid] = acc;
-    }
+    block_stats<T>(p, ct, sh.red, tid, p.stats_row0 + e0 / BE);
 
     if constexpr (OBS) {
         // ---- D: obs of the block's envs, 16-byte coalesced stores ----
@@ -1434,6 +1548,97 @@ __global__ void __launch_bounds__(128) step_v2(Params p) {
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// fear_v2 (GW_KERNEL=defer, FeAR on): the FeAR half of CustomMAEnv.step + the rollout's reward
+// shaping (custom/Responsibility.py:135-210, ma_customenv.py:247-252, maddpg/agent.py:124-173),
+// launched after step_v2<.., DEFER> on a second stream so that its integer-VALU-bound world
+// updates overlap the HBM-store-bound obs_kernel.  Inputs: the FearRec of each env (pre-step
+// cells, joint action, env rewards, done) and score / fear_score; same phases A/B/C as step_v2
+// without the env's own update.  Dynamic LDS: [cell table][Resp 100 f64] (no CDFs).
+// ---------------------------------------------------------------------------------------
+template <int N, int KMAX>
+__global__ void __launch_bounds__(128) fear_v2(Params p) {
+    using Cfg = V2Cfg<N, KMAX, true>;
+    using Sh = V2Shared<N, KMAX, true, false>;
+    constexpr int BE = Cfg::BE, T = Cfg::THREADS;
+    __shared__ Sh sh;
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+    uint32_t *ctab = reinterpret_cast<uint32_t *>(dyn + p.ctab_off);
+    double *resp_s = reinterpret_cast<double *>(dyn + p.resp_off);
+
+    const int tid = threadIdx.x;
+    if (p.e_begin + (int64_t)blockIdx.x * BE >= p.e_end) return;  // uniform per block
+    const int64_t e0 = p.e_begin + (int64_t)blockIdx.x * BE;
+    const int nenv = (int)min((int64_t)BE, p.e_end - e0);
+    const int K = p.K;
+    int pos[N], act[N], rew[MAXN];
+    bool done = false;
+    double score0 = 0.0, fscore0 = 0.0;
+    if (tid < nenv) {
+        const int64_t e = e0 + tid;
+        load_fear_rec<N>(p, e, pos, act, rew, done);
+        score0 = p.st.score[e];
+        fscore0 = p.st.fscore[e];
+    }
+    lds_fill<T>(ctab, p.tb.celltab, p.HW, tid);
+    lds_fill<T>(reinterpret_cast<uint32_t *>(resp_s), reinterpret_cast<const uint32_t *>(p.tb.resp), 200, tid);
+    if (tid == 0) sh.ntask = 0;
+    __syncthreads();
+    const CtabOk okv{ctab};
+    // ---- A ----
+    int mdr[N];
+    if (tid < nenv) {
+#pragma unroll
+        for (int n = 0; n < N; ++n) {
+            mdr[n] = (int)((ctab[pos[n]] >> CT_MDR) & 0xFu);
+            sh.pos[tid][n] = pos[n];
+            sh.act[tid][n] = (int8_t)act[n];
+            sh.mdr[tid][n] = (int8_t)mdr[n];
+        }
+        fear_plan<N, KMAX>(p, sh, tid, pos, act);
+    }
+    __syncthreads();
+    // ---- B ----
+    const int ntask = sh.ntask;
+    for (int ti = tid; ti < ntask; ti += T) fear_task<N, KMAX>(p, sh, sh.tasks[ti], okv);
+    __syncthreads();
+    // ---- C ----
+    Contrib ct;
+    contrib_zero(ct);
+    if (tid < nenv) {
+        const int64_t e = e0 + tid;
+        double fear[MAXN];
+        fear_values<N, KMAX>(p, sh, tid, act, mdr, resp_s, fear);
+        double shaped[MAXN], fsum_in[MAXN];
+#pragma unroll
+        for (int k = 0; k < MAXN; ++k) {
+            shaped[k] = fsum_in[k] = 0.0;
+            if (k >= K) continue;
+            shaped[k] = __dadd_rn(__dmul_rn(p.fear_weight, fear[k]), (double)rew[k]);  // agent.py:130
+            fsum_in[k] = fear[k];
+        }
+        const double score = __dadd_rn(score0, np_sum_small(shaped, K));    // agent.py:173
+        const double fscore = __dadd_rn(fscore0, np_sum_small(fsum_in, K));  // agent.py:141
+        const gw_step_out &o = p.out;
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) {
+            if (k >= K) continue;
+            const int64_t ek = e * K + k;
+            if (o.fear) o.fear[ek] = fear[k];
+            if (o.shaped) o.shaped[ek] = shaped[k];
+        }
+        if (o.ep_return) o.ep_return[e] = score;
+        if (o.ep_fear) o.ep_fear[e] = fscore;
+        const bool fresh = done && p.auto_reset;  // the next episode starts from 0
+        p.st.score[e] = fresh ? 0.0 : score;
+        p.st.fscore[e] = fresh ? 0.0 : fscore;
+        ct.v[0] = done ? score : 0.0;
+        ct.v[2] = np_sum_small(fsum_in, K);
+        ct.v[5] = np_sum_small(shaped, K);
+    }
+    block_stats<T>(p, ct, sh.red, tid, p.stats_row0 + e0 / BE);
+}
+
 }  // namespace gw
 
 // =========================================================================================
@@ -1463,11 +1668,14 @@ struct Env {
     uint64_t seed = 0;
     int apples[GW_MAX_AGENTS] = {0};
     bool initialized = false;
-    int mode = 1;        // GW_KERNEL: 0 "v1" (first kernels), 1 "split" step_v2 + obs_kernel (default), 2 "fused"
+    int mode = 3;        // GW_KERNEL: 0 "v1" (first kernels), 1 "split" step_v2 (FeAR inline) + obs_kernel,
+                         // 2 "fused", 3 "defer" (default; FeAR on: step_v2 <DEFER>, then fear_v2 || obs_kernel)
     int obs_be = 2;      // GW_OBS_BE: envs per obs_kernel block (2 measured best, 32x32 and 64x64)
     bool obs_nt = true;  // GW_OBS_NT=0: plain instead of nontemporal obs stores
     uint32_t *celltab = nullptr;
     uint32_t *roadbits = nullptr;
+    int defer_order = 3;            // GW_DEFER (A/B): 0 fear then obs on one stream, 1 fear on aux first,
+                                    // 2 obs first then fear on aux, 3 (default) as 1, aux stream high priority
     int chunks = 1;                 // GW_CHUNKS: step/obs pipeline depth (split path; 1 = off, measured best)
     hipStream_t aux = nullptr;      // second stream of the pipeline (created on first use)
     std::vector<hipEvent_t> sync_ev;  // fork/chunk/join events (timing disabled)
@@ -1480,16 +1688,36 @@ struct Env {
     // state
     int32_t *pos = nullptr, *t = nullptr, *prev = nullptr;
     uint32_t *flags = nullptr, *episode = nullptr, *desc = nullptr;
+    uint4 *fwork = nullptr;  // deferred-FeAR records (mode 3 with FeAR on)
     double *score = nullptr, *fscore = nullptr;
     std::vector<void *> allocs;
     // per-launch profiling events (gw_profile)
     bool profiling = false;
     std::vector<hipEvent_t> ev_pool;   // timing events, reused across calls
     size_t ev_used = 0;
-    struct Span { size_t b, e; int kind; };  // kind 0 = step kernel(s), 1 = obs kernel(s)
+    struct Span { size_t b, e; int kind; };  // kind 0 = step kernel(s), 1 = obs kernel(s), 2 = fear_v2
     std::vector<Span> spans;
     int64_t steps_timed = 0;
 };
+
+// the second stream and n fork/join events (timing disabled), created on first use
+gw_status ensure_aux(Env *env, int n) {
+    if (!env->aux) {
+        if (env->mode == 3 && env->defer_order == 3) {
+            int lo = 0, hi = 0;
+            HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+            HIP_TRY(hipStreamCreateWithPriority(&env->aux, hipStreamNonBlocking, hi));
+        } else {
+            HIP_TRY(hipStreamCreateWithFlags(&env->aux, hipStreamNonBlocking));
+        }
+    }
+    while ((int)env->sync_ev.size() < n) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        env->sync_ev.push_back(e);
+    }
+    return GW_OK;
+}
 
 hipEvent_t next_event(Env *env) {
     if (env->ev_used == env->ev_pool.size()) {
@@ -1535,6 +1763,8 @@ gw::Params make_params(const Env *env) {
     p.obs_be = env->obs_be;
     p.e_begin = 0;
     p.e_end = env->E;
+    p.fwork = env->fwork;
+    p.stats_row0 = 0;
     p.tb.roadbits = env->roadbits;
     p.st.pos = env->pos;
     p.st.flags = env->flags;
@@ -1566,19 +1796,63 @@ gw::Params make_params(const Env *env) {
     return p;
 }
 
-template <int N, int KMAX, bool FEAR, bool OBS>
+template <int N, int KMAX, bool FEAR, bool OBS, bool DEFER = false>
 hipError_t launch_v2(const Env *env, const gw::Params &p, hipStream_t s) {
     constexpr int BE = gw::V2Cfg<N, KMAX, FEAR>::BE;
     const int64_t n = p.e_end - p.e_begin;  // this launch's env range (a pipeline chunk or all)
     if (n <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((n + BE - 1) / BE);
     const size_t dyn = (size_t)p.resp_off + (FEAR ? 100 * sizeof(double) : 0);
-    hipLaunchKernelGGL((gw::step_v2<N, KMAX, FEAR, OBS>), dim3(grid), dim3(gw::V2Cfg<N, KMAX, FEAR>::THREADS), dyn, s, p);
+    hipLaunchKernelGGL((gw::step_v2<N, KMAX, FEAR, OBS, DEFER>), dim3(grid), dim3(gw::V2Cfg<N, KMAX, FEAR>::THREADS), dyn, s, p);
     return hipGetLastError();
+}
+
+// stats rows of the deferred world-update kernel; fear_v2's rows follow them
+template <int N>
+int64_t defer_step_rows(const Env *env) {
+    const int be = env->K <= 2 ? gw::V2Cfg<N, 2, false>::BE : gw::V2Cfg<N, N, false>::BE;
+    return (env->E + be - 1) / be;
+}
+
+template <int N, int KMAX>
+hipError_t launch_fear_k(const Env *env, const gw::Params &p0, hipStream_t s) {
+    constexpr int BE = gw::V2Cfg<N, KMAX, true>::BE;
+    gw::Params p = p0;
+    p.lds_cdf = 0;  // dynamic LDS [cell table][Resp]
+    p.ctab_off = 0;
+    p.resp_off = ((env->HW * 4 + 15) / 16) * 16;
+    p.stats_row0 = defer_step_rows<N>(env);
+    const int64_t n = p.e_end - p.e_begin;
+    if (n <= 0) return hipSuccess;
+    const unsigned grid = (unsigned)((n + BE - 1) / BE);
+    const size_t dyn = (size_t)p.resp_off + 100 * sizeof(double);
+    hipLaunchKernelGGL((gw::fear_v2<N, KMAX>), dim3(grid), dim3(gw::V2Cfg<N, KMAX, true>::THREADS), dyn, s, p);
+    return hipGetLastError();
+}
+
+template <int N>
+hipError_t launch_fear(const Env *env, const gw::Params &p, hipStream_t s) {
+    return env->K <= 2 ? launch_fear_k<N, 2>(env, p, s) : launch_fear_k<N, N>(env, p, s);
+}
+
+hipError_t dispatch_fear(const Env *env, const gw::Params &p, hipStream_t s) {
+    switch (env->N) {
+        case 1: return launch_fear<1>(env, p, s);
+        case 2: return launch_fear<2>(env, p, s);
+        case 3: return launch_fear<3>(env, p, s);
+        case 4: return launch_fear<4>(env, p, s);
+        case 5: return launch_fear<5>(env, p, s);
+        case 6: return launch_fear<6>(env, p, s);
+        case 7: return launch_fear<7>(env, p, s);
+        case 8: return launch_fear<8>(env, p, s);
+    }
+    return hipErrorInvalidValue;
 }
 
 template <int N, bool OBS>
 hipError_t launch_v2_k(const Env *env, const gw::Params &p, hipStream_t s) {
+    if (env->mode == 3 && env->fear && !OBS)  // deferred FeAR: the world update only, + FearRec
+        return env->K <= 2 ? launch_v2<N, 2, false, false, true>(env, p, s) : launch_v2<N, N, false, false, true>(env, p, s);
     if (env->fear)
         return env->K <= 2 ? launch_v2<N, 2, true, OBS>(env, p, s) : launch_v2<N, N, true, OBS>(env, p, s);
     return env->K <= 2 ? launch_v2<N, 2, false, OBS>(env, p, s) : launch_v2<N, N, false, OBS>(env, p, s);
@@ -1587,7 +1861,7 @@ hipError_t launch_v2_k(const Env *env, const gw::Params &p, hipStream_t s) {
 template <int N>
 hipError_t launch_step(const Env *env, const gw::Params &p, hipStream_t s) {
     if (env->mode == 2) return launch_v2_k<N, true>(env, p, s);
-    if (env->mode == 1) return launch_v2_k<N, false>(env, p, s);
+    if (env->mode == 1 || env->mode == 3) return launch_v2_k<N, false>(env, p, s);
     if (env->fear) {
         if (env->K <= 2) {
             constexpr int BE = gw::FearCfg<N, 2>::BE;
@@ -1662,6 +1936,10 @@ namespace {
 template <int N>
 int64_t stats_rows_n(const Env *env) {
     int be;
+    if (env->mode == 3 && env->fear) {
+        const int bf = env->K <= 2 ? gw::V2Cfg<N, 2, true>::BE : gw::V2Cfg<N, N, true>::BE;
+        return defer_step_rows<N>(env) + (env->E + bf - 1) / bf;
+    }
     if (env->mode >= 1) {
         if (env->fear) be = env->K <= 2 ? gw::V2Cfg<N, 2, true>::BE : gw::V2Cfg<N, N, true>::BE;
         else be = env->K <= 2 ? gw::V2Cfg<N, 2, false>::BE : gw::V2Cfg<N, N, false>::BE;
@@ -1752,9 +2030,13 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
     for (int k = 0; k < K; ++k) env->apples[k] = sc->apples[k];
     {
         const char *kv = std::getenv("GW_KERNEL");  // kernel path for A/B measurements
-        env->mode = 1;
+        env->mode = 3;
+        if (kv && std::strcmp(kv, "split") == 0) env->mode = 1;
         if (kv && std::strcmp(kv, "v1") == 0) env->mode = 0;
         if (kv && std::strcmp(kv, "fused") == 0 && HW % 4 == 0) env->mode = 2;
+        if (kv && std::strcmp(kv, "defer") == 0) env->mode = 3;
+        const char *dv = std::getenv("GW_DEFER");
+        if (dv) env->defer_order = std::max(0, std::min(3, std::atoi(dv)));
         const char *be = std::getenv("GW_OBS_BE");
         if (be) env->obs_be = std::max(1, std::min(gw::OBS_BE, std::atoi(be)));
         const char *nt = std::getenv("GW_OBS_NT");
@@ -1779,7 +2061,8 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
         (st = dalloc(env, &env->prev, (size_t)K * E)) || (st = dalloc(env, &env->flags, E)) ||
         (st = dalloc(env, &env->episode, E)) || (st = dalloc(env, &env->desc, E * gw::NDESC)) ||
         (st = dalloc(env, &env->score, E)) || (st = dalloc(env, &env->fscore, E)) ||
-        (st = dalloc(env, &env->celltab, HW)) || (st = dalloc(env, &env->roadbits, rbits.size())))
+        (st = dalloc(env, &env->celltab, HW)) || (st = dalloc(env, &env->roadbits, rbits.size())) ||
+        (env->mode == 3 && env->fear && (st = dalloc(env, &env->fwork, E * (N <= 4 ? 1 : 2)))))
         return cleanup(st);
     hipError_t he = hipSuccess;
 #define CP(dst, src, n) if (he == hipSuccess) he = hipMemcpy(dst, src, n, hipMemcpyHostToDevice)
@@ -1849,6 +2132,43 @@ gw_status gw_step(void *handle, const int32_t *rl_actions, const int32_t *script
     // chunk size: a multiple of every block size in play (v2 BE, obs_be) so blocks never straddle
     const int64_t unit = 128;  // multiple of every step_v2 BE (<= 128) and obs_be (<= 8)
     const int nch = (env->mode == 1 && want_obs && env->chunks > 1 && env->E >= unit * env->chunks) ? env->chunks : 1;
+    if (env->mode == 3 && env->fear) {
+        // world update; then fear_v2 on the aux stream || obs_kernel on s; join
+        size_t b;
+        GW_TRY(span_begin(s, b));
+        HIP_TRY(dispatch_step(env, p, s));
+        GW_TRY(span_end(s, b, 0));
+        if (!want_obs || env->defer_order == 0) {
+            GW_TRY(span_begin(s, b));
+            HIP_TRY(dispatch_fear(env, p, s));
+            GW_TRY(span_end(s, b, 2));
+            if (want_obs) {
+                GW_TRY(span_begin(s, b));
+                HIP_TRY(launch_obs(env, p, p.out.obs, p.out.final_obs, s));
+                GW_TRY(span_end(s, b, 1));
+            }
+            return GW_OK;
+        }
+        GW_TRY(ensure_aux(env, 2));
+        HIP_TRY(hipEventRecord(env->sync_ev[0], s));  // fork after the world update
+        if (env->defer_order == 2) {
+            GW_TRY(span_begin(s, b));
+            HIP_TRY(launch_obs(env, p, p.out.obs, p.out.final_obs, s));
+            GW_TRY(span_end(s, b, 1));
+        }
+        HIP_TRY(hipStreamWaitEvent(env->aux, env->sync_ev[0], 0));
+        GW_TRY(span_begin(env->aux, b));
+        HIP_TRY(dispatch_fear(env, p, env->aux));
+        GW_TRY(span_end(env->aux, b, 2));
+        if (env->defer_order != 2) {
+            GW_TRY(span_begin(s, b));
+            HIP_TRY(launch_obs(env, p, p.out.obs, p.out.final_obs, s));
+            GW_TRY(span_end(s, b, 1));
+        }
+        HIP_TRY(hipEventRecord(env->sync_ev[1], env->aux));
+        HIP_TRY(hipStreamWaitEvent(s, env->sync_ev[1], 0));
+        return GW_OK;
+    }
     if (nch == 1) {
         size_t b;
         GW_TRY(span_begin(s, b));
@@ -1863,12 +2183,7 @@ gw_status gw_step(void *handle, const int32_t *rl_actions, const int32_t *script
     }
     // Pipeline over env chunks: step_v2(chunk c) on `s`, obs_kernel(chunk c) on the aux stream
     // after an event; VALU-bound step chunks run concurrently with HBM-bound obs chunks.
-    if (!env->aux) HIP_TRY(hipStreamCreateWithFlags(&env->aux, hipStreamNonBlocking));
-    while ((int)env->sync_ev.size() < nch + 2) {
-        hipEvent_t e;
-        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        env->sync_ev.push_back(e);
-    }
+    GW_TRY(ensure_aux(env, nch + 2));
     HIP_TRY(hipEventRecord(env->sync_ev[0], s));           // fork: aux waits for prior work on s
     HIP_TRY(hipStreamWaitEvent(env->aux, env->sync_ev[0], 0));
     const int64_t per = ((env->E / nch + unit - 1) / unit) * unit;
@@ -1899,10 +2214,10 @@ gw_status gw_profile(void *handle, int enable) {
     return GW_OK;
 }
 
-gw_status gw_profile_read(void *handle, double out_ms[2], int64_t *n_steps) {
+gw_status gw_profile_read(void *handle, double out_ms[3], int64_t *n_steps) {
     Env *env = static_cast<Env *>(handle);
     if (!env || !out_ms) return fail(GW_ERR_ARG, "null argument");
-    out_ms[0] = out_ms[1] = 0.0;
+    out_ms[0] = out_ms[1] = out_ms[2] = 0.0;
     for (const Env::Span &sp : env->spans) {
         HIP_TRY(hipEventSynchronize(env->ev_pool[sp.e]));
         float ms = 0.f;

@@ -198,12 +198,13 @@ class VecGridEnv:
         _lib.check(self.lib.gw_profile(self.handle, int(enable)), "gw_profile")
 
     def profile_read(self):
-        """-> (ms summed over timed steps [step_kernel, obs_kernel], number of timed steps)."""
-        ms = (C.c_double * 2)()
+        """-> (ms summed over timed steps [step_kernel, obs_kernel, fear_kernel], timed steps).
+        fear_kernel is nonzero only with GW_KERNEL=defer (it overlaps obs_kernel there)."""
+        ms = (C.c_double * 3)()
         n = C.c_int64()
         with torch.cuda.device(self.device):
             _lib.check(self.lib.gw_profile_read(self.handle, ms, C.byref(n)), "gw_profile_read")
-        return (ms[0], ms[1]), n.value
+        return (ms[0], ms[1], ms[2]), n.value
 
     def positions(self) -> torch.Tensor:
         return self.state()["pos"].t().contiguous()

@@ -105,6 +105,10 @@ def _compare_native(sc, E, fear, steps, nthreads=16, offset=0, seed=7, weight=-5
         assert st[7] == E and st[1] == dn.sum()
         assert st[3] == sum(outs[e].crashes for e in range(E))
         np.testing.assert_allclose(st[0], sum(outs[e].ep_return for e in range(E) if outs[e].done), rtol=1e-12, atol=1e-9)
+        np.testing.assert_allclose(st[2], get("fear", K).sum(), rtol=1e-12, atol=1e-9)
+        np.testing.assert_allclose(st[5], get("shaped", K).sum(), rtol=1e-12, atol=1e-9)
+        assert st[4] == sum(outs[e].apples_caught for e in range(E))
+        assert st[6] == sum(outs[e].ep_len for e in range(E) if outs[e].done)
         done_total += int(dn.sum())
     assert bool((guard == 7.0).all()), "write past the stats buffer"
     env.close()
@@ -112,10 +116,12 @@ def _compare_native(sc, E, fear, steps, nthreads=16, offset=0, seed=7, weight=-5
 
 
 KERNEL_PATHS = {
-    "split": {"GW_KERNEL": "split"},                          # default: chunked 2-stream pipeline
+    "split": {"GW_KERNEL": "split", "GW_CHUNKS": "2"},       # FeAR inline in step_v2, chunked 2-stream pipeline
     "split1": {"GW_KERNEL": "split", "GW_CHUNKS": "1"},       # step_v2 then obs_kernel, one stream
     "split_plain": {"GW_KERNEL": "split", "GW_OBS_NT": "0", "GW_OBS_BE": "8"},
     "fused": {"GW_KERNEL": "fused"},                          # obs stores inside step_v2
+    "defer": {"GW_KERNEL": "defer"},                          # default: fear_v2 on a 2nd stream || obs_kernel
+    "defer_serial": {"GW_KERNEL": "defer", "GW_DEFER": "0"},  # step_v2 <DEFER>, fear_v2, obs_kernel, one stream
     "v1": {"GW_KERNEL": "v1"},                                # the first kernels
 }
 
