@@ -247,7 +247,13 @@ struct World {
                     const int ohc_j = t_j ? SubStep<S>::ohc2 : SubStep<S>::ohc1;
                     const bool same_dir = (Ac - Af) == (Bc - Bf);
                     bool coll;
-                    if (Af == Bf || Ac == Bc) {
+                    if constexpr (N <= 4) {  // the same elif chain as selects (few pairs: no VGPR pressure)
+                        const bool x1 = Af == Bc, x2 = Ac == Bf;
+                        const bool cross = ((Af == loc[jj]) | (Ac == loc[jj])) & ((loc[ii] == Bf) | (loc[ii] == Bc));
+                        const bool tail = x1 ? !((ohf_i + ohc_j) <= 4 && same_dir)
+                                             : (x2 ? !((ohf_j + ohc_i) <= 4 && same_dir) : cross);
+                        coll = (Af == Bf) | (Ac == Bc) | (x1 & x2) | tail;
+                    } else if (Af == Bf || Ac == Bc) {
                         coll = true;                                    // :276-278
                     } else if (Af == Bc && Ac == Bf) {
                         coll = true;                                    // :291-294
@@ -1114,24 +1120,31 @@ __global__ void __launch_bounds__(OBS_THREADS) obs_kernel(Params p, float *__res
 // cell table bits
 constexpr uint32_t CT_POL = 0, CT_MDR = 8, CT_AMASK = 12, CT_OK = 21, CT_ROAD = 25;
 
-template <int N, int KMAX, bool FEAR> struct V2Cfg {
+template <int N, int KMAX, bool FEAR, bool WIDE = false> struct V2Cfg {
     static constexpr int THREADS = 128;
-    static constexpr int BE = FEAR ? (KMAX <= 2 ? (N <= 4 ? 32 : 16) : (N <= 4 ? 16 : 4)) : (KMAX <= 2 ? 128 : 32);
-    static constexpr int MAXT = FEAR ? BE * (1 + KMAX * (2 + 16 * (N - 1))) : 1;
+    // WIDE (fear_v2, GW_FEAR_BE=wide): twice the envs per block, half the resident waves
+    static constexpr int BE = (WIDE ? 2 : 1) *
+        (FEAR ? (KMAX <= 2 ? (N <= 4 ? 32 : 16) : (N <= 4 ? 16 : 4)) : (KMAX <= 2 ? 128 : 32));
+    static_assert(!FEAR || BE <= 64, "task encoding holds 6 env bits");
+    // task list: [env sims (step_v2 only: BE)][base sims: 2 per actor k with act != MdR] then
+    // groups of 16 counterfactuals (one entry per (actor k, close j), expanded on the fly)
+    static constexpr int MAXB = FEAR ? BE * (1 + 2 * KMAX) : 1;
+    static constexpr int MAXG = FEAR ? BE * KMAX * (N > 1 ? N - 1 : 1) : 1;
     using Task = typename std::conditional<(KMAX <= 2), uint16_t, uint32_t>::type;
-    // task bits: env 0-5 | b 6-9 (15 = base sim) | var 10 | j 11-13 | k 14+; slots < BE = main sims
+    // task bits: env 0-5 | b 6-9 (15 = base sim) | var 10 | j 11-13 | k 14+
     static __device__ __forceinline__ Task enc(int el, int k, int j, int var, int b) {
         return (Task)((uint32_t)el | ((uint32_t)b << 6) | ((uint32_t)var << 10) | ((uint32_t)j << 11) |
                       ((uint32_t)k << 14));
     }
 };
 
-template <int N, int KMAX, bool FEAR, bool OBS>
+template <int N, int KMAX, bool FEAR, bool OBS, bool WIDE = false>
 struct alignas(16) V2Shared {
-    using Cfg = V2Cfg<N, KMAX, FEAR>;
+    using Cfg = V2Cfg<N, KMAX, FEAR, WIDE>;
     static constexpr int BE = Cfg::BE, FB = FEAR ? BE : 1, OB = OBS ? BE : 1, NP = N + 1;
     double red[Cfg::THREADS / 64][GW_STATS];
-    typename Cfg::Task tasks[Cfg::MAXT];
+    typename Cfg::Task tasks[Cfg::MAXB];
+    typename Cfg::Task groups[Cfg::MAXG];
     int pos[FB][N];
     int fin[FB][N];
     int apple[FB][KMAX];
@@ -1144,7 +1157,7 @@ struct alignas(16) V2Shared {
     uint16_t pc[2][OB][KMAX][NP];
     float pv[2][OB][KMAX][NP];
     uint32_t eflag[OB];
-    int ntask;
+    int nbase, ngroup;  // base-sim entries after the env sims; counterfactual groups
 };
 
 // setup_step (ma_customenv.py:432-452) + RL override (:239-242) from the LDS tables
@@ -1235,10 +1248,11 @@ __device__ __forceinline__ void lds_fill(uint32_t *dst, const uint32_t *__restri
 // (:456-464) into sh.close and the de-duplicated counterfactual task list appended to sh.tasks.
 // Expects sh.pos / sh.act / sh.mdr of the env filled.
 template <int N, int KMAX, class Sh>
-__device__ __forceinline__ void fear_plan(const Params &p, Sh &sh, int el, const int (&pos)[N], const int (&act)[N]) {
+__device__ __forceinline__ void fear_plan(const Params &p, Sh &sh, int el, const int (&pos)[N], const int (&act)[N],
+                                          int off0) {
     using Cfg = typename Sh::Cfg;
     const int K = p.K;
-    int ntask = 0;
+    int nb = 0, ng = 0;
     uint32_t close[KMAX];
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
@@ -1248,24 +1262,36 @@ __device__ __forceinline__ void fear_plan(const Params &p, Sh &sh, int el, const
         for (int n = 0; n < N; ++n)
             if (n == k || manhattan(p, pos[k], pos[n]) <= 5) close[k] |= 1u << n;
         sh.close[el][k] = (uint8_t)close[k];
-        if (act[k] != (int)sh.mdr[el][k]) ntask += 2 + 16 * (__popc(close[k]) - 1);
+        if (act[k] != (int)sh.mdr[el][k]) {
+            nb += 2;
+            ng += __popc(close[k]) - 1;
+        }
     }
-    if (!ntask) return;
-    int slot = atomicAdd(&sh.ntask, ntask);
+    if (!nb) return;
+    int sb = off0 + atomicAdd(&sh.nbase, nb);
+    int sg = ng ? atomicAdd(&sh.ngroup, ng) : 0;
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
         if (k >= K || act[k] == (int)sh.mdr[el][k]) continue;
-        sh.tasks[slot++] = Cfg::enc(el, k, 0, 0, 15);
-        sh.tasks[slot++] = Cfg::enc(el, k, 0, 1, 15);
+        sh.tasks[sb++] = Cfg::enc(el, k, 0, 0, 15);
+        sh.tasks[sb++] = Cfg::enc(el, k, 0, 1, 15);
 #pragma unroll
-        for (int j = 0; j < N; ++j) {
-            if (j == k || !((close[k] >> j) & 1u)) continue;
-#pragma unroll
-            for (int var = 0; var < 2; ++var)
-                for (int b = 0; b < NA; ++b)
-                    if (b != act[j]) sh.tasks[slot++] = Cfg::enc(el, k, j, var, b);
-        }
+        for (int j = 0; j < N; ++j)
+            if (j != k && ((close[k] >> j) & 1u)) sh.groups[sg++] = Cfg::enc(el, k, j, 0, 0);
     }
+}
+
+// Task ti of phase B: entries [0, nb_end) are stored; past them, group g = (ti - nb_end) / 16
+// expands to var = bit 3 and the 8 alternatives b != act[j] of agent j.
+template <class Sh>
+__device__ __forceinline__ uint32_t fear_task_at(const Sh &sh, int ti, int nb_end) {
+    if (ti < nb_end) return sh.tasks[ti];
+    const int g = (ti - nb_end) >> 4, s = (ti - nb_end) & 15;
+    const uint32_t tk = sh.groups[g];
+    const int el = tk & 63, j = (tk >> 11) & 7;
+    const int bi = s & 7;
+    const int b = bi + (bi >= (int)sh.act[el][j]);
+    return tk | ((uint32_t)b << 6) | ((uint32_t)(s >> 3) << 10);
 }
 
 // FeAR phase B, one counterfactual world update (task bits: see V2Cfg::enc): the joint action
@@ -1377,7 +1403,7 @@ __global__ void __launch_bounds__(128) step_v2(Params p) {
     if (p.lds_cdf)
         lds_fill<T>(reinterpret_cast<uint32_t *>(dyn), reinterpret_cast<const uint32_t *>(p.tb.cdf), 2 * p.n_cdf, tid);
     if (FEAR) lds_fill<T>(reinterpret_cast<uint32_t *>(resp_s), reinterpret_cast<const uint32_t *>(p.tb.resp), 200, tid);
-    if (tid == 0) sh.ntask = BE;
+    if (tid == 0) sh.nbase = sh.ngroup = 0;
     __syncthreads();
     const CtabOk okv{ctab};
 
@@ -1396,14 +1422,14 @@ __global__ void __launch_bounds__(128) step_v2(Params p) {
 #pragma unroll
             for (int k = 0; k < KMAX; ++k) sh.apple[tid][k] = (k < K && ((es.flags >> k) & 1u)) ? p.apples[k] : -1;
             sh.tasks[tid] = Cfg::enc(tid, 0, 0, 0, 0);
-            fear_plan<N, KMAX>(p, sh, tid, es.pos, act);
+            fear_plan<N, KMAX>(p, sh, tid, es.pos, act, BE);
         }
         __syncthreads();
         // ---- B ----
-        const int ntask = sh.ntask;
+        const int nb_end = BE + sh.nbase, ntask = nb_end + 16 * sh.ngroup;
         for (int ti = tid; ti < ntask; ti += T) {
             if (ti < BE && ti >= nenv) continue;
-            const uint32_t tk = sh.tasks[ti];
+            const uint32_t tk = fear_task_at(sh, ti, nb_end);
             const int el = tk & 63, b = (tk >> 6) & 15, var = (tk >> 10) & 1, j = (tk >> 11) & 7, k = (int)(tk >> 14);
             int pos[N], joint[N], fin[N];
 #pragma unroll
@@ -1556,10 +1582,10 @@ __global__ void __launch_bounds__(128) step_v2(Params p) {
 // cells, joint action, env rewards, done) and score / fear_score; same phases A/B/C as step_v2
 // without the env's own update.  Dynamic LDS: [cell table][Resp 100 f64] (no CDFs).
 // ---------------------------------------------------------------------------------------
-template <int N, int KMAX>
+template <int N, int KMAX, bool WIDE>
 __global__ void __launch_bounds__(128) fear_v2(Params p) {
-    using Cfg = V2Cfg<N, KMAX, true>;
-    using Sh = V2Shared<N, KMAX, true, false>;
+    using Cfg = V2Cfg<N, KMAX, true, WIDE>;
+    using Sh = V2Shared<N, KMAX, true, false, WIDE>;
     constexpr int BE = Cfg::BE, T = Cfg::THREADS;
     __shared__ Sh sh;
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
@@ -1582,7 +1608,7 @@ __global__ void __launch_bounds__(128) fear_v2(Params p) {
     }
     lds_fill<T>(ctab, p.tb.celltab, p.HW, tid);
     lds_fill<T>(reinterpret_cast<uint32_t *>(resp_s), reinterpret_cast<const uint32_t *>(p.tb.resp), 200, tid);
-    if (tid == 0) sh.ntask = 0;
+    if (tid == 0) sh.nbase = sh.ngroup = 0;
     __syncthreads();
     const CtabOk okv{ctab};
     // ---- A ----
@@ -1595,12 +1621,12 @@ __global__ void __launch_bounds__(128) fear_v2(Params p) {
             sh.act[tid][n] = (int8_t)act[n];
             sh.mdr[tid][n] = (int8_t)mdr[n];
         }
-        fear_plan<N, KMAX>(p, sh, tid, pos, act);
+        fear_plan<N, KMAX>(p, sh, tid, pos, act, 0);
     }
     __syncthreads();
     // ---- B ----
-    const int ntask = sh.ntask;
-    for (int ti = tid; ti < ntask; ti += T) fear_task<N, KMAX>(p, sh, sh.tasks[ti], okv);
+    const int nb_end = sh.nbase, ntask = nb_end + 16 * sh.ngroup;
+    for (int ti = tid; ti < ntask; ti += T) fear_task<N, KMAX>(p, sh, fear_task_at(sh, ti, nb_end), okv);
     __syncthreads();
     // ---- C ----
     Contrib ct;
@@ -1676,6 +1702,7 @@ struct Env {
     uint32_t *roadbits = nullptr;
     int defer_order = 3;            // GW_DEFER (A/B): 0 fear then obs on one stream, 1 fear on aux first,
                                     // 2 obs first then fear on aux, 3 (default) as 1, aux stream high priority
+    bool fear_wide = false;         // GW_FEAR_BE=wide: fear_v2 with 2x envs per block (A/B)
     int chunks = 1;                 // GW_CHUNKS: step/obs pipeline depth (split path; 1 = off, measured best)
     hipStream_t aux = nullptr;      // second stream of the pipeline (created on first use)
     std::vector<hipEvent_t> sync_ev;  // fork/chunk/join events (timing disabled)
@@ -1814,9 +1841,9 @@ int64_t defer_step_rows(const Env *env) {
     return (env->E + be - 1) / be;
 }
 
-template <int N, int KMAX>
+template <int N, int KMAX, bool WIDE>
 hipError_t launch_fear_k(const Env *env, const gw::Params &p0, hipStream_t s) {
-    constexpr int BE = gw::V2Cfg<N, KMAX, true>::BE;
+    constexpr int BE = gw::V2Cfg<N, KMAX, true, WIDE>::BE;
     gw::Params p = p0;
     p.lds_cdf = 0;  // dynamic LDS [cell table][Resp]
     p.ctab_off = 0;
@@ -1826,13 +1853,21 @@ hipError_t launch_fear_k(const Env *env, const gw::Params &p0, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((n + BE - 1) / BE);
     const size_t dyn = (size_t)p.resp_off + 100 * sizeof(double);
-    hipLaunchKernelGGL((gw::fear_v2<N, KMAX>), dim3(grid), dim3(gw::V2Cfg<N, KMAX, true>::THREADS), dyn, s, p);
+    hipLaunchKernelGGL((gw::fear_v2<N, KMAX, WIDE>), dim3(grid), dim3(gw::V2Cfg<N, KMAX, true, WIDE>::THREADS), dyn, s, p);
     return hipGetLastError();
 }
 
 template <int N>
 hipError_t launch_fear(const Env *env, const gw::Params &p, hipStream_t s) {
-    return env->K <= 2 ? launch_fear_k<N, 2>(env, p, s) : launch_fear_k<N, N>(env, p, s);
+    if (env->fear_wide)
+        return env->K <= 2 ? launch_fear_k<N, 2, true>(env, p, s) : launch_fear_k<N, N, true>(env, p, s);
+    return env->K <= 2 ? launch_fear_k<N, 2, false>(env, p, s) : launch_fear_k<N, N, false>(env, p, s);
+}
+
+template <int N>
+int fear_be(const Env *env) {
+    if (env->fear_wide) return env->K <= 2 ? gw::V2Cfg<N, 2, true, true>::BE : gw::V2Cfg<N, N, true, true>::BE;
+    return env->K <= 2 ? gw::V2Cfg<N, 2, true>::BE : gw::V2Cfg<N, N, true>::BE;
 }
 
 hipError_t dispatch_fear(const Env *env, const gw::Params &p, hipStream_t s) {
@@ -1937,7 +1972,7 @@ template <int N>
 int64_t stats_rows_n(const Env *env) {
     int be;
     if (env->mode == 3 && env->fear) {
-        const int bf = env->K <= 2 ? gw::V2Cfg<N, 2, true>::BE : gw::V2Cfg<N, N, true>::BE;
+        const int bf = fear_be<N>(env);
         return defer_step_rows<N>(env) + (env->E + bf - 1) / bf;
     }
     if (env->mode >= 1) {
@@ -2037,6 +2072,8 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
         if (kv && std::strcmp(kv, "defer") == 0) env->mode = 3;
         const char *dv = std::getenv("GW_DEFER");
         if (dv) env->defer_order = std::max(0, std::min(3, std::atoi(dv)));
+        const char *fb = std::getenv("GW_FEAR_BE");
+        if (fb && std::strcmp(fb, "wide") == 0) env->fear_wide = true;
         const char *be = std::getenv("GW_OBS_BE");
         if (be) env->obs_be = std::max(1, std::min(gw::OBS_BE, std::atoi(be)));
         const char *nt = std::getenv("GW_OBS_NT");

@@ -122,6 +122,7 @@ KERNEL_PATHS = {
     "fused": {"GW_KERNEL": "fused"},                          # obs stores inside step_v2
     "defer": {"GW_KERNEL": "defer"},                          # default: fear_v2 on a 2nd stream || obs_kernel
     "defer_serial": {"GW_KERNEL": "defer", "GW_DEFER": "0"},  # step_v2 <DEFER>, fear_v2, obs_kernel, one stream
+    "defer_wide": {"GW_KERNEL": "defer", "GW_FEAR_BE": "wide"},  # fear_v2 with 2x envs per block
     "v1": {"GW_KERNEL": "v1"},                                # the first kernels
 }
 
