@@ -43,6 +43,10 @@ CONFIGS = {
                 workload="8-agent 64x64 grid, 65536 envs, FeAR on"),
     "c1": dict(scenario="level3", envs=1, fear=False, fear_weight=-2.0,
                workload="BASELINE config 1: Level 3 (10x16), 1 env, random policy"),
+    "c5": dict(scenario="grid32", envs=65536, fear=True, fear_weight=-5.0, rollout=True,
+               workload="BASELINE config 5 per GPU: 32x32, N=4, K=2, 65536 envs/GPU, FeAR on, full rollout "
+                        "(stacked MLP actors + GumbelSoftmax + mask + argmax, env step, zero-copy replay ring of "
+                        "MEMORY_SIZE 200000, per-step RCCL reduction of the episode statistics)"),
 }
 
 
@@ -98,6 +102,8 @@ def main():
     ap.add_argument("--envs", type=int, default=0, help="override envs per GPU")
     ap.add_argument("--fear", type=int, default=-1, help="override FeAR on (1) / off (0)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--updates-per-step", type=int, default=0,
+                    help="c5 only: MADDPG updates (batch 128, one HIP-graph replay each) per env step")
     ap.add_argument("--profile-every", type=int, default=8,
                     help="bracket every n-th timed step's kernels with HIP events (0 = none); the "
                          "events themselves cost ~2-3 us per kernel boundary, so not every step")
@@ -138,7 +144,24 @@ def main():
             dist.all_reduce(r.stats, op=dist.ReduceOp.SUM)
         return r
 
-    env.reset()
+    if cfg.get("rollout"):  # c5: actor -> env -> replay (+ optional MADDPG updates) per step
+        from marlnav.maddpg import MADDPG
+        from marlnav.rollout import Rollout
+        learner = MADDPG(K, env.H, env.W, device=env.device, seed=rank, capturable=True)
+        ro = Rollout(env, learner.actors, replay_slots=-(-200_000 // E) + 1, training=True, seed=rank)
+        ro.reset()
+
+        def one_step(i):  # noqa: F811
+            r = ro.step()  # the StatsReducer inside does the per-step all-reduce across ranks
+            if args.updates_per_step and ro.replay.t >= 2:
+                if learner._graph is None:
+                    learner.capture(ro.replay)
+                for _ in range(args.updates_per_step):
+                    learner.replay_learn()
+            return r
+
+    if not cfg.get("rollout"):
+        env.reset()
     for i in range(args.warmup):
         one_step(i)
     if world > 1:

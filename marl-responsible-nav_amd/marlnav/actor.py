@@ -26,52 +26,82 @@ import torch.nn.functional as F
 N_ACTIONS = 9
 
 
-def _init_linear(K, fan_in, fan_out, device, dtype, gen=None):
+def _init_linear(K, fan_in, fan_out, gen=None):
     bound = 1.0 / math.sqrt(fan_in)  # nn.Linear's default (kaiming_uniform a=sqrt(5)) bound
     w = (torch.rand((K, fan_in, fan_out), generator=gen, device="cpu") * 2 - 1) * bound
     b = (torch.rand((K, 1, fan_out), generator=gen, device="cpu") * 2 - 1) * bound
-    return nn.Parameter(w.to(device=device, dtype=dtype)), nn.Parameter(b.to(device=device, dtype=dtype))
+    return w, b
 
 
 class StackedMLPActors(nn.Module):
-    """K independent MLP actors evaluated together: x [K, E, D] -> logits [K, E, 9]."""
+    """K independent MLPs evaluated together: x [K, E, D] -> [K, E, out] (out = 9 logits for an
+    actor, 1 for a critic).
+
+    All parameters live in ONE flat tensor (``flat``); ``weights[i]`` [K, in, out], ``biases[i]``
+    [K, 1, out], ``ln_w[i]`` / ``ln_b[i]`` [K, 1, h] are views into it.  A fused Adam step and the
+    soft target update are then one kernel each per network instead of one per tensor, which is
+    what bounds a batch-128 MADDPG update (launch latency, not FLOPs)."""
 
     def __init__(self, K: int, in_dim: int, hidden=(128, 128), n_actions: int = N_ACTIONS, layer_norm: bool = True,
                  device=None, dtype=torch.float32, seed: int = 0):
         super().__init__()
         gen = torch.Generator().manual_seed(seed)
         dims = [in_dim, *hidden, n_actions]
-        self.weights = nn.ParameterList()
-        self.biases = nn.ParameterList()
+        parts, self._shapes = [], []
         for a, b in zip(dims[:-1], dims[1:]):
-            w, bb = _init_linear(K, a, b, device, dtype, gen)
-            self.weights.append(w)
-            self.biases.append(bb)
+            w, bb = _init_linear(K, a, b, gen)
+            parts += [w, bb]
+            self._shapes += [("w", w.shape), ("b", bb.shape)]
+        for h in hidden:
+            parts += [torch.ones((K, 1, h)), torch.zeros((K, 1, h))]
+            self._shapes += [("lw", (K, 1, h)), ("lb", (K, 1, h))]
+        self.flat = nn.Parameter(torch.cat([t.reshape(-1) for t in parts]).to(device=device, dtype=dtype))
         self.layer_norm = layer_norm
-        self.ln_w = nn.ParameterList([nn.Parameter(torch.ones((K, 1, h), device=device, dtype=dtype)) for h in hidden])
-        self.ln_b = nn.ParameterList([nn.Parameter(torch.zeros((K, 1, h), device=device, dtype=dtype)) for h in hidden])
-        self.K, self.in_dim = K, in_dim
+        self.K, self.in_dim, self.n_layers = K, in_dim, len(dims) - 1
+
+    def _views(self):
+        out, off = {"w": [], "b": [], "lw": [], "lb": []}, 0
+        for kind, shape in self._shapes:
+            n = math.prod(shape)
+            out[kind].append(self.flat[off:off + n].view(shape))
+            off += n
+        return out
+
+    @property
+    def weights(self):
+        return self._views()["w"]
+
+    @property
+    def biases(self):
+        return self._views()["b"]
+
+    @property
+    def ln_w(self):
+        return self._views()["lw"]
+
+    @property
+    def ln_b(self):
+        return self._views()["lb"]
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        n = len(self.weights)
+        v = self._views()
+        n = self.n_layers
         for i in range(n):
-            x = torch.baddbmm(self.biases[i], x, self.weights[i])
+            x = torch.baddbmm(v["b"][i], x, v["w"][i])
             if i < n - 1:
-                if self.layer_norm:
-                    mu = x.mean(-1, keepdim=True)
-                    var = x.var(-1, unbiased=False, keepdim=True)
-                    x = (x - mu) * torch.rsqrt(var + 1e-5) * self.ln_w[i] + self.ln_b[i]
+                if self.layer_norm:  # nn.LayerNorm(h), eps 1e-5, per-agent affine
+                    x = torch.addcmul(v["lb"][i], F.layer_norm(x, (x.shape[-1],)), v["lw"][i])
                 x = F.relu(x)
         return x
 
     def load_agent(self, k: int, state: dict):
         """Per-agent weights in the checkpoint's naming (feature_net.linear_layer_i.weight [out, in], ...)."""
-        names = [f"linear_layer_{i}" for i in range(len(self.weights) - 1)] + ["linear_layer_output"]
+        names = [f"linear_layer_{i}" for i in range(self.n_layers - 1)] + ["linear_layer_output"]
         with torch.no_grad():
             for i, nm in enumerate(names):
                 self.weights[i][k].copy_(torch.as_tensor(state[f"{nm}.weight"]).t())
                 self.biases[i][k, 0].copy_(torch.as_tensor(state[f"{nm}.bias"]))
-            for i in range(len(self.ln_w)):
+            for i in range(self.n_layers - 1):
                 if f"layer_norm_{i}.weight" in state:
                     self.ln_w[i][k, 0].copy_(torch.as_tensor(state[f"layer_norm_{i}.weight"]))
                     self.ln_b[i][k, 0].copy_(torch.as_tensor(state[f"layer_norm_{i}.bias"]))

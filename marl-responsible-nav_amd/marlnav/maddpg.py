@@ -1,0 +1,177 @@
+"""MADDPG learner on the GPU: agilerl 1.0.15 ``MADDPG.learn`` restated for K stacked agents, with the
+whole update (replay sampling, target actions, critic and actor steps, soft target update)
+capturable as one HIP graph.
+
+Reference call sites: ``maddpg/agent.py:41-65`` (construction from ``configs/custom_fear_5.yaml``:
+LR_ACTOR = LR_CRITIC = 1e-3, GAMMA = 0.98, TAU = 0.01, BATCH_SIZE = 128, LEARN_STEP = 10,
+MEMORY_SIZE = 200000), ``:199-224`` (sample + learn schedule) and ``:190-197`` (what is stored:
+state, the GumbelSoftmax action probabilities, shaped reward, next_state, termination).
+
+agilerl is not installed, so its published algorithm is restated here ("parity
+unpinned" for its stochastic parts; tests/test_maddpg.py checks this batched form against a
+plain per-agent PyTorch fp32 restatement of the same update, agent by agent):
+
+  x  = [s_1 .. s_K, a_1 .. a_K]                      (flattened obs, action probabilities)
+  a'_k = GumbelSoftmax(actor_target_k(s'_k))         (detached)
+  y_k  = r_k + (1 - d_k) * gamma * critic_target_k([s'_1 .. s'_K, a'_1 .. a'_K])
+  critic_k  <- Adam step on  MSE(critic_k(x), y_k)
+  actor_k   <- Adam step on  -mean(critic_k(x with a_k := GumbelSoftmax(actor_k(s_k))))
+               (after the critic step; the other agents keep their replayed actions)
+  targets   <- tau * online + (1 - tau) * target      (after all agents)
+
+The K agents' parameters are disjoint and every agent's losses only read replayed data and
+detached target actions, so running the K updates together (stacked [K, ...] weights, one
+batched GEMM chain, the K losses summed before one backward, one Adam over the stacked
+tensors) is the same arithmetic as agilerl's per-agent loop.  Critic: the MLP of the shipped
+checkpoints' critic layout (input K*H*W + K*9 -> 128 -> 128 -> 1, LayerNorm, ReLU).
+"""
+from __future__ import annotations
+
+import copy
+
+import torch
+import torch.nn.functional as F
+
+from .actor import N_ACTIONS, MultiAgentActors, StackedMLPActors
+
+
+def gumbel_softmax(logits: torch.Tensor, u: torch.Tensor | None = None, tau: float = 1.0, eps: float = 1e-20,
+                   generator: torch.Generator | None = None) -> torch.Tensor:
+    """agilerl's GumbelSoftmax output activation: softmax((logits - log(-log(u + eps) + eps)) / tau)."""
+    if u is None:
+        u = torch.rand(logits.shape, device=logits.device, dtype=logits.dtype, generator=generator)
+    return F.softmax((logits - torch.log(-torch.log(u + eps) + eps)) / tau, dim=-1)
+
+
+class MADDPG:
+    """K MADDPG agents with stacked networks.  ``actors`` is a MultiAgentActors (mlp or cnn)."""
+
+    def __init__(self, K: int, H: int, W: int, arch: str = "mlp", hidden=(128, 128), lr_actor: float = 1e-3,
+                 lr_critic: float = 1e-3, gamma: float = 0.98, tau: float = 0.01, batch_size: int = 128,
+                 learn_step: int = 10, device=None, seed: int = 0, capturable: bool = False):
+        self.K, self.H, self.W, self.arch = K, H, W, arch
+        self.gamma, self.tau, self.batch_size, self.learn_step = gamma, tau, batch_size, learn_step
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        self.actors = MultiAgentActors(K, H, W, arch, hidden, device=self.device, seed=seed)
+        self.critics = StackedMLPActors(K, K * H * W + K * N_ACTIONS, hidden, n_actions=1, device=self.device,
+                                        seed=seed + 1)
+        self.actor_targets = copy.deepcopy(self.actors)
+        self.critic_targets = copy.deepcopy(self.critics)
+        for m in (self.actor_targets, self.critic_targets):
+            m.requires_grad_(False)
+        opt = dict(capturable=True) if capturable else {}
+        if self.device.type == "cuda":
+            opt["fused"] = True  # one Adam kernel per parameter tensor (one flat tensor per MLP net)
+        self.opt_actor = torch.optim.Adam(self.actors.parameters(), lr=lr_actor, **opt)
+        self.opt_critic = torch.optim.Adam(self.critics.parameters(), lr=lr_critic, **opt)
+        self._graph = None
+
+    # ---------------------------------------------------------------------------------------
+    def _critic_in(self, states: torch.Tensor, actions: torch.Tensor) -> torch.Tensor:
+        """[K, B, H, W] obs + [K, B, 9] actions -> [B, K*H*W + K*9] (agent-major, as agilerl's
+        torch.cat(list(states.values()) + actions, 1))."""
+        K, B = states.shape[0], states.shape[1]
+        s = states.reshape(K, B, -1).permute(1, 0, 2).reshape(B, -1)
+        a = actions.permute(1, 0, 2).reshape(B, -1)
+        return torch.cat([s, a], 1)
+
+    def learn(self, states, actions, rewards, next_states, dones, u_next=None, u_cur=None):
+        """One MADDPG update from a sampled batch.  states/next_states [K, B, H, W] f32, actions
+        [K, B, 9] (stored GumbelSoftmax probabilities), rewards [B, K], dones [B, K] (termination).
+        u_next / u_cur: optional uniforms [K, B, 9] for the two Gumbel samples (tests).
+        Returns (actor_loss [K], critic_loss [K]) device tensors (no host sync)."""
+        K, B = states.shape[0], states.shape[1]
+        D = K * self.H * self.W
+        r = rewards.to(torch.float32).t().unsqueeze(-1)          # [K, B, 1]
+        d = dones.to(torch.float32).t().unsqueeze(-1)
+        with torch.no_grad():
+            a_next = gumbel_softmax(self.actor_targets(next_states), u_next)          # [K, B, 9]
+            x_next = self._critic_in(next_states, a_next)
+            q_next = self.critic_targets(x_next.unsqueeze(0).expand(K, -1, -1))     # [K, B, 1]
+            y = r + (1.0 - d) * self.gamma * q_next
+        x = self._critic_in(states, actions)
+        q = self.critics(x.unsqueeze(0).expand(K, -1, -1))
+        critic_loss = ((q - y) ** 2).mean(dim=(1, 2))                                # MSELoss per agent
+        self.opt_critic.zero_grad(set_to_none=False)
+        critic_loss.sum().backward()
+        self.opt_critic.step()
+
+        probs = gumbel_softmax(self.actors(states), u_cur)                             # [K, B, 9]
+        xs = x.detach().unsqueeze(0).repeat(K, 1, 1)                                   # [K, B, D + K*9]
+        eye = torch.eye(K, device=x.device, dtype=x.dtype)                             # agent k's slot
+        a_rep = actions.permute(1, 0, 2).unsqueeze(0).expand(K, -1, -1, -1)           # [K, B, K, 9]
+        a_mix = a_rep * (1 - eye)[:, None, :, None] + probs.unsqueeze(2) * eye[:, None, :, None]
+        xs = torch.cat([xs[..., :D], a_mix.reshape(K, B, -1)], -1)
+        actor_loss = -self.critics(xs).mean(dim=(1, 2))
+        self.opt_actor.zero_grad(set_to_none=False)
+        actor_loss.sum().backward()
+        self.opt_actor.step()
+        self.soft_update()
+        return actor_loss.detach(), critic_loss.detach()
+
+    @torch.no_grad()
+    def soft_update(self):
+        """agilerl soft_update: target <- tau * online + (1 - tau) * target (two foreach kernels)."""
+        src = list(self.actors.parameters()) + list(self.critics.parameters())
+        dst = list(self.actor_targets.parameters()) + list(self.critic_targets.parameters())
+        torch._foreach_mul_(dst, 1.0 - self.tau)
+        torch._foreach_add_(dst, src, alpha=self.tau)
+
+    # ---------------------------------------------------------------------------------------
+    def learn_from(self, replay, generator: torch.Generator | None = None):
+        """Sample ``batch_size`` transitions from a ReplayRing and learn (eager)."""
+        return self.learn(*replay.sample(self.batch_size, generator=generator))
+
+    def capture(self, replay, warmup: int = 3):
+        """Capture sample + learn into one HIP graph (requires capturable=True and a CUDA device).
+        Later ``replay_learn()`` replays it: one launch instead of ~150 kernel launches."""
+        if self.device.type != "cuda":
+            raise RuntimeError("graph capture needs the GPU")
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):  # allocator + optimizer state warm-up outside the graph
+                self.learn_from(replay)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._graph_out = self.learn_from(replay)
+        self._graph = g
+        return g
+
+    def replay_learn(self):
+        self._graph.replay()
+        return self._graph_out
+
+    # ---------------------------------------------------------------------------------------
+    def state_dict(self) -> dict:
+        """Flat tensor dict in the checkpoint naming (per agent), for safetensors."""
+        out = {}
+        for name, m in (("actor", self.actors), ("actor_target", self.actor_targets), ("critic", self.critics),
+                        ("critic_target", self.critic_targets)):
+            for k, v in m.state_dict().items():
+                out[f"{name}.{k}"] = v.detach().contiguous()
+        return out
+
+    def load_state_dict(self, sd: dict):
+        for name, m in (("actor", self.actors), ("actor_target", self.actor_targets), ("critic", self.critics),
+                        ("critic_target", self.critic_targets)):
+            sub = {k[len(name) + 1:]: v for k, v in sd.items() if k.startswith(name + ".")}
+            m.load_state_dict(sub)
+
+    def save(self, path: str):
+        from safetensors.torch import save_file
+        save_file({k: v.cpu() for k, v in self.state_dict().items()}, path)
+
+    def load(self, path: str):
+        from safetensors.torch import load_file
+        self.load_state_dict({k: v.to(self.device) for k, v in load_file(path).items()})
+
+
+def learns_per_step(num_envs: int, learn_step: int, idx_step: int) -> int:
+    """agilerl/MADDPGAgent.train learn schedule (maddpg/agent.py:199-224): with learn_step >
+    num_envs, one learn every learn_step // num_envs env steps; otherwise num_envs // learn_step
+    learns per env step."""
+    if learn_step > num_envs:
+        return 1 if idx_step % (learn_step // num_envs) == 0 else 0
+    return num_envs // learn_step

@@ -37,27 +37,31 @@ class ReplayRing:
         self.term = torch.zeros((self.S, E, K), dtype=torch.uint8, device=dev)
         self.done = torch.zeros((self.S, E), dtype=torch.uint8, device=dev)
         self.t = 0          # transitions stored = steps taken
+        self.t_dev = torch.zeros((), dtype=torch.int64, device=dev)  # same, on device (graph-safe sampling)
         self.E, self.K = E, K
 
     def __len__(self):
         return min(self.t, self.S - 1) * self.E
 
     @torch.no_grad()
-    def sample(self, batch: int, generator: torch.Generator | None = None):
-        """Uniform transitions -> (state [K,B,H,W], probs [K,B,9], reward [B,K], next_state, term [B,K])."""
-        n_steps = min(self.t, self.S - 1)
-        if n_steps <= 0:
+    def sample(self, batch: int, generator: torch.Generator | None = None, return_idx: bool = False):
+        """Uniform transitions -> (state [K,B,H,W], probs [K,B,9], reward [B,K], next_state, term [B,K]).
+        Every index is computed on the device from ``t_dev``, so a captured graph stays valid as
+        the ring fills (MultiAgentReplayBuffer.sample, uniform without priorities)."""
+        if self.t <= 0:
             raise RuntimeError("empty replay ring")
         dev = self.obs.device
-        step = torch.randint(0, n_steps, (batch,), device=dev, generator=generator)
+        n = torch.clamp(self.t_dev, min=1, max=self.S - 1)
+        step = torch.minimum((torch.rand((batch,), device=dev, generator=generator) * n).long(), n - 1)
         env = torch.randint(0, self.E, (batch,), device=dev, generator=generator)
-        tr = (self.t - 1 - step) % self.S          # transition slot (its state is obs[tr])
+        tr = (self.t_dev - 1 - step) % self.S      # transition slot (its state is obs[tr])
         nx = (tr + 1) % self.S
         state = self.obs[tr, :, env].permute(1, 0, 2, 3)
         done = self.done[tr, env].bool()
         next_state = torch.where(done[None, :, None, None], self.final_obs[tr, :, env].permute(1, 0, 2, 3),
                                  self.obs[nx, :, env].permute(1, 0, 2, 3))
-        return state, self.probs[tr, :, env].permute(1, 0, 2), self.reward[tr, env], next_state, self.term[tr, env]
+        out = (state, self.probs[tr, :, env].permute(1, 0, 2), self.reward[tr, env], next_state, self.term[tr, env])
+        return out + ((tr, env),) if return_idx else out
 
 
 class Rollout:
@@ -76,6 +80,8 @@ class Rollout:
         if self.replay is not None:
             obs, mask = self.env.reset()
             self.replay.obs[0].copy_(obs)
+            self.replay.t = 0
+            self.replay.t_dev.zero_()
         else:
             self.env.reset()
         self.t = 0
@@ -103,6 +109,7 @@ class Rollout:
             rp.term[cur].copy_(r.term)
             rp.done[cur].copy_(r.done)
             rp.t = self.t + 1
+            rp.t_dev.add_(1)
         else:
             r = env.step(actions)
         self.t += 1

@@ -103,3 +103,89 @@ def test_cnn_actor_runs():
     x = torch.zeros((2, 16, 64, 64), device="cuda")
     a, p = actors.act(x, None, training=False)
     assert a.shape == (16, 2) and p.shape == (2, 16, 9)
+
+
+def test_graph_learn_equals_eager_learn():
+    """The HIP-graph replay of one MADDPG update == the eager update on the same batch and noise."""
+    from marlnav.maddpg import MADDPG
+    K, H, W, B = 2, 32, 32, 128
+    g = torch.Generator(device="cuda").manual_seed(0)
+    batch = (torch.randint(-1, 6, (K, B, H, W), device="cuda", generator=g).float(),
+             torch.softmax(torch.randn((K, B, 9), device="cuda", generator=g), -1),
+             torch.randn((B, K), device="cuda", generator=g, dtype=torch.float64),
+             torch.randint(-1, 6, (K, B, H, W), device="cuda", generator=g).float(),
+             (torch.rand((B, K), device="cuda", generator=g) < 0.1).to(torch.uint8),
+             torch.rand((K, B, 9), device="cuda", generator=g), torch.rand((K, B, 9), device="cuda", generator=g))
+    a = MADDPG(K, H, W, device="cuda", seed=1, capturable=True)
+    b = MADDPG(K, H, W, device="cuda", seed=1, capturable=True)
+    for _ in range(2):  # warm-up updates on both (optimizer state exists before capture)
+        a.learn(*batch)
+        b.learn(*batch)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s), torch.cuda.graph(graph):
+        out = a.learn(*batch)
+    torch.cuda.current_stream().wait_stream(s)
+    for _ in range(3):
+        graph.replay()
+        want = b.learn(*batch)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out[0], want[0], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(out[1], want[1], rtol=1e-5, atol=1e-6)
+    for x, y in zip(a.state_dict().values(), b.state_dict().values()):
+        torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6)
+
+
+def test_trainer_with_graph_learns_and_samples_the_live_window():
+    from marlnav.maddpg import MADDPG
+    from marlnav.train import MADDPGTrainer
+    sc = S.builtin("grid32")
+    env = VecGridEnv(sc, num_envs=512, fear=True, fear_weight=-5.0, stats=True, final_obs=True)
+    m = MADDPG(sc.K, sc.H, sc.W, device=env.device, seed=2, capturable=True)
+    w0 = m.actors.net.weights[0].detach().clone()
+    tr = MADDPGTrainer(env, m, memory_size=4096, updates_per_step=2, graph=True, seed=3)
+    tr.reset()
+    s = tr.train(24)
+    torch.cuda.synchronize()
+    assert s["updates"] > 0 and s["env_steps"] == 24 * 512
+    a_loss, c_loss = tr.losses[-1]
+    assert torch.isfinite(a_loss).all() and torch.isfinite(c_loss).all()
+    assert not torch.equal(w0, m.actors.net.weights[0])
+    # sampling indices are computed on device from t_dev: always inside the filled window
+    rp = tr.rollout.replay
+    *_, (slot, envi) = rp.sample(4096, return_idx=True)
+    n = min(rp.t, rp.S - 1)
+    age = (rp.t - 1 - slot.cpu().numpy()) % rp.S
+    assert age.max() < n and envi.max().item() < env.E
+    env.close()
+
+
+def test_evaluate_matches_oracle():
+    """customeval totals (crashes, apples, steps, FeAR) over 64 episodes == the C oracle fed the
+    same actions with the same early-stop rule."""
+    from marlnav.evaluate import evaluate
+    sc = S.builtin("level3")
+    E, T = 64, 150
+    actors = MultiAgentActors(sc.K, sc.H, sc.W, "mlp", device="cuda", seed=5)
+    r = evaluate(actors, sc, episodes=E, max_steps=T, fear=True, seed=11, record_actions=True)
+    acts = r["actions"].cpu().numpy()
+    orc = O.OracleEnvs(sc, E, fear=True, fear_weight=-5.0, max_steps=T, seed=11, reset=False)
+    obs_o = np.zeros((sc.K, E, sc.HW), np.float32)
+    orc.reset_all(obs=obs_o)
+    outs = (O.StepOut * E)()
+    active = np.ones(E, bool)
+    crashes = apples = steps = 0
+    fear = 0.0
+    for t in range(acts.shape[0]):
+        orc.vec_step(acts[t], obs=obs_o, outs=outs, nthreads=8, auto_reset=False)
+        for e in range(E):
+            if active[e]:
+                crashes += outs[e].crashes
+                apples += outs[e].apples_caught
+                steps += 1
+                fear += sum(outs[e].fear[k] for k in range(sc.K))
+        active &= ~np.array([bool(outs[e].done) for e in range(E)])
+    assert (r["crashes"], r["apples_caught"], r["steps"]) == (crashes, apples, steps)
+    assert abs(r["fear"] - fear) < 1e-9
+    assert not active.any() or acts.shape[0] == T

@@ -1,0 +1,143 @@
+"""The stacked GPU-shaped MADDPG update (marlnav/maddpg.py) == a plain per-agent PyTorch fp32
+restatement of agilerl 1.0.15's MADDPG.learn loop (maddpg/agent.py:199-224 call site), agent by
+agent: separate nn.Sequential actors/critics, separate Adam optimisers, critic step then actor
+step per agent, soft target update at the end.  Runs on the CPU (the learner is plain PyTorch;
+the GPU graph-capture path is in tests/test_gpu_rollout.py)."""
+import copy
+
+import pytest
+import torch
+import torch.nn as nn
+
+from marlnav.maddpg import MADDPG, gumbel_softmax, learns_per_step
+
+
+def _seq(stacked, k, n_layers=3):
+    """nn.Sequential copy of agent k of a StackedMLPActors."""
+    dims = [stacked.weights[i].shape[1] for i in range(n_layers)] + [stacked.weights[-1].shape[2]]
+    mods = []
+    for i in range(n_layers):
+        lin = nn.Linear(dims[i], dims[i + 1])
+        with torch.no_grad():
+            lin.weight.copy_(stacked.weights[i][k].t())
+            lin.bias.copy_(stacked.biases[i][k, 0])
+        mods.append(lin)
+        if i < n_layers - 1:
+            ln = nn.LayerNorm(dims[i + 1])
+            with torch.no_grad():
+                ln.weight.copy_(stacked.ln_w[i][k, 0])
+                ln.bias.copy_(stacked.ln_b[i][k, 0])
+            mods += [ln, nn.ReLU()]
+    return nn.Sequential(*mods)
+
+
+class PerAgentReference:
+    """agilerl-style MADDPG with one module and one Adam per agent and network."""
+
+    def __init__(self, m: MADDPG, lr_a, lr_c):
+        K = m.K
+        self.K, self.gamma, self.tau = K, m.gamma, m.tau
+        self.actors = [_seq(m.actors.net, k) for k in range(K)]
+        self.actor_t = [_seq(m.actor_targets.net, k) for k in range(K)]
+        self.critics = [_seq(m.critics, k) for k in range(K)]
+        self.critic_t = [_seq(m.critic_targets, k) for k in range(K)]
+        self.opt_a = [torch.optim.Adam(a.parameters(), lr=lr_a) for a in self.actors]
+        self.opt_c = [torch.optim.Adam(c.parameters(), lr=lr_c) for c in self.critics]
+
+    def learn(self, states, actions, rewards, next_states, dones, u_next, u_cur):
+        K, B = states.shape[0], states.shape[1]
+        s = [states[k].reshape(B, -1) for k in range(K)]
+        ns = [next_states[k].reshape(B, -1) for k in range(K)]
+        acts = [actions[k] for k in range(K)]
+        with torch.no_grad():
+            next_acts = [gumbel_softmax(self.actor_t[k](ns[k]), u_next[k]) for k in range(K)]
+        x = torch.cat(s + acts, 1)
+        x_next = torch.cat(ns + next_acts, 1)
+        losses = []
+        for k in range(K):
+            q = self.critics[k](x)
+            with torch.no_grad():
+                q_next = self.critic_t[k](x_next)
+            y = rewards[:, k:k + 1].float() + (1 - dones[:, k:k + 1].float()) * self.gamma * q_next
+            closs = nn.MSELoss()(q, y)
+            self.opt_c[k].zero_grad()
+            closs.backward()
+            self.opt_c[k].step()
+            a_k = gumbel_softmax(self.actors[k](s[k]), u_cur[k])
+            det = [a.detach() for a in acts]
+            det[k] = a_k
+            aloss = -self.critics[k](torch.cat(s + det, 1)).mean()
+            self.opt_a[k].zero_grad()
+            aloss.backward()
+            self.opt_a[k].step()
+            losses.append((aloss.item(), closs.item()))
+        with torch.no_grad():
+            for nets, tgts in ((self.actors, self.actor_t), (self.critics, self.critic_t)):
+                for n, t in zip(nets, tgts):
+                    for p, tp in zip(n.parameters(), t.parameters()):
+                        tp.copy_(self.tau * p + (1 - self.tau) * tp)
+        return losses
+
+
+def _assert_same(m: MADDPG, ref: PerAgentReference, tol=2e-5):
+    for k in range(m.K):
+        for stacked, seqs in ((m.actors.net, ref.actors), (m.actor_targets.net, ref.actor_t),
+                              (m.critics, ref.critics), (m.critic_targets, ref.critic_t)):
+            want = _seq(stacked, k)
+            for a, b in zip(want.parameters(), seqs[k].parameters()):
+                torch.testing.assert_close(a, b, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("K", [1, 2, 3])
+def test_stacked_learn_matches_per_agent_loop(K):
+    torch.manual_seed(0)
+    H, W, B = 4, 5, 16
+    m = MADDPG(K, H, W, hidden=(16, 16), lr_actor=1e-2, lr_critic=1e-2, gamma=0.98, tau=0.1, batch_size=B, seed=3)
+    # make the targets differ from the online nets, as after some training
+    with torch.no_grad():
+        for p in list(m.actor_targets.parameters()) + list(m.critic_targets.parameters()):
+            p.add_(0.05 * torch.randn_like(p))
+    ref = PerAgentReference(m, 1e-2, 1e-2)
+    g = torch.Generator().manual_seed(1)
+    for it in range(4):
+        states = torch.randint(-1, 6, (K, B, H, W), generator=g).float()
+        next_states = torch.randint(-1, 6, (K, B, H, W), generator=g).float()
+        actions = torch.softmax(torch.randn((K, B, 9), generator=g), -1)
+        rewards = torch.randn((B, K), generator=g, dtype=torch.float64) * 10
+        dones = (torch.rand((B, K), generator=g) < 0.2).to(torch.uint8)
+        u_next = torch.rand((K, B, 9), generator=g)
+        u_cur = torch.rand((K, B, 9), generator=g)
+        a_loss, c_loss = m.learn(states, actions, rewards, next_states, dones, u_next, u_cur)
+        want = ref.learn(states, actions, rewards, next_states, dones, u_next, u_cur)
+        for k in range(K):
+            assert abs(a_loss[k].item() - want[k][0]) < 1e-4 * max(1.0, abs(want[k][0]))
+            assert abs(c_loss[k].item() - want[k][1]) < 1e-4 * max(1.0, abs(want[k][1]))
+        _assert_same(m, ref)
+
+
+def test_gumbel_softmax_is_a_distribution_and_sharpens():
+    logits = torch.tensor([[0.0, 5.0, 0.0]])
+    g = torch.Generator().manual_seed(0)
+    p = torch.stack([gumbel_softmax(logits, generator=g) for _ in range(2000)])
+    torch.testing.assert_close(p.sum(-1), torch.ones_like(p.sum(-1)))
+    assert (p.argmax(-1) == 1).float().mean() > 0.9
+
+
+def test_learn_schedule_matches_reference_rule():
+    # maddpg/agent.py:199-224: learn_step > num_envs -> every learn_step // num_envs steps
+    assert [learns_per_step(1, 10, i) for i in range(21)].count(1) == 3
+    assert learns_per_step(4, 10, 0) == 1 and learns_per_step(4, 10, 1) == 0
+    # num_envs >= learn_step -> num_envs // learn_step learns every step
+    assert learns_per_step(65536, 10, 7) == 6553
+
+
+def test_checkpoint_roundtrip(tmp_path):
+    m = MADDPG(2, 4, 5, hidden=(8, 8), seed=1)
+    path = str(tmp_path / "maddpg.safetensors")
+    m.save(path)
+    m2 = MADDPG(2, 4, 5, hidden=(8, 8), seed=7)
+    m2.load(path)
+    for a, b in zip(m.state_dict().values(), m2.state_dict().values()):
+        assert torch.equal(a, b)
+    m3 = copy.deepcopy(m2)
+    assert torch.equal(m3.actors.net.weights[0], m.actors.net.weights[0])
