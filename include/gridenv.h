@@ -59,6 +59,12 @@ typedef struct gw_config {
     int32_t max_steps;          /* TRAIN_STEPS episode cap; 0 = none                     */
     int32_t auto_reset;         /* reset done envs inside gw_step                        */
     uint64_t seed;              /* Philox key (spawns, scripted policy, random RL policy)*/
+    int32_t variant;            /* 0: CustomMAEnv (custom/ma_customenv.py); 1: the single-
+                                   agent CustomEnv (custom/customenv.py:78-183): K must be 1,
+                                   rewards -10 crash (terminated only) / +20 apple (exactly one
+                                   apples_caught entry; truncated) / +0.1 closer to the apple,
+                                   step obs = raw WorldState ids (no relabel), prev distance set
+                                   at reset.  Everything else is shared.                    */
 } gw_config;
 
 /* Per-step outputs: device pointers, any may be NULL (not written). */

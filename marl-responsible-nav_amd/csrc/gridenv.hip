@@ -91,6 +91,7 @@ struct Params {
     int64_t e_begin, e_end;   // env range of this launch (step_v2 / obs_kernel chunks)
     uint4 *fwork;             // [E][FearRec<N>::R4] deferred-FeAR records (GW_KERNEL=defer)
     int64_t stats_row0;       // first gw_step_out.stats row this launch writes
+    int variant;              // 0 CustomMAEnv, 1 single-agent CustomEnv (custom/customenv.py)
     int apples[MAXN];
 };
 
@@ -290,6 +291,9 @@ struct World {
     }
 };
 
+// UpdateGWorld (grid_world.py:424-563).  caught: bits 0-7 = eaters k that stood on apple[k] at
+// some sub-step (floor position, :530-545); bits 8+ = the number of (k, apple) entries the
+// reference appends to apples_caught (the single-agent env rewards only len == 1).
 template <int N, bool APPLES, class OK>
 __device__ __forceinline__ void simulate(World<N> &w, const OK &okm, int K,
                                          const int (&apple)[MAXN], uint32_t &caught, int (&fin)[N]) {
@@ -299,21 +303,21 @@ __device__ __forceinline__ void simulate(World<N> &w, const OK &okm, int K,
     if (APPLES) {
 #pragma unroll
         for (int k = 0; k < N; ++k)
-            if (k < K && w.template cf<0>(k) == apple[k]) caught |= 1u << k;
+            if (k < K && w.template cf<0>(k) == apple[k]) caught = (caught | (1u << k)) + (1u << 8);
     }
     w.template move<1, OK>(okm);
     w.template resolve<1>();
     if (APPLES) {
 #pragma unroll
         for (int k = 0; k < N; ++k)
-            if (k < K && w.template cf<1>(k) == apple[k]) caught |= 1u << k;
+            if (k < K && w.template cf<1>(k) == apple[k]) caught = (caught | (1u << k)) + (1u << 8);
     }
     w.template move<2, OK>(okm);
     w.template resolve<2>();
     if (APPLES) {
 #pragma unroll
         for (int k = 0; k < N; ++k)
-            if (k < K && w.template cf<2>(k) == apple[k]) caught |= 1u << k;
+            if (k < K && w.template cf<2>(k) == apple[k]) caught = (caught | (1u << k)) + (1u << 8);
     }
     w.template move<3, OK>(okm);
     w.template resolve<3>();
@@ -322,7 +326,7 @@ __device__ __forceinline__ void simulate(World<N> &w, const OK &okm, int K,
     if (APPLES) {
 #pragma unroll
         for (int k = 0; k < N; ++k)
-            if (k < K && fin[k] == apple[k]) caught |= 1u << k;
+            if (k < K && fin[k] == apple[k]) caught = (caught | (1u << k)) + (1u << 8);
     }
 }
 
@@ -472,7 +476,8 @@ __device__ __forceinline__ void reset_env(const Params &p, int64_t e, uint32_t e
     p.st.flags[e] = all_bits(p.K);
     p.st.t[e] = 0;
     p.st.episode[e] = episode;
-    for (int k = 0; k < p.K; ++k) p.st.prev[(int64_t)k * p.E + e] = -1;
+    for (int k = 0; k < p.K; ++k)  // None (ma_customenv.py:213); customenv.py:342-345 sets it at reset
+        p.st.prev[(int64_t)k * p.E + e] = p.variant == 1 ? manhattan(p, pos[k], p.apples[k]) : -1;
     if (ZERO_SCORE) {  // with deferred FeAR the fear kernel owns score / fear_score
         p.st.score[e] = 0.0;
         p.st.fscore[e] = 0.0;
@@ -481,8 +486,9 @@ __device__ __forceinline__ void reset_env(const Params &p, int64_t e, uint32_t e
 
 // Deferred-FeAR record of one env step (GW_KERNEL=defer): what fear_v2 needs to finish the
 // step after step_v2 has moved the world on.  R4 uint4 words per env, AoS for 16-byte
-// coalesced access:  u16 pre-step cells [N] | u8 actions [N] (bit 7 of byte 0 = done) | i8 env
-// rewards [K].  N <= 4: words 0-1 | 2 | 3;  N <= 8: words 0-3 | 4-5 | 6-7.
+// coalesced access:  u16 pre-step cells [N] | u8 actions [N] (bit 7 of byte 0 = done, bit 6 of
+// byte k = the single-agent env's +0.1 distance reward of agent k) | i8 integer env rewards [K].
+// N <= 4: words 0-1 | 2 | 3;  N <= 8: words 0-3 | 4-5 | 6-7.
 template <int N>
 struct FearRec {
     static constexpr int R4 = N <= 4 ? 1 : 2, PW = 2 * R4, AW = PW, RW = PW + R4;
@@ -491,7 +497,7 @@ struct FearRec {
 
 template <int N>
 __device__ __forceinline__ void store_fear_rec(const Params &p, int64_t e, const int (&pos)[N], const int (&act)[N],
-                                               const int (&rew)[MAXN], bool done) {
+                                               const int (&rew)[MAXN], uint32_t bonus, bool done) {
     using R = FearRec<N>;
     R r;
 #pragma unroll
@@ -499,7 +505,7 @@ __device__ __forceinline__ void store_fear_rec(const Params &p, int64_t e, const
 #pragma unroll
     for (int n = 0; n < N; ++n) {
         r.w[n >> 1] |= ((uint32_t)pos[n] & 0xFFFFu) << (16 * (n & 1));
-        r.w[R::AW + (n >> 2)] |= ((uint32_t)act[n] & 0x7Fu) << (8 * (n & 3));
+        r.w[R::AW + (n >> 2)] |= (((uint32_t)act[n] & 0x3Fu) | (((bonus >> n) & 1u) << 6)) << (8 * (n & 3));
         if (n < p.K) r.w[R::RW + (n >> 2)] |= ((uint32_t)rew[n] & 0xFFu) << (8 * (n & 3));
     }
     r.w[R::AW] |= (uint32_t)done << 7;
@@ -510,7 +516,7 @@ __device__ __forceinline__ void store_fear_rec(const Params &p, int64_t e, const
 
 template <int N>
 __device__ __forceinline__ void load_fear_rec(const Params &p, int64_t e, int (&pos)[N], int (&act)[N],
-                                              int (&rew)[MAXN], bool &done) {
+                                              int (&rew)[MAXN], uint32_t &bonus, bool &done) {
     using R = FearRec<N>;
     R r;
     const uint4 *src = p.fwork + e * R::R4;
@@ -519,10 +525,13 @@ __device__ __forceinline__ void load_fear_rec(const Params &p, int64_t e, int (&
         const uint4 v = src[q];
         r.w[4 * q] = v.x; r.w[4 * q + 1] = v.y; r.w[4 * q + 2] = v.z; r.w[4 * q + 3] = v.w;
     }
+    bonus = 0;
 #pragma unroll
     for (int n = 0; n < N; ++n) {
         pos[n] = (int)((r.w[n >> 1] >> (16 * (n & 1))) & 0xFFFFu);
-        act[n] = (int)((r.w[R::AW + (n >> 2)] >> (8 * (n & 3))) & 0x7Fu);
+        const uint32_t byte = (r.w[R::AW + (n >> 2)] >> (8 * (n & 3))) & 0xFFu;
+        act[n] = (int)(byte & 0x3Fu);
+        bonus |= ((byte >> 6) & 1u) << n;
     }
 #pragma unroll
     for (int k = 0; k < MAXN; ++k)
@@ -605,20 +614,28 @@ __device__ __forceinline__ void finish_env(const Params &p, int64_t e, const Env
     int rew[MAXN];
 #pragma unroll
     for (int k = 0; k < MAXN; ++k) rew[k] = 0;
-    // apples (:258-275): own apple, once; all eaten -> +20 to all, truncation
-    const uint32_t popped = caught & apples;
+    const bool single = p.variant == 1;  // custom/customenv.py:127-160 (K = 1)
+    // apples (:258-275): own apple, once; all eaten -> +20 to all, truncation.  Single agent
+    // (customenv.py:142-148): rewarded only when apples_caught holds exactly one entry.
+    const uint32_t popped = single ? (((caught >> 8) == 1u) ? (caught & apples & 1u) : 0u) : (caught & apples & 0xFFu);
     apples &= ~popped;
     int apple_rewarded = __popc(popped);
 #pragma unroll
     for (int k = 0; k < N; ++k)
         if ((popped >> k) & 1u) rew[k] += 20;
     if (popped && apples == 0) {
+        if (single) {
+            trunc |= 1u;
+        } else {
 #pragma unroll
-        for (int k = 0; k < N; ++k)
-            if (k < K) rew[k] += 20;
-        trunc = allk;
+            for (int k = 0; k < N; ++k)
+                if (k < K) rew[k] += 20;
+            trunc = allk;
+        }
     }
     int crash_count = 0;
+    uint32_t bonus = 0;  // single agent: +0.1 for moving closer to the apple (customenv.py:155-156)
+    double rewd[MAXN];
     double shaped[MAXN];
     double fsum_in[MAXN];
 #pragma unroll
@@ -626,18 +643,25 @@ __device__ __forceinline__ void finish_env(const Params &p, int64_t e, const Env
 #pragma unroll
     for (int k = 0; k < N; ++k) {
         if (k >= K) continue;
-        if ((crash >> k) & 1u) {  // :281-285
+        if ((crash >> k) & 1u) {  // :281-285 (single agent :138-140: terminated only)
             rew[k] -= 10;
             ++crash_count;
-            trunc = allk;
+            if (!single) trunc = allk;
             term |= 1u << k;
         }
-        const int d = ((apples >> k) & 1u) ? manhattan(p, fin[k], p.apples[k]) : -1;  // :287-294
         const int64_t pi = (int64_t)k * p.E + e;
         const int prev = es.prev[k];
-        if (prev >= 0 && d >= 0 && prev > d) rew[k] += 1;  // :296-300
-        p.st.prev[pi] = d;
-        shaped[k] = __dadd_rn(__dmul_rn(p.fear_weight, fear[k]), (double)rew[k]);  // agent.py:130
+        if (single) {  // distance to the apple cell, eaten or not (apple_loc is read before the pop)
+            const int d = manhattan(p, fin[k], p.apples[k]);
+            bonus |= (uint32_t)(d < prev) << k;
+            p.st.prev[pi] = d;
+        } else {
+            const int d = ((apples >> k) & 1u) ? manhattan(p, fin[k], p.apples[k]) : -1;  // :287-294
+            if (prev >= 0 && d >= 0 && prev > d) rew[k] += 1;  // :296-300
+            p.st.prev[pi] = d;
+        }
+        rewd[k] = ((bonus >> k) & 1u) ? __dadd_rn((double)rew[k], 0.1) : (double)rew[k];
+        shaped[k] = __dadd_rn(__dmul_rn(p.fear_weight, fear[k]), rewd[k]);  // agent.py:130
         fsum_in[k] = fear[k];
     }
     const double score = DEFER ? 0.0 : __dadd_rn(es.score, np_sum_small(shaped, K));    // agent.py:173
@@ -658,7 +682,7 @@ __device__ __forceinline__ void finish_env(const Params &p, int64_t e, const Env
     for (int k = 0; k < N; ++k) {
         if (k >= K) continue;
         const int64_t ek = e * K + k;
-        if (o.reward) o.reward[ek] = (double)rew[k];
+        if (o.reward) o.reward[ek] = rewd[k];
         if (!DEFER && o.fear) o.fear[ek] = fear[k];
         if (!DEFER && o.shaped) o.shaped[ek] = shaped[k];
         if (o.term) o.term[ek] = (uint8_t)((term >> k) & 1u);
@@ -670,7 +694,7 @@ __device__ __forceinline__ void finish_env(const Params &p, int64_t e, const Env
     if (!DEFER && o.ep_return) o.ep_return[e] = score;
     if (!DEFER && o.ep_fear) o.ep_fear[e] = fscore;
     if (o.ep_len) o.ep_len[e] = t;
-    if (DEFER) store_fear_rec<N>(p, e, es.pos, act, rew, done);
+    if (DEFER) store_fear_rec<N>(p, e, es.pos, act, rew, bonus, done);
     if (o.crash_bits) o.crash_bits[e] = (uint8_t)crash;
     if (o.restr_bits) o.restr_bits[e] = (uint8_t)restr;
 #pragma unroll
@@ -960,7 +984,7 @@ __global__ void __launch_bounds__(256) step_kernel_fear(Params p) {
         EnvState<N> es;
         load_env<N>(p, e, es);
         ObsInfo<N> oi;
-        finish_env<N>(p, e, es, act, mdr, fear, bits & 0xFFu, (bits >> 8) & 0xFFu, fin, (bits >> 16) & 0xFFu, ct, oi);
+        finish_env<N>(p, e, es, act, mdr, fear, bits & 0xFFu, (bits >> 8) & 0xFFu, fin, bits >> 16, ct, oi);
         store_desc<N>(p, e, oi);
     }
     if (p.out.stats && tid < 64) {  // BE <= 64: every env of the block sits in wave 0
@@ -999,9 +1023,10 @@ __global__ void __launch_bounds__(256) reset_kernel(Params p) {
 constexpr int OBS_BE = 8;      // envs per block
 constexpr int OBS_THREADS = 256;
 
-__device__ __forceinline__ float agent_value(bool reset, int n, int k, bool on_apple) {
+__device__ __forceinline__ float agent_value(bool reset, int n, int k, bool on_apple, int variant) {
     if (reset) return on_apple ? 9.5f : 0.5f;
     if (on_apple) return (float)(n + 1 + 9);
+    if (variant == 1) return (float)(n + 1);  // customenv.py:163-166: raw WorldState ids
     int v = n + 1;
     if (v >= 1 && v <= 4 && v != k + 1) v = 5;   // other ids -> 5 (all_ids = [1,2,3,4], :314)
     if (v == k + 1) v = 1;                        // my id -> 1 (:321)
@@ -1043,7 +1068,7 @@ __global__ void __launch_bounds__(OBS_THREADS) obs_kernel(Params p, float *__res
             for (int n = 0; n < N; ++n) {
                 const int c = (int)((pw[n >> 1] >> (16 * (n & 1))) & 0xFFFFu);
                 s_pc[which][el][k][np] = c;
-                s_pv[which][el][k][np] = agent_value(reset, n, k, c == ac);
+                s_pv[which][el][k][np] = agent_value(reset, n, k, c == ac, p.variant);
                 ++np;
             }
             for (; np <= MAXN; ++np) s_pc[which][el][k][np] = -1;
@@ -1214,7 +1239,7 @@ __device__ __forceinline__ void v2_patches(const Params &p, int el, const ObsInf
         for (int n = 0; n < N; ++n) {
             const int c = WH == 0 ? oi.pos[n] : oi.fpos[n];
             pc[WH][el][k][np] = (uint16_t)c;
-            pv[WH][el][k][np] = agent_value(reset, n, k, c == ac);
+            pv[WH][el][k][np] = agent_value(reset, n, k, c == ac, p.variant);
             ++np;
         }
         for (; np < NP; ++np) pc[WH][el][k][np] = 0xFFFFu;
@@ -1488,7 +1513,7 @@ __global__ void __launch_bounds__(128) step_v2(Params p) {
             fear_values<N, KMAX>(p, sh, tid, act, mdr, resp_s, fear);
             const uint32_t bits = sh.bits[tid];
             ObsInfo<N> oi;
-            finish_env<N>(p, e, es, act, mdr, fear, bits & 0xFFu, (bits >> 8) & 0xFFu, fin, (bits >> 16) & 0xFFu, ct, oi, ctab);
+            finish_env<N>(p, e, es, act, mdr, fear, bits & 0xFFu, (bits >> 8) & 0xFFu, fin, bits >> 16, ct, oi, ctab);
             if constexpr (OBS) {
                 v2_patches<N, 0, OB, KMAX, NP>(p, tid, oi, ctab, sh.pc, sh.pv);
                 if (oi.flags & D_FINAL) v2_patches<N, 1, OB, KMAX, NP>(p, tid, oi, ctab, sh.pc, sh.pv);
@@ -1598,11 +1623,12 @@ __global__ void __launch_bounds__(128) fear_v2(Params p) {
     const int nenv = (int)min((int64_t)BE, p.e_end - e0);
     const int K = p.K;
     int pos[N], act[N], rew[MAXN];
+    uint32_t bonus = 0;
     bool done = false;
     double score0 = 0.0, fscore0 = 0.0;
     if (tid < nenv) {
         const int64_t e = e0 + tid;
-        load_fear_rec<N>(p, e, pos, act, rew, done);
+        load_fear_rec<N>(p, e, pos, act, rew, bonus, done);
         score0 = p.st.score[e];
         fscore0 = p.st.fscore[e];
     }
@@ -1640,7 +1666,8 @@ __global__ void __launch_bounds__(128) fear_v2(Params p) {
         for (int k = 0; k < MAXN; ++k) {
             shaped[k] = fsum_in[k] = 0.0;
             if (k >= K) continue;
-            shaped[k] = __dadd_rn(__dmul_rn(p.fear_weight, fear[k]), (double)rew[k]);  // agent.py:130
+            const double r = ((bonus >> k) & 1u) ? __dadd_rn((double)rew[k], 0.1) : (double)rew[k];
+            shaped[k] = __dadd_rn(__dmul_rn(p.fear_weight, fear[k]), r);  // agent.py:130
             fsum_in[k] = fear[k];
         }
         const double score = __dadd_rn(score0, np_sum_small(shaped, K));    // agent.py:173
@@ -1689,7 +1716,7 @@ struct Env {
     int device = 0;
     int H = 0, W = 0, HW = 0, N = 0, K = 0, F = 0, P = 0;
     int64_t E = 0, env_offset = 0;
-    int fear = 0, max_steps = 0, auto_reset = 1;
+    int fear = 0, max_steps = 0, auto_reset = 1, variant = 0;
     double fear_weight = 0.0;
     uint64_t seed = 0;
     int apples[GW_MAX_AGENTS] = {0};
@@ -1792,6 +1819,7 @@ gw::Params make_params(const Env *env) {
     p.e_end = env->E;
     p.fwork = env->fwork;
     p.stats_row0 = 0;
+    p.variant = env->variant;
     p.tb.roadbits = env->roadbits;
     p.st.pos = env->pos;
     p.st.flags = env->flags;
@@ -1998,6 +2026,8 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
     if (H < 1 || W < 2 || (int64_t)H * W > 4096) return fail(GW_ERR_ARG, "need W >= 2 and H*W <= 4096");
     if (N < 1 || N > GW_MAX_AGENTS || K < 1 || K > N) return fail(GW_ERR_ARG, "need 1 <= K <= N <= 8");
     if (cfg->num_envs < 1) return fail(GW_ERR_ARG, "num_envs must be >= 1");
+    if (cfg->variant != 0 && cfg->variant != 1) return fail(GW_ERR_ARG, "variant must be 0 or 1");
+    if (cfg->variant == 1 && K != 1) return fail(GW_ERR_ARG, "the single-agent variant needs K == 1");
     if (cfg->env_offset < 0 || cfg->env_offset + cfg->num_envs > ((int64_t)1 << 32))
         return fail(GW_ERR_ARG, "global env ids must fit in 32 bits");
     if (!sc->region || !sc->policy_id || !sc->policy_cdf || !sc->mdr || !sc->apples || sc->n_policies < 1)
@@ -2061,6 +2091,7 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
     env->fear_weight = cfg->fear_weight;
     env->max_steps = cfg->max_steps;
     env->auto_reset = cfg->auto_reset ? 1 : 0;
+    env->variant = cfg->variant;
     env->seed = cfg->seed;
     for (int k = 0; k < K; ++k) env->apples[k] = sc->apples[k];
     {

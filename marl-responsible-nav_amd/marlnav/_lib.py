@@ -81,7 +81,8 @@ class GwScenario(C.Structure):
 class GwConfig(C.Structure):
     _fields_ = [("N", C.c_int32), ("K", C.c_int32), ("num_envs", C.c_int64),
                 ("env_offset", C.c_int64), ("fear", C.c_int32), ("fear_weight", C.c_double),
-                ("max_steps", C.c_int32), ("auto_reset", C.c_int32), ("seed", C.c_uint64)]
+                ("max_steps", C.c_int32), ("auto_reset", C.c_int32), ("seed", C.c_uint64),
+                ("variant", C.c_int32)]
 
 
 STEP_OUT_FIELDS = ["obs", "final_obs", "reward", "fear", "shaped", "term", "trunc", "done", "mask",

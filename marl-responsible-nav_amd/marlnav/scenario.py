@@ -281,7 +281,16 @@ BUILTIN = {
     "level3": (10, 16, 4, 2),       # Level 3 of custom/Scenarios.json (BASELINE config 1)
     "grid32": (32, 32, 4, 2),       # BASELINE configs 2, 3, 5
     "grid64_n8": (64, 64, 8, 2),    # BASELINE config 4
+    "level3_single": (10, 16, 4, 1),  # single-agent CustomEnv: Level 3, apple_0 at (9, 15) (customenv.py:334)
 }
+
+
+def _builtin_dict(name: str) -> dict:
+    H, W, N, K = BUILTIN[name]
+    sc = level3_like(H, W, N, K)
+    if name == "level3_single":
+        sc["Apples"] = {"apple_0": [H - 1, W - 1]}
+    return sc
 
 
 def builtin(name: str) -> CompiledScenario:
@@ -290,8 +299,7 @@ def builtin(name: str) -> CompiledScenario:
         with open(path) as f:
             sc = json.load(f)
     elif name in BUILTIN:
-        H, W, N, K = BUILTIN[name]
-        sc = level3_like(H, W, N, K)
+        sc = _builtin_dict(name)
     else:
         raise KeyError(f"unknown scenario {name!r}; builtins: {sorted(BUILTIN)}")
     return compile_scenario(sc, name=name)
@@ -299,6 +307,6 @@ def builtin(name: str) -> CompiledScenario:
 
 def write_builtin_jsons() -> None:
     os.makedirs(SCENARIO_DIR, exist_ok=True)
-    for name, (H, W, N, K) in BUILTIN.items():
+    for name in BUILTIN:
         with open(os.path.join(SCENARIO_DIR, f"{name}.json"), "w") as f:
-            json.dump(level3_like(H, W, N, K), f)
+            json.dump(_builtin_dict(name), f)

@@ -62,7 +62,7 @@ class VecGridEnv:
     def __init__(self, scenario: CompiledScenario | str = "level3", num_envs: int = 1, fear: bool = True,
                  fear_weight: float = -5.0, max_steps: int = 150, auto_reset: bool = True, seed: int = 42,
                  device: torch.device | int | None = None, env_offset: int = 0, final_obs: bool = False,
-                 debug: bool = False, obs: bool = True, stats: bool = False):
+                 debug: bool = False, obs: bool = True, stats: bool = False, variant: int | str = 0):
         if not torch.cuda.is_available():
             raise _lib.GwError("VecGridEnv needs a HIP device (no CPU fallback by design)")
         sc = builtin(scenario) if isinstance(scenario, str) else scenario
@@ -74,6 +74,8 @@ class VecGridEnv:
         self.max_steps = int(max_steps)
         self.auto_reset = bool(auto_reset)
         self.seed = int(seed)
+        # 0 / "multi": CustomMAEnv;  1 / "single": the single-agent CustomEnv (custom/customenv.py)
+        self.variant = {"multi": 0, "single": 1}.get(variant, variant) if isinstance(variant, str) else int(variant)
         self.env_offset = int(env_offset)
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else
                                    (device if isinstance(device, int) else device.index or 0))
@@ -88,7 +90,7 @@ class VecGridEnv:
                               int(sc.policy_cdf.shape[0]), keep["cdf"].ctypes.data, keep["mdr"].ctypes.data,
                               keep["apples"].ctypes.data)
         cfg = _lib.GwConfig(self.N, self.K, self.E, self.env_offset, int(self.fear_enabled), self.fear_weight,
-                            self.max_steps, int(self.auto_reset), self.seed & 0xFFFFFFFFFFFFFFFF)
+                            self.max_steps, int(self.auto_reset), self.seed & 0xFFFFFFFFFFFFFFFF, self.variant)
         h = C.c_void_p()
         with torch.cuda.device(self.device):
             _lib.check(self.lib.gw_create(C.byref(scn), C.byref(cfg), self.device.index, C.byref(h)), "gw_create")

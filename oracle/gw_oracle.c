@@ -312,6 +312,7 @@ static void write_step_obs(const orc_world *w, const orc_env *s, float *obs, int
         for (int c = 0; c < HW; ++c) o[c] = w->region[c] ? 0.0f : -1.0f;
         for (int n = 0; n < w->N; ++n) o[s->pos[n]] = (float)(n + 1);
         if (s->apples & (1u << k)) o[w->apples[k]] += 9.0f;
+        if (w->variant == 1) continue; /* customenv.py:163-166: WorldState + 9 at the apple, raw ids */
         for (int c = 0; c < HW; ++c) {
             float v = o[c];
             for (int id = 1; id <= 4; ++id)
@@ -356,6 +357,8 @@ static void reset_state(const orc_world *w, int64_t env_id, orc_env *s, const in
     s->apples = (w->K >= 32) ? 0xFFFFFFFFu : ((1u << w->K) - 1u);
     s->term = s->trunc = 0;
     for (int k = 0; k < ORC_MAX_N; ++k) s->prev_dist[k] = -1;
+    if (w->variant == 1) /* customenv.py:342-345: prev_distance set at reset (never None) */
+        for (int k = 0; k < w->K; ++k) s->prev_dist[k] = manhattan(w->W, s->pos[k], w->apples[k]);
     s->t = 0;
     s->score = 0.0;
     s->fear_score = 0.0;
@@ -419,6 +422,7 @@ void orc_env_step(const orc_world *w, int64_t env_id, orc_env *s, const int32_t 
             }
             double resp[ORC_MAX_N * ORC_MAX_N];
             int32_t vm[ORC_MAX_N], va[ORC_MAX_N];
+            if (w->variant == 1 && len <= 1) continue; /* customenv.py:117-118: FeAR_vals = 0.0 */
             fear[k] = orc_fear_one_actor(H, W, w->region, N, s->pos, len, ids, la, mdr, k, resp, vm, va);
         }
     }
@@ -433,9 +437,28 @@ void orc_env_step(const orc_world *w, int64_t env_id, orc_env *s, const int32_t 
     for (int n = 0; n < N; ++n) s->pos[n] = fin[n];
 
     int32_t rew[ORC_MAX_N];
+    double rewd[ORC_MAX_N]; /* the env reward as the caller sees it (int valued unless variant 1) */
     for (int k = 0; k < K; ++k) rew[k] = 0; /* :235 */
     int apple_rewarded = 0, crash_count = 0;
     const uint32_t all_k = (K >= 32) ? 0xFFFFFFFFu : ((1u << K) - 1u);
+    if (w->variant == 1) { /* customenv.py:127-160 (K = 1, apple_eaters = [0]) */
+        int32_t d0 = manhattan(W, s->pos[0], w->apples[0]); /* apple_loc taken before the pop :130 */
+        double r = 0.0;
+        if (crash[0]) { /* :138-140 terminated only */
+            r -= 10;
+            crash_count++;
+            s->term |= 1u;
+        }
+        if (n_caught == 1 && (s->apples & 1u)) { /* :142-148 exactly one (agent, apple) entry */
+            s->apples &= ~1u;
+            r += 20;
+            apple_rewarded++;
+            if (s->apples == 0) s->trunc |= 1u;
+        }
+        if (d0 < s->prev_dist[0]) r += 0.1; /* :155-156 */
+        s->prev_dist[0] = d0;
+        rewd[0] = r;
+    } else {
     for (int i = 0; i < n_caught; ++i) { /* :258-275 */
         int agent = caught[2 * i], apple = caught[2 * i + 1];
         if (apple == agent && (s->apples >> apple & 1u)) {
@@ -460,12 +483,14 @@ void orc_env_step(const orc_world *w, int64_t env_id, orc_env *s, const int32_t 
         if (s->prev_dist[i] >= 0 && dist[i] >= 0 && s->prev_dist[i] > dist[i]) rew[i] += 1;
     }
     for (int i = 0; i < K; ++i) s->prev_dist[i] = dist[i];
+    for (int k = 0; k < K; ++k) rewd[k] = (double)rew[k];
+    } /* variant */
 
     /* maddpg/agent.py:124-141,173 — shaped reward, fear_score, scores */
     double shaped[ORC_MAX_N];
     for (int k = 0; k < K; ++k) {
         double x = w->fear_weight * fear[k];
-        shaped[k] = x + (double)rew[k];
+        shaped[k] = x + rewd[k];
     }
     s->score += orc_np_sum(shaped, K);
     s->fear_score += orc_np_sum(fear, K);
@@ -484,7 +509,7 @@ void orc_env_step(const orc_world *w, int64_t env_id, orc_env *s, const int32_t 
             out->restricted_bits |= (uint32_t)restr[n] << n;
         }
         for (int k = 0; k < K; ++k) {
-            out->reward[k] = (double)rew[k];
+            out->reward[k] = rewd[k];
             out->fear[k] = fear[k];
             out->shaped[k] = shaped[k];
             out->term[k] = (uint8_t)(s->term >> k & 1u);

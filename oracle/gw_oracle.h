@@ -41,6 +41,8 @@ typedef struct orc_world {
     int32_t max_steps;         /* TRAIN_STEPS episode cap               maddpg/agent.py:85,243  */
     uint64_t seed;             /* Philox key for native-RNG mode                                */
     int64_t env_offset;        /* global id of env 0 (RNG counter)                              */
+    int32_t variant;           /* 0 CustomMAEnv (ma_customenv.py), 1 single-agent CustomEnv
+                                  (customenv.py:78-183): K = 1, float rewards, no relabel       */
 } orc_world;
 
 /* Per-env mutable state. */

@@ -29,7 +29,8 @@ class World(C.Structure):
                 ("region", C.c_void_p), ("policy_id", C.c_void_p), ("policy_cdf", C.c_void_p),
                 ("mdr", C.c_void_p), ("apples", C.c_void_p), ("n_free", C.c_int32),
                 ("free_cells", C.c_void_p), ("fear", C.c_int32), ("fear_weight", C.c_double),
-                ("max_steps", C.c_int32), ("seed", C.c_uint64), ("env_offset", C.c_int64)]
+                ("max_steps", C.c_int32), ("seed", C.c_uint64), ("env_offset", C.c_int64),
+                ("variant", C.c_int32)]
 
 
 class Env(C.Structure):
@@ -137,7 +138,7 @@ class OracleEnvs:
     """E independent envs stepped by the C restatement (replay or native-RNG mode)."""
 
     def __init__(self, sc, E: int, fear: bool, fear_weight: float = -5.0, max_steps: int = 150,
-                 seed: int = 42, env_offset: int = 0, reset: bool = True):
+                 seed: int = 42, env_offset: int = 0, reset: bool = True, variant: int = 0):
         self.sc = sc
         self.E = int(E)
         self._keep = dict(region=np.ascontiguousarray(sc.region, np.uint8),
@@ -150,7 +151,7 @@ class OracleEnvs:
         self.world = World(sc.H, sc.W, sc.N, sc.K, _ptr(k["region"]), _ptr(k["policy_id"]),
                            _ptr(k["cdf"]), _ptr(k["mdr"]), _ptr(k["apples"]), k["free"].size,
                            _ptr(k["free"]), int(bool(fear)), float(fear_weight), int(max_steps),
-                           int(seed) & 0xFFFFFFFFFFFFFFFF, int(env_offset))
+                           int(seed) & 0xFFFFFFFFFFFFFFFF, int(env_offset), int(variant))
         self.envs = (Env * self.E)()
         self.env_offset = int(env_offset)
         if reset:

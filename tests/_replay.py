@@ -64,3 +64,56 @@ def replay(stepper, d, K, N, max_err=None):
             np.testing.assert_array_equal(np.round(np.asarray(o["obs"]).reshape(d["obs"][t].shape) * 2).astype(np.int8), d["obs"][t], err_msg=ctx + " obs")
             np.testing.assert_array_equal(o["mask"], d["mask"][t], err_msg=ctx + " mask")
     return T, (max(errs) if errs else 0.0)
+
+
+SINGLE = "single_traj.npz"
+
+
+def single_cases(gold_dir):
+    """Run tags of tests/golden/single_traj.npz (make_golden_single.py)."""
+    import os
+    z = np.load(os.path.join(gold_dir, SINGLE))
+    return sorted({k.split("/", 1)[0] for k in z.files})
+
+
+def load_single(gold_dir, tag):
+    import os
+    z = np.load(os.path.join(gold_dir, SINGLE))
+    return {k.split("/", 1)[1]: z[k] for k in z.files if k.startswith(tag + "/")}
+
+
+def replay_single(stepper, d):
+    """Replay a single-agent CustomEnv trajectory (custom/customenv.py:78-183, K = 1) with a
+    stepper built for variant 1 and fear_weight 0 (so ep_return is the env's episode reward)."""
+    reset_at, reset_pos = list(d["reset_at"]), d["reset_pos"]
+    obs, _ = stepper.reset(reset_pos[0])
+    shape = d["reset_obs"][0].shape
+    q = lambda o: np.round(np.asarray(o).reshape(shape) * 2).astype(np.int8)
+    np.testing.assert_array_equal(q(obs), d["reset_obs"][0], err_msg="reset obs")
+    nres = 1
+    T = len(d["rl"])
+    for t in range(T):
+        spawn_next = reset_pos[nres] if d["done"][t] else None
+        if d["done"][t]:
+            assert reset_at[nres] == t
+        o = stepper.step([d["rl"][t]], d["act"][t][1:], spawn_next)
+        ctx = f"step {t}"
+        np.testing.assert_array_equal(o["act"], d["act"][t], err_msg=ctx + " actions")
+        np.testing.assert_array_equal(o["mdr"], d["mdr"][t], err_msg=ctx + " mdr")
+        np.testing.assert_array_equal(o["final_pos"], d["pos"][t], err_msg=ctx + " positions")
+        assert int(o["crash_bits"]) == int(d["crash_bits"][t]), ctx + " crash bits"
+        assert (int(o["restr_bits"]) & 1) == int(d["restricted"][t]), ctx + " info['restricted']"
+        assert float(o["reward"][0]) == float(d["reward"][t]), (ctx + " reward", o["reward"][0], d["reward"][t])
+        assert float(o["fear"][0]) == float(d["fear"][t]), ctx + " info['fear']"
+        assert int(o["term"][0]) == int(d["term"][t]), ctx + " terminated"
+        assert int(o["trunc"][0]) == int(d["trunc"][t]), ctx + " truncated"
+        assert int(o["done"]) == int(d["done"][t]), ctx + " done"
+        assert float(o["ep_return"]) == float(d["ep_r"][t]), ctx + " info['episode']['r']"
+        assert int(o["ep_len"]) == int(d["ep_l"][t]), ctx + " info['episode']['l']"
+        if d["done"][t]:
+            np.testing.assert_array_equal(q(o["final_obs"]), d["obs"][t], err_msg=ctx + " final obs")
+            np.testing.assert_array_equal(q(o["obs"]), d["reset_obs"][nres], err_msg=ctx + " reset obs")
+            nres += 1
+        else:
+            np.testing.assert_array_equal(q(o["obs"]), d["obs"][t], err_msg=ctx + " obs")
+    return T

@@ -55,7 +55,11 @@ def install_stubs():
         def __init__(self, low, high, shape, dtype):
             self.shape = shape
 
+    class Env:  # gymnasium.Env base of the single-agent CustomEnv (customenv.py:45)
+        pass
+
     gym = types.ModuleType("gymnasium")
+    gym.Env = Env
     sp = types.ModuleType("gymnasium.spaces")
     sp.Discrete, sp.Box, gym.spaces = Discrete, Box, sp
     for k, v in {"pettingzoo": pz, "pettingzoo.utils": pzu, "gymnasium": gym,
@@ -67,6 +71,9 @@ def import_reference():
     install_stubs()
     sys.dont_write_bytecode = True
     os.chdir(REF)
+    # /root/reference/custom is a namespace package (no __init__.py): a regular package of the
+    # same name anywhere on sys.path (this repo's CustomMAEnv facade) would shadow it
+    sys.path[:] = [p for p in sys.path if os.path.abspath(p or ".") != os.path.join(REPO, "marl-responsible-nav_amd")]
     sys.path.insert(0, REF)
     import custom.grid_world as G
     import custom.custom_agent as CA

@@ -14,7 +14,7 @@ from oracle import oracle as O
 from marlnav import scenario as S
 from marlnav.vec_env import VecGridEnv
 
-from _replay import load, replay
+from _replay import load, load_single, replay, replay_single, single_cases
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -26,9 +26,9 @@ def scenario_for(fname):
 
 
 class GpuStepper:
-    def __init__(self, sc, fear, weight):
+    def __init__(self, sc, fear, weight, variant=0):
         self.env = VecGridEnv(sc, num_envs=1, fear=fear, fear_weight=weight, max_steps=150,
-                              auto_reset=True, final_obs=True, debug=True)
+                              auto_reset=True, final_obs=True, debug=True, variant=variant)
         self.K, self.N = sc.K, sc.N
 
     def reset(self, spawn):
@@ -47,6 +47,16 @@ class GpuStepper:
                     ep_len=int(g(r.ep_len)), obs=r.obs[:, 0].cpu().numpy().reshape(self.K, -1),
                     final_obs=r.final_obs[:, 0].cpu().numpy().reshape(self.K, -1),
                     mask=g(r.mask).astype(np.uint16))
+
+
+@pytest.mark.parametrize("tag", single_cases(GOLD))
+def test_gpu_replays_single_agent_trajectory(tag, kernel_path):
+    """custom/customenv.py (single-agent CustomEnv) trajectories from the reference, bit-exact
+    through the C ABI on every kernel path."""
+    d = load_single(GOLD, tag)
+    st = GpuStepper(S.builtin("level3_single"), tag.startswith("fear"), 0.0, variant=1)
+    assert replay_single(st, d) == len(d["rl"])
+    st.env.close()
 
 
 def traj_cases():

@@ -189,3 +189,36 @@ def test_evaluate_matches_oracle():
     assert (r["crashes"], r["apples_caught"], r["steps"]) == (crashes, apples, steps)
     assert abs(r["fear"] - fear) < 1e-9
     assert not active.any() or acts.shape[0] == T
+
+
+def test_single_agent_facade_matches_oracle():
+    """custom/customenv.py surface (CustomEnv, K = 1) == the C oracle's variant 1, native RNG."""
+    from custom.customenv import CustomEnv
+    sc = S.builtin("level3_single")
+    env = CustomEnv(render=False, fear=True, seed=99)
+    orc = O.OracleEnvs(sc, 1, fear=True, fear_weight=0.0, max_steps=0, seed=99, reset=False, variant=1)
+    rng = np.random.default_rng(3)
+    episode = 0
+    obs, info = env.reset()
+    o_obs, _ = orc.reset_one(0, episode=episode)
+    assert info == {} and obs.shape == (10, 16) and obs.dtype == np.float64
+    np.testing.assert_array_equal(obs, o_obs[0].reshape(10, 16))
+    ep_r, ep_l, seen_bonus = 0.0, 0, False
+    for t in range(400):
+        a = int(rng.integers(0, 9))
+        obs, rew, term, trunc, info = env.step([a])
+        o_obs, _, out = orc.step_one(0, rl_act=np.array([a], np.int32), auto_reset=False)
+        ep_r += out.reward[0]
+        ep_l += 1
+        assert rew == [out.reward[0]] and term == [bool(out.term[0])] and trunc == bool(out.trunc[0])
+        assert info["fear"] == out.fear[0] and info["restricted"] == bool(out.restricted_bits & 1)
+        assert info["episode"] == {"r": ep_r, "l": ep_l}
+        np.testing.assert_array_equal(obs, o_obs[0].reshape(10, 16))
+        seen_bonus |= abs(rew[0] - round(rew[0])) > 1e-9
+        if term[0] or trunc:
+            episode += 1
+            obs, _ = env.reset()
+            o_obs, _ = orc.reset_one(0, episode=episode)
+            np.testing.assert_array_equal(obs, o_obs[0].reshape(10, 16))
+            ep_r, ep_l = 0.0, 0
+    assert episode > 3 and seen_bonus

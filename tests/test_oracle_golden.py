@@ -14,7 +14,7 @@ import pytest
 from oracle import oracle as O
 from marlnav import scenario as S
 
-from _replay import load, replay
+from _replay import load, load_single, replay, replay_single, single_cases
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -116,8 +116,8 @@ def test_fear_kats(group):
 
 
 class OracleStepper:
-    def __init__(self, sc, fear, weight):
-        self.o = O.OracleEnvs(sc, 1, fear=fear, fear_weight=weight, max_steps=150, reset=False)
+    def __init__(self, sc, fear, weight, variant=0):
+        self.o = O.OracleEnvs(sc, 1, fear=fear, fear_weight=weight, max_steps=150, reset=False, variant=variant)
         self.K = sc.K
 
     def reset(self, spawn):
@@ -160,3 +160,11 @@ def test_oracle_replays_reference_trajectory(fname, seed):
     st = OracleStepper(sc, bool(meta["fear"]), float(meta["fear_weight"]))
     T, err = replay(st, d, sc.K, sc.N)
     assert T > 0 and err == 0.0
+
+
+@pytest.mark.parametrize("tag", single_cases(GOLD))
+def test_oracle_replays_single_agent_trajectory(tag):
+    """custom/customenv.py (single-agent CustomEnv) trajectories from the reference, bit-exact."""
+    d = load_single(GOLD, tag)
+    st = OracleStepper(S.builtin("level3_single"), tag.startswith("fear"), 0.0, variant=1)
+    assert replay_single(st, d) == len(d["rl"])
