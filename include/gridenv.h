@@ -143,6 +143,17 @@ gw_status gw_copy_state(void *env, const gw_state *buf, int to_env, void *stream
 gw_status gw_profile(void *env, int enable);
 gw_status gw_profile_read(void *env, double out_ms[3], int64_t *n_steps);
 
+/* Responsibility.FeAR (custom/Responsibility.py:57-132: the N x N Resp matrix, every agent as
+ * actor) and FeAL (:213-303) for n world snapshots of this env's map and N, on the device:
+ *   cells [n][N] agent cells, actions [n][N] the joint action, mdr [n][N] moves de rigueur
+ *   (NULL = the scenario's per-cell MdR), in_list [n] bit a = agent a is in ActionID4Agents
+ *   (unlisted agents stay and ignore swaps, as CustomMAEnv's close_agents lists; NULL = all);
+ *   resp [n][N][N] f64, vm / va [n][N][N] ValidMoves_moveDeRigueur / _action, feal [n][N] f64,
+ *   feal_vm / feal_va [n][N] (each output but resp may be NULL).  Enqueued on stream. */
+gw_status gw_fear_matrix(void *env, int64_t n, const int32_t *cells, const int32_t *actions,
+                         const int32_t *mdr, const uint8_t *in_list, double *resp, int32_t *vm,
+                         int32_t *va, double *feal, int32_t *feal_vm, int32_t *feal_va, void *stream);
+
 /* Rows of the gw_step_out.stats buffer (one per kernel block; GW_KERNEL=defer: the world-update
  * kernel's rows then fear_v2's rows, each kernel filling the fields it owns, zeros elsewhere). */
 int64_t gw_stats_rows(void *env);

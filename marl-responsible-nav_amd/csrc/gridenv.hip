@@ -1692,6 +1692,113 @@ __global__ void __launch_bounds__(128) fear_v2(Params p) {
     block_stats<T>(p, ct, sh.red, tid, p.stats_row0 + e0 / BE);
 }
 
+// ---------------------------------------------------------------------------------------
+// Responsibility.FeAR (custom/Responsibility.py:57-132, every agent as actor) and FeAL
+// (:213-303) for n world snapshots, one 128-thread block per snapshot.  Every world update the
+// two need is one task (9 per group):  "act" groups jj = 0..N-1 (the action list unchanged,
+// agent jj's 9 actions: ValidMoves_action[.][jj] and FeAL's action count of jj), "MdR" groups
+// (ii, jj != ii) (actor ii swapped to its MdR: ValidMoves_moveDeRigueur[ii][jj]) and "FeAL"
+// groups ii (every other listed agent swapped to its MdR).  Agents outside the action list
+// stay and ignore swaps (SwapActionIDs4Agents, grid_world.py:709-726).  Valid-move bits are
+// OR-ed into LDS, counted, and mapped through exact host-computed f64 tables.
+// ---------------------------------------------------------------------------------------
+struct FmParams {
+    const uint32_t *celltab;
+    const double *tab;        // [0, 100) Resp(vm, va), [100, 200) FeAL(vm, va)
+    int HW, W;
+    uint32_t w_magic;
+    const int32_t *cells, *acts, *mdr;  // [n][N]; mdr may be null (the cells' MdR)
+    const uint8_t *in_list;             // [n] bit a: agent a in ActionID4Agents; null = all
+    double *resp;                       // [n][N][N]
+    int32_t *vm, *va;                   // [n][N][N] or null
+    double *feal;                       // [n][N] or null
+    int32_t *feal_vm, *feal_va;         // [n][N] or null
+};
+
+template <int N>
+__global__ void __launch_bounds__(128) fear_matrix_kernel(FmParams q) {
+    constexpr int T = 128, NG = N + N * (N - 1) + N;
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+    uint32_t *ctab = reinterpret_cast<uint32_t *>(dyn);
+    __shared__ int s_loc[N], s_act[N], s_mdr[N];
+    __shared__ uint32_t s_bits[NG];  // 9-bit valid masks per group
+    __shared__ uint32_t s_in;
+    const int tid = threadIdx.x;
+    const int64_t e = blockIdx.x;
+    lds_fill<T>(ctab, q.celltab, q.HW, tid);
+    for (int g = tid; g < NG; g += T) s_bits[g] = 0;
+    if (tid < N) {
+        const int c = q.cells[e * N + tid];
+        const int a = q.acts[e * N + tid];
+        s_loc[tid] = ((unsigned)c < (unsigned)q.HW) ? c : 0;
+        s_act[tid] = ((unsigned)a < (unsigned)NA) ? a : 0;
+    }
+    if (tid == 0) s_in = q.in_list ? (uint32_t)q.in_list[e] : 0xFFu;
+    __syncthreads();
+    if (tid < N) {
+        const int m = q.mdr ? q.mdr[e * N + tid] : (int)((ctab[s_loc[tid]] >> CT_MDR) & 0xFu);
+        s_mdr[tid] = ((unsigned)m < (unsigned)NA) ? m : 0;
+    }
+    __syncthreads();
+    const uint32_t in = s_in;
+    const CtabOk okv{ctab};
+    for (int t = tid; t < 9 * NG; t += T) {
+        const int g = t / 9, b = t - 9 * (t / 9);
+        int joint[N], loc[N], fin[N];
+#pragma unroll
+        for (int n = 0; n < N; ++n) {
+            loc[n] = s_loc[n];
+            joint[n] = ((in >> n) & 1u) ? s_act[n] : 0;  // defaultAction 'stay' for the unlisted
+        }
+        int affected;
+        if (g < N) {  // action list unchanged
+            affected = g;
+        } else if (g < N + N * (N - 1)) {  // actor ii -> MdR
+            const int idx = g - N, ii = idx / (N - 1), r = idx - ii * (N - 1);
+            affected = r + (r >= ii);
+#pragma unroll
+            for (int n = 0; n < N; ++n)
+                if (n == ii && ((in >> n) & 1u)) joint[n] = s_mdr[n];
+        } else {  // everybody but ii -> MdR (FeAL)
+            affected = g - N - N * (N - 1);
+#pragma unroll
+            for (int n = 0; n < N; ++n)
+                if (n != affected && ((in >> n) & 1u)) joint[n] = s_mdr[n];
+        }
+#pragma unroll
+        for (int n = 0; n < N; ++n)
+            if (n == affected && ((in >> n) & 1u)) joint[n] = b;
+        int apple[MAXN];
+#pragma unroll
+        for (int k = 0; k < MAXN; ++k) apple[k] = -1;
+        World<N> w;
+        w.init(loc, joint, q.W, q.w_magic);
+        uint32_t caught;
+        simulate<N, false>(w, okv, 0, apple, caught, fin);
+        if (!(((w.crash | w.restr) >> affected) & 1u)) atomicOr(&s_bits[g], 1u << b);
+    }
+    __syncthreads();
+    if (tid < N * N) {
+        const int ii = tid / N, jj = tid - ii * N;
+        int m = 0, a = 0;
+        double r = 0.0;
+        if (ii != jj) {
+            m = __popc(s_bits[N + ii * (N - 1) + (jj - (jj > ii))]);
+            a = __popc(s_bits[jj]);
+            r = q.tab[m * 10 + a];
+        }
+        q.resp[e * N * N + tid] = r;
+        if (q.vm) q.vm[e * N * N + tid] = m;
+        if (q.va) q.va[e * N * N + tid] = a;
+    }
+    if (tid < N) {
+        const int m = __popc(s_bits[N + N * (N - 1) + tid]), a = __popc(s_bits[tid]);
+        if (q.feal) q.feal[e * N + tid] = q.tab[100 + m * 10 + a];
+        if (q.feal_vm) q.feal_vm[e * N + tid] = m;
+        if (q.feal_va) q.feal_va[e * N + tid] = a;
+    }
+}
+
 }  // namespace gw
 
 // =========================================================================================
@@ -2015,6 +2122,15 @@ int64_t stats_rows_n(const Env *env) {
 }
 }  // namespace
 
+namespace {
+template <int N>
+hipError_t launch_fear_matrix(const Env *env, int64_t n, const gw::FmParams &q, hipStream_t s) {
+    const size_t dyn = ((size_t)env->HW * 4 + 15) / 16 * 16;
+    hipLaunchKernelGGL((gw::fear_matrix_kernel<N>), dim3((unsigned)n), dim3(128), dyn, s, q);
+    return hipGetLastError();
+}
+}  // namespace
+
 extern "C" {
 
 const char *gw_last_error(void) { return g_err.c_str(); }
@@ -2068,8 +2184,9 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
     if ((int)freec.size() < N) return fail(GW_ERR_ARG, "fewer road cells than agents");
     for (int k = 0; k < K; ++k)
         if (sc->apples[k] < 0 || sc->apples[k] >= HW) return fail(GW_ERR_ARG, "apple outside the grid");
-    // Resp table: Responsibility.py:194-198 evaluated in IEEE f64 exactly as numpy does
-    std::vector<double> resp(100);
+    // Resp table: Responsibility.py:194-198 evaluated in IEEE f64 exactly as numpy does;
+    // entries 100-199: FeAL = clip(va / (vm + EPS), -1, 1) (:282-285)
+    std::vector<double> resp(200);
     for (int vm = 0; vm < 10; ++vm)
         for (int va = 0; va < 10; ++va) {
             volatile double num = (double)vm - (double)va;
@@ -2077,6 +2194,10 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
             double r = num / den;
             r = r < -1.0 ? -1.0 : (r > 1.0 ? 1.0 : r);
             resp[vm * 10 + va] = r;
+            volatile double fnum = (double)va;
+            double f = fnum / den;
+            f = f < -1.0 ? -1.0 : (f > 1.0 ? 1.0 : f);
+            resp[100 + vm * 10 + va] = f;
         }
 
     Env *env = new (std::nothrow) Env();
@@ -2123,7 +2244,7 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
     gw_status st = GW_OK;
     if ((st = dalloc(env, &env->okmask, HW)) || (st = dalloc(env, &env->policy, HW)) ||
         (st = dalloc(env, &env->mdr, HW)) || (st = dalloc(env, &env->cdf, (size_t)env->P * 2 * 9)) ||
-        (st = dalloc(env, &env->resp, 100)) || (st = dalloc(env, &env->amask, HW)) ||
+        (st = dalloc(env, &env->resp, 200)) || (st = dalloc(env, &env->amask, HW)) ||
         (st = dalloc(env, &env->free_cells, freec.size())) || (st = dalloc(env, &env->base, HW)) ||
         (st = dalloc(env, &env->pos, (size_t)N * E)) || (st = dalloc(env, &env->t, E)) ||
         (st = dalloc(env, &env->prev, (size_t)K * E)) || (st = dalloc(env, &env->flags, E)) ||
@@ -2138,7 +2259,7 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
     CP(env->policy, pol.data(), HW);
     CP(env->mdr, mdr.data(), HW);
     CP(env->cdf, sc->policy_cdf, sizeof(double) * env->P * 2 * 9);
-    CP(env->resp, resp.data(), sizeof(double) * 100);
+    CP(env->resp, resp.data(), sizeof(double) * 200);
     CP(env->amask, am.data(), sizeof(uint16_t) * HW);
     CP(env->free_cells, freec.data(), sizeof(int32_t) * freec.size());
     CP(env->base, base.data(), sizeof(float) * HW);
@@ -2352,6 +2473,45 @@ int64_t gw_stats_rows(void *handle) {
         case 8: return stats_rows_n<8>(env);
     }
     return -1;
+}
+
+gw_status gw_fear_matrix(void *handle, int64_t n, const int32_t *cells, const int32_t *actions,
+                         const int32_t *mdr, const uint8_t *in_list, double *resp, int32_t *vm, int32_t *va,
+                         double *feal, int32_t *feal_vm, int32_t *feal_va, void *stream) {
+    Env *env = static_cast<Env *>(handle);
+    if (!env || !cells || !actions || !resp) return fail(GW_ERR_ARG, "null argument");
+    if (n < 0 || n > 0x7FFFFFFF) return fail(GW_ERR_ARG, "n out of range");
+    if (n == 0) return GW_OK;
+    gw::FmParams q;
+    q.celltab = env->celltab;
+    q.tab = env->resp;
+    q.HW = env->HW;
+    q.W = env->W;
+    q.w_magic = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)env->W - 1) / (uint64_t)env->W);
+    q.cells = cells;
+    q.acts = actions;
+    q.mdr = mdr;
+    q.in_list = in_list;
+    q.resp = resp;
+    q.vm = vm;
+    q.va = va;
+    q.feal = feal;
+    q.feal_vm = feal_vm;
+    q.feal_va = feal_va;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipError_t e = hipErrorInvalidValue;
+    switch (env->N) {
+        case 1: return fail(GW_ERR_ARG, "FeAR needs N >= 2");
+        case 2: e = launch_fear_matrix<2>(env, n, q, s); break;
+        case 3: e = launch_fear_matrix<3>(env, n, q, s); break;
+        case 4: e = launch_fear_matrix<4>(env, n, q, s); break;
+        case 5: e = launch_fear_matrix<5>(env, n, q, s); break;
+        case 6: e = launch_fear_matrix<6>(env, n, q, s); break;
+        case 7: e = launch_fear_matrix<7>(env, n, q, s); break;
+        case 8: e = launch_fear_matrix<8>(env, n, q, s); break;
+    }
+    HIP_TRY(e);
+    return GW_OK;
 }
 
 gw_status gw_dims(void *handle, int64_t out[5]) {

@@ -104,7 +104,7 @@ class GwState(C.Structure):
 
 
 EXPORTS = ["gw_create", "gw_reset", "gw_step", "gw_state_view", "gw_copy_state", "gw_profile",
-           "gw_profile_read", "gw_stats_rows", "gw_dims", "gw_last_error", "gw_destroy"]
+           "gw_profile_read", "gw_stats_rows", "gw_dims", "gw_last_error", "gw_destroy", "gw_fear_matrix"]
 
 
 def _declare(L):
@@ -129,6 +129,8 @@ def _declare(L):
     L.gw_dims.restype = C.c_int
     L.gw_last_error.argtypes = []
     L.gw_last_error.restype = C.c_char_p
+    L.gw_fear_matrix.argtypes = [p, C.c_int64] + [p] * 11
+    L.gw_fear_matrix.restype = C.c_int
     L.gw_destroy.argtypes = [p]
     L.gw_destroy.restype = None
     return L

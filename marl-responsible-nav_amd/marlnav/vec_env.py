@@ -195,6 +195,32 @@ class VecGridEnv:
         with torch.cuda.device(self.device):
             _lib.check(self.lib.gw_copy_state(self.handle, C.byref(gs), 1, self._stream()), "gw_copy_state")
 
+    def fear_matrix(self, cells, actions, mdr=None, in_list=None) -> dict:
+        """Responsibility.FeAR (full N x N matrix) and FeAL for n world snapshots of this env's map
+        (gw_fear_matrix): cells / actions [n, N], mdr [n, N] or None (per-cell MdR), in_list [n]
+        N-bit masks of the agents in ActionID4Agents or None (all).  -> device tensors resp
+        [n, N, N] f64, vm, va [n, N, N] i32, feal [n, N] f64, feal_vm, feal_va [n, N] i32."""
+        cells = torch.as_tensor(cells, device=self.device).to(torch.int32).contiguous()
+        n, N = cells.shape[0], self.N
+        assert cells.shape == (n, N)
+        acts = self._as_i32(actions, (n, N))
+        mdr = self._as_i32(mdr, (n, N))
+        if in_list is not None:
+            in_list = torch.as_tensor(in_list, device=self.device).to(torch.uint8).contiguous().reshape(n)
+        dev = self.device
+        out = dict(resp=torch.empty((n, N, N), dtype=torch.float64, device=dev),
+                   vm=torch.empty((n, N, N), dtype=torch.int32, device=dev),
+                   va=torch.empty((n, N, N), dtype=torch.int32, device=dev),
+                   feal=torch.empty((n, N), dtype=torch.float64, device=dev),
+                   feal_vm=torch.empty((n, N), dtype=torch.int32, device=dev),
+                   feal_va=torch.empty((n, N), dtype=torch.int32, device=dev))
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.gw_fear_matrix(self.handle, n, _ptr(cells), _ptr(acts), _ptr(mdr), _ptr(in_list),
+                                               *[_ptr(out[k]) for k in ("resp", "vm", "va", "feal", "feal_vm",
+                                                                         "feal_va")], self._stream()),
+                       "gw_fear_matrix")
+        return out
+
     def profile(self, enable: bool = True):
         """Record HIP events around each gw_step kernel (see gw_profile)."""
         _lib.check(self.lib.gw_profile(self.handle, int(enable)), "gw_profile")

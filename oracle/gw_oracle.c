@@ -269,6 +269,64 @@ double orc_fear_one_actor(int H, int W, const uint8_t *region, int N, const int3
     return orc_np_sum(resp, N * N); /* np.sum(FeAR_vals), ma_customenv.py:252 */
 }
 
+/* Responsibility.FeAR (custom/Responsibility.py:57-132): every agent as actor.  resp, vm, va
+ * are [N*N] (diagonal 0). */
+void orc_fear_matrix(int H, int W, const uint8_t *region, int N, const int32_t *loc, int list_len,
+                     const int32_t *list_ids, const int32_t *list_acts, const int32_t *mdr_acts,
+                     double *resp, int32_t *vm, int32_t *va) {
+    int32_t action_inputs[ORC_MAX_N]; /* default Stay :63-65 */
+    for (int n = 0; n < N; ++n) action_inputs[n] = 0;
+    for (int i = 0; i < list_len; ++i) action_inputs[list_ids[i]] = list_acts[i];
+    for (int n = 0; n < N * N; ++n) {
+        resp[n] = 0.0;
+        vm[n] = va[n] = 0;
+    }
+    for (int ii = 0; ii < N; ++ii) {     /* actors :84 */
+        for (int jj = 0; jj < N; ++jj) { /* affected :85 */
+            if (jj == ii) continue;
+            int32_t a_mdr[ORC_MAX_N], a_act[ORC_MAX_N];
+            memcpy(a_mdr, list_acts, sizeof(int32_t) * list_len);
+            memcpy(a_act, list_acts, sizeof(int32_t) * list_len);
+            swap_action(list_len, list_ids, a_mdr, ii, mdr_acts[ii]);      /* :90-95 */
+            swap_action(list_len, list_ids, a_act, ii, action_inputs[ii]); /* :98-101 */
+            int32_t m = count_valid_moves(H, W, region, N, loc, list_len, list_ids, a_mdr, jj);
+            int32_t a = count_valid_moves(H, W, region, N, loc, list_len, list_ids, a_act, jj);
+            vm[ii * N + jj] = m;
+            va[ii * N + jj] = a;
+            double r = ((double)m - (double)a) / ((double)m + FEAR_EPS); /* :117-118 */
+            if (r < -1.0) r = -1.0;                                       /* np.clip :121 */
+            if (r > 1.0) r = 1.0;
+            resp[ii * N + jj] = r;
+        }
+    }
+}
+
+/* Responsibility.FeAL (custom/Responsibility.py:213-303): for each agent ii, the valid moves it
+ * keeps when all OTHER listed agents take their MdR vs their actions.  feal, vm, va are [N]. */
+void orc_feal(int H, int W, const uint8_t *region, int N, const int32_t *loc, int list_len,
+              const int32_t *list_ids, const int32_t *list_acts, const int32_t *mdr_acts, double *feal,
+              int32_t *vm, int32_t *va) {
+    int32_t action_inputs[ORC_MAX_N]; /* default Stay :221-223 */
+    for (int n = 0; n < N; ++n) action_inputs[n] = 0;
+    for (int i = 0; i < list_len; ++i) action_inputs[list_ids[i]] = list_acts[i];
+    for (int ii = 0; ii < N; ++ii) { /* affected :242 */
+        int32_t a_mdr[ORC_MAX_N], a_act[ORC_MAX_N];
+        memcpy(a_mdr, list_acts, sizeof(int32_t) * list_len);
+        memcpy(a_act, list_acts, sizeof(int32_t) * list_len);
+        for (int o = 0; o < N; ++o) { /* every agent but ii swapped :244-270 */
+            if (o == ii) continue;
+            swap_action(list_len, list_ids, a_mdr, o, mdr_acts[o]);
+            swap_action(list_len, list_ids, a_act, o, action_inputs[o]);
+        }
+        vm[ii] = count_valid_moves(H, W, region, N, loc, list_len, list_ids, a_mdr, ii);
+        va[ii] = count_valid_moves(H, W, region, N, loc, list_len, list_ids, a_act, ii);
+        double f = (double)va[ii] / ((double)vm[ii] + FEAR_EPS); /* :282-283 */
+        if (f < -1.0) f = -1.0;                                   /* np.clip :285 */
+        if (f > 1.0) f = 1.0;
+        feal[ii] = f;
+    }
+}
+
 /* ---------------------------------------------------------------------------------- */
 /* CustomMAEnv  (custom/ma_customenv.py)                                                */
 /* ---------------------------------------------------------------------------------- */

@@ -106,6 +106,17 @@ double orc_fear_one_actor(int H, int W, const uint8_t *region, int N, const int3
                           const int32_t *mdr_acts, int actor, double *resp, int32_t *vm,
                           int32_t *va);
 
+/* Responsibility.FeAR (custom/Responsibility.py:57-132): the full N x N Resp matrix with every
+ * agent as actor, for the action list (list_ids, list_acts); resp/vm/va are [N*N]. */
+void orc_fear_matrix(int H, int W, const uint8_t *region, int N, const int32_t *loc, int list_len,
+                     const int32_t *list_ids, const int32_t *list_acts, const int32_t *mdr_acts,
+                     double *resp, int32_t *vm, int32_t *va);
+
+/* Responsibility.FeAL (custom/Responsibility.py:213-303); feal/vm/va are [N]. */
+void orc_feal(int H, int W, const uint8_t *region, int N, const int32_t *loc, int list_len,
+              const int32_t *list_ids, const int32_t *list_acts, const int32_t *mdr_acts, double *feal,
+              int32_t *vm, int32_t *va);
+
 /* get_action_mask (custom/ma_customenv.py:467-506) as a 9-bit mask. */
 uint16_t orc_action_mask(int H, int W, const uint8_t *region, int cell);
 

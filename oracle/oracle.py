@@ -66,6 +66,10 @@ def lib():
         L.orc_update_world.restype = C.c_int
         L.orc_fear_one_actor.argtypes = [C.c_int, C.c_int, p, C.c_int, p, C.c_int, p, p, p, C.c_int, p, p, p]
         L.orc_fear_one_actor.restype = C.c_double
+        L.orc_fear_matrix.argtypes = [C.c_int, C.c_int, p, C.c_int, p, C.c_int, p, p, p, p, p, p]
+        L.orc_fear_matrix.restype = None
+        L.orc_feal.argtypes = [C.c_int, C.c_int, p, C.c_int, p, C.c_int, p, p, p, p, p, p]
+        L.orc_feal.restype = None
         L.orc_action_mask.argtypes = [C.c_int, C.c_int, p, C.c_int]
         L.orc_action_mask.restype = C.c_uint16
         L.orc_env_reset.argtypes = [p, C.c_int64, p, p, p, p]
@@ -196,3 +200,22 @@ class OracleEnvs:
     def positions(self) -> np.ndarray:
         N = self.sc.N
         return np.array([[self.envs[e].pos[n] for n in range(N)] for e in range(self.E)], np.int32)
+
+
+def fear_matrix(H, W, region, loc, acts, mdr, in_list=None):
+    """Responsibility.FeAR + FeAL of one world snapshot (C restatement).  in_list: which agents
+    are in ActionID4Agents (the others take 'stay' and ignore swaps); None = all.
+    -> dict resp [N,N], vm, va [N,N], feal [N], feal_vm, feal_va [N]."""
+    N = len(loc)
+    region = np.ascontiguousarray(region, np.uint8).reshape(-1)
+    loc = np.ascontiguousarray(loc, np.int32)
+    mdr = np.ascontiguousarray(mdr, np.int32)
+    ids = np.array([n for n in range(N) if in_list is None or in_list[n]], np.int32)
+    la = np.ascontiguousarray(np.asarray(acts, np.int32)[ids])
+    out = dict(resp=np.zeros((N, N)), vm=np.zeros((N, N), np.int32), va=np.zeros((N, N), np.int32),
+               feal=np.zeros(N), feal_vm=np.zeros(N, np.int32), feal_va=np.zeros(N, np.int32))
+    lib().orc_fear_matrix(H, W, _ptr(region), N, _ptr(loc), len(ids), _ptr(ids), _ptr(la), _ptr(mdr),
+                          _ptr(out["resp"]), _ptr(out["vm"]), _ptr(out["va"]))
+    lib().orc_feal(H, W, _ptr(region), N, _ptr(loc), len(ids), _ptr(ids), _ptr(la), _ptr(mdr),
+                   _ptr(out["feal"]), _ptr(out["feal_vm"]), _ptr(out["feal_va"]))
+    return out

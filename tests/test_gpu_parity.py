@@ -217,3 +217,55 @@ def test_full_size_properties(name, E, kernel_path):
                                       np.array([outs[e].ep_return for e in range(sl)]))
         np.testing.assert_array_equal(o[:, sl0:sl0 + sl].cpu().numpy(), obs_o)
     env.close()
+
+
+def _map_scenario(region2d, N):
+    """A compiled scenario of a golden map (single policy, MdR stay) with N world agents."""
+    H, W = region2d.shape
+    road = np.argwhere(region2d == 1)[0]
+    full = {"slicex": [0, H, 0], "slicey": [0, W, 0]}
+    return S.compile_scenario({
+        "AgentLocations": [], "Map": {"Region": region2d.tolist(), "Walls": [], "OneWays": []},
+        "MdRs": {"00": dict(mdr=0, **full)}, "N_Agents": N, "N_Intelligent": 1,
+        "Policies": {"00": dict(directionWeights=[1, 1, 1, 1], stepWeights=[1, 1, 0], **full)},
+        "SpecificAction4Agents": [], "defaultAction": "random", "Apples": {"apple_0": [int(road[0]), int(road[1])]}})
+
+
+@pytest.mark.parametrize("name", ["level3", "grid32", "open6_n8", "open6_n3", "open5x8_n5"])
+def test_gpu_fear_matrix_and_feal_match_reference(name):
+    """gw_fear_matrix == Responsibility.FeAR / FeAL golden vectors from the reference, every case
+    bit-exact, all cases of a map in one launch."""
+    z = np.load(os.path.join(GOLD, "fear_matrix.npz"))
+    d = {k.split("/", 1)[1]: z[k] for k in z.files if k.startswith(name + "/")}
+    N = d["loc"].shape[1]
+    env = VecGridEnv(_map_scenario(d["region"], N), num_envs=1, fear=True)
+    bits = (d["in_list"].astype(np.int64) << np.arange(N)).sum(1)
+    o = env.fear_matrix(d["loc"], d["act"], d["mdr"], bits)
+    torch.cuda.synchronize()
+    for k in ("vm", "va", "resp", "feal_vm", "feal_va", "feal"):
+        np.testing.assert_array_equal(o[k].cpu().numpy(), d[k], err_msg=f"{name} {k}")
+    env.close()
+
+
+def test_gpu_fear_matrix_row_equals_step_fear():
+    """Row k of the full matrix for the env's close-agent list reproduces the per-step FeAR of
+    RL agent k (ma_customenv.py:247-252), on live states of a native-RNG rollout."""
+    sc = S.builtin("grid32")
+    E = 1024
+    env = VecGridEnv(sc, num_envs=E, fear=True, seed=4, debug=True)
+    env.reset()
+    for _ in range(5):
+        pos = env.positions()
+        r = env.step()
+        torch.cuda.synchronize()
+        act, mdr = r.actions.clone(), r.mdr.clone()
+        for k in range(sc.K):
+            rr, cc = pos // sc.W, pos % sc.W
+            dist = (rr - rr[:, k:k + 1]).abs() + (cc - cc[:, k:k + 1]).abs()
+            in_list = ((dist <= 5).to(torch.int64) << torch.arange(sc.N, device=pos.device)).sum(1)
+            o = env.fear_matrix(pos, act, mdr, in_list)
+            row = o["resp"][:, k, :].cpu().numpy()
+            want = r.fear[:, k].cpu().numpy()
+            got = np.array([np.sum(np.pad(row[e][None], ((k, sc.N - 1 - k), (0, 0)))) for e in range(E)])
+            np.testing.assert_array_equal(got, want)
+    env.close()

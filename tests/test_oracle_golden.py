@@ -168,3 +168,24 @@ def test_oracle_replays_single_agent_trajectory(tag):
     d = load_single(GOLD, tag)
     st = OracleStepper(S.builtin("level3_single"), tag.startswith("fear"), 0.0, variant=1)
     assert replay_single(st, d) == len(d["rl"])
+
+
+def _fm_cases():
+    z = np.load(os.path.join(GOLD, "fear_matrix.npz"))
+    return sorted({k.split("/", 1)[0] for k in z.files})
+
+
+@pytest.mark.parametrize("name", _fm_cases())
+def test_oracle_fear_matrix_and_feal_match_reference(name):
+    """Responsibility.FeAR (full matrix) and FeAL golden vectors from the reference, bit-exact."""
+    z = np.load(os.path.join(GOLD, "fear_matrix.npz"))
+    d = {k.split("/", 1)[1]: z[k] for k in z.files if k.startswith(name + "/")}
+    H, W = d["region"].shape
+    for i in range(len(d["loc"])):
+        o = O.fear_matrix(H, W, d["region"], d["loc"][i], d["act"][i], d["mdr"][i], d["in_list"][i].astype(bool))
+        np.testing.assert_array_equal(o["vm"], d["vm"][i], err_msg=f"{name} case {i} vm")
+        np.testing.assert_array_equal(o["va"], d["va"][i], err_msg=f"{name} case {i} va")
+        np.testing.assert_array_equal(o["resp"], d["resp"][i], err_msg=f"{name} case {i} resp")
+        np.testing.assert_array_equal(o["feal_vm"], d["feal_vm"][i], err_msg=f"{name} case {i} feal vm")
+        np.testing.assert_array_equal(o["feal_va"], d["feal_va"][i], err_msg=f"{name} case {i} feal va")
+        np.testing.assert_array_equal(o["feal"], d["feal"][i], err_msg=f"{name} case {i} feal")
