@@ -137,11 +137,15 @@ def main():
     stream = torch.cuda.current_stream()
     stats_acc = torch.zeros_like(env.out["stats"][0])
 
+    from marlnav.parallel import StatsReducer
+    reducer = StatsReducer(env.out["stats"].shape[1], env.device) if world > 1 else None
+
     def one_step(i):
         r = env.step()
-        if world > 1:
-            # per-step RCCL reduction of the episode-return statistics across the shards
-            dist.all_reduce(r.stats, op=dist.ReduceOp.SUM)
+        if reducer is not None:
+            # per-step RCCL all-reduce of the episode statistics across the shards: rows summed
+            # locally first (64 B message), asynchronous, waited for one step later
+            reducer.push(r.stats)
         return r
 
     if cfg.get("rollout"):  # c5: actor -> env -> replay (+ optional MADDPG updates) per step

@@ -163,6 +163,14 @@ def test_many_agents_k_gt_2_matches_oracle(kernel_path):
     _compare_native(sc, 1024, False, 40)
 
 
+@pytest.mark.parametrize("E", [1, 77, 1000])
+def test_ragged_env_counts_match_oracle(E, kernel_path):
+    """E not a multiple of any block size (partial last blocks of step_v2, fear_v2, obs_kernel)
+    and a non-zero global env offset."""
+    _compare_native(S.builtin("grid32"), E, True, 12, offset=12345)
+    _compare_native(S.builtin("level3"), E, False, 12, offset=7)
+
+
 def test_sharding_is_invariant():
     """Two shards (env_offset 0 and E/2) reproduce the single-device run env for env."""
     sc = S.builtin("grid32")
