@@ -106,8 +106,10 @@ __device__ __forceinline__ uint4 philox(uint32_t c0, uint32_t c1, uint32_t c2, u
             k0 += 0x9E3779B9u;
             k1 += 0xBB67AE85u;
         }
-        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
-        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+        // one 32x32->64 multiply per product (v_mad_u64_u32) instead of mul_lo + mul_hi
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+        const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
         const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
         c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
     }
@@ -1830,15 +1832,16 @@ struct Env {
     bool initialized = false;
     int mode = 3;        // GW_KERNEL: 0 "v1" (first kernels), 1 "split" step_v2 (FeAR inline) + obs_kernel,
                          // 2 "fused", 3 "defer" (default; FeAR on: step_v2 <DEFER>, then fear_v2 || obs_kernel)
-    int obs_be = 2;      // GW_OBS_BE: envs per obs_kernel block (2 measured best, 32x32 and 64x64)
+    int obs_be = 2;      // GW_OBS_BE: envs per obs_kernel block (default: see gw_create)
     bool obs_nt = true;  // GW_OBS_NT=0: plain instead of nontemporal obs stores
     uint32_t *celltab = nullptr;
     uint32_t *roadbits = nullptr;
-    int defer_order = 3;            // GW_DEFER (A/B): 0 fear then obs on one stream, 1 fear on aux first,
-                                    // 2 obs first then fear on aux, 3 (default) as 1, aux stream high priority
+    int defer_order = 3;            // GW_DEFER (A/B): 0 fear then obs on one stream; 1 fear on a second
+                                    // stream || obs; 3 (default) as 1 with the second stream at high priority
     bool fear_wide = false;         // GW_FEAR_BE=wide: fear_v2 with 2x envs per block (A/B)
     int chunks = 1;                 // GW_CHUNKS: step/obs pipeline depth (split path; 1 = off, measured best)
     hipStream_t aux = nullptr;      // second stream of the pipeline (created on first use)
+    hipStream_t aux2 = nullptr;     // third stream: obs_kernel of the chunked defer pipeline
     std::vector<hipEvent_t> sync_ev;  // fork/chunk/join events (timing disabled)
     // tables
     uint8_t *okmask = nullptr, *policy = nullptr, *mdr = nullptr;
@@ -1877,6 +1880,7 @@ gw_status ensure_aux(Env *env, int n) {
         HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         env->sync_ev.push_back(e);
     }
+    if (!env->aux2) HIP_TRY(hipStreamCreateWithFlags(&env->aux2, hipStreamNonBlocking));
     return GW_OK;
 }
 
@@ -2223,9 +2227,15 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
         if (kv && std::strcmp(kv, "fused") == 0 && HW % 4 == 0) env->mode = 2;
         if (kv && std::strcmp(kv, "defer") == 0) env->mode = 3;
         const char *dv = std::getenv("GW_DEFER");
-        if (dv) env->defer_order = std::max(0, std::min(3, std::atoi(dv)));
+        if (dv) env->defer_order = std::atoi(dv) == 0 ? 0 : (std::atoi(dv) == 3 ? 3 : 1);
         const char *fb = std::getenv("GW_FEAR_BE");
         if (fb && std::strcmp(fb, "wide") == 0) env->fear_wide = true;
+        // obs_kernel block size (tools/gpu_ab2.sh): 4 float4 stores per thread when the writer
+        // runs alone (32x32 K=2 -> 2 envs, 64x64 -> 1), 8 while fear_v2 shares the CUs (32x32 ->
+        // 4 envs: 2.5 % faster step at C3)
+        int be_def = std::max(1, 4096 / std::max(1, K * HW));
+        if (env->mode == 3 && env->fear) be_def *= 2;
+        env->obs_be = std::max(1, std::min(gw::OBS_BE, be_def));
         const char *be = std::getenv("GW_OBS_BE");
         if (be) env->obs_be = std::max(1, std::min(gw::OBS_BE, std::atoi(be)));
         const char *nt = std::getenv("GW_OBS_NT");
@@ -2320,8 +2330,10 @@ gw_status gw_step(void *handle, const int32_t *rl_actions, const int32_t *script
     };
     // chunk size: a multiple of every block size in play (v2 BE, obs_be) so blocks never straddle
     const int64_t unit = 128;  // multiple of every step_v2 BE (<= 128) and obs_be (<= 8)
-    const int nch = (env->mode == 1 && want_obs && env->chunks > 1 && env->E >= unit * env->chunks) ? env->chunks : 1;
-    if (env->mode == 3 && env->fear) {
+    const bool defer = env->mode == 3 && env->fear;
+    const int nch = ((env->mode == 1 || defer) && want_obs && env->chunks > 1 && env->E >= unit * env->chunks)
+                        ? env->chunks : 1;
+    if (defer && (nch == 1 || env->defer_order == 0)) {
         // world update; then fear_v2 on the aux stream || obs_kernel on s; join
         size_t b;
         GW_TRY(span_begin(s, b));
@@ -2340,22 +2352,45 @@ gw_status gw_step(void *handle, const int32_t *rl_actions, const int32_t *script
         }
         GW_TRY(ensure_aux(env, 2));
         HIP_TRY(hipEventRecord(env->sync_ev[0], s));  // fork after the world update
-        if (env->defer_order == 2) {
-            GW_TRY(span_begin(s, b));
-            HIP_TRY(launch_obs(env, p, p.out.obs, p.out.final_obs, s));
-            GW_TRY(span_end(s, b, 1));
-        }
         HIP_TRY(hipStreamWaitEvent(env->aux, env->sync_ev[0], 0));
         GW_TRY(span_begin(env->aux, b));
         HIP_TRY(dispatch_fear(env, p, env->aux));
         GW_TRY(span_end(env->aux, b, 2));
-        if (env->defer_order != 2) {
-            GW_TRY(span_begin(s, b));
-            HIP_TRY(launch_obs(env, p, p.out.obs, p.out.final_obs, s));
-            GW_TRY(span_end(s, b, 1));
-        }
+        GW_TRY(span_begin(s, b));
+        HIP_TRY(launch_obs(env, p, p.out.obs, p.out.final_obs, s));
+        GW_TRY(span_end(s, b, 1));
         HIP_TRY(hipEventRecord(env->sync_ev[1], env->aux));
         HIP_TRY(hipStreamWaitEvent(s, env->sync_ev[1], 0));
+        return GW_OK;
+    }
+    if (defer) {
+        // env chunks: world update of chunk c on s, then its fear_v2 (aux) and obs_kernel (aux2)
+        // while s moves on to chunk c + 1; s joins both streams at the end
+        GW_TRY(ensure_aux(env, nch + 2));
+        const int64_t per = ((env->E / nch + unit - 1) / unit) * unit;
+        for (int c = 0; c < nch; ++c) {
+            gw::Params q = p;
+            q.e_begin = std::min<int64_t>(env->E, c * per);
+            q.e_end = std::min<int64_t>(env->E, (c + 1) * per);
+            if (q.e_begin >= q.e_end) break;
+            size_t b;
+            GW_TRY(span_begin(s, b));
+            HIP_TRY(dispatch_step(env, q, s));
+            GW_TRY(span_end(s, b, 0));
+            HIP_TRY(hipEventRecord(env->sync_ev[c], s));
+            HIP_TRY(hipStreamWaitEvent(env->aux, env->sync_ev[c], 0));
+            HIP_TRY(hipStreamWaitEvent(env->aux2, env->sync_ev[c], 0));
+            GW_TRY(span_begin(env->aux, b));
+            HIP_TRY(dispatch_fear(env, q, env->aux));
+            GW_TRY(span_end(env->aux, b, 2));
+            GW_TRY(span_begin(env->aux2, b));
+            HIP_TRY(launch_obs(env, q, q.out.obs, q.out.final_obs, env->aux2));
+            GW_TRY(span_end(env->aux2, b, 1));
+        }
+        HIP_TRY(hipEventRecord(env->sync_ev[nch], env->aux));
+        HIP_TRY(hipEventRecord(env->sync_ev[nch + 1], env->aux2));
+        HIP_TRY(hipStreamWaitEvent(s, env->sync_ev[nch], 0));
+        HIP_TRY(hipStreamWaitEvent(s, env->sync_ev[nch + 1], 0));
         return GW_OK;
     }
     if (nch == 1) {
@@ -2529,6 +2564,7 @@ void gw_destroy(void *handle) {
     for (hipEvent_t e : env->ev_pool) (void)hipEventDestroy(e);
     for (hipEvent_t e : env->sync_ev) (void)hipEventDestroy(e);
     if (env->aux) (void)hipStreamDestroy(env->aux);
+    if (env->aux2) (void)hipStreamDestroy(env->aux2);
     for (void *p : env->allocs) (void)hipFree(p);
     delete env;
 }
