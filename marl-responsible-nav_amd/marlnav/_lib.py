@@ -19,7 +19,8 @@ REPO_ROOT = os.path.dirname(PKG_ROOT)
 CSRC = os.path.join(PKG_ROOT, "csrc")
 INCLUDE = os.path.join(REPO_ROOT, "include")
 LIB_PATH = os.path.join(CSRC, "libgridenv.so")
-SOURCES = [os.path.join(CSRC, "gridenv.hip"), os.path.join(INCLUDE, "gridenv.h")]
+HIP_SOURCES = [os.path.join(CSRC, "gridenv.hip"), os.path.join(CSRC, "learner_ops.hip")]
+SOURCES = HIP_SOURCES + [os.path.join(INCLUDE, "gridenv.h"), os.path.join(INCLUDE, "learner_ops.h")]
 ARCH = os.environ.get("MARLNAV_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
@@ -60,7 +61,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_build():
         return LIB_PATH
     tmp = LIB_PATH + f".tmp{os.getpid()}"
-    cmd = [HIPCC, *HIPCC_FLAGS, f"-I{INCLUDE}", SOURCES[0], "-o", tmp]
+    cmd = [HIPCC, *HIPCC_FLAGS, f"-I{INCLUDE}", *HIP_SOURCES, "-o", tmp]
     if verbose:
         print(" ".join(cmd))
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -104,7 +105,8 @@ class GwState(C.Structure):
 
 
 EXPORTS = ["gw_create", "gw_reset", "gw_step", "gw_state_view", "gw_copy_state", "gw_profile",
-           "gw_profile_read", "gw_stats_rows", "gw_dims", "gw_last_error", "gw_destroy", "gw_fear_matrix"]
+           "gw_profile_read", "gw_stats_rows", "gw_dims", "gw_last_error", "gw_destroy", "gw_fear_matrix",
+           "gw_adam_step", "gw_soft_update"]
 
 
 def _declare(L):
@@ -131,6 +133,10 @@ def _declare(L):
     L.gw_last_error.restype = C.c_char_p
     L.gw_fear_matrix.argtypes = [p, C.c_int64] + [p] * 11
     L.gw_fear_matrix.restype = C.c_int
+    L.gw_adam_step.argtypes = [p, p, p, p, p, C.c_int64, C.c_float, C.c_float, C.c_float, C.c_float, p]
+    L.gw_adam_step.restype = C.c_int
+    L.gw_soft_update.argtypes = [p, p, C.c_int64, C.c_float, p]
+    L.gw_soft_update.restype = C.c_int
     L.gw_destroy.argtypes = [p]
     L.gw_destroy.restype = None
     return L

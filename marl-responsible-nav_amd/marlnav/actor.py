@@ -37,60 +37,56 @@ class StackedMLPActors(nn.Module):
     """K independent MLPs evaluated together: x [K, E, D] -> [K, E, out] (out = 9 logits for an
     actor, 1 for a critic).
 
-    All parameters live in ONE flat tensor (``flat``); ``weights[i]`` [K, in, out], ``biases[i]``
-    [K, 1, out], ``ln_w[i]`` / ``ln_b[i]`` [K, 1, h] are views into it.  A fused Adam step and the
-    soft target update are then one kernel each per network instead of one per tensor, which is
-    what bounds a batch-128 MADDPG update (launch latency, not FLOPs)."""
+    The per-layer parameters ``weights[i]`` [K, in, out], ``biases[i]`` [K, 1, out], ``ln_w[i]`` /
+    ``ln_b[i]`` [K, 1, h] are leaf Parameters that are views of ONE flat buffer, and
+    ``flat_params()`` returns that buffer as a Parameter whose ``.grad`` is a flat gradient buffer
+    the per-layer gradients accumulate into (in place).  An optimizer over the flat Parameter
+    then takes one fused step per network, and the soft target update is one kernel: what
+    bounds a batch-128 MADDPG update is launch count, not FLOPs."""
 
     def __init__(self, K: int, in_dim: int, hidden=(128, 128), n_actions: int = N_ACTIONS, layer_norm: bool = True,
                  device=None, dtype=torch.float32, seed: int = 0):
         super().__init__()
         gen = torch.Generator().manual_seed(seed)
         dims = [in_dim, *hidden, n_actions]
-        parts, self._shapes = [], []
+        parts, shapes = [], []
         for a, b in zip(dims[:-1], dims[1:]):
             w, bb = _init_linear(K, a, b, gen)
             parts += [w, bb]
-            self._shapes += [("w", w.shape), ("b", bb.shape)]
+            shapes += [("w", w.shape), ("b", bb.shape)]
         for h in hidden:
             parts += [torch.ones((K, 1, h)), torch.zeros((K, 1, h))]
-            self._shapes += [("lw", (K, 1, h)), ("lb", (K, 1, h))]
-        self.flat = nn.Parameter(torch.cat([t.reshape(-1) for t in parts]).to(device=device, dtype=dtype))
+            shapes += [("lw", (K, 1, h)), ("lb", (K, 1, h))]
+        flat = torch.cat([t.reshape(-1) for t in parts]).to(device=device, dtype=dtype)
+        # not registered: parameters() yields the per-layer views only (no double counting)
+        object.__setattr__(self, "_flat", nn.Parameter(flat))
+        self._flat.grad = torch.zeros_like(flat)
+        lists = {"w": [], "b": [], "lw": [], "lb": []}
+        off = 0
+        for kind, shape in shapes:
+            n = math.prod(shape)
+            p = nn.Parameter(flat[off:off + n].view(shape))
+            p.grad = self._flat.grad[off:off + n].view(shape)
+            lists[kind].append(p)
+            off += n
+        self.weights = nn.ParameterList(lists["w"])
+        self.biases = nn.ParameterList(lists["b"])
+        self.ln_w = nn.ParameterList(lists["lw"])
+        self.ln_b = nn.ParameterList(lists["lb"])
         self.layer_norm = layer_norm
         self.K, self.in_dim, self.n_layers = K, in_dim, len(dims) - 1
 
-    def _views(self):
-        out, off = {"w": [], "b": [], "lw": [], "lb": []}, 0
-        for kind, shape in self._shapes:
-            n = math.prod(shape)
-            out[kind].append(self.flat[off:off + n].view(shape))
-            off += n
-        return out
-
-    @property
-    def weights(self):
-        return self._views()["w"]
-
-    @property
-    def biases(self):
-        return self._views()["b"]
-
-    @property
-    def ln_w(self):
-        return self._views()["lw"]
-
-    @property
-    def ln_b(self):
-        return self._views()["lb"]
+    def flat_params(self) -> nn.Parameter:
+        """The single flat Parameter (shares storage with every layer; .grad = flat gradients)."""
+        return self._flat
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        v = self._views()
         n = self.n_layers
         for i in range(n):
-            x = torch.baddbmm(v["b"][i], x, v["w"][i])
+            x = torch.baddbmm(self.biases[i], x, self.weights[i])
             if i < n - 1:
                 if self.layer_norm:  # nn.LayerNorm(h), eps 1e-5, per-agent affine
-                    x = torch.addcmul(v["lb"][i], F.layer_norm(x, (x.shape[-1],)), v["lw"][i])
+                    x = torch.addcmul(self.ln_b[i], F.layer_norm(x, (x.shape[-1],)), self.ln_w[i])
                 x = F.relu(x)
         return x
 

@@ -32,6 +32,7 @@ import copy
 import torch
 import torch.nn.functional as F
 
+from . import _lib
 from .actor import N_ACTIONS, MultiAgentActors, StackedMLPActors
 
 
@@ -41,6 +42,41 @@ def gumbel_softmax(logits: torch.Tensor, u: torch.Tensor | None = None, tau: flo
     if u is None:
         u = torch.rand(logits.shape, device=logits.device, dtype=logits.dtype, generator=generator)
     return F.softmax((logits - torch.log(-torch.log(u + eps) + eps)) / tau, dim=-1)
+
+
+class FlatAdam:
+    """torch.optim.Adam semantics over one StackedMLPActors' flat parameter buffer with the
+    hand-written gw_adam_step kernel (include/learner_ops.h): one grid-stride launch per step,
+    the step count on the device (graph-capturable)."""
+
+    def __init__(self, net: StackedMLPActors, lr: float, betas=(0.9, 0.999), eps: float = 1e-8):
+        self.flat = net.flat_params()
+        self.m = torch.zeros_like(self.flat)
+        self.v = torch.zeros_like(self.flat)
+        self.count = torch.zeros(1, dtype=torch.int32, device=self.flat.device)
+        self.lr, self.betas, self.eps = float(lr), betas, float(eps)
+        self.lib = _lib.load()
+
+    def zero_grad(self, set_to_none: bool = False):
+        self.flat.grad.zero_()  # the per-layer .grad views accumulate into this buffer
+
+    def step(self):
+        s = torch.cuda.current_stream(self.flat.device).cuda_stream
+        _lib.check(self.lib.gw_adam_step(self.flat.data_ptr(), self.flat.grad.data_ptr(), self.m.data_ptr(),
+                                         self.v.data_ptr(), self.count.data_ptr(), self.flat.numel(), self.lr,
+                                         self.betas[0], self.betas[1], self.eps, s), "gw_adam_step")
+
+
+def _mlp_target(net: StackedMLPActors) -> StackedMLPActors:
+    """A frozen copy with its own flat buffer (copy.deepcopy would clone the layer views apart)."""
+    K, in_dim = net.K, net.in_dim
+    hidden = tuple(w.shape[2] for w in net.weights[:-1])
+    t = StackedMLPActors(K, in_dim, hidden, n_actions=net.weights[-1].shape[2], layer_norm=net.layer_norm,
+                         device=net.flat_params().device, dtype=net.flat_params().dtype)
+    with torch.no_grad():
+        t.flat_params().copy_(net.flat_params())
+    t.requires_grad_(False)
+    return t
 
 
 class MADDPG:
@@ -55,15 +91,23 @@ class MADDPG:
         self.actors = MultiAgentActors(K, H, W, arch, hidden, device=self.device, seed=seed)
         self.critics = StackedMLPActors(K, K * H * W + K * N_ACTIONS, hidden, n_actions=1, device=self.device,
                                         seed=seed + 1)
-        self.actor_targets = copy.deepcopy(self.actors)
-        self.critic_targets = copy.deepcopy(self.critics)
+        # on the GPU with MLP actors every network is one flat buffer: flat Adam + one-launch soft
+        # updates (learner_ops.hip); otherwise (CPU, CNN actors) torch's Adam and foreach ops
+        self.flat = self.device.type == "cuda" and arch == "mlp"
+        if self.flat:
+            self.actor_targets = copy.deepcopy(self.actors)
+            self.actor_targets.net = _mlp_target(self.actors.net)
+            self.critic_targets = _mlp_target(self.critics)
+            self.opt_actor = FlatAdam(self.actors.net, lr_actor)
+            self.opt_critic = FlatAdam(self.critics, lr_critic)
+        else:
+            self.actor_targets = copy.deepcopy(self.actors)
+            self.critic_targets = copy.deepcopy(self.critics)
+            opt = dict(capturable=True) if capturable and self.device.type == "cuda" else {}
+            self.opt_actor = torch.optim.Adam(self.actors.parameters(), lr=lr_actor, **opt)
+            self.opt_critic = torch.optim.Adam(self.critics.parameters(), lr=lr_critic, **opt)
         for m in (self.actor_targets, self.critic_targets):
             m.requires_grad_(False)
-        opt = dict(capturable=True) if capturable else {}
-        if self.device.type == "cuda":
-            opt["fused"] = True  # one Adam kernel per parameter tensor (one flat tensor per MLP net)
-        self.opt_actor = torch.optim.Adam(self.actors.parameters(), lr=lr_actor, **opt)
-        self.opt_critic = torch.optim.Adam(self.critics.parameters(), lr=lr_critic, **opt)
         self._graph = None
 
     # ---------------------------------------------------------------------------------------
@@ -111,7 +155,15 @@ class MADDPG:
 
     @torch.no_grad()
     def soft_update(self):
-        """agilerl soft_update: target <- tau * online + (1 - tau) * target (two foreach kernels)."""
+        """agilerl soft_update: target <- tau * online + (1 - tau) * target (flat: one gw_soft_update
+        launch per network; otherwise two foreach kernels)."""
+        if self.flat:
+            s = torch.cuda.current_stream(self.device).cuda_stream
+            lib = _lib.load()
+            for net, tgt in ((self.actors.net, self.actor_targets.net), (self.critics, self.critic_targets)):
+                t, p = tgt.flat_params(), net.flat_params()
+                _lib.check(lib.gw_soft_update(t.data_ptr(), p.data_ptr(), t.numel(), self.tau, s), "gw_soft_update")
+            return
         src = list(self.actors.parameters()) + list(self.critics.parameters())
         dst = list(self.actor_targets.parameters()) + list(self.critic_targets.parameters())
         torch._foreach_mul_(dst, 1.0 - self.tau)

@@ -14,10 +14,11 @@ from marlnav import scenario as S
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(REPO, "include", "gridenv.h")
+HEADERS = [HEADER, os.path.join(REPO, "include", "learner_ops.h")]
 
 
 def declared_functions():
-    text = open(HEADER).read()
+    text = "".join(open(h).read() for h in HEADERS)
     return sorted(set(re.findall(r"^\s*(?:gw_status|const char|void|int64_t)\s*\*?\s*(gw_\w+)\s*\(", text, re.M)))
 
 
