@@ -1,0 +1,63 @@
+/* Actor ops of libgridenv.so: the MADDPG actors' get_action fused into one MI355X kernel.
+ *
+ * Replaces, for every env of a grid-env handle at once, the per-step actor call of the
+ * reference rollout:
+ *   maddpg/agent.py:109-122   state flattening, agilerl MADDPG.get_action, argmax -> action ids
+ * with agilerl 1.0.15's MLP actor (EvolvableMLP: Linear -> LayerNorm -> ReLU -> Linear ->
+ * LayerNorm -> ReLU -> Linear, GumbelSoftmax output; layout from the shipped checkpoints,
+ * SURVEY.md §8c) and the env's action mask (ma_customenv.py:467-506).
+ *
+ * The observation an env last wrote (gw_reset / gw_step) is the static map plus at most N+1
+ * patched cells per RL agent (own apple, agents; ma_customenv.py:303-322), so the first layer
+ *   h1 = b1 + obs . W1  =  (b1 + map . W1)  +  sum over patched cells c of (obs[c] - map[c]) W1[c,:]
+ * is evaluated from the env's obs descriptors: no observation is read back from HBM.  Layers 2
+ * and 3 run on f32 MFMA (v_mfma_f32_32x32x2_f32: exact f32 products, k-ordered f32 sums),
+ * LayerNorm / ReLU / Gumbel noise / softmax / mask / argmax in registers.
+ *
+ * Shapes: hidden 128 (both layers), 9 actions, in_dim = H*W of the env, f32 parameters in
+ * the stacked [K][in][out] layout (torch.bmm), 16-byte aligned.  Plain device pointers;
+ * enqueued on `stream`; statuses as in gridenv.h.
+ */
+#ifndef ACTOR_OPS_H
+#define ACTOR_OPS_H
+
+#include <stdint.h>
+
+#include "gridenv.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct gw_mlp_actors {
+    int32_t K;            /* RL agents (must equal the env's K)                         */
+    int32_t in_dim;       /* H*W                                                        */
+    int32_t hidden;       /* 128                                                        */
+    int32_t n_actions;    /* 9                                                          */
+    int32_t layer_norm;   /* LayerNorm(eps 1e-5) + affine after layers 1 and 2           */
+    const float *w1;      /* [K][in_dim][128]                                           */
+    const float *b1;      /* [K][128]                                                   */
+    const float *ln1_w, *ln1_b;  /* [K][128] (unused without layer_norm)                */
+    const float *w2;      /* [K][128][128]                                              */
+    const float *b2;      /* [K][128]                                                   */
+    const float *ln2_w, *ln2_b;  /* [K][128]                                            */
+    const float *w3;      /* [K][128][9]                                                */
+    const float *b3;      /* [K][9]                                                     */
+} gw_mlp_actors;
+
+/* For every env e and RL agent k, on the observation the env last wrote:
+ *   logits = actor_k(obs_k);  training: logits -= log(-log(u + 1e-20) + 1e-20)  (Gumbel noise;
+ *   u = uniform[k][e][a] if `uniform` is given, else Philox(seed; global env id, counter, k));
+ *   probs = softmax(logits / tau);  action = argmax over the actions allowed by mask[e][k]
+ *   (first maximum; mask NULL = all allowed).
+ * Outputs: actions [E][K] int32 (gw_step's rl_actions layout), probs [K][E][9] f32 (the
+ * continuous actions agilerl stores in replay), logits [K][E][9] f32 before the noise (may be
+ * NULL).  c1_ws: [K][128] f32 workspace (b1 + map . W1, recomputed on every call). */
+gw_status gw_actor_act(void *env, const gw_mlp_actors *net, float *c1_ws, int training, float tau,
+                       uint64_t seed, uint64_t counter, const float *uniform, const uint16_t *mask,
+                       int32_t *actions, float *probs, float *logits, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

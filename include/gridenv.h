@@ -158,6 +158,23 @@ gw_status gw_fear_matrix(void *env, int64_t n, const int32_t *cells, const int32
  * kernel's rows then fear_v2's rows, each kernel filling the fields it owns, zeros elsewhere). */
 int64_t gw_stats_rows(void *env);
 
+/* What the observation an env last wrote (gw_reset / gw_step) is made of, for ops that work
+ * on it without reading it back (actor_ops.h): the static step-encoding map plus, per env, a
+ * 48-byte descriptor (agent cells, reset / apple flags; ma_customenv.py:197-209, 303-322).
+ * Device pointers owned by the handle, valid until gw_destroy; contents change with every
+ * gw_reset / gw_step (stream-ordered). */
+typedef struct gw_obs_source {
+    const uint32_t *desc;      /* [E][12] u32: words 0-3 agent cells (16 bits each), word 4
+                                  flags (bit 0 reset encoding, bits 8-15 apples present)      */
+    const float *base;         /* [H*W] 0 road, -1 inactive                                   */
+    int32_t apples[GW_MAX_AGENTS];  /* apple cell of RL agent k                               */
+    int32_t N, K, H, W, variant;
+    int64_t E, env_offset;
+} gw_obs_source;
+gw_status gw_obs_view(void *env, gw_obs_source *out);
+/* Set the thread-local error text returned by gw_last_error (for the library's other
+ * translation units: learner_ops, actor_ops). */
+void gw_set_last_error(const char *msg);
 /* Sizes: H, W, N, K, E (out[0..4]). */
 gw_status gw_dims(void *env, int64_t out[5]);
 

@@ -2549,6 +2549,19 @@ gw_status gw_fear_matrix(void *handle, int64_t n, const int32_t *cells, const in
     return GW_OK;
 }
 
+gw_status gw_obs_view(void *handle, gw_obs_source *out) {
+    Env *env = static_cast<Env *>(handle);
+    if (!env || !out) return fail(GW_ERR_ARG, "null argument");
+    out->desc = env->desc;
+    out->base = env->base;
+    for (int k = 0; k < GW_MAX_AGENTS; ++k) out->apples[k] = k < env->K ? env->apples[k] : -1;
+    out->N = env->N; out->K = env->K; out->H = env->H; out->W = env->W; out->variant = env->variant;
+    out->E = env->E; out->env_offset = env->env_offset;
+    return GW_OK;
+}
+
+void gw_set_last_error(const char *msg) { g_err = msg ? msg : ""; }
+
 gw_status gw_dims(void *handle, int64_t out[5]) {
     Env *env = static_cast<Env *>(handle);
     if (!env || !out) return fail(GW_ERR_ARG, "null argument");

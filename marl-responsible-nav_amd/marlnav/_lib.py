@@ -19,13 +19,18 @@ REPO_ROOT = os.path.dirname(PKG_ROOT)
 CSRC = os.path.join(PKG_ROOT, "csrc")
 INCLUDE = os.path.join(REPO_ROOT, "include")
 LIB_PATH = os.path.join(CSRC, "libgridenv.so")
-HIP_SOURCES = [os.path.join(CSRC, "gridenv.hip"), os.path.join(CSRC, "learner_ops.hip")]
-SOURCES = HIP_SOURCES + [os.path.join(INCLUDE, "gridenv.h"), os.path.join(INCLUDE, "learner_ops.h")]
+HIP_SOURCES = [os.path.join(CSRC, "gridenv.hip"), os.path.join(CSRC, "learner_ops.hip"),
+               os.path.join(CSRC, "actor_ops.hip")]
+HEADERS = [os.path.join(INCLUDE, "gridenv.h"), os.path.join(INCLUDE, "learner_ops.h"),
+           os.path.join(INCLUDE, "actor_ops.h")]
+SOURCES = HIP_SOURCES + HEADERS
+OBJ_DIR = os.path.join(CSRC, "build")
 ARCH = os.environ.get("MARLNAV_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 HIPCC_FLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared",
                "-ffp-contract=off", "-fno-fast-math", "-Wall"]
+COMPILE_FLAGS = [f for f in HIPCC_FLAGS if f != "-shared"]
 
 GW_MAX_AGENTS = 8
 _lock = threading.Lock()
@@ -56,17 +61,51 @@ def needs_build() -> bool:
         return f.read().strip() != source_hash()
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    """Compile csrc/gridenv.hip -> csrc/libgridenv.so for gfx950 (cross-compiles without a GPU)."""
-    if not force and not needs_build():
-        return LIB_PATH
-    tmp = LIB_PATH + f".tmp{os.getpid()}"
-    cmd = [HIPCC, *HIPCC_FLAGS, f"-I{INCLUDE}", *HIP_SOURCES, "-o", tmp]
+def _object(src: str, verbose: bool) -> str:
+    """Compile one HIP source to csrc/build/<name>.<hash>.o (hash of the source, every header
+    and the flags), reusing an existing object: only the changed translation units rebuild."""
+    import hashlib
+    h = hashlib.sha256(" ".join(COMPILE_FLAGS).encode())
+    for path in [src, *HEADERS]:
+        with open(path, "rb") as f:
+            h.update(f.read())
+    name = os.path.splitext(os.path.basename(src))[0]
+    obj = os.path.join(OBJ_DIR, f"{name}.{h.hexdigest()[:16]}.o")
+    if os.path.exists(obj):
+        return obj
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    for old in os.listdir(OBJ_DIR):  # drop this source's stale objects
+        if old.startswith(name + ".") and old.endswith(".o"):
+            os.remove(os.path.join(OBJ_DIR, old))
+    tmp = obj + f".tmp{os.getpid()}"
+    cmd = [HIPCC, *COMPILE_FLAGS, f"-I{INCLUDE}", "-c", src, "-o", tmp]
     if verbose:
-        print(" ".join(cmd))
+        print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
-        raise GwError(f"hipcc failed ({r.returncode}):\n{r.stderr[-4000:]}")
+        raise GwError(f"hipcc failed on {os.path.basename(src)} ({r.returncode}):\n{r.stderr[-4000:]}")
+    os.replace(tmp, obj)
+    return obj
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile csrc/*.hip -> csrc/libgridenv.so for gfx950 (cross-compiles without a GPU):
+    one object per source (cached by content hash), the sources compiled in parallel."""
+    if not force and not needs_build():
+        return LIB_PATH
+    if force and os.path.isdir(OBJ_DIR):
+        for old in os.listdir(OBJ_DIR):
+            os.remove(os.path.join(OBJ_DIR, old))
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(len(HIP_SOURCES)) as ex:
+        objs = list(ex.map(lambda s: _object(s, verbose), HIP_SOURCES))
+    tmp = LIB_PATH + f".tmp{os.getpid()}"
+    cmd = [HIPCC, *HIPCC_FLAGS, *objs, "-o", tmp]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise GwError(f"hipcc link failed ({r.returncode}):\n{r.stderr[-4000:]}")
     os.replace(tmp, LIB_PATH)
     with open(STAMP_PATH, "w") as f:
         f.write(source_hash())
@@ -106,7 +145,21 @@ class GwState(C.Structure):
 
 EXPORTS = ["gw_create", "gw_reset", "gw_step", "gw_state_view", "gw_copy_state", "gw_profile",
            "gw_profile_read", "gw_stats_rows", "gw_dims", "gw_last_error", "gw_destroy", "gw_fear_matrix",
-           "gw_adam_step", "gw_soft_update"]
+           "gw_adam_step", "gw_soft_update", "gw_obs_view", "gw_set_last_error", "gw_actor_act"]
+
+
+class GwObsSource(C.Structure):
+    _fields_ = [("desc", C.c_void_p), ("base", C.c_void_p), ("apples", C.c_int32 * GW_MAX_AGENTS),
+                ("N", C.c_int32), ("K", C.c_int32), ("H", C.c_int32), ("W", C.c_int32), ("variant", C.c_int32),
+                ("E", C.c_int64), ("env_offset", C.c_int64)]
+
+
+MLP_PARAM_FIELDS = ["w1", "b1", "ln1_w", "ln1_b", "w2", "b2", "ln2_w", "ln2_b", "w3", "b3"]
+
+
+class GwMlpActors(C.Structure):
+    _fields_ = [("K", C.c_int32), ("in_dim", C.c_int32), ("hidden", C.c_int32), ("n_actions", C.c_int32),
+                ("layer_norm", C.c_int32)] + [(n, C.c_void_p) for n in MLP_PARAM_FIELDS]
 
 
 def _declare(L):
@@ -137,6 +190,13 @@ def _declare(L):
     L.gw_adam_step.restype = C.c_int
     L.gw_soft_update.argtypes = [p, p, C.c_int64, C.c_float, p]
     L.gw_soft_update.restype = C.c_int
+    L.gw_obs_view.argtypes = [p, C.POINTER(GwObsSource)]
+    L.gw_obs_view.restype = C.c_int
+    L.gw_set_last_error.argtypes = [C.c_char_p]
+    L.gw_set_last_error.restype = None
+    L.gw_actor_act.argtypes = [p, C.POINTER(GwMlpActors), p, C.c_int, C.c_float, C.c_uint64, C.c_uint64,
+                               p, p, p, p, p, p]
+    L.gw_actor_act.restype = C.c_int
     L.gw_destroy.argtypes = [p]
     L.gw_destroy.restype = None
     return L

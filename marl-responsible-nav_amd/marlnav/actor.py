@@ -17,6 +17,7 @@ and the reference has no test of it); the deterministic logits are a plain resta
 """
 from __future__ import annotations
 
+import ctypes as C
 import math
 
 import torch
@@ -163,4 +164,57 @@ class MultiAgentActors(nn.Module):
         else:
             probs_m = probs
         actions = probs_m.argmax(-1).t().to(torch.int32).contiguous()
+        return actions, probs
+
+    # ---------------------------------------------------------------------------------------
+    def fusable(self, env) -> bool:
+        """The fused HIP get_action (gw_actor_act, include/actor_ops.h) covers the stacked f32
+        MLP with two 128-wide hidden layers over a VecGridEnv's own observations."""
+        if self.arch != "mlp" or self.dtype != torch.float32:
+            return False
+        net = self.net
+        return (net.n_layers == 3 and net.weights[0].shape[-1] == 128 and net.weights[1].shape == (self.K, 128, 128)
+                and net.weights[2].shape[-1] == N_ACTIONS and net.in_dim == env.H * env.W and self.K == env.K)
+
+    @torch.no_grad()
+    def act_env(self, env, mask: torch.Tensor | None = None, training: bool = True, tau: float = 1.0,
+                seed: int = 0, counter: int = 0, uniform: torch.Tensor | None = None,
+                actions_out: torch.Tensor | None = None, probs_out: torch.Tensor | None = None,
+                logits_out: torch.Tensor | None = None):
+        """``act`` on the observation ``env`` last wrote, as ONE fused HIP kernel (gw_actor_act):
+        the first layer from the env's obs descriptors (map + patched cells, no obs read back),
+        layers 2-3 on f32 MFMA, Gumbel noise from Philox(seed; env, counter, k) or ``uniform``
+        [K, E, 9], softmax, mask, argmax.  -> (actions [E, K] int32, probs [K, E, 9] float32).
+        Raises if the library or a GPU is missing (no fallback)."""
+        from . import _lib
+        if not self.fusable(env):
+            raise _lib.GwError("act_env: actor not fusable (needs the f32 MLP 128-128-9 over the env's H*W obs)")
+        net, K, E, dev = self.net, self.K, env.E, env.device
+        if getattr(self, "_c1", None) is None or self._c1.device != dev:
+            self._c1 = torch.empty((K, 128), dtype=torch.float32, device=dev)
+        actions = actions_out if actions_out is not None else torch.empty((E, K), dtype=torch.int32, device=dev)
+        probs = probs_out if probs_out is not None else torch.empty((K, E, N_ACTIONS), dtype=torch.float32, device=dev)
+        assert actions.dtype == torch.int32 and actions.shape == (E, K) and actions.is_contiguous()
+        assert probs.dtype == torch.float32 and probs.shape == (K, E, N_ACTIONS) and probs.is_contiguous()
+        if uniform is not None:
+            assert uniform.dtype == torch.float32 and uniform.shape == (K, E, N_ACTIONS)
+            uniform = uniform.contiguous()
+        if mask is not None:
+            assert mask.shape == (E, K) and mask.element_size() == 2
+            mask = mask.contiguous()
+        ln = net.layer_norm
+        ptrs = [net.weights[0], net.biases[0], net.ln_w[0] if ln else None, net.ln_b[0] if ln else None,
+                net.weights[1], net.biases[1], net.ln_w[1] if ln else None, net.ln_b[1] if ln else None,
+                net.weights[2], net.biases[2]]
+        spec = _lib.GwMlpActors(K, net.in_dim, 128, N_ACTIONS, int(ln),
+                                *[t.data_ptr() if t is not None else None for t in ptrs])
+        lib = _lib.load()
+        with torch.cuda.device(dev):
+            stream = torch.cuda.current_stream(dev).cuda_stream
+            _lib.check(lib.gw_actor_act(env.handle, C.byref(spec), self._c1.data_ptr(), int(bool(training)),
+                                        float(tau), int(seed) & 0xFFFFFFFFFFFFFFFF, int(counter) & 0xFFFFFFFFFFFFFFFF,
+                                        uniform.data_ptr() if uniform is not None else None,
+                                        mask.data_ptr() if mask is not None else None, actions.data_ptr(),
+                                        probs.data_ptr(), logits_out.data_ptr() if logits_out is not None else None,
+                                        stream), "gw_actor_act")
         return actions, probs

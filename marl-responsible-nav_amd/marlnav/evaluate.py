@@ -21,8 +21,9 @@ from .vec_env import VecGridEnv
 
 @torch.no_grad()
 def evaluate(actors: MultiAgentActors, scenario="level3", episodes: int = 100, max_steps: int = 150,
-             fear: bool = False, seed: int = 42, record_actions: bool = False) -> dict:
+             fear: bool = False, seed: int = 42, record_actions: bool = False, fused: bool | None = None) -> dict:
     env = VecGridEnv(scenario, num_envs=episodes, fear=fear, max_steps=max_steps, auto_reset=False, seed=seed)
+    fused = actors.fusable(env) if fused is None else fused
     try:
         obs, mask = env.reset()
         dev = env.device
@@ -33,7 +34,10 @@ def evaluate(actors: MultiAgentActors, scenario="level3", episodes: int = 100, m
         fear_sum = torch.zeros((), dtype=torch.float64, device=dev)
         recorded = []
         for _ in range(max_steps):
-            actions, _ = actors.act(env.out["obs"], env.out["mask"], training=False)
+            if fused:  # one kernel over the obs descriptors (include/actor_ops.h)
+                actions, _ = actors.act_env(env, env.out["mask"], training=False)
+            else:
+                actions, _ = actors.act(env.out["obs"], env.out["mask"], training=False)
             if record_actions:
                 recorded.append(actions.clone())
             r = env.step(actions)

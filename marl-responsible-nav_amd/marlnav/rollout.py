@@ -66,9 +66,16 @@ class ReplayRing:
 
 class Rollout:
     def __init__(self, env: VecGridEnv, actors: MultiAgentActors | None = None, replay_slots: int = 0,
-                 training: bool = True, group=None, seed: int = 0):
+                 training: bool = True, group=None, seed: int = 0, fused: bool | None = None):
+        """fused: get_action as the one-kernel gw_actor_act over the env's obs descriptors
+        (default when the actors are the f32 128-128 MLP), else the PyTorch forward over the
+        dense obs with torch's Gumbel noise."""
         self.env = env
         self.actors = actors
+        self.fused = (actors is not None and actors.fusable(env)) if fused is None else bool(fused)
+        self.seed = int(seed)
+        self._calls = 0  # Philox counter of the fused path's Gumbel noise (never repeats)
+        self._actions = torch.empty((env.E, env.K), dtype=torch.int32, device=env.device)
         self.training = training
         self.group = group
         self.replay = ReplayRing(env, replay_slots) if replay_slots else None
@@ -95,15 +102,21 @@ class Rollout:
     def step(self):
         env = self.env
         mask = env.out["mask"]
-        if self.actors is not None:
+        cur = self.t % self.replay.S if self.replay is not None else 0
+        if self.actors is not None and self.fused:
+            probs_out = self.replay.probs[cur] if self.replay is not None else None
+            actions, probs = self.actors.act_env(env, mask, self.training, seed=self.seed, counter=self._calls,
+                                                 actions_out=self._actions, probs_out=probs_out)
+            self._calls += 1
+        elif self.actors is not None:
             actions, probs = self.actors.act(self._obs_now(), mask, self.training, generator=self.gen)
         else:
             actions, probs = None, None  # device-RNG random policy
         if self.replay is not None:
             rp = self.replay
-            cur, nxt = self.t % rp.S, (self.t + 1) % rp.S
+            nxt = (self.t + 1) % rp.S
             r = env.step(actions, obs_out=rp.obs[nxt], final_obs_out=rp.final_obs[cur])
-            if probs is not None:
+            if probs is not None and probs.data_ptr() != rp.probs[cur].data_ptr():
                 rp.probs[cur].copy_(probs)
             rp.reward[cur].copy_(r.shaped)
             rp.term[cur].copy_(r.term)

@@ -14,7 +14,7 @@ from marlnav import scenario as S
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(REPO, "include", "gridenv.h")
-HEADERS = [HEADER, os.path.join(REPO, "include", "learner_ops.h")]
+HEADERS = [HEADER, os.path.join(REPO, "include", "learner_ops.h"), os.path.join(REPO, "include", "actor_ops.h")]
 
 
 def declared_functions():
@@ -46,12 +46,15 @@ STRUCTS = {
                                   "auto_reset", "seed"]),
     "gw_step_out": (_lib.GwStepOut, _lib.STEP_OUT_FIELDS),
     "gw_state": (_lib.GwState, _lib.STATE_FIELDS),
+    "gw_obs_source": (_lib.GwObsSource, ["desc", "base", "apples", "N", "K", "H", "W", "variant", "E", "env_offset"]),
+    "gw_mlp_actors": (_lib.GwMlpActors, ["K", "in_dim", "hidden", "n_actions", "layer_norm", *_lib.MLP_PARAM_FIELDS]),
 }
 
 
 def test_ctypes_layout_matches_header():
     """sizeof/offsetof of every ABI struct, compiled from include/gridenv.h with gcc."""
-    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "gridenv.h"', "int main(void){"]
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "gridenv.h"', '#include "actor_ops.h"',
+             "int main(void){"]
     for s, (_, fields) in STRUCTS.items():
         lines.append(f'printf("{s} %zu\\n", sizeof({s}));')
         for f in fields:

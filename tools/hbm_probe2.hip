@@ -40,6 +40,20 @@ __global__ void __launch_bounds__(256) chunk_store(f32x4 *__restrict__ dst, size
     }
 }
 
+// read stream: each lane sums U float4 per iteration (one result per lane, so no load is dead)
+template <int U>
+__global__ void __launch_bounds__(256) stride_read(const f32x4 *__restrict__ src, size_t n4, float *out) {
+    const size_t step = (size_t)gridDim.x * blockDim.x;
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (; i + (U - 1) * step < n4; i += U * step) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc += __builtin_nontemporal_load(src + i + u * step);
+    }
+    const float s = acc.x + acc.y + acc.z + acc.w;
+    if (s == 12345.f) out[threadIdx.x] = s;
+}
+
 template <class F>
 double timeit(F launch, size_t bytes) {
     hipEvent_t e0, e1;
@@ -76,5 +90,13 @@ int main(int argc, char **argv) {
            timeit([&](float v) { chunk_store<1024, true><<<(unsigned)((n4 + 1023) / 1024), 256>>>(a, n4, v); }, bytes),
            timeit([&](float v) { chunk_store<4096, true><<<(unsigned)((n4 + 4095) / 4096), 256>>>(a, n4, v); }, bytes),
            timeit([&](float v) { chunk_store<16384, true><<<(unsigned)((n4 + 16383) / 16384), 256>>>(a, n4, v); }, bytes));
+    float *o;
+    (void)hipMalloc(&o, 4096);
+    for (int g : grids)
+        printf("{\"probe\": \"read\", \"grid\": %d, \"U4\": %.0f, \"U8\": %.0f}\n", g,
+               timeit([&](float) { stride_read<4><<<g, 256>>>(a, n4, o); }, bytes),
+               timeit([&](float) { stride_read<8><<<g, 256>>>(a, n4, o); }, bytes));
+    printf("{\"probe\": \"memset\", \"hipMemsetD32Async\": %.0f}\n",
+           timeit([&](float v) { (void)hipMemsetD32Async((hipDeviceptr_t)a, (int)v, bytes / 4, 0); }, bytes));
     return 0;
 }

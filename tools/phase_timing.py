@@ -70,7 +70,7 @@ def main():
     import torch  # noqa: F401  (shared HIP runtime, before the library loads)
     from marlnav import _lib
     lib_path = os.path.join(OUT, "libgridenv_phase.so")
-    cmd = [_lib.HIPCC, *_lib.HIPCC_FLAGS, f"-I{_lib.INCLUDE}", hip, "-o", lib_path]
+    cmd = [_lib.HIPCC, *_lib.HIPCC_FLAGS, f"-I{_lib.INCLUDE}", hip, *_lib.HIP_SOURCES[1:], "-o", lib_path]
     subprocess.run(cmd, check=True)
     _lib.LIB_PATH = lib_path
     _lib.needs_build = lambda: False
