@@ -11,7 +11,7 @@
  * patched cells per RL agent (own apple, agents; ma_customenv.py:303-322), so the first layer
  *   h1 = b1 + obs . W1  =  (b1 + map . W1)  +  sum over patched cells c of (obs[c] - map[c]) W1[c,:]
  * is evaluated from the env's obs descriptors: no observation is read back from HBM.  Layers 2
- * and 3 run on f32 MFMA (v_mfma_f32_32x32x2_f32: exact f32 products, k-ordered f32 sums),
+ * and 3 run on f32 MFMA (v_mfma_f32_16x16x4_f32: exact f32 products, k-ordered f32 sums),
  * LayerNorm / ReLU / Gumbel noise / softmax / mask / argmax in registers.
  *
  * Shapes: hidden 128 (both layers), 9 actions, in_dim = H*W of the env, f32 parameters in
@@ -45,6 +45,14 @@ typedef struct gw_mlp_actors {
     const float *b3;      /* [K][9]                                                     */
 } gw_mlp_actors;
 
+/* Size (floats) of the workspace the two calls below share: per agent c1 = b1 + map . W1 (128),
+ * the W2 / W3 images the kernel stages in LDS, and map . W1 row slices. */
+int64_t gw_actor_workspace_floats(int32_t in_dim, int32_t K);
+
+/* Derive the workspace from the parameters (c1 and the MFMA-operand images of W2 / W3).  Enqueue
+ * it again after every change of the parameters (optimizer step, load); ws 16-byte aligned. */
+gw_status gw_actor_prepare(void *env, const gw_mlp_actors *net, float *ws, void *stream);
+
 /* For every env e and RL agent k, on the observation the env last wrote:
  *   logits = actor_k(obs_k);  training: logits -= log(-log(u + 1e-20) + 1e-20)  (Gumbel noise;
  *   u = uniform[k][e][a] if `uniform` is given, else Philox(seed; global env id, counter, k));
@@ -52,8 +60,8 @@ typedef struct gw_mlp_actors {
  *   (first maximum; mask NULL = all allowed).
  * Outputs: actions [E][K] int32 (gw_step's rl_actions layout), probs [K][E][9] f32 (the
  * continuous actions agilerl stores in replay), logits [K][E][9] f32 before the noise (may be
- * NULL).  c1_ws: [K][128] f32 workspace (b1 + map . W1, recomputed on every call). */
-gw_status gw_actor_act(void *env, const gw_mlp_actors *net, float *c1_ws, int training, float tau,
+ * NULL).  ws: prepared by gw_actor_prepare for the current parameters. */
+gw_status gw_actor_act(void *env, const gw_mlp_actors *net, const float *ws, int training, float tau,
                        uint64_t seed, uint64_t counter, const float *uniform, const uint16_t *mask,
                        int32_t *actions, float *probs, float *logits, void *stream);
 

@@ -3,17 +3,29 @@
 // flattened obs, argmax), agilerl 1.0.15 MADDPG.get_action with an EvolvableMLP actor
 // (Linear-LayerNorm-ReLU x2, Linear, GumbelSoftmax; parity of agilerl itself unpinned).
 //
-// Work split (block = 4 waves = one RL agent k, persistent over 32-env tiles, one tile per wave):
-//   layer 1   from the obs descriptors: h1 = c1_k + sum_{patched cells c} delta_c * W1_k[c, :],
-//             c1_k = b1_k + map . W1_k (prologue kernel).  Lane (env = l & 31, half = l >> 5)
-//             accumulates features [64 half, 64 half + 64) of its env (W1 rows are L2 resident).
-//   LN1/ReLU  in registers; the two halves of an env meet through one cross-half shuffle.
-//   layer 2   transposed f32 MFMA: H2^T = W2^T A1^T with v_mfma_f32_32x32x2_f32.  The lane's 64
-//             layer-1 registers ARE the B operand (k-step s pairs feature s of half 0 with feature
-//             64 + s of half 1), W2 is the A operand from LDS; the result has env on the lane and
-//             features in the registers, so LN2 again needs only the cross-half shuffle.
-//   layer 3   the same with A = W3^T (9 of 32 rows live), B = the LN2 registers in D order.
-//   epilogue  logits -> LDS -> one lane per env: Gumbel noise, softmax, mask, argmax.
+// gw_actor_prepare (once per weight update): c1_k = b1_k + map . W1_k, and the LDS images of the
+// layer-2/3 MFMA A operands (W2, W3 permuted so each lane's four consecutive k-steps are one
+// float4).  gw_actor_act (every step), block = 8 waves = one RL agent k, 2 blocks per CU,
+// persistent over 16-env tiles, one tile per wave at a time:
+//   layer 1   from the obs descriptors: h1 = c1_k + sum_{patched cells c} delta_c * W1_k[c, :].
+//             Lane (env = l & 15, quarter q = l >> 4) accumulates features 16j + 4q + i (j < 8,
+//             i < 4) of its env: W1 rows are L2 resident and the four lanes of an env read one
+//             contiguous 64-byte piece of the patched row per load instruction; the map
+//             value of a cell comes from a road bitmask in LDS; the next tile's descriptor is
+//             loaded while this tile computes.
+//   LN1/ReLU  in registers; the four quarters of an env meet through two lane shuffles.
+//   layer 2   transposed f32 MFMA: H2^T = W2^T A1^T with v_mfma_f32_16x16x4_f32.  The lane's 32
+//             layer-1 registers ARE the B operand (k-step s takes feature 16(s >> 2) + 4q + (s & 3)
+//             from quarter q: the same feature order as the layer-2 result),
+//             W2 the A operand (ds_read_b128: four k-steps per read); the result has env on the
+//             lane and features 16m + 4q + r in the registers, so LN2 needs only the shuffles.
+//   layer 3   the same with A = W3^T (9 of 16 rows live), B = the LN2 registers in D order.  Its
+//             result row 4q + r is action 4q + r, i.e. the logits are already spread over the
+//             env's lanes (q 0: actions 0-3, q 1: 4-7, q 2: 8):
+//   epilogue  Gumbel noise (one Philox draw per lane), softmax, mask and argmax as 4-lane
+//             reductions.
+// ~127 VGPRs per lane so 4 waves share each SIMD and one wave's gathers / LayerNorm / epilogue
+// overlap another's MFMA chain (the f32 MFMA rate, 64 FLOP/clk/SIMD, bounds layers 2-3).
 // f32 throughout: every product exact, k-ordered f32 sums (MFMA), so the result differs from a
 // torch fp32 forward only by summation order (tests/test_actor_ops.py states the tolerance).
 #include <hip/hip_runtime.h>
@@ -21,21 +33,56 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 
 #include "actor_ops.h"
 
 namespace {
 
-constexpr int HID = 128, NA = 9, TILE = 32, WAVES = 4, THREADS = 64 * WAVES, MAXN = GW_MAX_AGENTS;
+constexpr int HID = 128, NA = 9, TILE = 16, WAVES = 8, THREADS = 64 * WAVES, MAXN = GW_MAX_AGENTS;
 constexpr int NDESC = 12;
 constexpr uint32_t D_RESET = 1u;
 constexpr float LN_EPS = 1e-5f, G_EPS = 1e-20f;
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// workspace layout (floats, per gw_actor_workspace_floats)
+constexpr int W2IMG = HID * HID;          // per agent
+constexpr int W3IMG = 8 * 4 * NA * 4;     // per agent
+struct Ws {
+    float *c1;        // [K][128]
+    float4 *w2;       // [K][4096]  (w2_slot)
+    float4 *w3;       // [K][288]   (w3_slot)
+    float *part;      // [K][nslices][128] map . W1 row slices
+};
+inline Ws ws_layout(float *base, int K) {
+    Ws w;
+    w.c1 = base;
+    w.w2 = reinterpret_cast<float4 *>(base + (size_t)K * HID);
+    w.w3 = reinterpret_cast<float4 *>(base + (size_t)K * (HID + W2IMG));
+    w.part = base + (size_t)K * (HID + W2IMG + W3IMG);
+    return w;
+}
+
+// LDS images of the MFMA A operands, one float4 (4 consecutive k-steps) per lane and read:
+//   W2: [m 8][s4 8][q 4][el 16] float4, element j = W2[16 s4 + 4q + j][16m + el]
+//   W3: [m 8][q 4][el 9]        float4, element r = W3[16m + 4q + r][el]  (lanes el >= 9 read 0)
+// A wave's ds_read_b128 of W2 covers 1 KB contiguous; within each 16-lane bank group the 16 env
+// lanes are distinct and q steps by 256 B, so the reads are conflict-free.
+__host__ __device__ inline int w2_slot(int m, int s4, int q, int el) { return ((m * 8 + s4) * 4 + q) * 16 + el; }
+__host__ __device__ inline int w3_slot(int m, int q, int el) { return (m * 4 + q) * NA + el; }
+
+struct PrepParams {
+    gw_mlp_actors net;
+    Ws ws;
+    const float *base;
+    int HW, nslices;
+};
 
 struct ActParams {
     gw_mlp_actors net;
-    float *c1;                // [K][128] (written by c1_kernel)
+    const float *c1;          // [K][128]
+    const float4 *w2img, *w3img;
     const uint32_t *desc;     // [E][12]
     const float *base;        // [HW]
     const uint16_t *mask;     // [E][K] or null
@@ -45,10 +92,20 @@ struct ActParams {
     float *logits;            // [K][E][9] or null
     int64_t E, env_offset;
     int N, K, HW, variant, training, tiles;
+    int ab;                   // GW_ACT_AB (measurement only): bit 0 skip the W1 gathers, bit 1 skip
+                              // layer 2's MFMAs, bit 2 skip the epilogue
     float tau;
     uint32_t key0, key1, ctr0, ctr1;
     int apples[MAXN];
 };
+
+// GW_ACT_AB bit 3 (measurement only): wave 0 of each block stamps s_memtime at its phase
+// boundaries (tools/act_ab.py reads them through gw_actor_debug_clocks)
+__device__ unsigned long long g_act_clk[1024][16];
+#define ACT_STAMP(slot)                                                                  \
+    do {                                                                                 \
+        if ((p.ab & 8) && tid == 0 && bid < 1024 && (slot) < 16) g_act_clk[bid][slot] = clock64(); \
+    } while (0)
 
 // Philox4x32-10, the same generator as gridenv.hip (keyed draws, graph- and shard-invariant)
 __device__ __forceinline__ uint4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
@@ -79,44 +136,93 @@ __device__ __forceinline__ float agent_value(bool reset, int n, int k, bool on_a
     return (float)v;
 }
 
-// c1[k][j] = b1[k][j] + sum_c map[c] * W1[k][c][j]; block (k, 32-column group), 8 row slices
-__global__ void __launch_bounds__(256) c1_kernel(ActParams p) {
-    __shared__ float part[8][32];
-    const int k = blockIdx.y, j = blockIdx.x * 32 + (threadIdx.x & 31), sl = threadIdx.x >> 5;
+// ---- gw_actor_prepare ----------------------------------------------------------------------
+// map . W1 in row slices: part[k][sl][j] = sum_{c in rows [32 sl, 32 sl + 32)} map[c] * W1[k][c][j]
+__global__ void __launch_bounds__(HID) prep_slices(PrepParams p) {
+    const int sl = blockIdx.x, k = blockIdx.y, j = threadIdx.x;
     const float *w1 = p.net.w1 + (size_t)k * p.HW * HID;
+    const int c0 = sl * 32, c1 = min(p.HW, c0 + 32);
     float acc = 0.0f;
-    for (int c = sl; c < p.HW; c += 8) acc = fmaf(p.base[c], w1[(size_t)c * HID + j], acc);
-    part[sl][threadIdx.x & 31] = acc;
-    __syncthreads();
-    if (sl == 0) {
-        float s = 0.0f;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) s += part[q][threadIdx.x];
-        p.c1[k * HID + j] = p.net.b1[k * HID + j] + s;
+    for (int c = c0; c < c1; ++c) acc = fmaf(p.base[c], w1[(size_t)c * HID + j], acc);
+    p.ws.part[((size_t)k * p.nslices + sl) * HID + j] = acc;
+}
+
+// c1 = b1 + the slices in order (block 0 of each agent) and the W2 / W3 images (all blocks)
+__global__ void __launch_bounds__(256) prep_images(PrepParams p) {
+    const int k = blockIdx.y, tid = threadIdx.x;
+    if (blockIdx.x == 0 && tid < HID) {
+        float part = 0.0f;
+        for (int sl = 0; sl < p.nslices; ++sl) part += p.ws.part[((size_t)k * p.nslices + sl) * HID + tid];
+        p.ws.c1[k * HID + tid] = p.net.b1[k * HID + tid] + part;
+    }
+    const float *w2 = p.net.w2 + (size_t)k * HID * HID;
+    float *img2 = reinterpret_cast<float *>(p.ws.w2 + (size_t)k * (W2IMG / 4));
+    for (int f = blockIdx.x * 256 + tid; f < HID * HID; f += gridDim.x * 256) {
+        const int row = f / HID, col = f % HID;
+        img2[4 * w2_slot(col >> 4, row >> 4, (row >> 2) & 3, col & 15) + (row & 3)] = w2[f];
+    }
+    const float *w3 = p.net.w3 + (size_t)k * HID * NA;
+    float *img3 = reinterpret_cast<float *>(p.ws.w3 + (size_t)k * (W3IMG / 4));
+    for (int i = blockIdx.x * 256 + tid; i < W3IMG; i += gridDim.x * 256) {
+        const int r = i & 3, el = (i >> 2) % NA, q = ((i >> 2) / NA) & 3, m = (i >> 2) / (NA * 4);
+        img3[i] = w3[(16 * m + 4 * q + r) * NA + el];
     }
 }
 
-__device__ __forceinline__ float half_sum(float s) {  // sum over the two lanes of an env
+// ---- gw_actor_act --------------------------------------------------------------------------
+__device__ __forceinline__ float quad_sum(float s) {  // over the four lanes of an env
+    s += __shfl_xor(s, 16, 64);
     return s + __shfl_xor(s, 32, 64);
 }
+__device__ __forceinline__ float quad_max(float s) {
+    s = fmaxf(s, __shfl_xor(s, 16, 64));
+    return fmaxf(s, __shfl_xor(s, 32, 64));
+}
 
-__global__ void __launch_bounds__(THREADS, 2) act_kernel(ActParams p) {
-    __shared__ float s_w2[HID * HID];        // [in][out], 64 KB
-    __shared__ float s_w3[HID * NA];         // [in][a]
-    __shared__ float s_vec[8][HID];          // c1, ln1_w, ln1_b, b2, ln2_w, ln2_b
+struct Desc {
+    uint4 cells;     // 16-bit agent cells
+    uint32_t flags;
+    uint32_t mask;   // action mask of (e, k)
+};
+
+__device__ __forceinline__ Desc load_desc(const ActParams &p, int64_t e, int k) {
+    Desc d;
+    if (e < p.E) {
+        d.cells = *reinterpret_cast<const uint4 *>(p.desc + e * NDESC);
+        d.flags = p.desc[e * NDESC + 4];
+        d.mask = p.mask ? p.mask[e * p.K + k] : 0x1FFu;
+    } else {
+        d.cells = make_uint4(0, 0, 0, 0);
+        d.flags = 0;
+        d.mask = 0x1FFu;
+    }
+    return d;
+}
+
+template <int NP>  // patch slots per (env, agent) = N + 1
+__global__ void __launch_bounds__(THREADS, 4) act_kernel(ActParams p) {
+    __shared__ float4 s_w2[W2IMG / 4];       // W2 image (w2_slot), 64 KB
+    __shared__ float4 s_w3[W3IMG / 4];       // W3 image (w3_slot), 4.5 KB
+    __shared__ __attribute__((aligned(16))) float s_vec[6][HID];  // c1, ln1_w, ln1_b, b2, ln2_w, ln2_b
     __shared__ float s_b3[12];
-    __shared__ float s_lg[WAVES][TILE][NA + 1];
+    __shared__ uint32_t s_road[128];         // bit c: cell c is road (map value 0, else -1)
 
     const int k = blockIdx.y, tid = threadIdx.x;
     const bool ln = p.net.layer_norm != 0;
-    {   // stage this agent's layer-2/3 weights and vectors (all loads of a lane issued first)
-        const float4 *w2 = reinterpret_cast<const float4 *>(p.net.w2 + (size_t)k * HID * HID);
-        float4 r[HID * HID / 4 / THREADS];
+    const int wave = tid >> 6, lane = tid & 63, el = lane & 15, q = lane >> 4;
+    int tile = blockIdx.x * WAVES + wave;
+    const int bid = blockIdx.y * gridDim.x + blockIdx.x;
+    ACT_STAMP(0);
+    Desc dn = load_desc(p, (int64_t)tile * TILE + el, k);  // first tile's descriptor, in flight
+    {   // stage this agent's W2 / W3 images and vectors (all loads of a lane issued first)
+        const float4 *w2 = p.w2img + (size_t)k * (W2IMG / 4);
+        constexpr int R = W2IMG / 4 / THREADS;
+        float4 r[R];
 #pragma unroll
-        for (int i = 0; i < HID * HID / 4 / THREADS; ++i) r[i] = w2[i * THREADS + tid];
+        for (int i = 0; i < R; ++i) r[i] = w2[i * THREADS + tid];
 #pragma unroll
-        for (int i = 0; i < HID * HID / 4 / THREADS; ++i) reinterpret_cast<float4 *>(s_w2)[i * THREADS + tid] = r[i];
-        for (int i = tid; i < HID * NA; i += THREADS) s_w3[i] = p.net.w3[(size_t)k * HID * NA + i];
+        for (int i = 0; i < R; ++i) s_w2[i * THREADS + tid] = r[i];
+        for (int i = tid; i < W3IMG / 4; i += THREADS) s_w3[i] = p.w3img[(size_t)k * (W3IMG / 4) + i];
         if (tid < HID) {
             s_vec[0][tid] = p.c1[k * HID + tid];
             s_vec[1][tid] = ln ? p.net.ln1_w[k * HID + tid] : 1.0f;
@@ -124,213 +230,258 @@ __global__ void __launch_bounds__(THREADS, 2) act_kernel(ActParams p) {
             s_vec[3][tid] = p.net.b2[k * HID + tid];
             s_vec[4][tid] = ln ? p.net.ln2_w[k * HID + tid] : 1.0f;
             s_vec[5][tid] = ln ? p.net.ln2_b[k * HID + tid] : 0.0f;
+        } else if (tid < 2 * HID) {  // road bits of cells 32w .. 32w + 31 (HW % 32 == 0 or masked)
+            const int w = tid - HID;
+            if (32 * w < p.HW) {
+                float mv[32];
+#pragma unroll
+                for (int j = 0; j < 32; ++j) mv[j] = p.base[min(32 * w + j, p.HW - 1)];
+                uint32_t bits = 0;
+#pragma unroll
+                for (int j = 0; j < 32; ++j) bits |= (32 * w + j < p.HW && mv[j] == 0.0f) ? (1u << j) : 0u;
+                s_road[w] = bits;
+            }
         }
         if (tid < NA) s_b3[tid] = p.net.b3[k * NA + tid];
     }
     __syncthreads();
+    ACT_STAMP(1);
+    int it = 0;
 
-    const int wave = tid >> 6, lane = tid & 63, el = lane & 31, h = lane >> 5;
-    const float *w1 = p.net.w1 + (size_t)k * p.HW * HID + 64 * h;
-    const int K = p.K, N = p.N;
+    const float *w1 = p.net.w1 + (size_t)k * p.HW * HID;
+    const int K = p.K;
     const int ac_k = p.apples[k];
+    // layer-1 register 4j + i and layer-2 register (m = j, r = i) both hold feature 16j + 4q + i
+    auto vec4 = [q](const float *v, int j) { return *reinterpret_cast<const float4 *>(v + 16 * j + 4 * q); };
 
-    for (int tile = blockIdx.x * WAVES + wave; tile < p.tiles; tile += gridDim.x * WAVES) {
+    for (; tile < p.tiles; tile += gridDim.x * WAVES, ++it) {
         const int64_t e = (int64_t)tile * TILE + el;
         const bool valid = e < p.E;
+        const Desc d = dn;
         // ---- obs patches of (e, k): slot 0 own apple, slot 1 + n agent n; a later slot on
         //      the same cell overrides an earlier one (the obs writer's order) ----
-        int pc[MAXN + 1];
-        float pv[MAXN + 1];
+        int pc[NP];
+        float pv[NP];
+        {
+            const bool reset = (d.flags & D_RESET) != 0;
+            const int ac = (valid && ((d.flags >> (8 + k)) & 1u)) ? ac_k : -1;
+            const float ac_map = ac >= 0 ? (((s_road[ac >> 5] >> (ac & 31)) & 1u) ? 0.0f : -1.0f) : 0.0f;
+            float av = ac_map + 9.0f;
+            if (!reset && av == (float)(k + 1)) av = 1.0f;  // relabel of :321 (apple on a wall)
+            pc[0] = ac;
+            pv[0] = av;
+            const uint32_t dw[4] = {d.cells.x, d.cells.y, d.cells.z, d.cells.w};
 #pragma unroll
-        for (int q = 0; q <= MAXN; ++q) {
-            pc[q] = -1;
-            pv[q] = 0.0f;
-        }
-        if (valid) {
-            const uint4 d03 = *reinterpret_cast<const uint4 *>(p.desc + e * NDESC);
-            const uint32_t f = p.desc[e * NDESC + 4];
-            const bool reset = (f & D_RESET) != 0;
-            const int ac = ((f >> (8 + k)) & 1u) ? ac_k : -1;
-            if (ac >= 0) {
-                float av = p.base[ac] + 9.0f;
-                if (!reset && av == (float)(k + 1)) av = 1.0f;  // relabel of :321 (apple on a wall)
-                pc[0] = ac;
-                pv[0] = av;
-            }
-            const uint32_t dw[4] = {d03.x, d03.y, d03.z, d03.w};
-#pragma unroll
-            for (int n = 0; n < MAXN; ++n) {
-                if (n < N) {
-                    const int c = (int)((dw[n >> 1] >> (16 * (n & 1))) & 0xFFFFu);
-                    pc[1 + n] = c;
-                    pv[1 + n] = agent_value(reset, n, k, c == ac, p.variant);
-                }
+            for (int n = 0; n < NP - 1; ++n) {
+                const int c = (int)((dw[n >> 1] >> (16 * (n & 1))) & 0xFFFFu);
+                pc[1 + n] = valid ? c : -1;
+                pv[1 + n] = agent_value(reset, n, k, c == ac, p.variant);
             }
         }
+        // the next tile's descriptor, loaded while this tile computes
+        dn = load_desc(p, (int64_t)(tile + gridDim.x * WAVES) * TILE + el, k);
+        ACT_STAMP(2 + 5 * it);
         // ---- layer 1: c1 + sum of (value - map) * W1 row over the distinct patched cells ----
-        float a[64];
+        float a[32];
 #pragma unroll
-        for (int i = 0; i < 64; ++i) a[i] = s_vec[0][64 * h + i];
+        for (int j = 0; j < 8; ++j) {  // features 16j + 4q .. + 3: one 16-byte LDS read
+            const float4 c = vec4(s_vec[0], j);
+            a[4 * j] = c.x;
+            a[4 * j + 1] = c.y;
+            a[4 * j + 2] = c.z;
+            a[4 * j + 3] = c.w;
+        }
+        // unconditional loads (a dead slot reads row 0 with delta 0: fmaf(0, w, a) == a), so
+        // the scheduler can keep several slots' row pieces in flight
+        int rowc[NP];
+        float dlt[NP];
 #pragma unroll
-        for (int q = 0; q <= MAXN; ++q) {
-            const int c = pc[q];
+        for (int i = 0; i < NP; ++i) {
+            const int c = pc[i];
             bool last = (unsigned)c < (unsigned)p.HW;
 #pragma unroll
-            for (int r = q + 1; r <= MAXN; ++r) last = last && pc[r] != c;
-            const float dlt = last ? pv[q] - p.base[c] : 0.0f;
-            if (dlt != 0.0f) {
-                const float4 *row = reinterpret_cast<const float4 *>(w1 + (size_t)c * HID);
-                float4 wr[16];
+            for (int r = i + 1; r < NP; ++r) last = last && pc[r] != c;
+            const int cc = last ? c : 0;
+            const float map = ((s_road[cc >> 5] >> (cc & 31)) & 1u) ? 0.0f : -1.0f;
+            dlt[i] = (last && !(p.ab & 1)) ? pv[i] - map : 0.0f;
+            rowc[i] = cc * (HID / 4) + q;  // float4 index of features 4q .. 4q + 3 of row cc
+        }
+        const float4 *w1v = reinterpret_cast<const float4 *>(w1);
 #pragma unroll
-                for (int i = 0; i < 16; ++i) wr[i] = row[i];
+        for (int i = 0; i < NP; ++i) {
+            float4 wr[8];
 #pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    a[4 * i + 0] = fmaf(dlt, wr[i].x, a[4 * i + 0]);
-                    a[4 * i + 1] = fmaf(dlt, wr[i].y, a[4 * i + 1]);
-                    a[4 * i + 2] = fmaf(dlt, wr[i].z, a[4 * i + 2]);
-                    a[4 * i + 3] = fmaf(dlt, wr[i].w, a[4 * i + 3]);
-                }
+            for (int j = 0; j < 8; ++j) wr[j] = w1v[rowc[i] + 4 * j];  // features 16j + 4q .. + 3
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                a[4 * j + 0] = fmaf(dlt[i], wr[j].x, a[4 * j + 0]);
+                a[4 * j + 1] = fmaf(dlt[i], wr[j].y, a[4 * j + 1]);
+                a[4 * j + 2] = fmaf(dlt[i], wr[j].z, a[4 * j + 2]);
+                a[4 * j + 3] = fmaf(dlt[i], wr[j].w, a[4 * j + 3]);
             }
+            __builtin_amdgcn_sched_barrier(0);  // one slot's row pieces (32 VGPRs) in flight at a time
         }
         // ---- LN1 + ReLU (nn.LayerNorm(128), eps 1e-5, biased variance) ----
         if (ln) {
-            float s = 0.0f;
+            float sm = 0.0f;
 #pragma unroll
-            for (int i = 0; i < 64; ++i) s += a[i];
-            const float mean = half_sum(s) * (1.0f / HID);
+            for (int i = 0; i < 32; ++i) sm += a[i];
+            const float mean = quad_sum(sm) * (1.0f / HID);
             float v = 0.0f;
 #pragma unroll
-            for (int i = 0; i < 64; ++i) v = fmaf(a[i] - mean, a[i] - mean, v);
-            const float rstd = rsqrtf(half_sum(v) * (1.0f / HID) + LN_EPS);
+            for (int i = 0; i < 32; ++i) v = fmaf(a[i] - mean, a[i] - mean, v);
+            const float rstd = rsqrtf(quad_sum(v) * (1.0f / HID) + LN_EPS);
 #pragma unroll
-            for (int i = 0; i < 64; ++i)
-                a[i] = fmaxf(fmaf((a[i] - mean) * rstd, s_vec[1][64 * h + i], s_vec[2][64 * h + i]), 0.0f);
+            for (int j = 0; j < 8; ++j) {
+                const float4 g = vec4(s_vec[1], j), b = vec4(s_vec[2], j);
+                const float gv[4] = {g.x, g.y, g.z, g.w}, bv4[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    a[4 * j + i] = fmaxf(fmaf((a[4 * j + i] - mean) * rstd, gv[i], bv4[i]), 0.0f);
+            }
         } else {
 #pragma unroll
-            for (int i = 0; i < 64; ++i) a[i] = fmaxf(a[i], 0.0f);
+            for (int i = 0; i < 32; ++i) a[i] = fmaxf(a[i], 0.0f);
         }
-        // ---- layer 2: D[m] (32 features x 32 envs) = W2^T[32m.., k] . A1^T ----
-        f32x16 acc[4];
+        ACT_STAMP(4 + 5 * it);
+        // ---- layer 2: D[m] (16 features x 16 envs) = W2^T[16m.., k] . A1^T ----
+        f32x4 acc[8];
 #pragma unroll
-        for (int m = 0; m < 4; ++m)
+        for (int m = 0; m < 8; ++m) acc[m] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        if (!(p.ab & 2)) {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[m][r] = 0.0f;
+            for (int s4 = 0; s4 < 8; ++s4) {
 #pragma unroll
-        for (int s = 0; s < 64; ++s) {
-            const float *wrow = s_w2 + (64 * h + s) * HID + el;
+                for (int mh = 0; mh < 8; mh += 4) {
+                    float4 w[4];
 #pragma unroll
-            for (int m = 0; m < 4; ++m)
-                acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(wrow[32 * m], a[s], acc[m], 0, 0, 0);
+                    for (int m = 0; m < 4; ++m) w[m] = s_w2[w2_slot(mh + m, s4, q, el)];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+#pragma unroll
+                        for (int m = 0; m < 4; ++m) {
+                            const float wa = j == 0 ? w[m].x : j == 1 ? w[m].y : j == 2 ? w[m].z : w[m].w;
+                            acc[mh + m] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa, a[4 * s4 + j], acc[mh + m], 0, 0, 0);
+                        }
+                }
+            }
         }
-        // register r of tile m holds feature 32m + (r & 3) + 8 (r >> 2) + 4h of env el
-#define FEAT(m, r) (32 * (m) + ((r) & 3) + 8 * ((r) >> 2) + 4 * h)
+        ACT_STAMP(5 + 5 * it);
+        // register r of tile m holds feature 16m + 4q + r of env el
         float s2 = 0.0f;
 #pragma unroll
-        for (int m = 0; m < 4; ++m)
+        for (int m = 0; m < 8; ++m) {
+            const float4 b = vec4(s_vec[3], m);
+            acc[m] += f32x4{b.x, b.y, b.z, b.w};
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                acc[m][r] += s_vec[3][FEAT(m, r)];
-                s2 += acc[m][r];
-            }
+            for (int r = 0; r < 4; ++r) s2 += acc[m][r];
+        }
         if (ln) {
-            const float mean = half_sum(s2) * (1.0f / HID);
+            const float mean = quad_sum(s2) * (1.0f / HID);
             float v = 0.0f;
 #pragma unroll
-            for (int m = 0; m < 4; ++m)
+            for (int m = 0; m < 8; ++m)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) v = fmaf(acc[m][r] - mean, acc[m][r] - mean, v);
-            const float rstd = rsqrtf(half_sum(v) * (1.0f / HID) + LN_EPS);
+                for (int r = 0; r < 4; ++r) v = fmaf(acc[m][r] - mean, acc[m][r] - mean, v);
+            const float rstd = rsqrtf(quad_sum(v) * (1.0f / HID) + LN_EPS);
 #pragma unroll
-            for (int m = 0; m < 4; ++m)
+            for (int m = 0; m < 8; ++m) {
+                const float4 g = vec4(s_vec[4], m), b = vec4(s_vec[5], m);
+                const float gv[4] = {g.x, g.y, g.z, g.w}, bv4[4] = {b.x, b.y, b.z, b.w};
 #pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    acc[m][r] = fmaxf(fmaf((acc[m][r] - mean) * rstd, s_vec[4][FEAT(m, r)], s_vec[5][FEAT(m, r)]), 0.0f);
+                for (int r = 0; r < 4; ++r) acc[m][r] = fmaxf(fmaf((acc[m][r] - mean) * rstd, gv[r], bv4[r]), 0.0f);
+            }
         } else {
 #pragma unroll
-            for (int m = 0; m < 4; ++m)
+            for (int m = 0; m < 8; ++m)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) acc[m][r] = fmaxf(acc[m][r], 0.0f);
+                for (int r = 0; r < 4; ++r) acc[m][r] = fmaxf(acc[m][r], 0.0f);
         }
-        // ---- layer 3: D3 (32 action rows, 9 live x 32 envs) = W3^T . A2^T, one accumulator per
-        //      feature tile (independent MFMA chains), summed in tile order ----
-        f32x16 o3[4];
+        // ---- layer 3: D3 (16 action rows, 9 live x 16 envs) = W3^T . A2^T; k-step (m, r) pairs
+        //      feature 16m + 4q + r of the four quarters; two independent chains ----
+        f32x4 o3[2] = {f32x4{0.0f, 0.0f, 0.0f, 0.0f}, f32x4{0.0f, 0.0f, 0.0f, 0.0f}};
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
+        for (int m = 0; m < 8; ++m) {
+            const float4 w3 = el < NA ? s_w3[w3_slot(m, q, el)] : float4{0.0f, 0.0f, 0.0f, 0.0f};
+            const float wv[4] = {w3.x, w3.y, w3.z, w3.w};
 #pragma unroll
-            for (int r = 0; r < 16; ++r) o3[m][r] = 0.0f;
+            for (int r = 0; r < 4; ++r) o3[m & 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[r], acc[m][r], o3[m & 1], 0, 0, 0);
+        }
+        const f32x4 out = o3[0] + o3[1];
+        if (p.ab & 4) {
+            ACT_STAMP(6 + 5 * it);
+            continue;
+        }
+        // ---- epilogue: D3 row 4q + r = action 4q + r (q 0: 0-3, q 1: 4-7, q 2: 8) ----
+        const size_t o = ((size_t)k * p.E + (valid ? e : 0)) * NA;
+        float lg[4];
+        bool live[4];
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float wa = el < NA ? s_w3[FEAT(m, r) * NA + el] : 0.0f;
-                o3[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa, acc[m][r], o3[m], 0, 0, 0);
+        for (int r = 0; r < 4; ++r) {
+            live[r] = 4 * q + r < NA;
+            lg[r] = live[r] ? out[r] + s_b3[4 * q + r] : 0.0f;
+        }
+        if (p.logits && valid) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (live[r]) p.logits[o + 4 * q + r] = lg[r];
+        }
+        if (p.training) {  // agilerl GumbelSoftmax: logits - log(-log(u + eps) + eps)
+            float u[4];
+            if (p.uniform) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) u[r] = (live[r] && valid) ? p.uniform[o + 4 * q + r] : 0.5f;
+            } else {  // draw q of (env, counter, k): actions 4q .. 4q + 3
+                const uint4 x = philox((uint32_t)(p.env_offset + e), p.ctr0,
+                                       (uint32_t)k | ((uint32_t)q << 8) | (0xA7u << 24), p.ctr1, p.key0, p.key1);
+                u[0] = (float)(x.x >> 8) * (1.0f / 16777216.0f);
+                u[1] = (float)(x.y >> 8) * (1.0f / 16777216.0f);
+                u[2] = (float)(x.z >> 8) * (1.0f / 16777216.0f);
+                u[3] = (float)(x.w >> 8) * (1.0f / 16777216.0f);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (live[r]) lg[r] = lg[r] - logf(-logf(u[r] + G_EPS) + G_EPS);
+        }
+        float z[4], mx = -INFINITY;  // softmax(logits / tau) over the env's four lanes
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            z[r] = lg[r] / p.tau;
+            if (live[r]) mx = fmaxf(mx, z[r]);
+        }
+        mx = quad_max(mx);
+        float ex[4], sm = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            ex[r] = live[r] ? expf(z[r] - mx) : 0.0f;
+            sm += ex[r];
+        }
+        sm = quad_sum(sm);
+        const uint32_t mk = d.mask;
+        float bv = -1.0f;
+        int best = 64;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float pr = ex[r] / sm;
+            if (live[r] && valid) p.probs[o + 4 * q + r] = pr;
+            const float pm = ((mk >> (4 * q + r)) & 1u) ? pr : 0.0f;
+            if (live[r] && pm > bv) {  // first maximum within the lane
+                bv = pm;
+                best = 4 * q + r;
             }
         }
-        f32x16 out = o3[0] + o3[1] + o3[2] + o3[3];
-#undef FEAT
-        // D3 row (r & 3) + 8 (r >> 2) + 4h = action: h 0 -> r 0-3 (actions 0-3), r 4 (action 8);
-        // h 1 -> r 0-3 (actions 4-7)
+        // argmax across the quarters: larger value wins, ties go to the lower action
 #pragma unroll
-        for (int r = 0; r < 4; ++r) s_lg[wave][el][r + 4 * h] = out[r] + s_b3[r + 4 * h];
-        if (h == 0) s_lg[wave][el][8] = out[4] + s_b3[8];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // ---- epilogue: one lane per env ----
-        if (h == 0 && valid) {
-            float lg[NA];
-#pragma unroll
-            for (int a9 = 0; a9 < NA; ++a9) lg[a9] = s_lg[wave][el][a9];
-            const size_t o = ((size_t)k * p.E + e) * NA;
-            if (p.logits) {
-#pragma unroll
-                for (int a9 = 0; a9 < NA; ++a9) p.logits[o + a9] = lg[a9];
+        for (int off = 16; off <= 32; off <<= 1) {
+            const float ov = __shfl_xor(bv, off, 64);
+            const int ob = __shfl_xor(best, off, 64);
+            if (ov > bv || (ov == bv && ob < best)) {
+                bv = ov;
+                best = ob;
             }
-            if (p.training) {  // agilerl GumbelSoftmax: logits - log(-log(u + eps) + eps)
-                float u[12];
-                if (p.uniform) {
-#pragma unroll
-                    for (int a9 = 0; a9 < NA; ++a9) u[a9] = p.uniform[o + a9];
-                } else {
-                    const uint32_t ge = (uint32_t)(p.env_offset + e);
-#pragma unroll
-                    for (int q = 0; q < 3; ++q) {
-                        const uint4 x = philox(ge, p.ctr0, (uint32_t)k | ((uint32_t)q << 8) | (0xA7u << 24), p.ctr1,
-                                               p.key0, p.key1);
-                        u[4 * q + 0] = (float)(x.x >> 8) * (1.0f / 16777216.0f);
-                        u[4 * q + 1] = (float)(x.y >> 8) * (1.0f / 16777216.0f);
-                        u[4 * q + 2] = (float)(x.z >> 8) * (1.0f / 16777216.0f);
-                        u[4 * q + 3] = (float)(x.w >> 8) * (1.0f / 16777216.0f);
-                    }
-                }
-#pragma unroll
-                for (int a9 = 0; a9 < NA; ++a9) lg[a9] = lg[a9] - logf(-logf(u[a9] + G_EPS) + G_EPS);
-            }
-            float z[NA], ex[NA], mx = -INFINITY, sum = 0.0f;  // softmax(logits / tau)
-#pragma unroll
-            for (int a9 = 0; a9 < NA; ++a9) {
-                z[a9] = lg[a9] / p.tau;
-                mx = fmaxf(mx, z[a9]);
-            }
-#pragma unroll
-            for (int a9 = 0; a9 < NA; ++a9) {
-                ex[a9] = expf(z[a9] - mx);
-                sum += ex[a9];
-            }
-            const uint32_t mk = p.mask ? p.mask[e * K + k] : 0x1FFu;
-            int best = 0;
-            float bv = -1.0f;
-#pragma unroll
-            for (int a9 = 0; a9 < NA; ++a9) {
-                const float pr = ex[a9] / sum;
-                p.probs[o + a9] = pr;
-                const float pm = ((mk >> a9) & 1u) ? pr : 0.0f;
-                if (pm > bv) {
-                    bv = pm;
-                    best = a9;
-                }
-            }
-            p.actions[e * K + k] = best;
         }
-        __builtin_amdgcn_wave_barrier();  // s_lg is rewritten by the next tile
+        if (q == 0 && valid) p.actions[e * K + k] = best;
+        ACT_STAMP(6 + 5 * it);
     }
 }
 
@@ -339,30 +490,69 @@ gw_status err(gw_status s, const std::string &msg) {
     return s;
 }
 
+gw_status check_net(const gw_obs_source &src, const gw_mlp_actors *net, const char *who) {
+    const std::string w(who);
+    if (net->K != src.K) return err(GW_ERR_ARG, w + ": net K != env K");
+    if (net->in_dim != src.H * src.W) return err(GW_ERR_ARG, w + ": in_dim != H*W");
+    if (net->hidden != HID || net->n_actions != NA) return err(GW_ERR_ARG, w + ": only hidden 128 and 9 actions are fused");
+    if (!net->w1 || !net->b1 || !net->w2 || !net->b2 || !net->w3 || !net->b3 ||
+        (net->layer_norm && (!net->ln1_w || !net->ln1_b || !net->ln2_w || !net->ln2_b)))
+        return err(GW_ERR_ARG, w + ": null parameter");
+    if (reinterpret_cast<uintptr_t>(net->w1) & 15u) return err(GW_ERR_ARG, w + ": w1 must be 16-byte aligned");
+    return GW_OK;
+}
+
 }  // namespace
 
 extern "C" {
 
-gw_status gw_actor_act(void *env, const gw_mlp_actors *net, float *c1_ws, int training, float tau, uint64_t seed,
-                       uint64_t counter, const float *uniform, const uint16_t *mask, int32_t *actions, float *probs,
-                       float *logits, void *stream) {
-    if (!env || !net || !c1_ws || !actions || !probs) return err(GW_ERR_ARG, "gw_actor_act: null argument");
+// measurement only (not part of the ABI): the stamps of the last GW_ACT_AB & 8 launch
+int gw_actor_debug_clocks(unsigned long long *out, int nblocks) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_act_clk), sizeof(unsigned long long) * 16 * std::min(nblocks, 1024)) ==
+                   hipSuccess ? 0 : -1;
+}
+
+int64_t gw_actor_workspace_floats(int32_t in_dim, int32_t K) {
+    return (int64_t)K * (HID + W2IMG + W3IMG + (int64_t)((in_dim + 31) / 32) * HID);
+}
+
+gw_status gw_actor_prepare(void *env, const gw_mlp_actors *net, float *ws, void *stream) {
+    if (!env || !net || !ws) return err(GW_ERR_ARG, "gw_actor_prepare: null argument");
+    if (reinterpret_cast<uintptr_t>(ws) & 15u) return err(GW_ERR_ARG, "gw_actor_prepare: ws must be 16-byte aligned");
     gw_obs_source src;
     gw_status st = gw_obs_view(env, &src);
     if (st != GW_OK) return st;
-    if (net->K != src.K) return err(GW_ERR_ARG, "gw_actor_act: net K != env K");
-    if (net->in_dim != src.H * src.W) return err(GW_ERR_ARG, "gw_actor_act: in_dim != H*W");
-    if (net->hidden != HID || net->n_actions != NA)
-        return err(GW_ERR_ARG, "gw_actor_act: only hidden 128 and 9 actions are fused");
-    if (!net->w1 || !net->b1 || !net->w2 || !net->b2 || !net->w3 || !net->b3 ||
-        (net->layer_norm && (!net->ln1_w || !net->ln1_b || !net->ln2_w || !net->ln2_b)))
-        return err(GW_ERR_ARG, "gw_actor_act: null parameter");
-    if ((reinterpret_cast<uintptr_t>(net->w1) | reinterpret_cast<uintptr_t>(net->w2)) & 15u)
-        return err(GW_ERR_ARG, "gw_actor_act: w1 / w2 must be 16-byte aligned");
+    if ((st = check_net(src, net, "gw_actor_prepare")) != GW_OK) return st;
+    PrepParams p;
+    p.net = *net;
+    p.HW = src.H * src.W;
+    p.nslices = (p.HW + 31) / 32;
+    p.ws = ws_layout(ws, src.K);
+    p.base = src.base;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(prep_slices, dim3(p.nslices, src.K), dim3(HID), 0, s, p);
+    hipLaunchKernelGGL(prep_images, dim3(16, src.K), dim3(256), 0, s, p);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return err(GW_ERR_HIP, std::string("gw_actor_prepare: ") + hipGetErrorString(e));
+    return GW_OK;
+}
+
+gw_status gw_actor_act(void *env, const gw_mlp_actors *net, const float *ws, int training, float tau, uint64_t seed,
+                       uint64_t counter, const float *uniform, const uint16_t *mask, int32_t *actions, float *probs,
+                       float *logits, void *stream) {
+    if (!env || !net || !ws || !actions || !probs) return err(GW_ERR_ARG, "gw_actor_act: null argument");
+    if (reinterpret_cast<uintptr_t>(ws) & 15u) return err(GW_ERR_ARG, "gw_actor_act: ws must be 16-byte aligned");
+    gw_obs_source src;
+    gw_status st = gw_obs_view(env, &src);
+    if (st != GW_OK) return st;
+    if ((st = check_net(src, net, "gw_actor_act")) != GW_OK) return st;
     if (!(tau > 0.0f)) return err(GW_ERR_ARG, "gw_actor_act: tau must be > 0");
     ActParams p;
     p.net = *net;
-    p.c1 = c1_ws;
+    const Ws w = ws_layout(const_cast<float *>(ws), src.K);
+    p.c1 = w.c1;
+    p.w2img = w.w2;
+    p.w3img = w.w3;
     p.desc = src.desc;
     p.base = src.base;
     p.mask = mask;
@@ -383,14 +573,26 @@ gw_status gw_actor_act(void *env, const gw_mlp_actors *net, float *c1_ws, int tr
     p.ctr0 = (uint32_t)counter;
     p.ctr1 = (uint32_t)(counter >> 32);
     for (int k = 0; k < MAXN; ++k) p.apples[k] = src.apples[k];
+    const char *ab = std::getenv("GW_ACT_AB");
+    p.ab = ab ? std::atoi(ab) : 0;
     const int64_t tiles = (src.E + TILE - 1) / TILE;
     p.tiles = (int)tiles;
-    // 2 blocks of 4 waves per CU (77 KB LDS each): 512 resident blocks over the K agents
+    // 2 blocks of 8 waves per CU (~75 KB LDS each): 512 resident blocks over the K agents
     const int64_t want = (tiles + WAVES - 1) / WAVES;
     const int per_agent = (int)std::max<int64_t>(1, std::min<int64_t>(want, std::max(1, 512 / src.K)));
+    const dim3 grid(per_agent, src.K), block(THREADS);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(c1_kernel, dim3(HID / 32, src.K), dim3(256), 0, s, p);
-    hipLaunchKernelGGL(act_kernel, dim3(per_agent, src.K), dim3(THREADS), 0, s, p);
+    switch (src.N) {
+        case 1: hipLaunchKernelGGL(act_kernel<2>, grid, block, 0, s, p); break;
+        case 2: hipLaunchKernelGGL(act_kernel<3>, grid, block, 0, s, p); break;
+        case 3: hipLaunchKernelGGL(act_kernel<4>, grid, block, 0, s, p); break;
+        case 4: hipLaunchKernelGGL(act_kernel<5>, grid, block, 0, s, p); break;
+        case 5: hipLaunchKernelGGL(act_kernel<6>, grid, block, 0, s, p); break;
+        case 6: hipLaunchKernelGGL(act_kernel<7>, grid, block, 0, s, p); break;
+        case 7: hipLaunchKernelGGL(act_kernel<8>, grid, block, 0, s, p); break;
+        case 8: hipLaunchKernelGGL(act_kernel<9>, grid, block, 0, s, p); break;
+        default: return err(GW_ERR_ARG, "gw_actor_act: N out of range");
+    }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return err(GW_ERR_HIP, std::string("gw_actor_act: ") + hipGetErrorString(e));
     return GW_OK;

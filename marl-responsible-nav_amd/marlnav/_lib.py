@@ -61,12 +61,31 @@ def needs_build() -> bool:
         return f.read().strip() != source_hash()
 
 
+def _deps(src: str) -> list:
+    """src and the quoted #include files it pulls in (transitively) from csrc/ and include/."""
+    import re
+    seen, todo = [], [src]
+    while todo:
+        path = todo.pop()
+        if path in seen:
+            continue
+        seen.append(path)
+        with open(path) as f:
+            for name in re.findall(r'^\s*#\s*include\s+"([^"]+)"', f.read(), re.M):
+                for d in (os.path.dirname(path), INCLUDE, CSRC):
+                    cand = os.path.join(d, name)
+                    if os.path.exists(cand):
+                        todo.append(cand)
+                        break
+    return seen
+
+
 def _object(src: str, verbose: bool) -> str:
     """Compile one HIP source to csrc/build/<name>.<hash>.o (hash of the source, every header
     and the flags), reusing an existing object: only the changed translation units rebuild."""
     import hashlib
     h = hashlib.sha256(" ".join(COMPILE_FLAGS).encode())
-    for path in [src, *HEADERS]:
+    for path in _deps(src):
         with open(path, "rb") as f:
             h.update(f.read())
     name = os.path.splitext(os.path.basename(src))[0]
@@ -145,7 +164,8 @@ class GwState(C.Structure):
 
 EXPORTS = ["gw_create", "gw_reset", "gw_step", "gw_state_view", "gw_copy_state", "gw_profile",
            "gw_profile_read", "gw_stats_rows", "gw_dims", "gw_last_error", "gw_destroy", "gw_fear_matrix",
-           "gw_adam_step", "gw_soft_update", "gw_obs_view", "gw_set_last_error", "gw_actor_act"]
+           "gw_adam_step", "gw_soft_update", "gw_obs_view", "gw_set_last_error", "gw_actor_act",
+           "gw_actor_workspace_floats", "gw_actor_prepare"]
 
 
 class GwObsSource(C.Structure):
@@ -197,6 +217,10 @@ def _declare(L):
     L.gw_actor_act.argtypes = [p, C.POINTER(GwMlpActors), p, C.c_int, C.c_float, C.c_uint64, C.c_uint64,
                                p, p, p, p, p, p]
     L.gw_actor_act.restype = C.c_int
+    L.gw_actor_workspace_floats.argtypes = [C.c_int32, C.c_int32]
+    L.gw_actor_workspace_floats.restype = C.c_int64
+    L.gw_actor_prepare.argtypes = [p, C.POINTER(GwMlpActors), p, p]
+    L.gw_actor_prepare.restype = C.c_int
     L.gw_destroy.argtypes = [p]
     L.gw_destroy.restype = None
     return L

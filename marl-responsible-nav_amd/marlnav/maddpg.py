@@ -50,6 +50,7 @@ class FlatAdam:
     the step count on the device (graph-capturable)."""
 
     def __init__(self, net: StackedMLPActors, lr: float, betas=(0.9, 0.999), eps: float = 1e-8):
+        self.net = net
         self.flat = net.flat_params()
         self.m = torch.zeros_like(self.flat)
         self.v = torch.zeros_like(self.flat)
@@ -65,6 +66,7 @@ class FlatAdam:
         _lib.check(self.lib.gw_adam_step(self.flat.data_ptr(), self.flat.grad.data_ptr(), self.m.data_ptr(),
                                          self.v.data_ptr(), self.count.data_ptr(), self.flat.numel(), self.lr,
                                          self.betas[0], self.betas[1], self.eps, s), "gw_adam_step")
+        self.net.epoch += 1  # written behind torch's version counter (see MultiAgentActors.act_env)
 
 
 def _mlp_target(net: StackedMLPActors) -> StackedMLPActors:
@@ -163,6 +165,7 @@ class MADDPG:
             for net, tgt in ((self.actors.net, self.actor_targets.net), (self.critics, self.critic_targets)):
                 t, p = tgt.flat_params(), net.flat_params()
                 _lib.check(lib.gw_soft_update(t.data_ptr(), p.data_ptr(), t.numel(), self.tau, s), "gw_soft_update")
+                tgt.epoch += 1
             return
         src = list(self.actors.parameters()) + list(self.critics.parameters())
         dst = list(self.actor_targets.parameters()) + list(self.critic_targets.parameters())
@@ -193,6 +196,8 @@ class MADDPG:
 
     def replay_learn(self):
         self._graph.replay()
+        for m in (self.actors, self.actor_targets):  # the replayed optimizer / soft update wrote them
+            m.mark_updated()
         return self._graph_out
 
     # ---------------------------------------------------------------------------------------

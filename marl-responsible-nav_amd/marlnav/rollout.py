@@ -115,12 +115,12 @@ class Rollout:
         if self.replay is not None:
             rp = self.replay
             nxt = (self.t + 1) % rp.S
-            r = env.step(actions, obs_out=rp.obs[nxt], final_obs_out=rp.final_obs[cur])
+            # zero-copy: the step writes obs_{t+1}, the terminal obs, the shaped reward and the
+            # dones straight into the ring slots
+            r = env.step(actions, into=dict(obs=rp.obs[nxt], final_obs=rp.final_obs[cur], shaped=rp.reward[cur],
+                                            term=rp.term[cur], done=rp.done[cur]))
             if probs is not None and probs.data_ptr() != rp.probs[cur].data_ptr():
                 rp.probs[cur].copy_(probs)
-            rp.reward[cur].copy_(r.shaped)
-            rp.term[cur].copy_(r.term)
-            rp.done[cur].copy_(r.done)
             rp.t = self.t + 1
             rp.t_dev.add_(1)
         else:

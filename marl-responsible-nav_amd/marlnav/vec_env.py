@@ -136,27 +136,41 @@ class VecGridEnv:
                                          _ptr(self.out["mask"]), self._stream()), "gw_reset")
         return self.out["obs"], self.out["mask"]
 
+    _INTO_SPEC = {"obs": (torch.float32, "KEHW"), "final_obs": (torch.float32, "KEHW"),
+                  "reward": (torch.float64, "EK"), "fear": (torch.float64, "EK"), "shaped": (torch.float64, "EK"),
+                  "term": (torch.uint8, "EK"), "trunc": (torch.uint8, "EK"), "done": (torch.uint8, "E")}
+
     def step(self, rl_actions: torch.Tensor | None = None, scripted: torch.Tensor | None = None,
              spawn: torch.Tensor | None = None, obs_out: torch.Tensor | None = None,
-             final_obs_out: torch.Tensor | None = None) -> StepResult:
+             final_obs_out: torch.Tensor | None = None, into: dict | None = None) -> StepResult:
         """rl_actions [E, K] int32 (None = uniform random RL policy on device);
         scripted [E, N-K] (replay) or None (scenario policy on device);
         spawn [E, N] spawns for auto-resetting envs (replay) or None;
         obs_out / final_obs_out: [K, E, H, W] float32 buffers to write this step's obs into
-        instead of the env's own (e.g. a replay-ring slot: zero-copy replay storage)."""
+        instead of the env's own (e.g. a replay-ring slot: zero-copy replay storage);
+        into: the same for any of obs, final_obs, reward, fear, shaped, term, trunc, done
+        (contiguous tensors of the output's dtype and size)."""
         rl = self._as_i32(rl_actions, (self.E, self.K))
         sa = self._as_i32(scripted, (self.E, self.N - self.K))
         sp = self._as_i32(spawn, (self.E, self.N))
         so = self._step_out
         res = self.out
-        if obs_out is not None or final_obs_out is not None:
+        over = dict(into or {})
+        if obs_out is not None:
+            over["obs"] = obs_out
+        if final_obs_out is not None:
+            over["final_obs"] = final_obs_out
+        if over:
             so = _lib.GwStepOut.from_buffer_copy(self._step_out)
             res = dict(self.out)
-            for name, t in (("obs", obs_out), ("final_obs", final_obs_out)):
-                if t is not None:
-                    assert t.dtype == torch.float32 and t.numel() == self.K * self.E * self.H * self.W
-                    setattr(so, name, _ptr(t))
-                    res[name] = t
+            sizes = {"KEHW": self.K * self.E * self.H * self.W, "EK": self.E * self.K, "E": self.E}
+            for name, t in over.items():
+                dt, shp = self._INTO_SPEC[name]
+                if t.dtype != dt or t.numel() != sizes[shp] or not t.is_contiguous() or t.device != self.device:
+                    raise ValueError(f"step(into={name!r}): need a contiguous {dt} tensor of {sizes[shp]} elements "
+                                     f"on {self.device}")
+                setattr(so, name, _ptr(t))
+                res[name] = t
         with torch.cuda.device(self.device):
             _lib.check(self.lib.gw_step(self.handle, _ptr(rl), _ptr(sa), _ptr(sp), C.byref(so),
                                         self._stream()), "gw_step")

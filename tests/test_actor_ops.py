@@ -148,3 +148,37 @@ def test_rollout_fused_matches_unfused_without_noise():
     assert same == 25
     for e in envs:
         e.close()
+
+
+def test_fused_act_sees_every_weight_update():
+    """The workspace (c1, W2/W3 images) is re-derived after the HIP optimizer, a graph replay of
+    the update, a checkpoint load and a plain in-place torch write."""
+    from marlnav.maddpg import MADDPG
+    from marlnav.rollout import Rollout
+    sc = S.builtin("grid32")
+    env = VecGridEnv(sc, num_envs=512, fear=False, seed=2)
+    learner = MADDPG(sc.K, sc.H, sc.W, device="cuda", seed=1, capturable=True)
+    ro = Rollout(env, learner.actors, replay_slots=8, training=True, seed=3)
+    ro.reset()
+    for _ in range(4):
+        ro.step()
+
+    def agree():
+        u = torch.rand((sc.K, env.E, N_ACTIONS), device="cuda")
+        lk = torch.empty((sc.K, env.E, N_ACTIONS), device="cuda")
+        learner.actors.act_env(env, env.out["mask"], True, uniform=u, logits_out=lk)
+        torch.testing.assert_close(lk, learner.actors(ro._obs_now()), rtol=2e-4, atol=2e-4)  # the ring slot
+
+    agree()
+    learner.learn_from(ro.replay)  # FlatAdam (HIP) on the actors
+    agree()
+    learner.capture(ro.replay)
+    learner.replay_learn()         # graph replay
+    agree()
+    sd = {k: v.clone() for k, v in learner.state_dict().items()}
+    with torch.no_grad():
+        learner.actors.net.weights[1].mul_(-1.5)  # plain in-place write through a layer view
+    agree()
+    learner.load_state_dict(sd)   # checkpoint load
+    agree()
+    env.close()
