@@ -20,9 +20,9 @@ CSRC = os.path.join(PKG_ROOT, "csrc")
 INCLUDE = os.path.join(REPO_ROOT, "include")
 LIB_PATH = os.path.join(CSRC, "libgridenv.so")
 HIP_SOURCES = [os.path.join(CSRC, "gridenv.hip"), os.path.join(CSRC, "learner_ops.hip"),
-               os.path.join(CSRC, "actor_ops.hip")]
+               os.path.join(CSRC, "actor_ops.hip"), os.path.join(CSRC, "rollout_ops.hip")]
 HEADERS = [os.path.join(INCLUDE, "gridenv.h"), os.path.join(INCLUDE, "learner_ops.h"),
-           os.path.join(INCLUDE, "actor_ops.h")]
+           os.path.join(INCLUDE, "actor_ops.h"), os.path.join(INCLUDE, "rollout_ops.h")]
 SOURCES = HIP_SOURCES + HEADERS
 OBJ_DIR = os.path.join(CSRC, "build")
 ARCH = os.environ.get("MARLNAV_OFFLOAD_ARCH", "gfx950")
@@ -165,7 +165,7 @@ class GwState(C.Structure):
 EXPORTS = ["gw_create", "gw_reset", "gw_step", "gw_state_view", "gw_copy_state", "gw_profile",
            "gw_profile_read", "gw_stats_rows", "gw_dims", "gw_last_error", "gw_destroy", "gw_fear_matrix",
            "gw_adam_step", "gw_soft_update", "gw_obs_view", "gw_set_last_error", "gw_actor_act",
-           "gw_actor_workspace_floats", "gw_actor_prepare"]
+           "gw_actor_workspace_floats", "gw_actor_prepare", "gw_rollout_tick"]
 
 
 class GwObsSource(C.Structure):
@@ -221,6 +221,8 @@ def _declare(L):
     L.gw_actor_workspace_floats.restype = C.c_int64
     L.gw_actor_prepare.argtypes = [p, C.POINTER(GwMlpActors), p, p]
     L.gw_actor_prepare.restype = C.c_int
+    L.gw_rollout_tick.argtypes = [p, C.c_int64, C.c_int32, p, p, p, p]
+    L.gw_rollout_tick.restype = C.c_int
     L.gw_destroy.argtypes = [p]
     L.gw_destroy.restype = None
     return L

@@ -55,15 +55,40 @@ class StatsReducer:
         self.totals = torch.zeros(n_fields, dtype=torch.float64, device=device)
         self._pending = None
         self.distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+        self._bufs = [torch.zeros(n_fields, dtype=torch.float64, device=device) for _ in range(2)]
+        self._flip = 0
 
-    def push(self, partials: torch.Tensor):
+    def push(self, partials: torch.Tensor, counter: torch.Tensor | None = None):
+        """Fold one step's [rows, F] partial sums in; ``counter`` (int64 device scalar, e.g. the
+        replay ring's step count) is incremented in the same launch.  On the GPU this is ONE
+        gw_rollout_tick launch (include/rollout_ops.h); CPU tensors (gloo tests) use torch ops."""
         self._drain()
-        local = partials.sum(0) if partials.dim() == 2 else partials.clone()
+        if partials.dim() == 1:
+            partials = partials.unsqueeze(0)
+        if partials.is_cuda:
+            import ctypes as C
+            from . import _lib
+            lib = _lib.load()
+            buf = self._bufs[self._flip] if self.distributed else None
+            self._flip ^= 1
+            assert partials.dtype == torch.float64 and partials.is_contiguous()
+            assert counter is None or (counter.dtype == torch.int64 and counter.is_cuda)
+            _lib.check(lib.gw_rollout_tick(partials.data_ptr(), partials.shape[0], partials.shape[1],
+                                           buf.data_ptr() if buf is not None else None,
+                                           None if self.distributed else self.totals.data_ptr(),
+                                           counter.data_ptr() if counter is not None else None,
+                                           C.c_void_p(torch.cuda.current_stream(partials.device).cuda_stream)),
+                       "gw_rollout_tick")
+            local = buf
+        else:
+            local = partials.sum(0)
+            if counter is not None:
+                counter.add_(1)
+            if not self.distributed:
+                self.totals += local
         if self.distributed:
             work = dist.all_reduce(local, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
             self._pending = (work, local)
-        else:
-            self.totals += local
 
     def _drain(self):
         if self._pending is not None:

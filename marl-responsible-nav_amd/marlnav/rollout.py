@@ -122,12 +122,16 @@ class Rollout:
             if probs is not None and probs.data_ptr() != rp.probs[cur].data_ptr():
                 rp.probs[cur].copy_(probs)
             rp.t = self.t + 1
-            rp.t_dev.add_(1)
         else:
             r = env.step(actions)
         self.t += 1
+        tick = self.replay.t_dev if self.replay is not None else None
         if self.reducer is not None:
-            self.reducer.push(r.stats)  # per-step (RCCL) reduction of the episode statistics
+            # per-step (RCCL) reduction of the episode statistics; the ring's device step count
+            # advances in the same launch
+            self.reducer.push(r.stats, counter=tick)
+        elif tick is not None:
+            tick.add_(1)
         return r
 
     def totals(self) -> dict:

@@ -222,3 +222,24 @@ def test_single_agent_facade_matches_oracle():
             np.testing.assert_array_equal(obs, o_obs[0].reshape(10, 16))
             ep_r, ep_l = 0.0, 0
     assert episode > 3 and seen_bonus
+
+
+def test_rollout_tick_reduces_partials_and_counts():
+    """gw_rollout_tick (include/rollout_ops.h) == torch row sum (deterministic order, f64)."""
+    from marlnav.parallel import StatsReducer
+    g = torch.Generator(device="cuda").manual_seed(4)
+    red = StatsReducer(8, "cuda")
+    ctr = torch.zeros((), dtype=torch.int64, device="cuda")
+    want = torch.zeros(8, dtype=torch.float64, device="cuda")
+    for rows in (1, 7, 512, 2561):
+        p = torch.randn((rows, 8), dtype=torch.float64, device="cuda", generator=g)
+        red.push(p, counter=ctr)
+        want += p.sum(0)
+    torch.testing.assert_close(red.result(), want, rtol=1e-12, atol=1e-12)
+    assert int(ctr) == 4
+    again = StatsReducer(8, "cuda")
+    again.push(p)
+    first = again.result().clone()
+    again2 = StatsReducer(8, "cuda")
+    again2.push(p)
+    assert torch.equal(first, again2.result())  # bit-identical run to run

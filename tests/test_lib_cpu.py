@@ -14,7 +14,8 @@ from marlnav import scenario as S
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(REPO, "include", "gridenv.h")
-HEADERS = [HEADER, os.path.join(REPO, "include", "learner_ops.h"), os.path.join(REPO, "include", "actor_ops.h")]
+HEADERS = [HEADER, os.path.join(REPO, "include", "learner_ops.h"), os.path.join(REPO, "include", "actor_ops.h"),
+           os.path.join(REPO, "include", "rollout_ops.h")]
 
 
 def declared_functions():
