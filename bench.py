@@ -108,6 +108,10 @@ def main():
                     help="bracket every n-th timed step's kernels with HIP events (0 = none); the "
                          "events themselves cost ~2-3 us per kernel boundary, so not every step")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--sync-obs", action="store_true",
+                    help="write each step's obs before the next step starts (no step pipeline; A/B)")
+    ap.add_argument("--obs-lazy", action="store_true",
+                    help="launch each step's obs writer at the next step (gw_set_obs_async 2; A/B)")
     args = ap.parse_args()
 
     import torch
@@ -125,6 +129,10 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     cfg = dict(CONFIGS[args.config])
+    # obs writer pipelined with the next step (gw_set_obs_async): right after the world update
+    # for the env-only workloads; launched at the next step (behind the fused actor, which would
+    # otherwise lose CUs to it) for the full rollout.  Measured A/B: profiles/r1_async/
+    obs_mode = False if args.sync_obs else ("lazy" if (args.obs_lazy or cfg.get("rollout")) else True)
     if args.envs:
         cfg["envs"] = args.envs
     if args.fear >= 0:
@@ -152,12 +160,14 @@ def main():
         from marlnav.maddpg import MADDPG
         from marlnav.rollout import Rollout
         learner = MADDPG(K, env.H, env.W, device=env.device, seed=rank, capturable=True)
-        ro = Rollout(env, learner.actors, replay_slots=-(-200_000 // E) + 1, training=True, seed=rank)
+        ro = Rollout(env, learner.actors, replay_slots=-(-200_000 // E) + 1, training=True, seed=rank,
+                     obs_async=obs_mode)
         ro.reset()
 
         def one_step(i):  # noqa: F811
             r = ro.step()  # the StatsReducer inside does the per-step all-reduce across ranks
             if args.updates_per_step and ro.replay.t >= 2:
+                ro.fence()  # sampling reads the ring's obs slots
                 if learner._graph is None:
                     learner.capture(ro.replay)
                 for _ in range(args.updates_per_step):
@@ -165,6 +175,7 @@ def main():
             return r
 
     if not cfg.get("rollout"):
+        env.set_obs_async(obs_mode)
         env.reset()
     for i in range(args.warmup):
         one_step(i)
@@ -183,6 +194,7 @@ def main():
         if pe > 0:
             env.profile(i % pe == 0)
         r = one_step(i)
+    env.obs_fence()  # the last step's obs writes belong to the timed region
     ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -240,11 +252,15 @@ def main():
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "bytes_per_launch": bytes_per_launch, "avg_launch_ms": dur},
+                         "bytes_per_launch": bytes_per_launch, "avg_launch_ms": dur,
+                         # every algorithmic byte of a whole step (state + obs) over the wall time
+                         # per step: what the pipelined steps sustain end to end
+                         "step_level_GBps": (step_b + obs_b) * E / (t_max / args.steps) / 1e9},
             "kernels_ms": {"profiled_steps": nprof, "step_kernel": avg_step_ms, "obs_kernel": avg_obs_ms, "fear_kernel": avg_fear_ms,
                            "kernel_path": os.environ.get("GW_KERNEL", "defer"),
                            "stream_ms_per_step": gpu_ms / args.steps,
-                           "pipeline_chunks": int(os.environ.get("GW_CHUNKS", "1")) if not env.fused else 1},
+                           "pipeline_chunks": int(os.environ.get("GW_CHUNKS", "1")) if not env.fused else 1,
+                           "obs_async": obs_mode},
             "last_step_episodes": {"completed": stats[1], "mean_return": stats[0] / max(stats[1], 1.0),
                          "mean_len": stats[6] / max(stats[1], 1.0)},
         }

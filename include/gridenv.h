@@ -162,7 +162,7 @@ int64_t gw_stats_rows(void *env);
  * on it without reading it back (actor_ops.h): the static step-encoding map plus, per env, a
  * 48-byte descriptor (agent cells, reset / apple flags; ma_customenv.py:197-209, 303-322).
  * Device pointers owned by the handle, valid until gw_destroy; contents change with every
- * gw_reset / gw_step (stream-ordered). */
+ * gw_reset / gw_step (stream-ordered; with async obs the desc pointer alternates per step). */
 typedef struct gw_obs_source {
     const uint32_t *desc;      /* [E][12] u32: words 0-3 agent cells (16 bits each), word 4
                                   flags (bit 0 reset encoding, bits 8-15 apples present)      */
@@ -172,6 +172,21 @@ typedef struct gw_obs_source {
     int64_t E, env_offset;
 } gw_obs_source;
 gw_status gw_obs_view(void *env, gw_obs_source *out);
+
+/* Async observation writes (a software pipeline across steps; default off).  While enabled,
+ * gw_step enqueues the world update (+ FeAR) on an internal stream that waits for the caller's
+ * prior work on `stream`, and `stream` joins it: rewards, dones, masks, state and stats are
+ * stream-ordered as in the synchronous mode.  The observation writer of the step runs on a
+ * second internal stream and overlaps the NEXT step's world update (which reads only the
+ * state).  The obs / final_obs buffers of a step are therefore ready on `stream` only after
+ * gw_obs_fence(env, stream) (or gw_reset, which fences itself).  The obs descriptor alternates
+ * between two buffers: re-read gw_obs_view after every gw_step.  Disabling drains the writer.
+ * enable = 1: the writer starts right after the step's world update; enable = 2 (lazy): it is
+ * launched at the start of the next gw_step (behind the caller's work between the steps, e.g.
+ * an actor kernel that should not share the CUs with it) or at a fence.
+ * Only the split / defer kernel paths pipeline; the others stay synchronous. */
+gw_status gw_set_obs_async(void *env, int enable);
+gw_status gw_obs_fence(void *env, void *stream);
 /* Set the thread-local error text returned by gw_last_error (for the library's other
  * translation units: learner_ops, actor_ops). */
 void gw_set_last_error(const char *msg);

@@ -1038,20 +1038,27 @@ __device__ __forceinline__ float agent_value(bool reset, int n, int k, bool on_a
 template <bool VEC4, bool NT>
 __global__ void __launch_bounds__(OBS_THREADS) obs_kernel(Params p, float *__restrict__ obs,
                                                           float *__restrict__ final_obs) {
-    __shared__ uint32_t s_road[128];                   // road bitmask of the map (HW <= 4096)
-    __shared__ int s_pc[2][OBS_BE][MAXN][MAXN + 1];    // [which][env][k][patch] cell (-1 none)
-    __shared__ float s_pv[2][OBS_BE][MAXN][MAXN + 1];
-    __shared__ uint32_t s_flag[OBS_BE];
+    // LDS sized to the launch (obs_lds_bytes): road bitmask, flags, then per (which, env, k)
+    // N + 1 patch cells and values.  Small (640 B at 32x32, N = 4, K = 2, 4 envs), so obs blocks
+    // never take the LDS a co-resident kernel (the fused actor, 2 x 78 KB per CU) needs.
+    extern __shared__ uint32_t obs_lds[];
     const int tid = threadIdx.x;
     const int HW = p.HW, N = p.N, K = p.K;
+    const int npatch = N + 1;
+    const int nroad = (HW + 31) / 32;
+    uint32_t *s_road = obs_lds;
+    uint32_t *s_flag = s_road + nroad;
+    int *s_pc = reinterpret_cast<int *>(s_flag + OBS_BE);          // [2][obs_be][K][npatch]
+    float *s_pv = reinterpret_cast<float *>(s_pc + 2 * p.obs_be * K * npatch);
     const int64_t e0 = p.e_begin + (int64_t)blockIdx.x * p.obs_be;
     if (e0 >= p.e_end) return;  // uniform per block
     const int nenv = (int)min((int64_t)p.obs_be, p.e_end - e0);
-    for (int w = tid; w < (HW + 31) / 32; w += OBS_THREADS) s_road[w] = p.tb.roadbits[w];
+    for (int w = tid; w < nroad; w += OBS_THREADS) s_road[w] = p.tb.roadbits[w];
     // patches: one thread per (which, env, k)
-    if (tid < 2 * OBS_BE * MAXN) {
-        const int which = tid / (OBS_BE * MAXN), el = (tid / MAXN) % OBS_BE, k = tid % MAXN;
-        if (el < nenv && k < K) {
+    if (tid < 2 * p.obs_be * K) {
+        const int which = tid / (p.obs_be * K), el = (tid / K) % p.obs_be, k = tid % K;
+        const int slot = ((which * p.obs_be + el) * K + k) * npatch;
+        if (el < nenv) {
             const uint32_t *d = p.desc + (e0 + el) * NDESC;
             const uint32_t f = d[4];
             if (k == 0 && which == 0) s_flag[el] = f;
@@ -1063,23 +1070,22 @@ __global__ void __launch_bounds__(OBS_THREADS) obs_kernel(Params p, float *__res
             if (ac >= 0) {  // apple first, agents override it
                 float av = p.tb.base[ac] + 9.0f;
                 if (!reset && av == (float)(k + 1)) av = 1.0f;  // relabel of :321 (apple on a wall, K = 8)
-                s_pc[which][el][k][np] = ac;
-                s_pv[which][el][k][np] = av;
+                s_pc[slot + np] = ac;
+                s_pv[slot + np] = av;
                 ++np;
             }
             for (int n = 0; n < N; ++n) {
                 const int c = (int)((pw[n >> 1] >> (16 * (n & 1))) & 0xFFFFu);
-                s_pc[which][el][k][np] = c;
-                s_pv[which][el][k][np] = agent_value(reset, n, k, c == ac, p.variant);
+                s_pc[slot + np] = c;
+                s_pv[slot + np] = agent_value(reset, n, k, c == ac, p.variant);
                 ++np;
             }
-            for (; np <= MAXN; ++np) s_pc[which][el][k][np] = -1;
+            for (; np < npatch; ++np) s_pc[slot + np] = -1;
         }
     }
     if (tid < OBS_BE && tid >= nenv) s_flag[tid] = 0;
     __syncthreads();
 
-    const int npatch = N + 1;
     for (int which = 0; which < 2; ++which) {
         float *dst = which == 0 ? obs : final_obs;
         if (!dst) continue;
@@ -1099,10 +1105,11 @@ __global__ void __launch_bounds__(OBS_THREADS) obs_kernel(Params p, float *__res
                     v.y = (rb & 2u) ? 0.0f : -1.0f;
                     v.z = (rb & 4u) ? 0.0f : -1.0f;
                     v.w = (rb & 8u) ? 0.0f : -1.0f;
+                    const int slot = ((which * p.obs_be + el) * K + k) * npatch;
                     for (int q = 0; q < npatch; ++q) {
-                        const int dd = s_pc[which][el][k][q] - c0;
+                        const int dd = s_pc[slot + q] - c0;
                         if ((unsigned)dd < 4u) {
-                            const float pv = s_pv[which][el][k][q];
+                            const float pv = s_pv[slot + q];
                             v.x = dd == 0 ? pv : v.x;
                             v.y = dd == 1 ? pv : v.y;
                             v.z = dd == 2 ? pv : v.z;
@@ -1124,8 +1131,9 @@ __global__ void __launch_bounds__(OBS_THREADS) obs_kernel(Params p, float *__res
                     if (!(s_flag[el] & need)) continue;
                     const int c = i - el * HW;
                     float v = ((s_road[c >> 5] >> (c & 31)) & 1u) ? 0.0f : -1.0f;
+                    const int slot = ((which * p.obs_be + el) * K + k) * npatch;
                     for (int q = 0; q < npatch; ++q)
-                        if (s_pc[which][el][k][q] == c) v = s_pv[which][el][k][q];
+                        if (s_pc[slot + q] == c) v = s_pv[slot + q];
                     o[i] = v;
                 }
             }
@@ -1843,6 +1851,22 @@ struct Env {
     hipStream_t aux = nullptr;      // second stream of the pipeline (created on first use)
     hipStream_t aux2 = nullptr;     // third stream: obs_kernel of the chunked defer pipeline
     std::vector<hipEvent_t> sync_ev;  // fork/chunk/join events (timing disabled)
+    // async obs (gw_set_obs_async): obs_kernel of step t runs on obs_stream while the world update
+    // of step t+1 runs; the descriptor is double-buffered (desc_buf[dcur] = the latest step's)
+    // (launched lazily: at the start of gw_step t+1, behind the caller's work between the steps,
+    // e.g. the fused actor, so the writer never competes with it for the CUs; or at a fence)
+    bool obs_async = false;
+    bool obs_lazy = false;                        // gw_set_obs_async(env, 2): launch at the next step
+    hipStream_t obs_stream = nullptr;
+    hipEvent_t obs_done[2] = {nullptr, nullptr};  // obs_kernel that read desc_buf[i] has finished
+    bool obs_pending[2] = {false, false};
+    hipEvent_t world_ev = nullptr;                // world update of the queued step has finished
+    bool obs_queued = false;                      // an obs_kernel launch waits in qobs
+    bool qobs_prof = false;                       // profiling state of the step that queued it
+    int qobs_buf = 0;
+    gw::Params qobs;
+    uint32_t *desc_buf[2] = {nullptr, nullptr};
+    int dcur = 0;
     // tables
     uint8_t *okmask = nullptr, *policy = nullptr, *mdr = nullptr;
     double *cdf = nullptr, *resp = nullptr;
@@ -1881,6 +1905,59 @@ gw_status ensure_aux(Env *env, int n) {
         env->sync_ev.push_back(e);
     }
     if (!env->aux2) HIP_TRY(hipStreamCreateWithFlags(&env->aux2, hipStreamNonBlocking));
+    return GW_OK;
+}
+
+// the async-obs stream (normal priority; the world update and FeAR go to the high-priority aux
+// stream) and its per-descriptor-buffer completion events, created on first use
+gw_status ensure_obs_stream(Env *env) {
+    const gw_status st = ensure_aux(env, 3);
+    if (st != GW_OK) return st;
+    if (!env->obs_stream) HIP_TRY(hipStreamCreateWithFlags(&env->obs_stream, hipStreamNonBlocking));
+    for (hipEvent_t &e : env->obs_done)
+        if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (!env->world_ev) HIP_TRY(hipEventCreateWithFlags(&env->world_ev, hipEventDisableTiming));
+    return GW_OK;
+}
+
+hipError_t launch_obs(const Env *env, const gw::Params &p, float *obs, float *final_obs, hipStream_t s);
+hipEvent_t next_event(Env *env);
+
+// launch the queued obs_kernel on the obs stream, after its world update and (after != null)
+// after the caller's work up to `after`
+gw_status flush_obs(Env *env, hipEvent_t after) {
+    if (!env->obs_queued) return GW_OK;
+    hipStream_t os = env->obs_stream;
+    HIP_TRY(hipStreamWaitEvent(os, env->world_ev, 0));
+    if (after) HIP_TRY(hipStreamWaitEvent(os, after, 0));
+    const bool prof = env->qobs_prof;  // timed iff the step that queued it was
+    size_t b = env->ev_used;
+    if (prof) {
+        hipEvent_t e = next_event(env);
+        if (!e) return fail(GW_ERR_HIP, "hipEventCreate failed");
+        HIP_TRY(hipEventRecord(e, os));
+    }
+    HIP_TRY(launch_obs(env, env->qobs, env->qobs.out.obs, env->qobs.out.final_obs, os));
+    if (prof) {
+        hipEvent_t e = next_event(env);
+        if (!e) return fail(GW_ERR_HIP, "hipEventCreate failed");
+        HIP_TRY(hipEventRecord(e, os));
+        env->spans.push_back({b, env->ev_used - 1, 1});
+    }
+    HIP_TRY(hipEventRecord(env->obs_done[env->qobs_buf], os));
+    env->obs_pending[env->qobs_buf] = true;
+    env->obs_queued = false;
+    return GW_OK;
+}
+
+// launch a queued obs_kernel and make `s` wait for every obs_kernel of the async-obs stream
+gw_status wait_obs(Env *env, hipStream_t s) {
+    if (env->obs_queued) {
+        const gw_status st = flush_obs(env, nullptr);
+        if (st != GW_OK) return st;
+    }
+    for (int i = 0; i < 2; ++i)
+        if (env->obs_pending[i]) HIP_TRY(hipStreamWaitEvent(s, env->obs_done[i], 0));
     return GW_OK;
 }
 
@@ -2093,13 +2170,16 @@ hipError_t launch_obs(const Env *env, const gw::Params &p, float *obs, float *fi
     const int64_t n = p.e_end - p.e_begin;
     if (n <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((n + env->obs_be - 1) / env->obs_be);
+    // obs_kernel's LDS: road bitmask, OBS_BE flags, [2][obs_be][K][N + 1] patch cells + values
+    const size_t lds = sizeof(uint32_t) * ((env->HW + 31) / 32 + gw::OBS_BE) +
+                       (size_t)2 * 2 * env->obs_be * env->K * (env->N + 1) * sizeof(uint32_t);
     if (env->HW % 4 == 0) {
         if (env->obs_nt)
-            hipLaunchKernelGGL((gw::obs_kernel<true, true>), dim3(grid), dim3(gw::OBS_THREADS), 0, s, p, obs, final_obs);
+            hipLaunchKernelGGL((gw::obs_kernel<true, true>), dim3(grid), dim3(gw::OBS_THREADS), lds, s, p, obs, final_obs);
         else
-            hipLaunchKernelGGL((gw::obs_kernel<true, false>), dim3(grid), dim3(gw::OBS_THREADS), 0, s, p, obs, final_obs);
+            hipLaunchKernelGGL((gw::obs_kernel<true, false>), dim3(grid), dim3(gw::OBS_THREADS), lds, s, p, obs, final_obs);
     } else {
-        hipLaunchKernelGGL((gw::obs_kernel<false, false>), dim3(grid), dim3(gw::OBS_THREADS), 0, s, p, obs, final_obs);
+        hipLaunchKernelGGL((gw::obs_kernel<false, false>), dim3(grid), dim3(gw::OBS_THREADS), lds, s, p, obs, final_obs);
     }
     return hipGetLastError();
 }
@@ -2258,7 +2338,7 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
         (st = dalloc(env, &env->free_cells, freec.size())) || (st = dalloc(env, &env->base, HW)) ||
         (st = dalloc(env, &env->pos, (size_t)N * E)) || (st = dalloc(env, &env->t, E)) ||
         (st = dalloc(env, &env->prev, (size_t)K * E)) || (st = dalloc(env, &env->flags, E)) ||
-        (st = dalloc(env, &env->episode, E)) || (st = dalloc(env, &env->desc, E * gw::NDESC)) ||
+        (st = dalloc(env, &env->episode, E)) || (st = dalloc(env, &env->desc, 2 * E * gw::NDESC)) ||
         (st = dalloc(env, &env->score, E)) || (st = dalloc(env, &env->fscore, E)) ||
         (st = dalloc(env, &env->celltab, HW)) || (st = dalloc(env, &env->roadbits, rbits.size())) ||
         (env->mode == 3 && env->fear && (st = dalloc(env, &env->fwork, E * (N <= 4 ? 1 : 2)))))
@@ -2277,7 +2357,9 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
     CP(env->roadbits, rbits.data(), sizeof(uint32_t) * rbits.size());
 #undef CP
     if (he == hipSuccess) he = hipMemset(env->episode, 0xFF, sizeof(uint32_t) * E);  // first reset -> 0
-    if (he == hipSuccess) he = hipMemset(env->desc, 0, sizeof(uint32_t) * E * gw::NDESC);
+    if (he == hipSuccess) he = hipMemset(env->desc, 0, sizeof(uint32_t) * 2 * E * gw::NDESC);
+    env->desc_buf[0] = env->desc;
+    env->desc_buf[1] = env->desc + E * gw::NDESC;
     if (he == hipSuccess) he = hipDeviceSynchronize();
     if (he != hipSuccess) return cleanup(fail(GW_ERR_HIP, std::string("init: ") + hipGetErrorString(he)));
     *out_env = env;
@@ -2293,6 +2375,7 @@ gw_status gw_reset(void *handle, const uint8_t *env_mask, const int32_t *spawn_c
     p.spawn = spawn_cells;
     p.out.mask = mask;
     hipStream_t s = static_cast<hipStream_t>(stream);
+    GW_TRY(wait_obs(env, s));  // async obs: the descriptors are rewritten in place below
     HIP_TRY(dispatch_reset(env, p, s));
     HIP_TRY(launch_obs(env, p, obs, nullptr, s));
     env->initialized = true;
@@ -2333,6 +2416,42 @@ gw_status gw_step(void *handle, const int32_t *rl_actions, const int32_t *script
     const bool defer = env->mode == 3 && env->fear;
     const int nch = ((env->mode == 1 || defer) && want_obs && env->chunks > 1 && env->E >= unit * env->chunks)
                         ? env->chunks : 1;
+    if (env->obs_async && want_obs && nch == 1 && (env->mode == 1 || env->mode == 3)) {
+        // Software pipeline over steps.  The world update (and FeAR) of step t runs on the
+        // high-priority aux stream after the caller's prior work on s, and s joins it (rewards,
+        // dones, masks, state, stats: stream-ordered as usual).  The obs writer of step t runs
+        // on obs_stream right after the world update (eager), or is queued and launched at the
+        // start of step t+1 behind the caller's work in between (lazy), and overlaps FeAR and
+        // the world update + FeAR of step t+1, which read only the state.  The descriptor is double-buffered: step t writes
+        // desc_buf[nb]; obs_kernel(t-2) read that buffer, so the world update waits for it.
+        GW_TRY(ensure_obs_stream(env));
+        HIP_TRY(hipEventRecord(env->sync_ev[0], s));  // fork: the caller's prior work on s
+        GW_TRY(flush_obs(env, env->sync_ev[0]));       // obs_kernel(t-1)
+        const int nb = env->dcur ^ 1;
+        p.desc = env->desc_buf[nb];
+        size_t b;
+        HIP_TRY(hipStreamWaitEvent(env->aux, env->sync_ev[0], 0));
+        if (env->obs_pending[nb]) HIP_TRY(hipStreamWaitEvent(env->aux, env->obs_done[nb], 0));
+        GW_TRY(span_begin(env->aux, b));
+        HIP_TRY(dispatch_step(env, p, env->aux));
+        GW_TRY(span_end(env->aux, b, 0));
+        HIP_TRY(hipEventRecord(env->world_ev, env->aux));
+        if (defer) {
+            GW_TRY(span_begin(env->aux, b));
+            HIP_TRY(dispatch_fear(env, p, env->aux));
+            GW_TRY(span_end(env->aux, b, 2));
+        }
+        HIP_TRY(hipEventRecord(env->sync_ev[2], env->aux));  // join the world update + FeAR
+        HIP_TRY(hipStreamWaitEvent(s, env->sync_ev[2], 0));
+        env->qobs = p;
+        env->qobs_buf = nb;
+        env->qobs_prof = env->profiling;
+        env->obs_queued = true;
+        if (!env->obs_lazy) GW_TRY(flush_obs(env, nullptr));  // eager: right after the world update
+        env->dcur = nb;
+        env->desc = env->desc_buf[nb];
+        return GW_OK;
+    }
     if (defer && (nch == 1 || env->defer_order == 0)) {
         // world update; then fear_v2 on the aux stream || obs_kernel on s; join
         size_t b;
@@ -2428,6 +2547,27 @@ gw_status gw_step(void *handle, const int32_t *rl_actions, const int32_t *script
     }
     HIP_TRY(hipEventRecord(env->sync_ev[nch + 1], env->aux));  // join
     HIP_TRY(hipStreamWaitEvent(s, env->sync_ev[nch + 1], 0));
+    return GW_OK;
+}
+
+gw_status gw_set_obs_async(void *handle, int enable) {
+    Env *env = static_cast<Env *>(handle);
+    if (!env) return fail(GW_ERR_ARG, "null env");
+    if (!enable && env->obs_async && env->obs_stream) {
+        // the synchronous path writes the current descriptor buffer in place: drain the writer
+        GW_TRY(flush_obs(env, nullptr));
+        HIP_TRY(hipStreamSynchronize(env->obs_stream));
+        env->obs_pending[0] = env->obs_pending[1] = false;
+    }
+    env->obs_async = enable != 0;
+    env->obs_lazy = enable == 2;
+    return GW_OK;
+}
+
+gw_status gw_obs_fence(void *handle, void *stream) {
+    Env *env = static_cast<Env *>(handle);
+    if (!env) return fail(GW_ERR_ARG, "null env");
+    GW_TRY(wait_obs(env, static_cast<hipStream_t>(stream)));
     return GW_OK;
 }
 
@@ -2578,6 +2718,10 @@ void gw_destroy(void *handle) {
     for (hipEvent_t e : env->sync_ev) (void)hipEventDestroy(e);
     if (env->aux) (void)hipStreamDestroy(env->aux);
     if (env->aux2) (void)hipStreamDestroy(env->aux2);
+    if (env->obs_stream) (void)hipStreamDestroy(env->obs_stream);
+    for (hipEvent_t e : env->obs_done)
+        if (e) (void)hipEventDestroy(e);
+    if (env->world_ev) (void)hipEventDestroy(env->world_ev);
     for (void *p : env->allocs) (void)hipFree(p);
     delete env;
 }

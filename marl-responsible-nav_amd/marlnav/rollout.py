@@ -66,10 +66,14 @@ class ReplayRing:
 
 class Rollout:
     def __init__(self, env: VecGridEnv, actors: MultiAgentActors | None = None, replay_slots: int = 0,
-                 training: bool = True, group=None, seed: int = 0, fused: bool | None = None):
+                 training: bool = True, group=None, seed: int = 0, fused: bool | None = None,
+                 obs_async: bool = False):
         """fused: get_action as the one-kernel gw_actor_act over the env's obs descriptors
         (default when the actors are the f32 128-128 MLP), else the PyTorch forward over the
-        dense obs with torch's Gumbel noise."""
+        dense obs with torch's Gumbel noise.
+        obs_async: pipeline the env's obs writes (the replay ring's obs slots) with the next
+        step's actor + world update (VecGridEnv.set_obs_async); whoever reads the obs or the ring
+        afterwards calls ``fence()`` first (the learner does)."""
         self.env = env
         self.actors = actors
         self.fused = (actors is not None and actors.fusable(env)) if fused is None else bool(fused)
@@ -82,6 +86,12 @@ class Rollout:
         self.gen = torch.Generator(device=env.device).manual_seed(seed) if actors is not None else None
         self.t = 0
         self.reducer = StatsReducer(_lib.GW_STATS, env.device, group) if env.out.get("stats") is not None else None
+        env.set_obs_async(obs_async)
+
+    def fence(self):
+        """Order the observations written so far (ring slots / env obs) before later work on
+        the current stream (a no-op unless obs_async)."""
+        self.env.obs_fence()
 
     def reset(self):
         if self.replay is not None:
@@ -109,6 +119,7 @@ class Rollout:
                                                  actions_out=self._actions, probs_out=probs_out)
             self._calls += 1
         elif self.actors is not None:
+            self.env.obs_fence()  # the PyTorch forward reads the dense obs
             actions, probs = self.actors.act(self._obs_now(), mask, self.training, generator=self.gen)
         else:
             actions, probs = None, None  # device-RNG random policy

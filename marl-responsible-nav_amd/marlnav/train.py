@@ -28,7 +28,10 @@ class MADDPGTrainer:
                  updates_per_step: int | None = None, graph: bool = True, seed: int = 0):
         self.env, self.m = env, maddpg
         slots = max(2, -(-memory_size // env.E) + 1)
-        self.rollout = Rollout(env, maddpg.actors, replay_slots=slots, training=True, seed=seed)
+        # obs writes pipelined with the next step when the actor is the fused op (it never reads
+        # the dense obs), launched behind it ("lazy"); the ring is fenced before every learn
+        self.rollout = Rollout(env, maddpg.actors, replay_slots=slots, training=True, seed=seed,
+                               obs_async="lazy" if maddpg.actors.fusable(env) else False)
         self.learning_delay = learning_delay
         self.updates_per_step = updates_per_step
         self.use_graph = graph and env.device.type == "cuda"
@@ -41,6 +44,7 @@ class MADDPGTrainer:
         self.rollout.reset()
 
     def _learn(self):
+        self.rollout.fence()  # the sampled transitions read the ring's obs slots
         if self.use_graph:
             if self.m._graph is None:
                 self.m.capture(self.rollout.replay)

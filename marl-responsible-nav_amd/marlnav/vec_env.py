@@ -119,6 +119,7 @@ class VecGridEnv:
         )
         self._step_out = _lib.GwStepOut(*[_ptr(self.out[n]) for n in _lib.STEP_OUT_FIELDS])
         self._closed = False
+        self.obs_async = False
         self.fused = (sc.HW % 4 == 0) and os.environ.get("GW_KERNEL", "split") == "fused"
 
     # ------------------------------------------------------------------------------------
@@ -234,6 +235,22 @@ class VecGridEnv:
                                                                          "feal_va")], self._stream()),
                        "gw_fear_matrix")
         return out
+
+    def set_obs_async(self, enable: bool | str = True):
+        """Pipeline the obs writer of step t with the world update of step t+1 (gw_set_obs_async).
+        While on, ``step``'s obs / final_obs are ready on the current stream only after
+        ``obs_fence()`` (rewards, dones, masks and state are ordered as usual).
+        enable="lazy": the writer is launched at the next step, behind the caller's work between
+        the steps (an actor kernel), instead of right after the world update."""
+        mode = 2 if enable == "lazy" else int(bool(enable))
+        _lib.check(self.lib.gw_set_obs_async(self.handle, mode), "gw_set_obs_async")
+        self.obs_async = bool(mode)
+
+    def obs_fence(self):
+        """Order the last step's obs before later work on the current stream (async obs)."""
+        if self.obs_async:
+            with torch.cuda.device(self.device):
+                _lib.check(self.lib.gw_obs_fence(self.handle, self._stream()), "gw_obs_fence")
 
     def profile(self, enable: bool = True):
         """Record HIP events around each gw_step kernel (see gw_profile)."""

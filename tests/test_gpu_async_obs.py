@@ -1,0 +1,95 @@
+"""Async obs writes (gw_set_obs_async: the obs writer of step t overlaps the world update of
+step t+1, descriptors double-buffered) == the synchronous path, bit for bit.
+
+No host synchronisation inside the stepping loops: every step's obs goes to its own slot and
+every other output is cloned on the caller's stream right after the step, so a missing
+dependency (descriptor WAR, join, fence) shows up as a mismatch instead of being hidden by
+an idle GPU.  The synchronous path itself is pinned to the oracle in test_gpu_parity.py.
+"""
+import pytest
+import torch
+
+from marlnav import scenario as S
+from marlnav.vec_env import VecGridEnv
+
+pytestmark = pytest.mark.gpu
+
+OUTS = ("reward", "fear", "shaped", "term", "trunc", "done", "mask", "ep_return", "actions", "final_pos")
+
+
+@pytest.mark.parametrize("path,fear,name,mode", [("defer", True, "grid32", True), ("defer", False, "grid32", True),
+                                                 ("split", True, "grid32", True), ("defer", True, "grid64_n8", True),
+                                                 ("defer", True, "grid32", "lazy"), ("split", False, "grid32", "lazy")])
+def test_async_obs_matches_sync(path, fear, name, mode, monkeypatch):
+    monkeypatch.setenv("GW_KERNEL", path)
+    monkeypatch.setenv("GW_CHUNKS", "1")
+    sc = S.builtin(name)
+    E, T = (4096, 24) if name == "grid32" else (1024, 12)
+    mk = lambda: VecGridEnv(sc, num_envs=E, fear=fear, fear_weight=-5.0, seed=5, final_obs=True, debug=True,
+                            stats=True)
+    a, b = mk(), mk()
+    b.set_obs_async(mode)
+    shape = (T, sc.K, E, sc.H, sc.W)
+    obs_a = torch.empty(shape, dtype=torch.float32, device="cuda")
+    fin_a = torch.full(shape, -7.0, dtype=torch.float32, device="cuda")
+    obs_b = torch.empty(shape, dtype=torch.float32, device="cuda")
+    fin_b = torch.full(shape, -7.0, dtype=torch.float32, device="cuda")
+    ra, rb = a.reset(), b.reset()
+    b.obs_fence()
+    assert torch.equal(ra[0], rb[0])
+    bad = torch.zeros((), dtype=torch.int64, device="cuda")
+    for t in range(T):
+        r1 = a.step(obs_out=obs_a[t], final_obs_out=fin_a[t])
+        r2 = b.step(obs_out=obs_b[t], final_obs_out=fin_b[t])
+        for n in OUTS:  # stream-ordered without any fence
+            bad += (getattr(r1, n) != getattr(r2, n)).sum()
+        bad += (r1.stats.sum(0) != r2.stats.sum(0)).sum()
+        if t == T // 2:  # a partial reset in the middle of the pipeline fences itself
+            m = (torch.arange(E, device="cuda") % 3 == 0).to(torch.uint8)
+            a.reset(env_mask=m)
+            b.reset(env_mask=m)
+    b.obs_fence()
+    bad += (obs_a != obs_b).sum() + (fin_a != fin_b).sum()
+    torch.cuda.synchronize()
+    assert int(bad) == 0
+    # the same state afterwards; switching async off drains the writer
+    sa, sb = a.state(), b.state()
+    assert all(torch.equal(sa[k], sb[k]) for k in sa)
+    b.set_obs_async(False)
+    r1, r2 = a.step(), b.step()
+    torch.cuda.synchronize()
+    assert torch.equal(r1.obs, r2.obs) and torch.equal(r1.reward, r2.reward)
+    a.close()
+    b.close()
+
+
+@pytest.mark.parametrize("mode", [True, "lazy"])
+def test_async_rollout_fused_actor_matches_sync(mode):
+    """Rollout(obs_async) with the fused actor (reads the alternating descriptors) == the
+    synchronous rollout: same actions, probs, rewards and replay-ring contents."""
+    from marlnav.actor import MultiAgentActors
+    from marlnav.rollout import Rollout
+    sc = S.builtin("grid32")
+    E = 4096
+    torch.manual_seed(0)
+    actors = MultiAgentActors(sc.K, sc.H, sc.W, "mlp", device="cuda", seed=9)
+    envs = [VecGridEnv(sc, num_envs=E, fear=True, fear_weight=-5.0, seed=3, final_obs=True, stats=True)
+            for _ in range(2)]
+    ros = [Rollout(envs[0], actors, replay_slots=40, training=True, seed=4, obs_async=False),
+           Rollout(envs[1], actors, replay_slots=40, training=True, seed=4, obs_async=mode)]
+    assert all(ro.fused for ro in ros)
+    for ro in ros:
+        ro.reset()
+    bad = torch.zeros((), dtype=torch.int64, device="cuda")
+    for t in range(30):
+        r0, r1 = ros[0].step(), ros[1].step()
+        bad += (r0.shaped != r1.shaped).sum() + (r0.done != r1.done).sum()
+    ros[1].fence()
+    for name in ("obs", "final_obs", "probs", "reward", "term", "done"):
+        bad += (getattr(ros[0].replay, name) != getattr(ros[1].replay, name)).sum()
+    torch.cuda.synchronize()
+    assert int(bad) == 0
+    t0, t1 = ros[0].totals(), ros[1].totals()
+    assert t0 == t1
+    for e in envs:
+        e.close()
