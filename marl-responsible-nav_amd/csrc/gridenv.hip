@@ -1857,6 +1857,7 @@ struct Env {
     // e.g. the fused actor, so the writer never competes with it for the CUs; or at a fence)
     bool obs_async = false;
     bool obs_lazy = false;                        // gw_set_obs_async(env, 2): launch at the next step
+    bool obs_hi = false;                          // GW_OBS_PRIO=hi (A/B): obs stream high priority, aux normal
     hipStream_t obs_stream = nullptr;
     hipEvent_t obs_done[2] = {nullptr, nullptr};  // obs_kernel that read desc_buf[i] has finished
     bool obs_pending[2] = {false, false};
@@ -1891,7 +1892,7 @@ struct Env {
 // the second stream and n fork/join events (timing disabled), created on first use
 gw_status ensure_aux(Env *env, int n) {
     if (!env->aux) {
-        if (env->mode == 3 && env->defer_order == 3) {
+        if (env->mode == 3 && env->defer_order == 3 && !env->obs_hi) {
             int lo = 0, hi = 0;
             HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
             HIP_TRY(hipStreamCreateWithPriority(&env->aux, hipStreamNonBlocking, hi));
@@ -1913,7 +1914,15 @@ gw_status ensure_aux(Env *env, int n) {
 gw_status ensure_obs_stream(Env *env) {
     const gw_status st = ensure_aux(env, 3);
     if (st != GW_OK) return st;
-    if (!env->obs_stream) HIP_TRY(hipStreamCreateWithFlags(&env->obs_stream, hipStreamNonBlocking));
+    if (!env->obs_stream) {
+        if (env->obs_hi) {
+            int lo = 0, hi = 0;
+            HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+            HIP_TRY(hipStreamCreateWithPriority(&env->obs_stream, hipStreamNonBlocking, hi));
+        } else {
+            HIP_TRY(hipStreamCreateWithFlags(&env->obs_stream, hipStreamNonBlocking));
+        }
+    }
     for (hipEvent_t &e : env->obs_done)
         if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (!env->world_ev) HIP_TRY(hipEventCreateWithFlags(&env->world_ev, hipEventDisableTiming));
@@ -2320,6 +2329,8 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
         if (be) env->obs_be = std::max(1, std::min(gw::OBS_BE, std::atoi(be)));
         const char *nt = std::getenv("GW_OBS_NT");
         if (nt) env->obs_nt = std::atoi(nt) != 0;
+        const char *op = std::getenv("GW_OBS_PRIO");
+        if (op && std::strcmp(op, "hi") == 0) env->obs_hi = true;
         const char *ch = std::getenv("GW_CHUNKS");
         if (ch) env->chunks = std::max(1, std::min(16, std::atoi(ch)));
     }
