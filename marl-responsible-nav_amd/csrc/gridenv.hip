@@ -2463,6 +2463,9 @@ gw_status gw_step(void *handle, const int32_t *rl_actions, const int32_t *script
         env->desc = env->desc_buf[nb];
         return GW_OK;
     }
+    // every other path writes the current descriptor buffer in place: an async obs_kernel still
+    // reading it (a step without obs outputs, or a non-pipelining kernel path) must finish first
+    if (env->obs_async) GW_TRY(wait_obs(env, s));
     if (defer && (nch == 1 || env->defer_order == 0)) {
         // world update; then fear_v2 on the aux stream || obs_kernel on s; join
         size_t b;

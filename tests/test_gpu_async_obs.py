@@ -52,6 +52,20 @@ def test_async_obs_matches_sync(path, fear, name, mode, monkeypatch):
     bad += (obs_a != obs_b).sum() + (fin_a != fin_b).sum()
     torch.cuda.synchronize()
     assert int(bad) == 0
+    # a step without obs outputs in the middle of the pipeline (the in-place descriptor path)
+    a.set_obs_async(True)
+    a.step(obs_out=obs_a[0])
+    b.step(obs_out=obs_b[0])
+    for env in (a, b):  # gw_step with no outputs at all (null gw_step_out)
+        assert env.lib.gw_step(env.handle, None, None, None, None, env._stream()) == 0
+    r1 = a.step(obs_out=obs_a[1])
+    r2 = b.step(obs_out=obs_b[1])
+    a.obs_fence()
+    b.obs_fence()
+    bad += (obs_a[:2] != obs_b[:2]).sum() + (r1.reward != r2.reward).sum()
+    torch.cuda.synchronize()
+    assert int(bad) == 0
+    a.set_obs_async(False)
     # the same state afterwards; switching async off drains the writer
     sa, sb = a.state(), b.state()
     assert all(torch.equal(sa[k], sb[k]) for k in sa)
