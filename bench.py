@@ -110,6 +110,11 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--sync-obs", action="store_true",
                     help="write each step's obs before the next step starts (no step pipeline; A/B)")
+    ap.add_argument("--fear-async", action="store_true",
+                    help="c5: let the next actor overlap the FeAR kernel (gw_set_obs_async | 4; A/B, "
+                         "measured slower: profiles/r1_async)")
+    ap.add_argument("--obs-eager", action="store_true",
+                    help="c5: start each step's obs writer right after its world update (A/B)")
     ap.add_argument("--obs-lazy", action="store_true",
                     help="launch each step's obs writer at the next step (gw_set_obs_async 2; A/B)")
     args = ap.parse_args()
@@ -132,7 +137,8 @@ def main():
     # obs writer pipelined with the next step (gw_set_obs_async): right after the world update
     # for the env-only workloads; launched at the next step (behind the fused actor, which would
     # otherwise lose CUs to it) for the full rollout.  Measured A/B: profiles/r1_async/
-    obs_mode = False if args.sync_obs else ("lazy" if (args.obs_lazy or cfg.get("rollout")) else True)
+    obs_mode = False if args.sync_obs else \
+        ("lazy" if (args.obs_lazy or (cfg.get("rollout") and not args.obs_eager)) else True)
     if args.envs:
         cfg["envs"] = args.envs
     if args.fear >= 0:
@@ -161,7 +167,7 @@ def main():
         from marlnav.rollout import Rollout
         learner = MADDPG(K, env.H, env.W, device=env.device, seed=rank, capturable=True)
         ro = Rollout(env, learner.actors, replay_slots=-(-200_000 // E) + 1, training=True, seed=rank,
-                     obs_async=obs_mode)
+                     obs_async=obs_mode, fear_async=bool(obs_mode) and args.fear_async)
         ro.reset()
 
         def one_step(i):  # noqa: F811
@@ -194,7 +200,9 @@ def main():
         if pe > 0:
             env.profile(i % pe == 0)
         r = one_step(i)
-    env.obs_fence()  # the last step's obs writes belong to the timed region
+    if cfg.get("rollout"):
+        ro.fence()  # the last step's obs writes, FeAR outputs and statistics
+    env.obs_fence()  # belong to the timed region
     ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -260,7 +268,7 @@ def main():
                            "kernel_path": os.environ.get("GW_KERNEL", "defer"),
                            "stream_ms_per_step": gpu_ms / args.steps,
                            "pipeline_chunks": int(os.environ.get("GW_CHUNKS", "1")) if not env.fused else 1,
-                           "obs_async": obs_mode},
+                           "obs_async": obs_mode, "fear_async": env.fear_async},
             "last_step_episodes": {"completed": stats[1], "mean_return": stats[0] / max(stats[1], 1.0),
                          "mean_len": stats[6] / max(stats[1], 1.0)},
         }

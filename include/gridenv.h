@@ -184,9 +184,15 @@ gw_status gw_obs_view(void *env, gw_obs_source *out);
  * enable = 1: the writer starts right after the step's world update; enable = 2 (lazy): it is
  * launched at the start of the next gw_step (behind the caller's work between the steps, e.g.
  * an actor kernel that should not share the CUs with it) or at a fence.
+ * enable | 4 (defer path, FeAR on): `stream` joins only the world update; fear_v2 (fear,
+ * shaped, ep_return, ep_fear, the FeAR stats rows, score / fear_score) finishes on the internal
+ * stream and overlaps the caller's next work (an actor that needs only the descriptors and
+ * masks); those outputs are ready on `stream` after gw_fear_fence (gw_reset, gw_copy_state
+ * and the next gw_step order themselves).
  * Only the split / defer kernel paths pipeline; the others stay synchronous. */
 gw_status gw_set_obs_async(void *env, int enable);
 gw_status gw_obs_fence(void *env, void *stream);
+gw_status gw_fear_fence(void *env, void *stream);
 /* Set the thread-local error text returned by gw_last_error (for the library's other
  * translation units: learner_ops, actor_ops). */
 void gw_set_last_error(const char *msg);

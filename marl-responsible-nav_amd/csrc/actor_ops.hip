@@ -5,7 +5,7 @@
 //
 // gw_actor_prepare (once per weight update): c1_k = b1_k + map . W1_k, and the LDS images of the
 // layer-2/3 MFMA A operands (W2, W3 permuted so each lane's four consecutive k-steps are one
-// float4).  gw_actor_act (every step), block = 8 waves = one RL agent k, 2 blocks per CU,
+// float4).  gw_actor_act (every step), block = 16 waves = one RL agent k, one block per CU,
 // persistent over 16-env tiles, one tile per wave at a time:
 //   layer 1   from the obs descriptors: h1 = c1_k + sum_{patched cells c} delta_c * W1_k[c, :].
 //             Lane (env = l & 15, quarter q = l >> 4) accumulates features 16j + 4q + i (j < 8,
@@ -40,7 +40,7 @@
 
 namespace {
 
-constexpr int HID = 128, NA = 9, TILE = 16, WAVES = 8, THREADS = 64 * WAVES, MAXN = GW_MAX_AGENTS;
+constexpr int HID = 128, NA = 9, TILE = 16, MAXN = GW_MAX_AGENTS;
 constexpr int NDESC = 12;
 constexpr uint32_t D_RESET = 1u;
 constexpr float LN_EPS = 1e-5f, G_EPS = 1e-20f;
@@ -92,8 +92,8 @@ struct ActParams {
     float *logits;            // [K][E][9] or null
     int64_t E, env_offset;
     int N, K, HW, variant, training, tiles;
-    int ab;                   // GW_ACT_AB (measurement only): bit 0 skip the W1 gathers, bit 1 skip
-                              // layer 2's MFMAs, bit 2 skip the epilogue
+    int ab;                   // GW_ACT_AB (measurement only): bit 0 zero the W1 deltas, bit 1 skip
+                              // layer 2's MFMAs, bit 2 skip the epilogue, bit 4 gather row 0 only
     float tau;
     uint32_t key0, key1, ctr0, ctr1;
     int apples[MAXN];
@@ -199,8 +199,11 @@ __device__ __forceinline__ Desc load_desc(const ActParams &p, int64_t e, int k) 
     return d;
 }
 
-template <int NP>  // patch slots per (env, agent) = N + 1
-__global__ void __launch_bounds__(THREADS, 4) act_kernel(ActParams p) {
+// WAVES per block (16: one block per CU holding ONE copy of the 74 KB W2/W3 image, so other
+// kernels' blocks fit beside it; 8: two blocks per CU), 4 waves per SIMD (128 VGPRs)
+template <int NP, int WAVES>  // NP = patch slots per (env, agent) = N + 1
+__global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
+    constexpr int THREADS = 64 * WAVES;
     __shared__ float4 s_w2[W2IMG / 4];       // W2 image (w2_slot), 64 KB
     __shared__ float4 s_w3[W3IMG / 4];       // W3 image (w3_slot), 4.5 KB
     __shared__ __attribute__((aligned(16))) float s_vec[6][HID];  // c1, ln1_w, ln1_b, b2, ln2_w, ln2_b
@@ -247,6 +250,7 @@ __global__ void __launch_bounds__(THREADS, 4) act_kernel(ActParams p) {
     __syncthreads();
     ACT_STAMP(1);
     int it = 0;
+    const int stride = gridDim.x * WAVES;
 
     const float *w1 = p.net.w1 + (size_t)k * p.HW * HID;
     const int K = p.K;
@@ -254,7 +258,7 @@ __global__ void __launch_bounds__(THREADS, 4) act_kernel(ActParams p) {
     // layer-1 register 4j + i and layer-2 register (m = j, r = i) both hold feature 16j + 4q + i
     auto vec4 = [q](const float *v, int j) { return *reinterpret_cast<const float4 *>(v + 16 * j + 4 * q); };
 
-    for (; tile < p.tiles; tile += gridDim.x * WAVES, ++it) {
+    for (; tile < p.tiles; tile += stride, ++it) {
         const int64_t e = (int64_t)tile * TILE + el;
         const bool valid = e < p.E;
         const Desc d = dn;
@@ -304,7 +308,7 @@ __global__ void __launch_bounds__(THREADS, 4) act_kernel(ActParams p) {
             const int cc = last ? c : 0;
             const float map = ((s_road[cc >> 5] >> (cc & 31)) & 1u) ? 0.0f : -1.0f;
             dlt[i] = (last && !(p.ab & 1)) ? pv[i] - map : 0.0f;
-            rowc[i] = cc * (HID / 4) + q;  // float4 index of features 4q .. 4q + 3 of row cc
+            rowc[i] = (p.ab & 16) ? q : cc * (HID / 4) + q;  // float4 index of features 4q .. 4q + 3 of row cc
         }
         const float4 *w1v = reinterpret_cast<const float4 *>(w1);
 #pragma unroll
@@ -577,22 +581,34 @@ gw_status gw_actor_act(void *env, const gw_mlp_actors *net, const float *ws, int
     p.ab = ab ? std::atoi(ab) : 0;
     const int64_t tiles = (src.E + TILE - 1) / TILE;
     p.tiles = (int)tiles;
-    // 2 blocks of 8 waves per CU (~75 KB LDS each): 512 resident blocks over the K agents
-    const int64_t want = (tiles + WAVES - 1) / WAVES;
-    const int per_agent = (int)std::max<int64_t>(1, std::min<int64_t>(want, std::max(1, 512 / src.K)));
-    const dim3 grid(per_agent, src.K), block(THREADS);
+    // GW_ACT_V (A/B): 2 (default) = one 16-wave block per CU; 0 = two 8-wave blocks per CU
+    const char *av = std::getenv("GW_ACT_V");
+    const int v = av ? std::atoi(av) : 2;
+    const int waves = v == 0 ? 8 : 16;
+    const int resident = v == 0 ? 512 : 256;
+    const int64_t want = (tiles + waves - 1) / waves;
+    const int per_agent = (int)std::max<int64_t>(1, std::min<int64_t>(want, std::max(1, resident / src.K)));
+    const dim3 grid(per_agent, src.K), block(64 * waves);
     hipStream_t s = static_cast<hipStream_t>(stream);
+#define ACT_LAUNCH(NP)                                                                   \
+    do {                                                                                 \
+        if (v == 0)                                                                      \
+            hipLaunchKernelGGL((act_kernel<NP, 8>), grid, block, 0, s, p);               \
+        else                                                                             \
+            hipLaunchKernelGGL((act_kernel<NP, 16>), grid, block, 0, s, p);              \
+    } while (0)
     switch (src.N) {
-        case 1: hipLaunchKernelGGL(act_kernel<2>, grid, block, 0, s, p); break;
-        case 2: hipLaunchKernelGGL(act_kernel<3>, grid, block, 0, s, p); break;
-        case 3: hipLaunchKernelGGL(act_kernel<4>, grid, block, 0, s, p); break;
-        case 4: hipLaunchKernelGGL(act_kernel<5>, grid, block, 0, s, p); break;
-        case 5: hipLaunchKernelGGL(act_kernel<6>, grid, block, 0, s, p); break;
-        case 6: hipLaunchKernelGGL(act_kernel<7>, grid, block, 0, s, p); break;
-        case 7: hipLaunchKernelGGL(act_kernel<8>, grid, block, 0, s, p); break;
-        case 8: hipLaunchKernelGGL(act_kernel<9>, grid, block, 0, s, p); break;
+        case 1: ACT_LAUNCH(2); break;
+        case 2: ACT_LAUNCH(3); break;
+        case 3: ACT_LAUNCH(4); break;
+        case 4: ACT_LAUNCH(5); break;
+        case 5: ACT_LAUNCH(6); break;
+        case 6: ACT_LAUNCH(7); break;
+        case 7: ACT_LAUNCH(8); break;
+        case 8: ACT_LAUNCH(9); break;
         default: return err(GW_ERR_ARG, "gw_actor_act: N out of range");
     }
+#undef ACT_LAUNCH
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return err(GW_ERR_HIP, std::string("gw_actor_act: ") + hipGetErrorString(e));
     return GW_OK;

@@ -1862,6 +1862,11 @@ struct Env {
     hipEvent_t obs_done[2] = {nullptr, nullptr};  // obs_kernel that read desc_buf[i] has finished
     bool obs_pending[2] = {false, false};
     hipEvent_t world_ev = nullptr;                // world update of the queued step has finished
+    // gw_set_obs_async(env, | 4): the caller's stream joins only the world update; fear_v2 (FeAR,
+    // shaped reward, returns, FeAR stats rows) finishes on the aux stream, ordered by gw_fear_fence
+    bool fear_async = false;
+    bool fear_pending = false;
+    hipEvent_t fear_ev = nullptr;
     bool obs_queued = false;                      // an obs_kernel launch waits in qobs
     bool qobs_prof = false;                       // profiling state of the step that queued it
     int qobs_buf = 0;
@@ -1926,6 +1931,7 @@ gw_status ensure_obs_stream(Env *env) {
     for (hipEvent_t &e : env->obs_done)
         if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (!env->world_ev) HIP_TRY(hipEventCreateWithFlags(&env->world_ev, hipEventDisableTiming));
+    if (!env->fear_ev) HIP_TRY(hipEventCreateWithFlags(&env->fear_ev, hipEventDisableTiming));
     return GW_OK;
 }
 
@@ -1959,8 +1965,19 @@ gw_status flush_obs(Env *env, hipEvent_t after) {
     return GW_OK;
 }
 
+// make `s` wait for an async fear_v2 still in flight
+gw_status wait_fear(Env *env, hipStream_t s) {
+    if (env->fear_pending) HIP_TRY(hipStreamWaitEvent(s, env->fear_ev, 0));
+    return GW_OK;
+}
+
 // launch a queued obs_kernel and make `s` wait for every obs_kernel of the async-obs stream
+// (and for an async fear_v2: the callers rewrite state or descriptors in place)
 gw_status wait_obs(Env *env, hipStream_t s) {
+    {
+        const gw_status st = wait_fear(env, s);
+        if (st != GW_OK) return st;
+    }
     if (env->obs_queued) {
         const gw_status st = flush_obs(env, nullptr);
         if (st != GW_OK) return st;
@@ -2447,13 +2464,24 @@ gw_status gw_step(void *handle, const int32_t *rl_actions, const int32_t *script
         HIP_TRY(dispatch_step(env, p, env->aux));
         GW_TRY(span_end(env->aux, b, 0));
         HIP_TRY(hipEventRecord(env->world_ev, env->aux));
-        if (defer) {
+        if (defer && env->fear_async) {
+            // s joins the world update only: the caller's next work (the actor reads the
+            // descriptors and masks) overlaps fear_v2; FeAR-owned outputs wait for gw_fear_fence
+            HIP_TRY(hipStreamWaitEvent(s, env->world_ev, 0));
             GW_TRY(span_begin(env->aux, b));
             HIP_TRY(dispatch_fear(env, p, env->aux));
             GW_TRY(span_end(env->aux, b, 2));
+            HIP_TRY(hipEventRecord(env->fear_ev, env->aux));
+            env->fear_pending = true;
+        } else {
+            if (defer) {
+                GW_TRY(span_begin(env->aux, b));
+                HIP_TRY(dispatch_fear(env, p, env->aux));
+                GW_TRY(span_end(env->aux, b, 2));
+            }
+            HIP_TRY(hipEventRecord(env->sync_ev[2], env->aux));  // join the world update + FeAR
+            HIP_TRY(hipStreamWaitEvent(s, env->sync_ev[2], 0));
         }
-        HIP_TRY(hipEventRecord(env->sync_ev[2], env->aux));  // join the world update + FeAR
-        HIP_TRY(hipStreamWaitEvent(s, env->sync_ev[2], 0));
         env->qobs = p;
         env->qobs_buf = nb;
         env->qobs_prof = env->profiling;
@@ -2465,7 +2493,7 @@ gw_status gw_step(void *handle, const int32_t *rl_actions, const int32_t *script
     }
     // every other path writes the current descriptor buffer in place: an async obs_kernel still
     // reading it (a step without obs outputs, or a non-pipelining kernel path) must finish first
-    if (env->obs_async) GW_TRY(wait_obs(env, s));
+    if (env->obs_async || env->fear_pending) GW_TRY(wait_obs(env, s));
     if (defer && (nch == 1 || env->defer_order == 0)) {
         // world update; then fear_v2 on the aux stream || obs_kernel on s; join
         size_t b;
@@ -2573,8 +2601,13 @@ gw_status gw_set_obs_async(void *handle, int enable) {
         HIP_TRY(hipStreamSynchronize(env->obs_stream));
         env->obs_pending[0] = env->obs_pending[1] = false;
     }
+    if (!(enable & 4) && env->fear_pending) {
+        HIP_TRY(hipEventSynchronize(env->fear_ev));
+        env->fear_pending = false;
+    }
     env->obs_async = enable != 0;
-    env->obs_lazy = enable == 2;
+    env->obs_lazy = (enable & 2) != 0;
+    env->fear_async = (enable & 4) != 0;
     return GW_OK;
 }
 
@@ -2582,6 +2615,13 @@ gw_status gw_obs_fence(void *handle, void *stream) {
     Env *env = static_cast<Env *>(handle);
     if (!env) return fail(GW_ERR_ARG, "null env");
     GW_TRY(wait_obs(env, static_cast<hipStream_t>(stream)));
+    return GW_OK;
+}
+
+gw_status gw_fear_fence(void *handle, void *stream) {
+    Env *env = static_cast<Env *>(handle);
+    if (!env) return fail(GW_ERR_ARG, "null env");
+    GW_TRY(wait_fear(env, static_cast<hipStream_t>(stream)));
     return GW_OK;
 }
 
@@ -2626,6 +2666,7 @@ gw_status gw_copy_state(void *handle, const gw_state *buf, int to_env, void *str
     Env *env = static_cast<Env *>(handle);
     if (!env || !buf) return fail(GW_ERR_ARG, "null argument");
     hipStream_t s = static_cast<hipStream_t>(stream);
+    GW_TRY(wait_fear(env, s));  // async FeAR writes score / fear_score
     const size_t E = (size_t)env->E;
     struct Item { void *mine; void *theirs; size_t bytes; } items[] = {
         {env->pos, buf->pos, sizeof(int32_t) * env->N * E},
@@ -2736,6 +2777,7 @@ void gw_destroy(void *handle) {
     for (hipEvent_t e : env->obs_done)
         if (e) (void)hipEventDestroy(e);
     if (env->world_ev) (void)hipEventDestroy(env->world_ev);
+    if (env->fear_ev) (void)hipEventDestroy(env->fear_ev);
     for (void *p : env->allocs) (void)hipFree(p);
     delete env;
 }

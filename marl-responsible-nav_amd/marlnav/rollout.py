@@ -67,13 +67,15 @@ class ReplayRing:
 class Rollout:
     def __init__(self, env: VecGridEnv, actors: MultiAgentActors | None = None, replay_slots: int = 0,
                  training: bool = True, group=None, seed: int = 0, fused: bool | None = None,
-                 obs_async: bool = False):
+                 obs_async: bool | str = False, fear_async: bool = False):
         """fused: get_action as the one-kernel gw_actor_act over the env's obs descriptors
         (default when the actors are the f32 128-128 MLP), else the PyTorch forward over the
         dense obs with torch's Gumbel noise.
         obs_async: pipeline the env's obs writes (the replay ring's obs slots) with the next
         step's actor + world update (VecGridEnv.set_obs_async); whoever reads the obs or the ring
-        afterwards calls ``fence()`` first (the learner does)."""
+        afterwards calls ``fence()`` first (the learner does).
+        fear_async (with obs_async): the next step's actor overlaps this step's FeAR kernel; the
+        step's statistics are reduced one step later, after a FeAR fence."""
         self.env = env
         self.actors = actors
         self.fused = (actors is not None and actors.fusable(env)) if fused is None else bool(fused)
@@ -86,11 +88,29 @@ class Rollout:
         self.gen = torch.Generator(device=env.device).manual_seed(seed) if actors is not None else None
         self.t = 0
         self.reducer = StatsReducer(_lib.GW_STATS, env.device, group) if env.out.get("stats") is not None else None
-        env.set_obs_async(obs_async)
+        env.set_obs_async(obs_async, fear_async=fear_async)
+        self._pending = None  # (stats, tick) of a step whose FeAR may still be in flight
+
+    def _flush(self):
+        """Reduce the statistics of the previous step once its FeAR outputs are ordered."""
+        if self._pending is not None:
+            stats, tick = self._pending
+            self._pending = None
+            self.env.fear_fence()
+            self._reduce(stats, tick)
+
+    def _reduce(self, stats, tick):
+        if self.reducer is not None:
+            # per-step (RCCL) reduction of the episode statistics; the ring's device step count
+            # advances in the same launch
+            self.reducer.push(stats, counter=tick)
+        elif tick is not None:
+            tick.add_(1)
 
     def fence(self):
-        """Order the observations written so far (ring slots / env obs) before later work on
-        the current stream (a no-op unless obs_async)."""
+        """Order everything written so far (ring slots / env obs, rewards, statistics) before
+        later work on the current stream (a no-op unless obs_async)."""
+        self._flush()
         self.env.obs_fence()
 
     def reset(self):
@@ -123,6 +143,7 @@ class Rollout:
             actions, probs = self.actors.act(self._obs_now(), mask, self.training, generator=self.gen)
         else:
             actions, probs = None, None  # device-RNG random policy
+        self._flush()  # after the actor: it overlapped the previous step's FeAR kernel
         if self.replay is not None:
             rp = self.replay
             nxt = (self.t + 1) % rp.S
@@ -137,12 +158,10 @@ class Rollout:
             r = env.step(actions)
         self.t += 1
         tick = self.replay.t_dev if self.replay is not None else None
-        if self.reducer is not None:
-            # per-step (RCCL) reduction of the episode statistics; the ring's device step count
-            # advances in the same launch
-            self.reducer.push(r.stats, counter=tick)
-        elif tick is not None:
-            tick.add_(1)
+        if self.env.fear_async:
+            self._pending = (r.stats, tick)
+        else:
+            self._reduce(r.stats, tick)
         return r
 
     def totals(self) -> dict:
@@ -150,4 +169,5 @@ class Rollout:
         episodes, FeAR, crashes, apples, shaped reward, completed-episode length sum, env-steps."""
         if self.reducer is None:
             return {}
+        self._flush()
         return dict(zip(_lib.STATS_NAMES, self.reducer.result().cpu().tolist()))

@@ -120,6 +120,7 @@ class VecGridEnv:
         self._step_out = _lib.GwStepOut(*[_ptr(self.out[n]) for n in _lib.STEP_OUT_FIELDS])
         self._closed = False
         self.obs_async = False
+        self.fear_async = False
         self.fused = (sc.HW % 4 == 0) and os.environ.get("GW_KERNEL", "split") == "fused"
 
     # ------------------------------------------------------------------------------------
@@ -236,21 +237,34 @@ class VecGridEnv:
                        "gw_fear_matrix")
         return out
 
-    def set_obs_async(self, enable: bool | str = True):
+    def set_obs_async(self, enable: bool | str = True, fear_async: bool = False):
         """Pipeline the obs writer of step t with the world update of step t+1 (gw_set_obs_async).
         While on, ``step``'s obs / final_obs are ready on the current stream only after
         ``obs_fence()`` (rewards, dones, masks and state are ordered as usual).
         enable="lazy": the writer is launched at the next step, behind the caller's work between
-        the steps (an actor kernel), instead of right after the world update."""
+        the steps (an actor kernel), instead of right after the world update.
+        fear_async (defer path, FeAR on): the FeAR-owned outputs (fear, shaped, ep_return,
+        ep_fear, the FeAR stats rows) are ready only after ``fear_fence()``, so the caller's next
+        work (the fused actor) overlaps the FeAR kernel."""
         mode = 2 if enable == "lazy" else int(bool(enable))
+        if mode and fear_async:
+            mode |= 4
         _lib.check(self.lib.gw_set_obs_async(self.handle, mode), "gw_set_obs_async")
         self.obs_async = bool(mode)
+        self.fear_async = bool(mode & 4)
 
     def obs_fence(self):
-        """Order the last step's obs before later work on the current stream (async obs)."""
+        """Order the last step's outputs (obs, and FeAR-owned ones) before later work on the
+        current stream (async mode)."""
         if self.obs_async:
             with torch.cuda.device(self.device):
                 _lib.check(self.lib.gw_obs_fence(self.handle, self._stream()), "gw_obs_fence")
+
+    def fear_fence(self):
+        """Order the last step's FeAR-owned outputs before later work on the current stream."""
+        if self.fear_async:
+            with torch.cuda.device(self.device):
+                _lib.check(self.lib.gw_fear_fence(self.handle, self._stream()), "gw_fear_fence")
 
     def profile(self, enable: bool = True):
         """Record HIP events around each gw_step kernel (see gw_profile)."""

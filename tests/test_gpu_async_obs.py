@@ -77,8 +77,8 @@ def test_async_obs_matches_sync(path, fear, name, mode, monkeypatch):
     b.close()
 
 
-@pytest.mark.parametrize("mode", [True, "lazy"])
-def test_async_rollout_fused_actor_matches_sync(mode):
+@pytest.mark.parametrize("mode,fear_async", [(True, False), ("lazy", False), ("lazy", True), (True, True)])
+def test_async_rollout_fused_actor_matches_sync(mode, fear_async):
     """Rollout(obs_async) with the fused actor (reads the alternating descriptors) == the
     synchronous rollout: same actions, probs, rewards and replay-ring contents."""
     from marlnav.actor import MultiAgentActors
@@ -90,20 +90,53 @@ def test_async_rollout_fused_actor_matches_sync(mode):
     envs = [VecGridEnv(sc, num_envs=E, fear=True, fear_weight=-5.0, seed=3, final_obs=True, stats=True)
             for _ in range(2)]
     ros = [Rollout(envs[0], actors, replay_slots=40, training=True, seed=4, obs_async=False),
-           Rollout(envs[1], actors, replay_slots=40, training=True, seed=4, obs_async=mode)]
+           Rollout(envs[1], actors, replay_slots=40, training=True, seed=4, obs_async=mode,
+                   fear_async=fear_async)]
     assert all(ro.fused for ro in ros)
     for ro in ros:
         ro.reset()
     bad = torch.zeros((), dtype=torch.int64, device="cuda")
     for t in range(30):
         r0, r1 = ros[0].step(), ros[1].step()
-        bad += (r0.shaped != r1.shaped).sum() + (r0.done != r1.done).sum()
+        bad += (r0.done != r1.done).sum() + (r0.mask != r1.mask).sum()
+        if not fear_async:  # else the FeAR outputs are ordered by the next step / fence
+            bad += (r0.shaped != r1.shaped).sum()
     ros[1].fence()
-    for name in ("obs", "final_obs", "probs", "reward", "term", "done"):
+    for name in ("obs", "final_obs", "probs", "reward", "term", "done", "t_dev"):
         bad += (getattr(ros[0].replay, name) != getattr(ros[1].replay, name)).sum()
+    st0, st1 = envs[0].state(), envs[1].state()
+    bad += sum((st0[k] != st1[k]).sum() for k in st0)
     torch.cuda.synchronize()
     assert int(bad) == 0
     t0, t1 = ros[0].totals(), ros[1].totals()
     assert t0 == t1
     for e in envs:
         e.close()
+
+
+def test_fear_async_env_outputs_after_fence():
+    """gw_set_obs_async(| 4): the FeAR-owned outputs of every step equal the synchronous env's
+    once fenced, with no host synchronisation in the loop (the fence is stream-ordered)."""
+    sc = S.builtin("grid32")
+    E, T = 4096, 20
+    mk = lambda: VecGridEnv(sc, num_envs=E, fear=True, fear_weight=-5.0, seed=8, stats=True)
+    a, b = mk(), mk()
+    b.set_obs_async("lazy", fear_async=True)
+    a.reset()
+    b.reset()
+    bad = torch.zeros((), dtype=torch.int64, device="cuda")
+    for t in range(T):
+        r1, r2 = a.step(), b.step()
+        bad += (r1.done != r2.done).sum() + (r1.reward != r2.reward).sum()
+        b.fear_fence()
+        for n in ("fear", "shaped", "ep_return", "ep_fear"):
+            bad += (getattr(r1, n) != getattr(r2, n)).sum()
+        bad += (r1.stats.sum(0) != r2.stats.sum(0)).sum()
+    b.obs_fence()
+    bad += (a.out["obs"] != b.out["obs"]).sum()
+    sa, sb = a.state(), b.state()
+    bad += sum((sa[k] != sb[k]).sum() for k in sa)
+    torch.cuda.synchronize()
+    assert int(bad) == 0
+    a.close()
+    b.close()
