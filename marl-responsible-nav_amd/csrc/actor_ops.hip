@@ -14,7 +14,11 @@
 //             value of a cell comes from a road bitmask in LDS; the next tile's descriptor is
 //             loaded while this tile computes.
 //   LN1/ReLU  in registers; the four quarters of an env meet through two lane shuffles.
-//   layer 2   transposed f32 MFMA: H2^T = W2^T A1^T with v_mfma_f32_16x16x4_f32.  The lane's 32
+//   layer 2   (default) bf16x3 on v_mfma_f32_16x16x32_bf16: A1 and W2 split into bf16 hi + mid + lo,
+//             6 of the 9 part products (~2^-24 relative each, f32 accumulation) at 16x the f32
+//             MFMA rate per instruction; the K order inside each 32-block follows the lane's
+//             layer-1 registers (kperm), so A1 needs no lane movement.  GW_ACT_V=2: exact f32:
+//             transposed f32 MFMA: H2^T = W2^T A1^T with v_mfma_f32_16x16x4_f32.  The lane's 32
 //             layer-1 registers ARE the B operand (k-step s takes feature 16(s >> 2) + 4q + (s & 3)
 //             from quarter q: the same feature order as the layer-2 result),
 //             W2 the A operand (ds_read_b128: four k-steps per read); the result has env on the
@@ -49,10 +53,15 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // workspace layout (floats, per gw_actor_workspace_floats)
 constexpr int W2IMG = HID * HID;          // per agent
 constexpr int W3IMG = 8 * 4 * NA * 4;     // per agent
+constexpr int W2B_U4 = 3 * 8 * 4 * 64;    // per agent: the bf16x3 W2 image in 16-byte units
+constexpr int W2BIMG = W2B_U4 * 4;        // (floats)
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 struct Ws {
     float *c1;        // [K][128]
     float4 *w2;       // [K][4096]  (w2_slot)
     float4 *w3;       // [K][288]   (w3_slot)
+    u32x4 *w2b;       // [K][6144]  (w2b_slot)
     float *part;      // [K][nslices][128] map . W1 row slices
 };
 inline Ws ws_layout(float *base, int K) {
@@ -60,8 +69,38 @@ inline Ws ws_layout(float *base, int K) {
     w.c1 = base;
     w.w2 = reinterpret_cast<float4 *>(base + (size_t)K * HID);
     w.w3 = reinterpret_cast<float4 *>(base + (size_t)K * (HID + W2IMG));
-    w.part = base + (size_t)K * (HID + W2IMG + W3IMG);
+    w.w2b = reinterpret_cast<u32x4 *>(base + (size_t)K * (HID + W2IMG + W3IMG));
+    w.part = base + (size_t)K * (HID + W2IMG + W3IMG + W2BIMG);
     return w;
+}
+
+// bf16x3 split of an f32 (x = hi + mid + lo to ~2^-24 relative; round-to-nearest-even bits)
+__host__ __device__ inline uint32_t bf16_rn_bits(float x) {
+    uint32_t u;
+    __builtin_memcpy(&u, &x, 4);
+    return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
+__host__ __device__ inline float bf16_float(uint32_t b) {
+    const uint32_t u = b << 16;
+    float f;
+    __builtin_memcpy(&f, &u, 4);
+    return f;
+}
+__host__ __device__ inline void split3(float x, uint32_t &h, uint32_t &m, uint32_t &l) {
+    h = bf16_rn_bits(x);
+    float r = x - bf16_float(h);
+    m = bf16_rn_bits(r);
+    r = r - bf16_float(m);
+    l = bf16_rn_bits(r);
+}
+// bf16x3 W2 image for v_mfma_f32_16x16x32_bf16 (GW_ACT_V=4): [part 3][m 8][kb 4][lane 64] x 8 bf16,
+// element j of lane l = part of W2[in = kperm(kb, 8 (l >> 4) + j)][out = 16 m + (l & 15)], where the
+// K-block's order kperm follows the layer-1 register order of the B operand (lane quarter q holds
+// features 32 kb + 4q + j, j < 4, and 32 kb + 16 + 4q + j - 4)
+__host__ __device__ inline int w2b_slot(int part, int m, int kb, int lane) { return ((part * 8 + m) * 4 + kb) * 64 + lane; }
+__host__ __device__ inline int kperm(int kb, int k) {
+    const int q = k >> 3, j = k & 7;
+    return 32 * kb + (j < 4 ? 4 * q + j : 16 + 4 * q + j - 4);
 }
 
 // LDS images of the MFMA A operands, one float4 (4 consecutive k-steps) per lane and read:
@@ -83,6 +122,7 @@ struct ActParams {
     gw_mlp_actors net;
     const float *c1;          // [K][128]
     const float4 *w2img, *w3img;
+    const u32x4 *w2bimg;
     const uint32_t *desc;     // [E][12]
     const float *base;        // [HW]
     const uint16_t *mask;     // [E][K] or null
@@ -161,6 +201,19 @@ __global__ void __launch_bounds__(256) prep_images(PrepParams p) {
         const int row = f / HID, col = f % HID;
         img2[4 * w2_slot(col >> 4, row >> 4, (row >> 2) & 3, col & 15) + (row & 3)] = w2[f];
     }
+    uint32_t *img2b = reinterpret_cast<uint32_t *>(p.ws.w2b + (size_t)k * W2B_U4);
+    for (int wd = blockIdx.x * 256 + tid; wd < W2B_U4 * 4; wd += gridDim.x * 256) {
+        const int jp = wd & 3, lane = (wd >> 2) & 63, kb = (wd >> 8) & 3, m = (wd >> 10) & 7, part = wd >> 13;
+        uint32_t bits[2];
+        for (int h = 0; h < 2; ++h) {
+            const int j = 2 * jp + h;
+            const float x = w2[kperm(kb, 8 * (lane >> 4) + j) * HID + 16 * m + (lane & 15)];
+            uint32_t hi, mi, lo;
+            split3(x, hi, mi, lo);
+            bits[h] = part == 0 ? hi : part == 1 ? mi : lo;
+        }
+        img2b[wd] = bits[0] | (bits[1] << 16);
+    }
     const float *w3 = p.net.w3 + (size_t)k * HID * NA;
     float *img3 = reinterpret_cast<float *>(p.ws.w3 + (size_t)k * (W3IMG / 4));
     for (int i = blockIdx.x * 256 + tid; i < W3IMG; i += gridDim.x * 256) {
@@ -200,11 +253,14 @@ __device__ __forceinline__ Desc load_desc(const ActParams &p, int64_t e, int k) 
 }
 
 // WAVES per block (16: one block per CU holding ONE copy of the 74 KB W2/W3 image, so other
-// kernels' blocks fit beside it; 8: two blocks per CU), 4 waves per SIMD (128 VGPRs)
-template <int NP, int WAVES>  // NP = patch slots per (env, agent) = N + 1
+// kernels' blocks fit beside it; 8: two blocks per CU), 4 waves per SIMD (128 VGPRs).
+// BF3: layer 2 as bf16x3 products on v_mfma_f32_16x16x32_bf16 (6 of the 9 part products, f32
+// accumulation; ~2^-24 relative per product, 16x the f32 MFMA rate per instruction)
+template <int NP, int WAVES, bool BF3 = false>  // NP = patch slots per (env, agent) = N + 1
 __global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
     constexpr int THREADS = 64 * WAVES;
-    __shared__ float4 s_w2[W2IMG / 4];       // W2 image (w2_slot), 64 KB
+    constexpr int NW2 = BF3 ? W2B_U4 : W2IMG / 4;
+    __shared__ float4 s_w2[NW2];             // W2 image (w2_slot, 64 KB; BF3: w2b_slot, 96 KB)
     __shared__ float4 s_w3[W3IMG / 4];       // W3 image (w3_slot), 4.5 KB
     __shared__ __attribute__((aligned(16))) float s_vec[6][HID];  // c1, ln1_w, ln1_b, b2, ln2_w, ln2_b
     __shared__ float s_b3[12];
@@ -218,8 +274,9 @@ __global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
     ACT_STAMP(0);
     Desc dn = load_desc(p, (int64_t)tile * TILE + el, k);  // first tile's descriptor, in flight
     {   // stage this agent's W2 / W3 images and vectors (all loads of a lane issued first)
-        const float4 *w2 = p.w2img + (size_t)k * (W2IMG / 4);
-        constexpr int R = W2IMG / 4 / THREADS;
+        const float4 *w2 = BF3 ? reinterpret_cast<const float4 *>(p.w2bimg + (size_t)k * W2B_U4)
+                               : p.w2img + (size_t)k * (W2IMG / 4);
+        constexpr int R = NW2 / THREADS;
         float4 r[R];
 #pragma unroll
         for (int i = 0; i < R; ++i) r[i] = w2[i * THREADS + tid];
@@ -352,7 +409,38 @@ __global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
         f32x4 acc[8];
 #pragma unroll
         for (int m = 0; m < 8; ++m) acc[m] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        if (!(p.ab & 2)) {
+        if (BF3 && !(p.ab & 2)) {
+#pragma unroll
+            for (int kb = 0; kb < 4; ++kb) {
+                // B fragments: registers 8kb .. 8kb + 7 = features 32kb + 4q + j (j < 4) and
+                // 32kb + 16 + 4q + j - 4 (the image's kperm), split into bf16 hi / mid / lo
+                u32x4 bh, bm, bl;
+#pragma unroll
+                for (int jp = 0; jp < 4; ++jp) {
+                    uint32_t h0, m0, l0, h1, m1, l1;
+                    split3(a[8 * kb + 2 * jp], h0, m0, l0);
+                    split3(a[8 * kb + 2 * jp + 1], h1, m1, l1);
+                    bh[jp] = h0 | (h1 << 16);
+                    bm[jp] = m0 | (m1 << 16);
+                    bl[jp] = l0 | (l1 << 16);
+                }
+                const bf16x8 Bh = __builtin_bit_cast(bf16x8, bh), Bm = __builtin_bit_cast(bf16x8, bm),
+                             Bl = __builtin_bit_cast(bf16x8, bl);
+#pragma unroll
+                for (int m = 0; m < 8; ++m) {
+                    const bf16x8 Ah = __builtin_bit_cast(bf16x8, s_w2[w2b_slot(0, m, kb, lane)]);
+                    const bf16x8 Am = __builtin_bit_cast(bf16x8, s_w2[w2b_slot(1, m, kb, lane)]);
+                    const bf16x8 Al = __builtin_bit_cast(bf16x8, s_w2[w2b_slot(2, m, kb, lane)]);
+                    // small terms first
+                    acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Al, Bh, acc[m], 0, 0, 0);
+                    acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bl, acc[m], 0, 0, 0);
+                    acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bm, acc[m], 0, 0, 0);
+                    acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bh, acc[m], 0, 0, 0);
+                    acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bm, acc[m], 0, 0, 0);
+                    acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bh, acc[m], 0, 0, 0);
+                }
+            }
+        } else if (!(p.ab & 2)) {
 #pragma unroll
             for (int s4 = 0; s4 < 8; ++s4) {
 #pragma unroll
@@ -517,7 +605,7 @@ int gw_actor_debug_clocks(unsigned long long *out, int nblocks) {
 }
 
 int64_t gw_actor_workspace_floats(int32_t in_dim, int32_t K) {
-    return (int64_t)K * (HID + W2IMG + W3IMG + (int64_t)((in_dim + 31) / 32) * HID);
+    return (int64_t)K * (HID + W2IMG + W3IMG + W2BIMG + (int64_t)((in_dim + 31) / 32) * HID);
 }
 
 gw_status gw_actor_prepare(void *env, const gw_mlp_actors *net, float *ws, void *stream) {
@@ -557,6 +645,7 @@ gw_status gw_actor_act(void *env, const gw_mlp_actors *net, const float *ws, int
     p.c1 = w.c1;
     p.w2img = w.w2;
     p.w3img = w.w3;
+    p.w2bimg = w.w2b;
     p.desc = src.desc;
     p.base = src.base;
     p.mask = mask;
@@ -581,9 +670,10 @@ gw_status gw_actor_act(void *env, const gw_mlp_actors *net, const float *ws, int
     p.ab = ab ? std::atoi(ab) : 0;
     const int64_t tiles = (src.E + TILE - 1) / TILE;
     p.tiles = (int)tiles;
-    // GW_ACT_V (A/B): 2 (default) = one 16-wave block per CU; 0 = two 8-wave blocks per CU
+    // GW_ACT_V (A/B): 4 (default) = one 16-wave block per CU, layer 2 as bf16x3 MFMA products;
+    // 2 = the same with f32 MFMA (exact products); 0 = two 8-wave blocks per CU, f32 MFMA
     const char *av = std::getenv("GW_ACT_V");
-    const int v = av ? std::atoi(av) : 2;
+    const int v = av ? std::atoi(av) : 4;
     const int waves = v == 0 ? 8 : 16;
     const int resident = v == 0 ? 512 : 256;
     const int64_t want = (tiles + waves - 1) / waves;
@@ -594,6 +684,8 @@ gw_status gw_actor_act(void *env, const gw_mlp_actors *net, const float *ws, int
     do {                                                                                 \
         if (v == 0)                                                                      \
             hipLaunchKernelGGL((act_kernel<NP, 8>), grid, block, 0, s, p);               \
+        else if (v == 4)                                                                 \
+            hipLaunchKernelGGL((act_kernel<NP, 16, true>), grid, block, 0, s, p);        \
         else                                                                             \
             hipLaunchKernelGGL((act_kernel<NP, 16>), grid, block, 0, s, p);              \
     } while (0)

@@ -182,3 +182,31 @@ def test_fused_act_sees_every_weight_update():
     learner.load_state_dict(sd)   # checkpoint load
     agree()
     env.close()
+
+
+@pytest.mark.parametrize("variant", ["4", "2"])
+def test_fused_act_layer2_precision(variant, monkeypatch):
+    """Logits of the fused op (GW_ACT_V=4: layer 2 as bf16x3 MFMA products, the default; 2: exact
+    f32 MFMA) against a float64 forward of the same weights: both within f32 rounding noise."""
+    monkeypatch.setenv("GW_ACT_V", variant)
+    sc = S.builtin("grid32")
+    env = VecGridEnv(sc, num_envs=2048, fear=True, fear_weight=-5.0, seed=6)
+    actors = _actors(sc, seed=11)
+    env.reset()
+    for _ in range(3):
+        env.step()
+    logits = torch.empty((sc.K, env.E, N_ACTIONS), device="cuda")
+    actors.act_env(env, env.out["mask"], False, logits_out=logits)
+    net = actors.net
+    x = env.out["obs"].reshape(sc.K, env.E, -1).double()
+    h = x
+    for i in range(3):
+        h = torch.bmm(h, net.weights[i].double()) + net.biases[i].double().reshape(sc.K, 1, -1)
+        if i < 2:
+            if net.layer_norm:
+                h = torch.nn.functional.layer_norm(h, (h.shape[-1],), eps=1e-5)
+                h = h * net.ln_w[i].double().reshape(sc.K, 1, -1) + net.ln_b[i].double().reshape(sc.K, 1, -1)
+            h = torch.relu(h)
+    err = (logits.double() - h).abs().max().item()
+    assert err < 2e-5, err
+    env.close()
