@@ -17,14 +17,17 @@ pytestmark = pytest.mark.gpu
 OUTS = ("reward", "fear", "shaped", "term", "trunc", "done", "mask", "ep_return", "actions", "final_pos")
 
 
-@pytest.mark.parametrize("path,fear,name,mode", [("defer", True, "grid32", True), ("defer", False, "grid32", True),
-                                                 ("split", True, "grid32", True), ("defer", True, "grid64_n8", True),
-                                                 ("defer", True, "grid32", "lazy"), ("split", False, "grid32", "lazy")])
-def test_async_obs_matches_sync(path, fear, name, mode, monkeypatch):
+@pytest.mark.parametrize("path,fear,name,mode,E", [
+    ("defer", True, "grid32", True, 4096), ("defer", False, "grid32", True, 4096),
+    ("split", True, "grid32", True, 4096), ("defer", True, "grid64_n8", True, 1024),
+    ("defer", True, "grid32", "lazy", 4096), ("split", False, "grid32", "lazy", 4096),
+    ("defer", True, "level3", True, 1), ("defer", True, "level3", "lazy", 333),   # ragged env counts
+    ("fused", True, "grid32", True, 515), ("v1", True, "grid32", True, 257)])      # non-pipelining paths
+def test_async_obs_matches_sync(path, fear, name, mode, E, monkeypatch):
     monkeypatch.setenv("GW_KERNEL", path)
     monkeypatch.setenv("GW_CHUNKS", "1")
     sc = S.builtin(name)
-    E, T = (4096, 24) if name == "grid32" else (1024, 12)
+    T = 12 if name == "grid64_n8" else 24
     mk = lambda: VecGridEnv(sc, num_envs=E, fear=fear, fear_weight=-5.0, seed=5, final_obs=True, debug=True,
                             stats=True)
     a, b = mk(), mk()
