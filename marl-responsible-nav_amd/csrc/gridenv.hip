@@ -1040,7 +1040,7 @@ __global__ void __launch_bounds__(OBS_THREADS) obs_kernel(Params p, float *__res
                                                           float *__restrict__ final_obs) {
     // LDS sized to the launch (obs_lds_bytes): road bitmask, flags, then per (which, env, k)
     // N + 1 patch cells and values.  Small (640 B at 32x32, N = 4, K = 2, 4 envs), so obs blocks
-    // never take the LDS a co-resident kernel (the fused actor, 2 x 78 KB per CU) needs.
+    // never take the LDS a co-resident kernel (the fused actor's 74-104 KB per CU) needs.
     extern __shared__ uint32_t obs_lds[];
     const int tid = threadIdx.x;
     const int HW = p.HW, N = p.N, K = p.K;
@@ -1866,6 +1866,7 @@ struct Env {
     // shaped reward, returns, FeAR stats rows) finishes on the aux stream, ordered by gw_fear_fence
     bool fear_async = false;
     bool fear_pending = false;
+    bool async_aux = false;                       // GW_ASYNC_AUX=1 (A/B): world + FeAR on the aux stream
     hipEvent_t fear_ev = nullptr;
     bool obs_queued = false;                      // an obs_kernel launch waits in qobs
     bool qobs_prof = false;                       // profiling state of the step that queued it
@@ -2346,6 +2347,8 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
         if (be) env->obs_be = std::max(1, std::min(gw::OBS_BE, std::atoi(be)));
         const char *nt = std::getenv("GW_OBS_NT");
         if (nt) env->obs_nt = std::atoi(nt) != 0;
+        const char *aa = std::getenv("GW_ASYNC_AUX");
+        if (aa) env->async_aux = std::atoi(aa) != 0;
         const char *op = std::getenv("GW_OBS_PRIO");
         if (op && std::strcmp(op, "hi") == 0) env->obs_hi = true;
         const char *ch = std::getenv("GW_CHUNKS");
@@ -2445,42 +2448,49 @@ gw_status gw_step(void *handle, const int32_t *rl_actions, const int32_t *script
     const int nch = ((env->mode == 1 || defer) && want_obs && env->chunks > 1 && env->E >= unit * env->chunks)
                         ? env->chunks : 1;
     if (env->obs_async && want_obs && nch == 1 && (env->mode == 1 || env->mode == 3)) {
-        // Software pipeline over steps.  The world update (and FeAR) of step t runs on the
-        // high-priority aux stream after the caller's prior work on s, and s joins it (rewards,
-        // dones, masks, state, stats: stream-ordered as usual).  The obs writer of step t runs
-        // on obs_stream right after the world update (eager), or is queued and launched at the
-        // start of step t+1 behind the caller's work in between (lazy), and overlaps FeAR and
-        // the world update + FeAR of step t+1, which read only the state.  The descriptor is double-buffered: step t writes
-        // desc_buf[nb]; obs_kernel(t-2) read that buffer, so the world update waits for it.
+        // Software pipeline over steps.  The world update (and FeAR) of step t runs on s
+        // (rewards, dones, masks, state, stats: stream-ordered as usual).  The obs writer of
+        // step t runs on obs_stream right after the world update (eager), or is queued and
+        // launched at the start of step t+1 behind the caller's work in between (lazy), and
+        // overlaps FeAR and the world update + FeAR of step t+1, which read only the state.
+        // The descriptor is double-buffered: step t writes desc_buf[nb]; obs_kernel(t-2) read
+        // that buffer, so the world update waits for it.
         GW_TRY(ensure_obs_stream(env));
-        HIP_TRY(hipEventRecord(env->sync_ev[0], s));  // fork: the caller's prior work on s
-        GW_TRY(flush_obs(env, env->sync_ev[0]));       // obs_kernel(t-1)
+        // the world update + FeAR chain runs on the caller's stream itself (no fork / join hops
+        // between consecutive steps); only with the unjoined FeAR (| 4) or GW_ASYNC_AUX=1 (A/B)
+        // does it go to the aux stream
+        const bool on_aux = (defer && env->fear_async) || env->async_aux;
+        hipStream_t ws = on_aux ? env->aux : s;
+        if (on_aux || env->obs_queued) HIP_TRY(hipEventRecord(env->sync_ev[0], s));  // the caller's prior work
+        GW_TRY(flush_obs(env, env->sync_ev[0]));       // lazy: obs_kernel(t-1), behind that work
         const int nb = env->dcur ^ 1;
         p.desc = env->desc_buf[nb];
         size_t b;
-        HIP_TRY(hipStreamWaitEvent(env->aux, env->sync_ev[0], 0));
-        if (env->obs_pending[nb]) HIP_TRY(hipStreamWaitEvent(env->aux, env->obs_done[nb], 0));
-        GW_TRY(span_begin(env->aux, b));
-        HIP_TRY(dispatch_step(env, p, env->aux));
-        GW_TRY(span_end(env->aux, b, 0));
-        HIP_TRY(hipEventRecord(env->world_ev, env->aux));
+        if (on_aux) HIP_TRY(hipStreamWaitEvent(ws, env->sync_ev[0], 0));
+        if (env->obs_pending[nb]) HIP_TRY(hipStreamWaitEvent(ws, env->obs_done[nb], 0));
+        GW_TRY(span_begin(ws, b));
+        HIP_TRY(dispatch_step(env, p, ws));
+        GW_TRY(span_end(ws, b, 0));
+        HIP_TRY(hipEventRecord(env->world_ev, ws));
         if (defer && env->fear_async) {
             // s joins the world update only: the caller's next work (the actor reads the
             // descriptors and masks) overlaps fear_v2; FeAR-owned outputs wait for gw_fear_fence
             HIP_TRY(hipStreamWaitEvent(s, env->world_ev, 0));
-            GW_TRY(span_begin(env->aux, b));
-            HIP_TRY(dispatch_fear(env, p, env->aux));
-            GW_TRY(span_end(env->aux, b, 2));
-            HIP_TRY(hipEventRecord(env->fear_ev, env->aux));
+            GW_TRY(span_begin(ws, b));
+            HIP_TRY(dispatch_fear(env, p, ws));
+            GW_TRY(span_end(ws, b, 2));
+            HIP_TRY(hipEventRecord(env->fear_ev, ws));
             env->fear_pending = true;
         } else {
             if (defer) {
-                GW_TRY(span_begin(env->aux, b));
-                HIP_TRY(dispatch_fear(env, p, env->aux));
-                GW_TRY(span_end(env->aux, b, 2));
+                GW_TRY(span_begin(ws, b));
+                HIP_TRY(dispatch_fear(env, p, ws));
+                GW_TRY(span_end(ws, b, 2));
             }
-            HIP_TRY(hipEventRecord(env->sync_ev[2], env->aux));  // join the world update + FeAR
-            HIP_TRY(hipStreamWaitEvent(s, env->sync_ev[2], 0));
+            if (on_aux) {
+                HIP_TRY(hipEventRecord(env->sync_ev[2], ws));  // join the world update + FeAR
+                HIP_TRY(hipStreamWaitEvent(s, env->sync_ev[2], 0));
+            }
         }
         env->qobs = p;
         env->qobs_buf = nb;
