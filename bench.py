@@ -47,6 +47,10 @@ CONFIGS = {
                workload="BASELINE config 5 per GPU: 32x32, N=4, K=2, 65536 envs/GPU, FeAR on, full rollout "
                         "(stacked MLP actors + GumbelSoftmax + mask + argmax, env step, zero-copy replay ring of "
                         "MEMORY_SIZE 200000, per-step RCCL reduction of the episode statistics)"),
+    "c4cnn": dict(scenario="grid64_n8", envs=65536, fear=False, fear_weight=-5.0, rollout=True, arch="cnn",
+                  workload="BASELINE config 4 as a rollout: 8-agent 64x64 grid, 65536 envs, the configs/cnn.yaml "
+                           "actor head (conv 32-64, k2 s2, 128-128; PyTorch/MIOpen f32) on the dense obs, env "
+                           "step, replay ring"),
 }
 
 
@@ -165,14 +169,21 @@ def main():
     if cfg.get("rollout"):  # c5: actor -> env -> replay (+ optional MADDPG updates) per step
         from marlnav.maddpg import MADDPG
         from marlnav.rollout import Rollout
-        learner = MADDPG(K, env.H, env.W, device=env.device, seed=rank, capturable=True)
-        ro = Rollout(env, learner.actors, replay_slots=-(-200_000 // E) + 1, training=True, seed=rank,
+        if cfg.get("arch") == "cnn":  # PyTorch CNN head on the dense obs (reads it: synchronous obs)
+            from marlnav.actor import MultiAgentActors
+            learner = None
+            actors = MultiAgentActors(K, env.H, env.W, arch="cnn", device=env.device, seed=rank)
+            obs_mode = False
+        else:
+            learner = MADDPG(K, env.H, env.W, device=env.device, seed=rank, capturable=True)
+            actors = learner.actors
+        ro = Rollout(env, actors, replay_slots=-(-200_000 // E) + 1, training=True, seed=rank,
                      obs_async=obs_mode, fear_async=bool(obs_mode) and args.fear_async)
         ro.reset()
 
         def one_step(i):  # noqa: F811
             r = ro.step()  # the StatsReducer inside does the per-step all-reduce across ranks
-            if args.updates_per_step and ro.replay.t >= 2:
+            if args.updates_per_step and learner is not None and ro.replay.t >= 2:
                 ro.fence()  # sampling reads the ring's obs slots
                 if learner._graph is None:
                     learner.capture(ro.replay)

@@ -123,8 +123,36 @@ class CNNActor(nn.Module):
         mlp.append(nn.Linear(dims[-1], n_actions))
         self.mlp = nn.Sequential(*mlp)
 
+        # configs/cnn.yaml's convs have kernel == stride (non-overlapping 2x2 patches, no padding):
+        # both convs are then per-patch GEMMs on hipBLASLt instead of MIOpen convolutions
+        self.patchify = (len(channels) == 2 and all(k == s for k, s in zip(kernels, strides))
+                         and H % (kernels[0] * kernels[1]) == 0 and W % (kernels[0] * kernels[1]) == 0)
+
     def forward(self, x):
+        if self.patchify:
+            return self._forward_patch_gemm(x)
         return self.mlp(self.conv(x).flatten(1))
+
+    def _forward_patch_gemm(self, x):
+        """Same function as ``conv -> flatten -> mlp`` (f32), with the two kernel == stride convs
+        as GEMMs: obs pixels are grouped by conv-2 patch once, so conv 1's output rows are already
+        conv 2's patch vectors (ky, kx, c order; the weights are permuted to match), and the
+        flattened NHWC conv-2 output meets a column-permuted first Linear."""
+        c1, c2 = self.conv[0], self.conv[2]
+        k1, k2 = c1.kernel_size[0], c2.kernel_size[0]
+        E, _, H, W = x.shape
+        H2, W2 = H // (k1 * k2), W // (k1 * k2)
+        # y = (k1 k2) y2 + k1 ky + py, x = (k1 k2) x2 + k1 kx + px
+        p = x.reshape(E, H2, k2, k1, W2, k2, k1).permute(0, 1, 4, 2, 5, 3, 6).reshape(-1, k1 * k1)
+        h = torch.relu(torch.addmm(c1.bias, p, c1.weight.reshape(c1.out_channels, -1).t()))
+        h = h.reshape(E * H2 * W2, k2 * k2 * c1.out_channels)                 # (ky, kx, c) per patch
+        w2 = c2.weight.permute(0, 2, 3, 1).reshape(c2.out_channels, -1)
+        h = torch.relu(torch.addmm(c2.bias, h, w2.t())).reshape(E, -1)       # NHWC flatten
+        lin = self.mlp[0]
+        wl = lin.weight.reshape(lin.out_features, c2.out_channels, H2, W2).permute(0, 2, 3, 1).reshape(
+            lin.out_features, -1)
+        h = torch.relu(torch.addmm(lin.bias, h, wl.t()))
+        return self.mlp[2:](h)
 
 
 class MultiAgentActors(nn.Module):
