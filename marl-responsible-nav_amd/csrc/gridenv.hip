@@ -1858,6 +1858,9 @@ struct Env {
     bool obs_async = false;
     bool obs_lazy = false;                        // gw_set_obs_async(env, 2): launch at the next step
     bool obs_hi = false;                          // GW_OBS_PRIO=hi (A/B): obs stream high priority, aux normal
+    // one obs stream: a second one alternating with the descriptor buffer (so obs_kernel(t+1)
+    // could start while obs_kernel(t) drains) measured 2.1x slower at C3 (more streams than the
+    // process's hardware queues, GPU_MAX_HW_QUEUES = 4; profiles/r1_async)
     hipStream_t obs_stream = nullptr;
     hipEvent_t obs_done[2] = {nullptr, nullptr};  // obs_kernel that read desc_buf[i] has finished
     bool obs_pending[2] = {false, false};
@@ -1896,7 +1899,20 @@ struct Env {
 };
 
 // the second stream and n fork/join events (timing disabled), created on first use
-gw_status ensure_aux(Env *env, int n) {
+// n fork/join events (timing disabled), created on first use
+gw_status ensure_events(Env *env, int n) {
+    while ((int)env->sync_ev.size() < n) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        env->sync_ev.push_back(e);
+    }
+    return GW_OK;
+}
+
+// the second stream (+ the third, aux2, for the chunked defer pipeline only) and n events.
+// Streams are created only where a path uses them: a process has few hardware queues
+// (GPU_MAX_HW_QUEUES = 4 on the box) and every extra stream competes for them.
+gw_status ensure_aux(Env *env, int n, bool need_aux2 = false) {
     if (!env->aux) {
         if (env->mode == 3 && env->defer_order == 3 && !env->obs_hi) {
             int lo = 0, hi = 0;
@@ -1906,19 +1922,17 @@ gw_status ensure_aux(Env *env, int n) {
             HIP_TRY(hipStreamCreateWithFlags(&env->aux, hipStreamNonBlocking));
         }
     }
-    while ((int)env->sync_ev.size() < n) {
-        hipEvent_t e;
-        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        env->sync_ev.push_back(e);
+    {
+        const gw_status st = ensure_events(env, n);
+        if (st != GW_OK) return st;
     }
-    if (!env->aux2) HIP_TRY(hipStreamCreateWithFlags(&env->aux2, hipStreamNonBlocking));
+    if (need_aux2 && !env->aux2) HIP_TRY(hipStreamCreateWithFlags(&env->aux2, hipStreamNonBlocking));
     return GW_OK;
 }
 
-// the async-obs stream (normal priority; the world update and FeAR go to the high-priority aux
-// stream) and its per-descriptor-buffer completion events, created on first use
+// the async-obs stream and its per-descriptor-buffer completion events, created on first use
 gw_status ensure_obs_stream(Env *env) {
-    const gw_status st = ensure_aux(env, 3);
+    const gw_status st = ensure_events(env, 3);
     if (st != GW_OK) return st;
     if (!env->obs_stream) {
         if (env->obs_hi) {
@@ -2460,6 +2474,7 @@ gw_status gw_step(void *handle, const int32_t *rl_actions, const int32_t *script
         // between consecutive steps); only with the unjoined FeAR (| 4) or GW_ASYNC_AUX=1 (A/B)
         // does it go to the aux stream
         const bool on_aux = (defer && env->fear_async) || env->async_aux;
+        if (on_aux) GW_TRY(ensure_aux(env, 3));
         hipStream_t ws = on_aux ? env->aux : s;
         if (on_aux || env->obs_queued) HIP_TRY(hipEventRecord(env->sync_ev[0], s));  // the caller's prior work
         GW_TRY(flush_obs(env, env->sync_ev[0]));       // lazy: obs_kernel(t-1), behind that work
@@ -2537,7 +2552,7 @@ gw_status gw_step(void *handle, const int32_t *rl_actions, const int32_t *script
     if (defer) {
         // env chunks: world update of chunk c on s, then its fear_v2 (aux) and obs_kernel (aux2)
         // while s moves on to chunk c + 1; s joins both streams at the end
-        GW_TRY(ensure_aux(env, nch + 2));
+        GW_TRY(ensure_aux(env, nch + 2, true));
         const int64_t per = ((env->E / nch + unit - 1) / unit) * unit;
         for (int c = 0; c < nch; ++c) {
             gw::Params q = p;

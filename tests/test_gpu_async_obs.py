@@ -143,3 +143,51 @@ def test_fear_async_env_outputs_after_fence():
     assert int(bad) == 0
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("mode", [True, "lazy"])
+def test_async_obs_same_buffer_every_step(mode):
+    """Async writers of consecutive steps into the SAME buffers (the env's own obs / final_obs,
+    two obs streams): the write-after-write order holds, the buffers end as the last step's."""
+    sc = S.builtin("grid32")
+    E, T = 4096, 15
+    mk = lambda: VecGridEnv(sc, num_envs=E, fear=True, fear_weight=-5.0, seed=12, final_obs=True, stats=True)
+    a, b = mk(), mk()
+    b.set_obs_async(mode)
+    a.reset()
+    b.reset()
+    for t in range(T):
+        r1, r2 = a.step(), b.step()
+    b.obs_fence()
+    differ = lambda x, y: (~((x == y) | (x.isnan() & y.isnan()))).sum()  # final_obs starts as NaN
+    bad = differ(r1.obs, r2.obs) + differ(r1.final_obs, r2.final_obs) + (r1.reward != r2.reward).sum()
+    torch.cuda.synchronize()
+    assert int(bad) == 0
+    a.close()
+    b.close()
+
+
+def test_async_obs_alternating_buffers():
+    """The bench's double-buffered obs outputs (step t into buffer t & 1): every buffer holds
+    the obs of the last step that wrote it."""
+    sc = S.builtin("grid32")
+    E, T = 4096, 16
+    a = VecGridEnv(sc, num_envs=E, fear=True, fear_weight=-5.0, seed=13)
+    b = VecGridEnv(sc, num_envs=E, fear=True, fear_weight=-5.0, seed=13)
+    b.set_obs_async(True)
+    bufs = [b.out["obs"], torch.empty_like(b.out["obs"])]
+    a.reset()
+    b.reset()
+    bad = torch.zeros((), dtype=torch.int64, device="cuda")
+    last = [None, None]
+    for t in range(T):
+        r1 = a.step()
+        b.step(obs_out=bufs[t & 1])
+        last[t & 1] = r1.obs.clone()
+    b.obs_fence()
+    for i in range(2):
+        bad += (last[i] != bufs[i]).sum()
+    torch.cuda.synchronize()
+    assert int(bad) == 0
+    a.close()
+    b.close()
