@@ -54,17 +54,17 @@ CONFIGS = {
 }
 
 
-def algorithmic_bytes(N: int, K: int, HW: int):
+def algorithmic_bytes(N: int, K: int, HW: int, obs_bytes: int = 4):
     """Bytes per env-step each kernel must move at minimum:
     step_kernel: state read+write (pos 4N, flags 4, t 4, prev 4K, score 8, fear_score 8; x2)
                  + episode 4 read + outputs (reward/fear/shaped 24K, term/trunc 2K, mask 2K,
                  done 1, crashes 4, apples 4, ep_return 8, ep_fear 8, ep_len 4)
                  + obs descriptor 20 written;
-    obs_kernel:  obs 4*K*HW written + descriptor 20 read."""
+    obs_kernel:  obs 4*K*HW written (2*K*HW with --obs-dtype bf16) + descriptor 20 read."""
     state = 2 * (4 * N + 4 + 4 + 4 * K + 8 + 8) + 4
     outputs = 24 * K + 2 * K + 2 * K + 1 + 4 + 4 + 8 + 8 + 4
     step_b = state + outputs + 20
-    obs_b = 4 * K * HW + 20
+    obs_b = obs_bytes * K * HW + 20
     return step_b, obs_b
 
 
@@ -117,6 +117,9 @@ def main():
     ap.add_argument("--fear-async", action="store_true",
                     help="c5: let the next actor overlap the FeAR kernel (gw_set_obs_async | 4; A/B, "
                          "measured slower: profiles/r1_async)")
+    ap.add_argument("--obs-dtype", default="f32", choices=["f32", "bf16"],
+                    help="bf16: the lossless compact obs format (gw_set_obs_dtype); reported separately, "
+                         "the metric's definition is f32 obs")
     ap.add_argument("--obs-eager", action="store_true",
                     help="c5: start each step's obs writer right after its world update (A/B)")
     ap.add_argument("--obs-lazy", action="store_true",
@@ -150,7 +153,8 @@ def main():
         cfg["workload"] += f" [override: FeAR {'on' if cfg['fear'] else 'off'}]"
     E = cfg["envs"]
     env = VecGridEnv(cfg["scenario"], num_envs=E, fear=cfg["fear"], fear_weight=cfg["fear_weight"],
-                     max_steps=150, auto_reset=True, seed=42, env_offset=rank * E, stats=True)
+                     max_steps=150, auto_reset=True, seed=42, env_offset=rank * E, stats=True,
+                     obs_dtype=torch.bfloat16 if args.obs_dtype == "bf16" else torch.float32)
     N, K, HW = env.N, env.K, env.H * env.W
     stream = torch.cuda.current_stream()
     stats_acc = torch.zeros_like(env.out["stats"][0])
@@ -231,7 +235,7 @@ def main():
     stats = r.stats.sum(0).cpu().tolist()
 
     if rank == 0:
-        step_b, obs_b = algorithmic_bytes(N, K, HW)
+        step_b, obs_b = algorithmic_bytes(N, K, HW, 2 if args.obs_dtype == "bf16" else 4)
         avg_step_ms, avg_obs_ms = ms_step / max(nprof, 1), ms_obs / max(nprof, 1)
         avg_fear_ms = ms_fear / max(nprof, 1)
         fused = env.fused
@@ -246,7 +250,8 @@ def main():
         try:  # HBM bytes measured by the PMC passes committed under profiles/ for this workload
             with open(os.path.join(REPO, "profiles", "latest.json")) as f:
                 prof = json.load(f)
-            if prof.get("config") == args.config and not args.envs and args.fear < 0 and not fused:
+            if prof.get("config") == args.config and not args.envs and args.fear < 0 and not fused \
+                    and args.obs_dtype == "f32":
                 traffic = prof["kernels"][dom]["hbm_bytes_per_launch"]
                 traffic_src = prof["source"]
         except (OSError, KeyError, ValueError):
@@ -267,7 +272,7 @@ def main():
             "data": "synthetic (device Philox spawns / scripted policy / random RL policy)",
             "config": {"workload": cfg["workload"], "scenario": cfg["scenario"], "envs_per_gpu": E,
                        "global_envs": world * E, "agents": N, "rl_agents": K, "grid": [env.H, env.W],
-                       "fear": cfg["fear"], "parallelism": f"env-sharded dp{world}"},
+                       "fear": cfg["fear"], "parallelism": f"env-sharded dp{world}", "obs_dtype": args.obs_dtype},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
                          "traffic_source": traffic_src,

@@ -191,6 +191,14 @@ gw_status gw_obs_view(void *env, gw_obs_source *out);
  * and the next gw_step order themselves).
  * Only the split / defer kernel paths pipeline; the others stay synchronous. */
 gw_status gw_set_obs_async(void *env, int enable);
+
+/* Observation element type of every obs / final_obs buffer the env writes (gw_reset, gw_step):
+ * GW_OBS_F32 (default; the reference's values as float32) or GW_OBS_BF16 (the same values as
+ * bfloat16 bits, [K][E][H*W] uint16: every value the env produces is exact in bf16, so this is
+ * lossless and halves the obs bytes; needs H*W % 8 == 0 and the split / defer kernel paths).
+ * The float* obs pointers then address bf16 buffers. */
+enum { GW_OBS_F32 = 0, GW_OBS_BF16 = 1 };
+gw_status gw_set_obs_dtype(void *env, int dtype);
 gw_status gw_obs_fence(void *env, void *stream);
 gw_status gw_fear_fence(void *env, void *stream);
 /* Set the thread-local error text returned by gw_last_error (for the library's other

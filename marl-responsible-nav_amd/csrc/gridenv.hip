@@ -35,6 +35,7 @@ namespace gw {
 constexpr int NA = GW_N_ACTIONS;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void store_nt(float4 *dst, const float4 &v) {
     const f32x4 x = {v.x, v.y, v.z, v.w};
     __builtin_nontemporal_store(x, reinterpret_cast<f32x4 *>(dst));
@@ -86,6 +87,7 @@ struct Params {
     uint32_t key0, key1;
     uint32_t w_magic;         // ceil(2^32 / W)  (exact /W for cells < 2^16)
     uint32_t hw4_magic;       // ceil(2^32 / (H*W/4))
+    uint32_t hw8_magic;       // ceil(2^32 / (H*W/8))
     int lds_cdf, n_cdf, ctab_off, resp_off;  // step_v2 dynamic LDS: [cdf][cell table][Resp 100 f64]
     int obs_be;               // envs per obs_kernel block (<= OBS_BE)
     int64_t e_begin, e_end;   // env range of this launch (step_v2 / obs_kernel chunks)
@@ -1022,7 +1024,7 @@ __global__ void __launch_bounds__(256) reset_kernel(Params p) {
 // Each (env, k) has at most N+1 non-map cells ("patches"), computed once per block in LDS;
 // the store loop is then map float4 + <= N+1 compares per 16-byte store.
 // ---------------------------------------------------------------------------------------
-constexpr int OBS_BE = 8;      // envs per block
+constexpr int OBS_BE = 16;     // envs per block (max)
 constexpr int OBS_THREADS = 256;
 
 __device__ __forceinline__ float agent_value(bool reset, int n, int k, bool on_apple, int variant) {
@@ -1035,7 +1037,11 @@ __device__ __forceinline__ float agent_value(bool reset, int n, int k, bool on_a
     return (float)v;
 }
 
-template <bool VEC4, bool NT>
+// bf16 bits of an obs value: every value the env writes (-1, 0, 0.5, 1, 5..13, 9.5) is exact in
+// bf16, so the compact format is lossless (the low 16 bits of the f32 are zero)
+__device__ __forceinline__ uint32_t bf16_bits(float v) { return __float_as_uint(v) >> 16; }
+
+template <bool VEC4, bool NT, bool BF16 = false>
 __global__ void __launch_bounds__(OBS_THREADS) obs_kernel(Params p, float *__restrict__ obs,
                                                           float *__restrict__ final_obs) {
     // LDS sized to the launch (obs_lds_bytes): road bitmask, flags, then per (which, env, k)
@@ -1090,7 +1096,38 @@ __global__ void __launch_bounds__(OBS_THREADS) obs_kernel(Params p, float *__res
         float *dst = which == 0 ? obs : final_obs;
         if (!dst) continue;
         const uint32_t need = which == 0 ? D_WRITE : D_FINAL;
-        if (VEC4) {
+        if constexpr (BF16) {  // 8 cells = one 16-byte store per thread (HW % 8 == 0)
+            const int HW8 = HW >> 3;
+            const int total8 = nenv * HW8;
+            for (int k = 0; k < K; ++k) {
+                uint4 *out8 = reinterpret_cast<uint4 *>(reinterpret_cast<uint16_t *>(dst) + ((int64_t)k * p.E + e0) * HW);
+                for (int i8 = tid; i8 < total8; i8 += OBS_THREADS) {
+                    const int el = HW8 == 1 ? i8 : (int)__umulhi((uint32_t)i8, p.hw8_magic);
+                    if (!(s_flag[el] & need)) continue;
+                    const int c0 = (i8 - el * HW8) << 3;
+                    const uint32_t rb = s_road[c0 >> 5] >> (c0 & 31);  // 8 cells share one word
+                    // map: road 0.0 (bits 0x0000), inactive -1.0 (0xBF80), two cells per word
+                    u32x4 w;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        w[j] = (((rb >> (2 * j)) & 1u) ? 0u : 0xBF80u) | (((rb >> (2 * j + 1)) & 1u) ? 0u : 0xBF800000u);
+                    const int slot = ((which * p.obs_be + el) * K + k) * npatch;
+                    for (int q = 0; q < npatch; ++q) {  // later patches override earlier ones
+                        const int dd = s_pc[slot + q] - c0;
+                        if ((unsigned)dd < 8u) {
+                            const uint32_t sh = 16u * (dd & 1), b = bf16_bits(s_pv[slot + q]) << sh;
+#pragma unroll
+                            for (int j = 0; j < 4; ++j)
+                                w[j] = (dd >> 1) == j ? ((w[j] & ~(0xFFFFu << sh)) | b) : w[j];
+                        }
+                    }
+                    if (NT)
+                        __builtin_nontemporal_store(w, reinterpret_cast<u32x4 *>(&out8[i8]));
+                    else
+                        *reinterpret_cast<u32x4 *>(&out8[i8]) = w;
+                }
+            }
+        } else if (VEC4) {
             const int HW4 = HW >> 2;
             const int total4 = nenv * HW4;
             for (int k = 0; k < K; ++k) {
@@ -1842,6 +1879,9 @@ struct Env {
                          // 2 "fused", 3 "defer" (default; FeAR on: step_v2 <DEFER>, then fear_v2 || obs_kernel)
     int obs_be = 2;      // GW_OBS_BE: envs per obs_kernel block (default: see gw_create)
     bool obs_nt = true;  // GW_OBS_NT=0: plain instead of nontemporal obs stores
+    bool obs_bf16 = false;  // gw_set_obs_dtype(env, GW_OBS_BF16): obs buffers hold bf16 (lossless)
+    bool obs_be_fixed = false;  // GW_OBS_BE given
+    int obs_be_f32 = 2;         // the float32 writer's default
     uint32_t *celltab = nullptr;
     uint32_t *roadbits = nullptr;
     int defer_order = 3;            // GW_DEFER (A/B): 0 fear then obs on one stream; 1 fear on a second
@@ -2075,6 +2115,8 @@ gw::Params make_params(const Env *env) {
     {
         const uint64_t hw4 = (uint64_t)std::max(1, env->HW / 4);
         p.hw4_magic = (uint32_t)std::min<uint64_t>(0xFFFFFFFFull, (((uint64_t)1 << 32) + hw4 - 1) / hw4);
+        const uint64_t hw8 = (uint64_t)std::max(1, env->HW / 8);
+        p.hw8_magic = (uint32_t)std::min<uint64_t>(0xFFFFFFFFull, (((uint64_t)1 << 32) + hw8 - 1) / hw8);
     }
     for (int k = 0; k < GW_MAX_AGENTS; ++k) p.apples[k] = env->apples[k];
     return p;
@@ -2214,7 +2256,9 @@ hipError_t launch_obs(const Env *env, const gw::Params &p, float *obs, float *fi
     // obs_kernel's LDS: road bitmask, OBS_BE flags, [2][obs_be][K][N + 1] patch cells + values
     const size_t lds = sizeof(uint32_t) * ((env->HW + 31) / 32 + gw::OBS_BE) +
                        (size_t)2 * 2 * env->obs_be * env->K * (env->N + 1) * sizeof(uint32_t);
-    if (env->HW % 4 == 0) {
+    if (env->obs_bf16) {  // gw_set_obs_dtype checked HW % 8 == 0
+        hipLaunchKernelGGL((gw::obs_kernel<true, true, true>), dim3(grid), dim3(gw::OBS_THREADS), lds, s, p, obs, final_obs);
+    } else if (env->HW % 4 == 0) {
         if (env->obs_nt)
             hipLaunchKernelGGL((gw::obs_kernel<true, true>), dim3(grid), dim3(gw::OBS_THREADS), lds, s, p, obs, final_obs);
         else
@@ -2356,9 +2400,11 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
         // 4 envs: 2.5 % faster step at C3)
         int be_def = std::max(1, 4096 / std::max(1, K * HW));
         if (env->mode == 3 && env->fear) be_def *= 2;
-        env->obs_be = std::max(1, std::min(gw::OBS_BE, be_def));
+        env->obs_be = std::max(1, std::min(8, be_def));  // f32 default <= 8 envs per block
         const char *be = std::getenv("GW_OBS_BE");
         if (be) env->obs_be = std::max(1, std::min(gw::OBS_BE, std::atoi(be)));
+        env->obs_be_fixed = be != nullptr;
+        env->obs_be_f32 = env->obs_be;
         const char *nt = std::getenv("GW_OBS_NT");
         if (nt) env->obs_nt = std::atoi(nt) != 0;
         const char *aa = std::getenv("GW_ASYNC_AUX");
@@ -2640,6 +2686,22 @@ gw_status gw_obs_fence(void *handle, void *stream) {
     Env *env = static_cast<Env *>(handle);
     if (!env) return fail(GW_ERR_ARG, "null env");
     GW_TRY(wait_obs(env, static_cast<hipStream_t>(stream)));
+    return GW_OK;
+}
+
+gw_status gw_set_obs_dtype(void *handle, int dtype) {
+    Env *env = static_cast<Env *>(handle);
+    if (!env) return fail(GW_ERR_ARG, "null env");
+    if (dtype != GW_OBS_F32 && dtype != GW_OBS_BF16) return fail(GW_ERR_ARG, "gw_set_obs_dtype: unknown dtype");
+    if (dtype == GW_OBS_BF16 && (env->HW % 8 != 0 || env->mode == 0 || env->mode == 2))
+        return fail(GW_ERR_ARG, "gw_set_obs_dtype: bf16 obs needs H*W % 8 == 0 and the split / defer kernel paths");
+    const bool bf = dtype == GW_OBS_BF16;
+    // bf16 writer: ~64 KB of obs per block (C3: 16 envs, 4.3 TB/s; 4 envs 3.4, 8 envs 4.2;
+    // C4: 4 envs; profiles/r1_bf16); f32: the create-time default
+    if (!env->obs_be_fixed)
+        env->obs_be = bf ? std::max(1, std::min(gw::OBS_BE, 32768 / std::max(1, env->K * env->HW)))
+                         : env->obs_be_f32;
+    env->obs_bf16 = bf;
     return GW_OK;
 }
 

@@ -166,7 +166,7 @@ EXPORTS = ["gw_create", "gw_reset", "gw_step", "gw_state_view", "gw_copy_state",
            "gw_profile_read", "gw_stats_rows", "gw_dims", "gw_last_error", "gw_destroy", "gw_fear_matrix",
            "gw_adam_step", "gw_soft_update", "gw_obs_view", "gw_set_last_error", "gw_actor_act",
            "gw_actor_workspace_floats", "gw_actor_prepare", "gw_rollout_tick", "gw_set_obs_async",
-           "gw_obs_fence", "gw_fear_fence"]
+           "gw_obs_fence", "gw_fear_fence", "gw_set_obs_dtype"]
 
 
 class GwObsSource(C.Structure):
@@ -230,6 +230,8 @@ def _declare(L):
     L.gw_obs_fence.restype = C.c_int
     L.gw_fear_fence.argtypes = [p, p]
     L.gw_fear_fence.restype = C.c_int
+    L.gw_set_obs_dtype.argtypes = [p, C.c_int]
+    L.gw_set_obs_dtype.restype = C.c_int
     L.gw_destroy.argtypes = [p]
     L.gw_destroy.restype = None
     return L

@@ -30,8 +30,9 @@ class ReplayRing:
     def __init__(self, env: VecGridEnv, slots: int):
         self.S = max(2, int(slots))
         K, E, H, W, dev = env.K, env.E, env.H, env.W, env.device
-        self.obs = torch.zeros((self.S, K, E, H, W), dtype=torch.float32, device=dev)
-        self.final_obs = torch.zeros((self.S, K, E, H, W), dtype=torch.float32, device=dev)
+        od = env.obs_dtype  # bf16 obs (lossless) halves the ring; sample() hands out float32
+        self.obs = torch.zeros((self.S, K, E, H, W), dtype=od, device=dev)
+        self.final_obs = torch.zeros((self.S, K, E, H, W), dtype=od, device=dev)
         self.probs = torch.zeros((self.S, K, E, 9), dtype=torch.float32, device=dev)
         self.reward = torch.zeros((self.S, E, K), dtype=torch.float64, device=dev)
         self.term = torch.zeros((self.S, E, K), dtype=torch.uint8, device=dev)
@@ -56,10 +57,10 @@ class ReplayRing:
         env = torch.randint(0, self.E, (batch,), device=dev, generator=generator)
         tr = (self.t_dev - 1 - step) % self.S      # transition slot (its state is obs[tr])
         nx = (tr + 1) % self.S
-        state = self.obs[tr, :, env].permute(1, 0, 2, 3)
+        state = self.obs[tr, :, env].permute(1, 0, 2, 3).float()
         done = self.done[tr, env].bool()
         next_state = torch.where(done[None, :, None, None], self.final_obs[tr, :, env].permute(1, 0, 2, 3),
-                                 self.obs[nx, :, env].permute(1, 0, 2, 3))
+                                 self.obs[nx, :, env].permute(1, 0, 2, 3)).float()
         out = (state, self.probs[tr, :, env].permute(1, 0, 2), self.reward[tr, env], next_state, self.term[tr, env])
         return out + ((tr, env),) if return_idx else out
 

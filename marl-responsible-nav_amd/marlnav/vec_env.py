@@ -7,6 +7,7 @@ optional auto-reset (the ``break`` + ``env.reset()`` of maddpg/agent.py:241 / ma
 
 Layouts (device tensors, owned by the env and overwritten by the next call):
   obs        [K, E, H, W] float32   agent-major: obs[k] is RL agent k's actor input batch
+             (obs_dtype=torch.bfloat16: the same values, exact, in half the bytes)
   reward, fear, shaped      [E, K] float64
   term, trunc               [E, K] uint8;  done [E] uint8
   mask       [E, K] int16 (9-bit action mask, bit a = action a allowed)
@@ -62,7 +63,8 @@ class VecGridEnv:
     def __init__(self, scenario: CompiledScenario | str = "level3", num_envs: int = 1, fear: bool = True,
                  fear_weight: float = -5.0, max_steps: int = 150, auto_reset: bool = True, seed: int = 42,
                  device: torch.device | int | None = None, env_offset: int = 0, final_obs: bool = False,
-                 debug: bool = False, obs: bool = True, stats: bool = False, variant: int | str = 0):
+                 debug: bool = False, obs: bool = True, stats: bool = False, variant: int | str = 0,
+                 obs_dtype: torch.dtype = torch.float32):
         if not torch.cuda.is_available():
             raise _lib.GwError("VecGridEnv needs a HIP device (no CPU fallback by design)")
         sc = builtin(scenario) if isinstance(scenario, str) else scenario
@@ -95,12 +97,17 @@ class VecGridEnv:
         with torch.cuda.device(self.device):
             _lib.check(self.lib.gw_create(C.byref(scn), C.byref(cfg), self.device.index, C.byref(h)), "gw_create")
         self.handle = h
+        if obs_dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError("obs_dtype: torch.float32 or torch.bfloat16")
+        self.obs_dtype = obs_dtype
+        if obs_dtype == torch.bfloat16:  # lossless: every obs value is exact in bf16
+            _lib.check(self.lib.gw_set_obs_dtype(self.handle, 1), "gw_set_obs_dtype")
 
         dev, E, K, N = self.device, self.E, self.K, self.N
         f64 = dict(dtype=torch.float64, device=dev)
         self.out = dict(
-            obs=torch.empty((K, E, sc.H, sc.W), dtype=torch.float32, device=dev) if obs else None,
-            final_obs=torch.full((K, E, sc.H, sc.W), float("nan"), dtype=torch.float32, device=dev) if final_obs else None,
+            obs=torch.empty((K, E, sc.H, sc.W), dtype=obs_dtype, device=dev) if obs else None,
+            final_obs=torch.full((K, E, sc.H, sc.W), float("nan"), dtype=obs_dtype, device=dev) if final_obs else None,
             reward=torch.zeros((E, K), **f64), fear=torch.zeros((E, K), **f64), shaped=torch.zeros((E, K), **f64),
             term=torch.zeros((E, K), dtype=torch.uint8, device=dev),
             trunc=torch.zeros((E, K), dtype=torch.uint8, device=dev),
@@ -168,6 +175,8 @@ class VecGridEnv:
             sizes = {"KEHW": self.K * self.E * self.H * self.W, "EK": self.E * self.K, "E": self.E}
             for name, t in over.items():
                 dt, shp = self._INTO_SPEC[name]
+                if shp == "KEHW":
+                    dt = self.obs_dtype
                 if t.dtype != dt or t.numel() != sizes[shp] or not t.is_contiguous() or t.device != self.device:
                     raise ValueError(f"step(into={name!r}): need a contiguous {dt} tensor of {sizes[shp]} elements "
                                      f"on {self.device}")
