@@ -2696,6 +2696,11 @@ gw_status gw_set_obs_dtype(void *handle, int dtype) {
     if (dtype == GW_OBS_BF16 && (env->HW % 8 != 0 || env->mode == 0 || env->mode == 2))
         return fail(GW_ERR_ARG, "gw_set_obs_dtype: bf16 obs needs H*W % 8 == 0 and the split / defer kernel paths");
     const bool bf = dtype == GW_OBS_BF16;
+    if (bf != env->obs_bf16 && env->obs_stream) {
+        // an obs_kernel still queued or in flight was sized for the old format: drain it first
+        GW_TRY(flush_obs(env, nullptr));
+        HIP_TRY(hipStreamSynchronize(env->obs_stream));
+    }
     // bf16 writer: ~64 KB of obs per block (C3: 16 envs, 4.3 TB/s; 4 envs 3.4, 8 envs 4.2;
     // C4: 4 envs; profiles/r1_bf16); f32: the create-time default
     if (!env->obs_be_fixed)
