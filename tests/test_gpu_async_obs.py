@@ -168,8 +168,8 @@ def test_async_obs_same_buffer_every_step(mode):
 
 
 def test_async_obs_alternating_buffers():
-    """The bench's double-buffered obs outputs (step t into buffer t & 1): every buffer holds
-    the obs of the last step that wrote it."""
+    """Double-buffered obs outputs (step t into buffer t & 1, e.g. replay slots): every buffer
+    holds the obs of the last step that wrote it."""
     sc = S.builtin("grid32")
     E, T = 4096, 16
     a = VecGridEnv(sc, num_envs=E, fear=True, fear_weight=-5.0, seed=13)
