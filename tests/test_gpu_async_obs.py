@@ -104,7 +104,8 @@ def test_async_rollout_fused_actor_matches_sync(mode, fear_async):
         bad += (r0.done != r1.done).sum() + (r0.mask != r1.mask).sum()
         if not fear_async:  # else the FeAR outputs are ordered by the next step / fence
             bad += (r0.shaped != r1.shaped).sum()
-    ros[1].fence()
+    for ro in ros:
+        ro.fence()
     for name in ("obs", "final_obs", "probs", "reward", "term", "done", "t_dev"):
         bad += (getattr(ros[0].replay, name) != getattr(ros[1].replay, name)).sum()
     st0, st1 = envs[0].state(), envs[1].state()
