@@ -136,9 +136,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
-    torch.cuda.set_device(local)
+    torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # RCCL ("nccl") over xGMI; MARLNAV_DIST_BACKEND=gloo only rehearses the multi-rank path
+        # with several ranks on one GPU (RCCL refuses duplicate devices)
+        backend = os.environ.get("MARLNAV_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     cfg = dict(CONFIGS[args.config])
     # obs writer pipelined with the next step (gw_set_obs_async): right after the world update
