@@ -108,7 +108,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--updates-per-step", type=int, default=0,
                     help="c5 only: MADDPG updates (batch 128, one HIP-graph replay each) per env step")
-    ap.add_argument("--profile-every", type=int, default=8,
+    ap.add_argument("--profile-every", type=int, default=16,
                     help="bracket every n-th timed step's kernels with HIP events (0 = none); the "
                          "events themselves cost ~2-3 us per kernel boundary, so not every step")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
