@@ -152,6 +152,13 @@ def main():
     # otherwise lose CUs to it) for the full rollout.  Measured A/B: profiles/r1_async/
     obs_mode = False if args.sync_obs else \
         ("lazy" if (args.obs_lazy or (cfg.get("rollout") and not args.obs_eager)) else True)
+    # small batches (C2: 34 MB of obs per step) are bound by the launch chain, where the async
+    # path's extra event records / waits cost more host time than the overlap saves
+    # (tools/host_cost.py: 24.1 sync vs 25.8 us async wall per step at 4,096 envs)
+    hw = {"grid32": 1024, "grid64_n8": 4096, "level3": 160}.get(cfg["scenario"], 1024)
+    if obs_mode and not cfg.get("rollout") and not (args.obs_lazy or args.obs_eager) and \
+            (args.envs or cfg["envs"]) * 2 * hw * (2 if args.obs_dtype == "bf16" else 4) < (128 << 20):
+        obs_mode = False
     if args.envs:
         cfg["envs"] = args.envs
     if args.fear >= 0:
