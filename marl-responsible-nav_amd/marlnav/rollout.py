@@ -115,6 +115,9 @@ class Rollout:
         self.env.obs_fence()
 
     def reset(self):
+        # the previous step's statistics (and its ring tick) are reduced before the ring's step
+        # count restarts, so t_dev never runs ahead of the transitions written
+        self._flush()
         if self.replay is not None:
             obs, mask = self.env.reset()
             self.replay.obs[0].copy_(obs)

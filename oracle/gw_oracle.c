@@ -600,21 +600,30 @@ static void gather_obs(const orc_world *w, float *dst, int64_t E, int64_t e, con
     for (int k = 0; k < w->K; ++k) memcpy(dst + ((int64_t)k * E + e) * HW, src + k * HW, sizeof(float) * HW);
 }
 
-void orc_vec_step(const orc_world *w, orc_env *envs, int64_t E, const int32_t *rl_act,
-                  int auto_reset, float *obs, orc_step_out *outs, int nthreads) {
+void orc_vec_step_final(const orc_world *w, orc_env *envs, int64_t E, const int32_t *rl_act,
+                        int auto_reset, float *obs, float *final_obs, orc_step_out *outs, int nthreads) {
     int64_t HW = (int64_t)w->H * w->W;
 #pragma omp parallel num_threads(nthreads)
     {
         float *tmp = (float *)malloc(sizeof(float) * HW * w->K);
+        float *fin = (float *)malloc(sizeof(float) * HW * w->K);
 #pragma omp for schedule(static)
         for (int64_t e = 0; e < E; ++e) {
             orc_step_out o;
+            orc_step_out *op = outs ? &outs[e] : &o;
             orc_env_step(w, w->env_offset + e, &envs[e], rl_act ? rl_act + e * w->K : NULL, NULL,
-                         NULL, auto_reset, obs ? tmp : NULL, NULL, outs ? &outs[e] : &o);
+                         NULL, auto_reset, obs ? tmp : NULL, final_obs ? fin : NULL, op);
             if (obs) gather_obs(w, obs, E, e, tmp);
+            if (final_obs && op->done) gather_obs(w, final_obs, E, e, fin);
         }
         free(tmp);
+        free(fin);
     }
+}
+
+void orc_vec_step(const orc_world *w, orc_env *envs, int64_t E, const int32_t *rl_act,
+                  int auto_reset, float *obs, orc_step_out *outs, int nthreads) {
+    orc_vec_step_final(w, envs, E, rl_act, auto_reset, obs, NULL, outs, nthreads);
 }
 
 void orc_vec_reset(const orc_world *w, orc_env *envs, int64_t E, float *obs, int nthreads) {

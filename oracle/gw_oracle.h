@@ -142,6 +142,10 @@ void orc_env_step(const orc_world *w, int64_t env_id, orc_env *s, const int32_t 
  * per-env outputs are written to outs[E] (may be NULL).  nthreads OpenMP threads. */
 void orc_vec_step(const orc_world *w, orc_env *envs, int64_t E, const int32_t *rl_act,
                   int auto_reset, float *obs, orc_step_out *outs, int nthreads);
+/* The same; final_obs [K][E][H*W] (or NULL) receives the terminal obs of the envs that ended
+ * this step (their rows are left untouched otherwise). */
+void orc_vec_step_final(const orc_world *w, orc_env *envs, int64_t E, const int32_t *rl_act,
+                        int auto_reset, float *obs, float *final_obs, orc_step_out *outs, int nthreads);
 void orc_vec_reset(const orc_world *w, orc_env *envs, int64_t E, float *obs, int nthreads);
 
 int orc_sizeof_env(void);

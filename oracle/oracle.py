@@ -75,6 +75,7 @@ def lib():
         L.orc_env_reset.argtypes = [p, C.c_int64, p, p, p, p]
         L.orc_env_step.argtypes = [p, C.c_int64, p, p, p, p, C.c_int, p, p, p]
         L.orc_vec_step.argtypes = [p, p, C.c_int64, p, C.c_int, p, p, C.c_int]
+        L.orc_vec_step_final.argtypes = [p, p, C.c_int64, p, C.c_int, p, p, p, C.c_int]
         L.orc_vec_reset.argtypes = [p, p, C.c_int64, p, C.c_int]
         L.orc_sizeof_env.restype = C.c_int
         L.orc_sizeof_step_out.restype = C.c_int
@@ -189,10 +190,11 @@ class OracleEnvs:
         return obs, final_obs, out
 
     def vec_step(self, rl_act=None, obs: np.ndarray | None = None, outs=None, nthreads: int = 1,
-                 auto_reset: bool = True):
+                 auto_reset: bool = True, final_obs: np.ndarray | None = None):
+        """obs / final_obs: [K, E, H*W] float32 (final_obs rows written for the envs that ended)."""
         ra = None if rl_act is None else np.ascontiguousarray(rl_act, np.int32)
-        lib().orc_vec_step(C.byref(self.world), self.envs, self.E, _ptr(ra), int(auto_reset),
-                           _ptr(obs), outs, nthreads)
+        lib().orc_vec_step_final(C.byref(self.world), self.envs, self.E, _ptr(ra), int(auto_reset),
+                                 _ptr(obs), _ptr(final_obs), outs, nthreads)
 
     def state(self, e: int) -> Env:
         return self.envs[e]

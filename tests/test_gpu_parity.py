@@ -78,22 +78,26 @@ def test_gpu_replays_reference_trajectory(fname, seed):
     st.env.close()
 
 
-def _compare_native(sc, E, fear, steps, nthreads=16, offset=0, seed=7, weight=-5.0):
-    """GPU native-RNG rollout == C oracle rollout, every output, every step (bit-exact)."""
-    env = VecGridEnv(sc, num_envs=E, fear=fear, fear_weight=weight, max_steps=150, auto_reset=True,
+def _compare_native(sc, E, fear, steps, nthreads=16, offset=0, seed=7, weight=-5.0, max_steps=150,
+                    return_capped=False):
+    """GPU native-RNG rollout == C oracle rollout, every output, every step (bit-exact).
+    Returns the number of completed episodes (and, with return_capped, how many of them ended
+    at the max_steps cap, maddpg/agent.py:243-247)."""
+    env = VecGridEnv(sc, num_envs=E, fear=fear, fear_weight=weight, max_steps=max_steps, auto_reset=True,
                      seed=seed, env_offset=offset, final_obs=True, debug=True, stats=True)
     guard = torch.full((1 << 16,), 7.0, dtype=torch.float64, device=env.device)  # canary after stats
-    orc = O.OracleEnvs(sc, E, fear=fear, fear_weight=weight, max_steps=150, seed=seed, env_offset=offset,
+    orc = O.OracleEnvs(sc, E, fear=fear, fear_weight=weight, max_steps=max_steps, seed=seed, env_offset=offset,
                        reset=False)
     obs_o = np.zeros((sc.K, E, sc.HW), np.float32)
     orc.reset_all(obs=obs_o, nthreads=nthreads)
     obs_g, _ = env.reset()
     np.testing.assert_array_equal(obs_g.reshape(sc.K, E, -1).cpu().numpy(), obs_o, err_msg="reset obs")
     outs = (O.StepOut * E)()
-    done_total = 0
+    fin_o = np.zeros((sc.K, E, sc.HW), np.float32)
+    done_total = capped = 0
     for t in range(steps):
         r = env.step()
-        orc.vec_step(None, obs=obs_o, outs=outs, nthreads=nthreads)
+        orc.vec_step(None, obs=obs_o, outs=outs, nthreads=nthreads, final_obs=fin_o)
         torch.cuda.synchronize()
         K, N = sc.K, sc.N
         get = lambda name, n: np.array([list(getattr(outs[e], name))[:n] for e in range(E)])
@@ -110,6 +114,16 @@ def _compare_native(sc, E, fear, steps, nthreads=16, offset=0, seed=7, weight=-5
         np.testing.assert_array_equal(r.ep_return.cpu().numpy(), np.array([outs[e].ep_return for e in range(E)]), err_msg=f"t={t} ret")
         np.testing.assert_array_equal(r.mask.cpu().numpy().astype(np.uint16), get("mask", K), err_msg=f"t={t} mask")
         np.testing.assert_array_equal(r.obs.reshape(K, E, -1).cpu().numpy(), obs_o, err_msg=f"t={t} obs")
+        ep_len = np.array([outs[e].ep_len for e in range(E)])
+        np.testing.assert_array_equal(r.ep_len.cpu().numpy(), ep_len, err_msg=f"t={t} ep_len")
+        np.testing.assert_array_equal(r.ep_fear.cpu().numpy(), np.array([outs[e].ep_fear for e in range(E)]),
+                                      err_msg=f"t={t} ep_fear")
+        np.testing.assert_array_equal(r.apples.cpu().numpy(), np.array([outs[e].apples_caught for e in range(E)]),
+                                      err_msg=f"t={t} apples")
+        ended = np.flatnonzero(dn)  # terminal obs of the envs that ended (their next_state)
+        np.testing.assert_array_equal(r.final_obs.reshape(K, E, -1)[:, ended].cpu().numpy(), fin_o[:, ended],
+                                      err_msg=f"t={t} final_obs")
+        capped += int(((dn != 0) & (ep_len == max_steps)).sum())
         # per-block statistics == the same sums over the oracle's outputs
         st = r.stats.sum(0).cpu().numpy()
         assert st[7] == E and st[1] == dn.sum()
@@ -122,7 +136,7 @@ def _compare_native(sc, E, fear, steps, nthreads=16, offset=0, seed=7, weight=-5
         done_total += int(dn.sum())
     assert bool((guard == 7.0).all()), "write past the stats buffer"
     env.close()
-    return done_total
+    return (done_total, capped) if return_capped else done_total
 
 
 KERNEL_PATHS = {
@@ -162,6 +176,16 @@ def test_many_agents_k_gt_2_matches_oracle(kernel_path):
     sc = S.compile_scenario(S.level3_like(10, 16, 5, 3))
     _compare_native(sc, 512, True, 20)
     _compare_native(sc, 1024, False, 40)
+
+
+@pytest.mark.parametrize("max_steps,steps,E", [(8, 40, 512), (150, 165, 192)])
+def test_episode_cap_matches_oracle(max_steps, steps, E, kernel_path):
+    """The TRAIN_STEPS cap (configs/custom_fear_5.yaml:5, maddpg/agent.py:243-247): episodes cut
+    at max_steps are compared bit-exact (done, ep_len, ep_return, the terminal obs and the
+    auto-reset obs after the cap), and some episodes do reach the cap."""
+    sc = S.builtin("grid32")
+    done, capped = _compare_native(sc, E, True, steps, max_steps=max_steps, seed=42, return_capped=True)
+    assert done > 0 and capped > 0, (done, capped)
 
 
 @pytest.mark.parametrize("E", [1, 77, 1000])

@@ -1,8 +1,10 @@
 """The stacked GPU-shaped MADDPG update (marlnav/maddpg.py) == a plain per-agent PyTorch fp32
 restatement of agilerl 1.0.15's MADDPG.learn loop (maddpg/agent.py:199-224 call site), agent by
 agent: separate nn.Sequential actors/critics, separate Adam optimisers, critic step then actor
-step per agent, soft target update at the end.  Runs on the CPU (the learner is plain PyTorch;
-the GPU graph-capture path is in tests/test_gpu_rollout.py)."""
+step per agent, soft target update at the end.  On the CPU the learner uses torch's Adam; the
+GPU tests (marked gpu) run its HIP path (flat buffers, gw_adam_step, gw_soft_update) against
+the same per-agent loop and against torch.optim.Adam; the graph-capture path is in
+tests/test_gpu_rollout.py."""
 import copy
 
 import pytest
@@ -13,7 +15,7 @@ from marlnav.maddpg import MADDPG, gumbel_softmax, learns_per_step
 
 
 def _seq(stacked, k, n_layers=3):
-    """nn.Sequential copy of agent k of a StackedMLPActors."""
+    """nn.Sequential copy of agent k of a StackedMLPActors (on the stacked net's device)."""
     dims = [stacked.weights[i].shape[1] for i in range(n_layers)] + [stacked.weights[-1].shape[2]]
     mods = []
     for i in range(n_layers):
@@ -28,7 +30,7 @@ def _seq(stacked, k, n_layers=3):
                 ln.weight.copy_(stacked.ln_w[i][k, 0])
                 ln.bias.copy_(stacked.ln_b[i][k, 0])
             mods += [ln, nn.ReLU()]
-    return nn.Sequential(*mods)
+    return nn.Sequential(*mods).to(stacked.weights[0].device)
 
 
 class PerAgentReference:
@@ -113,6 +115,87 @@ def test_stacked_learn_matches_per_agent_loop(K):
             assert abs(a_loss[k].item() - want[k][0]) < 1e-4 * max(1.0, abs(want[k][0]))
             assert abs(c_loss[k].item() - want[k][1]) < 1e-4 * max(1.0, abs(want[k][1]))
         _assert_same(m, ref)
+
+
+@pytest.mark.gpu
+def test_gpu_flat_learn_matches_per_agent_loop():
+    """On the GPU the learner takes its HIP path (flat parameter buffers, gw_adam_step,
+    gw_soft_update).  At the C3/C5 shape (32x32 obs, K = 2, batch 128, hidden 128-128, the
+    configs/custom_fear_5.yaml learning rates) four updates == the per-agent fp32 loop with
+    torch.optim.Adam on the same device.
+    Tolerance: losses within 1e-4 relative; every parameter tensor within 1e-4 relative L2 error
+    (GEMM summation order differs between the stacked bmm and the per-agent Linear, and Adam's
+    normalised step turns rounding-level gradients into steps of up to lr, so elementwise
+    bit-exactness is not expected) and within 2 * lr * steps elementwise."""
+    torch.manual_seed(0)
+    K, H, W, B, steps, lr = 2, 32, 32, 128, 4, 1e-3
+    m = MADDPG(K, H, W, lr_actor=lr, lr_critic=lr, gamma=0.98, tau=0.01, batch_size=B, device="cuda", seed=3)
+    assert m.flat  # the HIP optimizer / soft-update path
+    with torch.no_grad():
+        for net in (m.actor_targets.net, m.critic_targets):
+            net.flat_params().add_(0.05 * torch.randn_like(net.flat_params()))
+    ref = PerAgentReference(m, lr, lr)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    for it in range(steps):
+        states = torch.randint(-1, 6, (K, B, H, W), generator=g, device="cuda").float()
+        next_states = torch.randint(-1, 6, (K, B, H, W), generator=g, device="cuda").float()
+        actions = torch.softmax(torch.randn((K, B, 9), generator=g, device="cuda"), -1)
+        rewards = torch.randn((B, K), generator=g, dtype=torch.float64, device="cuda") * 10
+        dones = (torch.rand((B, K), generator=g, device="cuda") < 0.2).to(torch.uint8)
+        u_next = torch.rand((K, B, 9), generator=g, device="cuda")
+        u_cur = torch.rand((K, B, 9), generator=g, device="cuda")
+        a_loss, c_loss = m.learn(states, actions, rewards, next_states, dones, u_next, u_cur)
+        want = ref.learn(states, actions, rewards, next_states, dones, u_next, u_cur)
+        for k in range(K):
+            assert abs(a_loss[k].item() - want[k][0]) < 1e-4 * max(1.0, abs(want[k][0]))
+            assert abs(c_loss[k].item() - want[k][1]) < 1e-4 * max(1.0, abs(want[k][1]))
+    for k in range(K):
+        for stacked, seqs in ((m.actors.net, ref.actors), (m.actor_targets.net, ref.actor_t),
+                              (m.critics, ref.critics), (m.critic_targets, ref.critic_t)):
+            for a, b in zip(_seq(stacked, k).parameters(), seqs[k].parameters()):
+                rel = float((a - b).norm() / b.norm().clamp_min(1e-12))
+                assert rel < 1e-4, rel
+                assert float((a - b).abs().max()) <= 2 * lr * steps
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 1000, 300_001])
+def test_gpu_adam_and_soft_update_match_torch(n):
+    """gw_adam_step == torch.optim.Adam (single-tensor, non-capturable) over 6 steps on the same
+    flat buffer and gradients; gw_soft_update == tau * p + (1 - tau) * t in torch f32 (bit for
+    bit) and p.lerp_ within 2 ulp-scale tolerance."""
+    from marlnav import _lib
+    from marlnav.actor import StackedMLPActors
+    from marlnav.maddpg import FlatAdam
+    torch.manual_seed(1)
+    net = StackedMLPActors(1, 4, (4, 4), device="cuda")  # a FlatAdam host; its buffer is swapped below
+    flat = torch.nn.Parameter(torch.randn(n, device="cuda"))
+    flat.grad = torch.zeros_like(flat)
+    net.flat_params = lambda: flat
+    opt = FlatAdam(net, lr=1e-3)
+    ref = torch.nn.Parameter(flat.detach().clone())
+    topt = torch.optim.Adam([ref], lr=1e-3, foreach=False, capturable=False)
+    g = torch.Generator(device="cuda").manual_seed(2)
+    for _ in range(6):
+        grad = torch.randn(n, device="cuda", generator=g) * torch.rand(n, device="cuda", generator=g) * 3
+        flat.grad.copy_(grad)
+        ref.grad = grad.clone()
+        opt.step()
+        topt.step()
+        torch.testing.assert_close(flat.detach(), ref.detach(), rtol=2e-6, atol=1e-7)
+        # torch's kernels may contract to FMAs (hipcc's default), ours are built -ffp-contract=off
+        torch.testing.assert_close(opt.m, topt.state[ref]["exp_avg"], rtol=1e-6, atol=1e-9)
+        torch.testing.assert_close(opt.v, topt.state[ref]["exp_avg_sq"], rtol=1e-6, atol=1e-9)
+    assert int(opt.count) == 6
+    lib = _lib.load()
+    t = torch.randn(n, device="cuda")
+    p = torch.randn(n, device="cuda")
+    want = 0.01 * p + (1.0 - 0.01) * t
+    lerp = t.clone().lerp_(p, 0.01)
+    _lib.check(lib.gw_soft_update(t.data_ptr(), p.data_ptr(), n, 0.01,
+                                  torch.cuda.current_stream().cuda_stream), "gw_soft_update")
+    torch.testing.assert_close(t, want, rtol=2e-7, atol=1e-7)
+    torch.testing.assert_close(t, lerp, rtol=1e-6, atol=1e-7)
 
 
 def test_gumbel_softmax_is_a_distribution_and_sharpens():
