@@ -5,8 +5,9 @@ A "step" = one batched CustomMAEnv.step (custom/ma_customenv.py:217-334) over ev
 this rank: scripted policy + random RL policy drawn on device, FeAR counterfactuals
 (custom/Responsibility.py:135-210), world update, rewards, the rollout reward/score arithmetic
 (maddpg/agent.py:124-173), auto-reset, float32 observations for every RL agent and the
-per-block statistics; with --gpus N > 1 also the per-step RCCL reduction of those statistics
-(episode returns) across ranks.  Inputs are resident in HBM before the timed region.
+per-block statistics, and the per-step all-gather of every env's completed-episode return
+(RCCL over xGMI with --gpus N > 1, plus the RCCL all-reduce of the statistics).  Inputs are
+resident in HBM before the timed region.
 
 Default workload = BASELINE config 3 (the north-star shape): 4-agent 32x32 grid, 65536 envs
 per GPU, FeAR on with weight -5 (configs/custom_fear_5.yaml).  value = all ranks' envs x N
@@ -68,17 +69,56 @@ def algorithmic_bytes(N: int, K: int, HW: int, obs_bytes: int = 4):
     return step_b, obs_b
 
 
+def host_cpus():
+    """What the host offers this job: the machine's logical CPUs, the ones this process may run
+    on (affinity), the cgroup CPU quota (cpu.max) and the CPU model (lscpu / /proc/cpuinfo)."""
+    total = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = total
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for ln in out.splitlines():
+            if ln.startswith("Model name:"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except (OSError, ValueError, subprocess.SubprocessError):
+        pass
+    if model is None:
+        try:
+            with open("/proc/cpuinfo") as f:
+                model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), None)
+        except OSError:
+            pass
+    usable = affinity if quota is None else max(1, min(affinity, int(quota)))
+    return {"nproc": total, "affinity": affinity, "cgroup_quota_cpus": quota, "usable": usable, "model": model}
+
+
 def cpu_baseline(cfg, seconds: float = 12.0):
     """The C restatement (oracle/, test infrastructure) on the host cores: same scenario,
-    same step semantics, native-RNG mode, OpenMP over envs.  Bounded sample."""
+    same step semantics, native-RNG mode, OpenMP over envs (one thread per usable host core:
+    the job's CPU affinity capped by its cgroup quota; MARLNAV_CPU_THREADS overrides).
+    Bounded sample (~`seconds` of CPU work)."""
     import numpy as np
     from marlnav import scenario as S
     from oracle import oracle as O
 
     sc = S.builtin(cfg["scenario"])
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    threads = max(1, min(threads, 16))
-    E = 4096 if cfg["fear"] else 16384
+    cpus = host_cpus()
+    threads = int(os.environ.get("MARLNAV_CPU_THREADS", "0") or 0) or cpus["usable"]
+    threads = max(1, threads)
+    E = max(4096 if cfg["fear"] else 16384, 256 * threads)
     orc = O.OracleEnvs(sc, E, fear=cfg["fear"], fear_weight=cfg["fear_weight"], seed=42, reset=False)
     obs = np.zeros((sc.K, E, sc.HW), np.float32)
     orc.reset_all(obs=obs, nthreads=threads)
@@ -92,9 +132,12 @@ def cpu_baseline(cfg, seconds: float = 12.0):
             break
     value = E * sc.N * steps / el
     return {"value": value, "unit": "agent-env-steps/s", "cores": threads, "kind": "port",
+            "per_core": value / threads, "host": cpus,
             "sample": f"{E} envs x {steps} steps of {cfg['scenario']} (fear={'on' if cfg['fear'] else 'off'}, "
                       f"obs written) in {el:.1f}s by oracle/gw_oracle.c (bit-exact C restatement of the "
-                      f"reference step), {threads} OpenMP threads"}
+                      f"reference step), {threads} OpenMP threads = every core this job may use "
+                      f"(affinity {cpus['affinity']} of nproc {cpus['nproc']}, cgroup quota "
+                      f"{cpus['cgroup_quota_cpus']}; {cpus['model']})"}
 
 
 def main():
@@ -108,10 +151,13 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--updates-per-step", type=int, default=0,
                     help="c5 only: MADDPG updates (batch 128, one HIP-graph replay each) per env step")
-    ap.add_argument("--profile-every", type=int, default=16,
-                    help="bracket every n-th timed step's kernels with HIP events (0 = none); the "
-                         "events themselves cost ~2-3 us per kernel boundary, so not every step")
+    ap.add_argument("--profile-every", type=int, default=-1,
+                    help="bracket every n-th timed step's kernels with HIP events (0 = none, -1 = auto: "
+                         "every step up to 64 timed steps, else about 64 samples); the events cost "
+                         "~2-3 us per kernel boundary")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-gather", action="store_true",
+                    help="skip the per-step all-gather of every env's completed-episode return (A/B)")
     ap.add_argument("--sync-obs", action="store_true",
                     help="write each step's obs before the next step starts (no step pipeline; A/B)")
     ap.add_argument("--fear-async", action="store_true",
@@ -155,9 +201,10 @@ def main():
     # small batches (C2: 34 MB of obs per step) are bound by the launch chain, where the async
     # path's extra event records / waits cost more host time than the overlap saves
     # (tools/host_cost.py: 24.1 sync vs 25.8 us async wall per step at 4,096 envs)
-    hw = {"grid32": 1024, "grid64_n8": 4096, "level3": 160}.get(cfg["scenario"], 1024)
+    from marlnav import scenario as S
+    sc = S.builtin(cfg["scenario"])
     if obs_mode and not cfg.get("rollout") and not (args.obs_lazy or args.obs_eager) and \
-            (args.envs or cfg["envs"]) * 2 * hw * (2 if args.obs_dtype == "bf16" else 4) < (128 << 20):
+            (args.envs or cfg["envs"]) * sc.K * sc.HW * (2 if args.obs_dtype == "bf16" else 4) < (128 << 20):
         obs_mode = False
     if args.envs:
         cfg["envs"] = args.envs
@@ -172,11 +219,16 @@ def main():
     stream = torch.cuda.current_stream()
     stats_acc = torch.zeros_like(env.out["stats"][0])
 
-    from marlnav.parallel import StatsReducer
+    from marlnav.parallel import ReturnGather, StatsReducer
     reducer = StatsReducer(env.out["stats"].shape[1], env.device) if world > 1 else None
+    # per-step RCCL all-gather of every env's completed-episode return + done flag (SURVEY §8e;
+    # maddpg/agent.py:229-247): gw_step writes them straight into the send buffer
+    gather = None if args.no_gather else ReturnGather(world * E, rank, world, env.device)
 
     def one_step(i):
-        r = env.step()
+        r = env.step(into=gather.into() if gather is not None else None)
+        if gather is not None:
+            gather.push()
         if reducer is not None:
             # per-step RCCL all-reduce of the episode statistics across the shards: rows summed
             # locally first (64 B message), asynchronous, waited for one step later
@@ -195,7 +247,7 @@ def main():
             learner = MADDPG(K, env.H, env.W, device=env.device, seed=rank, capturable=True)
             actors = learner.actors
         ro = Rollout(env, actors, replay_slots=-(-200_000 // E) + 1, training=True, seed=rank,
-                     obs_async=obs_mode, fear_async=bool(obs_mode) and args.fear_async)
+                     obs_async=obs_mode, fear_async=bool(obs_mode) and args.fear_async, gather=gather)
         ro.reset()
 
         def one_step(i):  # noqa: F811
@@ -223,7 +275,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ev0.record(stream)
-    pe = args.profile_every
+    pe = args.profile_every if args.profile_every >= 0 else (1 if args.steps <= 64 else args.steps // 64)
     for i in range(args.steps):
         if pe > 0:
             env.profile(i % pe == 0)
@@ -231,6 +283,8 @@ def main():
     if cfg.get("rollout"):
         ro.fence()  # the last step's obs writes, FeAR outputs and statistics
     env.obs_fence()  # belong to the timed region
+    if gather is not None:
+        gather.compact()  # the gathered returns of the last steps, compacted on the device
     ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -246,6 +300,10 @@ def main():
         dist.all_reduce(t_local, op=dist.ReduceOp.MAX)
     t_max = float(t_local.item())
     stats = r.stats.sum(0).cpu().tolist()
+    gathered = None
+    if gather is not None:
+        gathered = {"episodes": int(gather.n_completed.item()), "bytes_per_rank_per_step": 9 * gather.emax,
+                    "mean_return_last_100": float(gather.completed(last=100).mean()) if int(gather.n_completed) else None}
 
     if rank == 0:
         step_b, obs_b = algorithmic_bytes(N, K, HW, 2 if args.obs_dtype == "bf16" else 4)
@@ -259,7 +317,7 @@ def main():
         else:
             dom, bytes_per_launch, dur = "step_kernel", step_b * E, avg_step_ms
         achieved = bytes_per_launch / (dur * 1e-3) / 1e9 if dur > 0 else None
-        traffic, traffic_src = None, None
+        traffic, traffic_src, prof_frac = None, None, None
         try:  # HBM bytes measured by the PMC passes committed under profiles/ for this workload
             with open(os.path.join(REPO, "profiles", "latest.json")) as f:
                 prof = json.load(f)
@@ -267,6 +325,8 @@ def main():
                     and args.obs_dtype == "f32":
                 traffic = prof["kernels"][dom]["hbm_bytes_per_launch"]
                 traffic_src = prof["source"]
+                # the same kernel's rocprofv3 average duration (many launches) for comparison
+                prof_frac = bytes_per_launch / (prof["kernels"][dom]["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS
         except (OSError, KeyError, ValueError):
             pass
         total_units = world * E * N * args.steps
@@ -288,7 +348,7 @@ def main():
                        "fear": cfg["fear"], "parallelism": f"env-sharded dp{world}", "obs_dtype": args.obs_dtype},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
-                         "traffic_source": traffic_src,
+                         "traffic_source": traffic_src, "frac_rocprof": prof_frac,
                          "bytes_per_launch": bytes_per_launch, "avg_launch_ms": dur,
                          # every algorithmic byte of a whole step (state + obs) over the wall time
                          # per step: what the pipelined steps sustain end to end
@@ -300,6 +360,8 @@ def main():
                            "obs_async": obs_mode, "fear_async": env.fear_async},
             "last_step_episodes": {"completed": stats[1], "mean_return": stats[0] / max(stats[1], 1.0),
                          "mean_len": stats[6] / max(stats[1], 1.0)},
+            # completed-episode returns all-gathered every step (warmup + timed steps, all ranks)
+            "return_gather": gathered,
         }
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)

@@ -207,7 +207,7 @@ def _declare(L):
     L.gw_last_error.restype = C.c_char_p
     L.gw_fear_matrix.argtypes = [p, C.c_int64] + [p] * 11
     L.gw_fear_matrix.restype = C.c_int
-    L.gw_adam_step.argtypes = [p, p, p, p, p, C.c_int64, C.c_float, C.c_float, C.c_float, C.c_float, p]
+    L.gw_adam_step.argtypes = [p, p, p, p, p, C.c_int64, C.c_double, C.c_double, C.c_double, C.c_double, p]
     L.gw_adam_step.restype = C.c_int
     L.gw_soft_update.argtypes = [p, p, C.c_int64, C.c_float, p]
     L.gw_soft_update.restype = C.c_int

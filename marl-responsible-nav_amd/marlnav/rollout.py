@@ -68,7 +68,7 @@ class ReplayRing:
 class Rollout:
     def __init__(self, env: VecGridEnv, actors: MultiAgentActors | None = None, replay_slots: int = 0,
                  training: bool = True, group=None, seed: int = 0, fused: bool | None = None,
-                 obs_async: bool | str = False, fear_async: bool = False):
+                 obs_async: bool | str = False, fear_async: bool = False, gather=None):
         """fused: get_action as the one-kernel gw_actor_act over the env's obs descriptors
         (default when the actors are the f32 128-128 MLP), else the PyTorch forward over the
         dense obs with torch's Gumbel noise.
@@ -76,7 +76,10 @@ class Rollout:
         step's actor + world update (VecGridEnv.set_obs_async); whoever reads the obs or the ring
         afterwards calls ``fence()`` first (the learner does).
         fear_async (with obs_async): the next step's actor overlaps this step's FeAR kernel; the
-        step's statistics are reduced one step later, after a FeAR fence."""
+        step's statistics are reduced one step later, after a FeAR fence.
+        gather: a parallel.ReturnGather; every step writes its ep_return / done into the gather's
+        send buffer and the completed-episode returns of all ranks are all-gathered
+        (maddpg/agent.py:229-247 ``completed_episode_scores``)."""
         self.env = env
         self.actors = actors
         self.fused = (actors is not None and actors.fusable(env)) if fused is None else bool(fused)
@@ -89,6 +92,9 @@ class Rollout:
         self.gen = torch.Generator(device=env.device).manual_seed(seed) if actors is not None else None
         self.t = 0
         self.reducer = StatsReducer(_lib.GW_STATS, env.device, group) if env.out.get("stats") is not None else None
+        self.gather = gather
+        if gather is not None and gather.count != env.E:
+            raise ValueError("ReturnGather shard size != env.E")
         env.set_obs_async(obs_async, fear_async=fear_async)
         self._pending = None  # (stats, tick) of a step whose FeAR may still be in flight
 
@@ -101,6 +107,8 @@ class Rollout:
             self._reduce(stats, tick)
 
     def _reduce(self, stats, tick):
+        if self.gather is not None:
+            self.gather.push()  # the step wrote ep_return / done into the gather's send buffer
         if self.reducer is not None:
             # per-step (RCCL) reduction of the episode statistics; the ring's device step count
             # advances in the same launch
@@ -153,13 +161,22 @@ class Rollout:
             nxt = (self.t + 1) % rp.S
             # zero-copy: the step writes obs_{t+1}, the terminal obs, the shaped reward and the
             # dones straight into the ring slots
-            r = env.step(actions, into=dict(obs=rp.obs[nxt], final_obs=rp.final_obs[cur], shaped=rp.reward[cur],
-                                            term=rp.term[cur], done=rp.done[cur]))
+            into = dict(obs=rp.obs[nxt], final_obs=rp.final_obs[cur], shaped=rp.reward[cur],
+                        term=rp.term[cur], done=rp.done[cur])
+            if self.gather is not None:
+                g = self.gather.into()
+                into["ep_return"] = g["ep_return"]
+                # done goes to the ring; the gather gets an E-byte copy (an elementwise kernel:
+                # hipMemcpy's blit took 18 us per 64 KB beside the obs writer)
+                self._gather_done = g["done"].view(torch.bool)
+            r = env.step(actions, into=into)
+            if self.gather is not None:
+                torch.ne(rp.done[cur], 0, out=self._gather_done)
             if probs is not None and probs.data_ptr() != rp.probs[cur].data_ptr():
                 rp.probs[cur].copy_(probs)
             rp.t = self.t + 1
         else:
-            r = env.step(actions)
+            r = env.step(actions, into=self.gather.into() if self.gather is not None else None)
         self.t += 1
         tick = self.replay.t_dev if self.replay is not None else None
         if self.env.fear_async:
@@ -175,3 +192,11 @@ class Rollout:
             return {}
         self._flush()
         return dict(zip(_lib.STATS_NAMES, self.reducer.result().cpu().tolist()))
+
+    def completed_scores(self, last: int | None = None):
+        """The completed-episode returns of every rank, oldest first (``completed_episode_scores``
+        of maddpg/agent.py:229-247); needs ``gather``.  Synchronises."""
+        if self.gather is None:
+            raise RuntimeError("Rollout(gather=ReturnGather(...)) needed")
+        self._flush()
+        return self.gather.completed(last)

@@ -147,7 +147,8 @@ class VecGridEnv:
 
     _INTO_SPEC = {"obs": (torch.float32, "KEHW"), "final_obs": (torch.float32, "KEHW"),
                   "reward": (torch.float64, "EK"), "fear": (torch.float64, "EK"), "shaped": (torch.float64, "EK"),
-                  "term": (torch.uint8, "EK"), "trunc": (torch.uint8, "EK"), "done": (torch.uint8, "E")}
+                  "term": (torch.uint8, "EK"), "trunc": (torch.uint8, "EK"), "done": (torch.uint8, "E"),
+                  "ep_return": (torch.float64, "E")}
 
     def step(self, rl_actions: torch.Tensor | None = None, scripted: torch.Tensor | None = None,
              spawn: torch.Tensor | None = None, obs_out: torch.Tensor | None = None,
@@ -157,8 +158,9 @@ class VecGridEnv:
         spawn [E, N] spawns for auto-resetting envs (replay) or None;
         obs_out / final_obs_out: [K, E, H, W] float32 buffers to write this step's obs into
         instead of the env's own (e.g. a replay-ring slot: zero-copy replay storage);
-        into: the same for any of obs, final_obs, reward, fear, shaped, term, trunc, done
-        (contiguous tensors of the output's dtype and size)."""
+        into: the same for any of obs, final_obs, reward, fear, shaped, term, trunc, done,
+        ep_return (contiguous tensors of the output's dtype and size; e.g. the send buffer of
+        parallel.ReturnGather)."""
         rl = self._as_i32(rl_actions, (self.E, self.K))
         sa = self._as_i32(scripted, (self.E, self.N - self.K))
         sp = self._as_i32(spawn, (self.E, self.N))

@@ -50,9 +50,12 @@ def bench_run(request):
         env.obs_fence()
         torch.cuda.synchronize()
         env.close()
-        capped = torch.nonzero(capped_at >= 0).flatten().cpu().numpy()
-        pick = [int(g) for g in capped if not SLICE0 <= g < SLICE0 + SLICE][:24]
-        sel = np.concatenate([np.arange(SLICE0, SLICE0 + SLICE), np.array(pick, np.int64)])
+        capped_at = capped_at.cpu().numpy()
+        capped = np.nonzero(capped_at >= 0)[0]
+        cand = [(int(g), int(capped_at[g])) for g in capped if not SLICE0 <= g < SLICE0 + SLICE]
+        # 12 envs whose FIRST episode hit the cap, 12 whose capped episode followed shorter ones
+        pick = [c for c in cand if c[1] == MAX_STEPS - 1][:12] + [c for c in cand if c[1] > MAX_STEPS - 1][:12]
+        sel = np.concatenate([np.arange(SLICE0, SLICE0 + SLICE), np.array([g for g, _ in pick], np.int64)])
 
         # pass 2: the bench's stepping with per-step captures of the selected envs
         env = _bench_env()
@@ -143,13 +146,16 @@ def test_bench_mode_slice_matches_oracle(bench_run):
 
 
 def test_bench_mode_capped_episodes_match_oracle(bench_run):
-    """Envs whose first episode is cut at the 150-step cap: done / ep_len / ep_return at the cap
-    and the auto-reset episode after it, bit-exact."""
+    """Envs with an episode cut at the 150-step cap (the first such episode ends at step index
+    ``t_cap``, after 0+ shorter episodes): done / ep_len / ep_return at the cap and the auto-reset
+    episode after it, bit-exact."""
     sel, pick, host, full = bench_run
     assert len(pick) > 0 and full["capped"] > 0, "no episode reached the cap"
     sc = S.builtin("grid32")
-    for j, g in enumerate(pick):
+    assert any(t_cap == MAX_STEPS - 1 for _, t_cap in pick) and any(t_cap > MAX_STEPS - 1 for _, t_cap in pick)
+    for j, (g, t_cap) in enumerate(pick):
         ref = _oracle_run(sc, g, 1)
         col = np.array([SLICE + j])
-        assert int(np.asarray(ref["ep_len"])[MAX_STEPS - 1, 0]) == MAX_STEPS and ref["done"][MAX_STEPS - 1][0]
+        assert MAX_STEPS - 1 <= t_cap < T
+        assert int(np.asarray(ref["ep_len"])[t_cap, 0]) == MAX_STEPS and ref["done"][t_cap][0]
         _check(host, col, ref, f"capped env {g}")

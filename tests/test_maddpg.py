@@ -183,9 +183,12 @@ def test_gpu_adam_and_soft_update_match_torch(n):
         opt.step()
         topt.step()
         torch.testing.assert_close(flat.detach(), ref.detach(), rtol=2e-6, atol=1e-7)
-        # torch's kernels may contract to FMAs (hipcc's default), ours are built -ffp-contract=off
-        torch.testing.assert_close(opt.m, topt.state[ref]["exp_avg"], rtol=1e-6, atol=1e-9)
-        torch.testing.assert_close(opt.v, topt.state[ref]["exp_avg_sq"], rtol=1e-6, atol=1e-9)
+        # the same ops and roundings as torch's single-tensor Adam (fmas where torch's contracted
+        # elementwise kernels fuse); tolerance: a few f32 ulps of the moment's scale, since a
+        # contraction difference inside lerp / addcmul shows up where the moment nearly cancels
+        for mine, theirs in ((opt.m, topt.state[ref]["exp_avg"]), (opt.v, topt.state[ref]["exp_avg_sq"])):
+            scale = float(theirs.abs().max())
+            torch.testing.assert_close(mine, theirs, rtol=1e-6, atol=4e-7 * scale)
     assert int(opt.count) == 6
     lib = _lib.load()
     t = torch.randn(n, device="cuda")

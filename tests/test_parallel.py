@@ -15,7 +15,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from marlnav.parallel import StatsReducer, shard
+from marlnav.parallel import ReturnGather, StatsReducer, shard
 
 STATS = 8
 
@@ -58,38 +58,85 @@ def _worker(rank, world, port, G, steps, outdir):
     orc = O.OracleEnvs(sc, cnt, fear=True, seed=5, env_offset=off)
     outs = (O.StepOut * cnt)()
     red = StatsReducer(STATS, "cpu")
-    rets = []
+    gat = ReturnGather(G, rank, world, "cpu", window=4)          # wraps the receive ring 3x
+    gat_small = ReturnGather(G, rank, world, "cpu", window=5, capacity=37)  # keeps the last 37
     for _ in range(steps):
         orc.vec_step(None, outs=outs, nthreads=1)
         partial = torch.tensor(_per_env_stats(outs, cnt))
         red.push(partial)  # async all-reduce, double-buffered
-        rets.append([outs[e].ep_return for e in range(cnt)])
+        ret = torch.tensor([outs[e].ep_return for e in range(cnt)], dtype=torch.float64)
+        done = torch.tensor([outs[e].done for e in range(cnt)], dtype=torch.uint8)
+        gat.push(ret, done)          # copy path
+        into = gat_small.into()      # zero-copy path: the "step" writes the send buffer
+        into["ep_return"].copy_(ret)
+        into["done"].copy_(done)
+        gat_small.push()
     totals = red.result().numpy()
-    pos = torch.tensor(orc.positions())
-    gathered = [torch.zeros((shard(G, r, world)[1], sc.N), dtype=pos.dtype) for r in range(world)]
-    dist.all_gather(gathered, pos) if all(g.shape == pos.shape for g in gathered) else None
+    np.save(os.path.join(outdir, f"completed{rank}.npy"), gat.completed())
+    np.save(os.path.join(outdir, f"completed_small{rank}.npy"), gat_small.completed())
+    emax = -(-G // world)
+    pos = torch.zeros((emax, sc.N), dtype=torch.int32)
+    pos[:cnt] = torch.tensor(orc.positions(), dtype=torch.int32)
+    gathered = [torch.zeros_like(pos) for _ in range(world)]
+    dist.all_gather(gathered, pos)
     if rank == 0:
         np.save(os.path.join(outdir, "totals.npy"), totals)
-        np.save(os.path.join(outdir, "pos.npy"), torch.cat(gathered).numpy())
+        np.save(os.path.join(outdir, "pos.npy"),
+                torch.cat([g[: shard(G, r, world)[1]] for r, g in enumerate(gathered)]).numpy())
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_gloo_world2_matches_single_process():
-    G, steps, world = 512, 15, 2
+@pytest.mark.parametrize("G", [512, 513])
+def test_gloo_world2_matches_single_process(G):
+    """Sharded over 2 gloo ranks (513: ragged shards, the gather pads the shorter one) ==
+    one process: positions, the all-reduced statistics, and the all-gathered completed-episode
+    returns (every rank gets the global list, in the reference's order: step, then env id)."""
+    steps, world = 15, 2
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker, args=(world, _free_port(), G, steps, d), nprocs=world, join=True)
         totals = np.load(os.path.join(d, "totals.npy"))
         pos = np.load(os.path.join(d, "pos.npy"))
+        completed = [np.load(os.path.join(d, f"completed{r}.npy")) for r in range(world)]
+        completed_small = [np.load(os.path.join(d, f"completed_small{r}.npy")) for r in range(world)]
     from marlnav import scenario as S
     from oracle import oracle as O
     sc = S.builtin("grid32")
     orc = O.OracleEnvs(sc, G, fear=True, seed=5)
     outs = (O.StepOut * G)()
     ref = np.zeros(STATS)
+    scores = []  # maddpg/agent.py:229-247: completed_episode_scores.append(scores[i]) per done env
     for _ in range(steps):
         orc.vec_step(None, outs=outs, nthreads=4)
         ref += _per_env_stats(outs, G).sum(0)
+        scores.extend(outs[e].ep_return for e in range(G) if outs[e].done)
+    scores = np.array(scores)
+    for r in range(world):
+        np.testing.assert_array_equal(completed[r], scores)
+        np.testing.assert_array_equal(completed_small[r], scores[-37:])
+    assert len(scores) > 37                                    # the small ring wrapped
     np.testing.assert_array_equal(pos, orc.positions())       # sharded trajectories == single run
     np.testing.assert_allclose(totals, ref, rtol=1e-12)        # reduced statistics == single run
     assert ref[1] > 0                                          # some episodes completed
+
+
+def test_return_gather_single_process_order_and_rings():
+    """World size 1 (no process group): the compacted list == the per-step done envs' returns in
+    env order, across receive-ring wraps (window 3) and a score ring smaller than the total."""
+    rng = np.random.default_rng(0)
+    E, steps = 50, 20
+    big = ReturnGather(E, 0, 1, "cpu", window=3)
+    small = ReturnGather(E, 0, 1, "cpu", window=7, capacity=13)
+    want = []
+    for t in range(steps):
+        ret = torch.tensor(rng.normal(size=E))
+        done = torch.tensor(rng.random(E) < 0.2, dtype=torch.uint8)
+        want.extend(ret[done.bool()].tolist())
+        big.push(ret, done)
+        small.push(ret, done)
+        if t == 10:  # a mid-window read compacts early; later steps continue the list
+            np.testing.assert_array_equal(big.completed(), np.array(want))
+    np.testing.assert_array_equal(big.completed(), np.array(want))
+    np.testing.assert_array_equal(small.completed(), np.array(want[-13:]))
+    np.testing.assert_array_equal(big.completed(last=5), np.array(want[-5:]))
+    assert int(big.n_completed) == len(want) > 13
