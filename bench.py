@@ -50,8 +50,8 @@ CONFIGS = {
                         "MEMORY_SIZE 200000, per-step RCCL reduction of the episode statistics)"),
     "c4cnn": dict(scenario="grid64_n8", envs=65536, fear=False, fear_weight=-5.0, rollout=True, arch="cnn",
                   workload="BASELINE config 4 as a rollout: 8-agent 64x64 grid, 65536 envs, the configs/cnn.yaml "
-                           "actor head (conv 32-64, k2 s2, 128-128; PyTorch/MIOpen f32) on the dense obs, env "
-                           "step, replay ring"),
+                           "actor head (conv 32-64, k2 s2, 128-128, f32; fused gw_cnn_act from the obs "
+                           "descriptors), env step, replay ring"),
 }
 
 
@@ -156,6 +156,11 @@ def main():
                          "every step up to 64 timed steps, else about 64 samples); the events cost "
                          "~2-3 us per kernel boundary")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cnn-torch", action="store_true",
+                    help="c4cnn: the PyTorch CNN forward on the dense obs instead of gw_cnn_act (A/B)")
+    ap.add_argument("--high-prio", action="store_true",
+                    help="run the step chain on a high-priority stream (its kernels' workgroups are "
+                         "dispatched ahead of the concurrent obs writer's)")
     ap.add_argument("--no-gather", action="store_true",
                     help="skip the per-step all-gather of every env's completed-episode return (A/B)")
     ap.add_argument("--sync-obs", action="store_true",
@@ -192,6 +197,8 @@ def main():
         else:
             dist.init_process_group(backend)
 
+    if args.high_prio:
+        torch.cuda.set_stream(torch.cuda.Stream(priority=-1))
     cfg = dict(CONFIGS[args.config])
     # obs writer pipelined with the next step (gw_set_obs_async): right after the world update
     # for the env-only workloads; launched at the next step (behind the fused actor, which would
@@ -206,6 +213,12 @@ def main():
     if obs_mode and not cfg.get("rollout") and not (args.obs_lazy or args.obs_eager) and \
             (args.envs or cfg["envs"]) * sc.K * sc.HW * (2 if args.obs_dtype == "bf16" else 4) < (128 << 20):
         obs_mode = False
+    if cfg.get("arch") == "cnn" and not (args.cnn_torch or args.obs_lazy or args.sync_obs):
+        # the 2.1 GB writer starts right after the world update, as 4 launches so that the next
+        # actor's kernels are dispatched between them (profiles/r2_cnn: 0.715 ms per step lazy in
+        # one launch -> 0.636); read by gw_create
+        obs_mode = True
+        os.environ.setdefault("GW_OBS_CHUNKS", "4")
     if args.envs:
         cfg["envs"] = args.envs
     if args.fear >= 0:
@@ -238,15 +251,17 @@ def main():
     if cfg.get("rollout"):  # c5: actor -> env -> replay (+ optional MADDPG updates) per step
         from marlnav.maddpg import MADDPG
         from marlnav.rollout import Rollout
-        if cfg.get("arch") == "cnn":  # PyTorch CNN head on the dense obs (reads it: synchronous obs)
+        if cfg.get("arch") == "cnn":  # configs/cnn.yaml head: fused gw_cnn_act (or PyTorch, A/B)
             from marlnav.actor import MultiAgentActors
             learner = None
             actors = MultiAgentActors(K, env.H, env.W, arch="cnn", device=env.device, seed=rank)
-            obs_mode = False
+            if args.cnn_torch:  # the PyTorch forward reads the dense obs: synchronous obs
+                obs_mode = False
         else:
             learner = MADDPG(K, env.H, env.W, device=env.device, seed=rank, capturable=True)
             actors = learner.actors
         ro = Rollout(env, actors, replay_slots=-(-200_000 // E) + 1, training=True, seed=rank,
+                     fused=False if args.cnn_torch else None,
                      obs_async=obs_mode, fear_async=bool(obs_mode) and args.fear_async, gather=gather)
         ro.reset()
 

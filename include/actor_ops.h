@@ -65,6 +65,50 @@ gw_status gw_actor_act(void *env, const gw_mlp_actors *net, const float *ws, int
                        uint64_t seed, uint64_t counter, const float *uniform, const uint16_t *mask,
                        int32_t *actions, float *probs, float *logits, void *stream);
 
+/* ---- the configs/cnn.yaml actor head ------------------------------------------------------
+ * Conv2d(1, 32, 2, stride 2) - ReLU - Conv2d(32, 64, 2, stride 2) - ReLU - flatten (c, y, x)
+ * - Linear(64 (H/4) (W/4), 128) - ReLU - Linear(128, 128) - ReLU - Linear(128, 9), per RL agent
+ * (maddpg/agent.py:94-100 with configs/cnn.yaml:2-6; agilerl's EvolvableCNN, parity unpinned).
+ *
+ * Both convolutions have kernel == stride, so conv-2 output position (Y, X) sees exactly the 4x4
+ * obs cells [4Y, 4Y + 4) x [4X, 4X + 4), and an observation (static map + at most N + 1 patched
+ * cells) changes at most N + 1 of the (H/4)(W/4) positions.  The first Linear is therefore
+ *   z = z_map + sum over changed positions P of Wl[:, P] . (a2(P) - a2_map(P))
+ * with z_map = b + Wl . a2(map) derived once per weight version.  A position holding ONE patched
+ * cell (the common case) reads its 128-float delta from a table built by gw_cnn_prepare for every
+ * (agent, position, cell, value); a position holding several is recomputed (conv 1, conv 2 on
+ * its 16 cells, then its 64 x 128 block of Wl).  No observation is read back from HBM. */
+typedef struct gw_cnn_actors {
+    int32_t K;            /* RL agents (must equal the env's K)                          */
+    int32_t H, W;         /* obs grid (the env's), multiples of 4                        */
+    int32_t c1, c2;       /* conv channels: 32, 64                                       */
+    int32_t hidden;       /* 128                                                         */
+    int32_t n_actions;    /* 9                                                           */
+    const float *conv1_w; /* [K][c1][1][2][2]  (torch Conv2d weight)                     */
+    const float *conv1_b; /* [K][c1]                                                     */
+    const float *conv2_w; /* [K][c2][c1][2][2]                                           */
+    const float *conv2_b; /* [K][c2]                                                     */
+    const float *lin1_w;  /* [K][128][c2 (H/4) (W/4)]  (torch Linear weight, out x in)    */
+    const float *lin1_b;  /* [K][128]                                                    */
+    const float *w2;      /* [K][128][128]  ([in][out], the stacked torch.bmm layout)     */
+    const float *b2;      /* [K][128]                                                    */
+    const float *w3;      /* [K][128][9]                                                 */
+    const float *b3;      /* [K][9]                                                      */
+} gw_cnn_actors;
+
+/* Workspace (floats) of the CNN calls for E envs: the delta table (K (H/4)(W/4) 16 19 128
+ * floats: 40 MB at 64x64, K = 2), the transposed Linear-1 weight, the map activations, the
+ * layer-2/3 MFMA images and a [K][E][128] layer-1 buffer. */
+int64_t gw_cnn_workspace_floats(int32_t H, int32_t W, int32_t K, int64_t E);
+
+/* Derive the workspace from the parameters; enqueue again after every parameter change. */
+gw_status gw_cnn_prepare(void *env, const gw_cnn_actors *net, float *ws, void *stream);
+
+/* gw_actor_act with the CNN head: the same noise, softmax, mask, argmax and outputs. */
+gw_status gw_cnn_act(void *env, const gw_cnn_actors *net, const float *ws, int training, float tau,
+                     uint64_t seed, uint64_t counter, const float *uniform, const uint16_t *mask,
+                     int32_t *actions, float *probs, float *logits, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

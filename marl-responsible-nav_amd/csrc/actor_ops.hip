@@ -46,6 +46,8 @@ namespace {
 
 constexpr int HID = 128, NA = 9, TILE = 16, MAXN = GW_MAX_AGENTS;
 constexpr int NDESC = 12;
+// CNN head: RS = recomputed conv-2 positions per (env, agent) (<= (N + 1) / 2), L1_WAVES per block
+constexpr int L1_WAVES = 8, RS = 4;
 constexpr uint32_t D_RESET = 1u;
 constexpr float LN_EPS = 1e-5f, G_EPS = 1e-20f;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -127,6 +129,9 @@ struct ActParams {
     const float *base;        // [HW]
     const uint16_t *mask;     // [E][K] or null
     const float *uniform;     // [K][E][9] or null
+    const float *h1;          // [K][E][128] layer-1 pre-activations (H1 kernels: the CNN head)
+    const float *rare_z;      // [K][E][RS][128] further layer-1 terms, rare_n[k][e] of them
+    const int *rare_n;
     int32_t *actions;         // [E][K]
     float *probs;             // [K][E][9]
     float *logits;            // [K][E][9] or null
@@ -256,7 +261,8 @@ __device__ __forceinline__ Desc load_desc(const ActParams &p, int64_t e, int k) 
 // kernels' blocks fit beside it; 8: two blocks per CU), 4 waves per SIMD (128 VGPRs).
 // BF3: layer 2 as bf16x3 products on v_mfma_f32_16x16x32_bf16 (6 of the 9 part products, f32
 // accumulation; ~2^-24 relative per product, 16x the f32 MFMA rate per instruction)
-template <int NP, int WAVES, bool BF3 = false>  // NP = patch slots per (env, agent) = N + 1
+// H1: layer 1 is read from p.h1 (computed by cnn_l1_kernel) instead of the obs descriptors
+template <int NP, int WAVES, bool BF3 = false, bool H1 = false>  // NP = patch slots per (env, agent) = N + 1
 __global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
     constexpr int THREADS = 64 * WAVES;
     constexpr int NW2 = BF3 ? W2B_U4 : W2IMG / 4;
@@ -342,8 +348,32 @@ __global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
         // the next tile's descriptor, loaded while this tile computes
         dn = load_desc(p, (int64_t)(tile + gridDim.x * WAVES) * TILE + el, k);
         ACT_STAMP(2 + 5 * it);
-        // ---- layer 1: c1 + sum of (value - map) * W1 row over the distinct patched cells ----
         float a[32];
+        if (H1) {  // ---- layer 1 from the buffer (features 16j + 4q .. + 3: one float4 each) ----
+            const size_t ek = (size_t)k * p.E + (valid ? e : 0);
+            const float4 *h = reinterpret_cast<const float4 *>(p.h1 + ek * HID);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float4 v = h[4 * j + q];
+                a[4 * j] = v.x;
+                a[4 * j + 1] = v.y;
+                a[4 * j + 2] = v.z;
+                a[4 * j + 3] = v.w;
+            }
+            const int nr = valid ? p.rare_n[ek] : 0;
+            for (int r = 0; r < nr; ++r) {  // the recomputed positions' terms, in slot order
+                const float4 *z = reinterpret_cast<const float4 *>(p.rare_z + (ek * RS + r) * HID);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float4 v = z[4 * j + q];
+                    a[4 * j] += v.x;
+                    a[4 * j + 1] += v.y;
+                    a[4 * j + 2] += v.z;
+                    a[4 * j + 3] += v.w;
+                }
+            }
+        } else {
+        // ---- layer 1: c1 + sum of (value - map) * W1 row over the distinct patched cells ----
 #pragma unroll
         for (int j = 0; j < 8; ++j) {  // features 16j + 4q .. + 3: one 16-byte LDS read
             const float4 c = vec4(s_vec[0], j);
@@ -382,6 +412,7 @@ __global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
             }
             __builtin_amdgcn_sched_barrier(0);  // one slot's row pieces (32 VGPRs) in flight at a time
         }
+        }  // !H1
         // ---- LN1 + ReLU (nn.LayerNorm(128), eps 1e-5, biased variance) ----
         if (ln) {
             float sm = 0.0f;
@@ -577,6 +608,485 @@ __global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
     }
 }
 
+
+// ---- the configs/cnn.yaml head (gw_cnn_prepare / gw_cnn_act; include/actor_ops.h) -------------
+// Geometry: conv-2 position P = (Y, X) (P = Y (W/4) + X) sees obs cells (4Y + ry, 4X + rx); the
+// region's cell t = 4 ry + rx lies in conv-1 window d = 2 (ry >> 1) + (rx >> 1) at tap
+// 2 (ry & 1) + (rx & 1), and conv-2 tap d.  Linear-1 feature of (channel o, position P) is o P_n + P.
+constexpr int C1 = 32, C2 = 64, NV = 19;  // NV: obs values of a patched cell (cnn_value_index)
+struct CnnWs {
+    Ws mlp;           // layer-2/3 MFMA images (and an unused c1)
+    float *wlt;       // [K][P][64][128]  Linear-1 weight, transposed per position
+    float *a2map;     // [K][P][64]       conv-2 activations of the static map
+    float *pre2map;   // [K][P][64]       ... before the ReLU
+    float *a1map;     // [K][P][4][32]    conv-1 activations of the map, per window
+    float *zpart;     // [K][P][128]
+    float *zmap;      // [K][128]         b + Wl . a2(map)
+    float *table;     // [K][P][16][NV][128]  Wl[:, P] . (a2(P with cell t := value v) - a2map(P))
+    float *w2t;       // [K][4][64][32]   conv-2 weight, window-major
+    uint32_t *road;   // [128]            road bitmask of the map (bit c: cell c is road)
+    float *h1;        // [K][E][128]      z_map + table rows
+    float *rare_z;    // [K][E][RS][128]  their Linear-1 contributions
+    int *rare_n;      // [K][E]           recomputed positions per (env, agent)
+    int *bucket_n;    // [K][P]           items per position (0 between calls)
+    int *bucket;      // [K][P][E]        items (e RS + slot) per position
+    int *unit_off;    // [K P + 1]        cnn_rare_plan's unit offsets
+};
+inline int64_t cnn_mlp_floats(int K) { return (int64_t)K * (HID + W2IMG + W3IMG + W2BIMG); }
+inline CnnWs cnn_ws_layout(float *base, int K, int P, int64_t E) {
+    CnnWs w;
+    w.mlp = ws_layout(base, K);
+    float *f = base + cnn_mlp_floats(K);
+    w.wlt = f;        f += (int64_t)K * P * C2 * HID;
+    w.a2map = f;      f += (int64_t)K * P * C2;
+    w.pre2map = f;    f += (int64_t)K * P * C2;
+    w.a1map = f;      f += (int64_t)K * P * 4 * C1;
+    w.zpart = f;      f += (int64_t)K * P * HID;
+    w.zmap = f;       f += (int64_t)K * HID;
+    w.table = f;      f += (int64_t)K * P * 16 * NV * HID;
+    w.w2t = f;        f += (int64_t)K * 4 * C2 * C1;
+    w.road = reinterpret_cast<uint32_t *>(f);  f += 128;
+    w.h1 = f;         f += (int64_t)K * E * HID;
+    w.rare_z = f;     f += (int64_t)K * E * RS * HID;
+    w.rare_n = reinterpret_cast<int *>(f);    f += (int64_t)K * E;
+    w.bucket_n = reinterpret_cast<int *>(f);  f += (int64_t)K * P;
+    w.bucket = reinterpret_cast<int *>(f);    f += (int64_t)K * P * E;
+    w.unit_off = reinterpret_cast<int *>(f);  f += (int64_t)K * P + 1;
+    return w;
+}
+inline int64_t cnn_ws_floats(int K, int P, int64_t E) {
+    return (int64_t)(cnn_ws_layout(nullptr, K, P, E).unit_off - (int *)nullptr) + (int64_t)K * P + 1;
+}
+// value of a patched obs cell -> table column: 0.5 (reset agent), 9.5 (reset agent on its apple),
+// 1 .. 17 (agents, relabelled or raw, apples, agents on apples); -1 = not tabulated
+__host__ __device__ inline int cnn_value_index(float v) {
+    if (v == 0.5f) return 0;
+    if (v == 9.5f) return 1;
+    const int i = (int)v;
+    return ((float)i == v && i >= 1 && i <= NV - 2) ? i + 1 : -1;
+}
+__host__ __device__ inline float cnn_index_value(int vi) { return vi == 0 ? 0.5f : vi == 1 ? 9.5f : (float)(vi - 1); }
+
+struct CnnParams {
+    gw_cnn_actors net;
+    CnnWs ws;
+    const float *base;        // [HW] map obs values (0 road, -1 inactive)
+    const uint32_t *desc;     // [E][12]
+    int64_t E;
+    int N, K, H, W, P, Wq, HW, variant;
+    int ab;                   // GW_CNN_AB (measurement only): bit 0 skip the recomputed positions,
+                              // bit 1 skip the table rows
+    int apples[MAXN];
+};
+
+// Linear-1 weight, transposed: wlt[k][P][o][j] = lin1_w[k][j][o P_n + P]
+__global__ void __launch_bounds__(256) cnn_prep_wlt(CnnParams p) {
+    const int64_t F = (int64_t)C2 * p.P, n = (int64_t)p.K * F * HID;
+    for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const int j = (int)(i % HID);
+        const int64_t r = i / HID;
+        const int o = (int)(r % C2), P = (int)((r / C2) % p.P), k = (int)(r / (C2 * (int64_t)p.P));
+        p.ws.wlt[i] = p.net.lin1_w[((int64_t)k * HID + j) * F + (int64_t)o * p.P + P];
+    }
+}
+
+// map activations of position P (block (P, k), 128 threads)
+__global__ void __launch_bounds__(128) cnn_prep_map(CnnParams p) {
+    const int P = blockIdx.x, k = blockIdx.y, t = threadIdx.x;
+    __shared__ float s_a1[4][C1];
+    if (t == 0) p.ws.bucket_n[k * p.P + P] = 0;
+    if (P == 0) {  // this agent's window-major conv-2 weight; (agent 0) the road bitmask
+        for (int i = t; i < 4 * C2 * C1; i += 128) {
+            const int d = i / (C2 * C1), o = (i / C1) % C2, c = i % C1;
+            p.ws.w2t[(size_t)k * 4 * C2 * C1 + i] = p.net.conv2_w[((k * C2 + o) * C1 + c) * 4 + d];
+        }
+        if (k == 0) {
+            uint32_t bits = 0;
+            for (int j = 0; j < 32; ++j) bits |= (32 * t + j < p.HW && p.base[min(32 * t + j, p.HW - 1)] == 0.0f) ? (1u << j) : 0u;
+            p.ws.road[t] = bits;
+        }
+    }
+    const int Y = P / p.Wq, X = P % p.Wq;
+    {   // conv 1: window d = t >> 5, channel c = t & 31
+        const int d = t >> 5, c = t & 31;
+        float acc = p.net.conv1_b[k * C1 + c];
+        for (int tap = 0; tap < 4; ++tap) {
+            const int y = 4 * Y + 2 * (d >> 1) + (tap >> 1), x = 4 * X + 2 * (d & 1) + (tap & 1);
+            acc = fmaf(p.net.conv1_w[(k * C1 + c) * 4 + tap], p.base[y * p.W + x], acc);
+        }
+        const float a1 = fmaxf(acc, 0.0f);
+        s_a1[d][c] = a1;
+        p.ws.a1map[(((size_t)k * p.P + P) * 4 + d) * C1 + c] = a1;
+    }
+    __syncthreads();
+    if (t < C2) {  // conv 2
+        float acc = p.net.conv2_b[k * C2 + t];
+        for (int c = 0; c < C1; ++c)
+            for (int d = 0; d < 4; ++d) acc = fmaf(p.net.conv2_w[((k * C2 + t) * C1 + c) * 4 + d], s_a1[d][c], acc);
+        p.ws.pre2map[((size_t)k * p.P + P) * C2 + t] = acc;
+        p.ws.a2map[((size_t)k * p.P + P) * C2 + t] = fmaxf(acc, 0.0f);
+    }
+}
+
+// zpart[k][P][j] = Wl[:, P] . a2map(P)   (block (P, k), 128 threads)
+__global__ void __launch_bounds__(128) cnn_prep_zpart(CnnParams p) {
+    const int P = blockIdx.x, k = blockIdx.y, j = threadIdx.x;
+    const float *w = p.ws.wlt + ((size_t)k * p.P + P) * C2 * HID;
+    const float *a2 = p.ws.a2map + ((size_t)k * p.P + P) * C2;
+    float acc = 0.0f;
+    for (int o = 0; o < C2; ++o) acc = fmaf(w[o * HID + j], a2[o], acc);
+    p.ws.zpart[((size_t)k * p.P + P) * HID + j] = acc;
+}
+
+// zmap = b + the positions' parts in order (block k, 128 threads); also c1 := 0 (unused)
+__global__ void __launch_bounds__(128) cnn_prep_zmap(CnnParams p) {
+    const int k = blockIdx.x, j = threadIdx.x;
+    float acc = 0.0f;
+    for (int P = 0; P < p.P; ++P) acc += p.ws.zpart[((size_t)k * p.P + P) * HID + j];
+    p.ws.zmap[k * HID + j] = p.net.lin1_b[k * HID + j] + acc;
+    p.ws.mlp.c1[k * HID + j] = 0.0f;
+}
+
+// the delta table of position P (block (P, k), 4 waves; wave w takes items w, w + 4, ... of the
+// 16 cells x NV values)
+__global__ void __launch_bounds__(256) cnn_prep_table(CnnParams p) {
+    const int P = blockIdx.x, k = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    __shared__ float s_wl[C2][HID];        // Wl block of P, 32 KB
+    __shared__ float s_w2[C2][C1][4];      // conv-2 weight, 32 KB
+    __shared__ float s_map[16], s_a1[4][C1], s_pre2[C2], s_a2[C2];
+    __shared__ float s_da1[4][C1], s_dl[4][C2];
+    const int Y = P / p.Wq, X = P % p.Wq;
+    const float *wl = p.ws.wlt + ((size_t)k * p.P + P) * C2 * HID;
+    for (int i = tid; i < C2 * HID; i += 256) (&s_wl[0][0])[i] = wl[i];
+    for (int i = tid; i < C2 * C1 * 4; i += 256) (&s_w2[0][0][0])[i] = p.net.conv2_w[(size_t)k * C2 * C1 * 4 + i];
+    if (tid < 16) s_map[tid] = p.base[(4 * Y + (tid >> 2)) * p.W + 4 * X + (tid & 3)];
+    if (tid < 4 * C1) (&s_a1[0][0])[tid] = p.ws.a1map[((size_t)k * p.P + P) * 4 * C1 + tid];
+    if (tid < C2) {
+        s_pre2[tid] = p.ws.pre2map[((size_t)k * p.P + P) * C2 + tid];
+        s_a2[tid] = p.ws.a2map[((size_t)k * p.P + P) * C2 + tid];
+    }
+    __syncthreads();
+    for (int item = wave; item < 16 * NV; item += 4) {
+        const int t = item / NV, vi = item % NV;
+        const int ry = t >> 2, rx = t & 3, d = 2 * (ry >> 1) + (rx >> 1), tap = 2 * (ry & 1) + (rx & 1);
+        const float v = cnn_index_value(vi);
+        if (lane < C1) {  // conv 1 of window d with cell t := v
+            const int c = lane;
+            float acc = p.net.conv1_b[k * C1 + c];
+            for (int u = 0; u < 4; ++u) {
+                const int cy = 2 * (d >> 1) + (u >> 1), cx = 2 * (d & 1) + (u & 1);
+                acc = fmaf(p.net.conv1_w[(k * C1 + c) * 4 + u], u == tap ? v : s_map[4 * cy + cx], acc);
+            }
+            s_da1[wave][c] = fmaxf(acc, 0.0f) - s_a1[d][c];
+        }
+        __syncthreads();  // (every wave runs the same 76 items)
+        {   // conv 2, lane = output channel
+            float acc = s_pre2[lane];
+            for (int c = 0; c < C1; ++c) acc = fmaf(s_w2[lane][c][d], s_da1[wave][c], acc);
+            s_dl[wave][lane] = fmaxf(acc, 0.0f) - s_a2[lane];
+        }
+        __syncthreads();
+        float t0 = 0.0f, t1 = 0.0f;
+        for (int o = 0; o < C2; ++o) {
+            const float dl = s_dl[wave][o];
+            t0 = fmaf(s_wl[o][lane], dl, t0);
+            t1 = fmaf(s_wl[o][lane + 64], dl, t1);
+        }
+        float *row = p.ws.table + ((((size_t)k * p.P + P) * 16 + t) * NV + vi) * HID;
+        row[lane] = t0;
+        row[lane + 64] = t1;
+        __syncthreads();
+    }
+}
+
+
+// Layer 1 of the CNN head for every (env, agent): h1 = z_map + the changed positions' deltas.
+// cnn_l1_kernel sums the table rows of the positions with one patched cell into h1 and appends
+// each position with several to that (agent, position)'s bucket as an (env, slot) item;
+// cnn_rare_plan cuts the buckets into units of up to 16 x RARE_WAVES items; cnn_rare_kernel
+// (persistent) takes units with the position's Linear-1 block staged in LDS, recomputes each
+// item's position (conv 1, conv 2) and writes its 128-float contribution; act_kernel<H1> adds an
+// env's contributions (in slot order) to h1.  Every sum runs in a fixed order, so the result
+// does not depend on the order items entered a bucket.
+template <int NP>
+__global__ void __launch_bounds__(64 * L1_WAVES, 4) cnn_l1_kernel(CnnParams p) {
+    __shared__ uint32_t s_road[128];
+    __shared__ int s_rows[L1_WAVES][NP][64];   // the lanes' table rows
+    const int k = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, el = lane & 15, q = lane >> 4;
+    const int64_t e = ((int64_t)blockIdx.x * L1_WAVES + wave) * TILE + el;
+    const bool valid = e < p.E;
+    uint4 cells = make_uint4(0, 0, 0, 0);
+    uint32_t flags = 0;
+    if (valid) {
+        cells = *reinterpret_cast<const uint4 *>(p.desc + e * NDESC);
+        flags = p.desc[e * NDESC + 4];
+    }
+    if (tid < 128) s_road[tid] = p.ws.road[tid];
+    __syncthreads();
+    auto map_at = [&](int c) { return ((s_road[c >> 5] >> (c & 31)) & 1u) ? 0.0f : -1.0f; };
+    // ---- the (env, agent)'s patched cells (act_kernel's decoding) ----
+    int pc[NP];
+    float pv[NP];
+    {
+        const bool reset = (flags & D_RESET) != 0;
+        const int ac = (valid && ((flags >> (8 + k)) & 1u)) ? p.apples[k] : -1;
+        float av = (ac >= 0 ? map_at(ac) : 0.0f) + 9.0f;
+        if (!reset && av == (float)(k + 1)) av = 1.0f;
+        pc[0] = ac;
+        pv[0] = av;
+        const uint32_t dw[4] = {cells.x, cells.y, cells.z, cells.w};
+#pragma unroll
+        for (int n = 0; n < NP - 1; ++n) {
+            const int c = (int)((dw[n >> 1] >> (16 * (n & 1))) & 0xFFFFu);
+            pc[1 + n] = valid ? c : -1;
+            pv[1 + n] = agent_value(reset, n, k, c == ac, p.variant);
+        }
+    }
+    // distinct cells (a later slot on the same cell wins), their positions, table columns
+    int pos[NP], vidx[NP];
+    bool live[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+        const int c = pc[i];
+        bool l = (unsigned)c < (unsigned)p.HW;
+#pragma unroll
+        for (int r = i + 1; r < NP; ++r) l = l && pc[r] != c;
+        live[i] = l;
+        const int cc = l ? c : 0, y = cc / p.W, x = cc % p.W;
+        pos[i] = l ? (y >> 2) * p.Wq + (x >> 2) : -1 - i;
+        vidx[i] = cnn_value_index(pv[i]);
+    }
+    // per slot: the table row (float4 index) of a position with exactly one patched cell goes to
+    // the lane's row list; `rare` marks the first slot of each position holding several
+    unsigned rare = 0;
+    int nrow = 0;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+        int cnt = 0;
+        bool leader = live[i];
+#pragma unroll
+        for (int r = 0; r < NP; ++r) {
+            const bool same = live[r] && pos[r] == pos[i];
+            cnt += same ? 1 : 0;
+            leader = leader && !(r < i && same);
+        }
+        const bool single = live[i] && cnt == 1 && vidx[i] >= 0;
+        rare |= (leader && !single) ? (1u << i) : 0u;
+        if (single) {
+            const int c = pc[i], y = c / p.W, x = c % p.W;
+            s_rows[wave][nrow++][lane] = (((k * p.P + pos[i]) * 16 + 4 * (y & 3) + (x & 3)) * NV + vidx[i]) * (HID / 4);
+        }
+    }
+    if (p.ab & 2) nrow = 0;
+    if (p.ab & 1) rare = 0;
+    {
+        float a[32];
+        const float4 *z = reinterpret_cast<const float4 *>(p.ws.zmap + k * HID);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float4 v = z[4 * j + q];
+            a[4 * j] = v.x;
+            a[4 * j + 1] = v.y;
+            a[4 * j + 2] = v.z;
+            a[4 * j + 3] = v.w;
+        }
+        const float4 *tab = reinterpret_cast<const float4 *>(p.ws.table);
+#pragma unroll 1
+        for (int i = 0; i < nrow; ++i) {  // one row (8 float4 per lane) in flight per wave
+            const int r0 = s_rows[wave][i][lane];
+            float4 w0[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) w0[j] = tab[r0 + 4 * j + q];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                a[4 * j + 0] += w0[j].x;
+                a[4 * j + 1] += w0[j].y;
+                a[4 * j + 2] += w0[j].z;
+                a[4 * j + 3] += w0[j].w;
+            }
+        }
+        if (valid) {
+            float4 *h = reinterpret_cast<float4 *>(p.ws.h1 + ((size_t)k * p.E + e) * HID);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) h[4 * j + q] = make_float4(a[4 * j], a[4 * j + 1], a[4 * j + 2], a[4 * j + 3]);
+        }
+    }
+    // ---- positions with several patched cells: (env, slot) into the position's bucket; the
+    //      slot's contribution is computed by cnn_rare_kernel ----
+    int ns = 0;
+    while (rare) {
+        const int i0 = __builtin_ctz(rare);
+        rare &= rare - 1;
+        int P = 0;
+#pragma unroll
+        for (int i = 0; i < NP; ++i)
+            if (i == i0) P = pos[i];
+        if (q == 0 && valid) {
+            const int idx = atomicAdd(p.ws.bucket_n + k * p.P + P, 1);
+            p.ws.bucket[((size_t)k * p.P + P) * p.E + idx] = (int)(e * RS + ns);
+        }
+        ++ns;
+    }
+    if (q == 0 && valid) p.ws.rare_n[(size_t)k * p.E + e] = ns;
+}
+
+// Units of work over the buckets: bucket b (= k P_n + P) holds ceil(n_b / RARE_ITEMS) units;
+// unit_off[b] = the units before bucket b (one block, K P_n <= 2048 buckets).
+constexpr int RARE_WAVES = 8, RARE_ITEMS = 16 * RARE_WAVES, RARE_BLOCKS = 256;
+__global__ void __launch_bounds__(1024) cnn_rare_plan(CnnParams p) {
+    __shared__ int s_sum[1024];
+    const int nb = p.K * p.P, tid = threadIdx.x;
+    const int per = (nb + 1023) / 1024, b0 = tid * per;   // each thread scans `per` buckets
+    int loc = 0;
+    for (int i = 0; i < per; ++i)
+        if (b0 + i < nb) loc += (p.ws.bucket_n[b0 + i] + RARE_ITEMS - 1) / RARE_ITEMS;
+    s_sum[tid] = loc;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {  // inclusive Hillis-Steele scan
+        const int v = tid >= off ? s_sum[tid - off] : 0;
+        __syncthreads();
+        s_sum[tid] += v;
+        __syncthreads();
+    }
+    int run = s_sum[tid] - loc;
+    for (int i = 0; i < per; ++i)
+        if (b0 + i < nb) {
+            p.ws.unit_off[b0 + i] = run;
+            run += (p.ws.bucket_n[b0 + i] + RARE_ITEMS - 1) / RARE_ITEMS;
+        }
+    if (tid == 1023) p.ws.unit_off[nb] = s_sum[1023];
+}
+
+// Persistent: block b takes units b, b + RARE_BLOCKS, ...; per unit the position's conv weights,
+// map activations and Linear-1 block are staged in LDS.  Lane (item it = l & 15, quarter q): the
+// item's env observation is decoded from its descriptor (act_kernel's rule), lane q evaluates
+// conv-1 window q of the position, conv 2 sums the four windows through two lane shuffles, the 64
+// deltas go through LDS, and the lane writes features 16j + 4q + i of Wl[:, P] . delta.
+constexpr int W2Q = C2 * C1 / 4 + 1;  // window stride of the conv-2 image in float4 (+1: no bank conflicts)
+template <int NP>
+__global__ void __launch_bounds__(64 * RARE_WAVES) cnn_rare_kernel(CnnParams p) {
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int it = lane & 15, q = lane >> 4;
+    const int nb = p.K * p.P;
+    const int nunits = p.ws.unit_off[nb];
+    __shared__ float4 s_wl[C2 * HID / 4];      // Wl block of P: [o][128], 32 KB
+    __shared__ float4 s_w2[4 * W2Q];           // conv-2 weight [window][o][c], 32 KB
+    __shared__ float s_w1[C1][4], s_b1[C1], s_b2[C2], s_a2m[C2];
+    __shared__ uint32_t s_road[128];
+    __shared__ float s_dl[RARE_WAVES][C2][TILE];
+    if (tid < 128) s_road[tid] = p.ws.road[tid];
+    int staged_k = -1, staged_P = -1;
+    for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
+        int lo = 0, hi = nb;  // the bucket holding unit u: unit_off[lo] <= u < unit_off[lo + 1]
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (p.ws.unit_off[mid] <= u) lo = mid; else hi = mid;
+        }
+        const int k = lo / p.P, P = lo % p.P;
+        const int n = p.ws.bucket_n[lo];
+        const int i_begin = (u - p.ws.unit_off[lo]) * RARE_ITEMS, i_end = min(n, i_begin + RARE_ITEMS);
+        __syncthreads();  // the previous unit is done with the LDS images
+        if (k != staged_k) {
+            const float4 *w2 = reinterpret_cast<const float4 *>(p.ws.w2t) + (size_t)k * (4 * C2 * C1 / 4);
+            for (int i = tid; i < 4 * C2 * C1 / 4; i += 64 * RARE_WAVES) s_w2[(i / (C2 * C1 / 4)) * W2Q + i % (C2 * C1 / 4)] = w2[i];
+            if (tid < C1 * 4) (&s_w1[0][0])[tid] = p.net.conv1_w[k * C1 * 4 + tid];
+            if (tid < C1) s_b1[tid] = p.net.conv1_b[k * C1 + tid];
+            if (tid < C2) s_b2[tid] = p.net.conv2_b[k * C2 + tid];
+        }
+        if (k != staged_k || P != staged_P) {
+            const float4 *wl = reinterpret_cast<const float4 *>(p.ws.wlt + ((size_t)k * p.P + P) * C2 * HID);
+            for (int i = tid; i < C2 * HID / 4; i += 64 * RARE_WAVES) s_wl[i] = wl[i];
+            if (tid < C2) s_a2m[tid] = p.ws.a2map[((size_t)k * p.P + P) * C2 + tid];
+        }
+        staged_k = k;
+        staged_P = P;
+        __syncthreads();
+        auto map_at = [&](int c) { return ((s_road[c >> 5] >> (c & 31)) & 1u) ? 0.0f : -1.0f; };
+        const int Y = P / p.Wq, X = P % p.Wq;
+        const int b = i_begin + 16 * wave;
+        if (b >= i_end) continue;  // (wave-uniform; no barrier until the next unit's)
+        const bool ok = b + it < i_end;
+        const int item = ok ? p.ws.bucket[(size_t)lo * p.E + b + it] : 0;
+        const int64_t e = item / RS;
+        // ---- this env's patched cells (act_kernel's decoding), then window q's four cells ----
+        const uint4 cells = *reinterpret_cast<const uint4 *>(p.desc + e * NDESC);
+        const uint32_t flags = p.desc[e * NDESC + 4];
+        const bool reset = (flags & D_RESET) != 0;
+        const int ac = ((flags >> (8 + k)) & 1u) ? p.apples[k] : -1;
+        float v4[4];
+#pragma unroll
+        for (int u4 = 0; u4 < 4; ++u4) v4[u4] = map_at((4 * Y + 2 * (q >> 1) + (u4 >> 1)) * p.W + 4 * X + 2 * (q & 1) + (u4 & 1));
+        {
+            float av = (ac >= 0 ? map_at(ac) : 0.0f) + 9.0f;
+            if (!reset && av == (float)(k + 1)) av = 1.0f;
+            const uint32_t dw[4] = {cells.x, cells.y, cells.z, cells.w};
+#pragma unroll
+            for (int sl = 0; sl < NP; ++sl) {  // in slot order: a later slot on the same cell wins
+                const int c = sl == 0 ? ac : (int)((dw[(sl - 1) >> 1] >> (16 * ((sl - 1) & 1))) & 0xFFFFu);
+                const float v = sl == 0 ? av : agent_value(reset, sl - 1, k, c == ac, p.variant);
+                const int y = c / p.W - 4 * Y - 2 * (q >> 1), x = c % p.W - 4 * X - 2 * (q & 1);
+                const bool in = c >= 0 && (unsigned)y < 2u && (unsigned)x < 2u;
+#pragma unroll
+                for (int u4 = 0; u4 < 4; ++u4) v4[u4] = (in && 2 * y + x == u4) ? v : v4[u4];
+            }
+        }
+        float a1[C1];
+#pragma unroll
+        for (int c = 0; c < C1; ++c) {
+            float acc = s_b1[c];
+#pragma unroll
+            for (int u4 = 0; u4 < 4; ++u4) acc = fmaf(s_w1[c][u4], v4[u4], acc);
+            a1[c] = fmaxf(acc, 0.0f);
+        }
+        // ---- conv 2: window q's partial sums meet through the shuffles; deltas to LDS ----
+#pragma unroll 2
+        for (int o = 0; o < C2; ++o) {
+            const float4 *w = &s_w2[q * W2Q + o * (C1 / 4)];
+            float acc = 0.0f;
+#pragma unroll
+            for (int c4 = 0; c4 < C1 / 4; ++c4) {
+                const float4 wv = w[c4];
+                acc = fmaf(wv.x, a1[4 * c4], acc);
+                acc = fmaf(wv.y, a1[4 * c4 + 1], acc);
+                acc = fmaf(wv.z, a1[4 * c4 + 2], acc);
+                acc = fmaf(wv.w, a1[4 * c4 + 3], acc);
+            }
+            const float dl = fmaxf(s_b2[o] + quad_sum(acc), 0.0f) - s_a2m[o];
+            if (q == (o & 3)) s_dl[wave][o][it] = dl;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // ---- Linear 1 on the position: features 16j + 4q .. + 3 ----
+        float a[32];
+#pragma unroll
+        for (int i = 0; i < 32; ++i) a[i] = 0.0f;
+#pragma unroll 4
+        for (int o = 0; o < C2; ++o) {
+            const float dl = s_dl[wave][o][it];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float4 w = s_wl[o * (HID / 4) + 4 * j + q];
+                a[4 * j + 0] = fmaf(dl, w.x, a[4 * j + 0]);
+                a[4 * j + 1] = fmaf(dl, w.y, a[4 * j + 1]);
+                a[4 * j + 2] = fmaf(dl, w.z, a[4 * j + 2]);
+                a[4 * j + 3] = fmaf(dl, w.w, a[4 * j + 3]);
+            }
+        }
+        if (ok) {
+            float4 *z = reinterpret_cast<float4 *>(p.ws.rare_z + ((size_t)k * p.E * RS + item) * HID);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) z[4 * j + q] = make_float4(a[4 * j], a[4 * j + 1], a[4 * j + 2], a[4 * j + 3]);
+        }
+    }
+}
+
+// the buckets are emptied for the next call once every split has read its count
+__global__ void __launch_bounds__(256) cnn_bucket_reset(CnnParams p) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < p.K * p.P) p.ws.bucket_n[i] = 0;
+}
+
 gw_status err(gw_status s, const std::string &msg) {
     gw_set_last_error(msg.c_str());
     return s;
@@ -592,6 +1102,58 @@ gw_status check_net(const gw_obs_source &src, const gw_mlp_actors *net, const ch
         return err(GW_ERR_ARG, w + ": null parameter");
     if (reinterpret_cast<uintptr_t>(net->w1) & 15u) return err(GW_ERR_ARG, w + ": w1 must be 16-byte aligned");
     return GW_OK;
+}
+
+
+gw_status check_cnn(const gw_obs_source &src, const gw_cnn_actors *net, const char *who) {
+    const std::string w(who);
+    if (net->K != src.K) return err(GW_ERR_ARG, w + ": net K != env K");
+    if (net->H != src.H || net->W != src.W) return err(GW_ERR_ARG, w + ": net H, W != env H, W");
+    if (net->H % 4 || net->W % 4 || net->H * net->W > 128 * 32)
+        return err(GW_ERR_ARG, w + ": H and W must be multiples of 4, H*W <= 4096");
+    if (net->c1 != C1 || net->c2 != C2 || net->hidden != HID || net->n_actions != NA)
+        return err(GW_ERR_ARG, w + ": only channels 32-64, hidden 128 and 9 actions are fused");
+    if (!net->conv1_w || !net->conv1_b || !net->conv2_w || !net->conv2_b || !net->lin1_w || !net->lin1_b ||
+        !net->w2 || !net->b2 || !net->w3 || !net->b3)
+        return err(GW_ERR_ARG, w + ": null parameter");
+    return GW_OK;
+}
+
+CnnParams cnn_params(const gw_obs_source &src, const gw_cnn_actors *net, float *ws) {
+    CnnParams p;
+    p.net = *net;
+    p.H = src.H;
+    p.W = src.W;
+    p.HW = src.H * src.W;
+    p.Wq = src.W / 4;
+    p.P = (src.H / 4) * p.Wq;
+    p.ws = cnn_ws_layout(ws, src.K, p.P, src.E);
+    p.base = src.base;
+    p.desc = src.desc;
+    p.E = src.E;
+    p.N = src.N;
+    p.K = src.K;
+    p.variant = src.variant;
+    for (int k = 0; k < MAXN; ++k) p.apples[k] = src.apples[k];
+    const char *ab = std::getenv("GW_CNN_AB");
+    p.ab = ab ? std::atoi(ab) : 0;
+    return p;
+}
+
+gw_mlp_actors cnn_tail(const gw_cnn_actors *net) {  // layers 2-3 as act_kernel's net (no LayerNorm)
+    gw_mlp_actors m{};
+    m.K = net->K;
+    m.in_dim = net->H * net->W;
+    m.hidden = HID;
+    m.n_actions = NA;
+    m.layer_norm = 0;
+    m.w1 = net->lin1_w;
+    m.b1 = net->lin1_b;
+    m.w2 = net->w2;
+    m.b2 = net->b2;
+    m.w3 = net->w3;
+    m.b3 = net->b3;
+    return m;
 }
 
 }  // namespace
@@ -650,6 +1212,9 @@ gw_status gw_actor_act(void *env, const gw_mlp_actors *net, const float *ws, int
     p.base = src.base;
     p.mask = mask;
     p.uniform = uniform;
+    p.h1 = nullptr;
+    p.rare_z = nullptr;
+    p.rare_n = nullptr;
     p.actions = actions;
     p.probs = probs;
     p.logits = logits;
@@ -703,6 +1268,114 @@ gw_status gw_actor_act(void *env, const gw_mlp_actors *net, const float *ws, int
 #undef ACT_LAUNCH
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return err(GW_ERR_HIP, std::string("gw_actor_act: ") + hipGetErrorString(e));
+    return GW_OK;
+}
+
+int64_t gw_cnn_workspace_floats(int32_t H, int32_t W, int32_t K, int64_t E) {
+    return cnn_ws_floats(K, (H / 4) * (W / 4), E);
+}
+
+gw_status gw_cnn_prepare(void *env, const gw_cnn_actors *net, float *ws, void *stream) {
+    if (!env || !net || !ws) return err(GW_ERR_ARG, "gw_cnn_prepare: null argument");
+    if (reinterpret_cast<uintptr_t>(ws) & 15u) return err(GW_ERR_ARG, "gw_cnn_prepare: ws must be 16-byte aligned");
+    gw_obs_source src;
+    gw_status st = gw_obs_view(env, &src);
+    if (st != GW_OK) return st;
+    if ((st = check_cnn(src, net, "gw_cnn_prepare")) != GW_OK) return st;
+    const CnnParams p = cnn_params(src, net, ws);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(cnn_prep_wlt, dim3(2048), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(cnn_prep_map, dim3(p.P, src.K), dim3(128), 0, s, p);
+    hipLaunchKernelGGL(cnn_prep_zpart, dim3(p.P, src.K), dim3(128), 0, s, p);
+    hipLaunchKernelGGL(cnn_prep_zmap, dim3(src.K), dim3(128), 0, s, p);
+    hipLaunchKernelGGL(cnn_prep_table, dim3(p.P, src.K), dim3(256), 0, s, p);
+    PrepParams pp;  // the layer-2/3 MFMA images (prep_images; nslices 0: c1 is rewritten below)
+    pp.net = cnn_tail(net);
+    pp.HW = p.HW;
+    pp.nslices = 0;
+    pp.ws = p.ws.mlp;
+    pp.base = src.base;
+    hipLaunchKernelGGL(prep_images, dim3(16, src.K), dim3(256), 0, s, pp);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return err(GW_ERR_HIP, std::string("gw_cnn_prepare: ") + hipGetErrorString(e));
+    return GW_OK;
+}
+
+gw_status gw_cnn_act(void *env, const gw_cnn_actors *net, const float *ws, int training, float tau, uint64_t seed,
+                     uint64_t counter, const float *uniform, const uint16_t *mask, int32_t *actions, float *probs,
+                     float *logits, void *stream) {
+    if (!env || !net || !ws || !actions || !probs) return err(GW_ERR_ARG, "gw_cnn_act: null argument");
+    if (reinterpret_cast<uintptr_t>(ws) & 15u) return err(GW_ERR_ARG, "gw_cnn_act: ws must be 16-byte aligned");
+    gw_obs_source src;
+    gw_status st = gw_obs_view(env, &src);
+    if (st != GW_OK) return st;
+    if ((st = check_cnn(src, net, "gw_cnn_act")) != GW_OK) return st;
+    if (!(tau > 0.0f)) return err(GW_ERR_ARG, "gw_cnn_act: tau must be > 0");
+    const CnnParams cp = cnn_params(src, net, const_cast<float *>(ws));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int64_t tiles = (src.E + TILE - 1) / TILE;
+    const dim3 lgrid((unsigned)((tiles + L1_WAVES - 1) / L1_WAVES), src.K);
+    switch (src.N) {
+        case 1: hipLaunchKernelGGL(cnn_l1_kernel<2>, lgrid, dim3(64 * L1_WAVES), 0, s, cp); break;
+        case 2: hipLaunchKernelGGL(cnn_l1_kernel<3>, lgrid, dim3(64 * L1_WAVES), 0, s, cp); break;
+        case 3: hipLaunchKernelGGL(cnn_l1_kernel<4>, lgrid, dim3(64 * L1_WAVES), 0, s, cp); break;
+        case 4: hipLaunchKernelGGL(cnn_l1_kernel<5>, lgrid, dim3(64 * L1_WAVES), 0, s, cp); break;
+        case 5: hipLaunchKernelGGL(cnn_l1_kernel<6>, lgrid, dim3(64 * L1_WAVES), 0, s, cp); break;
+        case 6: hipLaunchKernelGGL(cnn_l1_kernel<7>, lgrid, dim3(64 * L1_WAVES), 0, s, cp); break;
+        case 7: hipLaunchKernelGGL(cnn_l1_kernel<8>, lgrid, dim3(64 * L1_WAVES), 0, s, cp); break;
+        case 8: hipLaunchKernelGGL(cnn_l1_kernel<9>, lgrid, dim3(64 * L1_WAVES), 0, s, cp); break;
+        default: return err(GW_ERR_ARG, "gw_cnn_act: N out of range");
+    }
+    hipLaunchKernelGGL(cnn_rare_plan, dim3(1), dim3(1024), 0, s, cp);
+#define RARE(NP) hipLaunchKernelGGL(cnn_rare_kernel<NP>, dim3(RARE_BLOCKS), dim3(64 * RARE_WAVES), 0, s, cp)
+    switch (src.N) {
+        case 1: RARE(2); break;
+        case 2: RARE(3); break;
+        case 3: RARE(4); break;
+        case 4: RARE(5); break;
+        case 5: RARE(6); break;
+        case 6: RARE(7); break;
+        case 7: RARE(8); break;
+        default: RARE(9); break;
+    }
+#undef RARE
+    hipLaunchKernelGGL(cnn_bucket_reset, dim3((src.K * cp.P + 255) / 256), dim3(256), 0, s, cp);
+    ActParams p;
+    p.net = cnn_tail(net);
+    p.c1 = cp.ws.mlp.c1;
+    p.w2img = cp.ws.mlp.w2;
+    p.w3img = cp.ws.mlp.w3;
+    p.w2bimg = cp.ws.mlp.w2b;
+    p.desc = src.desc;
+    p.base = src.base;
+    p.mask = mask;
+    p.uniform = uniform;
+    p.h1 = cp.ws.h1;
+    p.rare_z = cp.ws.rare_z;
+    p.rare_n = cp.ws.rare_n;
+    p.actions = actions;
+    p.probs = probs;
+    p.logits = logits;
+    p.E = src.E;
+    p.env_offset = src.env_offset;
+    p.N = src.N;
+    p.K = src.K;
+    p.HW = src.H * src.W;
+    p.variant = src.variant;
+    p.training = training ? 1 : 0;
+    p.tau = tau;
+    p.key0 = (uint32_t)seed;
+    p.key1 = (uint32_t)(seed >> 32);
+    p.ctr0 = (uint32_t)counter;
+    p.ctr1 = (uint32_t)(counter >> 32);
+    for (int k = 0; k < MAXN; ++k) p.apples[k] = src.apples[k];
+    p.ab = 0;
+    p.tiles = (int)tiles;
+    const int64_t want = (tiles + 15) / 16;
+    const int per_agent = (int)std::max<int64_t>(1, std::min<int64_t>(want, std::max(1, 256 / src.K)));
+    hipLaunchKernelGGL((act_kernel<2, 16, true, true>), dim3(per_agent, src.K), dim3(1024), 0, s, p);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return err(GW_ERR_HIP, std::string("gw_cnn_act: ") + hipGetErrorString(e));
     return GW_OK;
 }
 

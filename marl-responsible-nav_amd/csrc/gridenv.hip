@@ -1898,6 +1898,7 @@ struct Env {
     bool obs_async = false;
     bool obs_lazy = false;                        // gw_set_obs_async(env, 2): launch at the next step
     bool obs_hi = false;                          // GW_OBS_PRIO=hi (A/B): obs stream high priority, aux normal
+    int obs_chunks = 1;                           // GW_OBS_CHUNKS: the obs writer as this many launches
     // one obs stream: a second one alternating with the descriptor buffer (so obs_kernel(t+1)
     // could start while obs_kernel(t) drains) measured 2.1x slower at C3 (more streams than the
     // process's hardware queues, GPU_MAX_HW_QUEUES = 4; profiles/r1_async)
@@ -2248,8 +2249,29 @@ hipError_t dispatch_reset(const Env *env, const gw::Params &p, hipStream_t s) {
     return hipErrorInvalidValue;
 }
 
+hipError_t launch_obs_range(const Env *env, const gw::Params &p, float *obs, float *final_obs, hipStream_t s);
+
+// GW_OBS_CHUNKS = c > 1: the writer as c launches over consecutive env ranges.  The hardware
+// dispatches one kernel's workgroups ahead of a later kernel of another queue, so a single
+// long writer holds the CUs until its last workgroup is placed; between chunk launches the
+// caller stream's kernels (the next actor) get their turn.
 hipError_t launch_obs(const Env *env, const gw::Params &p, float *obs, float *final_obs, hipStream_t s) {
     if (!obs && !final_obs) return hipSuccess;
+    const int64_t n = p.e_end - p.e_begin;
+    if (n <= 0) return hipSuccess;
+    const int64_t blocks = (n + env->obs_be - 1) / env->obs_be;
+    const int64_t c = std::max<int64_t>(1, std::min<int64_t>(env->obs_chunks, blocks));
+    for (int64_t i = 0; i < c; ++i) {
+        gw::Params q = p;
+        q.e_begin = p.e_begin + blocks * i / c * env->obs_be;
+        q.e_end = std::min(p.e_end, p.e_begin + blocks * (i + 1) / c * env->obs_be);
+        const hipError_t e = launch_obs_range(env, q, obs, final_obs, s);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_obs_range(const Env *env, const gw::Params &p, float *obs, float *final_obs, hipStream_t s) {
     const int64_t n = p.e_end - p.e_begin;
     if (n <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((n + env->obs_be - 1) / env->obs_be);
@@ -2411,6 +2433,8 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
         if (aa) env->async_aux = std::atoi(aa) != 0;
         const char *op = std::getenv("GW_OBS_PRIO");
         if (op && std::strcmp(op, "hi") == 0) env->obs_hi = true;
+        const char *oc = std::getenv("GW_OBS_CHUNKS");
+        if (oc) env->obs_chunks = std::max(1, std::min(64, std::atoi(oc)));
         const char *ch = std::getenv("GW_CHUNKS");
         if (ch) env->chunks = std::max(1, std::min(16, std::atoi(ch)));
     }

@@ -166,7 +166,8 @@ EXPORTS = ["gw_create", "gw_reset", "gw_step", "gw_state_view", "gw_copy_state",
            "gw_profile_read", "gw_stats_rows", "gw_dims", "gw_last_error", "gw_destroy", "gw_fear_matrix",
            "gw_adam_step", "gw_soft_update", "gw_obs_view", "gw_set_last_error", "gw_actor_act",
            "gw_actor_workspace_floats", "gw_actor_prepare", "gw_rollout_tick", "gw_set_obs_async",
-           "gw_obs_fence", "gw_fear_fence", "gw_set_obs_dtype"]
+           "gw_obs_fence", "gw_fear_fence", "gw_set_obs_dtype", "gw_cnn_workspace_floats", "gw_cnn_prepare",
+           "gw_cnn_act"]
 
 
 class GwObsSource(C.Structure):
@@ -183,8 +184,23 @@ class GwMlpActors(C.Structure):
                 ("layer_norm", C.c_int32)] + [(n, C.c_void_p) for n in MLP_PARAM_FIELDS]
 
 
+CNN_PARAM_FIELDS = ["conv1_w", "conv1_b", "conv2_w", "conv2_b", "lin1_w", "lin1_b", "w2", "b2", "w3", "b3"]
+
+
+class GwCnnActors(C.Structure):
+    _fields_ = [("K", C.c_int32), ("H", C.c_int32), ("W", C.c_int32), ("c1", C.c_int32), ("c2", C.c_int32),
+                ("hidden", C.c_int32), ("n_actions", C.c_int32)] + [(n, C.c_void_p) for n in CNN_PARAM_FIELDS]
+
+
 def _declare(L):
     p = C.c_void_p
+    L.gw_cnn_workspace_floats.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_int64]
+    L.gw_cnn_workspace_floats.restype = C.c_int64
+    L.gw_cnn_prepare.argtypes = [p, C.POINTER(GwCnnActors), p, p]
+    L.gw_cnn_prepare.restype = C.c_int
+    L.gw_cnn_act.argtypes = [p, C.POINTER(GwCnnActors), p, C.c_int, C.c_float, C.c_uint64, C.c_uint64,
+                             p, p, p, p, p, p]
+    L.gw_cnn_act.restype = C.c_int
     L.gw_create.argtypes = [C.POINTER(GwScenario), C.POINTER(GwConfig), C.c_int, C.POINTER(C.c_void_p)]
     L.gw_create.restype = C.c_int
     L.gw_reset.argtypes = [p, p, p, p, p, p]

@@ -128,6 +128,15 @@ class CNNActor(nn.Module):
         self.patchify = (len(channels) == 2 and all(k == s for k, s in zip(kernels, strides))
                          and H % (kernels[0] * kernels[1]) == 0 and W % (kernels[0] * kernels[1]) == 0)
 
+    def fusable(self) -> bool:
+        """configs/cnn.yaml exactly: conv 1 -> 32 -> 64, kernel 2 stride 2, hidden 128-128, 9 actions."""
+        c1, c2 = self.conv[0], self.conv[2]
+        return (len(self.conv) == 4 and c1.in_channels == 1 and c1.out_channels == 32 and c2.out_channels == 64
+                and c1.kernel_size == (2, 2) and c1.stride == (2, 2) and c2.kernel_size == (2, 2)
+                and c2.stride == (2, 2) and c1.padding == (0, 0) and c2.padding == (0, 0) and len(self.mlp) == 5
+                and self.mlp[0].out_features == 128 and self.mlp[2].out_features == 128
+                and self.mlp[4].out_features == N_ACTIONS)
+
     def forward(self, x):
         if self.patchify:
             return self._forward_patch_gemm(x)
@@ -198,19 +207,27 @@ class MultiAgentActors(nn.Module):
 
     # ---------------------------------------------------------------------------------------
     def fusable(self, env) -> bool:
-        """The fused HIP get_action (gw_actor_act, include/actor_ops.h) covers the stacked f32
-        MLP with two 128-wide hidden layers over a VecGridEnv's own observations."""
-        if self.arch != "mlp" or self.dtype != torch.float32:
+        """The fused HIP get_action covers (gw_actor_act, include/actor_ops.h) the stacked f32 MLP
+        with two 128-wide hidden layers and (gw_cnn_act) the configs/cnn.yaml CNN head, over a
+        VecGridEnv's own observations."""
+        if self.dtype != torch.float32 or self.K != env.K:
+            return False
+        if self.arch == "cnn":
+            return ((self.H, self.W) == (env.H, env.W) and env.H % 4 == 0 and env.W % 4 == 0
+                    and env.H * env.W <= 4096 and all(n.fusable() for n in self.nets))
+        if self.arch != "mlp":
             return False
         net = self.net
         return (net.n_layers == 3 and net.weights[0].shape[-1] == 128 and net.weights[1].shape == (self.K, 128, 128)
-                and net.weights[2].shape[-1] == N_ACTIONS and net.in_dim == env.H * env.W and self.K == env.K)
+                and net.weights[2].shape[-1] == N_ACTIONS and net.in_dim == env.H * env.W)
 
     def mark_updated(self):
         """Declare the parameters changed outside torch's in-place ops (HIP optimizer, graph
         replay): the fused path re-derives its workspace before the next act_env."""
         if self.arch == "mlp":
             self.net.epoch += 1
+        else:
+            self._epoch = getattr(self, "_epoch", 0) + 1
 
     @torch.no_grad()
     def act_env(self, env, mask: torch.Tensor | None = None, training: bool = True, tau: float = 1.0,
@@ -223,6 +240,9 @@ class MultiAgentActors(nn.Module):
         [K, E, 9], softmax, mask, argmax.  -> (actions [E, K] int32, probs [K, E, 9] float32).
         Raises if the library or a GPU is missing (no fallback)."""
         from . import _lib
+        if self.arch == "cnn":
+            return self._act_env_cnn(env, mask, training, tau, seed, counter, uniform, actions_out, probs_out,
+                                     logits_out)
         net, K, E, dev = self.net, self.K, env.E, env.device
         st = self._fast
         if st is None or st["env"] is not env:  # per-(actors, env) constants, built once
@@ -268,4 +288,61 @@ class MultiAgentActors(nn.Module):
                                           probs_out.data_ptr(),
                                           logits_out.data_ptr() if logits_out is not None else None,
                                           torch.cuda.current_stream(dev).cuda_stream), "gw_actor_act")
+        return actions_out, probs_out
+
+    def _act_env_cnn(self, env, mask, training, tau, seed, counter, uniform, actions_out, probs_out, logits_out):
+        """act_env for the CNN head: gw_cnn_act (layer 1 from the obs descriptors through the
+        per-position delta table, include/actor_ops.h), then the same fused layers 2-3 + noise +
+        softmax + mask + argmax as the MLP path."""
+        from . import _lib
+        K, E, dev = self.K, env.E, env.device
+        st = self._fast
+        if st is None or st["env"] is not env:
+            if not self.fusable(env):
+                raise _lib.GwError("act_env: CNN actor not fusable (needs conv 32-64 k2 s2, hidden 128-128, "
+                                   "9 actions, f32, the env's H x W, multiples of 4)")
+            lib = _lib.load()
+            ws_n = int(lib.gw_cnn_workspace_floats(env.H, env.W, K, E))
+            st = self._fast = dict(env=env, lib=lib, ws=torch.empty(ws_n, dtype=torch.float32, device=dev), key=None,
+                                   spec=None, packed=None)
+        params = [p for n in self.nets for p in n.parameters()]
+        key = (tuple(p._version for p in params), tuple(p.data_ptr() for p in params), getattr(self, "_epoch", 0))
+        if key != st["key"]:
+            with torch.no_grad():  # the ABI's stacked layouts (include/actor_ops.h gw_cnn_actors)
+                pk = dict(
+                    conv1_w=torch.stack([n.conv[0].weight for n in self.nets]).contiguous(),
+                    conv1_b=torch.stack([n.conv[0].bias for n in self.nets]).contiguous(),
+                    conv2_w=torch.stack([n.conv[2].weight for n in self.nets]).contiguous(),
+                    conv2_b=torch.stack([n.conv[2].bias for n in self.nets]).contiguous(),
+                    lin1_w=torch.stack([n.mlp[0].weight for n in self.nets]).contiguous(),
+                    lin1_b=torch.stack([n.mlp[0].bias for n in self.nets]).contiguous(),
+                    w2=torch.stack([n.mlp[2].weight.t() for n in self.nets]).contiguous(),
+                    b2=torch.stack([n.mlp[2].bias for n in self.nets]).contiguous(),
+                    w3=torch.stack([n.mlp[4].weight.t() for n in self.nets]).contiguous(),
+                    b3=torch.stack([n.mlp[4].bias for n in self.nets]).contiguous())
+            st["packed"] = pk
+            st["spec"] = _lib.GwCnnActors(K, env.H, env.W, 32, 64, 128, N_ACTIONS,
+                                          *[pk[n].data_ptr() for n in _lib.CNN_PARAM_FIELDS])
+            with torch.cuda.device(dev):
+                _lib.check(st["lib"].gw_cnn_prepare(env.handle, C.byref(st["spec"]), st["ws"].data_ptr(),
+                                                    torch.cuda.current_stream(dev).cuda_stream), "gw_cnn_prepare")
+            st["key"] = key
+        if actions_out is None:
+            actions_out = torch.empty((E, K), dtype=torch.int32, device=dev)
+        if probs_out is None:
+            probs_out = torch.empty((K, E, N_ACTIONS), dtype=torch.float32, device=dev)
+        if not (actions_out.dtype == torch.int32 and actions_out.shape == (E, K) and actions_out.is_contiguous()):
+            raise ValueError("act_env: actions_out must be a contiguous int32 [E, K] tensor")
+        if not (probs_out.dtype == torch.float32 and probs_out.shape == (K, E, N_ACTIONS) and probs_out.is_contiguous()):
+            raise ValueError("act_env: probs_out must be a contiguous float32 [K, E, 9] tensor")
+        if uniform is not None and not (uniform.dtype == torch.float32 and uniform.shape == (K, E, N_ACTIONS)):
+            raise ValueError("act_env: uniform must be float32 [K, E, 9]")
+        if mask is not None and not (mask.shape == (E, K) and mask.element_size() == 2 and mask.is_contiguous()):
+            raise ValueError("act_env: mask must be a contiguous 16-bit [E, K] tensor")
+        _lib.check(st["lib"].gw_cnn_act(env.handle, C.byref(st["spec"]), st["ws"].data_ptr(), int(bool(training)),
+                                        float(tau), int(seed) & 0xFFFFFFFFFFFFFFFF, int(counter) & 0xFFFFFFFFFFFFFFFF,
+                                        uniform.contiguous().data_ptr() if uniform is not None else None,
+                                        mask.data_ptr() if mask is not None else None, actions_out.data_ptr(),
+                                        probs_out.data_ptr(), logits_out.data_ptr() if logits_out is not None else None,
+                                        torch.cuda.current_stream(dev).cuda_stream), "gw_cnn_act")
         return actions_out, probs_out

@@ -11,7 +11,7 @@ def main(path):
             m = re.search(r"\n\s+" + re.escape(key) + r":\s+(\S+)", blk)
             return m.group(1) if m else "?"
         name = g(".name")
-        if "gw" not in name:
+        if "gw" not in name and "cnn" not in name and "act" not in name:
             continue
         print("%-48s vgpr=%-4s sgpr=%-4s scratch=%-4s lds=%s" % (
             name[:48], g(".vgpr_count"), g(".sgpr_count"), g(".private_segment_fixed_size"),
