@@ -152,9 +152,9 @@ def main():
     ap.add_argument("--updates-per-step", type=int, default=0,
                     help="c5 only: MADDPG updates (batch 128, one HIP-graph replay each) per env step")
     ap.add_argument("--profile-every", type=int, default=-1,
-                    help="bracket every n-th timed step's kernels with HIP events (0 = none, -1 = auto: "
-                         "every step up to 64 timed steps, else about 64 samples); the events cost "
-                         "~2-3 us per kernel boundary")
+                    help="time every n-th timed step's kernels with HIP events carried by their launches "
+                         "(0 = none, -1 = auto: every 4th step up to 256 timed steps, else about 64 "
+                         "samples); a profiled step costs ~4-6 us more")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cnn-torch", action="store_true",
                     help="c4cnn: the PyTorch CNN forward on the dense obs instead of gw_cnn_act (A/B)")
@@ -175,6 +175,10 @@ def main():
                     help="c5: start each step's obs writer right after its world update (A/B)")
     ap.add_argument("--obs-lazy", action="store_true",
                     help="launch each step's obs writer at the next step (gw_set_obs_async 2; A/B)")
+    ap.add_argument("--graph", type=int, default=-1,
+                    help="replay the timed steps as HIP graphs of this many captured steps (0 = eager "
+                         "launches, -1 = auto: 16 for the launch-bound env-only workloads that run "
+                         "synchronous obs on one rank, i.e. C1/C2, else eager)")
     args = ap.parse_args()
 
     import torch
@@ -205,14 +209,6 @@ def main():
     # otherwise lose CUs to it) for the full rollout.  Measured A/B: profiles/r1_async/
     obs_mode = False if args.sync_obs else \
         ("lazy" if (args.obs_lazy or (cfg.get("rollout") and not args.obs_eager)) else True)
-    # small batches (C2: 34 MB of obs per step) are bound by the launch chain, where the async
-    # path's extra event records / waits cost more host time than the overlap saves
-    # (tools/host_cost.py: 24.1 sync vs 25.8 us async wall per step at 4,096 envs)
-    from marlnav import scenario as S
-    sc = S.builtin(cfg["scenario"])
-    if obs_mode and not cfg.get("rollout") and not (args.obs_lazy or args.obs_eager) and \
-            (args.envs or cfg["envs"]) * sc.K * sc.HW * (2 if args.obs_dtype == "bf16" else 4) < (128 << 20):
-        obs_mode = False
     if cfg.get("arch") == "cnn" and not (args.cnn_torch or args.obs_lazy or args.sync_obs):
         # the 2.1 GB writer starts right after the world update, as 4 launches so that the next
         # actor's kernels are dispatched between them (profiles/r2_cnn: 0.715 ms per step lazy in
@@ -229,14 +225,29 @@ def main():
                      max_steps=150, auto_reset=True, seed=42, env_offset=rank * E, stats=True,
                      obs_dtype=torch.bfloat16 if args.obs_dtype == "bf16" else torch.float32)
     N, K, HW = env.N, env.K, env.H * env.W
+    # the defer path's small batches (below 128 MB of obs per step) run synchronous obs: its
+    # pipeline's cross-queue waits cost more than the overlap saves there.  Batches of at most
+    # 64 MiB run the merged path (gw_kernel_path), whose pipeline has no cross-queue waits.
+    obs_bytes = E * K * HW * (2 if args.obs_dtype == "bf16" else 4)
+    if obs_mode and env.kernel_path != "merged" and not cfg.get("rollout") and \
+            not (args.obs_lazy or args.obs_eager) and obs_bytes < (128 << 20):
+        obs_mode = False
+    # a step of a few envs (C1) is bound by the host's launches: synchronous obs, HIP graphs
+    if args.graph < 0 and not cfg.get("rollout") and world == 1 and obs_bytes <= (1 << 20) and \
+            not (args.obs_lazy or args.obs_eager):
+        obs_mode = False
     stream = torch.cuda.current_stream()
-    stats_acc = torch.zeros_like(env.out["stats"][0])
 
     from marlnav.parallel import ReturnGather, StatsReducer
     reducer = StatsReducer(env.out["stats"].shape[1], env.device) if world > 1 else None
     # per-step RCCL all-gather of every env's completed-episode return + done flag (SURVEY §8e;
     # maddpg/agent.py:229-247): gw_step writes them straight into the send buffer
-    gather = None if args.no_gather else ReturnGather(world * E, rank, world, env.device)
+    graph_n = args.graph
+    if graph_n < 0:  # auto: the launch-chain-bound regime (synchronous obs, env only, one rank)
+        graph_n = 16 if (not cfg.get("rollout") and not obs_mode and world == 1) else 0
+    graph_n = min(graph_n, args.steps)
+    gather = None if args.no_gather else ReturnGather(world * E, rank, world, env.device,
+                                                      **({"window": graph_n} if graph_n else {}))
 
     def one_step(i):
         r = env.step(into=gather.into() if gather is not None else None)
@@ -284,17 +295,32 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
 
+    # kernel spans are sampled: each profiled step costs ~4-6 us of event bookkeeping in the
+    # pipeline (profiles/r2_events), so a short run samples every 4th step (5 of the driver's 20)
+    pe = args.profile_every if args.profile_every >= 0 else \
+        (1 if args.steps < 8 else (4 if args.steps <= 256 else args.steps // 64))
+    graph = None
+    if graph_n:
+        # the timed steps as HIP graphs of graph_n steps (captured here, before the timed region:
+        # nothing runs at capture), the remainder eagerly after them; the kernel spans are those
+        # of the last replay's sampled steps
+        if gather is not None:
+            gather.compact()  # the warmup's partial window
+        graph = env.capture_steps(graph_n, gather)
+    n_graph = args.steps - args.steps % graph_n if graph_n else 0
+
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ev0.record(stream)
-    pe = args.profile_every if args.profile_every >= 0 else (1 if args.steps <= 64 else args.steps // 64)
-    for i in range(args.steps):
-        if pe > 0:
+    for i in range(0, n_graph, max(graph_n, 1)):
+        graph.replay()
+    for i in range(n_graph, args.steps):
+        if pe > 0 and graph is None:
             env.profile(i % pe == 0)
-        r = one_step(i)
+        one_step(i)
     if cfg.get("rollout"):
         ro.fence()  # the last step's obs writes, FeAR outputs and statistics
     env.obs_fence()  # belong to the timed region
@@ -306,6 +332,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
+    if graph is not None:
+        # HIP timing events cannot be recorded inside a graph: the kernel spans come from 16
+        # eager steps right after the timed region (same env, same kernels, untimed)
+        env.profile(True)
+        for i in range(16):
+            one_step(i)
+        torch.cuda.synchronize()
     env.profile(False)
     (ms_step, ms_obs, ms_fear), nprof = env.profile_read()
     gpu_ms = ev0.elapsed_time(ev1)
@@ -314,7 +347,7 @@ def main():
     if world > 1:
         dist.all_reduce(t_local, op=dist.ReduceOp.MAX)
     t_max = float(t_local.item())
-    stats = r.stats.sum(0).cpu().tolist()
+    stats = env.out["stats"].sum(0).cpu().tolist()
     gathered = None
     if gather is not None:
         gathered = {"episodes": int(gather.n_completed.item()), "bytes_per_rank_per_step": 9 * gather.emax,
@@ -325,8 +358,11 @@ def main():
         avg_step_ms, avg_obs_ms = ms_step / max(nprof, 1), ms_obs / max(nprof, 1)
         avg_fear_ms = ms_fear / max(nprof, 1)
         fused = env.fused
+        merged = env.kernel_path == "merged" and bool(obs_mode)
         if fused:  # one launch per step moves every byte of the step
             dom, bytes_per_launch, dur = "step_fused", (step_b + obs_b) * E, avg_step_ms
+        elif merged:  # step_obs: step t + the obs writer of step t-1 in one launch (its spans: kind 1)
+            dom, bytes_per_launch, dur = "step_obs", (step_b + obs_b) * E, avg_obs_ms
         elif avg_obs_ms >= avg_step_ms:
             dom, bytes_per_launch, dur = "obs_kernel", obs_b * E, avg_obs_ms
         else:
@@ -337,6 +373,7 @@ def main():
             with open(os.path.join(REPO, "profiles", "latest.json")) as f:
                 prof = json.load(f)
             if prof.get("config") == args.config and not args.envs and args.fear < 0 and not fused \
+                    and dom in prof["kernels"] \
                     and args.obs_dtype == "f32":
                 traffic = prof["kernels"][dom]["hbm_bytes_per_launch"]
                 traffic_src = prof["source"]
@@ -369,10 +406,12 @@ def main():
                          # per step: what the pipelined steps sustain end to end
                          "step_level_GBps": (step_b + obs_b) * E / (t_max / args.steps) / 1e9},
             "kernels_ms": {"profiled_steps": nprof, "step_kernel": avg_step_ms, "obs_kernel": avg_obs_ms, "fear_kernel": avg_fear_ms,
-                           "kernel_path": os.environ.get("GW_KERNEL", "defer"),
+                           "kernel_path": env.kernel_path,
                            "stream_ms_per_step": gpu_ms / args.steps,
                            "pipeline_chunks": int(os.environ.get("GW_CHUNKS", "1")) if not env.fused else 1,
-                           "obs_async": obs_mode, "fear_async": env.fear_async},
+                           "obs_async": obs_mode, "fear_async": env.fear_async,
+                           "graph_steps": graph_n,
+                           "spans_from": "16 eager steps after the timed region" if graph_n else "the timed steps"},
             "last_step_episodes": {"completed": stats[1], "mean_return": stats[0] / max(stats[1], 1.0),
                          "mean_len": stats[6] / max(stats[1], 1.0)},
             # completed-episode returns all-gathered every step (warmup + timed steps, all ranks)

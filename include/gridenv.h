@@ -158,6 +158,12 @@ gw_status gw_fear_matrix(void *env, int64_t n, const int32_t *cells, const int32
  * kernel's rows then fear_v2's rows, each kernel filling the fields it owns, zeros elsewhere). */
 int64_t gw_stats_rows(void *env);
 
+/* The kernel path gw_create chose: 0 "v1", 1 "split", 2 "fused", 3 "defer", 4 "merged".
+ * GW_KERNEL selects it; unset: "merged" when a step's obs is at most GW_MERGE_BYTES (default
+ * 192 MiB: small batches, bound by the step's latency chain, gain from one step_obs launch per
+ * pipelined step), else "defer".  -1 on a null handle. */
+int64_t gw_kernel_path(void *env);
+
 /* What the observation an env last wrote (gw_reset / gw_step) is made of, for ops that work
  * on it without reading it back (actor_ops.h): the static step-encoding map plus, per env, a
  * 48-byte descriptor (agent cells, reset / apple flags; ma_customenv.py:197-209, 303-322).

@@ -23,6 +23,20 @@ extern "C" {
 gw_status gw_rollout_tick(const double *partials, int64_t rows, int32_t n_fields, double *row_sum,
                           double *totals, int64_t *counter, void *stream);
 
+/* Completed-episode return compaction of a window of gathered steps (marlnav/parallel.py
+ * ReturnGather.compact; the reference appends scores[i] to completed_episode_scores for every
+ * env done this step, maddpg/agent.py:229-247).  recv holds `steps` x `world` slots of
+ * slot_bytes bytes: [emax] f64 returns, then [emax] u8 done flags (slot_bytes % 8 == 0,
+ * slot_bytes >= 9 * emax).  Every done element, in (step, rank, env) order, is appended to the
+ * ring scores[capacity] at (*n_completed + its rank) % capacity (only the last `capacity` of
+ * the window are written), and *n_completed grows by the window's count.  scratch:
+ * gw_return_compact_scratch(steps, world, emax) int32 words of device memory.  Two launches,
+ * deterministic, no host synchronisation (graph-capturable). */
+gw_status gw_return_compact(const uint8_t *recv, int64_t steps, int32_t world, int64_t emax,
+                            int64_t slot_bytes, double *scores, int64_t capacity,
+                            int64_t *n_completed, int32_t *scratch, void *stream);
+int64_t gw_return_compact_scratch(int64_t steps, int32_t world, int64_t emax);
+
 #ifdef __cplusplus
 }
 #endif

@@ -17,6 +17,7 @@
 // compiled with -ffp-contract=off and written with explicit _rn intrinsics in the order
 // numpy/Python evaluate it.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cstdint>
 #include <cstdio>
@@ -90,6 +91,7 @@ struct Params {
     uint32_t hw8_magic;       // ceil(2^32 / (H*W/8))
     int lds_cdf, n_cdf, ctab_off, resp_off;  // step_v2 dynamic LDS: [cdf][cell table][Resp 100 f64]
     int obs_be;               // envs per obs_kernel block (<= OBS_BE)
+    int obs_bf16;             // obs buffers hold bf16 (the merged step_obs kernel's writer role)
     int64_t e_begin, e_end;   // env range of this launch (step_v2 / obs_kernel chunks)
     uint4 *fwork;             // [E][FearRec<N>::R4] deferred-FeAR records (GW_KERNEL=defer)
     int64_t stats_row0;       // first gw_step_out.stats row this launch writes
@@ -1041,13 +1043,13 @@ __device__ __forceinline__ float agent_value(bool reset, int n, int k, bool on_a
 // bf16, so the compact format is lossless (the low 16 bits of the f32 are zero)
 __device__ __forceinline__ uint32_t bf16_bits(float v) { return __float_as_uint(v) >> 16; }
 
-template <bool VEC4, bool NT, bool BF16 = false>
-__global__ void __launch_bounds__(OBS_THREADS) obs_kernel(Params p, float *__restrict__ obs,
-                                                          float *__restrict__ final_obs) {
-    // LDS sized to the launch (obs_lds_bytes): road bitmask, flags, then per (which, env, k)
-    // N + 1 patch cells and values.  Small (640 B at 32x32, N = 4, K = 2, 4 envs), so obs blocks
-    // never take the LDS a co-resident kernel (the fused actor's 74-104 KB per CU) needs.
-    extern __shared__ uint32_t obs_lds[];
+// One obs block (T threads): the envs [e_begin + bid * obs_be, + obs_be) of the launch.
+// obs_lds: road bitmask, flags, then per (which, env, k) N + 1 patch cells and values, sized to
+// the launch (640 B at 32x32, N = 4, K = 2, 4 envs), so obs blocks never take the LDS a
+// co-resident kernel (the fused actor's 74-104 KB per CU) needs.
+template <int T, bool VEC4, bool NT, bool BF16>
+__device__ __forceinline__ void obs_block(const Params &p, float *__restrict__ obs, float *__restrict__ final_obs,
+                                          int64_t bid, uint32_t *obs_lds) {
     const int tid = threadIdx.x;
     const int HW = p.HW, N = p.N, K = p.K;
     const int npatch = N + 1;
@@ -1056,10 +1058,10 @@ __global__ void __launch_bounds__(OBS_THREADS) obs_kernel(Params p, float *__res
     uint32_t *s_flag = s_road + nroad;
     int *s_pc = reinterpret_cast<int *>(s_flag + OBS_BE);          // [2][obs_be][K][npatch]
     float *s_pv = reinterpret_cast<float *>(s_pc + 2 * p.obs_be * K * npatch);
-    const int64_t e0 = p.e_begin + (int64_t)blockIdx.x * p.obs_be;
+    const int64_t e0 = p.e_begin + bid * p.obs_be;
     if (e0 >= p.e_end) return;  // uniform per block
     const int nenv = (int)min((int64_t)p.obs_be, p.e_end - e0);
-    for (int w = tid; w < nroad; w += OBS_THREADS) s_road[w] = p.tb.roadbits[w];
+    for (int w = tid; w < nroad; w += T) s_road[w] = p.tb.roadbits[w];
     // patches: one thread per (which, env, k)
     if (tid < 2 * p.obs_be * K) {
         const int which = tid / (p.obs_be * K), el = (tid / K) % p.obs_be, k = tid % K;
@@ -1101,7 +1103,7 @@ __global__ void __launch_bounds__(OBS_THREADS) obs_kernel(Params p, float *__res
             const int total8 = nenv * HW8;
             for (int k = 0; k < K; ++k) {
                 uint4 *out8 = reinterpret_cast<uint4 *>(reinterpret_cast<uint16_t *>(dst) + ((int64_t)k * p.E + e0) * HW);
-                for (int i8 = tid; i8 < total8; i8 += OBS_THREADS) {
+                for (int i8 = tid; i8 < total8; i8 += T) {
                     const int el = HW8 == 1 ? i8 : (int)__umulhi((uint32_t)i8, p.hw8_magic);
                     if (!(s_flag[el] & need)) continue;
                     const int c0 = (i8 - el * HW8) << 3;
@@ -1132,7 +1134,7 @@ __global__ void __launch_bounds__(OBS_THREADS) obs_kernel(Params p, float *__res
             const int total4 = nenv * HW4;
             for (int k = 0; k < K; ++k) {
                 float4 *out4 = reinterpret_cast<float4 *>(dst + ((int64_t)k * p.E + e0) * HW);
-                for (int i4 = tid; i4 < total4; i4 += OBS_THREADS) {
+                for (int i4 = tid; i4 < total4; i4 += T) {
                     const int el = HW4 == 1 ? i4 : (int)__umulhi((uint32_t)i4, p.hw4_magic);
                     if (!(s_flag[el] & need)) continue;
                     const int c0 = (i4 - el * HW4) << 2;
@@ -1163,7 +1165,7 @@ __global__ void __launch_bounds__(OBS_THREADS) obs_kernel(Params p, float *__res
             const int total = nenv * HW;
             for (int k = 0; k < K; ++k) {
                 float *o = dst + ((int64_t)k * p.E + e0) * HW;
-                for (int i = tid; i < total; i += OBS_THREADS) {
+                for (int i = tid; i < total; i += T) {
                     const int el = i / HW;
                     if (!(s_flag[el] & need)) continue;
                     const int c = i - el * HW;
@@ -1176,6 +1178,13 @@ __global__ void __launch_bounds__(OBS_THREADS) obs_kernel(Params p, float *__res
             }
         }
     }
+}
+
+template <bool VEC4, bool NT, bool BF16 = false>
+__global__ void __launch_bounds__(OBS_THREADS) obs_kernel(Params p, float *__restrict__ obs,
+                                                          float *__restrict__ final_obs) {
+    extern __shared__ uint32_t obs_lds[];
+    obs_block<OBS_THREADS, VEC4, NT, BF16>(p, obs, final_obs, blockIdx.x, obs_lds);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1448,13 +1457,12 @@ __device__ __forceinline__ void block_stats(const Params &p, Contrib &ct, double
     }
 }
 
-template <int N, int KMAX, bool FEAR, bool OBS, bool DEFER = false>
-__global__ void __launch_bounds__(128) step_v2(Params p) {
+template <int N, int KMAX, bool FEAR, bool OBS, bool DEFER>
+__device__ __forceinline__ void step_v2_block(const Params &p, int64_t bid, V2Shared<N, KMAX, FEAR, OBS> &sh,
+                                              uint8_t *dyn) {  // dyn: [cdf P*18 f64][cell table HW u32][Resp]
     using Cfg = V2Cfg<N, KMAX, FEAR>;
     using Sh = V2Shared<N, KMAX, FEAR, OBS>;
     constexpr int BE = Cfg::BE, T = Cfg::THREADS, NP = N + 1, OB = Sh::OB;
-    __shared__ Sh sh;
-    extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];  // [cdf P*18 f64][cell table HW u32]
     const double *cdf_s = p.lds_cdf ? reinterpret_cast<const double *>(dyn) : nullptr;
     uint32_t *ctab = reinterpret_cast<uint32_t *>(dyn + p.ctab_off);
     double *resp_s = reinterpret_cast<double *>(dyn + p.resp_off);  // [10][10] Resp table
@@ -1462,8 +1470,8 @@ __global__ void __launch_bounds__(128) step_v2(Params p) {
     (void)okb;
 
     const int tid = threadIdx.x;
-    if (p.e_begin + (int64_t)blockIdx.x * BE >= p.e_end) return;  // uniform per block
-    const int64_t e0 = p.e_begin + (int64_t)blockIdx.x * BE;
+    if (p.e_begin + bid * BE >= p.e_end) return;  // uniform per block
+    const int64_t e0 = p.e_begin + bid * BE;
     const int nenv = (int)min((int64_t)BE, p.e_end - e0);
     const int K = p.K;
     Contrib ct;
@@ -1644,6 +1652,38 @@ __global__ void __launch_bounds__(128) step_v2(Params p) {
             }
         }
     }
+}
+
+template <int N, int KMAX, bool FEAR, bool OBS, bool DEFER = false>
+__global__ void __launch_bounds__(128) step_v2(Params p) {
+    __shared__ V2Shared<N, KMAX, FEAR, OBS> sh;
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+    step_v2_block<N, KMAX, FEAR, OBS, DEFER>(p, blockIdx.x, sh, dyn);
+}
+
+// ---------------------------------------------------------------------------------------
+// step_obs (GW_KERNEL=merged with async obs): ONE launch per gw_step on the caller's stream.
+// Blocks [0, nstep) are step_v2 (FeAR inline) of step t; blocks [nstep, grid) write the obs of
+// step t-1 from its descriptor buffer (q; the step writes the other buffer).  The two roles
+// share no data, so the latency-bound world update + FeAR and the HBM-bound store stream
+// overlap inside one kernel, with no second queue and no cross-queue events between steps.
+// ---------------------------------------------------------------------------------------
+template <int N, int KMAX, bool FEAR>
+__global__ void __launch_bounds__(128) step_obs(Params p, Params q, float *__restrict__ obs,
+                                                float *__restrict__ final_obs, uint32_t nstep, uint32_t order) {
+    __shared__ V2Shared<N, KMAX, FEAR, false> sh;
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+    const uint32_t nobs = gridDim.x - nstep;
+    // order 0: step blocks first (the long latency chains start first); 1: obs blocks first
+    const bool is_step = order == 0 ? blockIdx.x < nstep : blockIdx.x >= nobs;
+    const uint32_t rb = order == 0 ? (is_step ? blockIdx.x : blockIdx.x - nstep)
+                                   : (is_step ? blockIdx.x - nobs : blockIdx.x);
+    if (is_step)
+        step_v2_block<N, KMAX, FEAR, false, false>(p, rb, sh, dyn);
+    else if (q.obs_bf16)
+        obs_block<128, true, true, true>(q, obs, final_obs, rb, reinterpret_cast<uint32_t *>(dyn));
+    else
+        obs_block<128, true, true, false>(q, obs, final_obs, rb, reinterpret_cast<uint32_t *>(dyn));
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1866,6 +1906,12 @@ gw_status fail(gw_status s, const std::string &msg) {
         if (_e != hipSuccess) return fail(GW_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
     } while (0)
 
+#define GW_TRY(expr)                   \
+    do {                               \
+        gw_status _s = (expr);         \
+        if (_s != GW_OK) return _s;    \
+    } while (0)
+
 struct Env {
     int device = 0;
     int H = 0, W = 0, HW = 0, N = 0, K = 0, F = 0, P = 0;
@@ -1876,7 +1922,8 @@ struct Env {
     int apples[GW_MAX_AGENTS] = {0};
     bool initialized = false;
     int mode = 3;        // GW_KERNEL: 0 "v1" (first kernels), 1 "split" step_v2 (FeAR inline) + obs_kernel,
-                         // 2 "fused", 3 "defer" (default; FeAR on: step_v2 <DEFER>, then fear_v2 || obs_kernel)
+                         // 2 "fused", 3 "defer" (default; FeAR on: step_v2 <DEFER>, then fear_v2 || obs_kernel),
+                         // 4 "merged" (as split; with async obs one step_obs launch per step)
     int obs_be = 2;      // GW_OBS_BE: envs per obs_kernel block (default: see gw_create)
     bool obs_nt = true;  // GW_OBS_NT=0: plain instead of nontemporal obs stores
     bool obs_bf16 = false;  // gw_set_obs_dtype(env, GW_OBS_BF16): obs buffers hold bf16 (lossless)
@@ -1896,6 +1943,8 @@ struct Env {
     // (launched lazily: at the start of gw_step t+1, behind the caller's work between the steps,
     // e.g. the fused actor, so the writer never competes with it for the CUs; or at a fence)
     bool obs_async = false;
+    int merge_order = 0;                          // GW_MERGE_ORDER (A/B): step_obs role order
+    hipStream_t last_stream = nullptr;            // merged mode: the stream of the last gw_step
     bool obs_lazy = false;                        // gw_set_obs_async(env, 2): launch at the next step
     bool obs_hi = false;                          // GW_OBS_PRIO=hi (A/B): obs stream high priority, aux normal
     int obs_chunks = 1;                           // GW_OBS_CHUNKS: the obs writer as this many launches
@@ -1937,6 +1986,13 @@ struct Env {
     struct Span { size_t b, e; int kind; };  // kind 0 = step kernel(s), 1 = obs kernel(s), 2 = fear_v2
     std::vector<Span> spans;
     int64_t steps_timed = 0;
+    // flags of the pipeline's events.  They only order kernels of this device's queues (every
+    // kernel already ends with an agent-scope release), so by default they skip the
+    // system-scope fence (L2 write-back + invalidate) that a plain event record / wait costs at
+    // every use: 5 us per record and 11-18 us between consecutive obs writers at C3 with it.
+    // GW_EVENT_FENCE=system restores the plain events (A/B).
+    unsigned sync_flags = hipEventDisableTiming | hipEventDisableSystemFence;
+    unsigned prof_flags = hipEventDisableSystemFence;  // timing events of gw_profile
 };
 
 // the second stream and n fork/join events (timing disabled), created on first use
@@ -1944,7 +2000,7 @@ struct Env {
 gw_status ensure_events(Env *env, int n) {
     while ((int)env->sync_ev.size() < n) {
         hipEvent_t e;
-        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&e, env->sync_flags));
         env->sync_ev.push_back(e);
     }
     return GW_OK;
@@ -1985,36 +2041,54 @@ gw_status ensure_obs_stream(Env *env) {
         }
     }
     for (hipEvent_t &e : env->obs_done)
-        if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    if (!env->world_ev) HIP_TRY(hipEventCreateWithFlags(&env->world_ev, hipEventDisableTiming));
-    if (!env->fear_ev) HIP_TRY(hipEventCreateWithFlags(&env->fear_ev, hipEventDisableTiming));
+        if (!e) HIP_TRY(hipEventCreateWithFlags(&e, env->sync_flags));
+    if (!env->world_ev) HIP_TRY(hipEventCreateWithFlags(&env->world_ev, env->sync_flags));
+    if (!env->fear_ev) HIP_TRY(hipEventCreateWithFlags(&env->fear_ev, env->sync_flags));
     return GW_OK;
+}
+
+// gw_profile spans: the span's kernel launches carry its timing events in their dispatch
+// (hipExtLaunchKernelGGL start / stop events: the kernel's own begin / end timestamps, no
+// marker packets between the kernels of the pipeline).  The span's first launch takes the
+// start event, every launch the stop event (the last one's end wins).
+thread_local hipEvent_t t_span_start = nullptr, t_span_stop = nullptr;
+
+template <typename F, typename... Args>
+void gw_launch(F kernel, dim3 grid, dim3 block, size_t lds, hipStream_t s, Args... args) {
+    if (t_span_stop) {
+        hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)lds, s, t_span_start, t_span_stop, 0u, args...);
+        t_span_start = nullptr;
+    } else {
+        hipLaunchKernelGGL(kernel, grid, block, lds, s, args...);
+    }
 }
 
 hipError_t launch_obs(const Env *env, const gw::Params &p, float *obs, float *final_obs, hipStream_t s);
 hipEvent_t next_event(Env *env);
+gw_status prof_span_begin(Env *env, size_t &idx);
+gw_status prof_span_end(Env *env, size_t idx, int kind);
 
 // launch the queued obs_kernel on the obs stream, after its world update and (after != null)
 // after the caller's work up to `after`
 gw_status flush_obs(Env *env, hipEvent_t after) {
     if (!env->obs_queued) return GW_OK;
+    if (env->mode == 4) {  // merged: the last step's writer alone, on the stream of that step
+        const bool prof = env->qobs_prof;
+        size_t b = 0;
+        if (prof && prof_span_begin(env, b) != GW_OK) return GW_ERR_HIP;
+        HIP_TRY(launch_obs(env, env->qobs, env->qobs.out.obs, env->qobs.out.final_obs, env->last_stream));
+        if (prof) (void)prof_span_end(env, b, 1);
+        env->obs_queued = false;
+        return GW_OK;
+    }
     hipStream_t os = env->obs_stream;
     HIP_TRY(hipStreamWaitEvent(os, env->world_ev, 0));
     if (after) HIP_TRY(hipStreamWaitEvent(os, after, 0));
     const bool prof = env->qobs_prof;  // timed iff the step that queued it was
-    size_t b = env->ev_used;
-    if (prof) {
-        hipEvent_t e = next_event(env);
-        if (!e) return fail(GW_ERR_HIP, "hipEventCreate failed");
-        HIP_TRY(hipEventRecord(e, os));
-    }
+    size_t b = 0;
+    if (prof && prof_span_begin(env, b) != GW_OK) return GW_ERR_HIP;
     HIP_TRY(launch_obs(env, env->qobs, env->qobs.out.obs, env->qobs.out.final_obs, os));
-    if (prof) {
-        hipEvent_t e = next_event(env);
-        if (!e) return fail(GW_ERR_HIP, "hipEventCreate failed");
-        HIP_TRY(hipEventRecord(e, os));
-        env->spans.push_back({b, env->ev_used - 1, 1});
-    }
+    if (prof) (void)prof_span_end(env, b, 1);
     HIP_TRY(hipEventRecord(env->obs_done[env->qobs_buf], os));
     env->obs_pending[env->qobs_buf] = true;
     env->obs_queued = false;
@@ -2035,8 +2109,14 @@ gw_status wait_obs(Env *env, hipStream_t s) {
         if (st != GW_OK) return st;
     }
     if (env->obs_queued) {
+        const bool merged = env->mode == 4;
         const gw_status st = flush_obs(env, nullptr);
         if (st != GW_OK) return st;
+        if (merged && env->last_stream != s) {  // the writer ran on the last step's stream
+            GW_TRY(ensure_events(env, 1));
+            HIP_TRY(hipEventRecord(env->sync_ev[0], env->last_stream));
+            HIP_TRY(hipStreamWaitEvent(s, env->sync_ev[0], 0));
+        }
     }
     for (int i = 0; i < 2; ++i)
         if (env->obs_pending[i]) HIP_TRY(hipStreamWaitEvent(s, env->obs_done[i], 0));
@@ -2046,10 +2126,30 @@ gw_status wait_obs(Env *env, hipStream_t s) {
 hipEvent_t next_event(Env *env) {
     if (env->ev_used == env->ev_pool.size()) {
         hipEvent_t e = nullptr;
-        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        if (hipEventCreateWithFlags(&e, env->prof_flags) != hipSuccess) return nullptr;
         env->ev_pool.push_back(e);
     }
     return env->ev_pool[env->ev_used++];
+}
+
+// a profiled span: two timing events handed to the span's kernel launches (gw_launch)
+gw_status prof_span_begin(Env *env, size_t &idx) {
+    idx = env->ev_used;
+    hipEvent_t a = next_event(env), b = next_event(env);
+    if (!a || !b) return fail(GW_ERR_HIP, "hipEventCreate failed");
+    t_span_start = a;
+    t_span_stop = b;
+    return GW_OK;
+}
+
+gw_status prof_span_end(Env *env, size_t idx, int kind) {
+    if (t_span_start) {  // no kernel was launched in the span: nothing to time
+        env->ev_used = idx;
+    } else {
+        env->spans.push_back({idx, idx + 1, kind});
+    }
+    t_span_start = t_span_stop = nullptr;
+    return GW_OK;
 }
 
 template <typename T>
@@ -2062,11 +2162,6 @@ gw_status dalloc(Env *env, T **ptr, size_t count) {
     return GW_OK;
 }
 
-#define GW_TRY(expr)                   \
-    do {                               \
-        gw_status _s = (expr);         \
-        if (_s != GW_OK) return _s;    \
-    } while (0)
 
 gw::Params make_params(const Env *env) {
     gw::Params p;
@@ -2085,6 +2180,7 @@ gw::Params make_params(const Env *env) {
     p.ctab_off = p.lds_cdf ? ((p.n_cdf * 8 + 15) / 16) * 16 : 0;
     p.resp_off = p.ctab_off + ((env->HW * 4 + 15) / 16) * 16;
     p.obs_be = env->obs_be;
+    p.obs_bf16 = env->obs_bf16 ? 1 : 0;
     p.e_begin = 0;
     p.e_end = env->E;
     p.fwork = env->fwork;
@@ -2130,7 +2226,7 @@ hipError_t launch_v2(const Env *env, const gw::Params &p, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((n + BE - 1) / BE);
     const size_t dyn = (size_t)p.resp_off + (FEAR ? 100 * sizeof(double) : 0);
-    hipLaunchKernelGGL((gw::step_v2<N, KMAX, FEAR, OBS, DEFER>), dim3(grid), dim3(gw::V2Cfg<N, KMAX, FEAR>::THREADS), dyn, s, p);
+    gw_launch((gw::step_v2<N, KMAX, FEAR, OBS, DEFER>), dim3(grid), dim3(gw::V2Cfg<N, KMAX, FEAR>::THREADS), dyn, s, p);
     return hipGetLastError();
 }
 
@@ -2153,7 +2249,7 @@ hipError_t launch_fear_k(const Env *env, const gw::Params &p0, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((n + BE - 1) / BE);
     const size_t dyn = (size_t)p.resp_off + 100 * sizeof(double);
-    hipLaunchKernelGGL((gw::fear_v2<N, KMAX, WIDE>), dim3(grid), dim3(gw::V2Cfg<N, KMAX, true, WIDE>::THREADS), dyn, s, p);
+    gw_launch((gw::fear_v2<N, KMAX, WIDE>), dim3(grid), dim3(gw::V2Cfg<N, KMAX, true, WIDE>::THREADS), dyn, s, p);
     return hipGetLastError();
 }
 
@@ -2196,20 +2292,20 @@ hipError_t launch_v2_k(const Env *env, const gw::Params &p, hipStream_t s) {
 template <int N>
 hipError_t launch_step(const Env *env, const gw::Params &p, hipStream_t s) {
     if (env->mode == 2) return launch_v2_k<N, true>(env, p, s);
-    if (env->mode == 1 || env->mode == 3) return launch_v2_k<N, false>(env, p, s);
+    if (env->mode == 1 || env->mode == 3 || env->mode == 4) return launch_v2_k<N, false>(env, p, s);
     if (env->fear) {
         if (env->K <= 2) {
             constexpr int BE = gw::FearCfg<N, 2>::BE;
             const unsigned grid = (unsigned)((env->E + BE - 1) / BE);
-            hipLaunchKernelGGL((gw::step_kernel_fear<N, 2>), dim3(grid), dim3(256), 0, s, p);
+            gw_launch((gw::step_kernel_fear<N, 2>), dim3(grid), dim3(256), 0, s, p);
         } else {
             constexpr int BE = gw::FearCfg<N, N>::BE;
             const unsigned grid = (unsigned)((env->E + BE - 1) / BE);
-            hipLaunchKernelGGL((gw::step_kernel_fear<N, N>), dim3(grid), dim3(256), 0, s, p);
+            gw_launch((gw::step_kernel_fear<N, N>), dim3(grid), dim3(256), 0, s, p);
         }
     } else {
         const unsigned grid = (unsigned)((env->E + 255) / 256);
-        hipLaunchKernelGGL((gw::step_kernel_nofear<N>), dim3(grid), dim3(256), env->HW, s, p);
+        gw_launch((gw::step_kernel_nofear<N>), dim3(grid), dim3(256), env->HW, s, p);
     }
     return hipGetLastError();
 }
@@ -2217,7 +2313,7 @@ hipError_t launch_step(const Env *env, const gw::Params &p, hipStream_t s) {
 template <int N>
 hipError_t launch_reset(const Env *env, const gw::Params &p, hipStream_t s) {
     const unsigned grid = (unsigned)((env->E + 255) / 256);
-    hipLaunchKernelGGL((gw::reset_kernel<N>), dim3(grid), dim3(256), 0, s, p);
+    gw_launch((gw::reset_kernel<N>), dim3(grid), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 
@@ -2251,6 +2347,47 @@ hipError_t dispatch_reset(const Env *env, const gw::Params &p, hipStream_t s) {
 
 hipError_t launch_obs_range(const Env *env, const gw::Params &p, float *obs, float *final_obs, hipStream_t s);
 
+// obs_kernel's LDS: road bitmask, OBS_BE flags, [2][obs_be][K][N + 1] patch cells + values
+size_t obs_lds_bytes(const Env *env) {
+    return sizeof(uint32_t) * ((env->HW + 31) / 32 + gw::OBS_BE) +
+           (size_t)2 * 2 * env->obs_be * env->K * (env->N + 1) * sizeof(uint32_t);
+}
+
+template <int N, int KMAX, bool FEAR>
+hipError_t launch_step_obs_k(const Env *env, const gw::Params &p, const gw::Params &q, hipStream_t s) {
+    constexpr int BE = gw::V2Cfg<N, KMAX, FEAR>::BE;
+    const int64_t n = p.e_end - p.e_begin, nq = q.e_end - q.e_begin;
+    const unsigned nstep = (unsigned)((n + BE - 1) / BE);
+    const unsigned nobs = (unsigned)((nq + env->obs_be - 1) / env->obs_be);
+    const size_t step_dyn = (size_t)p.resp_off + (FEAR ? 100 * sizeof(double) : 0);
+    const size_t dyn = std::max(step_dyn, obs_lds_bytes(env));
+    gw_launch((gw::step_obs<N, KMAX, FEAR>), dim3(nstep + nobs), dim3(128), dyn, s, p, q, q.out.obs, q.out.final_obs,
+              nstep, (uint32_t)env->merge_order);
+    return hipGetLastError();
+}
+
+template <int N>
+hipError_t launch_step_obs_n(const Env *env, const gw::Params &p, const gw::Params &q, hipStream_t s) {
+    if (env->fear)
+        return env->K <= 2 ? launch_step_obs_k<N, 2, true>(env, p, q, s) : launch_step_obs_k<N, N, true>(env, p, q, s);
+    return env->K <= 2 ? launch_step_obs_k<N, 2, false>(env, p, q, s) : launch_step_obs_k<N, N, false>(env, p, q, s);
+}
+
+// merged mode: step t (p) and the obs writer of step t-1 (q) as one step_obs launch
+hipError_t launch_step_obs(const Env *env, const gw::Params &p, const gw::Params &q, hipStream_t s) {
+    switch (env->N) {
+        case 1: return launch_step_obs_n<1>(env, p, q, s);
+        case 2: return launch_step_obs_n<2>(env, p, q, s);
+        case 3: return launch_step_obs_n<3>(env, p, q, s);
+        case 4: return launch_step_obs_n<4>(env, p, q, s);
+        case 5: return launch_step_obs_n<5>(env, p, q, s);
+        case 6: return launch_step_obs_n<6>(env, p, q, s);
+        case 7: return launch_step_obs_n<7>(env, p, q, s);
+        case 8: return launch_step_obs_n<8>(env, p, q, s);
+    }
+    return hipErrorInvalidValue;
+}
+
 // GW_OBS_CHUNKS = c > 1: the writer as c launches over consecutive env ranges.  The hardware
 // dispatches one kernel's workgroups ahead of a later kernel of another queue, so a single
 // long writer holds the CUs until its last workgroup is placed; between chunk launches the
@@ -2275,18 +2412,16 @@ hipError_t launch_obs_range(const Env *env, const gw::Params &p, float *obs, flo
     const int64_t n = p.e_end - p.e_begin;
     if (n <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((n + env->obs_be - 1) / env->obs_be);
-    // obs_kernel's LDS: road bitmask, OBS_BE flags, [2][obs_be][K][N + 1] patch cells + values
-    const size_t lds = sizeof(uint32_t) * ((env->HW + 31) / 32 + gw::OBS_BE) +
-                       (size_t)2 * 2 * env->obs_be * env->K * (env->N + 1) * sizeof(uint32_t);
+    const size_t lds = obs_lds_bytes(env);
     if (env->obs_bf16) {  // gw_set_obs_dtype checked HW % 8 == 0
-        hipLaunchKernelGGL((gw::obs_kernel<true, true, true>), dim3(grid), dim3(gw::OBS_THREADS), lds, s, p, obs, final_obs);
+        gw_launch((gw::obs_kernel<true, true, true>), dim3(grid), dim3(gw::OBS_THREADS), lds, s, p, obs, final_obs);
     } else if (env->HW % 4 == 0) {
         if (env->obs_nt)
-            hipLaunchKernelGGL((gw::obs_kernel<true, true>), dim3(grid), dim3(gw::OBS_THREADS), lds, s, p, obs, final_obs);
+            gw_launch((gw::obs_kernel<true, true>), dim3(grid), dim3(gw::OBS_THREADS), lds, s, p, obs, final_obs);
         else
-            hipLaunchKernelGGL((gw::obs_kernel<true, false>), dim3(grid), dim3(gw::OBS_THREADS), lds, s, p, obs, final_obs);
+            gw_launch((gw::obs_kernel<true, false>), dim3(grid), dim3(gw::OBS_THREADS), lds, s, p, obs, final_obs);
     } else {
-        hipLaunchKernelGGL((gw::obs_kernel<false, false>), dim3(grid), dim3(gw::OBS_THREADS), lds, s, p, obs, final_obs);
+        gw_launch((gw::obs_kernel<false, false>), dim3(grid), dim3(gw::OBS_THREADS), lds, s, p, obs, final_obs);
     }
     return hipGetLastError();
 }
@@ -2317,7 +2452,7 @@ namespace {
 template <int N>
 hipError_t launch_fear_matrix(const Env *env, int64_t n, const gw::FmParams &q, hipStream_t s) {
     const size_t dyn = ((size_t)env->HW * 4 + 15) / 16 * 16;
-    hipLaunchKernelGGL((gw::fear_matrix_kernel<N>), dim3((unsigned)n), dim3(128), dyn, s, q);
+    gw_launch((gw::fear_matrix_kernel<N>), dim3((unsigned)n), dim3(128), dyn, s, q);
     return hipGetLastError();
 }
 }  // namespace
@@ -2409,10 +2544,20 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
     {
         const char *kv = std::getenv("GW_KERNEL");  // kernel path for A/B measurements
         env->mode = 3;
+        if (!kv && HW % 4 == 0) {  // small batches: the merged pipeline (profiles/r2_merged)
+            const char *mb = std::getenv("GW_MERGE_BYTES");
+            // crossover at C3's shape: merged wins up to 16,384 envs (134 MB of obs per step),
+            // defer from 32,768 (268 MB)
+            const int64_t lim = mb ? std::atoll(mb) : ((int64_t)192 << 20);
+            if (cfg->num_envs * (int64_t)K * HW * 4 <= lim) env->mode = 4;
+        }
         if (kv && std::strcmp(kv, "split") == 0) env->mode = 1;
         if (kv && std::strcmp(kv, "v1") == 0) env->mode = 0;
         if (kv && std::strcmp(kv, "fused") == 0 && HW % 4 == 0) env->mode = 2;
         if (kv && std::strcmp(kv, "defer") == 0) env->mode = 3;
+        if (kv && std::strcmp(kv, "merged") == 0 && HW % 4 == 0) env->mode = 4;
+        const char *mo = std::getenv("GW_MERGE_ORDER");
+        if (mo) env->merge_order = std::atoi(mo) ? 1 : 0;
         const char *dv = std::getenv("GW_DEFER");
         if (dv) env->defer_order = std::atoi(dv) == 0 ? 0 : (std::atoi(dv) == 3 ? 3 : 1);
         const char *fb = std::getenv("GW_FEAR_BE");
@@ -2437,6 +2582,11 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
         if (oc) env->obs_chunks = std::max(1, std::min(64, std::atoi(oc)));
         const char *ch = std::getenv("GW_CHUNKS");
         if (ch) env->chunks = std::max(1, std::min(16, std::atoi(ch)));
+        const char *ef = std::getenv("GW_EVENT_FENCE");
+        if (ef && std::strcmp(ef, "system") == 0) {
+            env->sync_flags = hipEventDisableTiming;
+            env->prof_flags = hipEventDefault;
+        }
     }
 
     auto cleanup = [&](gw_status s) {
@@ -2510,27 +2660,42 @@ gw_status gw_step(void *handle, const int32_t *rl_actions, const int32_t *script
     hipStream_t s = static_cast<hipStream_t>(stream);
     const bool want_obs = p.out.obs || p.out.final_obs;
     if (env->profiling) env->steps_timed++;
-    auto span_begin = [&](hipStream_t st, size_t &idx) -> gw_status {
-        idx = env->profiling ? env->ev_used : 0;
-        if (!env->profiling) return GW_OK;
-        hipEvent_t e = next_event(env);
-        if (!e) return fail(GW_ERR_HIP, "hipEventCreate failed");
-        HIP_TRY(hipEventRecord(e, st));
-        return GW_OK;
+    auto span_begin = [&](hipStream_t, size_t &idx) -> gw_status {
+        idx = 0;
+        return env->profiling ? prof_span_begin(env, idx) : GW_OK;
     };
-    auto span_end = [&](hipStream_t st, size_t b, int kind) -> gw_status {
-        if (!env->profiling) return GW_OK;
-        hipEvent_t e = next_event(env);
-        if (!e) return fail(GW_ERR_HIP, "hipEventCreate failed");
-        HIP_TRY(hipEventRecord(e, st));
-        env->spans.push_back({b, env->ev_used - 1, kind});
-        return GW_OK;
+    auto span_end = [&](hipStream_t, size_t b, int kind) -> gw_status {
+        return env->profiling ? prof_span_end(env, b, kind) : GW_OK;
     };
     // chunk size: a multiple of every block size in play (v2 BE, obs_be) so blocks never straddle
     const int64_t unit = 128;  // multiple of every step_v2 BE (<= 128) and obs_be (<= 8)
     const bool defer = env->mode == 3 && env->fear;
     const int nch = ((env->mode == 1 || defer) && want_obs && env->chunks > 1 && env->E >= unit * env->chunks)
                         ? env->chunks : 1;
+    if (env->obs_async && want_obs && env->mode == 4) {
+        // Merged pipeline: ONE launch per step on the caller's stream: this step's world update
+        // + FeAR (writing descriptor buffer nb) and the obs writer of the previous step (reading
+        // the other buffer) as the two block roles of step_obs (§5.7).  The writer of the last
+        // step stays queued until the next step or a fence.
+        env->last_stream = s;
+        const int nb = env->dcur ^ 1;
+        p.desc = env->desc_buf[nb];
+        const bool merge = env->obs_queued;
+        size_t b;
+        GW_TRY(span_begin(s, b));
+        if (merge)
+            HIP_TRY(launch_step_obs(env, p, env->qobs, s));
+        else
+            HIP_TRY(dispatch_step(env, p, s));
+        GW_TRY(span_end(s, b, merge ? 1 : 0));
+        env->qobs = p;
+        env->qobs_buf = nb;
+        env->qobs_prof = env->profiling;
+        env->obs_queued = true;
+        env->dcur = nb;
+        env->desc = env->desc_buf[nb];
+        return GW_OK;
+    }
     if (env->obs_async && want_obs && nch == 1 && (env->mode == 1 || env->mode == 3)) {
         // Software pipeline over steps.  The world update (and FeAR) of step t runs on s
         // (rewards, dones, masks, state, stats: stream-ordered as usual).  The obs writer of
@@ -2690,6 +2855,11 @@ gw_status gw_step(void *handle, const int32_t *rl_actions, const int32_t *script
 gw_status gw_set_obs_async(void *handle, int enable) {
     Env *env = static_cast<Env *>(handle);
     if (!env) return fail(GW_ERR_ARG, "null env");
+    if (!enable && env->obs_async && env->mode == 4 && env->obs_queued) {  // merged: drain the queued writer
+        hipStream_t ls = env->last_stream;
+        GW_TRY(flush_obs(env, nullptr));
+        HIP_TRY(hipStreamSynchronize(ls));
+    }
     if (!enable && env->obs_async && env->obs_stream) {
         // the synchronous path writes the current descriptor buffer in place: drain the writer
         GW_TRY(flush_obs(env, nullptr));
@@ -2720,6 +2890,11 @@ gw_status gw_set_obs_dtype(void *handle, int dtype) {
     if (dtype == GW_OBS_BF16 && (env->HW % 8 != 0 || env->mode == 0 || env->mode == 2))
         return fail(GW_ERR_ARG, "gw_set_obs_dtype: bf16 obs needs H*W % 8 == 0 and the split / defer kernel paths");
     const bool bf = dtype == GW_OBS_BF16;
+    if (bf != env->obs_bf16 && env->mode == 4 && env->obs_queued) {  // merged: the queued writer
+        hipStream_t ls = env->last_stream;
+        GW_TRY(flush_obs(env, nullptr));
+        HIP_TRY(hipStreamSynchronize(ls));
+    }
     if (bf != env->obs_bf16 && env->obs_stream) {
         // an obs_kernel still queued or in flight was sized for the old format: drain it first
         GW_TRY(flush_obs(env, nullptr));
@@ -2872,6 +3047,11 @@ gw_status gw_obs_view(void *handle, gw_obs_source *out) {
 }
 
 void gw_set_last_error(const char *msg) { g_err = msg ? msg : ""; }
+
+int64_t gw_kernel_path(void *handle) {
+    const Env *env = static_cast<const Env *>(handle);
+    return env ? env->mode : -1;
+}
 
 gw_status gw_dims(void *handle, int64_t out[5]) {
     Env *env = static_cast<Env *>(handle);

@@ -48,6 +48,101 @@ __global__ void __launch_bounds__(T) tick_kernel(const double *__restrict__ part
     if (tid == 0 && counter) counter[0] += 1;
 }
 
+// ---- completed-episode return compaction (parallel.ReturnGather.compact) ----
+// Element i of a window = (step t, rank r, env e) in that order, e fastest: slot (t, r) starts
+// at byte (t * world + r) * slot_bytes and holds [emax] f64 returns then [emax] u8 done flags.
+// Pass 1 counts each chunk's done flags; pass 2 gives every chunk its exclusive prefix (a sum
+// over the previous chunks' counts), scans the chunk in the block, and scatters the last
+// `capacity` completions into the ring in element order.  Deterministic; two launches.
+constexpr int CT = 256, CPT = 16, CCH = CT * CPT;  // threads, elements per thread, per chunk
+
+__device__ __forceinline__ uint32_t done_at(const uint8_t *__restrict__ recv, int64_t i, int64_t emax,
+                                            int64_t slot_bytes) {
+    const int64_t slot = i / emax, e = i - slot * emax;
+    return recv[slot * slot_bytes + 8 * emax + e] != 0;
+}
+
+__device__ __forceinline__ int block_sum_int(int v, int *red) {
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    const int tid = threadIdx.x;
+    __syncthreads();
+    if ((tid & 63) == 0) red[tid >> 6] = v;
+    __syncthreads();
+    int s = 0;
+#pragma unroll
+    for (int w = 0; w < CT / 64; ++w) s += red[w];
+    return s;
+}
+
+__global__ void __launch_bounds__(CT) compact_count(const uint8_t *__restrict__ recv, int64_t n, int64_t emax,
+                                                    int64_t slot_bytes, int32_t *__restrict__ counts,
+                                                    const int64_t *__restrict__ n_completed,
+                                                    int64_t *__restrict__ base) {
+    __shared__ int red[CT / 64];
+    const int64_t i0 = (int64_t)blockIdx.x * CCH + (int64_t)threadIdx.x * CPT;
+    int c = 0;
+#pragma unroll
+    for (int u = 0; u < CPT; ++u)
+        if (i0 + u < n) c += (int)done_at(recv, i0 + u, emax, slot_bytes);
+    c = block_sum_int(c, red);
+    if (threadIdx.x == 0) {
+        counts[blockIdx.x] = c;
+        if (blockIdx.x == 0) base[0] = n_completed[0];  // snapshot: pass 2 updates n_completed
+    }
+}
+
+__global__ void __launch_bounds__(CT) compact_scatter(const uint8_t *__restrict__ recv, int64_t n, int64_t emax,
+                                                      int64_t slot_bytes, const int32_t *__restrict__ counts,
+                                                      int32_t nchunks, const int64_t *__restrict__ base,
+                                                      double *__restrict__ scores, int64_t capacity,
+                                                      int64_t *__restrict__ n_completed) {
+    __shared__ int red[CT / 64];
+    __shared__ int wsum[CT / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    // prefix of this chunk and the window's total
+    int pre = 0, tot = 0;
+    for (int b = tid; b < nchunks; b += CT) {
+        const int c = counts[b];
+        tot += c;
+        if (b < (int)blockIdx.x) pre += c;
+    }
+    pre = block_sum_int(pre, red);
+    tot = block_sum_int(tot, red);
+    const int64_t n0 = base[0];
+    if (blockIdx.x == 0 && tid == 0) n_completed[0] = n0 + tot;
+    // this thread's flags and its exclusive rank inside the chunk
+    const int64_t i0 = (int64_t)blockIdx.x * CCH + (int64_t)tid * CPT;
+    uint32_t bits = 0;
+#pragma unroll
+    for (int u = 0; u < CPT; ++u)
+        if (i0 + u < n) bits |= done_at(recv, i0 + u, emax, slot_bytes) << u;
+    const int mine = __popc(bits);
+    int incl = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    int woff = 0;
+#pragma unroll
+    for (int w = 0; w < CT / 64; ++w) woff += (w < wv) ? wsum[w] : 0;
+    int64_t pos = (int64_t)pre + woff + incl - mine;  // completions before this thread's first
+    // kept: the last `capacity` completions of the window (older ones would be overwritten)
+    const int64_t first_kept = (int64_t)tot - capacity;
+    while (bits) {
+        const int u = __ffs(bits) - 1;
+        bits &= bits - 1;
+        if (pos >= first_kept) {
+            const int64_t i = i0 + u, slot = i / emax, e = i - slot * emax;
+            const double r = reinterpret_cast<const double *>(recv + slot * slot_bytes)[e];
+            scores[(n0 + pos) % capacity] = r;
+        }
+        ++pos;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -66,6 +161,41 @@ gw_status gw_rollout_tick(const double *partials, int64_t rows, int32_t n_fields
         return GW_ERR_HIP;
     }
     return GW_OK;
+}
+
+gw_status gw_return_compact(const uint8_t *recv, int64_t steps, int32_t world, int64_t emax, int64_t slot_bytes,
+                            double *scores, int64_t capacity, int64_t *n_completed, int32_t *scratch,
+                            void *stream) {
+    if (steps < 0 || world < 1 || emax < 1 || slot_bytes < 9 * emax || slot_bytes % 8 || capacity < 1 ||
+        !scores || !n_completed || !scratch || (steps > 0 && !recv)) {
+        gw_set_last_error("gw_return_compact: bad argument");
+        return GW_ERR_ARG;
+    }
+    const int64_t n = steps * world * emax;
+    if (n == 0) return GW_OK;
+    const int64_t nchunks = (n + CCH - 1) / CCH;
+    if (nchunks > (int64_t)1 << 30) {
+        gw_set_last_error("gw_return_compact: window too large");
+        return GW_ERR_ARG;
+    }
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int64_t *base = reinterpret_cast<int64_t *>(scratch);  // scratch: [2] i32 (base), then counts
+    int32_t *counts = scratch + 2;
+    hipLaunchKernelGGL(compact_count, dim3((unsigned)nchunks), dim3(CT), 0, s, recv, n, emax, slot_bytes, counts,
+                       n_completed, base);
+    hipLaunchKernelGGL(compact_scatter, dim3((unsigned)nchunks), dim3(CT), 0, s, recv, n, emax, slot_bytes, counts,
+                       (int32_t)nchunks, base, scores, capacity, n_completed);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        gw_set_last_error((std::string("gw_return_compact: ") + hipGetErrorString(e)).c_str());
+        return GW_ERR_HIP;
+    }
+    return GW_OK;
+}
+
+int64_t gw_return_compact_scratch(int64_t steps, int32_t world, int64_t emax) {
+    const int64_t n = steps * (int64_t)world * emax;
+    return 2 + (n + CCH - 1) / CCH;
 }
 
 }  // extern "C"

@@ -198,6 +198,29 @@ class ReturnGather:
             if w is not None:
                 w.wait()
         self._work = [None, None]
+        if self._recv.is_cuda:
+            self._compact_hip()
+            return
+        self._compact_torch()
+
+    def _compact_hip(self):
+        """gw_return_compact (include/rollout_ops.h): count + scatter, two launches."""
+        import ctypes as C
+        from . import _lib
+        lib = _lib.load()
+        need = int(lib.gw_return_compact_scratch(self._fill, self.world, self.emax))
+        if getattr(self, "_scratch", None) is None or self._scratch.numel() < need:
+            self._scratch = torch.zeros(max(need, 2 + (self.window * self.world * self.emax + 4095) // 4096),
+                                        dtype=torch.int32, device=self.device)
+        _lib.check(lib.gw_return_compact(self._recv.data_ptr(), self._fill, self.world, self.emax, self.slot_bytes,
+                                         self.scores.data_ptr(), self.capacity, self.n_completed.data_ptr(),
+                                         self._scratch.data_ptr(),
+                                         C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)),
+                   "gw_return_compact")
+        self._fill = 0
+
+    def _compact_torch(self):
+        """The same compaction as torch ops (CPU tensors: the gloo tests; the GPU test's reference)."""
         block = self._recv[: self._fill]                               # [T, world, slot]
         rets = block.view(torch.float64)[:, :, : self.emax]            # [T, world, E_max] (slot_bytes % 8 == 0)
         done = block[:, :, 8 * self.emax: 9 * self.emax] != 0

@@ -128,7 +128,9 @@ class VecGridEnv:
         self._closed = False
         self.obs_async = False
         self.fear_async = False
-        self.fused = (sc.HW % 4 == 0) and os.environ.get("GW_KERNEL", "split") == "fused"
+        # the kernel path gw_create picked (GW_KERNEL, or by batch size: gw_kernel_path)
+        self.kernel_path = ("v1", "split", "fused", "defer", "merged")[int(self.lib.gw_kernel_path(self.handle))]
+        self.fused = self.kernel_path == "fused"
 
     # ------------------------------------------------------------------------------------
     def _stream(self):
@@ -188,6 +190,33 @@ class VecGridEnv:
             _lib.check(self.lib.gw_step(self.handle, _ptr(rl), _ptr(sa), _ptr(sp), C.byref(so),
                                         self._stream()), "gw_step")
         return StepResult(**res)
+
+    def capture_steps(self, n: int, gather=None) -> torch.cuda.CUDAGraph:
+        """Capture ``n`` consecutive ``step()`` calls (device RNG policies, no host inputs) into
+        one HIP graph; each ``replay()`` then advances every env by n steps with a single launch
+        from the host.  For the small-E regime, where a step is bound by its launch chain
+        (C2: 4,096 envs), not by the GPU.  Nothing runs at capture time: the env's state is
+        untouched until the first replay.
+
+        gather: a parallel.ReturnGather with ``window == n`` and no steps pending (one rank):
+        each captured step writes its returns into the gather's next slot and the window is
+        compacted at the end of the graph, so every replay leaves the gather as it found it.
+        HIP timing events cannot be recorded in a graph: profiling is switched off for the capture.
+        Synchronous obs only (the async pipeline's cross-step events do not fit a closed graph)."""
+        if self.obs_async:
+            raise _lib.GwError("capture_steps: synchronous obs only (set_obs_async(False))")
+        if gather is not None and (gather.window != n or gather._fill != 0 or gather.distributed):
+            raise _lib.GwError("capture_steps: the gather needs window == n, no pending steps and one rank")
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.device(self.device):
+            torch.cuda.synchronize(self.device)
+            with torch.cuda.graph(g):
+                self.profile(False)
+                for i in range(n):
+                    self.step(into=gather.into() if gather is not None else None)
+                    if gather is not None:
+                        gather.push()
+        return g
 
     def _as_i32(self, t, shape):
         if t is None:

@@ -22,7 +22,11 @@ OUTS = ("reward", "fear", "shaped", "term", "trunc", "done", "mask", "ep_return"
     ("split", True, "grid32", True, 4096), ("defer", True, "grid64_n8", True, 1024),
     ("defer", True, "grid32", "lazy", 4096), ("split", False, "grid32", "lazy", 4096),
     ("defer", True, "level3", True, 1), ("defer", True, "level3", "lazy", 333),   # ragged env counts
-    ("fused", True, "grid32", True, 515), ("v1", True, "grid32", True, 257)])      # non-pipelining paths
+    ("fused", True, "grid32", True, 515), ("v1", True, "grid32", True, 257),       # non-pipelining paths
+    # merged: one step_obs launch per step (step t + the obs writer of step t-1), one stream
+    ("merged", True, "grid32", True, 4096), ("merged", False, "grid32", True, 4099),
+    ("merged", True, "grid64_n8", "lazy", 1024), ("merged", True, "level3", True, 1),
+    ("merged", False, "level3", True, 333)])
 def test_async_obs_matches_sync(path, fear, name, mode, E, monkeypatch):
     monkeypatch.setenv("GW_KERNEL", path)
     monkeypatch.setenv("GW_CHUNKS", "1")
@@ -80,10 +84,13 @@ def test_async_obs_matches_sync(path, fear, name, mode, E, monkeypatch):
     b.close()
 
 
-@pytest.mark.parametrize("mode,fear_async", [(True, False), ("lazy", False), ("lazy", True), (True, True)])
-def test_async_rollout_fused_actor_matches_sync(mode, fear_async):
+@pytest.mark.parametrize("mode,fear_async,path", [(True, False, "defer"), ("lazy", False, "defer"),
+                                                  ("lazy", True, "defer"), (True, True, "defer"),
+                                                  ("lazy", False, "merged"), (True, True, "merged")])
+def test_async_rollout_fused_actor_matches_sync(mode, fear_async, path, monkeypatch):
     """Rollout(obs_async) with the fused actor (reads the alternating descriptors) == the
     synchronous rollout: same actions, probs, rewards and replay-ring contents."""
+    monkeypatch.setenv("GW_KERNEL", path)
     from marlnav.actor import MultiAgentActors
     from marlnav.rollout import Rollout
     sc = S.builtin("grid32")

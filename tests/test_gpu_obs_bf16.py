@@ -78,3 +78,34 @@ def test_bf16_rollout_matches_f32():
     assert ros[0].totals() == ros[1].totals()
     for e in envs:
         e.close()
+
+
+@pytest.mark.parametrize("path", ["merged", "defer"])
+def test_bf16_pipelined_ring_equals_f32(path, monkeypatch):
+    """bf16 obs through the step pipeline with no fence inside the loop (every step's obs into
+    its own ring slot; with GW_KERNEL=merged each step is one step_obs launch whose writer role
+    produces the previous step's bf16 obs) == the synchronous float32 env."""
+    monkeypatch.setenv("GW_KERNEL", path)
+    sc = S.builtin("grid32")
+    E, T = 3000, 24
+    a = VecGridEnv(sc, num_envs=E, fear=True, fear_weight=-5.0, seed=31, final_obs=True, max_steps=20)
+    b = VecGridEnv(sc, num_envs=E, fear=True, fear_weight=-5.0, seed=31, final_obs=True, max_steps=20,
+                   obs_dtype=torch.bfloat16)
+    b.set_obs_async(True)
+    ring = torch.empty((T, sc.K, E, sc.H, sc.W), dtype=torch.bfloat16, device="cuda")
+    fin = torch.full((T, sc.K, E, sc.H, sc.W), -3.0, dtype=torch.bfloat16, device="cuda")
+    ref = torch.empty((T, sc.K, E, sc.H, sc.W), dtype=torch.float32, device="cuda")
+    reff = torch.full((T, sc.K, E, sc.H, sc.W), -3.0, dtype=torch.float32, device="cuda")
+    a.reset()
+    b.reset()
+    bad = torch.zeros((), dtype=torch.int64, device="cuda")
+    for t in range(T):
+        r1 = a.step(obs_out=ref[t], final_obs_out=reff[t])
+        r2 = b.step(obs_out=ring[t], final_obs_out=fin[t])
+        bad += (r1.reward != r2.reward).sum() + (r1.done != r2.done).sum() + (r1.shaped != r2.shaped).sum()
+    b.obs_fence()
+    bad += (ref != ring.float()).sum() + (reff != fin.float()).sum()
+    torch.cuda.synchronize()
+    assert int(bad) == 0
+    a.close()
+    b.close()

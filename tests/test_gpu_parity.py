@@ -149,6 +149,7 @@ KERNEL_PATHS = {
     "defer_wide": {"GW_KERNEL": "defer", "GW_FEAR_BE": "wide"},  # fear_v2 with 2x envs per block
     "defer_chunks": {"GW_KERNEL": "defer", "GW_CHUNKS": "2"},  # 2 env chunks over 3 streams
     "v1": {"GW_KERNEL": "v1"},                                # the first kernels
+    "merged": {"GW_KERNEL": "merged"},                        # synchronous: as split1 (async: step_obs)
 }
 
 
