@@ -243,9 +243,12 @@ def main():
     # per-step RCCL all-gather of every env's completed-episode return + done flag (SURVEY §8e;
     # maddpg/agent.py:229-247): gw_step writes them straight into the send buffer
     graph_n = args.graph
-    if graph_n < 0:  # auto: the launch-chain-bound regime (synchronous obs, env only, one rank)
-        graph_n = 16 if (not cfg.get("rollout") and not obs_mode and world == 1) else 0
+    if graph_n < 0:  # auto: the host-bound regime (env only, one rank; synchronous obs or merged path)
+        graph_n = 16 if (not cfg.get("rollout") and world == 1 and
+                         (not obs_mode or env.kernel_path == "merged")) else 0
     graph_n = min(graph_n, args.steps)
+    if obs_mode and env.kernel_path == "merged":
+        graph_n -= graph_n % 2  # merged async: an even number of captured steps
     gather = None if args.no_gather else ReturnGather(world * E, rank, world, env.device,
                                                       **({"window": graph_n} if graph_n else {}))
 
@@ -302,8 +305,10 @@ def main():
     graph = None
     if graph_n:
         # the timed steps as HIP graphs of graph_n steps (captured here, before the timed region:
-        # nothing runs at capture), the remainder eagerly after them; the kernel spans are those
-        # of the last replay's sampled steps
+        # nothing runs at capture), the remainder eagerly after them
+        if env.obs_async and not env._obs_queued:  # merged async: capture after a queued writer
+            graph_n = 0
+    if graph_n:
         if gather is not None:
             gather.compact()  # the warmup's partial window
         graph = env.capture_steps(graph_n, gather)

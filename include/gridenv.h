@@ -164,6 +164,12 @@ int64_t gw_stats_rows(void *env);
  * pipelined step), else "defer".  -1 on a null handle. */
 int64_t gw_kernel_path(void *env);
 
+/* After replaying (on `stream`) a HIP graph of captured gw_step calls: the env's host-side
+ * pipeline state is again the one the capture ended in (merged path with async obs: the
+ * writer of the last captured step is queued, for the next gw_step or fence).  The capture
+ * itself leaves that state; a fence between replays clears it, this re-arms it. */
+gw_status gw_graph_replayed(void *env, void *stream);
+
 /* What the observation an env last wrote (gw_reset / gw_step) is made of, for ops that work
  * on it without reading it back (actor_ops.h): the static step-encoding map plus, per env, a
  * 48-byte descriptor (agent cells, reset / apple flags; ma_customenv.py:197-209, 303-322).

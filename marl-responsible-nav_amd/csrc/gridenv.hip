@@ -1993,6 +1993,9 @@ struct Env {
     // GW_EVENT_FENCE=system restores the plain events (A/B).
     unsigned sync_flags = hipEventDisableTiming | hipEventDisableSystemFence;
     unsigned prof_flags = hipEventDisableSystemFence;  // timing events of gw_profile
+    // obs_done / world_ev bound to the kernel launch they follow (hipExtLaunchKernelGGL stop
+    // event) instead of a marker packet after it; GW_BIND_EVENTS=0 records them (A/B)
+    bool bind_events = true;
 };
 
 // the second stream and n fork/join events (timing disabled), created on first use
@@ -2051,12 +2054,15 @@ gw_status ensure_obs_stream(Env *env) {
 // (hipExtLaunchKernelGGL start / stop events: the kernel's own begin / end timestamps, no
 // marker packets between the kernels of the pipeline).  The span's first launch takes the
 // start event, every launch the stop event (the last one's end wins).
-thread_local hipEvent_t t_span_start = nullptr, t_span_stop = nullptr;
+// t_bind_stop: a pipeline event (obs_done, world_ev) bound to the launch the same way, instead
+// of a marker packet recorded after it (used when no timing span is open).
+thread_local hipEvent_t t_span_start = nullptr, t_span_stop = nullptr, t_bind_stop = nullptr;
 
 template <typename F, typename... Args>
 void gw_launch(F kernel, dim3 grid, dim3 block, size_t lds, hipStream_t s, Args... args) {
-    if (t_span_stop) {
-        hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)lds, s, t_span_start, t_span_stop, 0u, args...);
+    hipEvent_t stop = t_span_stop ? t_span_stop : t_bind_stop;
+    if (stop) {
+        hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)lds, s, t_span_start, stop, 0u, args...);
         t_span_start = nullptr;
     } else {
         hipLaunchKernelGGL(kernel, grid, block, lds, s, args...);
@@ -2070,13 +2076,13 @@ gw_status prof_span_end(Env *env, size_t idx, int kind);
 
 // launch the queued obs_kernel on the obs stream, after its world update and (after != null)
 // after the caller's work up to `after`
-gw_status flush_obs(Env *env, hipEvent_t after) {
+gw_status flush_obs(Env *env, hipEvent_t after, hipStream_t on = nullptr) {
     if (!env->obs_queued) return GW_OK;
-    if (env->mode == 4) {  // merged: the last step's writer alone, on the stream of that step
+    if (env->mode == 4) {  // merged: the last step's writer alone, on `on` (default: that step's stream)
         const bool prof = env->qobs_prof;
         size_t b = 0;
         if (prof && prof_span_begin(env, b) != GW_OK) return GW_ERR_HIP;
-        HIP_TRY(launch_obs(env, env->qobs, env->qobs.out.obs, env->qobs.out.final_obs, env->last_stream));
+        HIP_TRY(launch_obs(env, env->qobs, env->qobs.out.obs, env->qobs.out.final_obs, on ? on : env->last_stream));
         if (prof) (void)prof_span_end(env, b, 1);
         env->obs_queued = false;
         return GW_OK;
@@ -2087,9 +2093,13 @@ gw_status flush_obs(Env *env, hipEvent_t after) {
     const bool prof = env->qobs_prof;  // timed iff the step that queued it was
     size_t b = 0;
     if (prof && prof_span_begin(env, b) != GW_OK) return GW_ERR_HIP;
-    HIP_TRY(launch_obs(env, env->qobs, env->qobs.out.obs, env->qobs.out.final_obs, os));
+    const bool bind = env->bind_events && !prof;  // obs_done carried by the writer's launch
+    if (bind) t_bind_stop = env->obs_done[env->qobs_buf];
+    const hipError_t le = launch_obs(env, env->qobs, env->qobs.out.obs, env->qobs.out.final_obs, os);
+    t_bind_stop = nullptr;
+    HIP_TRY(le);
     if (prof) (void)prof_span_end(env, b, 1);
-    HIP_TRY(hipEventRecord(env->obs_done[env->qobs_buf], os));
+    if (!bind) HIP_TRY(hipEventRecord(env->obs_done[env->qobs_buf], os));
     env->obs_pending[env->qobs_buf] = true;
     env->obs_queued = false;
     return GW_OK;
@@ -2109,13 +2119,18 @@ gw_status wait_obs(Env *env, hipStream_t s) {
         if (st != GW_OK) return st;
     }
     if (env->obs_queued) {
-        const bool merged = env->mode == 4;
-        const gw_status st = flush_obs(env, nullptr);
-        if (st != GW_OK) return st;
-        if (merged && env->last_stream != s) {  // the writer ran on the last step's stream
-            GW_TRY(ensure_events(env, 1));
-            HIP_TRY(hipEventRecord(env->sync_ev[0], env->last_stream));
-            HIP_TRY(hipStreamWaitEvent(s, env->sync_ev[0], 0));
+        if (env->mode == 4) {
+            // merged: the writer runs on s, after the step that queued it (a graph replay of
+            // captured steps runs on s itself; its capture stream holds no work)
+            if (env->last_stream != s) {
+                GW_TRY(ensure_events(env, 1));
+                HIP_TRY(hipEventRecord(env->sync_ev[0], env->last_stream));
+                HIP_TRY(hipStreamWaitEvent(s, env->sync_ev[0], 0));
+            }
+            GW_TRY(flush_obs(env, nullptr, s));
+        } else {
+            const gw_status st = flush_obs(env, nullptr);
+            if (st != GW_OK) return st;
         }
     }
     for (int i = 0; i < 2; ++i)
@@ -2582,6 +2597,8 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
         if (oc) env->obs_chunks = std::max(1, std::min(64, std::atoi(oc)));
         const char *ch = std::getenv("GW_CHUNKS");
         if (ch) env->chunks = std::max(1, std::min(16, std::atoi(ch)));
+        const char *bev = std::getenv("GW_BIND_EVENTS");
+        if (bev) env->bind_events = std::atoi(bev) != 0;
         const char *ef = std::getenv("GW_EVENT_FENCE");
         if (ef && std::strcmp(ef, "system") == 0) {
             env->sync_flags = hipEventDisableTiming;
@@ -2719,9 +2736,13 @@ gw_status gw_step(void *handle, const int32_t *rl_actions, const int32_t *script
         if (on_aux) HIP_TRY(hipStreamWaitEvent(ws, env->sync_ev[0], 0));
         if (env->obs_pending[nb]) HIP_TRY(hipStreamWaitEvent(ws, env->obs_done[nb], 0));
         GW_TRY(span_begin(ws, b));
-        HIP_TRY(dispatch_step(env, p, ws));
+        const bool bind = env->bind_events && !env->profiling;  // world_ev carried by the launch
+        if (bind) t_bind_stop = env->world_ev;
+        const hipError_t se = dispatch_step(env, p, ws);
+        t_bind_stop = nullptr;
+        HIP_TRY(se);
         GW_TRY(span_end(ws, b, 0));
-        HIP_TRY(hipEventRecord(env->world_ev, ws));
+        if (!bind) HIP_TRY(hipEventRecord(env->world_ev, ws));
         if (defer && env->fear_async) {
             // s joins the world update only: the caller's next work (the actor reads the
             // descriptors and masks) overlaps fear_v2; FeAR-owned outputs wait for gw_fear_fence
@@ -3047,6 +3068,17 @@ gw_status gw_obs_view(void *handle, gw_obs_source *out) {
 }
 
 void gw_set_last_error(const char *msg) { g_err = msg ? msg : ""; }
+
+gw_status gw_graph_replayed(void *handle, void *stream) {
+    Env *env = static_cast<Env *>(handle);
+    if (!env) return fail(GW_ERR_ARG, "null env");
+    if (env->mode == 4 && env->obs_async && env->qobs.desc) {
+        env->obs_queued = true;  // qobs: the last captured step's writer
+        env->qobs_prof = false;
+        env->last_stream = static_cast<hipStream_t>(stream);
+    }
+    return GW_OK;
+}
 
 int64_t gw_kernel_path(void *handle) {
     const Env *env = static_cast<const Env *>(handle);

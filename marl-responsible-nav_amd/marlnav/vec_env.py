@@ -52,6 +52,18 @@ class StepResult:
     stats: torch.Tensor | None = None   # [rows, 8] per-block partial sums (_lib.STATS_NAMES)
 
 
+class StepGraph:
+    """n captured VecGridEnv.step calls (VecGridEnv.capture_steps); replay() advances every env by
+    n steps with one graph launch on the current stream."""
+
+    def __init__(self, env, graph: torch.cuda.CUDAGraph):
+        self.env, self.graph = env, graph
+
+    def replay(self):
+        self.graph.replay()
+        self.env._replayed()
+
+
 def _ptr(t: torch.Tensor | None):
     if t is None:
         return None
@@ -126,6 +138,7 @@ class VecGridEnv:
         )
         self._step_out = _lib.GwStepOut(*[_ptr(self.out[n]) for n in _lib.STEP_OUT_FIELDS])
         self._closed = False
+        self._obs_queued = False  # async obs: the last step's writer not yet launched / fenced
         self.obs_async = False
         self.fear_async = False
         # the kernel path gw_create picked (GW_KERNEL, or by batch size: gw_kernel_path)
@@ -145,6 +158,7 @@ class VecGridEnv:
         with torch.cuda.device(self.device):
             _lib.check(self.lib.gw_reset(self.handle, _ptr(env_mask), _ptr(spawn), _ptr(self.out["obs"]),
                                          _ptr(self.out["mask"]), self._stream()), "gw_reset")
+        self._obs_queued = False
         return self.out["obs"], self.out["mask"]
 
     _INTO_SPEC = {"obs": (torch.float32, "KEHW"), "final_obs": (torch.float32, "KEHW"),
@@ -189,9 +203,10 @@ class VecGridEnv:
         with torch.cuda.device(self.device):
             _lib.check(self.lib.gw_step(self.handle, _ptr(rl), _ptr(sa), _ptr(sp), C.byref(so),
                                         self._stream()), "gw_step")
+        self._obs_queued = self.obs_async and (res["obs"] is not None or res["final_obs"] is not None)
         return StepResult(**res)
 
-    def capture_steps(self, n: int, gather=None) -> torch.cuda.CUDAGraph:
+    def capture_steps(self, n: int, gather=None) -> "StepGraph":
         """Capture ``n`` consecutive ``step()`` calls (device RNG policies, no host inputs) into
         one HIP graph; each ``replay()`` then advances every env by n steps with a single launch
         from the host.  For the small-E regime, where a step is bound by its launch chain
@@ -202,9 +217,19 @@ class VecGridEnv:
         each captured step writes its returns into the gather's next slot and the window is
         compacted at the end of the graph, so every replay leaves the gather as it found it.
         HIP timing events cannot be recorded in a graph: profiling is switched off for the capture.
-        Synchronous obs only (the async pipeline's cross-step events do not fit a closed graph)."""
+
+        Synchronous obs, or async obs on the merged kernel path: there every step is ONE
+        step_obs launch (step t + the obs writer of step t-1, no events), so a capture of an EVEN
+        number of steps that starts with the previous step's writer queued (at least one step
+        since the last reset / fence, writing the same obs buffers as the captured steps) ends
+        in the state it started from, and replays chain.  The defer path's async pipeline
+        (cross-queue events between steps) cannot be captured."""
         if self.obs_async:
-            raise _lib.GwError("capture_steps: synchronous obs only (set_obs_async(False))")
+            if self.kernel_path != "merged":
+                raise _lib.GwError("capture_steps: synchronous obs, or async obs on the merged path only")
+            if n % 2 or not self._obs_queued:
+                raise _lib.GwError("capture_steps (merged async obs): an even n, after a step (the previous "
+                                   "step's obs writer queued)")
         if gather is not None and (gather.window != n or gather._fill != 0 or gather.distributed):
             raise _lib.GwError("capture_steps: the gather needs window == n, no pending steps and one rank")
         g = torch.cuda.CUDAGraph()
@@ -216,7 +241,13 @@ class VecGridEnv:
                     self.step(into=gather.into() if gather is not None else None)
                     if gather is not None:
                         gather.push()
-        return g
+        return StepGraph(self, g)
+
+    def _replayed(self):
+        """Host-side pipeline state after a StepGraph replay (gw_graph_replayed)."""
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.gw_graph_replayed(self.handle, self._stream()), "gw_graph_replayed")
+        self._obs_queued = self.obs_async
 
     def _as_i32(self, t, shape):
         if t is None:
@@ -290,6 +321,8 @@ class VecGridEnv:
         if mode and fear_async:
             mode |= 4
         _lib.check(self.lib.gw_set_obs_async(self.handle, mode), "gw_set_obs_async")
+        if not mode:
+            self._obs_queued = False
         self.obs_async = bool(mode)
         self.fear_async = bool(mode & 4)
 
@@ -299,6 +332,7 @@ class VecGridEnv:
         if self.obs_async:
             with torch.cuda.device(self.device):
                 _lib.check(self.lib.gw_obs_fence(self.handle, self._stream()), "gw_obs_fence")
+            self._obs_queued = False
 
     def fear_fence(self):
         """Order the last step's FeAR-owned outputs before later work on the current stream."""

@@ -19,12 +19,19 @@ OUTS = ("obs", "reward", "fear", "shaped", "term", "trunc", "done", "mask", "cra
         "ep_fear", "ep_len", "stats")
 
 
-@pytest.mark.parametrize("scenario,E,fear,n", [("grid32", 1000, False, 8), ("grid32", 777, True, 6),
-                                               ("grid64_n8", 300, True, 4), ("level3", 1, False, 16)])
-def test_graph_replay_equals_eager(scenario, E, fear, n):
+@pytest.mark.parametrize("scenario,E,fear,n,path,async_obs", [
+    ("grid32", 1000, False, 8, "defer", False), ("grid32", 777, True, 6, "defer", False),
+    ("grid64_n8", 300, True, 4, "defer", False), ("level3", 1, False, 16, "defer", False),
+    # merged async: each captured step is one step_obs launch (step t + the writer of step t-1)
+    ("grid32", 4096, False, 8, "merged", True), ("grid32", 999, True, 6, "merged", True),
+    ("grid64_n8", 200, True, 4, "merged", True)])
+def test_graph_replay_equals_eager(scenario, E, fear, n, path, async_obs, monkeypatch):
+    monkeypatch.setenv("GW_KERNEL", path)
     envs, gathers = [], []
-    for _ in range(2):
+    for i in range(2):
         env = VecGridEnv(scenario, num_envs=E, fear=fear, fear_weight=-5.0, max_steps=12, seed=5, stats=True)
+        if async_obs and i == 1:
+            env.set_obs_async(True)
         env.reset()
         envs.append(env)
         gathers.append(ReturnGather(E, 0, 1, env.device, window=n))
@@ -42,6 +49,7 @@ def test_graph_replay_equals_eager(scenario, E, fear, n):
             eager.step(into=gathers[0].into())
             gathers[0].push()
         graph.replay()
+        graphed.obs_fence()  # async: the last captured step's writer
         torch.cuda.synchronize()
         for name in OUTS:
             a, b = eager.out[name], graphed.out[name]
@@ -58,10 +66,24 @@ def test_graph_replay_equals_eager(scenario, E, fear, n):
         env.close()
 
 
-def test_capture_rejects_async_obs():
+def test_capture_rejects_async_obs_off_the_merged_path(monkeypatch):
+    monkeypatch.setenv("GW_KERNEL", "defer")
     env = VecGridEnv("grid32", num_envs=64, fear=False, seed=1)
     env.set_obs_async(True)
     env.reset()
     with pytest.raises(Exception, match="synchronous obs"):
         env.capture_steps(4)
+    env.close()
+
+
+def test_merged_capture_needs_even_steps_after_a_step(monkeypatch):
+    monkeypatch.setenv("GW_KERNEL", "merged")
+    env = VecGridEnv("grid32", num_envs=64, fear=False, seed=1)
+    env.set_obs_async(True)
+    env.reset()
+    with pytest.raises(Exception, match="even n"):
+        env.capture_steps(4)  # no step since the reset: no writer queued
+    env.step()
+    with pytest.raises(Exception, match="even n"):
+        env.capture_steps(3)
     env.close()
