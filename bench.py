@@ -48,6 +48,10 @@ CONFIGS = {
                workload="BASELINE config 5 per GPU: 32x32, N=4, K=2, 65536 envs/GPU, FeAR on, full rollout "
                         "(stacked MLP actors + GumbelSoftmax + mask + argmax, env step, zero-copy replay ring of "
                         "MEMORY_SIZE 200000, per-step RCCL reduction of the episode statistics)"),
+    "c5patch": dict(scenario="grid32", envs=65536, fear=True, fear_weight=-5.0, rollout=True, patch=11,
+                    workload="C5's rollout with egocentric 11x11 local observations (gw_obs_patch; not a "
+                             "reference format, reported separately): no dense obs, stacked MLP actors (121 "
+                             "inputs, PyTorch), patch replay ring, FeAR on"),
     "c4cnn": dict(scenario="grid64_n8", envs=65536, fear=False, fear_weight=-5.0, rollout=True, arch="cnn",
                   workload="BASELINE config 4 as a rollout: 8-agent 64x64 grid, 65536 envs, the configs/cnn.yaml "
                            "actor head (conv 32-64, k2 s2, 128-128, f32; fused gw_cnn_act from the obs "
@@ -209,6 +213,8 @@ def main():
     # otherwise lose CUs to it) for the full rollout.  Measured A/B: profiles/r1_async/
     obs_mode = False if args.sync_obs else \
         ("lazy" if (args.obs_lazy or (cfg.get("rollout") and not args.obs_eager)) else True)
+    if cfg.get("patch"):  # no dense obs: nothing to pipeline
+        obs_mode = False
     if cfg.get("arch") == "cnn" and not (args.cnn_torch or args.obs_lazy or args.sync_obs):
         # the 2.1 GB writer starts right after the world update, as 4 launches so that the next
         # actor's kernels are dispatched between them (profiles/r2_cnn: 0.715 ms per step lazy in
@@ -223,6 +229,7 @@ def main():
     E = cfg["envs"]
     env = VecGridEnv(cfg["scenario"], num_envs=E, fear=cfg["fear"], fear_weight=cfg["fear_weight"],
                      max_steps=150, auto_reset=True, seed=42, env_offset=rank * E, stats=True,
+                     obs=not cfg.get("patch"),
                      obs_dtype=torch.bfloat16 if args.obs_dtype == "bf16" else torch.float32)
     N, K, HW = env.N, env.K, env.H * env.W
     # the defer path's small batches (below 128 MB of obs per step) run synchronous obs: its
@@ -265,7 +272,11 @@ def main():
     if cfg.get("rollout"):  # c5: actor -> env -> replay (+ optional MADDPG updates) per step
         from marlnav.maddpg import MADDPG
         from marlnav.rollout import Rollout
-        if cfg.get("arch") == "cnn":  # configs/cnn.yaml head: fused gw_cnn_act (or PyTorch, A/B)
+        if cfg.get("patch"):  # local observations: PyTorch MLP actors on the P x P windows
+            from marlnav.actor import MultiAgentActors
+            learner = None
+            actors = MultiAgentActors(K, cfg["patch"], cfg["patch"], "mlp", device=env.device, seed=rank)
+        elif cfg.get("arch") == "cnn":  # configs/cnn.yaml head: fused gw_cnn_act (or PyTorch, A/B)
             from marlnav.actor import MultiAgentActors
             learner = None
             actors = MultiAgentActors(K, env.H, env.W, arch="cnn", device=env.device, seed=rank)
@@ -276,7 +287,8 @@ def main():
             actors = learner.actors
         ro = Rollout(env, actors, replay_slots=-(-200_000 // E) + 1, training=True, seed=rank,
                      fused=False if args.cnn_torch else None,
-                     obs_async=obs_mode, fear_async=bool(obs_mode) and args.fear_async, gather=gather)
+                     obs_async=obs_mode, fear_async=bool(obs_mode) and args.fear_async, gather=gather,
+                     patch=cfg.get("patch", 0))
         ro.reset()
 
         def one_step(i):  # noqa: F811
@@ -359,7 +371,8 @@ def main():
                     "mean_return_last_100": float(gather.completed(last=100).mean()) if int(gather.n_completed) else None}
 
     if rank == 0:
-        step_b, obs_b = algorithmic_bytes(N, K, HW, 2 if args.obs_dtype == "bf16" else 4)
+        step_b, obs_b = algorithmic_bytes(N, K, cfg["patch"] ** 2 if cfg.get("patch") else HW,
+                                          2 if args.obs_dtype == "bf16" else 4)
         avg_step_ms, avg_obs_ms = ms_step / max(nprof, 1), ms_obs / max(nprof, 1)
         avg_fear_ms = ms_fear / max(nprof, 1)
         fused = env.fused

@@ -185,6 +185,15 @@ typedef struct gw_obs_source {
 } gw_obs_source;
 gw_status gw_obs_view(void *env, gw_obs_source *out);
 
+/* Egocentric local patches of the env's last observation (an opt-in input format; the
+ * reference observes the whole grid, ma_customenv.py:303-322): for every env and RL agent k the
+ * P x P window of that agent's obs centred on its own cell (rows / cols -P/2 .. P-1-P/2), cells
+ * outside the grid -1.  patch [K][E][P][P] f32 (envs whose obs the last gw_step / gw_reset
+ * wrote), final_patch [K][E][P][P] (the terminal obs of envs done at the last step, centred on
+ * the terminal cell); either may be NULL.  Works from the descriptors, so it needs no full obs
+ * (gw_step_out.obs may be NULL).  Enqueued on stream, after the step on the same stream. */
+gw_status gw_obs_patch(void *env, int32_t P, float *patch, float *final_patch, void *stream);
+
 /* Async observation writes (a software pipeline across steps; default off).  While enabled,
  * gw_step enqueues the world update (+ FeAR) on an internal stream that waits for the caller's
  * prior work on `stream`, and `stream` joins it: rewards, dones, masks, state and stats are

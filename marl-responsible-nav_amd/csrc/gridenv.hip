@@ -720,7 +720,9 @@ __device__ __forceinline__ void finish_env(const Params &p, int64_t e, const Env
             oi.fpos[n] = fin[n];
             oi.pos[n] = np_[n];
         }
-        oi.flags = D_RESET | D_WRITE | (o.final_obs ? D_FINAL : 0u) | (all_bits(K) << 8) | (apples << 16);
+        // the terminal descriptor is kept for every done env (writers skip it without a
+        // final_obs buffer; gw_obs_patch's terminal windows need no dense obs)
+        oi.flags = D_RESET | D_WRITE | D_FINAL | (all_bits(K) << 8) | (apples << 16);
 #pragma unroll
         for (int k = 0; k < N; ++k)
             if (k < K && o.mask) o.mask[e * K + k] = ctab ? (uint16_t)((ctab[np_[k]] >> 12) & 0x1FFu) : p.tb.amask[np_[k]];
@@ -1659,6 +1661,87 @@ __global__ void __launch_bounds__(128) step_v2(Params p) {
     __shared__ V2Shared<N, KMAX, FEAR, OBS> sh;
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
     step_v2_block<N, KMAX, FEAR, OBS, DEFER>(p, blockIdx.x, sh, dyn);
+}
+
+// ---------------------------------------------------------------------------------------
+// patch_kernel (gw_obs_patch): egocentric P x P windows of the env's last observation, centred
+// on each RL agent's cell (row / col offsets -P/2 .. P-1-P/2), cells outside the grid -1 (the
+// map's inactive value).  The same encoding as obs_block (static map + the N + 1 patched
+// cells of the descriptor), so window == a crop of the full obs padded with -1.  Layout
+// [K][E][P*P] (agent-major like the full obs); which = 0 the step's obs (D_WRITE envs), 1 the
+// terminal obs (D_FINAL envs, centred on the terminal cell).  Not a reference feature (the
+// reference observes the whole grid, custom/ma_customenv.py:303-322): an opt-in input format.
+// ---------------------------------------------------------------------------------------
+constexpr int PATCH_THREADS = 256;
+
+__global__ void __launch_bounds__(PATCH_THREADS) patch_kernel(Params p, int P, float *__restrict__ patch,
+                                                              float *__restrict__ final_patch) {
+    extern __shared__ uint32_t plds[];
+    const int tid = threadIdx.x;
+    const int HW = p.HW, W = p.W, H = p.H, N = p.N, K = p.K, be = p.obs_be;
+    const int npatch = N + 1, nroad = (HW + 31) / 32;
+    uint32_t *s_road = plds;
+    uint32_t *s_flag = s_road + nroad;                                   // [be]
+    int *s_ctr = reinterpret_cast<int *>(s_flag + be);                   // [2][be][K]
+    int *s_pc = s_ctr + 2 * be * K;                                      // [2][be][K][npatch]
+    float *s_pv = reinterpret_cast<float *>(s_pc + 2 * be * K * npatch);
+    const int64_t e0 = (int64_t)blockIdx.x * be;
+    if (e0 >= p.E) return;  // uniform per block
+    const int nenv = (int)min((int64_t)be, p.E - e0);
+    for (int w = tid; w < nroad; w += PATCH_THREADS) s_road[w] = p.tb.roadbits[w];
+    for (int u = tid; u < 2 * be * K; u += PATCH_THREADS) {  // one thread per (which, env, k)
+        const int which = u / (be * K), el = (u / K) % be, k = u % K;
+        const int slot = (which * be + el) * K + k;
+        if (el >= nenv) continue;
+        const uint32_t *d = p.desc + (e0 + el) * NDESC;
+        const uint32_t f = d[4];
+        if (k == 0 && which == 0) s_flag[el] = f;
+        const bool reset = (which == 0) && (f & D_RESET);
+        const uint32_t apples = which == 0 ? (f >> 8) & 0xFFu : (f >> 16) & 0xFFu;
+        const uint32_t *pw = d + (which == 0 ? 0 : 8);
+        const int ac = ((apples >> k) & 1u) ? p.apples[k] : -1;
+        int np = 0;
+        if (ac >= 0) {
+            float av = p.tb.base[ac] + 9.0f;
+            if (!reset && av == (float)(k + 1)) av = 1.0f;
+            s_pc[slot * npatch + np] = ac;
+            s_pv[slot * npatch + np] = av;
+            ++np;
+        }
+        for (int n = 0; n < N; ++n) {
+            const int c = (int)((pw[n >> 1] >> (16 * (n & 1))) & 0xFFFFu);
+            if (n == k) s_ctr[slot] = c;
+            s_pc[slot * npatch + np] = c;
+            s_pv[slot * npatch + np] = agent_value(reset, n, k, c == ac, p.variant);
+            ++np;
+        }
+        for (; np < npatch; ++np) s_pc[slot * npatch + np] = -1;
+    }
+    __syncthreads();
+    const int PP = P * P, half = P / 2;
+    for (int which = 0; which < 2; ++which) {
+        float *dst = which == 0 ? patch : final_patch;
+        if (!dst) continue;
+        const uint32_t need = which == 0 ? D_WRITE : D_FINAL;
+        for (int k = 0; k < K; ++k) {
+            float *o = dst + ((int64_t)k * p.E + e0) * PP;
+            for (int i = tid; i < nenv * PP; i += PATCH_THREADS) {
+                const int el = i / PP, c = i - el * PP;
+                if (!(s_flag[el] & need)) continue;
+                const int slot = (which * be + el) * K + k;
+                const int ctr = s_ctr[slot];
+                const int r = ctr / W + c / P - half, q = ctr % W + c % P - half;
+                float v = -1.0f;
+                if (r >= 0 && r < H && q >= 0 && q < W) {
+                    const int cell = r * W + q;
+                    v = ((s_road[cell >> 5] >> (cell & 31)) & 1u) ? 0.0f : -1.0f;
+                    for (int u = 0; u < npatch; ++u)  // later patches override earlier ones
+                        if (s_pc[slot * npatch + u] == cell) v = s_pv[slot * npatch + u];
+                }
+                o[i] = v;
+            }
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -3053,6 +3136,24 @@ gw_status gw_fear_matrix(void *handle, int64_t n, const int32_t *cells, const in
         case 8: e = launch_fear_matrix<8>(env, n, q, s); break;
     }
     HIP_TRY(e);
+    return GW_OK;
+}
+
+gw_status gw_obs_patch(void *handle, int32_t P, float *patch, float *final_patch, void *stream) {
+    Env *env = static_cast<Env *>(handle);
+    if (!env) return fail(GW_ERR_ARG, "null env");
+    if (P < 1 || P > 129) return fail(GW_ERR_ARG, "gw_obs_patch: need 1 <= P <= 129");
+    if (!patch && !final_patch) return GW_OK;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    GW_TRY(wait_fear(env, s));  // async FeAR: the descriptors are written by the world update (joined)
+    gw::Params p = make_params(env);
+    const int be = std::max(1, std::min(gw::OBS_BE, 8192 / std::max(1, env->K * P * P)));
+    p.obs_be = be;
+    const size_t lds = sizeof(uint32_t) * ((env->HW + 31) / 32 + be) +
+                       sizeof(int) * 2 * be * env->K + (size_t)2 * 2 * be * env->K * (env->N + 1) * sizeof(uint32_t);
+    const unsigned grid = (unsigned)((env->E + be - 1) / be);
+    hipLaunchKernelGGL(gw::patch_kernel, dim3(grid), dim3(gw::PATCH_THREADS), lds, s, p, (int)P, patch, final_patch);
+    HIP_TRY(hipGetLastError());
     return GW_OK;
 }
 

@@ -167,7 +167,7 @@ EXPORTS = ["gw_create", "gw_reset", "gw_step", "gw_state_view", "gw_copy_state",
            "gw_adam_step", "gw_soft_update", "gw_obs_view", "gw_set_last_error", "gw_actor_act",
            "gw_actor_workspace_floats", "gw_actor_prepare", "gw_rollout_tick", "gw_set_obs_async",
            "gw_obs_fence", "gw_fear_fence", "gw_set_obs_dtype", "gw_cnn_workspace_floats", "gw_cnn_prepare",
-           "gw_cnn_act", "gw_return_compact", "gw_return_compact_scratch", "gw_kernel_path", "gw_graph_replayed"]
+           "gw_cnn_act", "gw_return_compact", "gw_return_compact_scratch", "gw_kernel_path", "gw_graph_replayed", "gw_obs_patch"]
 
 
 class GwObsSource(C.Structure):
@@ -215,6 +215,8 @@ def _declare(L):
     L.gw_profile.restype = C.c_int
     L.gw_profile_read.argtypes = [p, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
     L.gw_profile_read.restype = C.c_int
+    L.gw_obs_patch.argtypes = [p, C.c_int32, p, p, p]
+    L.gw_obs_patch.restype = C.c_int
     L.gw_graph_replayed.argtypes = [p, p]
     L.gw_graph_replayed.restype = C.c_int
     L.gw_kernel_path.argtypes = [p]

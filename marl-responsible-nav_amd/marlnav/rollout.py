@@ -27,10 +27,14 @@ from .vec_env import VecGridEnv
 class ReplayRing:
     """S steps of E transitions each, in HBM.  obs slots are written by the env directly."""
 
-    def __init__(self, env: VecGridEnv, slots: int):
+    def __init__(self, env: VecGridEnv, slots: int, patch: int = 0):
+        """patch > 0: the ring holds the agents' egocentric patch x patch observations
+        (VecGridEnv.obs_patch) instead of the full grids."""
         self.S = max(2, int(slots))
         K, E, H, W, dev = env.K, env.E, env.H, env.W, env.device
-        od = env.obs_dtype  # bf16 obs (lossless) halves the ring; sample() hands out float32
+        if patch:
+            H = W = int(patch)
+        od = env.obs_dtype if not patch else torch.float32  # bf16 obs (lossless) halves the ring
         self.obs = torch.zeros((self.S, K, E, H, W), dtype=od, device=dev)
         self.final_obs = torch.zeros((self.S, K, E, H, W), dtype=od, device=dev)
         self.probs = torch.zeros((self.S, K, E, 9), dtype=torch.float32, device=dev)
@@ -68,7 +72,7 @@ class ReplayRing:
 class Rollout:
     def __init__(self, env: VecGridEnv, actors: MultiAgentActors | None = None, replay_slots: int = 0,
                  training: bool = True, group=None, seed: int = 0, fused: bool | None = None,
-                 obs_async: bool | str = False, fear_async: bool = False, gather=None):
+                 obs_async: bool | str = False, fear_async: bool = False, gather=None, patch: int = 0):
         """fused: get_action as the one-kernel gw_actor_act over the env's obs descriptors
         (default when the actors are the f32 128-128 MLP), else the PyTorch forward over the
         dense obs with torch's Gumbel noise.
@@ -79,16 +83,24 @@ class Rollout:
         step's statistics are reduced one step later, after a FeAR fence.
         gather: a parallel.ReturnGather; every step writes its ep_return / done into the gather's
         send buffer and the completed-episode returns of all ranks are all-gathered
-        (maddpg/agent.py:229-247 ``completed_episode_scores``)."""
+        (maddpg/agent.py:229-247 ``completed_episode_scores``).
+        patch > 0: the actors see (and the ring stores) each agent's egocentric patch x patch
+        window of its observation (VecGridEnv.obs_patch; an opt-in input format, the reference
+        observes the whole grid): actors built for (H, W) = (patch, patch); the env may run
+        with obs=False."""
         self.env = env
         self.actors = actors
-        self.fused = (actors is not None and actors.fusable(env)) if fused is None else bool(fused)
+        self.fused = (actors is not None and not patch and actors.fusable(env)) if fused is None else bool(fused)
         self.seed = int(seed)
         self._calls = 0  # Philox counter of the fused path's Gumbel noise (never repeats)
         self._actions = torch.empty((env.E, env.K), dtype=torch.int32, device=env.device)
         self.training = training
         self.group = group
-        self.replay = ReplayRing(env, replay_slots) if replay_slots else None
+        self.patch = int(patch)
+        if self.patch and actors is not None and (actors.H, actors.W) != (self.patch, self.patch):
+            raise ValueError("Rollout(patch=P) needs actors built for a P x P input")
+        self.replay = ReplayRing(env, replay_slots, patch=self.patch) if replay_slots else None
+        self._patch = None  # the current obs' patches when there is no ring
         self.gen = torch.Generator(device=env.device).manual_seed(seed) if actors is not None else None
         self.t = 0
         self.reducer = StatsReducer(_lib.GW_STATS, env.device, group) if env.out.get("stats") is not None else None
@@ -128,17 +140,22 @@ class Rollout:
         self._flush()
         if self.replay is not None:
             obs, mask = self.env.reset()
-            self.replay.obs[0].copy_(obs)
+            if self.patch:
+                self.env.obs_patch(self.patch, out=self.replay.obs[0])
+            else:
+                self.replay.obs[0].copy_(obs)
             self.replay.t = 0
             self.replay.t_dev.zero_()
         else:
             self.env.reset()
+            if self.patch:
+                self._patch = self.env.obs_patch(self.patch, out=self._patch)
         self.t = 0
 
     def _obs_now(self):
         if self.replay is not None:
             return self.replay.obs[self.t % self.replay.S]
-        return self.env.out["obs"]
+        return self._patch if self.patch else self.env.out["obs"]
 
     @torch.no_grad()
     def step(self):
@@ -151,7 +168,8 @@ class Rollout:
                                                  actions_out=self._actions, probs_out=probs_out)
             self._calls += 1
         elif self.actors is not None:
-            self.env.obs_fence()  # the PyTorch forward reads the dense obs
+            if not self.patch:
+                self.env.obs_fence()  # the PyTorch forward reads the dense obs
             actions, probs = self.actors.act(self._obs_now(), mask, self.training, generator=self.gen)
         else:
             actions, probs = None, None  # device-RNG random policy
@@ -161,8 +179,9 @@ class Rollout:
             nxt = (self.t + 1) % rp.S
             # zero-copy: the step writes obs_{t+1}, the terminal obs, the shaped reward and the
             # dones straight into the ring slots
-            into = dict(obs=rp.obs[nxt], final_obs=rp.final_obs[cur], shaped=rp.reward[cur],
-                        term=rp.term[cur], done=rp.done[cur])
+            into = dict(shaped=rp.reward[cur], term=rp.term[cur], done=rp.done[cur])
+            if not self.patch:
+                into.update(obs=rp.obs[nxt], final_obs=rp.final_obs[cur])
             if self.gather is not None:
                 g = self.gather.into()
                 into["ep_return"] = g["ep_return"]
@@ -170,6 +189,8 @@ class Rollout:
                 # hipMemcpy's blit took 18 us per 64 KB beside the obs writer)
                 self._gather_done = g["done"].view(torch.bool)
             r = env.step(actions, into=into)
+            if self.patch:  # the step's obs / terminal obs as patches, straight into the ring
+                env.obs_patch(self.patch, final=True, out=rp.obs[nxt], final_out=rp.final_obs[cur])
             if self.gather is not None:
                 torch.ne(rp.done[cur], 0, out=self._gather_done)
             if probs is not None and probs.data_ptr() != rp.probs[cur].data_ptr():
@@ -177,6 +198,8 @@ class Rollout:
             rp.t = self.t + 1
         else:
             r = env.step(actions, into=self.gather.into() if self.gather is not None else None)
+            if self.patch:
+                self._patch = env.obs_patch(self.patch, out=self._patch)
         self.t += 1
         tick = self.replay.t_dev if self.replay is not None else None
         if self.env.fear_async:

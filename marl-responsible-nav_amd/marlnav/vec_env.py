@@ -308,6 +308,26 @@ class VecGridEnv:
                        "gw_fear_matrix")
         return out
 
+    def obs_patch(self, size: int, final: bool = False, out: torch.Tensor | None = None,
+                  final_out: torch.Tensor | None = None):
+        """Egocentric local observations (gw_obs_patch): [K, E, size, size] float32, agent k's obs
+        cropped to the size x size window centred on its own cell, cells outside the grid -1.
+        An opt-in input format (the reference observes the whole grid); derived from the obs
+        descriptors, so the env may run without dense obs (``obs=False``).  final=True also
+        returns the terminal-obs patches of the envs done at the last step: (patch, final)."""
+        K, E, P = self.K, self.E, int(size)
+        if out is None:
+            out = torch.empty((K, E, P, P), dtype=torch.float32, device=self.device)
+        if final and final_out is None:
+            final_out = torch.full((K, E, P, P), float("nan"), dtype=torch.float32, device=self.device)
+        for t in (out, final_out):
+            if t is not None and (t.dtype != torch.float32 or t.numel() != K * E * P * P or not t.is_contiguous()):
+                raise ValueError(f"obs_patch: need contiguous float32 [K, E, {P}, {P}] buffers")
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.gw_obs_patch(self.handle, P, _ptr(out), _ptr(final_out) if final else None,
+                                             self._stream()), "gw_obs_patch")
+        return (out, final_out) if final else out
+
     def set_obs_async(self, enable: bool | str = True, fear_async: bool = False):
         """Pipeline the obs writer of step t with the world update of step t+1 (gw_set_obs_async).
         While on, ``step``'s obs / final_obs are ready on the current stream only after
