@@ -34,7 +34,7 @@ def main(src, dst):
         fmb = (sum(f) / len(f)) * 1024 * 2 / 1e6 if f else None
         wmb = (sum(w) / len(w)) * 1024 / 1e6 if w else None
         tot = (fmb or 0) + (wmb or 0) if (f or w) else None
-        short = name.split("(")[0].replace("void ", "")
+        short = name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
         lines.append(f"| `{short}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.2f} | {float(r['MinNs'])/1e3:.2f} | "
                      f"{float(r['MaxNs'])/1e3:.2f} | {float(r['Percentage']):.1f} | "
                      f"{'' if fmb is None else f'{fmb:.2f}'} | {'' if wmb is None else f'{wmb:.2f}'} | "
