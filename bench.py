@@ -327,6 +327,12 @@ def main():
     n_graph = args.steps - args.steps % graph_n if graph_n else 0
 
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # no Python garbage collection inside the timed region (as timeit does): the warmup's step
+    # results would otherwise trigger a collection pause that idles the GPU (measured: +30 us per
+    # step over 20 steps after 2,000 warmup steps)
+    import gc
+    gc.collect()
+    gc.disable()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -338,6 +344,7 @@ def main():
         if pe > 0 and graph is None:
             env.profile(i % pe == 0)
         one_step(i)
+    t_enq = time.perf_counter() - t0  # host time to enqueue the timed steps (host-bound if ~ wall)
     if cfg.get("rollout"):
         ro.fence()  # the last step's obs writes, FeAR outputs and statistics
     env.obs_fence()  # belong to the timed region
@@ -349,6 +356,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
+    gc.enable()
     if graph is not None:
         # HIP timing events cannot be recorded inside a graph: the kernel spans come from 16
         # eager steps right after the timed region (same env, same kernels, untimed)
@@ -429,6 +437,7 @@ def main():
                            "pipeline_chunks": int(os.environ.get("GW_CHUNKS", "1")) if not env.fused else 1,
                            "obs_async": obs_mode, "fear_async": env.fear_async,
                            "graph_steps": graph_n,
+                           "host_enqueue_ms_per_step": t_enq * 1e3 / args.steps,
                            "spans_from": "16 eager steps after the timed region" if graph_n else "the timed steps"},
             "last_step_episodes": {"completed": stats[1], "mean_return": stats[0] / max(stats[1], 1.0),
                          "mean_len": stats[6] / max(stats[1], 1.0)},

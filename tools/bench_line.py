@@ -9,4 +9,5 @@ lab = sys.argv[2] if len(sys.argv) > 2 else sys.argv[1]
 print(f"{lab:>14}: {d['value'] / 1e9:.3f} G  {d['ms_per_step'] * 1e3:.1f} us/step  stream "
       f"{k['stream_ms_per_step'] * 1e3:.1f}  obs {k['obs_kernel'] * 1e3:.1f} step {k['step_kernel'] * 1e3:.1f} "
       f"fear {k['fear_kernel'] * 1e3:.1f} (n={k['profiled_steps']}, graph {k.get('graph_steps')}) "
-      f"{r['kernel']} frac {r['frac'] if r['frac'] is None else round(r['frac'], 3)}")
+      f"{r['kernel']} frac {r['frac'] if r['frac'] is None else round(r['frac'], 3)} "
+      f"host {k.get('host_enqueue_ms_per_step', 0) * 1e3:.1f} us/step")
