@@ -7,7 +7,9 @@
 
 namespace {
 
-constexpr int T = 1024, MAXF = 64, U = 8;
+// One block of 256 threads (4 waves: it finds a CU slot even while a concurrent obs writer
+// fills the chip; the 1024-thread form waited up to 40 us for 16 free wave slots, profiles/r2_c5)
+constexpr int T = 256, MAXF = 64, U = 16;
 
 // one block: lane group g = tid / n_fields sums rows g, g + G, ... of field tid % n_fields (U
 // loads in flight per lane, added in row order), then the G group sums of each field meet in a
