@@ -179,6 +179,10 @@ def main():
                     help="c5: start each step's obs writer right after its world update (A/B)")
     ap.add_argument("--obs-lazy", action="store_true",
                     help="launch each step's obs writer at the next step (gw_set_obs_async 2; A/B)")
+    ap.add_argument("--obs-ring", type=int, default=-1,
+                    help="env-only workloads: write each step's obs into the next of this many buffers "
+                         "(a replay ring's slots), so consecutive pipelined writers need no order "
+                         "between them (-1 = auto: 2 with async obs on the defer path, else 1)")
     ap.add_argument("--graph", type=int, default=-1,
                     help="replay the timed steps as HIP graphs of this many captured steps (0 = eager "
                          "launches, -1 = auto: 16 for the launch-bound env-only workloads that run "
@@ -259,8 +263,16 @@ def main():
     gather = None if args.no_gather else ReturnGather(world * E, rank, world, env.device,
                                                       **({"window": graph_n} if graph_n else {}))
 
+    n_ring = args.obs_ring if args.obs_ring >= 0 else \
+        (2 if (obs_mode and env.kernel_path == "defer" and not cfg.get("rollout")) else 1)
+    obs_ring = [env.out["obs"]] + [torch.empty_like(env.out["obs"]) for _ in range(n_ring - 1)] \
+        if (n_ring > 1 and env.out["obs"] is not None) else None
+
     def one_step(i):
-        r = env.step(into=gather.into() if gather is not None else None)
+        into = gather.into() if gather is not None else {}
+        if obs_ring is not None:
+            into["obs"] = obs_ring[i % len(obs_ring)]
+        r = env.step(into=into or None)
         if gather is not None:
             gather.push()
         if reducer is not None:
@@ -430,13 +442,20 @@ def main():
                          "bytes_per_launch": bytes_per_launch, "avg_launch_ms": dur,
                          # every algorithmic byte of a whole step (state + obs) over the wall time
                          # per step: what the pipelined steps sustain end to end
-                         "step_level_GBps": (step_b + obs_b) * E / (t_max / args.steps) / 1e9},
+                         "step_level_GBps": (step_b + obs_b) * E / (t_max / args.steps) / 1e9,
+                         # with an obs ring the writers of consecutive steps overlap on two streams
+                         # (DESIGN §5.8), so a launch's duration spans two writers' shared bandwidth:
+                         # the dominant kernel's bytes per launch over the launch PERIOD (= the
+                         # stream time per step) is its sustained rate
+                         "writers_overlap": n_ring > 1 and bool(obs_mode) and env.kernel_path == "defer",
+                         "achieved_per_period": bytes_per_launch / (gpu_ms / args.steps * 1e-3) / 1e9,
+                         "frac_per_period": bytes_per_launch / (gpu_ms / args.steps * 1e-3) / 1e9 / HBM_PEAK_GBS},
             "kernels_ms": {"profiled_steps": nprof, "step_kernel": avg_step_ms, "obs_kernel": avg_obs_ms, "fear_kernel": avg_fear_ms,
                            "kernel_path": env.kernel_path,
                            "stream_ms_per_step": gpu_ms / args.steps,
                            "pipeline_chunks": int(os.environ.get("GW_CHUNKS", "1")) if not env.fused else 1,
                            "obs_async": obs_mode, "fear_async": env.fear_async,
-                           "graph_steps": graph_n,
+                           "graph_steps": graph_n, "obs_ring": n_ring,
                            "host_enqueue_ms_per_step": t_enq * 1e3 / args.steps,
                            "spans_from": "16 eager steps after the timed region" if graph_n else "the timed steps"},
             "last_step_episodes": {"completed": stats[1], "mean_return": stats[0] / max(stats[1], 1.0),

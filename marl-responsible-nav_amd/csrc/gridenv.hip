@@ -2035,6 +2035,13 @@ struct Env {
     // could start while obs_kernel(t) drains) measured 2.1x slower at C3 (more streams than the
     // process's hardware queues, GPU_MAX_HW_QUEUES = 4; profiles/r1_async)
     hipStream_t obs_stream = nullptr;
+    // a second obs stream, used when consecutive steps write DIFFERENT obs buffers (a replay
+    // ring's slots): writer t+1 then needs no order after writer t and starts while it drains,
+    // instead of behind the ~10 us kernel boundary + cross-queue wait (GW_OBS_STREAMS=1: off)
+    hipStream_t obs_stream2 = nullptr;
+    int obs_streams = 2;
+    int obs_cur = 0;                              // stream of the last writer (0 / 1)
+    const void *obs_last[2] = {nullptr, nullptr}; // obs / final_obs buffers of the last writer
     hipEvent_t obs_done[2] = {nullptr, nullptr};  // obs_kernel that read desc_buf[i] has finished
     bool obs_pending[2] = {false, false};
     hipEvent_t world_ev = nullptr;                // world update of the queued step has finished
@@ -2170,7 +2177,15 @@ gw_status flush_obs(Env *env, hipEvent_t after, hipStream_t on = nullptr) {
         env->obs_queued = false;
         return GW_OK;
     }
-    hipStream_t os = env->obs_stream;
+    // writers into the buffers of the last writer stay on its stream (write-after-write order);
+    // a writer into other buffers alternates to the other obs stream
+    const bool other = env->obs_streams > 1 && env->qobs.out.obs != env->obs_last[0] &&
+                       (env->qobs.out.final_obs == nullptr || env->qobs.out.final_obs != env->obs_last[1]);
+    if (other && !env->obs_stream2) HIP_TRY(hipStreamCreateWithFlags(&env->obs_stream2, hipStreamNonBlocking));
+    if (other) env->obs_cur ^= 1;
+    env->obs_last[0] = env->qobs.out.obs;
+    env->obs_last[1] = env->qobs.out.final_obs;
+    hipStream_t os = env->obs_cur ? env->obs_stream2 : env->obs_stream;
     HIP_TRY(hipStreamWaitEvent(os, env->world_ev, 0));
     if (after) HIP_TRY(hipStreamWaitEvent(os, after, 0));
     const bool prof = env->qobs_prof;  // timed iff the step that queued it was
@@ -2682,6 +2697,8 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
         if (ch) env->chunks = std::max(1, std::min(16, std::atoi(ch)));
         const char *bev = std::getenv("GW_BIND_EVENTS");
         if (bev) env->bind_events = std::atoi(bev) != 0;
+        const char *osn = std::getenv("GW_OBS_STREAMS");
+        if (osn) env->obs_streams = std::atoi(osn) > 1 ? 2 : 1;
         const char *ef = std::getenv("GW_EVENT_FENCE");
         if (ef && std::strcmp(ef, "system") == 0) {
             env->sync_flags = hipEventDisableTiming;
@@ -2968,6 +2985,7 @@ gw_status gw_set_obs_async(void *handle, int enable) {
         // the synchronous path writes the current descriptor buffer in place: drain the writer
         GW_TRY(flush_obs(env, nullptr));
         HIP_TRY(hipStreamSynchronize(env->obs_stream));
+        if (env->obs_stream2) HIP_TRY(hipStreamSynchronize(env->obs_stream2));
         env->obs_pending[0] = env->obs_pending[1] = false;
     }
     if (!(enable & 4) && env->fear_pending) {
@@ -3003,6 +3021,7 @@ gw_status gw_set_obs_dtype(void *handle, int dtype) {
         // an obs_kernel still queued or in flight was sized for the old format: drain it first
         GW_TRY(flush_obs(env, nullptr));
         HIP_TRY(hipStreamSynchronize(env->obs_stream));
+        if (env->obs_stream2) HIP_TRY(hipStreamSynchronize(env->obs_stream2));
     }
     // bf16 writer: ~64 KB of obs per block (C3: 16 envs, 4.3 TB/s; 4 envs 3.4, 8 envs 4.2;
     // C4: 4 envs; profiles/r1_bf16); f32: the create-time default
@@ -3203,6 +3222,7 @@ void gw_destroy(void *handle) {
     if (env->aux) (void)hipStreamDestroy(env->aux);
     if (env->aux2) (void)hipStreamDestroy(env->aux2);
     if (env->obs_stream) (void)hipStreamDestroy(env->obs_stream);
+    if (env->obs_stream2) (void)hipStreamDestroy(env->obs_stream2);
     for (hipEvent_t e : env->obs_done)
         if (e) (void)hipEventDestroy(e);
     if (env->world_ev) (void)hipEventDestroy(env->world_ev);

@@ -27,9 +27,11 @@ def patch(src: str) -> str:
     src = ins(src, "namespace gw {\n", "__device__ unsigned long long gw_phase_clk[65536][8];\n"
               "__device__ unsigned long long gw_fear_clk[65536][8];\n")
     # step_v2: start / tables+state in LDS / actions / world update / finish / end
-    a = src.index("__global__ void __launch_bounds__(128) step_v2(Params p) {")
+    a = src.index("__device__ __forceinline__ void step_v2_block(")
+    b1 = src.index("template <int N, int KMAX, bool FEAR, bool OBS, bool DEFER = false>\n"
+                   "__global__ void __launch_bounds__(128) step_v2(Params p) {")
     b = src.index("__global__ void __launch_bounds__(128) fear_v2(Params p) {")
-    step, rest = src[a:b], src[b:]
+    step, mid, rest = src[a:b1], src[b1:b], src[b:]
     step = ins(step, "    const int tid = threadIdx.x;\n", "    " + STAMP.format(slot=0))
     step = ins(step, "    const CtabOk okv{ctab};\n", "    " + STAMP.format(slot=1))
     step = ins(step, "            select_actions_v2<N>(p, e, es, ctab, cdf_s, act);\n#pragma unroll\n            for (int n = 0; n < N; ++n) {\n                pos[n] = es.pos[n];\n                mdr[n] = (int)((ctab[pos[n]] >> CT_MDR) & 0xFu);\n            }\n",
@@ -50,7 +52,7 @@ def patch(src: str) -> str:
     fear = ins(fear, "        ct.v[5] = np_sum_small(shaped, K);\n    }\n", "    " + fstamp.format(slot=4))
     fear = ins(fear, "    block_stats<T>(p, ct, sh.red, tid, p.stats_row0 + e0 / BE);\n", "    " + fstamp.format(slot=5))
     fear = ins(fear, "        fear_plan<N, KMAX>(p, sh, tid, pos, act, 0);\n", "        " + fstamp.format(slot=6), after=False)
-    src = src[:a] + step + fear + tail
+    src = src[:a] + step + mid + fear + tail
     src += ('\nextern "C" int gw_phase_read(unsigned long long *step, unsigned long long *fear, int n) {\n'
             '    if (hipMemcpyFromSymbol(step, HIP_SYMBOL(gw::gw_phase_clk), sizeof(unsigned long long) * 8 * n) != hipSuccess) return -1;\n'
             '    return hipMemcpyFromSymbol(fear, HIP_SYMBOL(gw::gw_fear_clk), sizeof(unsigned long long) * 8 * n) == hipSuccess ? 0 : -1;\n}\n')
@@ -60,6 +62,8 @@ def patch(src: str) -> str:
 def main():
     scen = sys.argv[1] if len(sys.argv) > 1 else "grid32"
     E = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
+    fear = bool(int(sys.argv[3])) if len(sys.argv) > 3 else True
+    os.environ.setdefault("GW_KERNEL", "defer")
     os.makedirs(OUT, exist_ok=True)
     with open(SRC) as f:
         src = patch(f.read())
@@ -75,7 +79,7 @@ def main():
     _lib.LIB_PATH = lib_path
     _lib.needs_build = lambda: False
     from marlnav.vec_env import VecGridEnv
-    env = VecGridEnv(scen, num_envs=E, fear=True, fear_weight=-5.0, stats=True)
+    env = VecGridEnv(scen, num_envs=E, fear=fear, fear_weight=-5.0, stats=True)
     env.reset()
     for _ in range(30):
         env.step()
@@ -89,6 +93,8 @@ def main():
     for name, arr, labels in (("step_v2<DEFER>", st, ["fill+state", "actions", "simulate", "finish_env", "desc", "stats"]),
                               ("fear_v2", fe, ["fill+rec", "plan(A)", "sims(B)", "resp(C)", "stats"])):
         used = arr[:, 0] != 0
+        if not used.any():
+            continue
         a = arr[used].astype(np.int64)
         last = len(labels)
         print(f"{name}: {used.sum()} blocks; block span cycles mean {np.mean(a[:, last] - a[:, 0]):.0f}")
@@ -96,7 +102,8 @@ def main():
             d = a[:, i + 1] - a[:, i]
             print(f"  {lab:12s} mean {d.mean():8.0f}  p50 {np.percentile(d, 50):8.0f}  p90 {np.percentile(d, 90):8.0f}")
     a = fe[fe[:, 0] != 0].astype(np.int64)
-    print(f"  fear_v2 A split: decode {np.mean(a[:, 6] - a[:, 1]):.0f}  fear_plan+barrier {np.mean(a[:, 2] - a[:, 6]):.0f}")
+    if len(a):
+        print(f"  fear_v2 A split: decode {np.mean(a[:, 6] - a[:, 1]):.0f}  fear_plan+barrier {np.mean(a[:, 2] - a[:, 6]):.0f}")
     env.close()
 
 
