@@ -160,7 +160,7 @@ int64_t gw_stats_rows(void *env);
 
 /* The kernel path gw_create chose: 0 "v1", 1 "split", 2 "fused", 3 "defer", 4 "merged".
  * GW_KERNEL selects it; unset: "merged" when a step's obs is at most GW_MERGE_BYTES (default
- * 192 MiB: small batches, bound by the step's latency chain, gain from one step_obs launch per
+ * 160 MiB: small batches, bound by the step's latency chain, gain from one step_obs launch per
  * pipelined step), else "defer".  -1 on a null handle. */
 int64_t gw_kernel_path(void *env);
 

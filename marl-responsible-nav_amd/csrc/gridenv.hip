@@ -2659,9 +2659,9 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
         env->mode = 3;
         if (!kv && HW % 4 == 0) {  // small batches: the merged pipeline (profiles/r2_merged)
             const char *mb = std::getenv("GW_MERGE_BYTES");
-            // crossover at C3's shape: merged wins up to 16,384 envs (134 MB of obs per step),
-            // defer from 32,768 (268 MB)
-            const int64_t lim = mb ? std::atoll(mb) : ((int64_t)192 << 20);
+            // crossover at C3's shape (defer with the obs ring's overlapping writers): merged
+            // wins up to 16,384 envs (128 MiB of obs per step), defer from 24,576 (192 MiB)
+            const int64_t lim = mb ? std::atoll(mb) : ((int64_t)160 << 20);
             if (cfg->num_envs * (int64_t)K * HW * 4 <= lim) env->mode = 4;
         }
         if (kv && std::strcmp(kv, "split") == 0) env->mode = 1;
