@@ -2016,7 +2016,10 @@ struct Env {
     uint32_t *roadbits = nullptr;
     int defer_order = 3;            // GW_DEFER (A/B): 0 fear then obs on one stream; 1 fear on a second
                                     // stream || obs; 3 (default) as 1 with the second stream at high priority
-    bool fear_wide = false;         // GW_FEAR_BE=wide: fear_v2 with 2x envs per block (A/B)
+    // fear_v2 with 2x envs per block (default since the obs writers overlap: C3 93.8 -> 92.1 us,
+    // C5 175 -> 166, C4f 368 -> 358 per step; the bf16 line loses 2 %: profiles/r2_events);
+    // GW_FEAR_BE=narrow: 1x (A/B)
+    bool fear_wide = true;
     int chunks = 1;                 // GW_CHUNKS: step/obs pipeline depth (split path; 1 = off, measured best)
     hipStream_t aux = nullptr;      // second stream of the pipeline (created on first use)
     hipStream_t aux2 = nullptr;     // third stream: obs_kernel of the chunked defer pipeline
@@ -2675,6 +2678,7 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
         if (dv) env->defer_order = std::atoi(dv) == 0 ? 0 : (std::atoi(dv) == 3 ? 3 : 1);
         const char *fb = std::getenv("GW_FEAR_BE");
         if (fb && std::strcmp(fb, "wide") == 0) env->fear_wide = true;
+        if (fb && std::strcmp(fb, "narrow") == 0) env->fear_wide = false;
         // obs_kernel block size (tools/gpu_ab2.sh): 4 float4 stores per thread when the writer
         // runs alone (32x32 K=2 -> 2 envs, 64x64 -> 1), 8 while fear_v2 shares the CUs (32x32 ->
         // 4 envs: 2.5 % faster step at C3)

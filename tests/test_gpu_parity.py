@@ -146,7 +146,8 @@ KERNEL_PATHS = {
     "fused": {"GW_KERNEL": "fused"},                          # obs stores inside step_v2
     "defer": {"GW_KERNEL": "defer"},                          # default: fear_v2 on a 2nd stream || obs_kernel
     "defer_serial": {"GW_KERNEL": "defer", "GW_DEFER": "0"},  # step_v2 <DEFER>, fear_v2, obs_kernel, one stream
-    "defer_wide": {"GW_KERNEL": "defer", "GW_FEAR_BE": "wide"},  # fear_v2 with 2x envs per block
+    "defer_wide": {"GW_KERNEL": "defer", "GW_FEAR_BE": "wide"},  # fear_v2 with 2x envs per block (default)
+    "defer_narrow": {"GW_KERNEL": "defer", "GW_FEAR_BE": "narrow"},  # fear_v2 with 1x
     "defer_chunks": {"GW_KERNEL": "defer", "GW_CHUNKS": "2"},  # 2 env chunks over 3 streams
     "v1": {"GW_KERNEL": "v1"},                                # the first kernels
     "merged": {"GW_KERNEL": "merged"},                        # synchronous: as split1 (async: step_obs)
