@@ -340,6 +340,9 @@ def main():
         graph = env.capture_steps(graph_n, gather)
     n_graph = args.steps - args.steps % graph_n if graph_n else 0
 
+    if pe > 0:  # the profiling events exist before the timed region (gw_profile creates them)
+        env.profile(True, reserve=8 * (args.steps // pe + 2))
+        env.profile(False)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     # no Python garbage collection inside the timed region (as timeit does): the warmup's step
     # results would otherwise trigger a collection pause that idles the GPU (measured: +30 us per

@@ -134,12 +134,14 @@ gw_status gw_state_view(void *env, gw_state *out);
  * gw_state layout (device or pinned host memory), enqueued on stream. */
 gw_status gw_copy_state(void *env, const gw_state *buf, int to_env, void *stream);
 
-/* Per-launch timing: while enabled, gw_step records HIP events around each of its kernels on
- * the stream each is launched on: [0] the world-update kernel (step_v2), [1] the obs writer
- * (obs_kernel), [2] the deferred FeAR kernel (fear_v2, GW_KERNEL=defer only; it runs on a second
- * stream concurrently with [1]).  gw_profile_read synchronises on those events, returns the
- * summed elapsed milliseconds per kernel and the number of gw_step calls timed, and clears
- * them.  Used by bench.py for the live roofline. */
+/* Per-launch timing: while enabled, gw_step's kernels carry HIP timing events in their
+ * dispatch (start / stop of the launch itself, on the stream each is launched on): [0] the
+ * world-update kernel (step_v2), [1] the obs writer (obs_kernel; the merged path's step_obs),
+ * [2] the deferred FeAR kernel (fear_v2, GW_KERNEL=defer only; it runs concurrently with [1]).
+ * enable > 1 also makes sure `enable` timing events exist now (creating them inside a profiled
+ * step would put their host cost between its launches).  gw_profile_read synchronises on those
+ * events, returns the summed elapsed milliseconds per kernel and the number of gw_step calls
+ * timed, and clears them.  Used by bench.py for the live roofline. */
 gw_status gw_profile(void *env, int enable);
 gw_status gw_profile_read(void *env, double out_ms[3], int64_t *n_steps);
 

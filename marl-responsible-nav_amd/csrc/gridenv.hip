@@ -3047,6 +3047,14 @@ gw_status gw_profile(void *handle, int enable) {
     Env *env = static_cast<Env *>(handle);
     if (!env) return fail(GW_ERR_ARG, "null env");
     env->profiling = enable != 0;
+    // the timing events are created here, ahead of the profiled steps (enable > 1: at least
+    // `enable` of them): hipEventCreate inside a step puts its host cost between the launches
+    const size_t want = env->profiling ? env->ev_used + (size_t)std::max(enable, 32) : 0;
+    while (env->ev_pool.size() < want) {
+        hipEvent_t e = nullptr;
+        HIP_TRY(hipEventCreateWithFlags(&e, env->prof_flags));
+        env->ev_pool.push_back(e);
+    }
     return GW_OK;
 }
 

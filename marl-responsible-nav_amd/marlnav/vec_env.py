@@ -360,9 +360,10 @@ class VecGridEnv:
             with torch.cuda.device(self.device):
                 _lib.check(self.lib.gw_fear_fence(self.handle, self._stream()), "gw_fear_fence")
 
-    def profile(self, enable: bool = True):
-        """Record HIP events around each gw_step kernel (see gw_profile)."""
-        _lib.check(self.lib.gw_profile(self.handle, int(enable)), "gw_profile")
+    def profile(self, enable: bool = True, reserve: int = 0):
+        """Time each gw_step kernel with HIP events (see gw_profile); reserve: create that many
+        timing events now, outside any timed region."""
+        _lib.check(self.lib.gw_profile(self.handle, max(int(enable), int(reserve)) if enable else 0), "gw_profile")
 
     def profile_read(self):
         """-> (ms summed over timed steps [step_kernel, obs_kernel, fear_kernel], timed steps).
