@@ -93,6 +93,12 @@ typedef struct gw_step_out {
                             apples caught, shaped rewards, completed-episode lengths, envs.
                             Deterministic (fixed reduction tree); fed to the RCCL
                             reduction of the multi-GPU rollout.                          */
+    uint8_t *done_copy;  /* [E]   a second destination of `done` (e.g. the per-step return
+                            gather's send buffer beside the replay ring's done slot)     */
+    double *stats_acc;   /* [gw_stats_rows()][GW_STATS]: every step ADDS its per-block rows
+                            (a running total without a per-step reduction launch; one
+                            block owns each row, so the sums are deterministic)          */
+    int64_t *tick;       /* [1]   += 1 per gw_step (e.g. the replay ring's step count)   */
 } gw_step_out;
 
 #define GW_STATS 8
@@ -219,7 +225,9 @@ gw_status gw_set_obs_async(void *env, int enable);
  * GW_OBS_F32 (default; the reference's values as float32) or GW_OBS_BF16 (the same values as
  * bfloat16 bits, [K][E][H*W] uint16: every value the env produces is exact in bf16, so this is
  * lossless and halves the obs bytes; needs H*W % 8 == 0 and the split / defer kernel paths).
- * The float* obs pointers then address bf16 buffers. */
+ * The float* obs pointers then address bf16 buffers.  Called before the first gw_reset it may
+ * also change gw_stats_rows (the FeAR kernel's envs per block follow the format's best choice):
+ * size the stats buffer after it. */
 enum { GW_OBS_F32 = 0, GW_OBS_BF16 = 1 };
 gw_status gw_set_obs_dtype(void *env, int dtype);
 gw_status gw_obs_fence(void *env, void *stream);

@@ -551,6 +551,17 @@ struct Contrib {  // this env's share of gw_step_out.stats
     double v[GW_STATS];
 };
 
+// one field of a block's stats row: the step's value (stats) and / or its running total
+__device__ __forceinline__ void stats_put(const gw_step_out &o, int64_t idx, double v) {
+    if (o.stats) o.stats[idx] = v;
+    if (o.stats_acc) o.stats_acc[idx] = __dadd_rn(o.stats_acc[idx], v);
+}
+
+// the step's tick (gw_step_out.tick): one vector atomic by one lane of the step's first block
+__device__ __forceinline__ void step_tick(const gw_step_out &o) {
+    if (o.tick) __hip_atomic_fetch_add(o.tick, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ void contrib_zero(Contrib &c) {
 #pragma unroll
     for (int i = 0; i < GW_STATS; ++i) c.v[i] = 0.0;
@@ -695,6 +706,7 @@ __device__ __forceinline__ void finish_env(const Params &p, int64_t e, const Env
         if (o.trunc) o.trunc[ek] = (uint8_t)((trunc >> k) & 1u);
     }
     if (o.done) o.done[e] = done;
+    if (o.done_copy) o.done_copy[e] = done;
     if (o.crashes) o.crashes[e] = crash_count;
     if (o.apples) o.apples[e] = apple_rewarded;
     if (!DEFER && o.ep_return) o.ep_return[e] = score;
@@ -782,7 +794,8 @@ __global__ void __launch_bounds__(256) step_kernel_nofear(Params p) {
     Contrib ct;
     contrib_zero(ct);
     if (e < p.E) step_env_nofear<N>(p, e, s_ok, ct);
-    if (p.out.stats) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) step_tick(p.out);
+    if (p.out.stats || p.out.stats_acc) {
         __shared__ double s_red[4][GW_STATS];
         wave_sum(ct);
         const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -791,8 +804,8 @@ __global__ void __launch_bounds__(256) step_kernel_nofear(Params p) {
         __syncthreads();
         if (threadIdx.x < GW_STATS) {
             const int i = threadIdx.x;
-            p.out.stats[(int64_t)blockIdx.x * GW_STATS + i] =
-                __dadd_rn(__dadd_rn(s_red[0][i], s_red[1][i]), __dadd_rn(s_red[2][i], s_red[3][i]));
+            stats_put(p.out, (int64_t)blockIdx.x * GW_STATS + i,
+                      __dadd_rn(__dadd_rn(s_red[0][i], s_red[1][i]), __dadd_rn(s_red[2][i], s_red[3][i])));
         }
     }
 }
@@ -995,9 +1008,10 @@ __global__ void __launch_bounds__(256) step_kernel_fear(Params p) {
         finish_env<N>(p, e, es, act, mdr, fear, bits & 0xFFu, (bits >> 8) & 0xFFu, fin, bits >> 16, ct, oi);
         store_desc<N>(p, e, oi);
     }
-    if (p.out.stats && tid < 64) {  // BE <= 64: every env of the block sits in wave 0
+    if (blockIdx.x == 0 && tid == 0) step_tick(p.out);
+    if ((p.out.stats || p.out.stats_acc) && tid < 64) {  // BE <= 64: every env of the block sits in wave 0
         wave_sum(ct);
-        if (tid < GW_STATS) p.out.stats[(int64_t)blockIdx.x * GW_STATS + tid] = ct.v[tid];
+        if (tid < GW_STATS) stats_put(p.out, (int64_t)blockIdx.x * GW_STATS + tid, ct.v[tid]);
     }
 }
 
@@ -1444,18 +1458,19 @@ __device__ __forceinline__ void fear_values(const Params &p, const Sh &sh, int e
 template <int T>
 __device__ __forceinline__ void block_stats(const Params &p, Contrib &ct, double (&red)[T / 64][GW_STATS], int tid,
                                             int64_t row) {
-    if (p.out.stats) {
+    const bool want = p.out.stats || p.out.stats_acc;
+    if (want) {
         wave_sum(ct);
         if ((tid & 63) == 0)
 #pragma unroll
             for (int i = 0; i < GW_STATS; ++i) red[tid >> 6][i] = ct.v[i];
     }
     __syncthreads();
-    if (p.out.stats && tid < GW_STATS) {
+    if (want && tid < GW_STATS) {
         double acc = red[0][tid];
 #pragma unroll
         for (int w = 1; w < T / 64; ++w) acc = __dadd_rn(acc, red[w][tid]);
-        p.out.stats[row * GW_STATS + tid] = acc;
+        stats_put(p.out, row * GW_STATS + tid, acc);
     }
 }
 
@@ -1476,6 +1491,7 @@ __device__ __forceinline__ void step_v2_block(const Params &p, int64_t bid, V2Sh
     const int64_t e0 = p.e_begin + bid * BE;
     const int nenv = (int)min((int64_t)BE, p.e_end - e0);
     const int K = p.K;
+    if (e0 == 0 && tid == 0) step_tick(p.out);  // once per step: the block of env 0
     Contrib ct;
     contrib_zero(ct);
     EnvState<N> es;
@@ -2020,6 +2036,7 @@ struct Env {
     // C5 175 -> 166, C4f 368 -> 358 per step; the bf16 line loses 2 %: profiles/r2_events);
     // GW_FEAR_BE=narrow: 1x (A/B)
     bool fear_wide = true;
+    bool fear_wide_fixed = false;   // GW_FEAR_BE given (else the obs format picks, before any reset)
     int chunks = 1;                 // GW_CHUNKS: step/obs pipeline depth (split path; 1 = off, measured best)
     hipStream_t aux = nullptr;      // second stream of the pipeline (created on first use)
     hipStream_t aux2 = nullptr;     // third stream: obs_kernel of the chunked defer pipeline
@@ -2679,6 +2696,7 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
         const char *fb = std::getenv("GW_FEAR_BE");
         if (fb && std::strcmp(fb, "wide") == 0) env->fear_wide = true;
         if (fb && std::strcmp(fb, "narrow") == 0) env->fear_wide = false;
+        env->fear_wide_fixed = fb != nullptr;
         // obs_kernel block size (tools/gpu_ab2.sh): 4 float4 stores per thread when the writer
         // runs alone (32x32 K=2 -> 2 envs, 64x64 -> 1), 8 while fear_v2 shares the CUs (32x32 ->
         // 4 envs: 2.5 % faster step at C3)
@@ -3033,6 +3051,9 @@ gw_status gw_set_obs_dtype(void *handle, int dtype) {
         env->obs_be = bf ? std::max(1, std::min(gw::OBS_BE, 32768 / std::max(1, env->K * env->HW)))
                          : env->obs_be_f32;
     env->obs_bf16 = bf;
+    // the bf16 step is bound by the world update + FeAR chain, where 32 envs per fear block is
+    // 2 % faster; the stats rows depend on it, so only before the first reset
+    if (!env->initialized && !env->fear_wide_fixed) env->fear_wide = !bf;
     return GW_OK;
 }
 

@@ -104,6 +104,12 @@ class Rollout:
         self.gen = torch.Generator(device=env.device).manual_seed(seed) if actors is not None else None
         self.t = 0
         self.reducer = StatsReducer(_lib.GW_STATS, env.device, group) if env.out.get("stats") is not None else None
+        # one rank: the step kernels add their per-block rows into a running total and advance
+        # the ring's device step count themselves (gw_step_out.stats_acc / tick), so a step
+        # needs no reduction launch; across ranks the per-step all-reduce stays
+        self._acc = None
+        if self.reducer is not None and not self.reducer.distributed:
+            self._acc = torch.zeros_like(env.out["stats"])
         self.gather = gather
         if gather is not None and gather.count != env.E:
             raise ValueError("ReturnGather shard size != env.E")
@@ -121,6 +127,8 @@ class Rollout:
     def _reduce(self, stats, tick):
         if self.gather is not None:
             self.gather.push()  # the step wrote ep_return / done into the gather's send buffer
+        if self._acc is not None:
+            return  # the step kernels accumulated the rows and advanced the tick
         if self.reducer is not None:
             # per-step (RCCL) reduction of the episode statistics; the ring's device step count
             # advances in the same launch
@@ -180,24 +188,26 @@ class Rollout:
             # zero-copy: the step writes obs_{t+1}, the terminal obs, the shaped reward and the
             # dones straight into the ring slots
             into = dict(shaped=rp.reward[cur], term=rp.term[cur], done=rp.done[cur])
+            if self._acc is not None:
+                into.update(stats_acc=self._acc, tick=rp.t_dev)
             if not self.patch:
                 into.update(obs=rp.obs[nxt], final_obs=rp.final_obs[cur])
             if self.gather is not None:
                 g = self.gather.into()
                 into["ep_return"] = g["ep_return"]
-                # done goes to the ring; the gather gets an E-byte copy (an elementwise kernel:
-                # hipMemcpy's blit took 18 us per 64 KB beside the obs writer)
-                self._gather_done = g["done"].view(torch.bool)
+                # done goes to the ring slot and, from the same kernel, to the gather's send buffer
+                into["done_copy"] = g["done"]
             r = env.step(actions, into=into)
             if self.patch:  # the step's obs / terminal obs as patches, straight into the ring
                 env.obs_patch(self.patch, final=True, out=rp.obs[nxt], final_out=rp.final_obs[cur])
-            if self.gather is not None:
-                torch.ne(rp.done[cur], 0, out=self._gather_done)
             if probs is not None and probs.data_ptr() != rp.probs[cur].data_ptr():
                 rp.probs[cur].copy_(probs)
             rp.t = self.t + 1
         else:
-            r = env.step(actions, into=self.gather.into() if self.gather is not None else None)
+            into = dict(self.gather.into()) if self.gather is not None else {}
+            if self._acc is not None:
+                into["stats_acc"] = self._acc
+            r = env.step(actions, into=into or None)
             if self.patch:
                 self._patch = env.obs_patch(self.patch, out=self._patch)
         self.t += 1
@@ -214,6 +224,8 @@ class Rollout:
         if self.reducer is None:
             return {}
         self._flush()
+        if self._acc is not None:
+            return dict(zip(_lib.STATS_NAMES, self._acc.sum(0).cpu().tolist()))
         return dict(zip(_lib.STATS_NAMES, self.reducer.result().cpu().tolist()))
 
     def completed_scores(self, last: int | None = None):

@@ -50,6 +50,9 @@ class StepResult:
     crash_bits: torch.Tensor | None = None
     restr_bits: torch.Tensor | None = None
     stats: torch.Tensor | None = None   # [rows, 8] per-block partial sums (_lib.STATS_NAMES)
+    done_copy: torch.Tensor | None = None  # a second destination of done (step(into=...))
+    stats_acc: torch.Tensor | None = None  # running per-block totals (step(into=...))
+    tick: torch.Tensor | None = None       # += 1 per step (step(into=...))
 
 
 class StepGraph:
@@ -135,6 +138,7 @@ class VecGridEnv:
             crash_bits=torch.zeros(E, dtype=torch.uint8, device=dev) if debug else None,
             restr_bits=torch.zeros(E, dtype=torch.uint8, device=dev) if debug else None,
             stats=torch.zeros((int(self.lib.gw_stats_rows(self.handle)), _lib.GW_STATS), **f64) if stats else None,
+            done_copy=None, stats_acc=None, tick=None,
         )
         self._step_out = _lib.GwStepOut(*[_ptr(self.out[n]) for n in _lib.STEP_OUT_FIELDS])
         self._closed = False
@@ -164,6 +168,8 @@ class VecGridEnv:
     _INTO_SPEC = {"obs": (torch.float32, "KEHW"), "final_obs": (torch.float32, "KEHW"),
                   "reward": (torch.float64, "EK"), "fear": (torch.float64, "EK"), "shaped": (torch.float64, "EK"),
                   "term": (torch.uint8, "EK"), "trunc": (torch.uint8, "EK"), "done": (torch.uint8, "E"),
+                  "done_copy": (torch.uint8, "E"), "stats_acc": (torch.float64, "ROWS"),
+                  "tick": (torch.int64, "ONE"),
                   "ep_return": (torch.float64, "E")}
 
     def step(self, rl_actions: torch.Tensor | None = None, scripted: torch.Tensor | None = None,
@@ -175,8 +181,9 @@ class VecGridEnv:
         obs_out / final_obs_out: [K, E, H, W] float32 buffers to write this step's obs into
         instead of the env's own (e.g. a replay-ring slot: zero-copy replay storage);
         into: the same for any of obs, final_obs, reward, fear, shaped, term, trunc, done,
-        ep_return (contiguous tensors of the output's dtype and size; e.g. the send buffer of
-        parallel.ReturnGather)."""
+        done_copy (a second destination of done), ep_return, stats_acc (per-block rows every
+        step ADDS to: a running total), tick (int64 scalar, += 1 per step) (contiguous tensors of
+        the output's dtype and size; e.g. the send buffer of parallel.ReturnGather)."""
         rl = self._as_i32(rl_actions, (self.E, self.K))
         sa = self._as_i32(scripted, (self.E, self.N - self.K))
         sp = self._as_i32(spawn, (self.E, self.N))
@@ -190,7 +197,8 @@ class VecGridEnv:
         if over:
             so = _lib.GwStepOut.from_buffer_copy(self._step_out)
             res = dict(self.out)
-            sizes = {"KEHW": self.K * self.E * self.H * self.W, "EK": self.E * self.K, "E": self.E}
+            sizes = {"KEHW": self.K * self.E * self.H * self.W, "EK": self.E * self.K, "E": self.E, "ONE": 1,
+                     "ROWS": int(self.lib.gw_stats_rows(self.handle)) * _lib.GW_STATS}
             for name, t in over.items():
                 dt, shp = self._INTO_SPEC[name]
                 if shp == "KEHW":
