@@ -199,3 +199,37 @@ def test_async_obs_alternating_buffers():
     assert int(bad) == 0
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("ring,same_final", [(3, False), (2, True), (5, True)])
+def test_async_obs_rings_and_shared_final_buffer(ring, same_final, monkeypatch):
+    """The writers of consecutive steps go to alternating obs streams only when both their obs and
+    final_obs buffers differ; a ring of 3 / 5 slots reuses a slot on the OTHER stream two steps
+    later (ordered through the descriptor WAR chain), and a final_obs buffer shared by every step
+    keeps the writers on one stream.  Every slot holds the obs of the last step that wrote it."""
+    monkeypatch.setenv("GW_KERNEL", "defer")
+    sc = S.builtin("grid32")
+    E, T = 4096, 17
+    a = VecGridEnv(sc, num_envs=E, fear=True, fear_weight=-5.0, seed=23, max_steps=10, final_obs=True)
+    b = VecGridEnv(sc, num_envs=E, fear=True, fear_weight=-5.0, seed=23, max_steps=10, final_obs=True)
+    b.set_obs_async(True)
+    obs = [torch.empty_like(b.out["obs"]) for _ in range(ring)]
+    fin = [torch.full_like(b.out["obs"], -3.0) for _ in range(1 if same_final else ring)]
+    ref_fin = [torch.full_like(a.out["obs"], -3.0) for _ in range(len(fin))]
+    a.reset()
+    b.reset()
+    last = [None] * ring
+    for t in range(T):
+        ra = a.step(final_obs_out=ref_fin[t % len(ref_fin)])
+        b.step(obs_out=obs[t % ring], final_obs_out=fin[t % len(fin)])
+        last[t % ring] = ra.obs.clone()
+    b.obs_fence()
+    bad = torch.zeros((), dtype=torch.int64, device="cuda")
+    for i in range(ring):
+        bad += (last[i] != obs[i]).sum()
+    for x, y in zip(ref_fin, fin):
+        bad += (x != y).sum()
+    torch.cuda.synchronize()
+    assert int(bad) == 0
+    a.close()
+    b.close()
