@@ -33,7 +33,7 @@ def evaluate(actors: MultiAgentActors, scenario="level3", episodes: int = 100, m
         steps = torch.zeros((), dtype=torch.int64, device=dev)
         fear_sum = torch.zeros((), dtype=torch.float64, device=dev)
         recorded = []
-        for _ in range(max_steps):
+        for i in range(max_steps):
             if fused:  # one kernel over the obs descriptors (include/actor_ops.h)
                 actions, _ = actors.act_env(env, env.out["mask"], training=False)
             else:
@@ -46,7 +46,9 @@ def evaluate(actors: MultiAgentActors, scenario="level3", episodes: int = 100, m
             steps += active.sum()
             fear_sum += (r.fear.sum(1) * active).sum()
             active &= ~r.done.bool()
-            if not bool(active.any()):  # one host sync per step; evaluation is not the hot path
+            # a host sync every 8 steps: stepping envs whose episode ended changes no total
+            # (they are masked out), so checking late only costs the few extra steps
+            if i % 8 == 7 and not bool(active.any()):
                 break
         out = {"episodes": episodes, "crashes": int(crashes), "apples_caught": int(apples), "steps": int(steps),
                "fear": float(fear_sum)}
