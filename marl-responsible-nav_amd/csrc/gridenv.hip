@@ -575,6 +575,31 @@ __device__ __forceinline__ void wave_sum(Contrib &c) {
         for (int i = 0; i < GW_STATS; ++i) c.v[i] = __dadd_rn(c.v[i], __shfl_xor(c.v[i], off, 64));
 }
 
+// The same butterfly for the fields a kernel can make non-zero only: FM = f64 fields (the same
+// order as wave_sum: bit-identical), IM = integer-valued fields (exact counts, summed as int32:
+// the same values), every other field 0.0.  Fewer cross-lane moves on the step's latency chain.
+template <uint32_t FM, uint32_t IM>
+__device__ __forceinline__ void wave_sum_sel(Contrib &c) {
+    int iv[GW_STATS];
+#pragma unroll
+    for (int i = 0; i < GW_STATS; ++i) iv[i] = ((IM >> i) & 1u) ? (int)c.v[i] : 0;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+        for (int i = 0; i < GW_STATS; ++i) {
+            if ((FM >> i) & 1u) c.v[i] = __dadd_rn(c.v[i], __shfl_xor(c.v[i], off, 64));
+            else if ((IM >> i) & 1u) iv[i] += __shfl_xor(iv[i], off, 64);
+        }
+#pragma unroll
+    for (int i = 0; i < GW_STATS; ++i)
+        if (!((FM >> i) & 1u)) c.v[i] = ((IM >> i) & 1u) ? (double)iv[i] : 0.0;
+}
+
+// stats fields: 0 completed-episode return, 2 FeAR, 5 shaped reward (f64); 1 episodes,
+// 3 crashes, 4 apples, 6 completed-episode length, 7 env-steps (integer counts)
+constexpr uint32_t ST_INT = (1u << 1) | (1u << 3) | (1u << 4) | (1u << 6) | (1u << 7);
+constexpr uint32_t ST_F64_FEAR = (1u << 0) | (1u << 2) | (1u << 5);
+
 // One env's state, loaded once (prefetched before the counterfactual phase in step_v2).
 template <int N>
 struct EnvState {
@@ -1455,12 +1480,12 @@ __device__ __forceinline__ void fear_values(const Params &p, const Sh &sh, int e
 }
 
 // Block statistics: deterministic wave butterfly + fixed-order cross-wave sum, one row per block.
-template <int T>
+template <int T, uint32_t FM = 0xFFu, uint32_t IM = 0u>
 __device__ __forceinline__ void block_stats(const Params &p, Contrib &ct, double (&red)[T / 64][GW_STATS], int tid,
                                             int64_t row) {
     const bool want = p.out.stats || p.out.stats_acc;
     if (want) {
-        wave_sum(ct);
+        wave_sum_sel<FM, IM>(ct);
         if ((tid & 63) == 0)
 #pragma unroll
             for (int i = 0; i < GW_STATS; ++i) red[tid >> 6][i] = ct.v[i];
@@ -1631,7 +1656,9 @@ __device__ __forceinline__ void step_v2_block(const Params &p, int64_t bid, V2Sh
     }
 
     // ---- block statistics (deterministic tree) ----
-    block_stats<T>(p, ct, sh.red, tid, p.stats_row0 + e0 / BE);
+    // deferred FeAR: the FeAR-owned f64 fields are fear_v2's; without FeAR field 2 stays 0
+    constexpr uint32_t FM = DEFER ? 0u : ((1u << 0) | (1u << 5) | (FEAR ? (1u << 2) : 0u));
+    block_stats<T, FM, ST_INT>(p, ct, sh.red, tid, p.stats_row0 + e0 / BE);
 
     if constexpr (OBS) {
         // ---- D: obs of the block's envs, 16-byte coalesced stores ----
@@ -1875,7 +1902,7 @@ __global__ void __launch_bounds__(128) fear_v2(Params p) {
         ct.v[2] = np_sum_small(fsum_in, K);
         ct.v[5] = np_sum_small(shaped, K);
     }
-    block_stats<T>(p, ct, sh.red, tid, p.stats_row0 + e0 / BE);
+    block_stats<T, ST_F64_FEAR, 0u>(p, ct, sh.red, tid, p.stats_row0 + e0 / BE);
 }
 
 // ---------------------------------------------------------------------------------------
