@@ -176,7 +176,7 @@ def main():
                     help="bf16: the lossless compact obs format (gw_set_obs_dtype); reported separately, "
                          "the metric's definition is f32 obs")
     ap.add_argument("--obs-eager", action="store_true",
-                    help="c5: start each step's obs writer right after its world update (A/B)")
+                    help="start each step's obs writer right after its world update (the default)")
     ap.add_argument("--obs-lazy", action="store_true",
                     help="launch each step's obs writer at the next step (gw_set_obs_async 2; A/B)")
     ap.add_argument("--obs-ring", type=int, default=-1,
@@ -212,11 +212,14 @@ def main():
     if args.high_prio:
         torch.cuda.set_stream(torch.cuda.Stream(priority=-1))
     cfg = dict(CONFIGS[args.config])
-    # obs writer pipelined with the next step (gw_set_obs_async): right after the world update
-    # for the env-only workloads; launched at the next step (behind the fused actor, which would
-    # otherwise lose CUs to it) for the full rollout.  Measured A/B: profiles/r1_async/
-    obs_mode = False if args.sync_obs else \
-        ("lazy" if (args.obs_lazy or (cfg.get("rollout") and not args.obs_eager)) else True)
+    # obs writer pipelined with the next step (gw_set_obs_async), launched right after the world
+    # update.  Measured A/B: profiles/r1_async/, profiles/r2_c5modes/
+    obs_mode = False if args.sync_obs else ("lazy" if args.obs_lazy else True)
+    if cfg.get("rollout") and not cfg.get("arch") and not cfg.get("patch") and not (args.obs_lazy or args.sync_obs):
+        # the rollout's writer starts right after the world update, as 2 launches so that the next
+        # actor's kernels are dispatched between them (150 vs 168 us per step lazily in one launch,
+        # profiles/r2_c5modes); read by gw_create
+        os.environ.setdefault("GW_OBS_CHUNKS", "2")
     if cfg.get("patch"):  # no dense obs: nothing to pipeline
         obs_mode = False
     if cfg.get("arch") == "cnn" and not (args.cnn_torch or args.obs_lazy or args.sync_obs):

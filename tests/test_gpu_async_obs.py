@@ -233,3 +233,19 @@ def test_async_obs_rings_and_shared_final_buffer(ring, same_final, monkeypatch):
     assert int(bad) == 0
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("chunks,mode,E", [(2, True, 4099), (4, True, 4096), (3, "lazy", 1000)])
+def test_async_obs_chunked_writer(chunks, mode, E, monkeypatch):
+    """GW_OBS_CHUNKS: each step's writer as several launches over consecutive env ranges (the
+    C5 / c4cnn default, so the next actor's kernels are dispatched between them) == sync."""
+    monkeypatch.setenv("GW_OBS_CHUNKS", str(chunks))
+    test_async_obs_matches_sync("defer", True, "grid32", mode, E, monkeypatch)
+
+
+@pytest.mark.parametrize("chunks", [2, 4])
+def test_async_rollout_chunked_writer_matches_sync(chunks, monkeypatch):
+    """The C5 default pipeline (eager writer in GW_OBS_CHUNKS launches, replay-ring slots on
+    alternating obs streams, fused actor) == the synchronous rollout."""
+    monkeypatch.setenv("GW_OBS_CHUNKS", str(chunks))
+    test_async_rollout_fused_actor_matches_sync(True, False, "defer", monkeypatch)
