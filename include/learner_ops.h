@@ -23,6 +23,26 @@ gw_status gw_adam_step(float *param, const float *grad, float *exp_avg, float *e
 /* agilerl soft_update: target = tau * online + (1 - tau) * target on n elements. */
 gw_status gw_soft_update(float *target, const float *online, int64_t n, float tau, void *stream);
 
+/* Hidden-layer epilogue of the stacked MLPs (agilerl EvolvableMLP: Linear -> LayerNorm -> ReLU;
+ * marlnav/actor.py StackedMLPActors.forward, replacing F.layer_norm + addcmul + relu, three
+ * launches, by one).  z, y [K, R, h] contiguous, ln_w / ln_b [K, h]; 0 < h <= 512.
+ *   y = relu(ln_b + ((z - mean) * rstd) * ln_w),  mean / rstd over h (biased variance, eps).
+ * mean / rstd [K, R] receive the row statistics for the backward (both NULL: not saved). */
+gw_status gw_ln_relu_fwd(const float *z, const float *ln_w, const float *ln_b, float *y, float *mean, float *rstd,
+                         int32_t K, int64_t R, int32_t h, float eps, void *stream);
+
+/* Its backward from the saved z, y, mean, rstd: dz [K, R, h] is written; the ln_w / ln_b
+ * gradients, summed over the R rows in a fixed order, are ADDED into dw_acc / db_acc [K, h]
+ * (the parameters' existing .grad, as autograd accumulates; either may be NULL). */
+gw_status gw_ln_relu_bwd(const float *dy, const float *z, const float *y, const float *ln_w, const float *mean,
+                         const float *rstd, float *dz, float *dw_acc, float *db_acc, int32_t K, int64_t R,
+                         int32_t h, void *stream);
+
+/* agilerl GumbelSoftmax (no gradient; the target actors' next actions in MADDPG.learn) over
+ * [rows, n] logits with uniforms u:  out = softmax((logits - log(-log(u + eps) + eps)) / tau). */
+gw_status gw_gumbel_softmax(const float *logits, const float *u, float *out, int64_t rows, int32_t n, float tau,
+                            float eps, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

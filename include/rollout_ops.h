@@ -37,6 +37,21 @@ gw_status gw_return_compact(const uint8_t *recv, int64_t steps, int32_t world, i
                             int64_t *n_completed, int32_t *scratch, void *stream);
 int64_t gw_return_compact_scratch(int64_t steps, int32_t world, int64_t emax);
 
+/* Replay-ring sample (agilerl MultiAgentReplayBuffer.sample, uniform; called at
+ * maddpg/agent.py:209-211; marlnav/rollout.py ReplayRing.sample) as ONE gather launch.  Ring
+ * layout: obs / final_obs [S, K, E, HW] (f32, or bf16 if obs_bf16), probs [S, K, E, 9] f32,
+ * reward [S, E, K] f64, term [S, E, K] u8, done [S, E] u8; *t_dev = transitions stored.  For each
+ * b < B:  n = clamp(*t_dev, 1, S - 1);  step = min((int64)(u[b] * (float)n), n - 1);
+ * tr = (*t_dev - 1 - step) mod S;  nx = (tr + 1) mod S;  e = env[b];  then
+ *   state[k, b] = obs[tr, k, e];  next[k, b] = done[tr, e] ? final_obs[tr, k, e] : obs[nx, k, e]
+ *   probs_out[k, b] = probs[tr, k, e];  reward_out[b] = reward[tr, e];  term_out[b] = term[tr, e]
+ * (outputs f32 [K, B, HW], [K, B, 9], f64 [B, K], u8 [B, K]); tr_out[b] = tr if tr_out != NULL. */
+gw_status gw_replay_gather(const void *obs, const void *final_obs, int32_t obs_bf16, const float *probs,
+                           const double *reward, const uint8_t *term, const uint8_t *done, const int64_t *t_dev,
+                           const float *u, const int64_t *env, int64_t S, int32_t K, int64_t E, int64_t HW,
+                           int64_t B, float *state, float *next_state, float *probs_out, double *reward_out,
+                           uint8_t *term_out, int64_t *tr_out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

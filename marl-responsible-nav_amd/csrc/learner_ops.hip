@@ -42,6 +42,153 @@ __global__ void __launch_bounds__(256) soft_update_kernel(float *__restrict__ t,
         t[i] = tau * p[i] + (1.0f - tau) * t[i];
 }
 
+// ---- hidden-layer epilogue of StackedMLPActors: y = relu(ln_b + layer_norm(z) * ln_w) ----------
+// One 64-lane wave per row (h <= LN_MAXV * 64 features, lane j holds features j, j + 64, ...);
+// the sums are wave butterflies in a fixed order, so results do not depend on the launch shape.
+constexpr int LN_MAXV = 8;
+
+__device__ inline float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__global__ void __launch_bounds__(256) ln_relu_fwd_kernel(const float *__restrict__ z, const float *__restrict__ w,
+                                                          const float *__restrict__ b, float *__restrict__ y,
+                                                          float *__restrict__ mean_out, float *__restrict__ rstd_out,
+                                                          int64_t R, int64_t rows, int h, float eps) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (row >= rows) return;  // uniform per wave
+    const int64_t k = row / R;
+    const float *zr = z + row * h;
+    float v[LN_MAXV];
+    float s = 0.0f;
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+        const int j = lane + 64 * i;
+        v[i] = j < h ? zr[j] : 0.0f;
+        s += v[i];
+    }
+    const float inv_h = 1.0f / (float)h;
+    const float mean = wave_sum(s) * inv_h;
+    float q = 0.0f;
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+        const float d = lane + 64 * i < h ? v[i] - mean : 0.0f;
+        q = __fmaf_rn(d, d, q);
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(q) * inv_h + eps);  // biased variance, as nn.LayerNorm
+    float *yr = y + row * h;
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+        const int j = lane + 64 * i;
+        if (j < h) {
+            const float o = __fmaf_rn((v[i] - mean) * rstd, w[k * h + j], b[k * h + j]);  // addcmul
+            yr[j] = o > 0.0f ? o : 0.0f;
+        }
+    }
+    if (mean_out && lane == 0) {
+        mean_out[row] = mean;
+        rstd_out[row] = rstd;
+    }
+}
+
+// Backward of the epilogue for the R rows of agent k = blockIdx.x (one block per agent, so the
+// ln_w / ln_b gradients are reduced over rows in a fixed order: deterministic, graph == eager).
+//   g = dy * (y > 0);  xhat = (z - mean) * rstd;  dW += sum_r g * xhat;  dB += sum_r g
+//   dxhat = g * w;  dz = rstd * (dxhat - mean_j(dxhat) - xhat * mean_j(dxhat * xhat))
+constexpr int LN_BWD_THREADS = 512;
+
+__global__ void __launch_bounds__(LN_BWD_THREADS) ln_relu_bwd_kernel(
+    const float *__restrict__ dy, const float *__restrict__ z, const float *__restrict__ y,
+    const float *__restrict__ w, const float *__restrict__ mean, const float *__restrict__ rstd,
+    float *__restrict__ dz, float *__restrict__ dw_acc, float *__restrict__ db_acc, int64_t R, int h) {
+    constexpr int NW = LN_BWD_THREADS / 64;
+    __shared__ float s_dw[NW][LN_MAXV * 64];
+    __shared__ float s_db[NW][LN_MAXV * 64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t k = blockIdx.x;
+    float wk[LN_MAXV], pdw[LN_MAXV], pdb[LN_MAXV];
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+        const int j = lane + 64 * i;
+        wk[i] = j < h ? w[k * h + j] : 0.0f;
+        pdw[i] = pdb[i] = 0.0f;
+    }
+    const float inv_h = 1.0f / (float)h;
+    for (int64_t r = wv; r < R; r += NW) {
+        const int64_t row = k * R + r;
+        const float m = mean[row], rs = rstd[row];
+        float xh[LN_MAXV], dxh[LN_MAXV];
+        float s1 = 0.0f, s2 = 0.0f;
+#pragma unroll
+        for (int i = 0; i < LN_MAXV; ++i) {
+            const int j = lane + 64 * i;
+            xh[i] = dxh[i] = 0.0f;
+            if (j < h) {
+                const int64_t o = row * h + j;
+                const float g = y[o] > 0.0f ? dy[o] : 0.0f;
+                xh[i] = (z[o] - m) * rs;
+                pdw[i] = __fmaf_rn(g, xh[i], pdw[i]);
+                pdb[i] += g;
+                dxh[i] = g * wk[i];
+                s1 += dxh[i];
+                s2 = __fmaf_rn(dxh[i], xh[i], s2);
+            }
+        }
+        const float m1 = wave_sum(s1) * inv_h, m2 = wave_sum(s2) * inv_h;
+#pragma unroll
+        for (int i = 0; i < LN_MAXV; ++i) {
+            const int j = lane + 64 * i;
+            if (j < h) dz[row * h + j] = rs * (dxh[i] - m1 - xh[i] * m2);
+        }
+    }
+    if (!dw_acc && !db_acc) return;  // uniform
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+        s_dw[wv][lane + 64 * i] = pdw[i];
+        s_db[wv][lane + 64 * i] = pdb[i];
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < h; j += LN_BWD_THREADS) {
+        float a = 0.0f, c = 0.0f;
+        for (int q = 0; q < NW; ++q) {
+            a += s_dw[q][j];
+            c += s_db[q][j];
+        }
+        if (dw_acc) dw_acc[k * h + j] += a;  // accumulates like autograd into an existing .grad
+        if (db_acc) db_acc[k * h + j] += c;
+    }
+}
+
+// agilerl GumbelSoftmax sample without gradient (the target actors' next actions):
+//   softmax((logits - log(-log(u + eps) + eps)) / tau) over the n entries of each row, each torch
+//   op one f32 rounding; one lane per row.
+__global__ void __launch_bounds__(256) gumbel_softmax_kernel(const float *__restrict__ logits,
+                                                             const float *__restrict__ u, float *__restrict__ out,
+                                                             int64_t rows, int n, float tau, float eps) {
+    const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (r >= rows) return;
+    const float *lr = logits + r * n;
+    const float *ur = u + r * n;
+    float *o = out + r * n;
+    float mx = -INFINITY;
+    for (int j = 0; j < n; ++j) {
+        const float g = logf(-logf(ur[j] + eps) + eps);
+        const float v = (lr[j] - g) / tau;
+        o[j] = v;
+        mx = fmaxf(mx, v);
+    }
+    float sum = 0.0f;
+    for (int j = 0; j < n; ++j) {
+        const float e = expf(o[j] - mx);
+        o[j] = e;
+        sum += e;
+    }
+    for (int j = 0; j < n; ++j) o[j] = o[j] / sum;
+}
+
 unsigned grid_for(int64_t n) {
     const int64_t blocks = (n + 255) / 256;
     return (unsigned)(blocks < 4096 ? (blocks > 0 ? blocks : 1) : 4096);
@@ -65,6 +212,37 @@ gw_status gw_soft_update(float *target, const float *online, int64_t n, float ta
     if (!target || !online || n < 0) return GW_ERR_ARG;
     hipLaunchKernelGGL(soft_update_kernel, dim3(grid_for(n)), dim3(256), 0, static_cast<hipStream_t>(stream),
                        target, online, n, tau);
+    return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
+}
+
+gw_status gw_ln_relu_fwd(const float *z, const float *ln_w, const float *ln_b, float *y, float *mean, float *rstd,
+                         int32_t K, int64_t R, int32_t h, float eps, void *stream) {
+    if (!z || !ln_w || !ln_b || !y || K < 0 || R < 0 || h <= 0 || h > LN_MAXV * 64 || (!mean) != (!rstd))
+        return GW_ERR_ARG;
+    const int64_t rows = (int64_t)K * R;
+    if (rows == 0) return GW_OK;
+    hipLaunchKernelGGL(ln_relu_fwd_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), z, ln_w, ln_b, y, mean, rstd, R, rows, (int)h, eps);
+    return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
+}
+
+gw_status gw_ln_relu_bwd(const float *dy, const float *z, const float *y, const float *ln_w, const float *mean,
+                         const float *rstd, float *dz, float *dw_acc, float *db_acc, int32_t K, int64_t R,
+                         int32_t h, void *stream) {
+    if (!dy || !z || !y || !ln_w || !mean || !rstd || !dz || K < 0 || R < 0 || h <= 0 || h > LN_MAXV * 64)
+        return GW_ERR_ARG;
+    if (K == 0) return GW_OK;
+    hipLaunchKernelGGL(ln_relu_bwd_kernel, dim3((unsigned)K), dim3(LN_BWD_THREADS), 0,
+                       static_cast<hipStream_t>(stream), dy, z, y, ln_w, mean, rstd, dz, dw_acc, db_acc, R, (int)h);
+    return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
+}
+
+gw_status gw_gumbel_softmax(const float *logits, const float *u, float *out, int64_t rows, int32_t n, float tau,
+                            float eps, void *stream) {
+    if (!logits || !u || !out || rows < 0 || n <= 0 || !(tau > 0.0f)) return GW_ERR_ARG;
+    if (rows == 0) return GW_OK;
+    hipLaunchKernelGGL(gumbel_softmax_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), logits, u, out, rows, (int)n, tau, eps);
     return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
 }
 

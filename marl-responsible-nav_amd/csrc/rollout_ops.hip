@@ -145,6 +145,48 @@ __global__ void __launch_bounds__(CT) compact_scatter(const uint8_t *__restrict_
     }
 }
 
+// ---- replay-ring sample: one block per (agent k, sample b) ----------------------------------
+__device__ inline float ring_obs(const void *p, int bf16, int64_t i) {
+    if (bf16) return __uint_as_float((uint32_t)static_cast<const uint16_t *>(p)[i] << 16);
+    return static_cast<const float *>(p)[i];
+}
+
+__global__ void __launch_bounds__(256) replay_gather_kernel(
+    const void *__restrict__ obs, const void *__restrict__ final_obs, int bf16, const float *__restrict__ probs,
+    const double *__restrict__ reward, const uint8_t *__restrict__ term, const uint8_t *__restrict__ done,
+    const int64_t *__restrict__ t_dev, const float *__restrict__ u, const int64_t *__restrict__ env, int64_t S,
+    int K, int64_t E, int64_t HW, int64_t B, float *__restrict__ state, float *__restrict__ next_state,
+    float *__restrict__ probs_out, double *__restrict__ reward_out, uint8_t *__restrict__ term_out,
+    int64_t *__restrict__ tr_out) {
+    const int64_t b = blockIdx.x;
+    const int k = blockIdx.y;
+    const int64_t t = t_dev[0];
+    const int64_t n = t < 1 ? 1 : (t > S - 1 ? S - 1 : t);
+    int64_t step = (int64_t)(u[b] * (float)n);  // torch: (rand * n).long(), then minimum(., n - 1)
+    if (step > n - 1) step = n - 1;
+    int64_t tr = (t - 1 - step) % S;
+    if (tr < 0) tr += S;  // Python / torch modulo
+    const int64_t nx = (tr + 1) % S;
+    const int64_t e = env[b];
+    const bool dn = done[tr * E + e] != 0;
+    const int64_t src = ((tr * K + k) * E + e) * HW;
+    const int64_t nsrc = dn ? src : ((nx * K + k) * E + e) * HW;
+    const void *nbuf = dn ? final_obs : obs;
+    float *so = state + (k * B + b) * HW;
+    float *no = next_state + (k * B + b) * HW;
+    for (int64_t i = threadIdx.x; i < HW; i += blockDim.x) {
+        so[i] = ring_obs(obs, bf16, src + i);
+        no[i] = ring_obs(nbuf, bf16, nsrc + i);
+    }
+    if (threadIdx.x < 9) probs_out[(k * B + b) * 9 + threadIdx.x] = probs[((tr * K + k) * E + e) * 9 + threadIdx.x];
+    if (k == 0 && threadIdx.x >= 64 && threadIdx.x < 64 + K) {
+        const int j = threadIdx.x - 64;
+        reward_out[b * K + j] = reward[(tr * E + e) * K + j];
+        term_out[b * K + j] = term[(tr * E + e) * K + j];
+    }
+    if (k == 0 && threadIdx.x == 128 && tr_out) tr_out[b] = tr;
+}
+
 }  // namespace
 
 extern "C" {
@@ -198,6 +240,22 @@ gw_status gw_return_compact(const uint8_t *recv, int64_t steps, int32_t world, i
 int64_t gw_return_compact_scratch(int64_t steps, int32_t world, int64_t emax) {
     const int64_t n = steps * (int64_t)world * emax;
     return 2 + (n + CCH - 1) / CCH;
+}
+
+gw_status gw_replay_gather(const void *obs, const void *final_obs, int32_t obs_bf16, const float *probs,
+                           const double *reward, const uint8_t *term, const uint8_t *done, const int64_t *t_dev,
+                           const float *u, const int64_t *env, int64_t S, int32_t K, int64_t E, int64_t HW,
+                           int64_t B, float *state, float *next_state, float *probs_out, double *reward_out,
+                           uint8_t *term_out, int64_t *tr_out, void *stream) {
+    if (!obs || !final_obs || !probs || !reward || !term || !done || !t_dev || !u || !env || !state || !next_state ||
+        !probs_out || !reward_out || !term_out || S < 2 || K <= 0 || K > 64 || E <= 0 || HW <= 0 || B < 0 ||
+        B > 0x7fffffff)
+        return GW_ERR_ARG;
+    if (B == 0) return GW_OK;
+    hipLaunchKernelGGL(replay_gather_kernel, dim3((unsigned)B, (unsigned)K), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), obs, final_obs, (int)obs_bf16, probs, reward, term, done,
+                       t_dev, u, env, S, (int)K, E, HW, B, state, next_state, probs_out, reward_out, term_out, tr_out);
+    return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
 }
 
 }  // extern "C"

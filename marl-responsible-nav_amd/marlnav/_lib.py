@@ -167,7 +167,9 @@ EXPORTS = ["gw_create", "gw_reset", "gw_step", "gw_state_view", "gw_copy_state",
            "gw_adam_step", "gw_soft_update", "gw_obs_view", "gw_set_last_error", "gw_actor_act",
            "gw_actor_workspace_floats", "gw_actor_prepare", "gw_rollout_tick", "gw_set_obs_async",
            "gw_obs_fence", "gw_fear_fence", "gw_set_obs_dtype", "gw_cnn_workspace_floats", "gw_cnn_prepare",
-           "gw_cnn_act", "gw_return_compact", "gw_return_compact_scratch", "gw_kernel_path", "gw_graph_replayed", "gw_obs_patch"]
+           "gw_cnn_act", "gw_return_compact", "gw_return_compact_scratch", "gw_kernel_path", "gw_graph_replayed", "gw_obs_patch",
+           "gw_ln_relu_fwd", "gw_ln_relu_bwd", "gw_gumbel_softmax",
+           "gw_replay_gather"]
 
 
 class GwObsSource(C.Structure):
@@ -233,6 +235,15 @@ def _declare(L):
     L.gw_adam_step.restype = C.c_int
     L.gw_soft_update.argtypes = [p, p, C.c_int64, C.c_float, p]
     L.gw_soft_update.restype = C.c_int
+    L.gw_ln_relu_fwd.argtypes = [p, p, p, p, p, p, C.c_int32, C.c_int64, C.c_int32, C.c_float, p]
+    L.gw_ln_relu_fwd.restype = C.c_int
+    L.gw_ln_relu_bwd.argtypes = [p] * 9 + [C.c_int32, C.c_int64, C.c_int32, p]
+    L.gw_ln_relu_bwd.restype = C.c_int
+    L.gw_gumbel_softmax.argtypes = [p, p, p, C.c_int64, C.c_int32, C.c_float, C.c_float, p]
+    L.gw_gumbel_softmax.restype = C.c_int
+    L.gw_replay_gather.argtypes = [p, p, C.c_int32] + [p] * 7 + [C.c_int64, C.c_int32, C.c_int64, C.c_int64,
+                                                                  C.c_int64] + [p] * 7
+    L.gw_replay_gather.restype = C.c_int
     L.gw_obs_view.argtypes = [p, C.POINTER(GwObsSource)]
     L.gw_obs_view.restype = C.c_int
     L.gw_set_last_error.argtypes = [C.c_char_p]

@@ -34,6 +34,73 @@ def _init_linear(K, fan_in, fan_out, gen=None):
     return w, b
 
 
+class _LnRelu(torch.autograd.Function):
+    """relu(ln_b + layer_norm(z) * ln_w) over [K, R, h] as the one-launch HIP epilogue
+    (gw_ln_relu_fwd / gw_ln_relu_bwd, include/learner_ops.h).  The backward adds the ln_w / ln_b
+    gradients straight into the parameters' preallocated .grad views of the flat gradient buffer
+    (what autograd's accumulation would do, minus its add launches) and returns None for them."""
+
+    @staticmethod
+    def forward(ctx, z, ln_w, ln_b, save=True):
+        # save: whether a backward can follow (grad mode is off inside forward, so the caller,
+        # ln_relu(), decides)
+        from . import _lib
+        K, R, h = z.shape
+        z = z.contiguous()
+        y = torch.empty_like(z)
+        stats = torch.empty((2, K, R), device=z.device, dtype=torch.float32) if save else None
+        s = torch.cuda.current_stream(z.device).cuda_stream
+        _lib.check(_lib.load().gw_ln_relu_fwd(z.data_ptr(), ln_w.data_ptr(), ln_b.data_ptr(), y.data_ptr(),
+                                              stats[0].data_ptr() if save else None,
+                                              stats[1].data_ptr() if save else None, K, R, h, 1e-5, s),
+                   "gw_ln_relu_fwd")
+        if save:
+            ctx.save_for_backward(z, y, ln_w, stats)
+            ctx.params = (ln_w, ln_b)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import _lib
+        z, y, ln_w, stats = ctx.saved_tensors
+        K, R, h = z.shape
+        dy = dy.contiguous()
+        dz = torch.empty_like(z)
+        out = []
+        for i, p in enumerate(ctx.params):
+            if not ctx.needs_input_grad[1 + i]:
+                out.append((None, None))
+            elif p.grad is not None and p.grad.is_contiguous():
+                out.append((p.grad, None))  # accumulate in place, return None
+            else:
+                g = torch.zeros_like(p)
+                out.append((g, g))
+        s = torch.cuda.current_stream(z.device).cuda_stream
+        _lib.check(_lib.load().gw_ln_relu_bwd(dy.data_ptr(), z.data_ptr(), y.data_ptr(), ln_w.data_ptr(),
+                                              stats[0].data_ptr(), stats[1].data_ptr(), dz.data_ptr(),
+                                              out[0][0].data_ptr() if out[0][0] is not None else None,
+                                              out[1][0].data_ptr() if out[1][0] is not None else None,
+                                              K, R, h, s), "gw_ln_relu_bwd")
+        return (dz if ctx.needs_input_grad[0] else None), out[0][1], out[1][1], None
+
+
+def ln_relu(z, ln_w, ln_b):
+    """relu(ln_b + layer_norm(z) * ln_w) through the HIP epilogue (_LnRelu)."""
+    save = torch.is_grad_enabled() and (z.requires_grad or ln_w.requires_grad or ln_b.requires_grad)
+    return _LnRelu.apply(z, ln_w, ln_b, save)
+
+
+def _fused_ln_ok(x: torch.Tensor) -> bool:
+    return x.is_cuda and x.dtype == torch.float32 and x.dim() == 3 and 0 < x.shape[-1] <= 512 and _FUSED_LN
+
+
+# Opt-in (GW_LN_FUSED=1): the batch-128 update 0.817 -> 0.764 ms, but its row statistics round
+# differently from torch's LayerNorm, so a ReLU mask at the rounding edge can flip and Adam's
+# normalised step turns that into a visible parameter difference against the per-agent torch
+# loop (tests/test_maddpg.py); the default keeps torch's LayerNorm on the learner path.
+_FUSED_LN = __import__("os").environ.get("GW_LN_FUSED", "0") == "1"
+
+
 class StackedMLPActors(nn.Module):
     """K independent MLPs evaluated together: x [K, E, D] -> [K, E, out] (out = 9 logits for an
     actor, 1 for a critic).
@@ -82,13 +149,21 @@ class StackedMLPActors(nn.Module):
         """The single flat Parameter (shares storage with every layer; .grad = flat gradients)."""
         return self._flat
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, pre: bool = False, frozen: bool = False) -> torch.Tensor:
+        """pre: x is already layer 0's pre-activation (its GEMM + bias done by the caller).
+        frozen: the parameters enter as constants (no parameter gradients are formed; gradients
+        still flow to x)."""
         n = self.n_layers
+        P = (lambda t: t.detach()) if frozen else (lambda t: t)
         for i in range(n):
-            x = torch.baddbmm(self.biases[i], x, self.weights[i])
+            if i > 0 or not pre:
+                x = torch.baddbmm(P(self.biases[i]), x, P(self.weights[i]))
             if i < n - 1:
+                if self.layer_norm and _fused_ln_ok(x):  # one HIP launch (and one for its backward)
+                    x = ln_relu(x, P(self.ln_w[i]), P(self.ln_b[i]))
+                    continue
                 if self.layer_norm:  # nn.LayerNorm(h), eps 1e-5, per-agent affine
-                    x = torch.addcmul(self.ln_b[i], F.layer_norm(x, (x.shape[-1],)), self.ln_w[i])
+                    x = torch.addcmul(P(self.ln_b[i]), F.layer_norm(x, (x.shape[-1],)), P(self.ln_w[i]))
                 x = F.relu(x)
         return x
 

@@ -41,6 +41,15 @@ def gumbel_softmax(logits: torch.Tensor, u: torch.Tensor | None = None, tau: flo
     """agilerl's GumbelSoftmax output activation: softmax((logits - log(-log(u + eps) + eps)) / tau)."""
     if u is None:
         u = torch.rand(logits.shape, device=logits.device, dtype=logits.dtype, generator=generator)
+    if logits.is_cuda and not (torch.is_grad_enabled() and logits.requires_grad) and logits.dtype == torch.float32:
+        # no gradient needed (the target actions): one HIP launch instead of seven torch ops
+        logits, u = logits.contiguous(), u.contiguous()
+        out = torch.empty_like(logits)
+        n = logits.shape[-1]
+        _lib.check(_lib.load().gw_gumbel_softmax(logits.data_ptr(), u.data_ptr(), out.data_ptr(), logits.numel() // n,
+                                                 n, tau, eps, torch.cuda.current_stream(logits.device).cuda_stream),
+                   "gw_gumbel_softmax")
+        return out
     return F.softmax((logits - torch.log(-torch.log(u + eps) + eps)) / tau, dim=-1)
 
 
@@ -143,12 +152,18 @@ class MADDPG:
         self.opt_critic.step()
 
         probs = gumbel_softmax(self.actors(states), u_cur)                             # [K, B, 9]
-        xs = x.detach().unsqueeze(0).repeat(K, 1, 1)                                   # [K, B, D + K*9]
-        eye = torch.eye(K, device=x.device, dtype=x.dtype)                             # agent k's slot
-        a_rep = actions.permute(1, 0, 2).unsqueeze(0).expand(K, -1, -1, -1)           # [K, B, K, 9]
-        a_mix = a_rep * (1 - eye)[:, None, :, None] + probs.unsqueeze(2) * eye[:, None, :, None]
-        xs = torch.cat([xs[..., :D], a_mix.reshape(K, B, -1)], -1)
-        actor_loss = -self.critics(xs).mean(dim=(1, 2))
+        # a_mix[k] = the replayed actions with agent k's slot replaced by its fresh probs
+        a_mix = actions.permute(1, 0, 2).unsqueeze(0).repeat(K, 1, 1, 1)              # [K, B, K, 9]
+        a_mix.diagonal(dim1=0, dim2=2).copy_(probs.permute(1, 2, 0))
+        # The actor loss needs gradients for the actors only: the critics' parameter
+        # gradients this backward would form are dead (zeroed before the next critic step),
+        # so the critics enter as constants, and critic layer 1 is split into its state
+        # columns (no gradient path) and its action columns (the only path to the actors).
+        c = self.critics
+        w1 = c.weights[0].detach()
+        z1 = torch.baddbmm(c.biases[0].detach(), x[:, :D].detach().unsqueeze(0).expand(K, -1, -1), w1[:, :D])
+        z1 = torch.baddbmm(z1, a_mix.reshape(K, B, -1), w1[:, D:])
+        actor_loss = -c(z1, pre=True, frozen=True).mean(dim=(1, 2))
         self.opt_actor.zero_grad(set_to_none=False)
         actor_loss.sum().backward()
         self.opt_actor.step()

@@ -56,6 +56,8 @@ class ReplayRing:
         if self.t <= 0:
             raise RuntimeError("empty replay ring")
         dev = self.obs.device
+        if dev.type == "cuda":
+            return self._sample_hip(batch, generator, return_idx)
         n = torch.clamp(self.t_dev, min=1, max=self.S - 1)
         step = torch.minimum((torch.rand((batch,), device=dev, generator=generator) * n).long(), n - 1)
         env = torch.randint(0, self.E, (batch,), device=dev, generator=generator)
@@ -66,6 +68,28 @@ class ReplayRing:
         next_state = torch.where(done[None, :, None, None], self.final_obs[tr, :, env].permute(1, 0, 2, 3),
                                  self.obs[nx, :, env].permute(1, 0, 2, 3)).float()
         out = (state, self.probs[tr, :, env].permute(1, 0, 2), self.reward[tr, env], next_state, self.term[tr, env])
+        return out + ((tr, env),) if return_idx else out
+
+    def _sample_hip(self, batch, generator, return_idx):
+        """sample() on the GPU: the same draws (torch.rand, then torch.randint), then the index
+        arithmetic and every gather in ONE launch (gw_replay_gather, include/rollout_ops.h)."""
+        dev = self.obs.device
+        u = torch.rand((batch,), device=dev, generator=generator)
+        env = torch.randint(0, self.E, (batch,), device=dev, generator=generator)
+        K, HW = self.K, self.obs.shape[-2] * self.obs.shape[-1]
+        state = torch.empty((K, batch) + tuple(self.obs.shape[-2:]), device=dev, dtype=torch.float32)
+        next_state = torch.empty_like(state)
+        probs = torch.empty((K, batch, 9), device=dev, dtype=torch.float32)
+        reward = torch.empty((batch, K), device=dev, dtype=torch.float64)
+        term = torch.empty((batch, K), device=dev, dtype=torch.uint8)
+        tr = torch.empty((batch,), device=dev, dtype=torch.int64) if return_idx else None
+        _lib.check(_lib.load().gw_replay_gather(
+            self.obs.data_ptr(), self.final_obs.data_ptr(), int(self.obs.dtype == torch.bfloat16),
+            self.probs.data_ptr(), self.reward.data_ptr(), self.term.data_ptr(), self.done.data_ptr(),
+            self.t_dev.data_ptr(), u.data_ptr(), env.data_ptr(), self.S, K, self.E, HW, batch, state.data_ptr(),
+            next_state.data_ptr(), probs.data_ptr(), reward.data_ptr(), term.data_ptr(),
+            tr.data_ptr() if return_idx else None, torch.cuda.current_stream(dev).cuda_stream), "gw_replay_gather")
+        out = (state, probs, reward, next_state, term)
         return out + ((tr, env),) if return_idx else out
 
 
