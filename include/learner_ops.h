@@ -38,6 +38,17 @@ gw_status gw_ln_relu_bwd(const float *dy, const float *z, const float *y, const 
                          const float *rstd, float *dz, float *dw_acc, float *db_acc, int32_t K, int64_t R,
                          int32_t h, void *stream);
 
+/* The affine + ReLU half of that epilogue after torch's own (non-affine) F.layer_norm, so the
+ * normalised rows stay torch's bit for bit (the default learner path): xhat, y [K, R, h],
+ * ln_w / ln_b [K, h];  y = relu(fma(xhat, ln_w, ln_b))  (torch.addcmul contracted, then relu). */
+gw_status gw_affine_relu_fwd(const float *xhat, const float *ln_w, const float *ln_b, float *y, int32_t K, int64_t R,
+                             int32_t h, void *stream);
+
+/* Its backward: g = dy * (y > 0);  dxhat = g * ln_w (if dxhat != NULL);  the row sums of g * xhat
+ * and g ADDED into dw_acc / db_acc [K, h] (either may be NULL), in a fixed order. */
+gw_status gw_affine_relu_bwd(const float *dy, const float *xhat, const float *y, const float *ln_w, float *dxhat,
+                             float *dw_acc, float *db_acc, int32_t K, int64_t R, int32_t h, void *stream);
+
 /* agilerl GumbelSoftmax (no gradient; the target actors' next actions in MADDPG.learn) over
  * [rows, n] logits with uniforms u:  out = softmax((logits - log(-log(u + eps) + eps)) / tau). */
 gw_status gw_gumbel_softmax(const float *logits, const float *u, float *out, int64_t rows, int32_t n, float tau,

@@ -84,7 +84,7 @@ __global__ void __launch_bounds__(256) ln_relu_fwd_kernel(const float *__restric
     for (int i = 0; i < LN_MAXV; ++i) {
         const int j = lane + 64 * i;
         if (j < h) {
-            const float o = __fmaf_rn((v[i] - mean) * rstd, w[k * h + j], b[k * h + j]);  // addcmul
+            const float o = (v[i] - mean) * rstd * w[k * h + j] + b[k * h + j];  // addcmul: two roundings
             yr[j] = o > 0.0f ? o : 0.0f;
         }
     }
@@ -189,6 +189,63 @@ __global__ void __launch_bounds__(256) gumbel_softmax_kernel(const float *__rest
     for (int j = 0; j < n; ++j) o[j] = o[j] / sum;
 }
 
+// ---- affine + ReLU after torch's (non-affine) layer_norm: y = relu(ln_b + xhat * ln_w) ----------
+// Forward: torch's addcmul (self + t1 * t2: the product rounded, then the sum) then relu, one launch.
+__global__ void __launch_bounds__(256) affine_relu_fwd_kernel(const float *__restrict__ xh, const float *__restrict__ w,
+                                                              const float *__restrict__ b, float *__restrict__ y,
+                                                              int64_t R, int64_t n, int h) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = i / (R * h);
+        const int j = (int)(i % h);
+        const float o = xh[i] * w[k * h + j] + b[k * h + j];  // two roundings (file built -ffp-contract=off)
+        y[i] = o > 0.0f ? o : 0.0f;
+    }
+}
+
+// Backward for block (column chunk of 64, agent k): g = dy * (y > 0); dxh = g * w;
+// dW += sum_r g * xh; dB += sum_r g.  AR_RG row groups of 64 columns each (1024 threads), rows
+// strided over the groups with the loads of 4 rows in flight per thread; the group partials are
+// combined in a fixed order (deterministic).
+constexpr int AR_RG = 16;
+
+__global__ void __launch_bounds__(AR_RG * 64) affine_relu_bwd_kernel(const float *__restrict__ dy,
+                                                                    const float *__restrict__ xh,
+                                                                    const float *__restrict__ y,
+                                                                    const float *__restrict__ w,
+                                                                    float *__restrict__ dxh, float *__restrict__ dw_acc,
+                                                                    float *__restrict__ db_acc, int64_t R, int h) {
+    __shared__ float s_dw[AR_RG][64], s_db[AR_RG][64];
+    const int c = threadIdx.x & 63, rg = threadIdx.x >> 6;
+    const int j = blockIdx.x * 64 + c;
+    const int64_t k = blockIdx.y;
+    const bool ok = j < h;
+    const float wj = ok ? w[k * h + j] : 0.0f;
+    float pdw = 0.0f, pdb = 0.0f;
+    if (ok) {
+        const int64_t base = k * R * h + j;
+#pragma unroll 4
+        for (int64_t r = rg; r < R; r += AR_RG) {
+            const int64_t o = base + r * h;
+            const float g = y[o] > 0.0f ? dy[o] : 0.0f;
+            if (dxh) dxh[o] = g * wj;
+            pdw = __fmaf_rn(g, xh[o], pdw);
+            pdb += g;
+        }
+    }
+    s_dw[rg][c] = pdw;
+    s_db[rg][c] = pdb;
+    __syncthreads();
+    if (rg == 0 && ok) {
+        float a = 0.0f, d = 0.0f;
+        for (int q = 0; q < AR_RG; ++q) {
+            a += s_dw[q][c];
+            d += s_db[q][c];
+        }
+        if (dw_acc) dw_acc[k * h + j] += a;
+        if (db_acc) db_acc[k * h + j] += d;
+    }
+}
+
 unsigned grid_for(int64_t n) {
     const int64_t blocks = (n + 255) / 256;
     return (unsigned)(blocks < 4096 ? (blocks > 0 ? blocks : 1) : 4096);
@@ -243,6 +300,25 @@ gw_status gw_gumbel_softmax(const float *logits, const float *u, float *out, int
     if (rows == 0) return GW_OK;
     hipLaunchKernelGGL(gumbel_softmax_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0,
                        static_cast<hipStream_t>(stream), logits, u, out, rows, (int)n, tau, eps);
+    return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
+}
+
+gw_status gw_affine_relu_fwd(const float *xhat, const float *ln_w, const float *ln_b, float *y, int32_t K, int64_t R,
+                             int32_t h, void *stream) {
+    if (!xhat || !ln_w || !ln_b || !y || K < 0 || R < 0 || h <= 0) return GW_ERR_ARG;
+    const int64_t n = (int64_t)K * R * h;
+    if (n == 0) return GW_OK;
+    hipLaunchKernelGGL(affine_relu_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, static_cast<hipStream_t>(stream), xhat,
+                       ln_w, ln_b, y, R, n, (int)h);
+    return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
+}
+
+gw_status gw_affine_relu_bwd(const float *dy, const float *xhat, const float *y, const float *ln_w, float *dxhat,
+                             float *dw_acc, float *db_acc, int32_t K, int64_t R, int32_t h, void *stream) {
+    if (!dy || !xhat || !y || !ln_w || K < 0 || R < 0 || h <= 0) return GW_ERR_ARG;
+    if ((int64_t)K * R == 0) return GW_OK;
+    hipLaunchKernelGGL(affine_relu_bwd_kernel, dim3((unsigned)((h + 63) / 64), (unsigned)K), dim3(AR_RG * 64), 0,
+                       static_cast<hipStream_t>(stream), dy, xhat, y, ln_w, dxhat, dw_acc, db_acc, R, (int)h);
     return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
 }
 

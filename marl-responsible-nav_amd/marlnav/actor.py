@@ -90,6 +90,63 @@ def ln_relu(z, ln_w, ln_b):
     return _LnRelu.apply(z, ln_w, ln_b, save)
 
 
+class _AffineRelu(torch.autograd.Function):
+    """relu(ln_b + xhat * ln_w) after torch's own F.layer_norm (gw_affine_relu_fwd / _bwd): the
+    addcmul + relu and their backward (relu mask, addcmul's three products, the two row
+    reductions and autograd's accumulation adds) as one launch each; the normalised rows are
+    torch's, so the forward equals the torch composition bit for bit.  Parameter gradients are
+    added into the preallocated .grad views like _LnRelu."""
+
+    @staticmethod
+    def forward(ctx, xhat, ln_w, ln_b, save=True):
+        from . import _lib
+        K, R, h = xhat.shape
+        xhat = xhat.contiguous()
+        y = torch.empty_like(xhat)
+        _lib.check(_lib.load().gw_affine_relu_fwd(xhat.data_ptr(), ln_w.data_ptr(), ln_b.data_ptr(), y.data_ptr(), K, R,
+                                                  h, torch.cuda.current_stream(xhat.device).cuda_stream),
+                   "gw_affine_relu_fwd")
+        if save:
+            ctx.save_for_backward(xhat, y, ln_w)
+            ctx.params = (ln_w, ln_b)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import _lib
+        xhat, y, ln_w = ctx.saved_tensors
+        K, R, h = xhat.shape
+        dy = dy.contiguous()
+        dx = torch.empty_like(xhat) if ctx.needs_input_grad[0] else None
+        out = []
+        for i, p in enumerate(ctx.params):
+            if not ctx.needs_input_grad[1 + i]:
+                out.append((None, None))
+            elif p.grad is not None and p.grad.is_contiguous():
+                out.append((p.grad, None))
+            else:
+                g = torch.zeros_like(p)
+                out.append((g, g))
+        _lib.check(_lib.load().gw_affine_relu_bwd(
+            dy.data_ptr(), xhat.data_ptr(), y.data_ptr(), ln_w.data_ptr(), dx.data_ptr() if dx is not None else None,
+            out[0][0].data_ptr() if out[0][0] is not None else None,
+            out[1][0].data_ptr() if out[1][0] is not None else None, K, R, h,
+            torch.cuda.current_stream(xhat.device).cuda_stream), "gw_affine_relu_bwd")
+        return dx, out[0][1], out[1][1], None
+
+
+def affine_relu(xhat, ln_w, ln_b):
+    save = torch.is_grad_enabled() and (xhat.requires_grad or ln_w.requires_grad or ln_b.requires_grad)
+    return _AffineRelu.apply(xhat, ln_w, ln_b, save)
+
+
+def _affine_ok(x: torch.Tensor) -> bool:
+    return x.is_cuda and x.dtype == torch.float32 and x.dim() == 3 and _AFFINE
+
+
+_AFFINE = __import__("os").environ.get("GW_AFFINE_FUSED", "1") != "0"
+
+
 def _fused_ln_ok(x: torch.Tensor) -> bool:
     return x.is_cuda and x.dtype == torch.float32 and x.dim() == 3 and 0 < x.shape[-1] <= 512 and _FUSED_LN
 
@@ -161,6 +218,9 @@ class StackedMLPActors(nn.Module):
             if i < n - 1:
                 if self.layer_norm and _fused_ln_ok(x):  # one HIP launch (and one for its backward)
                     x = ln_relu(x, P(self.ln_w[i]), P(self.ln_b[i]))
+                    continue
+                if self.layer_norm and _affine_ok(x):  # torch's layer_norm, then one HIP launch
+                    x = affine_relu(F.layer_norm(x, (x.shape[-1],)), P(self.ln_w[i]), P(self.ln_b[i]))
                     continue
                 if self.layer_norm:  # nn.LayerNorm(h), eps 1e-5, per-agent affine
                     x = torch.addcmul(P(self.ln_b[i]), F.layer_norm(x, (x.shape[-1],)), P(self.ln_w[i]))

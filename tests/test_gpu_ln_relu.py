@@ -94,3 +94,32 @@ def test_gumbel_softmax_hip_matches_torch(rows, n):
     lg = logits.clone().requires_grad_(True)  # with a gradient the torch ops run (and backprop)
     gumbel_softmax(lg, u, tau=0.7).sum().backward()
     assert lg.grad is not None
+
+
+@pytest.mark.parametrize("K,R,h", [(2, 128, 128), (3, 37, 100), (1, 5, 200)])
+def test_affine_relu_matches_torch(K, R, h):
+    """gw_affine_relu_fwd / _bwd (the default learner epilogue after torch's F.layer_norm) ==
+    addcmul + relu: the forward bit for bit; the input gradient bit for bit; the affine
+    gradients (row sums in another order) within 1e-5 relative."""
+    from marlnav.actor import affine_relu
+    g = torch.Generator(device="cuda").manual_seed(K * 7 + h)
+    xh0 = torch.randn((K, R, h), device="cuda", generator=g)
+    w0 = torch.randn((K, 1, h), device="cuda", generator=g)
+    b0 = torch.randn((K, 1, h), device="cuda", generator=g) * 0.3
+    dy = torch.randn((K, R, h), device="cuda", generator=g)
+    pre_w = torch.randn((K, 1, h), device="cuda", generator=g)
+    pre_b = torch.randn((K, 1, h), device="cuda", generator=g)
+    xr, wr, br = (t.clone().requires_grad_(True) for t in (xh0, w0, b0))
+    yr = torch.relu(torch.addcmul(br, xr, wr))
+    wr.grad, br.grad = pre_w.clone(), pre_b.clone()
+    yr.backward(dy)
+    x, w, b = (t.clone().requires_grad_(True) for t in (xh0, w0, b0))
+    w.grad, b.grad = pre_w.clone(), pre_b.clone()
+    y = affine_relu(x, w, b)
+    # torch's addcmul on ROCm rounds the product, then the sum (no fma contraction): measured
+    assert torch.equal(yr.detach(), torch.relu(xh0 * w0 + b0))
+    assert torch.equal(y, yr.detach())
+    y.backward(dy)
+    assert torch.equal(x.grad, xr.grad)
+    torch.testing.assert_close(w.grad, wr.grad, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(b.grad, br.grad, rtol=1e-5, atol=1e-5)
