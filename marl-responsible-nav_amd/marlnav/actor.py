@@ -140,6 +140,47 @@ def affine_relu(xhat, ln_w, ln_b):
     return _AffineRelu.apply(xhat, ln_w, ln_b, save)
 
 
+class _StackedLinear(torch.autograd.Function):
+    """baddbmm(b, x, w) whose backward writes the parameter gradients straight into their
+    preallocated .grad views: W.grad += x^T dy as ONE GEMM with beta = 1, b.grad += 1^T dy as
+    another (autograd's version is GEMM + add and reduction + add)."""
+
+    _ones = {}
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.params = (w, b)
+        return torch.baddbmm(b, x, w)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        wp, bp = ctx.params
+        dx = torch.bmm(dy, w.transpose(1, 2)) if ctx.needs_input_grad[0] else None
+        gw = gb = None
+        if ctx.needs_input_grad[1]:
+            if wp.grad is not None:
+                wp.grad.baddbmm_(x.transpose(1, 2), dy)
+            else:
+                gw = torch.bmm(x.transpose(1, 2), dy)
+        if ctx.needs_input_grad[2]:
+            K, R = dy.shape[0], dy.shape[1]
+            key = (K, R, dy.device, dy.dtype)
+            ones = _StackedLinear._ones.get(key)
+            if ones is None:
+                ones = _StackedLinear._ones[key] = torch.ones((K, 1, R), device=dy.device, dtype=dy.dtype)
+            if bp.grad is not None:
+                bp.grad.baddbmm_(ones, dy)
+            else:
+                gb = torch.bmm(ones, dy)
+        return dx, gw, gb
+
+
+def _linear_ok(x: torch.Tensor) -> bool:
+    return x.is_cuda and _AFFINE and torch.is_grad_enabled()
+
+
 def _affine_ok(x: torch.Tensor) -> bool:
     return x.is_cuda and x.dtype == torch.float32 and x.dim() == 3 and _AFFINE
 
@@ -214,7 +255,10 @@ class StackedMLPActors(nn.Module):
         P = (lambda t: t.detach()) if frozen else (lambda t: t)
         for i in range(n):
             if i > 0 or not pre:
-                x = torch.baddbmm(P(self.biases[i]), x, P(self.weights[i]))
+                if not frozen and _linear_ok(x) and self.weights[i].requires_grad:
+                    x = _StackedLinear.apply(x, self.weights[i], self.biases[i])
+                else:
+                    x = torch.baddbmm(P(self.biases[i]), x, P(self.weights[i]))
             if i < n - 1:
                 if self.layer_norm and _fused_ln_ok(x):  # one HIP launch (and one for its backward)
                     x = ln_relu(x, P(self.ln_w[i]), P(self.ln_b[i]))
