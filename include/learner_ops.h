@@ -50,9 +50,11 @@ gw_status gw_affine_relu_bwd(const float *dy, const float *xhat, const float *y,
                              float *dw_acc, float *db_acc, int32_t K, int64_t R, int32_t h, void *stream);
 
 /* agilerl GumbelSoftmax (no gradient; the target actors' next actions in MADDPG.learn) over
- * [rows, n] logits with uniforms u:  out = softmax((logits - log(-log(u + eps) + eps)) / tau). */
+ * [rows, n] logits with uniforms u:  out = softmax((logits - log(-log(u + eps) + eps)) / tau).
+ * out_ld == 0: out is [rows, n].  out_ld > 0: row r = k * out_b + b is written at
+ * out + b * out_ld + k * n (straight into the action slots of the critic's input rows). */
 gw_status gw_gumbel_softmax(const float *logits, const float *u, float *out, int64_t rows, int32_t n, float tau,
-                            float eps, void *stream);
+                            float eps, int64_t out_b, int64_t out_ld, void *stream);
 
 #ifdef __cplusplus
 }

@@ -45,12 +45,16 @@ int64_t gw_return_compact_scratch(int64_t steps, int32_t world, int64_t emax);
  * tr = (*t_dev - 1 - step) mod S;  nx = (tr + 1) mod S;  e = env[b];  then
  *   state[k, b] = obs[tr, k, e];  next[k, b] = done[tr, e] ? final_obs[tr, k, e] : obs[nx, k, e]
  *   probs_out[k, b] = probs[tr, k, e];  reward_out[b] = reward[tr, e];  term_out[b] = term[tr, e]
- * (outputs f32 [K, B, HW], [K, B, 9], f64 [B, K], u8 [B, K]); tr_out[b] = tr if tr_out != NULL. */
+ * (outputs f32 [K, B, HW], [K, B, 9], f64 [B, K], u8 [B, K]); tr_out[b] = tr if tr_out != NULL.
+ * x_out / xn_out (may be NULL): the critic's input rows [B, K*HW + K*9] of MADDPG.learn, agent-major
+ * states then the K action slots (agilerl's torch.cat of states and actions):
+ *   x_out[b] = [state[0, b] .. state[K-1, b], probs_out[0, b] .. probs_out[K-1, b]];
+ *   xn_out[b][0, K*HW) = next_state[., b] (its action slots are left to the caller). */
 gw_status gw_replay_gather(const void *obs, const void *final_obs, int32_t obs_bf16, const float *probs,
                            const double *reward, const uint8_t *term, const uint8_t *done, const int64_t *t_dev,
                            const float *u, const int64_t *env, int64_t S, int32_t K, int64_t E, int64_t HW,
                            int64_t B, float *state, float *next_state, float *probs_out, double *reward_out,
-                           uint8_t *term_out, int64_t *tr_out, void *stream);
+                           uint8_t *term_out, int64_t *tr_out, float *x_out, float *xn_out, void *stream);
 
 #ifdef __cplusplus
 }

@@ -167,12 +167,14 @@ __global__ void __launch_bounds__(LN_BWD_THREADS) ln_relu_bwd_kernel(
 //   op one f32 rounding; one lane per row.
 __global__ void __launch_bounds__(256) gumbel_softmax_kernel(const float *__restrict__ logits,
                                                              const float *__restrict__ u, float *__restrict__ out,
-                                                             int64_t rows, int n, float tau, float eps) {
+                                                             int64_t rows, int n, float tau, float eps,
+                                                             int64_t out_b, int64_t out_ld) {
     const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (r >= rows) return;
     const float *lr = logits + r * n;
     const float *ur = u + r * n;
-    float *o = out + r * n;
+    // out_ld > 0: row r = k * out_b + b goes to out + b * out_ld + k * n (a critic-input slot)
+    float *o = out_ld > 0 ? out + (r % out_b) * out_ld + (r / out_b) * n : out + r * n;
     float mx = -INFINITY;
     for (int j = 0; j < n; ++j) {
         const float g = logf(-logf(ur[j] + eps) + eps);
@@ -295,11 +297,11 @@ gw_status gw_ln_relu_bwd(const float *dy, const float *z, const float *y, const 
 }
 
 gw_status gw_gumbel_softmax(const float *logits, const float *u, float *out, int64_t rows, int32_t n, float tau,
-                            float eps, void *stream) {
-    if (!logits || !u || !out || rows < 0 || n <= 0 || !(tau > 0.0f)) return GW_ERR_ARG;
+                            float eps, int64_t out_b, int64_t out_ld, void *stream) {
+    if (!logits || !u || !out || rows < 0 || n <= 0 || !(tau > 0.0f) || (out_ld > 0 && out_b <= 0)) return GW_ERR_ARG;
     if (rows == 0) return GW_OK;
     hipLaunchKernelGGL(gumbel_softmax_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0,
-                       static_cast<hipStream_t>(stream), logits, u, out, rows, (int)n, tau, eps);
+                       static_cast<hipStream_t>(stream), logits, u, out, rows, (int)n, tau, eps, out_b, out_ld);
     return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
 }
 

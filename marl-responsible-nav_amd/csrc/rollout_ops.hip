@@ -157,7 +157,7 @@ __global__ void __launch_bounds__(256) replay_gather_kernel(
     const int64_t *__restrict__ t_dev, const float *__restrict__ u, const int64_t *__restrict__ env, int64_t S,
     int K, int64_t E, int64_t HW, int64_t B, float *__restrict__ state, float *__restrict__ next_state,
     float *__restrict__ probs_out, double *__restrict__ reward_out, uint8_t *__restrict__ term_out,
-    int64_t *__restrict__ tr_out) {
+    int64_t *__restrict__ tr_out, float *__restrict__ x_out, float *__restrict__ xn_out) {
     const int64_t b = blockIdx.x;
     const int k = blockIdx.y;
     const int64_t t = t_dev[0];
@@ -174,11 +174,22 @@ __global__ void __launch_bounds__(256) replay_gather_kernel(
     const void *nbuf = dn ? final_obs : obs;
     float *so = state + (k * B + b) * HW;
     float *no = next_state + (k * B + b) * HW;
+    // the critic's input rows [B, K*HW + K*9] (agent-major states, then the K action slots)
+    const int64_t ldx = (int64_t)K * HW + (int64_t)K * 9;
+    float *xo = x_out ? x_out + b * ldx + (int64_t)k * HW : nullptr;
+    float *xno = xn_out ? xn_out + b * ldx + (int64_t)k * HW : nullptr;
     for (int64_t i = threadIdx.x; i < HW; i += blockDim.x) {
-        so[i] = ring_obs(obs, bf16, src + i);
-        no[i] = ring_obs(nbuf, bf16, nsrc + i);
+        const float sv = ring_obs(obs, bf16, src + i), nv = ring_obs(nbuf, bf16, nsrc + i);
+        so[i] = sv;
+        no[i] = nv;
+        if (xo) xo[i] = sv;
+        if (xno) xno[i] = nv;
     }
-    if (threadIdx.x < 9) probs_out[(k * B + b) * 9 + threadIdx.x] = probs[((tr * K + k) * E + e) * 9 + threadIdx.x];
+    if (threadIdx.x < 9) {
+        const float pv = probs[((tr * K + k) * E + e) * 9 + threadIdx.x];
+        probs_out[(k * B + b) * 9 + threadIdx.x] = pv;
+        if (x_out) x_out[b * ldx + (int64_t)K * HW + k * 9 + threadIdx.x] = pv;
+    }
     if (k == 0 && threadIdx.x >= 64 && threadIdx.x < 64 + K) {
         const int j = threadIdx.x - 64;
         reward_out[b * K + j] = reward[(tr * E + e) * K + j];
@@ -246,7 +257,7 @@ gw_status gw_replay_gather(const void *obs, const void *final_obs, int32_t obs_b
                            const double *reward, const uint8_t *term, const uint8_t *done, const int64_t *t_dev,
                            const float *u, const int64_t *env, int64_t S, int32_t K, int64_t E, int64_t HW,
                            int64_t B, float *state, float *next_state, float *probs_out, double *reward_out,
-                           uint8_t *term_out, int64_t *tr_out, void *stream) {
+                           uint8_t *term_out, int64_t *tr_out, float *x_out, float *xn_out, void *stream) {
     if (!obs || !final_obs || !probs || !reward || !term || !done || !t_dev || !u || !env || !state || !next_state ||
         !probs_out || !reward_out || !term_out || S < 2 || K <= 0 || K > 64 || E <= 0 || HW <= 0 || B < 0 ||
         B > 0x7fffffff)
@@ -254,7 +265,8 @@ gw_status gw_replay_gather(const void *obs, const void *final_obs, int32_t obs_b
     if (B == 0) return GW_OK;
     hipLaunchKernelGGL(replay_gather_kernel, dim3((unsigned)B, (unsigned)K), dim3(256), 0,
                        static_cast<hipStream_t>(stream), obs, final_obs, (int)obs_bf16, probs, reward, term, done,
-                       t_dev, u, env, S, (int)K, E, HW, B, state, next_state, probs_out, reward_out, term_out, tr_out);
+                       t_dev, u, env, S, (int)K, E, HW, B, state, next_state, probs_out, reward_out, term_out, tr_out,
+                       x_out, xn_out);
     return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
 }
 

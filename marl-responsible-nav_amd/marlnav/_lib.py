@@ -239,14 +239,14 @@ def _declare(L):
     L.gw_ln_relu_fwd.restype = C.c_int
     L.gw_ln_relu_bwd.argtypes = [p] * 9 + [C.c_int32, C.c_int64, C.c_int32, p]
     L.gw_ln_relu_bwd.restype = C.c_int
-    L.gw_gumbel_softmax.argtypes = [p, p, p, C.c_int64, C.c_int32, C.c_float, C.c_float, p]
+    L.gw_gumbel_softmax.argtypes = [p, p, p, C.c_int64, C.c_int32, C.c_float, C.c_float, C.c_int64, C.c_int64, p]
     L.gw_gumbel_softmax.restype = C.c_int
     L.gw_affine_relu_fwd.argtypes = [p, p, p, p, C.c_int32, C.c_int64, C.c_int32, p]
     L.gw_affine_relu_fwd.restype = C.c_int
     L.gw_affine_relu_bwd.argtypes = [p] * 7 + [C.c_int32, C.c_int64, C.c_int32, p]
     L.gw_affine_relu_bwd.restype = C.c_int
     L.gw_replay_gather.argtypes = [p, p, C.c_int32] + [p] * 7 + [C.c_int64, C.c_int32, C.c_int64, C.c_int64,
-                                                                  C.c_int64] + [p] * 7
+                                                                  C.c_int64] + [p] * 9
     L.gw_replay_gather.restype = C.c_int
     L.gw_obs_view.argtypes = [p, C.POINTER(GwObsSource)]
     L.gw_obs_view.restype = C.c_int

@@ -36,6 +36,19 @@ from . import _lib
 from .actor import N_ACTIONS, MultiAgentActors, StackedMLPActors
 
 
+def _gumbel_into_slots(logits: torch.Tensor, u: torch.Tensor | None, x_next: torch.Tensor, D: int):
+    """GumbelSoftmax of the target logits [K, B, 9] written straight into the action slots
+    x_next[:, D:] of the critic's input rows [B, D + K*9] (gw_gumbel_softmax, strided output)."""
+    K, B, n = logits.shape
+    logits = logits.contiguous()
+    if u is None:
+        u = torch.rand(logits.shape, device=logits.device, dtype=logits.dtype)
+    u = u.contiguous()
+    _lib.check(_lib.load().gw_gumbel_softmax(logits.data_ptr(), u.data_ptr(), x_next[:, D:].data_ptr(), K * B, n, 1.0,
+                                             1e-20, B, x_next.shape[1],
+                                             torch.cuda.current_stream(logits.device).cuda_stream), "gw_gumbel_softmax")
+
+
 def gumbel_softmax(logits: torch.Tensor, u: torch.Tensor | None = None, tau: float = 1.0, eps: float = 1e-20,
                    generator: torch.Generator | None = None) -> torch.Tensor:
     """agilerl's GumbelSoftmax output activation: softmax((logits - log(-log(u + eps) + eps)) / tau)."""
@@ -47,7 +60,7 @@ def gumbel_softmax(logits: torch.Tensor, u: torch.Tensor | None = None, tau: flo
         out = torch.empty_like(logits)
         n = logits.shape[-1]
         _lib.check(_lib.load().gw_gumbel_softmax(logits.data_ptr(), u.data_ptr(), out.data_ptr(), logits.numel() // n,
-                                                 n, tau, eps, torch.cuda.current_stream(logits.device).cuda_stream),
+                                                 n, tau, eps, 0, 0, torch.cuda.current_stream(logits.device).cuda_stream),
                    "gw_gumbel_softmax")
         return out
     return F.softmax((logits - torch.log(-torch.log(u + eps) + eps)) / tau, dim=-1)
@@ -130,21 +143,28 @@ class MADDPG:
         a = actions.permute(1, 0, 2).reshape(B, -1)
         return torch.cat([s, a], 1)
 
-    def learn(self, states, actions, rewards, next_states, dones, u_next=None, u_cur=None):
+    def learn(self, states, actions, rewards, next_states, dones, u_next=None, u_cur=None, critic_in=None):
         """One MADDPG update from a sampled batch.  states/next_states [K, B, H, W] f32, actions
         [K, B, 9] (stored GumbelSoftmax probabilities), rewards [B, K], dones [B, K] (termination).
         u_next / u_cur: optional uniforms [K, B, 9] for the two Gumbel samples (tests).
+        critic_in: optional (x, x_next) critic input rows from ReplayRing.sample(critic_in=True)
+        (GPU): the same values this method would assemble, without the permute / cat copies.
         Returns (actor_loss [K], critic_loss [K]) device tensors (no host sync)."""
         K, B = states.shape[0], states.shape[1]
         D = K * self.H * self.W
         r = rewards.to(torch.float32).t().unsqueeze(-1)          # [K, B, 1]
         d = dones.to(torch.float32).t().unsqueeze(-1)
         with torch.no_grad():
-            a_next = gumbel_softmax(self.actor_targets(next_states), u_next)          # [K, B, 9]
-            x_next = self._critic_in(next_states, a_next)
+            if critic_in is not None:
+                x, x_next = critic_in
+                _gumbel_into_slots(self.actor_targets(next_states), u_next, x_next, D)
+            else:
+                a_next = gumbel_softmax(self.actor_targets(next_states), u_next)      # [K, B, 9]
+                x_next = self._critic_in(next_states, a_next)
             q_next = self.critic_targets(x_next.unsqueeze(0).expand(K, -1, -1))     # [K, B, 1]
             y = r + (1.0 - d) * self.gamma * q_next
-        x = self._critic_in(states, actions)
+        if critic_in is None:
+            x = self._critic_in(states, actions)
         q = self.critics(x.unsqueeze(0).expand(K, -1, -1))
         critic_loss = ((q - y) ** 2).mean(dim=(1, 2))                                # MSELoss per agent
         self.opt_critic.zero_grad(set_to_none=False)
@@ -190,6 +210,9 @@ class MADDPG:
     # ---------------------------------------------------------------------------------------
     def learn_from(self, replay, generator: torch.Generator | None = None):
         """Sample ``batch_size`` transitions from a ReplayRing and learn (eager)."""
+        if self.device.type == "cuda":  # the critic's input rows come from the gather launch
+            *batch, ci = replay.sample(self.batch_size, generator=generator, critic_in=True)
+            return self.learn(*batch, critic_in=ci)
         return self.learn(*replay.sample(self.batch_size, generator=generator))
 
     def capture(self, replay, warmup: int = 3):

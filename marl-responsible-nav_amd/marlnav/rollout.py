@@ -49,15 +49,18 @@ class ReplayRing:
         return min(self.t, self.S - 1) * self.E
 
     @torch.no_grad()
-    def sample(self, batch: int, generator: torch.Generator | None = None, return_idx: bool = False):
+    def sample(self, batch: int, generator: torch.Generator | None = None, return_idx: bool = False,
+               critic_in: bool = False):
         """Uniform transitions -> (state [K,B,H,W], probs [K,B,9], reward [B,K], next_state, term [B,K]).
         Every index is computed on the device from ``t_dev``, so a captured graph stays valid as
-        the ring fills (MultiAgentReplayBuffer.sample, uniform without priorities)."""
+        the ring fills (MultiAgentReplayBuffer.sample, uniform without priorities).
+        critic_in (GPU): also return the critic's input rows (x, x_next) that MADDPG.learn would
+        build from them, from the same gather launch (x_next's action slots left to the learner)."""
         if self.t <= 0:
             raise RuntimeError("empty replay ring")
         dev = self.obs.device
         if dev.type == "cuda":
-            return self._sample_hip(batch, generator, return_idx)
+            return self._sample_hip(batch, generator, return_idx, critic_in)
         n = torch.clamp(self.t_dev, min=1, max=self.S - 1)
         step = torch.minimum((torch.rand((batch,), device=dev, generator=generator) * n).long(), n - 1)
         env = torch.randint(0, self.E, (batch,), device=dev, generator=generator)
@@ -70,7 +73,7 @@ class ReplayRing:
         out = (state, self.probs[tr, :, env].permute(1, 0, 2), self.reward[tr, env], next_state, self.term[tr, env])
         return out + ((tr, env),) if return_idx else out
 
-    def _sample_hip(self, batch, generator, return_idx):
+    def _sample_hip(self, batch, generator, return_idx, critic_in=False):
         """sample() on the GPU: the same draws (torch.rand, then torch.randint), then the index
         arithmetic and every gather in ONE launch (gw_replay_gather, include/rollout_ops.h)."""
         dev = self.obs.device
@@ -83,14 +86,21 @@ class ReplayRing:
         reward = torch.empty((batch, K), device=dev, dtype=torch.float64)
         term = torch.empty((batch, K), device=dev, dtype=torch.uint8)
         tr = torch.empty((batch,), device=dev, dtype=torch.int64) if return_idx else None
+        x = xn = None
+        if critic_in:
+            x = torch.empty((batch, K * HW + K * 9), device=dev, dtype=torch.float32)
+            xn = torch.empty_like(x)
         _lib.check(_lib.load().gw_replay_gather(
             self.obs.data_ptr(), self.final_obs.data_ptr(), int(self.obs.dtype == torch.bfloat16),
             self.probs.data_ptr(), self.reward.data_ptr(), self.term.data_ptr(), self.done.data_ptr(),
             self.t_dev.data_ptr(), u.data_ptr(), env.data_ptr(), self.S, K, self.E, HW, batch, state.data_ptr(),
             next_state.data_ptr(), probs.data_ptr(), reward.data_ptr(), term.data_ptr(),
-            tr.data_ptr() if return_idx else None, torch.cuda.current_stream(dev).cuda_stream), "gw_replay_gather")
+            tr.data_ptr() if return_idx else None, x.data_ptr() if critic_in else None,
+            xn.data_ptr() if critic_in else None, torch.cuda.current_stream(dev).cuda_stream), "gw_replay_gather")
         out = (state, probs, reward, next_state, term)
-        return out + ((tr, env),) if return_idx else out
+        if return_idx:
+            out = out + ((tr, env),)
+        return out + ((x, xn),) if critic_in else out
 
 
 class Rollout:

@@ -227,3 +227,36 @@ def test_checkpoint_roundtrip(tmp_path):
         assert torch.equal(a, b)
     m3 = copy.deepcopy(m2)
     assert torch.equal(m3.actors.net.weights[0], m.actors.net.weights[0])
+
+
+@pytest.mark.gpu
+def test_gpu_learn_from_critic_rows_equals_assembled():
+    """ReplayRing.sample(critic_in=True) returns the critic's input rows that MADDPG.learn would
+    assemble (agent-major states + the stored action probabilities) bit for bit, and learning
+    from them (target actions written into x_next's slots by gw_gumbel_softmax) leaves every
+    network bit-identical to the assembling path."""
+    from marlnav.rollout import Rollout
+    from marlnav.vec_env import VecGridEnv
+    env = VecGridEnv("grid32", num_envs=256, fear=True, fear_weight=-5.0, seed=1, stats=True, final_obs=True)
+    ms = [MADDPG(env.K, env.H, env.W, device="cuda", seed=1) for _ in range(2)]
+    ro = Rollout(env, ms[0].actors, replay_slots=8, training=True, seed=2)
+    ro.reset()
+    for _ in range(12):
+        ro.step()
+    ro.fence()
+    for it in range(3):
+        g = torch.Generator(device="cuda").manual_seed(10 + it)
+        *batch, (x, xn) = ro.replay.sample(64, generator=g, critic_in=True)
+        states, actions, rewards, next_states, dones = batch
+        assert torch.equal(x, ms[1]._critic_in(states, actions))
+        D = env.K * env.H * env.W
+        assert torch.equal(xn[:, :D], next_states.reshape(env.K, 64, -1).permute(1, 0, 2).reshape(64, -1))
+        u_next = torch.rand((env.K, 64, 9), device="cuda", generator=g)
+        u_cur = torch.rand((env.K, 64, 9), device="cuda", generator=g)
+        la = ms[0].learn(*batch, u_next=u_next, u_cur=u_cur, critic_in=(x, xn))
+        lb = ms[1].learn(*batch, u_next=u_next, u_cur=u_cur)
+        assert torch.equal(la[0], lb[0]) and torch.equal(la[1], lb[1])
+    for a, b in ((ms[0].actors.net, ms[1].actors.net), (ms[0].critics, ms[1].critics),
+                 (ms[0].actor_targets.net, ms[1].actor_targets.net), (ms[0].critic_targets, ms[1].critic_targets)):
+        assert torch.equal(a.flat_params(), b.flat_params())
+    env.close()
