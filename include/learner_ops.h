@@ -23,6 +23,16 @@ gw_status gw_adam_step(float *param, const float *grad, float *exp_avg, float *e
 /* agilerl soft_update: target = tau * online + (1 - tau) * target on n elements. */
 gw_status gw_soft_update(float *target, const float *online, int64_t n, float tau, void *stream);
 
+/* Both soft target updates of one learn (the actor and critic buffers) in one launch. */
+gw_status gw_soft_update2(float *target1, const float *online1, int64_t n1, float *target2, const float *online2,
+                          int64_t n2, float tau, void *stream);
+
+/* TD target of MADDPG.learn (agilerl: y = r + (1 - d) * gamma * Q'(s', a')):  rewards [B, K] f64
+ * (shaped), dones [B, K] u8 (termination), q_next / y [K, B] f32;  y[k, b] = f32(r[b, k]) +
+ * ((1 - d[b, k]) * gamma) * q_next[k, b], one f32 rounding per op as torch evaluates it. */
+gw_status gw_td_target(const double *rewards, const uint8_t *dones, const float *q_next, float gamma, float *y,
+                       int32_t K, int64_t B, void *stream);
+
 /* Hidden-layer epilogue of the stacked MLPs (agilerl EvolvableMLP: Linear -> LayerNorm -> ReLU;
  * marlnav/actor.py StackedMLPActors.forward, replacing F.layer_norm + addcmul + relu, three
  * launches, by one).  z, y [K, R, h] contiguous, ln_w / ln_b [K, h]; 0 < h <= 512.

@@ -248,6 +248,32 @@ __global__ void __launch_bounds__(AR_RG * 64) affine_relu_bwd_kernel(const float
     }
 }
 
+// Two soft target updates (actor and critic buffers) in one launch.
+__global__ void __launch_bounds__(256) soft_update2_kernel(float *__restrict__ t1, const float *__restrict__ p1, int64_t n1,
+                                                           float *__restrict__ t2, const float *__restrict__ p2, int64_t n2,
+                                                           float tau) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n1 + n2; i += (int64_t)gridDim.x * blockDim.x) {
+        if (i < n1)
+            t1[i] = tau * p1[i] + (1.0f - tau) * t1[i];
+        else
+            t2[i - n1] = tau * p2[i - n1] + (1.0f - tau) * t2[i - n1];
+    }
+}
+
+// TD target of MADDPG.learn: y[k, b] = r + (1 - d) * gamma * q_next in torch's op order, one
+// f32 rounding per op (r: the f64 shaped reward rounded to f32).
+__global__ void __launch_bounds__(256) td_target_kernel(const double *__restrict__ r, const uint8_t *__restrict__ d,
+                                                        const float *__restrict__ q_next, float gamma,
+                                                        float *__restrict__ y, int K, int64_t B) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;  // i = k * B + b
+    if (i >= (int64_t)K * B) return;
+    const int64_t k = i / B, b = i % B;
+    const float t1 = 1.0f - (float)d[b * K + k];
+    const float t2 = t1 * gamma;
+    const float t3 = t2 * q_next[i];
+    y[i] = (float)r[b * K + k] + t3;
+}
+
 unsigned grid_for(int64_t n) {
     const int64_t blocks = (n + 255) / 256;
     return (unsigned)(blocks < 4096 ? (blocks > 0 ? blocks : 1) : 4096);
@@ -321,6 +347,24 @@ gw_status gw_affine_relu_bwd(const float *dy, const float *xhat, const float *y,
     if ((int64_t)K * R == 0) return GW_OK;
     hipLaunchKernelGGL(affine_relu_bwd_kernel, dim3((unsigned)((h + 63) / 64), (unsigned)K), dim3(AR_RG * 64), 0,
                        static_cast<hipStream_t>(stream), dy, xhat, y, ln_w, dxhat, dw_acc, db_acc, R, (int)h);
+    return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
+}
+
+gw_status gw_soft_update2(float *target1, const float *online1, int64_t n1, float *target2, const float *online2,
+                          int64_t n2, float tau, void *stream) {
+    if (!target1 || !online1 || !target2 || !online2 || n1 < 0 || n2 < 0) return GW_ERR_ARG;
+    hipLaunchKernelGGL(soft_update2_kernel, dim3(grid_for(n1 + n2)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       target1, online1, n1, target2, online2, n2, tau);
+    return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
+}
+
+gw_status gw_td_target(const double *rewards, const uint8_t *dones, const float *q_next, float gamma, float *y,
+                       int32_t K, int64_t B, void *stream) {
+    if (!rewards || !dones || !q_next || !y || K <= 0 || B < 0) return GW_ERR_ARG;
+    const int64_t n = (int64_t)K * B;
+    if (n == 0) return GW_OK;
+    hipLaunchKernelGGL(td_target_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), rewards, dones, q_next, gamma, y, (int)K, B);
     return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
 }
 

@@ -152,8 +152,6 @@ class MADDPG:
         Returns (actor_loss [K], critic_loss [K]) device tensors (no host sync)."""
         K, B = states.shape[0], states.shape[1]
         D = K * self.H * self.W
-        r = rewards.to(torch.float32).t().unsqueeze(-1)          # [K, B, 1]
-        d = dones.to(torch.float32).t().unsqueeze(-1)
         with torch.no_grad():
             if critic_in is not None:
                 x, x_next = critic_in
@@ -162,7 +160,7 @@ class MADDPG:
                 a_next = gumbel_softmax(self.actor_targets(next_states), u_next)      # [K, B, 9]
                 x_next = self._critic_in(next_states, a_next)
             q_next = self.critic_targets(x_next.unsqueeze(0).expand(K, -1, -1))     # [K, B, 1]
-            y = r + (1.0 - d) * self.gamma * q_next
+            y = self._td_target(rewards, dones, q_next)
         if critic_in is None:
             x = self._critic_in(states, actions)
         q = self.critics(x.unsqueeze(0).expand(K, -1, -1))
@@ -190,17 +188,32 @@ class MADDPG:
         self.soft_update()
         return actor_loss.detach(), critic_loss.detach()
 
+    def _td_target(self, rewards, dones, q_next):
+        """y = r + (1 - d) * gamma * q_next  ([K, B, 1]; rewards f64 / dones [B, K])."""
+        if self.flat and rewards.dtype == torch.float64 and dones.dtype == torch.uint8:
+            q_next = q_next.contiguous()
+            y = torch.empty_like(q_next)
+            _lib.check(_lib.load().gw_td_target(rewards.contiguous().data_ptr(), dones.contiguous().data_ptr(),
+                                                q_next.data_ptr(), self.gamma, y.data_ptr(), q_next.shape[0],
+                                                q_next.shape[1], torch.cuda.current_stream(self.device).cuda_stream),
+                       "gw_td_target")
+            return y
+        r = rewards.to(torch.float32).t().unsqueeze(-1)          # [K, B, 1]
+        d = dones.to(torch.float32).t().unsqueeze(-1)
+        return r + (1.0 - d) * self.gamma * q_next
+
     @torch.no_grad()
     def soft_update(self):
         """agilerl soft_update: target <- tau * online + (1 - tau) * target (flat: one gw_soft_update
         launch per network; otherwise two foreach kernels)."""
         if self.flat:
             s = torch.cuda.current_stream(self.device).cuda_stream
-            lib = _lib.load()
-            for net, tgt in ((self.actors.net, self.actor_targets.net), (self.critics, self.critic_targets)):
-                t, p = tgt.flat_params(), net.flat_params()
-                _lib.check(lib.gw_soft_update(t.data_ptr(), p.data_ptr(), t.numel(), self.tau, s), "gw_soft_update")
-                tgt.epoch += 1
+            t1, p1 = self.actor_targets.net.flat_params(), self.actors.net.flat_params()
+            t2, p2 = self.critic_targets.flat_params(), self.critics.flat_params()
+            _lib.check(_lib.load().gw_soft_update2(t1.data_ptr(), p1.data_ptr(), t1.numel(), t2.data_ptr(),
+                                                   p2.data_ptr(), t2.numel(), self.tau, s), "gw_soft_update2")
+            self.actor_targets.net.epoch += 1
+            self.critic_targets.epoch += 1
             return
         src = list(self.actors.parameters()) + list(self.critics.parameters())
         dst = list(self.actor_targets.parameters()) + list(self.critic_targets.parameters())

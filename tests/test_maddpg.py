@@ -260,3 +260,27 @@ def test_gpu_learn_from_critic_rows_equals_assembled():
                  (ms[0].actor_targets.net, ms[1].actor_targets.net), (ms[0].critic_targets, ms[1].critic_targets)):
         assert torch.equal(a.flat_params(), b.flat_params())
     env.close()
+
+
+@pytest.mark.gpu
+def test_gpu_td_target_and_paired_soft_update_bit_exact():
+    """gw_td_target == torch's r + (1 - d) * gamma * q_next (f64 reward and u8 done converted to
+    f32 first) bit for bit; gw_soft_update2 == two gw_soft_update launches bit for bit."""
+    from marlnav import _lib
+    K, B = 2, 128
+    m = MADDPG(K, 4, 4, device="cuda", seed=0)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    rewards = torch.randn((B, K), generator=g, dtype=torch.float64, device="cuda") * 37
+    dones = (torch.rand((B, K), generator=g, device="cuda") < 0.3).to(torch.uint8)
+    q_next = torch.randn((K, B, 1), generator=g, device="cuda") * 11
+    want = rewards.to(torch.float32).t().unsqueeze(-1) + (1.0 - dones.to(torch.float32).t().unsqueeze(-1)) * m.gamma * q_next
+    assert torch.equal(m._td_target(rewards, dones, q_next), want)
+    lib, s = _lib.load(), torch.cuda.current_stream().cuda_stream
+    t1, p1 = torch.randn(1001, device="cuda", generator=g), torch.randn(1001, device="cuda", generator=g)
+    t2, p2 = torch.randn(70_000, device="cuda", generator=g), torch.randn(70_000, device="cuda", generator=g)
+    a1, a2 = t1.clone(), t2.clone()
+    _lib.check(lib.gw_soft_update(a1.data_ptr(), p1.data_ptr(), 1001, 0.01, s), "gw_soft_update")
+    _lib.check(lib.gw_soft_update(a2.data_ptr(), p2.data_ptr(), 70_000, 0.01, s), "gw_soft_update")
+    _lib.check(lib.gw_soft_update2(t1.data_ptr(), p1.data_ptr(), 1001, t2.data_ptr(), p2.data_ptr(), 70_000, 0.01, s),
+               "gw_soft_update2")
+    assert torch.equal(t1, a1) and torch.equal(t2, a2)
