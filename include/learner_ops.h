@@ -33,6 +33,15 @@ gw_status gw_soft_update2(float *target1, const float *online1, int64_t n1, floa
 gw_status gw_td_target(const double *rewards, const uint8_t *dones, const float *q_next, float gamma, float *y,
                        int32_t K, int64_t B, void *stream);
 
+/* The per-agent losses of MADDPG.learn over q [K, B] (one value per row):  mode 0 the critic's
+ * MSELoss  loss[k] = mean_b (q - y)^2;  mode 1 the actor's  loss[k] = -mean_b q  (y unused).
+ * The backward writes dq [K, B] from grad_loss [K]:  (g / B) * (2 (q - y))  or  -(g / B), the
+ * op order of torch's mean / pow / neg backward. */
+gw_status gw_mean_loss_fwd(const float *q, const float *y, float *loss, int32_t K, int64_t B, int32_t mode,
+                           void *stream);
+gw_status gw_mean_loss_bwd(const float *q, const float *y, const float *grad_loss, float *dq, int32_t K, int64_t B,
+                           int32_t mode, void *stream);
+
 /* Hidden-layer epilogue of the stacked MLPs (agilerl EvolvableMLP: Linear -> LayerNorm -> ReLU;
  * marlnav/actor.py StackedMLPActors.forward, replacing F.layer_norm + addcmul + relu, three
  * launches, by one).  z, y [K, R, h] contiguous, ln_w / ln_b [K, h]; 0 < h <= 512.

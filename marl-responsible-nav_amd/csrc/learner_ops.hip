@@ -274,6 +274,41 @@ __global__ void __launch_bounds__(256) td_target_kernel(const double *__restrict
     y[i] = (float)r[b * K + k] + t3;
 }
 
+// Per-agent losses of MADDPG.learn over q [K, B]: mode 0 MSE (mean_b (q - y)^2, the critic),
+// mode 1 -mean_b q (the actor).  Forward: one 256-thread block per agent (fixed-order sum).
+// Backward: dq[k, b] = (g[k] / B) * (2 (q - y)) or -(g[k] / B), torch's op order bit for bit.
+__global__ void __launch_bounds__(256) mean_loss_fwd_kernel(const float *__restrict__ q, const float *__restrict__ y,
+                                                            float *__restrict__ loss, int64_t B, int mode) {
+    __shared__ float part[256];
+    const int64_t k = blockIdx.x;
+    float acc = 0.0f;
+    for (int64_t b = threadIdx.x; b < B; b += 256) {
+        const float v = q[k * B + b];
+        if (mode == 0) {
+            const float d = v - y[k * B + b];
+            acc += d * d;
+        } else {
+            acc += v;
+        }
+    }
+    part[threadIdx.x] = acc;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) part[threadIdx.x] += part[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) loss[k] = mode == 0 ? part[0] / (float)B : -(part[0] / (float)B);
+}
+
+__global__ void __launch_bounds__(256) mean_loss_bwd_kernel(const float *__restrict__ q, const float *__restrict__ y,
+                                                            const float *__restrict__ g, float *__restrict__ dq,
+                                                            int64_t B, int64_t n, int mode) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float a = g[i / B] / (float)B;
+    dq[i] = mode == 0 ? a * (2.0f * (q[i] - y[i])) : -a;
+}
+
 unsigned grid_for(int64_t n) {
     const int64_t blocks = (n + 255) / 256;
     return (unsigned)(blocks < 4096 ? (blocks > 0 ? blocks : 1) : 4096);
@@ -365,6 +400,23 @@ gw_status gw_td_target(const double *rewards, const uint8_t *dones, const float 
     if (n == 0) return GW_OK;
     hipLaunchKernelGGL(td_target_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                        static_cast<hipStream_t>(stream), rewards, dones, q_next, gamma, y, (int)K, B);
+    return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
+}
+
+gw_status gw_mean_loss_fwd(const float *q, const float *y, float *loss, int32_t K, int64_t B, int32_t mode,
+                           void *stream) {
+    if (!q || !loss || (mode == 0 && !y) || mode < 0 || mode > 1 || K <= 0 || B <= 0) return GW_ERR_ARG;
+    hipLaunchKernelGGL(mean_loss_fwd_kernel, dim3((unsigned)K), dim3(256), 0, static_cast<hipStream_t>(stream), q, y,
+                       loss, B, (int)mode);
+    return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
+}
+
+gw_status gw_mean_loss_bwd(const float *q, const float *y, const float *grad_loss, float *dq, int32_t K, int64_t B,
+                           int32_t mode, void *stream) {
+    if (!q || !grad_loss || !dq || (mode == 0 && !y) || mode < 0 || mode > 1 || K <= 0 || B <= 0) return GW_ERR_ARG;
+    const int64_t n = (int64_t)K * B;
+    hipLaunchKernelGGL(mean_loss_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), q, y, grad_loss, dq, B, n, (int)mode);
     return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
 }
 

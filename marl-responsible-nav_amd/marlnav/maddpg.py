@@ -36,6 +36,35 @@ from . import _lib
 from .actor import N_ACTIONS, MultiAgentActors, StackedMLPActors
 
 
+class _MeanLoss(torch.autograd.Function):
+    """Per-agent loss over q [K, B, 1]: MSE against y (mode 0) or -mean q (mode 1), forward and
+    backward one launch each (gw_mean_loss_fwd / _bwd); the gradient is torch's bit for bit."""
+
+    @staticmethod
+    def forward(ctx, q, y, mode):
+        K, B = q.shape[0], q.shape[1]
+        q = q.contiguous()
+        y = y.contiguous() if y is not None else None
+        loss = torch.empty((K,), device=q.device, dtype=q.dtype)
+        _lib.check(_lib.load().gw_mean_loss_fwd(q.data_ptr(), y.data_ptr() if y is not None else None, loss.data_ptr(),
+                                                K, B, mode, torch.cuda.current_stream(q.device).cuda_stream),
+                   "gw_mean_loss_fwd")
+        ctx.save_for_backward(q, y) if y is not None else ctx.save_for_backward(q)
+        ctx.mode = mode
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        saved = ctx.saved_tensors
+        q, y = saved[0], (saved[1] if len(saved) > 1 else None)
+        K, B = q.shape[0], q.shape[1]
+        dq = torch.empty_like(q)
+        _lib.check(_lib.load().gw_mean_loss_bwd(q.data_ptr(), y.data_ptr() if y is not None else None,
+                                                g.contiguous().data_ptr(), dq.data_ptr(), K, B, ctx.mode,
+                                                torch.cuda.current_stream(q.device).cuda_stream), "gw_mean_loss_bwd")
+        return dq, None, None
+
+
 def _gumbel_into_slots(logits: torch.Tensor, u: torch.Tensor | None, x_next: torch.Tensor, D: int):
     """GumbelSoftmax of the target logits [K, B, 9] written straight into the action slots
     x_next[:, D:] of the critic's input rows [B, D + K*9] (gw_gumbel_softmax, strided output)."""
@@ -164,7 +193,10 @@ class MADDPG:
         if critic_in is None:
             x = self._critic_in(states, actions)
         q = self.critics(x.unsqueeze(0).expand(K, -1, -1))
-        critic_loss = ((q - y) ** 2).mean(dim=(1, 2))                                # MSELoss per agent
+        if self.flat:
+            critic_loss = _MeanLoss.apply(q, y, 0)                                    # MSELoss per agent
+        else:
+            critic_loss = ((q - y) ** 2).mean(dim=(1, 2))
         self.opt_critic.zero_grad(set_to_none=False)
         critic_loss.sum().backward()
         self.opt_critic.step()
@@ -181,7 +213,8 @@ class MADDPG:
         w1 = c.weights[0].detach()
         z1 = torch.baddbmm(c.biases[0].detach(), x[:, :D].detach().unsqueeze(0).expand(K, -1, -1), w1[:, :D])
         z1 = torch.baddbmm(z1, a_mix.reshape(K, B, -1), w1[:, D:])
-        actor_loss = -c(z1, pre=True, frozen=True).mean(dim=(1, 2))
+        qa = c(z1, pre=True, frozen=True)
+        actor_loss = _MeanLoss.apply(qa, None, 1) if self.flat else -qa.mean(dim=(1, 2))
         self.opt_actor.zero_grad(set_to_none=False)
         actor_loss.sum().backward()
         self.opt_actor.step()

@@ -284,3 +284,23 @@ def test_gpu_td_target_and_paired_soft_update_bit_exact():
     _lib.check(lib.gw_soft_update2(t1.data_ptr(), p1.data_ptr(), 1001, t2.data_ptr(), p2.data_ptr(), 70_000, 0.01, s),
                "gw_soft_update2")
     assert torch.equal(t1, a1) and torch.equal(t2, a2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B", [128, 100])
+def test_gpu_mean_losses_match_torch(B):
+    """gw_mean_loss_fwd / _bwd (the critic's MSELoss and the actor's -mean Q per agent): the
+    gradient equals torch's bit for bit; the loss values (another summation order) within 1e-6
+    relative."""
+    from marlnav.maddpg import _MeanLoss
+    g = torch.Generator(device="cuda").manual_seed(B)
+    q0 = torch.randn((3, B, 1), generator=g, device="cuda") * 5
+    y = torch.randn((3, B, 1), generator=g, device="cuda") * 5
+    for mode in (0, 1):
+        qa, qb = q0.clone().requires_grad_(True), q0.clone().requires_grad_(True)
+        la = _MeanLoss.apply(qa, y if mode == 0 else None, mode)
+        lb = ((qb - y) ** 2).mean(dim=(1, 2)) if mode == 0 else -qb.mean(dim=(1, 2))
+        torch.testing.assert_close(la, lb, rtol=1e-6, atol=1e-6)
+        la.sum().backward()
+        lb.sum().backward()
+        assert torch.equal(qa.grad, qb.grad)
