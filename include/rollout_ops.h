@@ -56,6 +56,13 @@ gw_status gw_replay_gather(const void *obs, const void *final_obs, int32_t obs_b
                            int64_t B, float *state, float *next_state, float *probs_out, double *reward_out,
                            uint8_t *term_out, int64_t *tr_out, float *x_out, float *xn_out, void *stream);
 
+/* One evaluation step's totals (customeval.py:70-133 over E episodes at once; marlnav/evaluate.py):
+ * for every env e with active[e]:  counts[0] += crashes[e];  counts[1] += apples[e];
+ * counts[2] += 1;  *fear_total += sum_k fear[e, k];  then active[e] = 0 if done[e].
+ * crashes / apples [E] i32, fear [E, K] f64, done / active [E] u8.  One block, fixed order. */
+gw_status gw_eval_accum(const int32_t *crashes, const int32_t *apples, const double *fear, const uint8_t *done,
+                        uint8_t *active, int64_t *counts, double *fear_total, int64_t E, int32_t K, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

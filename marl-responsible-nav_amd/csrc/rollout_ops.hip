@@ -198,6 +198,52 @@ __global__ void __launch_bounds__(256) replay_gather_kernel(
     if (k == 0 && threadIdx.x == 128 && tr_out) tr_out[b] = tr;
 }
 
+// ---- evaluation totals (customeval.py:70-133): one 1024-thread block, fixed-order sums ------------
+constexpr int EV_T = 1024;
+
+__global__ void __launch_bounds__(EV_T) eval_accum_kernel(const int32_t *__restrict__ crashes,
+                                                           const int32_t *__restrict__ apples,
+                                                           const double *__restrict__ fear, const uint8_t *__restrict__ done,
+                                                           uint8_t *__restrict__ active, int64_t *__restrict__ counts,
+                                                           double *__restrict__ fear_total, int64_t E, int K) {
+    __shared__ int64_t s_c[EV_T], s_a[EV_T], s_s[EV_T];
+    __shared__ double s_f[EV_T];
+    int64_t c = 0, a = 0, n = 0;
+    double fs = 0.0;
+    for (int64_t e = threadIdx.x; e < E; e += EV_T) {
+        if (active[e]) {
+            c += crashes[e];
+            a += apples[e];
+            n += 1;
+            double fe = 0.0;
+            for (int k = 0; k < K; ++k) fe += fear[e * K + k];
+            fs += fe;
+            if (done[e]) active[e] = 0;
+        }
+    }
+    const int t = threadIdx.x;
+    s_c[t] = c;
+    s_a[t] = a;
+    s_s[t] = n;
+    s_f[t] = fs;
+    __syncthreads();
+    for (int o = EV_T / 2; o > 0; o >>= 1) {
+        if (t < o) {
+            s_c[t] += s_c[t + o];
+            s_a[t] += s_a[t + o];
+            s_s[t] += s_s[t + o];
+            s_f[t] += s_f[t + o];
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        counts[0] += s_c[0];
+        counts[1] += s_a[0];
+        counts[2] += s_s[0];
+        fear_total[0] += s_f[0];
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -267,6 +313,15 @@ gw_status gw_replay_gather(const void *obs, const void *final_obs, int32_t obs_b
                        static_cast<hipStream_t>(stream), obs, final_obs, (int)obs_bf16, probs, reward, term, done,
                        t_dev, u, env, S, (int)K, E, HW, B, state, next_state, probs_out, reward_out, term_out, tr_out,
                        x_out, xn_out);
+    return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
+}
+
+gw_status gw_eval_accum(const int32_t *crashes, const int32_t *apples, const double *fear, const uint8_t *done,
+                        uint8_t *active, int64_t *counts, double *fear_total, int64_t E, int32_t K, void *stream) {
+    if (!crashes || !apples || !fear || !done || !active || !counts || !fear_total || E < 0 || K <= 0)
+        return GW_ERR_ARG;
+    hipLaunchKernelGGL(eval_accum_kernel, dim3(1), dim3(EV_T), 0, static_cast<hipStream_t>(stream), crashes, apples,
+                       fear, done, active, counts, fear_total, E, (int)K);
     return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
 }
 

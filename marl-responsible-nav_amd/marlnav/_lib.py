@@ -170,7 +170,8 @@ EXPORTS = ["gw_create", "gw_reset", "gw_step", "gw_state_view", "gw_copy_state",
            "gw_cnn_act", "gw_return_compact", "gw_return_compact_scratch", "gw_kernel_path", "gw_graph_replayed", "gw_obs_patch",
            "gw_ln_relu_fwd", "gw_ln_relu_bwd", "gw_gumbel_softmax",
            "gw_replay_gather", "gw_affine_relu_fwd", "gw_affine_relu_bwd",
-           "gw_soft_update2", "gw_td_target", "gw_mean_loss_fwd", "gw_mean_loss_bwd"]
+           "gw_soft_update2", "gw_td_target", "gw_mean_loss_fwd", "gw_mean_loss_bwd",
+           "gw_eval_accum"]
 
 
 class GwObsSource(C.Structure):
@@ -250,6 +251,8 @@ def _declare(L):
     L.gw_mean_loss_fwd.restype = C.c_int
     L.gw_mean_loss_bwd.argtypes = [p, p, p, p, C.c_int32, C.c_int64, C.c_int32, p]
     L.gw_mean_loss_bwd.restype = C.c_int
+    L.gw_eval_accum.argtypes = [p] * 7 + [C.c_int64, C.c_int32, p]
+    L.gw_eval_accum.restype = C.c_int
     L.gw_affine_relu_fwd.argtypes = [p, p, p, p, C.c_int32, C.c_int64, C.c_int32, p]
     L.gw_affine_relu_fwd.restype = C.c_int
     L.gw_affine_relu_bwd.argtypes = [p] * 7 + [C.c_int32, C.c_int64, C.c_int32, p]

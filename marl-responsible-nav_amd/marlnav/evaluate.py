@@ -7,31 +7,39 @@ RL agents are terminated or all are truncated; it sums ``info["agent_crashes"]``
 E = episodes envs in parallel (auto-reset off, step cap = TRAIN_STEPS); an env stops counting
 after its episode ends, so the totals are the same sums.  Actions: ``training=False`` (no
 Gumbel noise), the env's action mask, argmax — agilerl's eval-mode ``get_action`` restated.
+With the fused actor the env writes no dense obs (the actor reads the obs descriptors).
 Weights come from this package's safetensors checkpoints (marlnav/maddpg.py ``MADDPG.save``);
 the reference's pickled ``.pt`` checkpoints are not loadable with a non-executing loader and
 are not used.
 """
 from __future__ import annotations
 
+from types import SimpleNamespace
+
 import torch
 
+from . import _lib
 from .actor import MultiAgentActors
+from .scenario import builtin
 from .vec_env import VecGridEnv
 
 
 @torch.no_grad()
 def evaluate(actors: MultiAgentActors, scenario="level3", episodes: int = 100, max_steps: int = 150,
              fear: bool = False, seed: int = 42, record_actions: bool = False, fused: bool | None = None) -> dict:
-    env = VecGridEnv(scenario, num_envs=episodes, fear=fear, max_steps=max_steps, auto_reset=False, seed=seed)
-    fused = actors.fusable(env) if fused is None else fused
+    sc = builtin(scenario) if isinstance(scenario, str) else scenario
+    if fused is None:
+        fused = actors.fusable(SimpleNamespace(K=sc.K, H=sc.H, W=sc.W))
+    # the fused actor reads the obs descriptors: no dense obs is written at all
+    env = VecGridEnv(sc, num_envs=episodes, fear=fear, max_steps=max_steps, auto_reset=False, seed=seed,
+                     obs=not fused)
     try:
         obs, mask = env.reset()
         dev = env.device
-        active = torch.ones(episodes, dtype=torch.bool, device=dev)
-        crashes = torch.zeros((), dtype=torch.int64, device=dev)
-        apples = torch.zeros((), dtype=torch.int64, device=dev)
-        steps = torch.zeros((), dtype=torch.int64, device=dev)
-        fear_sum = torch.zeros((), dtype=torch.float64, device=dev)
+        active = torch.ones(episodes, dtype=torch.uint8, device=dev)
+        counts = torch.zeros(3, dtype=torch.int64, device=dev)       # crashes, apples, steps
+        fear_sum = torch.zeros(1, dtype=torch.float64, device=dev)
+        lib = _lib.load()
         recorded = []
         for i in range(max_steps):
             if fused:  # one kernel over the obs descriptors (include/actor_ops.h)
@@ -41,17 +49,17 @@ def evaluate(actors: MultiAgentActors, scenario="level3", episodes: int = 100, m
             if record_actions:
                 recorded.append(actions.clone())
             r = env.step(actions)
-            crashes += (r.crashes * active).sum()
-            apples += (r.apples * active).sum()
-            steps += active.sum()
-            fear_sum += (r.fear.sum(1) * active).sum()
-            active &= ~r.done.bool()
+            # the active envs' crashes, apples, steps and FeAR summed, then the done ones retired
+            _lib.check(lib.gw_eval_accum(r.crashes.data_ptr(), r.apples.data_ptr(), r.fear.data_ptr(),
+                                         r.done.data_ptr(), active.data_ptr(), counts.data_ptr(), fear_sum.data_ptr(),
+                                         episodes, env.K, torch.cuda.current_stream(dev).cuda_stream),
+                       "gw_eval_accum")
             # a host sync every 8 steps: stepping envs whose episode ended changes no total
             # (they are masked out), so checking late only costs the few extra steps
             if i % 8 == 7 and not bool(active.any()):
                 break
-        out = {"episodes": episodes, "crashes": int(crashes), "apples_caught": int(apples), "steps": int(steps),
-               "fear": float(fear_sum)}
+        c = counts.tolist()
+        out = {"episodes": episodes, "crashes": c[0], "apples_caught": c[1], "steps": c[2], "fear": float(fear_sum)}
         if record_actions:
             out["actions"] = torch.stack(recorded)
         return out
