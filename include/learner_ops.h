@@ -50,9 +50,10 @@ gw_status gw_mean_loss_bwd(const float *q, const float *y, const float *grad_los
 gw_status gw_ln_relu_fwd(const float *z, const float *ln_w, const float *ln_b, float *y, float *mean, float *rstd,
                          int32_t K, int64_t R, int32_t h, float eps, void *stream);
 
-/* Its backward from the saved z, y, mean, rstd: dz [K, R, h] is written; the ln_w / ln_b
- * gradients, summed over the R rows in a fixed order, are ADDED into dw_acc / db_acc [K, h]
- * (the parameters' existing .grad, as autograd accumulates; either may be NULL). */
+/* Its backward from the saved z, y, mean, rstd: dz [K, R, h] is written (one launch, a wave per
+ * row); the ln_w / ln_b gradients, summed over the R rows in a fixed order, are ADDED into
+ * dw_acc / db_acc [K, h] (a second launch; the parameters' existing .grad, as autograd
+ * accumulates; either may be NULL). */
 gw_status gw_ln_relu_bwd(const float *dy, const float *z, const float *y, const float *ln_w, const float *mean,
                          const float *rstd, float *dz, float *dw_acc, float *db_acc, int32_t K, int64_t R,
                          int32_t h, void *stream);

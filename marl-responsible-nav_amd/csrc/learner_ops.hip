@@ -94,71 +94,77 @@ __global__ void __launch_bounds__(256) ln_relu_fwd_kernel(const float *__restric
     }
 }
 
-// Backward of the epilogue for the R rows of agent k = blockIdx.x (one block per agent, so the
-// ln_w / ln_b gradients are reduced over rows in a fixed order: deterministic, graph == eager).
-//   g = dy * (y > 0);  xhat = (z - mean) * rstd;  dW += sum_r g * xhat;  dB += sum_r g
-//   dxhat = g * w;  dz = rstd * (dxhat - mean_j(dxhat) - xhat * mean_j(dxhat * xhat))
-constexpr int LN_BWD_THREADS = 512;
-
-__global__ void __launch_bounds__(LN_BWD_THREADS) ln_relu_bwd_kernel(
+// Backward of the epilogue, two launches:
+//   rows (one wave per row, any number of rows in flight):
+//     g = dy * (y > 0);  xhat = (z - mean) * rstd;  dxhat = g * w
+//     dz = rstd * (dxhat - mean_j(dxhat) - xhat * mean_j(dxhat * xhat))
+//   columns (block = 64 columns x 16 row groups of agent k, fixed-order sums: deterministic):
+//     dW += sum_r g * xhat;  dB += sum_r g
+__global__ void __launch_bounds__(256) ln_relu_bwd_rows_kernel(
     const float *__restrict__ dy, const float *__restrict__ z, const float *__restrict__ y,
     const float *__restrict__ w, const float *__restrict__ mean, const float *__restrict__ rstd,
-    float *__restrict__ dz, float *__restrict__ dw_acc, float *__restrict__ db_acc, int64_t R, int h) {
-    constexpr int NW = LN_BWD_THREADS / 64;
-    __shared__ float s_dw[NW][LN_MAXV * 64];
-    __shared__ float s_db[NW][LN_MAXV * 64];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t k = blockIdx.x;
-    float wk[LN_MAXV], pdw[LN_MAXV], pdb[LN_MAXV];
+    float *__restrict__ dz, int64_t R, int64_t rows, int h) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (row >= rows) return;  // uniform per wave
+    const int64_t k = row / R;
+    const float m = mean[row], rs = rstd[row];
+    float xh[LN_MAXV], dxh[LN_MAXV];
+    float s1 = 0.0f, s2 = 0.0f;
 #pragma unroll
     for (int i = 0; i < LN_MAXV; ++i) {
         const int j = lane + 64 * i;
-        wk[i] = j < h ? w[k * h + j] : 0.0f;
-        pdw[i] = pdb[i] = 0.0f;
+        xh[i] = dxh[i] = 0.0f;
+        if (j < h) {
+            const int64_t o = row * h + j;
+            const float g = y[o] > 0.0f ? dy[o] : 0.0f;
+            xh[i] = (z[o] - m) * rs;
+            dxh[i] = g * w[k * h + j];
+            s1 += dxh[i];
+            s2 = __fmaf_rn(dxh[i], xh[i], s2);
+        }
     }
     const float inv_h = 1.0f / (float)h;
-    for (int64_t r = wv; r < R; r += NW) {
-        const int64_t row = k * R + r;
-        const float m = mean[row], rs = rstd[row];
-        float xh[LN_MAXV], dxh[LN_MAXV];
-        float s1 = 0.0f, s2 = 0.0f;
-#pragma unroll
-        for (int i = 0; i < LN_MAXV; ++i) {
-            const int j = lane + 64 * i;
-            xh[i] = dxh[i] = 0.0f;
-            if (j < h) {
-                const int64_t o = row * h + j;
-                const float g = y[o] > 0.0f ? dy[o] : 0.0f;
-                xh[i] = (z[o] - m) * rs;
-                pdw[i] = __fmaf_rn(g, xh[i], pdw[i]);
-                pdb[i] += g;
-                dxh[i] = g * wk[i];
-                s1 += dxh[i];
-                s2 = __fmaf_rn(dxh[i], xh[i], s2);
-            }
-        }
-        const float m1 = wave_sum(s1) * inv_h, m2 = wave_sum(s2) * inv_h;
-#pragma unroll
-        for (int i = 0; i < LN_MAXV; ++i) {
-            const int j = lane + 64 * i;
-            if (j < h) dz[row * h + j] = rs * (dxh[i] - m1 - xh[i] * m2);
-        }
-    }
-    if (!dw_acc && !db_acc) return;  // uniform
+    const float m1 = wave_sum(s1) * inv_h, m2 = wave_sum(s2) * inv_h;
 #pragma unroll
     for (int i = 0; i < LN_MAXV; ++i) {
-        s_dw[wv][lane + 64 * i] = pdw[i];
-        s_db[wv][lane + 64 * i] = pdb[i];
+        const int j = lane + 64 * i;
+        if (j < h) dz[row * h + j] = rs * (dxh[i] - m1 - xh[i] * m2);
     }
-    __syncthreads();
-    for (int j = threadIdx.x; j < h; j += LN_BWD_THREADS) {
-        float a = 0.0f, c = 0.0f;
-        for (int q = 0; q < NW; ++q) {
-            a += s_dw[q][j];
-            c += s_db[q][j];
+}
+
+constexpr int LN_RG = 16;
+
+__global__ void __launch_bounds__(LN_RG * 64) ln_relu_bwd_cols_kernel(
+    const float *__restrict__ dy, const float *__restrict__ z, const float *__restrict__ y,
+    const float *__restrict__ mean, const float *__restrict__ rstd, float *__restrict__ dw_acc,
+    float *__restrict__ db_acc, int64_t R, int h) {
+    __shared__ float s_dw[LN_RG][64], s_db[LN_RG][64];
+    const int c = threadIdx.x & 63, rg = threadIdx.x >> 6;
+    const int j = blockIdx.x * 64 + c;
+    const int64_t k = blockIdx.y;
+    const bool ok = j < h;
+    float pdw = 0.0f, pdb = 0.0f;
+    if (ok) {
+#pragma unroll 4
+        for (int64_t r = rg; r < R; r += LN_RG) {
+            const int64_t row = k * R + r, o = row * h + j;
+            const float g = y[o] > 0.0f ? dy[o] : 0.0f;
+            pdw = __fmaf_rn(g, (z[o] - mean[row]) * rstd[row], pdw);
+            pdb += g;
         }
-        if (dw_acc) dw_acc[k * h + j] += a;  // accumulates like autograd into an existing .grad
-        if (db_acc) db_acc[k * h + j] += c;
+    }
+    s_dw[rg][c] = pdw;
+    s_db[rg][c] = pdb;
+    __syncthreads();
+    if (rg == 0 && ok) {
+        float a = 0.0f, d = 0.0f;
+        for (int q = 0; q < LN_RG; ++q) {
+            a += s_dw[q][c];
+            d += s_db[q][c];
+        }
+        if (dw_acc) dw_acc[k * h + j] += a;
+        if (db_acc) db_acc[k * h + j] += d;
     }
 }
 
@@ -352,8 +358,14 @@ gw_status gw_ln_relu_bwd(const float *dy, const float *z, const float *y, const 
     if (!dy || !z || !y || !ln_w || !mean || !rstd || !dz || K < 0 || R < 0 || h <= 0 || h > LN_MAXV * 64)
         return GW_ERR_ARG;
     if (K == 0) return GW_OK;
-    hipLaunchKernelGGL(ln_relu_bwd_kernel, dim3((unsigned)K), dim3(LN_BWD_THREADS), 0,
-                       static_cast<hipStream_t>(stream), dy, z, y, ln_w, mean, rstd, dz, dw_acc, db_acc, R, (int)h);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const int64_t rows = (int64_t)K * R;
+    if (rows == 0) return GW_OK;
+    hipLaunchKernelGGL(ln_relu_bwd_rows_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, dy, z, y, ln_w,
+                       mean, rstd, dz, R, rows, (int)h);
+    if (dw_acc || db_acc)
+        hipLaunchKernelGGL(ln_relu_bwd_cols_kernel, dim3((unsigned)((h + 63) / 64), (unsigned)K), dim3(LN_RG * 64), 0,
+                           st, dy, z, y, mean, rstd, dw_acc, db_acc, R, (int)h);
     return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
 }
 
