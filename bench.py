@@ -144,6 +144,67 @@ def cpu_baseline(cfg, seconds: float = 12.0):
                       f"{cpus['cgroup_quota_cpus']}; {cpus['model']})"}
 
 
+def launch_plan(gpus: int, argv: list, base_env: dict, port: int):
+    """The per-rank (argv, env) of ``bench.py --gpus N`` started without a launcher: N child
+    processes of this script, one per GPU, with torchrun's variables (RANK = LOCAL_RANK = r,
+    WORLD_SIZE = N, rendezvous on 127.0.0.1:port).  Pure function (tests/test_bench_cpu.py)."""
+    plans = []
+    for r in range(int(gpus)):
+        env = dict(base_env)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(gpus), LOCAL_WORLD_SIZE=str(gpus),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        plans.append(([sys.executable, os.path.abspath(__file__)] + list(argv), env))
+    return plans
+
+
+def launch_ranks(gpus: int, argv: list) -> int:
+    """Run ``launch_plan`` and wait; a rank that fails ends the others.  Called before anything
+    touches the GPU (the children initialise it, each on its own device)."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = [subprocess.Popen(cmd, env=env) for cmd, env in launch_plan(gpus, argv, os.environ, port)]
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 1
+                    for q in live:
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
+def busy_ms(spans, kind: int):
+    """(union of the launch intervals of `kind`, launches): a kernel's busy time, with launches
+    that overlap (obs writers of consecutive steps on two streams) counted once."""
+    iv = sorted((float(b), float(e)) for k, b, e in spans if int(k) == kind)
+    total, cur_b, cur_e = 0.0, None, None
+    for b, e in iv:
+        if cur_e is None or b > cur_e:
+            if cur_e is not None:
+                total += cur_e - cur_b
+            cur_b, cur_e = b, e
+        else:
+            cur_e = max(cur_e, e)
+    if cur_e is not None:
+        total += cur_e - cur_b
+    return total, len(iv)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -155,10 +216,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--updates-per-step", type=int, default=0,
                     help="c5 only: MADDPG updates (batch 128, one HIP-graph replay each) per env step")
-    ap.add_argument("--profile-every", type=int, default=-1,
-                    help="time every n-th timed step's kernels with HIP events carried by their launches "
-                         "(0 = none, -1 = auto: every 4th step up to 256 timed steps, else about 64 "
-                         "samples); a profiled step costs ~4-6 us more")
+    ap.add_argument("--profile-steps", type=int, default=16,
+                    help="after the timed region, time this many more steps' kernels with HIP events "
+                         "carried by their launches (the live roofline; 0 = none)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cnn-torch", action="store_true",
                     help="c4cnn: the PyTorch CNN forward on the dense obs instead of gw_cnn_act (A/B)")
@@ -188,6 +248,9 @@ def main():
                          "launches, -1 = auto: 16 for the launch-bound env-only workloads that run "
                          "synchronous obs on one rank, i.e. C1/C2, else eager)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: start one rank per GPU ourselves, before any GPU call in this process
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
     import torch
     import torch.distributed as dist
@@ -197,8 +260,6 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world > 1:
-        print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
     torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
     if world > 1:
         # RCCL ("nccl") over xGMI; MARLNAV_DIST_BACKEND=gloo only rehearses the multi-rank path
@@ -208,6 +269,12 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        world = dist.get_world_size()
+    if world != args.gpus:
+        print(f"bench.py: the process group has {world} rank(s) but --gpus {args.gpus}", file=sys.stderr)
+        if world > 1:
+            dist.destroy_process_group()
+        sys.exit(2)
 
     if args.high_prio:
         torch.cuda.set_stream(torch.cuda.Stream(priority=-1))
@@ -254,8 +321,10 @@ def main():
         obs_mode = False
     stream = torch.cuda.current_stream()
 
-    from marlnav.parallel import ReturnGather, StatsReducer
-    reducer = StatsReducer(env.out["stats"].shape[1], env.device) if world > 1 else None
+    from marlnav.parallel import ReturnGather
+    # the step kernels add their statistics rows into a running total (gw_step_out.stats_acc):
+    # no per-step reduction launch or collective; the per-step exchange is the return gather
+    stats_acc = torch.zeros_like(env.out["stats"])
     # per-step RCCL all-gather of every env's completed-episode return + done flag (SURVEY §8e;
     # maddpg/agent.py:229-247): gw_step writes them straight into the send buffer
     graph_n = args.graph
@@ -275,41 +344,46 @@ def main():
 
     def one_step(i):
         into = gather.into() if gather is not None else {}
+        into["stats_acc"] = stats_acc
         if obs_ring is not None:
             into["obs"] = obs_ring[i % len(obs_ring)]
-        r = env.step(into=into or None)
+        r = env.step(into=into)
         if gather is not None:
             gather.push()
-        if reducer is not None:
-            # per-step RCCL all-reduce of the episode statistics across the shards: rows summed
-            # locally first (64 B message), asynchronous, waited for one step later
-            reducer.push(r.stats)
         return r
 
     if cfg.get("rollout"):  # c5: actor -> env -> replay (+ optional MADDPG updates) per step
         from marlnav.maddpg import MADDPG
         from marlnav.rollout import Rollout
+        from marlnav.parallel import broadcast_module
+        # one set of actor weights for every rank: built from the same seed and broadcast from
+        # rank 0 (MADDPG does it itself); every rank's sampling draws its own batches
+        torch.cuda.manual_seed(1234 + rank)
         if cfg.get("patch"):  # local observations: PyTorch MLP actors on the P x P windows
             from marlnav.actor import MultiAgentActors
             learner = None
-            actors = MultiAgentActors(K, cfg["patch"], cfg["patch"], "mlp", device=env.device, seed=rank)
+            actors = MultiAgentActors(K, cfg["patch"], cfg["patch"], "mlp", device=env.device, seed=0)
+            broadcast_module(actors)
         elif cfg.get("arch") == "cnn":  # configs/cnn.yaml head: fused gw_cnn_act (or PyTorch, A/B)
             from marlnav.actor import MultiAgentActors
             learner = None
-            actors = MultiAgentActors(K, env.H, env.W, arch="cnn", device=env.device, seed=rank)
+            actors = MultiAgentActors(K, env.H, env.W, arch="cnn", device=env.device, seed=0)
+            broadcast_module(actors)
             if args.cnn_torch:  # the PyTorch forward reads the dense obs: synchronous obs
                 obs_mode = False
         else:
-            learner = MADDPG(K, env.H, env.W, device=env.device, seed=rank, capturable=True)
+            learner = MADDPG(K, env.H, env.W, device=env.device, seed=0, capturable=True)
             actors = learner.actors
-        ro = Rollout(env, actors, replay_slots=-(-200_000 // E) + 1, training=True, seed=rank,
+        # the fused actor's Gumbel noise is Philox keyed by (seed; global env id, step, agent):
+        # one seed for all ranks keeps every env's trajectory independent of the rank count
+        ro = Rollout(env, actors, replay_slots=-(-200_000 // E) + 1, training=True, seed=42,
                      fused=False if args.cnn_torch else None,
                      obs_async=obs_mode, fear_async=bool(obs_mode) and args.fear_async, gather=gather,
                      patch=cfg.get("patch", 0))
         ro.reset()
 
         def one_step(i):  # noqa: F811
-            r = ro.step()  # the StatsReducer inside does the per-step all-reduce across ranks
+            r = ro.step()  # the return gather inside is the per-step exchange across ranks
             if args.updates_per_step and learner is not None and ro.replay.t >= 2:
                 ro.fence()  # sampling reads the ring's obs slots
                 if learner._graph is None:
@@ -327,10 +401,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
 
-    # kernel spans are sampled: each profiled step costs ~4-6 us of event bookkeeping in the
-    # pipeline (profiles/r2_events), so a short run samples every 4th step (5 of the driver's 20)
-    pe = args.profile_every if args.profile_every >= 0 else \
-        (1 if args.steps < 8 else (4 if args.steps <= 256 else args.steps // 64))
+    # kernel spans come from --profile-steps eager steps AFTER the timed region (each profiled step
+    # costs ~4-6 us of event bookkeeping in the pipeline, profiles/r2_events), so the timed steps
+    # carry no profiling at all
+    n_prof = max(0, args.profile_steps)
     graph = None
     if graph_n:
         # the timed steps as HIP graphs of graph_n steps (captured here, before the timed region:
@@ -343,8 +417,8 @@ def main():
         graph = env.capture_steps(graph_n, gather)
     n_graph = args.steps - args.steps % graph_n if graph_n else 0
 
-    if pe > 0:  # the profiling events exist before the timed region (gw_profile creates them)
-        env.profile(True, reserve=8 * (args.steps // pe + 2))
+    if n_prof:  # the profiling events exist before they are used (gw_profile creates them)
+        env.profile(True, reserve=8 * (n_prof + 2))
         env.profile(False)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     # no Python garbage collection inside the timed region (as timeit does): the warmup's step
@@ -361,8 +435,6 @@ def main():
     for i in range(0, n_graph, max(graph_n, 1)):
         graph.replay()
     for i in range(n_graph, args.steps):
-        if pe > 0 and graph is None:
-            env.profile(i % pe == 0)
         one_step(i)
     t_enq = time.perf_counter() - t0  # host time to enqueue the timed steps (host-bound if ~ wall)
     if cfg.get("rollout"):
@@ -377,16 +449,21 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     gc.enable()
-    if graph is not None:
-        # HIP timing events cannot be recorded inside a graph: the kernel spans come from 16
-        # eager steps right after the timed region (same env, same kernels, untimed)
-        env.profile(True)
-        for i in range(16):
-            one_step(i)
-        torch.cuda.synchronize()
-    env.profile(False)
-    (ms_step, ms_obs, ms_fear), nprof = env.profile_read()
     gpu_ms = ev0.elapsed_time(ev1)
+    spans = None
+    if n_prof:
+        # the kernel spans: n_prof eager steps right after the timed region (same env, same
+        # kernels and pipeline, untimed; HIP timing events cannot be recorded inside a graph)
+        env.profile(True)
+        for i in range(n_prof):
+            one_step(args.steps + i)
+        if cfg.get("rollout"):
+            ro.fence()
+        env.obs_fence()  # the last profiled step's writer
+        torch.cuda.synchronize()
+        env.profile(False)
+        spans = env.profile_spans()
+    (ms_step, ms_obs, ms_fear), nprof = env.profile_read()
 
     t_local = torch.tensor([wall], dtype=torch.float64, device="cuda")
     if world > 1:
@@ -403,16 +480,22 @@ def main():
                                           2 if args.obs_dtype == "bf16" else 4)
         avg_step_ms, avg_obs_ms = ms_step / max(nprof, 1), ms_obs / max(nprof, 1)
         avg_fear_ms = ms_fear / max(nprof, 1)
+        # busy time per launch: the union of the launches' intervals / launches.  Equal to the
+        # mean launch duration when launches do not overlap; with the obs writers of consecutive
+        # steps overlapping on two streams a launch's own span covers part of its
+        # neighbours' work, and the busy time is what a launch costs the timeline
+        busy = {k: busy_ms(spans, k) if spans is not None and len(spans) else (0.0, 0) for k in (0, 1, 2)}
+        busy_step_ms, busy_obs_ms = (busy[k][0] / max(busy[k][1], 1) for k in (0, 1))
         fused = env.fused
         merged = env.kernel_path == "merged" and bool(obs_mode)
         if fused:  # one launch per step moves every byte of the step
-            dom, bytes_per_launch, dur = "step_fused", (step_b + obs_b) * E, avg_step_ms
+            dom, bytes_per_launch, span, dur = "step_fused", (step_b + obs_b) * E, avg_step_ms, busy_step_ms
         elif merged:  # step_obs: step t + the obs writer of step t-1 in one launch (its spans: kind 1)
-            dom, bytes_per_launch, dur = "step_obs", (step_b + obs_b) * E, avg_obs_ms
-        elif avg_obs_ms >= avg_step_ms:
-            dom, bytes_per_launch, dur = "obs_kernel", obs_b * E, avg_obs_ms
+            dom, bytes_per_launch, span, dur = "step_obs", (step_b + obs_b) * E, avg_obs_ms, busy_obs_ms
+        elif busy_obs_ms >= busy_step_ms:
+            dom, bytes_per_launch, span, dur = "obs_kernel", obs_b * E, avg_obs_ms, busy_obs_ms
         else:
-            dom, bytes_per_launch, dur = "step_kernel", step_b * E, avg_step_ms
+            dom, bytes_per_launch, span, dur = "step_kernel", step_b * E, avg_step_ms, busy_step_ms
         achieved = bytes_per_launch / (dur * 1e-3) / 1e9 if dur > 0 else None
         traffic, traffic_src, prof_frac = None, None, None
         try:  # HBM bytes measured by the PMC passes committed under profiles/ for this workload
@@ -423,8 +506,10 @@ def main():
                     and args.obs_dtype == "f32":
                 traffic = prof["kernels"][dom]["hbm_bytes_per_launch"]
                 traffic_src = prof["source"]
-                # the same kernel's rocprofv3 average duration (many launches) for comparison
-                prof_frac = bytes_per_launch / (prof["kernels"][dom]["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS
+                # the same kernel's rocprofv3 busy time per launch (union of its launches'
+                # intervals in the kernel trace / launches) for comparison
+                pk = prof["kernels"][dom]
+                prof_frac = bytes_per_launch / (pk.get("busy_us", pk["avg_us"]) * 1e-6) / 1e9 / HBM_PEAK_GBS
         except (OSError, KeyError, ValueError):
             pass
         total_units = world * E * N * args.steps
@@ -447,7 +532,14 @@ def main():
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
                          "traffic_source": traffic_src, "frac_rocprof": prof_frac,
-                         "bytes_per_launch": bytes_per_launch, "avg_launch_ms": dur,
+                         "bytes_per_launch": bytes_per_launch,
+                         # achieved = bytes_per_launch / avg_launch_ms, the kernel's busy time per
+                         # launch (see busy_ms); avg_launch_span_ms = the launches' own mean
+                         # duration, which overlapping writers stretch (the per-span figure
+                         # beside it is the lower, per-launch view)
+                         "avg_launch_ms": dur, "avg_launch_span_ms": span,
+                         "frac_per_launch_span": bytes_per_launch / (span * 1e-3) / 1e9 / HBM_PEAK_GBS if span > 0 else None,
+                         "launches_profiled": busy[1 if dom in ("obs_kernel", "step_obs") else 0][1],
                          # every algorithmic byte of a whole step (state + obs) over the wall time
                          # per step: what the pipelined steps sustain end to end
                          "step_level_GBps": (step_b + obs_b) * E / (t_max / args.steps) / 1e9,
@@ -465,7 +557,7 @@ def main():
                            "obs_async": obs_mode, "fear_async": env.fear_async,
                            "graph_steps": graph_n, "obs_ring": n_ring,
                            "host_enqueue_ms_per_step": t_enq * 1e3 / args.steps,
-                           "spans_from": "16 eager steps after the timed region" if graph_n else "the timed steps"},
+                           "spans_from": f"{n_prof} eager steps after the timed region"},
             "last_step_episodes": {"completed": stats[1], "mean_return": stats[0] / max(stats[1], 1.0),
                          "mean_len": stats[6] / max(stats[1], 1.0)},
             # completed-episode returns all-gathered every step (warmup + timed steps, all ranks)

@@ -150,6 +150,13 @@ gw_status gw_copy_state(void *env, const gw_state *buf, int to_env, void *stream
  * timed, and clears them.  Used by bench.py for the live roofline. */
 gw_status gw_profile(void *env, int enable);
 gw_status gw_profile_read(void *env, double out_ms[3], int64_t *n_steps);
+/* The spans gw_profile_read would sum, one by one (call it first: gw_profile_read clears them):
+ * out[3 i + 0] = kind (0 world update, 1 obs writer, 2 FeAR), out[3 i + 1] / [3 i + 2] = the
+ * launch's start / end in milliseconds after the first span's start; at most cap spans are
+ * written, *n_spans = how many exist.  Synchronises on their events.  bench.py merges the obs
+ * writers' intervals (writers of consecutive steps overlap on two streams) into the writer's
+ * busy time per launch. */
+gw_status gw_profile_spans(void *env, double *out, int64_t cap, int64_t *n_spans);
 
 /* Responsibility.FeAR (custom/Responsibility.py:57-132: the N x N Resp matrix, every agent as
  * actor) and FeAL (:213-303) for n world snapshots of this env's map and N, on the device:

@@ -3106,6 +3106,25 @@ gw_status gw_profile(void *handle, int enable) {
     return GW_OK;
 }
 
+gw_status gw_profile_spans(void *handle, double *out, int64_t cap, int64_t *n_spans) {
+    Env *env = static_cast<Env *>(handle);
+    if (!env || !n_spans || (cap > 0 && !out)) return fail(GW_ERR_ARG, "null argument");
+    *n_spans = (int64_t)env->spans.size();
+    if (env->spans.empty() || cap <= 0) return GW_OK;
+    const hipEvent_t t0 = env->ev_pool[env->spans.front().b];
+    for (size_t i = 0; i < env->spans.size() && (int64_t)i < cap; ++i) {
+        const Env::Span &sp = env->spans[i];
+        HIP_TRY(hipEventSynchronize(env->ev_pool[sp.e]));
+        float b = 0.f, e = 0.f;
+        HIP_TRY(hipEventElapsedTime(&b, t0, env->ev_pool[sp.b]));
+        HIP_TRY(hipEventElapsedTime(&e, t0, env->ev_pool[sp.e]));
+        out[3 * i + 0] = (double)sp.kind;
+        out[3 * i + 1] = (double)b;
+        out[3 * i + 2] = (double)e;
+    }
+    return GW_OK;
+}
+
 gw_status gw_profile_read(void *handle, double out_ms[3], int64_t *n_steps) {
     Env *env = static_cast<Env *>(handle);
     if (!env || !out_ms) return fail(GW_ERR_ARG, "null argument");

@@ -171,7 +171,7 @@ EXPORTS = ["gw_create", "gw_reset", "gw_step", "gw_state_view", "gw_copy_state",
            "gw_ln_relu_fwd", "gw_ln_relu_bwd", "gw_gumbel_softmax",
            "gw_replay_gather", "gw_affine_relu_fwd", "gw_affine_relu_bwd",
            "gw_soft_update2", "gw_td_target", "gw_mean_loss_fwd", "gw_mean_loss_bwd",
-           "gw_eval_accum"]
+           "gw_eval_accum", "gw_profile_spans"]
 
 
 class GwObsSource(C.Structure):
@@ -219,6 +219,8 @@ def _declare(L):
     L.gw_profile.restype = C.c_int
     L.gw_profile_read.argtypes = [p, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
     L.gw_profile_read.restype = C.c_int
+    L.gw_profile_spans.argtypes = [p, C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_int64)]
+    L.gw_profile_spans.restype = C.c_int
     L.gw_obs_patch.argtypes = [p, C.c_int32, p, p, p]
     L.gw_obs_patch.restype = C.c_int
     L.gw_graph_replayed.argtypes = [p, p]

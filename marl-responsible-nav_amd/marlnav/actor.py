@@ -146,6 +146,22 @@ class _StackedLinear(torch.autograd.Function):
     another (autograd's version is GEMM + add and reduction + add)."""
 
     _ones = {}
+    _ONES_MAX = 16
+
+    @staticmethod
+    def _ones_for(dy):
+        """The cached [K, 1, R] ones of dy's shape.  Never created during a graph capture: there
+        the fill kernel would only be recorded, and an eager backward before the first replay
+        would read uninitialised memory; None then.  At most _ONES_MAX shapes are kept."""
+        key = (dy.shape[0], dy.shape[1], dy.device, dy.dtype)
+        ones = _StackedLinear._ones.get(key)
+        if ones is None:
+            if dy.is_cuda and torch.cuda.is_current_stream_capturing():
+                return None
+            if len(_StackedLinear._ones) >= _StackedLinear._ONES_MAX:
+                _StackedLinear._ones.clear()
+            ones = _StackedLinear._ones[key] = torch.ones((key[0], 1, key[1]), device=dy.device, dtype=dy.dtype)
+        return ones
 
     @staticmethod
     def forward(ctx, x, w, b):
@@ -165,12 +181,13 @@ class _StackedLinear(torch.autograd.Function):
             else:
                 gw = torch.bmm(x.transpose(1, 2), dy)
         if ctx.needs_input_grad[2]:
-            K, R = dy.shape[0], dy.shape[1]
-            key = (K, R, dy.device, dy.dtype)
-            ones = _StackedLinear._ones.get(key)
-            if ones is None:
-                ones = _StackedLinear._ones[key] = torch.ones((K, 1, R), device=dy.device, dtype=dy.dtype)
-            if bp.grad is not None:
+            ones = _StackedLinear._ones_for(dy)
+            if ones is None:  # inside a graph capture with no cached ones: a row sum instead
+                if bp.grad is not None:
+                    bp.grad.add_(dy.sum(1, keepdim=True))
+                else:
+                    gb = dy.sum(1, keepdim=True)
+            elif bp.grad is not None:
                 bp.grad.baddbmm_(ones, dy)
             else:
                 gb = torch.bmm(ones, dy)

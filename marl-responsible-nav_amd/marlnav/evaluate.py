@@ -41,6 +41,7 @@ def evaluate(actors: MultiAgentActors, scenario="level3", episodes: int = 100, m
         fear_sum = torch.zeros(1, dtype=torch.float64, device=dev)
         lib = _lib.load()
         recorded = []
+        alive = torch.zeros(max_steps, dtype=torch.bool, device=dev) if record_actions else None
         for i in range(max_steps):
             if fused:  # one kernel over the obs descriptors (include/actor_ops.h)
                 actions, _ = actors.act_env(env, env.out["mask"], training=False)
@@ -54,6 +55,8 @@ def evaluate(actors: MultiAgentActors, scenario="level3", episodes: int = 100, m
                                          r.done.data_ptr(), active.data_ptr(), counts.data_ptr(), fear_sum.data_ptr(),
                                          episodes, env.K, torch.cuda.current_stream(dev).cuda_stream),
                        "gw_eval_accum")
+            if record_actions:
+                alive[i] = active.any()  # device-side: is any episode still running after step i
             # a host sync every 8 steps: stepping envs whose episode ended changes no total
             # (they are masked out), so checking late only costs the few extra steps
             if i % 8 == 7 and not bool(active.any()):
@@ -61,7 +64,13 @@ def evaluate(actors: MultiAgentActors, scenario="level3", episodes: int = 100, m
         c = counts.tolist()
         out = {"episodes": episodes, "crashes": c[0], "apples_caught": c[1], "steps": c[2], "fear": float(fear_sum)}
         if record_actions:
-            out["actions"] = torch.stack(recorded)
+            # the early-stop check runs every 8 steps: keep the actions up to the first step after
+            # which every episode had ended (the steps an env-at-a-time loop would have taken)
+            n = len(recorded)
+            dead = (~alive[:n]).nonzero()
+            if dead.numel():
+                n = int(dead[0, 0]) + 1
+            out["actions"] = torch.stack(recorded[:n])
         return out
     finally:
         env.close()

@@ -30,6 +30,7 @@ from __future__ import annotations
 import copy
 
 import torch
+import torch.distributed as dist
 import torch.nn.functional as F
 
 from . import _lib
@@ -69,29 +70,43 @@ def _gumbel_into_slots(logits: torch.Tensor, u: torch.Tensor | None, x_next: tor
     """GumbelSoftmax of the target logits [K, B, 9] written straight into the action slots
     x_next[:, D:] of the critic's input rows [B, D + K*9] (gw_gumbel_softmax, strided output)."""
     K, B, n = logits.shape
+    if not (x_next.is_cuda and x_next.dtype == torch.float32 and x_next.is_contiguous()
+            and tuple(x_next.shape) == (B, D + K * n) and x_next.device == logits.device):
+        raise ValueError(f"critic input rows must be a contiguous float32 [B, D + K*9] = [{B}, {D + K * n}] CUDA "
+                         f"tensor on the logits' device, got {tuple(x_next.shape)} {x_next.dtype}")
     logits = logits.contiguous()
     if u is None:
         u = torch.rand(logits.shape, device=logits.device, dtype=logits.dtype)
+    if tuple(u.shape) != (K, B, n) or u.dtype != torch.float32:
+        raise ValueError("u must be float32 [K, B, 9]")
     u = u.contiguous()
     _lib.check(_lib.load().gw_gumbel_softmax(logits.data_ptr(), u.data_ptr(), x_next[:, D:].data_ptr(), K * B, n, 1.0,
                                              1e-20, B, x_next.shape[1],
                                              torch.cuda.current_stream(logits.device).cuda_stream), "gw_gumbel_softmax")
 
 
+def _gumbel_hip(logits: torch.Tensor, u: torch.Tensor | None, tau: float = 1.0, eps: float = 1e-20) -> torch.Tensor:
+    """The learner's target actions: gumbel_softmax as ONE gw_gumbel_softmax
+    launch (no gradient).  Its sum order and logf / expf differ from the torch formula by ~2e-6
+    relative, so the public ``gumbel_softmax`` stays the torch formula (the tests' reference)."""
+    logits = logits.contiguous()
+    if u is None:
+        u = torch.rand(logits.shape, device=logits.device, dtype=logits.dtype)
+    u = u.contiguous()
+    out = torch.empty_like(logits)
+    n = logits.shape[-1]
+    _lib.check(_lib.load().gw_gumbel_softmax(logits.data_ptr(), u.data_ptr(), out.data_ptr(), logits.numel() // n,
+                                             n, tau, eps, 0, 0, torch.cuda.current_stream(logits.device).cuda_stream),
+               "gw_gumbel_softmax")
+    return out
+
+
 def gumbel_softmax(logits: torch.Tensor, u: torch.Tensor | None = None, tau: float = 1.0, eps: float = 1e-20,
                    generator: torch.Generator | None = None) -> torch.Tensor:
-    """agilerl's GumbelSoftmax output activation: softmax((logits - log(-log(u + eps) + eps)) / tau)."""
+    """agilerl's GumbelSoftmax output activation: softmax((logits - log(-log(u + eps) + eps)) / tau)
+    (plain torch ops)."""
     if u is None:
         u = torch.rand(logits.shape, device=logits.device, dtype=logits.dtype, generator=generator)
-    if logits.is_cuda and not (torch.is_grad_enabled() and logits.requires_grad) and logits.dtype == torch.float32:
-        # no gradient needed (the target actions): one HIP launch instead of seven torch ops
-        logits, u = logits.contiguous(), u.contiguous()
-        out = torch.empty_like(logits)
-        n = logits.shape[-1]
-        _lib.check(_lib.load().gw_gumbel_softmax(logits.data_ptr(), u.data_ptr(), out.data_ptr(), logits.numel() // n,
-                                                 n, tau, eps, 0, 0, torch.cuda.current_stream(logits.device).cuda_stream),
-                   "gw_gumbel_softmax")
-        return out
     return F.softmax((logits - torch.log(-torch.log(u + eps) + eps)) / tau, dim=-1)
 
 
@@ -133,12 +148,22 @@ def _mlp_target(net: StackedMLPActors) -> StackedMLPActors:
 
 
 class MADDPG:
-    """K MADDPG agents with stacked networks.  ``actors`` is a MultiAgentActors (mlp or cnn)."""
+    """K MADDPG agents with stacked networks.  ``actors`` is a MultiAgentActors (mlp or cnn).
+
+    Data-parallel across ranks when a torch.distributed group of more
+    than one rank exists (``group``, default the world): the networks are broadcast from rank 0
+    at construction (``broadcast_parameters``), every rank learns on its own sampled batch, and
+    each of the two backward passes is followed by ONE all-reduce of that network's flat gradient
+    buffer, averaged over the ranks, before its Adam step, so the replicas stay identical.  Equal
+    per-rank batches make the averaged gradient that of the mean loss over the concatenated
+    batch (tests/test_maddpg_dp.py)."""
 
     def __init__(self, K: int, H: int, W: int, arch: str = "mlp", hidden=(128, 128), lr_actor: float = 1e-3,
                  lr_critic: float = 1e-3, gamma: float = 0.98, tau: float = 0.01, batch_size: int = 128,
-                 learn_step: int = 10, device=None, seed: int = 0, capturable: bool = False):
+                 learn_step: int = 10, device=None, seed: int = 0, capturable: bool = False, group=None):
         self.K, self.H, self.W, self.arch = K, H, W, arch
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
         self.gamma, self.tau, self.batch_size, self.learn_step = gamma, tau, batch_size, learn_step
         self.device = torch.device(device) if device is not None else torch.device("cpu")
         self.actors = MultiAgentActors(K, H, W, arch, hidden, device=self.device, seed=seed)
@@ -154,14 +179,71 @@ class MADDPG:
             self.opt_actor = FlatAdam(self.actors.net, lr_actor)
             self.opt_critic = FlatAdam(self.critics, lr_critic)
         else:
+            # MLP targets with their own flat buffer (every layer a view of it, like the online
+            # nets; copy.deepcopy would clone the layer views apart from it)
             self.actor_targets = copy.deepcopy(self.actors)
-            self.critic_targets = copy.deepcopy(self.critics)
+            if arch == "mlp":
+                self.actor_targets.net = _mlp_target(self.actors.net)
+            self.critic_targets = _mlp_target(self.critics)
             opt = dict(capturable=True) if capturable and self.device.type == "cuda" else {}
             self.opt_actor = torch.optim.Adam(self.actors.parameters(), lr=lr_actor, **opt)
             self.opt_critic = torch.optim.Adam(self.critics.parameters(), lr=lr_critic, **opt)
         for m in (self.actor_targets, self.critic_targets):
             m.requires_grad_(False)
         self._graph = None
+        self._graphs = None  # world > 1: three graph segments between the gradient all-reduces
+        if self.world > 1:
+            self.broadcast_parameters()
+
+    # ---------------------------------------------------------------------------------------
+    def _networks(self):
+        """(name, module, flat parameter buffer or None) of the four networks."""
+        mlp = self.arch == "mlp"
+        return (("actor", self.actors, self.actors.net.flat_params() if mlp else None),
+                ("actor_target", self.actor_targets, self.actor_targets.net.flat_params() if mlp else None),
+                ("critic", self.critics, self.critics.flat_params()),
+                ("critic_target", self.critic_targets, self.critic_targets.flat_params()))
+
+    @torch.no_grad()
+    def broadcast_parameters(self, src: int = 0):
+        """Every network's parameters from rank ``src`` (one broadcast per flat buffer; the CNN
+        actors' parameters coalesced into one), so all replicas act and learn identically."""
+        if self.world <= 1:
+            return
+        from torch._utils import _flatten_dense_tensors, _unflatten_dense_tensors
+        for _, module, flat in self._networks():
+            if flat is not None:
+                dist.broadcast(flat.detach(), src, group=self.group)
+                continue
+            ps = [p.detach() for p in module.parameters()]
+            buf = _flatten_dense_tensors(ps)
+            dist.broadcast(buf, src, group=self.group)
+            for p, v in zip(ps, _unflatten_dense_tensors(buf, ps)):
+                p.copy_(v)
+        self.actors.mark_updated()
+        self.actor_targets.mark_updated()
+        for m in (self.critics, self.critic_targets):
+            m.epoch += 1
+
+    @torch.no_grad()
+    def _allreduce_grads(self, which: str):
+        """Average ``which`` ("actor" / "critic") gradients over the ranks: one all-reduce of the
+        network's flat gradient buffer (MLP), or of its coalesced gradients (CNN actors)."""
+        if self.world <= 1:
+            return
+        module = self.critics if which == "critic" else self.actors
+        if which == "critic" or self.arch == "mlp":
+            g = (module if which == "critic" else module.net).flat_params().grad
+            dist.all_reduce(g, group=self.group)
+            g.mul_(1.0 / self.world)
+            return
+        from torch._utils import _flatten_dense_tensors, _unflatten_dense_tensors
+        gs = [p.grad for p in module.parameters() if p.grad is not None]
+        buf = _flatten_dense_tensors(gs)
+        dist.all_reduce(buf, group=self.group)
+        buf.mul_(1.0 / self.world)
+        for g, v in zip(gs, _unflatten_dense_tensors(buf, gs)):
+            g.copy_(v)
 
     # ---------------------------------------------------------------------------------------
     def _critic_in(self, states: torch.Tensor, actions: torch.Tensor) -> torch.Tensor:
@@ -178,7 +260,17 @@ class MADDPG:
         u_next / u_cur: optional uniforms [K, B, 9] for the two Gumbel samples (tests).
         critic_in: optional (x, x_next) critic input rows from ReplayRing.sample(critic_in=True)
         (GPU): the same values this method would assemble, without the permute / cat copies.
+        With several ranks each backward is followed by the gradient all-reduce.
         Returns (actor_loss [K], critic_loss [K]) device tensors (no host sync)."""
+        ctx = self._learn_critic(states, actions, rewards, next_states, dones, u_next, critic_in)
+        self._allreduce_grads("critic")
+        self._learn_actor(ctx, u_cur)
+        self._allreduce_grads("actor")
+        return self._learn_finish(ctx)
+
+    def _learn_critic(self, states, actions, rewards, next_states, dones, u_next=None, critic_in=None) -> dict:
+        """Phase 1: target actions, TD target, critic forward and backward (gradients in the
+        critics' .grad, not yet applied)."""
         K, B = states.shape[0], states.shape[1]
         D = K * self.H * self.W
         with torch.no_grad():
@@ -186,7 +278,8 @@ class MADDPG:
                 x, x_next = critic_in
                 _gumbel_into_slots(self.actor_targets(next_states), u_next, x_next, D)
             else:
-                a_next = gumbel_softmax(self.actor_targets(next_states), u_next)      # [K, B, 9]
+                logits = self.actor_targets(next_states)
+                a_next = _gumbel_hip(logits, u_next) if self.flat else gumbel_softmax(logits, u_next)  # [K, B, 9]
                 x_next = self._critic_in(next_states, a_next)
             q_next = self.critic_targets(x_next.unsqueeze(0).expand(K, -1, -1))     # [K, B, 1]
             y = self._td_target(rewards, dones, q_next)
@@ -199,8 +292,14 @@ class MADDPG:
             critic_loss = ((q - y) ** 2).mean(dim=(1, 2))
         self.opt_critic.zero_grad(set_to_none=False)
         critic_loss.sum().backward()
-        self.opt_critic.step()
+        return dict(states=states, actions=actions, x=x, critic_loss=critic_loss.detach())
 
+    def _learn_actor(self, ctx: dict, u_cur=None):
+        """Phase 2: the critic's Adam step, then the actor loss through the updated critics and
+        its backward (gradients in the actors' .grad, not yet applied)."""
+        self.opt_critic.step()
+        states, actions, x = ctx["states"], ctx["actions"], ctx["x"]
+        K, B = states.shape[0], states.shape[1]
         probs = gumbel_softmax(self.actors(states), u_cur)                             # [K, B, 9]
         # a_mix[k] = the replayed actions with agent k's slot replaced by its fresh probs
         a_mix = actions.permute(1, 0, 2).unsqueeze(0).repeat(K, 1, 1, 1)              # [K, B, K, 9]
@@ -209,17 +308,31 @@ class MADDPG:
         # gradients this backward would form are dead (zeroed before the next critic step),
         # so the critics enter as constants, and critic layer 1 is split into its state
         # columns (no gradient path) and its action columns (the only path to the actors).
-        c = self.critics
-        w1 = c.weights[0].detach()
-        z1 = torch.baddbmm(c.biases[0].detach(), x[:, :D].detach().unsqueeze(0).expand(K, -1, -1), w1[:, :D])
-        z1 = torch.baddbmm(z1, a_mix.reshape(K, B, -1), w1[:, D:])
-        qa = c(z1, pre=True, frozen=True)
+        qa = self._q_split(x, a_mix.reshape(K, B, -1))
         actor_loss = _MeanLoss.apply(qa, None, 1) if self.flat else -qa.mean(dim=(1, 2))
         self.opt_actor.zero_grad(set_to_none=False)
         actor_loss.sum().backward()
+        ctx["actor_loss"] = actor_loss.detach()
+
+    def _learn_finish(self, ctx: dict):
+        """Phase 3: the actor's Adam step and the soft target update."""
         self.opt_actor.step()
         self.soft_update()
-        return actor_loss.detach(), critic_loss.detach()
+        return ctx["actor_loss"], ctx["critic_loss"]
+
+    def _q_split(self, x: torch.Tensor, a: torch.Tensor) -> torch.Tensor:
+        """Q_k of the critics as constants on rows whose state columns are x[:, :D] and whose action
+        columns are a [K, B, K*9] (per agent k): critic layer 1 as a state-column GEMM plus an
+        action-column GEMM.  The same function as critics(cat(x[:, :D], a_k)); the split changes
+        layer 1's summation order (two partial sums instead of one), so Q differs from the
+        concatenated forward by f32 rounding only (tests/test_maddpg.py::test_split_q_matches_concat_q)."""
+        K, B = a.shape[0], a.shape[1]
+        D = K * self.H * self.W
+        c = self.critics
+        w1 = c.weights[0].detach()
+        z1 = torch.baddbmm(c.biases[0].detach(), x[:, :D].detach().unsqueeze(0).expand(K, -1, -1), w1[:, :D])
+        z1 = torch.baddbmm(z1, a, w1[:, D:])
+        return c(z1, pre=True, frozen=True)
 
     def _td_target(self, rewards, dones, q_next):
         """y = r + (1 - d) * gamma * q_next  ([K, B, 1]; rewards f64 / dones [B, K])."""
@@ -256,30 +369,70 @@ class MADDPG:
     # ---------------------------------------------------------------------------------------
     def learn_from(self, replay, generator: torch.Generator | None = None):
         """Sample ``batch_size`` transitions from a ReplayRing and learn (eager)."""
+        return self.learn(*self._sample(replay, generator))
+
+    def _sample(self, replay, generator=None):
+        """(states, actions, rewards, next_states, dones, u_next, u_cur, critic_in) as ``learn``
+        takes them (no explicit uniforms; critic_in from the gather launch on the GPU)."""
         if self.device.type == "cuda":  # the critic's input rows come from the gather launch
             *batch, ci = replay.sample(self.batch_size, generator=generator, critic_in=True)
-            return self.learn(*batch, critic_in=ci)
-        return self.learn(*replay.sample(self.batch_size, generator=generator))
+            return (*batch, None, None, ci)
+        return (*replay.sample(self.batch_size, generator=generator), None, None, None)
 
-    def capture(self, replay, warmup: int = 3):
-        """Capture sample + learn into one HIP graph (requires capturable=True and a CUDA device).
-        Later ``replay_learn()`` replays it: one launch instead of ~150 kernel launches."""
+    def capture(self, replay=None, warmup: int = 3, batch: tuple | None = None):
+        """Capture sample + learn into HIP graphs (requires capturable=True and a CUDA device).
+        Later ``replay_learn()`` replays them.  ``batch`` (instead of a ReplayRing): fixed input
+        tensors (states, actions, rewards, next_states, dones[, u_next, u_cur]) the graphs read
+        at every replay.  One rank: ONE graph (one launch instead of ~150 kernel launches).
+        Several ranks: three graph segments sharing one memory pool (sample + critic backward |
+        critic step + actor backward | actor step + soft update) with the two gradient
+        all-reduces issued eagerly between their replays (a collective is not captured: the gloo
+        backend cannot be, and RCCL's own launches stay outside the graph)."""
         if self.device.type != "cuda":
             raise RuntimeError("graph capture needs the GPU")
+        if batch is not None:
+            fixed = tuple(batch) + (None,) * (8 - len(batch))
+
+            def draw():
+                return fixed
+        else:
+            def draw():
+                return self._sample(replay)
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
             for _ in range(warmup):  # allocator + optimizer state warm-up outside the graph
-                self.learn_from(replay)
+                self.learn(*draw())
         torch.cuda.current_stream(self.device).wait_stream(s)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self._graph_out = self.learn_from(replay)
-        self._graph = g
-        return g
+        if self.world <= 1:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._graph_out = self.learn(*draw())
+            self._graph = g
+            return g
+        g1, g2, g3 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g1):
+            st, ac, rw, ns, dn, un, uc, ci = draw()
+            ctx = self._learn_critic(st, ac, rw, ns, dn, un, ci)
+        with torch.cuda.graph(g2, pool=g1.pool()):
+            self._learn_actor(ctx, uc)
+        with torch.cuda.graph(g3, pool=g1.pool()):
+            self._graph_out = self._learn_finish(ctx)
+        self._graph_ctx = ctx  # keeps the segments' shared tensors alive
+        self._graphs = (g1, g2, g3)
+        self._graph = g3
+        return g3
 
     def replay_learn(self):
-        self._graph.replay()
+        if self._graphs is not None:
+            g1, g2, g3 = self._graphs
+            g1.replay()
+            self._allreduce_grads("critic")
+            g2.replay()
+            self._allreduce_grads("actor")
+            g3.replay()
+        else:
+            self._graph.replay()
         for m in (self.actors, self.actor_targets):  # the replayed optimizer / soft update wrote them
             m.mark_updated()
         return self._graph_out

@@ -1,12 +1,14 @@
-"""Multi-GPU pieces: env sharding and the per-step reduction of episode statistics.
+"""Multi-GPU pieces: env sharding, the per-step gather of episode returns, replicated weights.
 
 One process per GPU (torch.distributed, backend "nccl" = RCCL on ROCm).  Envs are
 independent units: rank r owns the contiguous global ids [offset, offset + count), and every
 random draw is keyed by the global env id, so per-env trajectories are identical for any
-number of ranks (tests/test_parallel.py).  The only exchange is a per-step all-reduce of the
-step kernel's per-block partial sums (episode returns, completions, FeAR, crashes, apples):
-a few KB per rank, latency-bound over xGMI, issued asynchronously so that the collective of
-step t overlaps step t+1.
+number of ranks (tests/test_parallel.py).  The only per-step exchange is the all-gather of
+every env's episode return and done flag (ReturnGather: 9 bytes per env, asynchronous, SURVEY.md
+§8e).  Episode statistics are summed by the step kernels into a per-rank running total and
+all-reduced only when read (Rollout.totals); StatsReducer remains for callers that want a
+per-step reduction of partial sums.  Weights are replicated by broadcast (broadcast_module,
+MADDPG.broadcast_parameters) and kept equal by the learner's gradient all-reduce.
 """
 from __future__ import annotations
 
@@ -35,14 +37,33 @@ def init_from_env(backend: str | None = None):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and not dist.is_initialized():
-        if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend is None:  # MARLNAV_DIST_BACKEND=gloo rehearses several ranks on one GPU
+            backend = os.environ.get("MARLNAV_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         kw = {}
         if backend == "nccl":
             torch.cuda.set_device(local)
             kw["device_id"] = torch.device("cuda", local)
         dist.init_process_group(backend, **kw)
     return rank, world, local
+
+
+@torch.no_grad()
+def broadcast_module(module: torch.nn.Module, src: int = 0, group=None):
+    """Replicate a module's parameters and buffers from rank ``src`` (one broadcast of their
+    coalesced values), e.g. actors that act without a learner (actor weights are
+    broadcast once at start).  No-op without a process group of more than one rank."""
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1):
+        return
+    from torch._utils import _flatten_dense_tensors, _unflatten_dense_tensors
+    ts = [t.detach() for t in list(module.parameters()) + list(module.buffers())]
+    if not ts:
+        return
+    buf = _flatten_dense_tensors(ts)
+    dist.broadcast(buf, src, group=group)
+    for t, v in zip(ts, _unflatten_dense_tensors(buf, ts)):
+        t.copy_(v)
+    if hasattr(module, "mark_updated"):
+        module.mark_updated()
 
 
 class StatsReducer:

@@ -1,26 +1,30 @@
 """Batched MADDPG rollout: the per-step body of MADDPGAgent.train (maddpg/agent.py:77-252) over
-E envs of one GPU, plus the multi-GPU pieces.
+the E envs of this rank's shard.
 
 Per step (all on the GPU, no host sync):
   actions, probs = actors.act(obs_t, mask_t)                 get_action          agent.py:109-122
   env.step(actions) -> obs_{t+1}, shaped reward, dones         env.step + :124-141 (in-kernel)
   replay ring <- (slot of obs_t, probs, shaped reward, term)  memory.save_to_memory :190-197
   auto-reset of done envs (in-kernel)                          the break / env.reset :241, main :129
-  [multi-GPU] RCCL all-reduce of the per-block episode stats   (north_star: per-step return gather)
+  episode statistics added into a running total (in-kernel, gw_step_out.stats_acc)
+  [multi-GPU] RCCL all-gather of every env's ep_return / done  completed_episode_scores :229-247
+              (parallel.ReturnGather; the only per-step exchange)
 
 Replay storage is zero-copy: the env writes obs_{t+1} straight into ring slot (t+1) % S, so
 the obs of step t is both the next_state of transition t-1 and the state of transition t;
 terminal observations of done envs go to a parallel final-obs ring (their next_state).
-Learning (agilerl MADDPG.learn, agent.py:199-224) is SURVEY §8f "next" and not part of this
-rollout.
+Learning (agilerl MADDPG.learn, agent.py:199-224) runs beside this rollout: marlnav/maddpg.py
+(data-parallel across ranks) driven by marlnav/train.py or bench.py --updates-per-step.
+The statistics totals are all-reduced across ranks only when read (``totals()``).
 """
 from __future__ import annotations
 
 import torch
+import torch.distributed as dist
 
 from . import _lib
 from .actor import MultiAgentActors
-from .parallel import StatsReducer, shard  # noqa: F401  (re-exported)
+from .parallel import shard  # noqa: F401  (re-exported)
 from .vec_env import VecGridEnv
 
 
@@ -135,15 +139,24 @@ class Rollout:
             raise ValueError("Rollout(patch=P) needs actors built for a P x P input")
         self.replay = ReplayRing(env, replay_slots, patch=self.patch) if replay_slots else None
         self._patch = None  # the current obs' patches when there is no ring
-        self.gen = torch.Generator(device=env.device).manual_seed(seed) if actors is not None else None
+        self.distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+        rank = dist.get_rank(group) if self.distributed else 0
+        # the PyTorch actor's Gumbel noise: one stream per rank (the fused actor's Philox noise is
+        # keyed by the global env id instead, so it is the same for any number of ranks)
+        self.gen = torch.Generator(device=env.device).manual_seed(seed + 7919 * rank) if actors is not None else None
         self.t = 0
-        self.reducer = StatsReducer(_lib.GW_STATS, env.device, group) if env.out.get("stats") is not None else None
-        # one rank: the step kernels add their per-block rows into a running total and advance
-        # the ring's device step count themselves (gw_step_out.stats_acc / tick), so a step
-        # needs no reduction launch; across ranks the per-step all-reduce stays
-        self._acc = None
-        if self.reducer is not None and not self.reducer.distributed:
-            self._acc = torch.zeros_like(env.out["stats"])
+        # the step kernels add their per-block statistics rows into a running total and advance
+        # the ring's device step count themselves (gw_step_out.stats_acc / tick), so a step needs
+        # no reduction launch on any number of ranks; totals() all-reduces the total when read
+        self._acc = torch.zeros_like(env.out["stats"]) if env.out.get("stats") is not None else None
+
+    def group_rank(self) -> int:
+        return dist.get_rank(self.group) if self.distributed else 0
+
+    @property
+    def has_stats(self) -> bool:
+        """Whether the env produces the statistics rows that ``totals()`` sums."""
+        return self._acc is not None
         self.gather = gather
         if gather is not None and gather.count != env.E:
             raise ValueError("ReturnGather shard size != env.E")
@@ -163,11 +176,7 @@ class Rollout:
             self.gather.push()  # the step wrote ep_return / done into the gather's send buffer
         if self._acc is not None:
             return  # the step kernels accumulated the rows and advanced the tick
-        if self.reducer is not None:
-            # per-step (RCCL) reduction of the episode statistics; the ring's device step count
-            # advances in the same launch
-            self.reducer.push(stats, counter=tick)
-        elif tick is not None:
+        if tick is not None:
             tick.add_(1)
 
     def fence(self):
@@ -254,13 +263,15 @@ class Rollout:
 
     def totals(self) -> dict:
         """Episode statistics summed over all steps (and ranks): completed-episode return sum,
-        episodes, FeAR, crashes, apples, shaped reward, completed-episode length sum, env-steps."""
-        if self.reducer is None:
+        episodes, FeAR, crashes, apples, shaped reward, completed-episode length sum, env-steps.
+        With several ranks this is a collective (one all-reduce of 8 doubles): every rank calls it."""
+        if self._acc is None:
             return {}
         self._flush()
-        if self._acc is not None:
-            return dict(zip(_lib.STATS_NAMES, self._acc.sum(0).cpu().tolist()))
-        return dict(zip(_lib.STATS_NAMES, self.reducer.result().cpu().tolist()))
+        local = self._acc.sum(0)
+        if self.distributed:
+            dist.all_reduce(local, group=self.group)
+        return dict(zip(_lib.STATS_NAMES, local.cpu().tolist()))
 
     def completed_scores(self, last: int | None = None):
         """The completed-episode returns of every rank, oldest first (``completed_episode_scores``

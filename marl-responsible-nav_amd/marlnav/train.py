@@ -1,5 +1,6 @@
-"""Batched MADDPG training driver: ``MADDPGAgent.train`` (maddpg/agent.py:77-252) over E envs of
-one GPU, with the learner of marlnav/maddpg.py.
+"""Batched MADDPG training driver: ``MADDPGAgent.train`` (maddpg/agent.py:77-252) over the E envs
+of this rank's shard, with the learner of marlnav/maddpg.py (data-parallel across ranks when a
+process group exists: replicated weights, one gradient all-reduce per backward).
 
 Per env step (all device work, no host sync):
   actor (GumbelSoftmax sample, action mask, argmax) -> gw_step (world update, FeAR, shaped
@@ -35,7 +36,8 @@ class MADDPGTrainer:
         self.learning_delay = learning_delay
         self.updates_per_step = updates_per_step
         self.use_graph = graph and env.device.type == "cuda"
-        self.gen = torch.Generator(device=env.device).manual_seed(seed + 1)
+        rank = self.rollout.group_rank()
+        self.gen = torch.Generator(device=env.device).manual_seed(seed + 1 + 7919 * rank)
         self.updates = 0
         self.losses = []            # (actor_loss [K], critic_loss [K]) device tensors of the last updates
         self.total_steps = 0
@@ -55,7 +57,7 @@ class MADDPGTrainer:
         """Advance every env by env_steps steps with learning; returns the episode statistics of
         these steps (completed-episode return / length means, FeAR, crashes, apples)."""
         rp = self.rollout.replay
-        before = self.rollout.totals() if self.rollout.reducer is not None else None
+        before = self.rollout.totals() if self.rollout.has_stats else None
         for idx_step in range(env_steps):
             self.rollout.step()
             self.total_steps += self.env.E
@@ -66,7 +68,7 @@ class MADDPGTrainer:
                     out = self._learn()
                     self.updates += 1
                 self.losses = [tuple(t.clone() for t in out)]
-        tot = self.rollout.totals() if self.rollout.reducer is not None else {}
+        tot = self.rollout.totals() if self.rollout.has_stats else {}
         if before:
             tot = {k: v - before.get(k, 0.0) for k, v in tot.items()}
         eps = max(tot.get("episodes", 0.0), 1.0)

@@ -373,6 +373,17 @@ class VecGridEnv:
         timing events now, outside any timed region."""
         _lib.check(self.lib.gw_profile(self.handle, max(int(enable), int(reserve)) if enable else 0), "gw_profile")
 
+    def profile_spans(self):
+        """-> float64 [n, 3] (kind, start ms, end ms) of every timed launch since the last
+        profile_read (gw_profile_spans; call before profile_read, which clears them)."""
+        import numpy as np
+        n = C.c_int64()
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.gw_profile_spans(self.handle, None, 0, C.byref(n)), "gw_profile_spans")
+            buf = (C.c_double * (3 * max(n.value, 1)))()
+            _lib.check(self.lib.gw_profile_spans(self.handle, buf, n.value, C.byref(n)), "gw_profile_spans")
+        return np.frombuffer(buf, dtype=np.float64)[: 3 * n.value].reshape(-1, 3).copy()
+
     def profile_read(self):
         """-> (ms summed over timed steps [step_kernel, obs_kernel, fear_kernel], timed steps).
         fear_kernel is nonzero only with GW_KERNEL=defer (it overlaps obs_kernel there)."""

@@ -32,3 +32,24 @@ def test_cli_help_without_gpu():
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--help"], capture_output=True, text=True,
                        timeout=120)
     assert r.returncode == 0 and "--steps" in r.stdout and "--obs-dtype" in r.stdout
+
+
+def test_launch_plan_one_rank_per_gpu():
+    """`bench.py --gpus N` without a launcher starts N copies of itself with torchrun's variables
+    (the plan only: nothing is started and no GPU is touched here)."""
+    argv = ["--gpus", "4", "--steps", "20", "--warmup", "5"]
+    plans = bench.launch_plan(4, argv, {"PATH": "/bin", "HSA_ENABLE_IPC_MODE_LEGACY": "0"}, 29511)
+    assert len(plans) == 4
+    for r, (cmd, env) in enumerate(plans):
+        assert cmd[0] == sys.executable and cmd[1] == os.path.join(REPO, "bench.py") and cmd[2:] == argv
+        assert (env["RANK"], env["LOCAL_RANK"], env["WORLD_SIZE"]) == (str(r), str(r), "4")
+        assert env["MASTER_ADDR"] == "127.0.0.1" and env["MASTER_PORT"] == "29511"
+        assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and env["PATH"] == "/bin"
+
+
+def test_busy_time_merges_overlapping_launches():
+    spans = [(1, 0.0, 1.4), (1, 1.0, 2.4), (0, 0.0, 0.2), (1, 2.0, 3.4), (1, 5.0, 6.0)]
+    total, n = bench.busy_ms(spans, 1)
+    assert n == 4 and abs(total - (3.4 + 1.0)) < 1e-12
+    assert bench.busy_ms(spans, 0) == (0.2, 1)
+    assert bench.busy_ms([], 1) == (0.0, 0)

@@ -3,9 +3,10 @@
 RCCL refuses two ranks on one device, so the ranks use the gloo backend on CUDA tensors (the
 same torch.distributed calls bench.py / Rollout issue under RCCL on an 8-GPU node).  What runs
 on the GPU is the product path: each rank steps its contiguous shard of global env ids with
-the HIP env, the StatsReducer's GPU branch (one gw_rollout_tick launch feeding an async
-all-reduce) and the ReturnGather (ep_return / done written by gw_step straight into the send
-buffer, one all_gather_into_tensor per step, device-side compaction).  The sharded run must
+the HIP env, the step kernels' running statistics total (gw_step_out.stats_acc, all-reduced
+once when Rollout.totals() reads it: no per-step reduction launch) and the ReturnGather
+(ep_return / done written by gw_step straight into the send buffer, one all_gather_into_tensor
+per step, device-side compaction).  The sharded run must
 equal ONE process stepping all envs: identical completed-episode returns in the reference's
 order (maddpg/agent.py:229-247: step, then env id) on every rank, identical positions, and the
 same statistics (sums in a different order: rtol 1e-12).

@@ -82,16 +82,17 @@ def test_gumbel_softmax_hip_matches_torch(rows, n):
     """gw_gumbel_softmax (the no-gradient GumbelSoftmax of MADDPG.learn's target actions) == the
     torch composition softmax((logits - log(-log(u + eps) + eps)) / tau).  Tolerance 2e-6 abs
     (logf / expf ulps and the softmax sum order)."""
-    from marlnav.maddpg import gumbel_softmax
+    from marlnav.maddpg import _gumbel_hip, gumbel_softmax
     g = torch.Generator(device="cuda").manual_seed(rows + n)
     logits = torch.randn((rows, n), device="cuda", generator=g) * 4
     u = torch.rand((rows, n), device="cuda", generator=g)
     u[0, 0] = 0.0  # the eps guards
-    with torch.no_grad():
-        got = gumbel_softmax(logits, u, tau=0.7)
+    got = _gumbel_hip(logits, u, tau=0.7)
     want = torch.softmax((logits - torch.log(-torch.log(u + 1e-20) + 1e-20)) / 0.7, dim=-1)
     torch.testing.assert_close(got, want, rtol=1e-5, atol=2e-6)
-    lg = logits.clone().requires_grad_(True)  # with a gradient the torch ops run (and backprop)
+    with torch.no_grad():  # the public helper is the torch formula itself, gradient or not
+        assert torch.equal(gumbel_softmax(logits, u, tau=0.7), want)
+    lg = logits.clone().requires_grad_(True)
     gumbel_softmax(lg, u, tau=0.7).sum().backward()
     assert lg.grad is not None
 

@@ -177,7 +177,10 @@ def test_evaluate_matches_oracle():
     active = np.ones(E, bool)
     crashes = apples = steps = 0
     fear = 0.0
+    alive_before_last = True
     for t in range(acts.shape[0]):
+        if t == acts.shape[0] - 1:
+            alive_before_last = bool(active.any())
         orc.vec_step(acts[t], obs=obs_o, outs=outs, nthreads=8, auto_reset=False)
         for e in range(E):
             if active[e]:
@@ -189,6 +192,9 @@ def test_evaluate_matches_oracle():
     assert (r["crashes"], r["apples_caught"], r["steps"]) == (crashes, apples, steps)
     assert abs(r["fear"] - fear) < 1e-9
     assert not active.any() or acts.shape[0] == T
+    # the recorded actions end at the first step after which every episode had ended (no extra
+    # rows from the every-8-steps early-stop check)
+    assert alive_before_last
 
 
 def test_single_agent_facade_matches_oracle():

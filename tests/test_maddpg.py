@@ -304,3 +304,54 @@ def test_gpu_mean_losses_match_torch(B):
         la.sum().backward()
         lb.sum().backward()
         assert torch.equal(qa.grad, qb.grad)
+
+
+def _split_vs_concat(device):
+    K, H, W, B = 2, 32, 32, 128
+    m = MADDPG(K, H, W, device=device, seed=4)
+    g = torch.Generator(device=device).manual_seed(5)
+    states = torch.randint(-1, 14, (K, B, H, W), generator=g, device=device).float()
+    actions = torch.softmax(torch.randn((K, B, 9), generator=g, device=device) * 3, -1)
+    x = m._critic_in(states, actions)
+    with torch.no_grad():
+        q_cat = m.critics(x.unsqueeze(0).expand(K, -1, -1))
+        a_rep = x[:, K * H * W:].unsqueeze(0).expand(K, -1, -1).contiguous()
+        q_split = m._q_split(x, a_rep)
+    return q_cat, q_split
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_split_q_matches_concat_q(device):
+    """The actor loss evaluates the critic with layer 1 split into state and action columns
+    (MADDPG._q_split); on rows whose action slots hold the replayed actions that is the critic's
+    forward on the concatenated input (agilerl's single Linear over torch.cat) up to f32
+    summation order.  Tolerance: 2e-5 relative + 2e-5 absolute on Q (a 2,066-term f32 dot product
+    split in two partial sums; layer-2/3 LayerNorms keep the scale ~1)."""
+    q_cat, q_split = _split_vs_concat(device)
+    torch.testing.assert_close(q_split, q_cat, rtol=2e-5, atol=2e-5)
+
+
+@pytest.mark.gpu
+def test_gpu_capture_without_warmup_then_eager_learn():
+    """MADDPG.capture(warmup=0) records the update without running it; an eager learn before the
+    first replay must equal a twin that never captured (bit for bit): nothing the capture records
+    (e.g. a cached ones tensor for the bias gradients) may be read before it is filled."""
+    from marlnav.actor import _StackedLinear
+    from marlnav.rollout import Rollout
+    from marlnav.vec_env import VecGridEnv
+    _StackedLinear._ones.clear()
+    env = VecGridEnv("grid32", num_envs=256, fear=True, fear_weight=-5.0, seed=1, stats=True, final_obs=True)
+    ms = [MADDPG(env.K, env.H, env.W, device="cuda", seed=1, capturable=True) for _ in range(2)]
+    ro = Rollout(env, ms[0].actors, replay_slots=8, training=True, seed=2)
+    ro.reset()
+    for _ in range(6):
+        ro.step()
+    ro.fence()
+    ms[0].capture(ro.replay, warmup=0)
+    ms[0].learn_from(ro.replay, generator=torch.Generator(device="cuda").manual_seed(3))
+    _StackedLinear._ones.clear()  # the twin builds its own cache eagerly
+    ms[1].learn_from(ro.replay, generator=torch.Generator(device="cuda").manual_seed(3))
+    torch.cuda.synchronize()
+    for a, b in ((ms[0].actors.net, ms[1].actors.net), (ms[0].critics, ms[1].critics)):
+        assert torch.equal(a.flat_params(), b.flat_params())
+    env.close()
