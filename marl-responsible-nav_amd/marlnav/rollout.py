@@ -149,6 +149,11 @@ class Rollout:
         # the ring's device step count themselves (gw_step_out.stats_acc / tick), so a step needs
         # no reduction launch on any number of ranks; totals() all-reduces the total when read
         self._acc = torch.zeros_like(env.out["stats"]) if env.out.get("stats") is not None else None
+        self.gather = gather
+        if gather is not None and gather.count != env.E:
+            raise ValueError("ReturnGather shard size != env.E")
+        env.set_obs_async(obs_async, fear_async=fear_async)
+        self._pending = None  # (stats, tick) of a step whose FeAR may still be in flight
 
     def group_rank(self) -> int:
         return dist.get_rank(self.group) if self.distributed else 0
@@ -157,11 +162,6 @@ class Rollout:
     def has_stats(self) -> bool:
         """Whether the env produces the statistics rows that ``totals()`` sums."""
         return self._acc is not None
-        self.gather = gather
-        if gather is not None and gather.count != env.E:
-            raise ValueError("ReturnGather shard size != env.E")
-        env.set_obs_async(obs_async, fear_async=fear_async)
-        self._pending = None  # (stats, tick) of a step whose FeAR may still be in flight
 
     def _flush(self):
         """Reduce the statistics of the previous step once its FeAR outputs are ordered."""

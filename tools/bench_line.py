@@ -10,4 +10,6 @@ print(f"{lab:>14}: {d['value'] / 1e9:.3f} G  {d['ms_per_step'] * 1e3:.1f} us/ste
       f"{k['stream_ms_per_step'] * 1e3:.1f}  obs {k['obs_kernel'] * 1e3:.1f} step {k['step_kernel'] * 1e3:.1f} "
       f"fear {k['fear_kernel'] * 1e3:.1f} (n={k['profiled_steps']}, graph {k.get('graph_steps')}) "
       f"{r['kernel']} frac {r['frac'] if r['frac'] is None else round(r['frac'], 3)} "
+      f"(span {r.get('frac_per_launch_span') and round(r['frac_per_launch_span'], 3)}, "
+      f"period {r.get('frac_per_period') and round(r['frac_per_period'], 3)}) "
       f"host {k.get('host_enqueue_ms_per_step', 0) * 1e3:.1f} us/step")
