@@ -348,8 +348,10 @@ def test_gpu_capture_without_warmup_then_eager_learn():
         ro.step()
     ro.fence()
     ms[0].capture(ro.replay, warmup=0)
+    torch.cuda.manual_seed(7)  # the Gumbel uniforms come from the default generator
     ms[0].learn_from(ro.replay, generator=torch.Generator(device="cuda").manual_seed(3))
     _StackedLinear._ones.clear()  # the twin builds its own cache eagerly
+    torch.cuda.manual_seed(7)
     ms[1].learn_from(ro.replay, generator=torch.Generator(device="cuda").manual_seed(3))
     torch.cuda.synchronize()
     for a, b in ((ms[0].actors.net, ms[1].actors.net), (ms[0].critics, ms[1].critics)):
