@@ -65,6 +65,20 @@ gw_status gw_actor_act(void *env, const gw_mlp_actors *net, const float *ws, int
                        uint64_t seed, uint64_t counter, const float *uniform, const uint16_t *mask,
                        int32_t *actions, float *probs, float *logits, void *stream);
 
+/* ---- local windows (X1: not a reference format) ---------------------------------------------
+ * The same MLP actors over each RL agent's P x P egocentric window of its observation (the layout
+ * of gw_obs_patch: rows / cols -P/2 .. P-1-P/2 around the agent's own cell, -1 outside the grid);
+ * net->in_dim = P*P.  The window's static part depends only on its centre cell, so
+ *   h1 = T_k[centre] + sum over patched cells c inside the window of (obs[c] - map[c]) W1[pos(c), :]
+ * with T_k[c] = b1 + (the -1-padded map window centred on c) . W1 derived for every cell by
+ * gw_patch_actor_prepare.  No window is read back from HBM (gw_obs_patch writes them for the
+ * replay ring only).  Tolerance against torch on the cropped windows: tests/test_gpu_patch_actor.py. */
+int64_t gw_patch_actor_workspace_floats(int32_t P, int32_t H, int32_t W, int32_t K);
+gw_status gw_patch_actor_prepare(void *env, int32_t P, const gw_mlp_actors *net, float *ws, void *stream);
+gw_status gw_patch_actor_act(void *env, int32_t P, const gw_mlp_actors *net, const float *ws, int training, float tau,
+                             uint64_t seed, uint64_t counter, const float *uniform, const uint16_t *mask,
+                             int32_t *actions, float *probs, float *logits, void *stream);
+
 /* ---- the configs/cnn.yaml actor head ------------------------------------------------------
  * Conv2d(1, 32, 2, stride 2) - ReLU - Conv2d(32, 64, 2, stride 2) - ReLU - flatten (c, y, x)
  * - Linear(64 (H/4) (W/4), 128) - ReLU - Linear(128, 128) - ReLU - Linear(128, 9), per RL agent

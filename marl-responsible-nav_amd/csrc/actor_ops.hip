@@ -76,6 +76,9 @@ inline Ws ws_layout(float *base, int K) {
     return w;
 }
 
+// the window-variant workspace: the standard images (c1 / part unused), then [K][HW][128]
+inline float *patch_table(float *base, int K) { return base + (size_t)K * (HID + W2IMG + W3IMG + W2BIMG); }
+
 // bf16x3 split of an f32 (x = hi + mid + lo to ~2^-24 relative; round-to-nearest-even bits)
 __host__ __device__ inline uint32_t bf16_rn_bits(float x) {
     uint32_t u;
@@ -135,8 +138,10 @@ struct ActParams {
     int32_t *actions;         // [E][K]
     float *probs;             // [K][E][9]
     float *logits;            // [K][E][9] or null
+    const float *tbl;         // PW: [K][HW][128] layer-1 map part of the window centred on each cell
     int64_t E, env_offset;
     int N, K, HW, variant, training, tiles;
+    int W, P, in_dim;         // grid width; PW: window side P, in_dim = P * P (else in_dim = HW)
     int ab;                   // GW_ACT_AB (measurement only): bit 0 zero the W1 deltas, bit 1 skip
                               // layer 2's MFMAs, bit 2 skip the epilogue, bit 4 gather row 0 only
     float tau;
@@ -227,6 +232,27 @@ __global__ void __launch_bounds__(256) prep_images(PrepParams p) {
     }
 }
 
+// ---- gw_patch_actor_prepare: tbl[k][c][j] = b1[k][j] + sum over window positions o of the map
+//      value under o (-1 outside the grid) * W1[k][o][j], for the window centred on cell c ----
+struct TblParams {
+    const float *w1, *b1, *base;
+    float *tbl;
+    int H, W, P;
+};
+__global__ void __launch_bounds__(HID) prep_patch_table(TblParams p) {
+    const int c = blockIdx.x, k = blockIdx.y, j = threadIdx.x;
+    const int HW = p.H * p.W, PP = p.P * p.P, half = p.P / 2;
+    const int cr = c / p.W, cc = c % p.W;
+    const float *w1 = p.w1 + (size_t)k * PP * HID;
+    float acc = 0.0f;
+    for (int o = 0; o < PP; ++o) {
+        const int r = cr + o / p.P - half, q = cc + o % p.P - half;
+        const float mv = (r >= 0 && r < p.H && q >= 0 && q < p.W) ? p.base[r * p.W + q] : -1.0f;
+        if (mv != 0.0f) acc = fmaf(mv, w1[(size_t)o * HID + j], acc);
+    }
+    p.tbl[((size_t)k * HW + c) * HID + j] = p.b1[k * HID + j] + acc;
+}
+
 // ---- gw_actor_act --------------------------------------------------------------------------
 __device__ __forceinline__ float quad_sum(float s) {  // over the four lanes of an env
     s += __shfl_xor(s, 16, 64);
@@ -262,7 +288,10 @@ __device__ __forceinline__ Desc load_desc(const ActParams &p, int64_t e, int k) 
 // BF3: layer 2 as bf16x3 products on v_mfma_f32_16x16x32_bf16 (6 of the 9 part products, f32
 // accumulation; ~2^-24 relative per product, 16x the f32 MFMA rate per instruction)
 // H1: layer 1 is read from p.h1 (computed by cnn_l1_kernel) instead of the obs descriptors
-template <int NP, int WAVES, bool BF3 = false, bool H1 = false>  // NP = patch slots per (env, agent) = N + 1
+// PW: the input is the agent's P x P egocentric window (gw_obs_patch's layout): layer 1 starts
+//     from the table row of the agent's cell (p.tbl: bias + the window's map part) and a patched
+//     cell inside the window adds its delta times the W1 row of its window position
+template <int NP, int WAVES, bool BF3 = false, bool H1 = false, bool PW = false>  // NP = patch slots per (env, agent) = N + 1
 __global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
     constexpr int THREADS = 64 * WAVES;
     constexpr int NW2 = BF3 ? W2B_U4 : W2IMG / 4;
@@ -315,9 +344,10 @@ __global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
     int it = 0;
     const int stride = gridDim.x * WAVES;
 
-    const float *w1 = p.net.w1 + (size_t)k * p.HW * HID;
+    const float *w1 = p.net.w1 + (size_t)k * p.in_dim * HID;
     const int K = p.K;
     const int ac_k = p.apples[k];
+    const int half = p.P / 2;
     // layer-1 register 4j + i and layer-2 register (m = j, r = i) both hold feature 16j + 4q + i
     auto vec4 = [q](const float *v, int j) { return *reinterpret_cast<const float4 *>(v + 16 * j + 4 * q); };
 
@@ -374,6 +404,18 @@ __global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
             }
         } else {
         // ---- layer 1: c1 + sum of (value - map) * W1 row over the distinct patched cells ----
+        const int ctr = PW ? ((unsigned)pc[1 + k] < (unsigned)p.HW ? pc[1 + k] : 0) : 0;  // PW: the window's centre
+        if (PW) {  // the table row of the centre: b1 + the window's map part (L2 resident)
+            const float4 *t = reinterpret_cast<const float4 *>(p.tbl + ((size_t)k * p.HW + ctr) * HID);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float4 c = t[4 * j + q];
+                a[4 * j] = c.x;
+                a[4 * j + 1] = c.y;
+                a[4 * j + 2] = c.z;
+                a[4 * j + 3] = c.w;
+            }
+        } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {  // features 16j + 4q .. + 3: one 16-byte LDS read
             const float4 c = vec4(s_vec[0], j);
@@ -381,6 +423,7 @@ __global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
             a[4 * j + 1] = c.y;
             a[4 * j + 2] = c.z;
             a[4 * j + 3] = c.w;
+        }
         }
         // unconditional loads (a dead slot reads row 0 with delta 0: fmaf(0, w, a) == a), so
         // the scheduler can keep several slots' row pieces in flight
@@ -394,8 +437,15 @@ __global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
             for (int r = i + 1; r < NP; ++r) last = last && pc[r] != c;
             const int cc = last ? c : 0;
             const float map = ((s_road[cc >> 5] >> (cc & 31)) & 1u) ? 0.0f : -1.0f;
+            int row = cc;
+            if (PW) {  // window position of the cell (rows / cols -P/2 .. P-1-P/2 around the centre)
+                const int wr = cc / p.W - ctr / p.W + half, wc = cc % p.W - ctr % p.W + half;
+                const bool in = (unsigned)wr < (unsigned)p.P && (unsigned)wc < (unsigned)p.P;
+                last = last && in;
+                row = in ? wr * p.P + wc : 0;
+            }
             dlt[i] = (last && !(p.ab & 1)) ? pv[i] - map : 0.0f;
-            rowc[i] = (p.ab & 16) ? q : cc * (HID / 4) + q;  // float4 index of features 4q .. 4q + 3 of row cc
+            rowc[i] = (p.ab & 16) ? q : row * (HID / 4) + q;  // float4 index of features 4q .. 4q + 3 of row
         }
         const float4 *w1v = reinterpret_cast<const float4 *>(w1);
 #pragma unroll
@@ -1092,10 +1142,12 @@ gw_status err(gw_status s, const std::string &msg) {
     return s;
 }
 
-gw_status check_net(const gw_obs_source &src, const gw_mlp_actors *net, const char *who) {
+gw_status check_net(const gw_obs_source &src, const gw_mlp_actors *net, const char *who, int P = 0) {
     const std::string w(who);
     if (net->K != src.K) return err(GW_ERR_ARG, w + ": net K != env K");
-    if (net->in_dim != src.H * src.W) return err(GW_ERR_ARG, w + ": in_dim != H*W");
+    if (P > 0 && (P > 129 || net->in_dim != P * P)) return err(GW_ERR_ARG, w + ": need 1 <= P <= 129 and in_dim == P*P");
+    if (P <= 0 && net->in_dim != src.H * src.W) return err(GW_ERR_ARG, w + ": in_dim != H*W");
+    if (src.H * src.W > 128 * 32) return err(GW_ERR_ARG, w + ": H*W must be <= 4096");
     if (net->hidden != HID || net->n_actions != NA) return err(GW_ERR_ARG, w + ": only hidden 128 and 9 actions are fused");
     if (!net->w1 || !net->b1 || !net->w2 || !net->b2 || !net->w3 || !net->b3 ||
         (net->layer_norm && (!net->ln1_w || !net->ln1_b || !net->ln2_w || !net->ln2_b)))
@@ -1191,23 +1243,28 @@ gw_status gw_actor_prepare(void *env, const gw_mlp_actors *net, float *ws, void 
     return GW_OK;
 }
 
-gw_status gw_actor_act(void *env, const gw_mlp_actors *net, const float *ws, int training, float tau, uint64_t seed,
-                       uint64_t counter, const float *uniform, const uint16_t *mask, int32_t *actions, float *probs,
-                       float *logits, void *stream) {
-    if (!env || !net || !ws || !actions || !probs) return err(GW_ERR_ARG, "gw_actor_act: null argument");
-    if (reinterpret_cast<uintptr_t>(ws) & 15u) return err(GW_ERR_ARG, "gw_actor_act: ws must be 16-byte aligned");
+}  // extern "C"
+
+namespace {
+// gw_actor_act (P = 0) and gw_patch_actor_act (P > 0: the P x P window variant)
+gw_status actor_act(const char *who, void *env, int32_t P, const gw_mlp_actors *net, const float *ws, int training,
+                    float tau, uint64_t seed, uint64_t counter, const float *uniform, const uint16_t *mask,
+                    int32_t *actions, float *probs, float *logits, void *stream) {
+    const std::string w(who);
+    if (!env || !net || !ws || !actions || !probs) return err(GW_ERR_ARG, w + ": null argument");
+    if (reinterpret_cast<uintptr_t>(ws) & 15u) return err(GW_ERR_ARG, w + ": ws must be 16-byte aligned");
     gw_obs_source src;
     gw_status st = gw_obs_view(env, &src);
     if (st != GW_OK) return st;
-    if ((st = check_net(src, net, "gw_actor_act")) != GW_OK) return st;
-    if (!(tau > 0.0f)) return err(GW_ERR_ARG, "gw_actor_act: tau must be > 0");
+    if ((st = check_net(src, net, who, P)) != GW_OK) return st;
+    if (!(tau > 0.0f)) return err(GW_ERR_ARG, w + ": tau must be > 0");
     ActParams p;
     p.net = *net;
-    const Ws w = ws_layout(const_cast<float *>(ws), src.K);
-    p.c1 = w.c1;
-    p.w2img = w.w2;
-    p.w3img = w.w3;
-    p.w2bimg = w.w2b;
+    const Ws wl = ws_layout(const_cast<float *>(ws), src.K);
+    p.c1 = wl.c1;
+    p.w2img = wl.w2;
+    p.w3img = wl.w3;
+    p.w2bimg = wl.w2b;
     p.desc = src.desc;
     p.base = src.base;
     p.mask = mask;
@@ -1223,6 +1280,10 @@ gw_status gw_actor_act(void *env, const gw_mlp_actors *net, const float *ws, int
     p.N = src.N;
     p.K = src.K;
     p.HW = src.H * src.W;
+    p.W = src.W;
+    p.P = P;
+    p.in_dim = P > 0 ? P * P : p.HW;
+    p.tbl = P > 0 ? patch_table(const_cast<float *>(ws), src.K) : nullptr;
     p.variant = src.variant;
     p.training = training ? 1 : 0;
     p.tau = tau;
@@ -1238,7 +1299,7 @@ gw_status gw_actor_act(void *env, const gw_mlp_actors *net, const float *ws, int
     // GW_ACT_V (A/B): 4 (default) = one 16-wave block per CU, layer 2 as bf16x3 MFMA products;
     // 2 = the same with f32 MFMA (exact products); 0 = two 8-wave blocks per CU, f32 MFMA
     const char *av = std::getenv("GW_ACT_V");
-    const int v = av ? std::atoi(av) : 4;
+    const int v = P > 0 ? 4 : (av ? std::atoi(av) : 4);
     const int waves = v == 0 ? 8 : 16;
     const int resident = v == 0 ? 512 : 256;
     const int64_t want = (tiles + waves - 1) / waves;
@@ -1247,7 +1308,9 @@ gw_status gw_actor_act(void *env, const gw_mlp_actors *net, const float *ws, int
     hipStream_t s = static_cast<hipStream_t>(stream);
 #define ACT_LAUNCH(NP)                                                                   \
     do {                                                                                 \
-        if (v == 0)                                                                      \
+        if (P > 0)                                                                       \
+            hipLaunchKernelGGL((act_kernel<NP, 16, true, false, true>), grid, block, 0, s, p); \
+        else if (v == 0)                                                                 \
             hipLaunchKernelGGL((act_kernel<NP, 8>), grid, block, 0, s, p);               \
         else if (v == 4)                                                                 \
             hipLaunchKernelGGL((act_kernel<NP, 16, true>), grid, block, 0, s, p);        \
@@ -1263,13 +1326,66 @@ gw_status gw_actor_act(void *env, const gw_mlp_actors *net, const float *ws, int
         case 6: ACT_LAUNCH(7); break;
         case 7: ACT_LAUNCH(8); break;
         case 8: ACT_LAUNCH(9); break;
-        default: return err(GW_ERR_ARG, "gw_actor_act: N out of range");
+        default: return err(GW_ERR_ARG, w + ": N out of range");
     }
 #undef ACT_LAUNCH
     const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return err(GW_ERR_HIP, std::string("gw_actor_act: ") + hipGetErrorString(e));
+    if (e != hipSuccess) return err(GW_ERR_HIP, w + ": " + hipGetErrorString(e));
     return GW_OK;
 }
+}  // namespace
+
+extern "C" {
+
+gw_status gw_actor_act(void *env, const gw_mlp_actors *net, const float *ws, int training, float tau, uint64_t seed,
+                       uint64_t counter, const float *uniform, const uint16_t *mask, int32_t *actions, float *probs,
+                       float *logits, void *stream) {
+    return actor_act("gw_actor_act", env, 0, net, ws, training, tau, seed, counter, uniform, mask, actions, probs,
+                     logits, stream);
+}
+
+int64_t gw_patch_actor_workspace_floats(int32_t P, int32_t H, int32_t W, int32_t K) {
+    (void)P;
+    return (int64_t)K * (HID + W2IMG + W3IMG + W2BIMG) + (int64_t)K * H * W * HID;
+}
+
+gw_status gw_patch_actor_prepare(void *env, int32_t P, const gw_mlp_actors *net, float *ws, void *stream) {
+    if (!env || !net || !ws) return err(GW_ERR_ARG, "gw_patch_actor_prepare: null argument");
+    if (reinterpret_cast<uintptr_t>(ws) & 15u) return err(GW_ERR_ARG, "gw_patch_actor_prepare: ws must be 16-byte aligned");
+    gw_obs_source src;
+    gw_status st = gw_obs_view(env, &src);
+    if (st != GW_OK) return st;
+    if ((st = check_net(src, net, "gw_patch_actor_prepare", P)) != GW_OK) return st;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    TblParams tp;
+    tp.w1 = net->w1;
+    tp.b1 = net->b1;
+    tp.base = src.base;
+    tp.tbl = patch_table(ws, src.K);
+    tp.H = src.H;
+    tp.W = src.W;
+    tp.P = P;
+    hipLaunchKernelGGL(prep_patch_table, dim3(src.H * src.W, src.K), dim3(HID), 0, s, tp);
+    PrepParams pp;  // the layer-2/3 MFMA images (prep_images; nslices 0: c1 = b1, unused)
+    pp.net = *net;
+    pp.HW = P * P;
+    pp.nslices = 0;
+    pp.ws = ws_layout(ws, src.K);
+    pp.base = src.base;
+    hipLaunchKernelGGL(prep_images, dim3(16, src.K), dim3(256), 0, s, pp);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return err(GW_ERR_HIP, std::string("gw_patch_actor_prepare: ") + hipGetErrorString(e));
+    return GW_OK;
+}
+
+gw_status gw_patch_actor_act(void *env, int32_t P, const gw_mlp_actors *net, const float *ws, int training, float tau,
+                             uint64_t seed, uint64_t counter, const float *uniform, const uint16_t *mask,
+                             int32_t *actions, float *probs, float *logits, void *stream) {
+    if (P < 1) return err(GW_ERR_ARG, "gw_patch_actor_act: P must be >= 1");
+    return actor_act("gw_patch_actor_act", env, P, net, ws, training, tau, seed, counter, uniform, mask, actions,
+                     probs, logits, stream);
+}
+
 
 int64_t gw_cnn_workspace_floats(int32_t H, int32_t W, int32_t K, int64_t E) {
     return cnn_ws_floats(K, (H / 4) * (W / 4), E);
@@ -1361,6 +1477,10 @@ gw_status gw_cnn_act(void *env, const gw_cnn_actors *net, const float *ws, int t
     p.N = src.N;
     p.K = src.K;
     p.HW = src.H * src.W;
+    p.W = src.W;
+    p.P = 0;
+    p.in_dim = p.HW;
+    p.tbl = nullptr;
     p.variant = src.variant;
     p.training = training ? 1 : 0;
     p.tau = tau;

@@ -171,7 +171,8 @@ EXPORTS = ["gw_create", "gw_reset", "gw_step", "gw_state_view", "gw_copy_state",
            "gw_ln_relu_fwd", "gw_ln_relu_bwd", "gw_gumbel_softmax",
            "gw_replay_gather", "gw_affine_relu_fwd", "gw_affine_relu_bwd",
            "gw_soft_update2", "gw_td_target", "gw_mean_loss_fwd", "gw_mean_loss_bwd",
-           "gw_eval_accum", "gw_profile_spans"]
+           "gw_eval_accum", "gw_profile_spans", "gw_patch_actor_workspace_floats", "gw_patch_actor_prepare",
+           "gw_patch_actor_act"]
 
 
 class GwObsSource(C.Structure):
@@ -269,6 +270,13 @@ def _declare(L):
     L.gw_actor_act.argtypes = [p, C.POINTER(GwMlpActors), p, C.c_int, C.c_float, C.c_uint64, C.c_uint64,
                                p, p, p, p, p, p]
     L.gw_actor_act.restype = C.c_int
+    L.gw_patch_actor_workspace_floats.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_int32]
+    L.gw_patch_actor_workspace_floats.restype = C.c_int64
+    L.gw_patch_actor_prepare.argtypes = [p, C.c_int32, C.POINTER(GwMlpActors), p, p]
+    L.gw_patch_actor_prepare.restype = C.c_int
+    L.gw_patch_actor_act.argtypes = [p, C.c_int32, C.POINTER(GwMlpActors), p, C.c_int, C.c_float, C.c_uint64,
+                                     C.c_uint64, p, p, p, p, p, p]
+    L.gw_patch_actor_act.restype = C.c_int
     L.gw_actor_workspace_floats.argtypes = [C.c_int32, C.c_int32]
     L.gw_actor_workspace_floats.restype = C.c_int64
     L.gw_actor_prepare.argtypes = [p, C.POINTER(GwMlpActors), p, p]

@@ -402,12 +402,18 @@ class MultiAgentActors(nn.Module):
         return actions, probs
 
     # ---------------------------------------------------------------------------------------
-    def fusable(self, env) -> bool:
+    def fusable(self, env, patch: int = 0) -> bool:
         """The fused HIP get_action covers (gw_actor_act, include/actor_ops.h) the stacked f32 MLP
         with two 128-wide hidden layers and (gw_cnn_act) the configs/cnn.yaml CNN head, over a
-        VecGridEnv's own observations."""
+        VecGridEnv's own observations; patch = P > 0: the MLP over each agent's P x P window
+        (gw_patch_actor_act)."""
         if self.dtype != torch.float32 or self.K != env.K:
             return False
+        if patch:
+            net = getattr(self, "net", None)
+            return (self.arch == "mlp" and (self.H, self.W) == (patch, patch) and env.H * env.W <= 4096
+                    and net.n_layers == 3 and net.weights[0].shape[-1] == 128
+                    and net.weights[1].shape == (self.K, 128, 128) and net.weights[2].shape[-1] == N_ACTIONS)
         if self.arch == "cnn":
             return ((self.H, self.W) == (env.H, env.W) and env.H % 4 == 0 and env.W % 4 == 0
                     and env.H * env.W <= 4096 and all(n.fusable() for n in self.nets))
@@ -429,25 +435,30 @@ class MultiAgentActors(nn.Module):
     def act_env(self, env, mask: torch.Tensor | None = None, training: bool = True, tau: float = 1.0,
                 seed: int = 0, counter: int = 0, uniform: torch.Tensor | None = None,
                 actions_out: torch.Tensor | None = None, probs_out: torch.Tensor | None = None,
-                logits_out: torch.Tensor | None = None):
+                logits_out: torch.Tensor | None = None, patch: int = 0):
         """``act`` on the observation ``env`` last wrote, as ONE fused HIP kernel (gw_actor_act):
         the first layer from the env's obs descriptors (map + patched cells, no obs read back),
         layers 2-3 on f32 MFMA, Gumbel noise from Philox(seed; env, counter, k) or ``uniform``
         [K, E, 9], softmax, mask, argmax.  -> (actions [E, K] int32, probs [K, E, 9] float32).
+        patch = P > 0: actors built for P x P inputs act on each agent's egocentric window
+        (gw_patch_actor_act; the windows VecGridEnv.obs_patch(P) would write).
         Raises if the library or a GPU is missing (no fallback)."""
         from . import _lib
         if self.arch == "cnn":
             return self._act_env_cnn(env, mask, training, tau, seed, counter, uniform, actions_out, probs_out,
                                      logits_out)
         net, K, E, dev = self.net, self.K, env.E, env.device
+        patch = int(patch)
         st = self._fast
-        if st is None or st["env"] is not env:  # per-(actors, env) constants, built once
-            if not self.fusable(env):
-                raise _lib.GwError("act_env: actor not fusable (needs the f32 MLP 128-128-9 over the env's H*W obs)")
+        if st is None or st["env"] is not env or st.get("patch", 0) != patch:  # per-(actors, env) constants
+            if not self.fusable(env, patch):
+                raise _lib.GwError("act_env: actor not fusable (needs the f32 MLP 128-128-9 over the env's H*W obs, "
+                                   "or over P x P windows with patch=P)")
             lib = _lib.load()
-            ws_n = int(lib.gw_actor_workspace_floats(net.in_dim, K))
+            ws_n = int(lib.gw_patch_actor_workspace_floats(patch, env.H, env.W, K) if patch
+                       else lib.gw_actor_workspace_floats(net.in_dim, K))
             st = self._fast = dict(env=env, lib=lib, ws=torch.empty(ws_n, dtype=torch.float32, device=dev), key=None,
-                                   spec=None, actions=None, probs=None)
+                                   spec=None, actions=None, probs=None, patch=patch)
         ln = net.layer_norm
         flat = net.flat_params()
         # the workspace (c1 = b1 + map . W1, W2/W3 operand images) is derived once per parameter
@@ -462,8 +473,15 @@ class MultiAgentActors(nn.Module):
                                           *[t.data_ptr() if (ln or i % 4 < 2 or i >= 8) else None
                                             for i, t in enumerate(ptrs)])
             with torch.cuda.device(dev):
-                _lib.check(st["lib"].gw_actor_prepare(env.handle, C.byref(st["spec"]), st["ws"].data_ptr(),
-                                                      torch.cuda.current_stream(dev).cuda_stream), "gw_actor_prepare")
+                if patch:
+                    _lib.check(st["lib"].gw_patch_actor_prepare(env.handle, patch, C.byref(st["spec"]),
+                                                                st["ws"].data_ptr(),
+                                                                torch.cuda.current_stream(dev).cuda_stream),
+                               "gw_patch_actor_prepare")
+                else:
+                    _lib.check(st["lib"].gw_actor_prepare(env.handle, C.byref(st["spec"]), st["ws"].data_ptr(),
+                                                          torch.cuda.current_stream(dev).cuda_stream),
+                               "gw_actor_prepare")
             st["key"] = key
         if actions_out is None:
             actions_out = torch.empty((E, K), dtype=torch.int32, device=dev)
@@ -477,13 +495,15 @@ class MultiAgentActors(nn.Module):
             raise ValueError("act_env: uniform must be float32 [K, E, 9]")
         if mask is not None and not (mask.shape == (E, K) and mask.element_size() == 2 and mask.is_contiguous()):
             raise ValueError("act_env: mask must be a contiguous 16-bit [E, K] tensor")
-        _lib.check(st["lib"].gw_actor_act(env.handle, C.byref(st["spec"]), st["ws"].data_ptr(), int(bool(training)),
-                                          float(tau), int(seed) & 0xFFFFFFFFFFFFFFFF, int(counter) & 0xFFFFFFFFFFFFFFFF,
-                                          uniform.contiguous().data_ptr() if uniform is not None else None,
-                                          mask.data_ptr() if mask is not None else None, actions_out.data_ptr(),
-                                          probs_out.data_ptr(),
-                                          logits_out.data_ptr() if logits_out is not None else None,
-                                          torch.cuda.current_stream(dev).cuda_stream), "gw_actor_act")
+        args = (C.byref(st["spec"]), st["ws"].data_ptr(), int(bool(training)),
+                float(tau), int(seed) & 0xFFFFFFFFFFFFFFFF, int(counter) & 0xFFFFFFFFFFFFFFFF,
+                uniform.contiguous().data_ptr() if uniform is not None else None,
+                mask.data_ptr() if mask is not None else None, actions_out.data_ptr(), probs_out.data_ptr(),
+                logits_out.data_ptr() if logits_out is not None else None, torch.cuda.current_stream(dev).cuda_stream)
+        if patch:
+            _lib.check(st["lib"].gw_patch_actor_act(env.handle, patch, *args), "gw_patch_actor_act")
+        else:
+            _lib.check(st["lib"].gw_actor_act(env.handle, *args), "gw_actor_act")
         return actions_out, probs_out
 
     def _act_env_cnn(self, env, mask, training, tau, seed, counter, uniform, actions_out, probs_out, logits_out):

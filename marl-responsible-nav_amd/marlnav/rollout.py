@@ -128,7 +128,7 @@ class Rollout:
         with obs=False."""
         self.env = env
         self.actors = actors
-        self.fused = (actors is not None and not patch and actors.fusable(env)) if fused is None else bool(fused)
+        self.fused = (actors is not None and actors.fusable(env, patch)) if fused is None else bool(fused)
         self.seed = int(seed)
         self._calls = 0  # Philox counter of the fused path's Gumbel noise (never repeats)
         self._actions = torch.empty((env.E, env.K), dtype=torch.int32, device=env.device)
@@ -199,7 +199,7 @@ class Rollout:
             self.replay.t_dev.zero_()
         else:
             self.env.reset()
-            if self.patch:
+            if self.patch and not self.fused:
                 self._patch = self.env.obs_patch(self.patch, out=self._patch)
         self.t = 0
 
@@ -216,7 +216,7 @@ class Rollout:
         if self.actors is not None and self.fused:
             probs_out = self.replay.probs[cur] if self.replay is not None else None
             actions, probs = self.actors.act_env(env, mask, self.training, seed=self.seed, counter=self._calls,
-                                                 actions_out=self._actions, probs_out=probs_out)
+                                                 actions_out=self._actions, probs_out=probs_out, patch=self.patch)
             self._calls += 1
         elif self.actors is not None:
             if not self.patch:
@@ -251,7 +251,7 @@ class Rollout:
             if self._acc is not None:
                 into["stats_acc"] = self._acc
             r = env.step(actions, into=into or None)
-            if self.patch:
+            if self.patch and not self.fused:  # the fused actor reads the descriptors, not the windows
                 self._patch = env.obs_patch(self.patch, out=self._patch)
         self.t += 1
         tick = self.replay.t_dev if self.replay is not None else None

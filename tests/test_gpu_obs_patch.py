@@ -91,7 +91,7 @@ def test_patch_rollout_feeds_the_actor_and_the_ring():
     E, P, T, S = 1500, 9, 20, 24
     actors = MultiAgentActors(2, P, P, "mlp", device="cuda", seed=4)
     env_p = VecGridEnv("grid32", num_envs=E, fear=True, fear_weight=-5.0, seed=11, max_steps=12, obs=False, stats=True)
-    ro = Rollout(env_p, actors, replay_slots=S, training=True, seed=6, patch=P)
+    ro = Rollout(env_p, actors, replay_slots=S, training=True, seed=6, patch=P, fused=False)  # the torch actor
     assert not ro.fused
     ro.reset()
     env_f = VecGridEnv("grid32", num_envs=E, fear=True, fear_weight=-5.0, seed=11, max_steps=12, final_obs=True,
