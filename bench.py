@@ -50,8 +50,8 @@ CONFIGS = {
                         "MEMORY_SIZE 200000, per-step RCCL reduction of the episode statistics)"),
     "c5patch": dict(scenario="grid32", envs=65536, fear=True, fear_weight=-5.0, rollout=True, patch=11,
                     workload="C5's rollout with egocentric 11x11 local observations (gw_obs_patch; not a "
-                             "reference format, reported separately): no dense obs, stacked MLP actors (121 "
-                             "inputs, PyTorch), patch replay ring, FeAR on"),
+                             "reference format, reported separately): no dense obs, the MADDPG MLP actors on "
+                             "121 inputs (fused gw_patch_actor_act), patch replay ring, FeAR on"),
     "c4cnn": dict(scenario="grid64_n8", envs=65536, fear=False, fear_weight=-5.0, rollout=True, arch="cnn",
                   workload="BASELINE config 4 as a rollout: 8-agent 64x64 grid, 65536 envs, the configs/cnn.yaml "
                            "actor head (conv 32-64, k2 s2, 128-128, f32; fused gw_cnn_act from the obs "
@@ -222,6 +222,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cnn-torch", action="store_true",
                     help="c4cnn: the PyTorch CNN forward on the dense obs instead of gw_cnn_act (A/B)")
+    ap.add_argument("--patch-torch", action="store_true",
+                    help="c5patch: the PyTorch actor forward on the written windows instead of gw_patch_actor_act (A/B)")
     ap.add_argument("--high-prio", action="store_true",
                     help="run the step chain on a high-priority stream (its kernels' workgroups are "
                          "dispatched ahead of the concurrent obs writer's)")
@@ -359,11 +361,10 @@ def main():
         # one set of actor weights for every rank: built from the same seed and broadcast from
         # rank 0 (MADDPG does it itself); every rank's sampling draws its own batches
         torch.cuda.manual_seed(1234 + rank)
-        if cfg.get("patch"):  # local observations: PyTorch MLP actors on the P x P windows
-            from marlnav.actor import MultiAgentActors
-            learner = None
-            actors = MultiAgentActors(K, cfg["patch"], cfg["patch"], "mlp", device=env.device, seed=0)
-            broadcast_module(actors)
+        if cfg.get("patch"):  # local observations: the MADDPG actors on the P x P windows (fused
+            # gw_patch_actor_act from the obs descriptors; --patch-torch: the PyTorch forward, A/B)
+            learner = MADDPG(K, cfg["patch"], cfg["patch"], device=env.device, seed=0, capturable=True)
+            actors = learner.actors
         elif cfg.get("arch") == "cnn":  # configs/cnn.yaml head: fused gw_cnn_act (or PyTorch, A/B)
             from marlnav.actor import MultiAgentActors
             learner = None
@@ -377,7 +378,7 @@ def main():
         # the fused actor's Gumbel noise is Philox keyed by (seed; global env id, step, agent):
         # one seed for all ranks keeps every env's trajectory independent of the rank count
         ro = Rollout(env, actors, replay_slots=-(-200_000 // E) + 1, training=True, seed=42,
-                     fused=False if args.cnn_torch else None,
+                     fused=False if (args.cnn_torch or args.patch_torch) else None,
                      obs_async=obs_mode, fear_async=bool(obs_mode) and args.fear_async, gather=gather,
                      patch=cfg.get("patch", 0))
         ro.reset()
