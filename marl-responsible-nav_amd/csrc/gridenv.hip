@@ -1716,25 +1716,31 @@ __global__ void __launch_bounds__(128) step_v2(Params p) {
 // reference observes the whole grid, custom/ma_customenv.py:303-322): an opt-in input format.
 // ---------------------------------------------------------------------------------------
 constexpr int PATCH_THREADS = 256;
+constexpr int PATCH_BE = 32;  // envs per block: a block's windows of one agent are one contiguous run
 
+// Block = PATCH_BE envs.  Per (which, env, agent) the window's centre and its patched cells as
+// window positions (-1: outside the window) are staged in LDS; then each agent's contiguous run
+// of nenv * P * P floats is written as 16-byte stores where the run is 16-byte aligned (scalar
+// stores otherwise, and for the terminal windows of envs that did not end).
 __global__ void __launch_bounds__(PATCH_THREADS) patch_kernel(Params p, int P, float *__restrict__ patch,
                                                               float *__restrict__ final_patch) {
     extern __shared__ uint32_t plds[];
     const int tid = threadIdx.x;
-    const int HW = p.HW, W = p.W, H = p.H, N = p.N, K = p.K, be = p.obs_be;
-    const int npatch = N + 1, nroad = (HW + 31) / 32;
+    const int W = p.W, H = p.H, N = p.N, K = p.K;
+    const int npatch = N + 1, nroad = (p.HW + 31) / 32;
     uint32_t *s_road = plds;
-    uint32_t *s_flag = s_road + nroad;                                   // [be]
-    int *s_ctr = reinterpret_cast<int *>(s_flag + be);                   // [2][be][K]
-    int *s_pc = s_ctr + 2 * be * K;                                      // [2][be][K][npatch]
-    float *s_pv = reinterpret_cast<float *>(s_pc + 2 * be * K * npatch);
-    const int64_t e0 = (int64_t)blockIdx.x * be;
+    uint32_t *s_flag = s_road + nroad;                                   // [PATCH_BE]
+    int *s_ctr = reinterpret_cast<int *>(s_flag + PATCH_BE);             // [2][PATCH_BE][K]: row << 16 | col
+    int *s_pw = s_ctr + 2 * PATCH_BE * K;                                // [2][PATCH_BE][K][npatch] window positions
+    float *s_pv = reinterpret_cast<float *>(s_pw + 2 * PATCH_BE * K * npatch);
+    const int64_t e0 = (int64_t)blockIdx.x * PATCH_BE;
     if (e0 >= p.E) return;  // uniform per block
-    const int nenv = (int)min((int64_t)be, p.E - e0);
+    const int nenv = (int)min((int64_t)PATCH_BE, p.E - e0);
+    const int PP = P * P, half = P / 2;
     for (int w = tid; w < nroad; w += PATCH_THREADS) s_road[w] = p.tb.roadbits[w];
-    for (int u = tid; u < 2 * be * K; u += PATCH_THREADS) {  // one thread per (which, env, k)
-        const int which = u / (be * K), el = (u / K) % be, k = u % K;
-        const int slot = (which * be + el) * K + k;
+    for (int u = tid; u < 2 * PATCH_BE * K; u += PATCH_THREADS) {  // one thread per (which, env, k)
+        const int which = u / (PATCH_BE * K), el = (u / K) % PATCH_BE, k = u % K;
+        const int slot = (which * PATCH_BE + el) * K + k;
         if (el >= nenv) continue;
         const uint32_t *d = p.desc + (e0 + el) * NDESC;
         const uint32_t f = d[4];
@@ -1743,45 +1749,83 @@ __global__ void __launch_bounds__(PATCH_THREADS) patch_kernel(Params p, int P, f
         const uint32_t apples = which == 0 ? (f >> 8) & 0xFFu : (f >> 16) & 0xFFu;
         const uint32_t *pw = d + (which == 0 ? 0 : 8);
         const int ac = ((apples >> k) & 1u) ? p.apples[k] : -1;
+        const int ctr = (int)((pw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
+        const int cr = ctr / W, cc = ctr - cr * W;
+        s_ctr[slot] = (cr << 16) | cc;
         int np = 0;
+        auto put = [&](int c, float v) {  // window position of cell c, or -1 outside the window
+            const int wr = c / W - cr + half, wc = c % W - cc + half;
+            s_pw[slot * npatch + np] = ((unsigned)wr < (unsigned)P && (unsigned)wc < (unsigned)P) ? wr * P + wc : -1;
+            s_pv[slot * npatch + np] = v;
+            ++np;
+        };
         if (ac >= 0) {
             float av = p.tb.base[ac] + 9.0f;
             if (!reset && av == (float)(k + 1)) av = 1.0f;
-            s_pc[slot * npatch + np] = ac;
-            s_pv[slot * npatch + np] = av;
-            ++np;
+            put(ac, av);
         }
         for (int n = 0; n < N; ++n) {
             const int c = (int)((pw[n >> 1] >> (16 * (n & 1))) & 0xFFFFu);
-            if (n == k) s_ctr[slot] = c;
-            s_pc[slot * npatch + np] = c;
-            s_pv[slot * npatch + np] = agent_value(reset, n, k, c == ac, p.variant);
-            ++np;
+            put(c, agent_value(reset, n, k, c == ac, p.variant));
         }
-        for (; np < npatch; ++np) s_pc[slot * npatch + np] = -1;
+        for (; np < npatch; ++np) s_pw[slot * npatch + np] = -1;
     }
     __syncthreads();
-    const int PP = P * P, half = P / 2;
+    // value of window position c of (which, el, k): the map under it (-1 outside the grid), then
+    // the patched cells in order (a later one overrides an earlier one, as the obs writer does)
+    auto value = [&](int which, int el, int k, int c) -> float {
+        const int slot = (which * PATCH_BE + el) * K + k;
+        const int ctr = s_ctr[slot];
+        const int wr = c / P;
+        const int r = (ctr >> 16) + wr - half, q = (ctr & 0xFFFF) + (c - wr * P) - half;
+        float v = -1.0f;
+        if (r >= 0 && r < H && q >= 0 && q < W) {
+            const int cell = r * W + q;
+            v = ((s_road[cell >> 5] >> (cell & 31)) & 1u) ? 0.0f : -1.0f;
+        }
+        const int *pwv = s_pw + slot * npatch;
+        for (int u = 0; u < npatch; ++u)
+            if (pwv[u] == c) v = s_pv[slot * npatch + u];
+        return v;
+    };
     for (int which = 0; which < 2; ++which) {
         float *dst = which == 0 ? patch : final_patch;
         if (!dst) continue;
         const uint32_t need = which == 0 ? D_WRITE : D_FINAL;
         for (int k = 0; k < K; ++k) {
-            float *o = dst + ((int64_t)k * p.E + e0) * PP;
-            for (int i = tid; i < nenv * PP; i += PATCH_THREADS) {
-                const int el = i / PP, c = i - el * PP;
-                if (!(s_flag[el] & need)) continue;
-                const int slot = (which * be + el) * K + k;
-                const int ctr = s_ctr[slot];
-                const int r = ctr / W + c / P - half, q = ctr % W + c % P - half;
-                float v = -1.0f;
-                if (r >= 0 && r < H && q >= 0 && q < W) {
-                    const int cell = r * W + q;
-                    v = ((s_road[cell >> 5] >> (cell & 31)) & 1u) ? 0.0f : -1.0f;
-                    for (int u = 0; u < npatch; ++u)  // later patches override earlier ones
-                        if (s_pc[slot * npatch + u] == cell) v = s_pv[slot * npatch + u];
+            const int64_t off = ((int64_t)k * p.E + e0) * PP;  // this block's run of agent k
+            float *o = dst + off;
+            const int len = nenv * PP;
+            // 16-byte stores from the first aligned element of the run on
+            const int lead = (int)((4 - (off & 3)) & 3);
+            for (int i = tid; i < min(lead, len); i += PATCH_THREADS) {
+                const int el = i / PP;
+                if (s_flag[el] & need) o[i] = value(which, el, k, i - el * PP);
+            }
+            const int n4 = (len - lead) / 4;
+            float4 *o4 = reinterpret_cast<float4 *>(o + lead);
+            for (int j = tid; j < n4; j += PATCH_THREADS) {
+                const int i0 = lead + 4 * j;
+                const int ea = i0 / PP, eb = (i0 + 3) / PP;
+                const bool wa = (s_flag[ea] & need) != 0, wb = (s_flag[eb] & need) != 0;
+                if (!wa && !wb) continue;
+                float v[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const int i = i0 + t, el = i / PP;
+                    v[t] = value(which, el, k, i - el * PP);
                 }
-                o[i] = v;
+                if (wa && wb) {
+                    store_nt(o4 + j, make_float4(v[0], v[1], v[2], v[3]));
+                } else {  // a run boundary between a written and a skipped env
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        if (s_flag[(i0 + t) / PP] & need) o[i0 + t] = v[t];
+                }
+            }
+            for (int i = lead + 4 * n4 + tid; i < len; i += PATCH_THREADS) {
+                const int el = i / PP;
+                if (s_flag[el] & need) o[i] = value(which, el, k, i - el * PP);
             }
         }
     }
@@ -3245,8 +3289,7 @@ gw_status gw_obs_patch(void *handle, int32_t P, float *patch, float *final_patch
     hipStream_t s = static_cast<hipStream_t>(stream);
     GW_TRY(wait_fear(env, s));  // async FeAR: the descriptors are written by the world update (joined)
     gw::Params p = make_params(env);
-    const int be = std::max(1, std::min(gw::OBS_BE, 8192 / std::max(1, env->K * P * P)));
-    p.obs_be = be;
+    const int be = gw::PATCH_BE;
     const size_t lds = sizeof(uint32_t) * ((env->HW + 31) / 32 + be) +
                        sizeof(int) * 2 * be * env->K + (size_t)2 * 2 * be * env->K * (env->N + 1) * sizeof(uint32_t);
     const unsigned grid = (unsigned)((env->E + be - 1) / be);
