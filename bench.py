@@ -52,6 +52,11 @@ CONFIGS = {
                     workload="C5's rollout with egocentric 11x11 local observations (gw_obs_patch; not a "
                              "reference format, reported separately): no dense obs, the MADDPG MLP actors on "
                              "121 inputs (fused gw_patch_actor_act), patch replay ring, FeAR on"),
+    "c4patch": dict(scenario="grid64_n8", envs=65536, fear=False, fear_weight=-5.0, rollout=True, arch="cnn", patch=16,
+                    workload="BASELINE config 4's CNN head (configs/cnn.yaml: conv 32-64 k2 s2, 128-128, f32) on "
+                             "egocentric 16x16 local windows (gw_obs_patch; not a reference format, reported "
+                             "separately): 8-agent 64x64 grid, 65536 envs, no dense obs, the PyTorch CNN forward "
+                             "(hipBLASLt GEMMs) on the windows written into the patch replay ring"),
     "c4cnn": dict(scenario="grid64_n8", envs=65536, fear=False, fear_weight=-5.0, rollout=True, arch="cnn",
                   workload="BASELINE config 4 as a rollout: 8-agent 64x64 grid, 65536 envs, the configs/cnn.yaml "
                            "actor head (conv 32-64, k2 s2, 128-128, f32; fused gw_cnn_act from the obs "
@@ -291,7 +296,7 @@ def main():
         os.environ.setdefault("GW_OBS_CHUNKS", "2")
     if cfg.get("patch"):  # no dense obs: nothing to pipeline
         obs_mode = False
-    if cfg.get("arch") == "cnn" and not (args.cnn_torch or args.obs_lazy or args.sync_obs):
+    if cfg.get("arch") == "cnn" and not cfg.get("patch") and not (args.cnn_torch or args.obs_lazy or args.sync_obs):
         # the 2.1 GB writer starts right after the world update, as 4 launches so that the next
         # actor's kernels are dispatched between them (profiles/r2_cnn: 0.715 ms per step lazy in
         # one launch -> 0.636); read by gw_create
@@ -361,7 +366,12 @@ def main():
         # one set of actor weights for every rank: built from the same seed and broadcast from
         # rank 0 (MADDPG does it itself); every rank's sampling draws its own batches
         torch.cuda.manual_seed(1234 + rank)
-        if cfg.get("patch"):  # local observations: the MADDPG actors on the P x P windows (fused
+        if cfg.get("patch") and cfg.get("arch") == "cnn":  # the CNN head on the P x P windows (PyTorch)
+            from marlnav.actor import MultiAgentActors
+            learner = None
+            actors = MultiAgentActors(K, cfg["patch"], cfg["patch"], arch="cnn", device=env.device, seed=0)
+            broadcast_module(actors)
+        elif cfg.get("patch"):  # local observations: the MADDPG actors on the P x P windows (fused
             # gw_patch_actor_act from the obs descriptors; --patch-torch: the PyTorch forward, A/B)
             learner = MADDPG(K, cfg["patch"], cfg["patch"], device=env.device, seed=0, capturable=True)
             actors = learner.actors

@@ -1718,25 +1718,12 @@ __global__ void __launch_bounds__(128) step_v2(Params p) {
 constexpr int PATCH_THREADS = 256;
 constexpr int PATCH_BE = 32;  // envs per block: a block's windows of one agent are one contiguous run
 
-// Block = PATCH_BE envs.  Per (which, env, agent) the window's centre and its patched cells as
-// window positions (-1: outside the window) are staged in LDS; then each agent's contiguous run
-// of nenv * P * P floats is written as 16-byte stores where the run is 16-byte aligned (scalar
-// stores otherwise, and for the terminal windows of envs that did not end).
-__global__ void __launch_bounds__(PATCH_THREADS) patch_kernel(Params p, int P, float *__restrict__ patch,
-                                                              float *__restrict__ final_patch) {
-    extern __shared__ uint32_t plds[];
+// the per-(which, env, agent) window centres and patched cells of a patch block, in LDS
+__device__ void patch_stage(const Params &p, int P, uint32_t *s_road, uint32_t *s_flag, int *s_ctr, int *s_pw,
+                            float *s_pv, int64_t e0, int nenv) {
     const int tid = threadIdx.x;
-    const int W = p.W, H = p.H, N = p.N, K = p.K;
-    const int npatch = N + 1, nroad = (p.HW + 31) / 32;
-    uint32_t *s_road = plds;
-    uint32_t *s_flag = s_road + nroad;                                   // [PATCH_BE]
-    int *s_ctr = reinterpret_cast<int *>(s_flag + PATCH_BE);             // [2][PATCH_BE][K]: row << 16 | col
-    int *s_pw = s_ctr + 2 * PATCH_BE * K;                                // [2][PATCH_BE][K][npatch] window positions
-    float *s_pv = reinterpret_cast<float *>(s_pw + 2 * PATCH_BE * K * npatch);
-    const int64_t e0 = (int64_t)blockIdx.x * PATCH_BE;
-    if (e0 >= p.E) return;  // uniform per block
-    const int nenv = (int)min((int64_t)PATCH_BE, p.E - e0);
-    const int PP = P * P, half = P / 2;
+    const int W = p.W, N = p.N, K = p.K;
+    const int npatch = N + 1, nroad = (p.HW + 31) / 32, half = P / 2;
     for (int w = tid; w < nroad; w += PATCH_THREADS) s_road[w] = p.tb.roadbits[w];
     for (int u = tid; u < 2 * PATCH_BE * K; u += PATCH_THREADS) {  // one thread per (which, env, k)
         const int which = u / (PATCH_BE * K), el = (u / K) % PATCH_BE, k = u % K;
@@ -1770,62 +1757,117 @@ __global__ void __launch_bounds__(PATCH_THREADS) patch_kernel(Params p, int P, f
         }
         for (; np < npatch; ++np) s_pw[slot * npatch + np] = -1;
     }
+}
+
+// Block = PATCH_BE envs (P <= 16).  Per (which, env, agent) the window's centre and its patched
+// cells as window positions (-1: outside the window) are staged in LDS (patch_stage); then each
+// wave writes whole windows.
+__global__ void __launch_bounds__(PATCH_THREADS) patch_kernel(Params p, int P, float *__restrict__ patch,
+                                                              float *__restrict__ final_patch) {
+    extern __shared__ uint32_t plds[];
+    const int tid = threadIdx.x;
+    const int W = p.W, H = p.H, N = p.N, K = p.K;
+    const int npatch = N + 1, nroad = (p.HW + 31) / 32;
+    uint32_t *s_road = plds;
+    uint32_t *s_flag = s_road + nroad;                                   // [PATCH_BE]
+    int *s_ctr = reinterpret_cast<int *>(s_flag + PATCH_BE);             // [2][PATCH_BE][K]: row << 16 | col
+    int *s_pw = s_ctr + 2 * PATCH_BE * K;                                // [2][PATCH_BE][K][npatch] window positions
+    float *s_pv = reinterpret_cast<float *>(s_pw + 2 * PATCH_BE * K * npatch);
+    const int64_t e0 = (int64_t)blockIdx.x * PATCH_BE;
+    if (e0 >= p.E) return;  // uniform per block
+    const int nenv = (int)min((int64_t)PATCH_BE, p.E - e0);
+    const int PP = P * P, half = P / 2;
+    patch_stage(p, P, s_road, s_flag, s_ctr, s_pw, s_pv, e0, nenv);
     __syncthreads();
-    // value of window position c of (which, el, k): the map under it (-1 outside the grid), then
-    // the patched cells in order (a later one overrides an earlier one, as the obs writer does)
-    auto value = [&](int which, int el, int k, int c) -> float {
-        const int slot = (which * PATCH_BE + el) * K + k;
-        const int ctr = s_ctr[slot];
-        const int wr = c / P;
-        const int r = (ctr >> 16) + wr - half, q = (ctr & 0xFFFF) + (c - wr * P) - half;
-        float v = -1.0f;
-        if (r >= 0 && r < H && q >= 0 && q < W) {
-            const int cell = r * W + q;
-            v = ((s_road[cell >> 5] >> (cell & 31)) & 1u) ? 0.0f : -1.0f;
+    // One wave per window at a time: lane l owns window positions l, l + 64, ... (the same for
+    // every window, so their (row, col) are computed once); the map under each (-1 outside the
+    // grid), then the patched cells in order (a later one overrides an earlier one, as the obs
+    // writer does; their window positions are wave-uniform LDS reads).  Stores: consecutive
+    // lanes, consecutive floats.
+    constexpr int MAXPL = 4;                      // positions per lane: P * P <= 256 (P <= 16)
+    const int wave = tid >> 6, lane = tid & 63;
+    int pr[MAXPL], pcl[MAXPL];
+#pragma unroll
+    for (int t = 0; t < MAXPL; ++t) {
+        const int c = lane + 64 * t;
+        pr[t] = c / P - half;
+        pcl[t] = c - (c / P) * P - half;
+    }
+    const int npl = (PP + 63) / 64;
+    for (int which = 0; which < 2; ++which) {
+        float *dst = which == 0 ? patch : final_patch;
+        if (!dst) continue;
+        const uint32_t need = which == 0 ? D_WRITE : D_FINAL;
+        for (int wi = wave; wi < nenv * K; wi += PATCH_THREADS / 64) {
+            const int el = wi / K, k = wi - el * K;
+            if (!(s_flag[el] & need)) continue;   // wave-uniform
+            const int slot = (which * PATCH_BE + el) * K + k;
+            const int ctr = s_ctr[slot];
+            const int cr = ctr >> 16, cc = ctr & 0xFFFF;
+            float v[MAXPL];
+#pragma unroll
+            for (int t = 0; t < MAXPL; ++t) {
+                const int r = cr + pr[t], q = cc + pcl[t];
+                float m = -1.0f;
+                if (r >= 0 && r < H && q >= 0 && q < W) {
+                    const int cell = r * W + q;
+                    m = ((s_road[cell >> 5] >> (cell & 31)) & 1u) ? 0.0f : -1.0f;
+                }
+                v[t] = m;
+            }
+            for (int u = 0; u < npatch; ++u) {
+                const int pw = s_pw[slot * npatch + u];
+                const float pv = s_pv[slot * npatch + u];
+#pragma unroll
+                for (int t = 0; t < MAXPL; ++t)
+                    if (pw == lane + 64 * t) v[t] = pv;
+            }
+            float *o = dst + ((int64_t)k * p.E + e0 + el) * PP;
+#pragma unroll
+            for (int t = 0; t < MAXPL; ++t)
+                if (t < npl && lane + 64 * t < PP) __builtin_nontemporal_store(v[t], o + lane + 64 * t);
         }
-        const int *pwv = s_pw + slot * npatch;
-        for (int u = 0; u < npatch; ++u)
-            if (pwv[u] == c) v = s_pv[slot * npatch + u];
-        return v;
-    };
+    }
+}
+
+// P > 16: the general form, one thread per element
+__global__ void __launch_bounds__(PATCH_THREADS) patch_kernel_big(Params p, int P, float *__restrict__ patch,
+                                                                  float *__restrict__ final_patch) {
+    extern __shared__ uint32_t plds[];
+    const int tid = threadIdx.x;
+    const int W = p.W, H = p.H, N = p.N, K = p.K;
+    const int npatch = N + 1, nroad = (p.HW + 31) / 32;
+    uint32_t *s_road = plds;
+    uint32_t *s_flag = s_road + nroad;
+    int *s_ctr = reinterpret_cast<int *>(s_flag + PATCH_BE);
+    int *s_pw = s_ctr + 2 * PATCH_BE * K;
+    float *s_pv = reinterpret_cast<float *>(s_pw + 2 * PATCH_BE * K * npatch);
+    const int64_t e0 = (int64_t)blockIdx.x * PATCH_BE;
+    if (e0 >= p.E) return;
+    const int nenv = (int)min((int64_t)PATCH_BE, p.E - e0);
+    const int PP = P * P, half = P / 2;
+    patch_stage(p, P, s_road, s_flag, s_ctr, s_pw, s_pv, e0, nenv);
+    __syncthreads();
     for (int which = 0; which < 2; ++which) {
         float *dst = which == 0 ? patch : final_patch;
         if (!dst) continue;
         const uint32_t need = which == 0 ? D_WRITE : D_FINAL;
         for (int k = 0; k < K; ++k) {
-            const int64_t off = ((int64_t)k * p.E + e0) * PP;  // this block's run of agent k
-            float *o = dst + off;
-            const int len = nenv * PP;
-            // 16-byte stores from the first aligned element of the run on
-            const int lead = (int)((4 - (off & 3)) & 3);
-            for (int i = tid; i < min(lead, len); i += PATCH_THREADS) {
-                const int el = i / PP;
-                if (s_flag[el] & need) o[i] = value(which, el, k, i - el * PP);
-            }
-            const int n4 = (len - lead) / 4;
-            float4 *o4 = reinterpret_cast<float4 *>(o + lead);
-            for (int j = tid; j < n4; j += PATCH_THREADS) {
-                const int i0 = lead + 4 * j;
-                const int ea = i0 / PP, eb = (i0 + 3) / PP;
-                const bool wa = (s_flag[ea] & need) != 0, wb = (s_flag[eb] & need) != 0;
-                if (!wa && !wb) continue;
-                float v[4];
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const int i = i0 + t, el = i / PP;
-                    v[t] = value(which, el, k, i - el * PP);
+            float *o = dst + ((int64_t)k * p.E + e0) * PP;
+            for (int i = tid; i < nenv * PP; i += PATCH_THREADS) {
+                const int el = i / PP, c = i - el * PP;
+                if (!(s_flag[el] & need)) continue;
+                const int slot = (which * PATCH_BE + el) * K + k;
+                const int ctr = s_ctr[slot];
+                const int r = (ctr >> 16) + c / P - half, q = (ctr & 0xFFFF) + c % P - half;
+                float v = -1.0f;
+                if (r >= 0 && r < H && q >= 0 && q < W) {
+                    const int cell = r * W + q;
+                    v = ((s_road[cell >> 5] >> (cell & 31)) & 1u) ? 0.0f : -1.0f;
                 }
-                if (wa && wb) {
-                    store_nt(o4 + j, make_float4(v[0], v[1], v[2], v[3]));
-                } else {  // a run boundary between a written and a skipped env
-#pragma unroll
-                    for (int t = 0; t < 4; ++t)
-                        if (s_flag[(i0 + t) / PP] & need) o[i0 + t] = v[t];
-                }
-            }
-            for (int i = lead + 4 * n4 + tid; i < len; i += PATCH_THREADS) {
-                const int el = i / PP;
-                if (s_flag[el] & need) o[i] = value(which, el, k, i - el * PP);
+                for (int u = 0; u < npatch; ++u)
+                    if (s_pw[slot * npatch + u] == c) v = s_pv[slot * npatch + u];
+                o[i] = v;
             }
         }
     }
@@ -3293,7 +3335,11 @@ gw_status gw_obs_patch(void *handle, int32_t P, float *patch, float *final_patch
     const size_t lds = sizeof(uint32_t) * ((env->HW + 31) / 32 + be) +
                        sizeof(int) * 2 * be * env->K + (size_t)2 * 2 * be * env->K * (env->N + 1) * sizeof(uint32_t);
     const unsigned grid = (unsigned)((env->E + be - 1) / be);
-    hipLaunchKernelGGL(gw::patch_kernel, dim3(grid), dim3(gw::PATCH_THREADS), lds, s, p, (int)P, patch, final_patch);
+    if (P <= 16)
+        hipLaunchKernelGGL(gw::patch_kernel, dim3(grid), dim3(gw::PATCH_THREADS), lds, s, p, (int)P, patch, final_patch);
+    else
+        hipLaunchKernelGGL(gw::patch_kernel_big, dim3(grid), dim3(gw::PATCH_THREADS), lds, s, p, (int)P, patch,
+                           final_patch);
     HIP_TRY(hipGetLastError());
     return GW_OK;
 }

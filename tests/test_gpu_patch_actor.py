@@ -103,3 +103,27 @@ def test_fused_patch_rollout_matches_torch_rollout_without_noise():
         torch.testing.assert_close(ros[0].replay.probs, ros[1].replay.probs, rtol=0, atol=2e-5)
     for e in envs:
         e.close()
+
+
+def test_cnn_head_on_windows_matches_conv2d_at_65536_envs():
+    """The configs/cnn.yaml head on 16 x 16 windows (bench.py --config c4patch: the PyTorch forward
+    as per-patch GEMMs, CNNActor._forward_patch_gemm) == nn.Conv2d -> flatten -> MLP on the same
+    windows, fp32, 65,536 envs of the 64 x 64 / N = 8 grid.  Tolerance 1e-4 relative + 1e-4
+    absolute on the logits (GEMM vs convolution summation order)."""
+    sc = S.builtin("grid64_n8")
+    P = 16
+    env = VecGridEnv(sc, num_envs=65536, fear=False, seed=12, max_steps=30, obs=False)
+    actors = MultiAgentActors(sc.K, P, P, "cnn", device="cuda", seed=4)
+    env.reset()
+    for _ in range(5):
+        env.step()
+    win = env.obs_patch(P)                                   # [K, E, P, P]
+    with torch.no_grad():
+        for k in range(sc.K):
+            m = actors.nets[k]
+            assert m.patchify
+            x = win[k].unsqueeze(1)
+            got = m(x)
+            ref = m.mlp(m.conv(x).flatten(1))
+            torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-4)
+    env.close()
