@@ -1782,8 +1782,10 @@ __global__ void __launch_bounds__(PATCH_THREADS) patch_kernel(Params p, int P, f
     // One wave per window at a time: lane l owns window positions l, l + 64, ... (the same for
     // every window, so their (row, col) are computed once); the map under each (-1 outside the
     // grid), then the patched cells in order (a later one overrides an earlier one, as the obs
-    // writer does; their window positions are wave-uniform LDS reads).  Stores: consecutive
-    // lanes, consecutive floats.
+    // writer does; their window positions are wave-uniform LDS reads).  The step's windows are
+    // assembled in LDS and leave as aligned 16-byte stores along each agent's contiguous run
+    // (whole cache lines: a window is not a multiple of a line, and partial-line writes from
+    // different waves cost HBM read-modify-writes); terminal windows (few envs) go out directly.
     constexpr int MAXPL = 4;                      // positions per lane: P * P <= 256 (P <= 16)
     const int wave = tid >> 6, lane = tid & 63;
     int pr[MAXPL], pcl[MAXPL];
@@ -1794,6 +1796,7 @@ __global__ void __launch_bounds__(PATCH_THREADS) patch_kernel(Params p, int P, f
         pcl[t] = c - (c / P) * P - half;
     }
     const int npl = (PP + 63) / 64;
+    float *s_out = s_pv + 2 * PATCH_BE * K * npatch;  // [K][nenv * PP]
     for (int which = 0; which < 2; ++which) {
         float *dst = which == 0 ? patch : final_patch;
         if (!dst) continue;
@@ -1822,10 +1825,42 @@ __global__ void __launch_bounds__(PATCH_THREADS) patch_kernel(Params p, int P, f
                 for (int t = 0; t < MAXPL; ++t)
                     if (pw == lane + 64 * t) v[t] = pv;
             }
-            float *o = dst + ((int64_t)k * p.E + e0 + el) * PP;
+            if (which == 0) {
+                float *o = s_out + (size_t)k * nenv * PP + el * PP;
 #pragma unroll
-            for (int t = 0; t < MAXPL; ++t)
-                if (t < npl && lane + 64 * t < PP) __builtin_nontemporal_store(v[t], o + lane + 64 * t);
+                for (int t = 0; t < MAXPL; ++t)
+                    if (t < npl && lane + 64 * t < PP) o[lane + 64 * t] = v[t];
+            } else {
+                float *o = dst + ((int64_t)k * p.E + e0 + el) * PP;
+#pragma unroll
+                for (int t = 0; t < MAXPL; ++t)
+                    if (t < npl && lane + 64 * t < PP) o[lane + 64 * t] = v[t];
+            }
+        }
+        if (which == 0) {
+            __syncthreads();
+            const int len = nenv * PP;
+            for (int k = 0; k < K; ++k) {
+                const int64_t off = ((int64_t)k * p.E + e0) * PP;
+                float *o = dst + off;
+                const float *so = s_out + (size_t)k * len;
+                const int lead = (int)((4 - (off & 3)) & 3);
+                bool all = true;  // every env of the block writes (the usual case): one aligned run
+                for (int el = 0; el < nenv; ++el) all = all && (s_flag[el] & D_WRITE);
+                if (!all) {
+                    for (int i = tid; i < len; i += PATCH_THREADS)
+                        if (s_flag[i / PP] & D_WRITE) o[i] = so[i];
+                    continue;
+                }
+                for (int i = tid; i < min(lead, len); i += PATCH_THREADS) o[i] = so[i];
+                const int n4 = (len - lead) / 4;
+                float4 *o4 = reinterpret_cast<float4 *>(o + lead);
+                for (int j = tid; j < n4; j += PATCH_THREADS) {
+                    const int i = lead + 4 * j;
+                    o4[j] = make_float4(so[i], so[i + 1], so[i + 2], so[i + 3]);
+                }
+                for (int i = lead + 4 * n4 + tid; i < len; i += PATCH_THREADS) o[i] = so[i];
+            }
         }
     }
 }
@@ -3333,7 +3368,8 @@ gw_status gw_obs_patch(void *handle, int32_t P, float *patch, float *final_patch
     gw::Params p = make_params(env);
     const int be = gw::PATCH_BE;
     const size_t lds = sizeof(uint32_t) * ((env->HW + 31) / 32 + be) +
-                       sizeof(int) * 2 * be * env->K + (size_t)2 * 2 * be * env->K * (env->N + 1) * sizeof(uint32_t);
+                       sizeof(int) * 2 * be * env->K + (size_t)2 * 2 * be * env->K * (env->N + 1) * sizeof(uint32_t) +
+                       (P <= 16 ? sizeof(float) * (size_t)env->K * be * P * P : 0);  // the assembled windows
     const unsigned grid = (unsigned)((env->E + be - 1) / be);
     if (P <= 16)
         hipLaunchKernelGGL(gw::patch_kernel, dim3(grid), dim3(gw::PATCH_THREADS), lds, s, p, (int)P, patch, final_patch);
