@@ -6,6 +6,7 @@
 
 #include <stdint.h>
 
+#include "actor_ops.h"
 #include "gridenv.h"
 
 #ifdef __cplusplus
@@ -75,6 +76,42 @@ gw_status gw_affine_relu_bwd(const float *dy, const float *xhat, const float *y,
  * out + b * out_ld + k * n (straight into the action slots of the critic's input rows). */
 gw_status gw_gumbel_softmax(const float *logits, const float *u, float *out, int64_t rows, int32_t n, float tau,
                             float eps, int64_t out_b, int64_t out_ld, void *stream);
+
+/* ---- the fused MADDPG update (csrc/maddpg_ops.hip) ------------------------------------------
+ * agilerl 1.0.15 MADDPG.learn (maddpg/agent.py:199-224; restated in marlnav/maddpg.py) on a
+ * sampled batch for K stacked agents, networks in StackedMLPActors' layout (gw_mlp_actors: in ->
+ * 128 -> LayerNorm -> ReLU -> 128 -> LayerNorm -> ReLU -> out; actors out = 9 over D = H*W obs
+ * floats, critics out = 1 over the critic rows [s_1 .. s_K, a_1 .. a_K]).  Two calls carry the
+ * update's two backward passes; between them the caller runs the critic's Adam step
+ * (gw_adam_step), and after the second the actor's Adam step and the soft update
+ * (gw_soft_update2); with several ranks each call's gradients are all-reduced before its Adam
+ * step.  Gradients are WRITTEN (not accumulated) through the *_grad views, losses [K] f32. */
+typedef struct gw_maddpg_batch {
+    int32_t K, B, D;       /* agents, rows (a positive multiple of 16), obs floats per agent       */
+    const float *x;        /* [B][K*D + 9K] critic input rows: states, stored action probabilities */
+    float *x_next;         /* [B][K*D + 9K] next states; the target actions are written into its
+                            * action slots by gw_maddpg_critic_grads                              */
+    const double *reward;  /* [B][K] shaped rewards                                                */
+    const uint8_t *done;   /* [B][K] terminations                                                  */
+    const float *u;        /* [K][B][9] the call's Gumbel uniforms (u_next, then u_cur)            */
+} gw_maddpg_batch;
+
+/* Workspace (floats) both calls share: layer-1 partial sums and the rows' saved activations. */
+int64_t gw_maddpg_workspace_floats(int32_t K, int32_t B, int32_t D);
+
+/* a'_k = GumbelSoftmax(actor_target_k(s'_k)) into x_next's slots; y = r + (1 - d) gamma
+ * critic_target_k(x_next); critic_grad = d/dtheta of mean_b (critic_k(x) - y)^2 per agent;
+ * loss [K] the MSE values. */
+gw_status gw_maddpg_critic_grads(const gw_mlp_actors *actor_target, const gw_mlp_actors *critic_target,
+                                 const gw_mlp_actors *critic, const gw_mlp_actors *critic_grad,
+                                 const gw_maddpg_batch *batch, float gamma, float *ws, float *loss, void *stream);
+
+/* probs_k = GumbelSoftmax(actor_k(s_k)) (probs [K][B][9], may be NULL); actor_grad = d/dtheta of
+ * -mean_b critic_k(s, a with a_k := probs_k) per agent (the critic as given, i.e. after its Adam
+ * step; no critic gradients); loss [K]. */
+gw_status gw_maddpg_actor_grads(const gw_mlp_actors *actor, const gw_mlp_actors *critic,
+                                const gw_mlp_actors *actor_grad, const gw_maddpg_batch *batch, float *ws, float *loss,
+                                float *probs, void *stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,828 @@
+// maddpg_ops.hip — one MADDPG update (agilerl 1.0.15 MADDPG.learn as called by
+// maddpg/agent.py:199-224, restated in marlnav/maddpg.py) in a handful of MI355X launches
+// (include/learner_ops.h: gw_maddpg_critic_grads, gw_maddpg_actor_grads; the Adam steps and the
+// soft update are gw_adam_step / gw_soft_update2).
+//
+// The networks are K stacked MLPs in marlnav/actor.py's StackedMLPActors layout: in -> 128 ->
+// LayerNorm -> ReLU -> 128 -> LayerNorm -> ReLU -> out (9 actor logits, 1 critic value).  A batch
+// of B rows (B a multiple of 16) is processed as:
+//   l1_kernel       layer 1 (the only wide GEMM: in = K*D + 9K for a critic) split over
+//                   64-input chunks: one workgroup per (job, agent, chunk, 128-row tile) writes
+//                   the chunk's partial [rows][128]; the consumer adds the chunks in order.
+//   *_tail kernels  everything per row: the chunk sum, LayerNorms, ReLUs, layers 2-3 (W2 and
+//                   W2^T staged in LDS), Gumbel softmax, TD target, the loss gradient and the
+//                   backward through layers 3, 2 and the LayerNorms.  One workgroup per (agent,
+//                   16 rows); a row's 128 features live on 16 lanes (8 each), LayerNorm sums
+//                   are 16-lane butterflies.
+//   grads_kernel    the parameter gradients, reductions over the rows in row order: W1 = X^T dz1,
+//                   W2 = h1^T dz2, W3 = h2^T g3, biases, LayerNorm affines, the loss value; written
+//                   (not accumulated) into the flat gradient buffer's per-layer views.
+// Everything is f32 with fixed summation orders (deterministic).  It differs from the torch
+// composition (tests/test_maddpg_fused.py) by f32 summation order, including inside LayerNorm's
+// row statistics, so a ReLU whose input sits at the rounding edge can take the other side; the
+// tests state the flip-tolerant bound.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <string>
+
+#include "learner_ops.h"
+
+namespace {
+
+constexpr int HID = 128, NA = 9, RB = 16, TILE_R = 128, DC = 64, MAXK = GW_MAX_AGENTS, MAXJOB = 4;
+constexpr float LN_EPS = 1e-5f, G_EPS = 1e-20f;
+
+gw_status fail(gw_status s, const std::string &msg) {
+    gw_set_last_error(msg.c_str());
+    return s;
+}
+
+// ---- layer 1, split over input chunks ---------------------------------------------------------
+// job: rows r of agent k read x[r * ldx + k * xk + col0 + d], weights w[k * wk + (wrow0 + d) * 128 + j]
+// for d < D; part[((chunk * K + k) * B + r) * 128 + j] = sum over the chunk's inputs in order.
+struct L1Job {
+    const float *x;
+    const float *w;
+    float *part;
+    int64_t ldx, xk, wk;
+    int col0, wrow0, D, nchunk;
+};
+struct L1Params {
+    L1Job job[MAXJOB];
+    int njob, K, B, ntile;
+    int start[MAXJOB + 1];  // first block of each job (blocks: job, k, chunk, row tile)
+};
+
+__global__ void __launch_bounds__(256) l1_kernel(L1Params p) {
+    __shared__ __attribute__((aligned(16))) float s_x[DC][TILE_R + 4];  // [input][row]
+    __shared__ __attribute__((aligned(16))) float s_w[DC][HID];         // [input][feature]
+    int b = blockIdx.x, j = 0;
+    while (j + 1 < p.njob && b >= p.start[j + 1]) ++j;
+    const L1Job &jb = p.job[j];
+    b -= p.start[j];
+    const int tile = b % p.ntile;
+    b /= p.ntile;
+    const int chunk = b % jb.nchunk, k = b / jb.nchunk;
+    const int tid = threadIdx.x;
+    const int d0 = chunk * DC, r0 = tile * TILE_R;
+    const int nd = min(DC, jb.D - d0);
+    // stage x^T (rows of this tile, inputs of this chunk) and the chunk's weight rows
+    const float *xb = jb.x + (int64_t)k * jb.xk + jb.col0 + d0;
+    for (int i = tid; i < DC * TILE_R; i += 256) {
+        const int r = i / DC, d = i % DC;  // consecutive threads: consecutive inputs of a row
+        s_x[d][r] = (d < nd && r0 + r < p.B) ? xb[(int64_t)(r0 + r) * jb.ldx + d] : 0.0f;
+    }
+    const float *wb = jb.w + (int64_t)k * jb.wk + (int64_t)(jb.wrow0 + d0) * HID;
+    for (int i = tid; i < DC * HID / 4; i += 256) {
+        const int d = i / (HID / 4), c = i % (HID / 4);
+        const float4 v = d < nd ? reinterpret_cast<const float4 *>(wb + (int64_t)d * HID)[c] : make_float4(0, 0, 0, 0);
+        *reinterpret_cast<float4 *>(&s_w[d][4 * c]) = v;
+    }
+    __syncthreads();
+    const int rg = tid >> 4, jg = tid & 15;  // rows 8 rg .. + 8, features 8 jg .. + 8
+    float acc[8][8];
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int c = 0; c < 8; ++c) acc[a][c] = 0.0f;
+    for (int d = 0; d < nd; ++d) {
+        const float4 xa = *reinterpret_cast<const float4 *>(&s_x[d][8 * rg]);
+        const float4 xb4 = *reinterpret_cast<const float4 *>(&s_x[d][8 * rg + 4]);
+        const float4 wa = *reinterpret_cast<const float4 *>(&s_w[d][8 * jg]);
+        const float4 wb4 = *reinterpret_cast<const float4 *>(&s_w[d][8 * jg + 4]);
+        const float xv[8] = {xa.x, xa.y, xa.z, xa.w, xb4.x, xb4.y, xb4.z, xb4.w};
+        const float wv[8] = {wa.x, wa.y, wa.z, wa.w, wb4.x, wb4.y, wb4.z, wb4.w};
+#pragma unroll
+        for (int a = 0; a < 8; ++a)
+#pragma unroll
+            for (int c = 0; c < 8; ++c) acc[a][c] = fmaf(xv[a], wv[c], acc[a][c]);
+    }
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+        const int r = r0 + 8 * rg + a;
+        if (r >= p.B) break;
+        float *o = jb.part + (((int64_t)chunk * p.K + k) * p.B + r) * HID + 8 * jg;
+        *reinterpret_cast<float4 *>(o) = make_float4(acc[a][0], acc[a][1], acc[a][2], acc[a][3]);
+        *reinterpret_cast<float4 *>(o + 4) = make_float4(acc[a][4], acc[a][5], acc[a][6], acc[a][7]);
+    }
+}
+
+// ---- per-row helpers (a row = 16 lanes, lane g holds features 8 g .. 8 g + 7) ---------------------
+__device__ __forceinline__ float row_sum(float v) {  // over the row's 16 lanes
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    v += __shfl_xor(v, 4, 64);
+    v += __shfl_xor(v, 8, 64);
+    return v;
+}
+
+struct Mlp {  // one agent's parameters (pointers already offset to agent k)
+    const float *w1, *b1, *lw1, *lb1, *w2, *b2, *lw2, *lb2, *w3, *b3;
+};
+__device__ __forceinline__ Mlp mlp_k(const gw_mlp_actors &n, int k, int in_dim, int out) {
+    Mlp m;
+    m.w1 = n.w1 + (int64_t)k * in_dim * HID;
+    m.b1 = n.b1 + k * HID;
+    m.lw1 = n.ln1_w + k * HID;
+    m.lb1 = n.ln1_b + k * HID;
+    m.w2 = n.w2 + (int64_t)k * HID * HID;
+    m.b2 = n.b2 + k * HID;
+    m.lw2 = n.ln2_w + k * HID;
+    m.lb2 = n.ln2_b + k * HID;
+    m.w3 = n.w3 + (int64_t)k * HID * out;
+    m.b3 = n.b3 + k * out;
+    return m;
+}
+
+// LayerNorm (biased variance, eps 1e-5) + affine + ReLU of the 8 features z; xhat / relu output
+__device__ __forceinline__ void ln_relu(const float z[8], const float *lw, const float *lb, int g, float xh[8],
+                                        float y[8], float &rstd_out) {
+    float s = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += z[i];
+    const float mean = row_sum(s) * (1.0f / HID);
+    float v = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v = fmaf(z[i] - mean, z[i] - mean, v);
+    const float rstd = rsqrtf(row_sum(v) * (1.0f / HID) + LN_EPS);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        xh[i] = (z[i] - mean) * rstd;
+        const float o = xh[i] * lw[8 * g + i] + lb[8 * g + i];
+        y[i] = o > 0.0f ? o : 0.0f;
+    }
+    rstd_out = rstd;
+}
+
+// backward of ln_relu: gy = grad at the ReLU output; gv = gy * (y > 0) (the affine output's
+// gradient, kept for the LayerNorm parameter gradients); dz = rstd (dxh - mean(dxh) - xh mean(dxh xh))
+__device__ __forceinline__ void ln_relu_bwd(const float gy[8], const float y[8], const float xh[8], float rstd,
+                                            const float *lw, int g, float gv[8], float dz[8]) {
+    float dx[8], s1 = 0.0f, s2 = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        gv[i] = y[i] > 0.0f ? gy[i] : 0.0f;
+        dx[i] = gv[i] * lw[8 * g + i];
+        s1 += dx[i];
+        s2 = fmaf(dx[i], xh[i], s2);
+    }
+    const float m1 = row_sum(s1) * (1.0f / HID), m2 = row_sum(s2) * (1.0f / HID);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dz[i] = rstd * (dx[i] - m1 - xh[i] * m2);
+}
+
+// out[8] = sum_c h[c] W[c][8 g + i]  (W [128][128] in LDS, h the row's 128 values in LDS)
+__device__ __forceinline__ void row_gemv(const float *h, const float (*w)[HID + 4], int g, float out[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) out[i] = 0.0f;
+    for (int c = 0; c < HID; ++c) {
+        const float hv = h[c];
+        const float4 a = *reinterpret_cast<const float4 *>(&w[c][8 * g]);
+        const float4 b = *reinterpret_cast<const float4 *>(&w[c][8 * g + 4]);
+        out[0] = fmaf(hv, a.x, out[0]);
+        out[1] = fmaf(hv, a.y, out[1]);
+        out[2] = fmaf(hv, a.z, out[2]);
+        out[3] = fmaf(hv, a.w, out[3]);
+        out[4] = fmaf(hv, b.x, out[4]);
+        out[5] = fmaf(hv, b.y, out[5]);
+        out[6] = fmaf(hv, b.z, out[6]);
+        out[7] = fmaf(hv, b.w, out[7]);
+    }
+}
+
+// s_w = W [128][128] and s_wt = W^T from global (block-wide; caller syncs)
+__device__ __forceinline__ void stage_w2(const float *w, float (*s_w)[HID + 4], float (*s_wt)[HID + 4]) {
+    for (int i = threadIdx.x; i < HID * HID; i += 256) {
+        const int r = i / HID, c = i % HID;
+        const float v = w[i];
+        s_w[r][c] = v;
+        s_wt[c][r] = v;
+    }
+}
+
+// the layer-1 pre-activation of (k, row): the chunk partials in order + bias (+ extra: the
+// action-column terms a caller adds)
+__device__ __forceinline__ void l1_sum(const float *part, int nchunk, int K, int B, int k, int r, int g,
+                                       const float *b1, float z[8]) {
+    float acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = 0.0f;
+    for (int c = 0; c < nchunk; ++c) {
+        const float *pp = part + (((int64_t)c * K + k) * B + r) * HID + 8 * g;
+        const float4 a = *reinterpret_cast<const float4 *>(pp);
+        const float4 b = *reinterpret_cast<const float4 *>(pp + 4);
+        acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+        acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) z[i] = acc[i] + b1[8 * g + i];
+}
+
+// save 8 features of row r to buf [K][B][128]
+__device__ __forceinline__ void put8(float *buf, int K, int B, int k, int r, int g, const float v[8]) {
+    (void)K;
+    float *o = buf + ((int64_t)k * B + r) * HID + 8 * g;
+    *reinterpret_cast<float4 *>(o) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4 *>(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+
+// saved per-row quantities of one network's forward + backward (for grads_kernel)
+struct Saved {
+    float *h1, *h2, *xh1, *xh2, *gv1, *gv2, *dz1, *dz2;  // [K][B][128]
+    float *g3;                                           // [K][B][out] gradient at layer 3's output
+    float *aux;                                          // [K][B]: the loss terms
+};
+
+struct TailParams {
+    gw_mlp_actors actor_t, critic_t, critic, actor;  // parameter sets
+    const float *x;        // [B][ldx] critic input rows (states, stored actions)
+    float *x_next;         // [B][ldx] next states; target actions written into the action slots
+    const double *reward;  // [B][K]
+    const uint8_t *done;   // [B][K]
+    const float *u;        // [K][B][9] Gumbel uniforms of this phase's sample
+    const float *part_a, *part_ct, *part_c;  // layer-1 partials (actor-like, critic target, critic)
+    Saved sv;
+    float gamma;
+    int64_t ldx;
+    int K, B, D, nch_a, nch_c, nch_cs;  // chunks: actor (D inputs), critic full (ldx), critic state part (K D)
+    float *probs_out;      // actor phase: [K][B][9] the fresh action probabilities (tests), may be null
+};
+
+// ---- phase 1a: target actions a'_k = GumbelSoftmax(actor_target_k(s'_k)) into x_next's slots ----
+__global__ void __launch_bounds__(256) target_actor_tail(TailParams p) {
+    __shared__ __attribute__((aligned(16))) float s_w[HID][HID + 4];
+    __shared__ float s_h[RB][HID];
+    const int k = blockIdx.y, tid = threadIdx.x, rl = tid >> 4, g = tid & 15;
+    const int r = blockIdx.x * RB + rl;
+    const Mlp m = mlp_k(p.actor_t, k, p.D, NA);
+    for (int i = tid; i < HID * HID; i += 256) s_w[i / HID][i % HID] = m.w2[i];
+    float z[8], xh[8], y[8], rs;
+    l1_sum(p.part_a, p.nch_a, p.K, p.B, k, r, g, m.b1, z);
+    ln_relu(z, m.lw1, m.lb1, g, xh, y, rs);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s_h[rl][8 * g + i] = y[i];
+    __syncthreads();
+    row_gemv(s_h[rl], s_w, g, z);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) z[i] += m.b2[8 * g + i];
+    ln_relu(z, m.lw2, m.lb2, g, xh, y, rs);
+    float lg[NA];
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        float s = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s = fmaf(y[i], m.w3[(8 * g + i) * NA + a], s);
+        lg[a] = row_sum(s) + m.b3[a];
+    }
+    // GumbelSoftmax (tau 1): softmax(logits - log(-log(u + eps) + eps)), gw_gumbel_softmax's op order
+    const float *ur = p.u + ((int64_t)k * p.B + r) * NA;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        lg[a] = (lg[a] - logf(-logf(ur[a] + G_EPS) + G_EPS)) / 1.0f;
+        mx = fmaxf(mx, lg[a]);
+    }
+    float sum = 0.0f;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        lg[a] = expf(lg[a] - mx);
+        sum += lg[a];
+    }
+    if (g == 0) {
+        float *o = p.x_next + (int64_t)r * p.ldx + (int64_t)p.K * p.D + NA * k;
+#pragma unroll
+        for (int a = 0; a < NA; ++a) o[a] = lg[a] / sum;
+    }
+}
+
+// forward of critic (m) on row r: z1 = partial sum + b1 + the action columns of `act` (9K values
+// of this row, from LDS); saves into the given arrays; returns q
+struct RowFwd {
+    float xh1[8], y1[8], rs1, xh2[8], y2[8], rs2;
+};
+__device__ __forceinline__ float critic_fwd(const Mlp &m, const float *part, int nch, const TailParams &p, int k,
+                                            int r, int g, const float *act, float (*s_w)[HID + 4], float *s_hrow,
+                                            RowFwd &f) {
+    float z[8];
+    l1_sum(part, nch, p.K, p.B, k, r, g, m.b1, z);
+    const int Ds = p.K * p.D;
+    for (int a = 0; a < NA * p.K; ++a) {
+        const float av = act[a];
+        const float *wr = m.w1 + (int64_t)(Ds + a) * HID + 8 * g;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) z[i] = fmaf(av, wr[i], z[i]);
+    }
+    ln_relu(z, m.lw1, m.lb1, g, f.xh1, f.y1, f.rs1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s_hrow[8 * g + i] = f.y1[i];
+    __syncthreads();
+    row_gemv(s_hrow, s_w, g, z);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) z[i] += m.b2[8 * g + i];
+    ln_relu(z, m.lw2, m.lb2, g, f.xh2, f.y2, f.rs2);
+    float s = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s = fmaf(f.y2[i], m.w3[8 * g + i], s);
+    return row_sum(s) + m.b3[0];
+}
+
+// backward through the critic from dq to dz1 (and the per-row saves when sv != null)
+__device__ __forceinline__ void critic_bwd(const Mlp &m, float dq, int g, const RowFwd &f, float (*s_wt)[HID + 4],
+                                           float *s_grow, float gv1[8], float dz1[8], float gv2[8], float dz2[8]) {
+    float gy[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) gy[i] = dq * m.w3[8 * g + i];
+    ln_relu_bwd(gy, f.y2, f.xh2, f.rs2, m.lw2, g, gv2, dz2);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s_grow[8 * g + i] = dz2[i];
+    __syncthreads();
+    row_gemv(s_grow, s_wt, g, gy);  // dh1 = dz2 W2^T
+    ln_relu_bwd(gy, f.y1, f.xh1, f.rs1, m.lw1, g, gv1, dz1);
+}
+
+// ---- phase 1b: TD target from the critic target, the critic's forward, MSE gradient, backward ----
+__global__ void __launch_bounds__(256) critic_tail(TailParams p) {
+    __shared__ __attribute__((aligned(16))) float s_w[HID][HID + 4];
+    __shared__ __attribute__((aligned(16))) float s_wt[HID][HID + 4];
+    __shared__ float s_h[RB][HID];
+    __shared__ float s_act[RB][NA * MAXK];
+    const int k = blockIdx.y, tid = threadIdx.x, rl = tid >> 4, g = tid & 15;
+    const int r = blockIdx.x * RB + rl;
+    const int na = NA * p.K;
+    const int64_t Ds = (int64_t)p.K * p.D;
+    // target critic on (s', a'): the action slots written by target_actor_tail
+    const Mlp mt = mlp_k(p.critic_t, k, p.K * p.D + na, 1);
+    for (int i = tid; i < RB * na; i += 256) s_act[i / na][i % na] = p.x_next[(int64_t)(blockIdx.x * RB + i / na) * p.ldx + Ds + i % na];
+    for (int i = tid; i < HID * HID; i += 256) s_w[i / HID][i % HID] = mt.w2[i];
+    __syncthreads();
+    RowFwd f;
+    const float q_next = critic_fwd(mt, p.part_ct, p.nch_cs, p, k, r, g, s_act[rl], s_w, s_h[rl], f);
+    // y = f32(r) + ((1 - d) * gamma) * q_next, gw_td_target's op order
+    const float t1 = 1.0f - (float)p.done[(int64_t)r * p.K + k];
+    const float y = (float)p.reward[(int64_t)r * p.K + k] + (t1 * p.gamma) * q_next;
+    __syncthreads();
+    // online critic on (s, a): the stored actions are the x rows' action slots (in the partials)
+    const Mlp m = mlp_k(p.critic, k, p.K * p.D + na, 1);
+    stage_w2(m.w2, s_w, s_wt);
+    __syncthreads();
+    float z[8];
+    l1_sum(p.part_c, p.nch_c, p.K, p.B, k, r, g, m.b1, z);
+    RowFwd o;
+    ln_relu(z, m.lw1, m.lb1, g, o.xh1, o.y1, o.rs1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s_h[rl][8 * g + i] = o.y1[i];
+    __syncthreads();
+    row_gemv(s_h[rl], s_w, g, z);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) z[i] += m.b2[8 * g + i];
+    ln_relu(z, m.lw2, m.lb2, g, o.xh2, o.y2, o.rs2);
+    float s = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s = fmaf(o.y2[i], m.w3[8 * g + i], s);
+    const float q = row_sum(s) + m.b3[0];
+    const float diff = q - y;
+    const float dq = (1.0f / (float)p.B) * (2.0f * diff);  // MSELoss backward (gw_mean_loss_bwd's order)
+    float gv1[8], dz1[8], gv2[8], dz2[8];
+    __syncthreads();
+    critic_bwd(m, dq, g, o, s_wt, s_h[rl], gv1, dz1, gv2, dz2);
+    const Saved &sv = p.sv;
+    put8(sv.h1, p.K, p.B, k, r, g, o.y1);
+    put8(sv.h2, p.K, p.B, k, r, g, o.y2);
+    put8(sv.xh1, p.K, p.B, k, r, g, o.xh1);
+    put8(sv.xh2, p.K, p.B, k, r, g, o.xh2);
+    put8(sv.gv1, p.K, p.B, k, r, g, gv1);
+    put8(sv.gv2, p.K, p.B, k, r, g, gv2);
+    put8(sv.dz1, p.K, p.B, k, r, g, dz1);
+    put8(sv.dz2, p.K, p.B, k, r, g, dz2);
+    if (g == 0) {
+        sv.g3[(int64_t)k * p.B + r] = dq;
+        sv.aux[(int64_t)k * p.B + r] = diff * diff;
+    }
+}
+
+// ---- phase 2: the actor's forward, GumbelSoftmax, the (updated) critic on the mixed actions,
+//      -mean Q gradient, backward through the critic (no parameter gradients) and the actor ----
+__global__ void __launch_bounds__(256) actor_tail(TailParams p) {
+    __shared__ __attribute__((aligned(16))) float s_w[HID][HID + 4];
+    __shared__ __attribute__((aligned(16))) float s_wt[HID][HID + 4];
+    __shared__ float s_h[RB][HID];
+    __shared__ float s_act[RB][NA * MAXK];
+    const int k = blockIdx.y, tid = threadIdx.x, rl = tid >> 4, g = tid & 15;
+    const int r = blockIdx.x * RB + rl;
+    const int na = NA * p.K;
+    const int64_t Ds = (int64_t)p.K * p.D;
+    const Mlp ma = mlp_k(p.actor, k, p.D, NA);
+    // actor forward
+    stage_w2(ma.w2, s_w, s_wt);
+    for (int i = tid; i < RB * na; i += 256) s_act[i / na][i % na] = p.x[(int64_t)(blockIdx.x * RB + i / na) * p.ldx + Ds + i % na];
+    __syncthreads();
+    float z[8];
+    RowFwd fa;
+    l1_sum(p.part_a, p.nch_a, p.K, p.B, k, r, g, ma.b1, z);
+    ln_relu(z, ma.lw1, ma.lb1, g, fa.xh1, fa.y1, fa.rs1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s_h[rl][8 * g + i] = fa.y1[i];
+    __syncthreads();
+    row_gemv(s_h[rl], s_w, g, z);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) z[i] += ma.b2[8 * g + i];
+    ln_relu(z, ma.lw2, ma.lb2, g, fa.xh2, fa.y2, fa.rs2);
+    float lg[NA];
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        float s = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s = fmaf(fa.y2[i], ma.w3[(8 * g + i) * NA + a], s);
+        lg[a] = row_sum(s) + ma.b3[a];
+    }
+    // GumbelSoftmax (tau 1) with its gradient: torch's softmax((logits - log(-log(u + eps) + eps)) / 1)
+    const float *ur = p.u + ((int64_t)k * p.B + r) * NA;
+    float pr[NA], mx = -INFINITY;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        pr[a] = (lg[a] - logf(-logf(ur[a] + G_EPS) + G_EPS)) / 1.0f;
+        mx = fmaxf(mx, pr[a]);
+    }
+    float sum = 0.0f;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        pr[a] = expf(pr[a] - mx);
+        sum += pr[a];
+    }
+#pragma unroll
+    for (int a = 0; a < NA; ++a) pr[a] = pr[a] / sum;
+    if (p.probs_out && g == 0)
+        for (int a = 0; a < NA; ++a) p.probs_out[((int64_t)k * p.B + r) * NA + a] = pr[a];
+    __syncthreads();
+    // the critic k on the mixed actions (own slot: the fresh probabilities)
+    if (g == 0)
+        for (int a = 0; a < NA; ++a) s_act[rl][NA * k + a] = pr[a];
+    const Mlp mc = mlp_k(p.critic, k, p.K * p.D + na, 1);
+    stage_w2(mc.w2, s_w, s_wt);
+    __syncthreads();
+    RowFwd fc;
+    const float q = critic_fwd(mc, p.part_c, p.nch_cs, p, k, r, g, s_act[rl], s_w, s_h[rl], fc);
+    const float dq = -(1.0f / (float)p.B);  // -mean Q backward (gw_mean_loss_bwd mode 1)
+    float gv1[8], dz1[8], gv2[8], dz2[8];
+    __syncthreads();
+    critic_bwd(mc, dq, g, fc, s_wt, s_h[rl], gv1, dz1, gv2, dz2);
+    // d probs_k = dz1 . W1[the agent's action rows]^T
+    float dp[NA];
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        const float *wr = mc.w1 + (Ds + NA * k + a) * HID + 8 * g;
+        float s = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s = fmaf(dz1[i], wr[i], s);
+        dp[a] = row_sum(s);
+    }
+    // softmax backward: dlogits = p (dp - sum p dp)  (tau 1)
+    float dot = 0.0f;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) dot = fmaf(pr[a], dp[a], dot);
+    float dl[NA];
+#pragma unroll
+    for (int a = 0; a < NA; ++a) dl[a] = pr[a] * (dp[a] - dot);
+    // actor backward
+    __syncthreads();
+    stage_w2(ma.w2, s_w, s_wt);
+    __syncthreads();
+    float gy[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        float s = 0.0f;
+#pragma unroll
+        for (int a = 0; a < NA; ++a) s = fmaf(dl[a], ma.w3[(8 * g + i) * NA + a], s);
+        gy[i] = s;
+    }
+    ln_relu_bwd(gy, fa.y2, fa.xh2, fa.rs2, ma.lw2, g, gv2, dz2);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s_h[rl][8 * g + i] = dz2[i];
+    __syncthreads();
+    row_gemv(s_h[rl], s_wt, g, gy);
+    ln_relu_bwd(gy, fa.y1, fa.xh1, fa.rs1, ma.lw1, g, gv1, dz1);
+    const Saved &sv = p.sv;
+    put8(sv.h1, p.K, p.B, k, r, g, fa.y1);
+    put8(sv.h2, p.K, p.B, k, r, g, fa.y2);
+    put8(sv.xh1, p.K, p.B, k, r, g, fa.xh1);
+    put8(sv.xh2, p.K, p.B, k, r, g, fa.xh2);
+    put8(sv.gv1, p.K, p.B, k, r, g, gv1);
+    put8(sv.gv2, p.K, p.B, k, r, g, gv2);
+    put8(sv.dz1, p.K, p.B, k, r, g, dz1);
+    put8(sv.dz2, p.K, p.B, k, r, g, dz2);
+    if (g == 0) {
+        for (int a = 0; a < NA; ++a) sv.g3[((int64_t)k * p.B + r) * NA + a] = dl[a];
+        sv.aux[(int64_t)k * p.B + r] = q;
+    }
+}
+
+// ---- parameter gradients: reductions over the B rows, in row order ---------------------------
+// blocks [0, nw1): W1 rows (16 inputs each); [nw1, nw1 + 8): W2 rows; then one block for W3, the
+// vectors and the loss.  x: rows r of agent k's layer-1 input at x[r * ldx + k * xk + col0 + d].
+struct GradParams {
+    gw_mlp_actors grad;    // the gradient views (same layout as the parameters), written
+    const float *x;
+    int64_t ldx, xk;
+    int col0, in_dim, out, K, B, nw1, mode;  // mode 0: critic (loss mean (q - y)^2), 1: actor (-mean q)
+    Saved sv;
+    float *loss;           // [K]
+};
+
+__global__ void __launch_bounds__(256) grads_kernel(GradParams p) {
+    __shared__ __attribute__((aligned(16))) float s_in[RB][TILE_R + 4];   // [input][row]
+    __shared__ __attribute__((aligned(16))) float s_dz[TILE_R][HID];       // [row][feature] (one row tile)
+    const int k = blockIdx.y, tid = threadIdx.x;
+    const int b = blockIdx.x;
+    if (b < p.nw1 + HID / RB) {
+        const bool w1 = b < p.nw1;
+        const int d0 = (w1 ? b : b - p.nw1) * RB;
+        const int D = w1 ? p.in_dim : HID;
+        const float *dz = w1 ? p.sv.dz1 : p.sv.dz2;
+        const int di = tid >> 4, g = tid & 15;  // input d0 + di, features 8 g .. + 8
+        float acc[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] = 0.0f;
+        for (int r0 = 0; r0 < p.B; r0 += TILE_R) {
+            const int nr = min(TILE_R, p.B - r0);
+            __syncthreads();
+            for (int i = tid; i < RB * nr; i += 256) {
+                const int r = i / RB, d = i % RB;
+                float v = 0.0f;
+                if (d0 + d < D)
+                    v = w1 ? p.x[(int64_t)(r0 + r) * p.ldx + (int64_t)k * p.xk + p.col0 + d0 + d]
+                           : p.sv.h1[((int64_t)k * p.B + r0 + r) * HID + d0 + d];
+                s_in[d][r] = v;
+            }
+            for (int i = tid; i < nr * HID / 4; i += 256) {
+                const int r = i / (HID / 4), c = i % (HID / 4);
+                *reinterpret_cast<float4 *>(&s_dz[r][4 * c]) =
+                    reinterpret_cast<const float4 *>(dz + ((int64_t)k * p.B + r0 + r) * HID)[c];
+            }
+            __syncthreads();
+            for (int r = 0; r < nr; ++r) {
+                const float xv = s_in[di][r];
+                const float4 a = *reinterpret_cast<const float4 *>(&s_dz[r][8 * g]);
+                const float4 c = *reinterpret_cast<const float4 *>(&s_dz[r][8 * g + 4]);
+                acc[0] = fmaf(xv, a.x, acc[0]);
+                acc[1] = fmaf(xv, a.y, acc[1]);
+                acc[2] = fmaf(xv, a.z, acc[2]);
+                acc[3] = fmaf(xv, a.w, acc[3]);
+                acc[4] = fmaf(xv, c.x, acc[4]);
+                acc[5] = fmaf(xv, c.y, acc[5]);
+                acc[6] = fmaf(xv, c.z, acc[6]);
+                acc[7] = fmaf(xv, c.w, acc[7]);
+            }
+        }
+        if (d0 + di < D) {
+            float *o = const_cast<float *>(w1 ? p.grad.w1 + (int64_t)k * p.in_dim * HID
+                                              : p.grad.w2 + (int64_t)k * HID * HID) +
+                       (int64_t)(d0 + di) * HID + 8 * g;
+            // the per-layer gradient views are 4-byte aligned only in general: scalar stores
+#pragma unroll
+            for (int i = 0; i < 8; ++i) o[i] = acc[i];
+        }
+        return;
+    }
+    // W3 [128][out], b3, the biases / LayerNorm affines of both hidden layers, the loss: one thread
+    // per feature j (rows summed in order)
+    const int j = tid;
+    const int64_t base = (int64_t)k * p.B * HID;
+    if (j < HID) {
+        float db1 = 0.0f, dlw1 = 0.0f, dlb1 = 0.0f, db2 = 0.0f, dlw2 = 0.0f, dlb2 = 0.0f;
+        float w3[NA];
+        for (int a = 0; a < p.out; ++a) w3[a] = 0.0f;
+        for (int r = 0; r < p.B; ++r) {
+            const int64_t o = base + (int64_t)r * HID + j;
+            db1 += p.sv.dz1[o];
+            dlw1 = fmaf(p.sv.gv1[o], p.sv.xh1[o], dlw1);
+            dlb1 += p.sv.gv1[o];
+            db2 += p.sv.dz2[o];
+            dlw2 = fmaf(p.sv.gv2[o], p.sv.xh2[o], dlw2);
+            dlb2 += p.sv.gv2[o];
+            const float h2 = p.sv.h2[o];
+            for (int a = 0; a < p.out; ++a) w3[a] = fmaf(h2, p.sv.g3[((int64_t)k * p.B + r) * p.out + a], w3[a]);
+        }
+        const_cast<float *>(p.grad.b1)[k * HID + j] = db1;
+        const_cast<float *>(p.grad.ln1_w)[k * HID + j] = dlw1;
+        const_cast<float *>(p.grad.ln1_b)[k * HID + j] = dlb1;
+        const_cast<float *>(p.grad.b2)[k * HID + j] = db2;
+        const_cast<float *>(p.grad.ln2_w)[k * HID + j] = dlw2;
+        const_cast<float *>(p.grad.ln2_b)[k * HID + j] = dlb2;
+        for (int a = 0; a < p.out; ++a) const_cast<float *>(p.grad.w3)[((int64_t)k * HID + j) * p.out + a] = w3[a];
+    } else if (j < HID + p.out) {
+        const int a = j - HID;
+        float s = 0.0f;
+        for (int r = 0; r < p.B; ++r) s += p.sv.g3[((int64_t)k * p.B + r) * p.out + a];
+        const_cast<float *>(p.grad.b3)[k * p.out + a] = s;
+    } else if (j == HID + NA + 1 && p.loss) {
+        float s = 0.0f;
+        for (int r = 0; r < p.B; ++r) s += p.sv.aux[(int64_t)k * p.B + r];
+        p.loss[k] = p.mode == 0 ? s / (float)p.B : -(s / (float)p.B);
+    }
+}
+
+// ---- workspace ---------------------------------------------------------------------------------
+struct Ws {
+    float *part_a, *part_ct, *part_c;
+    Saved sv;
+};
+inline int nchunks(int64_t D) { return (int)((D + DC - 1) / DC); }
+inline Ws ws_layout(float *w, int K, int B, int D) {
+    const int64_t ldx = (int64_t)K * D + (int64_t)NA * K;
+    Ws s;
+    s.part_a = w;
+    w += (int64_t)nchunks(D) * K * B * HID;
+    s.part_ct = w;
+    w += (int64_t)nchunks((int64_t)K * D) * K * B * HID;
+    s.part_c = w;
+    w += (int64_t)nchunks(ldx) * K * B * HID;
+    float **f[8] = {&s.sv.h1, &s.sv.h2, &s.sv.xh1, &s.sv.xh2, &s.sv.gv1, &s.sv.gv2, &s.sv.dz1, &s.sv.dz2};
+    for (float **q : f) {
+        *q = w;
+        w += (int64_t)K * B * HID;
+    }
+    s.sv.g3 = w;
+    w += (int64_t)K * B * NA;
+    s.sv.aux = w;
+    return s;
+}
+int64_t ws_floats(int K, int B, int D) {
+    const int64_t ldx = (int64_t)K * D + (int64_t)NA * K;
+    return ((int64_t)nchunks(D) + nchunks((int64_t)K * D) + nchunks(ldx)) * K * B * HID + 8LL * K * B * HID +
+           (int64_t)K * B * NA + (int64_t)K * B + 64;
+}
+
+void add_job(L1Params &lp, int &blocks, const float *x, int64_t ldx, int64_t xk, int col0, const float *w, int64_t wk,
+             int wrow0, int D, float *part) {
+    L1Job &j = lp.job[lp.njob];
+    j.x = x;
+    j.w = w;
+    j.part = part;
+    j.ldx = ldx;
+    j.xk = xk;
+    j.wk = wk;
+    j.col0 = col0;
+    j.wrow0 = wrow0;
+    j.D = D;
+    j.nchunk = nchunks(D);
+    lp.start[lp.njob] = blocks;
+    blocks += j.nchunk * lp.K * lp.ntile;
+    lp.njob++;
+    lp.start[lp.njob] = blocks;
+}
+
+gw_status check(const gw_maddpg_batch *b, const char *who) {
+    const std::string w(who);
+    if (!b || !b->x || !b->x_next || !b->u) return fail(GW_ERR_ARG, w + ": null argument");
+    if (b->K < 1 || b->K > MAXK) return fail(GW_ERR_ARG, w + ": K out of range");
+    if (b->B < RB || b->B % RB) return fail(GW_ERR_ARG, w + ": B must be a positive multiple of 16");
+    if (b->D < 1) return fail(GW_ERR_ARG, w + ": D must be >= 1");
+    if ((reinterpret_cast<uintptr_t>(b->x) | reinterpret_cast<uintptr_t>(b->x_next)) & 3u)
+        return fail(GW_ERR_ARG, w + ": misaligned rows");
+    return GW_OK;
+}
+
+gw_status check_net(const gw_mlp_actors &n, int K, int in_dim, int out, const std::string &w) {
+    if (n.K != K || n.in_dim != in_dim || n.hidden != HID || n.n_actions != out || !n.layer_norm)
+        return fail(GW_ERR_ARG, w + ": network shape (needs K, in_dim, hidden 128, LayerNorm, out)");
+    if (!n.w1 || !n.b1 || !n.ln1_w || !n.ln1_b || !n.w2 || !n.b2 || !n.ln2_w || !n.ln2_b || !n.w3 || !n.b3)
+        return fail(GW_ERR_ARG, w + ": null parameter");
+    if ((reinterpret_cast<uintptr_t>(n.w1) | reinterpret_cast<uintptr_t>(n.w2)) & 15u)
+        return fail(GW_ERR_ARG, w + ": w1 / w2 must be 16-byte aligned");
+    return GW_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t gw_maddpg_workspace_floats(int32_t K, int32_t B, int32_t D) { return ws_floats(K, B, D); }
+
+gw_status gw_maddpg_critic_grads(const gw_mlp_actors *actor_target, const gw_mlp_actors *critic_target,
+                                 const gw_mlp_actors *critic, const gw_mlp_actors *critic_grad,
+                                 const gw_maddpg_batch *batch, float gamma, float *ws, float *loss, void *stream) {
+    gw_status st = check(batch, "gw_maddpg_critic_grads");
+    if (st != GW_OK) return st;
+    if (!actor_target || !critic_target || !critic || !critic_grad || !ws || !batch->reward || !batch->done)
+        return fail(GW_ERR_ARG, "gw_maddpg_critic_grads: null argument");
+    const int K = batch->K, B = batch->B, D = batch->D;
+    const int64_t ldx = (int64_t)K * D + (int64_t)NA * K;
+    const std::string who("gw_maddpg_critic_grads");
+    if ((st = check_net(*actor_target, K, D, NA, who)) != GW_OK) return st;
+    if ((st = check_net(*critic_target, K, (int)ldx, 1, who)) != GW_OK) return st;
+    if ((st = check_net(*critic, K, (int)ldx, 1, who)) != GW_OK) return st;
+    const Ws w = ws_layout(ws, K, B, D);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    L1Params lp{};
+    lp.K = K;
+    lp.B = B;
+    lp.ntile = (B + TILE_R - 1) / TILE_R;
+    int blocks = 0;
+    add_job(lp, blocks, batch->x_next, ldx, D, 0, actor_target->w1, (int64_t)D * HID, 0, D, w.part_a);
+    add_job(lp, blocks, batch->x_next, ldx, 0, 0, critic_target->w1, ldx * HID, 0, K * D, w.part_ct);
+    add_job(lp, blocks, batch->x, ldx, 0, 0, critic->w1, ldx * HID, 0, (int)ldx, w.part_c);
+    hipLaunchKernelGGL(l1_kernel, dim3(blocks), dim3(256), 0, s, lp);
+    TailParams tp{};
+    tp.actor_t = *actor_target;
+    tp.critic_t = *critic_target;
+    tp.critic = *critic;
+    tp.x = batch->x;
+    tp.x_next = batch->x_next;
+    tp.reward = batch->reward;
+    tp.done = batch->done;
+    tp.u = batch->u;
+    tp.part_a = w.part_a;
+    tp.part_ct = w.part_ct;
+    tp.part_c = w.part_c;
+    tp.sv = w.sv;
+    tp.gamma = gamma;
+    tp.ldx = ldx;
+    tp.K = K;
+    tp.B = B;
+    tp.D = D;
+    tp.nch_a = nchunks(D);
+    tp.nch_c = nchunks(ldx);
+    tp.nch_cs = nchunks((int64_t)K * D);
+    hipLaunchKernelGGL(target_actor_tail, dim3(B / RB, K), dim3(256), 0, s, tp);
+    hipLaunchKernelGGL(critic_tail, dim3(B / RB, K), dim3(256), 0, s, tp);
+    GradParams gp{};
+    gp.grad = *critic_grad;
+    gp.x = batch->x;
+    gp.ldx = ldx;
+    gp.xk = 0;
+    gp.col0 = 0;
+    gp.in_dim = (int)ldx;
+    gp.out = 1;
+    gp.K = K;
+    gp.B = B;
+    gp.nw1 = (int)((ldx + RB - 1) / RB);
+    gp.mode = 0;
+    gp.sv = w.sv;
+    gp.loss = loss;
+    hipLaunchKernelGGL(grads_kernel, dim3(gp.nw1 + HID / RB + 1, K), dim3(256), 0, s, gp);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(GW_ERR_HIP, who + ": " + hipGetErrorString(e));
+    return GW_OK;
+}
+
+gw_status gw_maddpg_actor_grads(const gw_mlp_actors *actor, const gw_mlp_actors *critic,
+                                const gw_mlp_actors *actor_grad, const gw_maddpg_batch *batch, float *ws, float *loss,
+                                float *probs, void *stream) {
+    gw_status st = check(batch, "gw_maddpg_actor_grads");
+    if (st != GW_OK) return st;
+    if (!actor || !critic || !actor_grad || !ws) return fail(GW_ERR_ARG, "gw_maddpg_actor_grads: null argument");
+    const int K = batch->K, B = batch->B, D = batch->D;
+    const int64_t ldx = (int64_t)K * D + (int64_t)NA * K;
+    const std::string who("gw_maddpg_actor_grads");
+    if ((st = check_net(*actor, K, D, NA, who)) != GW_OK) return st;
+    if ((st = check_net(*critic, K, (int)ldx, 1, who)) != GW_OK) return st;
+    const Ws w = ws_layout(ws, K, B, D);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    L1Params lp{};
+    lp.K = K;
+    lp.B = B;
+    lp.ntile = (B + TILE_R - 1) / TILE_R;
+    int blocks = 0;
+    add_job(lp, blocks, batch->x, ldx, D, 0, actor->w1, (int64_t)D * HID, 0, D, w.part_a);
+    add_job(lp, blocks, batch->x, ldx, 0, 0, critic->w1, ldx * HID, 0, K * D, w.part_c);  // state columns
+    hipLaunchKernelGGL(l1_kernel, dim3(blocks), dim3(256), 0, s, lp);
+    TailParams tp{};
+    tp.actor = *actor;
+    tp.critic = *critic;
+    tp.x = batch->x;
+    tp.x_next = batch->x_next;
+    tp.u = batch->u;
+    tp.part_a = w.part_a;
+    tp.part_c = w.part_c;
+    tp.sv = w.sv;
+    tp.ldx = ldx;
+    tp.K = K;
+    tp.B = B;
+    tp.D = D;
+    tp.nch_a = nchunks(D);
+    tp.nch_cs = nchunks((int64_t)K * D);
+    tp.probs_out = probs;
+    hipLaunchKernelGGL(actor_tail, dim3(B / RB, K), dim3(256), 0, s, tp);
+    GradParams gp{};
+    gp.grad = *actor_grad;
+    gp.x = batch->x;
+    gp.ldx = ldx;
+    gp.xk = D;
+    gp.col0 = 0;
+    gp.in_dim = D;
+    gp.out = NA;
+    gp.K = K;
+    gp.B = B;
+    gp.nw1 = (D + RB - 1) / RB;
+    gp.mode = 1;
+    gp.sv = w.sv;
+    gp.loss = loss;
+    hipLaunchKernelGGL(grads_kernel, dim3(gp.nw1 + HID / RB + 1, K), dim3(256), 0, s, gp);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(GW_ERR_HIP, who + ": " + hipGetErrorString(e));
+    return GW_OK;
+}
+
+}  // extern "C"

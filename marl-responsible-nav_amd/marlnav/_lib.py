@@ -20,7 +20,8 @@ CSRC = os.path.join(PKG_ROOT, "csrc")
 INCLUDE = os.path.join(REPO_ROOT, "include")
 LIB_PATH = os.path.join(CSRC, "libgridenv.so")
 HIP_SOURCES = [os.path.join(CSRC, "gridenv.hip"), os.path.join(CSRC, "learner_ops.hip"),
-               os.path.join(CSRC, "actor_ops.hip"), os.path.join(CSRC, "rollout_ops.hip")]
+               os.path.join(CSRC, "actor_ops.hip"), os.path.join(CSRC, "rollout_ops.hip"),
+               os.path.join(CSRC, "maddpg_ops.hip")]
 HEADERS = [os.path.join(INCLUDE, "gridenv.h"), os.path.join(INCLUDE, "learner_ops.h"),
            os.path.join(INCLUDE, "actor_ops.h"), os.path.join(INCLUDE, "rollout_ops.h")]
 SOURCES = HIP_SOURCES + HEADERS
@@ -172,7 +173,7 @@ EXPORTS = ["gw_create", "gw_reset", "gw_step", "gw_state_view", "gw_copy_state",
            "gw_replay_gather", "gw_affine_relu_fwd", "gw_affine_relu_bwd",
            "gw_soft_update2", "gw_td_target", "gw_mean_loss_fwd", "gw_mean_loss_bwd",
            "gw_eval_accum", "gw_profile_spans", "gw_patch_actor_workspace_floats", "gw_patch_actor_prepare",
-           "gw_patch_actor_act"]
+           "gw_patch_actor_act", "gw_maddpg_workspace_floats", "gw_maddpg_critic_grads", "gw_maddpg_actor_grads"]
 
 
 class GwObsSource(C.Structure):
@@ -197,8 +198,19 @@ class GwCnnActors(C.Structure):
                 ("hidden", C.c_int32), ("n_actions", C.c_int32)] + [(n, C.c_void_p) for n in CNN_PARAM_FIELDS]
 
 
+class GwMaddpgBatch(C.Structure):
+    _fields_ = [("K", C.c_int32), ("B", C.c_int32), ("D", C.c_int32), ("x", C.c_void_p), ("x_next", C.c_void_p),
+                ("reward", C.c_void_p), ("done", C.c_void_p), ("u", C.c_void_p)]
+
+
 def _declare(L):
     p = C.c_void_p
+    L.gw_maddpg_workspace_floats.argtypes = [C.c_int32, C.c_int32, C.c_int32]
+    L.gw_maddpg_workspace_floats.restype = C.c_int64
+    L.gw_maddpg_critic_grads.argtypes = [C.POINTER(GwMlpActors)] * 4 + [C.POINTER(GwMaddpgBatch), C.c_float, p, p, p]
+    L.gw_maddpg_critic_grads.restype = C.c_int
+    L.gw_maddpg_actor_grads.argtypes = [C.POINTER(GwMlpActors)] * 3 + [C.POINTER(GwMaddpgBatch), p, p, p, p]
+    L.gw_maddpg_actor_grads.restype = C.c_int
     L.gw_cnn_workspace_floats.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_int64]
     L.gw_cnn_workspace_floats.restype = C.c_int64
     L.gw_cnn_prepare.argtypes = [p, C.POINTER(GwCnnActors), p, p]

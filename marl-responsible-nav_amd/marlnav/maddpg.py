@@ -147,6 +147,20 @@ def _mlp_target(net: StackedMLPActors) -> StackedMLPActors:
     return t
 
 
+def _mlp_spec(net: StackedMLPActors, grad: bool = False):
+    """gw_mlp_actors of a StackedMLPActors (in -> 128 -> LN -> 128 -> LN -> out): its parameters,
+    or (grad=True) their .grad views in the flat gradient buffer."""
+    f = (lambda t: t.grad) if grad else (lambda t: t)
+    ts = (net.weights[0], net.biases[0], net.ln_w[0], net.ln_b[0], net.weights[1], net.biases[1],
+          net.ln_w[1], net.ln_b[1], net.weights[2], net.biases[2])
+    return _lib.GwMlpActors(net.K, net.in_dim, 128, net.weights[2].shape[2], 1, *[f(t).data_ptr() for t in ts])
+
+
+def _fusable_net(net: StackedMLPActors) -> bool:
+    return (net.n_layers == 3 and net.layer_norm and net.weights[0].shape[2] == 128
+            and tuple(net.weights[1].shape[1:]) == (128, 128) and net.flat_params().dtype == torch.float32)
+
+
 class MADDPG:
     """K MADDPG agents with stacked networks.  ``actors`` is a MultiAgentActors (mlp or cnn).
 
@@ -192,6 +206,13 @@ class MADDPG:
             m.requires_grad_(False)
         self._graph = None
         self._graphs = None  # world > 1: three graph segments between the gradient all-reduces
+        # the fused update (csrc/maddpg_ops.hip: two launch sequences carry the two backward
+        # passes; GW_FUSED_LEARN=0 selects the torch-autograd composition)
+        import os
+        self.fused = (self.flat and os.environ.get("GW_FUSED_LEARN", "1") != "0"
+                      and all(_fusable_net(n) for n in (self.actors.net, self.actor_targets.net, self.critics,
+                                                       self.critic_targets)))
+        self._fws = {}
         if self.world > 1:
             self.broadcast_parameters()
 
@@ -268,9 +289,65 @@ class MADDPG:
         self._allreduce_grads("actor")
         return self._learn_finish(ctx)
 
+    def _fused_batch(self, x, x_next, rewards, dones, u):
+        return _lib.GwMaddpgBatch(self.K, x.shape[0], self.H * self.W, x.data_ptr(), x_next.data_ptr(), rewards.data_ptr(),
+                                  dones.data_ptr(), u.data_ptr())
+
+    def _fused_ws(self, B: int) -> torch.Tensor:
+        ws = self._fws.get(B)
+        if ws is None:
+            n = int(_lib.load().gw_maddpg_workspace_floats(self.K, B, self.H * self.W))
+            ws = self._fws[B] = torch.empty(n, dtype=torch.float32, device=self.device)
+        return ws
+
+    def _fused_critic(self, states, actions, rewards, next_states, dones, u_next, critic_in) -> dict:
+        """Phase 1 as gw_maddpg_critic_grads (include/learner_ops.h): 4 launches."""
+        import ctypes as C
+        K, B = states.shape[0], states.shape[1]
+        dev = self.device
+        if critic_in is not None:
+            x, x_next = critic_in
+        else:
+            x = self._critic_in(states, actions)
+            x_next = self._critic_in(next_states, torch.zeros_like(actions))
+        x, x_next = x.contiguous(), x_next.contiguous()
+        if not (x.dtype == x_next.dtype == torch.float32 and tuple(x.shape) == tuple(x_next.shape)
+                == (B, K * self.H * self.W + K * N_ACTIONS)):
+            raise ValueError("critic input rows must be float32 [B, K*H*W + K*9]")
+        u = (u_next if u_next is not None else torch.rand((K, B, N_ACTIONS), device=dev)).to(torch.float32).contiguous()
+        r = rewards.to(device=dev, dtype=torch.float64).contiguous()
+        d = dones.to(device=dev, dtype=torch.uint8).contiguous()
+        loss = torch.empty((K,), dtype=torch.float32, device=dev)
+        ws = self._fused_ws(B)
+        batch = self._fused_batch(x, x_next, r, d, u)
+        at, ct, c = _mlp_spec(self.actor_targets.net), _mlp_spec(self.critic_targets), _mlp_spec(self.critics)
+        cg = _mlp_spec(self.critics, grad=True)
+        _lib.check(_lib.load().gw_maddpg_critic_grads(C.byref(at), C.byref(ct), C.byref(c), C.byref(cg), C.byref(batch),
+                                                      float(self.gamma), ws.data_ptr(), loss.data_ptr(),
+                                                      torch.cuda.current_stream(dev).cuda_stream),
+                   "gw_maddpg_critic_grads")
+        return dict(fused=True, x=x, x_next=x_next, r=r, d=d, u_next=u, states=states, critic_loss=loss, B=B)
+
+    def _fused_actor(self, ctx: dict, u_cur=None):
+        """Phase 2 (after the critic's Adam step) as gw_maddpg_actor_grads: 3 launches."""
+        import ctypes as C
+        K, B, dev = self.K, ctx["B"], self.device
+        u = (u_cur if u_cur is not None else torch.rand((K, B, N_ACTIONS), device=dev)).to(torch.float32).contiguous()
+        loss = torch.empty((K,), dtype=torch.float32, device=dev)
+        batch = self._fused_batch(ctx["x"], ctx["x_next"], ctx["r"], ctx["d"], u)
+        a, c, ag = _mlp_spec(self.actors.net), _mlp_spec(self.critics), _mlp_spec(self.actors.net, grad=True)
+        _lib.check(_lib.load().gw_maddpg_actor_grads(C.byref(a), C.byref(c), C.byref(ag), C.byref(batch),
+                                                     self._fused_ws(B).data_ptr(), loss.data_ptr(), None,
+                                                     torch.cuda.current_stream(dev).cuda_stream),
+                   "gw_maddpg_actor_grads")
+        ctx["u_cur"] = u
+        ctx["actor_loss"] = loss
+
     def _learn_critic(self, states, actions, rewards, next_states, dones, u_next=None, critic_in=None) -> dict:
         """Phase 1: target actions, TD target, critic forward and backward (gradients in the
         critics' .grad, not yet applied)."""
+        if self.fused:
+            return self._fused_critic(states, actions, rewards, next_states, dones, u_next, critic_in)
         K, B = states.shape[0], states.shape[1]
         D = K * self.H * self.W
         with torch.no_grad():
@@ -298,6 +375,9 @@ class MADDPG:
         """Phase 2: the critic's Adam step, then the actor loss through the updated critics and
         its backward (gradients in the actors' .grad, not yet applied)."""
         self.opt_critic.step()
+        if ctx.get("fused"):
+            self._fused_actor(ctx, u_cur)
+            return
         states, actions, x = ctx["states"], ctx["actions"], ctx["x"]
         K, B = states.shape[0], states.shape[1]
         probs = gumbel_softmax(self.actors(states), u_cur)                             # [K, B, 9]

@@ -131,6 +131,7 @@ def test_gpu_flat_learn_matches_per_agent_loop():
     K, H, W, B, steps, lr = 2, 32, 32, 128, 4, 1e-3
     m = MADDPG(K, H, W, lr_actor=lr, lr_critic=lr, gamma=0.98, tau=0.01, batch_size=B, device="cuda", seed=3)
     assert m.flat  # the HIP optimizer / soft-update path
+    m.fused = False  # the autograd composition (the fused kernels: tests/test_maddpg_fused.py)
     with torch.no_grad():
         for net in (m.actor_targets.net, m.critic_targets):
             net.flat_params().add_(0.05 * torch.randn_like(net.flat_params()))

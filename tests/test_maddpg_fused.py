@@ -1,0 +1,145 @@
+"""The fused MADDPG update (csrc/maddpg_ops.hip: gw_maddpg_critic_grads / gw_maddpg_actor_grads,
+the default GPU learner) against the torch-autograd composition of the same update
+(marlnav/maddpg.py with GW_FUSED_LEARN=0, itself pinned to the per-agent agilerl-style loop in
+tests/test_maddpg.py) and against that per-agent loop.
+
+Tolerances.  The fused kernels sum in other orders than torch's GEMMs and LayerNorm (f32,
+deterministic).  (1) One update's gradients: every gradient tensor within 1e-3 relative L2 of
+autograd's, the losses within 1e-4 relative, the target actions (x_next's slots) within 2e-6.
+A ReLU whose input sits at the f32 rounding edge of its LayerNorm can take the other side in one
+of the two; that changes one row's contribution to the affected unit's gradients (hence L2 and
+not elementwise bounds).  (2) Four updates against the per-agent loop: losses within 1e-3
+relative, every parameter tensor within 5e-3 relative L2 and 2 * lr * updates elementwise (Adam's
+normalised step turns such a flip into a move of up to lr in the affected unit only).  (3) A
+HIP-graph replay of the fused update equals the eager fused update bit for bit (fixed orders).
+"""
+import pytest
+import torch
+
+from marlnav.maddpg import MADDPG
+
+pytestmark = pytest.mark.gpu
+
+K, H, W, B, LR = 2, 32, 32, 128, 1e-3
+
+
+def _batch(g, B_=B):
+    states = torch.randint(-1, 6, (K, B_, H, W), generator=g, device="cuda").float()
+    next_states = torch.randint(-1, 6, (K, B_, H, W), generator=g, device="cuda").float()
+    actions = torch.softmax(torch.randn((K, B_, 9), generator=g, device="cuda") * 2, -1)
+    rewards = torch.randn((B_, K), generator=g, dtype=torch.float64, device="cuda") * 10
+    dones = (torch.rand((B_, K), generator=g, device="cuda") < 0.2).to(torch.uint8)
+    u_next = torch.rand((K, B_, 9), generator=g, device="cuda")
+    u_cur = torch.rand((K, B_, 9), generator=g, device="cuda")
+    return states, actions, rewards, next_states, dones, u_next, u_cur
+
+
+def _pair(seed=3):
+    ms = [MADDPG(K, H, W, lr_actor=LR, lr_critic=LR, gamma=0.98, tau=0.01, batch_size=B, device="cuda", seed=seed,
+                 capturable=True) for _ in range(2)]
+    assert ms[0].fused
+    ms[1].fused = False
+    g = torch.Generator(device="cuda").manual_seed(seed + 50)
+    with torch.no_grad():  # targets apart from the online nets, non-trivial LayerNorm affines
+        for m in ms:
+            gg = torch.Generator(device="cuda").manual_seed(seed + 50)
+            for net in (m.actor_targets.net, m.critic_targets):
+                net.flat_params().add_(0.05 * torch.randn(net.flat_params().shape, device="cuda", generator=gg))
+            for net in (m.actors.net, m.critics):
+                for lw, lb in zip(net.ln_w, net.ln_b):
+                    lw.add_(0.2 * torch.randn(lw.shape, device="cuda", generator=gg))
+                    lb.add_(0.1 * torch.randn(lb.shape, device="cuda", generator=gg))
+    del g
+    return ms
+
+
+def _rel(a, b):
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def _grads(net):
+    return [p.grad.detach().clone() for p in (net.weights[0], net.biases[0], net.ln_w[0], net.ln_b[0], net.weights[1],
+                                              net.biases[1], net.ln_w[1], net.ln_b[1], net.weights[2], net.biases[2])]
+
+
+def test_fused_gradients_match_autograd():
+    ms = _pair()
+    g = torch.Generator(device="cuda").manual_seed(7)
+    st, ac, rw, ns, dn, un, uc = _batch(g)
+    x = ms[1]._critic_in(st, ac).contiguous()
+    xn = [ms[1]._critic_in(ns, torch.zeros_like(ac)).contiguous() for _ in range(2)]
+    ctx = [m._learn_critic(st, ac, rw, ns, dn, un, (x.clone(), xn[i])) for i, m in enumerate(ms)]
+    D = K * H * W
+    torch.testing.assert_close(xn[0][:, D:], xn[1][:, D:], rtol=0, atol=2e-6)       # target actions
+    torch.testing.assert_close(ctx[0]["critic_loss"], ctx[1]["critic_loss"], rtol=1e-4, atol=1e-6)
+    rels = [_rel(a, b) for a, b in zip(_grads(ms[0].critics), _grads(ms[1].critics))]
+    print("critic grad rel L2:", ["%.1e" % r for r in rels])
+    assert max(rels) < 1e-3, rels
+    for i, m in enumerate(ms):
+        m._learn_actor(ctx[i], uc)
+    torch.testing.assert_close(ctx[0]["actor_loss"], ctx[1]["actor_loss"], rtol=1e-4, atol=1e-6)
+    rels = [_rel(a, b) for a, b in zip(_grads(ms[0].actors.net), _grads(ms[1].actors.net))]
+    print("actor grad rel L2:", ["%.1e" % r for r in rels])
+    assert max(rels) < 1e-3, rels
+
+
+def test_fused_updates_match_per_agent_loop():
+    from test_maddpg import PerAgentReference, _seq
+    m = _pair()[0]
+    ref = PerAgentReference(m, LR, LR)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    steps = 4
+    for it in range(steps):
+        st, ac, rw, ns, dn, un, uc = _batch(g)
+        a_loss, c_loss = m.learn(st, ac, rw, ns, dn, un, uc)
+        want = ref.learn(st, ac, rw, ns, dn, un, uc)
+        for k in range(K):
+            assert abs(a_loss[k].item() - want[k][0]) < 1e-3 * max(1.0, abs(want[k][0]))
+            assert abs(c_loss[k].item() - want[k][1]) < 1e-3 * max(1.0, abs(want[k][1]))
+    worst = 0.0
+    for k in range(K):
+        for stacked, seqs in ((m.actors.net, ref.actors), (m.actor_targets.net, ref.actor_t),
+                              (m.critics, ref.critics), (m.critic_targets, ref.critic_t)):
+            for a, b in zip(_seq(stacked, k).parameters(), seqs[k].parameters()):
+                rel = _rel(a.detach(), b.detach())
+                worst = max(worst, rel)
+                assert rel < 5e-3, rel
+                assert float((a - b).abs().max()) <= 2 * LR * steps
+    print("worst parameter rel L2 after", steps, "updates:", worst)
+
+
+def test_fused_graph_replay_equals_eager():
+    ms = _pair()
+    ms[1].fused = True
+    g = torch.Generator(device="cuda").manual_seed(9)
+    batch = _batch(g)
+    ms[0].capture(batch=batch, warmup=2)
+    for _ in range(2):
+        ms[1].learn(*batch)
+    for _ in range(3):
+        ms[0].replay_learn()
+        ms[1].learn(*batch)
+    torch.cuda.synchronize()
+    for a, b in zip(ms[0].state_dict().values(), ms[1].state_dict().values()):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("Bt,patch", [(32, 0), (128, 11)])
+def test_fused_small_batch_and_patch_inputs(Bt, patch):
+    """Other batch sizes and the local-window input (D = P * P): fused == autograd, same bound."""
+    global H, W
+    h0, w0 = H, W
+    try:
+        if patch:
+            H = W = patch
+        ms = [MADDPG(K, H, W, device="cuda", seed=5, batch_size=Bt) for _ in range(2)]
+        ms[1].fused = False
+        g = torch.Generator(device="cuda").manual_seed(3)
+        st, ac, rw, ns, dn, un, uc = _batch(g, Bt)
+        outs = [m.learn(st, ac, rw, ns, dn, un, uc) for m in ms]
+        for a, b in zip(outs[0], outs[1]):
+            torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6)
+        for a, b in zip(ms[0].state_dict().values(), ms[1].state_dict().values()):
+            assert _rel(a, b) < 1e-3
+    finally:
+        H, W = h0, w0

@@ -1,0 +1,31 @@
+"""Time gw_obs_patch alone (HIP events) over E and P: where does the patch writer's time go."""
+import os
+import sys
+import time
+
+sys.path[:0] = [os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "marl-responsible-nav_amd"),
+                os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")]
+import torch  # noqa: E402
+
+from marlnav.vec_env import VecGridEnv  # noqa: E402
+
+for scen, E, P in [("grid32", 65536, 11), ("grid32", 16384, 11), ("grid32", 4096, 11), ("grid32", 65536, 3),
+                   ("grid32", 65536, 16), ("grid32", 65536, 20)]:
+    env = VecGridEnv(scen, num_envs=E, fear=False, seed=1, obs=False)
+    env.reset()
+    env.step()
+    out = torch.empty((env.K, E, P, P), device="cuda")
+    for _ in range(3):
+        env.obs_patch(P, out=out)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = 50
+    e0.record()
+    for _ in range(n):
+        env.obs_patch(P, out=out)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / n
+    gb = env.K * E * P * P * 4 / 1e9
+    print(f"{scen} E={E} P={P}: {us:.1f} us per launch, {gb * 1e3:.1f} MB, {gb / (us * 1e-6):.0f} GB/s", flush=True)
+    env.close()
