@@ -18,6 +18,8 @@ def main():
              torch.randint(-1, 6, (K, B, H, W), device="cuda", generator=g).float(),
              (torch.rand((B, K), device="cuda", generator=g) < 0.1).to(torch.uint8))
     m = MADDPG(K, H, W, device="cuda", seed=1, capturable=True, batch_size=B)
+    if len(sys.argv) > 2:
+        m.fused = sys.argv[2] == "fused"
     for _ in range(5):
         m.learn(*batch)
     torch.cuda.synchronize()
@@ -40,7 +42,7 @@ def main():
         graph.replay()
     torch.cuda.synchronize()
     gr = (time.perf_counter() - t0) / n * 1e3
-    print(f"batch {B}: eager {eager:.3f} ms/update, graph {gr:.3f} ms/update")
+    print(f"batch {B} ({'fused' if m.fused else 'autograd'}): eager {eager:.3f} ms/update, graph {gr:.3f} ms/update")
 
 
 if __name__ == "__main__":
