@@ -192,13 +192,23 @@ __device__ __forceinline__ void row_gemv(const float *h, const float (*w)[HID + 
     }
 }
 
-// s_w = W [128][128] and s_wt = W^T from global (block-wide; caller syncs)
-__device__ __forceinline__ void stage_w2(const float *w, float (*s_w)[HID + 4], float (*s_wt)[HID + 4]) {
-    for (int i = threadIdx.x; i < HID * HID; i += 256) {
-        const int r = i / HID, c = i % HID;
-        const float v = w[i];
-        s_w[r][c] = v;
-        s_wt[c][r] = v;
+// dst = W [128][128] (or its transpose) from global, in 4 x 4 register blocks: 16-byte global
+// loads and 16-byte LDS stores either way (block-wide; the caller syncs)
+__device__ __forceinline__ void stage_mat(const float *w, float (*dst)[HID + 4], bool transpose) {
+    for (int b = threadIdx.x; b < (HID / 4) * (HID / 4); b += 256) {
+        const int br = b / (HID / 4), bc = b % (HID / 4);
+        float4 v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = *reinterpret_cast<const float4 *>(w + (4 * br + q) * HID + 4 * bc);
+        if (!transpose) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) *reinterpret_cast<float4 *>(&dst[4 * br + q][4 * bc]) = v[q];
+        } else {
+            *reinterpret_cast<float4 *>(&dst[4 * bc + 0][4 * br]) = make_float4(v[0].x, v[1].x, v[2].x, v[3].x);
+            *reinterpret_cast<float4 *>(&dst[4 * bc + 1][4 * br]) = make_float4(v[0].y, v[1].y, v[2].y, v[3].y);
+            *reinterpret_cast<float4 *>(&dst[4 * bc + 2][4 * br]) = make_float4(v[0].z, v[1].z, v[2].z, v[3].z);
+            *reinterpret_cast<float4 *>(&dst[4 * bc + 3][4 * br]) = make_float4(v[0].w, v[1].w, v[2].w, v[3].w);
+        }
     }
 }
 
@@ -257,7 +267,7 @@ __global__ void __launch_bounds__(256) target_actor_tail(TailParams p) {
     const int k = blockIdx.y, tid = threadIdx.x, rl = tid >> 4, g = tid & 15;
     const int r = blockIdx.x * RB + rl;
     const Mlp m = mlp_k(p.actor_t, k, p.D, NA);
-    for (int i = tid; i < HID * HID; i += 256) s_w[i / HID][i % HID] = m.w2[i];
+    stage_mat(m.w2, s_w, false);
     float z[8], xh[8], y[8], rs;
     l1_sum(p.part_a, p.nch_a, p.K, p.B, k, r, g, m.b1, z);
     ln_relu(z, m.lw1, m.lb1, g, xh, y, rs);
@@ -344,8 +354,8 @@ __device__ __forceinline__ void critic_bwd(const Mlp &m, float dq, int g, const 
 
 // ---- phase 1b: TD target from the critic target, the critic's forward, MSE gradient, backward ----
 __global__ void __launch_bounds__(256) critic_tail(TailParams p) {
-    __shared__ __attribute__((aligned(16))) float s_w[HID][HID + 4];
-    __shared__ __attribute__((aligned(16))) float s_wt[HID][HID + 4];
+    __shared__ __attribute__((aligned(16))) float s_a[HID][HID + 4];
+    __shared__ __attribute__((aligned(16))) float s_b[HID][HID + 4];
     __shared__ float s_h[RB][HID];
     __shared__ float s_act[RB][NA * MAXK];
     const int k = blockIdx.y, tid = threadIdx.x, rl = tid >> 4, g = tid & 15;
@@ -354,19 +364,19 @@ __global__ void __launch_bounds__(256) critic_tail(TailParams p) {
     const int64_t Ds = (int64_t)p.K * p.D;
     // target critic on (s', a'): the action slots written by target_actor_tail
     const Mlp mt = mlp_k(p.critic_t, k, p.K * p.D + na, 1);
+    const Mlp m = mlp_k(p.critic, k, p.K * p.D + na, 1);
     for (int i = tid; i < RB * na; i += 256) s_act[i / na][i % na] = p.x_next[(int64_t)(blockIdx.x * RB + i / na) * p.ldx + Ds + i % na];
-    for (int i = tid; i < HID * HID; i += 256) s_w[i / HID][i % HID] = mt.w2[i];
+    stage_mat(mt.w2, s_a, false);
+    stage_mat(m.w2, s_b, false);
     __syncthreads();
     RowFwd f;
-    const float q_next = critic_fwd(mt, p.part_ct, p.nch_cs, p, k, r, g, s_act[rl], s_w, s_h[rl], f);
+    const float q_next = critic_fwd(mt, p.part_ct, p.nch_cs, p, k, r, g, s_act[rl], s_a, s_h[rl], f);
     // y = f32(r) + ((1 - d) * gamma) * q_next, gw_td_target's op order
     const float t1 = 1.0f - (float)p.done[(int64_t)r * p.K + k];
     const float y = (float)p.reward[(int64_t)r * p.K + k] + (t1 * p.gamma) * q_next;
     __syncthreads();
+    stage_mat(m.w2, s_a, true);  // W2^T for the backward, while the online forward reads s_b
     // online critic on (s, a): the stored actions are the x rows' action slots (in the partials)
-    const Mlp m = mlp_k(p.critic, k, p.K * p.D + na, 1);
-    stage_w2(m.w2, s_w, s_wt);
-    __syncthreads();
     float z[8];
     l1_sum(p.part_c, p.nch_c, p.K, p.B, k, r, g, m.b1, z);
     RowFwd o;
@@ -374,7 +384,7 @@ __global__ void __launch_bounds__(256) critic_tail(TailParams p) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) s_h[rl][8 * g + i] = o.y1[i];
     __syncthreads();
-    row_gemv(s_h[rl], s_w, g, z);
+    row_gemv(s_h[rl], s_b, g, z);
 #pragma unroll
     for (int i = 0; i < 8; ++i) z[i] += m.b2[8 * g + i];
     ln_relu(z, m.lw2, m.lb2, g, o.xh2, o.y2, o.rs2);
@@ -386,7 +396,7 @@ __global__ void __launch_bounds__(256) critic_tail(TailParams p) {
     const float dq = (1.0f / (float)p.B) * (2.0f * diff);  // MSELoss backward (gw_mean_loss_bwd's order)
     float gv1[8], dz1[8], gv2[8], dz2[8];
     __syncthreads();
-    critic_bwd(m, dq, g, o, s_wt, s_h[rl], gv1, dz1, gv2, dz2);
+    critic_bwd(m, dq, g, o, s_a, s_h[rl], gv1, dz1, gv2, dz2);
     const Saved &sv = p.sv;
     put8(sv.h1, p.K, p.B, k, r, g, o.y1);
     put8(sv.h2, p.K, p.B, k, r, g, o.y2);
@@ -405,8 +415,8 @@ __global__ void __launch_bounds__(256) critic_tail(TailParams p) {
 // ---- phase 2: the actor's forward, GumbelSoftmax, the (updated) critic on the mixed actions,
 //      -mean Q gradient, backward through the critic (no parameter gradients) and the actor ----
 __global__ void __launch_bounds__(256) actor_tail(TailParams p) {
-    __shared__ __attribute__((aligned(16))) float s_w[HID][HID + 4];
-    __shared__ __attribute__((aligned(16))) float s_wt[HID][HID + 4];
+    __shared__ __attribute__((aligned(16))) float s_w[HID][HID + 4];   // actor W2, then critic W2^T
+    __shared__ __attribute__((aligned(16))) float s_wt[HID][HID + 4];  // critic W2, then actor W2^T
     __shared__ float s_h[RB][HID];
     __shared__ float s_act[RB][NA * MAXK];
     const int k = blockIdx.y, tid = threadIdx.x, rl = tid >> 4, g = tid & 15;
@@ -414,8 +424,10 @@ __global__ void __launch_bounds__(256) actor_tail(TailParams p) {
     const int na = NA * p.K;
     const int64_t Ds = (int64_t)p.K * p.D;
     const Mlp ma = mlp_k(p.actor, k, p.D, NA);
+    const Mlp mc = mlp_k(p.critic, k, p.K * p.D + na, 1);
     // actor forward
-    stage_w2(ma.w2, s_w, s_wt);
+    stage_mat(ma.w2, s_w, false);
+    stage_mat(mc.w2, s_wt, false);
     for (int i = tid; i < RB * na; i += 256) s_act[i / na][i % na] = p.x[(int64_t)(blockIdx.x * RB + i / na) * p.ldx + Ds + i % na];
     __syncthreads();
     float z[8];
@@ -459,15 +471,13 @@ __global__ void __launch_bounds__(256) actor_tail(TailParams p) {
     // the critic k on the mixed actions (own slot: the fresh probabilities)
     if (g == 0)
         for (int a = 0; a < NA; ++a) s_act[rl][NA * k + a] = pr[a];
-    const Mlp mc = mlp_k(p.critic, k, p.K * p.D + na, 1);
-    stage_w2(mc.w2, s_w, s_wt);
-    __syncthreads();
     RowFwd fc;
-    const float q = critic_fwd(mc, p.part_c, p.nch_cs, p, k, r, g, s_act[rl], s_w, s_h[rl], fc);
+    const float q = critic_fwd(mc, p.part_c, p.nch_cs, p, k, r, g, s_act[rl], s_wt, s_h[rl], fc);
     const float dq = -(1.0f / (float)p.B);  // -mean Q backward (gw_mean_loss_bwd mode 1)
     float gv1[8], dz1[8], gv2[8], dz2[8];
+    stage_mat(mc.w2, s_w, true);  // critic W2^T (the actor's W2 is no longer read)
     __syncthreads();
-    critic_bwd(mc, dq, g, fc, s_wt, s_h[rl], gv1, dz1, gv2, dz2);
+    critic_bwd(mc, dq, g, fc, s_w, s_h[rl], gv1, dz1, gv2, dz2);
     // d probs_k = dz1 . W1[the agent's action rows]^T
     float dp[NA];
 #pragma unroll
@@ -487,7 +497,7 @@ __global__ void __launch_bounds__(256) actor_tail(TailParams p) {
     for (int a = 0; a < NA; ++a) dl[a] = pr[a] * (dp[a] - dot);
     // actor backward
     __syncthreads();
-    stage_w2(ma.w2, s_w, s_wt);
+    stage_mat(ma.w2, s_wt, true);  // actor W2^T
     __syncthreads();
     float gy[8];
 #pragma unroll
@@ -530,12 +540,18 @@ struct GradParams {
     float *loss;           // [K]
 };
 
+constexpr int GRG = 16;  // row groups of the vector / W3 blocks (rows rg, rg + 16, ...)
+
 __global__ void __launch_bounds__(256) grads_kernel(GradParams p) {
-    __shared__ __attribute__((aligned(16))) float s_in[RB][TILE_R + 4];   // [input][row]
-    __shared__ __attribute__((aligned(16))) float s_dz[TILE_R][HID];       // [row][feature] (one row tile)
+    // W blocks: s_in + s_dz; vector block: [16][6][128]; W3 block: [16][128][9] + [16][10]
+    __shared__ __attribute__((aligned(16))) float smem[GRG * HID * NA + GRG * (NA + 1) > RB * (TILE_R + 4) + TILE_R * HID
+                                                        ? GRG * HID * NA + GRG * (NA + 1)
+                                                        : RB * (TILE_R + 4) + TILE_R * HID];
     const int k = blockIdx.y, tid = threadIdx.x;
     const int b = blockIdx.x;
     if (b < p.nw1 + HID / RB) {
+        float (*s_in)[TILE_R + 4] = reinterpret_cast<float (*)[TILE_R + 4]>(smem);     // [input][row]
+        float (*s_dz)[HID] = reinterpret_cast<float (*)[HID]>(smem + RB * (TILE_R + 4));  // [row][feature]
         const bool w1 = b < p.nw1;
         const int d0 = (w1 ? b : b - p.nw1) * RB;
         const int D = w1 ? p.in_dim : HID;
@@ -585,41 +601,111 @@ __global__ void __launch_bounds__(256) grads_kernel(GradParams p) {
         }
         return;
     }
-    // W3 [128][out], b3, the biases / LayerNorm affines of both hidden layers, the loss: one thread
-    // per feature j (rows summed in order)
-    const int j = tid;
+    // thread (row group rg, features 8 g .. 8 g + 7) sums rows rg, rg + 16, ...; the 16 partials are
+    // then added in row-group order (fixed order, independent of the launch)
+    const int rg = tid >> 4, g = tid & 15;
     const int64_t base = (int64_t)k * p.B * HID;
-    if (j < HID) {
-        float db1 = 0.0f, dlw1 = 0.0f, dlb1 = 0.0f, db2 = 0.0f, dlw2 = 0.0f, dlb2 = 0.0f;
-        float w3[NA];
-        for (int a = 0; a < p.out; ++a) w3[a] = 0.0f;
-        for (int r = 0; r < p.B; ++r) {
-            const int64_t o = base + (int64_t)r * HID + j;
-            db1 += p.sv.dz1[o];
-            dlw1 = fmaf(p.sv.gv1[o], p.sv.xh1[o], dlw1);
-            dlb1 += p.sv.gv1[o];
-            db2 += p.sv.dz2[o];
-            dlw2 = fmaf(p.sv.gv2[o], p.sv.xh2[o], dlw2);
-            dlb2 += p.sv.gv2[o];
-            const float h2 = p.sv.h2[o];
-            for (int a = 0; a < p.out; ++a) w3[a] = fmaf(h2, p.sv.g3[((int64_t)k * p.B + r) * p.out + a], w3[a]);
+    if (b == p.nw1 + HID / RB) {  // the vectors: b1, ln1 affine, b2, ln2 affine
+        float acc[6][8];
+#pragma unroll
+        for (int v = 0; v < 6; ++v)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) acc[v][i] = 0.0f;
+        for (int r = rg; r < p.B; r += GRG) {
+            const int64_t o = base + (int64_t)r * HID + 8 * g;
+            const float *src[6] = {p.sv.dz1 + o, p.sv.gv1 + o, p.sv.xh1 + o, p.sv.dz2 + o, p.sv.gv2 + o, p.sv.xh2 + o};
+            float4 q[6][2];
+#pragma unroll
+            for (int v = 0; v < 6; ++v) {
+                q[v][0] = *reinterpret_cast<const float4 *>(src[v]);
+                q[v][1] = *reinterpret_cast<const float4 *>(src[v] + 4);
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int o2 = 3 * h;  // (dz, gv, xh) of layer h + 1
+                const float dzv[8] = {q[o2][0].x, q[o2][0].y, q[o2][0].z, q[o2][0].w,
+                                      q[o2][1].x, q[o2][1].y, q[o2][1].z, q[o2][1].w};
+                const float gvv[8] = {q[o2 + 1][0].x, q[o2 + 1][0].y, q[o2 + 1][0].z, q[o2 + 1][0].w,
+                                      q[o2 + 1][1].x, q[o2 + 1][1].y, q[o2 + 1][1].z, q[o2 + 1][1].w};
+                const float xhv[8] = {q[o2 + 2][0].x, q[o2 + 2][0].y, q[o2 + 2][0].z, q[o2 + 2][0].w,
+                                      q[o2 + 2][1].x, q[o2 + 2][1].y, q[o2 + 2][1].z, q[o2 + 2][1].w};
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    acc[o2][i] += dzv[i];                                  // db
+                    acc[o2 + 1][i] = fmaf(gvv[i], xhv[i], acc[o2 + 1][i]);  // d ln_w
+                    acc[o2 + 2][i] += gvv[i];                              // d ln_b
+                }
+            }
         }
-        const_cast<float *>(p.grad.b1)[k * HID + j] = db1;
-        const_cast<float *>(p.grad.ln1_w)[k * HID + j] = dlw1;
-        const_cast<float *>(p.grad.ln1_b)[k * HID + j] = dlb1;
-        const_cast<float *>(p.grad.b2)[k * HID + j] = db2;
-        const_cast<float *>(p.grad.ln2_w)[k * HID + j] = dlw2;
-        const_cast<float *>(p.grad.ln2_b)[k * HID + j] = dlb2;
-        for (int a = 0; a < p.out; ++a) const_cast<float *>(p.grad.w3)[((int64_t)k * HID + j) * p.out + a] = w3[a];
-    } else if (j < HID + p.out) {
-        const int a = j - HID;
-        float s = 0.0f;
-        for (int r = 0; r < p.B; ++r) s += p.sv.g3[((int64_t)k * p.B + r) * p.out + a];
-        const_cast<float *>(p.grad.b3)[k * p.out + a] = s;
-    } else if (j == HID + NA + 1 && p.loss) {
-        float s = 0.0f;
-        for (int r = 0; r < p.B; ++r) s += p.sv.aux[(int64_t)k * p.B + r];
-        p.loss[k] = p.mode == 0 ? s / (float)p.B : -(s / (float)p.B);
+        float (*part)[6][HID] = reinterpret_cast<float (*)[6][HID]>(smem);  // [rg][vector][feature]
+#pragma unroll
+        for (int v = 0; v < 6; ++v)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) part[rg][v][8 * g + i] = acc[v][i];
+        __syncthreads();
+        for (int t = tid; t < 6 * HID; t += 256) {
+            const int v = t / HID, j = t % HID;
+            float sum = 0.0f;
+            for (int q = 0; q < GRG; ++q) sum += part[q][v][j];
+            float *dst[6] = {const_cast<float *>(p.grad.b1), const_cast<float *>(p.grad.ln1_w),
+                             const_cast<float *>(p.grad.ln1_b), const_cast<float *>(p.grad.b2),
+                             const_cast<float *>(p.grad.ln2_w), const_cast<float *>(p.grad.ln2_b)};
+            dst[v][k * HID + j] = sum;
+        }
+        return;
+    }
+    // W3 = h2^T g3 [128][out], b3 = sum g3, the loss
+    const int out = p.out;
+    float acc[8][NA];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int a = 0; a < NA; ++a) acc[i][a] = 0.0f;
+    float bacc[NA], lacc = 0.0f;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) bacc[a] = 0.0f;
+    for (int r = rg; r < p.B; r += GRG) {
+        const float *hs = p.sv.h2 + base + (int64_t)r * HID + 8 * g;
+        const float4 h0 = *reinterpret_cast<const float4 *>(hs), h1 = *reinterpret_cast<const float4 *>(hs + 4);
+        const float hv[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+        const float *gs = p.sv.g3 + ((int64_t)k * p.B + r) * out;
+        float gv[NA];
+#pragma unroll
+        for (int a = 0; a < NA; ++a) gv[a] = a < out ? gs[a] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int a = 0; a < NA; ++a) acc[i][a] = fmaf(hv[i], gv[a], acc[i][a]);
+#pragma unroll
+        for (int a = 0; a < NA; ++a) bacc[a] += gv[a];
+        lacc += p.sv.aux[(int64_t)k * p.B + r];
+    }
+    float (*part)[HID][NA] = reinterpret_cast<float (*)[HID][NA]>(smem);            // [rg][feature][a]
+    float (*pb)[NA + 1] = reinterpret_cast<float (*)[NA + 1]>(smem + GRG * HID * NA);  // [rg][a | loss]
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int a = 0; a < NA; ++a) part[rg][8 * g + i][a] = acc[i][a];
+    if (g == 0) {
+#pragma unroll
+        for (int a = 0; a < NA; ++a) pb[rg][a] = bacc[a];
+        pb[rg][NA] = lacc;
+    }
+    __syncthreads();
+    for (int t = tid; t < HID * out; t += 256) {
+        const int j = t / out, a = t % out;
+        float sum = 0.0f;
+        for (int q = 0; q < GRG; ++q) sum += part[q][j][a];
+        const_cast<float *>(p.grad.w3)[((int64_t)k * HID + j) * out + a] = sum;
+    }
+    if (tid < out) {
+        float sum = 0.0f;
+        for (int q = 0; q < GRG; ++q) sum += pb[q][tid];
+        const_cast<float *>(p.grad.b3)[k * out + tid] = sum;
+    } else if (tid == 64 && p.loss) {
+        float sum = 0.0f;
+        for (int q = 0; q < GRG; ++q) sum += pb[q][NA];
+        p.loss[k] = p.mode == 0 ? sum / (float)p.B : -(sum / (float)p.B);
     }
 }
 
@@ -761,7 +847,7 @@ gw_status gw_maddpg_critic_grads(const gw_mlp_actors *actor_target, const gw_mlp
     gp.mode = 0;
     gp.sv = w.sv;
     gp.loss = loss;
-    hipLaunchKernelGGL(grads_kernel, dim3(gp.nw1 + HID / RB + 1, K), dim3(256), 0, s, gp);
+    hipLaunchKernelGGL(grads_kernel, dim3(gp.nw1 + HID / RB + 2, K), dim3(256), 0, s, gp);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(GW_ERR_HIP, who + ": " + hipGetErrorString(e));
     return GW_OK;
@@ -819,7 +905,7 @@ gw_status gw_maddpg_actor_grads(const gw_mlp_actors *actor, const gw_mlp_actors 
     gp.mode = 1;
     gp.sv = w.sv;
     gp.loss = loss;
-    hipLaunchKernelGGL(grads_kernel, dim3(gp.nw1 + HID / RB + 1, K), dim3(256), 0, s, gp);
+    hipLaunchKernelGGL(grads_kernel, dim3(gp.nw1 + HID / RB + 2, K), dim3(256), 0, s, gp);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(GW_ERR_HIP, who + ": " + hipGetErrorString(e));
     return GW_OK;
