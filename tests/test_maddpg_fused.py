@@ -5,12 +5,14 @@ tests/test_maddpg.py) and against that per-agent loop.
 
 Tolerances.  The fused kernels sum in other orders than torch's GEMMs and LayerNorm (f32,
 deterministic).  (1) One update's gradients: every gradient tensor within 1e-3 relative L2 of
-autograd's, the losses within 1e-4 relative, the target actions (x_next's slots) within 2e-6.
+autograd's and the median tensor within 1e-5 (measured: 2e-7 .. 6e-7, profiles/r3_learner), the
+losses within 1e-4 relative, the target actions (x_next's slots) within 2e-6.
 A ReLU whose input sits at the f32 rounding edge of its LayerNorm can take the other side in one
 of the two; that changes one row's contribution to the affected unit's gradients (hence L2 and
 not elementwise bounds).  (2) Four updates against the per-agent loop: losses within 1e-3
-relative, every parameter tensor within 5e-3 relative L2 and 2 * lr * updates elementwise (Adam's
-normalised step turns such a flip into a move of up to lr in the affected unit only).  (3) A
+relative, every parameter tensor within 5e-3 relative L2 (the median one within 1e-5) and 2 * lr *
+updates elementwise (Adam's normalised step turns such a flip into a move of up to lr in the
+affected unit only).  (3) A
 HIP-graph replay of the fused update equals the eager fused update bit for bit (fixed orders).
 """
 import pytest
@@ -75,12 +77,14 @@ def test_fused_gradients_match_autograd():
     rels = [_rel(a, b) for a, b in zip(_grads(ms[0].critics), _grads(ms[1].critics))]
     print("critic grad rel L2:", ["%.1e" % r for r in rels])
     assert max(rels) < 1e-3, rels
+    assert sorted(rels)[len(rels) // 2] < 1e-5, rels  # typical tensor: f32 summation order only
     for i, m in enumerate(ms):
         m._learn_actor(ctx[i], uc)
     torch.testing.assert_close(ctx[0]["actor_loss"], ctx[1]["actor_loss"], rtol=1e-4, atol=1e-6)
     rels = [_rel(a, b) for a, b in zip(_grads(ms[0].actors.net), _grads(ms[1].actors.net))]
     print("actor grad rel L2:", ["%.1e" % r for r in rels])
     assert max(rels) < 1e-3, rels
+    assert sorted(rels)[len(rels) // 2] < 1e-5, rels
 
 
 def test_fused_updates_match_per_agent_loop():
@@ -96,16 +100,18 @@ def test_fused_updates_match_per_agent_loop():
         for k in range(K):
             assert abs(a_loss[k].item() - want[k][0]) < 1e-3 * max(1.0, abs(want[k][0]))
             assert abs(c_loss[k].item() - want[k][1]) < 1e-3 * max(1.0, abs(want[k][1]))
-    worst = 0.0
+    worst, rels = 0.0, []
     for k in range(K):
         for stacked, seqs in ((m.actors.net, ref.actors), (m.actor_targets.net, ref.actor_t),
                               (m.critics, ref.critics), (m.critic_targets, ref.critic_t)):
             for a, b in zip(_seq(stacked, k).parameters(), seqs[k].parameters()):
                 rel = _rel(a.detach(), b.detach())
                 worst = max(worst, rel)
+                rels.append(rel)
                 assert rel < 5e-3, rel
                 assert float((a - b).abs().max()) <= 2 * LR * steps
     print("worst parameter rel L2 after", steps, "updates:", worst)
+    assert sorted(rels)[len(rels) // 2] < 1e-5, rels  # typical tensor: no flip, f32 order only
 
 
 def test_fused_graph_replay_equals_eager():
