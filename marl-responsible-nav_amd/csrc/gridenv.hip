@@ -1756,6 +1756,13 @@ __device__ void patch_stage(const Params &p, int P, uint32_t *s_road, uint32_t *
             put(c, agent_value(reset, n, k, c == ac, p.variant));
         }
         for (; np < npatch; ++np) s_pw[slot * npatch + np] = -1;
+        // a later patch on the same window position overrides an earlier one (the obs writer's
+        // order): keep only the last, so the surviving positions are distinct
+        for (int u = 0; u < npatch; ++u) {
+            const int pu = s_pw[slot * npatch + u];
+            for (int u2 = u + 1; u2 < npatch && pu >= 0; ++u2)
+                if (s_pw[slot * npatch + u2] == pu) s_pw[slot * npatch + u] = -1;
+        }
     }
 }
 
@@ -1801,66 +1808,54 @@ __global__ void __launch_bounds__(PATCH_THREADS) patch_kernel(Params p, int P, f
         float *dst = which == 0 ? patch : final_patch;
         if (!dst) continue;
         const uint32_t need = which == 0 ? D_WRITE : D_FINAL;
+        if (which == 1) __syncthreads();  // s_out of the step's windows has been copied out
         for (int wi = wave; wi < nenv * K; wi += PATCH_THREADS / 64) {
             const int el = wi / K, k = wi - el * K;
             if (!(s_flag[el] & need)) continue;   // wave-uniform
             const int slot = (which * PATCH_BE + el) * K + k;
             const int ctr = s_ctr[slot];
             const int cr = ctr >> 16, cc = ctr & 0xFFFF;
-            float v[MAXPL];
+            float *o = s_out + (size_t)k * nenv * PP + el * PP;
 #pragma unroll
             for (int t = 0; t < MAXPL; ++t) {
+                if (t >= npl) break;                    // wave-uniform
                 const int r = cr + pr[t], q = cc + pcl[t];
                 float m = -1.0f;
                 if (r >= 0 && r < H && q >= 0 && q < W) {
                     const int cell = r * W + q;
                     m = ((s_road[cell >> 5] >> (cell & 31)) & 1u) ? 0.0f : -1.0f;
                 }
-                v[t] = m;
+                if (lane + 64 * t < PP) o[lane + 64 * t] = m;
             }
-            for (int u = 0; u < npatch; ++u) {
-                const int pw = s_pw[slot * npatch + u];
-                const float pv = s_pv[slot * npatch + u];
-#pragma unroll
-                for (int t = 0; t < MAXPL; ++t)
-                    if (pw == lane + 64 * t) v[t] = pv;
-            }
-            if (which == 0) {
-                float *o = s_out + (size_t)k * nenv * PP + el * PP;
-#pragma unroll
-                for (int t = 0; t < MAXPL; ++t)
-                    if (t < npl && lane + 64 * t < PP) o[lane + 64 * t] = v[t];
-            } else {
-                float *o = dst + ((int64_t)k * p.E + e0 + el) * PP;
-#pragma unroll
-                for (int t = 0; t < MAXPL; ++t)
-                    if (t < npl && lane + 64 * t < PP) o[lane + 64 * t] = v[t];
+            // the patched cells (distinct window positions after patch_stage), after the map
+            // stores of the same wave (LDS operations of a wave complete in order)
+            if (lane < npatch) {
+                const int pw = s_pw[slot * npatch + lane];
+                if (pw >= 0) o[pw] = s_pv[slot * npatch + lane];
             }
         }
-        if (which == 0) {
-            __syncthreads();
-            const int len = nenv * PP;
-            for (int k = 0; k < K; ++k) {
-                const int64_t off = ((int64_t)k * p.E + e0) * PP;
-                float *o = dst + off;
-                const float *so = s_out + (size_t)k * len;
-                const int lead = (int)((4 - (off & 3)) & 3);
-                bool all = true;  // every env of the block writes (the usual case): one aligned run
-                for (int el = 0; el < nenv; ++el) all = all && (s_flag[el] & D_WRITE);
-                if (!all) {
-                    for (int i = tid; i < len; i += PATCH_THREADS)
-                        if (s_flag[i / PP] & D_WRITE) o[i] = so[i];
-                    continue;
-                }
-                for (int i = tid; i < min(lead, len); i += PATCH_THREADS) o[i] = so[i];
-                const int n4 = (len - lead) / 4;
-                float4 *o4 = reinterpret_cast<float4 *>(o + lead);
-                for (int j = tid; j < n4; j += PATCH_THREADS) {
-                    const int i = lead + 4 * j;
-                    o4[j] = make_float4(so[i], so[i + 1], so[i + 2], so[i + 3]);
-                }
-                for (int i = lead + 4 * n4 + tid; i < len; i += PATCH_THREADS) o[i] = so[i];
+        __syncthreads();
+        const int len = nenv * PP;
+        for (int k = 0; k < K; ++k) {
+            const int64_t off = ((int64_t)k * p.E + e0) * PP;
+            float *o = dst + off;
+            const float *so = s_out + (size_t)k * len;
+            bool all = true;  // every env of the block writes (the step's windows): one aligned run
+            for (int el = 0; el < nenv; ++el) all = all && (s_flag[el] & need);
+            if (!all) {  // terminal windows of the envs that ended (or a partial write)
+                for (int i = tid; i < len; i += PATCH_THREADS)
+                    if (s_flag[i / PP] & need) o[i] = so[i];
+                continue;
             }
+            const int lead = (int)((4 - (off & 3)) & 3);
+            for (int i = tid; i < min(lead, len); i += PATCH_THREADS) o[i] = so[i];
+            const int n4 = (len - lead) / 4;
+            float4 *o4 = reinterpret_cast<float4 *>(o + lead);
+            for (int j = tid; j < n4; j += PATCH_THREADS) {
+                const int i = lead + 4 * j;
+                o4[j] = make_float4(so[i], so[i + 1], so[i + 2], so[i + 3]);
+            }
+            for (int i = lead + 4 * n4 + tid; i < len; i += PATCH_THREADS) o[i] = so[i];
         }
     }
 }

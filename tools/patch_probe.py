@@ -9,8 +9,11 @@ import torch  # noqa: E402
 
 from marlnav.vec_env import VecGridEnv  # noqa: E402
 
-for scen, E, P in [("grid32", 65536, 11), ("grid32", 16384, 11), ("grid32", 4096, 11), ("grid32", 65536, 3),
-                   ("grid32", 65536, 16), ("grid32", 65536, 20)]:
+CASES = [("grid32", 65536, 11), ("grid32", 16384, 11), ("grid32", 4096, 11), ("grid32", 65536, 3),
+         ("grid32", 65536, 16), ("grid32", 65536, 20)]
+if len(sys.argv) > 2:
+    CASES = [("grid32", int(sys.argv[1]), int(sys.argv[2]))]
+for scen, E, P in CASES:
     env = VecGridEnv(scen, num_envs=E, fear=False, seed=1, obs=False)
     env.reset()
     env.step()
