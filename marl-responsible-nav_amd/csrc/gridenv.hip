@@ -29,6 +29,7 @@
 #include <string>
 #include <vector>
 
+#include "patch_ops.h"
 #include "gridenv.h"
 
 namespace gw {
@@ -1718,191 +1719,6 @@ __global__ void __launch_bounds__(128) step_v2(Params p) {
 constexpr int PATCH_THREADS = 256;
 constexpr int PATCH_BE = 32;  // envs per block: a block's windows of one agent are one contiguous run
 
-// the per-(which, env, agent) window centres and patched cells of a patch block, in LDS
-__device__ void patch_stage(const Params &p, int P, uint32_t *s_road, uint32_t *s_flag, int *s_ctr, int *s_pw,
-                            float *s_pv, int64_t e0, int nenv) {
-    const int tid = threadIdx.x;
-    const int W = p.W, N = p.N, K = p.K;
-    const int npatch = N + 1, nroad = (p.HW + 31) / 32, half = P / 2;
-    for (int w = tid; w < nroad; w += PATCH_THREADS) s_road[w] = p.tb.roadbits[w];
-    for (int u = tid; u < 2 * PATCH_BE * K; u += PATCH_THREADS) {  // one thread per (which, env, k)
-        const int which = u / (PATCH_BE * K), el = (u / K) % PATCH_BE, k = u % K;
-        const int slot = (which * PATCH_BE + el) * K + k;
-        if (el >= nenv) continue;
-        const uint32_t *d = p.desc + (e0 + el) * NDESC;
-        const uint32_t f = d[4];
-        if (k == 0 && which == 0) s_flag[el] = f;
-        const bool reset = (which == 0) && (f & D_RESET);
-        const uint32_t apples = which == 0 ? (f >> 8) & 0xFFu : (f >> 16) & 0xFFu;
-        const uint32_t *pw = d + (which == 0 ? 0 : 8);
-        const int ac = ((apples >> k) & 1u) ? p.apples[k] : -1;
-        const int ctr = (int)((pw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
-        const int cr = ctr / W, cc = ctr - cr * W;
-        s_ctr[slot] = (cr << 16) | cc;
-        int np = 0;
-        auto put = [&](int c, float v) {  // window position of cell c, or -1 outside the window
-            const int wr = c / W - cr + half, wc = c % W - cc + half;
-            s_pw[slot * npatch + np] = ((unsigned)wr < (unsigned)P && (unsigned)wc < (unsigned)P) ? wr * P + wc : -1;
-            s_pv[slot * npatch + np] = v;
-            ++np;
-        };
-        if (ac >= 0) {
-            float av = p.tb.base[ac] + 9.0f;
-            if (!reset && av == (float)(k + 1)) av = 1.0f;
-            put(ac, av);
-        }
-        for (int n = 0; n < N; ++n) {
-            const int c = (int)((pw[n >> 1] >> (16 * (n & 1))) & 0xFFFFu);
-            put(c, agent_value(reset, n, k, c == ac, p.variant));
-        }
-        for (; np < npatch; ++np) s_pw[slot * npatch + np] = -1;
-        // a later patch on the same window position overrides an earlier one (the obs writer's
-        // order): keep only the last, so the surviving positions are distinct
-        for (int u = 0; u < npatch; ++u) {
-            const int pu = s_pw[slot * npatch + u];
-            for (int u2 = u + 1; u2 < npatch && pu >= 0; ++u2)
-                if (s_pw[slot * npatch + u2] == pu) s_pw[slot * npatch + u] = -1;
-        }
-    }
-}
-
-// Block = PATCH_BE envs (P <= 16).  Per (which, env, agent) the window's centre and its patched
-// cells as window positions (-1: outside the window) are staged in LDS (patch_stage); then each
-// wave writes whole windows.
-__global__ void __launch_bounds__(PATCH_THREADS) patch_kernel(Params p, int P, float *__restrict__ patch,
-                                                              float *__restrict__ final_patch) {
-    extern __shared__ uint32_t plds[];
-    const int tid = threadIdx.x;
-    const int W = p.W, H = p.H, N = p.N, K = p.K;
-    const int npatch = N + 1, nroad = (p.HW + 31) / 32;
-    uint32_t *s_road = plds;
-    uint32_t *s_flag = s_road + nroad;                                   // [PATCH_BE]
-    int *s_ctr = reinterpret_cast<int *>(s_flag + PATCH_BE);             // [2][PATCH_BE][K]: row << 16 | col
-    int *s_pw = s_ctr + 2 * PATCH_BE * K;                                // [2][PATCH_BE][K][npatch] window positions
-    float *s_pv = reinterpret_cast<float *>(s_pw + 2 * PATCH_BE * K * npatch);
-    const int64_t e0 = (int64_t)blockIdx.x * PATCH_BE;
-    if (e0 >= p.E) return;  // uniform per block
-    const int nenv = (int)min((int64_t)PATCH_BE, p.E - e0);
-    const int PP = P * P, half = P / 2;
-    patch_stage(p, P, s_road, s_flag, s_ctr, s_pw, s_pv, e0, nenv);
-    __syncthreads();
-    // One wave per window at a time: lane l owns window positions l, l + 64, ... (the same for
-    // every window, so their (row, col) are computed once); the map under each (-1 outside the
-    // grid), then the patched cells in order (a later one overrides an earlier one, as the obs
-    // writer does; their window positions are wave-uniform LDS reads).  The step's windows are
-    // assembled in LDS and leave as aligned 16-byte stores along each agent's contiguous run
-    // (whole cache lines: a window is not a multiple of a line, and partial-line writes from
-    // different waves cost HBM read-modify-writes); terminal windows (few envs) go out directly.
-    constexpr int MAXPL = 4;                      // positions per lane: P * P <= 256 (P <= 16)
-    const int wave = tid >> 6, lane = tid & 63;
-    int pr[MAXPL], pcl[MAXPL];
-#pragma unroll
-    for (int t = 0; t < MAXPL; ++t) {
-        const int c = lane + 64 * t;
-        pr[t] = c / P - half;
-        pcl[t] = c - (c / P) * P - half;
-    }
-    const int npl = (PP + 63) / 64;
-    float *s_out = s_pv + 2 * PATCH_BE * K * npatch;  // [K][nenv * PP]
-    for (int which = 0; which < 2; ++which) {
-        float *dst = which == 0 ? patch : final_patch;
-        if (!dst) continue;
-        const uint32_t need = which == 0 ? D_WRITE : D_FINAL;
-        if (which == 1) __syncthreads();  // s_out of the step's windows has been copied out
-        for (int wi = wave; wi < nenv * K; wi += PATCH_THREADS / 64) {
-            const int el = wi / K, k = wi - el * K;
-            if (!(s_flag[el] & need)) continue;   // wave-uniform
-            const int slot = (which * PATCH_BE + el) * K + k;
-            const int ctr = s_ctr[slot];
-            const int cr = ctr >> 16, cc = ctr & 0xFFFF;
-            float *o = s_out + (size_t)k * nenv * PP + el * PP;
-#pragma unroll
-            for (int t = 0; t < MAXPL; ++t) {
-                if (t >= npl) break;                    // wave-uniform
-                const int r = cr + pr[t], q = cc + pcl[t];
-                float m = -1.0f;
-                if (r >= 0 && r < H && q >= 0 && q < W) {
-                    const int cell = r * W + q;
-                    m = ((s_road[cell >> 5] >> (cell & 31)) & 1u) ? 0.0f : -1.0f;
-                }
-                if (lane + 64 * t < PP) o[lane + 64 * t] = m;
-            }
-            // the patched cells (distinct window positions after patch_stage), after the map
-            // stores of the same wave (LDS operations of a wave complete in order)
-            if (lane < npatch) {
-                const int pw = s_pw[slot * npatch + lane];
-                if (pw >= 0) o[pw] = s_pv[slot * npatch + lane];
-            }
-        }
-        __syncthreads();
-        const int len = nenv * PP;
-        for (int k = 0; k < K; ++k) {
-            const int64_t off = ((int64_t)k * p.E + e0) * PP;
-            float *o = dst + off;
-            const float *so = s_out + (size_t)k * len;
-            bool all = true;  // every env of the block writes (the step's windows): one aligned run
-            for (int el = 0; el < nenv; ++el) all = all && (s_flag[el] & need);
-            if (!all) {  // terminal windows of the envs that ended (or a partial write)
-                for (int i = tid; i < len; i += PATCH_THREADS)
-                    if (s_flag[i / PP] & need) o[i] = so[i];
-                continue;
-            }
-            const int lead = (int)((4 - (off & 3)) & 3);
-            for (int i = tid; i < min(lead, len); i += PATCH_THREADS) o[i] = so[i];
-            const int n4 = (len - lead) / 4;
-            float4 *o4 = reinterpret_cast<float4 *>(o + lead);
-            for (int j = tid; j < n4; j += PATCH_THREADS) {
-                const int i = lead + 4 * j;
-                o4[j] = make_float4(so[i], so[i + 1], so[i + 2], so[i + 3]);
-            }
-            for (int i = lead + 4 * n4 + tid; i < len; i += PATCH_THREADS) o[i] = so[i];
-        }
-    }
-}
-
-// P > 16: the general form, one thread per element
-__global__ void __launch_bounds__(PATCH_THREADS) patch_kernel_big(Params p, int P, float *__restrict__ patch,
-                                                                  float *__restrict__ final_patch) {
-    extern __shared__ uint32_t plds[];
-    const int tid = threadIdx.x;
-    const int W = p.W, H = p.H, N = p.N, K = p.K;
-    const int npatch = N + 1, nroad = (p.HW + 31) / 32;
-    uint32_t *s_road = plds;
-    uint32_t *s_flag = s_road + nroad;
-    int *s_ctr = reinterpret_cast<int *>(s_flag + PATCH_BE);
-    int *s_pw = s_ctr + 2 * PATCH_BE * K;
-    float *s_pv = reinterpret_cast<float *>(s_pw + 2 * PATCH_BE * K * npatch);
-    const int64_t e0 = (int64_t)blockIdx.x * PATCH_BE;
-    if (e0 >= p.E) return;
-    const int nenv = (int)min((int64_t)PATCH_BE, p.E - e0);
-    const int PP = P * P, half = P / 2;
-    patch_stage(p, P, s_road, s_flag, s_ctr, s_pw, s_pv, e0, nenv);
-    __syncthreads();
-    for (int which = 0; which < 2; ++which) {
-        float *dst = which == 0 ? patch : final_patch;
-        if (!dst) continue;
-        const uint32_t need = which == 0 ? D_WRITE : D_FINAL;
-        for (int k = 0; k < K; ++k) {
-            float *o = dst + ((int64_t)k * p.E + e0) * PP;
-            for (int i = tid; i < nenv * PP; i += PATCH_THREADS) {
-                const int el = i / PP, c = i - el * PP;
-                if (!(s_flag[el] & need)) continue;
-                const int slot = (which * PATCH_BE + el) * K + k;
-                const int ctr = s_ctr[slot];
-                const int r = (ctr >> 16) + c / P - half, q = (ctr & 0xFFFF) + c % P - half;
-                float v = -1.0f;
-                if (r >= 0 && r < H && q >= 0 && q < W) {
-                    const int cell = r * W + q;
-                    v = ((s_road[cell >> 5] >> (cell & 31)) & 1u) ? 0.0f : -1.0f;
-                }
-                for (int u = 0; u < npatch; ++u)
-                    if (s_pw[slot * npatch + u] == c) v = s_pv[slot * npatch + u];
-                o[i] = v;
-            }
-        }
-    }
-}
-
 // ---------------------------------------------------------------------------------------
 // step_obs (GW_KERNEL=merged with async obs): ONE launch per gw_step on the caller's stream.
 // Blocks [0, nstep) are step_v2 (FeAR inline) of step t; blocks [nstep, grid) write the obs of
@@ -3360,18 +3176,21 @@ gw_status gw_obs_patch(void *handle, int32_t P, float *patch, float *final_patch
     if (!patch && !final_patch) return GW_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
     GW_TRY(wait_fear(env, s));  // async FeAR: the descriptors are written by the world update (joined)
-    gw::Params p = make_params(env);
-    const int be = gw::PATCH_BE;
-    const size_t lds = sizeof(uint32_t) * ((env->HW + 31) / 32 + be) +
-                       sizeof(int) * 2 * be * env->K + (size_t)2 * 2 * be * env->K * (env->N + 1) * sizeof(uint32_t) +
-                       (P <= 16 ? sizeof(float) * (size_t)env->K * be * P * P : 0);  // the assembled windows
-    const unsigned grid = (unsigned)((env->E + be - 1) / be);
-    if (P <= 16)
-        hipLaunchKernelGGL(gw::patch_kernel, dim3(grid), dim3(gw::PATCH_THREADS), lds, s, p, (int)P, patch, final_patch);
-    else
-        hipLaunchKernelGGL(gw::patch_kernel_big, dim3(grid), dim3(gw::PATCH_THREADS), lds, s, p, (int)P, patch,
-                           final_patch);
-    HIP_TRY(hipGetLastError());
+    gw::PatchArgs a;
+    a.desc = env->desc;
+    a.roadbits = env->roadbits;
+    a.base = env->base;
+    a.patch = patch;
+    a.final_patch = final_patch;
+    a.E = env->E;
+    a.H = env->H;
+    a.W = env->W;
+    a.N = env->N;
+    a.K = env->K;
+    a.P = P;
+    a.variant = env->variant;
+    for (int k = 0; k < GW_MAX_AGENTS; ++k) a.apples[k] = k < env->K ? env->apples[k] : -1;
+    HIP_TRY(gw::launch_windows(a, s));
     return GW_OK;
 }
 

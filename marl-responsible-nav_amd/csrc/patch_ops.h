@@ -1,0 +1,28 @@
+// Internal interface between gridenv.hip (gw_obs_patch) and patch_ops.hip (the window writer).
+#ifndef GW_PATCH_OPS_H
+#define GW_PATCH_OPS_H
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "gridenv.h"
+
+namespace gw {
+
+struct PatchArgs {
+    const uint32_t *desc;      // [E][12] obs descriptors of the env's last step
+    const uint32_t *roadbits;  // [ceil(H*W / 32)] bit c: cell c is road
+    const float *base;         // [H*W] static map values (0 road, -1 inactive)
+    float *patch;              // [K][E][P*P] or null
+    float *final_patch;        // [K][E][P*P] or null (terminal windows of the envs that ended)
+    int64_t E;
+    int H, W, N, K, P, variant;
+    int apples[GW_MAX_AGENTS];
+};
+
+hipError_t launch_windows(const PatchArgs &a, hipStream_t s);
+
+}  // namespace gw
+
+#endif

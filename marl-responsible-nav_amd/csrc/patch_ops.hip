@@ -1,0 +1,211 @@
+// patch_ops.hip — gw_obs_patch's writer: each RL agent's P x P egocentric window of its last
+// observation (X1; not a reference format: the reference observes the whole relabelled grid,
+// custom/ma_customenv.py:303-322).  Rows / cols -P/2 .. P-1-P/2 around the agent's own cell, -1
+// outside the grid (the map's inactive value), the same encoding as the full-grid obs writer
+// (static map + the <= N + 1 patched cells of the env's descriptor), so a window equals a crop of
+// the full obs.  Layout [K][E][P*P]; `patch` gets the step's windows (D_WRITE envs), `final` the
+// terminal windows of the envs that ended (D_FINAL, centred on the terminal cell).
+//
+// Block = PB envs (both agents).  Staging: one thread per (which, env, agent) builds the window's
+// patched cells in registers, drops a patch that a later one overrides (the obs writer's order),
+// and leaves window positions + values in LDS.  The step's windows: one wave per window writes
+// the map part into an LDS image of the block's run (lanes own fixed window positions, so their
+// (row, col) offsets are computed once), then the patched cells as one scattered LDS store; the
+// run leaves as aligned 16-byte stores of whole lines.  Terminal windows (few envs per step) go
+// straight to HBM from registers.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "patch_ops.h"
+
+namespace {
+
+constexpr int PB = 32, THREADS = 256, MAXP = GW_MAX_AGENTS + 1, MAXPL = 4;  // MAXPL: P * P <= 256
+constexpr uint32_t D_RESET = 1u, D_WRITE = 2u, D_FINAL = 4u;
+constexpr int NDESC = 12;
+
+__device__ __forceinline__ float agent_value(bool reset, int n, int k, bool on_apple, int variant) {
+    if (reset) return on_apple ? 9.5f : 0.5f;
+    if (on_apple) return (float)(n + 1 + 9);
+    if (variant == 1) return (float)(n + 1);
+    int v = n + 1;
+    if (v >= 1 && v <= 4 && v != k + 1) v = 5;
+    if (v == k + 1) v = 1;
+    return (float)v;
+}
+
+__device__ __forceinline__ float map_value(const uint32_t *road, int H, int W, int r, int q) {
+    if (r < 0 || r >= H || q < 0 || q >= W) return -1.0f;
+    const int cell = r * W + q;
+    return ((road[cell >> 5] >> (cell & 31)) & 1u) ? 0.0f : -1.0f;
+}
+
+template <bool SMALL>  // SMALL: P * P <= 256 (the LDS-assembled path); else one thread per element
+__global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int tid = threadIdx.x, K = a.K, N = a.N, W = a.W, H = a.H, P = a.P;
+    const int PP = P * P, half = P / 2, np = N + 1, nroad = (a.H * a.W + 31) / 32;
+    uint32_t *s_road = lds;
+    uint32_t *s_flag = s_road + nroad;                               // [PB]
+    int *s_ctr = reinterpret_cast<int *>(s_flag + PB);               // [2][PB][K]  row << 16 | col
+    int *s_pw = s_ctr + 2 * PB * K;                                  // [2][PB][K][np] window positions (-1: none)
+    float *s_pv = reinterpret_cast<float *>(s_pw + 2 * PB * K * np);
+    float *s_out = s_pv + 2 * PB * K * np;                           // SMALL: [K][nenv * PP]
+    const int64_t e0 = (int64_t)blockIdx.x * PB;
+    const int nenv = (int)min((int64_t)PB, a.E - e0);
+    for (int w = tid; w < nroad; w += THREADS) s_road[w] = a.roadbits[w];
+    int has_write = 1, has_final = 0;
+    for (int t = tid; t < 2 * PB * K; t += THREADS) {  // staging: thread = (which, env, agent)
+        const int which = t / (PB * K), el = (t / K) % PB, k = t % K;
+        const int slot = (which * PB + el) * K + k;
+        if (el < nenv) {
+            const uint32_t *d = a.desc + (e0 + el) * NDESC;
+            const uint32_t f = d[4];
+            if (k == 0 && which == 0) s_flag[el] = f;
+            if (which == 0) has_write &= (f & D_WRITE) != 0;
+            else has_final |= (f & D_FINAL) != 0;
+            const bool reset = which == 0 && (f & D_RESET);
+            const uint32_t apples = which == 0 ? (f >> 8) & 0xFFu : (f >> 16) & 0xFFu;
+            const uint32_t *pw = d + (which == 0 ? 0 : 8);
+            uint32_t words[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) words[i] = pw[i];
+            const int ac = ((apples >> k) & 1u) ? a.apples[k] : -1;
+            const int ctr = (int)((words[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
+            const int cr = ctr / W, cc = ctr - cr * W;
+            s_ctr[slot] = (cr << 16) | cc;
+            int cell[MAXP];
+            float val[MAXP];
+            int u = 0;
+            if (ac >= 0) {
+                float av = a.base[ac] + 9.0f;
+                if (!reset && av == (float)(k + 1)) av = 1.0f;
+                cell[0] = ac;
+                val[0] = av;
+                u = 1;
+            }
+#pragma unroll
+            for (int n = 0; n < GW_MAX_AGENTS; ++n) {
+                if (n >= N) break;
+                const int c = (int)((words[n >> 1] >> (16 * (n & 1))) & 0xFFFFu);
+                cell[u] = c;
+                val[u] = agent_value(reset, n, k, c == ac, a.variant);
+                ++u;
+            }
+            for (int i = 0; i < np; ++i) {
+                int pos = -1;
+                if (i < u) {
+                    const int c = cell[i];
+                    const int wr = c / W - cr + half, wc = c % W - cc + half;
+                    bool last = (unsigned)wr < (unsigned)P && (unsigned)wc < (unsigned)P;
+                    for (int j = i + 1; j < u; ++j) last = last && cell[j] != c;  // a later patch overrides
+                    pos = last ? wr * P + wc : -1;
+                }
+                s_pw[slot * np + i] = pos;
+                s_pv[slot * np + i] = i < u ? val[i] : 0.0f;
+            }
+        }
+    }
+    const bool all_write = __syncthreads_and(has_write) != 0;  // (also the barrier after the staging)
+    const bool any_final = __syncthreads_or(has_final) != 0;
+    const int wave = tid >> 6, lane = tid & 63;
+    if (SMALL && a.patch) {
+        int pr[MAXPL], pc[MAXPL];
+#pragma unroll
+        for (int t = 0; t < MAXPL; ++t) {
+            const int c = lane + 64 * t;
+            pr[t] = c / P - half;
+            pc[t] = c - (c / P) * P - half;
+        }
+        const int npl = (PP + 63) / 64;
+        for (int wi = wave; wi < nenv * K; wi += THREADS / 64) {
+            const int el = wi / K, k = wi - el * K;
+            const int slot = el * K + k;
+            const int ctr = s_ctr[slot], cr = ctr >> 16, cc = ctr & 0xFFFF;
+            float *o = s_out + (size_t)k * nenv * PP + el * PP;
+#pragma unroll
+            for (int t = 0; t < MAXPL; ++t) {
+                if (t >= npl) break;
+                const float m = map_value(s_road, H, W, cr + pr[t], cc + pc[t]);
+                if (lane + 64 * t < PP) o[lane + 64 * t] = m;
+            }
+            // the patched cells (distinct positions), after this wave's map stores (a wave's LDS
+            // operations complete in order)
+            if (lane < np) {
+                const int pw = s_pw[slot * np + lane];
+                if (pw >= 0) o[pw] = s_pv[slot * np + lane];
+            }
+        }
+        __syncthreads();
+        const int len = nenv * PP;
+        for (int k = 0; k < K; ++k) {
+            const int64_t off = ((int64_t)k * a.E + e0) * PP;
+            float *o = a.patch + off;
+            const float *so = s_out + (size_t)k * len;
+            if (!all_write) {
+                for (int i = tid; i < len; i += THREADS)
+                    if (s_flag[i / PP] & D_WRITE) o[i] = so[i];
+                continue;
+            }
+            const int lead = (int)((4 - (off & 3)) & 3);
+            for (int i = tid; i < min(lead, len); i += THREADS) o[i] = so[i];
+            const int n4 = (len - lead) / 4;
+            float4 *o4 = reinterpret_cast<float4 *>(o + lead);
+            for (int j = tid; j < n4; j += THREADS) {
+                const int i = lead + 4 * j;
+                o4[j] = make_float4(so[i], so[i + 1], so[i + 2], so[i + 3]);
+            }
+            for (int i = lead + 4 * n4 + tid; i < len; i += THREADS) o[i] = so[i];
+        }
+    } else if (a.patch) {  // large windows: one thread per element, overrides in registers
+        for (int k = 0; k < K; ++k) {
+            float *o = a.patch + ((int64_t)k * a.E + e0) * PP;
+            for (int i = tid; i < nenv * PP; i += THREADS) {
+                const int el = i / PP, c = i - el * PP;
+                if (!(s_flag[el] & D_WRITE)) continue;
+                const int slot = el * K + k;
+                const int ctr = s_ctr[slot];
+                float v = map_value(s_road, H, W, (ctr >> 16) + c / P - half, (ctr & 0xFFFF) + c % P - half);
+                for (int u = 0; u < np; ++u)
+                    if (s_pw[slot * np + u] == c) v = s_pv[slot * np + u];
+                o[i] = v;
+            }
+        }
+    }
+    if (!a.final_patch || !any_final) return;
+    // terminal windows: one wave per (ended env, agent), values in registers, straight to HBM
+    for (int wi = wave; wi < nenv * K; wi += THREADS / 64) {
+        const int el = wi / K, k = wi - el * K;
+        if (!(s_flag[el] & D_FINAL)) continue;  // wave-uniform
+        const int slot = (PB + el) * K + k;
+        const int ctr = s_ctr[slot], cr = ctr >> 16, cc = ctr & 0xFFFF;
+        float *o = a.final_patch + ((int64_t)k * a.E + e0 + el) * PP;
+        for (int c = lane; c < PP; c += 64) {
+            float v = map_value(s_road, H, W, cr + c / P - half, cc + c % P - half);
+            for (int u = 0; u < np; ++u)
+                if (s_pw[slot * np + u] == c) v = s_pv[slot * np + u];
+            o[c] = v;
+        }
+    }
+}
+
+}  // namespace
+
+namespace gw {
+
+hipError_t launch_windows(const PatchArgs &a, hipStream_t s) {
+    const int np = a.N + 1, PP = a.P * a.P;
+    const bool small = PP <= 64 * MAXPL;
+    const size_t lds = sizeof(uint32_t) * ((a.H * a.W + 31) / 32 + PB) + sizeof(int) * 2 * PB * a.K +
+                       sizeof(uint32_t) * (size_t)2 * 2 * PB * a.K * np +
+                       (small ? sizeof(float) * (size_t)a.K * PB * PP : 0);
+    const unsigned grid = (unsigned)((a.E + PB - 1) / PB);
+    if (small)
+        hipLaunchKernelGGL(window_kernel<true>, dim3(grid), dim3(THREADS), lds, s, a);
+    else
+        hipLaunchKernelGGL(window_kernel<false>, dim3(grid), dim3(THREADS), lds, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace gw

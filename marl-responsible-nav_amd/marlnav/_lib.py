@@ -21,10 +21,10 @@ INCLUDE = os.path.join(REPO_ROOT, "include")
 LIB_PATH = os.path.join(CSRC, "libgridenv.so")
 HIP_SOURCES = [os.path.join(CSRC, "gridenv.hip"), os.path.join(CSRC, "learner_ops.hip"),
                os.path.join(CSRC, "actor_ops.hip"), os.path.join(CSRC, "rollout_ops.hip"),
-               os.path.join(CSRC, "maddpg_ops.hip")]
+               os.path.join(CSRC, "maddpg_ops.hip"), os.path.join(CSRC, "patch_ops.hip")]
 HEADERS = [os.path.join(INCLUDE, "gridenv.h"), os.path.join(INCLUDE, "learner_ops.h"),
            os.path.join(INCLUDE, "actor_ops.h"), os.path.join(INCLUDE, "rollout_ops.h")]
-SOURCES = HIP_SOURCES + HEADERS
+SOURCES = HIP_SOURCES + HEADERS + [os.path.join(CSRC, "patch_ops.h")]
 OBJ_DIR = os.path.join(CSRC, "build")
 ARCH = os.environ.get("MARLNAV_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

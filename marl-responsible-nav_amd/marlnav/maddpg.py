@@ -533,13 +533,53 @@ class MADDPG:
             sub = {k[len(name) + 1:]: v for k, v in sd.items() if k.startswith(name + ".")}
             m.load_state_dict(sub)
 
-    def save(self, path: str):
+    def optim_state_dict(self) -> dict:
+        """The two optimizers' state as flat tensors (agilerl's save_checkpoint keeps the optimizer
+        state dicts beside the networks): FlatAdam's moments and step count, or torch Adam's
+        per-parameter exp_avg / exp_avg_sq / step in parameter order."""
+        out = {}
+        for name, opt in (("opt_actor", self.opt_actor), ("opt_critic", self.opt_critic)):
+            if isinstance(opt, FlatAdam):
+                out[f"{name}.m"], out[f"{name}.v"], out[f"{name}.count"] = opt.m, opt.v, opt.count
+                continue
+            for i, p in enumerate(opt.param_groups[0]["params"]):
+                st = opt.state.get(p)
+                if not st:
+                    continue
+                for key in ("exp_avg", "exp_avg_sq", "step"):
+                    out[f"{name}.{i}.{key}"] = torch.as_tensor(st[key])
+        return {k: v.detach().contiguous() for k, v in out.items()}
+
+    @torch.no_grad()
+    def load_optim_state_dict(self, sd: dict):
+        for name, opt in (("opt_actor", self.opt_actor), ("opt_critic", self.opt_critic)):
+            if isinstance(opt, FlatAdam):
+                if f"{name}.m" in sd:
+                    opt.m.copy_(sd[f"{name}.m"])
+                    opt.v.copy_(sd[f"{name}.v"])
+                    opt.count.copy_(sd[f"{name}.count"])
+                continue
+            for i, p in enumerate(opt.param_groups[0]["params"]):
+                if f"{name}.{i}.exp_avg" not in sd:
+                    continue
+                opt.state[p] = {key: sd[f"{name}.{i}.{key}"].to(p.device if key != "step" else
+                                                                     sd[f"{name}.{i}.step"].device).clone()
+                                for key in ("exp_avg", "exp_avg_sq", "step")}
+
+    def save(self, path: str, optimizer: bool = True):
+        """Networks (+ optimizer state) as safetensors."""
         from safetensors.torch import save_file
-        save_file({k: v.cpu() for k, v in self.state_dict().items()}, path)
+        sd = dict(self.state_dict())
+        if optimizer:
+            sd.update(self.optim_state_dict())
+        save_file({k: v.cpu() for k, v in sd.items()}, path)
 
     def load(self, path: str):
         from safetensors.torch import load_file
-        self.load_state_dict({k: v.to(self.device) for k, v in load_file(path).items()})
+        sd = load_file(path)
+        self.load_state_dict({k: v.to(self.device) for k, v in sd.items() if not k.startswith("opt_")})
+        self.load_optim_state_dict({k: v.to(self.device) for k, v in sd.items() if k.startswith("opt_")})
+        self.actors.mark_updated()
 
 
 def learns_per_step(num_envs: int, learn_step: int, idx_step: int) -> int:

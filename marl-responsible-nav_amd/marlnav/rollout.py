@@ -52,6 +52,25 @@ class ReplayRing:
     def __len__(self):
         return min(self.t, self.S - 1) * self.E
 
+    _TENSORS = ("obs", "final_obs", "probs", "reward", "term", "done")
+
+    def state_dict(self) -> dict:
+        """The ring's contents and fill state (MADDPGAgent.save_checkpoint's memory.pkl,
+        maddpg/agent.py:255-266; safetensors here, nothing is pickled)."""
+        out = {n: getattr(self, n) for n in self._TENSORS}
+        out["t"] = torch.tensor([self.t], dtype=torch.int64)
+        out["t_dev"] = self.t_dev.reshape(1)
+        return out
+
+    @torch.no_grad()
+    def load_state_dict(self, sd: dict):
+        for n in self._TENSORS:
+            if tuple(sd[n].shape) != tuple(getattr(self, n).shape):
+                raise ValueError(f"replay ring {n}: shape {tuple(sd[n].shape)} != {tuple(getattr(self, n).shape)}")
+            getattr(self, n).copy_(sd[n])
+        self.t = int(sd["t"][0])
+        self.t_dev.copy_(sd["t_dev"].reshape(()))
+
     @torch.no_grad()
     def sample(self, batch: int, generator: torch.Generator | None = None, return_idx: bool = False,
                critic_in: bool = False):
@@ -202,6 +221,29 @@ class Rollout:
             if self.patch and not self.fused:
                 self._patch = self.env.obs_patch(self.patch, out=self._patch)
         self.t = 0
+
+    @torch.no_grad()
+    def resume(self):
+        """Continue after ReplayRing.load_state_dict: the envs start new episodes (as the reference
+        does after load_checkpoint) and their first obs goes into the ring's current slot.  That
+        slot was the next state of the last stored transition, so that transition keeps it as its
+        terminal-obs entry (done set: sampling then reads the final-obs slot), unchanged."""
+        rp = self.replay
+        if rp is None:
+            self.reset()
+            return
+        self._flush()
+        t, S = rp.t, rp.S
+        cur, prev = t % S, (t - 1) % S
+        if t > 0:
+            rp.final_obs[prev].copy_(rp.obs[cur])
+            rp.done[prev].fill_(1)
+        obs, _ = self.env.reset()
+        if self.patch:
+            self.env.obs_patch(self.patch, out=rp.obs[cur])
+        else:
+            rp.obs[cur].copy_(obs)
+        self.t = t
 
     def _obs_now(self):
         if self.replay is not None:

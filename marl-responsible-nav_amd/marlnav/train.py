@@ -77,6 +77,39 @@ class MADDPGTrainer:
                 "episodes": tot.get("episodes", 0.0), "fear": tot.get("fear", 0.0),
                 "crashes": tot.get("crashes", 0.0), "apples": tot.get("apples", 0.0)}
 
+    # ---- MADDPGAgent.save_checkpoint / load_checkpoint / load_wo_memory (maddpg/agent.py:255-281)
+    def save_checkpoint(self, path: str, filename: str, steps: int | None = None):
+        """The networks + optimizers (`filename`, safetensors), the replay memory
+        (`memory.safetensors`: the ring's slots and fill state, where the reference pickles its
+        buffer) and the step counter (`steps.txt`), as the reference lays them out."""
+        import os
+        from safetensors.torch import save_file
+        os.makedirs(path, exist_ok=True)
+        self.rollout.fence()  # the ring's last obs slots are written
+        self.m.save(os.path.join(path, filename))
+        if self.rollout.replay is not None:
+            save_file({k: v.detach().contiguous().cpu() for k, v in self.rollout.replay.state_dict().items()},
+                      os.path.join(path, "memory.safetensors"))
+        with open(os.path.join(path, "steps.txt"), "w") as f:
+            f.write(str(self.total_steps if steps is None else int(steps)))
+
+    def load_checkpoint(self, path: str, filename: str):
+        import os
+        from safetensors.torch import load_file
+        self.load_wo_memory(path, filename)
+        mem = os.path.join(path, "memory.safetensors")
+        if self.rollout.replay is not None and os.path.exists(mem):
+            self.rollout.fence()
+            self.rollout.replay.load_state_dict({k: v.to(self.env.device) for k, v in load_file(mem).items()})
+            self.rollout.resume()
+        with open(os.path.join(path, "steps.txt")) as f:
+            self.total_steps = int(f.read())
+
+    def load_wo_memory(self, path: str, filename: str):
+        """The networks and optimizers only (in place: a captured update graph stays valid)."""
+        import os
+        self.m.load(os.path.join(path, filename))
+
     def total_loss(self) -> float:
         """MADDPGAgent.total_loss: sum of the most recent per-agent losses (actor + critic)."""
         if not self.losses:

@@ -249,3 +249,45 @@ def test_rollout_tick_reduces_partials_and_counts():
     again2 = StatsReducer(8, "cuda")
     again2.push(p)
     assert torch.equal(first, again2.result())  # bit-identical run to run
+
+
+def test_trainer_checkpoint_resume(tmp_path):
+    """MADDPGAgent.save_checkpoint / load_checkpoint (maddpg/agent.py:255-281): networks +
+    optimizers, the replay memory and the step counter come back; after resume() the last stored
+    transition keeps its next state (read through the final-obs slot) and the ring continues with
+    the fresh episodes' obs; the resumed trainer samples, learns and steps on."""
+    from marlnav.maddpg import MADDPG
+    from marlnav.train import MADDPGTrainer
+    sc = S.builtin("grid32")
+
+    def make(seed):
+        env = VecGridEnv(sc, num_envs=256, fear=True, fear_weight=-5.0, stats=True, final_obs=True, seed=seed)
+        m = MADDPG(sc.K, sc.H, sc.W, device=env.device, seed=seed, capturable=False)
+        return env, m, MADDPGTrainer(env, m, memory_size=2048, updates_per_step=1, graph=False, seed=seed)
+
+    env, m, tr = make(2)
+    tr.reset()
+    tr.train(12)
+    rp = tr.rollout.replay
+    tr.rollout.fence()
+    t = rp.t
+    prev = (t - 1) % rp.S
+    want_next = rp.obs[t % rp.S].clone()
+    tr.save_checkpoint(str(tmp_path), "agent.safetensors")
+    env2, m2, tr2 = make(5)
+    tr2.reset()
+    tr2.load_checkpoint(str(tmp_path), "agent.safetensors")
+    rp2 = tr2.rollout.replay
+    assert rp2.t == t and int(rp2.t_dev) == int(rp.t_dev) and tr2.total_steps == tr.total_steps
+    for n in ("probs", "reward", "term"):
+        assert torch.equal(getattr(rp2, n), getattr(rp, n))
+    assert torch.equal(rp2.final_obs[prev], want_next) and bool((rp2.done[prev] == 1).all())
+    for a, b in zip(m.state_dict().values(), m2.state_dict().values()):
+        assert torch.equal(a, b)
+    assert torch.equal(m.opt_actor.m, m2.opt_actor.m) and int(m.opt_actor.count) == int(m2.opt_actor.count)
+    u0 = tr2.updates
+    tr2.train(3)  # the resumed trainer keeps stepping and learning
+    torch.cuda.synchronize()
+    assert tr2.updates > u0 and torch.isfinite(tr2.losses[-1][0]).all()
+    env.close()
+    env2.close()

@@ -358,3 +358,28 @@ def test_gpu_capture_without_warmup_then_eager_learn():
     for a, b in ((ms[0].actors.net, ms[1].actors.net), (ms[0].critics, ms[1].critics)):
         assert torch.equal(a.flat_params(), b.flat_params())
     env.close()
+
+
+def test_checkpoint_keeps_optimizer_state(tmp_path):
+    """MADDPG.save / load carry the optimizers (agilerl's save_checkpoint keeps them): a restored
+    learner's next update equals the original's (CPU, torch Adam state per parameter)."""
+    K, H, W, B = 2, 4, 5, 8
+    m = MADDPG(K, H, W, hidden=(8, 8), batch_size=B, seed=1)
+    g = torch.Generator().manual_seed(0)
+
+    def batch():
+        return (torch.randint(-1, 6, (K, B, H, W), generator=g).float(), torch.softmax(torch.randn((K, B, 9), generator=g), -1),
+                torch.randn((B, K), generator=g, dtype=torch.float64), torch.randint(-1, 6, (K, B, H, W), generator=g).float(),
+                (torch.rand((B, K), generator=g) < 0.2).to(torch.uint8), torch.rand((K, B, 9), generator=g),
+                torch.rand((K, B, 9), generator=g))
+    for _ in range(3):
+        m.learn(*batch())
+    path = str(tmp_path / "ck.safetensors")
+    m.save(path)
+    m2 = MADDPG(K, H, W, hidden=(8, 8), batch_size=B, seed=9)
+    m2.load(path)
+    b = batch()
+    m.learn(*b)
+    m2.learn(*b)
+    for a, c in zip(m.state_dict().values(), m2.state_dict().values()):
+        assert torch.equal(a, c)
