@@ -42,44 +42,63 @@ __device__ __forceinline__ float map_value(const uint32_t *road, int H, int W, i
 }
 
 template <bool SMALL>  // SMALL: P * P <= 256 (the LDS-assembled path); else one thread per element
-__global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a) {
+__global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a, unsigned long long *dbg) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int tid = threadIdx.x, K = a.K, N = a.N, W = a.W, H = a.H, P = a.P;
     const int PP = P * P, half = P / 2, np = N + 1, nroad = (a.H * a.W + 31) / 32;
+    // c / W as a multiply-high: exact for cells < 2^16 with ceil(2^32 / W)
+    const uint32_t a_wmagic = (uint32_t)((0x100000000ull + (uint64_t)W - 1) / (uint64_t)W);
     uint32_t *s_road = lds;
     uint32_t *s_flag = s_road + nroad;                               // [PB]
     int *s_ctr = reinterpret_cast<int *>(s_flag + PB);               // [2][PB][K]  row << 16 | col
     int *s_pw = s_ctr + 2 * PB * K;                                  // [2][PB][K][np] window positions (-1: none)
     float *s_pv = reinterpret_cast<float *>(s_pw + 2 * PB * K * np);
-    float *s_out = s_pv + 2 * PB * K * np;                           // SMALL: [K][nenv * PP]
+    float *s_out = s_pv + 2 * PB * K * np;                           // SMALL: one agent's run [nenv * PP]
     const int64_t e0 = (int64_t)blockIdx.x * PB;
     const int nenv = (int)min((int64_t)PB, a.E - e0);
+    if (dbg && tid == 0) dbg[4 * blockIdx.x + 0] = wall_clock64();
+    // the descriptors of this thread's (which, env, agent) items are loaded first, the road
+    // bitmask beside them; the apple cell's map value then comes from LDS (no dependent load)
+    constexpr int ITEMS = (2 * PB * GW_MAX_AGENTS + THREADS - 1) / THREADS;
+    uint32_t fl[ITEMS], wd[ITEMS][4];
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+        const int t = tid + it * THREADS;
+        const int which = t / (PB * K), el = (t / K) % PB;
+        const bool ok = t < 2 * PB * K && el < nenv;
+        const uint32_t *d = a.desc + (e0 + (ok ? el : 0)) * NDESC;
+        fl[it] = ok ? d[4] : 0u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) wd[it][i] = ok ? d[(which == 0 ? 0 : 8) + i] : 0u;
+    }
     for (int w = tid; w < nroad; w += THREADS) s_road[w] = a.roadbits[w];
+    __syncthreads();
     int has_write = 1, has_final = 0;
-    for (int t = tid; t < 2 * PB * K; t += THREADS) {  // staging: thread = (which, env, agent)
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {  // staging: thread = (which, env, agent)
+        const int t = tid + it * THREADS;
+        if (t >= 2 * PB * K) break;
         const int which = t / (PB * K), el = (t / K) % PB, k = t % K;
         const int slot = (which * PB + el) * K + k;
         if (el < nenv) {
-            const uint32_t *d = a.desc + (e0 + el) * NDESC;
-            const uint32_t f = d[4];
+            const uint32_t f = fl[it];
             if (k == 0 && which == 0) s_flag[el] = f;
             if (which == 0) has_write &= (f & D_WRITE) != 0;
             else has_final |= (f & D_FINAL) != 0;
             const bool reset = which == 0 && (f & D_RESET);
             const uint32_t apples = which == 0 ? (f >> 8) & 0xFFu : (f >> 16) & 0xFFu;
-            const uint32_t *pw = d + (which == 0 ? 0 : 8);
             uint32_t words[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) words[i] = pw[i];
+            for (int i = 0; i < 4; ++i) words[i] = wd[it][i];
             const int ac = ((apples >> k) & 1u) ? a.apples[k] : -1;
             const int ctr = (int)((words[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
-            const int cr = ctr / W, cc = ctr - cr * W;
+            const int cr = (int)__umulhi((uint32_t)ctr, a_wmagic), cc = ctr - cr * W;
             s_ctr[slot] = (cr << 16) | cc;
             int cell[MAXP];
             float val[MAXP];
             int u = 0;
             if (ac >= 0) {
-                float av = a.base[ac] + 9.0f;
+                float av = (((s_road[ac >> 5] >> (ac & 31)) & 1u) ? 0.0f : -1.0f) + 9.0f;
                 if (!reset && av == (float)(k + 1)) av = 1.0f;
                 cell[0] = ac;
                 val[0] = av;
@@ -97,7 +116,8 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a) {
                 int pos = -1;
                 if (i < u) {
                     const int c = cell[i];
-                    const int wr = c / W - cr + half, wc = c % W - cc + half;
+                    const int rr = (int)__umulhi((uint32_t)c, a_wmagic);
+                    const int wr = rr - cr + half, wc = c - rr * W - cc + half;
                     bool last = (unsigned)wr < (unsigned)P && (unsigned)wc < (unsigned)P;
                     for (int j = i + 1; j < u; ++j) last = last && cell[j] != c;  // a later patch overrides
                     pos = last ? wr * P + wc : -1;
@@ -109,6 +129,7 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a) {
     }
     const bool all_write = __syncthreads_and(has_write) != 0;  // (also the barrier after the staging)
     const bool any_final = __syncthreads_or(has_final) != 0;
+    if (dbg && tid == 0) dbg[4 * blockIdx.x + 1] = wall_clock64();
     const int wave = tid >> 6, lane = tid & 63;
     if (SMALL && a.patch) {
         int pr[MAXPL], pc[MAXPL];
@@ -119,44 +140,44 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a) {
             pc[t] = c - (c / P) * P - half;
         }
         const int npl = (PP + 63) / 64;
-        for (int wi = wave; wi < nenv * K; wi += THREADS / 64) {
-            const int el = wi / K, k = wi - el * K;
-            const int slot = el * K + k;
-            const int ctr = s_ctr[slot], cr = ctr >> 16, cc = ctr & 0xFFFF;
-            float *o = s_out + (size_t)k * nenv * PP + el * PP;
-#pragma unroll
-            for (int t = 0; t < MAXPL; ++t) {
-                if (t >= npl) break;
-                const float m = map_value(s_road, H, W, cr + pr[t], cc + pc[t]);
-                if (lane + 64 * t < PP) o[lane + 64 * t] = m;
-            }
-            // the patched cells (distinct positions), after this wave's map stores (a wave's LDS
-            // operations complete in order)
-            if (lane < np) {
-                const int pw = s_pw[slot * np + lane];
-                if (pw >= 0) o[pw] = s_pv[slot * np + lane];
-            }
-        }
-        __syncthreads();
         const int len = nenv * PP;
-        for (int k = 0; k < K; ++k) {
+        for (int k = 0; k < K; ++k) {  // one agent's contiguous run at a time (LDS: nenv * PP floats)
+            if (k > 0) __syncthreads();  // the previous agent's run has been stored
+            for (int el = wave; el < nenv; el += THREADS / 64) {
+                const int slot = el * K + k;
+                const int ctr = s_ctr[slot], cr = ctr >> 16, cc = ctr & 0xFFFF;
+                float *o = s_out + el * PP;
+#pragma unroll
+                for (int t = 0; t < MAXPL; ++t) {
+                    if (t >= npl) break;
+                    const float m = map_value(s_road, H, W, cr + pr[t], cc + pc[t]);
+                    if (lane + 64 * t < PP) o[lane + 64 * t] = m;
+                }
+                // the patched cells (distinct positions), after this wave's map stores (a wave's
+                // LDS operations complete in order)
+                if (lane < np) {
+                    const int pw = s_pw[slot * np + lane];
+                    if (pw >= 0) o[pw] = s_pv[slot * np + lane];
+                }
+            }
+            __syncthreads();
+            if (dbg && tid == 0 && k == 0) dbg[4 * blockIdx.x + 2] = wall_clock64();
             const int64_t off = ((int64_t)k * a.E + e0) * PP;
             float *o = a.patch + off;
-            const float *so = s_out + (size_t)k * len;
             if (!all_write) {
                 for (int i = tid; i < len; i += THREADS)
-                    if (s_flag[i / PP] & D_WRITE) o[i] = so[i];
+                    if (s_flag[i / PP] & D_WRITE) o[i] = s_out[i];
                 continue;
             }
             const int lead = (int)((4 - (off & 3)) & 3);
-            for (int i = tid; i < min(lead, len); i += THREADS) o[i] = so[i];
+            for (int i = tid; i < min(lead, len); i += THREADS) o[i] = s_out[i];
             const int n4 = (len - lead) / 4;
             float4 *o4 = reinterpret_cast<float4 *>(o + lead);
             for (int j = tid; j < n4; j += THREADS) {
                 const int i = lead + 4 * j;
-                o4[j] = make_float4(so[i], so[i + 1], so[i + 2], so[i + 3]);
+                o4[j] = make_float4(s_out[i], s_out[i + 1], s_out[i + 2], s_out[i + 3]);
             }
-            for (int i = lead + 4 * n4 + tid; i < len; i += THREADS) o[i] = so[i];
+            for (int i = lead + 4 * n4 + tid; i < len; i += THREADS) o[i] = s_out[i];
         }
     } else if (a.patch) {  // large windows: one thread per element, overrides in registers
         for (int k = 0; k < K; ++k) {
@@ -172,6 +193,10 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a) {
                 o[i] = v;
             }
         }
+    }
+    if (dbg) {
+        __syncthreads();
+        if (tid == 0) dbg[4 * blockIdx.x + 3] = wall_clock64();
     }
     if (!a.final_patch || !any_final) return;
     // terminal windows: one wave per (ended env, agent), values in registers, straight to HBM
@@ -194,18 +219,23 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a) {
 
 namespace gw {
 
+unsigned long long *g_patch_dbg = nullptr;
+
 hipError_t launch_windows(const PatchArgs &a, hipStream_t s) {
     const int np = a.N + 1, PP = a.P * a.P;
     const bool small = PP <= 64 * MAXPL;
     const size_t lds = sizeof(uint32_t) * ((a.H * a.W + 31) / 32 + PB) + sizeof(int) * 2 * PB * a.K +
                        sizeof(uint32_t) * (size_t)2 * 2 * PB * a.K * np +
-                       (small ? sizeof(float) * (size_t)a.K * PB * PP : 0);
+                       (small ? sizeof(float) * (size_t)PB * PP : 0);
     const unsigned grid = (unsigned)((a.E + PB - 1) / PB);
     if (small)
-        hipLaunchKernelGGL(window_kernel<true>, dim3(grid), dim3(THREADS), lds, s, a);
+        hipLaunchKernelGGL(window_kernel<true>, dim3(grid), dim3(THREADS), lds, s, a, g_patch_dbg);
     else
-        hipLaunchKernelGGL(window_kernel<false>, dim3(grid), dim3(THREADS), lds, s, a);
+        hipLaunchKernelGGL(window_kernel<false>, dim3(grid), dim3(THREADS), lds, s, a, g_patch_dbg);
     return hipGetLastError();
 }
 
 }  // namespace gw
+
+// measurement only (tools/patch_probe.py): per-block wall-clock stamps of the next launches
+extern "C" void gw_patch_debug_buffer(void *buf) { gw::g_patch_dbg = static_cast<unsigned long long *>(buf); }
