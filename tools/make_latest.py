@@ -15,6 +15,8 @@ def main(tag, config):
         kind = KIND.get(name.split("<")[0].strip())
         if kind and v.get("hbm_mb") is not None:
             kernels[kind] = {"hbm_bytes_per_launch": v["hbm_mb"] * 1e6, "avg_us": v["avg_us"]}
+            if v.get("busy_us"):
+                kernels[kind]["busy_us"] = v["busy_us"]  # union of the launches' intervals / launches
     out = {"source": f"profiles/{tag} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of `python bench.py "
                      f"--config {config}`; FETCH_SIZE x2 per MI355X_MICROARCH.md)",
            "config": config, "kernels": kernels}

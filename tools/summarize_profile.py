@@ -10,9 +10,35 @@ import shutil
 import sys
 
 
+def busy_per_launch(trace_csv):
+    """kernel short name -> (launches, union of their [start, end] intervals / launches in us):
+    the busy time per launch bench.py reports as avg_launch_ms (overlapping launches of one
+    kernel, e.g. obs writers of consecutive steps on two streams, counted once)."""
+    iv = {}
+    for r in csv.DictReader(open(trace_csv)):
+        name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
+        iv.setdefault(name, []).append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+    out = {}
+    for name, v in iv.items():
+        v.sort()
+        total, cb, ce = 0, None, None
+        for b, e in v:
+            if ce is None or b > ce:
+                if ce is not None:
+                    total += ce - cb
+                cb, ce = b, e
+            else:
+                ce = max(ce, e)
+        total += ce - cb
+        out[name] = (len(v), total / len(v) / 1e3)
+    return out
+
+
 def main(src, dst):
     os.makedirs(dst, exist_ok=True)
     stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
+    trace = os.path.join(src, "trace", "run_kernel_trace.csv")
+    busy = busy_per_launch(trace) if os.path.exists(trace) else {}
     pmc = {}
     for which, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
         path = os.path.join(src, which, "run_counter_collection.csv")
@@ -23,8 +49,8 @@ def main(src, dst):
                 continue
             pmc.setdefault(r["Kernel_Name"], {}).setdefault(ctr, []).append(float(r["Counter_Value"]))
     lines = [f"# rocprofv3 summary ({os.path.basename(dst)})", "",
-             "| kernel | calls | avg us | min us | max us | % time | FETCH MB/launch (x2 corr.) | WRITE MB/launch | HBM MB/launch |",
-             "|---|---|---|---|---|---|---|---|---|"]
+             "| kernel | calls | avg us | busy us / launch | min us | max us | % time | FETCH MB/launch (x2 corr.) | WRITE MB/launch | HBM MB/launch |",
+             "|---|---|---|---|---|---|---|---|---|---|"]
     out = {}
     for r in stats:
         name = r["Name"]
@@ -35,12 +61,14 @@ def main(src, dst):
         wmb = (sum(w) / len(w)) * 1024 / 1e6 if w else None
         tot = (fmb or 0) + (wmb or 0) if (f or w) else None
         short = name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
-        lines.append(f"| `{short}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.2f} | {float(r['MinNs'])/1e3:.2f} | "
+        bz = busy.get(short, (0, None))[1]
+        lines.append(f"| `{short}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.2f} | "
+                     f"{'' if bz is None else f'{bz:.2f}'} | {float(r['MinNs'])/1e3:.2f} | "
                      f"{float(r['MaxNs'])/1e3:.2f} | {float(r['Percentage']):.1f} | "
                      f"{'' if fmb is None else f'{fmb:.2f}'} | {'' if wmb is None else f'{wmb:.2f}'} | "
                      f"{'' if tot is None else f'{tot:.2f}'} |")
-        out[short] = dict(calls=int(r["Calls"]), avg_us=float(r["AverageNs"]) / 1e3, fetch_mb=fmb, write_mb=wmb,
-                          hbm_mb=tot)
+        out[short] = dict(calls=int(r["Calls"]), avg_us=float(r["AverageNs"]) / 1e3, busy_us=bz, fetch_mb=fmb,
+                          write_mb=wmb, hbm_mb=tot)
     for log in ("trace.log", "fetch.log", "write.log"):
         p = os.path.join(src, log)
         if os.path.exists(p):
