@@ -55,8 +55,8 @@ CONFIGS = {
     "c4patch": dict(scenario="grid64_n8", envs=65536, fear=False, fear_weight=-5.0, rollout=True, arch="cnn", patch=16,
                     workload="BASELINE config 4's CNN head (configs/cnn.yaml: conv 32-64 k2 s2, 128-128, f32) on "
                              "egocentric 16x16 local windows (gw_obs_patch; not a reference format, reported "
-                             "separately): 8-agent 64x64 grid, 65536 envs, no dense obs, the PyTorch CNN forward "
-                             "(hipBLASLt GEMMs) on the windows written into the patch replay ring"),
+                             "separately): 8-agent 64x64 grid, 65536 envs, no dense obs, the fused CNN head "
+                             "(gw_patch_cnn_act: per-centre tables + recomputed positions), patch replay ring"),
     "c4cnn": dict(scenario="grid64_n8", envs=65536, fear=False, fear_weight=-5.0, rollout=True, arch="cnn",
                   workload="BASELINE config 4 as a rollout: 8-agent 64x64 grid, 65536 envs, the configs/cnn.yaml "
                            "actor head (conv 32-64, k2 s2, 128-128, f32; fused gw_cnn_act from the obs "
@@ -228,7 +228,8 @@ def main():
     ap.add_argument("--cnn-torch", action="store_true",
                     help="c4cnn: the PyTorch CNN forward on the dense obs instead of gw_cnn_act (A/B)")
     ap.add_argument("--patch-torch", action="store_true",
-                    help="c5patch: the PyTorch actor forward on the written windows instead of gw_patch_actor_act (A/B)")
+                    help="c5patch / c4patch: the PyTorch actor forward on the written windows instead of "
+                         "gw_patch_actor_act / gw_patch_cnn_act (A/B)")
     ap.add_argument("--high-prio", action="store_true",
                     help="run the step chain on a high-priority stream (its kernels' workgroups are "
                          "dispatched ahead of the concurrent obs writer's)")
@@ -366,7 +367,8 @@ def main():
         # one set of actor weights for every rank: built from the same seed and broadcast from
         # rank 0 (MADDPG does it itself); every rank's sampling draws its own batches
         torch.cuda.manual_seed(1234 + rank)
-        if cfg.get("patch") and cfg.get("arch") == "cnn":  # the CNN head on the P x P windows (PyTorch)
+        if cfg.get("patch") and cfg.get("arch") == "cnn":  # the CNN head on the P x P windows (fused
+            # gw_patch_cnn_act from the obs descriptors; --patch-torch: the PyTorch forward, A/B)
             from marlnav.actor import MultiAgentActors
             learner = None
             actors = MultiAgentActors(K, cfg["patch"], cfg["patch"], arch="cnn", device=env.device, seed=0)

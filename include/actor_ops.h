@@ -123,6 +123,24 @@ gw_status gw_cnn_act(void *env, const gw_cnn_actors *net, const float *ws, int t
                      uint64_t seed, uint64_t counter, const float *uniform, const uint16_t *mask,
                      int32_t *actions, float *probs, float *logits, void *stream);
 
+/* ---- the CNN head on local windows (X1: not a reference format) -----------------------------
+ * The configs/cnn.yaml head built for P x P inputs (net->H = net->W = P; P = 4, 8, 12, 16) over
+ * each RL agent's gw_obs_patch window.  The window centred on cell c differs from its BASE window
+ * (the -1-padded map under it, with the agent's usual own value -- 1, or k + 1 in variant 1 -- at
+ * the centre) only at patched cells, so
+ *   z = tbl_k[c] + sum over the positions Q where the window differs of Wl[:, Q] . (a2(Q) - a2b_k[c][Q])
+ * with tbl_k[c] = b + Wl . a2(base window of c) and a2b derived for every cell by
+ * gw_patch_cnn_prepare (K H W (P/4)^2 64 + K H W 128 floats).  Differing positions (typically
+ * 0-2 per (env, agent)) are recomputed from the obs descriptors; no window is read back.  Workspace
+ * (floats) for E envs: gw_patch_cnn_workspace_floats (includes a [K][E][N + 1][128] buffer of the
+ * recomputed positions' terms).  Tolerance against nn.Conv2d on the written windows:
+ * tests/test_gpu_patch_cnn.py. */
+int64_t gw_patch_cnn_workspace_floats(int32_t P, int32_t H, int32_t W, int32_t K, int64_t E);
+gw_status gw_patch_cnn_prepare(void *env, int32_t P, const gw_cnn_actors *net, float *ws, void *stream);
+gw_status gw_patch_cnn_act(void *env, int32_t P, const gw_cnn_actors *net, const float *ws, int training, float tau,
+                           uint64_t seed, uint64_t counter, const float *uniform, const uint16_t *mask,
+                           int32_t *actions, float *probs, float *logits, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

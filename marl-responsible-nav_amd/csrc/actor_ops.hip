@@ -291,7 +291,9 @@ __device__ __forceinline__ Desc load_desc(const ActParams &p, int64_t e, int k) 
 // PW: the input is the agent's P x P egocentric window (gw_obs_patch's layout): layer 1 starts
 //     from the table row of the agent's cell (p.tbl: bias + the window's map part) and a patched
 //     cell inside the window adds its delta times the W1 row of its window position
-template <int NP, int WAVES, bool BF3 = false, bool H1 = false, bool PW = false>  // NP = patch slots per (env, agent) = N + 1
+// H1 && PW: the window CNN head (gw_patch_cnn_act): layer 1 = the centre's table row + the
+//     recomputed positions' terms (RSX slots per (env, agent))
+template <int NP, int WAVES, bool BF3 = false, bool H1 = false, bool PW = false, int RSX = RS>  // NP = patch slots per (env, agent) = N + 1
 __global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
     constexpr int THREADS = 64 * WAVES;
     constexpr int NW2 = BF3 ? W2B_U4 : W2IMG / 4;
@@ -381,7 +383,10 @@ __global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
         float a[32];
         if (H1) {  // ---- layer 1 from the buffer (features 16j + 4q .. + 3: one float4 each) ----
             const size_t ek = (size_t)k * p.E + (valid ? e : 0);
-            const float4 *h = reinterpret_cast<const float4 *>(p.h1 + ek * HID);
+            // PW: the table row of the window's centre (b + Linear-1 of the base window)
+            const int ctr = PW ? ((unsigned)pc[1 + k] < (unsigned)p.HW ? pc[1 + k] : 0) : 0;
+            const float4 *h = reinterpret_cast<const float4 *>(PW ? p.tbl + ((size_t)k * p.HW + ctr) * HID
+                                                                  : p.h1 + ek * HID);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const float4 v = h[4 * j + q];
@@ -392,7 +397,7 @@ __global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
             }
             const int nr = valid ? p.rare_n[ek] : 0;
             for (int r = 0; r < nr; ++r) {  // the recomputed positions' terms, in slot order
-                const float4 *z = reinterpret_cast<const float4 *>(p.rare_z + (ek * RS + r) * HID);
+                const float4 *z = reinterpret_cast<const float4 *>(p.rare_z + (ek * RSX + r) * HID);
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const float4 v = z[4 * j + q];
@@ -724,6 +729,7 @@ struct CnnParams {
     const uint32_t *desc;     // [E][12]
     int64_t E;
     int N, K, H, W, P, Wq, HW, variant;
+    int PW;                   // window side (gw_patch_cnn_*: P = (PW / 4)^2 positions), 0 = the whole grid
     int ab;                   // GW_CNN_AB (measurement only): bit 0 skip the recomputed positions,
                               // bit 1 skip the table rows
     int apples[MAXN];
@@ -1137,6 +1143,316 @@ __global__ void __launch_bounds__(256) cnn_bucket_reset(CnnParams p) {
     if (i < p.K * p.P) p.ws.bucket_n[i] = 0;
 }
 
+
+// ---- the CNN head on P x P egocentric windows (gw_patch_cnn_*; include/actor_ops.h) ------------
+// The window of agent k centred on cell c differs from its BASE window B_c (the map under the
+// window, -1 outside the grid, and the agent's usual own value vo_k at the centre) only at the
+// patched cells.  gw_patch_cnn_prepare tabulates, per (agent, centre): a2b = conv-2 activations of
+// B_c at every window position Q, and tbl = b + Linear-1(a2b).  Per step, wcnn_l1_kernel lists the
+// positions where the actual window differs from B_c (a patched cell inside the window other than
+// the centre holding vo_k) as bucket items (env, slot) keyed (agent, Q); cnn_rare_plan / the
+// persistent wcnn_rare_kernel recompute each item's position and write Wl[:, Q] . (a2 - a2b);
+// act_kernel<H1, PW> sums tbl[centre] + those terms (slot order) and runs layers 2-3.
+constexpr int RSW = MAXN + 1;   // recomputed positions per (env, agent): <= N + 1 patched cells
+constexpr int WCG = 8;          // centres per wcnn_prep_base block
+constexpr int WNQ = 16;         // positions per window (P <= 16)
+inline CnnWs wcnn_ws_layout(float *base, int K, int NQ, int HW, int64_t E) {
+    CnnWs w{};
+    w.mlp = ws_layout(base, K);
+    float *f = base + cnn_mlp_floats(K);
+    w.wlt = f;        f += (int64_t)K * NQ * C2 * HID;
+    w.a2map = f;      f += (int64_t)K * HW * NQ * C2;     // a2b [K][HW][NQ][64]
+    w.table = f;      f += (int64_t)K * HW * HID;         // tbl [K][HW][128]
+    w.w2t = f;        f += (int64_t)K * 4 * C2 * C1;
+    w.road = reinterpret_cast<uint32_t *>(f);  f += 128;
+    w.rare_z = f;     f += (int64_t)K * E * RSW * HID;
+    w.rare_n = reinterpret_cast<int *>(f);    f += (int64_t)K * E;
+    w.bucket_n = reinterpret_cast<int *>(f);  f += (int64_t)K * NQ;
+    w.bucket = reinterpret_cast<int *>(f);    f += (int64_t)K * NQ * E;
+    w.unit_off = reinterpret_cast<int *>(f);
+    return w;
+}
+inline int64_t wcnn_ws_floats(int K, int NQ, int HW, int64_t E) {
+    return (int64_t)(wcnn_ws_layout(nullptr, K, NQ, HW, E).unit_off - (int *)nullptr) + (int64_t)K * NQ + 1;
+}
+// the agent's own obs value in a non-reset step off its apple (agent_value(false, k, k, false))
+__device__ __forceinline__ float own_value(int k, int variant) { return variant == 1 ? (float)(k + 1) : 1.0f; }
+
+// block (centre group, k), 256 threads: a2b and tbl of WCG centres; block (0, k) also writes the
+// window-major conv-2 weight and (k = 0) the road bitmask
+__global__ void __launch_bounds__(256) wcnn_prep_base(CnnParams p) {
+    const int k = blockIdx.y, tid = threadIdx.x, c0 = blockIdx.x * WCG;
+    const int half = p.PW / 2, NF = p.P * C2;
+    __shared__ float s_w2[C2 * C1 * 4];          // conv2_w [o][c][d], 32 KB
+    __shared__ float s_w1[C1 * 4], s_b1[C1], s_b2[C2];
+    __shared__ float s_a1[WNQ][4][C1];           // 8 KB
+    __shared__ float s_a2[WCG][WNQ * C2];        // 32 KB
+    for (int i = tid; i < C2 * C1 * 4; i += 256) s_w2[i] = p.net.conv2_w[(size_t)k * C2 * C1 * 4 + i];
+    if (tid < C1 * 4) s_w1[tid] = p.net.conv1_w[k * C1 * 4 + tid];
+    if (tid < C1) s_b1[tid] = p.net.conv1_b[k * C1 + tid];
+    if (tid < C2) s_b2[tid] = p.net.conv2_b[k * C2 + tid];
+    if (blockIdx.x == 0) {
+        for (int i = tid; i < 4 * C2 * C1; i += 256) {
+            const int d = i / (C2 * C1), o = (i / C1) % C2, c = i % C1;
+            p.ws.w2t[(size_t)k * 4 * C2 * C1 + i] = p.net.conv2_w[((k * C2 + o) * C1 + c) * 4 + d];
+        }
+        if (k == 0 && tid < 128) {
+            uint32_t bits = 0;
+            for (int j = 0; j < 32; ++j) bits |= (32 * tid + j < p.HW && p.base[min(32 * tid + j, p.HW - 1)] == 0.0f) ? (1u << j) : 0u;
+            p.ws.road[tid] = bits;
+        }
+    }
+    const float vo = own_value(k, p.variant);
+    __syncthreads();
+    for (int ci = 0; ci < WCG; ++ci) {
+        const int c = min(c0 + ci, p.HW - 1);   // (a trailing group repeats its last centre)
+        const int cr = c / p.W, cc = c % p.W;
+        for (int i = tid; i < p.P * 4 * C1; i += 256) {   // conv 1: (position, window d, channel)
+            const int Q = i >> 7, d = (i >> 5) & 3, ch = i & 31, Y = Q / p.Wq, X = Q % p.Wq;
+            float acc = s_b1[ch];
+            for (int tap = 0; tap < 4; ++tap) {
+                const int wr = 4 * Y + 2 * (d >> 1) + (tap >> 1), wc = 4 * X + 2 * (d & 1) + (tap & 1);
+                const int r = cr - half + wr, col = cc - half + wc;
+                const float v = (wr == half && wc == half) ? vo
+                              : (r >= 0 && r < p.H && col >= 0 && col < p.W) ? p.base[r * p.W + col] : -1.0f;
+                acc = fmaf(s_w1[ch * 4 + tap], v, acc);
+            }
+            s_a1[Q][d][ch] = fmaxf(acc, 0.0f);
+        }
+        __syncthreads();
+        for (int i = tid; i < NF; i += 256) {              // conv 2: (position, channel o)
+            const int Q = i >> 6, o = i & 63;
+            float acc = s_b2[o];
+            for (int ch = 0; ch < C1; ++ch)
+#pragma unroll
+                for (int d = 0; d < 4; ++d) acc = fmaf(s_w2[(o * C1 + ch) * 4 + d], s_a1[Q][d][ch], acc);
+            const float a2 = fmaxf(acc, 0.0f);
+            s_a2[ci][i] = a2;
+            if (c0 + ci < p.HW) p.ws.a2map[((size_t)k * p.HW + c) * NF + i] = a2;
+        }
+        __syncthreads();
+    }
+    {   // tbl = b + Wl . a2b: thread (half h, feature j) takes centres 4h .. 4h + 3
+        const int j = tid & (HID - 1), h = tid >> 7;
+        float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        const float *wl = p.ws.wlt + (size_t)k * NF * HID + j;
+        for (int f = 0; f < NF; ++f) {
+            const float w = wl[(size_t)f * HID];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[i] = fmaf(w, s_a2[4 * h + i][f], acc[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int c = c0 + 4 * h + i;
+            if (c < p.HW) p.ws.table[((size_t)k * p.HW + c) * HID + j] = p.net.lin1_b[k * HID + j] + acc[i];
+        }
+    }
+}
+
+// one thread per (env, agent): the positions where the window differs from its base window, in
+// ascending order, as bucket items (e RSW + slot); rare_n = their count
+template <int NP>
+__global__ void __launch_bounds__(256) wcnn_l1_kernel(CnnParams p) {
+    __shared__ uint32_t s_road[128];
+    const int k = blockIdx.y, tid = threadIdx.x;
+    const int64_t e = (int64_t)blockIdx.x * 256 + tid;
+    const bool valid = e < p.E;
+    if (tid < 128) s_road[tid] = p.ws.road[tid];
+    __syncthreads();
+    if (!valid) return;
+    auto map_at = [&](int c) { return ((s_road[c >> 5] >> (c & 31)) & 1u) ? 0.0f : -1.0f; };
+    const uint4 cells = *reinterpret_cast<const uint4 *>(p.desc + e * NDESC);
+    const uint32_t flags = p.desc[e * NDESC + 4];
+    int pc[NP];
+    float pv[NP];
+    {
+        const bool reset = (flags & D_RESET) != 0;
+        const int ac = ((flags >> (8 + k)) & 1u) ? p.apples[k] : -1;
+        float av = (ac >= 0 ? map_at(ac) : 0.0f) + 9.0f;
+        if (!reset && av == (float)(k + 1)) av = 1.0f;
+        pc[0] = ac;
+        pv[0] = av;
+        const uint32_t dw[4] = {cells.x, cells.y, cells.z, cells.w};
+#pragma unroll
+        for (int n = 0; n < NP - 1; ++n) {
+            const int c = (int)((dw[n >> 1] >> (16 * (n & 1))) & 0xFFFFu);
+            pc[1 + n] = c;
+            pv[1 + n] = agent_value(reset, n, k, c == ac, p.variant);
+        }
+    }
+    const int ctr = (unsigned)pc[1 + k] < (unsigned)p.HW ? pc[1 + k] : 0;
+    const int cr = ctr / p.W, cc = ctr % p.W, half = p.PW / 2;
+    const float vo = own_value(k, p.variant);
+    uint32_t qmask = 0;
+    bool ctr_set = false;   // a patched cell on the centre (else the centre shows its map value)
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+        const int c = pc[i];
+        bool live = (unsigned)c < (unsigned)p.HW;
+#pragma unroll
+        for (int r = i + 1; r < NP; ++r) live = live && pc[r] != c;   // a later slot wins
+        if (!live) continue;
+        const int wr = c / p.W - cr + half, wc = c % p.W - cc + half;
+        if ((unsigned)wr >= (unsigned)p.PW || (unsigned)wc >= (unsigned)p.PW) continue;
+        const bool centre = c == ctr;
+        ctr_set = ctr_set || centre;
+        if (centre && pv[i] == vo) continue;
+        qmask |= 1u << ((wr >> 2) * p.Wq + (wc >> 2));
+    }
+    if (!ctr_set && map_at(ctr) != vo) qmask |= 1u << ((half >> 2) * p.Wq + (half >> 2));
+    int ns = 0;
+    while (qmask) {
+        const int Q = __builtin_ctz(qmask);
+        qmask &= qmask - 1;
+        const int idx = atomicAdd(p.ws.bucket_n + k * p.P + Q, 1);
+        p.ws.bucket[((size_t)k * p.P + Q) * p.E + idx] = (int)(e * RSW + ns);
+        ++ns;
+    }
+    p.ws.rare_n[(size_t)k * p.E + e] = ns;
+}
+
+// cnn_rare_kernel over window positions: per unit (agent k, position Q) the Linear-1 block in LDS;
+// lane (item it, quarter q) rebuilds conv-1 window q of Q from the item's descriptor (map under
+// the window, -1 outside, the patched cells), conv 2 meets through the shuffles, a2 - a2b goes
+// through LDS, and the lane writes features 16j + 4q + i of Wl[:, Q] . (a2 - a2b).
+template <int NP>
+__global__ void __launch_bounds__(64 * RARE_WAVES) wcnn_rare_kernel(CnnParams p) {
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int it = lane & 15, q = lane >> 4;
+    const int nb = p.K * p.P, half = p.PW / 2;
+    const int nunits = p.ws.unit_off[nb];
+    __shared__ float4 s_wl[C2 * HID / 4];      // Wl block of Q: [o][128], 32 KB
+    __shared__ float4 s_w2[4 * W2Q];           // conv-2 weight [window][o][c], 32 KB
+    __shared__ float s_w1[C1][4], s_b1[C1], s_b2[C2];
+    __shared__ uint32_t s_road[128];
+    __shared__ float s_dl[RARE_WAVES][C2][TILE];
+    if (tid < 128) s_road[tid] = p.ws.road[tid];
+    int staged_k = -1, staged_Q = -1;
+    for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
+        int lo = 0, hi = nb;  // the bucket holding unit u: unit_off[lo] <= u < unit_off[lo + 1]
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (p.ws.unit_off[mid] <= u) lo = mid; else hi = mid;
+        }
+        const int k = lo / p.P, Q = lo % p.P;
+        const int n = p.ws.bucket_n[lo];
+        const int i_begin = (u - p.ws.unit_off[lo]) * RARE_ITEMS, i_end = min(n, i_begin + RARE_ITEMS);
+        __syncthreads();  // the previous unit is done with the LDS images
+        if (k != staged_k) {
+            const float4 *w2 = reinterpret_cast<const float4 *>(p.ws.w2t) + (size_t)k * (4 * C2 * C1 / 4);
+            for (int i = tid; i < 4 * C2 * C1 / 4; i += 64 * RARE_WAVES) s_w2[(i / (C2 * C1 / 4)) * W2Q + i % (C2 * C1 / 4)] = w2[i];
+            if (tid < C1 * 4) (&s_w1[0][0])[tid] = p.net.conv1_w[k * C1 * 4 + tid];
+            if (tid < C1) s_b1[tid] = p.net.conv1_b[k * C1 + tid];
+            if (tid < C2) s_b2[tid] = p.net.conv2_b[k * C2 + tid];
+        }
+        if (k != staged_k || Q != staged_Q) {
+            const float4 *wl = reinterpret_cast<const float4 *>(p.ws.wlt + ((size_t)k * p.P + Q) * C2 * HID);
+            for (int i = tid; i < C2 * HID / 4; i += 64 * RARE_WAVES) s_wl[i] = wl[i];
+        }
+        staged_k = k;
+        staged_Q = Q;
+        __syncthreads();
+        auto map_at = [&](int c) { return ((s_road[c >> 5] >> (c & 31)) & 1u) ? 0.0f : -1.0f; };
+        const int Y = Q / p.Wq, X = Q % p.Wq;
+        const int b = i_begin + 16 * wave;
+        if (b >= i_end) continue;  // (wave-uniform; no barrier until the next unit's)
+        const bool ok = b + it < i_end;
+        const int item = ok ? p.ws.bucket[(size_t)lo * p.E + b + it] : 0;
+        const int64_t e = item / RSW;
+        const uint4 cells = *reinterpret_cast<const uint4 *>(p.desc + e * NDESC);
+        const uint32_t flags = p.desc[e * NDESC + 4];
+        const bool reset = (flags & D_RESET) != 0;
+        const int ac = ((flags >> (8 + k)) & 1u) ? p.apples[k] : -1;
+        const uint32_t dw[4] = {cells.x, cells.y, cells.z, cells.w};
+        const int own = (int)((dw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
+        const int ctr = (unsigned)own < (unsigned)p.HW ? own : 0;
+        // grid row / col of window q's top-left cell
+        const int r0 = ctr / p.W - half + 4 * Y + 2 * (q >> 1), c0 = ctr % p.W - half + 4 * X + 2 * (q & 1);
+        float v4[4];
+#pragma unroll
+        for (int u4 = 0; u4 < 4; ++u4) {
+            const int r = r0 + (u4 >> 1), c = c0 + (u4 & 1);
+            v4[u4] = (r >= 0 && r < p.H && c >= 0 && c < p.W) ? map_at(r * p.W + c) : -1.0f;
+        }
+        {
+            float av = (ac >= 0 ? map_at(ac) : 0.0f) + 9.0f;
+            if (!reset && av == (float)(k + 1)) av = 1.0f;
+#pragma unroll
+            for (int sl = 0; sl < NP; ++sl) {  // in slot order: a later slot on the same cell wins
+                const int c = sl == 0 ? ac : (int)((dw[(sl - 1) >> 1] >> (16 * ((sl - 1) & 1))) & 0xFFFFu);
+                const float v = sl == 0 ? av : agent_value(reset, sl - 1, k, c == ac, p.variant);
+                const bool on = (unsigned)c < (unsigned)p.HW;
+                const int y = (on ? c / p.W : -8) - r0, x = (on ? c % p.W : -8) - c0;
+                const bool in = on && (unsigned)y < 2u && (unsigned)x < 2u;
+#pragma unroll
+                for (int u4 = 0; u4 < 4; ++u4) v4[u4] = (in && 2 * y + x == u4) ? v : v4[u4];
+            }
+        }
+        float a1[C1];
+#pragma unroll
+        for (int c = 0; c < C1; ++c) {
+            float acc = s_b1[c];
+#pragma unroll
+            for (int u4 = 0; u4 < 4; ++u4) acc = fmaf(s_w1[c][u4], v4[u4], acc);
+            a1[c] = fmaxf(acc, 0.0f);
+        }
+        // ---- conv 2: window q's partial sums meet through the shuffles; lane q keeps channels
+        //      16q .. 16q + 15 ----
+#pragma unroll 2
+        for (int o = 0; o < C2; ++o) {
+            const float4 *w = &s_w2[q * W2Q + o * (C1 / 4)];
+            float acc = 0.0f;
+#pragma unroll
+            for (int c4 = 0; c4 < C1 / 4; ++c4) {
+                const float4 wv = w[c4];
+                acc = fmaf(wv.x, a1[4 * c4], acc);
+                acc = fmaf(wv.y, a1[4 * c4 + 1], acc);
+                acc = fmaf(wv.z, a1[4 * c4 + 2], acc);
+                acc = fmaf(wv.w, a1[4 * c4 + 3], acc);
+            }
+            const float a2 = fmaxf(s_b2[o] + quad_sum(acc), 0.0f);
+            if (q == (o >> 4)) s_dl[wave][o][it] = a2;
+        }
+        {   // minus the base window's activations of these 16 channels
+            const float4 *ab = reinterpret_cast<const float4 *>(p.ws.a2map + (((size_t)k * p.HW + ctr) * p.P + Q) * C2 + 16 * q);
+            float4 bv[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) bv[i] = ab[i];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                s_dl[wave][16 * q + 4 * i + 0][it] -= bv[i].x;
+                s_dl[wave][16 * q + 4 * i + 1][it] -= bv[i].y;
+                s_dl[wave][16 * q + 4 * i + 2][it] -= bv[i].z;
+                s_dl[wave][16 * q + 4 * i + 3][it] -= bv[i].w;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // ---- Linear 1 on the position: features 16j + 4q .. + 3 ----
+        float a[32];
+#pragma unroll
+        for (int i = 0; i < 32; ++i) a[i] = 0.0f;
+#pragma unroll 4
+        for (int o = 0; o < C2; ++o) {
+            const float dl = s_dl[wave][o][it];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float4 w = s_wl[o * (HID / 4) + 4 * j + q];
+                a[4 * j + 0] = fmaf(dl, w.x, a[4 * j + 0]);
+                a[4 * j + 1] = fmaf(dl, w.y, a[4 * j + 1]);
+                a[4 * j + 2] = fmaf(dl, w.z, a[4 * j + 2]);
+                a[4 * j + 3] = fmaf(dl, w.w, a[4 * j + 3]);
+            }
+        }
+        if (ok) {
+            float4 *z = reinterpret_cast<float4 *>(p.ws.rare_z + ((size_t)k * p.E * RSW + item) * HID);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) z[4 * j + q] = make_float4(a[4 * j], a[4 * j + 1], a[4 * j + 2], a[4 * j + 3]);
+        }
+    }
+}
+
 gw_status err(gw_status s, const std::string &msg) {
     gw_set_last_error(msg.c_str());
     return s;
@@ -1186,6 +1502,7 @@ CnnParams cnn_params(const gw_obs_source &src, const gw_cnn_actors *net, float *
     p.N = src.N;
     p.K = src.K;
     p.variant = src.variant;
+    p.PW = 0;
     for (int k = 0; k < MAXN; ++k) p.apples[k] = src.apples[k];
     const char *ab = std::getenv("GW_CNN_AB");
     p.ab = ab ? std::atoi(ab) : 0;
@@ -1496,6 +1813,156 @@ gw_status gw_cnn_act(void *env, const gw_cnn_actors *net, const float *ws, int t
     hipLaunchKernelGGL((act_kernel<2, 16, true, true>), dim3(per_agent, src.K), dim3(1024), 0, s, p);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return err(GW_ERR_HIP, std::string("gw_cnn_act: ") + hipGetErrorString(e));
+    return GW_OK;
+}
+
+int64_t gw_patch_cnn_workspace_floats(int32_t P, int32_t H, int32_t W, int32_t K, int64_t E) {
+    const int NQ = (P / 4) * (P / 4);
+    return wcnn_ws_floats(K, NQ, H * W, E);
+}
+
+}  // extern "C"
+
+namespace {
+gw_status check_patch_cnn(const gw_obs_source &src, int32_t P, const gw_cnn_actors *net, const char *who) {
+    const std::string w(who);
+    if (P < 4 || P > 16 || P % 4) return err(GW_ERR_ARG, w + ": P must be 4, 8, 12 or 16");
+    if (net->K != src.K) return err(GW_ERR_ARG, w + ": net K != env K");
+    if (net->H != P || net->W != P) return err(GW_ERR_ARG, w + ": net H, W != P");
+    if (src.H * src.W > 128 * 32) return err(GW_ERR_ARG, w + ": H*W must be <= 4096");
+    if (net->c1 != C1 || net->c2 != C2 || net->hidden != HID || net->n_actions != NA)
+        return err(GW_ERR_ARG, w + ": only channels 32-64, hidden 128 and 9 actions are fused");
+    if (!net->conv1_w || !net->conv1_b || !net->conv2_w || !net->conv2_b || !net->lin1_w || !net->lin1_b ||
+        !net->w2 || !net->b2 || !net->w3 || !net->b3)
+        return err(GW_ERR_ARG, w + ": null parameter");
+    return GW_OK;
+}
+CnnParams wcnn_params(const gw_obs_source &src, int32_t P, const gw_cnn_actors *net, float *ws) {
+    CnnParams p = cnn_params(src, net, ws);   // (its full-grid layout is replaced below)
+    p.PW = P;
+    p.Wq = P / 4;
+    p.P = p.Wq * p.Wq;
+    p.ws = wcnn_ws_layout(ws, src.K, p.P, p.HW, src.E);
+    return p;
+}
+}  // namespace
+
+extern "C" {
+
+gw_status gw_patch_cnn_prepare(void *env, int32_t P, const gw_cnn_actors *net, float *ws, void *stream) {
+    if (!env || !net || !ws) return err(GW_ERR_ARG, "gw_patch_cnn_prepare: null argument");
+    if (reinterpret_cast<uintptr_t>(ws) & 15u) return err(GW_ERR_ARG, "gw_patch_cnn_prepare: ws must be 16-byte aligned");
+    gw_obs_source src;
+    gw_status st = gw_obs_view(env, &src);
+    if (st != GW_OK) return st;
+    if ((st = check_patch_cnn(src, P, net, "gw_patch_cnn_prepare")) != GW_OK) return st;
+    const CnnParams p = wcnn_params(src, P, net, ws);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(cnn_prep_wlt, dim3(2048), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(wcnn_prep_base, dim3((p.HW + WCG - 1) / WCG, src.K), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(cnn_bucket_reset, dim3((src.K * p.P + 255) / 256), dim3(256), 0, s, p);
+    PrepParams pp;  // the layer-2/3 MFMA images (c1 unused)
+    pp.net = cnn_tail(net);
+    pp.HW = P * P;
+    pp.nslices = 0;
+    pp.ws = p.ws.mlp;
+    pp.base = src.base;
+    hipLaunchKernelGGL(prep_images, dim3(16, src.K), dim3(256), 0, s, pp);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return err(GW_ERR_HIP, std::string("gw_patch_cnn_prepare: ") + hipGetErrorString(e));
+    return GW_OK;
+}
+
+gw_status gw_patch_cnn_act(void *env, int32_t P, const gw_cnn_actors *net, const float *ws, int training, float tau,
+                           uint64_t seed, uint64_t counter, const float *uniform, const uint16_t *mask,
+                           int32_t *actions, float *probs, float *logits, void *stream) {
+    if (!env || !net || !ws || !actions || !probs) return err(GW_ERR_ARG, "gw_patch_cnn_act: null argument");
+    if (reinterpret_cast<uintptr_t>(ws) & 15u) return err(GW_ERR_ARG, "gw_patch_cnn_act: ws must be 16-byte aligned");
+    gw_obs_source src;
+    gw_status st = gw_obs_view(env, &src);
+    if (st != GW_OK) return st;
+    if ((st = check_patch_cnn(src, P, net, "gw_patch_cnn_act")) != GW_OK) return st;
+    if (!(tau > 0.0f)) return err(GW_ERR_ARG, "gw_patch_cnn_act: tau must be > 0");
+    const CnnParams cp = wcnn_params(src, P, net, const_cast<float *>(ws));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const dim3 lgrid((unsigned)((src.E + 255) / 256), src.K);
+    switch (src.N) {
+        case 1: hipLaunchKernelGGL(wcnn_l1_kernel<2>, lgrid, dim3(256), 0, s, cp); break;
+        case 2: hipLaunchKernelGGL(wcnn_l1_kernel<3>, lgrid, dim3(256), 0, s, cp); break;
+        case 3: hipLaunchKernelGGL(wcnn_l1_kernel<4>, lgrid, dim3(256), 0, s, cp); break;
+        case 4: hipLaunchKernelGGL(wcnn_l1_kernel<5>, lgrid, dim3(256), 0, s, cp); break;
+        case 5: hipLaunchKernelGGL(wcnn_l1_kernel<6>, lgrid, dim3(256), 0, s, cp); break;
+        case 6: hipLaunchKernelGGL(wcnn_l1_kernel<7>, lgrid, dim3(256), 0, s, cp); break;
+        case 7: hipLaunchKernelGGL(wcnn_l1_kernel<8>, lgrid, dim3(256), 0, s, cp); break;
+        case 8: hipLaunchKernelGGL(wcnn_l1_kernel<9>, lgrid, dim3(256), 0, s, cp); break;
+        default: return err(GW_ERR_ARG, "gw_patch_cnn_act: N out of range");
+    }
+    hipLaunchKernelGGL(cnn_rare_plan, dim3(1), dim3(1024), 0, s, cp);
+#define RARE(NP) hipLaunchKernelGGL(wcnn_rare_kernel<NP>, dim3(RARE_BLOCKS), dim3(64 * RARE_WAVES), 0, s, cp)
+    switch (src.N) {
+        case 1: RARE(2); break;
+        case 2: RARE(3); break;
+        case 3: RARE(4); break;
+        case 4: RARE(5); break;
+        case 5: RARE(6); break;
+        case 6: RARE(7); break;
+        case 7: RARE(8); break;
+        default: RARE(9); break;
+    }
+#undef RARE
+    hipLaunchKernelGGL(cnn_bucket_reset, dim3((src.K * cp.P + 255) / 256), dim3(256), 0, s, cp);
+    ActParams p;
+    p.net = cnn_tail(net);
+    p.c1 = cp.ws.mlp.c1;
+    p.w2img = cp.ws.mlp.w2;
+    p.w3img = cp.ws.mlp.w3;
+    p.w2bimg = cp.ws.mlp.w2b;
+    p.desc = src.desc;
+    p.base = src.base;
+    p.mask = mask;
+    p.uniform = uniform;
+    p.h1 = nullptr;
+    p.rare_z = cp.ws.rare_z;
+    p.rare_n = cp.ws.rare_n;
+    p.actions = actions;
+    p.probs = probs;
+    p.logits = logits;
+    p.E = src.E;
+    p.env_offset = src.env_offset;
+    p.N = src.N;
+    p.K = src.K;
+    p.HW = src.H * src.W;
+    p.W = src.W;
+    p.P = P;
+    p.in_dim = P * P;
+    p.tbl = cp.ws.table;
+    p.variant = src.variant;
+    p.training = training ? 1 : 0;
+    p.tau = tau;
+    p.key0 = (uint32_t)seed;
+    p.key1 = (uint32_t)(seed >> 32);
+    p.ctr0 = (uint32_t)counter;
+    p.ctr1 = (uint32_t)(counter >> 32);
+    for (int k = 0; k < MAXN; ++k) p.apples[k] = src.apples[k];
+    p.ab = 0;
+    const int64_t tiles = (src.E + TILE - 1) / TILE;
+    p.tiles = (int)tiles;
+    const int64_t want = (tiles + 15) / 16;
+    const int per_agent = (int)std::max<int64_t>(1, std::min<int64_t>(want, std::max(1, 256 / src.K)));
+#define ACTW(NP) hipLaunchKernelGGL((act_kernel<NP, 16, true, true, true, RSW>), dim3(per_agent, src.K), dim3(1024), 0, s, p)
+    switch (src.N) {
+        case 1: ACTW(2); break;
+        case 2: ACTW(3); break;
+        case 3: ACTW(4); break;
+        case 4: ACTW(5); break;
+        case 5: ACTW(6); break;
+        case 6: ACTW(7); break;
+        case 7: ACTW(8); break;
+        default: ACTW(9); break;
+    }
+#undef ACTW
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return err(GW_ERR_HIP, std::string("gw_patch_cnn_act: ") + hipGetErrorString(e));
     return GW_OK;
 }
 

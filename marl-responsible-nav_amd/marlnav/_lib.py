@@ -173,7 +173,8 @@ EXPORTS = ["gw_create", "gw_reset", "gw_step", "gw_state_view", "gw_copy_state",
            "gw_replay_gather", "gw_affine_relu_fwd", "gw_affine_relu_bwd",
            "gw_soft_update2", "gw_td_target", "gw_mean_loss_fwd", "gw_mean_loss_bwd",
            "gw_eval_accum", "gw_profile_spans", "gw_patch_actor_workspace_floats", "gw_patch_actor_prepare",
-           "gw_patch_actor_act", "gw_maddpg_workspace_floats", "gw_maddpg_critic_grads", "gw_maddpg_actor_grads"]
+           "gw_patch_actor_act", "gw_patch_cnn_workspace_floats", "gw_patch_cnn_prepare", "gw_patch_cnn_act",
+           "gw_maddpg_workspace_floats", "gw_maddpg_critic_grads", "gw_maddpg_actor_grads"]
 
 
 class GwObsSource(C.Structure):
@@ -289,6 +290,13 @@ def _declare(L):
     L.gw_patch_actor_act.argtypes = [p, C.c_int32, C.POINTER(GwMlpActors), p, C.c_int, C.c_float, C.c_uint64,
                                      C.c_uint64, p, p, p, p, p, p]
     L.gw_patch_actor_act.restype = C.c_int
+    L.gw_patch_cnn_workspace_floats.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int64]
+    L.gw_patch_cnn_workspace_floats.restype = C.c_int64
+    L.gw_patch_cnn_prepare.argtypes = [p, C.c_int32, C.POINTER(GwCnnActors), p, p]
+    L.gw_patch_cnn_prepare.restype = C.c_int
+    L.gw_patch_cnn_act.argtypes = [p, C.c_int32, C.POINTER(GwCnnActors), p, C.c_int, C.c_float, C.c_uint64,
+                                   C.c_uint64, p, p, p, p, p, p]
+    L.gw_patch_cnn_act.restype = C.c_int
     L.gw_actor_workspace_floats.argtypes = [C.c_int32, C.c_int32]
     L.gw_actor_workspace_floats.restype = C.c_int64
     L.gw_actor_prepare.argtypes = [p, C.POINTER(GwMlpActors), p, p]

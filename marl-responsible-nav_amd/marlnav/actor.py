@@ -405,10 +405,13 @@ class MultiAgentActors(nn.Module):
     def fusable(self, env, patch: int = 0) -> bool:
         """The fused HIP get_action covers (gw_actor_act, include/actor_ops.h) the stacked f32 MLP
         with two 128-wide hidden layers and (gw_cnn_act) the configs/cnn.yaml CNN head, over a
-        VecGridEnv's own observations; patch = P > 0: the MLP over each agent's P x P window
-        (gw_patch_actor_act)."""
+        VecGridEnv's own observations; patch = P > 0: the MLP (gw_patch_actor_act) or the CNN head
+        (gw_patch_cnn_act) over each agent's P x P window."""
         if self.dtype != torch.float32 or self.K != env.K:
             return False
+        if patch and self.arch == "cnn":  # gw_patch_cnn_act
+            return ((self.H, self.W) == (patch, patch) and patch in (4, 8, 12, 16) and env.H * env.W <= 4096
+                    and all(n.fusable() for n in self.nets))
         if patch:
             net = getattr(self, "net", None)
             return (self.arch == "mlp" and (self.H, self.W) == (patch, patch) and env.H * env.W <= 4096
@@ -446,7 +449,7 @@ class MultiAgentActors(nn.Module):
         from . import _lib
         if self.arch == "cnn":
             return self._act_env_cnn(env, mask, training, tau, seed, counter, uniform, actions_out, probs_out,
-                                     logits_out)
+                                     logits_out, int(patch))
         net, K, E, dev = self.net, self.K, env.E, env.device
         patch = int(patch)
         st = self._fast
@@ -506,21 +509,25 @@ class MultiAgentActors(nn.Module):
             _lib.check(st["lib"].gw_actor_act(env.handle, *args), "gw_actor_act")
         return actions_out, probs_out
 
-    def _act_env_cnn(self, env, mask, training, tau, seed, counter, uniform, actions_out, probs_out, logits_out):
+    def _act_env_cnn(self, env, mask, training, tau, seed, counter, uniform, actions_out, probs_out, logits_out,
+                     patch=0):
         """act_env for the CNN head: gw_cnn_act (layer 1 from the obs descriptors through the
         per-position delta table, include/actor_ops.h), then the same fused layers 2-3 + noise +
-        softmax + mask + argmax as the MLP path."""
+        softmax + mask + argmax as the MLP path.  patch = P: the head built for P x P inputs on each
+        agent's window (gw_patch_cnn_act: per-centre tables + the recomputed positions)."""
         from . import _lib
         K, E, dev = self.K, env.E, env.device
         st = self._fast
-        if st is None or st["env"] is not env:
-            if not self.fusable(env):
+        if st is None or st["env"] is not env or st.get("patch", 0) != patch:
+            if not self.fusable(env, patch):
                 raise _lib.GwError("act_env: CNN actor not fusable (needs conv 32-64 k2 s2, hidden 128-128, "
-                                   "9 actions, f32, the env's H x W, multiples of 4)")
+                                   "9 actions, f32, the env's H x W, multiples of 4; or patch=P in 4, 8, 12, 16 "
+                                   "with a P x P head)")
             lib = _lib.load()
-            ws_n = int(lib.gw_cnn_workspace_floats(env.H, env.W, K, E))
+            ws_n = int(lib.gw_patch_cnn_workspace_floats(patch, env.H, env.W, K, E) if patch
+                       else lib.gw_cnn_workspace_floats(env.H, env.W, K, E))
             st = self._fast = dict(env=env, lib=lib, ws=torch.empty(ws_n, dtype=torch.float32, device=dev), key=None,
-                                   spec=None, packed=None)
+                                   spec=None, packed=None, patch=patch)
         params = [p for n in self.nets for p in n.parameters()]
         key = (tuple(p._version for p in params), tuple(p.data_ptr() for p in params), getattr(self, "_epoch", 0))
         if key != st["key"]:
@@ -537,11 +544,16 @@ class MultiAgentActors(nn.Module):
                     w3=torch.stack([n.mlp[4].weight.t() for n in self.nets]).contiguous(),
                     b3=torch.stack([n.mlp[4].bias for n in self.nets]).contiguous())
             st["packed"] = pk
-            st["spec"] = _lib.GwCnnActors(K, env.H, env.W, 32, 64, 128, N_ACTIONS,
+            st["spec"] = _lib.GwCnnActors(K, self.H, self.W, 32, 64, 128, N_ACTIONS,
                                           *[pk[n].data_ptr() for n in _lib.CNN_PARAM_FIELDS])
             with torch.cuda.device(dev):
-                _lib.check(st["lib"].gw_cnn_prepare(env.handle, C.byref(st["spec"]), st["ws"].data_ptr(),
-                                                    torch.cuda.current_stream(dev).cuda_stream), "gw_cnn_prepare")
+                stream = torch.cuda.current_stream(dev).cuda_stream
+                if patch:
+                    _lib.check(st["lib"].gw_patch_cnn_prepare(env.handle, patch, C.byref(st["spec"]),
+                                                              st["ws"].data_ptr(), stream), "gw_patch_cnn_prepare")
+                else:
+                    _lib.check(st["lib"].gw_cnn_prepare(env.handle, C.byref(st["spec"]), st["ws"].data_ptr(), stream),
+                               "gw_cnn_prepare")
             st["key"] = key
         if actions_out is None:
             actions_out = torch.empty((E, K), dtype=torch.int32, device=dev)
@@ -555,10 +567,13 @@ class MultiAgentActors(nn.Module):
             raise ValueError("act_env: uniform must be float32 [K, E, 9]")
         if mask is not None and not (mask.shape == (E, K) and mask.element_size() == 2 and mask.is_contiguous()):
             raise ValueError("act_env: mask must be a contiguous 16-bit [E, K] tensor")
-        _lib.check(st["lib"].gw_cnn_act(env.handle, C.byref(st["spec"]), st["ws"].data_ptr(), int(bool(training)),
-                                        float(tau), int(seed) & 0xFFFFFFFFFFFFFFFF, int(counter) & 0xFFFFFFFFFFFFFFFF,
-                                        uniform.contiguous().data_ptr() if uniform is not None else None,
-                                        mask.data_ptr() if mask is not None else None, actions_out.data_ptr(),
-                                        probs_out.data_ptr(), logits_out.data_ptr() if logits_out is not None else None,
-                                        torch.cuda.current_stream(dev).cuda_stream), "gw_cnn_act")
+        args = (C.byref(st["spec"]), st["ws"].data_ptr(), int(bool(training)), float(tau),
+                int(seed) & 0xFFFFFFFFFFFFFFFF, int(counter) & 0xFFFFFFFFFFFFFFFF,
+                uniform.contiguous().data_ptr() if uniform is not None else None,
+                mask.data_ptr() if mask is not None else None, actions_out.data_ptr(), probs_out.data_ptr(),
+                logits_out.data_ptr() if logits_out is not None else None, torch.cuda.current_stream(dev).cuda_stream)
+        if patch:
+            _lib.check(st["lib"].gw_patch_cnn_act(env.handle, patch, *args), "gw_patch_cnn_act")
+        else:
+            _lib.check(st["lib"].gw_cnn_act(env.handle, *args), "gw_cnn_act")
         return actions_out, probs_out
