@@ -731,7 +731,7 @@ struct CnnParams {
     int N, K, H, W, P, Wq, HW, variant;
     int PW;                   // window side (gw_patch_cnn_*: P = (PW / 4)^2 positions), 0 = the whole grid
     int ab;                   // GW_CNN_AB (measurement only): bit 0 skip the recomputed positions,
-                              // bit 1 skip the table rows
+                              // bit 1 skip the table rows; windows: bit 2 list no positions
     int apples[MAXN];
 };
 
@@ -1150,8 +1150,9 @@ __global__ void __launch_bounds__(256) cnn_bucket_reset(CnnParams p) {
 // patched cells.  gw_patch_cnn_prepare tabulates, per (agent, centre): a2b = conv-2 activations of
 // B_c at every window position Q, and tbl = b + Linear-1(a2b).  Per step, wcnn_l1_kernel lists the
 // positions where the actual window differs from B_c (a patched cell inside the window other than
-// the centre holding vo_k) as bucket items (env, slot) keyed (agent, Q); cnn_rare_plan / the
-// persistent wcnn_rare_kernel recompute each item's position and write Wl[:, Q] . (a2 - a2b);
+// the centre holding vo_k); wcnn_plan / wcnn_scatter file them as items (env, slot) into buckets
+// keyed (agent, Q) in env order (a scan of per-block counts: no atomics); the persistent
+// wcnn_rare_kernel recomputes each item's position and writes Wl[:, Q] . (a2 - a2b);
 // act_kernel<H1, PW> sums tbl[centre] + those terms (slot order) and runs layers 2-3.
 constexpr int RSW = MAXN + 1;   // recomputed positions per (env, agent): <= N + 1 patched cells
 constexpr int WCG = 8;          // centres per wcnn_prep_base block
@@ -1172,8 +1173,25 @@ inline CnnWs wcnn_ws_layout(float *base, int K, int NQ, int HW, int64_t E) {
     w.unit_off = reinterpret_cast<int *>(f);
     return w;
 }
+// wcnn_l1_kernel's outputs for the atomic-free bucket fill (after unit_off):
+//   qmask [K][E] positions to recompute, cnt / off [K NQ][nblk] items per (bucket, l1 block) and
+//   their offsets in the bucket (nblk = ceil(E / 256))
+struct WcnnLists {
+    int *qmask, *cnt, *off;
+    int nblk;
+};
+inline WcnnLists wcnn_lists(const CnnWs &w, int K, int NQ, int64_t E) {
+    WcnnLists l;
+    l.nblk = (int)((E + 255) / 256);
+    l.qmask = w.unit_off + K * NQ + 1;
+    l.cnt = l.qmask + (int64_t)K * E;
+    l.off = l.cnt + (int64_t)K * NQ * l.nblk;
+    return l;
+}
 inline int64_t wcnn_ws_floats(int K, int NQ, int HW, int64_t E) {
-    return (int64_t)(wcnn_ws_layout(nullptr, K, NQ, HW, E).unit_off - (int *)nullptr) + (int64_t)K * NQ + 1;
+    const CnnWs w = wcnn_ws_layout(nullptr, K, NQ, HW, E);
+    const WcnnLists l = wcnn_lists(w, K, NQ, E);
+    return (int64_t)(l.off - (int *)nullptr) + (int64_t)K * NQ * l.nblk;
 }
 // the agent's own obs value in a non-reset step off its apple (agent_value(false, k, k, false))
 __device__ __forceinline__ float own_value(int k, int variant) { return variant == 1 ? (float)(k + 1) : 1.0f; }
@@ -1249,20 +1267,21 @@ __global__ void __launch_bounds__(256) wcnn_prep_base(CnnParams p) {
     }
 }
 
-// one thread per (env, agent): the positions where the window differs from its base window, in
-// ascending order, as bucket items (e RSW + slot); rare_n = their count
+// one thread per (env, agent): the positions where the window differs from its base window as a
+// mask (slot = rank of the position in it; rare_n = their count) and the items per (position,
+// block); wcnn_plan scans the counts, wcnn_scatter fills the buckets
 template <int NP>
-__global__ void __launch_bounds__(256) wcnn_l1_kernel(CnnParams p) {
+__global__ void __launch_bounds__(256) wcnn_l1_kernel(CnnParams p, WcnnLists lists) {
     __shared__ uint32_t s_road[128];
+    __shared__ int s_cnt[4][WNQ];
     const int k = blockIdx.y, tid = threadIdx.x;
     const int64_t e = (int64_t)blockIdx.x * 256 + tid;
     const bool valid = e < p.E;
     if (tid < 128) s_road[tid] = p.ws.road[tid];
     __syncthreads();
-    if (!valid) return;
     auto map_at = [&](int c) { return ((s_road[c >> 5] >> (c & 31)) & 1u) ? 0.0f : -1.0f; };
-    const uint4 cells = *reinterpret_cast<const uint4 *>(p.desc + e * NDESC);
-    const uint32_t flags = p.desc[e * NDESC + 4];
+    const uint4 cells = valid ? *reinterpret_cast<const uint4 *>(p.desc + e * NDESC) : make_uint4(0, 0, 0, 0);
+    const uint32_t flags = valid ? p.desc[e * NDESC + 4] : 0u;
     int pc[NP];
     float pv[NP];
     {
@@ -1300,15 +1319,79 @@ __global__ void __launch_bounds__(256) wcnn_l1_kernel(CnnParams p) {
         qmask |= 1u << ((wr >> 2) * p.Wq + (wc >> 2));
     }
     if (!ctr_set && map_at(ctr) != vo) qmask |= 1u << ((half >> 2) * p.Wq + (half >> 2));
-    int ns = 0;
-    while (qmask) {
-        const int Q = __builtin_ctz(qmask);
-        qmask &= qmask - 1;
-        const int idx = atomicAdd(p.ws.bucket_n + k * p.P + Q, 1);
-        p.ws.bucket[((size_t)k * p.P + Q) * p.E + idx] = (int)(e * RSW + ns);
-        ++ns;
+    if (!valid || (p.ab & 4)) qmask = 0;  // (bit 2, measurement only: decode, list nothing)
+    if (valid) {
+        p.ws.rare_n[(size_t)k * p.E + e] = __popc(qmask);
+        lists.qmask[(size_t)k * p.E + e] = (int)qmask;
     }
-    p.ws.rare_n[(size_t)k * p.E + e] = ns;
+    // items per (position, block): the waves' ballot counts summed in LDS (no global atomics:
+    // nearly every item shares the centre's position, and same-address atomics serialise)
+    const int wave = tid >> 6, lane = tid & 63;
+    for (int Q = 0; Q < p.P; ++Q) {
+        const uint64_t b = __ballot((qmask >> Q) & 1u);
+        if (lane == 0) s_cnt[wave][Q] = __popcll(b);
+    }
+    __syncthreads();
+    if (tid < p.P)
+        lists.cnt[((size_t)k * p.P + tid) * lists.nblk + blockIdx.x] = s_cnt[0][tid] + s_cnt[1][tid] + s_cnt[2][tid] + s_cnt[3][tid];
+}
+
+// one block, 16 waves: per bucket (agent, position), the offsets of the l1 blocks' items (a wave
+// scan over the blocks in order), the bucket sizes and cnn_rare_plan's unit offsets
+__global__ void __launch_bounds__(1024) wcnn_plan(CnnParams p, WcnnLists lists) {
+    __shared__ int s_units[1024];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, nb = p.K * p.P;
+    for (int b = wave; b < nb; b += 16) {
+        int run = 0;
+        for (int c0 = 0; c0 < lists.nblk; c0 += 64) {
+            const int i = c0 + lane;
+            const int v = i < lists.nblk ? lists.cnt[(size_t)b * lists.nblk + i] : 0;
+            int incl = v;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const int o = __shfl_up(incl, d, 64);
+                if (lane >= d) incl += o;
+            }
+            if (i < lists.nblk) lists.off[(size_t)b * lists.nblk + i] = run + incl - v;
+            run += __shfl(incl, 63, 64);
+        }
+        if (lane == 0) {
+            p.ws.bucket_n[b] = run;
+            s_units[b] = (run + RARE_ITEMS - 1) / RARE_ITEMS;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {  // nb <= 8 * 16 buckets
+        int u = 0;
+        for (int b = 0; b < nb; ++b) {
+            p.ws.unit_off[b] = u;
+            u += s_units[b];
+        }
+        p.ws.unit_off[nb] = u;
+    }
+}
+
+// fills the buckets in (block, wave, lane) order: item (e RSW + slot), slot = the position's rank
+// in the (env, agent)'s mask
+__global__ void __launch_bounds__(256) wcnn_scatter(CnnParams p, WcnnLists lists) {
+    __shared__ int s_cnt[4][WNQ];
+    const int k = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int64_t e = (int64_t)blockIdx.x * 256 + tid;
+    const uint32_t qmask = e < p.E ? (uint32_t)lists.qmask[(size_t)k * p.E + e] : 0u;
+    const uint64_t below = (1ull << lane) - 1;
+    for (int Q = 0; Q < p.P; ++Q) {
+        const uint64_t b = __ballot((qmask >> Q) & 1u);
+        if (lane == 0) s_cnt[wave][Q] = __popcll(b);
+    }
+    __syncthreads();
+    for (int Q = 0; Q < p.P; ++Q) {
+        const bool has = (qmask >> Q) & 1u;
+        const uint64_t b = __ballot(has);
+        if (!has) continue;
+        int pos = lists.off[((size_t)k * p.P + Q) * lists.nblk + blockIdx.x] + __popcll(b & below);
+        for (int w = 0; w < wave; ++w) pos += s_cnt[w][Q];
+        p.ws.bucket[((size_t)k * p.P + Q) * p.E + pos] = (int)(e * RSW + __popc(qmask & ((1u << Q) - 1u)));
+    }
 }
 
 // cnn_rare_kernel over window positions: per unit (agent k, position Q) the Linear-1 block in LDS;
@@ -1860,7 +1943,6 @@ gw_status gw_patch_cnn_prepare(void *env, int32_t P, const gw_cnn_actors *net, f
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(cnn_prep_wlt, dim3(2048), dim3(256), 0, s, p);
     hipLaunchKernelGGL(wcnn_prep_base, dim3((p.HW + WCG - 1) / WCG, src.K), dim3(256), 0, s, p);
-    hipLaunchKernelGGL(cnn_bucket_reset, dim3((src.K * p.P + 255) / 256), dim3(256), 0, s, p);
     PrepParams pp;  // the layer-2/3 MFMA images (c1 unused)
     pp.net = cnn_tail(net);
     pp.HW = P * P;
@@ -1885,19 +1967,21 @@ gw_status gw_patch_cnn_act(void *env, int32_t P, const gw_cnn_actors *net, const
     if (!(tau > 0.0f)) return err(GW_ERR_ARG, "gw_patch_cnn_act: tau must be > 0");
     const CnnParams cp = wcnn_params(src, P, net, const_cast<float *>(ws));
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const dim3 lgrid((unsigned)((src.E + 255) / 256), src.K);
+    const WcnnLists lists = wcnn_lists(cp.ws, src.K, cp.P, src.E);
+    const dim3 lgrid((unsigned)lists.nblk, src.K);
     switch (src.N) {
-        case 1: hipLaunchKernelGGL(wcnn_l1_kernel<2>, lgrid, dim3(256), 0, s, cp); break;
-        case 2: hipLaunchKernelGGL(wcnn_l1_kernel<3>, lgrid, dim3(256), 0, s, cp); break;
-        case 3: hipLaunchKernelGGL(wcnn_l1_kernel<4>, lgrid, dim3(256), 0, s, cp); break;
-        case 4: hipLaunchKernelGGL(wcnn_l1_kernel<5>, lgrid, dim3(256), 0, s, cp); break;
-        case 5: hipLaunchKernelGGL(wcnn_l1_kernel<6>, lgrid, dim3(256), 0, s, cp); break;
-        case 6: hipLaunchKernelGGL(wcnn_l1_kernel<7>, lgrid, dim3(256), 0, s, cp); break;
-        case 7: hipLaunchKernelGGL(wcnn_l1_kernel<8>, lgrid, dim3(256), 0, s, cp); break;
-        case 8: hipLaunchKernelGGL(wcnn_l1_kernel<9>, lgrid, dim3(256), 0, s, cp); break;
+        case 1: hipLaunchKernelGGL(wcnn_l1_kernel<2>, lgrid, dim3(256), 0, s, cp, lists); break;
+        case 2: hipLaunchKernelGGL(wcnn_l1_kernel<3>, lgrid, dim3(256), 0, s, cp, lists); break;
+        case 3: hipLaunchKernelGGL(wcnn_l1_kernel<4>, lgrid, dim3(256), 0, s, cp, lists); break;
+        case 4: hipLaunchKernelGGL(wcnn_l1_kernel<5>, lgrid, dim3(256), 0, s, cp, lists); break;
+        case 5: hipLaunchKernelGGL(wcnn_l1_kernel<6>, lgrid, dim3(256), 0, s, cp, lists); break;
+        case 6: hipLaunchKernelGGL(wcnn_l1_kernel<7>, lgrid, dim3(256), 0, s, cp, lists); break;
+        case 7: hipLaunchKernelGGL(wcnn_l1_kernel<8>, lgrid, dim3(256), 0, s, cp, lists); break;
+        case 8: hipLaunchKernelGGL(wcnn_l1_kernel<9>, lgrid, dim3(256), 0, s, cp, lists); break;
         default: return err(GW_ERR_ARG, "gw_patch_cnn_act: N out of range");
     }
-    hipLaunchKernelGGL(cnn_rare_plan, dim3(1), dim3(1024), 0, s, cp);
+    hipLaunchKernelGGL(wcnn_plan, dim3(1), dim3(1024), 0, s, cp, lists);
+    hipLaunchKernelGGL(wcnn_scatter, lgrid, dim3(256), 0, s, cp, lists);
 #define RARE(NP) hipLaunchKernelGGL(wcnn_rare_kernel<NP>, dim3(RARE_BLOCKS), dim3(64 * RARE_WAVES), 0, s, cp)
     switch (src.N) {
         case 1: RARE(2); break;
@@ -1910,7 +1994,6 @@ gw_status gw_patch_cnn_act(void *env, int32_t P, const gw_cnn_actors *net, const
         default: RARE(9); break;
     }
 #undef RARE
-    hipLaunchKernelGGL(cnn_bucket_reset, dim3((src.K * cp.P + 255) / 256), dim3(256), 0, s, cp);
     ActParams p;
     p.net = cnn_tail(net);
     p.c1 = cp.ws.mlp.c1;
