@@ -683,7 +683,7 @@ struct CnnWs {
     float *h1;        // [K][E][128]      z_map + table rows
     float *rare_z;    // [K][E][RS][128]  their Linear-1 contributions
     int *rare_n;      // [K][E]           recomputed positions per (env, agent)
-    int *bucket_n;    // [K][P]           items per position (0 between calls)
+    int *bucket_n;    // [K][P]           items per position (bucket_scan)
     int *bucket;      // [K][P][E]        items (e RS + slot) per position
     int *unit_off;    // [K P + 1]        cnn_rare_plan's unit offsets
 };
@@ -709,8 +709,30 @@ inline CnnWs cnn_ws_layout(float *base, int K, int P, int64_t E) {
     w.unit_off = reinterpret_cast<int *>(f);  f += (int64_t)K * P + 1;
     return w;
 }
+// The layer-1 kernels' outputs for filling the buckets without global atomics (after unit_off):
+//   item [K][E]      the (env, agent)'s positions to recompute (grid: up to RS position bytes in
+//                    slot order; windows: a position mask, slot = rank in the mask)
+//   cnt / off [nb][nblk]  items per (bucket, layer-1 block) and their offsets in the bucket
+// bucket_scan turns the counts into offsets and bucket sizes, the scatter kernels fill the buckets.
+struct Lists {
+    int *item, *cnt, *off;
+    int nblk;
+};
+inline Lists lists_at(int *unit_off, int nb, int K, int64_t E, int per_block) {
+    Lists l;
+    l.nblk = (int)((E + per_block - 1) / per_block);
+    l.item = unit_off + nb + 1;
+    l.cnt = l.item + (int64_t)K * E;
+    l.off = l.cnt + (int64_t)nb * l.nblk;
+    return l;
+}
+inline int64_t lists_floats(int nb, int K, int64_t E, int per_block) {
+    return (int64_t)K * E + 2 * (int64_t)nb * ((E + per_block - 1) / per_block);
+}
+constexpr int L1_ENVS = TILE * L1_WAVES;  // envs per cnn_l1_kernel block
 inline int64_t cnn_ws_floats(int K, int P, int64_t E) {
-    return (int64_t)(cnn_ws_layout(nullptr, K, P, E).unit_off - (int *)nullptr) + (int64_t)K * P + 1;
+    return (int64_t)(cnn_ws_layout(nullptr, K, P, E).unit_off - (int *)nullptr) + (int64_t)K * P + 1 +
+           lists_floats(K * P, K, E, L1_ENVS);
 }
 // value of a patched obs cell -> table column: 0.5 (reset agent), 9.5 (reset agent on its apple),
 // 1 .. 17 (agents, relabelled or raw, apples, agents on apples); -1 = not tabulated
@@ -750,7 +772,6 @@ __global__ void __launch_bounds__(256) cnn_prep_wlt(CnnParams p) {
 __global__ void __launch_bounds__(128) cnn_prep_map(CnnParams p) {
     const int P = blockIdx.x, k = blockIdx.y, t = threadIdx.x;
     __shared__ float s_a1[4][C1];
-    if (t == 0) p.ws.bucket_n[k * p.P + P] = 0;
     if (P == 0) {  // this agent's window-major conv-2 weight; (agent 0) the road bitmask
         for (int i = t; i < 4 * C2 * C1; i += 128) {
             const int d = i / (C2 * C1), o = (i / C1) % C2, c = i % C1;
@@ -857,16 +878,18 @@ __global__ void __launch_bounds__(256) cnn_prep_table(CnnParams p) {
 
 
 // Layer 1 of the CNN head for every (env, agent): h1 = z_map + the changed positions' deltas.
-// cnn_l1_kernel sums the table rows of the positions with one patched cell into h1 and appends
-// each position with several to that (agent, position)'s bucket as an (env, slot) item;
-// cnn_rare_plan cuts the buckets into units of up to 16 x RARE_WAVES items; cnn_rare_kernel
+// cnn_l1_kernel sums the table rows of the positions with one patched cell into h1 and lists the
+// positions with several (slot order) with per-block counts; bucket_scan / cnn_scatter file them
+// as (env, slot) items into per-(agent, position) buckets (no global atomics); cnn_rare_plan cuts
+// the buckets into units of up to 16 x RARE_WAVES items; cnn_rare_kernel
 // (persistent) takes units with the position's Linear-1 block staged in LDS, recomputes each
 // item's position (conv 1, conv 2) and writes its 128-float contribution; act_kernel<H1> adds an
 // env's contributions (in slot order) to h1.  Every sum runs in a fixed order, so the result
 // does not depend on the order items entered a bucket.
 template <int NP>
-__global__ void __launch_bounds__(64 * L1_WAVES, 4) cnn_l1_kernel(CnnParams p) {
+__global__ void __launch_bounds__(64 * L1_WAVES, 4) cnn_l1_kernel(CnnParams p, Lists lists) {
     __shared__ uint32_t s_road[128];
+    __shared__ int s_hist[256];                 // items per position in this block
     __shared__ int s_rows[L1_WAVES][NP][64];   // the lanes' table rows
     const int k = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, el = lane & 15, q = lane >> 4;
     const int64_t e = ((int64_t)blockIdx.x * L1_WAVES + wave) * TILE + el;
@@ -878,6 +901,7 @@ __global__ void __launch_bounds__(64 * L1_WAVES, 4) cnn_l1_kernel(CnnParams p) {
         flags = p.desc[e * NDESC + 4];
     }
     if (tid < 128) s_road[tid] = p.ws.road[tid];
+    if (tid < 256) s_hist[tid] = 0;
     __syncthreads();
     auto map_at = [&](int c) { return ((s_road[c >> 5] >> (c & 31)) & 1u) ? 0.0f : -1.0f; };
     // ---- the (env, agent)'s patched cells (act_kernel's decoding) ----
@@ -967,9 +991,11 @@ __global__ void __launch_bounds__(64 * L1_WAVES, 4) cnn_l1_kernel(CnnParams p) {
             for (int j = 0; j < 8; ++j) h[4 * j + q] = make_float4(a[4 * j], a[4 * j + 1], a[4 * j + 2], a[4 * j + 3]);
         }
     }
-    // ---- positions with several patched cells: (env, slot) into the position's bucket; the
-    //      slot's contribution is computed by cnn_rare_kernel ----
+    // ---- positions with several patched cells: listed per (env, agent) in slot order and
+    //      counted per position (cnn_scatter files them into the buckets, cnn_rare_kernel
+    //      computes their contributions) ----
     int ns = 0;
+    uint32_t rp = 0;
     while (rare) {
         const int i0 = __builtin_ctz(rare);
         rare &= rare - 1;
@@ -977,13 +1003,37 @@ __global__ void __launch_bounds__(64 * L1_WAVES, 4) cnn_l1_kernel(CnnParams p) {
 #pragma unroll
         for (int i = 0; i < NP; ++i)
             if (i == i0) P = pos[i];
-        if (q == 0 && valid) {
-            const int idx = atomicAdd(p.ws.bucket_n + k * p.P + P, 1);
-            p.ws.bucket[((size_t)k * p.P + P) * p.E + idx] = (int)(e * RS + ns);
-        }
+        if (q == 0 && valid) atomicAdd(&s_hist[P], 1);   // (LDS)
+        rp |= (uint32_t)P << (8 * ns);
         ++ns;
     }
-    if (q == 0 && valid) p.ws.rare_n[(size_t)k * p.E + e] = ns;
+    if (q == 0 && valid) {
+        p.ws.rare_n[(size_t)k * p.E + e] = ns;
+        lists.item[(size_t)k * p.E + e] = (int)rp;
+    }
+    __syncthreads();
+    for (int i = tid; i < p.P; i += 64 * L1_WAVES)
+        lists.cnt[((size_t)k * p.P + i) * lists.nblk + blockIdx.x] = s_hist[i];
+}
+
+// files the listed positions into the buckets: block = cnn_l1_kernel's block of envs; the rank
+// inside the block's share of a bucket comes from an LDS counter (the order inside a bucket does
+// not change any result: every item writes its own slot)
+__global__ void __launch_bounds__(L1_ENVS) cnn_scatter(CnnParams p, Lists lists) {
+    __shared__ int s_ctr[256];
+    const int k = blockIdx.y, tid = threadIdx.x;
+    const int64_t e = (int64_t)blockIdx.x * L1_ENVS + tid;
+    for (int i = tid; i < 256; i += L1_ENVS) s_ctr[i] = 0;
+    __syncthreads();
+    if (e >= p.E) return;
+    const int ns = p.ws.rare_n[(size_t)k * p.E + e];
+    const uint32_t rp = (uint32_t)lists.item[(size_t)k * p.E + e];
+    for (int sl = 0; sl < ns; ++sl) {
+        const int P = (rp >> (8 * sl)) & 255;
+        const int r = atomicAdd(&s_ctr[P], 1);
+        const size_t b = (size_t)k * p.P + P;
+        p.ws.bucket[b * p.E + lists.off[b * lists.nblk + blockIdx.x] + r] = (int)(e * RS + sl);
+    }
 }
 
 // Units of work over the buckets: bucket b (= k P_n + P) holds ceil(n_b / RARE_ITEMS) units;
@@ -1137,20 +1187,13 @@ __global__ void __launch_bounds__(64 * RARE_WAVES) cnn_rare_kernel(CnnParams p) 
     }
 }
 
-// the buckets are emptied for the next call once every split has read its count
-__global__ void __launch_bounds__(256) cnn_bucket_reset(CnnParams p) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i < p.K * p.P) p.ws.bucket_n[i] = 0;
-}
-
-
 // ---- the CNN head on P x P egocentric windows (gw_patch_cnn_*; include/actor_ops.h) ------------
 // The window of agent k centred on cell c differs from its BASE window B_c (the map under the
 // window, -1 outside the grid, and the agent's usual own value vo_k at the centre) only at the
 // patched cells.  gw_patch_cnn_prepare tabulates, per (agent, centre): a2b = conv-2 activations of
 // B_c at every window position Q, and tbl = b + Linear-1(a2b).  Per step, wcnn_l1_kernel lists the
 // positions where the actual window differs from B_c (a patched cell inside the window other than
-// the centre holding vo_k); wcnn_plan / wcnn_scatter file them as items (env, slot) into buckets
+// the centre holding vo_k); bucket_scan / wcnn_scatter file them as items (env, slot) into buckets
 // keyed (agent, Q) in env order (a scan of per-block counts: no atomics); the persistent
 // wcnn_rare_kernel recomputes each item's position and writes Wl[:, Q] . (a2 - a2b);
 // act_kernel<H1, PW> sums tbl[centre] + those terms (slot order) and runs layers 2-3.
@@ -1173,25 +1216,9 @@ inline CnnWs wcnn_ws_layout(float *base, int K, int NQ, int HW, int64_t E) {
     w.unit_off = reinterpret_cast<int *>(f);
     return w;
 }
-// wcnn_l1_kernel's outputs for the atomic-free bucket fill (after unit_off):
-//   qmask [K][E] positions to recompute, cnt / off [K NQ][nblk] items per (bucket, l1 block) and
-//   their offsets in the bucket (nblk = ceil(E / 256))
-struct WcnnLists {
-    int *qmask, *cnt, *off;
-    int nblk;
-};
-inline WcnnLists wcnn_lists(const CnnWs &w, int K, int NQ, int64_t E) {
-    WcnnLists l;
-    l.nblk = (int)((E + 255) / 256);
-    l.qmask = w.unit_off + K * NQ + 1;
-    l.cnt = l.qmask + (int64_t)K * E;
-    l.off = l.cnt + (int64_t)K * NQ * l.nblk;
-    return l;
-}
 inline int64_t wcnn_ws_floats(int K, int NQ, int HW, int64_t E) {
-    const CnnWs w = wcnn_ws_layout(nullptr, K, NQ, HW, E);
-    const WcnnLists l = wcnn_lists(w, K, NQ, E);
-    return (int64_t)(l.off - (int *)nullptr) + (int64_t)K * NQ * l.nblk;
+    return (int64_t)(wcnn_ws_layout(nullptr, K, NQ, HW, E).unit_off - (int *)nullptr) + (int64_t)K * NQ + 1 +
+           lists_floats(K * NQ, K, E, 256);
 }
 // the agent's own obs value in a non-reset step off its apple (agent_value(false, k, k, false))
 __device__ __forceinline__ float own_value(int k, int variant) { return variant == 1 ? (float)(k + 1) : 1.0f; }
@@ -1269,9 +1296,9 @@ __global__ void __launch_bounds__(256) wcnn_prep_base(CnnParams p) {
 
 // one thread per (env, agent): the positions where the window differs from its base window as a
 // mask (slot = rank of the position in it; rare_n = their count) and the items per (position,
-// block); wcnn_plan scans the counts, wcnn_scatter fills the buckets
+// block); bucket_scan scans the counts, wcnn_scatter fills the buckets
 template <int NP>
-__global__ void __launch_bounds__(256) wcnn_l1_kernel(CnnParams p, WcnnLists lists) {
+__global__ void __launch_bounds__(256) wcnn_l1_kernel(CnnParams p, Lists lists) {
     __shared__ uint32_t s_road[128];
     __shared__ int s_cnt[4][WNQ];
     const int k = blockIdx.y, tid = threadIdx.x;
@@ -1322,7 +1349,7 @@ __global__ void __launch_bounds__(256) wcnn_l1_kernel(CnnParams p, WcnnLists lis
     if (!valid || (p.ab & 4)) qmask = 0;  // (bit 2, measurement only: decode, list nothing)
     if (valid) {
         p.ws.rare_n[(size_t)k * p.E + e] = __popc(qmask);
-        lists.qmask[(size_t)k * p.E + e] = (int)qmask;
+        lists.item[(size_t)k * p.E + e] = (int)qmask;
     }
     // items per (position, block): the waves' ballot counts summed in LDS (no global atomics:
     // nearly every item shares the centre's position, and same-address atomics serialise)
@@ -1336,48 +1363,34 @@ __global__ void __launch_bounds__(256) wcnn_l1_kernel(CnnParams p, WcnnLists lis
         lists.cnt[((size_t)k * p.P + tid) * lists.nblk + blockIdx.x] = s_cnt[0][tid] + s_cnt[1][tid] + s_cnt[2][tid] + s_cnt[3][tid];
 }
 
-// one block, 16 waves: per bucket (agent, position), the offsets of the l1 blocks' items (a wave
-// scan over the blocks in order), the bucket sizes and cnn_rare_plan's unit offsets
-__global__ void __launch_bounds__(1024) wcnn_plan(CnnParams p, WcnnLists lists) {
-    __shared__ int s_units[1024];
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, nb = p.K * p.P;
-    for (int b = wave; b < nb; b += 16) {
-        int run = 0;
-        for (int c0 = 0; c0 < lists.nblk; c0 += 64) {
-            const int i = c0 + lane;
-            const int v = i < lists.nblk ? lists.cnt[(size_t)b * lists.nblk + i] : 0;
-            int incl = v;
+// one wave per bucket: the offsets of the layer-1 blocks' items in the bucket (a wave scan over
+// the blocks in order) and the bucket's size (cnn_rare_plan then cuts the buckets into units)
+__global__ void __launch_bounds__(1024) bucket_scan(CnnParams p, Lists lists) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, b = blockIdx.x * 16 + wave;
+    if (b >= p.K * p.P) return;
+    int run = 0;
+    for (int c0 = 0; c0 < lists.nblk; c0 += 64) {
+        const int i = c0 + lane;
+        const int v = i < lists.nblk ? lists.cnt[(size_t)b * lists.nblk + i] : 0;
+        int incl = v;
 #pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const int o = __shfl_up(incl, d, 64);
-                if (lane >= d) incl += o;
-            }
-            if (i < lists.nblk) lists.off[(size_t)b * lists.nblk + i] = run + incl - v;
-            run += __shfl(incl, 63, 64);
+        for (int d = 1; d < 64; d <<= 1) {
+            const int o = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += o;
         }
-        if (lane == 0) {
-            p.ws.bucket_n[b] = run;
-            s_units[b] = (run + RARE_ITEMS - 1) / RARE_ITEMS;
-        }
+        if (i < lists.nblk) lists.off[(size_t)b * lists.nblk + i] = run + incl - v;
+        run += __shfl(incl, 63, 64);
     }
-    __syncthreads();
-    if (tid == 0) {  // nb <= 8 * 16 buckets
-        int u = 0;
-        for (int b = 0; b < nb; ++b) {
-            p.ws.unit_off[b] = u;
-            u += s_units[b];
-        }
-        p.ws.unit_off[nb] = u;
-    }
+    if (lane == 0) p.ws.bucket_n[b] = run;
 }
 
 // fills the buckets in (block, wave, lane) order: item (e RSW + slot), slot = the position's rank
 // in the (env, agent)'s mask
-__global__ void __launch_bounds__(256) wcnn_scatter(CnnParams p, WcnnLists lists) {
+__global__ void __launch_bounds__(256) wcnn_scatter(CnnParams p, Lists lists) {
     __shared__ int s_cnt[4][WNQ];
     const int k = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int64_t e = (int64_t)blockIdx.x * 256 + tid;
-    const uint32_t qmask = e < p.E ? (uint32_t)lists.qmask[(size_t)k * p.E + e] : 0u;
+    const uint32_t qmask = e < p.E ? (uint32_t)lists.item[(size_t)k * p.E + e] : 0u;
     const uint64_t below = (1ull << lane) - 1;
     for (int Q = 0; Q < p.P; ++Q) {
         const uint64_t b = __ballot((qmask >> Q) & 1u);
@@ -1830,19 +1843,22 @@ gw_status gw_cnn_act(void *env, const gw_cnn_actors *net, const float *ws, int t
     const CnnParams cp = cnn_params(src, net, const_cast<float *>(ws));
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int64_t tiles = (src.E + TILE - 1) / TILE;
-    const dim3 lgrid((unsigned)((tiles + L1_WAVES - 1) / L1_WAVES), src.K);
+    const Lists lists = lists_at(cp.ws.unit_off, src.K * cp.P, src.K, src.E, L1_ENVS);
+    const dim3 lgrid((unsigned)lists.nblk, src.K);
     switch (src.N) {
-        case 1: hipLaunchKernelGGL(cnn_l1_kernel<2>, lgrid, dim3(64 * L1_WAVES), 0, s, cp); break;
-        case 2: hipLaunchKernelGGL(cnn_l1_kernel<3>, lgrid, dim3(64 * L1_WAVES), 0, s, cp); break;
-        case 3: hipLaunchKernelGGL(cnn_l1_kernel<4>, lgrid, dim3(64 * L1_WAVES), 0, s, cp); break;
-        case 4: hipLaunchKernelGGL(cnn_l1_kernel<5>, lgrid, dim3(64 * L1_WAVES), 0, s, cp); break;
-        case 5: hipLaunchKernelGGL(cnn_l1_kernel<6>, lgrid, dim3(64 * L1_WAVES), 0, s, cp); break;
-        case 6: hipLaunchKernelGGL(cnn_l1_kernel<7>, lgrid, dim3(64 * L1_WAVES), 0, s, cp); break;
-        case 7: hipLaunchKernelGGL(cnn_l1_kernel<8>, lgrid, dim3(64 * L1_WAVES), 0, s, cp); break;
-        case 8: hipLaunchKernelGGL(cnn_l1_kernel<9>, lgrid, dim3(64 * L1_WAVES), 0, s, cp); break;
+        case 1: hipLaunchKernelGGL(cnn_l1_kernel<2>, lgrid, dim3(64 * L1_WAVES), 0, s, cp, lists); break;
+        case 2: hipLaunchKernelGGL(cnn_l1_kernel<3>, lgrid, dim3(64 * L1_WAVES), 0, s, cp, lists); break;
+        case 3: hipLaunchKernelGGL(cnn_l1_kernel<4>, lgrid, dim3(64 * L1_WAVES), 0, s, cp, lists); break;
+        case 4: hipLaunchKernelGGL(cnn_l1_kernel<5>, lgrid, dim3(64 * L1_WAVES), 0, s, cp, lists); break;
+        case 5: hipLaunchKernelGGL(cnn_l1_kernel<6>, lgrid, dim3(64 * L1_WAVES), 0, s, cp, lists); break;
+        case 6: hipLaunchKernelGGL(cnn_l1_kernel<7>, lgrid, dim3(64 * L1_WAVES), 0, s, cp, lists); break;
+        case 7: hipLaunchKernelGGL(cnn_l1_kernel<8>, lgrid, dim3(64 * L1_WAVES), 0, s, cp, lists); break;
+        case 8: hipLaunchKernelGGL(cnn_l1_kernel<9>, lgrid, dim3(64 * L1_WAVES), 0, s, cp, lists); break;
         default: return err(GW_ERR_ARG, "gw_cnn_act: N out of range");
     }
+    hipLaunchKernelGGL(bucket_scan, dim3((src.K * cp.P + 15) / 16), dim3(1024), 0, s, cp, lists);
     hipLaunchKernelGGL(cnn_rare_plan, dim3(1), dim3(1024), 0, s, cp);
+    hipLaunchKernelGGL(cnn_scatter, lgrid, dim3(L1_ENVS), 0, s, cp, lists);
 #define RARE(NP) hipLaunchKernelGGL(cnn_rare_kernel<NP>, dim3(RARE_BLOCKS), dim3(64 * RARE_WAVES), 0, s, cp)
     switch (src.N) {
         case 1: RARE(2); break;
@@ -1855,7 +1871,6 @@ gw_status gw_cnn_act(void *env, const gw_cnn_actors *net, const float *ws, int t
         default: RARE(9); break;
     }
 #undef RARE
-    hipLaunchKernelGGL(cnn_bucket_reset, dim3((src.K * cp.P + 255) / 256), dim3(256), 0, s, cp);
     ActParams p;
     p.net = cnn_tail(net);
     p.c1 = cp.ws.mlp.c1;
@@ -1967,7 +1982,7 @@ gw_status gw_patch_cnn_act(void *env, int32_t P, const gw_cnn_actors *net, const
     if (!(tau > 0.0f)) return err(GW_ERR_ARG, "gw_patch_cnn_act: tau must be > 0");
     const CnnParams cp = wcnn_params(src, P, net, const_cast<float *>(ws));
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const WcnnLists lists = wcnn_lists(cp.ws, src.K, cp.P, src.E);
+    const Lists lists = lists_at(cp.ws.unit_off, src.K * cp.P, src.K, src.E, 256);
     const dim3 lgrid((unsigned)lists.nblk, src.K);
     switch (src.N) {
         case 1: hipLaunchKernelGGL(wcnn_l1_kernel<2>, lgrid, dim3(256), 0, s, cp, lists); break;
@@ -1980,7 +1995,8 @@ gw_status gw_patch_cnn_act(void *env, int32_t P, const gw_cnn_actors *net, const
         case 8: hipLaunchKernelGGL(wcnn_l1_kernel<9>, lgrid, dim3(256), 0, s, cp, lists); break;
         default: return err(GW_ERR_ARG, "gw_patch_cnn_act: N out of range");
     }
-    hipLaunchKernelGGL(wcnn_plan, dim3(1), dim3(1024), 0, s, cp, lists);
+    hipLaunchKernelGGL(bucket_scan, dim3((src.K * cp.P + 15) / 16), dim3(1024), 0, s, cp, lists);
+    hipLaunchKernelGGL(cnn_rare_plan, dim3(1), dim3(1024), 0, s, cp);
     hipLaunchKernelGGL(wcnn_scatter, lgrid, dim3(256), 0, s, cp, lists);
 #define RARE(NP) hipLaunchKernelGGL(wcnn_rare_kernel<NP>, dim3(RARE_BLOCKS), dim3(64 * RARE_WAVES), 0, s, cp)
     switch (src.N) {

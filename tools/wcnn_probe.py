@@ -1,6 +1,7 @@
-"""Measurement only: gw_patch_cnn_act at bench.py --config c4patch's size, K act calls on a fixed
-env state (run under rocprofv3 --kernel-trace --stats; GW_CNN_AB selects the A/B variants of
-wcnn_l1_kernel, csrc/actor_ops.hip).  Prints the item counts per position bucket once."""
+"""Measurement only: gw_patch_cnn_act at bench.py --config c4patch's size (or with "full":
+gw_cnn_act at c4cnn's), CALLS act calls on a fixed env state (run under rocprofv3 --kernel-trace
+--stats; GW_CNN_AB selects the A/B variants of the layer-1 kernels, csrc/actor_ops.hip).
+Usage: wcnn_probe.py [CALLS] [full]"""
 import os
 import sys
 
@@ -15,16 +16,20 @@ from marlnav.vec_env import VecGridEnv  # noqa: E402
 
 def main():
     calls = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    full = "full" in sys.argv[2:]
     sc = S.builtin("grid64_n8")
-    P = 16
-    env = VecGridEnv(sc, num_envs=65536, fear=False, seed=8, max_steps=30, obs=False)
-    actors = MultiAgentActors(sc.K, P, P, arch="cnn", device="cuda", seed=0)
+    P = 0 if full else 16
+    env = VecGridEnv(sc, num_envs=65536, fear=False, seed=8, max_steps=30, obs=full)
+    actors = MultiAgentActors(sc.K, P or env.H, P or env.W, arch="cnn", device="cuda", seed=0)
     env.reset()
     for _ in range(5):
         env.step()
     for _ in range(calls):
         actors.act_env(env, env.out["mask"], True, seed=1, counter=0, patch=P)
     torch.cuda.synchronize()
+    if full:
+        env.close()
+        return
     ws = actors._fast["ws"]
     rn = None
     try:  # items per (env, agent): rare_n sits right after rare_z in the workspace (wcnn_ws_layout)
