@@ -1065,21 +1065,85 @@ __global__ void __launch_bounds__(1024) cnn_rare_plan(CnnParams p) {
 
 // Persistent: block b takes units b, b + RARE_BLOCKS, ...; per unit the position's conv weights,
 // map activations and Linear-1 block are staged in LDS.  Lane (item it = l & 15, quarter q): the
-// item's env observation is decoded from its descriptor (act_kernel's rule), lane q evaluates
-// conv-1 window q of the position, conv 2 sums the four windows through two lane shuffles, the 64
-// deltas go through LDS, and the lane writes features 16j + 4q + i of Wl[:, P] . delta.
-constexpr int W2Q = C2 * C1 / 4 + 1;  // window stride of the conv-2 image in float4 (+1: no bank conflicts)
+// item's env observation is decoded from its descriptor (act_kernel's rule) and lane q evaluates
+// conv-1 window q of the position; conv 2 and the Linear-1 block are f32 MFMAs over the wave's 16
+// items (rare_mfma), with the items as the N dimension.
+constexpr int W2R = C1 + 4;   // LDS row stride (floats) of the conv-2 image [window][o][c]
+constexpr int WLR = C2 + 4;   // LDS row stride (floats) of the Linear-1 block image [j][o]
+constexpr int RARE_LDS_W2 = 4 * C2 * W2R, RARE_LDS_WL = HID * WLR;
+
+// stage agent k's conv-2 weight (window-major w2t[k][q][o][c] -> [q][o][W2R]) ...
+__device__ __forceinline__ void stage_w2(float *s_w2, const float *w2t, int tid, int nthreads) {
+    const float4 *src = reinterpret_cast<const float4 *>(w2t);
+    for (int i = tid; i < 4 * C2 * C1 / 4; i += nthreads) {
+        const int row = i / (C1 / 4), c4 = i % (C1 / 4);
+        *reinterpret_cast<float4 *>(s_w2 + row * W2R + 4 * c4) = src[i];
+    }
+}
+// ... and a position's Linear-1 block (wlt[o][j] -> [j][WLR])
+__device__ __forceinline__ void stage_wl(float *s_wl, const float *wlt, int tid, int nthreads) {
+    for (int i = tid; i < C2 * HID; i += nthreads) s_wl[(i & (HID - 1)) * WLR + (i >> 7)] = wlt[i];
+}
+
+// conv 2 and Linear 1 of one position for the wave's 16 items on v_mfma_f32_16x16x4f32:
+//   conv 2:   D[o][it] = sum over k-steps c of W2[o][c][q] (A: lane = (o & 15, window q)) x
+//             a1[it][q][c] (B: lane = (window q, item it), the lane's own conv-1 register c);
+//             lane (it, q) receives o = 16t + 4q + r (tile t, register r)
+//   Linear:   z[j][it] = sum over k-steps (t, r) of Wl[j][16t + 4q + r] (A) x d[it][16t + 4q + r]
+//             (B: the lane's own delta), lane (it, q) receives features 16jt + 4q + r: the layout
+//             act_kernel sums (one float4 per jt)
+// base[4t + r]: the base activation of channel 16t + 4q + r (map / base window).  Products are
+// exact in f32, sums in f32 (another order than torch's).
+__device__ __forceinline__ void rare_mfma(const float (&a1)[C1], const float *s_w2, const float *s_wl,
+                                          const float *s_b2, const float (&base)[16], int lane, float4 (&z)[8]) {
+    const int ol = lane & 15, q = lane >> 4;
+    f32x4 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int c4 = 0; c4 < C1 / 4; ++c4) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const float4 w = *reinterpret_cast<const float4 *>(s_w2 + (q * C2 + 16 * t + ol) * W2R + 4 * c4);
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, a1[4 * c4 + 0], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, a1[4 * c4 + 1], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, a1[4 * c4 + 2], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, a1[4 * c4 + 3], acc[t], 0, 0, 0);
+        }
+    }
+    float d[16];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) d[4 * t + r] = fmaxf(acc[t][r] + s_b2[16 * t + 4 * q + r], 0.0f) - base[4 * t + r];
+    f32x4 zz[8];
+#pragma unroll
+    for (int jt = 0; jt < 8; ++jt) zz[jt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+        for (int jt = 0; jt < 8; ++jt) {
+            const float4 w = *reinterpret_cast<const float4 *>(s_wl + (16 * jt + ol) * WLR + 16 * t + 4 * q);
+            zz[jt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, d[4 * t + 0], zz[jt], 0, 0, 0);
+            zz[jt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, d[4 * t + 1], zz[jt], 0, 0, 0);
+            zz[jt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, d[4 * t + 2], zz[jt], 0, 0, 0);
+            zz[jt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, d[4 * t + 3], zz[jt], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int jt = 0; jt < 8; ++jt) z[jt] = make_float4(zz[jt][0], zz[jt][1], zz[jt][2], zz[jt][3]);
+}
+
 template <int NP>
 __global__ void __launch_bounds__(64 * RARE_WAVES) cnn_rare_kernel(CnnParams p) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int it = lane & 15, q = lane >> 4;
     const int nb = p.K * p.P;
     const int nunits = p.ws.unit_off[nb];
-    __shared__ float4 s_wl[C2 * HID / 4];      // Wl block of P: [o][128], 32 KB
-    __shared__ float4 s_w2[4 * W2Q];           // conv-2 weight [window][o][c], 32 KB
+    __shared__ __attribute__((aligned(16))) float s_w2[RARE_LDS_W2];   // 36 KB
+    __shared__ __attribute__((aligned(16))) float s_wl[RARE_LDS_WL];   // 34 KB
     __shared__ float s_w1[C1][4], s_b1[C1], s_b2[C2], s_a2m[C2];
     __shared__ uint32_t s_road[128];
-    __shared__ float s_dl[RARE_WAVES][C2][TILE];
     if (tid < 128) s_road[tid] = p.ws.road[tid];
     int staged_k = -1, staged_P = -1;
     for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
@@ -1093,15 +1157,13 @@ __global__ void __launch_bounds__(64 * RARE_WAVES) cnn_rare_kernel(CnnParams p) 
         const int i_begin = (u - p.ws.unit_off[lo]) * RARE_ITEMS, i_end = min(n, i_begin + RARE_ITEMS);
         __syncthreads();  // the previous unit is done with the LDS images
         if (k != staged_k) {
-            const float4 *w2 = reinterpret_cast<const float4 *>(p.ws.w2t) + (size_t)k * (4 * C2 * C1 / 4);
-            for (int i = tid; i < 4 * C2 * C1 / 4; i += 64 * RARE_WAVES) s_w2[(i / (C2 * C1 / 4)) * W2Q + i % (C2 * C1 / 4)] = w2[i];
+            stage_w2(s_w2, p.ws.w2t + (size_t)k * 4 * C2 * C1, tid, 64 * RARE_WAVES);
             if (tid < C1 * 4) (&s_w1[0][0])[tid] = p.net.conv1_w[k * C1 * 4 + tid];
             if (tid < C1) s_b1[tid] = p.net.conv1_b[k * C1 + tid];
             if (tid < C2) s_b2[tid] = p.net.conv2_b[k * C2 + tid];
         }
         if (k != staged_k || P != staged_P) {
-            const float4 *wl = reinterpret_cast<const float4 *>(p.ws.wlt + ((size_t)k * p.P + P) * C2 * HID);
-            for (int i = tid; i < C2 * HID / 4; i += 64 * RARE_WAVES) s_wl[i] = wl[i];
+            stage_wl(s_wl, p.ws.wlt + ((size_t)k * p.P + P) * C2 * HID, tid, 64 * RARE_WAVES);
             if (tid < C2) s_a2m[tid] = p.ws.a2map[((size_t)k * p.P + P) * C2 + tid];
         }
         staged_k = k;
@@ -1144,45 +1206,17 @@ __global__ void __launch_bounds__(64 * RARE_WAVES) cnn_rare_kernel(CnnParams p) 
             for (int u4 = 0; u4 < 4; ++u4) acc = fmaf(s_w1[c][u4], v4[u4], acc);
             a1[c] = fmaxf(acc, 0.0f);
         }
-        // ---- conv 2: window q's partial sums meet through the shuffles; deltas to LDS ----
-#pragma unroll 2
-        for (int o = 0; o < C2; ++o) {
-            const float4 *w = &s_w2[q * W2Q + o * (C1 / 4)];
-            float acc = 0.0f;
+        float base[16];
 #pragma unroll
-            for (int c4 = 0; c4 < C1 / 4; ++c4) {
-                const float4 wv = w[c4];
-                acc = fmaf(wv.x, a1[4 * c4], acc);
-                acc = fmaf(wv.y, a1[4 * c4 + 1], acc);
-                acc = fmaf(wv.z, a1[4 * c4 + 2], acc);
-                acc = fmaf(wv.w, a1[4 * c4 + 3], acc);
-            }
-            const float dl = fmaxf(s_b2[o] + quad_sum(acc), 0.0f) - s_a2m[o];
-            if (q == (o & 3)) s_dl[wave][o][it] = dl;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // ---- Linear 1 on the position: features 16j + 4q .. + 3 ----
-        float a[32];
+        for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int i = 0; i < 32; ++i) a[i] = 0.0f;
-#pragma unroll 4
-        for (int o = 0; o < C2; ++o) {
-            const float dl = s_dl[wave][o][it];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float4 w = s_wl[o * (HID / 4) + 4 * j + q];
-                a[4 * j + 0] = fmaf(dl, w.x, a[4 * j + 0]);
-                a[4 * j + 1] = fmaf(dl, w.y, a[4 * j + 1]);
-                a[4 * j + 2] = fmaf(dl, w.z, a[4 * j + 2]);
-                a[4 * j + 3] = fmaf(dl, w.w, a[4 * j + 3]);
-            }
-        }
+            for (int r = 0; r < 4; ++r) base[4 * t + r] = s_a2m[16 * t + 4 * q + r];
+        float4 z[8];
+        rare_mfma(a1, s_w2, s_wl, s_b2, base, lane, z);
         if (ok) {
-            float4 *z = reinterpret_cast<float4 *>(p.ws.rare_z + ((size_t)k * p.E * RS + item) * HID);
+            float4 *zo = reinterpret_cast<float4 *>(p.ws.rare_z + ((size_t)k * p.E * RS + item) * HID);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) z[4 * j + q] = make_float4(a[4 * j], a[4 * j + 1], a[4 * j + 2], a[4 * j + 3]);
+            for (int j = 0; j < 8; ++j) zo[4 * j + q] = z[j];
         }
     }
 }
@@ -1409,19 +1443,17 @@ __global__ void __launch_bounds__(256) wcnn_scatter(CnnParams p, Lists lists) {
 
 // cnn_rare_kernel over window positions: per unit (agent k, position Q) the Linear-1 block in LDS;
 // lane (item it, quarter q) rebuilds conv-1 window q of Q from the item's descriptor (map under
-// the window, -1 outside, the patched cells), conv 2 meets through the shuffles, a2 - a2b goes
-// through LDS, and the lane writes features 16j + 4q + i of Wl[:, Q] . (a2 - a2b).
+// the window, -1 outside, the patched cells); rare_mfma against the base window's activations a2b.
 template <int NP>
 __global__ void __launch_bounds__(64 * RARE_WAVES) wcnn_rare_kernel(CnnParams p) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int it = lane & 15, q = lane >> 4;
     const int nb = p.K * p.P, half = p.PW / 2;
     const int nunits = p.ws.unit_off[nb];
-    __shared__ float4 s_wl[C2 * HID / 4];      // Wl block of Q: [o][128], 32 KB
-    __shared__ float4 s_w2[4 * W2Q];           // conv-2 weight [window][o][c], 32 KB
+    __shared__ __attribute__((aligned(16))) float s_w2[RARE_LDS_W2];   // 36 KB
+    __shared__ __attribute__((aligned(16))) float s_wl[RARE_LDS_WL];   // 34 KB
     __shared__ float s_w1[C1][4], s_b1[C1], s_b2[C2];
     __shared__ uint32_t s_road[128];
-    __shared__ float s_dl[RARE_WAVES][C2][TILE];
     if (tid < 128) s_road[tid] = p.ws.road[tid];
     int staged_k = -1, staged_Q = -1;
     for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
@@ -1435,16 +1467,12 @@ __global__ void __launch_bounds__(64 * RARE_WAVES) wcnn_rare_kernel(CnnParams p)
         const int i_begin = (u - p.ws.unit_off[lo]) * RARE_ITEMS, i_end = min(n, i_begin + RARE_ITEMS);
         __syncthreads();  // the previous unit is done with the LDS images
         if (k != staged_k) {
-            const float4 *w2 = reinterpret_cast<const float4 *>(p.ws.w2t) + (size_t)k * (4 * C2 * C1 / 4);
-            for (int i = tid; i < 4 * C2 * C1 / 4; i += 64 * RARE_WAVES) s_w2[(i / (C2 * C1 / 4)) * W2Q + i % (C2 * C1 / 4)] = w2[i];
+            stage_w2(s_w2, p.ws.w2t + (size_t)k * 4 * C2 * C1, tid, 64 * RARE_WAVES);
             if (tid < C1 * 4) (&s_w1[0][0])[tid] = p.net.conv1_w[k * C1 * 4 + tid];
             if (tid < C1) s_b1[tid] = p.net.conv1_b[k * C1 + tid];
             if (tid < C2) s_b2[tid] = p.net.conv2_b[k * C2 + tid];
         }
-        if (k != staged_k || Q != staged_Q) {
-            const float4 *wl = reinterpret_cast<const float4 *>(p.ws.wlt + ((size_t)k * p.P + Q) * C2 * HID);
-            for (int i = tid; i < C2 * HID / 4; i += 64 * RARE_WAVES) s_wl[i] = wl[i];
-        }
+        if (k != staged_k || Q != staged_Q) stage_wl(s_wl, p.ws.wlt + ((size_t)k * p.P + Q) * C2 * HID, tid, 64 * RARE_WAVES);
         staged_k = k;
         staged_Q = Q;
         __syncthreads();
@@ -1462,6 +1490,11 @@ __global__ void __launch_bounds__(64 * RARE_WAVES) wcnn_rare_kernel(CnnParams p)
         const uint32_t dw[4] = {cells.x, cells.y, cells.z, cells.w};
         const int own = (int)((dw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
         const int ctr = (unsigned)own < (unsigned)p.HW ? own : 0;
+        // the base window's activations of channels 16t + 4q + r (in flight during conv 1)
+        const float4 *ab = reinterpret_cast<const float4 *>(p.ws.a2map + (((size_t)k * p.HW + ctr) * p.P + Q) * C2 + 4 * q);
+        float4 bq[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) bq[t] = ab[4 * t];
         // grid row / col of window q's top-left cell
         const int r0 = ctr / p.W - half + 4 * Y + 2 * (q >> 1), c0 = ctr % p.W - half + 4 * X + 2 * (q & 1);
         float v4[4];
@@ -1492,59 +1525,20 @@ __global__ void __launch_bounds__(64 * RARE_WAVES) wcnn_rare_kernel(CnnParams p)
             for (int u4 = 0; u4 < 4; ++u4) acc = fmaf(s_w1[c][u4], v4[u4], acc);
             a1[c] = fmaxf(acc, 0.0f);
         }
-        // ---- conv 2: window q's partial sums meet through the shuffles; lane q keeps channels
-        //      16q .. 16q + 15 ----
-#pragma unroll 2
-        for (int o = 0; o < C2; ++o) {
-            const float4 *w = &s_w2[q * W2Q + o * (C1 / 4)];
-            float acc = 0.0f;
+        float base[16];
 #pragma unroll
-            for (int c4 = 0; c4 < C1 / 4; ++c4) {
-                const float4 wv = w[c4];
-                acc = fmaf(wv.x, a1[4 * c4], acc);
-                acc = fmaf(wv.y, a1[4 * c4 + 1], acc);
-                acc = fmaf(wv.z, a1[4 * c4 + 2], acc);
-                acc = fmaf(wv.w, a1[4 * c4 + 3], acc);
-            }
-            const float a2 = fmaxf(s_b2[o] + quad_sum(acc), 0.0f);
-            if (q == (o >> 4)) s_dl[wave][o][it] = a2;
+        for (int t = 0; t < 4; ++t) {
+            base[4 * t + 0] = bq[t].x;
+            base[4 * t + 1] = bq[t].y;
+            base[4 * t + 2] = bq[t].z;
+            base[4 * t + 3] = bq[t].w;
         }
-        {   // minus the base window's activations of these 16 channels
-            const float4 *ab = reinterpret_cast<const float4 *>(p.ws.a2map + (((size_t)k * p.HW + ctr) * p.P + Q) * C2 + 16 * q);
-            float4 bv[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) bv[i] = ab[i];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                s_dl[wave][16 * q + 4 * i + 0][it] -= bv[i].x;
-                s_dl[wave][16 * q + 4 * i + 1][it] -= bv[i].y;
-                s_dl[wave][16 * q + 4 * i + 2][it] -= bv[i].z;
-                s_dl[wave][16 * q + 4 * i + 3][it] -= bv[i].w;
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // ---- Linear 1 on the position: features 16j + 4q .. + 3 ----
-        float a[32];
-#pragma unroll
-        for (int i = 0; i < 32; ++i) a[i] = 0.0f;
-#pragma unroll 4
-        for (int o = 0; o < C2; ++o) {
-            const float dl = s_dl[wave][o][it];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float4 w = s_wl[o * (HID / 4) + 4 * j + q];
-                a[4 * j + 0] = fmaf(dl, w.x, a[4 * j + 0]);
-                a[4 * j + 1] = fmaf(dl, w.y, a[4 * j + 1]);
-                a[4 * j + 2] = fmaf(dl, w.z, a[4 * j + 2]);
-                a[4 * j + 3] = fmaf(dl, w.w, a[4 * j + 3]);
-            }
-        }
+        float4 z[8];
+        rare_mfma(a1, s_w2, s_wl, s_b2, base, lane, z);
         if (ok) {
-            float4 *z = reinterpret_cast<float4 *>(p.ws.rare_z + ((size_t)k * p.E * RSW + item) * HID);
+            float4 *zo = reinterpret_cast<float4 *>(p.ws.rare_z + ((size_t)k * p.E * RSW + item) * HID);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) z[4 * j + q] = make_float4(a[4 * j], a[4 * j + 1], a[4 * j + 2], a[4 * j + 3]);
+            for (int j = 0; j < 8; ++j) zo[4 * j + q] = z[j];
         }
     }
 }
