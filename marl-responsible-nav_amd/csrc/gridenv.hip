@@ -1247,7 +1247,11 @@ template <int N, int KMAX, bool FEAR, bool WIDE = false> struct V2Cfg {
     static constexpr int THREADS = 128;
     // WIDE (fear_v2, GW_FEAR_BE=wide): twice the envs per block, half the resident waves
     static constexpr int BE = (WIDE ? 2 : 1) *
-        (FEAR ? (KMAX <= 2 ? (N <= 4 ? 32 : 16) : (N <= 4 ? 16 : 4)) : (KMAX <= 2 ? 128 : 32));
+        (FEAR ? (KMAX <= 2 ? (N <= 4 ? 32 : 16) : (N <= 4 ? 16 : 4)) : (KMAX <= 2 && N > 4 ? 128 : 32));
+    // FeAR off with 32 envs per block: the 128 threads draw the (env, agent) actions in parallel
+    // before one thread per env runs the rest (step_v2_block); with 128 envs per block (N > 4,
+    // large batches) each env thread draws its own
+    static constexpr bool XDRAW = !FEAR && BE == 32 && N <= 4;
     static_assert(!FEAR || BE <= 64, "task encoding holds 6 env bits");
     // task list: [env sims (step_v2 only: BE)][base sims: 2 per actor k with act != MdR] then
     // groups of 16 counterfactuals (one entry per (actor k, close j), expanded on the fly)
@@ -1280,39 +1284,44 @@ struct alignas(16) V2Shared {
     uint16_t pc[2][OB][KMAX][NP];
     float pv[2][OB][KMAX][NP];
     uint32_t eflag[OB];
+    int8_t xact[Cfg::XDRAW ? BE : 1][N];   // FeAR off: the (env, agent) threads' action draws and MdRs
+    int8_t xmdr[Cfg::XDRAW ? BE : 1][N];
     int nbase, ngroup;  // base-sim entries after the env sims; counterfactual groups
 };
 
-// setup_step (ma_customenv.py:432-452) + RL override (:239-242) from the LDS tables
+// setup_step (ma_customenv.py:432-452) + RL override (:239-242) from the LDS tables: agent n
+__device__ __forceinline__ int draw_action(const Params &p, int64_t e, int n, uint32_t episode, int t, int pos,
+                                           const uint32_t *ctab, const double *cdf_s) {
+    const uint32_t gid = (uint32_t)(p.env_offset + e);
+    int a;
+    if (n < p.K) {
+        if (p.rl) {
+            a = p.rl[e * p.K + n];
+        } else {
+            const uint4 r = philox(gid, episode, (uint32_t)t, (2u << 24) | (uint32_t)n, p.key0, p.key1);
+            a = (int)(((uint64_t)r.x * 9u) >> 32);
+        }
+    } else if (p.scripted) {
+        a = p.scripted[e * (p.N - p.K) + (n - p.K)];
+    } else {
+        const uint4 r = philox(gid, episode, (uint32_t)t, (1u << 24) | (uint32_t)n, p.key0, p.key1);
+        const int uni = r.x < 0x40000000u;  // random.random() < 0.25 (:441)
+        const double u = ((double)(r.y >> 5) * 67108864.0 + (double)(r.z >> 6)) * (1.0 / 9007199254740992.0);
+        const int pid = (int)((ctab[pos] >> CT_POL) & 0xFFu);
+        const double *cdf = (cdf_s ? cdf_s : p.tb.cdf) + (pid * 2 + uni) * NA;
+        a = NA - 1;
+#pragma unroll
+        for (int q = NA - 2; q >= 0; --q)
+            if (u < cdf[q]) a = q;  // searchsorted(cdf, u, 'right')
+    }
+    return ((unsigned)a < (unsigned)NA) ? a : 0;
+}
+
 template <int N>
 __device__ __forceinline__ void select_actions_v2(const Params &p, int64_t e, const EnvState<N> &es,
                                                   const uint32_t *ctab, const double *cdf_s, int (&act)[N]) {
-    const uint32_t gid = (uint32_t)(p.env_offset + e);
 #pragma unroll
-    for (int n = 0; n < N; ++n) {
-        if (n < p.K) {
-            if (p.rl) {
-                act[n] = p.rl[e * p.K + n];
-            } else {
-                const uint4 r = philox(gid, es.episode, (uint32_t)es.t, (2u << 24) | (uint32_t)n, p.key0, p.key1);
-                act[n] = (int)(((uint64_t)r.x * 9u) >> 32);
-            }
-        } else if (p.scripted) {
-            act[n] = p.scripted[e * (p.N - p.K) + (n - p.K)];
-        } else {
-            const uint4 r = philox(gid, es.episode, (uint32_t)es.t, (1u << 24) | (uint32_t)n, p.key0, p.key1);
-            const int uni = r.x < 0x40000000u;  // random.random() < 0.25 (:441)
-            const double u = ((double)(r.y >> 5) * 67108864.0 + (double)(r.z >> 6)) * (1.0 / 9007199254740992.0);
-            const int pid = (int)((ctab[es.pos[n]] >> CT_POL) & 0xFFu);
-            const double *cdf = (cdf_s ? cdf_s : p.tb.cdf) + (pid * 2 + uni) * NA;
-            int a = NA - 1;
-#pragma unroll
-            for (int q = NA - 2; q >= 0; --q)
-                if (u < cdf[q]) a = q;  // searchsorted(cdf, u, 'right')
-            act[n] = a;
-        }
-        act[n] = ((unsigned)act[n] < (unsigned)NA) ? act[n] : 0;
-    }
+    for (int n = 0; n < N; ++n) act[n] = draw_action(p, e, n, es.episode, es.t, es.pos[n], ctab, cdf_s);
 }
 
 template <int N, int WH, int OB, int KMAX, int NP>
@@ -1500,6 +1509,18 @@ __device__ __forceinline__ void block_stats(const Params &p, Contrib &ct, double
     }
 }
 
+#ifdef GW_STEP_CLK  // measurement build only (tools/step_clk.sh): thread 0's phase stamps per block
+__device__ unsigned long long g_step_clk[64][16];
+#define STEP_STAMP(slot)                                                             \
+    do {                                                                             \
+        if (tid == 0 && bid < 64) g_step_clk[bid][slot] = clock64();                 \
+    } while (0)
+#else
+#define STEP_STAMP(slot) \
+    do {                 \
+    } while (0)
+#endif
+
 template <int N, int KMAX, bool FEAR, bool OBS, bool DEFER>
 __device__ __forceinline__ void step_v2_block(const Params &p, int64_t bid, V2Shared<N, KMAX, FEAR, OBS> &sh,
                                               uint8_t *dyn) {  // dyn: [cdf P*18 f64][cell table HW u32][Resp]
@@ -1517,18 +1538,42 @@ __device__ __forceinline__ void step_v2_block(const Params &p, int64_t bid, V2Sh
     const int64_t e0 = p.e_begin + bid * BE;
     const int nenv = (int)min((int64_t)BE, p.e_end - e0);
     const int K = p.K;
+    STEP_STAMP(0);
+#ifdef GW_STEP_CLK
+    if (tid == 0 && bid < 64) g_step_clk[bid][15] = wall_clock64();
+#endif
     if (e0 == 0 && tid == 0) step_tick(p.out);  // once per step: the block of env 0
     Contrib ct;
     contrib_zero(ct);
     EnvState<N> es;
     // the env's state loads are issued first so that their latency overlaps the table fill
     if (tid < nenv) load_env<N>(p, e0 + tid, es);
+    // XDRAW: thread i also draws agent i / BE of env i % BE: its inputs
+    constexpr bool XDRAW = Cfg::XDRAW;
+    constexpr int NPAIR = XDRAW ? (BE * N + T - 1) / T : 1;
+    int xpos[NPAIR], xt[NPAIR];
+    uint32_t xep[NPAIR];
+    if constexpr (XDRAW) {
+#pragma unroll
+        for (int j = 0; j < NPAIR; ++j) {
+            const int i = tid + j * T, el = i % BE, n = i / BE;
+            xpos[j] = xt[j] = 0;
+            xep[j] = 0;
+            if (n < N && el < nenv) {
+                const int64_t e = e0 + el;
+                xpos[j] = p.st.pos[(int64_t)n * p.E + e];
+                xep[j] = p.st.episode[e];
+                xt[j] = p.st.t[e];
+            }
+        }
+    }
     lds_fill<T>(ctab, p.tb.celltab, p.HW, tid);
     if (p.lds_cdf)
         lds_fill<T>(reinterpret_cast<uint32_t *>(dyn), reinterpret_cast<const uint32_t *>(p.tb.cdf), 2 * p.n_cdf, tid);
     if (FEAR) lds_fill<T>(reinterpret_cast<uint32_t *>(resp_s), reinterpret_cast<const uint32_t *>(p.tb.resp), 200, tid);
     if (tid == 0) sh.nbase = sh.ngroup = 0;
     __syncthreads();
+    STEP_STAMP(1);
     const CtabOk okv{ctab};
 
     if constexpr (FEAR) {
@@ -1622,15 +1667,38 @@ __device__ __forceinline__ void step_v2_block(const Params &p, int64_t bid, V2Sh
             }
         }
     } else {
-        if (tid < nenv) {  // fear off: one thread does the whole env
+        if constexpr (XDRAW) {  // the action draws and MdRs, one thread per (env, agent)
+#pragma unroll
+            for (int j = 0; j < NPAIR; ++j) {
+                const int i = tid + j * T, el = i % BE, n = i / BE;
+                if (n < N && el < nenv) {
+                    sh.xact[el][n] = (int8_t)draw_action(p, e0 + el, n, xep[j], xt[j], xpos[j], ctab, cdf_s);
+                    sh.xmdr[el][n] = (int8_t)((ctab[xpos[j]] >> CT_MDR) & 0xFu);
+                }
+            }
+            __syncthreads();
+        }
+        if (tid < nenv) {  // the rest of the env on one thread
             const int64_t e = e0 + tid;
             int act[N], mdr[N], fin[N], pos[N];
-            select_actions_v2<N>(p, e, es, ctab, cdf_s, act);
+            if constexpr (XDRAW) {
 #pragma unroll
-            for (int n = 0; n < N; ++n) {
-                pos[n] = es.pos[n];
-                mdr[n] = (int)((ctab[pos[n]] >> CT_MDR) & 0xFu);
+                for (int n = 0; n < N; ++n) {
+                    act[n] = sh.xact[tid][n];
+                    mdr[n] = sh.xmdr[tid][n];
+                    pos[n] = es.pos[n];
+                }
+            } else {
+                select_actions_v2<N>(p, e, es, ctab, cdf_s, act);
+#pragma unroll
+                for (int n = 0; n < N; ++n) {
+                    pos[n] = es.pos[n];
+                    mdr[n] = (int)((ctab[pos[n]] >> CT_MDR) & 0xFu);
+                }
             }
+#ifdef GW_STEP_CLK
+            if (bid < 64 && tid == 0) g_step_clk[bid][2] = clock64() + (uint64_t)(act[0] + mdr[N - 1] < -1000);
+#endif
             int apple[MAXN];
 #pragma unroll
             for (int k = 0; k < MAXN; ++k) apple[k] = (k < K && ((es.flags >> k) & 1u)) ? p.apples[k] : -1;
@@ -1638,11 +1706,15 @@ __device__ __forceinline__ void step_v2_block(const Params &p, int64_t bid, V2Sh
             w.init(pos, act, p.W, p.w_magic);
             uint32_t caught;
             simulate<N, true>(w, okv, K, apple, caught, fin);
+#ifdef GW_STEP_CLK
+            if (bid < 64 && tid == 0) g_step_clk[bid][3] = clock64() + (uint64_t)(fin[0] + (int)caught < -1000);
+#endif
             double fear[MAXN];
 #pragma unroll
             for (int k = 0; k < MAXN; ++k) fear[k] = 0.0;
             ObsInfo<N> oi;
             finish_env<N, DEFER>(p, e, es, act, mdr, fear, w.crash, w.restr, fin, caught, ct, oi, ctab);
+            STEP_STAMP(4);
             if constexpr (OBS) {
                 v2_patches<N, 0, OB, KMAX, NP>(p, tid, oi, ctab, sh.pc, sh.pv);
                 if (oi.flags & D_FINAL) v2_patches<N, 1, OB, KMAX, NP>(p, tid, oi, ctab, sh.pc, sh.pv);
@@ -1659,7 +1731,9 @@ __device__ __forceinline__ void step_v2_block(const Params &p, int64_t bid, V2Sh
     // ---- block statistics (deterministic tree) ----
     // deferred FeAR: the FeAR-owned f64 fields are fear_v2's; without FeAR field 2 stays 0
     constexpr uint32_t FM = DEFER ? 0u : ((1u << 0) | (1u << 5) | (FEAR ? (1u << 2) : 0u));
+    STEP_STAMP(5);
     block_stats<T, FM, ST_INT>(p, ct, sh.red, tid, p.stats_row0 + e0 / BE);
+    STEP_STAMP(6);
 
     if constexpr (OBS) {
         // ---- D: obs of the block's envs, 16-byte coalesced stores ----
@@ -1707,17 +1781,8 @@ __global__ void __launch_bounds__(128) step_v2(Params p) {
     step_v2_block<N, KMAX, FEAR, OBS, DEFER>(p, blockIdx.x, sh, dyn);
 }
 
-// ---------------------------------------------------------------------------------------
-// patch_kernel (gw_obs_patch): egocentric P x P windows of the env's last observation, centred
-// on each RL agent's cell (row / col offsets -P/2 .. P-1-P/2), cells outside the grid -1 (the
-// map's inactive value).  The same encoding as obs_block (static map + the N + 1 patched
-// cells of the descriptor), so window == a crop of the full obs padded with -1.  Layout
-// [K][E][P*P] (agent-major like the full obs); which = 0 the step's obs (D_WRITE envs), 1 the
-// terminal obs (D_FINAL envs, centred on the terminal cell).  Not a reference feature (the
-// reference observes the whole grid, custom/ma_customenv.py:303-322): an opt-in input format.
-// ---------------------------------------------------------------------------------------
-constexpr int PATCH_THREADS = 256;
-constexpr int PATCH_BE = 32;  // envs per block: a block's windows of one agent are one contiguous run
+// gw_obs_patch (egocentric P x P windows of the env's last observation, -1 outside the grid,
+// the same encoding as obs_block) is written by csrc/patch_ops.hip (launch_windows).
 
 // ---------------------------------------------------------------------------------------
 // step_obs (GW_KERNEL=merged with async obs): ONE launch per gw_step on the caller's stream.
@@ -3037,6 +3102,14 @@ gw_status gw_profile(void *handle, int enable) {
     }
     return GW_OK;
 }
+
+#ifdef GW_STEP_CLK
+// measurement build only: thread 0's phase stamps of the last step_v2_block of blocks 0-63
+int gw_step_debug_clocks(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(gw::g_step_clk), sizeof(unsigned long long) * 64 * 16) == hipSuccess
+               ? 0 : -1;
+}
+#endif
 
 gw_status gw_profile_spans(void *handle, double *out, int64_t cap, int64_t *n_spans) {
     Env *env = static_cast<Env *>(handle);

@@ -327,6 +327,10 @@ def load(build_if_needed: bool = True):
         if _lib is not None:
             return _lib
         import torch  # noqa: F401  (bind to torch's HIP runtime)
+        alt = os.environ.get("MARLNAV_LIB")  # measurement builds only (tools/step_clk.sh)
+        if alt:
+            _lib = _declare(C.CDLL(alt))
+            return _lib
         if build_if_needed and needs_build():
             build()
         if not os.path.exists(LIB_PATH):
