@@ -8,14 +8,16 @@
 //
 // Block = PB envs (both agents).  Staging: one thread per (which, env, agent) builds the window's
 // patched cells in registers, drops a patch that a later one overrides (the obs writer's order),
-// and leaves window positions + values in LDS.  The step's windows: one wave per window writes
-// the map part into an LDS image of the block's run (lanes own fixed window positions, so their
-// (row, col) offsets are computed once), then the patched cells as one scattered LDS store; the
-// run leaves as aligned 16-byte stores of whole lines.  Terminal windows (few envs per step) go
-// straight to HBM from registers.
+// and leaves window positions + values in LDS.  The step's windows, P % 4 == 0: one thread per
+// 16-byte piece of a window row (four map bits + the window's <= N + 1 overrides, one aligned
+// float4 store); other P <= 16: one wave per window writes the map part into an LDS image of the
+// block's run (lanes own fixed window positions, so their (row, col) offsets are computed once),
+// then the patched cells as one scattered LDS store; the run leaves as aligned 16-byte stores of
+// whole lines.  Terminal windows (few envs per step) go straight to HBM from registers.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "patch_ops.h"
 
@@ -41,8 +43,12 @@ __device__ __forceinline__ float map_value(const uint32_t *road, int H, int W, i
     return ((road[cell >> 5] >> (cell & 31)) & 1u) ? 0.0f : -1.0f;
 }
 
-template <bool SMALL>  // SMALL: P * P <= 256 (the LDS-assembled path); else one thread per element
+// MODE 0: P * P <= 256, the windows assembled in LDS; 1: one thread per element (large windows);
+// 2: P % 4 == 0, one thread per 16-byte piece of a window row (map bits + overrides in registers,
+// no LDS image: every store is a whole aligned float4 of the [K][E][P*P] run)
+template <int MODE>
 __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a, unsigned long long *dbg) {
+    constexpr bool SMALL = MODE == 0;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int tid = threadIdx.x, K = a.K, N = a.N, W = a.W, H = a.H, P = a.P;
     const int PP = P * P, half = P / 2, np = N + 1, nroad = (a.H * a.W + 31) / 32;
@@ -179,17 +185,55 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a, unsign
             }
             for (int i = lead + 4 * n4 + tid; i < len; i += THREADS) o[i] = s_out[i];
         }
-    } else if (a.patch) {  // large windows: one thread per element, overrides in registers
+    } else if (MODE == 2 && a.patch) {
+        const int P4 = P / 4, Q4 = PP / 4, per_k = nenv * Q4;
+        // q / P4 and j / Q4 as multiply-highs (exact for the small numerators here; Q4 >= 4,
+        // P4 = 1 is q itself: its magic 2^32 does not fit)
+        const uint32_t m_p4 = P4 > 1 ? (uint32_t)((0x100000000ull + (uint64_t)P4 - 1) / (uint64_t)P4) : 0u;
+        const uint32_t m_q4 = (uint32_t)((0x100000000ull + (uint64_t)Q4 - 1) / (uint64_t)Q4);
         for (int k = 0; k < K; ++k) {
-            float *o = a.patch + ((int64_t)k * a.E + e0) * PP;
-            for (int i = tid; i < nenv * PP; i += THREADS) {
-                const int el = i / PP, c = i - el * PP;
+            float4 *o4 = reinterpret_cast<float4 *>(a.patch + ((int64_t)k * a.E + e0) * PP);
+            for (int j = tid; j < per_k; j += THREADS) {
+                const int el = (int)__umulhi((uint32_t)j, m_q4), q = j - el * Q4;
                 if (!(s_flag[el] & D_WRITE)) continue;
                 const int slot = el * K + k;
                 const int ctr = s_ctr[slot];
-                float v = map_value(s_road, H, W, (ctr >> 16) + c / P - half, (ctr & 0xFFFF) + c % P - half);
-                for (int u = 0; u < np; ++u)
-                    if (s_pw[slot * np + u] == c) v = s_pv[slot * np + u];
+                const int wr = P4 > 1 ? (int)__umulhi((uint32_t)q, m_p4) : q, wc = 4 * (q - wr * P4);
+                const int row = (ctr >> 16) - half + wr, col0 = (ctr & 0xFFFF) - half + wc;
+                float v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = map_value(s_road, H, W, row, col0 + u);
+                const int base = wr * P + wc;
+                for (int u = 0; u < np; ++u) {
+                    const int d = s_pw[slot * np + u] - base;
+                    if ((unsigned)d < 4u) {
+                        const float pv = s_pv[slot * np + u];
+                        v[0] = d == 0 ? pv : v[0];
+                        v[1] = d == 1 ? pv : v[1];
+                        v[2] = d == 2 ? pv : v[2];
+                        v[3] = d == 3 ? pv : v[3];
+                    }
+                }
+                o4[j] = make_float4(v[0], v[1], v[2], v[3]);
+            }
+        }
+    } else if (a.patch) {  // one thread per element (consecutive lanes: consecutive floats), overrides in registers
+        // i / PP and c / P as multiply-highs (i < PB * PP; P >= 2)
+        const uint32_t m_pp = (uint32_t)((0x100000000ull + (uint64_t)PP - 1) / (uint64_t)PP);
+        const uint32_t m_p = (uint32_t)((0x100000000ull + (uint64_t)P - 1) / (uint64_t)P);
+        for (int k = 0; k < K; ++k) {
+            float *o = a.patch + ((int64_t)k * a.E + e0) * PP;
+            for (int i = tid; i < nenv * PP; i += THREADS) {
+                const int el = (int)__umulhi((uint32_t)i, m_pp), c = i - el * PP;
+                if (!(s_flag[el] & D_WRITE)) continue;
+                const int slot = el * K + k;
+                const int ctr = s_ctr[slot];
+                const int wr = (int)__umulhi((uint32_t)c, m_p);
+                float v = map_value(s_road, H, W, (ctr >> 16) + wr - half, (ctr & 0xFFFF) + c - wr * P - half);
+                for (int u = 0; u < np; ++u) {
+                    const float pv = s_pv[slot * np + u];
+                    v = s_pw[slot * np + u] == c ? pv : v;
+                }
                 o[i] = v;
             }
         }
@@ -223,15 +267,19 @@ unsigned long long *g_patch_dbg = nullptr;
 
 hipError_t launch_windows(const PatchArgs &a, hipStream_t s) {
     const int np = a.N + 1, PP = a.P * a.P;
-    const bool small = PP <= 64 * MAXPL;
+    int mode = a.P % 4 == 0 ? 2 : PP <= 64 * MAXPL ? 0 : 1;
+    static const char *force = std::getenv("GW_PATCH_MODE");  // (measurement only: A/B of the writers)
+    if (force && (std::atoi(force) == 1 || (std::atoi(force) == 0 && PP <= 64 * MAXPL))) mode = std::atoi(force);
     const size_t lds = sizeof(uint32_t) * ((a.H * a.W + 31) / 32 + PB) + sizeof(int) * 2 * PB * a.K +
                        sizeof(uint32_t) * (size_t)2 * 2 * PB * a.K * np +
-                       (small ? sizeof(float) * (size_t)PB * PP : 0);
+                       (mode == 0 ? sizeof(float) * (size_t)PB * PP : 0);
     const unsigned grid = (unsigned)((a.E + PB - 1) / PB);
-    if (small)
-        hipLaunchKernelGGL(window_kernel<true>, dim3(grid), dim3(THREADS), lds, s, a, g_patch_dbg);
+    if (mode == 2)
+        hipLaunchKernelGGL(window_kernel<2>, dim3(grid), dim3(THREADS), lds, s, a, g_patch_dbg);
+    else if (mode == 0)
+        hipLaunchKernelGGL(window_kernel<0>, dim3(grid), dim3(THREADS), lds, s, a, g_patch_dbg);
     else
-        hipLaunchKernelGGL(window_kernel<false>, dim3(grid), dim3(THREADS), lds, s, a, g_patch_dbg);
+        hipLaunchKernelGGL(window_kernel<1>, dim3(grid), dim3(THREADS), lds, s, a, g_patch_dbg);
     return hipGetLastError();
 }
 

@@ -31,7 +31,8 @@ def crop(full, centers, P, W):
 
 @pytest.mark.parametrize("scen,E,P,fear,async_obs", [("grid32", 2048, 11, True, False), ("grid32", 777, 8, False, True),
                                                      ("level3", 300, 5, True, False), ("level3", 64, 40, False, False),
-                                                     ("grid64_n8", 512, 15, True, "lazy")])
+                                                     ("grid64_n8", 512, 15, True, "lazy"),
+                                                     ("grid64_n8", 1000, 16, False, True), ("level3", 50, 4, True, False)])
 def test_patch_equals_cropped_full_obs(scen, E, P, fear, async_obs):
     env = VecGridEnv(scen, num_envs=E, fear=fear, fear_weight=-5.0, max_steps=15, seed=7, final_obs=True, debug=True)
     if async_obs:
