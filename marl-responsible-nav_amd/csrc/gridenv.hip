@@ -1243,11 +1243,15 @@ __global__ void __launch_bounds__(OBS_THREADS) obs_kernel(Params p, float *__res
 // cell table bits
 constexpr uint32_t CT_POL = 0, CT_MDR = 8, CT_AMASK = 12, CT_OK = 21, CT_ROAD = 25;
 
-template <int N, int KMAX, bool FEAR, bool WIDE = false> struct V2Cfg {
+// DEF: the deferred-FeAR world-update kernel (step_v2<.., DEFER>, GW_KERNEL=defer with FeAR on):
+// one env per thread in 128-env blocks (it runs beside the large obs writer, where per-block
+// table fills and barriers cost more than the lane-parallel draws save)
+template <int N, int KMAX, bool FEAR, bool WIDE = false, bool DEF = false> struct V2Cfg {
     static constexpr int THREADS = 128;
     // WIDE (fear_v2, GW_FEAR_BE=wide): twice the envs per block, half the resident waves
     static constexpr int BE = (WIDE ? 2 : 1) *
-        (FEAR ? (KMAX <= 2 ? (N <= 4 ? 32 : 16) : (N <= 4 ? 16 : 4)) : (KMAX <= 2 && N > 4 ? 128 : 32));
+        (FEAR ? (KMAX <= 2 ? (N <= 4 ? 32 : 16) : (N <= 4 ? 16 : 4))
+              : (KMAX <= 2 && (N > 4 || DEF) ? 128 : 32));
     // FeAR off with 32 envs per block: the 128 threads draw the (env, agent) actions in parallel
     // before one thread per env runs the rest (step_v2_block); with 128 envs per block (N > 4,
     // large batches) each env thread draws its own
@@ -1265,9 +1269,9 @@ template <int N, int KMAX, bool FEAR, bool WIDE = false> struct V2Cfg {
     }
 };
 
-template <int N, int KMAX, bool FEAR, bool OBS, bool WIDE = false>
+template <int N, int KMAX, bool FEAR, bool OBS, bool WIDE = false, bool DEF = false>
 struct alignas(16) V2Shared {
-    using Cfg = V2Cfg<N, KMAX, FEAR, WIDE>;
+    using Cfg = V2Cfg<N, KMAX, FEAR, WIDE, DEF>;
     static constexpr int BE = Cfg::BE, FB = FEAR ? BE : 1, OB = OBS ? BE : 1, NP = N + 1;
     double red[Cfg::THREADS / 64][GW_STATS];
     typename Cfg::Task tasks[Cfg::MAXB];
@@ -1522,10 +1526,10 @@ __device__ unsigned long long g_step_clk[64][16];
 #endif
 
 template <int N, int KMAX, bool FEAR, bool OBS, bool DEFER>
-__device__ __forceinline__ void step_v2_block(const Params &p, int64_t bid, V2Shared<N, KMAX, FEAR, OBS> &sh,
+__device__ __forceinline__ void step_v2_block(const Params &p, int64_t bid, V2Shared<N, KMAX, FEAR, OBS, false, DEFER> &sh,
                                               uint8_t *dyn) {  // dyn: [cdf P*18 f64][cell table HW u32][Resp]
-    using Cfg = V2Cfg<N, KMAX, FEAR>;
-    using Sh = V2Shared<N, KMAX, FEAR, OBS>;
+    using Cfg = V2Cfg<N, KMAX, FEAR, false, DEFER>;
+    using Sh = V2Shared<N, KMAX, FEAR, OBS, false, DEFER>;
     constexpr int BE = Cfg::BE, T = Cfg::THREADS, NP = N + 1, OB = Sh::OB;
     const double *cdf_s = p.lds_cdf ? reinterpret_cast<const double *>(dyn) : nullptr;
     uint32_t *ctab = reinterpret_cast<uint32_t *>(dyn + p.ctab_off);
@@ -1776,7 +1780,7 @@ __device__ __forceinline__ void step_v2_block(const Params &p, int64_t bid, V2Sh
 
 template <int N, int KMAX, bool FEAR, bool OBS, bool DEFER = false>
 __global__ void __launch_bounds__(128) step_v2(Params p) {
-    __shared__ V2Shared<N, KMAX, FEAR, OBS> sh;
+    __shared__ V2Shared<N, KMAX, FEAR, OBS, false, DEFER> sh;
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
     step_v2_block<N, KMAX, FEAR, OBS, DEFER>(p, blockIdx.x, sh, dyn);
 }
@@ -2378,19 +2382,22 @@ gw::Params make_params(const Env *env) {
 
 template <int N, int KMAX, bool FEAR, bool OBS, bool DEFER = false>
 hipError_t launch_v2(const Env *env, const gw::Params &p, hipStream_t s) {
-    constexpr int BE = gw::V2Cfg<N, KMAX, FEAR>::BE;
+    constexpr int BE = gw::V2Cfg<N, KMAX, FEAR, false, DEFER>::BE;
     const int64_t n = p.e_end - p.e_begin;  // this launch's env range (a pipeline chunk or all)
     if (n <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((n + BE - 1) / BE);
+    // dynamic LDS [cdf][cell table][Resp (FeAR)].  (Staging the free-cell list there too for the
+    // auto-reset's spawn made C2's step kernel slower: 11.4 -> 12.2 us, profiles/r3_c2.)
     const size_t dyn = (size_t)p.resp_off + (FEAR ? 100 * sizeof(double) : 0);
-    gw_launch((gw::step_v2<N, KMAX, FEAR, OBS, DEFER>), dim3(grid), dim3(gw::V2Cfg<N, KMAX, FEAR>::THREADS), dyn, s, p);
+    gw_launch((gw::step_v2<N, KMAX, FEAR, OBS, DEFER>), dim3(grid), dim3(gw::V2Cfg<N, KMAX, FEAR, false, DEFER>::THREADS),
+              dyn, s, p);
     return hipGetLastError();
 }
 
 // stats rows of the deferred world-update kernel; fear_v2's rows follow them
 template <int N>
 int64_t defer_step_rows(const Env *env) {
-    const int be = env->K <= 2 ? gw::V2Cfg<N, 2, false>::BE : gw::V2Cfg<N, N, false>::BE;
+    const int be = env->K <= 2 ? gw::V2Cfg<N, 2, false, false, true>::BE : gw::V2Cfg<N, N, false, false, true>::BE;
     return (env->E + be - 1) / be;
 }
 

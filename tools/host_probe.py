@@ -1,6 +1,7 @@
 """Measurement only: host time per C3 step (bench.py's default env loop) split into the return
 gather's into() / push() and env.step(), plus the GPU time of the same steps.
-Usage: python tools/host_probe.py [steps]"""
+Usage: python tools/host_probe.py [steps] [first]  (first: per-step host times of the bench's
+timed-region entry)"""
 import os
 import sys
 import time
@@ -56,5 +57,48 @@ def main():
     env.close()
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and not (len(sys.argv) > 2 and sys.argv[2] == "first"):
     main()
+
+
+def first_steps():
+    """The bench's timed-region entry (warmup 5, gc, sync, event record) with per-step host times."""
+    import gc
+    E = 65536
+    env = VecGridEnv("grid32", num_envs=E, fear=True, fear_weight=-5.0, max_steps=150, auto_reset=True, seed=42,
+                     stats=True)
+    env.set_obs_async(True)
+    env.reset()
+    stats_acc = torch.zeros_like(env.out["stats"])
+    gather = ReturnGather(E, 0, 1, env.device)
+    ring = [env.out["obs"], torch.empty_like(env.out["obs"])]
+
+    def one(i):
+        into = gather.into()
+        into["stats_acc"] = stats_acc
+        into["obs"] = ring[i % 2]
+        env.step(into=into)
+        gather.push()
+
+    for i in range(5):
+        one(i)
+    stream = torch.cuda.current_stream()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    gc.collect()
+    gc.disable()
+    torch.cuda.synchronize()
+    t = [time.perf_counter()]
+    ev0.record(stream)
+    t.append(time.perf_counter())
+    for i in range(5, 25):
+        one(i)
+        t.append(time.perf_counter())
+    torch.cuda.synchronize()
+    gc.enable()
+    d = [round((b - a) * 1e6, 1) for a, b in zip(t, t[1:])]
+    print("host us: ev0.record", d[0], "steps", d[1:])
+    env.close()
+
+
+if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[2] == "first":
+    first_steps()
