@@ -408,8 +408,21 @@ def main():
     if not cfg.get("rollout"):
         env.set_obs_async(obs_mode)
         env.reset()
+    # no Python garbage collection inside the timed region (as timeit does): the warmup's step
+    # results would otherwise trigger a collection pause that idles the GPU (measured: +30 us per
+    # step over 20 steps after 2,000 warmup steps).  The collection runs before the LAST warmup
+    # step, which re-warms the host path: collecting right before the timed region left the first
+    # timed step's host work (the return gather's views, gw_step's enqueue) 4-5x slower on cold
+    # CPU caches, ~230 us of idle GPU in a 20-step run (tools/host_probe.py ... first)
+    import gc
     for i in range(args.warmup):
+        if i == args.warmup - 1:
+            gc.collect()
+            gc.disable()
         one_step(i)
+    if args.warmup == 0:
+        gc.collect()
+        gc.disable()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -434,12 +447,6 @@ def main():
         env.profile(True, reserve=8 * (n_prof + 2))
         env.profile(False)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    # no Python garbage collection inside the timed region (as timeit does): the warmup's step
-    # results would otherwise trigger a collection pause that idles the GPU (measured: +30 us per
-    # step over 20 steps after 2,000 warmup steps)
-    import gc
-    gc.collect()
-    gc.disable()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

@@ -73,30 +73,60 @@ def first_steps():
     gather = ReturnGather(E, 0, 1, env.device)
     ring = [env.out["obs"], torch.empty_like(env.out["obs"])]
 
+    parts = []
+
     def one(i):
+        a = time.perf_counter()
         into = gather.into()
         into["stats_acc"] = stats_acc
         into["obs"] = ring[i % 2]
+        b = time.perf_counter()
         env.step(into=into)
+        c = time.perf_counter()
         gather.push()
+        parts.append((round((b - a) * 1e6, 1), round((c - b) * 1e6, 1), round((time.perf_counter() - c) * 1e6, 1)))
 
+    early = bool(os.environ.get("HOST_PROBE_GCEARLY"))  # collect before the last warmup step
     for i in range(5):
+        if early and i == 4:
+            gc.collect()
+            gc.disable()
         one(i)
     stream = torch.cuda.current_stream()
     ev0 = torch.cuda.Event(enable_timing=True)
-    gc.collect()
-    gc.disable()
+    if not early:
+        gc.collect()
+        gc.disable()
+    if os.environ.get("HOST_PROBE_SPINSYNC"):  # poll the streams until idle before the sync
+        while not stream.query():
+            pass
     torch.cuda.synchronize()
+    if len(sys.argv) > 3:  # spin the host for argv[3] us after the sync (CPU wake-up hypothesis)
+        ts = time.perf_counter()
+        while time.perf_counter() - ts < float(sys.argv[3]) * 1e-6:
+            pass
     t = [time.perf_counter()]
     ev0.record(stream)
     t.append(time.perf_counter())
+    prof = None
+    if os.environ.get("HOST_PROBE_PROFILE"):  # cProfile of the first timed step only
+        import cProfile
+        prof = cProfile.Profile()
     for i in range(5, 25):
+        if prof is not None and i == 5:
+            prof.enable()
         one(i)
+        if prof is not None and i == 5:
+            prof.disable()
         t.append(time.perf_counter())
     torch.cuda.synchronize()
     gc.enable()
     d = [round((b - a) * 1e6, 1) for a, b in zip(t, t[1:])]
     print("host us: ev0.record", d[0], "steps", d[1:])
+    print("into / env.step / push of the first timed steps:", parts[5:9])
+    if prof is not None:
+        import pstats
+        pstats.Stats(prof).sort_stats("tottime").print_stats(15)
     env.close()
 
 
