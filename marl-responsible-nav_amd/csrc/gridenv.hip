@@ -552,10 +552,13 @@ struct Contrib {  // this env's share of gw_step_out.stats
     double v[GW_STATS];
 };
 
-// one field of a block's stats row: the step's value (stats) and / or its running total
+// one field of a block's stats row: the step's value (stats) and / or its running total.  The
+// total is a no-return f64 atomic add (one IEEE add at the L2, as the load + add + store was):
+// each row belongs to one block per launch and launches are stream-ordered, so the sum order is
+// fixed, and the block's last wave no longer waits a load round trip before it can end.
 __device__ __forceinline__ void stats_put(const gw_step_out &o, int64_t idx, double v) {
     if (o.stats) o.stats[idx] = v;
-    if (o.stats_acc) o.stats_acc[idx] = __dadd_rn(o.stats_acc[idx], v);
+    if (o.stats_acc) __hip_atomic_fetch_add(o.stats_acc + idx, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // the step's tick (gw_step_out.tick): one vector atomic by one lane of the step's first block
@@ -1243,6 +1246,9 @@ __global__ void __launch_bounds__(OBS_THREADS) obs_kernel(Params p, float *__res
 // cell table bits
 constexpr uint32_t CT_POL = 0, CT_MDR = 8, CT_AMASK = 12, CT_OK = 21, CT_ROAD = 25;
 
+#ifndef GW_NOFEAR_BE  // envs per block of the FeAR-off step_v2 with N <= 4 (measurement builds: 16)
+#define GW_NOFEAR_BE 32
+#endif
 // DEF: the deferred-FeAR world-update kernel (step_v2<.., DEFER>, GW_KERNEL=defer with FeAR on):
 // one env per thread in 128-env blocks (it runs beside the large obs writer, where per-block
 // table fills and barriers cost more than the lane-parallel draws save)
@@ -1251,11 +1257,11 @@ template <int N, int KMAX, bool FEAR, bool WIDE = false, bool DEF = false> struc
     // WIDE (fear_v2, GW_FEAR_BE=wide): twice the envs per block, half the resident waves
     static constexpr int BE = (WIDE ? 2 : 1) *
         (FEAR ? (KMAX <= 2 ? (N <= 4 ? 32 : 16) : (N <= 4 ? 16 : 4))
-              : (KMAX <= 2 && (N > 4 || DEF) ? 128 : 32));
+              : (KMAX <= 2 && (N > 4 || DEF) ? 128 : GW_NOFEAR_BE));
     // FeAR off with 32 envs per block: the 128 threads draw the (env, agent) actions in parallel
     // before one thread per env runs the rest (step_v2_block); with 128 envs per block (N > 4,
     // large batches) each env thread draws its own
-    static constexpr bool XDRAW = !FEAR && BE == 32 && N <= 4;
+    static constexpr bool XDRAW = !FEAR && BE <= 32 && N <= 4;
     static_assert(!FEAR || BE <= 64, "task encoding holds 6 env bits");
     // task list: [env sims (step_v2 only: BE)][base sims: 2 per actor k with act != MdR] then
     // groups of 16 counterfactuals (one entry per (actor k, close j), expanded on the fly)
@@ -1550,10 +1556,14 @@ __device__ __forceinline__ void step_v2_block(const Params &p, int64_t bid, V2Sh
     Contrib ct;
     contrib_zero(ct);
     EnvState<N> es;
-    // the env's state loads are issued first so that their latency overlaps the table fill
-    if (tid < nenv) load_env<N>(p, e0 + tid, es);
-    // XDRAW: thread i also draws agent i / BE of env i % BE: its inputs
+    // XDRAW: the env chains run on the first BE / 2 lanes of each of the two waves (16 envs per
+    // wave instead of 32: a wave waits for fewer divergent collision passes and resets)
     constexpr bool XDRAW = Cfg::XDRAW;
+    constexpr int CPW = XDRAW ? BE / (T / 64) : 64;  // chain lanes per wave
+    const int cel = XDRAW ? (((tid & 63) < CPW) ? (tid >> 6) * CPW + (tid & 63) : BE) : tid;
+    // the env's state loads are issued first so that their latency overlaps the table fill
+    if (cel < nenv) load_env<N>(p, e0 + cel, es);
+    // XDRAW: thread i also draws agent i / BE of env i % BE: its inputs
     constexpr int NPAIR = XDRAW ? (BE * N + T - 1) / T : 1;
     int xpos[NPAIR], xt[NPAIR];
     uint32_t xep[NPAIR];
@@ -1682,14 +1692,14 @@ __device__ __forceinline__ void step_v2_block(const Params &p, int64_t bid, V2Sh
             }
             __syncthreads();
         }
-        if (tid < nenv) {  // the rest of the env on one thread
-            const int64_t e = e0 + tid;
+        if (cel < nenv) {  // the rest of the env on one thread
+            const int64_t e = e0 + cel;
             int act[N], mdr[N], fin[N], pos[N];
             if constexpr (XDRAW) {
 #pragma unroll
                 for (int n = 0; n < N; ++n) {
-                    act[n] = sh.xact[tid][n];
-                    mdr[n] = sh.xmdr[tid][n];
+                    act[n] = sh.xact[cel][n];
+                    mdr[n] = sh.xmdr[cel][n];
                     pos[n] = es.pos[n];
                 }
             } else {
@@ -1720,9 +1730,9 @@ __device__ __forceinline__ void step_v2_block(const Params &p, int64_t bid, V2Sh
             finish_env<N, DEFER>(p, e, es, act, mdr, fear, w.crash, w.restr, fin, caught, ct, oi, ctab);
             STEP_STAMP(4);
             if constexpr (OBS) {
-                v2_patches<N, 0, OB, KMAX, NP>(p, tid, oi, ctab, sh.pc, sh.pv);
-                if (oi.flags & D_FINAL) v2_patches<N, 1, OB, KMAX, NP>(p, tid, oi, ctab, sh.pc, sh.pv);
-                sh.eflag[tid] = oi.flags;
+                v2_patches<N, 0, OB, KMAX, NP>(p, cel, oi, ctab, sh.pc, sh.pv);
+                if (oi.flags & D_FINAL) v2_patches<N, 1, OB, KMAX, NP>(p, cel, oi, ctab, sh.pc, sh.pv);
+                sh.eflag[cel] = oi.flags;
             } else {
                 store_desc<N>(p, e, oi);
             }

@@ -60,6 +60,10 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a, unsign
     int *s_pw = s_ctr + 2 * PB * K;                                  // [2][PB][K][np] window positions (-1: none)
     float *s_pv = reinterpret_cast<float *>(s_pw + 2 * PB * K * np);
     float *s_out = s_pv + 2 * PB * K * np;                           // SMALL: one agent's run [nenv * PP]
+    // MODE 2: per step window (slot el * K + k) and 4-cell segment q, the surviving patch index + 1
+    // of each of the segment's cells, one nibble per cell (0: map value)
+    uint16_t *s_seg = reinterpret_cast<uint16_t *>(s_pv + 2 * PB * K * np);
+    const int Q4 = PP / 4;
     const int64_t e0 = (int64_t)blockIdx.x * PB;
     const int nenv = (int)min((int64_t)PB, a.E - e0);
     if (dbg && tid == 0) dbg[4 * blockIdx.x + 0] = wall_clock64();
@@ -100,6 +104,9 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a, unsign
             const int ctr = (int)((words[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
             const int cr = (int)__umulhi((uint32_t)ctr, a_wmagic), cc = ctr - cr * W;
             s_ctr[slot] = (cr << 16) | cc;
+            uint16_t *sg = s_seg + slot * Q4;  // which == 0: slot = el * K + k
+            if (MODE == 2 && which == 0)
+                for (int q = 0; q < Q4; q += 2) *reinterpret_cast<uint32_t *>(sg + q) = 0u;  // Q4 is even
             int cell[MAXP];
             float val[MAXP];
             int u = 0;
@@ -130,6 +137,8 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a, unsign
                 }
                 s_pw[slot * np + i] = pos;
                 s_pv[slot * np + i] = i < u ? val[i] : 0.0f;
+                if (MODE == 2 && which == 0 && pos >= 0)  // this thread owns the slot's segments
+                    sg[pos >> 2] |= (uint16_t)((i + 1) << (4 * (pos & 3)));
             }
         }
     }
@@ -186,7 +195,8 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a, unsign
             for (int i = lead + 4 * n4 + tid; i < len; i += THREADS) o[i] = s_out[i];
         }
     } else if (MODE == 2 && a.patch) {
-        const int P4 = P / 4, Q4 = PP / 4, per_k = nenv * Q4;
+        const int P4 = P / 4, per_k = nenv * Q4;
+        const int nroad1 = nroad - 1;
         // q / P4 and j / Q4 as multiply-highs (exact for the small numerators here; Q4 >= 4,
         // P4 = 1 is q itself: its magic 2^32 does not fit)
         const uint32_t m_p4 = P4 > 1 ? (uint32_t)((0x100000000ull + (uint64_t)P4 - 1) / (uint64_t)P4) : 0u;
@@ -200,18 +210,25 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a, unsign
                 const int ctr = s_ctr[slot];
                 const int wr = P4 > 1 ? (int)__umulhi((uint32_t)q, m_p4) : q, wc = 4 * (q - wr * P4);
                 const int row = (ctr >> 16) - half + wr, col0 = (ctr & 0xFFFF) - half + wc;
+                // the four map values from at most two road words: bits of cells cmin .. cmin + 31
+                const int cmin = max(col0, 0), cell = row * W + cmin;
+                const bool in_row = (unsigned)row < (unsigned)H;
+                const int w0 = in_row ? min(cell >> 5, nroad1) : 0;  // (cols past the edge: masked below)
+                const uint64_t bits = (((uint64_t)s_road[min(w0 + 1, nroad1)] << 32) | s_road[w0]) >> (cell & 31);
                 float v[4];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) v[u] = map_value(s_road, H, W, row, col0 + u);
-                const int base = wr * P + wc;
-                for (int u = 0; u < np; ++u) {
-                    const int d = s_pw[slot * np + u] - base;
-                    if ((unsigned)d < 4u) {
-                        const float pv = s_pv[slot * np + u];
-                        v[0] = d == 0 ? pv : v[0];
-                        v[1] = d == 1 ? pv : v[1];
-                        v[2] = d == 2 ? pv : v[2];
-                        v[3] = d == 3 ? pv : v[3];
+                for (int u = 0; u < 4; ++u) {
+                    const int col = col0 + u;
+                    const bool road = in_row && (unsigned)col < (unsigned)W && ((bits >> (col - cmin)) & 1u);
+                    v[u] = road ? 0.0f : -1.0f;
+                }
+                // the segment's patched cells (the nibble table built at staging)
+                const uint32_t sgv = s_seg[slot * Q4 + q];
+                if (sgv) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const uint32_t idx = (sgv >> (4 * u)) & 0xFu;
+                        if (idx) v[u] = s_pv[slot * np + (int)idx - 1];
                     }
                 }
                 o4[j] = make_float4(v[0], v[1], v[2], v[3]);
@@ -267,12 +284,14 @@ unsigned long long *g_patch_dbg = nullptr;
 
 hipError_t launch_windows(const PatchArgs &a, hipStream_t s) {
     const int np = a.N + 1, PP = a.P * a.P;
-    int mode = a.P % 4 == 0 ? 2 : PP <= 64 * MAXPL ? 0 : 1;
+    // MODE 2's nibble table: P <= 32 (32 KB of LDS at most), patch indices 1..15
+    int mode = (a.P % 4 == 0 && a.P <= 32 && np < 16) ? 2 : PP <= 64 * MAXPL ? 0 : 1;
     static const char *force = std::getenv("GW_PATCH_MODE");  // (measurement only: A/B of the writers)
     if (force && (std::atoi(force) == 1 || (std::atoi(force) == 0 && PP <= 64 * MAXPL))) mode = std::atoi(force);
     const size_t lds = sizeof(uint32_t) * ((a.H * a.W + 31) / 32 + PB) + sizeof(int) * 2 * PB * a.K +
                        sizeof(uint32_t) * (size_t)2 * 2 * PB * a.K * np +
-                       (mode == 0 ? sizeof(float) * (size_t)PB * PP : 0);
+                       (mode == 0 ? sizeof(float) * (size_t)PB * PP : 0) +
+                       (mode == 2 ? sizeof(uint16_t) * (size_t)PB * a.K * (PP / 4) : 0);
     const unsigned grid = (unsigned)((a.E + PB - 1) / PB);
     if (mode == 2)
         hipLaunchKernelGGL(window_kernel<2>, dim3(grid), dim3(THREADS), lds, s, a, g_patch_dbg);

@@ -12,7 +12,8 @@ from marlnav.vec_env import VecGridEnv  # noqa: E402
 CASES = [("grid32", 65536, 11), ("grid32", 16384, 11), ("grid32", 4096, 11), ("grid32", 65536, 3),
          ("grid32", 65536, 16), ("grid32", 65536, 20)]
 if len(sys.argv) > 2:
-    CASES = [("grid32", int(sys.argv[1]), int(sys.argv[2]))]
+    CASES = [(sys.argv[3] if len(sys.argv) > 3 and sys.argv[3] != "stamps" else "grid32", int(sys.argv[1]),
+              int(sys.argv[2]))]
 for scen, E, P in CASES:
     env = VecGridEnv(scen, num_envs=E, fear=False, seed=1, obs=False)
     env.reset()
