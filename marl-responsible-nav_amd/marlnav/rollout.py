@@ -19,6 +19,8 @@ The statistics totals are all-reduced across ranks only when read (``totals()``)
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -129,7 +131,8 @@ class ReplayRing:
 class Rollout:
     def __init__(self, env: VecGridEnv, actors: MultiAgentActors | None = None, replay_slots: int = 0,
                  training: bool = True, group=None, seed: int = 0, fused: bool | None = None,
-                 obs_async: bool | str = False, fear_async: bool = False, gather=None, patch: int = 0):
+                 obs_async: bool | str = False, fear_async: bool = False, gather=None, patch: int = 0,
+                 patch_async: bool | None = None):
         """fused: get_action as the one-kernel gw_actor_act over the env's obs descriptors
         (default when the actors are the f32 128-128 MLP), else the PyTorch forward over the
         dense obs with torch's Gumbel noise.
@@ -144,7 +147,10 @@ class Rollout:
         patch > 0: the actors see (and the ring stores) each agent's egocentric patch x patch
         window of its observation (VecGridEnv.obs_patch; an opt-in input format, the reference
         observes the whole grid): actors built for (H, W) = (patch, patch); the env may run
-        with obs=False."""
+        with obs=False.
+        patch_async (default: on for the CNN head, off for the MLP; GW_PATCH_ASYNC=0/1 overrides):
+        with a ring and the fused actor, the window writer runs on a side stream beside the next
+        step's actor (``fence()`` orders the ring slots)."""
         self.env = env
         self.actors = actors
         self.fused = (actors is not None and actors.fusable(env, patch)) if fused is None else bool(fused)
@@ -158,6 +164,21 @@ class Rollout:
             raise ValueError("Rollout(patch=P) needs actors built for a P x P input")
         self.replay = ReplayRing(env, replay_slots, patch=self.patch) if replay_slots else None
         self._patch = None  # the current obs' patches when there is no ring
+        # patch windows into the ring on a side stream: the fused actor of the next step reads the
+        # descriptors, not the windows, so the window writer of step t overlaps actor t+1; the
+        # world update of step t+1 (which rewrites the descriptors) waits for it, and fence()
+        # orders the ring slots for readers (GW_PATCH_ASYNC=0: on the caller's stream)
+        if patch_async is None:  # default: the CNN head (several short kernels the writer fits
+            # beside: c4patch 203 -> 184 us per step); the MLP head's one-block-per-CU actor loses
+            # more CUs to the writer than the overlap hides (c5patch 142 -> 148), profiles/r3_s2
+            env_pa = os.environ.get("GW_PATCH_ASYNC")
+            patch_async = (env_pa != "0") if env_pa is not None else getattr(actors, "arch", "") == "cnn"
+        self.patch_async = (bool(patch_async) and bool(self.patch) and self.fused and self.replay is not None
+                            and env.device.type == "cuda")
+        if self.patch_async:
+            self._pstream = torch.cuda.Stream(device=env.device)
+            self._pev = torch.cuda.Event()
+        self._pev_live = False
         self.distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
         rank = dist.get_rank(group) if self.distributed else 0
         # the PyTorch actor's Gumbel noise: one stream per rank (the fused actor's Philox noise is
@@ -198,15 +219,23 @@ class Rollout:
         if tick is not None:
             tick.add_(1)
 
+    def _patch_join(self):
+        """The current stream waits for the side stream's last window writer."""
+        if self._pev_live:
+            torch.cuda.current_stream(self.env.device).wait_event(self._pev)
+            self._pev_live = False
+
     def fence(self):
         """Order everything written so far (ring slots / env obs, rewards, statistics) before
-        later work on the current stream (a no-op unless obs_async)."""
+        later work on the current stream (a no-op unless obs_async or patch_async)."""
+        self._patch_join()
         self._flush()
         self.env.obs_fence()
 
     def reset(self):
         # the previous step's statistics (and its ring tick) are reduced before the ring's step
         # count restarts, so t_dev never runs ahead of the transitions written
+        self._patch_join()
         self._flush()
         if self.replay is not None:
             obs, mask = self.env.reset()
@@ -232,6 +261,7 @@ class Rollout:
         if rp is None:
             self.reset()
             return
+        self._patch_join()
         self._flush()
         t, S = rp.t, rp.S
         cur, prev = t % S, (t - 1) % S
@@ -282,8 +312,16 @@ class Rollout:
                 into["ep_return"] = g["ep_return"]
                 # done goes to the ring slot and, from the same kernel, to the gather's send buffer
                 into["done_copy"] = g["done"]
+            self._patch_join()  # the previous window writer has read the descriptors
             r = env.step(actions, into=into)
-            if self.patch:  # the step's obs / terminal obs as patches, straight into the ring
+            if self.patch_async:  # the step's windows, beside the next step's actor
+                main = torch.cuda.current_stream(env.device)
+                self._pstream.wait_stream(main)
+                with torch.cuda.stream(self._pstream):
+                    env.obs_patch(self.patch, final=True, out=rp.obs[nxt], final_out=rp.final_obs[cur])
+                self._pev.record(self._pstream)
+                self._pev_live = True
+            elif self.patch:  # the step's obs / terminal obs as patches, straight into the ring
                 env.obs_patch(self.patch, final=True, out=rp.obs[nxt], final_out=rp.final_obs[cur])
             if probs is not None and probs.data_ptr() != rp.probs[cur].data_ptr():
                 rp.probs[cur].copy_(probs)

@@ -99,8 +99,40 @@ def test_fused_patch_rollout_matches_torch_rollout_without_noise():
     for t in range(25):
         r0, r1 = ros[0].step(), ros[1].step()
         assert torch.equal(r0.shaped, r1.shaped) and torch.equal(r0.done, r1.done), t
+        ros[0].fence()  # the fused rollout writes its windows on a side stream (patch_async)
         assert torch.equal(ros[0].replay.obs, ros[1].replay.obs), t
         torch.testing.assert_close(ros[0].replay.probs, ros[1].replay.probs, rtol=0, atol=2e-5)
+    for e in envs:
+        e.close()
+
+
+@pytest.mark.parametrize("scenario,P", [("grid32", 11), ("grid64_n8", 16)])
+def test_async_window_writer_equals_sync(scenario, P):
+    """Rollout(patch=P) with the window writer on a side stream (patch_async, the default) ==
+    the same rollout with the writer on the caller's stream: every ring slot (windows, terminal
+    windows, probs, rewards, dones) after fence(), training mode (Philox noise), a ragged E."""
+    from marlnav.rollout import Rollout
+    sc = S.builtin(scenario)
+    E = 1000
+    envs = [VecGridEnv(sc, num_envs=E, fear=scenario == "grid32", fear_weight=-5.0, seed=9, max_steps=20,
+                       obs=False) for _ in range(2)]
+    actors = _actors(sc.K, P, seed=8) if scenario == "grid32" else MultiAgentActors(sc.K, P, P, "cnn", device="cuda", seed=8)
+    ros = [Rollout(envs[0], actors, replay_slots=5, training=True, seed=4, patch=P, patch_async=True),
+           Rollout(envs[1], actors, replay_slots=5, training=True, seed=4, patch=P, patch_async=False)]
+    assert ros[0].patch_async and not ros[1].patch_async
+    for ro in ros:
+        ro.reset()
+    for t in range(40):
+        for ro in ros:
+            ro.step()
+        if t % 7 == 6 or t == 39:
+            ros[0].fence()
+            a, b = ros[0].replay, ros[1].replay
+            assert torch.equal(a.obs, b.obs) and torch.equal(a.probs, b.probs), t
+            assert torch.equal(a.reward, b.reward) and torch.equal(a.done, b.done), t
+            done = b.done.bool()
+            assert torch.equal(a.final_obs.transpose(1, 2)[done], b.final_obs.transpose(1, 2)[done]), t
+    assert int(ros[1].replay.done.sum()) > 0  # terminal windows were exercised
     for e in envs:
         e.close()
 
