@@ -153,7 +153,12 @@ struct CtabOk {
     __device__ __forceinline__ uint32_t operator()(int c) const { return t[c] >> 21; }
 };
 
-template <int N>
+// LIST (N > 4, the 128-thread step_v2 chain): a collision pass walks this lane's own near pairs
+// (a 64-bit mask, bit 8 ii + jj) and reads the two agents' floor / ceiling / start cells from a
+// per-lane LDS row (`lw`, N uint2), instead of evaluating all N (N - 1) / 2 pairs under lane masks:
+// with 64 envs per wave nearly every pair index has some lane near, so the unrolled form paid the
+// whole pair list on every pass.
+template <int N, bool LIST = false>
 struct World {
     int nal[N][5];
     int loc[N];
@@ -161,6 +166,8 @@ struct World {
     uint32_t two, mv, dir0, dir1;   // bit masks: 2-step action, moving action, direction bits
     uint32_t crash, restr;
     uint32_t near;                  // bit pair(ii, jj): start cells within Manhattan 4
+    uint64_t near8 = 0;             // LIST: bit 8 ii + jj for the same pairs
+    uint2 *lw = nullptr;            // LIST: this lane's LDS row [N] {floor | ceil << 16, start | two << 16}
     // A pair whose start cells are more than 4 apart can never trigger a rule of
     // collision_checks_and_resolution: every sub-path entry stays within 2 of its own start
     // (reverts go back to the start), so equal / crossing cells need distance <= 4.  Such
@@ -182,7 +189,11 @@ struct World {
         for (int ii = 0; ii < N - 1; ++ii)
 #pragma unroll
             for (int jj = ii + 1; jj < N; ++jj)
-                near |= (uint32_t)(abs(rr[ii] - rr[jj]) + abs(cc[ii] - cc[jj]) <= 4) << pair_bit(ii, jj);
+            {
+                const bool nr = abs(rr[ii] - rr[jj]) + abs(cc[ii] - cc[jj]) <= 4;
+                near |= (uint32_t)nr << pair_bit(ii, jj);
+                if (LIST) near8 |= (uint64_t)nr << (8 * ii + jj);
+            }
 #pragma unroll
         for (int i = 0; i < N; ++i) {
             loc[i] = l[i];
@@ -236,7 +247,56 @@ struct World {
     }
 
     template <int S>
+    __device__ __forceinline__ void resolve_list() {  // LIST form of resolve<S>
+        if (near == 0) return;
+#pragma unroll
+        for (int i = 0; i < N; ++i) lw[i].y = (uint32_t)loc[i] | (((two >> i) & 1u) << 16);
+        for (int pass = 0; pass < 2 * N; ++pass) {
+#pragma unroll
+            for (int i = 0; i < N; ++i) lw[i].x = (uint32_t)fl<S>(i) | ((uint32_t)ce<S>(i) << 16);
+            uint32_t hit = 0;
+            uint64_t m = near8;
+            while (m) {  // this lane's near pairs, in ascending (ii, jj) order
+                const int pb = (int)__builtin_ctzll(m);
+                m &= m - 1;
+                const int ii = pb >> 3, jj = pb & 7;
+                const uint2 a = lw[ii], b = lw[jj];
+                const int Af = (int)(a.x & 0xFFFFu), Ac = (int)(a.x >> 16), Li = (int)(a.y & 0xFFFFu);
+                const int Bf = (int)(b.x & 0xFFFFu), Bc = (int)(b.x >> 16), Lj = (int)(b.y & 0xFFFFu);
+                const bool t_i = (a.y >> 16) & 1u, t_j = (b.y >> 16) & 1u;
+                const int ohf_i = t_i ? SubStep<S>::ohf2 : SubStep<S>::ohf1;
+                const int ohc_i = t_i ? SubStep<S>::ohc2 : SubStep<S>::ohc1;
+                const int ohf_j = t_j ? SubStep<S>::ohf2 : SubStep<S>::ohf1;
+                const int ohc_j = t_j ? SubStep<S>::ohc2 : SubStep<S>::ohc1;
+                const bool same_dir = (Ac - Af) == (Bc - Bf);
+                // the elif chain of :276-378 as selects (the N <= 4 form of resolve)
+                const bool x1 = Af == Bc, x2 = Ac == Bf;
+                const bool cross = ((Af == Lj) | (Ac == Lj)) & ((Li == Bf) | (Li == Bc));
+                const bool tail = x1 ? !((ohf_i + ohc_j) <= 4 && same_dir)
+                                     : (x2 ? !((ohf_j + ohc_i) <= 4 && same_dir) : cross);
+                const bool coll = (Af == Bf) | (Ac == Bc) | (x1 & x2) | tail;
+                hit |= coll ? ((1u << ii) | (1u << jj)) : 0u;
+            }
+            crash |= hit;
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                if ((crash >> i) & 1u) {
+                    const int f = ((two >> i) & 1u) ? SubStep<S>::f2 : SubStep<S>::f1;
+#pragma unroll
+                    for (int k = 0; k <= S + 1; ++k)
+                        if (k >= f) nal[i][k] = loc[i];
+                }
+            }
+            if (hit == 0) break;
+        }
+    }
+
+    template <int S>
     __device__ __forceinline__ void resolve() {  // collision_checks_and_resolution :233-405
+        if constexpr (LIST) {
+            resolve_list<S>();
+            return;
+        }
         if (near == 0) return;  // no pair can collide: every pass counts 0 (crash stays 0)
         for (int pass = 0; pass < 2 * N; ++pass) {
             uint32_t hit = 0;
@@ -301,8 +361,8 @@ struct World {
 // UpdateGWorld (grid_world.py:424-563).  caught: bits 0-7 = eaters k that stood on apple[k] at
 // some sub-step (floor position, :530-545); bits 8+ = the number of (k, apple) entries the
 // reference appends to apples_caught (the single-agent env rewards only len == 1).
-template <int N, bool APPLES, class OK>
-__device__ __forceinline__ void simulate(World<N> &w, const OK &okm, int K,
+template <int N, bool APPLES, class OK, bool LIST>
+__device__ __forceinline__ void simulate(World<N, LIST> &w, const OK &okm, int K,
                                          const int (&apple)[MAXN], uint32_t &caught, int (&fin)[N]) {
     caught = 0;
     w.template move<0, OK>(okm);
@@ -1294,6 +1354,7 @@ struct alignas(16) V2Shared {
     uint16_t pc[2][OB][KMAX][NP];
     float pv[2][OB][KMAX][NP];
     uint32_t eflag[OB];
+    uint2 wl[(!FEAR && N > 4) ? Cfg::THREADS * N : 1];  // World<N, true> rows of the FeAR-off chain
     int8_t xact[Cfg::XDRAW ? BE : 1][N];   // FeAR off: the (env, agent) threads' action draws and MdRs
     int8_t xmdr[Cfg::XDRAW ? BE : 1][N];
     int nbase, ngroup;  // base-sim entries after the env sims; counterfactual groups
@@ -1716,8 +1777,10 @@ __device__ __forceinline__ void step_v2_block(const Params &p, int64_t bid, V2Sh
             int apple[MAXN];
 #pragma unroll
             for (int k = 0; k < MAXN; ++k) apple[k] = (k < K && ((es.flags >> k) & 1u)) ? p.apples[k] : -1;
-            World<N> w;
+            constexpr bool LIST = N > 4;
+            World<N, LIST> w;
             w.init(pos, act, p.W, p.w_magic);
+            if constexpr (LIST) w.lw = &sh.wl[tid * N];
             uint32_t caught;
             simulate<N, true>(w, okv, K, apple, caught, fin);
 #ifdef GW_STEP_CLK
