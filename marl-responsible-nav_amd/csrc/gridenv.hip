@@ -1306,6 +1306,9 @@ __global__ void __launch_bounds__(OBS_THREADS) obs_kernel(Params p, float *__res
 // cell table bits
 constexpr uint32_t CT_POL = 0, CT_MDR = 8, CT_AMASK = 12, CT_OK = 21, CT_ROAD = 25;
 
+#ifndef GW_LIST_MIN_N  // the FeAR-off chain's world update walks per-lane near-pair lists from this N on
+#define GW_LIST_MIN_N 5
+#endif
 #ifndef GW_NOFEAR_BE  // envs per block of the FeAR-off step_v2 with N <= 4 (measurement builds: 16)
 #define GW_NOFEAR_BE 32
 #endif
@@ -1354,7 +1357,7 @@ struct alignas(16) V2Shared {
     uint16_t pc[2][OB][KMAX][NP];
     float pv[2][OB][KMAX][NP];
     uint32_t eflag[OB];
-    uint2 wl[(!FEAR && N > 4) ? Cfg::THREADS * N : 1];  // World<N, true> rows of the FeAR-off chain
+    uint2 wl[(!FEAR && N >= GW_LIST_MIN_N) ? Cfg::THREADS * N : 1];  // World<N, true> rows of the FeAR-off chain
     int8_t xact[Cfg::XDRAW ? BE : 1][N];   // FeAR off: the (env, agent) threads' action draws and MdRs
     int8_t xmdr[Cfg::XDRAW ? BE : 1][N];
     int nbase, ngroup;  // base-sim entries after the env sims; counterfactual groups
@@ -1777,7 +1780,7 @@ __device__ __forceinline__ void step_v2_block(const Params &p, int64_t bid, V2Sh
             int apple[MAXN];
 #pragma unroll
             for (int k = 0; k < MAXN; ++k) apple[k] = (k < K && ((es.flags >> k) & 1u)) ? p.apples[k] : -1;
-            constexpr bool LIST = N > 4;
+            constexpr bool LIST = N >= GW_LIST_MIN_N;
             World<N, LIST> w;
             w.init(pos, act, p.W, p.w_magic);
             if constexpr (LIST) w.lw = &sh.wl[tid * N];
