@@ -1357,7 +1357,7 @@ struct alignas(16) V2Shared {
     uint16_t pc[2][OB][KMAX][NP];
     float pv[2][OB][KMAX][NP];
     uint32_t eflag[OB];
-    uint2 wl[(!FEAR && N >= GW_LIST_MIN_N) ? Cfg::THREADS * N : 1];  // World<N, true> rows of the FeAR-off chain
+    uint2 wl[(N >= GW_LIST_MIN_N) ? Cfg::THREADS * N : 1];  // World<N, true> rows (one per thread)
     int8_t xact[Cfg::XDRAW ? BE : 1][N];   // FeAR off: the (env, agent) threads' action draws and MdRs
     int8_t xmdr[Cfg::XDRAW ? BE : 1][N];
     int nbase, ngroup;  // base-sim entries after the env sims; counterfactual groups
@@ -1518,8 +1518,10 @@ __device__ __forceinline__ void fear_task(const Params &p, Sh &sh, uint32_t tk, 
     int apple[MAXN];
 #pragma unroll
     for (int q = 0; q < MAXN; ++q) apple[q] = -1;
-    World<N> w;
+    constexpr bool LIST = N >= GW_LIST_MIN_N;  // a wave's sims belong to different envs
+    World<N, LIST> w;
     w.init(pos, joint, p.W, p.w_magic);
+    if constexpr (LIST) w.lw = &sh.wl[threadIdx.x * N];
     uint32_t caught;
     simulate<N, true>(w, okv, 0, apple, caught, fin);
     const uint32_t valid = ~(w.crash | w.restr) & ((1u << N) - 1u);
@@ -1704,8 +1706,10 @@ __device__ __forceinline__ void step_v2_block(const Params &p, int64_t bid, V2Sh
                         if (n == j) joint[n] = b;
                 }
             }
-            World<N> w;
+            constexpr bool LIST = N >= GW_LIST_MIN_N;
+            World<N, LIST> w;
             w.init(pos, joint, p.W, p.w_magic);
+            if constexpr (LIST) w.lw = &sh.wl[tid * N];
             uint32_t caught;
             simulate<N, true>(w, okv, nk, apple, caught, fin);
             if (ti < BE) {
