@@ -221,7 +221,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--updates-per-step", type=int, default=0,
                     help="c5 only: MADDPG updates (batch 128, one HIP-graph replay each) per env step")
-    ap.add_argument("--profile-steps", type=int, default=16,
+    ap.add_argument("--profile-steps", type=int, default=64,
                     help="after the timed region, time this many more steps' kernels with HIP events "
                          "carried by their launches (the live roofline; 0 = none)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
