@@ -284,14 +284,18 @@ unsigned long long *g_patch_dbg = nullptr;
 
 hipError_t launch_windows(const PatchArgs &a, hipStream_t s) {
     const int np = a.N + 1, PP = a.P * a.P;
-    // MODE 2's nibble table: P <= 32 (32 KB of LDS at most), patch indices 1..15
-    int mode = (a.P % 4 == 0 && a.P <= 32 && np < 16) ? 2 : PP <= 64 * MAXPL ? 0 : 1;
+    // LDS: road bitmask, flags, centres, patch cells + values; MODE 0 adds one agent's window run,
+    // MODE 2 its nibble table (PB * K * P * P / 4 u16, patch indices 1..15).  A mode is taken only
+    // if its LDS fits the 64 KB a launch gets without an attribute (else the per-element writer).
+    const size_t base = sizeof(uint32_t) * ((a.H * a.W + 31) / 32 + PB) + sizeof(int) * 2 * PB * a.K +
+                        sizeof(uint32_t) * (size_t)2 * 2 * PB * a.K * np;
+    const size_t extra[3] = {sizeof(float) * (size_t)PB * PP, 0, sizeof(uint16_t) * (size_t)PB * a.K * (PP / 4)};
+    constexpr size_t LDS_MAX = 64 * 1024;
+    int mode = (a.P % 4 == 0 && np < 16 && base + extra[2] <= LDS_MAX) ? 2
+               : (PP <= 64 * MAXPL && base + extra[0] <= LDS_MAX) ? 0 : 1;
     static const char *force = std::getenv("GW_PATCH_MODE");  // (measurement only: A/B of the writers)
     if (force && (std::atoi(force) == 1 || (std::atoi(force) == 0 && PP <= 64 * MAXPL))) mode = std::atoi(force);
-    const size_t lds = sizeof(uint32_t) * ((a.H * a.W + 31) / 32 + PB) + sizeof(int) * 2 * PB * a.K +
-                       sizeof(uint32_t) * (size_t)2 * 2 * PB * a.K * np +
-                       (mode == 0 ? sizeof(float) * (size_t)PB * PP : 0) +
-                       (mode == 2 ? sizeof(uint16_t) * (size_t)PB * a.K * (PP / 4) : 0);
+    const size_t lds = base + extra[mode];
     const unsigned grid = (unsigned)((a.E + PB - 1) / PB);
     if (mode == 2)
         hipLaunchKernelGGL(window_kernel<2>, dim3(grid), dim3(THREADS), lds, s, a, g_patch_dbg);
