@@ -78,6 +78,35 @@ def algorithmic_bytes(N: int, K: int, HW: int, obs_bytes: int = 4):
     return step_b, obs_b
 
 
+# gw_profile span kinds (include/gridenv.h GW_SPAN_*) -> the kernel names of bench lines / rocprofv3
+SPAN_KINDS = {0: "step_kernel", 1: "obs_kernel", 2: "fear_kernel", 3: "act_kernel", 4: "cnn_l1_kernel",
+              5: "cnn_list_kernels", 6: "cnn_rare_kernel", 7: "window_kernel"}
+F32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: dense f32 MFMA (v_mfma_f32_16x16x4_f32), no xf32 on gfx950
+HID, N_ACT = 128, 9        # the fused actors' hidden width and actions (configs/mlp.yaml, configs/cnn.yaml)
+
+
+def kernel_work(kind: int, N: int, K: int, HW: int, E: int, obs_bytes: int = 4, patch: int = 0):
+    """(bound, algorithmic work per step of one GW_SPAN kind, unit) for the roofline:
+    HBM bytes for the env / writer kernels, f32 MFMA flops for the fused
+    actors' MLP kernel (DESIGN.md §5.4: layers 2-3, 2 * (128 * 128 + 128 * 9) per (env, agent);
+    its layer 1 is a gather of table rows, not a GEMM).  None where the work is data-dependent
+    (the CNN recompute: a few positions per step)."""
+    step_b, obs_b = algorithmic_bytes(N, K, HW, obs_bytes)
+    if kind == 0:
+        return "hbm", step_b * E, "B"
+    if kind == 1:
+        return "hbm", obs_b * E, "B"
+    if kind == 2:  # FearRec 16 read, score / fear_score read + written, fear / shaped, ep_return / ep_fear
+        return "hbm", (16 + 32 + 16 * K + 16) * E, "B"
+    if kind == 3:
+        return "mfma", 2 * E * K * (HID * HID + HID * N_ACT), "flop"
+    if kind in (4, 5):  # descriptors read + a per-(env, agent) word of positions / list entries
+        return "hbm", (48 + 4 * K) * E, "B"
+    if kind == 7:  # the windows written (f32) + the 48-byte descriptors read
+        return "hbm", (4 * K * patch * patch + 48) * E, "B"
+    return "mfma", None, "flop"
+
+
 def host_cpus():
     """What the host offers this job: the machine's logical CPUs, the ones this process may run
     on (affinity), the cgroup CPU quota (cpu.max) and the CPU model (lscpu / /proc/cpuinfo)."""
@@ -444,7 +473,7 @@ def main():
     n_graph = args.steps - args.steps % graph_n if graph_n else 0
 
     if n_prof:  # the profiling events exist before they are used (gw_profile creates them)
-        env.profile(True, reserve=8 * (n_prof + 2))
+        env.profile(True, reserve=16 * (n_prof + 2))
         env.profile(False)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
@@ -504,33 +533,61 @@ def main():
         # mean launch duration when launches do not overlap; with the obs writers of consecutive
         # steps overlapping on two streams a launch's own span covers part of its
         # neighbours' work, and the busy time is what a launch costs the timeline
-        busy = {k: busy_ms(spans, k) if spans is not None and len(spans) else (0.0, 0) for k in (0, 1, 2)}
+        busy = {k: busy_ms(spans, k) if spans is not None and len(spans) else (0.0, 0) for k in SPAN_KINDS}
         busy_step_ms, busy_obs_ms = (busy[k][0] / max(busy[k][1], 1) for k in (0, 1))
         fused = env.fused
         merged = env.kernel_path == "merged" and bool(obs_mode)
+        obs_bytes = 2 if args.obs_dtype == "bf16" else 4
+        # every kernel kind's busy time per profiled step (the union of its launches' intervals /
+        # steps: overlapping launches of one kind count once) and its roofline
+        per_kind = {}
+        for k, name in SPAN_KINDS.items():
+            tot, n = busy[k]
+            if not n:
+                continue
+            bound, work, unit = kernel_work(k, N, K, HW, E, obs_bytes, cfg.get("patch", 0))
+            ms = tot / max(nprof, 1)
+            peak = F32_MFMA_PEAK_TFS * 1e3 if bound == "mfma" else HBM_PEAK_GBS
+            rate = work / (ms * 1e-3) / 1e9 if (work and ms > 0) else None  # GB/s or GFLOP/s
+            per_kind[name] = {"busy_ms_per_step": ms, "launches_per_step": n / max(nprof, 1), "bound": bound,
+                              "work_per_step": work, "work_unit": unit,
+                              "achieved": rate / 1e3 if (rate and bound == "mfma") else rate,
+                              "frac": rate / peak if rate else None}
         if fused:  # one launch per step moves every byte of the step
             dom, bytes_per_launch, span, dur = "step_fused", (step_b + obs_b) * E, avg_step_ms, busy_step_ms
         elif merged:  # step_obs: step t + the obs writer of step t-1 in one launch (its spans: kind 1)
             dom, bytes_per_launch, span, dur = "step_obs", (step_b + obs_b) * E, avg_obs_ms, busy_obs_ms
-        elif busy_obs_ms >= busy_step_ms:
-            dom, bytes_per_launch, span, dur = "obs_kernel", obs_b * E, avg_obs_ms, busy_obs_ms
-        else:
-            dom, bytes_per_launch, span, dur = "step_kernel", step_b * E, avg_step_ms, busy_step_ms
-        achieved = bytes_per_launch / (dur * 1e-3) / 1e9 if dur > 0 else None
+        else:  # the kernel kind with the largest busy time per step
+            dom = max(per_kind, key=lambda n: per_kind[n]["busy_ms_per_step"]) if per_kind else "obs_kernel"
+            kd = next(k for k, n in SPAN_KINDS.items() if n == dom)
+            _, bytes_per_launch, _ = kernel_work(kd, N, K, HW, E, obs_bytes, cfg.get("patch", 0))
+            launches = busy[kd][1] / max(nprof, 1)  # launches (spans) of the kind per step
+            dur = per_kind[dom]["busy_ms_per_step"] / max(launches, 1e-9) if per_kind else busy_obs_ms
+            if bytes_per_launch is not None:
+                bytes_per_launch = bytes_per_launch / max(launches, 1e-9)
+            span = {0: avg_step_ms, 1: avg_obs_ms, 2: avg_fear_ms}.get(kd, dur)
+        dom_bound = per_kind.get(dom, {}).get("bound", "hbm")
+        mfma = dom_bound == "mfma"
+        peak_u = F32_MFMA_PEAK_TFS if mfma else HBM_PEAK_GBS
+        # achieved: GB/s (hbm) or TFLOP/s (mfma) of the dominant kernel's algorithmic work per launch
+        # over its busy time per launch
+        achieved = (bytes_per_launch / (dur * 1e-3) / (1e12 if mfma else 1e9)) if (dur > 0 and bytes_per_launch) else None
         traffic, traffic_src, prof_frac = None, None, None
         try:  # HBM bytes measured by the PMC passes committed under profiles/ for this workload
             with open(os.path.join(REPO, "profiles", "latest.json")) as f:
                 prof = json.load(f)
-            if prof.get("config") == args.config and not args.envs and args.fear < 0 and not fused \
-                    and dom in prof["kernels"] \
+            pc = prof.get("configs", {}).get(args.config)
+            if pc and not args.envs and args.fear < 0 and not fused and dom in pc["kernels"] \
                     and args.obs_dtype == "f32":
-                traffic = prof["kernels"][dom]["hbm_bytes_per_launch"]
-                traffic_src = prof["source"]
+                pk = pc["kernels"][dom]
+                traffic = pk.get("hbm_bytes_per_launch")
+                traffic_src = pc["source"]
                 # the same kernel's rocprofv3 busy time per launch (union of its launches'
                 # intervals in the kernel trace / launches) for comparison
-                pk = prof["kernels"][dom]
-                prof_frac = bytes_per_launch / (pk.get("busy_us", pk["avg_us"]) * 1e-6) / 1e9 / HBM_PEAK_GBS
-        except (OSError, KeyError, ValueError):
+                if bytes_per_launch:
+                    prof_frac = bytes_per_launch / (pk.get("busy_us", pk["avg_us"]) * 1e-6) / \
+                        (1e12 if mfma else 1e9) / peak_u
+        except (OSError, KeyError, ValueError, TypeError):
             pass
         total_units = world * E * N * args.steps
         line = {
@@ -549,17 +606,20 @@ def main():
             "config": {"workload": cfg["workload"], "scenario": cfg["scenario"], "envs_per_gpu": E,
                        "global_envs": world * E, "agents": N, "rl_agents": K, "grid": [env.H, env.W],
                        "fear": cfg["fear"], "parallelism": f"env-sharded dp{world}", "obs_dtype": args.obs_dtype},
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
-                         "traffic_source": traffic_src, "frac_rocprof": prof_frac,
-                         "bytes_per_launch": bytes_per_launch,
-                         # achieved = bytes_per_launch / avg_launch_ms, the kernel's busy time per
-                         # launch (see busy_ms); avg_launch_span_ms = the launches' own mean
-                         # duration, which overlapping writers stretch (the per-span figure
-                         # beside it is the lower, per-launch view)
+            "roofline": {"bound": dom_bound, "kernel": dom, "achieved": achieved, "peak": peak_u,
+                         "unit": "TFLOP/s" if mfma else "GB/s", "frac": achieved / peak_u if achieved else None,
+                         "traffic": traffic, "traffic_source": traffic_src, "frac_rocprof": prof_frac,
+                         "bytes_per_launch": None if mfma else bytes_per_launch,
+                         "flops_per_launch": bytes_per_launch if mfma else None,
+                         # achieved = the algorithmic work per launch / avg_launch_ms, the kernel's busy
+                         # time per launch (see busy_ms); avg_launch_span_ms = the launches' own mean
+                         # duration, which overlapping writers stretch (the per-span figure beside it
+                         # is the lower, per-launch view)
                          "avg_launch_ms": dur, "avg_launch_span_ms": span,
-                         "frac_per_launch_span": bytes_per_launch / (span * 1e-3) / 1e9 / HBM_PEAK_GBS if span > 0 else None,
-                         "launches_profiled": busy[1 if dom in ("obs_kernel", "step_obs") else 0][1],
+                         "frac_per_launch_span": (bytes_per_launch / (span * 1e-3) / (1e12 if mfma else 1e9) / peak_u
+                                                  if (span and span > 0 and bytes_per_launch) else None),
+                         "launches_profiled": busy[1 if dom in ("obs_kernel", "step_obs") else
+                                                   next((k for k, n in SPAN_KINDS.items() if n == dom), 0)][1],
                          # every algorithmic byte of a whole step (state + obs) over the wall time
                          # per step: what the pipelined steps sustain end to end
                          "step_level_GBps": (step_b + obs_b) * E / (t_max / args.steps) / 1e9,
@@ -568,8 +628,12 @@ def main():
                          # the dominant kernel's bytes per launch over the launch PERIOD (= the
                          # stream time per step) is its sustained rate
                          "writers_overlap": n_ring > 1 and bool(obs_mode) and env.kernel_path == "defer",
-                         "achieved_per_period": bytes_per_launch / (gpu_ms / args.steps * 1e-3) / 1e9,
-                         "frac_per_period": bytes_per_launch / (gpu_ms / args.steps * 1e-3) / 1e9 / HBM_PEAK_GBS},
+                         "achieved_per_period": (bytes_per_launch / (gpu_ms / args.steps * 1e-3) /
+                                                 (1e12 if mfma else 1e9)) if bytes_per_launch else None,
+                         "frac_per_period": (bytes_per_launch / (gpu_ms / args.steps * 1e-3) / (1e12 if mfma else 1e9) /
+                                             peak_u) if bytes_per_launch else None,
+                         # every profiled kernel kind: busy time per step and its own roofline
+                         "kernels": per_kind},
             "kernels_ms": {"profiled_steps": nprof, "step_kernel": avg_step_ms, "obs_kernel": avg_obs_ms, "fear_kernel": avg_fear_ms,
                            "kernel_path": env.kernel_path,
                            "stream_ms_per_step": gpu_ms / args.steps,

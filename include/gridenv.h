@@ -140,18 +140,27 @@ gw_status gw_state_view(void *env, gw_state *out);
  * gw_state layout (device or pinned host memory), enqueued on stream. */
 gw_status gw_copy_state(void *env, const gw_state *buf, int to_env, void *stream);
 
-/* Per-launch timing: while enabled, gw_step's kernels carry HIP timing events in their
- * dispatch (start / stop of the launch itself, on the stream each is launched on): [0] the
- * world-update kernel (step_v2), [1] the obs writer (obs_kernel; the merged path's step_obs),
- * [2] the deferred FeAR kernel (fear_v2, GW_KERNEL=defer only; it runs concurrently with [1]).
+/* Per-launch timing: while enabled, the env's kernels carry HIP timing events in their dispatch
+ * (start / stop of the launch itself, on the stream each is launched on), one span per launch
+ * group of a kind: GW_SPAN_STEP the world-update kernel (step_v2), GW_SPAN_OBS the obs writer
+ * (obs_kernel; the merged path's step_obs), GW_SPAN_FEAR the deferred FeAR kernel (fear_v2,
+ * GW_KERNEL=defer only; it runs concurrently with the writer), and the ops that take this env's
+ * handle: GW_SPAN_ACT the fused actors' MLP kernel (act_kernel of gw_actor_act,
+ * gw_patch_actor_act, gw_cnn_act, gw_patch_cnn_act), GW_SPAN_CNN_L1 the CNN heads' layer-1
+ * listing kernel, GW_SPAN_CNN_LIST their bucket scan / plan / scatter (three launches), GW_SPAN_CNN_RARE
+ * their recompute of the listed conv positions, GW_SPAN_WINDOW the window writer (gw_obs_patch).
  * enable > 1 also makes sure `enable` timing events exist now (creating them inside a profiled
  * step would put their host cost between its launches).  gw_profile_read synchronises on those
- * events, returns the summed elapsed milliseconds per kernel and the number of gw_step calls
- * timed, and clears them.  Used by bench.py for the live roofline. */
+ * events, returns the summed elapsed milliseconds of the first three kinds and the number of
+ * gw_step calls timed, and clears every span.  Used by bench.py for the live roofline. */
+enum {
+    GW_SPAN_STEP = 0, GW_SPAN_OBS = 1, GW_SPAN_FEAR = 2, GW_SPAN_ACT = 3, GW_SPAN_CNN_L1 = 4,
+    GW_SPAN_CNN_LIST = 5, GW_SPAN_CNN_RARE = 6, GW_SPAN_WINDOW = 7
+};
 gw_status gw_profile(void *env, int enable);
 gw_status gw_profile_read(void *env, double out_ms[3], int64_t *n_steps);
 /* The spans gw_profile_read would sum, one by one (call it first: gw_profile_read clears them):
- * out[3 i + 0] = kind (0 world update, 1 obs writer, 2 FeAR), out[3 i + 1] / [3 i + 2] = the
+ * out[3 i + 0] = kind (GW_SPAN_*), out[3 i + 1] / [3 i + 2] = the
  * launch's start / end in milliseconds after the first span's start; at most cap spans are
  * written, *n_spans = how many exist.  Synchronises on their events.  bench.py merges the obs
  * writers' intervals (writers of consecutive steps overlap on two streams) into the writer's

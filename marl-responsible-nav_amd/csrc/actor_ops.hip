@@ -41,6 +41,7 @@
 #include <string>
 
 #include "actor_ops.h"
+#include "prof.h"
 
 namespace {
 
@@ -1713,16 +1714,17 @@ gw_status actor_act(const char *who, void *env, int32_t P, const gw_mlp_actors *
     const int per_agent = (int)std::max<int64_t>(1, std::min<int64_t>(want, std::max(1, resident / src.K)));
     const dim3 grid(per_agent, src.K), block(64 * waves);
     hipStream_t s = static_cast<hipStream_t>(stream);
+    gwprof::Span span(env, GW_SPAN_ACT);
 #define ACT_LAUNCH(NP)                                                                   \
     do {                                                                                 \
         if (P > 0)                                                                       \
-            hipLaunchKernelGGL((act_kernel<NP, 16, true, false, true>), grid, block, 0, s, p); \
+            gwprof::launch(act_kernel<NP, 16, true, false, true>, grid, block, 0, s, p); \
         else if (v == 0)                                                                 \
-            hipLaunchKernelGGL((act_kernel<NP, 8>), grid, block, 0, s, p);               \
+            gwprof::launch(act_kernel<NP, 8>, grid, block, 0, s, p);                     \
         else if (v == 4)                                                                 \
-            hipLaunchKernelGGL((act_kernel<NP, 16, true>), grid, block, 0, s, p);        \
+            gwprof::launch(act_kernel<NP, 16, true>, grid, block, 0, s, p);              \
         else                                                                             \
-            hipLaunchKernelGGL((act_kernel<NP, 16>), grid, block, 0, s, p);              \
+            gwprof::launch(act_kernel<NP, 16>, grid, block, 0, s, p);                    \
     } while (0)
     switch (src.N) {
         case 1: ACT_LAUNCH(2); break;
@@ -1839,30 +1841,39 @@ gw_status gw_cnn_act(void *env, const gw_cnn_actors *net, const float *ws, int t
     const int64_t tiles = (src.E + TILE - 1) / TILE;
     const Lists lists = lists_at(cp.ws.unit_off, src.K * cp.P, src.K, src.E, L1_ENVS);
     const dim3 lgrid((unsigned)lists.nblk, src.K);
-    switch (src.N) {
-        case 1: hipLaunchKernelGGL(cnn_l1_kernel<2>, lgrid, dim3(64 * L1_WAVES), 0, s, cp, lists); break;
-        case 2: hipLaunchKernelGGL(cnn_l1_kernel<3>, lgrid, dim3(64 * L1_WAVES), 0, s, cp, lists); break;
-        case 3: hipLaunchKernelGGL(cnn_l1_kernel<4>, lgrid, dim3(64 * L1_WAVES), 0, s, cp, lists); break;
-        case 4: hipLaunchKernelGGL(cnn_l1_kernel<5>, lgrid, dim3(64 * L1_WAVES), 0, s, cp, lists); break;
-        case 5: hipLaunchKernelGGL(cnn_l1_kernel<6>, lgrid, dim3(64 * L1_WAVES), 0, s, cp, lists); break;
-        case 6: hipLaunchKernelGGL(cnn_l1_kernel<7>, lgrid, dim3(64 * L1_WAVES), 0, s, cp, lists); break;
-        case 7: hipLaunchKernelGGL(cnn_l1_kernel<8>, lgrid, dim3(64 * L1_WAVES), 0, s, cp, lists); break;
-        case 8: hipLaunchKernelGGL(cnn_l1_kernel<9>, lgrid, dim3(64 * L1_WAVES), 0, s, cp, lists); break;
-        default: return err(GW_ERR_ARG, "gw_cnn_act: N out of range");
+    {
+        gwprof::Span span(env, GW_SPAN_CNN_L1);
+        switch (src.N) {
+            case 1: gwprof::launch(cnn_l1_kernel<2>, lgrid, dim3(64 * L1_WAVES), 0, s, cp, lists); break;
+            case 2: gwprof::launch(cnn_l1_kernel<3>, lgrid, dim3(64 * L1_WAVES), 0, s, cp, lists); break;
+            case 3: gwprof::launch(cnn_l1_kernel<4>, lgrid, dim3(64 * L1_WAVES), 0, s, cp, lists); break;
+            case 4: gwprof::launch(cnn_l1_kernel<5>, lgrid, dim3(64 * L1_WAVES), 0, s, cp, lists); break;
+            case 5: gwprof::launch(cnn_l1_kernel<6>, lgrid, dim3(64 * L1_WAVES), 0, s, cp, lists); break;
+            case 6: gwprof::launch(cnn_l1_kernel<7>, lgrid, dim3(64 * L1_WAVES), 0, s, cp, lists); break;
+            case 7: gwprof::launch(cnn_l1_kernel<8>, lgrid, dim3(64 * L1_WAVES), 0, s, cp, lists); break;
+            case 8: gwprof::launch(cnn_l1_kernel<9>, lgrid, dim3(64 * L1_WAVES), 0, s, cp, lists); break;
+            default: return err(GW_ERR_ARG, "gw_cnn_act: N out of range");
+        }
     }
-    hipLaunchKernelGGL(bucket_scan, dim3((src.K * cp.P + 15) / 16), dim3(1024), 0, s, cp, lists);
-    hipLaunchKernelGGL(cnn_rare_plan, dim3(1), dim3(1024), 0, s, cp);
-    hipLaunchKernelGGL(cnn_scatter, lgrid, dim3(L1_ENVS), 0, s, cp, lists);
-#define RARE(NP) hipLaunchKernelGGL(cnn_rare_kernel<NP>, dim3(RARE_BLOCKS), dim3(64 * RARE_WAVES), 0, s, cp)
-    switch (src.N) {
-        case 1: RARE(2); break;
-        case 2: RARE(3); break;
-        case 3: RARE(4); break;
-        case 4: RARE(5); break;
-        case 5: RARE(6); break;
-        case 6: RARE(7); break;
-        case 7: RARE(8); break;
-        default: RARE(9); break;
+    {
+        gwprof::Span span(env, GW_SPAN_CNN_LIST);
+        gwprof::launch(bucket_scan, dim3((src.K * cp.P + 15) / 16), dim3(1024), 0, s, cp, lists);
+        gwprof::launch(cnn_rare_plan, dim3(1), dim3(1024), 0, s, cp);
+        gwprof::launch(cnn_scatter, lgrid, dim3(L1_ENVS), 0, s, cp, lists);
+    }
+#define RARE(NP) gwprof::launch(cnn_rare_kernel<NP>, dim3(RARE_BLOCKS), dim3(64 * RARE_WAVES), 0, s, cp)
+    {
+        gwprof::Span span(env, GW_SPAN_CNN_RARE);
+        switch (src.N) {
+            case 1: RARE(2); break;
+            case 2: RARE(3); break;
+            case 3: RARE(4); break;
+            case 4: RARE(5); break;
+            case 5: RARE(6); break;
+            case 6: RARE(7); break;
+            case 7: RARE(8); break;
+            default: RARE(9); break;
+        }
     }
 #undef RARE
     ActParams p;
@@ -1902,7 +1913,10 @@ gw_status gw_cnn_act(void *env, const gw_cnn_actors *net, const float *ws, int t
     p.tiles = (int)tiles;
     const int64_t want = (tiles + 15) / 16;
     const int per_agent = (int)std::max<int64_t>(1, std::min<int64_t>(want, std::max(1, 256 / src.K)));
-    hipLaunchKernelGGL((act_kernel<2, 16, true, true>), dim3(per_agent, src.K), dim3(1024), 0, s, p);
+    {
+        gwprof::Span span(env, GW_SPAN_ACT);
+        gwprof::launch(act_kernel<2, 16, true, true>, dim3(per_agent, src.K), dim3(1024), 0, s, p);
+    }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return err(GW_ERR_HIP, std::string("gw_cnn_act: ") + hipGetErrorString(e));
     return GW_OK;
@@ -1978,30 +1992,39 @@ gw_status gw_patch_cnn_act(void *env, int32_t P, const gw_cnn_actors *net, const
     hipStream_t s = static_cast<hipStream_t>(stream);
     const Lists lists = lists_at(cp.ws.unit_off, src.K * cp.P, src.K, src.E, 256);
     const dim3 lgrid((unsigned)lists.nblk, src.K);
-    switch (src.N) {
-        case 1: hipLaunchKernelGGL(wcnn_l1_kernel<2>, lgrid, dim3(256), 0, s, cp, lists); break;
-        case 2: hipLaunchKernelGGL(wcnn_l1_kernel<3>, lgrid, dim3(256), 0, s, cp, lists); break;
-        case 3: hipLaunchKernelGGL(wcnn_l1_kernel<4>, lgrid, dim3(256), 0, s, cp, lists); break;
-        case 4: hipLaunchKernelGGL(wcnn_l1_kernel<5>, lgrid, dim3(256), 0, s, cp, lists); break;
-        case 5: hipLaunchKernelGGL(wcnn_l1_kernel<6>, lgrid, dim3(256), 0, s, cp, lists); break;
-        case 6: hipLaunchKernelGGL(wcnn_l1_kernel<7>, lgrid, dim3(256), 0, s, cp, lists); break;
-        case 7: hipLaunchKernelGGL(wcnn_l1_kernel<8>, lgrid, dim3(256), 0, s, cp, lists); break;
-        case 8: hipLaunchKernelGGL(wcnn_l1_kernel<9>, lgrid, dim3(256), 0, s, cp, lists); break;
-        default: return err(GW_ERR_ARG, "gw_patch_cnn_act: N out of range");
+    {
+        gwprof::Span span(env, GW_SPAN_CNN_L1);
+        switch (src.N) {
+            case 1: gwprof::launch(wcnn_l1_kernel<2>, lgrid, dim3(256), 0, s, cp, lists); break;
+            case 2: gwprof::launch(wcnn_l1_kernel<3>, lgrid, dim3(256), 0, s, cp, lists); break;
+            case 3: gwprof::launch(wcnn_l1_kernel<4>, lgrid, dim3(256), 0, s, cp, lists); break;
+            case 4: gwprof::launch(wcnn_l1_kernel<5>, lgrid, dim3(256), 0, s, cp, lists); break;
+            case 5: gwprof::launch(wcnn_l1_kernel<6>, lgrid, dim3(256), 0, s, cp, lists); break;
+            case 6: gwprof::launch(wcnn_l1_kernel<7>, lgrid, dim3(256), 0, s, cp, lists); break;
+            case 7: gwprof::launch(wcnn_l1_kernel<8>, lgrid, dim3(256), 0, s, cp, lists); break;
+            case 8: gwprof::launch(wcnn_l1_kernel<9>, lgrid, dim3(256), 0, s, cp, lists); break;
+            default: return err(GW_ERR_ARG, "gw_patch_cnn_act: N out of range");
+        }
     }
-    hipLaunchKernelGGL(bucket_scan, dim3((src.K * cp.P + 15) / 16), dim3(1024), 0, s, cp, lists);
-    hipLaunchKernelGGL(cnn_rare_plan, dim3(1), dim3(1024), 0, s, cp);
-    hipLaunchKernelGGL(wcnn_scatter, lgrid, dim3(256), 0, s, cp, lists);
-#define RARE(NP) hipLaunchKernelGGL(wcnn_rare_kernel<NP>, dim3(RARE_BLOCKS), dim3(64 * RARE_WAVES), 0, s, cp)
-    switch (src.N) {
-        case 1: RARE(2); break;
-        case 2: RARE(3); break;
-        case 3: RARE(4); break;
-        case 4: RARE(5); break;
-        case 5: RARE(6); break;
-        case 6: RARE(7); break;
-        case 7: RARE(8); break;
-        default: RARE(9); break;
+    {
+        gwprof::Span span(env, GW_SPAN_CNN_LIST);
+        gwprof::launch(bucket_scan, dim3((src.K * cp.P + 15) / 16), dim3(1024), 0, s, cp, lists);
+        gwprof::launch(cnn_rare_plan, dim3(1), dim3(1024), 0, s, cp);
+        gwprof::launch(wcnn_scatter, lgrid, dim3(256), 0, s, cp, lists);
+    }
+#define RARE(NP) gwprof::launch(wcnn_rare_kernel<NP>, dim3(RARE_BLOCKS), dim3(64 * RARE_WAVES), 0, s, cp)
+    {
+        gwprof::Span span(env, GW_SPAN_CNN_RARE);
+        switch (src.N) {
+            case 1: RARE(2); break;
+            case 2: RARE(3); break;
+            case 3: RARE(4); break;
+            case 4: RARE(5); break;
+            case 5: RARE(6); break;
+            case 6: RARE(7); break;
+            case 7: RARE(8); break;
+            default: RARE(9); break;
+        }
     }
 #undef RARE
     ActParams p;
@@ -2042,7 +2065,8 @@ gw_status gw_patch_cnn_act(void *env, int32_t P, const gw_cnn_actors *net, const
     p.tiles = (int)tiles;
     const int64_t want = (tiles + 15) / 16;
     const int per_agent = (int)std::max<int64_t>(1, std::min<int64_t>(want, std::max(1, 256 / src.K)));
-#define ACTW(NP) hipLaunchKernelGGL((act_kernel<NP, 16, true, true, true, RSW>), dim3(per_agent, src.K), dim3(1024), 0, s, p)
+#define ACTW(NP) gwprof::launch(act_kernel<NP, 16, true, true, true, RSW>, dim3(per_agent, src.K), dim3(1024), 0, s, p)
+    gwprof::Span span(env, GW_SPAN_ACT);
     switch (src.N) {
         case 1: ACTW(2); break;
         case 2: ACTW(3); break;

@@ -31,6 +31,7 @@
 
 #include "patch_ops.h"
 #include "gridenv.h"
+#include "prof.h"
 
 namespace gw {
 
@@ -2274,17 +2275,13 @@ gw_status ensure_obs_stream(Env *env) {
 // start event, every launch the stop event (the last one's end wins).
 // t_bind_stop: a pipeline event (obs_done, world_ev) bound to the launch the same way, instead
 // of a marker packet recorded after it (used when no timing span is open).
-thread_local hipEvent_t t_span_start = nullptr, t_span_stop = nullptr, t_bind_stop = nullptr;
+using gwprof::t_span_start;
+using gwprof::t_span_stop;
+using gwprof::t_bind_stop;
 
 template <typename F, typename... Args>
 void gw_launch(F kernel, dim3 grid, dim3 block, size_t lds, hipStream_t s, Args... args) {
-    hipEvent_t stop = t_span_stop ? t_span_stop : t_bind_stop;
-    if (stop) {
-        hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)lds, s, t_span_start, stop, 0u, args...);
-        t_span_start = nullptr;
-    } else {
-        hipLaunchKernelGGL(kernel, grid, block, lds, s, args...);
-    }
+    gwprof::launch(kernel, grid, block, lds, s, args...);
 }
 
 hipError_t launch_obs(const Env *env, const gw::Params &p, float *obs, float *final_obs, hipStream_t s);
@@ -2392,6 +2389,24 @@ gw_status prof_span_end(Env *env, size_t idx, int kind) {
     t_span_start = t_span_stop = nullptr;
     return GW_OK;
 }
+
+}  // namespace
+
+namespace gwprof {
+thread_local hipEvent_t t_span_start = nullptr, t_span_stop = nullptr, t_bind_stop = nullptr;
+
+bool span_begin(void *handle, size_t *idx) {
+    Env *env = static_cast<Env *>(handle);
+    if (!env || !env->profiling) return false;
+    return prof_span_begin(env, *idx) == GW_OK;
+}
+
+void span_end(void *handle, size_t idx, int kind) {
+    (void)prof_span_end(static_cast<Env *>(handle), idx, kind);
+}
+}  // namespace gwprof
+
+namespace {
 
 template <typename T>
 gw_status dalloc(Env *env, T **ptr, size_t count) {
@@ -3225,7 +3240,7 @@ gw_status gw_profile_read(void *handle, double out_ms[3], int64_t *n_steps) {
         HIP_TRY(hipEventSynchronize(env->ev_pool[sp.e]));
         float ms = 0.f;
         HIP_TRY(hipEventElapsedTime(&ms, env->ev_pool[sp.b], env->ev_pool[sp.e]));
-        out_ms[sp.kind] += ms;
+        if (sp.kind >= 0 && sp.kind < 3) out_ms[sp.kind] += ms;
     }
     if (n_steps) *n_steps = env->steps_timed;
     env->spans.clear();
@@ -3350,6 +3365,7 @@ gw_status gw_obs_patch(void *handle, int32_t P, float *patch, float *final_patch
     a.P = P;
     a.variant = env->variant;
     for (int k = 0; k < GW_MAX_AGENTS; ++k) a.apples[k] = k < env->K ? env->apples[k] : -1;
+    gwprof::Span span(env, GW_SPAN_WINDOW);
     HIP_TRY(gw::launch_windows(a, s));
     return GW_OK;
 }

@@ -20,6 +20,7 @@
 #include <cstdlib>
 
 #include "patch_ops.h"
+#include "prof.h"
 
 namespace {
 
@@ -298,11 +299,11 @@ hipError_t launch_windows(const PatchArgs &a, hipStream_t s) {
     const size_t lds = base + extra[mode];
     const unsigned grid = (unsigned)((a.E + PB - 1) / PB);
     if (mode == 2)
-        hipLaunchKernelGGL(window_kernel<2>, dim3(grid), dim3(THREADS), lds, s, a, g_patch_dbg);
+        gwprof::launch(window_kernel<2>, dim3(grid), dim3(THREADS), lds, s, a, g_patch_dbg);
     else if (mode == 0)
-        hipLaunchKernelGGL(window_kernel<0>, dim3(grid), dim3(THREADS), lds, s, a, g_patch_dbg);
+        gwprof::launch(window_kernel<0>, dim3(grid), dim3(THREADS), lds, s, a, g_patch_dbg);
     else
-        hipLaunchKernelGGL(window_kernel<1>, dim3(grid), dim3(THREADS), lds, s, a, g_patch_dbg);
+        gwprof::launch(window_kernel<1>, dim3(grid), dim3(THREADS), lds, s, a, g_patch_dbg);
     return hipGetLastError();
 }
 

@@ -24,7 +24,7 @@ HIP_SOURCES = [os.path.join(CSRC, "gridenv.hip"), os.path.join(CSRC, "learner_op
                os.path.join(CSRC, "maddpg_ops.hip"), os.path.join(CSRC, "patch_ops.hip")]
 HEADERS = [os.path.join(INCLUDE, "gridenv.h"), os.path.join(INCLUDE, "learner_ops.h"),
            os.path.join(INCLUDE, "actor_ops.h"), os.path.join(INCLUDE, "rollout_ops.h")]
-SOURCES = HIP_SOURCES + HEADERS + [os.path.join(CSRC, "patch_ops.h")]
+SOURCES = HIP_SOURCES + HEADERS + [os.path.join(CSRC, "patch_ops.h"), os.path.join(CSRC, "prof.h")]
 OBJ_DIR = os.path.join(CSRC, "build")
 ARCH = os.environ.get("MARLNAV_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -13,3 +13,7 @@ print(f"{lab:>14}: {d['value'] / 1e9:.3f} G  {d['ms_per_step'] * 1e3:.1f} us/ste
       f"(span {r.get('frac_per_launch_span') and round(r['frac_per_launch_span'], 3)}, "
       f"period {r.get('frac_per_period') and round(r['frac_per_period'], 3)}) "
       f"host {k.get('host_enqueue_ms_per_step', 0) * 1e3:.1f} us/step")
+kk = k.get("kernels") or r.get("kernels") or {}
+if kk:
+    print(" " * 16 + "  ".join(f"{n} {v['busy_ms_per_step'] * 1e3:.1f}us" + (f" ({v['frac']:.3f} {v['bound']})" if v.get('frac') else "")
+                                for n, v in sorted(kk.items(), key=lambda x: -x[1]['busy_ms_per_step'])))

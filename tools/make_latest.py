@@ -1,11 +1,16 @@
-"""profiles/<tag>/summary.json -> profiles/latest.json (per-launch HBM bytes that bench.py reports as
-roofline.traffic when it runs the same config)."""
+"""profiles/<tag>/summary.json -> profiles/latest.json["configs"][CONFIG]: per-launch HBM bytes and
+rocprofv3 busy time per launch of each kernel kind, which bench.py reports as roofline.traffic /
+frac_rocprof when it runs the same config.  Other configs' entries are kept."""
 import json
 import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KIND = {"gw::obs_kernel": "obs_kernel", "gw::step_v2": "step_kernel", "gw::fear_v2": "fear_kernel"}
+# rocprofv3 kernel name (namespace stripped, before the template arguments) -> bench.py's SPAN_KINDS name
+KIND = {"gw::obs_kernel": "obs_kernel", "gw::step_v2": "step_kernel", "gw::fear_v2": "fear_kernel",
+        "gw::step_obs": "step_obs", "act_kernel": "act_kernel", "window_kernel": "window_kernel",
+        "wcnn_rare_kernel": "cnn_rare_kernel", "cnn_rare_kernel": "cnn_rare_kernel",
+        "wcnn_l1_kernel": "cnn_l1_kernel", "cnn_l1_kernel": "cnn_l1_kernel"}
 
 
 def main(tag, config, cmd=None):
@@ -13,17 +18,29 @@ def main(tag, config, cmd=None):
     kernels = {}
     for name, v in s.items():
         kind = KIND.get(name.split("<")[0].strip())
-        if kind and v.get("hbm_mb") is not None:
-            kernels[kind] = {"hbm_bytes_per_launch": v["hbm_mb"] * 1e6, "avg_us": v["avg_us"]}
+        if kind and (v.get("hbm_mb") is not None or v.get("busy_us")):
+            k = {"avg_us": v["avg_us"], "calls": v.get("calls")}
+            if v.get("hbm_mb") is not None:
+                k["hbm_bytes_per_launch"] = v["hbm_mb"] * 1e6
             if v.get("busy_us"):
-                kernels[kind]["busy_us"] = v["busy_us"]  # union of the launches' intervals / launches
+                k["busy_us"] = v["busy_us"]  # union of the launches' intervals / launches
+            kernels[kind] = k
     cmd = cmd or f"python bench.py --config {config}"
-    out = {"source": f"profiles/{tag} (rocprofv3 --kernel-trace --stats and --pmc FETCH_SIZE / WRITE_SIZE passes of "
-                     f"`{cmd}`; FETCH_SIZE x2 per MI355X_MICROARCH.md; busy_us = the union of the launches' "
-                     f"intervals in the kernel trace / launches)",
-           "config": config, "kernels": kernels}
-    json.dump(out, open(os.path.join(ROOT, "profiles", "latest.json"), "w"), indent=1)
-    print(json.dumps(out, indent=1))
+    path = os.path.join(ROOT, "profiles", "latest.json")
+    try:
+        out = json.load(open(path))
+    except (OSError, ValueError):
+        out = {}
+    if "configs" not in out:  # round-3 layout (one config at the top level)
+        old = {k: out[k] for k in ("source", "config", "kernels") if k in out}
+        out = {"configs": {old["config"]: {"source": old["source"], "kernels": old["kernels"]}} if old else {}}
+    out["configs"][config] = {
+        "source": f"profiles/{tag} (rocprofv3 --kernel-trace --stats and --pmc FETCH_SIZE / WRITE_SIZE passes of "
+                  f"`{cmd}`; FETCH_SIZE x2 per MI355X_MICROARCH.md; busy_us = the union of the launches' "
+                  f"intervals in the kernel trace / launches)",
+        "kernels": kernels}
+    json.dump(out, open(path, "w"), indent=1)
+    print(json.dumps(out["configs"][config], indent=1))
 
 
 if __name__ == "__main__":
