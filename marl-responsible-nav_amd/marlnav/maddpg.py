@@ -346,9 +346,11 @@ class MADDPG:
     def _learn_critic(self, states, actions, rewards, next_states, dones, u_next=None, critic_in=None) -> dict:
         """Phase 1: target actions, TD target, critic forward and backward (gradients in the
         critics' .grad, not yet applied)."""
-        if self.fused:
-            return self._fused_critic(states, actions, rewards, next_states, dones, u_next, critic_in)
         K, B = states.shape[0], states.shape[1]
+        # the fused kernels take batches of 16-row tiles (gw_maddpg_* reject B % 16 != 0) and at
+        # most GW_MAX_AGENTS agents; any other batch runs the torch composition
+        if self.fused and B >= 16 and B % 16 == 0 and K <= _lib.GW_MAX_AGENTS:
+            return self._fused_critic(states, actions, rewards, next_states, dones, u_next, critic_in)
         D = K * self.H * self.W
         with torch.no_grad():
             if critic_in is not None:
@@ -562,9 +564,16 @@ class MADDPG:
             for i, p in enumerate(opt.param_groups[0]["params"]):
                 if f"{name}.{i}.exp_avg" not in sd:
                     continue
-                opt.state[p] = {key: sd[f"{name}.{i}.{key}"].to(p.device if key != "step" else
-                                                                     sd[f"{name}.{i}.step"].device).clone()
-                                for key in ("exp_avg", "exp_avg_sq", "step")}
+                st = opt.state.get(p)
+                if st and all(isinstance(st.get(key), torch.Tensor) for key in ("exp_avg", "exp_avg_sq", "step")):
+                    # in place: a captured update graph (capturable Adam) keeps reading and writing
+                    # these very tensors, so replacing them would silently detach it from the load
+                    for key in ("exp_avg", "exp_avg_sq", "step"):
+                        st[key].copy_(sd[f"{name}.{i}.{key}"])
+                else:
+                    opt.state[p] = {key: sd[f"{name}.{i}.{key}"].to(p.device if key != "step" else
+                                                                         sd[f"{name}.{i}.step"].device).clone()
+                                    for key in ("exp_avg", "exp_avg_sq", "step")}
 
     def save(self, path: str, optimizer: bool = True):
         """Networks (+ optimizer state) as safetensors."""

@@ -18,17 +18,55 @@ practical with a larger batch, so large-E runs set it explicitly.
 from __future__ import annotations
 
 import torch
+import torch.distributed as dist
 
 from .maddpg import MADDPG, learns_per_step
 from .rollout import Rollout
 from .vec_env import VecGridEnv
 
 
+def dp_env_counts(local_envs: int, device=None):
+    """(global env count, smallest shard) over the default process group (one all-reduce each;
+    (local_envs, local_envs) without one).  Every rank gets the same pair."""
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+        return int(local_envs), int(local_envs)
+    dev = device if (device is not None and dist.get_backend() == "nccl") else torch.device("cpu")
+    tot = torch.tensor([local_envs], dtype=torch.int64, device=dev)
+    neg_min = torch.tensor([-local_envs], dtype=torch.int64, device=dev)
+    dist.all_reduce(tot)
+    dist.all_reduce(neg_min, op=dist.ReduceOp.MAX)
+    return int(tot.item()), int(-neg_min.item())
+
+
+def learn_schedule(idx_step: int, ring_t: int, ring_slots: int, global_envs: int, min_shard: int, learn_step: int,
+                   batch_size: int, learning_delay: int = 0, updates_per_step: int | None = None) -> int:
+    """MADDPG updates after env step idx_step: the reference rule (maddpg/agent.py:199-224,
+    ``learns_per_step``) over the GLOBAL env count, once every rank's ring holds a batch (the
+    smallest shard decides; ring_t = steps stored, the same on every rank since each rank steps
+    once per step) and the transitions of all ranks exceed learning_delay.  Every input is the
+    same on every rank, so every rank issues the same learn() calls (and so the same gradient
+    all-reduces) even when envs % world != 0."""
+    n = updates_per_step if updates_per_step is not None else learns_per_step(global_envs, learn_step, idx_step)
+    filled = min(ring_t, ring_slots - 1)
+    if n and filled * min_shard >= batch_size and ring_t * global_envs > learning_delay:
+        return n
+    return 0
+
+
 class MADDPGTrainer:
     def __init__(self, env: VecGridEnv, maddpg: MADDPG, memory_size: int = 200_000, learning_delay: int = 0,
                  updates_per_step: int | None = None, graph: bool = True, seed: int = 0):
         self.env, self.m = env, maddpg
-        slots = max(2, -(-memory_size // env.E) + 1)
+        # data parallelism: every decision that gates a learn() (and so its two gradient
+        # all-reduces) is taken from GLOBAL quantities that every rank computes alike -- the global
+        # env count, the smallest shard and the ring's step count (each rank steps once per step) --
+        # never from this rank's shard size, which differs by one when envs % world != 0
+        self.distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        self.world = dist.get_world_size() if self.distributed else 1
+        self.rank = dist.get_rank() if self.distributed else 0
+        self.global_envs, self.min_shard = dp_env_counts(env.E, env.device)
+        # MEMORY_SIZE transitions in total over the ranks (each rank's ring holds its share)
+        slots = max(2, -(-memory_size // self.global_envs) + 1)
         # obs writes pipelined with the next step when the actor is the fused op (it never reads
         # the dense obs), launched behind it ("lazy"); the ring is fenced before every learn
         self.rollout = Rollout(env, maddpg.actors, replay_slots=slots, training=True, seed=seed,
@@ -41,6 +79,12 @@ class MADDPGTrainer:
         self.updates = 0
         self.losses = []            # (actor_loss [K], critic_loss [K]) device tensors of the last updates
         self.total_steps = 0
+
+    def learns_now(self, idx_step: int) -> int:
+        """Updates after env step idx_step (``learn_schedule``), identical on every rank."""
+        rp = self.rollout.replay
+        return learn_schedule(idx_step, rp.t, rp.S, self.global_envs, self.min_shard, self.m.learn_step,
+                              self.m.batch_size, self.learning_delay, self.updates_per_step)
 
     def reset(self):
         self.rollout.reset()
@@ -56,14 +100,12 @@ class MADDPGTrainer:
     def train(self, env_steps: int = 150) -> dict:
         """Advance every env by env_steps steps with learning; returns the episode statistics of
         these steps (completed-episode return / length means, FeAR, crashes, apples)."""
-        rp = self.rollout.replay
         before = self.rollout.totals() if self.rollout.has_stats else None
         for idx_step in range(env_steps):
             self.rollout.step()
             self.total_steps += self.env.E
-            n = self.updates_per_step if self.updates_per_step is not None else \
-                learns_per_step(self.env.E, self.m.learn_step, idx_step)
-            if n and len(rp) >= self.m.batch_size and rp.t * self.env.E > self.learning_delay:
+            n = self.learns_now(idx_step)
+            if n:
                 for _ in range(n):
                     out = self._learn()
                     self.updates += 1
@@ -78,37 +120,50 @@ class MADDPGTrainer:
                 "crashes": tot.get("crashes", 0.0), "apples": tot.get("apples", 0.0)}
 
     # ---- MADDPGAgent.save_checkpoint / load_checkpoint / load_wo_memory (maddpg/agent.py:255-281)
+    def _memory_file(self) -> str:
+        # every rank's ring holds its own shard's transitions: one memory file per rank
+        return "memory.safetensors" if self.world == 1 else f"memory_r{self.rank}.safetensors"
+
     def save_checkpoint(self, path: str, filename: str, steps: int | None = None):
-        """The networks + optimizers (`filename`, safetensors), the replay memory
-        (`memory.safetensors`: the ring's slots and fill state, where the reference pickles its
-        buffer) and the step counter (`steps.txt`), as the reference lays them out."""
+        """The networks + optimizers (`filename`, safetensors; rank 0 writes them, the replicas
+        are identical), the replay memory (`memory.safetensors`, one `memory_r<rank>` file per
+        rank with data parallelism: the ring's slots, fill state and the fused actor's noise
+        counter, where the reference pickles its buffer) and the step counter (`steps.txt`,
+        env steps over all ranks), as the reference lays them out.  Ranks meet at a barrier
+        after writing, so a load that follows sees every file."""
         import os
         from safetensors.torch import save_file
-        os.makedirs(path, exist_ok=True)
         self.rollout.fence()  # the ring's last obs slots are written
-        self.m.save(os.path.join(path, filename))
+        if self.rank == 0:
+            os.makedirs(path, exist_ok=True)
+            self.m.save(os.path.join(path, filename))
+            with open(os.path.join(path, "steps.txt"), "w") as f:
+                f.write(str(self.total_steps // max(self.env.E, 1) * self.global_envs if steps is None else int(steps)))
+        if self.distributed:
+            dist.barrier()  # the directory exists
         if self.rollout.replay is not None:
-            save_file({k: v.detach().contiguous().cpu() for k, v in self.rollout.replay.state_dict().items()},
-                      os.path.join(path, "memory.safetensors"))
-        with open(os.path.join(path, "steps.txt"), "w") as f:
-            f.write(str(self.total_steps if steps is None else int(steps)))
+            sd = {k: v.detach().contiguous().cpu() for k, v in self.rollout.replay.state_dict().items()}
+            sd["rollout_calls"] = torch.tensor([self.rollout._calls], dtype=torch.int64)
+            save_file(sd, os.path.join(path, self._memory_file()))
+        if self.distributed:
+            dist.barrier()
 
     def load_checkpoint(self, path: str, filename: str):
         import os
         from safetensors.torch import load_file
         self.load_wo_memory(path, filename)
-        mem = os.path.join(path, "memory.safetensors")
+        mem = os.path.join(path, self._memory_file())
         if self.rollout.replay is not None and os.path.exists(mem):
             self.rollout.fence()
-            self.rollout.replay.load_state_dict({k: v.to(self.env.device) for k, v in load_file(mem).items()})
+            sd = load_file(mem)
+            calls = sd.pop("rollout_calls", None)
+            self.rollout.replay.load_state_dict({k: v.to(self.env.device) for k, v in sd.items()})
             self.rollout.resume()
+            # the fused actor's Gumbel-noise Philox counter continues where the saved run stopped
+            # (restarting it at 0 would replay the original run's exploration noise)
+            self.rollout._calls = int(calls[0]) if calls is not None else self.rollout.replay.t
         with open(os.path.join(path, "steps.txt")) as f:
-            self.total_steps = int(f.read())
-
-    def load_wo_memory(self, path: str, filename: str):
-        """The networks and optimizers only (in place: a captured update graph stays valid)."""
-        import os
-        self.m.load(os.path.join(path, filename))
+            self.total_steps = int(f.read()) // self.global_envs * self.env.E
 
     def total_loss(self) -> float:
         """MADDPGAgent.total_loss: sum of the most recent per-agent losses (actor + critic)."""

@@ -383,3 +383,30 @@ def test_checkpoint_keeps_optimizer_state(tmp_path):
     m2.learn(*b)
     for a, c in zip(m.state_dict().values(), m2.state_dict().values()):
         assert torch.equal(a, c)
+
+
+def test_cnn_optimizer_load_is_in_place_cpu():
+    """loading the optimizer state must write into the existing Adam state tensors
+    (a captured update graph with capturable Adam keeps reading and writing those very tensors),
+    not replace them.  CNN arch (per-parameter torch Adam), CPU: the state tensors keep their
+    storage and take the loaded values."""
+    K, H, W, B = 2, 8, 8, 4
+    m = MADDPG(K, H, W, arch="cnn", batch_size=B, seed=1)
+    g = torch.Generator().manual_seed(0)
+
+    def batch():
+        return (torch.randint(-1, 6, (K, B, H, W), generator=g).float(), torch.softmax(torch.randn((K, B, 9), generator=g), -1),
+                torch.randn((B, K), generator=g, dtype=torch.float64), torch.randint(-1, 6, (K, B, H, W), generator=g).float(),
+                (torch.rand((B, K), generator=g) < 0.2).to(torch.uint8), torch.rand((K, B, 9), generator=g),
+                torch.rand((K, B, 9), generator=g))
+    m.learn(*batch())
+    sd = {k: v.clone() + 1.0 for k, v in m.optim_state_dict().items()}
+    ptrs = {id(p): {k: t.data_ptr() for k, t in st.items()} for opt in (m.opt_actor, m.opt_critic)
+            for p, st in opt.state.items()}
+    m.load_optim_state_dict(sd)
+    for name, opt in (("opt_actor", m.opt_actor), ("opt_critic", m.opt_critic)):
+        for i, p in enumerate(opt.param_groups[0]["params"]):
+            st = opt.state[p]
+            for key in ("exp_avg", "exp_avg_sq", "step"):
+                assert st[key].data_ptr() == ptrs[id(p)][key]
+                assert torch.equal(st[key], sd[f"{name}.{i}.{key}"].to(st[key].dtype))

@@ -176,3 +176,43 @@ def test_gpu_dp_graph_segments_equal_eager():
     np.testing.assert_array_equal(g[0], g[1])
     np.testing.assert_array_equal(e[0], e[1])
     np.testing.assert_allclose(g[0], e[0], rtol=1e-5, atol=1e-6)
+
+
+def _schedule_worker(rank, world, port, local_envs, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from marlnav.train import dp_env_counts, learn_schedule
+        g, m = dp_env_counts(local_envs[rank])
+        S = -(-200 // g) + 1
+        sched = [learn_schedule(i, i + 1, S, g, m, learn_step=10, batch_size=16) for i in range(40)]
+        q.put((rank, g, m, sched))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_learn_schedule_identical_on_uneven_shards_cpu():
+    """with --envs % world != 0 the shards differ by one env; the learn schedule (and
+    with it the number of learn() calls, each two gradient all-reduces) must still be the same on
+    every rank, or the collectives go out of step.  gloo, world size 2, shards 5 and 4 envs."""
+    from marlnav.parallel import shard
+    world, G = 2, 9
+    local = [shard(G, r, world)[1] for r in range(world)]
+    assert local == [5, 4]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_schedule_worker, args=(r, world, port, local, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    (_, g0, m0, s0), (_, g1, m1, s1) = res
+    assert (g0, m0) == (g1, m1) == (9, 4)
+    assert s0 == s1
+    # the rule over 9 global envs: learn_step 10 > 9 -> one learn every 10 // 9 = 1 step, once the
+    # smallest shard's ring holds a batch of 16 (4 envs x 4 steps)
+    assert s0[:3] == [0, 0, 0] and s0[3] == 1

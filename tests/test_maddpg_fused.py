@@ -149,3 +149,16 @@ def test_fused_small_batch_and_patch_inputs(Bt, patch):
             assert _rel(a, b) < 1e-3
     finally:
         H, W = h0, w0
+
+
+def test_fused_learner_takes_any_batch_size():
+    """the fused kernels take batches of 16-row tiles; a learner built with another
+    batch size (agilerl accepts any, e.g. 100) runs the torch composition instead of raising, and
+    its update equals the unfused learner's bit for bit (the same torch path)."""
+    ms = _pair()
+    g = torch.Generator(device="cuda").manual_seed(9)
+    b = _batch(g, 100)
+    for m in ms:
+        m.learn(*b)
+    for a, c in zip(ms[0].state_dict().values(), ms[1].state_dict().values()):
+        assert torch.equal(a, c)
