@@ -2,6 +2,13 @@
 prints the reference's three totals.
 
     python marl-responsible-nav_amd/customeval.py --checkpoint run.safetensors [--scenario level3]
+    python marl-responsible-nav_amd/customeval.py \
+        --checkpoint /root/reference/models/custom/single/level3/fear/Single_MADDPG_4k.pt
+
+A ``.pt`` checkpoint is the reference's own agilerl save (``agents.load_wo_memory(path,
+filename)``, customeval.py:39-64, maddpg/agent.py:279-281), read without unpickling
+(marlnav/checkpoint.py); the shipped ones are single-agent actors over Level 3's 10 x 16 grid, so
+they are evaluated on the single-agent CustomEnv (variant 1, scenario level3_single).
 """
 import argparse
 import os
@@ -22,13 +29,22 @@ def main(argv=None):
 
     from marlnav import scenario as S
     from marlnav.evaluate import evaluate
-    from marlnav.maddpg import MADDPG
 
-    sc = S.builtin(args.scenario)
     import torch
-    m = MADDPG(sc.K, sc.H, sc.W, arch=args.arch, device=torch.device("cuda"))
-    m.load(args.checkpoint)
-    r = evaluate(m.actors, sc, episodes=args.episodes, max_steps=args.train_steps, fear=False, seed=args.seed)
+    variant = 0
+    if args.checkpoint.endswith(".pt"):  # the reference's agilerl save: single-agent actors
+        from marlnav import checkpoint as ck
+        sc = S.builtin("level3_single" if args.scenario == "level3" else args.scenario)
+        actors = ck.load_actors([ck.actor_state(args.checkpoint)], sc.H, sc.W, device=torch.device("cuda"))
+        variant = 1
+    else:
+        from marlnav.maddpg import MADDPG
+        sc = S.builtin(args.scenario)
+        m = MADDPG(sc.K, sc.H, sc.W, arch=args.arch, device=torch.device("cuda"))
+        m.load(args.checkpoint)
+        actors = m.actors
+    r = evaluate(actors, sc, episodes=args.episodes, max_steps=args.train_steps, fear=False, seed=args.seed,
+                 variant=variant)
     n = args.episodes
     print(f"Total destination reached: {r['apples_caught']} across {n} episodes")
     print(f"Total crashes: {r['crashes']} across {n} episodes")

@@ -8,9 +8,11 @@ E = episodes envs in parallel (auto-reset off, step cap = TRAIN_STEPS); an env s
 after its episode ends, so the totals are the same sums.  Actions: ``training=False`` (no
 Gumbel noise), the env's action mask, argmax — agilerl's eval-mode ``get_action`` restated.
 With the fused actor the env writes no dense obs (the actor reads the obs descriptors).
-Weights come from this package's safetensors checkpoints (marlnav/maddpg.py ``MADDPG.save``);
-the reference's pickled ``.pt`` checkpoints are not loadable with a non-executing loader and
-are not used.
+Weights come from this package's safetensors checkpoints (marlnav/maddpg.py ``MADDPG.save``) or
+from the reference's shipped agilerl ``.pt`` checkpoints, read without unpickling by
+marlnav/checkpoint.py (``agents.load_wo_memory``, maddpg/agent.py:279-281); those are
+single-agent actors (obs 160 = Level 3's 10 x 16), evaluated on the single-agent CustomEnv
+(``variant=1``, custom/customenv.py:78-183).
 """
 from __future__ import annotations
 
@@ -26,13 +28,14 @@ from .vec_env import VecGridEnv
 
 @torch.no_grad()
 def evaluate(actors: MultiAgentActors, scenario="level3", episodes: int = 100, max_steps: int = 150,
-             fear: bool = False, seed: int = 42, record_actions: bool = False, fused: bool | None = None) -> dict:
+             fear: bool = False, seed: int = 42, record_actions: bool = False, fused: bool | None = None,
+             variant: int = 0) -> dict:
     sc = builtin(scenario) if isinstance(scenario, str) else scenario
     if fused is None:
         fused = actors.fusable(SimpleNamespace(K=sc.K, H=sc.H, W=sc.W))
     # the fused actor reads the obs descriptors: no dense obs is written at all
     env = VecGridEnv(sc, num_envs=episodes, fear=fear, max_steps=max_steps, auto_reset=False, seed=seed,
-                     obs=not fused)
+                     obs=not fused, variant=variant)
     try:
         obs, mask = env.reset()
         dev = env.device
