@@ -13,7 +13,7 @@ Default workload = BASELINE config 3 (the north-star shape): 4-agent 32x32 grid,
 per GPU, FeAR on with weight -5 (configs/custom_fear_5.yaml).  value = all ranks' envs x N
 agents x steps / max-over-ranks wall time.
 
-  python bench.py [--gpus N --steps K --warmup W] [--config c3|c2|c4|c1] [--no-cpu-baseline]
+  python bench.py [--gpus N --steps K --warmup W] [--config c3|c2|c2env|c4|c1|c5|...] [--no-cpu-baseline]
 """
 from __future__ import annotations
 
@@ -36,8 +36,14 @@ CONFIGS = {
     "c3": dict(scenario="grid32", envs=65536, fear=True, fear_weight=-5.0,
                workload="BASELINE config 3: 4-agent (2 RL) 32x32 Level-3-like grid, 65536 envs/GPU, "
                         "FeAR on (weight -5, configs/custom_fear_5.yaml), random RL policy"),
-    "c2": dict(scenario="grid32", envs=4096, fear=False, fear_weight=-2.0,
-               workload="BASELINE config 2: 4-agent 32x32 grid, 4096 envs, MLP obs, FeAR off"),
+    "c2": dict(scenario="grid32", envs=4096, fear=False, fear_weight=-2.0, rollout=True,
+               workload="BASELINE config 2: 4-agent 32x32 grid, 4096 envs, FeAR off (configs/custom.yaml), the "
+                        "MLP actors of configs/mlp.yaml (128-128, GumbelSoftmax + mask + argmax; fused "
+                        "gw_actor_act) acting on the full-grid obs every step, env step, zero-copy replay ring "
+                        "of MEMORY_SIZE 200000 (maddpg/agent.py:89,109-127,190-197)"),
+    "c2env": dict(scenario="grid32", envs=4096, fear=False, fear_weight=-2.0,
+                  workload="BASELINE config 2's env alone: 4-agent 32x32 grid, 4096 envs, FeAR off, random RL "
+                           "policy on device (no actor)"),
     "c4": dict(scenario="grid64_n8", envs=65536, fear=False, fear_weight=-5.0,
                workload="BASELINE config 4: 8-agent 64x64 grid, 65536 envs, FeAR off"),
     "c4f": dict(scenario="grid64_n8", envs=65536, fear=True, fear_weight=-5.0,
@@ -365,9 +371,12 @@ def main():
     # per-step RCCL all-gather of every env's completed-episode return + done flag (SURVEY §8e;
     # maddpg/agent.py:229-247): gw_step writes them straight into the send buffer
     graph_n = args.graph
-    if graph_n < 0:  # auto: the host-bound regime (env only, one rank; synchronous obs or merged path)
-        graph_n = 16 if (not cfg.get("rollout") and world == 1 and
-                         (not obs_mode or env.kernel_path == "merged")) else 0
+    if graph_n < 0:  # auto: the host-bound regime (one rank; synchronous obs or merged path): the
+        # env-only C1 / C2 lines, and the small-batch rollout (C2) with the fused MLP actor
+        small_rollout = (cfg.get("rollout") and not cfg.get("patch") and not cfg.get("arch") and
+                         env.kernel_path == "merged" and not args.updates_per_step)
+        graph_n = 16 if (world == 1 and (not obs_mode or env.kernel_path == "merged") and
+                         (not cfg.get("rollout") or small_rollout)) else 0
     graph_n = min(graph_n, args.steps)
     if obs_mode and env.kernel_path == "merged":
         graph_n -= graph_n % 2  # merged async: an even number of captured steps
@@ -418,7 +427,12 @@ def main():
             actors = learner.actors
         # the fused actor's Gumbel noise is Philox keyed by (seed; global env id, step, agent):
         # one seed for all ranks keeps every env's trajectory independent of the rank count
-        ro = Rollout(env, actors, replay_slots=-(-200_000 // E) + 1, training=True, seed=42,
+        # MEMORY_SIZE 200,000 transitions (configs/custom*.yaml); with graphs the ring's slots are
+        # rounded up to a multiple of the graph length (one captured graph per ring phase)
+        slots = -(-200_000 // E) + 1
+        if graph_n:
+            slots = -(-slots // graph_n) * graph_n
+        ro = Rollout(env, actors, replay_slots=slots, training=True, seed=42,
                      fused=False if (args.cnn_torch or args.patch_torch) else None,
                      obs_async=obs_mode, fear_async=bool(obs_mode) and args.fear_async, gather=gather,
                      patch=cfg.get("patch", 0))
@@ -469,7 +483,8 @@ def main():
     if graph_n:
         if gather is not None:
             gather.compact()  # the warmup's partial window
-        graph = env.capture_steps(graph_n, gather)
+        # env only: VecGridEnv.capture_steps; the rollout: one graph per ring phase (Rollout.capture)
+        graph = ro.capture(graph_n) if cfg.get("rollout") else env.capture_steps(graph_n, gather)
     n_graph = args.steps - args.steps % graph_n if graph_n else 0
 
     if n_prof:  # the profiling events exist before they are used (gw_profile creates them)

@@ -55,14 +55,17 @@ gw_status gw_actor_prepare(void *env, const gw_mlp_actors *net, float *ws, void 
 
 /* For every env e and RL agent k, on the observation the env last wrote:
  *   logits = actor_k(obs_k);  training: logits -= log(-log(u + 1e-20) + 1e-20)  (Gumbel noise;
- *   u = uniform[k][e][a] if `uniform` is given, else Philox(seed; global env id, counter, k));
+ *   u = uniform[k][e][a] if `uniform` is given, else Philox(seed; global env id, c, k) with
+ *   c = counter + *counter_dev (counter_dev: a device int64 read at launch time, e.g. the replay
+ *   ring's step count, so the replays of a captured HIP graph draw fresh noise; NULL = 0));
  *   probs = softmax(logits / tau);  action = argmax over the actions allowed by mask[e][k]
  *   (first maximum; mask NULL = all allowed).
  * Outputs: actions [E][K] int32 (gw_step's rl_actions layout), probs [K][E][9] f32 (the
  * continuous actions agilerl stores in replay), logits [K][E][9] f32 before the noise (may be
  * NULL).  ws: prepared by gw_actor_prepare for the current parameters. */
 gw_status gw_actor_act(void *env, const gw_mlp_actors *net, const float *ws, int training, float tau,
-                       uint64_t seed, uint64_t counter, const float *uniform, const uint16_t *mask,
+                       uint64_t seed, uint64_t counter, const int64_t *counter_dev, const float *uniform,
+                       const uint16_t *mask,
                        int32_t *actions, float *probs, float *logits, void *stream);
 
 /* ---- local windows (X1: not a reference format) ---------------------------------------------
@@ -76,7 +79,8 @@ gw_status gw_actor_act(void *env, const gw_mlp_actors *net, const float *ws, int
 int64_t gw_patch_actor_workspace_floats(int32_t P, int32_t H, int32_t W, int32_t K);
 gw_status gw_patch_actor_prepare(void *env, int32_t P, const gw_mlp_actors *net, float *ws, void *stream);
 gw_status gw_patch_actor_act(void *env, int32_t P, const gw_mlp_actors *net, const float *ws, int training, float tau,
-                             uint64_t seed, uint64_t counter, const float *uniform, const uint16_t *mask,
+                             uint64_t seed, uint64_t counter, const int64_t *counter_dev, const float *uniform,
+                             const uint16_t *mask,
                              int32_t *actions, float *probs, float *logits, void *stream);
 
 /* ---- the configs/cnn.yaml actor head ------------------------------------------------------
@@ -120,7 +124,8 @@ gw_status gw_cnn_prepare(void *env, const gw_cnn_actors *net, float *ws, void *s
 
 /* gw_actor_act with the CNN head: the same noise, softmax, mask, argmax and outputs. */
 gw_status gw_cnn_act(void *env, const gw_cnn_actors *net, const float *ws, int training, float tau,
-                     uint64_t seed, uint64_t counter, const float *uniform, const uint16_t *mask,
+                     uint64_t seed, uint64_t counter, const int64_t *counter_dev, const float *uniform,
+                     const uint16_t *mask,
                      int32_t *actions, float *probs, float *logits, void *stream);
 
 /* ---- the CNN head on local windows (X1: not a reference format) -----------------------------
@@ -138,7 +143,8 @@ gw_status gw_cnn_act(void *env, const gw_cnn_actors *net, const float *ws, int t
 int64_t gw_patch_cnn_workspace_floats(int32_t P, int32_t H, int32_t W, int32_t K, int64_t E);
 gw_status gw_patch_cnn_prepare(void *env, int32_t P, const gw_cnn_actors *net, float *ws, void *stream);
 gw_status gw_patch_cnn_act(void *env, int32_t P, const gw_cnn_actors *net, const float *ws, int training, float tau,
-                           uint64_t seed, uint64_t counter, const float *uniform, const uint16_t *mask,
+                           uint64_t seed, uint64_t counter, const int64_t *counter_dev, const float *uniform,
+                           const uint16_t *mask,
                            int32_t *actions, float *probs, float *logits, void *stream);
 
 #ifdef __cplusplus

@@ -194,6 +194,16 @@ int64_t gw_kernel_path(void *env);
  * itself leaves that state; a fence between replays clears it, this re-arms it. */
 gw_status gw_graph_replayed(void *env, void *stream);
 
+/* The host-side pipeline state of the merged path's async obs (the queued writer's parameters,
+ * the descriptor buffer in use) as an opaque blob of gw_pipeline_state_bytes() bytes.  For callers
+ * that capture several HIP graphs of steps writing DIFFERENT buffers (a replay ring's slots, one
+ * graph per ring phase): save the state after capturing each graph and load it after replaying
+ * that graph, so the next eager step, graph or fence launches the right queued writer (on
+ * `stream`).  Synchronous obs leaves nothing queued; the defer path's pipeline is not capturable. */
+int64_t gw_pipeline_state_bytes(void);
+gw_status gw_pipeline_save(void *env, void *buf);
+gw_status gw_pipeline_load(void *env, const void *buf, void *stream);
+
 /* What the observation an env last wrote (gw_reset / gw_step) is made of, for ops that work
  * on it without reading it back (actor_ops.h): the static step-encoding map plus, per env, a
  * 48-byte descriptor (agent cells, reset / apple flags; ma_customenv.py:197-209, 303-322).

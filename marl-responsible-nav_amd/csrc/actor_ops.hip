@@ -147,6 +147,7 @@ struct ActParams {
                               // layer 2's MFMAs, bit 2 skip the epilogue, bit 4 gather row 0 only
     float tau;
     uint32_t key0, key1, ctr0, ctr1;
+    const int64_t *ctr_dev;   // null, or a device counter added to (ctr1:ctr0) at launch time
     int apples[MAXN];
 };
 
@@ -611,8 +612,11 @@ __global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) u[r] = (live[r] && valid) ? p.uniform[o + 4 * q + r] : 0.5f;
             } else {  // draw q of (env, counter, k): actions 4q .. 4q + 3
-                const uint4 x = philox((uint32_t)(p.env_offset + e), p.ctr0,
-                                       (uint32_t)k | ((uint32_t)q << 8) | (0xA7u << 24), p.ctr1, p.key0, p.key1);
+                uint64_t ctr = ((uint64_t)p.ctr1 << 32) | p.ctr0;
+                if (p.ctr_dev) ctr += (uint64_t)*p.ctr_dev;
+                const uint4 x = philox((uint32_t)(p.env_offset + e), (uint32_t)ctr,
+                                       (uint32_t)k | ((uint32_t)q << 8) | (0xA7u << 24), (uint32_t)(ctr >> 32),
+                                       p.key0, p.key1);
                 u[0] = (float)(x.x >> 8) * (1.0f / 16777216.0f);
                 u[1] = (float)(x.y >> 8) * (1.0f / 16777216.0f);
                 u[2] = (float)(x.z >> 8) * (1.0f / 16777216.0f);
@@ -1656,7 +1660,8 @@ gw_status gw_actor_prepare(void *env, const gw_mlp_actors *net, float *ws, void 
 namespace {
 // gw_actor_act (P = 0) and gw_patch_actor_act (P > 0: the P x P window variant)
 gw_status actor_act(const char *who, void *env, int32_t P, const gw_mlp_actors *net, const float *ws, int training,
-                    float tau, uint64_t seed, uint64_t counter, const float *uniform, const uint16_t *mask,
+                    float tau, uint64_t seed, uint64_t counter, const int64_t *counter_dev, const float *uniform,
+                    const uint16_t *mask,
                     int32_t *actions, float *probs, float *logits, void *stream) {
     const std::string w(who);
     if (!env || !net || !ws || !actions || !probs) return err(GW_ERR_ARG, w + ": null argument");
@@ -1699,6 +1704,7 @@ gw_status actor_act(const char *who, void *env, int32_t P, const gw_mlp_actors *
     p.key1 = (uint32_t)(seed >> 32);
     p.ctr0 = (uint32_t)counter;
     p.ctr1 = (uint32_t)(counter >> 32);
+    p.ctr_dev = counter_dev;
     for (int k = 0; k < MAXN; ++k) p.apples[k] = src.apples[k];
     const char *ab = std::getenv("GW_ACT_AB");
     p.ab = ab ? std::atoi(ab) : 0;
@@ -1747,9 +1753,10 @@ gw_status actor_act(const char *who, void *env, int32_t P, const gw_mlp_actors *
 extern "C" {
 
 gw_status gw_actor_act(void *env, const gw_mlp_actors *net, const float *ws, int training, float tau, uint64_t seed,
-                       uint64_t counter, const float *uniform, const uint16_t *mask, int32_t *actions, float *probs,
+                       uint64_t counter, const int64_t *counter_dev, const float *uniform, const uint16_t *mask,
+                       int32_t *actions, float *probs,
                        float *logits, void *stream) {
-    return actor_act("gw_actor_act", env, 0, net, ws, training, tau, seed, counter, uniform, mask, actions, probs,
+    return actor_act("gw_actor_act", env, 0, net, ws, training, tau, seed, counter, counter_dev, uniform, mask, actions, probs,
                      logits, stream);
 }
 
@@ -1788,10 +1795,11 @@ gw_status gw_patch_actor_prepare(void *env, int32_t P, const gw_mlp_actors *net,
 }
 
 gw_status gw_patch_actor_act(void *env, int32_t P, const gw_mlp_actors *net, const float *ws, int training, float tau,
-                             uint64_t seed, uint64_t counter, const float *uniform, const uint16_t *mask,
+                             uint64_t seed, uint64_t counter, const int64_t *counter_dev, const float *uniform,
+                             const uint16_t *mask,
                              int32_t *actions, float *probs, float *logits, void *stream) {
     if (P < 1) return err(GW_ERR_ARG, "gw_patch_actor_act: P must be >= 1");
-    return actor_act("gw_patch_actor_act", env, P, net, ws, training, tau, seed, counter, uniform, mask, actions,
+    return actor_act("gw_patch_actor_act", env, P, net, ws, training, tau, seed, counter, counter_dev, uniform, mask, actions,
                      probs, logits, stream);
 }
 
@@ -1827,7 +1835,8 @@ gw_status gw_cnn_prepare(void *env, const gw_cnn_actors *net, float *ws, void *s
 }
 
 gw_status gw_cnn_act(void *env, const gw_cnn_actors *net, const float *ws, int training, float tau, uint64_t seed,
-                     uint64_t counter, const float *uniform, const uint16_t *mask, int32_t *actions, float *probs,
+                     uint64_t counter, const int64_t *counter_dev, const float *uniform, const uint16_t *mask,
+                     int32_t *actions, float *probs,
                      float *logits, void *stream) {
     if (!env || !net || !ws || !actions || !probs) return err(GW_ERR_ARG, "gw_cnn_act: null argument");
     if (reinterpret_cast<uintptr_t>(ws) & 15u) return err(GW_ERR_ARG, "gw_cnn_act: ws must be 16-byte aligned");
@@ -1908,6 +1917,7 @@ gw_status gw_cnn_act(void *env, const gw_cnn_actors *net, const float *ws, int t
     p.key1 = (uint32_t)(seed >> 32);
     p.ctr0 = (uint32_t)counter;
     p.ctr1 = (uint32_t)(counter >> 32);
+    p.ctr_dev = counter_dev;
     for (int k = 0; k < MAXN; ++k) p.apples[k] = src.apples[k];
     p.ab = 0;
     p.tiles = (int)tiles;
@@ -1979,7 +1989,8 @@ gw_status gw_patch_cnn_prepare(void *env, int32_t P, const gw_cnn_actors *net, f
 }
 
 gw_status gw_patch_cnn_act(void *env, int32_t P, const gw_cnn_actors *net, const float *ws, int training, float tau,
-                           uint64_t seed, uint64_t counter, const float *uniform, const uint16_t *mask,
+                           uint64_t seed, uint64_t counter, const int64_t *counter_dev, const float *uniform,
+                           const uint16_t *mask,
                            int32_t *actions, float *probs, float *logits, void *stream) {
     if (!env || !net || !ws || !actions || !probs) return err(GW_ERR_ARG, "gw_patch_cnn_act: null argument");
     if (reinterpret_cast<uintptr_t>(ws) & 15u) return err(GW_ERR_ARG, "gw_patch_cnn_act: ws must be 16-byte aligned");
@@ -2059,6 +2070,7 @@ gw_status gw_patch_cnn_act(void *env, int32_t P, const gw_cnn_actors *net, const
     p.key1 = (uint32_t)(seed >> 32);
     p.ctr0 = (uint32_t)counter;
     p.ctr1 = (uint32_t)(counter >> 32);
+    p.ctr_dev = counter_dev;
     for (int k = 0; k < MAXN; ++k) p.apples[k] = src.apples[k];
     p.ab = 0;
     const int64_t tiles = (src.E + TILE - 1) / TILE;

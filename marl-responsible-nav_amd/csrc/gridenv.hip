@@ -3394,6 +3394,50 @@ gw_status gw_graph_replayed(void *handle, void *stream) {
     return GW_OK;
 }
 
+namespace {
+// gw_pipeline_save / gw_pipeline_load: the host-side state a merged-path step leaves behind
+struct PipeState {
+    gw::Params qobs;
+    int32_t qobs_buf, dcur, obs_queued, mode;
+    uint32_t *desc;
+};
+}  // namespace
+
+int64_t gw_pipeline_state_bytes(void) { return (int64_t)sizeof(PipeState); }
+
+gw_status gw_pipeline_save(void *handle, void *buf) {
+    Env *env = static_cast<Env *>(handle);
+    if (!env || !buf) return fail(GW_ERR_ARG, "null argument");
+    PipeState st;
+    std::memset(&st, 0, sizeof(st));
+    st.qobs = env->qobs;
+    st.qobs_buf = env->qobs_buf;
+    st.dcur = env->dcur;
+    st.obs_queued = env->obs_queued ? 1 : 0;
+    st.mode = env->mode;
+    st.desc = env->desc;
+    std::memcpy(buf, &st, sizeof(st));
+    return GW_OK;
+}
+
+gw_status gw_pipeline_load(void *handle, const void *buf, void *stream) {
+    Env *env = static_cast<Env *>(handle);
+    if (!env || !buf) return fail(GW_ERR_ARG, "null argument");
+    PipeState st;
+    std::memcpy(&st, buf, sizeof(st));
+    if (st.mode != env->mode) return fail(GW_ERR_ARG, "gw_pipeline_load: state of another kernel path");
+    if (env->mode != 4 && (env->obs_async || st.obs_queued))
+        return fail(GW_ERR_STATE, "gw_pipeline_load: only the merged path's async pipeline (or synchronous obs)");
+    env->qobs = st.qobs;
+    env->qobs_buf = st.qobs_buf;
+    env->dcur = st.dcur;
+    env->desc = st.desc;
+    env->obs_queued = st.obs_queued != 0;
+    env->qobs_prof = false;
+    env->last_stream = static_cast<hipStream_t>(stream);
+    return GW_OK;
+}
+
 int64_t gw_kernel_path(void *handle) {
     const Env *env = static_cast<const Env *>(handle);
     return env ? env->mode : -1;

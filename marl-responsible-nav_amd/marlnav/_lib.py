@@ -174,7 +174,8 @@ EXPORTS = ["gw_create", "gw_reset", "gw_step", "gw_state_view", "gw_copy_state",
            "gw_soft_update2", "gw_td_target", "gw_mean_loss_fwd", "gw_mean_loss_bwd",
            "gw_eval_accum", "gw_profile_spans", "gw_patch_actor_workspace_floats", "gw_patch_actor_prepare",
            "gw_patch_actor_act", "gw_patch_cnn_workspace_floats", "gw_patch_cnn_prepare", "gw_patch_cnn_act",
-           "gw_maddpg_workspace_floats", "gw_maddpg_critic_grads", "gw_maddpg_actor_grads"]
+           "gw_maddpg_workspace_floats", "gw_maddpg_critic_grads", "gw_maddpg_actor_grads",
+           "gw_pipeline_state_bytes", "gw_pipeline_save", "gw_pipeline_load"]
 
 
 class GwObsSource(C.Structure):
@@ -217,7 +218,7 @@ def _declare(L):
     L.gw_cnn_prepare.argtypes = [p, C.POINTER(GwCnnActors), p, p]
     L.gw_cnn_prepare.restype = C.c_int
     L.gw_cnn_act.argtypes = [p, C.POINTER(GwCnnActors), p, C.c_int, C.c_float, C.c_uint64, C.c_uint64,
-                             p, p, p, p, p, p]
+                             p, p, p, p, p, p, p]
     L.gw_cnn_act.restype = C.c_int
     L.gw_create.argtypes = [C.POINTER(GwScenario), C.POINTER(GwConfig), C.c_int, C.POINTER(C.c_void_p)]
     L.gw_create.restype = C.c_int
@@ -237,6 +238,12 @@ def _declare(L):
     L.gw_profile_spans.restype = C.c_int
     L.gw_obs_patch.argtypes = [p, C.c_int32, p, p, p]
     L.gw_obs_patch.restype = C.c_int
+    L.gw_pipeline_state_bytes.argtypes = []
+    L.gw_pipeline_state_bytes.restype = C.c_int64
+    L.gw_pipeline_save.argtypes = [p, p]
+    L.gw_pipeline_save.restype = C.c_int
+    L.gw_pipeline_load.argtypes = [p, p, p]
+    L.gw_pipeline_load.restype = C.c_int
     L.gw_graph_replayed.argtypes = [p, p]
     L.gw_graph_replayed.restype = C.c_int
     L.gw_kernel_path.argtypes = [p]
@@ -281,21 +288,21 @@ def _declare(L):
     L.gw_set_last_error.argtypes = [C.c_char_p]
     L.gw_set_last_error.restype = None
     L.gw_actor_act.argtypes = [p, C.POINTER(GwMlpActors), p, C.c_int, C.c_float, C.c_uint64, C.c_uint64,
-                               p, p, p, p, p, p]
+                               p, p, p, p, p, p, p]
     L.gw_actor_act.restype = C.c_int
     L.gw_patch_actor_workspace_floats.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_int32]
     L.gw_patch_actor_workspace_floats.restype = C.c_int64
     L.gw_patch_actor_prepare.argtypes = [p, C.c_int32, C.POINTER(GwMlpActors), p, p]
     L.gw_patch_actor_prepare.restype = C.c_int
     L.gw_patch_actor_act.argtypes = [p, C.c_int32, C.POINTER(GwMlpActors), p, C.c_int, C.c_float, C.c_uint64,
-                                     C.c_uint64, p, p, p, p, p, p]
+                                     C.c_uint64, p, p, p, p, p, p, p]
     L.gw_patch_actor_act.restype = C.c_int
     L.gw_patch_cnn_workspace_floats.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int64]
     L.gw_patch_cnn_workspace_floats.restype = C.c_int64
     L.gw_patch_cnn_prepare.argtypes = [p, C.c_int32, C.POINTER(GwCnnActors), p, p]
     L.gw_patch_cnn_prepare.restype = C.c_int
     L.gw_patch_cnn_act.argtypes = [p, C.c_int32, C.POINTER(GwCnnActors), p, C.c_int, C.c_float, C.c_uint64,
-                                   C.c_uint64, p, p, p, p, p, p]
+                                   C.c_uint64, p, p, p, p, p, p, p]
     L.gw_patch_cnn_act.restype = C.c_int
     L.gw_actor_workspace_floats.argtypes = [C.c_int32, C.c_int32]
     L.gw_actor_workspace_floats.restype = C.c_int64

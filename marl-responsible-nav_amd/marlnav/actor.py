@@ -360,6 +360,15 @@ class CNNActor(nn.Module):
         return self.mlp[2:](h)
 
 
+def _ctr_ptr(counter_dev):
+    """Device address of the fused actors' noise-counter offset (a device int64 scalar) or None."""
+    if counter_dev is None:
+        return None
+    if not (counter_dev.is_cuda and counter_dev.dtype == torch.int64 and counter_dev.numel() == 1):
+        raise ValueError("counter_dev must be a device int64 scalar")
+    return counter_dev.data_ptr()
+
+
 class MultiAgentActors(nn.Module):
     """The K RL agents' actors: obs [K, E, H, W] -> logits [K, E, 9]."""
 
@@ -438,18 +447,20 @@ class MultiAgentActors(nn.Module):
     def act_env(self, env, mask: torch.Tensor | None = None, training: bool = True, tau: float = 1.0,
                 seed: int = 0, counter: int = 0, uniform: torch.Tensor | None = None,
                 actions_out: torch.Tensor | None = None, probs_out: torch.Tensor | None = None,
-                logits_out: torch.Tensor | None = None, patch: int = 0):
+                logits_out: torch.Tensor | None = None, patch: int = 0, counter_dev: torch.Tensor | None = None):
         """``act`` on the observation ``env`` last wrote, as ONE fused HIP kernel (gw_actor_act):
         the first layer from the env's obs descriptors (map + patched cells, no obs read back),
         layers 2-3 on f32 MFMA, Gumbel noise from Philox(seed; env, counter, k) or ``uniform``
         [K, E, 9], softmax, mask, argmax.  -> (actions [E, K] int32, probs [K, E, 9] float32).
+        counter_dev: a device int64 scalar added to ``counter`` when the kernel runs (the replay
+        ring's step count: a captured graph's replays then draw fresh noise).
         patch = P > 0: actors built for P x P inputs act on each agent's egocentric window
         (gw_patch_actor_act; the windows VecGridEnv.obs_patch(P) would write).
         Raises if the library or a GPU is missing (no fallback)."""
         from . import _lib
         if self.arch == "cnn":
             return self._act_env_cnn(env, mask, training, tau, seed, counter, uniform, actions_out, probs_out,
-                                     logits_out, int(patch))
+                                     logits_out, int(patch), counter_dev)
         net, K, E, dev = self.net, self.K, env.E, env.device
         patch = int(patch)
         st = self._fast
@@ -500,7 +511,7 @@ class MultiAgentActors(nn.Module):
             raise ValueError("act_env: mask must be a contiguous 16-bit [E, K] tensor")
         args = (C.byref(st["spec"]), st["ws"].data_ptr(), int(bool(training)),
                 float(tau), int(seed) & 0xFFFFFFFFFFFFFFFF, int(counter) & 0xFFFFFFFFFFFFFFFF,
-                uniform.contiguous().data_ptr() if uniform is not None else None,
+                _ctr_ptr(counter_dev), uniform.contiguous().data_ptr() if uniform is not None else None,
                 mask.data_ptr() if mask is not None else None, actions_out.data_ptr(), probs_out.data_ptr(),
                 logits_out.data_ptr() if logits_out is not None else None, torch.cuda.current_stream(dev).cuda_stream)
         if patch:
@@ -510,7 +521,7 @@ class MultiAgentActors(nn.Module):
         return actions_out, probs_out
 
     def _act_env_cnn(self, env, mask, training, tau, seed, counter, uniform, actions_out, probs_out, logits_out,
-                     patch=0):
+                     patch=0, counter_dev=None):
         """act_env for the CNN head: gw_cnn_act (layer 1 from the obs descriptors through the
         per-position delta table, include/actor_ops.h), then the same fused layers 2-3 + noise +
         softmax + mask + argmax as the MLP path.  patch = P: the head built for P x P inputs on each
@@ -568,7 +579,7 @@ class MultiAgentActors(nn.Module):
         if mask is not None and not (mask.shape == (E, K) and mask.element_size() == 2 and mask.is_contiguous()):
             raise ValueError("act_env: mask must be a contiguous 16-bit [E, K] tensor")
         args = (C.byref(st["spec"]), st["ws"].data_ptr(), int(bool(training)), float(tau),
-                int(seed) & 0xFFFFFFFFFFFFFFFF, int(counter) & 0xFFFFFFFFFFFFFFFF,
+                int(seed) & 0xFFFFFFFFFFFFFFFF, int(counter) & 0xFFFFFFFFFFFFFFFF, _ctr_ptr(counter_dev),
                 uniform.contiguous().data_ptr() if uniform is not None else None,
                 mask.data_ptr() if mask is not None else None, actions_out.data_ptr(), probs_out.data_ptr(),
                 logits_out.data_ptr() if logits_out is not None else None, torch.cuda.current_stream(dev).cuda_stream)

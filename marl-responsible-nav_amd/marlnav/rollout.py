@@ -156,6 +156,11 @@ class Rollout:
         self.fused = (actors is not None and actors.fusable(env, patch)) if fused is None else bool(fused)
         self.seed = int(seed)
         self._calls = 0  # Philox counter of the fused path's Gumbel noise (never repeats)
+        # with a replay ring the fused actor's counter is _noise_base + the ring's DEVICE step
+        # count (read by the kernel at launch: graph replays draw fresh noise), which equals
+        # _calls: _noise_base is _calls at the last ring reset
+        self._noise_base = 0
+        self._graphs = None
         self._actions = torch.empty((env.E, env.K), dtype=torch.int32, device=env.device)
         self.training = training
         self.group = group
@@ -245,6 +250,8 @@ class Rollout:
                 self.replay.obs[0].copy_(obs)
             self.replay.t = 0
             self.replay.t_dev.zero_()
+            self._noise_base = self._calls
+            self._graphs = None
         else:
             self.env.reset()
             if self.patch and not self.fused:
@@ -252,7 +259,7 @@ class Rollout:
         self.t = 0
 
     @torch.no_grad()
-    def resume(self):
+    def resume(self, calls: int | None = None):
         """Continue after ReplayRing.load_state_dict: the envs start new episodes (as the reference
         does after load_checkpoint) and their first obs goes into the ring's current slot.  That
         slot was the next state of the last stored transition, so that transition keeps it as its
@@ -274,6 +281,11 @@ class Rollout:
         else:
             rp.obs[cur].copy_(obs)
         self.t = t
+        # the fused actor's noise counter continues where the saved run stopped (calls = its
+        # actor calls; restarting at 0 would replay the original run's exploration noise)
+        self._calls = int(calls) if calls is not None else max(self._calls, t)
+        self._noise_base = self._calls - t
+        self._graphs = None
 
     def _obs_now(self):
         if self.replay is not None:
@@ -287,8 +299,13 @@ class Rollout:
         cur = self.t % self.replay.S if self.replay is not None else 0
         if self.actors is not None and self.fused:
             probs_out = self.replay.probs[cur] if self.replay is not None else None
-            actions, probs = self.actors.act_env(env, mask, self.training, seed=self.seed, counter=self._calls,
-                                                 actions_out=self._actions, probs_out=probs_out, patch=self.patch)
+            if self._dev_counter():  # counter = _noise_base + t_dev (== _calls), read on the device
+                actions, probs = self.actors.act_env(env, mask, self.training, seed=self.seed, counter=self._noise_base,
+                                                     counter_dev=self.replay.t_dev, actions_out=self._actions,
+                                                     probs_out=probs_out, patch=self.patch)
+            else:
+                actions, probs = self.actors.act_env(env, mask, self.training, seed=self.seed, counter=self._calls,
+                                                     actions_out=self._actions, probs_out=probs_out, patch=self.patch)
             self._calls += 1
         elif self.actors is not None:
             if not self.patch:
@@ -341,6 +358,57 @@ class Rollout:
             self._reduce(r.stats, tick)
         return r
 
+    def _dev_counter(self) -> bool:
+        """Whether the fused actor reads its noise counter from the ring's device step count:
+        with a ring whose count the step kernels advance (statistics on) or that is advanced right
+        after each step (FeAR joined); with the unjoined FeAR and no statistics the count is
+        advanced one step late, so the host counter is used."""
+        return self.replay is not None and (self._acc is not None or not self.env.fear_async)
+
+    def capture(self, n: int) -> "RolloutGraphs":
+        """Capture the rollout's steps (actor, env step, ring writes, statistics, return gather)
+        as HIP graphs for the launch-bound small-batch regime (C2: 4,096 envs), where a step is
+        bound by the host's launches, not by the GPU.  A step's ring slots depend on t mod S, so
+        there is one graph of n steps per phase of the ring (S // n graphs, S % n == 0), replayed
+        in rotation; the host-side env pipeline state each graph ends in is saved with it
+        (gw_pipeline_save) and restored after its replay.  The fused actor draws its noise
+        counter from the ring's device step count, so replays draw fresh noise, and a replayed
+        rollout equals the eager one bit for bit (tests/test_gpu_rollout_graph.py).
+
+        Requirements: the fused actor, a replay ring, full-grid obs, one rank, FeAR joined; the
+        env's obs synchronous, or async on the merged kernel path with n even after at least one
+        step; a ReturnGather (if any) with window == n and nothing pending.
+        Nothing runs at capture: the state is untouched until the first replay."""
+        env, rp = self.env, self.replay
+        if not (self.fused and rp is not None and not self.patch and not self.distributed and self._dev_counter()):
+            raise _lib.GwError("Rollout.capture: the fused actor, a replay ring, full-grid obs and one rank")
+        if rp.S % n:
+            raise _lib.GwError(f"Rollout.capture: n must divide the ring's {rp.S} slots")
+        if env.obs_async and (env.kernel_path != "merged" or n % 2 or not env._obs_queued):
+            raise _lib.GwError("Rollout.capture: async obs only on the merged path, an even n, after a step")
+        g = self.gather
+        if g is not None and (g.window != n or g._fill != 0 or g.distributed):
+            raise _lib.GwError("Rollout.capture: the gather needs window == n, no pending steps and one rank")
+        self._flush()
+        t0, rt0, calls0 = self.t, rp.t, self._calls
+        start = env.pipeline_save()
+        graphs, ends = [], []
+        with torch.cuda.device(env.device):
+            torch.cuda.synchronize(env.device)
+            for _ in range(rp.S // n):
+                cg = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(cg):
+                    env.profile(False)
+                    for _i in range(n):
+                        self.step()
+                graphs.append(cg)
+                ends.append(env.pipeline_save())
+        # nothing ran: the host-side state is the pre-capture one
+        self.t, rp.t, self._calls = t0, rt0, calls0
+        env.pipeline_load(start)
+        self._graphs = RolloutGraphs(self, n, graphs, ends, t0 % rp.S)
+        return self._graphs
+
     def totals(self) -> dict:
         """Episode statistics summed over all steps (and ranks): completed-episode return sum,
         episodes, FeAR, crashes, apples, shaped reward, completed-episode length sum, env-steps.
@@ -360,3 +428,26 @@ class Rollout:
             raise RuntimeError("Rollout(gather=ReturnGather(...)) needed")
         self._flush()
         return self.gather.completed(last)
+
+
+class RolloutGraphs:
+    """The ring-phase graphs of ``Rollout.capture``: ``replay()`` advances the rollout by n steps
+    with one graph launch (the graph of the current ring phase)."""
+
+    def __init__(self, ro: Rollout, n: int, graphs: list, ends: list, phase0: int):
+        self.ro, self.n, self.graphs, self.ends, self.phase0 = ro, n, graphs, ends, phase0
+
+    def replay(self):
+        ro = self.ro
+        if ro._graphs is not self:
+            raise RuntimeError("RolloutGraphs.replay: the rollout was reset / resumed / recaptured since the capture")
+        rp = ro.replay
+        off = (ro.t - self.phase0) % rp.S
+        if off % self.n:
+            raise RuntimeError("RolloutGraphs.replay: the rollout is not on a graph boundary (eager steps in between)")
+        g = off // self.n
+        self.graphs[g].replay()
+        ro.env.pipeline_load(self.ends[g])
+        ro.t += self.n
+        rp.t = ro.t
+        ro._calls += self.n

@@ -251,6 +251,21 @@ class VecGridEnv:
                         gather.push()
         return StepGraph(self, g)
 
+    def pipeline_save(self) -> bytes:
+        """The host-side pipeline state (gw_pipeline_save): after capturing a graph of steps."""
+        lib = self.lib
+        buf = (C.c_char * int(lib.gw_pipeline_state_bytes()))()
+        _lib.check(lib.gw_pipeline_save(self.handle, buf), "gw_pipeline_save")
+        return bytes(buf)
+
+    def pipeline_load(self, state: bytes, queued: bool | None = None):
+        """Restore a pipeline_save state (after replaying the graph it was saved for; the next
+        queued writer then runs on the current stream)."""
+        buf = (C.c_char * len(state)).from_buffer_copy(state)
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.gw_pipeline_load(self.handle, buf, self._stream()), "gw_pipeline_load")
+        self._obs_queued = self.obs_async if queued is None else bool(queued)
+
     def _replayed(self):
         """Host-side pipeline state after a StepGraph replay (gw_graph_replayed)."""
         with torch.cuda.device(self.device):

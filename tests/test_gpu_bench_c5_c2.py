@@ -15,7 +15,7 @@ and of envs whose episode ran into the cap are compared bit for bit.  Over all 6
 gathered completed-episode list equals the per-step done envs' returns in the reference's order
 (maddpg/agent.py:229-247).
 
-C2 (``bench.py --config c2``): 4,096 envs, FeAR off (weight -2), the merged ``step_obs`` path with
+C2's env alone (``bench.py --config c2env``): 4,096 envs, FeAR off (weight -2), the merged ``step_obs`` path with
 async obs, 5 eager warmup steps, then the timed steps as replays of a 16-step HIP graph
 (``VecGridEnv.capture_steps(16, gather)``) whose gather window is compacted inside the graph.  The
 oracle steps all 4,096 envs with the device RNG's policies (native mode): positions after every

@@ -1,0 +1,115 @@
+"""C2 as BASELINE names it (``bench.py --config c2``): the MADDPG rollout with the configs/mlp.yaml
+actors acting on the full-grid obs every step (maddpg/agent.py:89, 109-127, 190-197) at 4,096 envs,
+FeAR off (configs/custom.yaml, weight -2), replayed as HIP graphs (``Rollout.capture``: one graph
+of 16 steps per phase of the replay ring, the fused actor's noise counter read from the ring's
+device step count).
+
+1. The graph-replayed rollout == the eager rollout bit for bit: the whole replay ring (obs,
+   terminal obs, action probabilities, shaped rewards, terminations, dones), the env state, the
+   statistics totals and the gathered completed-episode list, after 5 eager warmup steps, every
+   ring-phase graph replayed (graph 0 twice: the cycle closes) and eager steps after them.
+2. The eager rollout == the C oracle fed the actions the actor chose (``vec_step(rl_act=...)``):
+   every step's shaped rewards (the ring's reward slots), terminations and dones for all 4,096
+   envs, and the observations in the ring at the end.
+"""
+import numpy as np
+import pytest
+import torch
+
+from marlnav import scenario as S
+from marlnav.vec_env import VecGridEnv
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+E, CAP, SEED, G, WARM = 4096, 150, 42, 16, 5
+SLOTS = 64                       # -(-200_000 // 4096) + 1 = 50, rounded up to a multiple of G
+T = WARM + (SLOTS // G + 1) * G + 3
+
+
+def _rollout(graph: bool):
+    from marlnav.maddpg import MADDPG
+    from marlnav.parallel import ReturnGather
+    from marlnav.rollout import Rollout
+    mp = pytest.MonkeyPatch()
+    mp.delenv("GW_KERNEL", raising=False)
+    mp.setenv("GW_OBS_CHUNKS", "2")  # bench.py's rollout default (read by gw_create)
+    try:
+        env = VecGridEnv("grid32", num_envs=E, fear=False, fear_weight=-2.0, max_steps=CAP, auto_reset=True,
+                         seed=SEED, stats=True)
+    finally:
+        mp.undo()
+    assert env.kernel_path == "merged"
+    learner = MADDPG(env.K, env.H, env.W, device=env.device, seed=0, capturable=True)
+    gather = ReturnGather(E, 0, 1, env.device, window=G)
+    ro = Rollout(env, learner.actors, replay_slots=SLOTS, training=True, seed=SEED, obs_async=True, gather=gather)
+    assert ro.fused
+    ro.reset()
+    acts = []
+    t = 0
+    while t < T:
+        if graph and t == WARM:
+            gather.compact()
+            graphs = ro.capture(G)
+            assert len(graphs.graphs) == SLOTS // G
+        if graph and WARM <= t and t + G <= T - 3:
+            graphs.replay()
+            t += G
+            continue
+        ro.step()
+        acts.append((t, ro._actions.clone()))
+        t += 1
+    ro.fence()
+    rp = ro.replay
+    out = {n: getattr(rp, n).clone() for n in ("obs", "final_obs", "probs", "reward", "term", "done")}
+    out["state"] = env.state()
+    out["totals"] = ro.totals()
+    out["scores"] = ro.completed_scores()
+    out["t"] = (ro.t, rp.t, int(rp.t_dev), ro._calls)
+    torch.cuda.synchronize()
+    env.close()
+    return out, acts
+
+
+@pytest.fixture(scope="module")
+def runs():
+    return _rollout(False), _rollout(True)
+
+
+def test_graph_rollout_equals_eager(runs):
+    (a, _), (b, _) = runs
+    assert a["t"] == b["t"] == (T, T, T, T)
+    for n in ("obs", "final_obs", "probs", "reward", "term", "done"):
+        assert torch.equal(a[n], b[n]), n
+    for n, v in a["state"].items():
+        assert torch.equal(v, b["state"][n]), n
+    assert a["totals"] == b["totals"]
+    np.testing.assert_array_equal(a["scores"], b["scores"])
+    assert len(a["scores"]) > 1000
+
+
+def test_eager_rollout_matches_oracle(runs):
+    (a, acts), _ = runs
+    assert len(acts) == T
+    sc = S.builtin("grid32")
+    orc = O.OracleEnvs(sc, E, fear=False, fear_weight=-2.0, max_steps=CAP, seed=SEED, reset=False)
+    obs = np.zeros((sc.K, E, sc.HW), np.float32)
+    orc.reset_all(obs=obs, nthreads=16)
+    outs = (O.StepOut * E)()
+    K = sc.K
+    ring_obs = a["obs"].cpu().numpy().reshape(SLOTS, K, E, -1)
+    reward = a["reward"].cpu().numpy()
+    term = a["term"].cpu().numpy()
+    done = a["done"].cpu().numpy()
+    for t, act in acts:
+        orc.vec_step(act.cpu().numpy(), obs=obs, outs=outs, nthreads=16)
+        slot = t % SLOTS
+        if t >= T - SLOTS + 1:  # the ring slots not overwritten since
+            o = [outs[e] for e in range(E)]
+            np.testing.assert_array_equal(reward[slot], np.array([list(x.shaped)[:K] for x in o]),
+                                          err_msg=f"shaped reward at step {t}")
+            np.testing.assert_array_equal(term[slot], np.array([list(x.term)[:K] for x in o], np.uint8),
+                                          err_msg=f"term at step {t}")
+            np.testing.assert_array_equal(done[slot], np.array([x.done for x in o], np.uint8),
+                                          err_msg=f"done at step {t}")
+    np.testing.assert_array_equal(ring_obs[T % SLOTS], obs, err_msg="the last step's obs in the ring")
