@@ -595,12 +595,15 @@ def main():
             if pc and not args.envs and args.fear < 0 and not fused and dom in pc["kernels"] \
                     and args.obs_dtype == "f32":
                 pk = pc["kernels"][dom]
-                traffic = pk.get("hbm_bytes_per_launch")
                 traffic_src = pc["source"]
-                # the same kernel's rocprofv3 busy time per launch (union of its launches'
-                # intervals in the kernel trace / launches) for comparison
-                if bytes_per_launch:
-                    prof_frac = bytes_per_launch / (pk.get("busy_us", pk["avg_us"]) * 1e-6) / \
+                # per step on both sides (the kernel trace may count a step's kernel as several
+                # launches, e.g. the chunked obs writer): the trace's HBM bytes and busy time per
+                # step, the live launches per step
+                live_lps = per_kind.get(dom, {}).get("launches_per_step") or 1.0
+                if pk.get("hbm_bytes_per_step") is not None:
+                    traffic = pk["hbm_bytes_per_step"] / live_lps
+                if bytes_per_launch and pk.get("busy_us_per_step"):
+                    prof_frac = bytes_per_launch * live_lps / (pk["busy_us_per_step"] * 1e-6) / \
                         (1e12 if mfma else 1e9) / peak_u
         except (OSError, KeyError, ValueError, TypeError):
             pass

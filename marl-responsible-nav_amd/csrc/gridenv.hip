@@ -2288,6 +2288,7 @@ hipError_t launch_obs(const Env *env, const gw::Params &p, float *obs, float *fi
 hipEvent_t next_event(Env *env);
 gw_status prof_span_begin(Env *env, size_t &idx);
 gw_status prof_span_end(Env *env, size_t idx, int kind);
+void prof_span_split(Env *env, int kind);
 
 // launch the queued obs_kernel on the obs stream, after its world update and (after != null)
 // after the caller's work up to `after`
@@ -2370,24 +2371,39 @@ hipEvent_t next_event(Env *env) {
     return env->ev_pool[env->ev_used++];
 }
 
-// a profiled span: two timing events handed to the span's kernel launches (gw_launch)
+// a profiled span: two timing events handed to the span's kernel launches (gw_launch).  The open
+// span's first event index is also kept thread-locally, so a launch sequence can split it
+// (prof_span_split: the obs writer's chunks are one span each, as a kernel trace counts them)
+thread_local size_t t_span_idx = 0;
+
 gw_status prof_span_begin(Env *env, size_t &idx) {
     idx = env->ev_used;
     hipEvent_t a = next_event(env), b = next_event(env);
     if (!a || !b) return fail(GW_ERR_HIP, "hipEventCreate failed");
     t_span_start = a;
     t_span_stop = b;
+    t_span_idx = idx;
     return GW_OK;
 }
 
 gw_status prof_span_end(Env *env, size_t idx, int kind) {
+    (void)idx;  // the span open now (a split may have replaced the one `idx` began)
     if (t_span_start) {  // no kernel was launched in the span: nothing to time
-        env->ev_used = idx;
+        env->ev_used = t_span_idx;
     } else {
-        env->spans.push_back({idx, idx + 1, kind});
+        env->spans.push_back({t_span_idx, t_span_idx + 1, kind});
     }
     t_span_start = t_span_stop = nullptr;
     return GW_OK;
+}
+
+// close the open span after the launches made so far and open the next one (no-op without an
+// open span or before its first launch)
+void prof_span_split(Env *env, int kind) {
+    if (!t_span_stop || t_span_start) return;
+    env->spans.push_back({t_span_idx, t_span_idx + 1, kind});
+    size_t idx = 0;
+    if (prof_span_begin(env, idx) != GW_OK) t_span_start = t_span_stop = nullptr;
 }
 
 }  // namespace
@@ -2658,6 +2674,7 @@ hipError_t launch_obs(const Env *env, const gw::Params &p, float *obs, float *fi
     const int64_t blocks = (n + env->obs_be - 1) / env->obs_be;
     const int64_t c = std::max<int64_t>(1, std::min<int64_t>(env->obs_chunks, blocks));
     for (int64_t i = 0; i < c; ++i) {
+        if (i > 0) prof_span_split(const_cast<Env *>(env), 1);  // profiled: one span per chunk
         gw::Params q = p;
         q.e_begin = p.e_begin + blocks * i / c * env->obs_be;
         q.e_end = std::min(p.e_end, p.e_begin + blocks * (i + 1) / c * env->obs_be);

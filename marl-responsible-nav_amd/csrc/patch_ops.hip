@@ -44,9 +44,11 @@ __device__ __forceinline__ float map_value(const uint32_t *road, int H, int W, i
     return ((road[cell >> 5] >> (cell & 31)) & 1u) ? 0.0f : -1.0f;
 }
 
-// MODE 0: P * P <= 256, the windows assembled in LDS; 1: one thread per element (large windows);
-// 2: P % 4 == 0, one thread per 16-byte piece of a window row (map bits + overrides in registers,
-// no LDS image: every store is a whole aligned float4 of the [K][E][P*P] run)
+// MODE 0: P * P <= 256, the windows assembled in LDS (kept for A/B); 1: one thread per element
+// (windows too large for the tables below); 2: P % 4 == 0, one thread per 16-byte piece of a
+// window row (map bits + overrides in registers, no LDS image: every store is a whole aligned
+// float4 of the [K][E][P*P] run); 3: any P, one thread per 16-byte piece of the block's run (a
+// byte table of the patched cells in LDS, map values from the road bits)
 template <int MODE>
 __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a, unsigned long long *dbg) {
     constexpr bool SMALL = MODE == 0;
@@ -235,6 +237,85 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a, unsign
                 o4[j] = make_float4(v[0], v[1], v[2], v[3]);
             }
         }
+    } else if (MODE == 3 && a.patch) {
+        // any P: the block's [nenv * PP] run of one agent leaves as aligned float4 stores; a byte
+        // table (the surviving patch index + 1 of every window cell, 0 = map value) is built in
+        // LDS per agent, so a thread's four cells need one u32 table read, not an override loop
+        uint8_t *s_tab = reinterpret_cast<uint8_t *>(s_pv + 2 * PB * K * np);
+        const int len = nenv * PP;
+        const uint32_t m_pp = (uint32_t)((0x100000000ull + (uint64_t)PP - 1) / (uint64_t)PP);
+        const uint32_t m_p = (uint32_t)((0x100000000ull + (uint64_t)P - 1) / (uint64_t)P);
+        for (int k = 0; k < K; ++k) {
+            const int64_t off = ((int64_t)k * a.E + e0) * PP;
+            float *o = a.patch + off;
+            const int lead = (int)((4 - (off & 3)) & 3);  // floats before the first 16-byte boundary
+            const int sh = (4 - lead) & 3;                  // table index = run index + sh: the float4
+                                                            // pieces' four entries are one aligned u32
+            if (k > 0) __syncthreads();                     // the previous agent's table is read
+            for (int w = tid; w < (len + sh + 3) / 4; w += THREADS) reinterpret_cast<uint32_t *>(s_tab)[w] = 0u;
+            __syncthreads();
+            for (int t = tid; t < nenv * np; t += THREADS) {
+                const int el = t / np, i = t - el * np;
+                const int pw = s_pw[(el * K + k) * np + i];
+                if (pw >= 0) s_tab[el * PP + pw + sh] = (uint8_t)(i + 1);
+            }
+            __syncthreads();
+            if (!all_write) {  // partial resets: only the written envs' windows (rare)
+                for (int i = tid; i < len; i += THREADS) {
+                    const int el = (int)__umulhi((uint32_t)i, m_pp), c = i - el * PP;
+                    if (!(s_flag[el] & D_WRITE)) continue;
+                    const int slot = el * K + k, ctr = s_ctr[slot];
+                    const int wr = (int)__umulhi((uint32_t)c, m_p);
+                    const int idx = s_tab[i + sh];
+                    o[i] = idx ? s_pv[slot * np + idx - 1]
+                               : map_value(s_road, H, W, (ctr >> 16) + wr - half, (ctr & 0xFFFF) + c - wr * P - half);
+                }
+                continue;
+            }
+            for (int i = tid; i < min(lead, len); i += THREADS) {
+                const int el = (int)__umulhi((uint32_t)i, m_pp), c = i - el * PP;
+                const int slot = el * K + k, ctr = s_ctr[slot];
+                const int wr = (int)__umulhi((uint32_t)c, m_p);
+                const int idx = s_tab[i + sh];
+                o[i] = idx ? s_pv[slot * np + idx - 1]
+                           : map_value(s_road, H, W, (ctr >> 16) + wr - half, (ctr & 0xFFFF) + c - wr * P - half);
+            }
+            const int n4 = (len - lead) / 4;
+            float4 *o4 = reinterpret_cast<float4 *>(o + lead);
+            for (int j = tid; j < n4; j += THREADS) {
+                const int i0 = lead + 4 * j;
+                int el = (int)__umulhi((uint32_t)i0, m_pp), c = i0 - el * PP;
+                int wr = (int)__umulhi((uint32_t)c, m_p), wc = c - wr * P;
+                int ctr = s_ctr[el * K + k];
+                const uint32_t tab = reinterpret_cast<const uint32_t *>(s_tab)[(i0 + sh) >> 2];
+                float v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (u > 0) {  // the next cell of the run: next column, row or window
+                        if (++wc == P) {
+                            wc = 0;
+                            if (++wr == P) {
+                                wr = 0;
+                                ++el;
+                                ctr = s_ctr[el * K + k];
+                            }
+                        }
+                    }
+                    const uint32_t idx = (tab >> (8 * u)) & 0xFFu;
+                    v[u] = idx ? s_pv[(el * K + k) * np + (int)idx - 1]
+                               : map_value(s_road, H, W, (ctr >> 16) + wr - half, (ctr & 0xFFFF) + wc - half);
+                }
+                o4[j] = make_float4(v[0], v[1], v[2], v[3]);
+            }
+            for (int i = lead + 4 * n4 + tid; i < len; i += THREADS) {
+                const int el = (int)__umulhi((uint32_t)i, m_pp), c = i - el * PP;
+                const int slot = el * K + k, ctr = s_ctr[slot];
+                const int wr = (int)__umulhi((uint32_t)c, m_p);
+                const int idx = s_tab[i + sh];
+                o[i] = idx ? s_pv[slot * np + idx - 1]
+                           : map_value(s_road, H, W, (ctr >> 16) + wr - half, (ctr & 0xFFFF) + c - wr * P - half);
+            }
+        }
     } else if (a.patch) {  // one thread per element (consecutive lanes: consecutive floats), overrides in registers
         // i / PP and c / P as multiply-highs (i < PB * PP; P >= 2)
         const uint32_t m_pp = (uint32_t)((0x100000000ull + (uint64_t)PP - 1) / (uint64_t)PP);
@@ -283,28 +364,51 @@ namespace gw {
 
 unsigned long long *g_patch_dbg = nullptr;
 
+template <int MODE>
+hipError_t launch_mode(const PatchArgs &a, unsigned grid, size_t lds, hipStream_t s) {
+    // above the 64 KB a launch gets by default, the kernel's dynamic-LDS limit is raised once (up
+    // to gfx950's 160 KB per workgroup)
+    static size_t granted = 64 * 1024;
+    if (lds > granted) {
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&window_kernel<MODE>),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        granted = lds;
+    }
+    gwprof::launch(window_kernel<MODE>, dim3(grid), dim3(THREADS), lds, s, a, g_patch_dbg);
+    return hipGetLastError();
+}
+
 hipError_t launch_windows(const PatchArgs &a, hipStream_t s) {
     const int np = a.N + 1, PP = a.P * a.P;
-    // LDS: road bitmask, flags, centres, patch cells + values; MODE 0 adds one agent's window run,
-    // MODE 2 its nibble table (PB * K * P * P / 4 u16, patch indices 1..15).  A mode is taken only
-    // if its LDS fits the 64 KB a launch gets without an attribute (else the per-element writer).
+    // LDS: road bitmask, flags, centres, patch cells + values, and per mode: MODE 0 one agent's
+    // window run (PP <= 256), MODE 2 the nibble table (PB * K * P * P / 4 u16, patch indices
+    // 1..15), MODE 3 one agent's byte table (PB * P * P + 4 bytes).  Preference: MODE 2 (P % 4 ==
+    // 0), else MODE 3, each if its LDS fits gfx950's 160 KB per workgroup (above 64 KB through the
+    // dynamic-LDS attribute), else the per-element writer (MODE 1, e.g. windows wider than the
+    // byte table allows).
     const size_t base = sizeof(uint32_t) * ((a.H * a.W + 31) / 32 + PB) + sizeof(int) * 2 * PB * a.K +
                         sizeof(uint32_t) * (size_t)2 * 2 * PB * a.K * np;
-    const size_t extra[3] = {sizeof(float) * (size_t)PB * PP, 0, sizeof(uint16_t) * (size_t)PB * a.K * (PP / 4)};
-    constexpr size_t LDS_MAX = 64 * 1024;
+    const size_t extra[4] = {sizeof(float) * (size_t)PB * PP, 0, sizeof(uint16_t) * (size_t)PB * a.K * (PP / 4),
+                             (size_t)PB * PP + 16};
+    constexpr size_t LDS_MAX = 160 * 1024;
     int mode = (a.P % 4 == 0 && np < 16 && base + extra[2] <= LDS_MAX) ? 2
-               : (PP <= 64 * MAXPL && base + extra[0] <= LDS_MAX) ? 0 : 1;
+               : (np < 256 && base + extra[3] <= LDS_MAX) ? 3 : 1;
     static const char *force = std::getenv("GW_PATCH_MODE");  // (measurement only: A/B of the writers)
-    if (force && (std::atoi(force) == 1 || (std::atoi(force) == 0 && PP <= 64 * MAXPL))) mode = std::atoi(force);
+    if (force) {
+        const int f = std::atoi(force);
+        if (f == 1 || (f == 0 && PP <= 64 * MAXPL && base + extra[0] <= LDS_MAX) ||
+            (f == 2 && a.P % 4 == 0 && np < 16 && base + extra[2] <= LDS_MAX) || (f == 3 && base + extra[3] <= LDS_MAX))
+            mode = f;
+    }
     const size_t lds = base + extra[mode];
     const unsigned grid = (unsigned)((a.E + PB - 1) / PB);
-    if (mode == 2)
-        gwprof::launch(window_kernel<2>, dim3(grid), dim3(THREADS), lds, s, a, g_patch_dbg);
-    else if (mode == 0)
-        gwprof::launch(window_kernel<0>, dim3(grid), dim3(THREADS), lds, s, a, g_patch_dbg);
-    else
-        gwprof::launch(window_kernel<1>, dim3(grid), dim3(THREADS), lds, s, a, g_patch_dbg);
-    return hipGetLastError();
+    switch (mode) {
+        case 0: return launch_mode<0>(a, grid, lds, s);
+        case 2: return launch_mode<2>(a, grid, lds, s);
+        case 3: return launch_mode<3>(a, grid, lds, s);
+        default: return launch_mode<1>(a, grid, lds, s);
+    }
 }
 
 }  // namespace gw

@@ -74,16 +74,18 @@ def test_fused_actor_on_reference_trajectories(tag):
             want = actors(obs.reshape(1, -1, 10, 16))[0]
         got = torch.stack(fused)
         torch.testing.assert_close(got, want, rtol=2e-4, atol=2e-4)
-        # eval-mode action = first maximum of the masked softmax (ma_customenv action mask)
+        # eval-mode action = first maximum of the masked softmax (ma_customenv action mask), i.e.
+        # of the masked logits; compared where the top two allowed logits are further apart than
+        # the logit tolerance (a trained policy's softmax saturates, so probabilities cannot tell)
         bits = (torch.stack(masks).to(torch.int32).unsqueeze(-1) >> torch.arange(9, device="cuda")) & 1
-        p = torch.where(bits.bool(), torch.softmax(want, -1), torch.zeros((), device="cuda"))
-        top2 = p.topk(2, -1).values
-        clear = (top2[:, 0] - top2[:, 1]) > 1e-5
-        torch.testing.assert_close(torch.stack(acts)[clear].long(), p.argmax(-1)[clear])
+        lm = torch.where(bits.bool(), want, torch.full((), float("-inf"), device="cuda"))
+        top2 = lm.topk(2, -1).values
+        clear = (top2[:, 0] - top2[:, 1]) > 1e-3
+        torch.testing.assert_close(torch.stack(acts)[clear].long(), lm.argmax(-1)[clear])
         n_cmp += int(clear.sum())
         n_tie += int((~clear).sum())
     print(f"{tag}: {n_cmp} actions compared, {n_tie} near-ties skipped")
-    assert n_cmp > 2000
+    assert n_cmp > 2500
 
 
 @pytest.mark.parametrize("tag", TAGS)

@@ -64,6 +64,42 @@ def test_patch_equals_cropped_full_obs(scen, E, P, fear, async_obs):
     env.close()
 
 
+@pytest.mark.parametrize("K,P", [(8, 16), (8, 32), (8, 23), (2, 64), (2, 100)])
+def test_patch_large_windows_and_many_agents(K, P):
+    """The K x P combinations whose LDS exceeds the 64 KB a launch gets by default (before
+    cca6a63 they failed to launch; until round 4 they fell back to the per-element writer): with
+    all 8 world agents learning (K = 8, 64 x 64) the nibble table of P = 16 (70 KB of LDS) and the
+    byte table of P = 32 / odd P = 23 run with the dynamic-LDS attribute raised; P = 64 (141 KB,
+    K = 2) too; P = 100 (a 320 KB table) takes the per-element writer.  Every window == the
+    -1-padded crop of the full obs, terminal windows included."""
+    from marlnav import scenario as S
+    sc = S.compile_scenario(S.level3_like(64, 64, 8, K), name=f"grid64_n8_k{K}")
+    E = 300
+    env = VecGridEnv(sc, num_envs=E, fear=False, max_steps=12, seed=5, final_obs=True, debug=True)
+    env.reset()
+    W = env.W
+    bad = torch.zeros((), dtype=torch.int64, device="cuda")
+    done_seen = torch.zeros((), dtype=torch.int64, device="cuda")
+    pos = env.state()["pos"]
+    p = env.obs_patch(P)
+    for k in range(K):
+        bad += (p[k] != crop(env.out["obs"][k], pos[k], P, W)).sum()
+    for t in range(16):
+        r = env.step()
+        patch, fin = env.obs_patch(P, final=True)
+        pos = env.state()["pos"]
+        d = r.done != 0
+        done_seen += d.sum()
+        for k in range(K):
+            bad += (patch[k] != crop(r.obs[k], pos[k], P, W)).sum()
+            ref_f = crop(r.final_obs[k], r.final_pos[:, k].contiguous(), P, W)
+            bad += (fin[k][d] != ref_f[d]).sum()
+    torch.cuda.synchronize()
+    assert int(done_seen) > 0
+    assert int(bad) == 0
+    env.close()
+
+
 def test_patch_without_dense_obs():
     """obs=False: no full-grid obs is written at all, the patches still come from the descriptors."""
     a = VecGridEnv("grid32", num_envs=1000, fear=True, seed=3, max_steps=20)

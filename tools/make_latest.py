@@ -13,8 +13,13 @@ KIND = {"gw::obs_kernel": "obs_kernel", "gw::step_v2": "step_kernel", "gw::fear_
         "wcnn_l1_kernel": "cnn_l1_kernel", "cnn_l1_kernel": "cnn_l1_kernel"}
 
 
+STEP_KERNELS = ("gw::step_v2", "gw::step_obs", "gw::step_kernel_fear", "gw::step_kernel_nofear")
+
+
 def main(tag, config, cmd=None):
     s = json.load(open(os.path.join(ROOT, "profiles", tag, "summary.json")))
+    # steps in the traced run: the world-update kernel runs once per step
+    steps = max((v["calls"] for n, v in s.items() if n.split("<")[0].strip() in STEP_KERNELS), default=0) or None
     kernels = {}
     for name, v in s.items():
         kind = KIND.get(name.split("<")[0].strip())
@@ -24,6 +29,12 @@ def main(tag, config, cmd=None):
                 k["hbm_bytes_per_launch"] = v["hbm_mb"] * 1e6
             if v.get("busy_us"):
                 k["busy_us"] = v["busy_us"]  # union of the launches' intervals / launches
+            if steps:  # per step (a kernel may run as several launches per step: the chunked writer)
+                k["launches_per_step"] = v["calls"] / steps
+                if v.get("busy_us"):
+                    k["busy_us_per_step"] = v["busy_us"] * v["calls"] / steps
+                if v.get("hbm_mb") is not None:
+                    k["hbm_bytes_per_step"] = v["hbm_mb"] * 1e6 * v["calls"] / steps
             kernels[kind] = k
     cmd = cmd or f"python bench.py --config {config}"
     path = os.path.join(ROOT, "profiles", "latest.json")
