@@ -536,7 +536,8 @@ def main():
     stats = env.out["stats"].sum(0).cpu().tolist()
     gathered = None
     if gather is not None:
-        gathered = {"episodes": int(gather.n_completed.item()), "bytes_per_rank_per_step": 9 * gather.emax,
+        gathered = {"episodes": int(gather.n_completed.item()), "bytes_per_rank_per_step": gather.slot_bytes,
+                    "cap": getattr(gather, "cap", None),
                     "mean_return_last_100": float(gather.completed(last=100).mean()) if int(gather.n_completed) else None}
 
     if rank == 0:

@@ -37,6 +37,33 @@ gw_status gw_return_compact(const uint8_t *recv, int64_t steps, int32_t world, i
                             int64_t *n_completed, int32_t *scratch, void *stream);
 int64_t gw_return_compact_scratch(int64_t steps, int32_t world, int64_t emax);
 
+/* The packed per-step return gather of several ranks (marlnav/parallel.py ReturnGather, world > 1;
+ * the reference's completed_episode_scores, maddpg/agent.py:229-247).  Instead of every env's
+ * return + done flag (9 B per env per step), a rank sends only its completed episodes' returns:
+ *
+ * gw_gather_pack (sender, per step): this step's done envs' ep_return (env order) are appended to
+ * the rank's FIFO fifo[fifo_cap] (ring, state ctl[4] = {head, tail, overflow, 0} int64, zeroed at
+ * start); the send slot (32 + 8 cap bytes) gets the header {count, sent, backlog after, overflow}
+ * (int64) and the FIFO's first sent = min(backlog, cap) entries.  scratch:
+ * gw_gather_pack_scratch(E) int32 words.  Two launches, no host synchronisation.
+ *
+ * gw_gather_unpack (receiver, per window of `steps` gathered slots [steps][world][slot_bytes]):
+ * appends every rank's payload to its mirror FIFO (mirror[world][mirror_cap]), queues the per-step
+ * counts in pend[pend_cap][world], and appends to the score ring scores[capacity] (the last
+ * `capacity` kept; *n_completed = completions ever) every pending step whose entries have all
+ * arrived, in (step, rank, env) order: the reference's order with rank-major contiguous shards.
+ * rstate: int64 [2 world + 4] = {received per rank, emitted per rank, pending head, pending tail,
+ * overflow (sticky: a FIFO, mirror or pending ring ran out), max sender backlog of the window},
+ * zeroed at start.  plan: gw_gather_unpack_plan_cap(steps, world, pend_cap) segments of 40 bytes
+ * + 32 bytes.  Three launches, no host synchronisation. */
+int64_t gw_gather_pack_scratch(int64_t E);
+gw_status gw_gather_pack(const double *ep_return, const uint8_t *done, int64_t E, int64_t cap, double *fifo,
+                         int64_t fifo_cap, int64_t *ctl, int32_t *scratch, uint8_t *slot, void *stream);
+int64_t gw_gather_unpack_plan_cap(int64_t steps, int32_t world, int64_t pend_cap);
+gw_status gw_gather_unpack(const uint8_t *recv, int64_t steps, int32_t world, int64_t slot_bytes, double *mirror,
+                           int64_t mirror_cap, int64_t *rstate, int32_t *pend, int64_t pend_cap, void *plan,
+                           int64_t plan_cap, double *scores, int64_t capacity, int64_t *n_completed, void *stream);
+
 /* Replay-ring sample (agilerl MultiAgentReplayBuffer.sample, uniform; called at
  * maddpg/agent.py:209-211; marlnav/rollout.py ReplayRing.sample) as ONE gather launch.  Ring
  * layout: obs / final_obs [S, K, E, HW] (f32, or bf16 if obs_bf16), probs [S, K, E, 9] f32,

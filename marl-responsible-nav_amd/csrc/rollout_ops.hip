@@ -1,6 +1,7 @@
 // rollout_ops.hip — the batched rollout's per-step bookkeeping in one launch (include/rollout_ops.h).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <string>
 
 #include "rollout_ops.h"
@@ -244,6 +245,198 @@ __global__ void __launch_bounds__(EV_T) eval_accum_kernel(const int32_t *__restr
     }
 }
 
+// ---- the packed per-step return gather (parallel.ReturnGather, world > 1) ----
+// Sender: this step's completed-episode returns (done envs, env order) are appended to a FIFO;
+// the send slot carries a 32-byte header {count, sent, backlog after, overflow} and the FIFO's
+// first `sent` = min(backlog, cap) entries.  Receiver: per source rank, a mirror FIFO of the
+// entries received and a ring of per-step counts; a step is emitted into the score ring, in
+// (step, rank, env) order, once every rank's entries of it have arrived.
+constexpr int PT = 256, PPT = 4, PCH = PT * PPT;  // pack: threads, envs per thread, envs per chunk
+constexpr int HDR = 32;                           // slot header bytes
+
+__device__ __forceinline__ int block_excl_scan(int v, int *red, int &total) {
+    // exclusive prefix of v over the block's threads (in thread order) and the block total
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int incl = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(incl, o);
+        if (lane >= o) incl += t;
+    }
+    __syncthreads();
+    if (lane == 63) red[wave] = incl;
+    __syncthreads();
+    int before = 0;
+    total = 0;
+#pragma unroll
+    for (int w = 0; w < PT / 64; ++w) {
+        const int x = red[w];
+        if (w < wave) before += x;
+        total += x;
+    }
+    return before + incl - v;
+}
+
+__global__ void __launch_bounds__(PT) pack_count(const uint8_t *__restrict__ done, int64_t E,
+                                                 const int64_t *__restrict__ ctl, int32_t *__restrict__ scratch) {
+    __shared__ int red[PT / 64];
+    const int64_t e0 = (int64_t)blockIdx.x * PCH + (int64_t)threadIdx.x * PPT;
+    int c = 0;
+#pragma unroll
+    for (int j = 0; j < PPT; ++j) c += (e0 + j < E && done[e0 + j]) ? 1 : 0;
+    int total = 0;
+    (void)block_excl_scan(c, red, total);
+    int64_t *snap = reinterpret_cast<int64_t *>(scratch);
+    if (threadIdx.x == 0) {
+        scratch[4 + blockIdx.x] = total;
+        if (blockIdx.x == 0) {
+            snap[0] = ctl[0];
+            snap[1] = ctl[1];
+        }
+    }
+}
+
+__global__ void __launch_bounds__(PT) pack_scatter(const double *__restrict__ ret, const uint8_t *__restrict__ done,
+                                                   int64_t E, int nchunks, int64_t cap, double *__restrict__ fifo,
+                                                   int64_t fifo_cap, int64_t *__restrict__ ctl,
+                                                   const int32_t *__restrict__ scratch, uint8_t *__restrict__ slot) {
+    __shared__ int red[PT / 64];
+    const int tid = threadIdx.x, b = blockIdx.x;
+    const int64_t *snap = reinterpret_cast<const int64_t *>(scratch);
+    const int32_t *counts = scratch + 4;
+    const int64_t head = snap[0], tail = snap[1];
+    // this step's total and (chunk blocks) the chunk's prefix over the earlier chunks
+    int pre = 0, all = 0;
+    for (int i = tid; i < nchunks; i += PT) {
+        const int x = counts[i];
+        all += x;
+        if (i < b) pre += x;
+    }
+    int tot_all = 0, tot_pre = 0;
+    (void)block_excl_scan(all, red, tot_all);
+    (void)block_excl_scan(pre, red, tot_pre);
+    const int64_t c = tot_all, backlog0 = tail - head;
+    const int64_t nsend = min(backlog0 + c, cap);
+    double *payload = reinterpret_cast<double *>(slot + HDR);
+    if (b < nchunks) {
+        const int64_t e0 = (int64_t)b * PCH + (int64_t)tid * PPT;
+        uint32_t bits = 0;
+        double v[PPT];
+#pragma unroll
+        for (int j = 0; j < PPT; ++j) {
+            const bool d = e0 + j < E && done[e0 + j];
+            bits |= (d ? 1u : 0u) << j;
+            v[j] = d ? ret[e0 + j] : 0.0;
+        }
+        int total = 0;
+        int pos = tot_pre + block_excl_scan(__popc(bits), red, total);
+#pragma unroll
+        for (int j = 0; j < PPT; ++j) {
+            if (!((bits >> j) & 1u)) continue;
+            const int64_t at = tail + pos;  // FIFO position of this completion
+            fifo[at % fifo_cap] = v[j];
+            const int64_t q = at - head;
+            if (q < nsend) payload[q] = v[j];
+            ++pos;
+        }
+    } else {  // the old backlog's entries that go out this step
+        const int64_t nold = min(backlog0, nsend);
+        for (int64_t i = (int64_t)(b - nchunks) * PT + tid; i < nold; i += (int64_t)(gridDim.x - nchunks) * PT)
+            payload[i] = fifo[(head + i) % fifo_cap];
+    }
+    if (b == 0 && tid == 0) {
+        const int64_t backlog1 = backlog0 + c - nsend;
+        const int64_t ovf = (ctl[2] != 0 || backlog0 + c > fifo_cap) ? 1 : 0;
+        int64_t *hdr = reinterpret_cast<int64_t *>(slot);
+        hdr[0] = c;
+        hdr[1] = nsend;
+        hdr[2] = backlog1;
+        hdr[3] = ovf;
+        ctl[0] = head + nsend;
+        ctl[1] = tail + c;
+        ctl[2] = ovf;
+    }
+}
+
+// receiver plan: one thread walks the window's headers (steps x world) and the pending steps;
+// segments: {kind (0 payload -> mirror, 1 mirror -> scores), rank, src, len, dst}
+struct Seg {
+    int64_t kind, rank, src, len, dst;
+};
+
+__global__ void unpack_plan(const uint8_t *__restrict__ recv, int64_t steps, int world, int64_t slot_bytes,
+                            int64_t *__restrict__ rst, int32_t *__restrict__ pend, int64_t pend_cap,
+                            Seg *__restrict__ plan, int64_t plan_cap, int64_t *__restrict__ n_completed,
+                            int64_t *__restrict__ plan_meta) {
+    if (threadIdx.x != 0) return;
+    int64_t *recv_tot = rst, *emitted = rst + world, *ph = rst + 2 * world, *pt = ph + 1, *ovf = pt + 1,
+            *maxb = ovf + 1;
+    int64_t na = 0, nb = 0, mb = 0, bad = *ovf;
+    for (int64_t s = 0; s < steps; ++s) {
+        if (*pt - *ph >= pend_cap) bad = 1;
+        for (int r = 0; r < world; ++r) {
+            const int64_t *hdr = reinterpret_cast<const int64_t *>(recv + (s * world + r) * slot_bytes);
+            const int64_t c = hdr[0], n = hdr[1];
+            mb = max(mb, hdr[2]);
+            bad |= hdr[3];
+            if (n > 0 && na < plan_cap) {
+                plan[na] = Seg{0, r, (s * world + r) * slot_bytes + HDR, n, recv_tot[r]};
+                ++na;
+            }
+            recv_tot[r] += n;
+            pend[(*pt % pend_cap) * world + r] = (int32_t)c;
+        }
+        *pt += 1;
+    }
+    // emit every pending step whose entries have all arrived, in order
+    const int64_t base = *n_completed;
+    int64_t off = 0;
+    while (*ph < *pt) {
+        const int32_t *cs = pend + (*ph % pend_cap) * world;
+        bool ready = true;
+        for (int r = 0; r < world; ++r) ready = ready && emitted[r] + cs[r] <= recv_tot[r];
+        if (!ready) break;
+        for (int r = 0; r < world; ++r) {
+            if (cs[r] > 0 && na + nb < plan_cap) {
+                plan[na + nb] = Seg{1, r, emitted[r], cs[r], base + off};
+                ++nb;
+            }
+            emitted[r] += cs[r];
+            off += cs[r];
+        }
+        *ph += 1;
+    }
+    if (na + nb >= plan_cap) bad = 1;
+    *n_completed = base + off;
+    *maxb = mb;
+    *ovf = bad;
+    plan_meta[0] = na;
+    plan_meta[1] = nb;
+    plan_meta[2] = base + off;  // the new total: entries before total - capacity are not kept
+}
+
+// grid (G, CPB): block (g, j) copies elements j, j + CPB * T, ... of segments g, g + G, ... of `kind`
+constexpr int CPB = 8;
+
+__global__ void __launch_bounds__(PT) unpack_copy(const uint8_t *__restrict__ recv, double *__restrict__ mirror,
+                                                  int64_t mirror_cap, const Seg *__restrict__ plan,
+                                                  const int64_t *__restrict__ plan_meta, int kind,
+                                                  double *__restrict__ scores, int64_t capacity) {
+    const int64_t na = plan_meta[0], nb = plan_meta[1], total = plan_meta[2];
+    const int64_t nseg = kind == 0 ? na : nb, first = kind == 0 ? 0 : na;
+    for (int64_t g = blockIdx.x; g < nseg; g += gridDim.x) {
+        const Seg sg = plan[first + g];
+        double *mr = mirror + sg.rank * mirror_cap;
+        for (int64_t i = (int64_t)blockIdx.y * PT + threadIdx.x; i < sg.len; i += (int64_t)CPB * PT) {
+            if (kind == 0) {
+                mr[(sg.dst + i) % mirror_cap] = reinterpret_cast<const double *>(recv + sg.src)[i];
+            } else {
+                const int64_t d = sg.dst + i;
+                if (d >= total - capacity) scores[d % capacity] = mr[(sg.src + i) % mirror_cap];
+            }
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -289,6 +482,62 @@ gw_status gw_return_compact(const uint8_t *recv, int64_t steps, int32_t world, i
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         gw_set_last_error((std::string("gw_return_compact: ") + hipGetErrorString(e)).c_str());
+        return GW_ERR_HIP;
+    }
+    return GW_OK;
+}
+
+int64_t gw_gather_pack_scratch(int64_t E) { return 4 + (E + PCH - 1) / PCH; }
+
+gw_status gw_gather_pack(const double *ep_return, const uint8_t *done, int64_t E, int64_t cap, double *fifo,
+                         int64_t fifo_cap, int64_t *ctl, int32_t *scratch, uint8_t *slot, void *stream) {
+    if (!ep_return || !done || E < 1 || cap < 1 || !fifo || fifo_cap < cap || !ctl || !scratch || !slot) {
+        gw_set_last_error("gw_gather_pack: bad argument");
+        return GW_ERR_ARG;
+    }
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int64_t nchunks = (E + PCH - 1) / PCH;
+    const int64_t ncopy = std::min<int64_t>((cap + PT * 4 - 1) / (PT * 4), 64);
+    hipLaunchKernelGGL(pack_count, dim3((unsigned)nchunks), dim3(PT), 0, s, done, E, ctl, scratch);
+    hipLaunchKernelGGL(pack_scatter, dim3((unsigned)(nchunks + ncopy)), dim3(PT), 0, s, ep_return, done, E,
+                       (int)nchunks, cap, fifo, fifo_cap, ctl, scratch, slot);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        gw_set_last_error((std::string("gw_gather_pack: ") + hipGetErrorString(e)).c_str());
+        return GW_ERR_HIP;
+    }
+    return GW_OK;
+}
+
+int64_t gw_gather_unpack_plan_cap(int64_t steps, int32_t world, int64_t pend_cap) {
+    return (steps + pend_cap) * (int64_t)world + 1;
+}
+
+gw_status gw_gather_unpack(const uint8_t *recv, int64_t steps, int32_t world, int64_t slot_bytes, double *mirror,
+                           int64_t mirror_cap, int64_t *rstate, int32_t *pend, int64_t pend_cap, void *plan,
+                           int64_t plan_cap, double *scores, int64_t capacity, int64_t *n_completed, void *stream) {
+    if (steps < 0 || world < 1 || slot_bytes < HDR + 8 || slot_bytes % 8 || !mirror || mirror_cap < 1 || !rstate ||
+        !pend || pend_cap < 1 || !plan || plan_cap < 2 || !scores || capacity < 1 || !n_completed ||
+        (steps > 0 && !recv)) {
+        gw_set_last_error("gw_gather_unpack: bad argument");
+        return GW_ERR_ARG;
+    }
+    if (steps == 0) return GW_OK;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    // plan: [plan_cap] segments, then 4 int64 of metadata
+    Seg *segs = static_cast<Seg *>(plan);
+    int64_t *meta = reinterpret_cast<int64_t *>(segs + plan_cap);
+    hipLaunchKernelGGL(unpack_plan, dim3(1), dim3(64), 0, s, recv, steps, (int)world, slot_bytes, rstate, pend,
+                       pend_cap, segs, plan_cap, n_completed, meta);
+    const unsigned na = (unsigned)std::min<int64_t>(std::min<int64_t>(steps * world, plan_cap), 512);
+    const unsigned nb = (unsigned)std::min<int64_t>(std::min<int64_t>(pend_cap * world, plan_cap), 512);
+    hipLaunchKernelGGL(unpack_copy, dim3(na, CPB), dim3(PT), 0, s, recv, mirror, mirror_cap, segs, meta, 0, scores,
+                       capacity);
+    hipLaunchKernelGGL(unpack_copy, dim3(nb, CPB), dim3(PT), 0, s, recv, mirror, mirror_cap, segs, meta, 1, scores,
+                       capacity);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        gw_set_last_error((std::string("gw_gather_unpack: ") + hipGetErrorString(e)).c_str());
         return GW_ERR_HIP;
     }
     return GW_OK;

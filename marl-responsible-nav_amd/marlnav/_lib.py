@@ -175,7 +175,8 @@ EXPORTS = ["gw_create", "gw_reset", "gw_step", "gw_state_view", "gw_copy_state",
            "gw_eval_accum", "gw_profile_spans", "gw_patch_actor_workspace_floats", "gw_patch_actor_prepare",
            "gw_patch_actor_act", "gw_patch_cnn_workspace_floats", "gw_patch_cnn_prepare", "gw_patch_cnn_act",
            "gw_maddpg_workspace_floats", "gw_maddpg_critic_grads", "gw_maddpg_actor_grads",
-           "gw_pipeline_state_bytes", "gw_pipeline_save", "gw_pipeline_load"]
+           "gw_pipeline_state_bytes", "gw_pipeline_save", "gw_pipeline_load",
+           "gw_gather_pack_scratch", "gw_gather_pack", "gw_gather_unpack_plan_cap", "gw_gather_unpack"]
 
 
 class GwObsSource(C.Structure):
@@ -238,6 +239,15 @@ def _declare(L):
     L.gw_profile_spans.restype = C.c_int
     L.gw_obs_patch.argtypes = [p, C.c_int32, p, p, p]
     L.gw_obs_patch.restype = C.c_int
+    L.gw_gather_pack_scratch.argtypes = [C.c_int64]
+    L.gw_gather_pack_scratch.restype = C.c_int64
+    L.gw_gather_pack.argtypes = [p, p, C.c_int64, C.c_int64, p, C.c_int64, p, p, p, p]
+    L.gw_gather_pack.restype = C.c_int
+    L.gw_gather_unpack_plan_cap.argtypes = [C.c_int64, C.c_int32, C.c_int64]
+    L.gw_gather_unpack_plan_cap.restype = C.c_int64
+    L.gw_gather_unpack.argtypes = [p, C.c_int64, C.c_int32, C.c_int64, p, C.c_int64, p, p, C.c_int64, p,
+                                   C.c_int64, p, C.c_int64, p, p]
+    L.gw_gather_unpack.restype = C.c_int
     L.gw_pipeline_state_bytes.argtypes = []
     L.gw_pipeline_state_bytes.restype = C.c_int64
     L.gw_pipeline_save.argtypes = [p, p]

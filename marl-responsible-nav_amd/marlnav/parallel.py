@@ -126,27 +126,34 @@ class StatsReducer:
 
 
 class ReturnGather:
-    """Per-step all-gather of every env's completed-episode return.
+    """Per-step gather of every rank's completed-episode returns.
 
     The reference appends ``scores[i]`` to ``completed_episode_scores`` for every env whose
-    episode ended this step (maddpg/agent.py:229-247).  Here each rank's step writes its
-    ``[E_local]`` f64 ``ep_return`` and u8 ``done`` straight into one packed send buffer
-    (zero-copy through ``VecGridEnv.step(into=...)``; shards shorter than the longest are padded
-    with done = 0), and ONE asynchronous ``all_gather_into_tensor`` (RCCL over xGMI on the GPU)
-    delivers ``[world][E_max]`` returns + dones to every rank: 9 bytes per env per step.
+    episode ended this step (maddpg/agent.py:229-247).  Each rank's step writes its ``[E_local]``
+    f64 ``ep_return`` and u8 ``done`` (zero-copy through ``VecGridEnv.step(into=...)``).
 
-    Received steps accumulate in a device ring of ``window`` slots; every ``window`` steps (and
-    on ``completed()``) they are compacted on the device, with no host synchronisation, into a
-    ring of the last ``capacity`` completed returns in the reference's order: step by step, and
-    within a step by global env id.  ``completed()`` returns them to the host (it synchronises).
+    One rank: the step writes straight into a receive slot (no copy), and every ``window`` steps
+    (and on ``completed()``) the slots are compacted on the device into a ring of the last
+    ``capacity`` completed returns in the reference's order: step by step, within a step by env id.
 
-    Double-buffered: step t writes send buffer t & 1 while the collective of step t-1 still
-    reads the other one; the stream waits on the collective of step t-2 before its buffer is
-    overwritten (a device-side wait, not a host one).  With one rank the step writes the
-    receive slot directly."""
+    Several ranks (packed): only completed episodes travel.  Per step each rank appends its done
+    envs' returns (env order) to a device FIFO and ONE asynchronous ``all_gather_into_tensor``
+    (RCCL over xGMI) carries a fixed slot per rank: a 32-byte header (this step's count, the
+    entries sent, the backlog left, an overflow flag) and up to ``cap`` returns from the FIFO's
+    head -- 32 + 8 cap bytes instead of 9 bytes per env (cap = E_local / 32 by default: 16 KB at
+    65,536 envs vs 576 KB).  A step with more completions than ``cap`` leaves a backlog that the
+    next steps drain; every rank sees every header, so all ranks double ``cap`` at the same window
+    boundary when the last window had one (a lagged host read of an already finished copy: no
+    stall).  Every ``window`` steps the receiver appends each rank's entries to a mirror FIFO and
+    emits, in (step, rank, env) order, every step whose entries have all arrived -- with
+    rank-major contiguous shards that is the reference's (step, global env id) order, bit for bit
+    the list of the round-3 full gather (tests/test_parallel.py, tests/test_gpu_dist.py).
+
+    The send slots are double-buffered: step t packs into buffer t & 1 while the collective of
+    step t-1 still reads the other one (the stream waits on the collective of step t-2)."""
 
     def __init__(self, global_envs: int, rank: int, world: int, device, group=None, window: int = 64,
-                 capacity: int = 1 << 20):
+                 capacity: int = 1 << 20, cap: int | None = None):
         self.group = group
         self.rank, self.world = int(rank), int(world)
         self.G = int(global_envs)
@@ -157,22 +164,136 @@ class ReturnGather:
                             and dist.get_world_size(group) > 1)
         if self.world > 1 and not self.distributed:
             raise RuntimeError("ReturnGather: world > 1 needs an initialised process group")
-        # packed slot: [E_max] f64 returns, then [E_max] u8 dones, padded to 8 bytes
-        self.slot_bytes = 8 * self.emax + (-(-self.emax // 8)) * 8
-        self._send = [torch.zeros(self.slot_bytes, dtype=torch.uint8, device=self.device) for _ in range(2)]
-        self._work = [None, None]
         self.window = int(window)
-        self._recv = torch.zeros((self.window, self.world, self.slot_bytes), dtype=torch.uint8, device=self.device)
+        self._work = [None, None]
         self._fill = 0           # received steps not yet compacted
         self._flip = 0
         self.capacity = int(capacity)
         self.scores = torch.zeros(self.capacity + 1, dtype=torch.float64, device=self.device)  # + spare slot
         self.n_completed = torch.zeros((), dtype=torch.int64, device=self.device)  # total ever (device)
-        # run the compaction once on an all-zero (no episode done) slot: loads its kernels here,
-        # not inside the first timed window that compacts
-        self._fill = 1
-        self.compact()
+        if self.distributed:
+            self._init_packed(cap)
+        else:
+            # packed slot: [E_max] f64 returns, then [E_max] u8 dones, padded to 8 bytes
+            self.slot_bytes = 8 * self.emax + (-(-self.emax // 8)) * 8
+            self._recv = torch.zeros((self.window, 1, self.slot_bytes), dtype=torch.uint8, device=self.device)
+        # run the compaction once on an all-zero (nothing done) slot: loads its kernels here, not
+        # inside the first timed window that compacts
+        if not self.distributed:
+            self._fill = 1
+            self.compact()
 
+    # ---- several ranks: the packed protocol ------------------------------------------------
+    def _init_packed(self, cap):
+        dev, E = self.device, self.emax
+        self.cap = int(cap) if cap else max(64, -(-E // 32))
+        self.cap = min(self.cap, E)
+        self.fifo_cap = 2 * self.window * E + E       # a backlog the cap adaptation cannot reach
+        self._ret = torch.zeros(E, dtype=torch.float64, device=dev)   # the step writes these (into())
+        self._done = torch.zeros(E, dtype=torch.uint8, device=dev)
+        self._fifo = torch.zeros(self.fifo_cap, dtype=torch.float64, device=dev)
+        self._ctl = torch.zeros(4, dtype=torch.int64, device=dev)
+        self.pend_cap = 8 * self.window
+        self._mirror = torch.zeros((self.world, self.fifo_cap), dtype=torch.float64, device=dev)
+        self._rst = torch.zeros(2 * self.world + 4, dtype=torch.int64, device=dev)
+        self._pend = torch.zeros((self.pend_cap, self.world), dtype=torch.int32, device=dev)
+        self._hip = dev.type == "cuda"
+        if self._hip:
+            from . import _lib
+            lib = _lib.load()
+            self._pack_scratch = torch.zeros(int(lib.gw_gather_pack_scratch(self.count)), dtype=torch.int32,
+                                             device=dev)
+            self.plan_cap = int(lib.gw_gather_unpack_plan_cap(self.window, self.world, self.pend_cap))
+            self._plan = torch.zeros(self.plan_cap * 40 + 32, dtype=torch.uint8, device=dev)
+            self._maxb_host = torch.zeros(2, dtype=torch.int64).pin_memory()
+        else:
+            self._maxb_host = torch.zeros(2, dtype=torch.int64)
+        self._maxb_ev = None
+        self._nwin = 0
+        self._alloc_slots()
+
+    def _alloc_slots(self):
+        self.slot_bytes = 32 + 8 * self.cap
+        self._send = [torch.zeros(self.slot_bytes, dtype=torch.uint8, device=self.device) for _ in range(2)]
+        self._recv = torch.zeros((self.window, self.world, self.slot_bytes), dtype=torch.uint8, device=self.device)
+
+    def _pack(self, buf: torch.Tensor):
+        if self._hip:
+            import ctypes as C
+            from . import _lib
+            _lib.check(_lib.load().gw_gather_pack(
+                self._ret.data_ptr(), self._done.data_ptr(), self.count, self.cap, self._fifo.data_ptr(),
+                self.fifo_cap, self._ctl.data_ptr(), self._pack_scratch.data_ptr(), buf.data_ptr(),
+                C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)), "gw_gather_pack")
+            return
+        # the same protocol as torch ops (CPU tensors: the gloo tests)
+        new = self._ret[: self.count][self._done[: self.count] != 0]
+        head, tail, ovf = (int(x) for x in self._ctl[:3])
+        c = new.numel()
+        if c:
+            self._fifo[(tail + torch.arange(c)) % self.fifo_cap] = new
+        n = min(tail - head + c, self.cap)
+        payload = buf[32:].view(torch.float64)
+        if n:
+            payload[:n] = self._fifo[(head + torch.arange(n)) % self.fifo_cap]
+        ovf = 1 if (ovf or tail - head + c > self.fifo_cap) else 0
+        buf[:32].view(torch.int64).copy_(torch.tensor([c, n, tail - head + c - n, ovf]))
+        self._ctl[:3] = torch.tensor([head + n, tail + c, ovf])
+
+    def _unpack(self):
+        steps = self._fill
+        if self._hip:
+            import ctypes as C
+            from . import _lib
+            _lib.check(_lib.load().gw_gather_unpack(
+                self._recv.data_ptr(), steps, self.world, self.slot_bytes, self._mirror.data_ptr(), self.fifo_cap,
+                self._rst.data_ptr(), self._pend.data_ptr(), self.pend_cap, self._plan.data_ptr(), self.plan_cap,
+                self.scores.data_ptr(), self.capacity, self.n_completed.data_ptr(),
+                C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)), "gw_gather_unpack")
+            return
+        W = self.world
+        rst = self._rst
+        recv_tot, emitted = rst[:W], rst[W:2 * W]
+        maxb, bad = 0, int(rst[2 * W + 2])
+        for t in range(steps):
+            if int(rst[2 * W + 1] - rst[2 * W]) >= self.pend_cap:
+                bad = 1
+            for r in range(W):
+                slot = self._recv[t, r]
+                c, n, backlog, ovf = (int(x) for x in slot[:32].view(torch.int64))
+                maxb, bad = max(maxb, backlog), bad | ovf
+                if n:
+                    idx = (int(recv_tot[r]) + torch.arange(n)) % self.fifo_cap
+                    self._mirror[r, idx] = slot[32:].view(torch.float64)[:n]
+                recv_tot[r] += n
+                self._pend[int(rst[2 * W + 1]) % self.pend_cap, r] = c
+            rst[2 * W + 1] += 1
+        out = []
+        while int(rst[2 * W]) < int(rst[2 * W + 1]):
+            cs = self._pend[int(rst[2 * W]) % self.pend_cap]
+            if not all(int(emitted[r]) + int(cs[r]) <= int(recv_tot[r]) for r in range(W)):
+                break
+            for r in range(W):
+                c = int(cs[r])
+                if c:
+                    out.append(self._mirror[r, (int(emitted[r]) + torch.arange(c)) % self.fifo_cap])
+                emitted[r] += c
+            rst[2 * W] += 1
+        rst[2 * W + 2], rst[2 * W + 3] = bad, maxb
+        if out:
+            vals = torch.cat(out)
+            n_old = int(self.n_completed)
+            keep = vals[-self.capacity:]
+            dst = (n_old + len(vals) - len(keep) + torch.arange(len(keep))) % self.capacity
+            self.scores[dst] = keep
+            self.n_completed += len(vals)
+
+    def overflowed(self) -> bool:
+        """Whether a FIFO, mirror or pending ring ran out (the gathered list is then incomplete).
+        Synchronises."""
+        return self.distributed and int(self._rst[2 * self.world + 2]) != 0
+
+    # ---- the per-step interface ------------------------------------------------------------
     def _views(self, buf: torch.Tensor):
         rets = buf[: 8 * self.emax].view(torch.float64)
         done = buf[8 * self.emax: 9 * self.emax]
@@ -190,19 +311,22 @@ class ReturnGather:
 
     def into(self) -> dict:
         """Output buffers for this rank's next ``VecGridEnv.step(into=...)``: ``ep_return`` and
-        ``done`` views of the current send buffer (its first E_local entries)."""
+        ``done`` [E_local] (one rank: views of the receive slot; several: the packer's inputs)."""
+        if self.distributed:
+            return {"ep_return": self._ret[: self.count], "done": self._done[: self.count]}
         rets, done = self._views(self._buf())
         return {"ep_return": rets[: self.count], "done": done[: self.count]}
 
     def push(self, ep_return: torch.Tensor | None = None, done: torch.Tensor | None = None):
         """Gather this step's returns.  Without arguments the step wrote them through
         ``into()``; otherwise ``ep_return`` [E_local] f64 and ``done`` [E_local] u8 are copied."""
-        buf = self._buf()
         if ep_return is not None:
-            rets, dn = self._views(buf)
-            rets[: self.count].copy_(ep_return)
-            dn[: self.count].copy_(done.to(torch.uint8))
+            into = self.into()
+            into["ep_return"].copy_(ep_return)
+            into["done"].copy_(done.to(torch.uint8))
         if self.distributed:
+            buf = self._buf()
+            self._pack(buf)
             slot = self._recv[self._fill]
             self._work[self._flip] = dist.all_gather_into_tensor(slot.view(-1), buf, group=self.group,
                                                                  async_op=True)
@@ -219,21 +343,47 @@ class ReturnGather:
             if w is not None:
                 w.wait()
         self._work = [None, None]
+        if self.distributed:
+            self._unpack()
+            self._fill = 0
+            # the window's max sender backlog, read by the host one window later (_adapt_from)
+            slot = self._nwin % 2
+            self._maxb_host[slot:slot + 1].copy_(self._rst[2 * self.world + 3:2 * self.world + 4],
+                                                 non_blocking=self._hip)
+            if self._hip:
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(self.device))
+                prev_ev, self._maxb_ev = self._maxb_ev, ev
+            self._nwin += 1
+            if self._nwin >= 2:
+                self._adapt_from(prev_ev if self._hip else None)
+            return
         if self._recv.is_cuda:
             self._compact_hip()
             return
         self._compact_torch()
+
+    def _adapt_from(self, ev):
+        """Grow ``cap`` (x2, up to the shard) when the window before this one left a backlog on any
+        rank.  Every rank reads the same gathered headers, so all ranks decide alike; the value was
+        copied a whole window ago, so the wait is normally on a long finished event."""
+        if ev is not None:
+            ev.synchronize()
+        prev = int(self._maxb_host[(self._nwin - 2) % 2])
+        if prev > 0 and self.cap < self.emax:
+            self.cap = min(2 * self.cap, self.emax)
+            self._alloc_slots()
 
     def _compact_hip(self):
         """gw_return_compact (include/rollout_ops.h): count + scatter, two launches."""
         import ctypes as C
         from . import _lib
         lib = _lib.load()
-        need = int(lib.gw_return_compact_scratch(self._fill, self.world, self.emax))
+        need = int(lib.gw_return_compact_scratch(self._fill, 1, self.emax))
         if getattr(self, "_scratch", None) is None or self._scratch.numel() < need:
-            self._scratch = torch.zeros(max(need, 2 + (self.window * self.world * self.emax + 4095) // 4096),
+            self._scratch = torch.zeros(max(need, 2 + (self.window * self.emax + 4095) // 4096),
                                         dtype=torch.int32, device=self.device)
-        _lib.check(lib.gw_return_compact(self._recv.data_ptr(), self._fill, self.world, self.emax, self.slot_bytes,
+        _lib.check(lib.gw_return_compact(self._recv.data_ptr(), self._fill, 1, self.emax, self.slot_bytes,
                                          self.scores.data_ptr(), self.capacity, self.n_completed.data_ptr(),
                                          self._scratch.data_ptr(),
                                          C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)),
@@ -241,11 +391,10 @@ class ReturnGather:
         self._fill = 0
 
     def _compact_torch(self):
-        """The same compaction as torch ops (CPU tensors: the gloo tests; the GPU test's reference)."""
-        block = self._recv[: self._fill]                               # [T, world, slot]
-        rets = block.view(torch.float64)[:, :, : self.emax]            # [T, world, E_max] (slot_bytes % 8 == 0)
+        """The same compaction as torch ops (CPU tensors: single-process tests)."""
+        block = self._recv[: self._fill]                               # [T, 1, slot]
+        rets = block.view(torch.float64)[:, :, : self.emax]            # [T, 1, E_max] (slot_bytes % 8 == 0)
         done = block[:, :, 8 * self.emax: 9 * self.emax] != 0
-        # order: step, then global env id (rank-major contiguous shards)
         rets, done = rets.reshape(-1), done.reshape(-1)
         pos = torch.cumsum(done, 0, dtype=torch.int64)
         # only the last `capacity` completions can survive; every other element (not done, or
@@ -262,6 +411,9 @@ class ReturnGather:
         first, on the host; ``last`` keeps only the most recent ones (the reference averages
         ``[-100:]`` style windows).  Synchronises."""
         self.compact()
+        if self.overflowed():
+            raise RuntimeError("ReturnGather: a FIFO / mirror / pending ring overflowed (completions per step far "
+                               "above cap for two windows); raise cap")
         n = int(self.n_completed.item())
         m = min(n, self.capacity) if last is None else min(n, self.capacity, int(last))
         if m == 0:

@@ -60,6 +60,9 @@ def _worker(rank, world, port, G, steps, outdir):
     red = StatsReducer(STATS, "cpu")
     gat = ReturnGather(G, rank, world, "cpu", window=4)          # wraps the receive ring 3x
     gat_small = ReturnGather(G, rank, world, "cpu", window=5, capacity=37)  # keeps the last 37
+    # a cap far below the completions per step: backlogs, late steps, the cap doubling per window
+    gat_tiny = ReturnGather(G, rank, world, "cpu", window=3, cap=2)
+    caps = []
     for _ in range(steps):
         orc.vec_step(None, outs=outs, nthreads=1)
         partial = torch.tensor(_per_env_stats(outs, cnt))
@@ -71,9 +74,15 @@ def _worker(rank, world, port, G, steps, outdir):
         into["ep_return"].copy_(ret)
         into["done"].copy_(done)
         gat_small.push()
+        gat_tiny.push(ret, done)
+        caps.append(gat_tiny.cap)
     totals = red.result().numpy()
     np.save(os.path.join(outdir, f"completed{rank}.npy"), gat.completed())
     np.save(os.path.join(outdir, f"completed_small{rank}.npy"), gat_small.completed())
+    np.save(os.path.join(outdir, f"completed_tiny{rank}.npy"), gat_tiny.completed())
+    np.save(os.path.join(outdir, f"caps{rank}.npy"), np.array(caps))
+    # the per-step message: a header and cap returns, not 9 bytes per env
+    assert gat.slot_bytes == 32 + 8 * gat.cap < 9 * gat.emax
     emax = -(-G // world)
     pos = torch.zeros((emax, sc.N), dtype=torch.int32)
     pos[:cnt] = torch.tensor(orc.positions(), dtype=torch.int32)
@@ -99,6 +108,8 @@ def test_gloo_world2_matches_single_process(G):
         pos = np.load(os.path.join(d, "pos.npy"))
         completed = [np.load(os.path.join(d, f"completed{r}.npy")) for r in range(world)]
         completed_small = [np.load(os.path.join(d, f"completed_small{r}.npy")) for r in range(world)]
+        completed_tiny = [np.load(os.path.join(d, f"completed_tiny{r}.npy")) for r in range(world)]
+        caps = [np.load(os.path.join(d, f"caps{r}.npy")) for r in range(world)]
     from marlnav import scenario as S
     from oracle import oracle as O
     sc = S.builtin("grid32")
@@ -114,6 +125,9 @@ def test_gloo_world2_matches_single_process(G):
     for r in range(world):
         np.testing.assert_array_equal(completed[r], scores)
         np.testing.assert_array_equal(completed_small[r], scores[-37:])
+        np.testing.assert_array_equal(completed_tiny[r], scores)
+    np.testing.assert_array_equal(caps[0], caps[1])             # every rank adapts alike
+    assert caps[0][0] == 2 and caps[0][-1] > 2                  # ... and the cap grew
     assert len(scores) > 37                                    # the small ring wrapped
     np.testing.assert_array_equal(pos, orc.positions())       # sharded trajectories == single run
     np.testing.assert_allclose(totals, ref, rtol=1e-12)        # reduced statistics == single run
