@@ -32,6 +32,7 @@
 namespace {
 
 constexpr int HID = 128, NA = 9, RB = 16, TILE_R = 128, DC = 64, MAXK = GW_MAX_AGENTS, MAXJOB = 4;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr float LN_EPS = 1e-5f, G_EPS = 1e-20f;
 
 gw_status fail(gw_status s, const std::string &msg) {
@@ -81,32 +82,39 @@ __global__ void __launch_bounds__(256) l1_kernel(L1Params p) {
         *reinterpret_cast<float4 *>(&s_w[d][4 * c]) = v;
     }
     __syncthreads();
-    const int rg = tid >> 4, jg = tid & 15;  // rows 8 rg .. + 8, features 8 jg .. + 8
-    float acc[8][8];
+    // v_mfma_f32_16x16x4_f32: wave w computes rows 32 w .. 32 w + 31 (two 16-row tiles) x all 128
+    // features (eight 16-column tiles) over the chunk's inputs in order, four per instruction: a
+    // k-ordered f32 fma chain from 0, bit for bit the VALU loop it replaced (inputs past the
+    // chunk's end are staged as zeros: fma(0, 0, acc) = acc)
+    const int lane = tid & 63, wave = tid >> 6, lr = lane & 15, lq = lane >> 4;
+    f32x4 acc[2][8];
 #pragma unroll
-    for (int a = 0; a < 8; ++a)
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int c = 0; c < 8; ++c) acc[a][c] = 0.0f;
-    for (int d = 0; d < nd; ++d) {
-        const float4 xa = *reinterpret_cast<const float4 *>(&s_x[d][8 * rg]);
-        const float4 xb4 = *reinterpret_cast<const float4 *>(&s_x[d][8 * rg + 4]);
-        const float4 wa = *reinterpret_cast<const float4 *>(&s_w[d][8 * jg]);
-        const float4 wb4 = *reinterpret_cast<const float4 *>(&s_w[d][8 * jg + 4]);
-        const float xv[8] = {xa.x, xa.y, xa.z, xa.w, xb4.x, xb4.y, xb4.z, xb4.w};
-        const float wv[8] = {wa.x, wa.y, wa.z, wa.w, wb4.x, wb4.y, wb4.z, wb4.w};
+        for (int c = 0; c < 8; ++c) acc[a][c] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    const int nk = (nd + 3) / 4;
+    for (int kk = 0; kk < nk; ++kk) {
+        const int d = 4 * kk + lq;
+        const float a0 = s_x[d][32 * wave + lr], a1 = s_x[d][32 * wave + 16 + lr];
 #pragma unroll
-        for (int a = 0; a < 8; ++a)
-#pragma unroll
-            for (int c = 0; c < 8; ++c) acc[a][c] = fmaf(xv[a], wv[c], acc[a][c]);
+        for (int c = 0; c < 8; ++c) {
+            const float bw = s_w[d][16 * c + lr];
+            acc[0][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bw, acc[0][c], 0, 0, 0);
+            acc[1][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, bw, acc[1][c], 0, 0, 0);
+        }
     }
+    // D: row 4 lq + i of the tile, column lr
+    float *ob = jb.part + ((int64_t)chunk * p.K + k) * p.B * HID;
 #pragma unroll
-    for (int a = 0; a < 8; ++a) {
-        const int r = r0 + 8 * rg + a;
-        if (r >= p.B) break;
-        float *o = jb.part + (((int64_t)chunk * p.K + k) * p.B + r) * HID + 8 * jg;
-        *reinterpret_cast<float4 *>(o) = make_float4(acc[a][0], acc[a][1], acc[a][2], acc[a][3]);
-        *reinterpret_cast<float4 *>(o + 4) = make_float4(acc[a][4], acc[a][5], acc[a][6], acc[a][7]);
-    }
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = r0 + 32 * wave + 16 * a + 4 * lq + i;
+            if (r < p.B) {
+#pragma unroll
+                for (int c = 0; c < 8; ++c) ob[(int64_t)r * HID + 16 * c + lr] = acc[a][c][i];
+            }
+        }
 }
 
 // ---- per-row helpers (a row = 16 lanes, lane g holds features 8 g .. 8 g + 7) ---------------------
@@ -173,43 +181,44 @@ __device__ __forceinline__ void ln_relu_bwd(const float gy[8], const float y[8],
     for (int i = 0; i < 8; ++i) dz[i] = rstd * (dx[i] - m1 - xh[i] * m2);
 }
 
-// out[8] = sum_c h[c] W[c][8 g + i]  (W [128][128] in LDS, h the row's 128 values in LDS)
-__device__ __forceinline__ void row_gemv(const float *h, const float (*w)[HID + 4], int g, float out[8]) {
+// The block's 16 rows through a 128 x 128 layer: z[r][n] = sum_c h[r][c] W[c][n] (transpose:
+// W[n][c]) on v_mfma_f32_16x16x4_f32, W read straight from global memory (L2-resident: every
+// block of the agent reads the same 64 KB), h from LDS.  Wave w computes columns 32 w .. 32 w +
+// 31; each output is the k-ordered f32 fma chain over c = 0 .. 127 from 0 (the per-row VALU
+// GEMV it replaced, bit for bit).  All threads call it; s_z [16][HP] receives z (the caller syncs
+// before reading it).
+constexpr int HP = HID + 4;  // padded LDS row
+__device__ __forceinline__ void gemv16(const float *s_h, const float *__restrict__ w, bool transpose, float *s_z) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, lr = lane & 15, lq = lane >> 4;
+    const int n0 = 32 * wave + lr, n1 = n0 + 16;
+    f32x4 acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll 8
+    for (int kk = 0; kk < HID / 4; ++kk) {
+        const int c = 4 * kk + lq;
+        const float a = s_h[lr * HP + c];
+        const float b0 = transpose ? w[n0 * HID + c] : w[c * HID + n0];
+        const float b1 = transpose ? w[n1 * HID + c] : w[c * HID + n1];
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b0, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b1, acc1, 0, 0, 0);
+    }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) out[i] = 0.0f;
-    for (int c = 0; c < HID; ++c) {
-        const float hv = h[c];
-        const float4 a = *reinterpret_cast<const float4 *>(&w[c][8 * g]);
-        const float4 b = *reinterpret_cast<const float4 *>(&w[c][8 * g + 4]);
-        out[0] = fmaf(hv, a.x, out[0]);
-        out[1] = fmaf(hv, a.y, out[1]);
-        out[2] = fmaf(hv, a.z, out[2]);
-        out[3] = fmaf(hv, a.w, out[3]);
-        out[4] = fmaf(hv, b.x, out[4]);
-        out[5] = fmaf(hv, b.y, out[5]);
-        out[6] = fmaf(hv, b.z, out[6]);
-        out[7] = fmaf(hv, b.w, out[7]);
+    for (int i = 0; i < 4; ++i) {
+        s_z[(4 * lq + i) * HP + n0] = acc0[i];
+        s_z[(4 * lq + i) * HP + n1] = acc1[i];
     }
 }
 
-// dst = W [128][128] (or its transpose) from global, in 4 x 4 register blocks: 16-byte global
-// loads and 16-byte LDS stores either way (block-wide; the caller syncs)
-__device__ __forceinline__ void stage_mat(const float *w, float (*dst)[HID + 4], bool transpose) {
-    for (int b = threadIdx.x; b < (HID / 4) * (HID / 4); b += 256) {
-        const int br = b / (HID / 4), bc = b % (HID / 4);
-        float4 v[4];
+// the block's rows through a 128 x 128 layer in the per-row layout (thread (rl, g) holds row rl's
+// features 8 g .. 8 g + 7): v -> LDS, gemv16, back to registers (two block barriers)
+__device__ __forceinline__ void rows_gemv(const float v[8], int rl, int g, const float *w, bool transpose, float *s_in,
+                                          float *s_out, float out[8]) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = *reinterpret_cast<const float4 *>(w + (4 * br + q) * HID + 4 * bc);
-        if (!transpose) {
+    for (int i = 0; i < 8; ++i) s_in[rl * HP + 8 * g + i] = v[i];
+    __syncthreads();
+    gemv16(s_in, w, transpose, s_out);
+    __syncthreads();
 #pragma unroll
-            for (int q = 0; q < 4; ++q) *reinterpret_cast<float4 *>(&dst[4 * br + q][4 * bc]) = v[q];
-        } else {
-            *reinterpret_cast<float4 *>(&dst[4 * bc + 0][4 * br]) = make_float4(v[0].x, v[1].x, v[2].x, v[3].x);
-            *reinterpret_cast<float4 *>(&dst[4 * bc + 1][4 * br]) = make_float4(v[0].y, v[1].y, v[2].y, v[3].y);
-            *reinterpret_cast<float4 *>(&dst[4 * bc + 2][4 * br]) = make_float4(v[0].z, v[1].z, v[2].z, v[3].z);
-            *reinterpret_cast<float4 *>(&dst[4 * bc + 3][4 * br]) = make_float4(v[0].w, v[1].w, v[2].w, v[3].w);
-        }
-    }
+    for (int i = 0; i < 8; ++i) out[i] = s_out[rl * HP + 8 * g + i];
 }
 
 // the layer-1 pre-activation of (k, row): the chunk partials in order + bias (+ extra: the
@@ -262,19 +271,15 @@ struct TailParams {
 
 // ---- phase 1a: target actions a'_k = GumbelSoftmax(actor_target_k(s'_k)) into x_next's slots ----
 __global__ void __launch_bounds__(256) target_actor_tail(TailParams p) {
-    __shared__ __attribute__((aligned(16))) float s_w[HID][HID + 4];
-    __shared__ float s_h[RB][HID];
+    __shared__ __attribute__((aligned(16))) float s_in[RB * HP];
+    __shared__ __attribute__((aligned(16))) float s_out[RB * HP];
     const int k = blockIdx.y, tid = threadIdx.x, rl = tid >> 4, g = tid & 15;
     const int r = blockIdx.x * RB + rl;
     const Mlp m = mlp_k(p.actor_t, k, p.D, NA);
-    stage_mat(m.w2, s_w, false);
     float z[8], xh[8], y[8], rs;
     l1_sum(p.part_a, p.nch_a, p.K, p.B, k, r, g, m.b1, z);
     ln_relu(z, m.lw1, m.lb1, g, xh, y, rs);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) s_h[rl][8 * g + i] = y[i];
-    __syncthreads();
-    row_gemv(s_h[rl], s_w, g, z);
+    rows_gemv(y, rl, g, m.w2, false, s_in, s_out, z);
 #pragma unroll
     for (int i = 0; i < 8; ++i) z[i] += m.b2[8 * g + i];
     ln_relu(z, m.lw2, m.lb2, g, xh, y, rs);
@@ -313,7 +318,7 @@ struct RowFwd {
     float xh1[8], y1[8], rs1, xh2[8], y2[8], rs2;
 };
 __device__ __forceinline__ float critic_fwd(const Mlp &m, const float *part, int nch, const TailParams &p, int k,
-                                            int r, int g, const float *act, float (*s_w)[HID + 4], float *s_hrow,
+                                            int r, int rl, int g, const float *act, float *s_in, float *s_out,
                                             RowFwd &f) {
     float z[8];
     l1_sum(part, nch, p.K, p.B, k, r, g, m.b1, z);
@@ -325,10 +330,7 @@ __device__ __forceinline__ float critic_fwd(const Mlp &m, const float *part, int
         for (int i = 0; i < 8; ++i) z[i] = fmaf(av, wr[i], z[i]);
     }
     ln_relu(z, m.lw1, m.lb1, g, f.xh1, f.y1, f.rs1);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) s_hrow[8 * g + i] = f.y1[i];
-    __syncthreads();
-    row_gemv(s_hrow, s_w, g, z);
+    rows_gemv(f.y1, rl, g, m.w2, false, s_in, s_out, z);
 #pragma unroll
     for (int i = 0; i < 8; ++i) z[i] += m.b2[8 * g + i];
     ln_relu(z, m.lw2, m.lb2, g, f.xh2, f.y2, f.rs2);
@@ -338,25 +340,21 @@ __device__ __forceinline__ float critic_fwd(const Mlp &m, const float *part, int
     return row_sum(s) + m.b3[0];
 }
 
-// backward through the critic from dq to dz1 (and the per-row saves when sv != null)
-__device__ __forceinline__ void critic_bwd(const Mlp &m, float dq, int g, const RowFwd &f, float (*s_wt)[HID + 4],
-                                           float *s_grow, float gv1[8], float dz1[8], float gv2[8], float dz2[8]) {
+// backward through the critic from dq to dz1 (dh1 = dz2 W2^T on MFMA)
+__device__ __forceinline__ void critic_bwd(const Mlp &m, float dq, int rl, int g, const RowFwd &f, float *s_in,
+                                           float *s_out, float gv1[8], float dz1[8], float gv2[8], float dz2[8]) {
     float gy[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) gy[i] = dq * m.w3[8 * g + i];
     ln_relu_bwd(gy, f.y2, f.xh2, f.rs2, m.lw2, g, gv2, dz2);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) s_grow[8 * g + i] = dz2[i];
-    __syncthreads();
-    row_gemv(s_grow, s_wt, g, gy);  // dh1 = dz2 W2^T
+    rows_gemv(dz2, rl, g, m.w2, true, s_in, s_out, gy);
     ln_relu_bwd(gy, f.y1, f.xh1, f.rs1, m.lw1, g, gv1, dz1);
 }
 
 // ---- phase 1b: TD target from the critic target, the critic's forward, MSE gradient, backward ----
 __global__ void __launch_bounds__(256) critic_tail(TailParams p) {
-    __shared__ __attribute__((aligned(16))) float s_a[HID][HID + 4];
-    __shared__ __attribute__((aligned(16))) float s_b[HID][HID + 4];
-    __shared__ float s_h[RB][HID];
+    __shared__ __attribute__((aligned(16))) float s_in[RB * HP];
+    __shared__ __attribute__((aligned(16))) float s_out[RB * HP];
     __shared__ float s_act[RB][NA * MAXK];
     const int k = blockIdx.y, tid = threadIdx.x, rl = tid >> 4, g = tid & 15;
     const int r = blockIdx.x * RB + rl;
@@ -366,25 +364,18 @@ __global__ void __launch_bounds__(256) critic_tail(TailParams p) {
     const Mlp mt = mlp_k(p.critic_t, k, p.K * p.D + na, 1);
     const Mlp m = mlp_k(p.critic, k, p.K * p.D + na, 1);
     for (int i = tid; i < RB * na; i += 256) s_act[i / na][i % na] = p.x_next[(int64_t)(blockIdx.x * RB + i / na) * p.ldx + Ds + i % na];
-    stage_mat(mt.w2, s_a, false);
-    stage_mat(m.w2, s_b, false);
     __syncthreads();
     RowFwd f;
-    const float q_next = critic_fwd(mt, p.part_ct, p.nch_cs, p, k, r, g, s_act[rl], s_a, s_h[rl], f);
+    const float q_next = critic_fwd(mt, p.part_ct, p.nch_cs, p, k, r, rl, g, s_act[rl], s_in, s_out, f);
     // y = f32(r) + ((1 - d) * gamma) * q_next, gw_td_target's op order
     const float t1 = 1.0f - (float)p.done[(int64_t)r * p.K + k];
     const float y = (float)p.reward[(int64_t)r * p.K + k] + (t1 * p.gamma) * q_next;
-    __syncthreads();
-    stage_mat(m.w2, s_a, true);  // W2^T for the backward, while the online forward reads s_b
     // online critic on (s, a): the stored actions are the x rows' action slots (in the partials)
     float z[8];
     l1_sum(p.part_c, p.nch_c, p.K, p.B, k, r, g, m.b1, z);
     RowFwd o;
     ln_relu(z, m.lw1, m.lb1, g, o.xh1, o.y1, o.rs1);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) s_h[rl][8 * g + i] = o.y1[i];
-    __syncthreads();
-    row_gemv(s_h[rl], s_b, g, z);
+    rows_gemv(o.y1, rl, g, m.w2, false, s_in, s_out, z);
 #pragma unroll
     for (int i = 0; i < 8; ++i) z[i] += m.b2[8 * g + i];
     ln_relu(z, m.lw2, m.lb2, g, o.xh2, o.y2, o.rs2);
@@ -395,8 +386,7 @@ __global__ void __launch_bounds__(256) critic_tail(TailParams p) {
     const float diff = q - y;
     const float dq = (1.0f / (float)p.B) * (2.0f * diff);  // MSELoss backward (gw_mean_loss_bwd's order)
     float gv1[8], dz1[8], gv2[8], dz2[8];
-    __syncthreads();
-    critic_bwd(m, dq, g, o, s_a, s_h[rl], gv1, dz1, gv2, dz2);
+    critic_bwd(m, dq, rl, g, o, s_in, s_out, gv1, dz1, gv2, dz2);
     const Saved &sv = p.sv;
     put8(sv.h1, p.K, p.B, k, r, g, o.y1);
     put8(sv.h2, p.K, p.B, k, r, g, o.y2);
@@ -415,9 +405,8 @@ __global__ void __launch_bounds__(256) critic_tail(TailParams p) {
 // ---- phase 2: the actor's forward, GumbelSoftmax, the (updated) critic on the mixed actions,
 //      -mean Q gradient, backward through the critic (no parameter gradients) and the actor ----
 __global__ void __launch_bounds__(256) actor_tail(TailParams p) {
-    __shared__ __attribute__((aligned(16))) float s_w[HID][HID + 4];   // actor W2, then critic W2^T
-    __shared__ __attribute__((aligned(16))) float s_wt[HID][HID + 4];  // critic W2, then actor W2^T
-    __shared__ float s_h[RB][HID];
+    __shared__ __attribute__((aligned(16))) float s_in[RB * HP];
+    __shared__ __attribute__((aligned(16))) float s_out[RB * HP];
     __shared__ float s_act[RB][NA * MAXK];
     const int k = blockIdx.y, tid = threadIdx.x, rl = tid >> 4, g = tid & 15;
     const int r = blockIdx.x * RB + rl;
@@ -426,18 +415,13 @@ __global__ void __launch_bounds__(256) actor_tail(TailParams p) {
     const Mlp ma = mlp_k(p.actor, k, p.D, NA);
     const Mlp mc = mlp_k(p.critic, k, p.K * p.D + na, 1);
     // actor forward
-    stage_mat(ma.w2, s_w, false);
-    stage_mat(mc.w2, s_wt, false);
     for (int i = tid; i < RB * na; i += 256) s_act[i / na][i % na] = p.x[(int64_t)(blockIdx.x * RB + i / na) * p.ldx + Ds + i % na];
     __syncthreads();
     float z[8];
     RowFwd fa;
     l1_sum(p.part_a, p.nch_a, p.K, p.B, k, r, g, ma.b1, z);
     ln_relu(z, ma.lw1, ma.lb1, g, fa.xh1, fa.y1, fa.rs1);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) s_h[rl][8 * g + i] = fa.y1[i];
-    __syncthreads();
-    row_gemv(s_h[rl], s_w, g, z);
+    rows_gemv(fa.y1, rl, g, ma.w2, false, s_in, s_out, z);
 #pragma unroll
     for (int i = 0; i < 8; ++i) z[i] += ma.b2[8 * g + i];
     ln_relu(z, ma.lw2, ma.lb2, g, fa.xh2, fa.y2, fa.rs2);
@@ -467,17 +451,15 @@ __global__ void __launch_bounds__(256) actor_tail(TailParams p) {
     for (int a = 0; a < NA; ++a) pr[a] = pr[a] / sum;
     if (p.probs_out && g == 0)
         for (int a = 0; a < NA; ++a) p.probs_out[((int64_t)k * p.B + r) * NA + a] = pr[a];
-    __syncthreads();
-    // the critic k on the mixed actions (own slot: the fresh probabilities)
+    // the critic k on the mixed actions (own slot: the fresh probabilities; the row's 16 lanes are
+    // one wave's, whose LDS operations complete in order)
     if (g == 0)
         for (int a = 0; a < NA; ++a) s_act[rl][NA * k + a] = pr[a];
     RowFwd fc;
-    const float q = critic_fwd(mc, p.part_c, p.nch_cs, p, k, r, g, s_act[rl], s_wt, s_h[rl], fc);
+    const float q = critic_fwd(mc, p.part_c, p.nch_cs, p, k, r, rl, g, s_act[rl], s_in, s_out, fc);
     const float dq = -(1.0f / (float)p.B);  // -mean Q backward (gw_mean_loss_bwd mode 1)
     float gv1[8], dz1[8], gv2[8], dz2[8];
-    stage_mat(mc.w2, s_w, true);  // critic W2^T (the actor's W2 is no longer read)
-    __syncthreads();
-    critic_bwd(mc, dq, g, fc, s_w, s_h[rl], gv1, dz1, gv2, dz2);
+    critic_bwd(mc, dq, rl, g, fc, s_in, s_out, gv1, dz1, gv2, dz2);
     // d probs_k = dz1 . W1[the agent's action rows]^T
     float dp[NA];
 #pragma unroll
@@ -496,9 +478,6 @@ __global__ void __launch_bounds__(256) actor_tail(TailParams p) {
 #pragma unroll
     for (int a = 0; a < NA; ++a) dl[a] = pr[a] * (dp[a] - dot);
     // actor backward
-    __syncthreads();
-    stage_mat(ma.w2, s_wt, true);  // actor W2^T
-    __syncthreads();
     float gy[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -508,10 +487,7 @@ __global__ void __launch_bounds__(256) actor_tail(TailParams p) {
         gy[i] = s;
     }
     ln_relu_bwd(gy, fa.y2, fa.xh2, fa.rs2, ma.lw2, g, gv2, dz2);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) s_h[rl][8 * g + i] = dz2[i];
-    __syncthreads();
-    row_gemv(s_h[rl], s_wt, g, gy);
+    rows_gemv(dz2, rl, g, ma.w2, true, s_in, s_out, gy);
     ln_relu_bwd(gy, fa.y1, fa.xh1, fa.rs1, ma.lw1, g, gv1, dz1);
     const Saved &sv = p.sv;
     put8(sv.h1, p.K, p.B, k, r, g, fa.y1);
@@ -556,10 +532,12 @@ __global__ void __launch_bounds__(256) grads_kernel(GradParams p) {
         const int d0 = (w1 ? b : b - p.nw1) * RB;
         const int D = w1 ? p.in_dim : HID;
         const float *dz = w1 ? p.sv.dz1 : p.sv.dz2;
-        const int di = tid >> 4, g = tid & 15;  // input d0 + di, features 8 g .. + 8
-        float acc[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) acc[i] = 0.0f;
+        // v_mfma_f32_16x16x4_f32: the block's 16 inputs x 128 features = X^T dz over the rows in
+        // order (a k-ordered f32 fma chain from 0 across the row tiles); wave w owns features
+        // 32 w .. 32 w + 31
+        const int lane = tid & 63, wave = tid >> 6, lr = lane & 15, lq = lane >> 4;
+        f32x4 acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = {0.0f, 0.0f, 0.0f, 0.0f};
+        const int n0 = 32 * wave + lr, n1 = n0 + 16;
         for (int r0 = 0; r0 < p.B; r0 += TILE_R) {
             const int nr = min(TILE_R, p.B - r0);
             __syncthreads();
@@ -577,27 +555,21 @@ __global__ void __launch_bounds__(256) grads_kernel(GradParams p) {
                     reinterpret_cast<const float4 *>(dz + ((int64_t)k * p.B + r0 + r) * HID)[c];
             }
             __syncthreads();
-            for (int r = 0; r < nr; ++r) {
-                const float xv = s_in[di][r];
-                const float4 a = *reinterpret_cast<const float4 *>(&s_dz[r][8 * g]);
-                const float4 c = *reinterpret_cast<const float4 *>(&s_dz[r][8 * g + 4]);
-                acc[0] = fmaf(xv, a.x, acc[0]);
-                acc[1] = fmaf(xv, a.y, acc[1]);
-                acc[2] = fmaf(xv, a.z, acc[2]);
-                acc[3] = fmaf(xv, a.w, acc[3]);
-                acc[4] = fmaf(xv, c.x, acc[4]);
-                acc[5] = fmaf(xv, c.y, acc[5]);
-                acc[6] = fmaf(xv, c.z, acc[6]);
-                acc[7] = fmaf(xv, c.w, acc[7]);
+            for (int kk = 0; kk < nr / 4; ++kk) {  // nr: a multiple of 16 (B % 16 == 0)
+                const int r = 4 * kk + lq;
+                const float a = s_in[lr][r];
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, s_dz[r][n0], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, s_dz[r][n1], acc1, 0, 0, 0);
             }
         }
-        if (d0 + di < D) {
-            float *o = const_cast<float *>(w1 ? p.grad.w1 + (int64_t)k * p.in_dim * HID
-                                              : p.grad.w2 + (int64_t)k * HID * HID) +
-                       (int64_t)(d0 + di) * HID + 8 * g;
-            // the per-layer gradient views are 4-byte aligned only in general: scalar stores
+        float *ob = const_cast<float *>(w1 ? p.grad.w1 + (int64_t)k * p.in_dim * HID : p.grad.w2 + (int64_t)k * HID * HID);
 #pragma unroll
-            for (int i = 0; i < 8; ++i) o[i] = acc[i];
+        for (int i = 0; i < 4; ++i) {
+            const int d = d0 + 4 * lq + i;
+            if (d < D) {
+                ob[(int64_t)d * HID + n0] = acc0[i];
+                ob[(int64_t)d * HID + n1] = acc1[i];
+            }
         }
         return;
     }
