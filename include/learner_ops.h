@@ -16,6 +16,8 @@ extern "C" {
 /* torch.optim.Adam (no weight decay, no amsgrad; torch/optim/adam.py _single_tensor_adam) on n
  * elements:  m = lerp(m, g, 1 - beta1);  v = beta2 * v + (1 - beta2) * g * g;  s = step[0] + 1
  *   p -= lr / (1 - beta1^s) * (m / (sqrt(v) / sqrt(1 - beta2^s) + eps));   then step[0] = s.
+ * step: int32 [2] device memory, [0] the steps taken, [1] zero (the launch's arrival counter: the
+ * last block to finish advances step[0], so the step is ONE launch).
  * The scalar hyper-parameters are doubles and the bias corrections are formed in double, as
  * torch forms them from Python floats, then rounded to float against the f32 tensors. */
 gw_status gw_adam_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int32_t *step,

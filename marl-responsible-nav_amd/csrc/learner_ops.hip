@@ -13,11 +13,12 @@ namespace {
 
 __global__ void __launch_bounds__(256) adam_kernel(float *__restrict__ p, const float *__restrict__ g,
                                                    float *__restrict__ m, float *__restrict__ v,
-                                                   const int32_t *__restrict__ step, int64_t n, double lr,
+                                                   int32_t *__restrict__ step, int64_t n, double lr,
                                                    double beta1, double beta2, double eps) {
     // the scalars exactly as torch's single-tensor Adam forms them: in double on the host side
     // (Python floats), rounded to float where they meet the f32 tensors
-    const double s = (double)(step[0] + 1);
+    const int32_t st = step[0];  // read by every block before the last one advances it (below)
+    const double s = (double)(st + 1);
     const float step_size = (float)(lr / (1.0 - pow(beta1, s)));
     const float bc2_sqrt = (float)sqrt(1.0 - pow(beta2, s));
     const float w1 = (float)(1.0 - beta1), b2 = (float)beta2, w2 = (float)(1.0 - beta2), e = (float)eps;
@@ -32,9 +33,18 @@ __global__ void __launch_bounds__(256) adam_kernel(float *__restrict__ p, const 
         const float denom = sqrtf(vi) / bc2_sqrt + e;             // (exp_avg_sq.sqrt() / bc2_sqrt).add_(eps)
         p[i] = __fmaf_rn(-step_size, mi / denom, p[i]);          // param.addcdiv_(exp_avg, denom, -step_size)
     }
+    // the last block to finish advances the step count: every block has read it by then (no
+    // separate increment launch); step[1] counts the arrivals and is left at 0
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(&step[1], 1) == (int32_t)gridDim.x - 1) {
+            step[0] = st + 1;
+            step[1] = 0;
+            __threadfence();
+        }
+    }
 }
-
-__global__ void step_inc(int32_t *step) { step[0] += 1; }
 
 __global__ void __launch_bounds__(256) soft_update_kernel(float *__restrict__ t, const float *__restrict__ p,
                                                           int64_t n, float tau) {
@@ -330,7 +340,6 @@ gw_status gw_adam_step(float *param, const float *grad, float *exp_avg, float *e
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, s, param, grad, exp_avg, exp_avg_sq, step, n,
                        lr, beta1, beta2, eps);
-    hipLaunchKernelGGL(step_inc, dim3(1), dim3(1), 0, s, step);
     return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
 }
 

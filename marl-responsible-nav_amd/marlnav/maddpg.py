@@ -120,7 +120,8 @@ class FlatAdam:
         self.flat = net.flat_params()
         self.m = torch.zeros_like(self.flat)
         self.v = torch.zeros_like(self.flat)
-        self.count = torch.zeros(1, dtype=torch.int32, device=self.flat.device)
+        # [0] steps taken, [1] the Adam launch's arrival counter (gw_adam_step; stays 0 between steps)
+        self.count = torch.zeros(2, dtype=torch.int32, device=self.flat.device)
         self.lr, self.betas, self.eps = float(lr), betas, float(eps)
         self.lib = _lib.load()
 
@@ -559,7 +560,9 @@ class MADDPG:
                 if f"{name}.m" in sd:
                     opt.m.copy_(sd[f"{name}.m"])
                     opt.v.copy_(sd[f"{name}.v"])
-                    opt.count.copy_(sd[f"{name}.count"])
+                    c = sd[f"{name}.count"].reshape(-1)  # round-3 checkpoints: [1] (no arrival counter)
+                    opt.count.zero_()
+                    opt.count[: c.numel()].copy_(c)
                 continue
             for i, p in enumerate(opt.param_groups[0]["params"]):
                 if f"{name}.{i}.exp_avg" not in sd:

@@ -284,7 +284,7 @@ def test_trainer_checkpoint_resume(tmp_path):
     assert torch.equal(rp2.final_obs[prev], want_next) and bool((rp2.done[prev] == 1).all())
     for a, b in zip(m.state_dict().values(), m2.state_dict().values()):
         assert torch.equal(a, b)
-    assert torch.equal(m.opt_actor.m, m2.opt_actor.m) and int(m.opt_actor.count) == int(m2.opt_actor.count)
+    assert torch.equal(m.opt_actor.m, m2.opt_actor.m) and int(m.opt_actor.count[0]) == int(m2.opt_actor.count[0])
     u0 = tr2.updates
     tr2.train(3)  # the resumed trainer keeps stepping and learning
     torch.cuda.synchronize()
