@@ -158,10 +158,9 @@ class MADDPGTrainer:
             sd = load_file(mem)
             calls = sd.pop("rollout_calls", None)
             self.rollout.replay.load_state_dict({k: v.to(self.env.device) for k, v in sd.items()})
-            self.rollout.resume()
             # the fused actor's Gumbel-noise Philox counter continues where the saved run stopped
             # (restarting it at 0 would replay the original run's exploration noise)
-            self.rollout._calls = int(calls[0]) if calls is not None else self.rollout.replay.t
+            self.rollout.resume(calls=int(calls[0]) if calls is not None else None)
         with open(os.path.join(path, "steps.txt")) as f:
             self.total_steps = int(f.read()) // self.global_envs * self.env.E
 

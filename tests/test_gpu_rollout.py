@@ -285,6 +285,9 @@ def test_trainer_checkpoint_resume(tmp_path):
     for a, b in zip(m.state_dict().values(), m2.state_dict().values()):
         assert torch.equal(a, b)
     assert torch.equal(m.opt_actor.m, m2.opt_actor.m) and int(m.opt_actor.count[0]) == int(m2.opt_actor.count[0])
+    # the fused actor's noise counter continues: no replay of the first run's noise
+    assert tr2.rollout._calls == tr.rollout._calls == 12
+    assert tr2.rollout._noise_base + rp2.t == tr2.rollout._calls
     u0 = tr2.updates
     tr2.train(3)  # the resumed trainer keeps stepping and learning
     torch.cuda.synchronize()
