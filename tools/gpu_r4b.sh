@@ -3,6 +3,8 @@ timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method threa
 timeout -k 10 120 python tools/bench_learn.py 128 > $O/learn.log 2>&1 && tail -2 $O/learn.log &&
 (cd /tmp && export TMPDIR=/tmp && timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$O/learnprof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/bench_learn.py 128 > $GRAFT_REPO_ROOT/$O/learnprof.log 2>&1) || exit 1
 for m in 0 3; do GW_PATCH_MODE=$m timeout -k 10 120 python tools/patch_probe.py > $O/probe_m$m.log 2>&1 || exit 1; done
+timeout -k 10 120 python tools/patch_probe.py 65536 16 grid64_n8 stamps > $O/probe_stamps_c4patch.log 2>&1 || exit 1
+timeout -k 10 120 python tools/patch_probe.py 65536 11 grid32 stamps > $O/probe_stamps_c5patch.log 2>&1 || exit 1
 timeout -k 10 300 python bench.py --config c2 --steps 20 --warmup 5 --no-cpu-baseline > $O/c2.log 2>&1 && python tools/bench_line.py $O/c2.log c2 &&
 timeout -k 10 300 python bench.py --config c2 --steps 200 --warmup 20 --no-cpu-baseline > $O/c2_200.log 2>&1 && python tools/bench_line.py $O/c2_200.log c2_200 &&
 timeout -k 10 300 python bench.py --config c2env --steps 200 --warmup 20 --no-cpu-baseline > $O/c2env.log 2>&1 && python tools/bench_line.py $O/c2env.log c2env &&

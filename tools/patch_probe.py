@@ -36,14 +36,15 @@ for scen, E, P in CASES:
 
 # per-block wall-clock stamps (100 MHz) of one launch: how many blocks overlap, where a block's
 # time goes (entry -> staged -> windows assembled -> stored)
-if len(sys.argv) > 3 and sys.argv[3] == "stamps":
+if "stamps" in sys.argv[3:]:
     import ctypes as C
     import numpy as np
     from marlnav import _lib
     lib = _lib.load()
     lib.gw_patch_debug_buffer.argtypes = [C.c_void_p]
     E, P = int(sys.argv[1]), int(sys.argv[2])
-    env = VecGridEnv("grid32", num_envs=E, fear=False, seed=1, obs=False)
+    scen = sys.argv[3] if sys.argv[3] != "stamps" else "grid32"
+    env = VecGridEnv(scen, num_envs=E, fear=False, seed=1, obs=False)
     env.reset()
     env.step()
     out = torch.empty((env.K, E, P, P), device="cuda")
@@ -55,6 +56,7 @@ if len(sys.argv) > 3 and sys.argv[3] == "stamps":
     torch.cuda.synchronize()
     lib.gw_patch_debug_buffer(None)
     d = dbg.cpu().numpy().astype(np.float64)
+    d[:, 2] = np.where(d[:, 2] == 0, d[:, 1], d[:, 2])  # MODE 2 / 3 assemble nothing in LDS
     d -= d[:, 0].min()
     us = d / 100.0
     print(f"blocks {nb}: kernel span {us[:, 3].max():.1f} us; block lifetime mean {np.mean(us[:, 3] - us[:, 0]):.2f} us "
