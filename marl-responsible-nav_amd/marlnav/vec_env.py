@@ -141,6 +141,8 @@ class VecGridEnv:
             done_copy=None, stats_acc=None, tick=None,
         )
         self._step_out = _lib.GwStepOut(*[_ptr(self.out[n]) for n in _lib.STEP_OUT_FIELDS])
+        self._into_cache = {}  # step(): (GwStepOut, fields, StepResult) per set of destination buffers
+        self._dev_index = self.device.index
         self._closed = False
         self._obs_queued = False  # async obs: the last step's writer not yet launched / fenced
         self.obs_async = False
@@ -187,13 +189,35 @@ class VecGridEnv:
         rl = self._as_i32(rl_actions, (self.E, self.K))
         sa = self._as_i32(scripted, (self.E, self.N - self.K))
         sp = self._as_i32(spawn, (self.E, self.N))
-        so = self._step_out
-        res = self.out
         over = dict(into or {})
         if obs_out is not None:
             over["obs"] = obs_out
         if final_obs_out is not None:
             over["final_obs"] = final_obs_out
+        # the step's output struct and result per set of destination buffers, built once: a
+        # pipelined step's host enqueue is on the critical path of short runs (the first step)
+        key = tuple((n, t.data_ptr(), t.dtype, t.numel()) for n, t in over.items())
+        cached = self._into_cache.get(key)
+        if cached is None:
+            cached = self._build_into(over)
+            if len(self._into_cache) >= 4096:
+                self._into_cache.clear()
+            self._into_cache[key] = cached
+        so, res, result = cached
+        if torch.cuda.current_device() != self._dev_index:
+            with torch.cuda.device(self.device):
+                _lib.check(self.lib.gw_step(self.handle, _ptr(rl), _ptr(sa), _ptr(sp), C.byref(so),
+                                            self._stream()), "gw_step")
+        else:
+            _lib.check(self.lib.gw_step(self.handle, _ptr(rl), _ptr(sa), _ptr(sp), C.byref(so),
+                                        torch.cuda.current_stream().cuda_stream), "gw_step")
+        self._obs_queued = self.obs_async and (res["obs"] is not None or res["final_obs"] is not None)
+        return result
+
+    def _build_into(self, over: dict):
+        """(GwStepOut, result fields, StepResult) for the destination buffers ``over``."""
+        so = self._step_out
+        res = self.out
         if over:
             so = _lib.GwStepOut.from_buffer_copy(self._step_out)
             res = dict(self.out)
@@ -208,11 +232,7 @@ class VecGridEnv:
                                      f"on {self.device}")
                 setattr(so, name, _ptr(t))
                 res[name] = t
-        with torch.cuda.device(self.device):
-            _lib.check(self.lib.gw_step(self.handle, _ptr(rl), _ptr(sa), _ptr(sp), C.byref(so),
-                                        self._stream()), "gw_step")
-        self._obs_queued = self.obs_async and (res["obs"] is not None or res["final_obs"] is not None)
-        return StepResult(**res)
+        return so, res, StepResult(**res)
 
     def capture_steps(self, n: int, gather=None) -> "StepGraph":
         """Capture ``n`` consecutive ``step()`` calls (device RNG policies, no host inputs) into
