@@ -501,11 +501,13 @@ def main():
     for i in range(n_graph, args.steps):
         one_step(i)
     t_enq = time.perf_counter() - t0  # host time to enqueue the timed steps (host-bound if ~ wall)
+    if gather is not None:
+        # the gathered returns of the last steps, compacted on the device (before the fences: the
+        # compaction reads what the world updates wrote, so it overlaps the last obs writer)
+        gather.compact()
     if cfg.get("rollout"):
         ro.fence()  # the last step's obs writes, FeAR outputs and statistics
     env.obs_fence()  # belong to the timed region
-    if gather is not None:
-        gather.compact()  # the gathered returns of the last steps, compacted on the device
     ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
