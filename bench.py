@@ -501,6 +501,8 @@ def main():
     for i in range(n_graph, args.steps):
         one_step(i)
     t_enq = time.perf_counter() - t0  # host time to enqueue the timed steps (host-bound if ~ wall)
+    if cfg.get("rollout"):
+        ro._flush()  # an unjoined FeAR step's statistics and return push (fear_async)
     if gather is not None:
         # the gathered returns of the last steps, compacted on the device (before the fences: the
         # compaction reads what the world updates wrote, so it overlaps the last obs writer)
