@@ -9,11 +9,12 @@
 //   l1_kernel       layer 1 (the only wide GEMM: in = K*D + 9K for a critic) split over
 //                   64-input chunks: one workgroup per (job, agent, chunk, 128-row tile) writes
 //                   the chunk's partial [rows][128]; the consumer adds the chunks in order.
-//   *_tail kernels  everything per row: the chunk sum, LayerNorms, ReLUs, layers 2-3 (W2 and
-//                   W2^T staged in LDS), Gumbel softmax, TD target, the loss gradient and the
-//                   backward through layers 3, 2 and the LayerNorms.  One workgroup per (agent,
-//                   16 rows); a row's 128 features live on 16 lanes (8 each), LayerNorm sums
-//                   are 16-lane butterflies.
+//   *_tail kernels  everything per row: the chunk sum, LayerNorms, ReLUs, layers 2-3 (the
+//                   block's 16 rows x 128 on v_mfma_f32_16x16x4_f32, W2 read from L2), Gumbel
+//                   softmax (the critic tail computes every agent's target action itself), TD
+//                   target, the loss gradient and the backward through layers 3, 2 and the
+//                   LayerNorms.  One workgroup per (agent, 16 rows); a row's 128 features live on
+//                   16 lanes (8 each), LayerNorm sums are 16-lane butterflies.
 //   grads_kernel    the parameter gradients, reductions over the rows in row order: W1 = X^T dz1,
 //                   W2 = h1^T dz2, W3 = h2^T g3, biases, LayerNorm affines, the loss value; written
 //                   (not accumulated) into the flat gradient buffer's per-layer views.
@@ -269,47 +270,41 @@ struct TailParams {
     float *probs_out;      // actor phase: [K][B][9] the fresh action probabilities (tests), may be null
 };
 
-// ---- phase 1a: target actions a'_k = GumbelSoftmax(actor_target_k(s'_k)) into x_next's slots ----
-__global__ void __launch_bounds__(256) target_actor_tail(TailParams p) {
-    __shared__ __attribute__((aligned(16))) float s_in[RB * HP];
-    __shared__ __attribute__((aligned(16))) float s_out[RB * HP];
-    const int k = blockIdx.y, tid = threadIdx.x, rl = tid >> 4, g = tid & 15;
-    const int r = blockIdx.x * RB + rl;
-    const Mlp m = mlp_k(p.actor_t, k, p.D, NA);
+// ---- phase 1a: target actions a'_k = GumbelSoftmax(actor_target_k(s'_k)) -------------------
+// agent kk's target action probabilities for row r (the per-row layout; all threads call it)
+__device__ __forceinline__ void target_probs(const TailParams &p, int kk, int r, int rl, int g, float *s_in,
+                                             float *s_out, float pr[NA]) {
+    const Mlp m = mlp_k(p.actor_t, kk, p.D, NA);
     float z[8], xh[8], y[8], rs;
-    l1_sum(p.part_a, p.nch_a, p.K, p.B, k, r, g, m.b1, z);
+    l1_sum(p.part_a, p.nch_a, p.K, p.B, kk, r, g, m.b1, z);
     ln_relu(z, m.lw1, m.lb1, g, xh, y, rs);
     rows_gemv(y, rl, g, m.w2, false, s_in, s_out, z);
 #pragma unroll
     for (int i = 0; i < 8; ++i) z[i] += m.b2[8 * g + i];
     ln_relu(z, m.lw2, m.lb2, g, xh, y, rs);
-    float lg[NA];
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
         float s = 0.0f;
 #pragma unroll
         for (int i = 0; i < 8; ++i) s = fmaf(y[i], m.w3[(8 * g + i) * NA + a], s);
-        lg[a] = row_sum(s) + m.b3[a];
+        pr[a] = row_sum(s) + m.b3[a];
     }
     // GumbelSoftmax (tau 1): softmax(logits - log(-log(u + eps) + eps)), gw_gumbel_softmax's op order
-    const float *ur = p.u + ((int64_t)k * p.B + r) * NA;
+    const float *ur = p.u + ((int64_t)kk * p.B + r) * NA;
     float mx = -INFINITY;
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
-        lg[a] = (lg[a] - logf(-logf(ur[a] + G_EPS) + G_EPS)) / 1.0f;
-        mx = fmaxf(mx, lg[a]);
+        pr[a] = (pr[a] - logf(-logf(ur[a] + G_EPS) + G_EPS)) / 1.0f;
+        mx = fmaxf(mx, pr[a]);
     }
     float sum = 0.0f;
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
-        lg[a] = expf(lg[a] - mx);
-        sum += lg[a];
+        pr[a] = expf(pr[a] - mx);
+        sum += pr[a];
     }
-    if (g == 0) {
-        float *o = p.x_next + (int64_t)r * p.ldx + (int64_t)p.K * p.D + NA * k;
 #pragma unroll
-        for (int a = 0; a < NA; ++a) o[a] = lg[a] / sum;
-    }
+    for (int a = 0; a < NA; ++a) pr[a] = pr[a] / sum;
 }
 
 // forward of critic (m) on row r: z1 = partial sum + b1 + the action columns of `act` (9K values
@@ -360,10 +355,25 @@ __global__ void __launch_bounds__(256) critic_tail(TailParams p) {
     const int r = blockIdx.x * RB + rl;
     const int na = NA * p.K;
     const int64_t Ds = (int64_t)p.K * p.D;
-    // target critic on (s', a'): the action slots written by target_actor_tail
+    // target critic on (s', a'): the target actions just computed
     const Mlp mt = mlp_k(p.critic_t, k, p.K * p.D + na, 1);
     const Mlp m = mlp_k(p.critic, k, p.K * p.D + na, 1);
-    for (int i = tid; i < RB * na; i += 256) s_act[i / na][i % na] = p.x_next[(int64_t)(blockIdx.x * RB + i / na) * p.ldx + Ds + i % na];
+    // every agent's target action on this block's rows (a block per agent recomputes the others':
+    // K x a small MLP instead of a launch and a round trip through x_next); agent k's go to x_next
+    // too (the caller's record of a')
+    for (int kk = 0; kk < p.K; ++kk) {
+        float pr[NA];
+        target_probs(p, kk, r, rl, g, s_in, s_out, pr);
+        if (g == 0) {
+#pragma unroll
+            for (int a = 0; a < NA; ++a) s_act[rl][NA * kk + a] = pr[a];
+            if (kk == k) {
+                float *o = p.x_next + (int64_t)r * p.ldx + Ds + NA * k;
+#pragma unroll
+                for (int a = 0; a < NA; ++a) o[a] = pr[a];
+            }
+        }
+    }
     __syncthreads();
     RowFwd f;
     const float q_next = critic_fwd(mt, p.part_ct, p.nch_cs, p, k, r, rl, g, s_act[rl], s_in, s_out, f);
@@ -803,7 +813,6 @@ gw_status gw_maddpg_critic_grads(const gw_mlp_actors *actor_target, const gw_mlp
     tp.nch_a = nchunks(D);
     tp.nch_c = nchunks(ldx);
     tp.nch_cs = nchunks((int64_t)K * D);
-    hipLaunchKernelGGL(target_actor_tail, dim3(B / RB, K), dim3(256), 0, s, tp);
     hipLaunchKernelGGL(critic_tail, dim3(B / RB, K), dim3(256), 0, s, tp);
     GradParams gp{};
     gp.grad = *critic_grad;

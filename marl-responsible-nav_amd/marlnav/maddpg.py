@@ -302,7 +302,7 @@ class MADDPG:
         return ws
 
     def _fused_critic(self, states, actions, rewards, next_states, dones, u_next, critic_in) -> dict:
-        """Phase 1 as gw_maddpg_critic_grads (include/learner_ops.h): 4 launches."""
+        """Phase 1 as gw_maddpg_critic_grads (include/learner_ops.h): 3 launches."""
         import ctypes as C
         K, B = states.shape[0], states.shape[1]
         dev = self.device
