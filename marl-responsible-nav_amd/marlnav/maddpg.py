@@ -458,8 +458,11 @@ class MADDPG:
         """(states, actions, rewards, next_states, dones, u_next, u_cur, critic_in) as ``learn``
         takes them (no explicit uniforms; critic_in from the gather launch on the GPU)."""
         if self.device.type == "cuda":  # the critic's input rows come from the gather launch
-            *batch, ci = replay.sample(self.batch_size, generator=generator, critic_in=True)
-            return (*batch, None, None, ci)
+            # the two Gumbel samples' uniforms come from the sample's own torch.rand launch
+            n = self.K * self.batch_size * N_ACTIONS
+            *batch, ci, uu = replay.sample(self.batch_size, generator=generator, critic_in=True, extra_uniform=2 * n)
+            shape = (self.K, self.batch_size, N_ACTIONS)
+            return (*batch, uu[:n].view(shape), uu[n:].view(shape), ci)
         return (*replay.sample(self.batch_size, generator=generator), None, None, None)
 
     def capture(self, replay=None, warmup: int = 3, batch: tuple | None = None):

@@ -75,7 +75,7 @@ class ReplayRing:
 
     @torch.no_grad()
     def sample(self, batch: int, generator: torch.Generator | None = None, return_idx: bool = False,
-               critic_in: bool = False):
+               critic_in: bool = False, extra_uniform: int = 0):
         """Uniform transitions -> (state [K,B,H,W], probs [K,B,9], reward [B,K], next_state, term [B,K]).
         Every index is computed on the device from ``t_dev``, so a captured graph stays valid as
         the ring fills (MultiAgentReplayBuffer.sample, uniform without priorities).
@@ -85,7 +85,7 @@ class ReplayRing:
             raise RuntimeError("empty replay ring")
         dev = self.obs.device
         if dev.type == "cuda":
-            return self._sample_hip(batch, generator, return_idx, critic_in)
+            return self._sample_hip(batch, generator, return_idx, critic_in, extra_uniform)
         n = torch.clamp(self.t_dev, min=1, max=self.S - 1)
         step = torch.minimum((torch.rand((batch,), device=dev, generator=generator) * n).long(), n - 1)
         env = torch.randint(0, self.E, (batch,), device=dev, generator=generator)
@@ -98,11 +98,14 @@ class ReplayRing:
         out = (state, self.probs[tr, :, env].permute(1, 0, 2), self.reward[tr, env], next_state, self.term[tr, env])
         return out + ((tr, env),) if return_idx else out
 
-    def _sample_hip(self, batch, generator, return_idx, critic_in=False):
+    def _sample_hip(self, batch, generator, return_idx, critic_in=False, extra=0):
         """sample() on the GPU: the same draws (torch.rand, then torch.randint), then the index
-        arithmetic and every gather in ONE launch (gw_replay_gather, include/rollout_ops.h)."""
+        arithmetic and every gather in ONE launch (gw_replay_gather, include/rollout_ops.h).
+        extra > 0: that many more uniforms from the same torch.rand launch, returned last (the
+        learner's Gumbel uniforms: one launch instead of three)."""
         dev = self.obs.device
-        u = torch.rand((batch,), device=dev, generator=generator)
+        u_all = torch.rand((batch + int(extra),), device=dev, generator=generator)
+        u = u_all[:batch]
         env = torch.randint(0, self.E, (batch,), device=dev, generator=generator)
         K, HW = self.K, self.obs.shape[-2] * self.obs.shape[-1]
         state = torch.empty((K, batch) + tuple(self.obs.shape[-2:]), device=dev, dtype=torch.float32)
@@ -125,7 +128,9 @@ class ReplayRing:
         out = (state, probs, reward, next_state, term)
         if return_idx:
             out = out + ((tr, env),)
-        return out + ((x, xn),) if critic_in else out
+        if critic_in:
+            out = out + ((x, xn),)
+        return out + (u_all[batch:],) if extra else out
 
 
 class Rollout:
