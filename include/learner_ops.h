@@ -23,6 +23,14 @@ extern "C" {
 gw_status gw_adam_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int32_t *step,
                        int64_t n, double lr, double beta1, double beta2, double eps, void *stream);
 
+/* gw_adam_step on param[0, n), then in the same launch the soft target updates that end
+ * MADDPG.learn: target[i] = tau * param[i] + (1 - tau) * target[i] with the stepped param, and
+ * target2 = tau * online2 + (1 - tau) * target2 on n2 elements (the other network, stepped
+ * earlier; n2 = 0: none).  Same arithmetic as gw_adam_step followed by gw_soft_update2. */
+gw_status gw_adam_soft_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int32_t *step,
+                            int64_t n, double lr, double beta1, double beta2, double eps, float *target, float tau,
+                            float *target2, const float *online2, int64_t n2, void *stream);
+
 /* agilerl soft_update: target = tau * online + (1 - tau) * target on n elements. */
 gw_status gw_soft_update(float *target, const float *online, int64_t n, float tau, void *stream);
 

@@ -11,10 +11,16 @@
 
 namespace {
 
+// torch.optim.Adam on p[0, n) and, when t1 != null, the soft target update that follows it in
+// MADDPG.learn (agilerl soft_update, both networks): t1[i] = tau p[i] + (1 - tau) t1[i] with the
+// just-updated p[i] (same element, same thread), and t2 = tau p2 + (1 - tau) t2 on [n, n + n2)
+// (the other network, already stepped): one launch instead of an Adam and a soft-update launch.
 __global__ void __launch_bounds__(256) adam_kernel(float *__restrict__ p, const float *__restrict__ g,
                                                    float *__restrict__ m, float *__restrict__ v,
                                                    int32_t *__restrict__ step, int64_t n, double lr,
-                                                   double beta1, double beta2, double eps) {
+                                                   double beta1, double beta2, double eps, float *__restrict__ t1,
+                                                   float *__restrict__ t2, const float *__restrict__ p2, int64_t n2,
+                                                   float tau) {
     // the scalars exactly as torch's single-tensor Adam forms them: in double on the host side
     // (Python floats), rounded to float where they meet the f32 tensors
     const int32_t st = step[0];  // read by every block before the last one advances it (below)
@@ -22,16 +28,24 @@ __global__ void __launch_bounds__(256) adam_kernel(float *__restrict__ p, const 
     const float step_size = (float)(lr / (1.0 - pow(beta1, s)));
     const float bc2_sqrt = (float)sqrt(1.0 - pow(beta2, s));
     const float w1 = (float)(1.0 - beta1), b2 = (float)beta2, w2 = (float)(1.0 - beta2), e = (float)eps;
+    const int64_t total = n + (t1 ? n2 : 0);
     // torch's elementwise kernels are built with FMA contraction; each torch op below is one
     // rounding (or one fma), and this file is built -ffp-contract=off, so the fmas are explicit
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        if (i >= n) {  // the other network's soft update (the soft_update2_kernel's op order)
+            const int64_t j = i - n;
+            t2[j] = tau * p2[j] + (1.0f - tau) * t2[j];
+            continue;
+        }
         const float gi = g[i];
         const float mi = __fmaf_rn(w1, gi - m[i], m[i]);         // exp_avg.lerp_(grad, 1 - beta1)
         const float vi = __fmaf_rn(w2 * gi, gi, v[i] * b2);      // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
         m[i] = mi;
         v[i] = vi;
         const float denom = sqrtf(vi) / bc2_sqrt + e;             // (exp_avg_sq.sqrt() / bc2_sqrt).add_(eps)
-        p[i] = __fmaf_rn(-step_size, mi / denom, p[i]);          // param.addcdiv_(exp_avg, denom, -step_size)
+        const float pi = __fmaf_rn(-step_size, mi / denom, p[i]);  // param.addcdiv_(exp_avg, denom, -step_size)
+        p[i] = pi;
+        if (t1) t1[i] = tau * pi + (1.0f - tau) * t1[i];
     }
     // the last block to finish advances the step count: every block has read it by then (no
     // separate increment launch); step[1] counts the arrivals and is left at 0
@@ -339,7 +353,19 @@ gw_status gw_adam_step(float *param, const float *grad, float *exp_avg, float *e
     if (!param || !grad || !exp_avg || !exp_avg_sq || !step || n < 0) return GW_ERR_ARG;
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, s, param, grad, exp_avg, exp_avg_sq, step, n,
-                       lr, beta1, beta2, eps);
+                       lr, beta1, beta2, eps, nullptr, nullptr, nullptr, (int64_t)0, 0.0f);
+    return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
+}
+
+gw_status gw_adam_soft_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int32_t *step,
+                            int64_t n, double lr, double beta1, double beta2, double eps, float *target, float tau,
+                            float *target2, const float *online2, int64_t n2, void *stream) {
+    if (!param || !grad || !exp_avg || !exp_avg_sq || !step || n < 0 || !target || n2 < 0 ||
+        (n2 > 0 && (!target2 || !online2)))
+        return GW_ERR_ARG;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n + n2)), dim3(256), 0, s, param, grad, exp_avg, exp_avg_sq, step, n,
+                       lr, beta1, beta2, eps, target, target2, online2, n2, tau);
     return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
 }
 

@@ -176,7 +176,8 @@ EXPORTS = ["gw_create", "gw_reset", "gw_step", "gw_state_view", "gw_copy_state",
            "gw_patch_actor_act", "gw_patch_cnn_workspace_floats", "gw_patch_cnn_prepare", "gw_patch_cnn_act",
            "gw_maddpg_workspace_floats", "gw_maddpg_critic_grads", "gw_maddpg_actor_grads",
            "gw_pipeline_state_bytes", "gw_pipeline_save", "gw_pipeline_load",
-           "gw_gather_pack_scratch", "gw_gather_pack", "gw_gather_unpack_plan_cap", "gw_gather_unpack"]
+           "gw_gather_pack_scratch", "gw_gather_pack", "gw_gather_unpack_plan_cap", "gw_gather_unpack",
+           "gw_adam_soft_step"]
 
 
 class GwObsSource(C.Structure):
@@ -268,6 +269,9 @@ def _declare(L):
     L.gw_fear_matrix.restype = C.c_int
     L.gw_adam_step.argtypes = [p, p, p, p, p, C.c_int64, C.c_double, C.c_double, C.c_double, C.c_double, p]
     L.gw_adam_step.restype = C.c_int
+    L.gw_adam_soft_step.argtypes = [p, p, p, p, p, C.c_int64, C.c_double, C.c_double, C.c_double, C.c_double, p,
+                                    C.c_float, p, p, C.c_int64, p]
+    L.gw_adam_soft_step.restype = C.c_int
     L.gw_soft_update.argtypes = [p, p, C.c_int64, C.c_float, p]
     L.gw_soft_update.restype = C.c_int
     L.gw_ln_relu_fwd.argtypes = [p, p, p, p, p, p, C.c_int32, C.c_int64, C.c_int32, C.c_float, p]

@@ -135,6 +135,17 @@ class FlatAdam:
                                          self.betas[0], self.betas[1], self.eps, s), "gw_adam_step")
         self.net.epoch += 1  # written behind torch's version counter (see MultiAgentActors.act_env)
 
+    def step_soft(self, target: torch.Tensor, tau: float, target2: torch.Tensor, online2: torch.Tensor):
+        """step(), then the soft target updates target <- tau p + (1 - tau) target (this buffer's
+        target) and target2 <- tau online2 + (1 - tau) target2, in ONE launch (gw_adam_soft_step)."""
+        s = torch.cuda.current_stream(self.flat.device).cuda_stream
+        _lib.check(self.lib.gw_adam_soft_step(self.flat.data_ptr(), self.flat.grad.data_ptr(), self.m.data_ptr(),
+                                              self.v.data_ptr(), self.count.data_ptr(), self.flat.numel(), self.lr,
+                                              self.betas[0], self.betas[1], self.eps, target.data_ptr(), float(tau),
+                                              target2.data_ptr(), online2.data_ptr(), online2.numel(), s),
+                   "gw_adam_soft_step")
+        self.net.epoch += 1
+
 
 def _mlp_target(net: StackedMLPActors) -> StackedMLPActors:
     """A frozen copy with its own flat buffer (copy.deepcopy would clone the layer views apart)."""
@@ -398,9 +409,17 @@ class MADDPG:
         ctx["actor_loss"] = actor_loss.detach()
 
     def _learn_finish(self, ctx: dict):
-        """Phase 3: the actor's Adam step and the soft target update."""
-        self.opt_actor.step()
-        self.soft_update()
+        """Phase 3: the actor's Adam step and the soft target update (flat buffers: one launch)."""
+        if self.flat and isinstance(self.opt_actor, FlatAdam):
+            t1 = self.actor_targets.net.flat_params()
+            t2, p2 = self.critic_targets.flat_params(), self.critics.flat_params()
+            with torch.no_grad():
+                self.opt_actor.step_soft(t1, self.tau, t2, p2)
+            self.actor_targets.net.epoch += 1
+            self.critic_targets.epoch += 1
+        else:
+            self.opt_actor.step()
+            self.soft_update()
         return ctx["actor_loss"], ctx["critic_loss"]
 
     def _q_split(self, x: torch.Tensor, a: torch.Tensor) -> torch.Tensor:
