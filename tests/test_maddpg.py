@@ -202,6 +202,37 @@ def test_gpu_adam_and_soft_update_match_torch(n):
     torch.testing.assert_close(t, lerp, rtol=1e-6, atol=1e-7)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,n2", [(1000, 3000), (300_001, 77)])
+def test_gpu_adam_soft_step_equals_adam_then_soft_update(n, n2):
+    """gw_adam_soft_step (the learner's last launch) == gw_adam_step followed by gw_soft_update2,
+    bit for bit: parameters, moments, step count and both targets, over 3 steps."""
+    from marlnav import _lib
+    lib = _lib.load()
+    s = torch.cuda.current_stream().cuda_stream
+    g = torch.Generator(device="cuda").manual_seed(4)
+    bufs = []
+    for _ in range(2):
+        torch.manual_seed(9)
+        bufs.append(dict(p=torch.randn(n, device="cuda"), m=torch.zeros(n, device="cuda"), v=torch.zeros(n, device="cuda"),
+                         c=torch.zeros(2, dtype=torch.int32, device="cuda"), t1=torch.randn(n, device="cuda"),
+                         t2=torch.randn(n2, device="cuda"), o2=torch.randn(n2, device="cuda")))
+    for _ in range(3):
+        grad = torch.randn(n, device="cuda", generator=g)
+        a, b = bufs
+        _lib.check(lib.gw_adam_step(a["p"].data_ptr(), grad.data_ptr(), a["m"].data_ptr(), a["v"].data_ptr(),
+                                    a["c"].data_ptr(), n, 1e-3, 0.9, 0.999, 1e-8, s), "gw_adam_step")
+        _lib.check(lib.gw_soft_update2(a["t1"].data_ptr(), a["p"].data_ptr(), n, a["t2"].data_ptr(), a["o2"].data_ptr(),
+                                       n2, 0.01, s), "gw_soft_update2")
+        _lib.check(lib.gw_adam_soft_step(b["p"].data_ptr(), grad.data_ptr(), b["m"].data_ptr(), b["v"].data_ptr(),
+                                         b["c"].data_ptr(), n, 1e-3, 0.9, 0.999, 1e-8, b["t1"].data_ptr(), 0.01,
+                                         b["t2"].data_ptr(), b["o2"].data_ptr(), n2, s), "gw_adam_soft_step")
+    torch.cuda.synchronize()
+    for key in ("p", "m", "v", "c", "t1", "t2"):
+        assert torch.equal(bufs[0][key], bufs[1][key]), key
+    assert int(bufs[1]["c"][0]) == 3 and int(bufs[1]["c"][1]) == 0
+
+
 def test_gumbel_softmax_is_a_distribution_and_sharpens():
     logits = torch.tensor([[0.0, 5.0, 0.0]])
     g = torch.Generator().manual_seed(0)
