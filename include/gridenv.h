@@ -147,7 +147,7 @@ gw_status gw_copy_state(void *env, const gw_state *buf, int to_env, void *stream
  * GW_KERNEL=defer only; it runs concurrently with the writer), and the ops that take this env's
  * handle: GW_SPAN_ACT the fused actors' MLP kernel (act_kernel of gw_actor_act,
  * gw_patch_actor_act, gw_cnn_act, gw_patch_cnn_act), GW_SPAN_CNN_L1 the CNN heads' layer-1
- * listing kernel, GW_SPAN_CNN_LIST their bucket scan / plan / scatter (three launches), GW_SPAN_CNN_RARE
+ * listing kernel, GW_SPAN_CNN_LIST their bucket scan + unit plan and scatter (two launches), GW_SPAN_CNN_RARE
  * their recompute of the listed conv positions, GW_SPAN_WINDOW the window writer (gw_obs_patch).
  * enable > 1 also makes sure `enable` timing events exist now (creating them inside a profiled
  * step would put their host cost between its launches).  gw_profile_read synchronises on those

@@ -688,9 +688,9 @@ struct CnnWs {
     float *h1;        // [K][E][128]      z_map + table rows
     float *rare_z;    // [K][E][RS][128]  their Linear-1 contributions
     int *rare_n;      // [K][E]           recomputed positions per (env, agent)
-    int *bucket_n;    // [K][P]           items per position (bucket_scan)
+    int *bucket_n;    // [K][P]           items per position (bucket_scan_plan)
     int *bucket;      // [K][P][E]        items (e RS + slot) per position
-    int *unit_off;    // [K P + 1]        cnn_rare_plan's unit offsets
+    int *unit_off;    // [K P + 1]        bucket_scan_plan's unit offsets
 };
 inline int64_t cnn_mlp_floats(int K) { return (int64_t)K * (HID + W2IMG + W3IMG + W2BIMG); }
 inline CnnWs cnn_ws_layout(float *base, int K, int P, int64_t E) {
@@ -718,9 +718,10 @@ inline CnnWs cnn_ws_layout(float *base, int K, int P, int64_t E) {
 //   item [K][E]      the (env, agent)'s positions to recompute (grid: up to RS position bytes in
 //                    slot order; windows: a position mask, slot = rank in the mask)
 //   cnt / off [nb][nblk]  items per (bucket, layer-1 block) and their offsets in the bucket
-// bucket_scan turns the counts into offsets and bucket sizes, the scatter kernels fill the buckets.
+// bucket_scan_plan turns the counts into offsets, bucket sizes and units, the scatter kernels fill the buckets.
+// ctr: bucket_scan_plan's arrival counter (zeroed by the prepare calls, left at 0 by every launch)
 struct Lists {
-    int *item, *cnt, *off;
+    int *item, *cnt, *off, *ctr;
     int nblk;
 };
 inline Lists lists_at(int *unit_off, int nb, int K, int64_t E, int per_block) {
@@ -729,10 +730,11 @@ inline Lists lists_at(int *unit_off, int nb, int K, int64_t E, int per_block) {
     l.item = unit_off + nb + 1;
     l.cnt = l.item + (int64_t)K * E;
     l.off = l.cnt + (int64_t)nb * l.nblk;
+    l.ctr = l.off + (int64_t)nb * l.nblk;
     return l;
 }
 inline int64_t lists_floats(int nb, int K, int64_t E, int per_block) {
-    return (int64_t)K * E + 2 * (int64_t)nb * ((E + per_block - 1) / per_block);
+    return (int64_t)K * E + 2 * (int64_t)nb * ((E + per_block - 1) / per_block) + 4;
 }
 constexpr int L1_ENVS = TILE * L1_WAVES;  // envs per cnn_l1_kernel block
 inline int64_t cnn_ws_floats(int K, int P, int64_t E) {
@@ -884,8 +886,8 @@ __global__ void __launch_bounds__(256) cnn_prep_table(CnnParams p) {
 
 // Layer 1 of the CNN head for every (env, agent): h1 = z_map + the changed positions' deltas.
 // cnn_l1_kernel sums the table rows of the positions with one patched cell into h1 and lists the
-// positions with several (slot order) with per-block counts; bucket_scan / cnn_scatter file them
-// as (env, slot) items into per-(agent, position) buckets (no global atomics); cnn_rare_plan cuts
+// positions with several (slot order) with per-block counts; bucket_scan_plan / cnn_scatter file them
+// as (env, slot) items into per-(agent, position) buckets (no global atomics); bucket_scan_plan cuts
 // the buckets into units of up to 16 x RARE_WAVES items; cnn_rare_kernel
 // (persistent) takes units with the position's Linear-1 block staged in LDS, recomputes each
 // item's position (conv 1, conv 2) and writes its 128-float contribution; act_kernel<H1> adds an
@@ -1042,31 +1044,8 @@ __global__ void __launch_bounds__(L1_ENVS) cnn_scatter(CnnParams p, Lists lists)
 }
 
 // Units of work over the buckets: bucket b (= k P_n + P) holds ceil(n_b / RARE_ITEMS) units;
-// unit_off[b] = the units before bucket b (one block, K P_n <= 2048 buckets).
+// unit_off[b] = the units before bucket b (bucket_scan_plan's last block).
 constexpr int RARE_WAVES = 8, RARE_ITEMS = 16 * RARE_WAVES, RARE_BLOCKS = 256;
-__global__ void __launch_bounds__(1024) cnn_rare_plan(CnnParams p) {
-    __shared__ int s_sum[1024];
-    const int nb = p.K * p.P, tid = threadIdx.x;
-    const int per = (nb + 1023) / 1024, b0 = tid * per;   // each thread scans `per` buckets
-    int loc = 0;
-    for (int i = 0; i < per; ++i)
-        if (b0 + i < nb) loc += (p.ws.bucket_n[b0 + i] + RARE_ITEMS - 1) / RARE_ITEMS;
-    s_sum[tid] = loc;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {  // inclusive Hillis-Steele scan
-        const int v = tid >= off ? s_sum[tid - off] : 0;
-        __syncthreads();
-        s_sum[tid] += v;
-        __syncthreads();
-    }
-    int run = s_sum[tid] - loc;
-    for (int i = 0; i < per; ++i)
-        if (b0 + i < nb) {
-            p.ws.unit_off[b0 + i] = run;
-            run += (p.ws.bucket_n[b0 + i] + RARE_ITEMS - 1) / RARE_ITEMS;
-        }
-    if (tid == 1023) p.ws.unit_off[nb] = s_sum[1023];
-}
 
 // Persistent: block b takes units b, b + RARE_BLOCKS, ...; per unit the position's conv weights,
 // map activations and Linear-1 block are staged in LDS.  Lane (item it = l & 15, quarter q): the
@@ -1232,7 +1211,7 @@ __global__ void __launch_bounds__(64 * RARE_WAVES) cnn_rare_kernel(CnnParams p) 
 // patched cells.  gw_patch_cnn_prepare tabulates, per (agent, centre): a2b = conv-2 activations of
 // B_c at every window position Q, and tbl = b + Linear-1(a2b).  Per step, wcnn_l1_kernel lists the
 // positions where the actual window differs from B_c (a patched cell inside the window other than
-// the centre holding vo_k); bucket_scan / wcnn_scatter file them as items (env, slot) into buckets
+// the centre holding vo_k); bucket_scan_plan / wcnn_scatter file them as items (env, slot) into buckets
 // keyed (agent, Q) in env order (a scan of per-block counts: no atomics); the persistent
 // wcnn_rare_kernel recomputes each item's position and writes Wl[:, Q] . (a2 - a2b);
 // act_kernel<H1, PW> sums tbl[centre] + those terms (slot order) and runs layers 2-3.
@@ -1335,7 +1314,7 @@ __global__ void __launch_bounds__(256) wcnn_prep_base(CnnParams p) {
 
 // one thread per (env, agent): the positions where the window differs from its base window as a
 // mask (slot = rank of the position in it; rare_n = their count) and the items per (position,
-// block); bucket_scan scans the counts, wcnn_scatter fills the buckets
+// block); bucket_scan_plan scans the counts, wcnn_scatter fills the buckets
 template <int NP>
 __global__ void __launch_bounds__(256) wcnn_l1_kernel(CnnParams p, Lists lists) {
     __shared__ uint32_t s_road[128];
@@ -1402,11 +1381,14 @@ __global__ void __launch_bounds__(256) wcnn_l1_kernel(CnnParams p, Lists lists) 
         lists.cnt[((size_t)k * p.P + tid) * lists.nblk + blockIdx.x] = s_cnt[0][tid] + s_cnt[1][tid] + s_cnt[2][tid] + s_cnt[3][tid];
 }
 
-// one wave per bucket: the offsets of the layer-1 blocks' items in the bucket (a wave scan over
-// the blocks in order) and the bucket's size (cnn_rare_plan then cuts the buckets into units)
-__global__ void __launch_bounds__(1024) bucket_scan(CnnParams p, Lists lists) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, b = blockIdx.x * 16 + wave;
-    if (b >= p.K * p.P) return;
+
+// one 64-thread block per bucket: the offsets of the layer-1 blocks' items in the bucket (a wave
+// scan over the blocks in order) and the bucket's size; the last bucket to finish (an arrival
+// counter) cuts every bucket into units of RARE_ITEMS (unit_off), which cnn_rare_plan did in a
+// launch of its own.  One-wave blocks find a CU slot beside a concurrent window writer (a
+// 1024-thread block waits for 16 free wave slots on one CU).
+__global__ void __launch_bounds__(64) bucket_scan_plan(CnnParams p, Lists lists) {
+    const int lane = threadIdx.x, b = blockIdx.x, nb = p.K * p.P;
     int run = 0;
     for (int c0 = 0; c0 < lists.nblk; c0 += 64) {
         const int i = c0 + lane;
@@ -1420,7 +1402,32 @@ __global__ void __launch_bounds__(1024) bucket_scan(CnnParams p, Lists lists) {
         if (i < lists.nblk) lists.off[(size_t)b * lists.nblk + i] = run + incl - v;
         run += __shfl(incl, 63, 64);
     }
-    if (lane == 0) p.ws.bucket_n[b] = run;
+    int last = 0;
+    if (lane == 0) {
+        p.ws.bucket_n[b] = run;
+        __threadfence();
+        last = atomicAdd(lists.ctr, 1) == nb - 1;
+    }
+    if (!__shfl(last, 0, 64)) return;
+    __threadfence();
+    int base = 0;
+    for (int c0 = 0; c0 < nb; c0 += 64) {
+        const int i = c0 + lane;
+        const int n = i < nb ? __hip_atomic_load(&p.ws.bucket_n[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        const int u = (n + RARE_ITEMS - 1) / RARE_ITEMS;
+        int incl = u;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int o = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += o;
+        }
+        if (i < nb) p.ws.unit_off[i] = base + incl - u;
+        base += __shfl(incl, 63, 64);
+    }
+    if (lane == 0) {
+        p.ws.unit_off[nb] = base;
+        *lists.ctr = 0;
+    }
 }
 
 // fills the buckets in (block, wave, lane) order: item (e RSW + slot), slot = the position's rank
@@ -1822,6 +1829,10 @@ gw_status gw_cnn_prepare(void *env, const gw_cnn_actors *net, float *ws, void *s
     hipLaunchKernelGGL(cnn_prep_zpart, dim3(p.P, src.K), dim3(128), 0, s, p);
     hipLaunchKernelGGL(cnn_prep_zmap, dim3(src.K), dim3(128), 0, s, p);
     hipLaunchKernelGGL(cnn_prep_table, dim3(p.P, src.K), dim3(256), 0, s, p);
+    {  // bucket_scan_plan's arrival counter starts at 0 (every launch leaves it there)
+        const Lists l = lists_at(p.ws.unit_off, src.K * p.P, src.K, src.E, L1_ENVS);
+        if (hipMemsetAsync(l.ctr, 0, sizeof(int), s) != hipSuccess) return err(GW_ERR_HIP, "gw_cnn_prepare: memset");
+    }
     PrepParams pp;  // the layer-2/3 MFMA images (prep_images; nslices 0: c1 is rewritten below)
     pp.net = cnn_tail(net);
     pp.HW = p.HW;
@@ -1866,8 +1877,7 @@ gw_status gw_cnn_act(void *env, const gw_cnn_actors *net, const float *ws, int t
     }
     {
         gwprof::Span span(env, GW_SPAN_CNN_LIST);
-        gwprof::launch(bucket_scan, dim3((src.K * cp.P + 15) / 16), dim3(1024), 0, s, cp, lists);
-        gwprof::launch(cnn_rare_plan, dim3(1), dim3(1024), 0, s, cp);
+        gwprof::launch(bucket_scan_plan, dim3(src.K * cp.P), dim3(64), 0, s, cp, lists);
         gwprof::launch(cnn_scatter, lgrid, dim3(L1_ENVS), 0, s, cp, lists);
     }
 #define RARE(NP) gwprof::launch(cnn_rare_kernel<NP>, dim3(RARE_BLOCKS), dim3(64 * RARE_WAVES), 0, s, cp)
@@ -1976,6 +1986,10 @@ gw_status gw_patch_cnn_prepare(void *env, int32_t P, const gw_cnn_actors *net, f
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(cnn_prep_wlt, dim3(2048), dim3(256), 0, s, p);
     hipLaunchKernelGGL(wcnn_prep_base, dim3((p.HW + WCG - 1) / WCG, src.K), dim3(256), 0, s, p);
+    {  // bucket_scan_plan's arrival counter starts at 0 (every launch leaves it there)
+        const Lists l = lists_at(p.ws.unit_off, src.K * p.P, src.K, src.E, 256);
+        if (hipMemsetAsync(l.ctr, 0, sizeof(int), s) != hipSuccess) return err(GW_ERR_HIP, "gw_patch_cnn_prepare: memset");
+    }
     PrepParams pp;  // the layer-2/3 MFMA images (c1 unused)
     pp.net = cnn_tail(net);
     pp.HW = P * P;
@@ -2019,8 +2033,7 @@ gw_status gw_patch_cnn_act(void *env, int32_t P, const gw_cnn_actors *net, const
     }
     {
         gwprof::Span span(env, GW_SPAN_CNN_LIST);
-        gwprof::launch(bucket_scan, dim3((src.K * cp.P + 15) / 16), dim3(1024), 0, s, cp, lists);
-        gwprof::launch(cnn_rare_plan, dim3(1), dim3(1024), 0, s, cp);
+        gwprof::launch(bucket_scan_plan, dim3(src.K * cp.P), dim3(64), 0, s, cp, lists);
         gwprof::launch(wcnn_scatter, lgrid, dim3(256), 0, s, cp, lists);
     }
 #define RARE(NP) gwprof::launch(wcnn_rare_kernel<NP>, dim3(RARE_BLOCKS), dim3(64 * RARE_WAVES), 0, s, cp)
