@@ -1721,7 +1721,13 @@ gw_status actor_act(const char *who, void *env, int32_t P, const gw_mlp_actors *
     // 2 = the same with f32 MFMA (exact products); 0 = two 8-wave blocks per CU, f32 MFMA
     const char *av = std::getenv("GW_ACT_V");
     const int v = P > 0 ? 4 : (av ? std::atoi(av) : 4);
-    const int waves = v == 0 ? 8 : 16;
+    // small env counts (C2: 4,096 envs = 256 tiles per agent): 16-wave blocks would leave most
+    // CUs idle with 4 waves per SIMD each doing one tile; 4-wave blocks spread the same tiles over
+    // 4x the CUs (one wave per SIMD).  GW_ACT_WAVES=16|4 forces either (A/B).
+    const char *aw = std::getenv("GW_ACT_WAVES");
+    const bool small = P == 0 && v == 4 &&
+                       (aw ? std::atoi(aw) == 4 : (tiles + 15) / 16 < std::max(1, 256 / src.K) / 2);
+    const int waves = v == 0 ? 8 : small ? 4 : 16;
     const int resident = v == 0 ? 512 : 256;
     const int64_t want = (tiles + waves - 1) / waves;
     const int per_agent = (int)std::max<int64_t>(1, std::min<int64_t>(want, std::max(1, resident / src.K)));
@@ -1734,6 +1740,8 @@ gw_status actor_act(const char *who, void *env, int32_t P, const gw_mlp_actors *
             gwprof::launch(act_kernel<NP, 16, true, false, true>, grid, block, 0, s, p); \
         else if (v == 0)                                                                 \
             gwprof::launch(act_kernel<NP, 8>, grid, block, 0, s, p);                     \
+        else if (v == 4 && small)                                                        \
+            gwprof::launch(act_kernel<NP, 4, true>, grid, block, 0, s, p);               \
         else if (v == 4)                                                                 \
             gwprof::launch(act_kernel<NP, 16, true>, grid, block, 0, s, p);              \
         else                                                                             \

@@ -210,3 +210,24 @@ def test_fused_act_layer2_precision(variant, monkeypatch):
     err = (logits.double() - h).abs().max().item()
     assert err < 2e-5, err
     env.close()
+
+
+@pytest.mark.parametrize("E", [4096, 777])
+def test_fused_act_block_shape_does_not_change_results(E, monkeypatch):
+    """Small env counts launch 4-wave blocks (one wave per SIMD on 4x the CUs) instead of one
+    16-wave block per CU; each wave still evaluates whole 16-env tiles in the same order, so
+    logits, probabilities and actions (Philox noise) are bit for bit those of 16-wave blocks."""
+    sc = S.builtin("grid32")
+    env = VecGridEnv(sc, num_envs=E, fear=False, seed=12)
+    actors = _actors(sc, seed=13)
+    env.reset()
+    env.step()
+    out = {}
+    for w in ("4", "16"):
+        monkeypatch.setenv("GW_ACT_WAVES", w)
+        lk = torch.empty((sc.K, E, N_ACTIONS), device="cuda")
+        a, p = actors.act_env(env, env.out["mask"], True, seed=5, counter=9, logits_out=lk)
+        out[w] = (a.clone(), p.clone(), lk)
+    for x, y in zip(out["4"], out["16"]):
+        assert torch.equal(x, y)
+    env.close()

@@ -7,6 +7,7 @@ timeout -k 10 120 python tools/patch_probe.py 65536 16 grid64_n8 stamps > $O/pro
 timeout -k 10 120 python tools/patch_probe.py 65536 11 grid32 stamps > $O/probe_stamps_c5patch.log 2>&1 || exit 1
 timeout -k 10 300 python bench.py --config c2 --steps 20 --warmup 5 --no-cpu-baseline > $O/c2.log 2>&1 && python tools/bench_line.py $O/c2.log c2 &&
 timeout -k 10 300 python bench.py --config c2 --steps 200 --warmup 20 --no-cpu-baseline > $O/c2_200.log 2>&1 && python tools/bench_line.py $O/c2_200.log c2_200 &&
+GW_ACT_WAVES=16 timeout -k 10 300 python bench.py --config c2 --steps 200 --warmup 20 --no-cpu-baseline > $O/c2_200_w16.log 2>&1 && python tools/bench_line.py $O/c2_200_w16.log c2_200_w16 &&
 timeout -k 10 300 python bench.py --config c2env --steps 200 --warmup 20 --no-cpu-baseline > $O/c2env.log 2>&1 && python tools/bench_line.py $O/c2env.log c2env &&
 timeout -k 10 300 python bench.py --config c5patch --steps 20 --warmup 5 --no-cpu-baseline > $O/c5patch.log 2>&1 && python tools/bench_line.py $O/c5patch.log c5patch &&
 timeout -k 10 300 python bench.py --config c5 --steps 20 --warmup 5 --no-cpu-baseline > $O/c5.log 2>&1 && python tools/bench_line.py $O/c5.log c5
