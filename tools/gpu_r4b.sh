@@ -20,3 +20,5 @@ for spec in "0 first" "48 first" "64 first" "96 first" "64 strided" "0 first" "4
   python tools/bench_line.py $O/c3_split_$1_$2.log "split $1 $2" | head -1
 done
 unset GW_CU_SPLIT GW_CU_PATTERN
+echo "== 2-rank gloo C5 rehearsal (one GPU): packed return gather bytes per rank per step"
+MARLNAV_DIST_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 --config c5 --steps 20 --warmup 5 --no-cpu-baseline > $O/c5_gloo2.log 2>&1 && python tools/bench_line.py $O/c5_gloo2.log c5_gloo2
