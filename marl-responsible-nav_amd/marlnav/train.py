@@ -148,6 +148,12 @@ class MADDPGTrainer:
         if self.distributed:
             dist.barrier()
 
+    def load_wo_memory(self, path: str, filename: str):
+        """The networks and optimizers only (in place: a captured update graph stays valid; every
+        rank reads rank 0's file, the replicas are identical)."""
+        import os
+        self.m.load(os.path.join(path, filename))
+
     def load_checkpoint(self, path: str, filename: str):
         import os
         from safetensors.torch import load_file

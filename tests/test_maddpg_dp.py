@@ -216,3 +216,10 @@ def test_learn_schedule_identical_on_uneven_shards_cpu():
     # the rule over 9 global envs: learn_step 10 > 9 -> one learn every 10 // 9 = 1 step, once the
     # smallest shard's ring holds a batch of 16 (4 envs x 4 steps)
     assert s0[:3] == [0, 0, 0] and s0[3] == 1
+
+
+def test_trainer_checkpoint_api():
+    """MADDPGAgent's checkpoint API (maddpg/agent.py:255-281) is all there on the trainer."""
+    from marlnav.train import MADDPGTrainer
+    for name in ("save_checkpoint", "load_checkpoint", "load_wo_memory"):
+        assert callable(getattr(MADDPGTrainer, name, None)), name
