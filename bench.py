@@ -256,6 +256,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--updates-per-step", type=int, default=0,
                     help="c5 only: MADDPG updates (batch 128, one HIP-graph replay each) per env step")
+    ap.add_argument("--dense-learn", action="store_true",
+                    help="with --updates-per-step: sample the dense obs slots (waiting for the obs writer) "
+                         "instead of the descriptor ring (A/B)")
     ap.add_argument("--profile-steps", type=int, default=64,
                     help="after the timed region, time this many more steps' kernels with HIP events "
                          "carried by their launches (the live roofline; 0 = none)")
@@ -435,13 +438,14 @@ def main():
         ro = Rollout(env, actors, replay_slots=slots, training=True, seed=42,
                      fused=False if (args.cnn_torch or args.patch_torch) else None,
                      obs_async=obs_mode, fear_async=bool(obs_mode) and args.fear_async, gather=gather,
-                     patch=cfg.get("patch", 0))
+                     patch=cfg.get("patch", 0),
+                     desc_ring=bool(args.updates_per_step) and not cfg.get("patch") and not args.dense_learn)
         ro.reset()
 
         def one_step(i):  # noqa: F811
             r = ro.step()  # the return gather inside is the per-step exchange across ranks
             if args.updates_per_step and learner is not None and ro.replay.t >= 2:
-                ro.fence()  # sampling reads the ring's obs slots
+                ro.learn_fence()  # sampling reads the ring's descriptor (or obs) slots
                 if learner._graph is None:
                     learner.capture(ro.replay)
                 for _ in range(args.updates_per_step):

@@ -219,6 +219,11 @@ typedef struct gw_obs_source {
 } gw_obs_source;
 gw_status gw_obs_view(void *env, gw_obs_source *out);
 
+/* Copy the descriptors of the last gw_reset / gw_step ([E][12] u32, as gw_obs_view's desc) to
+ * dst, enqueued on stream after that step (a replay ring of descriptors: gw_replay_gather_desc,
+ * include/rollout_ops.h). */
+gw_status gw_obs_desc_copy(void *env, uint32_t *dst, void *stream);
+
 /* Egocentric local patches of the env's last observation (an opt-in input format; the
  * reference observes the whole grid, ma_customenv.py:303-322): for every env and RL agent k the
  * P x P window of that agent's obs centred on its own cell (rows / cols -P/2 .. P-1-P/2), cells

@@ -83,6 +83,20 @@ gw_status gw_replay_gather(const void *obs, const void *final_obs, int32_t obs_b
                            int64_t B, float *state, float *next_state, float *probs_out, double *reward_out,
                            uint8_t *term_out, int64_t *tr_out, float *x_out, float *xn_out, void *stream);
 
+/* gw_replay_gather with the obs rows expanded from a ring of obs descriptors instead of read
+ * from the dense obs / final_obs slots (the learner then never waits for the obs writer of the
+ * step it follows; the rows are bit for bit the ones the obs writer put in the ring).
+ * desc [S][E][12] u32: slot j holds the descriptors of the step whose obs went to obs slot j
+ * (gw_obs_desc_copy after that step, into slot j); the terminal obs of transition slot tr
+ * comes from the terminal half of descriptor slot tr + 1.  src: gw_obs_view of the env
+ * (base map, apple cells, N, K, H, W, variant, E; its desc pointer is not used).  Every other
+ * argument and output as gw_replay_gather (f32 rows; K = src->K, HW = src->H * src->W). */
+gw_status gw_replay_gather_desc(const gw_obs_source *src, const uint32_t *desc, const float *probs,
+                                const double *reward, const uint8_t *term, const uint8_t *done, const int64_t *t_dev,
+                                const float *u, const int64_t *env, int64_t S, int64_t B, float *state,
+                                float *next_state, float *probs_out, double *reward_out, uint8_t *term_out,
+                                int64_t *tr_out, float *x_out, float *xn_out, void *stream);
+
 /* One evaluation step's totals (customeval.py:70-133 over E episodes at once; marlnav/evaluate.py):
  * for every env e with active[e]:  counts[0] += crashes[e];  counts[1] += apples[e];
  * counts[2] += 1;  *fear_total += sum_k fear[e, k];  then active[e] = 0 if done[e].

@@ -3423,6 +3423,16 @@ gw_status gw_obs_patch(void *handle, int32_t P, float *patch, float *final_patch
     return GW_OK;
 }
 
+gw_status gw_obs_desc_copy(void *handle, uint32_t *dst, void *stream) {
+    Env *env = static_cast<Env *>(handle);
+    if (!env || !dst) return fail(GW_ERR_ARG, "null argument");
+    // the world update that wrote env->desc is ordered before the caller's later work on its
+    // stream on every path (the pipelined ones join it); a later step writes the other buffer
+    HIP_TRY(hipMemcpyAsync(dst, env->desc, sizeof(uint32_t) * gw::NDESC * (size_t)env->E, hipMemcpyDeviceToDevice,
+                           static_cast<hipStream_t>(stream)));
+    return GW_OK;
+}
+
 gw_status gw_obs_view(void *handle, gw_obs_source *out) {
     Env *env = static_cast<Env *>(handle);
     if (!env || !out) return fail(GW_ERR_ARG, "null argument");

@@ -199,6 +199,117 @@ __global__ void __launch_bounds__(256) replay_gather_kernel(
     if (k == 0 && threadIdx.x == 128 && tr_out) tr_out[b] = tr;
 }
 
+// ---- replay-ring sample from the descriptor ring: the same rows, expanded from 48-byte obs
+// descriptors instead of read from the dense obs slots (so the learner never waits for the obs
+// writer of the step it follows).  The cell values restate the obs writer (gridenv.hip obs_block;
+// ma_customenv.py:197-209 reset encoding, :303-322 step encoding): map 0 / -1, own apple
+// +9 first, then agent n's cell (a later patch overrides an earlier one) ----
+constexpr int DESC_WORDS = 12;  // gridenv.hip NDESC
+constexpr uint32_t DF_RESET = 1u;
+
+__device__ __forceinline__ float desc_agent_value(bool reset, int n, int k, bool on_apple, int variant) {
+    if (reset) return on_apple ? 9.5f : 0.5f;
+    if (on_apple) return (float)(n + 1 + 9);
+    if (variant == 1) return (float)(n + 1);
+    int v = n + 1;
+    if (v >= 1 && v <= 4 && v != k + 1) v = 5;
+    if (v == k + 1) v = 1;
+    return (float)v;
+}
+
+struct DescSrc {
+    const float *base;
+    int apples[GW_MAX_AGENTS];
+    int N, K, HW, variant;
+    int64_t E;
+};
+
+// patches of (descriptor d, agent k): which 0 = the obs, 1 = the terminal obs (words 8-11)
+__device__ __forceinline__ int desc_patches(const DescSrc &q, const uint32_t *d, int which, int k, int *pc,
+                                            float *pv) {
+    const uint32_t f = d[4];
+    const bool reset = which == 0 && (f & DF_RESET);
+    const uint32_t apples = which == 0 ? (f >> 8) & 0xFFu : (f >> 16) & 0xFFu;
+    const uint32_t *pw = d + (which == 0 ? 0 : 8);
+    const int ac = ((apples >> k) & 1u) ? q.apples[k] : -1;
+    int np = 0;
+    if (ac >= 0) {
+        float av = q.base[ac] + 9.0f;
+        if (!reset && av == (float)(k + 1)) av = 1.0f;
+        pc[np] = ac;
+        pv[np] = av;
+        ++np;
+    }
+    for (int n = 0; n < q.N; ++n) {
+        const int c = (int)((pw[n >> 1] >> (16 * (n & 1))) & 0xFFFFu);
+        pc[np] = c;
+        pv[np] = desc_agent_value(reset, n, k, c == ac, q.variant);
+        ++np;
+    }
+    return np;
+}
+
+__global__ void __launch_bounds__(256) replay_gather_desc_kernel(
+    DescSrc q, const uint32_t *__restrict__ desc, const float *__restrict__ probs, const double *__restrict__ reward,
+    const uint8_t *__restrict__ term, const uint8_t *__restrict__ done, const int64_t *__restrict__ t_dev,
+    const float *__restrict__ u, const int64_t *__restrict__ env, int64_t S, int64_t B, float *__restrict__ state,
+    float *__restrict__ next_state, float *__restrict__ probs_out, double *__restrict__ reward_out,
+    uint8_t *__restrict__ term_out, int64_t *__restrict__ tr_out, float *__restrict__ x_out,
+    float *__restrict__ xn_out) {
+    __shared__ int s_pc[2][GW_MAX_AGENTS + 1];
+    __shared__ float s_pv[2][GW_MAX_AGENTS + 1];
+    __shared__ int s_np[2];
+    const int64_t b = blockIdx.x;
+    const int k = blockIdx.y, K = q.K;
+    const int64_t E = q.E, HW = q.HW;
+    const int64_t t = t_dev[0];
+    const int64_t n = t < 1 ? 1 : (t > S - 1 ? S - 1 : t);
+    int64_t step = (int64_t)(u[b] * (float)n);  // as replay_gather_kernel (torch's draw)
+    if (step > n - 1) step = n - 1;
+    int64_t tr = (t - 1 - step) % S;
+    if (tr < 0) tr += S;
+    const int64_t nx = (tr + 1) % S;
+    const int64_t e = env[b];
+    const bool dn = done[tr * E + e] != 0;
+    // obs slot j of the ring was written from descriptor slot j; the terminal obs of the
+    // transition in slot tr (its final_obs slot) from the terminal half of descriptor slot tr + 1
+    if (threadIdx.x < 2) {
+        const int w = threadIdx.x;
+        const uint32_t *d = desc + ((w == 0 ? tr : nx) * E + e) * DESC_WORDS;
+        s_np[w] = desc_patches(q, d, w == 0 ? 0 : (dn ? 1 : 0), k, s_pc[w], s_pv[w]);
+    }
+    __syncthreads();
+    const int np0 = s_np[0], np1 = s_np[1];
+    float *so = state + (k * B + b) * HW;
+    float *no = next_state + (k * B + b) * HW;
+    const int64_t ldx = (int64_t)K * HW + (int64_t)K * 9;
+    float *xo = x_out ? x_out + b * ldx + (int64_t)k * HW : nullptr;
+    float *xno = xn_out ? xn_out + b * ldx + (int64_t)k * HW : nullptr;
+    for (int64_t i = threadIdx.x; i < HW; i += blockDim.x) {
+        const float m = q.base[i];
+        float sv = m, nv = m;
+        for (int j = 0; j < np0; ++j)
+            if (s_pc[0][j] == i) sv = s_pv[0][j];
+        for (int j = 0; j < np1; ++j)
+            if (s_pc[1][j] == i) nv = s_pv[1][j];
+        so[i] = sv;
+        no[i] = nv;
+        if (xo) xo[i] = sv;
+        if (xno) xno[i] = nv;
+    }
+    if (threadIdx.x < 9) {
+        const float pv = probs[((tr * K + k) * E + e) * 9 + threadIdx.x];
+        probs_out[(k * B + b) * 9 + threadIdx.x] = pv;
+        if (x_out) x_out[b * ldx + (int64_t)K * HW + k * 9 + threadIdx.x] = pv;
+    }
+    if (k == 0 && threadIdx.x >= 64 && threadIdx.x < 64 + K) {
+        const int j = threadIdx.x - 64;
+        reward_out[b * K + j] = reward[(tr * E + e) * K + j];
+        term_out[b * K + j] = term[(tr * E + e) * K + j];
+    }
+    if (k == 0 && threadIdx.x == 128 && tr_out) tr_out[b] = tr;
+}
+
 // ---- evaluation totals (customeval.py:70-133): one 1024-thread block, fixed-order sums ------------
 constexpr int EV_T = 1024;
 
@@ -562,6 +673,31 @@ gw_status gw_replay_gather(const void *obs, const void *final_obs, int32_t obs_b
                        static_cast<hipStream_t>(stream), obs, final_obs, (int)obs_bf16, probs, reward, term, done,
                        t_dev, u, env, S, (int)K, E, HW, B, state, next_state, probs_out, reward_out, term_out, tr_out,
                        x_out, xn_out);
+    return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
+}
+
+gw_status gw_replay_gather_desc(const gw_obs_source *src, const uint32_t *desc, const float *probs,
+                                const double *reward, const uint8_t *term, const uint8_t *done, const int64_t *t_dev,
+                                const float *u, const int64_t *env, int64_t S, int64_t B, float *state,
+                                float *next_state, float *probs_out, double *reward_out, uint8_t *term_out,
+                                int64_t *tr_out, float *x_out, float *xn_out, void *stream) {
+    if (!src || !src->base || !desc || !probs || !reward || !term || !done || !t_dev || !u || !env || !state ||
+        !next_state || !probs_out || !reward_out || !term_out || S < 2 || src->K <= 0 || src->K > GW_MAX_AGENTS ||
+        src->N < src->K || src->N > GW_MAX_AGENTS || src->E <= 0 || src->H <= 0 || src->W <= 0 || B < 0 ||
+        B > 0x7fffffff)
+        return GW_ERR_ARG;
+    if (B == 0) return GW_OK;
+    DescSrc q;
+    q.base = src->base;
+    for (int k = 0; k < GW_MAX_AGENTS; ++k) q.apples[k] = src->apples[k];
+    q.N = src->N;
+    q.K = src->K;
+    q.HW = src->H * src->W;
+    q.variant = src->variant;
+    q.E = src->E;
+    hipLaunchKernelGGL(replay_gather_desc_kernel, dim3((unsigned)B, (unsigned)q.K), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), q, desc, probs, reward, term, done, t_dev, u, env, S, B,
+                       state, next_state, probs_out, reward_out, term_out, tr_out, x_out, xn_out);
     return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
 }
 

@@ -177,7 +177,7 @@ EXPORTS = ["gw_create", "gw_reset", "gw_step", "gw_state_view", "gw_copy_state",
            "gw_maddpg_workspace_floats", "gw_maddpg_critic_grads", "gw_maddpg_actor_grads",
            "gw_pipeline_state_bytes", "gw_pipeline_save", "gw_pipeline_load",
            "gw_gather_pack_scratch", "gw_gather_pack", "gw_gather_unpack_plan_cap", "gw_gather_unpack",
-           "gw_adam_soft_step"]
+           "gw_adam_soft_step", "gw_obs_desc_copy", "gw_replay_gather_desc"]
 
 
 class GwObsSource(C.Structure):
@@ -297,6 +297,10 @@ def _declare(L):
     L.gw_replay_gather.argtypes = [p, p, C.c_int32] + [p] * 7 + [C.c_int64, C.c_int32, C.c_int64, C.c_int64,
                                                                   C.c_int64] + [p] * 9
     L.gw_replay_gather.restype = C.c_int
+    L.gw_replay_gather_desc.argtypes = [C.POINTER(GwObsSource)] + [p] * 8 + [C.c_int64, C.c_int64] + [p] * 9
+    L.gw_replay_gather_desc.restype = C.c_int
+    L.gw_obs_desc_copy.argtypes = [p, p, p]
+    L.gw_obs_desc_copy.restype = C.c_int
     L.gw_obs_view.argtypes = [p, C.POINTER(GwObsSource)]
     L.gw_obs_view.restype = C.c_int
     L.gw_set_last_error.argtypes = [C.c_char_p]

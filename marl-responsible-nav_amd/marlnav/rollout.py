@@ -19,6 +19,7 @@ The statistics totals are all-reduced across ranks only when read (``totals()``)
 """
 from __future__ import annotations
 
+import ctypes as C
 import os
 
 import torch
@@ -33,9 +34,13 @@ from .vec_env import VecGridEnv
 class ReplayRing:
     """S steps of E transitions each, in HBM.  obs slots are written by the env directly."""
 
-    def __init__(self, env: VecGridEnv, slots: int, patch: int = 0):
+    def __init__(self, env: VecGridEnv, slots: int, patch: int = 0, desc: bool = False):
         """patch > 0: the ring holds the agents' egocentric patch x patch observations
-        (VecGridEnv.obs_patch) instead of the full grids."""
+        (VecGridEnv.obs_patch) instead of the full grids.
+        desc (full-grid obs on the GPU): also keep each step's 48-byte obs descriptors per slot
+        ([S][E][12] u32, 3 MB per slot at 65,536 envs); ``sample`` then expands the sampled rows
+        from them (gw_replay_gather_desc, the same values bit for bit), so a learner that follows a
+        step never waits for that step's obs writer.  Rollout fills it (``Rollout(desc_ring=True)``)."""
         self.S = max(2, int(slots))
         K, E, H, W, dev = env.K, env.E, env.H, env.W, env.device
         if patch:
@@ -50,6 +55,12 @@ class ReplayRing:
         self.t = 0          # transitions stored = steps taken
         self.t_dev = torch.zeros((), dtype=torch.int64, device=dev)  # same, on device (graph-safe sampling)
         self.E, self.K = E, K
+        self.desc = None
+        self.desc_ok = False  # every descriptor slot matches its obs slot (set by Rollout.reset)
+        if desc and not patch and dev.type == "cuda":
+            self.desc = torch.zeros((self.S, E, 12), dtype=torch.int32, device=dev)
+            self._src = _lib.GwObsSource()
+            _lib.check(_lib.load().gw_obs_view(env.handle, C.byref(self._src)), "gw_obs_view")
 
     def __len__(self):
         return min(self.t, self.S - 1) * self.E
@@ -72,6 +83,7 @@ class ReplayRing:
             getattr(self, n).copy_(sd[n])
         self.t = int(sd["t"][0])
         self.t_dev.copy_(sd["t_dev"].reshape(()))
+        self.desc_ok = False  # the descriptors are not saved: dense rows until the next reset
 
     @torch.no_grad()
     def sample(self, batch: int, generator: torch.Generator | None = None, return_idx: bool = False,
@@ -85,7 +97,7 @@ class ReplayRing:
             raise RuntimeError("empty replay ring")
         dev = self.obs.device
         if dev.type == "cuda":
-            return self._sample_hip(batch, generator, return_idx, critic_in, extra_uniform)
+            return self._sample_hip(batch, generator, return_idx, critic_in, extra_uniform, self.use_desc)
         n = torch.clamp(self.t_dev, min=1, max=self.S - 1)
         step = torch.minimum((torch.rand((batch,), device=dev, generator=generator) * n).long(), n - 1)
         env = torch.randint(0, self.E, (batch,), device=dev, generator=generator)
@@ -98,7 +110,12 @@ class ReplayRing:
         out = (state, self.probs[tr, :, env].permute(1, 0, 2), self.reward[tr, env], next_state, self.term[tr, env])
         return out + ((tr, env),) if return_idx else out
 
-    def _sample_hip(self, batch, generator, return_idx, critic_in=False, extra=0):
+    @property
+    def use_desc(self) -> bool:
+        """Whether ``sample`` expands the rows from the descriptor ring (no obs-writer wait)."""
+        return self.desc is not None and self.desc_ok
+
+    def _sample_hip(self, batch, generator, return_idx, critic_in=False, extra=0, use_desc=False):
         """sample() on the GPU: the same draws (torch.rand, then torch.randint), then the index
         arithmetic and every gather in ONE launch (gw_replay_gather, include/rollout_ops.h).
         extra > 0: that many more uniforms from the same torch.rand launch, returned last (the
@@ -118,13 +135,21 @@ class ReplayRing:
         if critic_in:
             x = torch.empty((batch, K * HW + K * 9), device=dev, dtype=torch.float32)
             xn = torch.empty_like(x)
-        _lib.check(_lib.load().gw_replay_gather(
-            self.obs.data_ptr(), self.final_obs.data_ptr(), int(self.obs.dtype == torch.bfloat16),
-            self.probs.data_ptr(), self.reward.data_ptr(), self.term.data_ptr(), self.done.data_ptr(),
-            self.t_dev.data_ptr(), u.data_ptr(), env.data_ptr(), self.S, K, self.E, HW, batch, state.data_ptr(),
-            next_state.data_ptr(), probs.data_ptr(), reward.data_ptr(), term.data_ptr(),
-            tr.data_ptr() if return_idx else None, x.data_ptr() if critic_in else None,
-            xn.data_ptr() if critic_in else None, torch.cuda.current_stream(dev).cuda_stream), "gw_replay_gather")
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        outs = (state.data_ptr(), next_state.data_ptr(), probs.data_ptr(), reward.data_ptr(), term.data_ptr(),
+                tr.data_ptr() if return_idx else None, x.data_ptr() if critic_in else None,
+                xn.data_ptr() if critic_in else None, stream)
+        if use_desc:
+            _lib.check(_lib.load().gw_replay_gather_desc(
+                C.byref(self._src), self.desc.data_ptr(), self.probs.data_ptr(), self.reward.data_ptr(),
+                self.term.data_ptr(), self.done.data_ptr(), self.t_dev.data_ptr(), u.data_ptr(), env.data_ptr(),
+                self.S, batch, *outs), "gw_replay_gather_desc")
+        else:
+            _lib.check(_lib.load().gw_replay_gather(
+                self.obs.data_ptr(), self.final_obs.data_ptr(), int(self.obs.dtype == torch.bfloat16),
+                self.probs.data_ptr(), self.reward.data_ptr(), self.term.data_ptr(), self.done.data_ptr(),
+                self.t_dev.data_ptr(), u.data_ptr(), env.data_ptr(), self.S, K, self.E, HW, batch, *outs),
+                "gw_replay_gather")
         out = (state, probs, reward, next_state, term)
         if return_idx:
             out = out + ((tr, env),)
@@ -137,7 +162,7 @@ class Rollout:
     def __init__(self, env: VecGridEnv, actors: MultiAgentActors | None = None, replay_slots: int = 0,
                  training: bool = True, group=None, seed: int = 0, fused: bool | None = None,
                  obs_async: bool | str = False, fear_async: bool = False, gather=None, patch: int = 0,
-                 patch_async: bool | None = None):
+                 patch_async: bool | None = None, desc_ring: bool = False):
         """fused: get_action as the one-kernel gw_actor_act over the env's obs descriptors
         (default when the actors are the f32 128-128 MLP), else the PyTorch forward over the
         dense obs with torch's Gumbel noise.
@@ -155,7 +180,10 @@ class Rollout:
         with obs=False.
         patch_async (default: on for the CNN head, off for the MLP; GW_PATCH_ASYNC=0/1 overrides):
         with a ring and the fused actor, the window writer runs on a side stream beside the next
-        step's actor (``fence()`` orders the ring slots)."""
+        step's actor (``fence()`` orders the ring slots).
+        desc_ring (full-grid obs, GPU): the ring also keeps every step's obs descriptors and the
+        learner samples from them (``ReplayRing(desc=True)``; ``learn_fence()`` then skips the
+        obs-writer wait, so the writer of step t overlaps the updates that follow it)."""
         self.env = env
         self.actors = actors
         self.fused = (actors is not None and actors.fusable(env, patch)) if fused is None else bool(fused)
@@ -172,7 +200,7 @@ class Rollout:
         self.patch = int(patch)
         if self.patch and actors is not None and (actors.H, actors.W) != (self.patch, self.patch):
             raise ValueError("Rollout(patch=P) needs actors built for a P x P input")
-        self.replay = ReplayRing(env, replay_slots, patch=self.patch) if replay_slots else None
+        self.replay = ReplayRing(env, replay_slots, patch=self.patch, desc=desc_ring) if replay_slots else None
         self._patch = None  # the current obs' patches when there is no ring
         # patch windows into the ring on a side stream: the fused actor of the next step reads the
         # descriptors, not the windows, so the window writer of step t overlaps actor t+1; the
@@ -242,6 +270,23 @@ class Rollout:
         self._flush()
         self.env.obs_fence()
 
+    def learn_fence(self):
+        """Order what ``ReplayRing.sample`` reads before later work on the current stream: with
+        the descriptor ring that is the rewards / terminations (FeAR-owned with the unjoined
+        FeAR) and the descriptor slots (stream-ordered), not the obs writer; else ``fence()``."""
+        if self.replay is not None and self.replay.use_desc:
+            self._patch_join()
+            self._flush()
+        else:
+            self.fence()
+
+    def _desc_copy(self, slot: int):
+        rp = self.replay
+        if rp is not None and rp.desc is not None:
+            _lib.check(self.env.lib.gw_obs_desc_copy(self.env.handle, rp.desc[slot].data_ptr(),
+                                                      torch.cuda.current_stream(self.env.device).cuda_stream),
+                       "gw_obs_desc_copy")
+
     def reset(self):
         # the previous step's statistics (and its ring tick) are reduced before the ring's step
         # count restarts, so t_dev never runs ahead of the transitions written
@@ -253,6 +298,8 @@ class Rollout:
                 self.env.obs_patch(self.patch, out=self.replay.obs[0])
             else:
                 self.replay.obs[0].copy_(obs)
+                self._desc_copy(0)
+                self.replay.desc_ok = self.replay.desc is not None
             self.replay.t = 0
             self.replay.t_dev.zero_()
             self._noise_base = self._calls
@@ -280,6 +327,7 @@ class Rollout:
         if t > 0:
             rp.final_obs[prev].copy_(rp.obs[cur])
             rp.done[prev].fill_(1)
+        rp.desc_ok = False  # that terminal obs has no descriptor: dense rows until the next reset
         obs, _ = self.env.reset()
         if self.patch:
             self.env.obs_patch(self.patch, out=rp.obs[cur])
@@ -345,6 +393,8 @@ class Rollout:
                 self._pev_live = True
             elif self.patch:  # the step's obs / terminal obs as patches, straight into the ring
                 env.obs_patch(self.patch, final=True, out=rp.obs[nxt], final_out=rp.final_obs[cur])
+            elif rp.desc is not None:
+                self._desc_copy(nxt)  # the descriptors of obs slot nxt (and of final-obs slot cur)
             if probs is not None and probs.data_ptr() != rp.probs[cur].data_ptr():
                 rp.probs[cur].copy_(probs)
             rp.t = self.t + 1

@@ -69,8 +69,12 @@ class MADDPGTrainer:
         slots = max(2, -(-memory_size // self.global_envs) + 1)
         # obs writes pipelined with the next step when the actor is the fused op (it never reads
         # the dense obs), launched behind it ("lazy"); the ring is fenced before every learn
+        # the learner samples the ring's rows from its obs descriptors when the actor is fused
+        # (Rollout(desc_ring)): an update never waits for the obs writer of the step before it
+        fusable = maddpg.actors.fusable(env)
         self.rollout = Rollout(env, maddpg.actors, replay_slots=slots, training=True, seed=seed,
-                               obs_async="lazy" if maddpg.actors.fusable(env) else False)
+                               obs_async="lazy" if fusable else False,
+                               desc_ring=fusable and env.device.type == "cuda")
         self.learning_delay = learning_delay
         self.updates_per_step = updates_per_step
         self.use_graph = graph and env.device.type == "cuda"
@@ -90,7 +94,7 @@ class MADDPGTrainer:
         self.rollout.reset()
 
     def _learn(self):
-        self.rollout.fence()  # the sampled transitions read the ring's obs slots
+        self.rollout.learn_fence()  # what the sampled transitions read (descriptor or obs slots)
         if self.use_graph:
             if self.m._graph is None:
                 self.m.capture(self.rollout.replay)
@@ -167,6 +171,7 @@ class MADDPGTrainer:
             # the fused actor's Gumbel-noise Philox counter continues where the saved run stopped
             # (restarting it at 0 would replay the original run's exploration noise)
             self.rollout.resume(calls=int(calls[0]) if calls is not None else None)
+            self.m._graph = None  # the ring's rows now come from its dense slots: capture again
         with open(os.path.join(path, "steps.txt")) as f:
             self.total_steps = int(f.read()) // self.global_envs * self.env.E
 
