@@ -379,11 +379,12 @@ class ReturnGather:
         import ctypes as C
         from . import _lib
         lib = _lib.load()
-        need = int(lib.gw_return_compact_scratch(self._fill, 1, self.emax))
+        world = self._recv.shape[1]  # 1 here; the kernel takes any rank count (its tests use several)
+        need = int(lib.gw_return_compact_scratch(self._fill, world, self.emax))
         if getattr(self, "_scratch", None) is None or self._scratch.numel() < need:
             self._scratch = torch.zeros(max(need, 2 + (self.window * self.emax + 4095) // 4096),
                                         dtype=torch.int32, device=self.device)
-        _lib.check(lib.gw_return_compact(self._recv.data_ptr(), self._fill, 1, self.emax, self.slot_bytes,
+        _lib.check(lib.gw_return_compact(self._recv.data_ptr(), self._fill, world, self.emax, self.slot_bytes,
                                          self.scores.data_ptr(), self.capacity, self.n_completed.data_ptr(),
                                          self._scratch.data_ptr(),
                                          C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)),

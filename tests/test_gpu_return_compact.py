@@ -25,6 +25,7 @@ def _hip_and_torch(world, emax, counts, steps, capacity, density, seed, windows=
     for dev in ("cuda", "cpu"):
         rg = ReturnGather.__new__(ReturnGather)
         rg.world, rg.emax, rg.G = world, emax, G
+        rg.distributed = False  # the full-slot format (one rank's path), fed `world` ranks' slots
         rg.slot_bytes = 8 * emax + (-(-emax // 8)) * 8
         rg.window, rg.capacity, rg.device = steps, capacity, torch.device(dev)
         rg._recv = torch.zeros((steps, world, rg.slot_bytes), dtype=torch.uint8, device=dev)

@@ -1,5 +1,5 @@
 O=gpurun_out/r4b; mkdir -p $O
-timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_obs_patch.py tests/test_gpu_checkpoint_eval.py tests/test_gpu_rollout_graph.py tests/test_gpu_patch_actor.py tests/test_gpu_patch_cnn.py tests/test_gpu_cnn_actor.py tests/test_actor_ops.py tests/test_gpu_rollout.py tests/test_gpu_async_obs.py tests/test_gpu_dist.py tests/test_gpu_return_compact.py tests/test_gpu_gather_pack.py tests/test_maddpg_dp.py tests/test_maddpg_fused.py tests/test_maddpg.py > $O/pytest.log 2>&1; s=$?; tail -3 $O/pytest.log; [ $s = 0 ] || exit $s
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_return_compact.py tests/test_gpu_replay_desc.py tests/test_gpu_obs_patch.py tests/test_gpu_checkpoint_eval.py tests/test_gpu_rollout_graph.py tests/test_gpu_patch_actor.py tests/test_gpu_patch_cnn.py tests/test_gpu_cnn_actor.py tests/test_actor_ops.py tests/test_gpu_rollout.py tests/test_gpu_async_obs.py tests/test_gpu_dist.py tests/test_gpu_return_compact.py tests/test_gpu_gather_pack.py tests/test_maddpg_dp.py tests/test_maddpg_fused.py tests/test_maddpg.py > $O/pytest.log 2>&1; s=$?; tail -3 $O/pytest.log; [ $s = 0 ] || exit $s
 timeout -k 10 120 python tools/bench_learn.py 128 > $O/learn.log 2>&1 && tail -2 $O/learn.log &&
 (cd /tmp && export TMPDIR=/tmp && timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$O/learnprof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/bench_learn.py 128 > $GRAFT_REPO_ROOT/$O/learnprof.log 2>&1) || exit 1
 for m in 0 3; do GW_PATCH_MODE=$m timeout -k 10 120 python tools/patch_probe.py > $O/probe_m$m.log 2>&1 || exit 1; done
