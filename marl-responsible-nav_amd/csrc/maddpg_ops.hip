@@ -229,10 +229,27 @@ __device__ __forceinline__ void l1_sum(const float *part, int nchunk, int K, int
     float acc[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[i] = 0.0f;
-    for (int c = 0; c < nchunk; ++c) {
-        const float *pp = part + (((int64_t)c * K + k) * B + r) * HID + 8 * g;
-        const float4 a = *reinterpret_cast<const float4 *>(pp);
-        const float4 b = *reinterpret_cast<const float4 *>(pp + 4);
+    // the partials of 8 chunks are loaded together, then added in chunk order (one L2 round
+    // trip per 8 chunks instead of per chunk: 33 chunks took ~8 us as a dependent chain)
+    const int64_t cstride = (int64_t)K * B * HID;
+    const float *p0 = part + ((int64_t)k * B + r) * HID + 8 * g;
+    int c = 0;
+    for (; c + 8 <= nchunk; c += 8) {
+        float4 a[8], b[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            a[j] = *reinterpret_cast<const float4 *>(p0 + (c + j) * cstride);
+            b[j] = *reinterpret_cast<const float4 *>(p0 + (c + j) * cstride + 4);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            acc[0] += a[j].x; acc[1] += a[j].y; acc[2] += a[j].z; acc[3] += a[j].w;
+            acc[4] += b[j].x; acc[5] += b[j].y; acc[6] += b[j].z; acc[7] += b[j].w;
+        }
+    }
+    for (; c < nchunk; ++c) {
+        const float4 a = *reinterpret_cast<const float4 *>(p0 + c * cstride);
+        const float4 b = *reinterpret_cast<const float4 *>(p0 + c * cstride + 4);
         acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
         acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
     }
@@ -318,11 +335,13 @@ __device__ __forceinline__ float critic_fwd(const Mlp &m, const float *part, int
     float z[8];
     l1_sum(part, nch, p.K, p.B, k, r, g, m.b1, z);
     const int Ds = p.K * p.D;
-    for (int a = 0; a < NA * p.K; ++a) {
+#pragma unroll 9
+    for (int a = 0; a < NA * p.K; ++a) {  // 9 rows' loads in flight together, fmas in row order
         const float av = act[a];
         const float *wr = m.w1 + (int64_t)(Ds + a) * HID + 8 * g;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) z[i] = fmaf(av, wr[i], z[i]);
+        const float4 w0 = *reinterpret_cast<const float4 *>(wr), w1 = *reinterpret_cast<const float4 *>(wr + 4);
+        z[0] = fmaf(av, w0.x, z[0]); z[1] = fmaf(av, w0.y, z[1]); z[2] = fmaf(av, w0.z, z[2]); z[3] = fmaf(av, w0.w, z[3]);
+        z[4] = fmaf(av, w1.x, z[4]); z[5] = fmaf(av, w1.y, z[5]); z[6] = fmaf(av, w1.z, z[6]); z[7] = fmaf(av, w1.w, z[7]);
     }
     ln_relu(z, m.lw1, m.lb1, g, f.xh1, f.y1, f.rs1);
     rows_gemv(f.y1, rl, g, m.w2, false, s_in, s_out, z);
