@@ -18,10 +18,14 @@ extern "C" {
  *   p -= lr / (1 - beta1^s) * (m / (sqrt(v) / sqrt(1 - beta2^s) + eps));   then step[0] = s.
  * step: int32 [2] device memory, [0] the steps taken, [1] zero (the launch's arrival counter: the
  * last block to finish advances step[0], so the step is ONE launch).
+ * advanced != 0: step[0] already counts this step (a preceding launch on the stream advanced it,
+ * e.g. gw_maddpg_critic_grads / gw_maddpg_actor_grads' adam_step): s = step[0], no arrival
+ * counter (its same-address atomics from every block cost ~30 us per launch on a 0.5 M-element
+ * buffer). 
  * The scalar hyper-parameters are doubles and the bias corrections are formed in double, as
  * torch forms them from Python floats, then rounded to float against the f32 tensors. */
 gw_status gw_adam_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int32_t *step,
-                       int64_t n, double lr, double beta1, double beta2, double eps, void *stream);
+                       int64_t n, double lr, double beta1, double beta2, double eps, int32_t advanced, void *stream);
 
 /* gw_adam_step on param[0, n), then in the same launch the soft target updates that end
  * MADDPG.learn: target[i] = tau * param[i] + (1 - tau) * target[i] with the stepped param, and
@@ -29,7 +33,7 @@ gw_status gw_adam_step(float *param, const float *grad, float *exp_avg, float *e
  * earlier; n2 = 0: none).  Same arithmetic as gw_adam_step followed by gw_soft_update2. */
 gw_status gw_adam_soft_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int32_t *step,
                             int64_t n, double lr, double beta1, double beta2, double eps, float *target, float tau,
-                            float *target2, const float *online2, int64_t n2, void *stream);
+                            float *target2, const float *online2, int64_t n2, int32_t advanced, void *stream);
 
 /* agilerl soft_update: target = tau * online + (1 - tau) * target on n elements. */
 gw_status gw_soft_update(float *target, const float *online, int64_t n, float tau, void *stream);
@@ -111,17 +115,21 @@ int64_t gw_maddpg_workspace_floats(int32_t K, int32_t B, int32_t D);
 
 /* a'_k = GumbelSoftmax(actor_target_k(s'_k)) into x_next's slots; y = r + (1 - d) gamma
  * critic_target_k(x_next); critic_grad = d/dtheta of mean_b (critic_k(x) - y)^2 per agent;
- * loss [K] the MSE values. */
+ * loss [K] the MSE values.  adam_step (may be NULL): the critic optimizer's step count
+ * (gw_adam_step's int32 [2]), advanced by one in this call's last launch, so the Adam step that
+ * follows runs with advanced = 1. 
 gw_status gw_maddpg_critic_grads(const gw_mlp_actors *actor_target, const gw_mlp_actors *critic_target,
                                  const gw_mlp_actors *critic, const gw_mlp_actors *critic_grad,
-                                 const gw_maddpg_batch *batch, float gamma, float *ws, float *loss, void *stream);
+                                 const gw_maddpg_batch *batch, float gamma, float *ws, float *loss,
+                                 int32_t *adam_step, void *stream);
 
 /* probs_k = GumbelSoftmax(actor_k(s_k)) (probs [K][B][9], may be NULL); actor_grad = d/dtheta of
- * -mean_b critic_k(s, a with a_k := probs_k) per agent (the critic as given, i.e. after its Adam
+ * -mean_b critic_k(s, a with a_k := probs_k) per agent (adam_step: the actor optimizer's count,
+ * as gw_maddpg_critic_grads') (the critic as given, i.e. after its Adam
  * step; no critic gradients); loss [K]. */
 gw_status gw_maddpg_actor_grads(const gw_mlp_actors *actor, const gw_mlp_actors *critic,
                                 const gw_mlp_actors *actor_grad, const gw_maddpg_batch *batch, float *ws, float *loss,
-                                float *probs, void *stream);
+                                float *probs, int32_t *adam_step, void *stream);
 
 #ifdef __cplusplus
 }

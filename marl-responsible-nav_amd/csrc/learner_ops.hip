@@ -20,11 +20,13 @@ __global__ void __launch_bounds__(256) adam_kernel(float *__restrict__ p, const 
                                                    int32_t *__restrict__ step, int64_t n, double lr,
                                                    double beta1, double beta2, double eps, float *__restrict__ t1,
                                                    float *__restrict__ t2, const float *__restrict__ p2, int64_t n2,
-                                                   float tau) {
+                                                   float tau, int advanced) {
     // the scalars exactly as torch's single-tensor Adam forms them: in double on the host side
     // (Python floats), rounded to float where they meet the f32 tensors
-    const int32_t st = step[0];  // read by every block before the last one advances it (below)
-    const double s = (double)(st + 1);
+    // advanced: the count already includes this step (the caller's preceding launch advanced it);
+    // else read by every block before the last one advances it (below)
+    const int32_t st = step[0];
+    const double s = (double)(advanced ? st : st + 1);
     const float step_size = (float)(lr / (1.0 - pow(beta1, s)));
     const float bc2_sqrt = (float)sqrt(1.0 - pow(beta2, s));
     const float w1 = (float)(1.0 - beta1), b2 = (float)beta2, w2 = (float)(1.0 - beta2), e = (float)eps;
@@ -53,6 +55,9 @@ __global__ void __launch_bounds__(256) adam_kernel(float *__restrict__ p, const 
     // arrival: the loop above consumed it), and the kernel's end publishes the last block's
     // stores.  A device-scope fence per block writes back the XCD's L2 on gfx950 (~2,200 blocks
     // of this launch took 79 us instead of 9)
+    // (same-address atomics from ~2,200 blocks still serialise: ~36 us per launch, so the learner
+    // advances its counts in the gradient launch before the step instead: advanced = 1)
+    if (advanced) return;
     __syncthreads();
     if (threadIdx.x == 0 && atomicAdd(&step[1], 1) == (int32_t)gridDim.x - 1) {
         step[0] = st + 1;
@@ -349,23 +354,23 @@ unsigned grid_for(int64_t n) {
 extern "C" {
 
 gw_status gw_adam_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int32_t *step,
-                       int64_t n, double lr, double beta1, double beta2, double eps, void *stream) {
+                       int64_t n, double lr, double beta1, double beta2, double eps, int32_t advanced, void *stream) {
     if (!param || !grad || !exp_avg || !exp_avg_sq || !step || n < 0) return GW_ERR_ARG;
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, s, param, grad, exp_avg, exp_avg_sq, step, n,
-                       lr, beta1, beta2, eps, nullptr, nullptr, nullptr, (int64_t)0, 0.0f);
+                       lr, beta1, beta2, eps, nullptr, nullptr, nullptr, (int64_t)0, 0.0f, (int)(advanced != 0));
     return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
 }
 
 gw_status gw_adam_soft_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int32_t *step,
                             int64_t n, double lr, double beta1, double beta2, double eps, float *target, float tau,
-                            float *target2, const float *online2, int64_t n2, void *stream) {
+                            float *target2, const float *online2, int64_t n2, int32_t advanced, void *stream) {
     if (!param || !grad || !exp_avg || !exp_avg_sq || !step || n < 0 || !target || n2 < 0 ||
         (n2 > 0 && (!target2 || !online2)))
         return GW_ERR_ARG;
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n + n2)), dim3(256), 0, s, param, grad, exp_avg, exp_avg_sq, step, n,
-                       lr, beta1, beta2, eps, target, target2, online2, n2, tau);
+                       lr, beta1, beta2, eps, target, target2, online2, n2, tau, (int)(advanced != 0));
     return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
 }
 

@@ -543,11 +543,13 @@ struct GradParams {
     int col0, in_dim, out, K, B, nw1, mode;  // mode 0: critic (loss mean (q - y)^2), 1: actor (-mean q)
     Saved sv;
     float *loss;           // [K]
+    int32_t *adam_step;    // the following Adam step's count, advanced here (may be null)
 };
 
 constexpr int GRG = 16;  // row groups of the vector / W3 blocks (rows rg, rg + 16, ...)
 
 __global__ void __launch_bounds__(256) grads_kernel(GradParams p) {
+    if (p.adam_step && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) p.adam_step[0] += 1;
     // W blocks: s_in + s_dz; vector block: [16][6][128]; W3 block: [16][128][9] + [16][10]
     __shared__ __attribute__((aligned(16))) float smem[GRG * HID * NA + GRG * (NA + 1) > RB * (TILE_R + 4) + TILE_R * HID
                                                         ? GRG * HID * NA + GRG * (NA + 1)
@@ -789,7 +791,8 @@ int64_t gw_maddpg_workspace_floats(int32_t K, int32_t B, int32_t D) { return ws_
 
 gw_status gw_maddpg_critic_grads(const gw_mlp_actors *actor_target, const gw_mlp_actors *critic_target,
                                  const gw_mlp_actors *critic, const gw_mlp_actors *critic_grad,
-                                 const gw_maddpg_batch *batch, float gamma, float *ws, float *loss, void *stream) {
+                                 const gw_maddpg_batch *batch, float gamma, float *ws, float *loss,
+                                 int32_t *adam_step, void *stream) {
     gw_status st = check(batch, "gw_maddpg_critic_grads");
     if (st != GW_OK) return st;
     if (!actor_target || !critic_target || !critic || !critic_grad || !ws || !batch->reward || !batch->done)
@@ -847,6 +850,7 @@ gw_status gw_maddpg_critic_grads(const gw_mlp_actors *actor_target, const gw_mlp
     gp.mode = 0;
     gp.sv = w.sv;
     gp.loss = loss;
+    gp.adam_step = adam_step;
     hipLaunchKernelGGL(grads_kernel, dim3(gp.nw1 + HID / RB + 2, K), dim3(256), 0, s, gp);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(GW_ERR_HIP, who + ": " + hipGetErrorString(e));
@@ -855,7 +859,7 @@ gw_status gw_maddpg_critic_grads(const gw_mlp_actors *actor_target, const gw_mlp
 
 gw_status gw_maddpg_actor_grads(const gw_mlp_actors *actor, const gw_mlp_actors *critic,
                                 const gw_mlp_actors *actor_grad, const gw_maddpg_batch *batch, float *ws, float *loss,
-                                float *probs, void *stream) {
+                                float *probs, int32_t *adam_step, void *stream) {
     gw_status st = check(batch, "gw_maddpg_actor_grads");
     if (st != GW_OK) return st;
     if (!actor || !critic || !actor_grad || !ws) return fail(GW_ERR_ARG, "gw_maddpg_actor_grads: null argument");
@@ -905,6 +909,7 @@ gw_status gw_maddpg_actor_grads(const gw_mlp_actors *actor, const gw_mlp_actors 
     gp.mode = 1;
     gp.sv = w.sv;
     gp.loss = loss;
+    gp.adam_step = adam_step;
     hipLaunchKernelGGL(grads_kernel, dim3(gp.nw1 + HID / RB + 2, K), dim3(256), 0, s, gp);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(GW_ERR_HIP, who + ": " + hipGetErrorString(e));

@@ -211,9 +211,9 @@ def _declare(L):
     p = C.c_void_p
     L.gw_maddpg_workspace_floats.argtypes = [C.c_int32, C.c_int32, C.c_int32]
     L.gw_maddpg_workspace_floats.restype = C.c_int64
-    L.gw_maddpg_critic_grads.argtypes = [C.POINTER(GwMlpActors)] * 4 + [C.POINTER(GwMaddpgBatch), C.c_float, p, p, p]
+    L.gw_maddpg_critic_grads.argtypes = [C.POINTER(GwMlpActors)] * 4 + [C.POINTER(GwMaddpgBatch), C.c_float, p, p, p, p]
     L.gw_maddpg_critic_grads.restype = C.c_int
-    L.gw_maddpg_actor_grads.argtypes = [C.POINTER(GwMlpActors)] * 3 + [C.POINTER(GwMaddpgBatch), p, p, p, p]
+    L.gw_maddpg_actor_grads.argtypes = [C.POINTER(GwMlpActors)] * 3 + [C.POINTER(GwMaddpgBatch), p, p, p, p, p]
     L.gw_maddpg_actor_grads.restype = C.c_int
     L.gw_cnn_workspace_floats.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_int64]
     L.gw_cnn_workspace_floats.restype = C.c_int64
@@ -267,10 +267,10 @@ def _declare(L):
     L.gw_last_error.restype = C.c_char_p
     L.gw_fear_matrix.argtypes = [p, C.c_int64] + [p] * 11
     L.gw_fear_matrix.restype = C.c_int
-    L.gw_adam_step.argtypes = [p, p, p, p, p, C.c_int64, C.c_double, C.c_double, C.c_double, C.c_double, p]
+    L.gw_adam_step.argtypes = [p, p, p, p, p, C.c_int64, C.c_double, C.c_double, C.c_double, C.c_double, C.c_int32, p]
     L.gw_adam_step.restype = C.c_int
     L.gw_adam_soft_step.argtypes = [p, p, p, p, p, C.c_int64, C.c_double, C.c_double, C.c_double, C.c_double, p,
-                                    C.c_float, p, p, C.c_int64, p]
+                                    C.c_float, p, p, C.c_int64, C.c_int32, p]
     L.gw_adam_soft_step.restype = C.c_int
     L.gw_soft_update.argtypes = [p, p, C.c_int64, C.c_float, p]
     L.gw_soft_update.restype = C.c_int

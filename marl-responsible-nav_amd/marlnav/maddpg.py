@@ -128,21 +128,25 @@ class FlatAdam:
     def zero_grad(self, set_to_none: bool = False):
         self.flat.grad.zero_()  # the per-layer .grad views accumulate into this buffer
 
-    def step(self):
+    def step(self, advanced: bool = False):
+        """advanced: the preceding gradient launch already advanced the step count (the fused
+        learner's gw_maddpg_*_grads(adam_step=count)), so the Adam launch only reads it."""
         s = torch.cuda.current_stream(self.flat.device).cuda_stream
         _lib.check(self.lib.gw_adam_step(self.flat.data_ptr(), self.flat.grad.data_ptr(), self.m.data_ptr(),
                                          self.v.data_ptr(), self.count.data_ptr(), self.flat.numel(), self.lr,
-                                         self.betas[0], self.betas[1], self.eps, s), "gw_adam_step")
+                                         self.betas[0], self.betas[1], self.eps, int(advanced), s), "gw_adam_step")
         self.net.epoch += 1  # written behind torch's version counter (see MultiAgentActors.act_env)
 
-    def step_soft(self, target: torch.Tensor, tau: float, target2: torch.Tensor, online2: torch.Tensor):
+    def step_soft(self, target: torch.Tensor, tau: float, target2: torch.Tensor, online2: torch.Tensor,
+                  advanced: bool = False):
         """step(), then the soft target updates target <- tau p + (1 - tau) target (this buffer's
         target) and target2 <- tau online2 + (1 - tau) target2, in ONE launch (gw_adam_soft_step)."""
         s = torch.cuda.current_stream(self.flat.device).cuda_stream
         _lib.check(self.lib.gw_adam_soft_step(self.flat.data_ptr(), self.flat.grad.data_ptr(), self.m.data_ptr(),
                                               self.v.data_ptr(), self.count.data_ptr(), self.flat.numel(), self.lr,
                                               self.betas[0], self.betas[1], self.eps, target.data_ptr(), float(tau),
-                                              target2.data_ptr(), online2.data_ptr(), online2.numel(), s),
+                                              target2.data_ptr(), online2.data_ptr(), online2.numel(),
+                                              int(advanced), s),
                    "gw_adam_soft_step")
         self.net.epoch += 1
 
@@ -336,9 +340,16 @@ class MADDPG:
         cg = _mlp_spec(self.critics, grad=True)
         _lib.check(_lib.load().gw_maddpg_critic_grads(C.byref(at), C.byref(ct), C.byref(c), C.byref(cg), C.byref(batch),
                                                       float(self.gamma), ws.data_ptr(), loss.data_ptr(),
+                                                      self._count_ptr(self.opt_critic),
                                                       torch.cuda.current_stream(dev).cuda_stream),
                    "gw_maddpg_critic_grads")
         return dict(fused=True, x=x, x_next=x_next, r=r, d=d, u_next=u, states=states, critic_loss=loss, B=B)
+
+    @staticmethod
+    def _count_ptr(opt):
+        """The FlatAdam step count the fused gradient launch advances (its Adam step then only
+        reads it: no arrival counter); None for another optimizer."""
+        return opt.count.data_ptr() if isinstance(opt, FlatAdam) else None
 
     def _fused_actor(self, ctx: dict, u_cur=None):
         """Phase 2 (after the critic's Adam step) as gw_maddpg_actor_grads: 3 launches."""
@@ -350,6 +361,7 @@ class MADDPG:
         a, c, ag = _mlp_spec(self.actors.net), _mlp_spec(self.critics), _mlp_spec(self.actors.net, grad=True)
         _lib.check(_lib.load().gw_maddpg_actor_grads(C.byref(a), C.byref(c), C.byref(ag), C.byref(batch),
                                                      self._fused_ws(B).data_ptr(), loss.data_ptr(), None,
+                                                     self._count_ptr(self.opt_actor),
                                                      torch.cuda.current_stream(dev).cuda_stream),
                    "gw_maddpg_actor_grads")
         ctx["u_cur"] = u
@@ -388,7 +400,10 @@ class MADDPG:
     def _learn_actor(self, ctx: dict, u_cur=None):
         """Phase 2: the critic's Adam step, then the actor loss through the updated critics and
         its backward (gradients in the actors' .grad, not yet applied)."""
-        self.opt_critic.step()
+        if isinstance(self.opt_critic, FlatAdam):
+            self.opt_critic.step(advanced=bool(ctx.get("fused")))
+        else:
+            self.opt_critic.step()
         if ctx.get("fused"):
             self._fused_actor(ctx, u_cur)
             return
@@ -414,7 +429,7 @@ class MADDPG:
             t1 = self.actor_targets.net.flat_params()
             t2, p2 = self.critic_targets.flat_params(), self.critics.flat_params()
             with torch.no_grad():
-                self.opt_actor.step_soft(t1, self.tau, t2, p2)
+                self.opt_actor.step_soft(t1, self.tau, t2, p2, advanced=bool(ctx.get("fused")))
             self.actor_targets.net.epoch += 1
             self.critic_targets.epoch += 1
         else:

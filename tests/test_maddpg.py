@@ -206,7 +206,9 @@ def test_gpu_adam_and_soft_update_match_torch(n):
 @pytest.mark.parametrize("n,n2", [(1000, 3000), (300_001, 77)])
 def test_gpu_adam_soft_step_equals_adam_then_soft_update(n, n2):
     """gw_adam_soft_step (the learner's last launch) == gw_adam_step followed by gw_soft_update2,
-    bit for bit: parameters, moments, step count and both targets, over 3 steps."""
+    bit for bit: parameters, moments, step count and both targets, over 3 steps.  The soft step
+    runs with advanced = 1 (its count advanced beforehand, as the fused gradient launch does), the
+    plain step advances its own count (the arrival counter)."""
     from marlnav import _lib
     lib = _lib.load()
     s = torch.cuda.current_stream().cuda_stream
@@ -221,12 +223,13 @@ def test_gpu_adam_soft_step_equals_adam_then_soft_update(n, n2):
         grad = torch.randn(n, device="cuda", generator=g)
         a, b = bufs
         _lib.check(lib.gw_adam_step(a["p"].data_ptr(), grad.data_ptr(), a["m"].data_ptr(), a["v"].data_ptr(),
-                                    a["c"].data_ptr(), n, 1e-3, 0.9, 0.999, 1e-8, s), "gw_adam_step")
+                                    a["c"].data_ptr(), n, 1e-3, 0.9, 0.999, 1e-8, 0, s), "gw_adam_step")
         _lib.check(lib.gw_soft_update2(a["t1"].data_ptr(), a["p"].data_ptr(), n, a["t2"].data_ptr(), a["o2"].data_ptr(),
                                        n2, 0.01, s), "gw_soft_update2")
+        b["c"][0] += 1  # the count advanced by a preceding launch
         _lib.check(lib.gw_adam_soft_step(b["p"].data_ptr(), grad.data_ptr(), b["m"].data_ptr(), b["v"].data_ptr(),
                                          b["c"].data_ptr(), n, 1e-3, 0.9, 0.999, 1e-8, b["t1"].data_ptr(), 0.01,
-                                         b["t2"].data_ptr(), b["o2"].data_ptr(), n2, s), "gw_adam_soft_step")
+                                         b["t2"].data_ptr(), b["o2"].data_ptr(), n2, 1, s), "gw_adam_soft_step")
     torch.cuda.synchronize()
     for key in ("p", "m", "v", "c", "t1", "t2"):
         assert torch.equal(bufs[0][key], bufs[1][key]), key

@@ -100,6 +100,9 @@ def test_fused_updates_match_per_agent_loop():
         for k in range(K):
             assert abs(a_loss[k].item() - want[k][0]) < 1e-3 * max(1.0, abs(want[k][0]))
             assert abs(c_loss[k].item() - want[k][1]) < 1e-3 * max(1.0, abs(want[k][1]))
+    # both step counts advanced once per update (by the gradient launches; the Adam launches read them)
+    for opt in (m.opt_actor, m.opt_critic):
+        assert opt.count.tolist() == [steps, 0]
     worst, rels = 0.0, []
     for k in range(K):
         for stacked, seqs in ((m.actors.net, ref.actors), (m.actor_targets.net, ref.actor_t),
