@@ -688,9 +688,9 @@ struct CnnWs {
     float *h1;        // [K][E][128]      z_map + table rows
     float *rare_z;    // [K][E][RS][128]  their Linear-1 contributions
     int *rare_n;      // [K][E]           recomputed positions per (env, agent)
-    int *bucket_n;    // [K][P]           items per position (bucket_scan_plan)
+    int *bucket_n;    // [K][P]           items per position (bucket_scan)
     int *bucket;      // [K][P][E]        items (e RS + slot) per position
-    int *unit_off;    // [K P + 1]        bucket_scan_plan's unit offsets
+    int *unit_off;    // [K P + 1]        (unused since the rare kernels plan their units in LDS)
 };
 inline int64_t cnn_mlp_floats(int K) { return (int64_t)K * (HID + W2IMG + W3IMG + W2BIMG); }
 inline CnnWs cnn_ws_layout(float *base, int K, int P, int64_t E) {
@@ -718,8 +718,8 @@ inline CnnWs cnn_ws_layout(float *base, int K, int P, int64_t E) {
 //   item [K][E]      the (env, agent)'s positions to recompute (grid: up to RS position bytes in
 //                    slot order; windows: a position mask, slot = rank in the mask)
 //   cnt / off [nb][nblk]  items per (bucket, layer-1 block) and their offsets in the bucket
-// bucket_scan_plan turns the counts into offsets, bucket sizes and units, the scatter kernels fill the buckets.
-// ctr: bucket_scan_plan's arrival counter (zeroed by the prepare calls, left at 0 by every launch)
+// bucket_scan turns the counts into offsets and bucket sizes, the scatter kernels fill the buckets.
+// ctr: unused (zeroed by the prepare calls)
 struct Lists {
     int *item, *cnt, *off, *ctr;
     int nblk;
@@ -886,8 +886,8 @@ __global__ void __launch_bounds__(256) cnn_prep_table(CnnParams p) {
 
 // Layer 1 of the CNN head for every (env, agent): h1 = z_map + the changed positions' deltas.
 // cnn_l1_kernel sums the table rows of the positions with one patched cell into h1 and lists the
-// positions with several (slot order) with per-block counts; bucket_scan_plan / cnn_scatter file them
-// as (env, slot) items into per-(agent, position) buckets (no global atomics); bucket_scan_plan cuts
+// positions with several (slot order) with per-block counts; bucket_scan / cnn_scatter file them
+// as (env, slot) items into per-(agent, position) buckets (no global atomics); bucket_scan cuts
 // the buckets into units of up to 16 x RARE_WAVES items; cnn_rare_kernel
 // (persistent) takes units with the position's Linear-1 block staged in LDS, recomputes each
 // item's position (conv 1, conv 2) and writes its 128-float contribution; act_kernel<H1> adds an
@@ -1044,8 +1044,40 @@ __global__ void __launch_bounds__(L1_ENVS) cnn_scatter(CnnParams p, Lists lists)
 }
 
 // Units of work over the buckets: bucket b (= k P_n + P) holds ceil(n_b / RARE_ITEMS) units;
-// unit_off[b] = the units before bucket b (bucket_scan_plan's last block).
+// unit_off[b] = the units before bucket b (block_unit_offsets, in each rare block's LDS).
 constexpr int RARE_WAVES = 8, RARE_ITEMS = 16 * RARE_WAVES, RARE_BLOCKS = 256;
+
+// s_uo[b] = the units (RARE_ITEMS items each) before bucket b, s_uo[nb] = all units: a block scan
+// of the bucket sizes in bucket order (every rare block computes the same table)
+constexpr int RARE_MAX_NB = 2048;  // K x positions (8 agents x 16 x 16 conv-2 positions)
+__device__ __forceinline__ void block_unit_offsets(const int *bucket_n, int nb, int *s_uo, int *s_wt) {
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    int base = 0;
+    for (int c0 = 0; c0 < nb; c0 += 64 * RARE_WAVES) {
+        const int i = c0 + tid;
+        const int n = i < nb ? bucket_n[i] : 0;
+        const int u = (n + RARE_ITEMS - 1) / RARE_ITEMS;
+        int incl = u;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int o = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += o;
+        }
+        if (lane == 63) s_wt[wave] = incl;
+        __syncthreads();
+        int before = base, tot = 0;
+#pragma unroll
+        for (int w = 0; w < RARE_WAVES; ++w) {
+            before += w < wave ? s_wt[w] : 0;
+            tot += s_wt[w];
+        }
+        if (i < nb) s_uo[i] = before + incl - u;
+        __syncthreads();  // s_wt is rewritten by the next chunk
+        base += tot;
+    }
+    if (tid == 0) s_uo[nb] = base;
+    __syncthreads();
+}
 
 // Persistent: block b takes units b, b + RARE_BLOCKS, ...; per unit the position's conv weights,
 // map activations and Linear-1 block are staged in LDS.  Lane (item it = l & 15, quarter q): the
@@ -1123,22 +1155,24 @@ __global__ void __launch_bounds__(64 * RARE_WAVES) cnn_rare_kernel(CnnParams p) 
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int it = lane & 15, q = lane >> 4;
     const int nb = p.K * p.P;
-    const int nunits = p.ws.unit_off[nb];
     __shared__ __attribute__((aligned(16))) float s_w2[RARE_LDS_W2];   // 36 KB
     __shared__ __attribute__((aligned(16))) float s_wl[RARE_LDS_WL];   // 34 KB
     __shared__ float s_w1[C1][4], s_b1[C1], s_b2[C2], s_a2m[C2];
     __shared__ uint32_t s_road[128];
+    __shared__ int s_uo[RARE_MAX_NB + 1], s_wt[RARE_WAVES];
     if (tid < 128) s_road[tid] = p.ws.road[tid];
+    block_unit_offsets(p.ws.bucket_n, nb, s_uo, s_wt);
+    const int nunits = s_uo[nb];
     int staged_k = -1, staged_P = -1;
     for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
         int lo = 0, hi = nb;  // the bucket holding unit u: unit_off[lo] <= u < unit_off[lo + 1]
         while (hi - lo > 1) {
             const int mid = (lo + hi) >> 1;
-            if (p.ws.unit_off[mid] <= u) lo = mid; else hi = mid;
+            if (s_uo[mid] <= u) lo = mid; else hi = mid;
         }
         const int k = lo / p.P, P = lo % p.P;
         const int n = p.ws.bucket_n[lo];
-        const int i_begin = (u - p.ws.unit_off[lo]) * RARE_ITEMS, i_end = min(n, i_begin + RARE_ITEMS);
+        const int i_begin = (u - s_uo[lo]) * RARE_ITEMS, i_end = min(n, i_begin + RARE_ITEMS);
         __syncthreads();  // the previous unit is done with the LDS images
         if (k != staged_k) {
             stage_w2(s_w2, p.ws.w2t + (size_t)k * 4 * C2 * C1, tid, 64 * RARE_WAVES);
@@ -1211,7 +1245,7 @@ __global__ void __launch_bounds__(64 * RARE_WAVES) cnn_rare_kernel(CnnParams p) 
 // patched cells.  gw_patch_cnn_prepare tabulates, per (agent, centre): a2b = conv-2 activations of
 // B_c at every window position Q, and tbl = b + Linear-1(a2b).  Per step, wcnn_l1_kernel lists the
 // positions where the actual window differs from B_c (a patched cell inside the window other than
-// the centre holding vo_k); bucket_scan_plan / wcnn_scatter file them as items (env, slot) into buckets
+// the centre holding vo_k); bucket_scan / wcnn_scatter file them as items (env, slot) into buckets
 // keyed (agent, Q) in env order (a scan of per-block counts: no atomics); the persistent
 // wcnn_rare_kernel recomputes each item's position and writes Wl[:, Q] . (a2 - a2b);
 // act_kernel<H1, PW> sums tbl[centre] + those terms (slot order) and runs layers 2-3.
@@ -1314,7 +1348,7 @@ __global__ void __launch_bounds__(256) wcnn_prep_base(CnnParams p) {
 
 // one thread per (env, agent): the positions where the window differs from its base window as a
 // mask (slot = rank of the position in it; rare_n = their count) and the items per (position,
-// block); bucket_scan_plan scans the counts, wcnn_scatter fills the buckets
+// block); bucket_scan scans the counts, wcnn_scatter fills the buckets
 template <int NP>
 __global__ void __launch_bounds__(256) wcnn_l1_kernel(CnnParams p, Lists lists) {
     __shared__ uint32_t s_road[128];
@@ -1383,52 +1417,41 @@ __global__ void __launch_bounds__(256) wcnn_l1_kernel(CnnParams p, Lists lists) 
 
 
 // one 64-thread block per bucket: the offsets of the layer-1 blocks' items in the bucket (a wave
-// scan over the blocks in order) and the bucket's size; the last bucket to finish (an arrival
-// counter) cuts every bucket into units of RARE_ITEMS (unit_off), which cnn_rare_plan did in a
-// launch of its own.  One-wave blocks find a CU slot beside a concurrent window writer (a
-// 1024-thread block waits for 16 free wave slots on one CU).
-__global__ void __launch_bounds__(64) bucket_scan_plan(CnnParams p, Lists lists) {
-    const int lane = threadIdx.x, b = blockIdx.x, nb = p.K * p.P;
+// scan over the blocks in order) and the bucket's size.  All of a lane's counts are loaded before
+// the scan (one memory round trip: beside a concurrent window writer every load waits behind its
+// stores).  The rare kernels cut the buckets into units themselves (block_unit_offsets): no
+// cross-block step here, so no arrival counter and no device-scope fence (an L2 writeback per
+// block on gfx950).  One-wave blocks find a CU slot beside the window writer (a 1024-thread block
+// waits for 16 free wave slots on one CU).
+constexpr int SCAN_PRE = 8;  // counts per lane loaded up front (nblk <= 512; more: a second pass)
+__global__ void __launch_bounds__(64) bucket_scan(CnnParams p, Lists lists) {
+    const int lane = threadIdx.x, b = blockIdx.x;
+    const int *cnt = lists.cnt + (size_t)b * lists.nblk;
+    int *off = lists.off + (size_t)b * lists.nblk;
     int run = 0;
-    for (int c0 = 0; c0 < lists.nblk; c0 += 64) {
-        const int i = c0 + lane;
-        const int v = i < lists.nblk ? lists.cnt[(size_t)b * lists.nblk + i] : 0;
-        int incl = v;
+    for (int c0 = 0; c0 < lists.nblk; c0 += 64 * SCAN_PRE) {
+        int v[SCAN_PRE];
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int o = __shfl_up(incl, d, 64);
-            if (lane >= d) incl += o;
+        for (int j = 0; j < SCAN_PRE; ++j) {
+            const int i = c0 + 64 * j + lane;
+            v[j] = i < lists.nblk ? cnt[i] : 0;
         }
-        if (i < lists.nblk) lists.off[(size_t)b * lists.nblk + i] = run + incl - v;
-        run += __shfl(incl, 63, 64);
-    }
-    int last = 0;
-    if (lane == 0) {
-        p.ws.bucket_n[b] = run;
-        __threadfence();
-        last = atomicAdd(lists.ctr, 1) == nb - 1;
-    }
-    if (!__shfl(last, 0, 64)) return;
-    __threadfence();
-    int base = 0;
-    for (int c0 = 0; c0 < nb; c0 += 64) {
-        const int i = c0 + lane;
-        const int n = i < nb ? __hip_atomic_load(&p.ws.bucket_n[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-        const int u = (n + RARE_ITEMS - 1) / RARE_ITEMS;
-        int incl = u;
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int o = __shfl_up(incl, d, 64);
-            if (lane >= d) incl += o;
+        for (int j = 0; j < SCAN_PRE; ++j) {
+            const int i = c0 + 64 * j + lane;
+            int incl = v[j];
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const int o = __shfl_up(incl, d, 64);
+                if (lane >= d) incl += o;
+            }
+            if (i < lists.nblk) off[i] = run + incl - v[j];
+            run += __shfl(incl, 63, 64);
         }
-        if (i < nb) p.ws.unit_off[i] = base + incl - u;
-        base += __shfl(incl, 63, 64);
     }
-    if (lane == 0) {
-        p.ws.unit_off[nb] = base;
-        *lists.ctr = 0;
-    }
+    if (lane == 0) p.ws.bucket_n[b] = run;
 }
+
 
 // fills the buckets in (block, wave, lane) order: item (e RSW + slot), slot = the position's rank
 // in the (env, agent)'s mask
@@ -1461,22 +1484,24 @@ __global__ void __launch_bounds__(64 * RARE_WAVES) wcnn_rare_kernel(CnnParams p)
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int it = lane & 15, q = lane >> 4;
     const int nb = p.K * p.P, half = p.PW / 2;
-    const int nunits = p.ws.unit_off[nb];
     __shared__ __attribute__((aligned(16))) float s_w2[RARE_LDS_W2];   // 36 KB
     __shared__ __attribute__((aligned(16))) float s_wl[RARE_LDS_WL];   // 34 KB
     __shared__ float s_w1[C1][4], s_b1[C1], s_b2[C2];
     __shared__ uint32_t s_road[128];
+    __shared__ int s_uo[RARE_MAX_NB + 1], s_wt[RARE_WAVES];
     if (tid < 128) s_road[tid] = p.ws.road[tid];
+    block_unit_offsets(p.ws.bucket_n, nb, s_uo, s_wt);
+    const int nunits = s_uo[nb];
     int staged_k = -1, staged_Q = -1;
     for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
         int lo = 0, hi = nb;  // the bucket holding unit u: unit_off[lo] <= u < unit_off[lo + 1]
         while (hi - lo > 1) {
             const int mid = (lo + hi) >> 1;
-            if (p.ws.unit_off[mid] <= u) lo = mid; else hi = mid;
+            if (s_uo[mid] <= u) lo = mid; else hi = mid;
         }
         const int k = lo / p.P, Q = lo % p.P;
         const int n = p.ws.bucket_n[lo];
-        const int i_begin = (u - p.ws.unit_off[lo]) * RARE_ITEMS, i_end = min(n, i_begin + RARE_ITEMS);
+        const int i_begin = (u - s_uo[lo]) * RARE_ITEMS, i_end = min(n, i_begin + RARE_ITEMS);
         __syncthreads();  // the previous unit is done with the LDS images
         if (k != staged_k) {
             stage_w2(s_w2, p.ws.w2t + (size_t)k * 4 * C2 * C1, tid, 64 * RARE_WAVES);
@@ -1837,7 +1862,7 @@ gw_status gw_cnn_prepare(void *env, const gw_cnn_actors *net, float *ws, void *s
     hipLaunchKernelGGL(cnn_prep_zpart, dim3(p.P, src.K), dim3(128), 0, s, p);
     hipLaunchKernelGGL(cnn_prep_zmap, dim3(src.K), dim3(128), 0, s, p);
     hipLaunchKernelGGL(cnn_prep_table, dim3(p.P, src.K), dim3(256), 0, s, p);
-    {  // bucket_scan_plan's arrival counter starts at 0 (every launch leaves it there)
+    {  // (the lists' spare counter word starts at 0)
         const Lists l = lists_at(p.ws.unit_off, src.K * p.P, src.K, src.E, L1_ENVS);
         if (hipMemsetAsync(l.ctr, 0, sizeof(int), s) != hipSuccess) return err(GW_ERR_HIP, "gw_cnn_prepare: memset");
     }
@@ -1883,9 +1908,10 @@ gw_status gw_cnn_act(void *env, const gw_cnn_actors *net, const float *ws, int t
             default: return err(GW_ERR_ARG, "gw_cnn_act: N out of range");
         }
     }
+    if (src.K * cp.P > RARE_MAX_NB) return err(GW_ERR_ARG, "gw_cnn_act: K x conv-2 positions above the rare kernels' table");
     {
         gwprof::Span span(env, GW_SPAN_CNN_LIST);
-        gwprof::launch(bucket_scan_plan, dim3(src.K * cp.P), dim3(64), 0, s, cp, lists);
+        gwprof::launch(bucket_scan, dim3(src.K * cp.P), dim3(64), 0, s, cp, lists);
         gwprof::launch(cnn_scatter, lgrid, dim3(L1_ENVS), 0, s, cp, lists);
     }
 #define RARE(NP) gwprof::launch(cnn_rare_kernel<NP>, dim3(RARE_BLOCKS), dim3(64 * RARE_WAVES), 0, s, cp)
@@ -1994,7 +2020,7 @@ gw_status gw_patch_cnn_prepare(void *env, int32_t P, const gw_cnn_actors *net, f
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(cnn_prep_wlt, dim3(2048), dim3(256), 0, s, p);
     hipLaunchKernelGGL(wcnn_prep_base, dim3((p.HW + WCG - 1) / WCG, src.K), dim3(256), 0, s, p);
-    {  // bucket_scan_plan's arrival counter starts at 0 (every launch leaves it there)
+    {  // (the lists' spare counter word starts at 0)
         const Lists l = lists_at(p.ws.unit_off, src.K * p.P, src.K, src.E, 256);
         if (hipMemsetAsync(l.ctr, 0, sizeof(int), s) != hipSuccess) return err(GW_ERR_HIP, "gw_patch_cnn_prepare: memset");
     }
@@ -2039,9 +2065,10 @@ gw_status gw_patch_cnn_act(void *env, int32_t P, const gw_cnn_actors *net, const
             default: return err(GW_ERR_ARG, "gw_patch_cnn_act: N out of range");
         }
     }
+    if (src.K * cp.P > RARE_MAX_NB) return err(GW_ERR_ARG, "gw_patch_cnn_act: K x window positions above the rare kernels' table");
     {
         gwprof::Span span(env, GW_SPAN_CNN_LIST);
-        gwprof::launch(bucket_scan_plan, dim3(src.K * cp.P), dim3(64), 0, s, cp, lists);
+        gwprof::launch(bucket_scan, dim3(src.K * cp.P), dim3(64), 0, s, cp, lists);
         gwprof::launch(wcnn_scatter, lgrid, dim3(256), 0, s, cp, lists);
     }
 #define RARE(NP) gwprof::launch(wcnn_rare_kernel<NP>, dim3(RARE_BLOCKS), dim3(64 * RARE_WAVES), 0, s, cp)
