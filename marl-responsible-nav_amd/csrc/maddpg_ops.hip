@@ -71,16 +71,32 @@ __global__ void __launch_bounds__(256) l1_kernel(L1Params p) {
     const int d0 = chunk * DC, r0 = tile * TILE_R;
     const int nd = min(DC, jb.D - d0);
     // stage x^T (rows of this tile, inputs of this chunk) and the chunk's weight rows
+    // every load of a thread is issued before the first LDS store (one memory round trip: the
+    // loop form waited for each of its 40 loads in turn, ~20 us per launch)
     const float *xb = jb.x + (int64_t)k * jb.xk + jb.col0 + d0;
-    for (int i = tid; i < DC * TILE_R; i += 256) {
-        const int r = i / DC, d = i % DC;  // consecutive threads: consecutive inputs of a row
-        s_x[d][r] = (d < nd && r0 + r < p.B) ? xb[(int64_t)(r0 + r) * jb.ldx + d] : 0.0f;
+    constexpr int XN = DC * TILE_R / 256, WN = DC * HID / 4 / 256;
+    float xv[XN];
+    float4 wv[WN];
+#pragma unroll
+    for (int t = 0; t < XN; ++t) {
+        const int i = tid + 256 * t, r = i / DC, d = i % DC;  // consecutive threads: consecutive inputs of a row
+        xv[t] = (d < nd && r0 + r < p.B) ? xb[(int64_t)(r0 + r) * jb.ldx + d] : 0.0f;
     }
     const float *wb = jb.w + (int64_t)k * jb.wk + (int64_t)(jb.wrow0 + d0) * HID;
-    for (int i = tid; i < DC * HID / 4; i += 256) {
-        const int d = i / (HID / 4), c = i % (HID / 4);
-        const float4 v = d < nd ? reinterpret_cast<const float4 *>(wb + (int64_t)d * HID)[c] : make_float4(0, 0, 0, 0);
-        *reinterpret_cast<float4 *>(&s_w[d][4 * c]) = v;
+#pragma unroll
+    for (int t = 0; t < WN; ++t) {
+        const int i = tid + 256 * t, d = i / (HID / 4), c = i % (HID / 4);
+        wv[t] = d < nd ? reinterpret_cast<const float4 *>(wb + (int64_t)d * HID)[c] : make_float4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int t = 0; t < XN; ++t) {
+        const int i = tid + 256 * t;
+        s_x[i % DC][i / DC] = xv[t];
+    }
+#pragma unroll
+    for (int t = 0; t < WN; ++t) {
+        const int i = tid + 256 * t;
+        *reinterpret_cast<float4 *>(&s_w[i / (HID / 4)][4 * (i % (HID / 4))]) = wv[t];
     }
     __syncthreads();
     // v_mfma_f32_16x16x4_f32: wave w computes rows 32 w .. 32 w + 31 (two 16-row tiles) x all 128
@@ -193,7 +209,9 @@ __device__ __forceinline__ void gemv16(const float *s_h, const float *__restrict
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, lr = lane & 15, lq = lane >> 4;
     const int n0 = 32 * wave + lr, n1 = n0 + 16;
     f32x4 acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll 8
+    // fully unrolled: the 64 weight loads of a lane are all in flight before the first MFMA
+    // needs one (one L2 round trip per layer instead of one per 8 k-steps)
+#pragma unroll
     for (int kk = 0; kk < HID / 4; ++kk) {
         const int c = 4 * kk + lq;
         const float a = s_h[lr * HP + c];
@@ -572,18 +590,34 @@ __global__ void __launch_bounds__(256) grads_kernel(GradParams p) {
         for (int r0 = 0; r0 < p.B; r0 += TILE_R) {
             const int nr = min(TILE_R, p.B - r0);
             __syncthreads();
-            for (int i = tid; i < RB * nr; i += 256) {
-                const int r = i / RB, d = i % RB;
+            // all of a thread's loads first, then the LDS stores (one memory round trip)
+            constexpr int XN = RB * TILE_R / 256, ZN = TILE_R * HID / 4 / 256;
+            float xv[XN];
+            float4 zv[ZN];
+#pragma unroll
+            for (int t = 0; t < XN; ++t) {
+                const int i = tid + 256 * t, r = i / RB, d = i % RB;
                 float v = 0.0f;
-                if (d0 + d < D)
+                if (r < nr && d0 + d < D)
                     v = w1 ? p.x[(int64_t)(r0 + r) * p.ldx + (int64_t)k * p.xk + p.col0 + d0 + d]
                            : p.sv.h1[((int64_t)k * p.B + r0 + r) * HID + d0 + d];
-                s_in[d][r] = v;
+                xv[t] = v;
             }
-            for (int i = tid; i < nr * HID / 4; i += 256) {
-                const int r = i / (HID / 4), c = i % (HID / 4);
-                *reinterpret_cast<float4 *>(&s_dz[r][4 * c]) =
-                    reinterpret_cast<const float4 *>(dz + ((int64_t)k * p.B + r0 + r) * HID)[c];
+#pragma unroll
+            for (int t = 0; t < ZN; ++t) {
+                const int i = tid + 256 * t, r = i / (HID / 4), c = i % (HID / 4);
+                zv[t] = r < nr ? reinterpret_cast<const float4 *>(dz + ((int64_t)k * p.B + r0 + r) * HID)[c]
+                               : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            }
+#pragma unroll
+            for (int t = 0; t < XN; ++t) {
+                const int i = tid + 256 * t;
+                if (i / RB < nr) s_in[i % RB][i / RB] = xv[t];
+            }
+#pragma unroll
+            for (int t = 0; t < ZN; ++t) {
+                const int i = tid + 256 * t;
+                if (i / (HID / 4) < nr) *reinterpret_cast<float4 *>(&s_dz[i / (HID / 4)][4 * (i % (HID / 4))]) = zv[t];
             }
             __syncthreads();
             for (int kk = 0; kk < nr / 4; ++kk) {  // nr: a multiple of 16 (B % 16 == 0)
@@ -614,6 +648,7 @@ __global__ void __launch_bounds__(256) grads_kernel(GradParams p) {
         for (int v = 0; v < 6; ++v)
 #pragma unroll
             for (int i = 0; i < 8; ++i) acc[v][i] = 0.0f;
+#pragma unroll 2
         for (int r = rg; r < p.B; r += GRG) {
             const int64_t o = base + (int64_t)r * HID + 8 * g;
             const float *src[6] = {p.sv.dz1 + o, p.sv.gv1 + o, p.sv.xh1 + o, p.sv.dz2 + o, p.sv.gv2 + o, p.sv.xh2 + o};
@@ -667,6 +702,7 @@ __global__ void __launch_bounds__(256) grads_kernel(GradParams p) {
     float bacc[NA], lacc = 0.0f;
 #pragma unroll
     for (int a = 0; a < NA; ++a) bacc[a] = 0.0f;
+#pragma unroll 4
     for (int r = rg; r < p.B; r += GRG) {
         const float *hs = p.sv.h2 + base + (int64_t)r * HID + 8 * g;
         const float4 h0 = *reinterpret_cast<const float4 *>(hs), h1 = *reinterpret_cast<const float4 *>(hs + 4);

@@ -24,7 +24,8 @@
 
 namespace {
 
-constexpr int PB = 32, THREADS = 256, MAXP = GW_MAX_AGENTS + 1, MAXPL = 4;  // MAXPL: P * P <= 256
+constexpr int THREADS = 256, MAXP = GW_MAX_AGENTS + 1, MAXPL = 4;  // MAXPL: P * P <= 256
+// PB: envs per block (a template parameter: 32, or 64 where the LDS leaves room for enough blocks)
 constexpr uint32_t D_RESET = 1u, D_WRITE = 2u, D_FINAL = 4u;
 constexpr int NDESC = 12;
 
@@ -49,7 +50,7 @@ __device__ __forceinline__ float map_value(const uint32_t *road, int H, int W, i
 // window row (map bits + overrides in registers, no LDS image: every store is a whole aligned
 // float4 of the [K][E][P*P] run); 3: any P, one thread per 16-byte piece of the block's run (a
 // byte table of the patched cells in LDS, map values from the road bits)
-template <int MODE>
+template <int MODE, int PB>
 __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a, unsigned long long *dbg) {
     constexpr bool SMALL = MODE == 0;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -364,23 +365,27 @@ namespace gw {
 
 unsigned long long *g_patch_dbg = nullptr;
 
-template <int MODE>
-hipError_t launch_mode(const PatchArgs &a, unsigned grid, size_t lds, hipStream_t s) {
+template <int MODE, int PB>
+hipError_t launch_mode(const PatchArgs &a, size_t lds, hipStream_t s) {
     // above the 64 KB a launch gets by default, the kernel's dynamic-LDS limit is raised once (up
     // to gfx950's 160 KB per workgroup)
     static size_t granted = 64 * 1024;
     if (lds > granted) {
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&window_kernel<MODE>),
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&window_kernel<MODE, PB>),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         granted = lds;
     }
-    gwprof::launch(window_kernel<MODE>, dim3(grid), dim3(THREADS), lds, s, a, g_patch_dbg);
+    const unsigned grid = (unsigned)((a.E + PB - 1) / PB);
+    gwprof::launch(window_kernel<MODE, PB>, dim3(grid), dim3(THREADS), lds, s, a, g_patch_dbg);
     return hipGetLastError();
 }
 
 hipError_t launch_windows(const PatchArgs &a, hipStream_t s) {
     const int np = a.N + 1, PP = a.P * a.P;
+    // envs per block: 32, or 64 (GW_PATCH_PB=64, measurement only for now)
+    static const char *pb_env = std::getenv("GW_PATCH_PB");
+    const int PB = (pb_env && std::atoi(pb_env) == 64) ? 64 : 32;
     // LDS: road bitmask, flags, centres, patch cells + values, and per mode: MODE 0 one agent's
     // window run (PP <= 256), MODE 2 the nibble table (PB * K * P * P / 4 u16, patch indices
     // 1..15), MODE 3 one agent's byte table (PB * P * P + 4 bytes).  Preference: MODE 2 (P % 4 ==
@@ -402,12 +407,19 @@ hipError_t launch_windows(const PatchArgs &a, hipStream_t s) {
             mode = f;
     }
     const size_t lds = base + extra[mode];
-    const unsigned grid = (unsigned)((a.E + PB - 1) / PB);
+    if (PB == 64) {
+        switch (mode) {
+            case 0: return launch_mode<0, 64>(a, lds, s);
+            case 2: return launch_mode<2, 64>(a, lds, s);
+            case 3: return launch_mode<3, 64>(a, lds, s);
+            default: return launch_mode<1, 64>(a, lds, s);
+        }
+    }
     switch (mode) {
-        case 0: return launch_mode<0>(a, grid, lds, s);
-        case 2: return launch_mode<2>(a, grid, lds, s);
-        case 3: return launch_mode<3>(a, grid, lds, s);
-        default: return launch_mode<1>(a, grid, lds, s);
+        case 0: return launch_mode<0, 32>(a, lds, s);
+        case 2: return launch_mode<2, 32>(a, lds, s);
+        case 3: return launch_mode<3, 32>(a, lds, s);
+        default: return launch_mode<1, 32>(a, lds, s);
     }
 }
 
