@@ -26,6 +26,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <initializer_list>
 #include <string>
 
 #include "learner_ops.h"
@@ -134,6 +135,51 @@ __global__ void __launch_bounds__(256) l1_kernel(L1Params p) {
         }
 }
 
+// ---- layer-1 pre-activations: the chunk partials summed in chunk order + the bias ------------------
+// z[k][r][j] = (sum over chunks c in order of part[c][k][r][j]) + b1[k][j]: the sum the tails formed
+// themselves until round 4, bit for bit, now with every (k, r, 4 features) of every job in
+// parallel (a thread's chunk loads 16 at a time in flight) instead of a dependent chain of L2/HBM
+// round trips inside each tail (the partials come from other XCDs' L2s: ~2 us per round trip).
+struct ReduceJob {
+    const float *part, *b1;  // [nch][K][B][HID], [K][HID]
+    float *z;                // [K][B][HID]
+    int nch;
+};
+struct ReduceParams {
+    ReduceJob job[MAXJOB];
+    int njob, K, B, per_job;  // per_job: float4 outputs of one job (K B HID / 4)
+};
+constexpr int RED_PRE = 16;
+__global__ void __launch_bounds__(256) l1_reduce(ReduceParams p) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int j = (int)(t / p.per_job);
+    if (j >= p.njob) return;
+    const ReduceJob &jb = p.job[j];
+    const int i = (int)(t - (int64_t)j * p.per_job);  // float4 index in [K][B][HID / 4]
+    const int k = i / (p.B * (HID / 4));
+    const int j4 = i % (HID / 4);
+    const int64_t cstride = (int64_t)p.K * p.B * (HID / 4);
+    const float4 *src = reinterpret_cast<const float4 *>(jb.part) + i;
+    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    for (int c0 = 0; c0 < jb.nch; c0 += RED_PRE) {
+        float4 v[RED_PRE];
+#pragma unroll
+        for (int c = 0; c < RED_PRE; ++c)
+            v[c] = c0 + c < jb.nch ? src[(c0 + c) * cstride] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+        for (int c = 0; c < RED_PRE; ++c) {
+            if (c0 + c < jb.nch) {  // (past the end: nothing added, not even a zero)
+                acc.x += v[c].x;
+                acc.y += v[c].y;
+                acc.z += v[c].z;
+                acc.w += v[c].w;
+            }
+        }
+    }
+    const float4 b = reinterpret_cast<const float4 *>(jb.b1 + (int64_t)k * HID)[j4];
+    reinterpret_cast<float4 *>(jb.z)[i] = make_float4(acc.x + b.x, acc.y + b.y, acc.z + b.z, acc.w + b.w);
+}
+
 // ---- per-row helpers (a row = 16 lanes, lane g holds features 8 g .. 8 g + 7) ---------------------
 __device__ __forceinline__ float row_sum(float v) {  // over the row's 16 lanes
     v += __shfl_xor(v, 1, 64);
@@ -240,39 +286,12 @@ __device__ __forceinline__ void rows_gemv(const float v[8], int rl, int g, const
     for (int i = 0; i < 8; ++i) out[i] = s_out[rl * HP + 8 * g + i];
 }
 
-// the layer-1 pre-activation of (k, row): the chunk partials in order + bias (+ extra: the
-// action-column terms a caller adds)
-__device__ __forceinline__ void l1_sum(const float *part, int nchunk, int K, int B, int k, int r, int g,
-                                       const float *b1, float z[8]) {
-    float acc[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] = 0.0f;
-    // the partials of 8 chunks are loaded together, then added in chunk order (one L2 round
-    // trip per 8 chunks instead of per chunk: 33 chunks took ~8 us as a dependent chain)
-    const int64_t cstride = (int64_t)K * B * HID;
-    const float *p0 = part + ((int64_t)k * B + r) * HID + 8 * g;
-    int c = 0;
-    for (; c + 8 <= nchunk; c += 8) {
-        float4 a[8], b[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            a[j] = *reinterpret_cast<const float4 *>(p0 + (c + j) * cstride);
-            b[j] = *reinterpret_cast<const float4 *>(p0 + (c + j) * cstride + 4);
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            acc[0] += a[j].x; acc[1] += a[j].y; acc[2] += a[j].z; acc[3] += a[j].w;
-            acc[4] += b[j].x; acc[5] += b[j].y; acc[6] += b[j].z; acc[7] += b[j].w;
-        }
-    }
-    for (; c < nchunk; ++c) {
-        const float4 a = *reinterpret_cast<const float4 *>(p0 + c * cstride);
-        const float4 b = *reinterpret_cast<const float4 *>(p0 + c * cstride + 4);
-        acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
-        acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) z[i] = acc[i] + b1[8 * g + i];
+// the 8 layer-1 pre-activations of (k, row r) lane g holds, from l1_reduce's z [K][B][128]
+__device__ __forceinline__ void z8(const float *zb, int B, int k, int r, int g, float z[8]) {
+    const float *o = zb + ((int64_t)k * B + r) * HID + 8 * g;
+    const float4 a = *reinterpret_cast<const float4 *>(o), b = *reinterpret_cast<const float4 *>(o + 4);
+    z[0] = a.x; z[1] = a.y; z[2] = a.z; z[3] = a.w;
+    z[4] = b.x; z[5] = b.y; z[6] = b.z; z[7] = b.w;
 }
 
 // save 8 features of row r to buf [K][B][128]
@@ -297,11 +316,11 @@ struct TailParams {
     const double *reward;  // [B][K]
     const uint8_t *done;   // [B][K]
     const float *u;        // [K][B][9] Gumbel uniforms of this phase's sample
-    const float *part_a, *part_ct, *part_c;  // layer-1 partials (actor-like, critic target, critic)
+    const float *z_a, *z_ct, *z_c;  // layer-1 pre-activations (l1_reduce: actor-like, critic target, critic)
     Saved sv;
     float gamma;
     int64_t ldx;
-    int K, B, D, nch_a, nch_c, nch_cs;  // chunks: actor (D inputs), critic full (ldx), critic state part (K D)
+    int K, B, D;
     float *probs_out;      // actor phase: [K][B][9] the fresh action probabilities (tests), may be null
 };
 
@@ -311,7 +330,7 @@ __device__ __forceinline__ void target_probs(const TailParams &p, int kk, int r,
                                              float *s_out, float pr[NA]) {
     const Mlp m = mlp_k(p.actor_t, kk, p.D, NA);
     float z[8], xh[8], y[8], rs;
-    l1_sum(p.part_a, p.nch_a, p.K, p.B, kk, r, g, m.b1, z);
+    z8(p.z_a, p.B, kk, r, g, z);
     ln_relu(z, m.lw1, m.lb1, g, xh, y, rs);
     rows_gemv(y, rl, g, m.w2, false, s_in, s_out, z);
 #pragma unroll
@@ -347,11 +366,11 @@ __device__ __forceinline__ void target_probs(const TailParams &p, int kk, int r,
 struct RowFwd {
     float xh1[8], y1[8], rs1, xh2[8], y2[8], rs2;
 };
-__device__ __forceinline__ float critic_fwd(const Mlp &m, const float *part, int nch, const TailParams &p, int k,
+__device__ __forceinline__ float critic_fwd(const Mlp &m, const float *zsrc, const TailParams &p, int k,
                                             int r, int rl, int g, const float *act, float *s_in, float *s_out,
                                             RowFwd &f) {
     float z[8];
-    l1_sum(part, nch, p.K, p.B, k, r, g, m.b1, z);
+    z8(zsrc, p.B, k, r, g, z);
     const int Ds = p.K * p.D;
 #pragma unroll 9
     for (int a = 0; a < NA * p.K; ++a) {  // 9 rows' loads in flight together, fmas in row order
@@ -413,13 +432,13 @@ __global__ void __launch_bounds__(256) critic_tail(TailParams p) {
     }
     __syncthreads();
     RowFwd f;
-    const float q_next = critic_fwd(mt, p.part_ct, p.nch_cs, p, k, r, rl, g, s_act[rl], s_in, s_out, f);
+    const float q_next = critic_fwd(mt, p.z_ct, p, k, r, rl, g, s_act[rl], s_in, s_out, f);
     // y = f32(r) + ((1 - d) * gamma) * q_next, gw_td_target's op order
     const float t1 = 1.0f - (float)p.done[(int64_t)r * p.K + k];
     const float y = (float)p.reward[(int64_t)r * p.K + k] + (t1 * p.gamma) * q_next;
     // online critic on (s, a): the stored actions are the x rows' action slots (in the partials)
     float z[8];
-    l1_sum(p.part_c, p.nch_c, p.K, p.B, k, r, g, m.b1, z);
+    z8(p.z_c, p.B, k, r, g, z);
     RowFwd o;
     ln_relu(z, m.lw1, m.lb1, g, o.xh1, o.y1, o.rs1);
     rows_gemv(o.y1, rl, g, m.w2, false, s_in, s_out, z);
@@ -466,7 +485,7 @@ __global__ void __launch_bounds__(256) actor_tail(TailParams p) {
     __syncthreads();
     float z[8];
     RowFwd fa;
-    l1_sum(p.part_a, p.nch_a, p.K, p.B, k, r, g, ma.b1, z);
+    z8(p.z_a, p.B, k, r, g, z);
     ln_relu(z, ma.lw1, ma.lb1, g, fa.xh1, fa.y1, fa.rs1);
     rows_gemv(fa.y1, rl, g, ma.w2, false, s_in, s_out, z);
 #pragma unroll
@@ -503,7 +522,7 @@ __global__ void __launch_bounds__(256) actor_tail(TailParams p) {
     if (g == 0)
         for (int a = 0; a < NA; ++a) s_act[rl][NA * k + a] = pr[a];
     RowFwd fc;
-    const float q = critic_fwd(mc, p.part_c, p.nch_cs, p, k, r, rl, g, s_act[rl], s_in, s_out, fc);
+    const float q = critic_fwd(mc, p.z_c, p, k, r, rl, g, s_act[rl], s_in, s_out, fc);
     const float dq = -(1.0f / (float)p.B);  // -mean Q backward (gw_mean_loss_bwd mode 1)
     float gv1[8], dz1[8], gv2[8], dz2[8];
     critic_bwd(mc, dq, rl, g, fc, s_in, s_out, gv1, dz1, gv2, dz2);
@@ -751,6 +770,7 @@ __global__ void __launch_bounds__(256) grads_kernel(GradParams p) {
 // ---- workspace ---------------------------------------------------------------------------------
 struct Ws {
     float *part_a, *part_ct, *part_c;
+    float *z_a, *z_ct, *z_c;  // [K][B][HID] each
     Saved sv;
 };
 inline int nchunks(int64_t D) { return (int)((D + DC - 1) / DC); }
@@ -763,6 +783,10 @@ inline Ws ws_layout(float *w, int K, int B, int D) {
     w += (int64_t)nchunks((int64_t)K * D) * K * B * HID;
     s.part_c = w;
     w += (int64_t)nchunks(ldx) * K * B * HID;
+    s.z_a = w;
+    s.z_ct = w + (int64_t)K * B * HID;
+    s.z_c = w + 2LL * K * B * HID;
+    w += 3LL * K * B * HID;
     float **f[8] = {&s.sv.h1, &s.sv.h2, &s.sv.xh1, &s.sv.xh2, &s.sv.gv1, &s.sv.gv2, &s.sv.dz1, &s.sv.dz2};
     for (float **q : f) {
         *q = w;
@@ -775,7 +799,7 @@ inline Ws ws_layout(float *w, int K, int B, int D) {
 }
 int64_t ws_floats(int K, int B, int D) {
     const int64_t ldx = (int64_t)K * D + (int64_t)NA * K;
-    return ((int64_t)nchunks(D) + nchunks((int64_t)K * D) + nchunks(ldx)) * K * B * HID + 8LL * K * B * HID +
+    return ((int64_t)nchunks(D) + nchunks((int64_t)K * D) + nchunks(ldx)) * K * B * HID + 11LL * K * B * HID +
            (int64_t)K * B * NA + (int64_t)K * B + 64;
 }
 
@@ -796,6 +820,16 @@ void add_job(L1Params &lp, int &blocks, const float *x, int64_t ldx, int64_t xk,
     blocks += j.nchunk * lp.K * lp.ntile;
     lp.njob++;
     lp.start[lp.njob] = blocks;
+}
+
+void launch_reduce(int K, int B, std::initializer_list<ReduceJob> jobs, hipStream_t s) {
+    ReduceParams rp{};
+    for (const ReduceJob &j : jobs) rp.job[rp.njob++] = j;
+    rp.K = K;
+    rp.B = B;
+    rp.per_job = K * B * (HID / 4);
+    const int64_t threads = (int64_t)rp.njob * rp.per_job;
+    hipLaunchKernelGGL(l1_reduce, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, rp);
 }
 
 gw_status check(const gw_maddpg_batch *b, const char *who) {
@@ -850,6 +884,9 @@ gw_status gw_maddpg_critic_grads(const gw_mlp_actors *actor_target, const gw_mlp
     add_job(lp, blocks, batch->x_next, ldx, 0, 0, critic_target->w1, ldx * HID, 0, K * D, w.part_ct);
     add_job(lp, blocks, batch->x, ldx, 0, 0, critic->w1, ldx * HID, 0, (int)ldx, w.part_c);
     hipLaunchKernelGGL(l1_kernel, dim3(blocks), dim3(256), 0, s, lp);
+    launch_reduce(K, B, {{w.part_a, actor_target->b1, w.z_a, nchunks(D)},
+                         {w.part_ct, critic_target->b1, w.z_ct, nchunks((int64_t)K * D)},
+                         {w.part_c, critic->b1, w.z_c, nchunks(ldx)}}, s);
     TailParams tp{};
     tp.actor_t = *actor_target;
     tp.critic_t = *critic_target;
@@ -859,18 +896,15 @@ gw_status gw_maddpg_critic_grads(const gw_mlp_actors *actor_target, const gw_mlp
     tp.reward = batch->reward;
     tp.done = batch->done;
     tp.u = batch->u;
-    tp.part_a = w.part_a;
-    tp.part_ct = w.part_ct;
-    tp.part_c = w.part_c;
+    tp.z_a = w.z_a;
+    tp.z_ct = w.z_ct;
+    tp.z_c = w.z_c;
     tp.sv = w.sv;
     tp.gamma = gamma;
     tp.ldx = ldx;
     tp.K = K;
     tp.B = B;
     tp.D = D;
-    tp.nch_a = nchunks(D);
-    tp.nch_c = nchunks(ldx);
-    tp.nch_cs = nchunks((int64_t)K * D);
     hipLaunchKernelGGL(critic_tail, dim3(B / RB, K), dim3(256), 0, s, tp);
     GradParams gp{};
     gp.grad = *critic_grad;
@@ -914,21 +948,20 @@ gw_status gw_maddpg_actor_grads(const gw_mlp_actors *actor, const gw_mlp_actors 
     add_job(lp, blocks, batch->x, ldx, D, 0, actor->w1, (int64_t)D * HID, 0, D, w.part_a);
     add_job(lp, blocks, batch->x, ldx, 0, 0, critic->w1, ldx * HID, 0, K * D, w.part_c);  // state columns
     hipLaunchKernelGGL(l1_kernel, dim3(blocks), dim3(256), 0, s, lp);
+    launch_reduce(K, B, {{w.part_a, actor->b1, w.z_a, nchunks(D)}, {w.part_c, critic->b1, w.z_c, nchunks((int64_t)K * D)}}, s);
     TailParams tp{};
     tp.actor = *actor;
     tp.critic = *critic;
     tp.x = batch->x;
     tp.x_next = batch->x_next;
     tp.u = batch->u;
-    tp.part_a = w.part_a;
-    tp.part_c = w.part_c;
+    tp.z_a = w.z_a;
+    tp.z_c = w.z_c;
     tp.sv = w.sv;
     tp.ldx = ldx;
     tp.K = K;
     tp.B = B;
     tp.D = D;
-    tp.nch_a = nchunks(D);
-    tp.nch_cs = nchunks((int64_t)K * D);
     tp.probs_out = probs;
     hipLaunchKernelGGL(actor_tail, dim3(B / RB, K), dim3(256), 0, s, tp);
     GradParams gp{};
