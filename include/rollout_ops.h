@@ -90,7 +90,7 @@ gw_status gw_replay_gather(const void *obs, const void *final_obs, int32_t obs_b
  * (gw_obs_desc_copy after that step, into slot j); the terminal obs of transition slot tr
  * comes from the terminal half of descriptor slot tr + 1.  src: gw_obs_view of the env
  * (base map, apple cells, N, K, H, W, variant, E; its desc pointer is not used).  Every other
- * argument and output as gw_replay_gather (f32 rows; K = src->K, HW = src->H * src->W). */
+ * argument and output as gw_replay_gather (f32 rows; K = src->K, HW = src->H * src->W <= 4096). */
 gw_status gw_replay_gather_desc(const gw_obs_source *src, const uint32_t *desc, const float *probs,
                                 const double *reward, const uint8_t *term, const uint8_t *done, const int64_t *t_dev,
                                 const float *u, const int64_t *env, int64_t S, int64_t B, float *state,

@@ -224,24 +224,25 @@ struct DescSrc {
     int64_t E;
 };
 
-// patches of (descriptor d, agent k): which 0 = the obs, 1 = the terminal obs (words 8-11)
-__device__ __forceinline__ int desc_patches(const DescSrc &q, const uint32_t *d, int which, int k, int *pc,
-                                            float *pv) {
+// patches of (descriptor words d[0..11], agent k): which 0 = the obs, 1 = the terminal obs (words
+// 8-11); apple_map = the map value under agent k's apple cell
+__device__ __forceinline__ int desc_patches(const DescSrc &q, const uint32_t (&d)[DESC_WORDS], int which, int k,
+                                            float apple_map, int *pc, float *pv) {
     const uint32_t f = d[4];
     const bool reset = which == 0 && (f & DF_RESET);
     const uint32_t apples = which == 0 ? (f >> 8) & 0xFFu : (f >> 16) & 0xFFu;
-    const uint32_t *pw = d + (which == 0 ? 0 : 8);
     const int ac = ((apples >> k) & 1u) ? q.apples[k] : -1;
     int np = 0;
     if (ac >= 0) {
-        float av = q.base[ac] + 9.0f;
+        float av = apple_map + 9.0f;
         if (!reset && av == (float)(k + 1)) av = 1.0f;
         pc[np] = ac;
         pv[np] = av;
         ++np;
     }
     for (int n = 0; n < q.N; ++n) {
-        const int c = (int)((pw[n >> 1] >> (16 * (n & 1))) & 0xFFFFu);
+        const uint32_t w = which == 0 ? d[n >> 1] : d[8 + (n >> 1)];
+        const int c = (int)((w >> (16 * (n & 1))) & 0xFFFFu);
         pc[np] = c;
         pv[np] = desc_agent_value(reset, n, k, c == ac, q.variant);
         ++np;
@@ -249,6 +250,11 @@ __device__ __forceinline__ int desc_patches(const DescSrc &q, const uint32_t *d,
     return np;
 }
 
+constexpr int GD_CELLS = 16;  // map cells per thread prefetched (HW <= 256 * GD_CELLS = 4096)
+
+// Every load of a block is issued in two waves: (t, u, env, the apple's map value, this thread's
+// map cells), then (done, both descriptors whole, probs, reward, term); the rest is register / LDS
+// work (each dependent global round trip costs ~1-2 us).
 __global__ void __launch_bounds__(256) replay_gather_desc_kernel(
     DescSrc q, const uint32_t *__restrict__ desc, const float *__restrict__ probs, const double *__restrict__ reward,
     const uint8_t *__restrict__ term, const uint8_t *__restrict__ done, const int64_t *__restrict__ t_dev,
@@ -260,34 +266,57 @@ __global__ void __launch_bounds__(256) replay_gather_desc_kernel(
     __shared__ float s_pv[2][GW_MAX_AGENTS + 1];
     __shared__ int s_np[2];
     const int64_t b = blockIdx.x;
-    const int k = blockIdx.y, K = q.K;
+    const int k = blockIdx.y, K = q.K, tid = threadIdx.x;
     const int64_t E = q.E, HW = q.HW;
+    // wave 1
     const int64_t t = t_dev[0];
+    const float ub = u[b];
+    const int64_t e = env[b];
+    const float apple_map = q.apples[k] >= 0 ? q.base[q.apples[k]] : 0.0f;
+    float mv[GD_CELLS];
+#pragma unroll
+    for (int c = 0; c < GD_CELLS; ++c) {
+        const int64_t i = tid + 256 * c;
+        mv[c] = i < HW ? q.base[i] : 0.0f;
+    }
     const int64_t n = t < 1 ? 1 : (t > S - 1 ? S - 1 : t);
-    int64_t step = (int64_t)(u[b] * (float)n);  // as replay_gather_kernel (torch's draw)
+    int64_t step = (int64_t)(ub * (float)n);  // as replay_gather_kernel (torch's draw)
     if (step > n - 1) step = n - 1;
     int64_t tr = (t - 1 - step) % S;
     if (tr < 0) tr += S;
     const int64_t nx = (tr + 1) % S;
-    const int64_t e = env[b];
-    const bool dn = done[tr * E + e] != 0;
-    // obs slot j of the ring was written from descriptor slot j; the terminal obs of the
+    // wave 2: obs slot j of the ring was written from descriptor slot j; the terminal obs of the
     // transition in slot tr (its final_obs slot) from the terminal half of descriptor slot tr + 1
-    if (threadIdx.x < 2) {
-        const int w = threadIdx.x;
-        const uint32_t *d = desc + ((w == 0 ? tr : nx) * E + e) * DESC_WORDS;
-        s_np[w] = desc_patches(q, d, w == 0 ? 0 : (dn ? 1 : 0), k, s_pc[w], s_pv[w]);
+    const bool dn = done[tr * E + e] != 0;
+    if (tid < 2) {
+        const uint4 *d4 = reinterpret_cast<const uint4 *>(desc + ((tid == 0 ? tr : nx) * E + e) * DESC_WORDS);
+        const uint4 a = d4[0], bq = d4[1], c = d4[2];
+        const uint32_t d[DESC_WORDS] = {a.x, a.y, a.z, a.w, bq.x, bq.y, bq.z, bq.w, c.x, c.y, c.z, c.w};
+        s_np[tid] = desc_patches(q, d, tid == 0 ? 0 : (dn ? 1 : 0), k, apple_map, s_pc[tid], s_pv[tid]);
     }
+    const int64_t ldx = (int64_t)K * HW + (int64_t)K * 9;
+    if (tid < 9) {
+        const float pv = probs[((tr * K + k) * E + e) * 9 + tid];
+        probs_out[(k * B + b) * 9 + tid] = pv;
+        if (x_out) x_out[b * ldx + (int64_t)K * HW + k * 9 + tid] = pv;
+    }
+    if (k == 0 && tid >= 64 && tid < 64 + K) {
+        const int j = tid - 64;
+        reward_out[b * K + j] = reward[(tr * E + e) * K + j];
+        term_out[b * K + j] = term[(tr * E + e) * K + j];
+    }
+    if (k == 0 && tid == 128 && tr_out) tr_out[b] = tr;
     __syncthreads();
     const int np0 = s_np[0], np1 = s_np[1];
     float *so = state + (k * B + b) * HW;
     float *no = next_state + (k * B + b) * HW;
-    const int64_t ldx = (int64_t)K * HW + (int64_t)K * 9;
     float *xo = x_out ? x_out + b * ldx + (int64_t)k * HW : nullptr;
     float *xno = xn_out ? xn_out + b * ldx + (int64_t)k * HW : nullptr;
-    for (int64_t i = threadIdx.x; i < HW; i += blockDim.x) {
-        const float m = q.base[i];
-        float sv = m, nv = m;
+#pragma unroll
+    for (int c = 0; c < GD_CELLS; ++c) {
+        const int64_t i = tid + 256 * c;
+        if (i >= HW) break;
+        float sv = mv[c], nv = mv[c];
         for (int j = 0; j < np0; ++j)
             if (s_pc[0][j] == i) sv = s_pv[0][j];
         for (int j = 0; j < np1; ++j)
@@ -297,17 +326,6 @@ __global__ void __launch_bounds__(256) replay_gather_desc_kernel(
         if (xo) xo[i] = sv;
         if (xno) xno[i] = nv;
     }
-    if (threadIdx.x < 9) {
-        const float pv = probs[((tr * K + k) * E + e) * 9 + threadIdx.x];
-        probs_out[(k * B + b) * 9 + threadIdx.x] = pv;
-        if (x_out) x_out[b * ldx + (int64_t)K * HW + k * 9 + threadIdx.x] = pv;
-    }
-    if (k == 0 && threadIdx.x >= 64 && threadIdx.x < 64 + K) {
-        const int j = threadIdx.x - 64;
-        reward_out[b * K + j] = reward[(tr * E + e) * K + j];
-        term_out[b * K + j] = term[(tr * E + e) * K + j];
-    }
-    if (k == 0 && threadIdx.x == 128 && tr_out) tr_out[b] = tr;
 }
 
 // ---- evaluation totals (customeval.py:70-133): one 1024-thread block, fixed-order sums ------------
@@ -684,7 +702,7 @@ gw_status gw_replay_gather_desc(const gw_obs_source *src, const uint32_t *desc, 
     if (!src || !src->base || !desc || !probs || !reward || !term || !done || !t_dev || !u || !env || !state ||
         !next_state || !probs_out || !reward_out || !term_out || S < 2 || src->K <= 0 || src->K > GW_MAX_AGENTS ||
         src->N < src->K || src->N > GW_MAX_AGENTS || src->E <= 0 || src->H <= 0 || src->W <= 0 || B < 0 ||
-        B > 0x7fffffff)
+        B > 0x7fffffff || (int64_t)src->H * src->W > 256 * GD_CELLS)
         return GW_ERR_ARG;
     if (B == 0) return GW_OK;
     DescSrc q;

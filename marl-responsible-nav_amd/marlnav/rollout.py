@@ -57,7 +57,7 @@ class ReplayRing:
         self.E, self.K = E, K
         self.desc = None
         self.desc_ok = False  # every descriptor slot matches its obs slot (set by Rollout.reset)
-        if desc and not patch and dev.type == "cuda":
+        if desc and not patch and dev.type == "cuda" and H * W <= 4096:  # (the expansion's cell limit)
             self.desc = torch.zeros((self.S, E, 12), dtype=torch.int32, device=dev)
             self._src = _lib.GwObsSource()
             _lib.check(_lib.load().gw_obs_view(env.handle, C.byref(self._src)), "gw_obs_view")
