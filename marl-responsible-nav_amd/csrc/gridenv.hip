@@ -1105,6 +1105,11 @@ __global__ void __launch_bounds__(256) step_kernel_fear(Params p) {
     }
 }
 
+// a plain 16-byte-per-lane copy (gw_obs_desc_copy)
+__global__ void __launch_bounds__(256) copy16_kernel(const uint4 *__restrict__ src, uint4 *__restrict__ dst, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) dst[i] = src[i];
+}
+
 // ---------------------------------------------------------------------------------------
 // reset kernel (CustomMAEnv.reset for masked envs)
 // ---------------------------------------------------------------------------------------
@@ -3426,10 +3431,16 @@ gw_status gw_obs_patch(void *handle, int32_t P, float *patch, float *final_patch
 gw_status gw_obs_desc_copy(void *handle, uint32_t *dst, void *stream) {
     Env *env = static_cast<Env *>(handle);
     if (!env || !dst) return fail(GW_ERR_ARG, "null argument");
+    if (reinterpret_cast<uintptr_t>(dst) & 15u) return fail(GW_ERR_ARG, "gw_obs_desc_copy: dst not 16-byte aligned");
     // the world update that wrote env->desc is ordered before the caller's later work on its
-    // stream on every path (the pipelined ones join it); a later step writes the other buffer
-    HIP_TRY(hipMemcpyAsync(dst, env->desc, sizeof(uint32_t) * gw::NDESC * (size_t)env->E, hipMemcpyDeviceToDevice,
-                           static_cast<hipStream_t>(stream)));
+    // stream on every path (the pipelined ones join it); a later step writes the other buffer.
+    // A 16-byte-per-lane copy kernel: the runtime's D2D blit took ~18 us for these 3 MB beside
+    // the obs writer (C5), this takes a few
+    const int64_t n16 = (int64_t)env->E * gw::NDESC / 4;  // NDESC = 12: whole uint4s per env
+    const unsigned grid = (unsigned)std::min<int64_t>((n16 + 255) / 256, 2048);
+    gw_launch(gw::copy16_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream),
+              reinterpret_cast<const uint4 *>(env->desc), reinterpret_cast<uint4 *>(dst), n16);
+    HIP_TRY(hipGetLastError());
     return GW_OK;
 }
 

@@ -25,10 +25,16 @@ __global__ void __launch_bounds__(256) adam_kernel(float *__restrict__ p, const 
     // (Python floats), rounded to float where they meet the f32 tensors
     // advanced: the count already includes this step (the caller's preceding launch advanced it);
     // else read by every block before the last one advances it (below)
+    // the two bias corrections (double pow) once per block, not per thread
+    __shared__ float s_sc[2];
     const int32_t st = step[0];
-    const double s = (double)(advanced ? st : st + 1);
-    const float step_size = (float)(lr / (1.0 - pow(beta1, s)));
-    const float bc2_sqrt = (float)sqrt(1.0 - pow(beta2, s));
+    if (threadIdx.x == 0) {
+        const double s = (double)(advanced ? st : st + 1);
+        s_sc[0] = (float)(lr / (1.0 - pow(beta1, s)));
+        s_sc[1] = (float)sqrt(1.0 - pow(beta2, s));
+    }
+    __syncthreads();
+    const float step_size = s_sc[0], bc2_sqrt = s_sc[1];
     const float w1 = (float)(1.0 - beta1), b2 = (float)beta2, w2 = (float)(1.0 - beta2), e = (float)eps;
     const int64_t total = n + (t1 ? n2 : 0);
     // torch's elementwise kernels are built with FMA contraction; each torch op below is one
