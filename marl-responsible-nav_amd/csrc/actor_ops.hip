@@ -194,8 +194,18 @@ __global__ void __launch_bounds__(HID) prep_slices(PrepParams p) {
     const int sl = blockIdx.x, k = blockIdx.y, j = threadIdx.x;
     const float *w1 = p.net.w1 + (size_t)k * p.HW * HID;
     const int c0 = sl * 32, c1 = min(p.HW, c0 + 32);
+    // the slice's 64 loads in flight together, then the fmas in row order
+    float bv[32], wv[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+        const int c = c0 + i;
+        bv[i] = c < c1 ? p.base[c] : 0.0f;
+        wv[i] = c < c1 ? w1[(size_t)c * HID + j] : 0.0f;
+    }
     float acc = 0.0f;
-    for (int c = c0; c < c1; ++c) acc = fmaf(p.base[c], w1[(size_t)c * HID + j], acc);
+#pragma unroll
+    for (int i = 0; i < 32; ++i)
+        if (c0 + i < c1) acc = fmaf(bv[i], wv[i], acc);
     p.ws.part[((size_t)k * p.nslices + sl) * HID + j] = acc;
 }
 
@@ -204,7 +214,16 @@ __global__ void __launch_bounds__(256) prep_images(PrepParams p) {
     const int k = blockIdx.y, tid = threadIdx.x;
     if (blockIdx.x == 0 && tid < HID) {
         float part = 0.0f;
-        for (int sl = 0; sl < p.nslices; ++sl) part += p.ws.part[((size_t)k * p.nslices + sl) * HID + tid];
+        const float *ps = p.ws.part + (size_t)k * p.nslices * HID + tid;
+        int sl = 0;
+        for (; sl + 8 <= p.nslices; sl += 8) {  // 8 slices' loads in flight, added in slice order
+            float v[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = ps[(size_t)(sl + i) * HID];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) part += v[i];
+        }
+        for (; sl < p.nslices; ++sl) part += ps[(size_t)sl * HID];
         p.ws.c1[k * HID + tid] = p.net.b1[k * HID + tid] + part;
     }
     const float *w2 = p.net.w2 + (size_t)k * HID * HID;
@@ -1681,7 +1700,7 @@ gw_status gw_actor_prepare(void *env, const gw_mlp_actors *net, float *ws, void 
     p.base = src.base;
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(prep_slices, dim3(p.nslices, src.K), dim3(HID), 0, s, p);
-    hipLaunchKernelGGL(prep_images, dim3(16, src.K), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(prep_images, dim3(64, src.K), dim3(256), 0, s, p);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return err(GW_ERR_HIP, std::string("gw_actor_prepare: ") + hipGetErrorString(e));
     return GW_OK;
@@ -1828,7 +1847,7 @@ gw_status gw_patch_actor_prepare(void *env, int32_t P, const gw_mlp_actors *net,
     pp.nslices = 0;
     pp.ws = ws_layout(ws, src.K);
     pp.base = src.base;
-    hipLaunchKernelGGL(prep_images, dim3(16, src.K), dim3(256), 0, s, pp);
+    hipLaunchKernelGGL(prep_images, dim3(64, src.K), dim3(256), 0, s, pp);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return err(GW_ERR_HIP, std::string("gw_patch_actor_prepare: ") + hipGetErrorString(e));
     return GW_OK;
@@ -1872,7 +1891,7 @@ gw_status gw_cnn_prepare(void *env, const gw_cnn_actors *net, float *ws, void *s
     pp.nslices = 0;
     pp.ws = p.ws.mlp;
     pp.base = src.base;
-    hipLaunchKernelGGL(prep_images, dim3(16, src.K), dim3(256), 0, s, pp);
+    hipLaunchKernelGGL(prep_images, dim3(64, src.K), dim3(256), 0, s, pp);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return err(GW_ERR_HIP, std::string("gw_cnn_prepare: ") + hipGetErrorString(e));
     return GW_OK;
@@ -2030,7 +2049,7 @@ gw_status gw_patch_cnn_prepare(void *env, int32_t P, const gw_cnn_actors *net, f
     pp.nslices = 0;
     pp.ws = p.ws.mlp;
     pp.base = src.base;
-    hipLaunchKernelGGL(prep_images, dim3(16, src.K), dim3(256), 0, s, pp);
+    hipLaunchKernelGGL(prep_images, dim3(64, src.K), dim3(256), 0, s, pp);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return err(GW_ERR_HIP, std::string("gw_patch_cnn_prepare: ") + hipGetErrorString(e));
     return GW_OK;

@@ -294,53 +294,6 @@ __device__ __forceinline__ void z8(const float *zb, int B, int k, int r, int g, 
     z[4] = b.x; z[5] = b.y; z[6] = b.z; z[7] = b.w;
 }
 
-// ---- LDS staging of a tail's small operands (one memory round trip for all of them) -------------
-// n floats src -> LDS dst; a thread's (<= NPER) loads are all issued before its stores, and the
-// stagings of a kernel's prologue have no barrier between them, so every load of the prologue is
-// in flight at once (a dependent global round trip costs ~1-2 us: the operands live in other
-// XCDs' L2s or HBM)
-template <int NPER>
-__device__ __forceinline__ void stage_n(float *dst, const float *__restrict__ src, int n) {
-    float v[NPER];
-#pragma unroll
-    for (int j = 0; j < NPER; ++j) {
-        const int i = threadIdx.x + 256 * j;
-        v[j] = i < n ? src[i] : 0.0f;
-    }
-#pragma unroll
-    for (int j = 0; j < NPER; ++j) {
-        const int i = threadIdx.x + 256 * j;
-        if (i < n) dst[i] = v[j];
-    }
-}
-template <int OUT>
-constexpr int small_floats() { return 5 * HID + HID * OUT + ((OUT + 3) & ~3); }
-// an MLP's per-agent small parameters (LayerNorm affines, b2, W3, b3) copied into LDS at dst;
-// returns the MLP with those pointers into LDS (w1, b1, w2 stay in global memory)
-template <int OUT>
-__device__ __forceinline__ Mlp stage_small(const Mlp &m, float *dst) {
-    stage_n<1>(dst, m.lw1, HID);
-    stage_n<1>(dst + HID, m.lb1, HID);
-    stage_n<1>(dst + 2 * HID, m.b2, HID);
-    stage_n<1>(dst + 3 * HID, m.lw2, HID);
-    stage_n<1>(dst + 4 * HID, m.lb2, HID);
-    stage_n<(HID * OUT + 255) / 256>(dst + 5 * HID, m.w3, HID * OUT);
-    stage_n<1>(dst + 5 * HID + HID * OUT, m.b3, OUT);
-    Mlp s = m;
-    s.lw1 = dst;
-    s.lb1 = dst + HID;
-    s.b2 = dst + 2 * HID;
-    s.lw2 = dst + 3 * HID;
-    s.lb2 = dst + 4 * HID;
-    s.w3 = dst + 5 * HID;
-    s.b3 = dst + 5 * HID + HID * OUT;
-    return s;
-}
-// n (<= 9 MAXK HID) floats of W1 action rows into LDS, 2,304 per pass
-__device__ __forceinline__ void stage_rows(float *dst, const float *__restrict__ src, int n) {
-    for (int c0 = 0; c0 < n; c0 += 256 * 9) stage_n<9>(dst + c0, src + c0, min(n - c0, 256 * 9));
-}
-
 // save 8 features of row r to buf [K][B][128]
 __device__ __forceinline__ void put8(float *buf, int K, int B, int k, int r, int g, const float v[8]) {
     (void)K;
@@ -373,8 +326,9 @@ struct TailParams {
 
 // ---- phase 1a: target actions a'_k = GumbelSoftmax(actor_target_k(s'_k)) -------------------
 // agent kk's target action probabilities for row r (the per-row layout; all threads call it)
-__device__ __forceinline__ void target_probs(const TailParams &p, const Mlp &m, const float *ur, int kk, int r,
-                                             int rl, int g, float *s_in, float *s_out, float pr[NA]) {
+__device__ __forceinline__ void target_probs(const TailParams &p, int kk, int r, int rl, int g, float *s_in,
+                                             float *s_out, float pr[NA]) {
+    const Mlp m = mlp_k(p.actor_t, kk, p.D, NA);
     float z[8], xh[8], y[8], rs;
     z8(p.z_a, p.B, kk, r, g, z);
     ln_relu(z, m.lw1, m.lb1, g, xh, y, rs);
@@ -390,6 +344,7 @@ __device__ __forceinline__ void target_probs(const TailParams &p, const Mlp &m, 
         pr[a] = row_sum(s) + m.b3[a];
     }
     // GumbelSoftmax (tau 1): softmax(logits - log(-log(u + eps) + eps)), gw_gumbel_softmax's op order
+    const float *ur = p.u + ((int64_t)kk * p.B + r) * NA;
     float mx = -INFINITY;
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
@@ -411,14 +366,16 @@ __device__ __forceinline__ void target_probs(const TailParams &p, const Mlp &m, 
 struct RowFwd {
     float xh1[8], y1[8], rs1, xh2[8], y2[8], rs2;
 };
-__device__ __forceinline__ float critic_fwd(const Mlp &m, const float *zsrc, const float *aw, const TailParams &p,
-                                            int k, int r, int rl, int g, const float *act, float *s_in,
-                                            float *s_out, RowFwd &f) {
+__device__ __forceinline__ float critic_fwd(const Mlp &m, const float *zsrc, const TailParams &p, int k,
+                                            int r, int rl, int g, const float *act, float *s_in, float *s_out,
+                                            RowFwd &f) {
     float z[8];
     z8(zsrc, p.B, k, r, g, z);
-    for (int a = 0; a < NA * p.K; ++a) {  // the action rows of W1 (staged in LDS: aw), in row order
+    const int Ds = p.K * p.D;
+#pragma unroll 9
+    for (int a = 0; a < NA * p.K; ++a) {  // 9 rows' loads in flight together, fmas in row order
         const float av = act[a];
-        const float *wr = aw + a * HID + 8 * g;
+        const float *wr = m.w1 + (int64_t)(Ds + a) * HID + 8 * g;
         const float4 w0 = *reinterpret_cast<const float4 *>(wr), w1 = *reinterpret_cast<const float4 *>(wr + 4);
         z[0] = fmaf(av, w0.x, z[0]); z[1] = fmaf(av, w0.y, z[1]); z[2] = fmaf(av, w0.z, z[2]); z[3] = fmaf(av, w0.w, z[3]);
         z[4] = fmaf(av, w1.x, z[4]); z[5] = fmaf(av, w1.y, z[5]); z[6] = fmaf(av, w1.z, z[6]); z[7] = fmaf(av, w1.w, z[7]);
@@ -446,59 +403,23 @@ __device__ __forceinline__ void critic_bwd(const Mlp &m, float dq, int rl, int g
 }
 
 // ---- phase 1b: TD target from the critic target, the critic's forward, MSE gradient, backward ----
-// dynamic LDS of critic_tail: K target actors' small parameters, the critic target's and the
-// critic's, the critic target's W1 action rows (9K x 128), the block's Gumbel uniforms [K][16][9]
-inline size_t critic_tail_lds(int K) {
-    return sizeof(float) * ((size_t)K * small_floats<NA>() + 2 * small_floats<1>() + (size_t)NA * K * HID +
-                            (size_t)K * RB * NA);
-}
-inline size_t actor_tail_lds(int K) {
-    return sizeof(float) * ((size_t)small_floats<NA>() + small_floats<1>() + (size_t)NA * K * HID + RB * NA);
-}
-
 __global__ void __launch_bounds__(256) critic_tail(TailParams p) {
     __shared__ __attribute__((aligned(16))) float s_in[RB * HP];
     __shared__ __attribute__((aligned(16))) float s_out[RB * HP];
     __shared__ float s_act[RB][NA * MAXK];
-    extern __shared__ __attribute__((aligned(16))) float s_dyn[];
     const int k = blockIdx.y, tid = threadIdx.x, rl = tid >> 4, g = tid & 15;
     const int r = blockIdx.x * RB + rl;
     const int na = NA * p.K;
     const int64_t Ds = (int64_t)p.K * p.D;
-    // the prologue: every small operand of the kernel into LDS in one round trip, the row's
-    // reward and done beside them
-    float *lp = s_dyn;
-    Mlp mtgt[MAXK];
-#pragma unroll
-    for (int kk = 0; kk < MAXK; ++kk) {
-        if (kk < p.K) {
-            mtgt[kk] = stage_small<NA>(mlp_k(p.actor_t, kk, p.D, NA), lp);
-            lp += small_floats<NA>();
-        }
-    }
     // target critic on (s', a'): the target actions just computed
-    const Mlp mt = stage_small<1>(mlp_k(p.critic_t, k, p.K * p.D + na, 1), lp);
-    lp += small_floats<1>();
-    const Mlp m = stage_small<1>(mlp_k(p.critic, k, p.K * p.D + na, 1), lp);
-    lp += small_floats<1>();
-    float *s_aw = lp;  // the critic target's W1 action rows
-    stage_rows(s_aw, mt.w1 + Ds * HID, na * HID);
-    lp += na * HID;
-    float *s_u = lp;   // [K][16][9]
-#pragma unroll
-    for (int kk = 0; kk < MAXK; ++kk)
-        if (kk < p.K) stage_n<1>(s_u + kk * RB * NA, p.u + ((int64_t)kk * p.B + blockIdx.x * RB) * NA, RB * NA);
-    const float done_rk = (float)p.done[(int64_t)r * p.K + k];
-    const double rew_rk = p.reward[(int64_t)r * p.K + k];
-    __syncthreads();
+    const Mlp mt = mlp_k(p.critic_t, k, p.K * p.D + na, 1);
+    const Mlp m = mlp_k(p.critic, k, p.K * p.D + na, 1);
     // every agent's target action on this block's rows (a block per agent recomputes the others':
     // K x a small MLP instead of a launch and a round trip through x_next); agent k's go to x_next
     // too (the caller's record of a')
-#pragma unroll
-    for (int kk = 0; kk < MAXK; ++kk) {
-        if (kk >= p.K) break;
+    for (int kk = 0; kk < p.K; ++kk) {
         float pr[NA];
-        target_probs(p, mtgt[kk], s_u + (kk * RB + rl) * NA, kk, r, rl, g, s_in, s_out, pr);
+        target_probs(p, kk, r, rl, g, s_in, s_out, pr);
         if (g == 0) {
 #pragma unroll
             for (int a = 0; a < NA; ++a) s_act[rl][NA * kk + a] = pr[a];
@@ -511,10 +432,10 @@ __global__ void __launch_bounds__(256) critic_tail(TailParams p) {
     }
     __syncthreads();
     RowFwd f;
-    const float q_next = critic_fwd(mt, p.z_ct, s_aw, p, k, r, rl, g, s_act[rl], s_in, s_out, f);
+    const float q_next = critic_fwd(mt, p.z_ct, p, k, r, rl, g, s_act[rl], s_in, s_out, f);
     // y = f32(r) + ((1 - d) * gamma) * q_next, gw_td_target's op order
-    const float t1 = 1.0f - done_rk;
-    const float y = (float)rew_rk + (t1 * p.gamma) * q_next;
+    const float t1 = 1.0f - (float)p.done[(int64_t)r * p.K + k];
+    const float y = (float)p.reward[(int64_t)r * p.K + k] + (t1 * p.gamma) * q_next;
     // online critic on (s, a): the stored actions are the x rows' action slots (in the partials)
     float z[8];
     z8(p.z_c, p.B, k, r, g, z);
@@ -557,18 +478,8 @@ __global__ void __launch_bounds__(256) actor_tail(TailParams p) {
     const int r = blockIdx.x * RB + rl;
     const int na = NA * p.K;
     const int64_t Ds = (int64_t)p.K * p.D;
-    extern __shared__ __attribute__((aligned(16))) float s_dyn[];
-    // the prologue: every small operand into LDS in one round trip (as critic_tail)
-    float *lp = s_dyn;
-    const Mlp ma = stage_small<NA>(mlp_k(p.actor, k, p.D, NA), lp);
-    lp += small_floats<NA>();
-    const Mlp mc = stage_small<1>(mlp_k(p.critic, k, p.K * p.D + na, 1), lp);
-    lp += small_floats<1>();
-    float *s_aw = lp;  // the critic's W1 action rows
-    stage_rows(s_aw, mc.w1 + Ds * HID, na * HID);
-    lp += na * HID;
-    float *s_u = lp;   // [16][9] agent k's uniforms
-    stage_n<1>(s_u, p.u + ((int64_t)k * p.B + blockIdx.x * RB) * NA, RB * NA);
+    const Mlp ma = mlp_k(p.actor, k, p.D, NA);
+    const Mlp mc = mlp_k(p.critic, k, p.K * p.D + na, 1);
     // actor forward
     for (int i = tid; i < RB * na; i += 256) s_act[i / na][i % na] = p.x[(int64_t)(blockIdx.x * RB + i / na) * p.ldx + Ds + i % na];
     __syncthreads();
@@ -589,7 +500,7 @@ __global__ void __launch_bounds__(256) actor_tail(TailParams p) {
         lg[a] = row_sum(s) + ma.b3[a];
     }
     // GumbelSoftmax (tau 1) with its gradient: torch's softmax((logits - log(-log(u + eps) + eps)) / 1)
-    const float *ur = s_u + rl * NA;
+    const float *ur = p.u + ((int64_t)k * p.B + r) * NA;
     float pr[NA], mx = -INFINITY;
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
@@ -611,7 +522,7 @@ __global__ void __launch_bounds__(256) actor_tail(TailParams p) {
     if (g == 0)
         for (int a = 0; a < NA; ++a) s_act[rl][NA * k + a] = pr[a];
     RowFwd fc;
-    const float q = critic_fwd(mc, p.z_c, s_aw, p, k, r, rl, g, s_act[rl], s_in, s_out, fc);
+    const float q = critic_fwd(mc, p.z_c, p, k, r, rl, g, s_act[rl], s_in, s_out, fc);
     const float dq = -(1.0f / (float)p.B);  // -mean Q backward (gw_mean_loss_bwd mode 1)
     float gv1[8], dz1[8], gv2[8], dz2[8];
     critic_bwd(mc, dq, rl, g, fc, s_in, s_out, gv1, dz1, gv2, dz2);
@@ -619,7 +530,7 @@ __global__ void __launch_bounds__(256) actor_tail(TailParams p) {
     float dp[NA];
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
-        const float *wr = s_aw + (NA * k + a) * HID + 8 * g;
+        const float *wr = mc.w1 + (Ds + NA * k + a) * HID + 8 * g;
         float s = 0.0f;
 #pragma unroll
         for (int i = 0; i < 8; ++i) s = fmaf(dz1[i], wr[i], s);
@@ -994,17 +905,7 @@ gw_status gw_maddpg_critic_grads(const gw_mlp_actors *actor_target, const gw_mlp
     tp.K = K;
     tp.B = B;
     tp.D = D;
-    {
-        const size_t lds = critic_tail_lds(K);
-        static size_t granted = 0;  // the dynamic-LDS limit raised once to the largest K seen
-        if (lds > granted) {
-            if (hipFuncSetAttribute(reinterpret_cast<const void *>(&critic_tail),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-                return fail(GW_ERR_HIP, who + ": LDS attribute");
-            granted = lds;
-        }
-        hipLaunchKernelGGL(critic_tail, dim3(B / RB, K), dim3(256), lds, s, tp);
-    }
+    hipLaunchKernelGGL(critic_tail, dim3(B / RB, K), dim3(256), 0, s, tp);
     GradParams gp{};
     gp.grad = *critic_grad;
     gp.x = batch->x;
@@ -1062,17 +963,7 @@ gw_status gw_maddpg_actor_grads(const gw_mlp_actors *actor, const gw_mlp_actors 
     tp.B = B;
     tp.D = D;
     tp.probs_out = probs;
-    {
-        const size_t lds = actor_tail_lds(K);
-        static size_t granted = 0;
-        if (lds > granted) {
-            if (hipFuncSetAttribute(reinterpret_cast<const void *>(&actor_tail),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-                return fail(GW_ERR_HIP, who + ": LDS attribute");
-            granted = lds;
-        }
-        hipLaunchKernelGGL(actor_tail, dim3(B / RB, K), dim3(256), lds, s, tp);
-    }
+    hipLaunchKernelGGL(actor_tail, dim3(B / RB, K), dim3(256), 0, s, tp);
     GradParams gp{};
     gp.grad = *actor_grad;
     gp.x = batch->x;
