@@ -359,6 +359,27 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a, unsign
     }
 }
 
+// measurement only (GW_PATCH_MODE=9): the same grid, block size and run layout as the writers,
+// every element of the step's windows stored as 0 with aligned float4 stores and no staging: the
+// store floor of this launch shape
+template <int PB>
+__global__ void __launch_bounds__(THREADS) store_floor_kernel(gw::PatchArgs a) {
+    const int PP = a.P * a.P;
+    const int64_t e0 = (int64_t)blockIdx.x * PB;
+    const int nenv = (int)min((int64_t)PB, a.E - e0);
+    const int len = nenv * PP;
+    for (int k = 0; k < a.K; ++k) {
+        const int64_t off = ((int64_t)k * a.E + e0) * PP;
+        float *o = a.patch + off;
+        const int lead = (int)((4 - (off & 3)) & 3);
+        for (int i = threadIdx.x; i < min(lead, len); i += THREADS) o[i] = 0.0f;
+        const int n4 = (len - lead) / 4;
+        float4 *o4 = reinterpret_cast<float4 *>(o + lead);
+        for (int j = threadIdx.x; j < n4; j += THREADS) o4[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        for (int i = lead + 4 * n4 + threadIdx.x; i < len; i += THREADS) o[i] = 0.0f;
+    }
+}
+
 }  // namespace
 
 namespace gw {
@@ -405,6 +426,14 @@ hipError_t launch_windows(const PatchArgs &a, hipStream_t s) {
         if (f == 1 || (f == 0 && PP <= 64 * MAXPL && base + extra[0] <= LDS_MAX) ||
             (f == 2 && a.P % 4 == 0 && np < 16 && base + extra[2] <= LDS_MAX) || (f == 3 && base + extra[3] <= LDS_MAX))
             mode = f;
+    }
+    if (force && std::atoi(force) == 9 && a.patch) {  // measurement only: the store floor
+        const unsigned grid = (unsigned)((a.E + PB - 1) / PB);
+        if (PB == 64)
+            gwprof::launch(store_floor_kernel<64>, dim3(grid), dim3(THREADS), 0, s, a);
+        else
+            gwprof::launch(store_floor_kernel<32>, dim3(grid), dim3(THREADS), 0, s, a);
+        return hipGetLastError();
     }
     const size_t lds = base + extra[mode];
     if (PB == 64) {
