@@ -19,6 +19,8 @@ struct PatchArgs {
     int64_t E;
     int H, W, N, K, P, variant;
     int apples[GW_MAX_AGENTS];
+    int probe = 0;  // measurement only (GW_PATCH_PROBE): 1 = MODE 3 stores zeros after its table build,
+                    // 2 = zeros right after the staging (no table)
 };
 
 hipError_t launch_windows(const PatchArgs &a, hipStream_t s);

@@ -246,6 +246,19 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a, unsign
         const int len = nenv * PP;
         const uint32_t m_pp = (uint32_t)((0x100000000ull + (uint64_t)PP - 1) / (uint64_t)PP);
         const uint32_t m_p = (uint32_t)((0x100000000ull + (uint64_t)P - 1) / (uint64_t)P);
+        if (a.probe == 2) {  // measurement only: staging, then zeros
+            for (int k = 0; k < K; ++k) {
+                const int64_t off = ((int64_t)k * a.E + e0) * PP;
+                float *o = a.patch + off;
+                const int lead = (int)((4 - (off & 3)) & 3);
+                for (int i = tid; i < min(lead, len); i += THREADS) o[i] = 0.0f;
+                const int n4 = (len - lead) / 4;
+                float4 *o4 = reinterpret_cast<float4 *>(o + lead);
+                for (int j = tid; j < n4; j += THREADS) o4[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                for (int i = lead + 4 * n4 + tid; i < len; i += THREADS) o[i] = 0.0f;
+            }
+            return;
+        }
         for (int k = 0; k < K; ++k) {
             const int64_t off = ((int64_t)k * a.E + e0) * PP;
             float *o = a.patch + off;
@@ -284,6 +297,10 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a, unsign
             const int n4 = (len - lead) / 4;
             float4 *o4 = reinterpret_cast<float4 *>(o + lead);
             for (int j = tid; j < n4; j += THREADS) {
+                if (a.probe == 1) {  // measurement only: the table was built, zeros stored
+                    reinterpret_cast<float4 *>(o + lead)[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                    continue;
+                }
                 const int i0 = lead + 4 * j;
                 int el = (int)__umulhi((uint32_t)i0, m_pp), c = i0 - el * PP;
                 int wr = (int)__umulhi((uint32_t)c, m_p), wc = c - wr * P;
@@ -402,9 +419,12 @@ hipError_t launch_mode(const PatchArgs &a, size_t lds, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_windows(const PatchArgs &a, hipStream_t s) {
+hipError_t launch_windows(const PatchArgs &args, hipStream_t s) {
+    PatchArgs a = args;
     const int np = a.N + 1, PP = a.P * a.P;
     // envs per block: 32, or 64 (GW_PATCH_PB=64, measurement only for now)
+    static const char *probe_env = std::getenv("GW_PATCH_PROBE");  // (measurement only)
+    if (probe_env) a.probe = std::atoi(probe_env);
     static const char *pb_env = std::getenv("GW_PATCH_PB");
     const int PB = (pb_env && std::atoi(pb_env) == 64) ? 64 : 32;
     // LDS: road bitmask, flags, centres, patch cells + values, and per mode: MODE 0 one agent's
