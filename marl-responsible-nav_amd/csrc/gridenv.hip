@@ -2206,6 +2206,8 @@ struct Env {
     int32_t *pos = nullptr, *t = nullptr, *prev = nullptr;
     uint32_t *flags = nullptr, *episode = nullptr, *desc = nullptr;
     uint4 *fwork = nullptr;  // deferred-FeAR records (mode 3 with FeAR on)
+    // gw_obs_patch's per-P tables of the map part of every window centre (patch_ops.hip MODE 4)
+    std::vector<std::pair<int, float *>> ptbls;
     double *score = nullptr, *fscore = nullptr;
     std::vector<void *> allocs;
     // per-launch profiling events (gw_profile)
@@ -3423,6 +3425,26 @@ gw_status gw_obs_patch(void *handle, int32_t P, float *patch, float *final_patch
     a.P = P;
     a.variant = env->variant;
     for (int k = 0; k < GW_MAX_AGENTS; ++k) a.apples[k] = k < env->K ? env->apples[k] : -1;
+    // the map part of each window comes from a table of every centre's window (built on first use
+    // of this P; up to 64 MB, e.g. 0.5 MB at 32 x 32 and P = 11, 4 MB at 64 x 64 and P = 16);
+    // GW_PATCH_TABLE=0: the table-free writers (A/B)
+    static const char *tbl_env = std::getenv("GW_PATCH_TABLE");
+    const size_t tb = gw::window_table_bytes(env->H, env->W, P);
+    if (tb <= (size_t)64 << 20 && !(tbl_env && tbl_env[0] == '0')) {
+        float *t = nullptr;
+        for (auto &pt : env->ptbls)
+            if (pt.first == P) t = pt.second;
+        if (!t) {
+            GW_TRY(dalloc(env, &t, tb / sizeof(float)));
+            HIP_TRY(gw::build_window_table(a, t, s));
+            // once per (env, P): later calls may come on other streams (a rollout's side stream)
+            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+            HIP_TRY(hipStreamIsCapturing(s, &cs));
+            if (cs == hipStreamCaptureStatusNone) HIP_TRY(hipStreamSynchronize(s));
+            env->ptbls.emplace_back(P, t);
+        }
+        a.tbl = t;
+    }
     gwprof::Span span(env, GW_SPAN_WINDOW);
     HIP_TRY(gw::launch_windows(a, s));
     return GW_OK;

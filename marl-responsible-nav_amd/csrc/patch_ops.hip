@@ -16,6 +16,7 @@
 // whole lines.  Terminal windows (few envs per step) go straight to HBM from registers.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 
@@ -99,6 +100,7 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a, unsign
             if (k == 0 && which == 0) s_flag[el] = f;
             if (which == 0) has_write &= (f & D_WRITE) != 0;
             else has_final |= (f & D_FINAL) != 0;
+            if (which == 1 && !(f & D_FINAL)) continue;  // no terminal window: nothing to stage
             const bool reset = which == 0 && (f & D_RESET);
             const uint32_t apples = which == 0 ? (f >> 8) & 0xFFu : (f >> 16) & 0xFFu;
             uint32_t words[4];
@@ -334,6 +336,30 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a, unsign
                            : map_value(s_road, H, W, (ctr >> 16) + wr - half, (ctr & 0xFFFF) + c - wr * P - half);
             }
         }
+    } else if (MODE == 4 && a.patch) {
+        // the map part of every window is a copy of the table row of its centre (one wave per
+        // window, 64 consecutive floats per store), then the patched cells are stored over it
+        // (staging left each surviving patch's window position, overridden ones at -1)
+        for (int k = 0; k < K; ++k) {
+            float *o = a.patch + ((int64_t)k * a.E + e0) * PP;
+            for (int el = wave; el < nenv; el += THREADS / 64) {
+                if (!(s_flag[el] & D_WRITE)) continue;  // wave-uniform
+                const int ctr = s_ctr[el * K + k];
+                const float *src = a.tbl + (int64_t)((ctr >> 16) * W + (ctr & 0xFFFF)) * PP;
+                float *dst = o + (int64_t)el * PP;
+                for (int c = lane; c < PP; c += 64) dst[c] = src[c];
+            }
+        }
+        // the block's map stores complete (vmcnt counts stores on gfx9) before any patch store
+        // to the same cells is issued
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        for (int t = tid; t < nenv * K * np; t += THREADS) {
+            const int slot = t / np, i = t - slot * np, el = slot / K, k = slot - el * K;
+            if (!(s_flag[el] & D_WRITE)) continue;
+            const int pw = s_pw[slot * np + i];
+            if (pw >= 0) a.patch[((int64_t)k * a.E + e0 + el) * PP + pw] = s_pv[slot * np + i];
+        }
     } else if (a.patch) {  // one thread per element (consecutive lanes: consecutive floats), overrides in registers
         // i / PP and c / P as multiply-highs (i < PB * PP; P >= 2)
         const uint32_t m_pp = (uint32_t)((0x100000000ull + (uint64_t)PP - 1) / (uint64_t)PP);
@@ -373,6 +399,18 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a, unsign
                 if (s_pw[slot * np + u] == c) v = s_pv[slot * np + u];
             o[c] = v;
         }
+    }
+}
+
+// MODE 4's table: tbl[c][o] = the map value under window position o of the window centred on
+// cell c (-1 outside the grid); built once per (env, P)
+__global__ void __launch_bounds__(256) window_table_kernel(gw::PatchArgs a, float *tbl) {
+    const int PP = a.P * a.P, half = a.P / 2;
+    const int64_t n = (int64_t)a.H * a.W * PP;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const int c = (int)(i / PP), o = (int)(i - (int64_t)c * PP);
+        const int cr = c / a.W, cc = c - cr * a.W;
+        tbl[i] = map_value(a.roadbits, a.H, a.W, cr + o / a.P - half, cc + o % a.P - half);
     }
 }
 
@@ -435,16 +473,18 @@ hipError_t launch_windows(const PatchArgs &args, hipStream_t s) {
     // byte table allows).
     const size_t base = sizeof(uint32_t) * ((a.H * a.W + 31) / 32 + PB) + sizeof(int) * 2 * PB * a.K +
                         sizeof(uint32_t) * (size_t)2 * 2 * PB * a.K * np;
-    const size_t extra[4] = {sizeof(float) * (size_t)PB * PP, 0, sizeof(uint16_t) * (size_t)PB * a.K * (PP / 4),
-                             (size_t)PB * PP + 16};
+    const size_t extra[5] = {sizeof(float) * (size_t)PB * PP, 0, sizeof(uint16_t) * (size_t)PB * a.K * (PP / 4),
+                             (size_t)PB * PP + 16, 0};
     constexpr size_t LDS_MAX = 160 * 1024;
-    int mode = (a.P % 4 == 0 && np < 16 && base + extra[2] <= LDS_MAX) ? 2
+    int mode = a.tbl ? 4
+               : (a.P % 4 == 0 && np < 16 && base + extra[2] <= LDS_MAX) ? 2
                : (np < 256 && base + extra[3] <= LDS_MAX) ? 3 : 1;
     static const char *force = std::getenv("GW_PATCH_MODE");  // (measurement only: A/B of the writers)
     if (force) {
         const int f = std::atoi(force);
         if (f == 1 || (f == 0 && PP <= 64 * MAXPL && base + extra[0] <= LDS_MAX) ||
-            (f == 2 && a.P % 4 == 0 && np < 16 && base + extra[2] <= LDS_MAX) || (f == 3 && base + extra[3] <= LDS_MAX))
+            (f == 2 && a.P % 4 == 0 && np < 16 && base + extra[2] <= LDS_MAX) || (f == 3 && base + extra[3] <= LDS_MAX) ||
+            (f == 4 && a.tbl))
             mode = f;
     }
     if (force && std::atoi(force) == 9 && a.patch) {  // measurement only: the store floor
@@ -461,6 +501,7 @@ hipError_t launch_windows(const PatchArgs &args, hipStream_t s) {
             case 0: return launch_mode<0, 64>(a, lds, s);
             case 2: return launch_mode<2, 64>(a, lds, s);
             case 3: return launch_mode<3, 64>(a, lds, s);
+            case 4: return launch_mode<4, 64>(a, lds, s);
             default: return launch_mode<1, 64>(a, lds, s);
         }
     }
@@ -468,8 +509,18 @@ hipError_t launch_windows(const PatchArgs &args, hipStream_t s) {
         case 0: return launch_mode<0, 32>(a, lds, s);
         case 2: return launch_mode<2, 32>(a, lds, s);
         case 3: return launch_mode<3, 32>(a, lds, s);
+        case 4: return launch_mode<4, 32>(a, lds, s);
         default: return launch_mode<1, 32>(a, lds, s);
     }
+}
+
+size_t window_table_bytes(int H, int W, int P) { return sizeof(float) * (size_t)H * W * P * P; }
+
+hipError_t build_window_table(const PatchArgs &a, float *tbl, hipStream_t s) {
+    const int64_t n = (int64_t)a.H * a.W * a.P * a.P;
+    const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(window_table_kernel, dim3(grid), dim3(256), 0, s, a, tbl);
+    return hipGetLastError();
 }
 
 }  // namespace gw
