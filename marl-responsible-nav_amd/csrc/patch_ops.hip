@@ -393,8 +393,9 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a, unsign
         const int slot = (PB + el) * K + k;
         const int ctr = s_ctr[slot], cr = ctr >> 16, cc = ctr & 0xFFFF;
         float *o = a.final_patch + ((int64_t)k * a.E + e0 + el) * PP;
+        const float *trow = a.tbl ? a.tbl + (int64_t)(cr * W + cc) * PP : nullptr;  // MODE 4's table
         for (int c = lane; c < PP; c += 64) {
-            float v = map_value(s_road, H, W, cr + c / P - half, cc + c % P - half);
+            float v = trow ? trow[c] : map_value(s_road, H, W, cr + c / P - half, cc + c % P - half);
             for (int u = 0; u < np; ++u)
                 if (s_pw[slot * np + u] == c) v = s_pv[slot * np + u];
             o[c] = v;
