@@ -502,8 +502,14 @@ def main():
     ev0.record(stream)
     for i in range(0, n_graph, max(graph_n, 1)):
         graph.replay()
+    t_first = []  # host time of the first eager timed steps (the pipeline fill is host-visible)
     for i in range(n_graph, args.steps):
-        one_step(i)
+        if len(t_first) < 4:
+            th = time.perf_counter()
+            one_step(i)
+            t_first.append((time.perf_counter() - th) * 1e6)
+        else:
+            one_step(i)
     t_enq = time.perf_counter() - t0  # host time to enqueue the timed steps (host-bound if ~ wall)
     if cfg.get("rollout"):
         ro._flush()  # an unjoined FeAR step's statistics and return push (fear_async)
@@ -668,6 +674,7 @@ def main():
                            "obs_async": obs_mode, "fear_async": env.fear_async,
                            "graph_steps": graph_n, "obs_ring": n_ring,
                            "host_enqueue_ms_per_step": t_enq * 1e3 / args.steps,
+                           "host_first_steps_us": [round(x, 1) for x in t_first],
                            "spans_from": f"{n_prof} eager steps after the timed region"},
             "last_step_episodes": {"completed": stats[1], "mean_return": stats[0] / max(stats[1], 1.0),
                          "mean_len": stats[6] / max(stats[1], 1.0)},

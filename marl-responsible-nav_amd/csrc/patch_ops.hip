@@ -340,14 +340,31 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a, unsign
         // the map part of every window is a copy of the table row of its centre (one wave per
         // window, 64 consecutive floats per store), then the patched cells are stored over it
         // (staging left each surviving patch's window position, overridden ones at -1)
+        // thread = consecutive cells of the block's run (coalesced loads and stores), U of them in
+        // flight per thread before any is stored
+        constexpr int U = 8;
+        const uint32_t m_pp = (uint32_t)((0x100000000ull + (uint64_t)PP - 1) / (uint64_t)PP);
+        const int len = nenv * PP;
         for (int k = 0; k < K; ++k) {
             float *o = a.patch + ((int64_t)k * a.E + e0) * PP;
-            for (int el = wave; el < nenv; el += THREADS / 64) {
-                if (!(s_flag[el] & D_WRITE)) continue;  // wave-uniform
-                const int ctr = s_ctr[el * K + k];
-                const float *src = a.tbl + (int64_t)((ctr >> 16) * W + (ctr & 0xFFFF)) * PP;
-                float *dst = o + (int64_t)el * PP;
-                for (int c = lane; c < PP; c += 64) dst[c] = src[c];
+            for (int b0 = 0; b0 < len; b0 += THREADS * U) {
+                float v[U];
+                bool w[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int i = b0 + tid + THREADS * u;
+                    w[u] = false;
+                    v[u] = 0.0f;
+                    if (i < len) {
+                        const int el = (int)__umulhi((uint32_t)i, m_pp), c = i - el * PP;
+                        w[u] = (s_flag[el] & D_WRITE) != 0;
+                        const int ctr = s_ctr[el * K + k];
+                        if (w[u]) v[u] = a.tbl[(int64_t)((ctr >> 16) * W + (ctr & 0xFFFF)) * PP + c];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (w[u]) o[b0 + tid + THREADS * u] = v[u];
             }
         }
         // the block's map stores complete (vmcnt counts stores on gfx9) before any patch store
