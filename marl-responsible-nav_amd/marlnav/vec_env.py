@@ -142,6 +142,7 @@ class VecGridEnv:
         )
         self._step_out = _lib.GwStepOut(*[_ptr(self.out[n]) for n in _lib.STEP_OUT_FIELDS])
         self._into_cache = {}  # step(): (GwStepOut, fields, StepResult) per set of destination buffers
+        self._into_sizes = None  # the destination sizes step(into=...) checks (built on first use)
         self._dev_index = self.device.index
         self._closed = False
         self._obs_queued = False  # async obs: the last step's writer not yet launched / fenced
@@ -221,8 +222,11 @@ class VecGridEnv:
         if over:
             so = _lib.GwStepOut.from_buffer_copy(self._step_out)
             res = dict(self.out)
-            sizes = {"KEHW": self.K * self.E * self.H * self.W, "EK": self.E * self.K, "E": self.E, "ONE": 1,
-                     "ROWS": int(self.lib.gw_stats_rows(self.handle)) * _lib.GW_STATS}
+            sizes = self._into_sizes
+            if sizes is None:
+                sizes = self._into_sizes = {"KEHW": self.K * self.E * self.H * self.W, "EK": self.E * self.K,
+                                            "E": self.E, "ONE": 1,
+                                            "ROWS": int(self.lib.gw_stats_rows(self.handle)) * _lib.GW_STATS}
             for name, t in over.items():
                 dt, shp = self._INTO_SPEC[name]
                 if shp == "KEHW":
