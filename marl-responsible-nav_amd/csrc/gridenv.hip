@@ -3425,12 +3425,12 @@ gw_status gw_obs_patch(void *handle, int32_t P, float *patch, float *final_patch
     a.P = P;
     a.variant = env->variant;
     for (int k = 0; k < GW_MAX_AGENTS; ++k) a.apples[k] = k < env->K ? env->apples[k] : -1;
-    // the map part of each window comes from a table of every centre's window (built on first use
-    // of this P; up to 64 MB, e.g. 0.5 MB at 32 x 32 and P = 11, 4 MB at 64 x 64 and P = 16);
+    // the map part of each window (P <= 16) comes from a table of every centre's window (built on
+    // first use of this P; 0.5 MB at 32 x 32 and P = 11, 4 MB at 64 x 64 and P = 16);
     // GW_PATCH_TABLE=0: the table-free writers (A/B)
     static const char *tbl_env = std::getenv("GW_PATCH_TABLE");
     const size_t tb = gw::window_table_bytes(env->H, env->W, P);
-    if (tb <= (size_t)64 << 20 && !(tbl_env && tbl_env[0] == '0')) {
+    if (P * P <= 256 && tb <= (size_t)64 << 20 && !(tbl_env && tbl_env[0] == '0')) {
         float *t = nullptr;
         for (auto &pt : env->ptbls)
             if (pt.first == P) t = pt.second;

@@ -340,31 +340,35 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a, unsign
         // the map part of every window is a copy of the table row of its centre (one wave per
         // window, 64 consecutive floats per store), then the patched cells are stored over it
         // (staging left each surviving patch's window position, overridden ones at -1)
-        // thread = consecutive cells of the block's run (coalesced loads and stores), U of them in
-        // flight per thread before any is stored
-        constexpr int U = 8;
-        const uint32_t m_pp = (uint32_t)((0x100000000ull + (uint64_t)PP - 1) / (uint64_t)PP);
-        const int len = nenv * PP;
-        for (int k = 0; k < K; ++k) {
-            float *o = a.patch + ((int64_t)k * a.E + e0) * PP;
-            for (int b0 = 0; b0 < len; b0 += THREADS * U) {
-                float v[U];
-                bool w[U];
+        // one wave per window (64 consecutive floats per load / store), WB windows' loads in flight
+        // per lane before their stores (a dependent load -> store per window measured 8 us per block)
+        constexpr int WB = 4, CPL = 4;  // windows per batch, cells per lane per window (P * P <= 256)
+        const int nwin = nenv * K;      // window slot = el * K + k
+        for (int w0 = wave; w0 < nwin; w0 += (THREADS / 64) * WB) {
+            float v[WB][CPL];
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int i = b0 + tid + THREADS * u;
-                    w[u] = false;
-                    v[u] = 0.0f;
-                    if (i < len) {
-                        const int el = (int)__umulhi((uint32_t)i, m_pp), c = i - el * PP;
-                        w[u] = (s_flag[el] & D_WRITE) != 0;
-                        const int ctr = s_ctr[el * K + k];
-                        if (w[u]) v[u] = a.tbl[(int64_t)((ctr >> 16) * W + (ctr & 0xFFFF)) * PP + c];
-                    }
+            for (int b = 0; b < WB; ++b) {
+                const int slot = w0 + (THREADS / 64) * b;
+                const bool ok = slot < nwin && (s_flag[slot / K] & D_WRITE);
+                const int ctr = ok ? s_ctr[slot] : 0;
+                const float *src = a.tbl + (int64_t)((ctr >> 16) * W + (ctr & 0xFFFF)) * PP;
+#pragma unroll
+                for (int q = 0; q < CPL; ++q) {
+                    const int c = lane + 64 * q;
+                    v[b][q] = (ok && c < PP) ? src[c] : 0.0f;
                 }
+            }
 #pragma unroll
-                for (int u = 0; u < U; ++u)
-                    if (w[u]) o[b0 + tid + THREADS * u] = v[u];
+            for (int b = 0; b < WB; ++b) {
+                const int slot = w0 + (THREADS / 64) * b;
+                if (slot >= nwin || !(s_flag[slot / K] & D_WRITE)) continue;  // wave-uniform
+                const int el = slot / K, k = slot - el * K;
+                float *dst = a.patch + ((int64_t)k * a.E + e0 + el) * PP;
+#pragma unroll
+                for (int q = 0; q < CPL; ++q) {
+                    const int c = lane + 64 * q;
+                    if (c < PP) dst[c] = v[b][q];
+                }
             }
         }
         // the block's map stores complete (vmcnt counts stores on gfx9) before any patch store
@@ -494,7 +498,7 @@ hipError_t launch_windows(const PatchArgs &args, hipStream_t s) {
     const size_t extra[5] = {sizeof(float) * (size_t)PB * PP, 0, sizeof(uint16_t) * (size_t)PB * a.K * (PP / 4),
                              (size_t)PB * PP + 16, 0};
     constexpr size_t LDS_MAX = 160 * 1024;
-    int mode = a.tbl ? 4
+    int mode = (a.tbl && PP <= 256) ? 4
                : (a.P % 4 == 0 && np < 16 && base + extra[2] <= LDS_MAX) ? 2
                : (np < 256 && base + extra[3] <= LDS_MAX) ? 3 : 1;
     static const char *force = std::getenv("GW_PATCH_MODE");  // (measurement only: A/B of the writers)
@@ -502,7 +506,7 @@ hipError_t launch_windows(const PatchArgs &args, hipStream_t s) {
         const int f = std::atoi(force);
         if (f == 1 || (f == 0 && PP <= 64 * MAXPL && base + extra[0] <= LDS_MAX) ||
             (f == 2 && a.P % 4 == 0 && np < 16 && base + extra[2] <= LDS_MAX) || (f == 3 && base + extra[3] <= LDS_MAX) ||
-            (f == 4 && a.tbl))
+            (f == 4 && a.tbl && PP <= 256))
             mode = f;
     }
     if (force && std::atoi(force) == 9 && a.patch) {  // measurement only: the store floor

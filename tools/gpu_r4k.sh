@@ -1,4 +1,4 @@
-# round 4 (k): MODE 4 with batched loads; C3 driver-size host timings of the first timed steps
+# round 4 (k): MODE 4 wave-per-window with batched loads
 O=gpurun_out/r4k; mkdir -p $O
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_obs_patch.py tests/test_gpu_patch_actor.py tests/test_gpu_patch_cnn.py > $O/pytest.log 2>&1; s=$?; tail -3 $O/pytest.log; [ $s = 0 ] || exit $s
 timeout -k 10 120 python tools/patch_probe.py > $O/probe_m4.log 2>&1 && tail -6 $O/probe_m4.log &&
