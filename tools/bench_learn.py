@@ -43,6 +43,31 @@ def main():
     torch.cuda.synchronize()
     gr = (time.perf_counter() - t0) / n * 1e3
     print(f"batch {B} ({'fused' if m.fused else 'autograd'}): eager {eager:.3f} ms/update, graph {gr:.3f} ms/update")
+    if m.fused:
+        # the update alone, as the rollout's learner runs it: critic rows and Gumbel uniforms come
+        # with the sample (ReplayRing.sample(critic_in=True, extra_uniform=...)), so no torch
+        # cat / rand launches inside the update
+        st, ac, rw, ns, dn = batch
+        x = m._critic_in(st, ac).contiguous()
+        xn = m._critic_in(ns, torch.zeros_like(ac)).contiguous()
+        u1 = torch.rand((K, B, 9), device="cuda", generator=g)
+        u2 = torch.rand((K, B, 9), device="cuda", generator=g)
+        args = (st, ac, rw, ns, dn, u1, u2, (x, xn))
+        for _ in range(3):
+            m.learn(*args)
+        s2 = torch.cuda.Stream()
+        s2.wait_stream(torch.cuda.current_stream())
+        g2 = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s2), torch.cuda.graph(g2):
+            m.learn(*args)
+        torch.cuda.current_stream().wait_stream(s2)
+        g2.replay()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            g2.replay()
+        torch.cuda.synchronize()
+        print(f"batch {B} (fused, rows and uniforms from the sample): graph {(time.perf_counter() - t0) / n * 1e3:.3f} ms/update")
 
 
 if __name__ == "__main__":
