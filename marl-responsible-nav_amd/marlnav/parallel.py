@@ -314,8 +314,14 @@ class ReturnGather:
         ``done`` [E_local] (one rank: views of the receive slot; several: the packer's inputs)."""
         if self.distributed:
             return {"ep_return": self._ret[: self.count], "done": self._done[: self.count]}
-        rets, done = self._views(self._buf())
-        return {"ep_return": rets[: self.count], "done": done[: self.count]}
+        # one rank: the views of each receive slot, made once (a step's host enqueue is on the
+        # critical path of short runs)
+        views = self.__dict__.setdefault("_slot_views", {})
+        v = views.get(self._fill)
+        if v is None:
+            rets, done = self._views(self._buf())
+            v = views[self._fill] = {"ep_return": rets[: self.count], "done": done[: self.count]}
+        return dict(v)
 
     def push(self, ep_return: torch.Tensor | None = None, done: torch.Tensor | None = None):
         """Gather this step's returns.  Without arguments the step wrote them through
