@@ -340,35 +340,16 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a, unsign
         // the map part of every window is a copy of the table row of its centre (one wave per
         // window, 64 consecutive floats per store), then the patched cells are stored over it
         // (staging left each surviving patch's window position, overridden ones at -1)
-        // one wave per window (64 consecutive floats per load / store), WB windows' loads in flight
-        // per lane before their stores (a dependent load -> store per window measured 8 us per block)
-        constexpr int WB = 4, CPL = 4;  // windows per batch, cells per lane per window (P * P <= 256)
-        const int nwin = nenv * K;      // window slot = el * K + k
-        for (int w0 = wave; w0 < nwin; w0 += (THREADS / 64) * WB) {
-            float v[WB][CPL];
-#pragma unroll
-            for (int b = 0; b < WB; ++b) {
-                const int slot = w0 + (THREADS / 64) * b;
-                const bool ok = slot < nwin && (s_flag[slot / K] & D_WRITE);
-                const int ctr = ok ? s_ctr[slot] : 0;
+        // one wave per window: 64 consecutive floats per load and store (batching several windows'
+        // loads per lane measured slower: 33.4 vs 28.9 us at c5patch's shape, profiles/r4_window)
+        for (int k = 0; k < K; ++k) {
+            float *o = a.patch + ((int64_t)k * a.E + e0) * PP;
+            for (int el = wave; el < nenv; el += THREADS / 64) {
+                if (!(s_flag[el] & D_WRITE)) continue;  // wave-uniform
+                const int ctr = s_ctr[el * K + k];
                 const float *src = a.tbl + (int64_t)((ctr >> 16) * W + (ctr & 0xFFFF)) * PP;
-#pragma unroll
-                for (int q = 0; q < CPL; ++q) {
-                    const int c = lane + 64 * q;
-                    v[b][q] = (ok && c < PP) ? src[c] : 0.0f;
-                }
-            }
-#pragma unroll
-            for (int b = 0; b < WB; ++b) {
-                const int slot = w0 + (THREADS / 64) * b;
-                if (slot >= nwin || !(s_flag[slot / K] & D_WRITE)) continue;  // wave-uniform
-                const int el = slot / K, k = slot - el * K;
-                float *dst = a.patch + ((int64_t)k * a.E + e0 + el) * PP;
-#pragma unroll
-                for (int q = 0; q < CPL; ++q) {
-                    const int c = lane + 64 * q;
-                    if (c < PP) dst[c] = v[b][q];
-                }
+                float *dst = o + (int64_t)el * PP;
+                for (int c = lane; c < PP; c += 64) dst[c] = src[c];
             }
         }
         // the block's map stores complete (vmcnt counts stores on gfx9) before any patch store
@@ -498,8 +479,10 @@ hipError_t launch_windows(const PatchArgs &args, hipStream_t s) {
     const size_t extra[5] = {sizeof(float) * (size_t)PB * PP, 0, sizeof(uint16_t) * (size_t)PB * a.K * (PP / 4),
                              (size_t)PB * PP + 16, 0};
     constexpr size_t LDS_MAX = 160 * 1024;
-    int mode = (a.tbl && PP <= 256) ? 4
-               : (a.P % 4 == 0 && np < 16 && base + extra[2] <= LDS_MAX) ? 2
+    // MODE 2 for P % 4 == 0 (c4patch: 171 us per step vs 179 with MODE 4), MODE 4 for the other
+    // P <= 16 (c5patch's P = 11: 28.9 us per launch vs MODE 3's 34.2), profiles/r4_window
+    int mode = (a.P % 4 == 0 && np < 16 && base + extra[2] <= LDS_MAX) ? 2
+               : (a.tbl && PP <= 256) ? 4
                : (np < 256 && base + extra[3] <= LDS_MAX) ? 3 : 1;
     static const char *force = std::getenv("GW_PATCH_MODE");  // (measurement only: A/B of the writers)
     if (force) {
