@@ -1,52 +1,21 @@
-"""Timeline of a short bench run from a rocprofv3 kernel trace (run_kernel_trace.csv): where the
-driver-size run's time goes beyond the steady-state period (pipeline fill, drain, host gaps).
-
-Usage: python tools/timeline.py <run_kernel_trace.csv> [timed_steps]
-Splits the trace at its largest idle gap after the first 10% of kernels (the synchronize that
-opens the timed region), then prints, for the kernels after it: the first start, the obs-writer
-launches' starts / ends, the steady period (median writer start-to-start), and the excess of the
-span over timed_steps x period, attributed to the head (first start -> first writer start) and the
-tail (last writer start -> last end)."""
+"""Per-step kernel timeline from a rocprofv3 kernel trace CSV (start/end relative to the step's
+first kernel, in us), to see which launches overlap and what sits on the critical path.
+    python tools/timeline.py run_kernel_trace.csv [first_kernel_substring] [n_steps]"""
 import csv
-import statistics
 import sys
 
 
-def main():
-    path = sys.argv[1]
-    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-    rows = []
-    with open(path) as f:
-        for r in csv.DictReader(f):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
-    rows.sort()
-    lo = max(1, len(rows) // 10)
-    gaps = [(rows[i][0] - max(e for _, e, _ in rows[:i]), i) for i in range(lo, len(rows))]
-    gap, cut = max(gaps)
-    tail = rows[cut:]
-    t0 = tail[0][0]
-    writers = [(s, e) for s, e, n in tail if "obs_kernel" in n or "step_obs" in n]
-    print(f"split at kernel {cut} of {len(rows)} after an idle gap of {gap / 1e3:.1f} us")
-    if not writers:
-        print("no obs writer launches after the split")
-        return
-    starts = [s for s, _ in writers]
-    period = statistics.median([b - a for a, b in zip(starts, starts[1:])]) if len(starts) > 1 else 0
-    end = max(e for _, e, _ in tail)
-    span = end - t0
-    print(f"kernels after the split: {len(tail)}, writer launches: {len(writers)}")
-    print(f"span first start -> last end: {span / 1e3:.1f} us; steady writer period {period / 1e3:.1f} us; "
-          f"{steps} x period = {steps * period / 1e3:.1f} us; excess {(span - steps * period) / 1e3:.1f} us")
-    print(f"head: first kernel -> first writer start {(starts[0] - t0) / 1e3:.1f} us")
-    print(f"tail: last writer start -> last kernel end {(end - starts[-1]) / 1e3:.1f} us "
-          f"(last writer lasts {(writers[-1][1] - writers[-1][0]) / 1e3:.1f} us)")
-    print("first kernels after the split:")
-    for s, e, n in tail[:8]:
-        print(f"  {(s - t0) / 1e3:8.1f} .. {(e - t0) / 1e3:8.1f} us  {n[:70]}")
-    print("last kernels:")
-    for s, e, n in tail[-6:]:
-        print(f"  {(s - t0) / 1e3:8.1f} .. {(e - t0) / 1e3:8.1f} us  {n[:70]}")
+def main(path, anchor="step_v2", nsteps=3):
+    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+    starts = [i for i, r in enumerate(rows) if anchor in r["Kernel_Name"]]
+    mid = starts[len(starts) // 2: len(starts) // 2 + nsteps + 1]
+    for a, b in zip(mid, mid[1:]):
+        t0 = int(rows[a]["Start_Timestamp"])
+        print(f"--- step (period {(int(rows[b]['Start_Timestamp']) - t0) / 1e3:.1f} us)")
+        for r in rows[a:b]:
+            s, e = (int(r["Start_Timestamp"]) - t0) / 1e3, (int(r["End_Timestamp"]) - t0) / 1e3
+            print(f"  q{r['Queue_Id']:>2} {s:8.1f} -> {e:8.1f} ({e - s:7.1f})  {r['Kernel_Name'][:70]}")
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1], *(sys.argv[2:3] or ["step_v2"]), *(map(int, sys.argv[3:4]) if len(sys.argv) > 3 else []))
