@@ -99,6 +99,10 @@ typedef struct gw_step_out {
                             (a running total without a per-step reduction launch; one
                             block owns each row, so the sums are deterministic)          */
     int64_t *tick;       /* [1]   += 1 per gw_step (e.g. the replay ring's step count)   */
+    uint32_t *desc_copy; /* [E][12] a second destination of the step's obs descriptors
+                            (gw_obs_view's layout; e.g. a descriptor replay ring's slot,
+                            include/rollout_ops.h gw_replay_gather_desc); the terminal half
+                            (words 8-11) only for envs that ended                         */
 } gw_step_out;
 
 #define GW_STATS 8

@@ -702,6 +702,12 @@ __device__ __forceinline__ void store_desc(const Params &p, int64_t e, const Obs
     write_desc_pos<N>(d, oi.pos);
     d[4] = oi.flags;
     if (oi.flags & D_FINAL) write_desc_pos<N>(d + 8, oi.fpos);
+    if (p.out.desc_copy) {  // the second destination (a descriptor replay ring's slot)
+        uint32_t *c = p.out.desc_copy + e * NDESC;
+        write_desc_pos<N>(c, oi.pos);
+        c[4] = oi.flags;
+        if (oi.flags & D_FINAL) write_desc_pos<N>(c + 8, oi.fpos);
+    }
 }
 
 // DEFER (GW_KERNEL=defer, FeAR on): everything FeAR touches -- fear, shaped reward, score,

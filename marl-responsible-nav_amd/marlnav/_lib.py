@@ -147,7 +147,8 @@ class GwConfig(C.Structure):
 
 STEP_OUT_FIELDS = ["obs", "final_obs", "reward", "fear", "shaped", "term", "trunc", "done", "mask",
                    "crashes", "apples", "ep_return", "ep_fear", "ep_len", "actions", "mdr",
-                   "final_pos", "crash_bits", "restr_bits", "stats", "done_copy", "stats_acc", "tick"]
+                   "final_pos", "crash_bits", "restr_bits", "stats", "done_copy", "stats_acc", "tick",
+                   "desc_copy"]
 GW_STATS = 8
 STATS_NAMES = ["done_return", "episodes", "fear", "crashes", "apples", "shaped", "done_len", "env_steps"]
 

@@ -377,6 +377,8 @@ class Rollout:
                 into.update(stats_acc=self._acc, tick=rp.t_dev)
             if not self.patch:
                 into.update(obs=rp.obs[nxt], final_obs=rp.final_obs[cur])
+                if rp.desc is not None:  # the step kernels write the descriptors of slot nxt too
+                    into["desc_copy"] = rp.desc[nxt]
             if self.gather is not None:
                 g = self.gather.into()
                 into["ep_return"] = g["ep_return"]
@@ -393,8 +395,6 @@ class Rollout:
                 self._pev_live = True
             elif self.patch:  # the step's obs / terminal obs as patches, straight into the ring
                 env.obs_patch(self.patch, final=True, out=rp.obs[nxt], final_out=rp.final_obs[cur])
-            elif rp.desc is not None:
-                self._desc_copy(nxt)  # the descriptors of obs slot nxt (and of final-obs slot cur)
             if probs is not None and probs.data_ptr() != rp.probs[cur].data_ptr():
                 rp.probs[cur].copy_(probs)
             rp.t = self.t + 1

@@ -53,6 +53,7 @@ class StepResult:
     done_copy: torch.Tensor | None = None  # a second destination of done (step(into=...))
     stats_acc: torch.Tensor | None = None  # running per-block totals (step(into=...))
     tick: torch.Tensor | None = None       # += 1 per step (step(into=...))
+    desc_copy: torch.Tensor | None = None  # [E, 12] int32 copy of the obs descriptors (step(into=...))
 
 
 class StepGraph:
@@ -138,7 +139,7 @@ class VecGridEnv:
             crash_bits=torch.zeros(E, dtype=torch.uint8, device=dev) if debug else None,
             restr_bits=torch.zeros(E, dtype=torch.uint8, device=dev) if debug else None,
             stats=torch.zeros((int(self.lib.gw_stats_rows(self.handle)), _lib.GW_STATS), **f64) if stats else None,
-            done_copy=None, stats_acc=None, tick=None,
+            done_copy=None, stats_acc=None, tick=None, desc_copy=None,
         )
         self._step_out = _lib.GwStepOut(*[_ptr(self.out[n]) for n in _lib.STEP_OUT_FIELDS])
         self._into_cache = {}  # step(): (GwStepOut, fields, StepResult) per set of destination buffers
@@ -172,7 +173,7 @@ class VecGridEnv:
                   "reward": (torch.float64, "EK"), "fear": (torch.float64, "EK"), "shaped": (torch.float64, "EK"),
                   "term": (torch.uint8, "EK"), "trunc": (torch.uint8, "EK"), "done": (torch.uint8, "E"),
                   "done_copy": (torch.uint8, "E"), "stats_acc": (torch.float64, "ROWS"),
-                  "tick": (torch.int64, "ONE"),
+                  "tick": (torch.int64, "ONE"), "desc_copy": (torch.int32, "DESC"),
                   "ep_return": (torch.float64, "E")}
 
     def step(self, rl_actions: torch.Tensor | None = None, scripted: torch.Tensor | None = None,
@@ -225,7 +226,7 @@ class VecGridEnv:
             sizes = self._into_sizes
             if sizes is None:
                 sizes = self._into_sizes = {"KEHW": self.K * self.E * self.H * self.W, "EK": self.E * self.K,
-                                            "E": self.E, "ONE": 1,
+                                            "E": self.E, "ONE": 1, "DESC": self.E * 12,
                                             "ROWS": int(self.lib.gw_stats_rows(self.handle)) * _lib.GW_STATS}
             for name, t in over.items():
                 dt, shp = self._INTO_SPEC[name]
