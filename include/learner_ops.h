@@ -107,7 +107,10 @@ typedef struct gw_maddpg_batch {
                             * action slots by gw_maddpg_critic_grads                              */
     const double *reward;  /* [B][K] shaped rewards                                                */
     const uint8_t *done;   /* [B][K] terminations                                                  */
-    const float *u;        /* [K][B][9] the call's Gumbel uniforms (u_next, then u_cur)            */
+    const float *u;        /* [K][B][9] the call's Gumbel uniforms (u_next, then u_cur), or NULL:    */
+    uint64_t seed;         /*   drawn in the kernels, Philox4x32-10(key seed; counter (row, *ctr,     */
+    const int32_t *ctr;    /*   'GUM' + phase, 4 agent + j)); ctr: a device int32 that changes per    */
+                           /*   update (e.g. the critic optimizer's step count)                       */
 } gw_maddpg_batch;
 
 /* Workspace (floats) both calls share: layer-1 partial sums and the rows' saved activations. */

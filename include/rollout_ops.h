@@ -76,12 +76,16 @@ gw_status gw_gather_unpack(const uint8_t *recv, int64_t steps, int32_t world, in
  * x_out / xn_out (may be NULL): the critic's input rows [B, K*HW + K*9] of MADDPG.learn, agent-major
  * states then the K action slots (agilerl's torch.cat of states and actions):
  *   x_out[b] = [state[0, b] .. state[K-1, b], probs_out[0, b] .. probs_out[K-1, b]];
- *   xn_out[b][0, K*HW) = next_state[., b] (its action slots are left to the caller). */
+ *   xn_out[b][0, K*HW) = next_state[., b] (its action slots are left to the caller).
+ * u = env = NULL: u[b] and e drawn in the kernel from Philox4x32-10(key seed; counter (b, *ctr,
+ * 'SAMP', 0)) (the uniform from the first word, e = (second word * E) >> 32), as
+ * gw_replay_gather_desc does, so both samplers pick the same rows. */
 gw_status gw_replay_gather(const void *obs, const void *final_obs, int32_t obs_bf16, const float *probs,
                            const double *reward, const uint8_t *term, const uint8_t *done, const int64_t *t_dev,
                            const float *u, const int64_t *env, int64_t S, int32_t K, int64_t E, int64_t HW,
                            int64_t B, float *state, float *next_state, float *probs_out, double *reward_out,
-                           uint8_t *term_out, int64_t *tr_out, float *x_out, float *xn_out, void *stream);
+                           uint8_t *term_out, int64_t *tr_out, float *x_out, float *xn_out, uint64_t seed,
+                           const int32_t *ctr, void *stream);
 
 /* gw_replay_gather with the obs rows expanded from a ring of obs descriptors instead of read
  * from the dense obs / final_obs slots (the learner then never waits for the obs writer of the
@@ -90,12 +94,17 @@ gw_status gw_replay_gather(const void *obs, const void *final_obs, int32_t obs_b
  * (gw_obs_desc_copy after that step, into slot j); the terminal obs of transition slot tr
  * comes from the terminal half of descriptor slot tr + 1.  src: gw_obs_view of the env
  * (base map, apple cells, N, K, H, W, variant, E; its desc pointer is not used).  Every other
- * argument and output as gw_replay_gather (f32 rows; K = src->K, HW = src->H * src->W <= 4096). */
+ * argument and output as gw_replay_gather (f32 rows; K = src->K, HW = src->H * src->W <= 4096).
+ * u = env = NULL: the (transition, env) draws are made in the kernel instead of read: row b's
+ * uniform and env index from Philox4x32-10(key seed; counter (b, *ctr, 'SAMP', 0)), the env as
+ * the multiply-high of a 32-bit draw and E (ctr: a device int32 that changes per sample, e.g.
+ * the critic optimizer's step count before the update advances it). */
 gw_status gw_replay_gather_desc(const gw_obs_source *src, const uint32_t *desc, const float *probs,
                                 const double *reward, const uint8_t *term, const uint8_t *done, const int64_t *t_dev,
                                 const float *u, const int64_t *env, int64_t S, int64_t B, float *state,
                                 float *next_state, float *probs_out, double *reward_out, uint8_t *term_out,
-                                int64_t *tr_out, float *x_out, float *xn_out, void *stream);
+                                int64_t *tr_out, float *x_out, float *xn_out, uint64_t seed, const int32_t *ctr,
+                                void *stream);
 
 /* One evaluation step's totals (customeval.py:70-133 over E episodes at once; marlnav/evaluate.py):
  * for every env e with active[e]:  counts[0] += crashes[e];  counts[1] += apples[e];

@@ -30,6 +30,7 @@
 #include <string>
 
 #include "learner_ops.h"
+#include "philox.h"
 
 namespace {
 
@@ -315,7 +316,9 @@ struct TailParams {
     float *x_next;         // [B][ldx] next states; target actions written into the action slots
     const double *reward;  // [B][K]
     const uint8_t *done;   // [B][K]
-    const float *u;        // [K][B][9] Gumbel uniforms of this phase's sample
+    const float *u;        // [K][B][9] Gumbel uniforms of this phase's sample, or null: Philox draws
+    uint64_t seed;         // (u null) key of the in-kernel draws
+    const int32_t *ctr;    // (u null) a device counter that changes per update
     const float *z_a, *z_ct, *z_c;  // layer-1 pre-activations (l1_reduce: actor-like, critic target, critic)
     Saved sv;
     float gamma;
@@ -323,6 +326,27 @@ struct TailParams {
     int K, B, D;
     float *probs_out;      // actor phase: [K][B][9] the fresh action probabilities (tests), may be null
 };
+
+// the 9 Gumbel uniforms of (agent kk, row r) in phase ph (0: the target actions, 1: the actor's
+// sample): from p.u, or Philox(seed; r, *ctr, 'GUM' + ph, 4 kk + j) when p.u is null
+__device__ __forceinline__ void gumbel_uniforms(const TailParams &p, int ph, int kk, int r, float ur[NA]) {
+    if (p.u) {
+        const float *src = p.u + ((int64_t)kk * p.B + r) * NA;
+#pragma unroll
+        for (int a = 0; a < NA; ++a) ur[a] = src[a];
+        return;
+    }
+    const uint32_t c = (uint32_t)p.ctr[0];
+#pragma unroll
+    for (int j = 0; j < (NA + 3) / 4; ++j) {
+        const uint4 d = gwrng::philox((uint32_t)r, c, gwrng::TAG_GUMBEL + (uint32_t)ph, (uint32_t)(4 * kk + j),
+                                      (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
+        const uint32_t w[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (4 * j + i < NA) ur[4 * j + i] = gwrng::unit(w[i]);
+    }
+}
 
 // ---- phase 1a: target actions a'_k = GumbelSoftmax(actor_target_k(s'_k)) -------------------
 // agent kk's target action probabilities for row r (the per-row layout; all threads call it)
@@ -344,7 +368,8 @@ __device__ __forceinline__ void target_probs(const TailParams &p, int kk, int r,
         pr[a] = row_sum(s) + m.b3[a];
     }
     // GumbelSoftmax (tau 1): softmax(logits - log(-log(u + eps) + eps)), gw_gumbel_softmax's op order
-    const float *ur = p.u + ((int64_t)kk * p.B + r) * NA;
+    float ur[NA];
+    gumbel_uniforms(p, 0, kk, r, ur);
     float mx = -INFINITY;
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
@@ -500,7 +525,8 @@ __global__ void __launch_bounds__(256) actor_tail(TailParams p) {
         lg[a] = row_sum(s) + ma.b3[a];
     }
     // GumbelSoftmax (tau 1) with its gradient: torch's softmax((logits - log(-log(u + eps) + eps)) / 1)
-    const float *ur = p.u + ((int64_t)k * p.B + r) * NA;
+    float ur[NA];
+    gumbel_uniforms(p, 1, k, r, ur);
     float pr[NA], mx = -INFINITY;
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
@@ -834,7 +860,7 @@ void launch_reduce(int K, int B, std::initializer_list<ReduceJob> jobs, hipStrea
 
 gw_status check(const gw_maddpg_batch *b, const char *who) {
     const std::string w(who);
-    if (!b || !b->x || !b->x_next || !b->u) return fail(GW_ERR_ARG, w + ": null argument");
+    if (!b || !b->x || !b->x_next || (!b->u && !b->ctr)) return fail(GW_ERR_ARG, w + ": null argument");
     if (b->K < 1 || b->K > MAXK) return fail(GW_ERR_ARG, w + ": K out of range");
     if (b->B < RB || b->B % RB) return fail(GW_ERR_ARG, w + ": B must be a positive multiple of 16");
     if (b->D < 1) return fail(GW_ERR_ARG, w + ": D must be >= 1");
@@ -896,6 +922,8 @@ gw_status gw_maddpg_critic_grads(const gw_mlp_actors *actor_target, const gw_mlp
     tp.reward = batch->reward;
     tp.done = batch->done;
     tp.u = batch->u;
+    tp.seed = batch->seed;
+    tp.ctr = batch->ctr;
     tp.z_a = w.z_a;
     tp.z_ct = w.z_ct;
     tp.z_c = w.z_c;
@@ -955,6 +983,8 @@ gw_status gw_maddpg_actor_grads(const gw_mlp_actors *actor, const gw_mlp_actors 
     tp.x = batch->x;
     tp.x_next = batch->x_next;
     tp.u = batch->u;
+    tp.seed = batch->seed;
+    tp.ctr = batch->ctr;
     tp.z_a = w.z_a;
     tp.z_c = w.z_c;
     tp.sv = w.sv;

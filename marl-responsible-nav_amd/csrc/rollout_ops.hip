@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <string>
 
+#include "philox.h"
 #include "rollout_ops.h"
 
 namespace {
@@ -158,17 +159,28 @@ __global__ void __launch_bounds__(256) replay_gather_kernel(
     const int64_t *__restrict__ t_dev, const float *__restrict__ u, const int64_t *__restrict__ env, int64_t S,
     int K, int64_t E, int64_t HW, int64_t B, float *__restrict__ state, float *__restrict__ next_state,
     float *__restrict__ probs_out, double *__restrict__ reward_out, uint8_t *__restrict__ term_out,
-    int64_t *__restrict__ tr_out, float *__restrict__ x_out, float *__restrict__ xn_out) {
+    int64_t *__restrict__ tr_out, float *__restrict__ x_out, float *__restrict__ xn_out, uint64_t seed,
+    const int32_t *__restrict__ ctr) {
     const int64_t b = blockIdx.x;
     const int k = blockIdx.y;
     const int64_t t = t_dev[0];
+    float ub;
+    int64_t e;
+    if (u) {
+        ub = u[b];
+        e = env[b];
+    } else {  // in-kernel draws, as replay_gather_desc_kernel
+        const uint4 r = gwrng::philox((uint32_t)b, (uint32_t)ctr[0], gwrng::TAG_SAMPLE, 0u, (uint32_t)seed,
+                                      (uint32_t)(seed >> 32));
+        ub = gwrng::unit(r.x);
+        e = (int64_t)(((uint64_t)r.y * (uint64_t)E) >> 32);
+    }
     const int64_t n = t < 1 ? 1 : (t > S - 1 ? S - 1 : t);
-    int64_t step = (int64_t)(u[b] * (float)n);  // torch: (rand * n).long(), then minimum(., n - 1)
+    int64_t step = (int64_t)(ub * (float)n);  // torch: (rand * n).long(), then minimum(., n - 1)
     if (step > n - 1) step = n - 1;
     int64_t tr = (t - 1 - step) % S;
     if (tr < 0) tr += S;  // Python / torch modulo
     const int64_t nx = (tr + 1) % S;
-    const int64_t e = env[b];
     const bool dn = done[tr * E + e] != 0;
     const int64_t src = ((tr * K + k) * E + e) * HW;
     const int64_t nsrc = dn ? src : ((nx * K + k) * E + e) * HW;
@@ -261,7 +273,7 @@ __global__ void __launch_bounds__(256) replay_gather_desc_kernel(
     const float *__restrict__ u, const int64_t *__restrict__ env, int64_t S, int64_t B, float *__restrict__ state,
     float *__restrict__ next_state, float *__restrict__ probs_out, double *__restrict__ reward_out,
     uint8_t *__restrict__ term_out, int64_t *__restrict__ tr_out, float *__restrict__ x_out,
-    float *__restrict__ xn_out) {
+    float *__restrict__ xn_out, uint64_t seed, const int32_t *__restrict__ ctr) {
     __shared__ int s_pc[2][GW_MAX_AGENTS + 1];
     __shared__ float s_pv[2][GW_MAX_AGENTS + 1];
     __shared__ int s_np[2];
@@ -270,8 +282,17 @@ __global__ void __launch_bounds__(256) replay_gather_desc_kernel(
     const int64_t E = q.E, HW = q.HW;
     // wave 1
     const int64_t t = t_dev[0];
-    const float ub = u[b];
-    const int64_t e = env[b];
+    float ub;
+    int64_t e;
+    if (u) {
+        ub = u[b];
+        e = env[b];
+    } else {  // in-kernel draws: Philox(seed; row, *ctr, tag), the env by a multiply-high of E
+        const uint4 r = gwrng::philox((uint32_t)b, (uint32_t)ctr[0], gwrng::TAG_SAMPLE, 0u, (uint32_t)seed,
+                                      (uint32_t)(seed >> 32));
+        ub = gwrng::unit(r.x);
+        e = (int64_t)(((uint64_t)r.y * (uint64_t)E) >> 32);
+    }
     const float apple_map = q.apples[k] >= 0 ? q.base[q.apples[k]] : 0.0f;
     float mv[GD_CELLS];
 #pragma unroll
@@ -681,8 +702,10 @@ gw_status gw_replay_gather(const void *obs, const void *final_obs, int32_t obs_b
                            const double *reward, const uint8_t *term, const uint8_t *done, const int64_t *t_dev,
                            const float *u, const int64_t *env, int64_t S, int32_t K, int64_t E, int64_t HW,
                            int64_t B, float *state, float *next_state, float *probs_out, double *reward_out,
-                           uint8_t *term_out, int64_t *tr_out, float *x_out, float *xn_out, void *stream) {
-    if (!obs || !final_obs || !probs || !reward || !term || !done || !t_dev || !u || !env || !state || !next_state ||
+                           uint8_t *term_out, int64_t *tr_out, float *x_out, float *xn_out, uint64_t seed,
+                           const int32_t *ctr, void *stream) {
+    if (!obs || !final_obs || !probs || !reward || !term || !done || !t_dev || (!u != !env) || (!u && !ctr) ||
+        !state || !next_state ||
         !probs_out || !reward_out || !term_out || S < 2 || K <= 0 || K > 64 || E <= 0 || HW <= 0 || B < 0 ||
         B > 0x7fffffff)
         return GW_ERR_ARG;
@@ -690,7 +713,7 @@ gw_status gw_replay_gather(const void *obs, const void *final_obs, int32_t obs_b
     hipLaunchKernelGGL(replay_gather_kernel, dim3((unsigned)B, (unsigned)K), dim3(256), 0,
                        static_cast<hipStream_t>(stream), obs, final_obs, (int)obs_bf16, probs, reward, term, done,
                        t_dev, u, env, S, (int)K, E, HW, B, state, next_state, probs_out, reward_out, term_out, tr_out,
-                       x_out, xn_out);
+                       x_out, xn_out, seed, ctr);
     return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
 }
 
@@ -698,8 +721,10 @@ gw_status gw_replay_gather_desc(const gw_obs_source *src, const uint32_t *desc, 
                                 const double *reward, const uint8_t *term, const uint8_t *done, const int64_t *t_dev,
                                 const float *u, const int64_t *env, int64_t S, int64_t B, float *state,
                                 float *next_state, float *probs_out, double *reward_out, uint8_t *term_out,
-                                int64_t *tr_out, float *x_out, float *xn_out, void *stream) {
-    if (!src || !src->base || !desc || !probs || !reward || !term || !done || !t_dev || !u || !env || !state ||
+                                int64_t *tr_out, float *x_out, float *xn_out, uint64_t seed, const int32_t *ctr,
+                                void *stream) {
+    if (!src || !src->base || !desc || !probs || !reward || !term || !done || !t_dev || (!u != !env) ||
+        (!u && !ctr) || !state ||
         !next_state || !probs_out || !reward_out || !term_out || S < 2 || src->K <= 0 || src->K > GW_MAX_AGENTS ||
         src->N < src->K || src->N > GW_MAX_AGENTS || src->E <= 0 || src->H <= 0 || src->W <= 0 || B < 0 ||
         B > 0x7fffffff || (int64_t)src->H * src->W > 256 * GD_CELLS)
@@ -715,7 +740,7 @@ gw_status gw_replay_gather_desc(const gw_obs_source *src, const uint32_t *desc, 
     q.E = src->E;
     hipLaunchKernelGGL(replay_gather_desc_kernel, dim3((unsigned)B, (unsigned)q.K), dim3(256), 0,
                        static_cast<hipStream_t>(stream), q, desc, probs, reward, term, done, t_dev, u, env, S, B,
-                       state, next_state, probs_out, reward_out, term_out, tr_out, x_out, xn_out);
+                       state, next_state, probs_out, reward_out, term_out, tr_out, x_out, xn_out, seed, ctr);
     return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
 }
 

@@ -24,7 +24,8 @@ HIP_SOURCES = [os.path.join(CSRC, "gridenv.hip"), os.path.join(CSRC, "learner_op
                os.path.join(CSRC, "maddpg_ops.hip"), os.path.join(CSRC, "patch_ops.hip")]
 HEADERS = [os.path.join(INCLUDE, "gridenv.h"), os.path.join(INCLUDE, "learner_ops.h"),
            os.path.join(INCLUDE, "actor_ops.h"), os.path.join(INCLUDE, "rollout_ops.h")]
-SOURCES = HIP_SOURCES + HEADERS + [os.path.join(CSRC, "patch_ops.h"), os.path.join(CSRC, "prof.h")]
+SOURCES = HIP_SOURCES + HEADERS + [os.path.join(CSRC, "patch_ops.h"), os.path.join(CSRC, "prof.h"),
+                                   os.path.join(CSRC, "philox.h")]
 OBJ_DIR = os.path.join(CSRC, "build")
 ARCH = os.environ.get("MARLNAV_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -205,7 +206,8 @@ class GwCnnActors(C.Structure):
 
 class GwMaddpgBatch(C.Structure):
     _fields_ = [("K", C.c_int32), ("B", C.c_int32), ("D", C.c_int32), ("x", C.c_void_p), ("x_next", C.c_void_p),
-                ("reward", C.c_void_p), ("done", C.c_void_p), ("u", C.c_void_p)]
+                ("reward", C.c_void_p), ("done", C.c_void_p), ("u", C.c_void_p), ("seed", C.c_uint64),
+                ("ctr", C.c_void_p)]
 
 
 def _declare(L):
@@ -296,9 +298,10 @@ def _declare(L):
     L.gw_affine_relu_bwd.argtypes = [p] * 7 + [C.c_int32, C.c_int64, C.c_int32, p]
     L.gw_affine_relu_bwd.restype = C.c_int
     L.gw_replay_gather.argtypes = [p, p, C.c_int32] + [p] * 7 + [C.c_int64, C.c_int32, C.c_int64, C.c_int64,
-                                                                  C.c_int64] + [p] * 9
+                                                                  C.c_int64] + [p] * 8 + [C.c_uint64, p, p]
     L.gw_replay_gather.restype = C.c_int
-    L.gw_replay_gather_desc.argtypes = [C.POINTER(GwObsSource)] + [p] * 8 + [C.c_int64, C.c_int64] + [p] * 9
+    L.gw_replay_gather_desc.argtypes = [C.POINTER(GwObsSource)] + [p] * 8 + [C.c_int64, C.c_int64] + [p] * 8 + \
+        [C.c_uint64, p, p]
     L.gw_replay_gather_desc.restype = C.c_int
     L.gw_obs_desc_copy.argtypes = [p, p, p]
     L.gw_obs_desc_copy.restype = C.c_int

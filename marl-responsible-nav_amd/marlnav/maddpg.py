@@ -229,6 +229,11 @@ class MADDPG:
                       and all(_fusable_net(n) for n in (self.actors.net, self.actor_targets.net, self.critics,
                                                        self.critic_targets)))
         self._fws = {}
+        # the key of the fused update's in-kernel draws (replay sample rows, Gumbel uniforms):
+        # Philox(key; row, the critic optimizer's step count, tag), one key per rank (each rank
+        # samples its own batch); the step count makes every update's draws new
+        rank = dist.get_rank(group) if self.world > 1 else 0
+        self._draw_key = (int(seed) * 0x9E3779B97F4A7C15 + 7919 * rank + 1) & 0xFFFFFFFFFFFFFFFF
         if self.world > 1:
             self.broadcast_parameters()
 
@@ -306,8 +311,15 @@ class MADDPG:
         return self._learn_finish(ctx)
 
     def _fused_batch(self, x, x_next, rewards, dones, u):
+        """u None: the kernels draw the Gumbel uniforms (Philox keyed by _draw_key and the critic
+        optimizer's step count)."""
         return _lib.GwMaddpgBatch(self.K, x.shape[0], self.H * self.W, x.data_ptr(), x_next.data_ptr(), rewards.data_ptr(),
-                                  dones.data_ptr(), u.data_ptr())
+                                  dones.data_ptr(), u.data_ptr() if u is not None else None, self._draw_key,
+                                  self.opt_critic.count.data_ptr() if u is None else None)
+
+    def _draws_in_kernel(self) -> bool:
+        """Whether the fused update draws its randomness itself (GPU, flat Adam step counts)."""
+        return self.fused and isinstance(self.opt_critic, FlatAdam)
 
     def _fused_ws(self, B: int) -> torch.Tensor:
         ws = self._fws.get(B)
@@ -330,7 +342,10 @@ class MADDPG:
         if not (x.dtype == x_next.dtype == torch.float32 and tuple(x.shape) == tuple(x_next.shape)
                 == (B, K * self.H * self.W + K * N_ACTIONS)):
             raise ValueError("critic input rows must be float32 [B, K*H*W + K*9]")
-        u = (u_next if u_next is not None else torch.rand((K, B, N_ACTIONS), device=dev)).to(torch.float32).contiguous()
+        if u_next is not None:
+            u = u_next.to(torch.float32).contiguous()
+        else:
+            u = None if self._draws_in_kernel() else torch.rand((K, B, N_ACTIONS), device=dev)
         r = rewards.to(device=dev, dtype=torch.float64).contiguous()
         d = dones.to(device=dev, dtype=torch.uint8).contiguous()
         loss = torch.empty((K,), dtype=torch.float32, device=dev)
@@ -355,7 +370,10 @@ class MADDPG:
         """Phase 2 (after the critic's Adam step) as gw_maddpg_actor_grads: 3 launches."""
         import ctypes as C
         K, B, dev = self.K, ctx["B"], self.device
-        u = (u_cur if u_cur is not None else torch.rand((K, B, N_ACTIONS), device=dev)).to(torch.float32).contiguous()
+        if u_cur is not None:
+            u = u_cur.to(torch.float32).contiguous()
+        else:
+            u = None if self._draws_in_kernel() else torch.rand((K, B, N_ACTIONS), device=dev)
         loss = torch.empty((K,), dtype=torch.float32, device=dev)
         batch = self._fused_batch(ctx["x"], ctx["x_next"], ctx["r"], ctx["d"], u)
         a, c, ag = _mlp_spec(self.actors.net), _mlp_spec(self.critics), _mlp_spec(self.actors.net, grad=True)
@@ -491,6 +509,13 @@ class MADDPG:
     def _sample(self, replay, generator=None):
         """(states, actions, rewards, next_states, dones, u_next, u_cur, critic_in) as ``learn``
         takes them (no explicit uniforms; critic_in from the gather launch on the GPU)."""
+        if self.device.type == "cuda" and generator is None and self._draws_in_kernel() \
+                and self.batch_size % 16 == 0 and self.K <= _lib.GW_MAX_AGENTS:
+            # the fused update: the sample's rows and both Gumbel samples' uniforms are drawn
+            # inside the gather launch and the tails (Philox, no torch RNG launch)
+            *batch, ci = replay.sample(self.batch_size, critic_in=True,
+                                       philox=(self._draw_key, self.opt_critic.count))
+            return (*batch, None, None, ci)
         if self.device.type == "cuda":  # the critic's input rows come from the gather launch
             # the two Gumbel samples' uniforms come from the sample's own torch.rand launch
             n = self.K * self.batch_size * N_ACTIONS

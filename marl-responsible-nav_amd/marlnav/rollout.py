@@ -87,7 +87,7 @@ class ReplayRing:
 
     @torch.no_grad()
     def sample(self, batch: int, generator: torch.Generator | None = None, return_idx: bool = False,
-               critic_in: bool = False, extra_uniform: int = 0):
+               critic_in: bool = False, extra_uniform: int = 0, philox: tuple | None = None):
         """Uniform transitions -> (state [K,B,H,W], probs [K,B,9], reward [B,K], next_state, term [B,K]).
         Every index is computed on the device from ``t_dev``, so a captured graph stays valid as
         the ring fills (MultiAgentReplayBuffer.sample, uniform without priorities).
@@ -97,7 +97,7 @@ class ReplayRing:
             raise RuntimeError("empty replay ring")
         dev = self.obs.device
         if dev.type == "cuda":
-            return self._sample_hip(batch, generator, return_idx, critic_in, extra_uniform, self.use_desc)
+            return self._sample_hip(batch, generator, return_idx, critic_in, extra_uniform, self.use_desc, philox)
         n = torch.clamp(self.t_dev, min=1, max=self.S - 1)
         step = torch.minimum((torch.rand((batch,), device=dev, generator=generator) * n).long(), n - 1)
         env = torch.randint(0, self.E, (batch,), device=dev, generator=generator)
@@ -115,15 +115,23 @@ class ReplayRing:
         """Whether ``sample`` expands the rows from the descriptor ring (no obs-writer wait)."""
         return self.desc is not None and self.desc_ok
 
-    def _sample_hip(self, batch, generator, return_idx, critic_in=False, extra=0, use_desc=False):
+    def _sample_hip(self, batch, generator, return_idx, critic_in=False, extra=0, use_desc=False, philox=None):
         """sample() on the GPU: the same draws (torch.rand, then torch.randint), then the index
         arithmetic and every gather in ONE launch (gw_replay_gather, include/rollout_ops.h).
         extra > 0: that many more uniforms from the same torch.rand launch, returned last (the
-        learner's Gumbel uniforms: one launch instead of three)."""
+        learner's Gumbel uniforms: one launch instead of three).
+        philox = (seed, int32 device counter): the draws are made inside the gather launch
+        (Philox keyed by seed, counter row / *counter; no torch RNG launch, so a captured update
+        has no RNG bookkeeping either); returns no extra uniforms and no env indices."""
         dev = self.obs.device
-        u_all = torch.rand((batch + int(extra),), device=dev, generator=generator)
-        u = u_all[:batch]
-        env = torch.randint(0, self.E, (batch,), device=dev, generator=generator)
+        if philox is not None:
+            seed, ctr = int(philox[0]), philox[1]
+            u = env = None
+        else:
+            seed, ctr = 0, None
+            u_all = torch.rand((batch + int(extra),), device=dev, generator=generator)
+            u = u_all[:batch]
+            env = torch.randint(0, self.E, (batch,), device=dev, generator=generator)
         K, HW = self.K, self.obs.shape[-2] * self.obs.shape[-1]
         state = torch.empty((K, batch) + tuple(self.obs.shape[-2:]), device=dev, dtype=torch.float32)
         next_state = torch.empty_like(state)
@@ -138,24 +146,26 @@ class ReplayRing:
         stream = torch.cuda.current_stream(dev).cuda_stream
         outs = (state.data_ptr(), next_state.data_ptr(), probs.data_ptr(), reward.data_ptr(), term.data_ptr(),
                 tr.data_ptr() if return_idx else None, x.data_ptr() if critic_in else None,
-                xn.data_ptr() if critic_in else None, stream)
+                xn.data_ptr() if critic_in else None, seed, ctr.data_ptr() if ctr is not None else None, stream)
+        up = u.data_ptr() if u is not None else None
+        ep = env.data_ptr() if env is not None else None
         if use_desc:
             _lib.check(_lib.load().gw_replay_gather_desc(
                 C.byref(self._src), self.desc.data_ptr(), self.probs.data_ptr(), self.reward.data_ptr(),
-                self.term.data_ptr(), self.done.data_ptr(), self.t_dev.data_ptr(), u.data_ptr(), env.data_ptr(),
+                self.term.data_ptr(), self.done.data_ptr(), self.t_dev.data_ptr(), up, ep,
                 self.S, batch, *outs), "gw_replay_gather_desc")
         else:
             _lib.check(_lib.load().gw_replay_gather(
                 self.obs.data_ptr(), self.final_obs.data_ptr(), int(self.obs.dtype == torch.bfloat16),
                 self.probs.data_ptr(), self.reward.data_ptr(), self.term.data_ptr(), self.done.data_ptr(),
-                self.t_dev.data_ptr(), u.data_ptr(), env.data_ptr(), self.S, K, self.E, HW, batch, *outs),
+                self.t_dev.data_ptr(), up, ep, self.S, K, self.E, HW, batch, *outs),
                 "gw_replay_gather")
         out = (state, probs, reward, next_state, term)
         if return_idx:
             out = out + ((tr, env),)
         if critic_in:
             out = out + ((x, xn),)
-        return out + (u_all[batch:],) if extra else out
+        return out + (u_all[batch:],) if (extra and philox is None) else out
 
 
 class Rollout:
