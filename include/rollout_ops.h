@@ -98,7 +98,8 @@ gw_status gw_replay_gather(const void *obs, const void *final_obs, int32_t obs_b
  * u = env = NULL: the (transition, env) draws are made in the kernel instead of read: row b's
  * uniform and env index from Philox4x32-10(key seed; counter (b, *ctr, 'SAMP', 0)), the env as
  * the multiply-high of a 32-bit draw and E (ctr: a device int32 that changes per sample, e.g.
- * the critic optimizer's step count before the update advances it). */
+ * the critic optimizer's step count before the update advances it).  state / next_state may be
+ * NULL when x_out and xn_out are given (the fused learner reads only the critic rows). */
 gw_status gw_replay_gather_desc(const gw_obs_source *src, const uint32_t *desc, const float *probs,
                                 const double *reward, const uint8_t *term, const uint8_t *done, const int64_t *t_dev,
                                 const float *u, const int64_t *env, int64_t S, int64_t B, float *state,

@@ -329,8 +329,9 @@ __global__ void __launch_bounds__(256) replay_gather_desc_kernel(
     if (k == 0 && tid == 128 && tr_out) tr_out[b] = tr;
     __syncthreads();
     const int np0 = s_np[0], np1 = s_np[1];
-    float *so = state + (k * B + b) * HW;
-    float *no = next_state + (k * B + b) * HW;
+    // state / next_state may be NULL when the critic rows are all the caller needs
+    float *so = state ? state + (k * B + b) * HW : nullptr;
+    float *no = next_state ? next_state + (k * B + b) * HW : nullptr;
     float *xo = x_out ? x_out + b * ldx + (int64_t)k * HW : nullptr;
     float *xno = xn_out ? xn_out + b * ldx + (int64_t)k * HW : nullptr;
 #pragma unroll
@@ -342,8 +343,8 @@ __global__ void __launch_bounds__(256) replay_gather_desc_kernel(
             if (s_pc[0][j] == i) sv = s_pv[0][j];
         for (int j = 0; j < np1; ++j)
             if (s_pc[1][j] == i) nv = s_pv[1][j];
-        so[i] = sv;
-        no[i] = nv;
+        if (so) so[i] = sv;
+        if (no) no[i] = nv;
         if (xo) xo[i] = sv;
         if (xno) xno[i] = nv;
     }
@@ -724,8 +725,8 @@ gw_status gw_replay_gather_desc(const gw_obs_source *src, const uint32_t *desc, 
                                 int64_t *tr_out, float *x_out, float *xn_out, uint64_t seed, const int32_t *ctr,
                                 void *stream) {
     if (!src || !src->base || !desc || !probs || !reward || !term || !done || !t_dev || (!u != !env) ||
-        (!u && !ctr) || !state ||
-        !next_state || !probs_out || !reward_out || !term_out || S < 2 || src->K <= 0 || src->K > GW_MAX_AGENTS ||
+        (!u && !ctr) || ((!state || !next_state) && (!x_out || !xn_out)) || !probs_out || !reward_out ||
+        !term_out || S < 2 || src->K <= 0 || src->K > GW_MAX_AGENTS ||
         src->N < src->K || src->N > GW_MAX_AGENTS || src->E <= 0 || src->H <= 0 || src->W <= 0 || B < 0 ||
         B > 0x7fffffff || (int64_t)src->H * src->W > 256 * GD_CELLS)
         return GW_ERR_ARG;

@@ -122,7 +122,9 @@ class ReplayRing:
         learner's Gumbel uniforms: one launch instead of three).
         philox = (seed, int32 device counter): the draws are made inside the gather launch
         (Philox keyed by seed, counter row / *counter; no torch RNG launch, so a captured update
-        has no RNG bookkeeping either); returns no extra uniforms and no env indices."""
+        has no RNG bookkeeping either); returns no extra uniforms and no env indices, and with
+        critic_in on the descriptor ring the state / next_state tensors come back UNWRITTEN
+        (only their shapes are meaningful: the fused learner reads the critic rows)."""
         dev = self.obs.device
         if philox is not None:
             seed, ctr = int(philox[0]), philox[1]
@@ -144,7 +146,11 @@ class ReplayRing:
             x = torch.empty((batch, K * HW + K * 9), device=dev, dtype=torch.float32)
             xn = torch.empty_like(x)
         stream = torch.cuda.current_stream(dev).cuda_stream
-        outs = (state.data_ptr(), next_state.data_ptr(), probs.data_ptr(), reward.data_ptr(), term.data_ptr(),
+        # the fused learner's in-kernel-draws path reads only the critic rows: the descriptor
+        # gather then skips the [K, B, H*W] state copies (returned unwritten)
+        rows_only = philox is not None and critic_in and use_desc
+        outs = (None if rows_only else state.data_ptr(), None if rows_only else next_state.data_ptr(),
+                probs.data_ptr(), reward.data_ptr(), term.data_ptr(),
                 tr.data_ptr() if return_idx else None, x.data_ptr() if critic_in else None,
                 xn.data_ptr() if critic_in else None, seed, ctr.data_ptr() if ctr is not None else None, stream)
         up = u.data_ptr() if u is not None else None
