@@ -447,7 +447,7 @@ def main():
             if args.updates_per_step and learner is not None and ro.replay.t >= 2:
                 ro.learn_fence()  # sampling reads the ring's descriptor (or obs) slots
                 if learner._graph is None:
-                    learner.capture(ro.replay)
+                    learner.capture(ro.replay, actor_env=env if ro.fused and not cfg.get("patch") else None)
                 for _ in range(args.updates_per_step):
                     learner.replay_learn()
             return r

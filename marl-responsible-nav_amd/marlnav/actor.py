@@ -435,6 +435,54 @@ class MultiAgentActors(nn.Module):
         return (net.n_layers == 3 and net.weights[0].shape[-1] == 128 and net.weights[1].shape == (self.K, 128, 128)
                 and net.weights[2].shape[-1] == N_ACTIONS and net.in_dim == env.H * env.W)
 
+    def _ws_key(self):
+        # the workspace (c1 = b1 + map . W1, W2/W3 operand images) is derived once per parameter
+        # version: torch in-place ops bump the flat buffer's version counter, the HIP optimizer
+        # (marlnav/maddpg.py) and graph replays bump net.epoch (mark_updated); every layer is a
+        # view of the flat buffer, so its address pins the layer pointers
+        flat = self.net.flat_params()
+        return (flat._version, self.net.epoch, self.net.layer_norm, flat.data_ptr())
+
+    def _prepare(self, env, st):
+        """Enqueue the fused path's workspace derivation (gw_actor_prepare /
+        gw_patch_actor_prepare) on the current stream."""
+        from . import _lib
+        net, K, dev, patch = self.net, self.K, env.device, st.get("patch", 0)
+        ln = net.layer_norm
+        ptrs = (net.weights[0], net.biases[0], net.ln_w[0], net.ln_b[0], net.weights[1], net.biases[1],
+                net.ln_w[1], net.ln_b[1], net.weights[2], net.biases[2])
+        st["spec"] = _lib.GwMlpActors(K, net.in_dim, 128, N_ACTIONS, int(ln),
+                                      *[t.data_ptr() if (ln or i % 4 < 2 or i >= 8) else None
+                                        for i, t in enumerate(ptrs)])
+        with torch.cuda.device(dev):
+            if patch:
+                _lib.check(st["lib"].gw_patch_actor_prepare(env.handle, patch, C.byref(st["spec"]),
+                                                            st["ws"].data_ptr(),
+                                                            torch.cuda.current_stream(dev).cuda_stream),
+                           "gw_patch_actor_prepare")
+            else:
+                _lib.check(st["lib"].gw_actor_prepare(env.handle, C.byref(st["spec"]), st["ws"].data_ptr(),
+                                                      torch.cuda.current_stream(dev).cuda_stream),
+                           "gw_actor_prepare")
+
+    def prepare_after_update(self, env):
+        """Enqueue the workspace derivation for ``env`` now, e.g. at the end of a captured update
+        graph (after the optimizer step), so the next act_env starts on a fresh workspace without
+        a host round trip; call ``mark_prepared(env)`` after each replay of that graph.  Only for
+        an env the fused MLP path already acts on (act_env called once).  Returns the workspace
+        tensor the enqueued launches write (a captured graph must hold it), or None."""
+        st = self._fast
+        if self.arch != "mlp" or st is None or st["env"] is not env or st.get("spec") is None:
+            return None
+        self._prepare(env, st)
+        return st["ws"]
+
+    def mark_prepared(self, env):
+        """The workspace for ``env`` matches the current parameters (a replayed graph derived it)."""
+        st = self._fast
+        if st is not None and st["env"] is env:
+            st["key"] = self._ws_key()
+
     def mark_updated(self):
         """Declare the parameters changed outside torch's in-place ops (HIP optimizer, graph
         replay): the fused path re-derives its workspace before the next act_env."""
@@ -473,29 +521,9 @@ class MultiAgentActors(nn.Module):
                        else lib.gw_actor_workspace_floats(net.in_dim, K))
             st = self._fast = dict(env=env, lib=lib, ws=torch.empty(ws_n, dtype=torch.float32, device=dev), key=None,
                                    spec=None, actions=None, probs=None, patch=patch)
-        ln = net.layer_norm
-        flat = net.flat_params()
-        # the workspace (c1 = b1 + map . W1, W2/W3 operand images) is derived once per parameter
-        # version: torch in-place ops bump the flat buffer's version counter, the HIP optimizer
-        # (marlnav/maddpg.py) and graph replays bump net.epoch (mark_updated); every layer is a
-        # view of the flat buffer, so its address pins the layer pointers
-        key = (flat._version, net.epoch, ln, flat.data_ptr())
+        key = self._ws_key()
         if key != st["key"]:
-            ptrs = (net.weights[0], net.biases[0], net.ln_w[0], net.ln_b[0], net.weights[1], net.biases[1],
-                    net.ln_w[1], net.ln_b[1], net.weights[2], net.biases[2])
-            st["spec"] = _lib.GwMlpActors(K, net.in_dim, 128, N_ACTIONS, int(ln),
-                                          *[t.data_ptr() if (ln or i % 4 < 2 or i >= 8) else None
-                                            for i, t in enumerate(ptrs)])
-            with torch.cuda.device(dev):
-                if patch:
-                    _lib.check(st["lib"].gw_patch_actor_prepare(env.handle, patch, C.byref(st["spec"]),
-                                                                st["ws"].data_ptr(),
-                                                                torch.cuda.current_stream(dev).cuda_stream),
-                               "gw_patch_actor_prepare")
-                else:
-                    _lib.check(st["lib"].gw_actor_prepare(env.handle, C.byref(st["spec"]), st["ws"].data_ptr(),
-                                                          torch.cuda.current_stream(dev).cuda_stream),
-                               "gw_actor_prepare")
+            self._prepare(env, st)
             st["key"] = key
         if actions_out is None:
             actions_out = torch.empty((E, K), dtype=torch.int32, device=dev)

@@ -524,7 +524,7 @@ class MADDPG:
             return (*batch, uu[:n].view(shape), uu[n:].view(shape), ci)
         return (*replay.sample(self.batch_size, generator=generator), None, None, None)
 
-    def capture(self, replay=None, warmup: int = 3, batch: tuple | None = None):
+    def capture(self, replay=None, warmup: int = 3, batch: tuple | None = None, actor_env=None):
         """Capture sample + learn into HIP graphs (requires capturable=True and a CUDA device).
         Later ``replay_learn()`` replays them.  ``batch`` (instead of a ReplayRing): fixed input
         tensors (states, actions, rewards, next_states, dones[, u_next, u_cur]) the graphs read
@@ -532,7 +532,9 @@ class MADDPG:
         Several ranks: three graph segments sharing one memory pool (sample + critic backward |
         critic step + actor backward | actor step + soft update) with the two gradient
         all-reduces issued eagerly between their replays (a collective is not captured: the gloo
-        backend cannot be, and RCCL's own launches stay outside the graph)."""
+        backend cannot be, and RCCL's own launches stay outside the graph).
+        actor_env: the env the fused actors act on; the graph then ends with the actors' workspace
+        derivation for it (one rank), so the next act_env after a replay needs no host round trip."""
         if self.device.type != "cuda":
             raise RuntimeError("graph capture needs the GPU")
         if batch is not None:
@@ -551,8 +553,13 @@ class MADDPG:
         torch.cuda.current_stream(self.device).wait_stream(s)
         if self.world <= 1:
             g = torch.cuda.CUDAGraph()
+            self._prep_env = self._prep_ws = None
             with torch.cuda.graph(g):
                 self._graph_out = self.learn(*draw())
+                if actor_env is not None:
+                    # the graph writes this workspace on every replay: hold it as long as the graph
+                    self._prep_ws = self.actors.prepare_after_update(actor_env)
+                    self._prep_env = actor_env if self._prep_ws is not None else None
             self._graph = g
             return g
         g1, g2, g3 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
@@ -580,6 +587,8 @@ class MADDPG:
             self._graph.replay()
         for m in (self.actors, self.actor_targets):  # the replayed optimizer / soft update wrote them
             m.mark_updated()
+        if self._graphs is None and getattr(self, "_prep_env", None) is not None:
+            self.actors.mark_prepared(self._prep_env)  # the graph ended with the workspace derivation
         return self._graph_out
 
     # ---------------------------------------------------------------------------------------

@@ -97,7 +97,8 @@ class MADDPGTrainer:
         self.rollout.learn_fence()  # what the sampled transitions read (descriptor or obs slots)
         if self.use_graph:
             if self.m._graph is None:
-                self.m.capture(self.rollout.replay)
+                self.m.capture(self.rollout.replay,
+                               actor_env=self.env if self.rollout.fused and not self.rollout.patch else None)
             return self.m.replay_learn()
         return self.m.learn_from(self.rollout.replay, generator=self.gen)
 

@@ -175,6 +175,16 @@ def test_fused_act_sees_every_weight_update():
     learner.capture(ro.replay)
     learner.replay_learn()         # graph replay
     agree()
+    learner.capture(ro.replay, actor_env=env)  # the graph ends with the workspace derivation
+    assert learner._prep_env is env
+    calls = []
+    eager = learner.actors._prepare
+    learner.actors._prepare = lambda *a: (calls.append(1), eager(*a))
+    for _ in range(2):
+        learner.replay_learn()
+        agree()
+    assert not calls  # act_env did not derive the workspace again
+    learner.actors._prepare = eager
     sd = {k: v.clone() for k, v in learner.state_dict().items()}
     with torch.no_grad():
         learner.actors.net.weights[1].mul_(-1.5)  # plain in-place write through a layer view

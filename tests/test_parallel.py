@@ -101,7 +101,7 @@ def test_gloo_world2_matches_single_process(G):
     """Sharded over 2 gloo ranks (513: ragged shards, the gather pads the shorter one) ==
     one process: positions, the all-reduced statistics, and the all-gathered completed-episode
     returns (every rank gets the global list, in the reference's order: step, then env id)."""
-    steps, world = 15, 2
+    steps, world = 30, 2
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker, args=(world, _free_port(), G, steps, d), nprocs=world, join=True)
         totals = np.load(os.path.join(d, "totals.npy"))
@@ -154,3 +154,25 @@ def test_return_gather_single_process_order_and_rings():
     np.testing.assert_array_equal(small.completed(), np.array(want[-13:]))
     np.testing.assert_array_equal(big.completed(last=5), np.array(want[-5:]))
     assert int(big.n_completed) == len(want) > 13
+
+
+def test_cap_grows_on_a_growing_backlog_only():
+    """ReturnGather._adapt_from: a one-off completion burst (a backlog shrinking window by window)
+    keeps ``cap``; a backlog that grows from one window to the next, or fills an eighth of the
+    FIFO, doubles it (every rank reads the same headers, so this is the whole decision)."""
+    def run(maxbs):
+        g = ReturnGather.__new__(ReturnGather)
+        g.cap, g.emax, g.fifo_cap = 64, 4096, 2 * 64 * 4096 + 4096
+        g._maxb_host = torch.zeros(2, dtype=torch.int64)
+        g._alloc_slots = lambda: None
+        caps = []
+        for w, mb in enumerate(maxbs):
+            g._maxb_host[w % 2] = mb
+            g._nwin = w + 2
+            g._adapt_from(None)
+            caps.append(g.cap)
+        return caps
+
+    assert run([4000, 2500, 900, 0, 0]) == [64] * 5            # a burst drains at the same cap
+    assert run([100, 300, 800, 0]) == [64, 128, 256, 256]      # sustained: doubles per window
+    assert run([70000, 68000]) == [128, 256]                   # an eighth of the FIFO
