@@ -259,6 +259,8 @@ def main():
     ap.add_argument("--dense-learn", action="store_true",
                     help="with --updates-per-step: sample the dense obs slots (waiting for the obs writer) "
                          "instead of the descriptor ring (A/B)")
+    ap.add_argument("--eager-learn", action="store_true",
+                    help="with --updates-per-step: issue the update eagerly instead of replaying its HIP graph (A/B)")
     ap.add_argument("--profile-steps", type=int, default=64,
                     help="after the timed region, time this many more steps' kernels with HIP events "
                          "carried by their launches (the live roofline; 0 = none)")
@@ -446,6 +448,10 @@ def main():
             r = ro.step()  # the return gather inside is the per-step exchange across ranks
             if args.updates_per_step and learner is not None and ro.replay.t >= 2:
                 ro.learn_fence()  # sampling reads the ring's descriptor (or obs) slots
+                if args.eager_learn:  # A/B: the update's launches issued from the host each step
+                    for _ in range(args.updates_per_step):
+                        learner.learn_from(ro.replay)
+                    return r
                 if learner._graph is None:
                     learner.capture(ro.replay, actor_env=env if ro.fused and not cfg.get("patch") else None)
                 for _ in range(args.updates_per_step):

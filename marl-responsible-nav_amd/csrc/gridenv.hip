@@ -2170,6 +2170,8 @@ struct Env {
     hipStream_t last_stream = nullptr;            // merged mode: the stream of the last gw_step
     bool obs_lazy = false;                        // gw_set_obs_async(env, 2): launch at the next step
     bool obs_hi = false;                          // GW_OBS_PRIO=hi (A/B): obs stream high priority, aux normal
+    bool obs_lo = false;                          // GW_OBS_PRIO=lo (A/B): obs streams low priority (the
+                                                  // learner / actor chain on the caller's stream first)
     int obs_chunks = 1;                           // GW_OBS_CHUNKS: the obs writer as this many launches
     // one obs stream: a second one alternating with the descriptor buffer (so obs_kernel(t+1)
     // could start while obs_kernel(t) drains) measured 2.1x slower at C3 (more streams than the
@@ -2291,10 +2293,10 @@ gw_status ensure_obs_stream(Env *env) {
     if (!env->obs_stream && env->cu_split > 0) {
         GW_TRY(create_split_stream(env, &env->obs_stream, false));
     } else if (!env->obs_stream) {
-        if (env->obs_hi) {
+        if (env->obs_hi || env->obs_lo) {
             int lo = 0, hi = 0;
             HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-            HIP_TRY(hipStreamCreateWithPriority(&env->obs_stream, hipStreamNonBlocking, hi));
+            HIP_TRY(hipStreamCreateWithPriority(&env->obs_stream, hipStreamNonBlocking, env->obs_lo ? lo : hi));
         } else {
             HIP_TRY(hipStreamCreateWithFlags(&env->obs_stream, hipStreamNonBlocking));
         }
@@ -2345,10 +2347,15 @@ gw_status flush_obs(Env *env, hipEvent_t after, hipStream_t on = nullptr) {
     const bool other = env->obs_streams > 1 && env->qobs.out.obs != env->obs_last[0] &&
                        (env->qobs.out.final_obs == nullptr || env->qobs.out.final_obs != env->obs_last[1]);
     if (other && !env->obs_stream2) {
-        if (env->cu_split > 0)
+        if (env->cu_split > 0) {
             GW_TRY(create_split_stream(env, &env->obs_stream2, false));
-        else
+        } else if (env->obs_lo) {
+            int lo = 0, hi = 0;
+            HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+            HIP_TRY(hipStreamCreateWithPriority(&env->obs_stream2, hipStreamNonBlocking, lo));
+        } else {
             HIP_TRY(hipStreamCreateWithFlags(&env->obs_stream2, hipStreamNonBlocking));
+        }
     }
     if (other) env->obs_cur ^= 1;
     env->obs_last[0] = env->qobs.out.obs;
@@ -2905,6 +2912,7 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
         }
         const char *op = std::getenv("GW_OBS_PRIO");
         if (op && std::strcmp(op, "hi") == 0) env->obs_hi = true;
+        if (op && std::strcmp(op, "lo") == 0) env->obs_lo = true;
         const char *oc = std::getenv("GW_OBS_CHUNKS");
         if (oc) env->obs_chunks = std::max(1, std::min(64, std::atoi(oc)));
         const char *ch = std::getenv("GW_CHUNKS");
