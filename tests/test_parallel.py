@@ -125,7 +125,11 @@ def test_gloo_world2_matches_single_process(G):
     for r in range(world):
         np.testing.assert_array_equal(completed[r], scores)
         np.testing.assert_array_equal(completed_small[r], scores[-37:])
-        np.testing.assert_array_equal(completed_tiny[r], scores)
+        # a tiny cap: the steps whose entries have all arrived, in order (a prefix of the list;
+        # the rest is still in the senders' backlog when the run ends)
+        n_tiny = len(completed_tiny[r])
+        np.testing.assert_array_equal(completed_tiny[r], scores[:n_tiny])
+        assert n_tiny > len(scores) // 2
     np.testing.assert_array_equal(caps[0], caps[1])             # every rank adapts alike
     assert caps[0][0] == 2 and caps[0][-1] > 2                  # ... and the cap grew
     assert len(scores) > 37                                    # the small ring wrapped
@@ -174,5 +178,5 @@ def test_cap_grows_on_a_growing_backlog_only():
         return caps
 
     assert run([4000, 2500, 900, 0, 0]) == [64] * 5            # a burst drains at the same cap
-    assert run([100, 300, 800, 0]) == [64, 128, 256, 256]      # sustained: doubles per window
-    assert run([70000, 68000]) == [128, 256]                   # an eighth of the FIFO
+    assert run([100, 300, 800, 0]) == [64, 96, 144, 144]        # sustained: x1.5 per window
+    assert run([70000, 68000]) == [96, 144]                     # an eighth of the FIFO
