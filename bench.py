@@ -259,6 +259,9 @@ def main():
     ap.add_argument("--dense-learn", action="store_true",
                     help="with --updates-per-step: sample the dense obs slots (waiting for the obs writer) "
                          "instead of the descriptor ring (A/B)")
+    ap.add_argument("--learn-launches", action="store_true",
+                    help="with --updates-per-step: re-issue the captured update's recorded launches instead of "
+                         "replaying its HIP graph (MADDPG.capture(launches=True))")
     ap.add_argument("--eager-learn", action="store_true",
                     help="with --updates-per-step: issue the update eagerly instead of replaying its HIP graph (A/B)")
     ap.add_argument("--profile-steps", type=int, default=64,
@@ -453,7 +456,8 @@ def main():
                         learner.learn_from(ro.replay)
                     return r
                 if learner._graph is None:
-                    learner.capture(ro.replay, actor_env=env if ro.fused and not cfg.get("patch") else None)
+                    learner.capture(ro.replay, actor_env=env if ro.fused and not cfg.get("patch") else None,
+                                    launches=args.learn_launches)
                 for _ in range(args.updates_per_step):
                     learner.replay_learn()
             return r

@@ -372,3 +372,50 @@ def check(status: int, what: str):
     if status != 0:
         msg = load().gw_last_error().decode(errors="replace")
         raise GwError(f"{what} failed (status {status}): {msg}")
+
+
+class LaunchRecorder:
+    """Records the stream-ordered C-ABI calls made while active: every exported function whose
+    last argument is ``stream`` (the handle of the stream being recorded).  ``replay(s)`` issues
+    them again, in order, on stream ``s``, with the same arguments (ctypes structs passed by
+    reference stay alive in the recorded tuples).  Used by MADDPG.capture(launches=True): the
+    update recorded once under a graph capture (whose private pool keeps every buffer the calls
+    point at), then re-issued as plain launches instead of a graph replay."""
+
+    def __init__(self, stream: int):
+        self.stream = int(stream)
+        self.calls = []
+        self._saved = {}
+
+    def __enter__(self):
+        L = load()
+        for name in EXPORTS:
+            f = getattr(L, name, None)
+            if f is None or name in self._saved:
+                continue
+            self._saved[name] = f
+            setattr(L, name, self._wrap(name, f))
+        return self
+
+    def __exit__(self, *exc):
+        L = load()
+        for name, f in self._saved.items():
+            setattr(L, name, f)
+        self._saved = {}
+        return False
+
+    def _wrap(self, name, f):
+        def call(*args):
+            last = args[-1] if args else None
+            if isinstance(last, C.c_void_p):
+                last = last.value
+            if isinstance(last, int) and last == self.stream:
+                self.calls.append((name, f, args[:-1]))
+            return f(*args)
+        return call
+
+    def replay(self, stream: int):
+        for name, f, args in self.calls:
+            status = f(*args, stream)
+            if status:
+                check(status, name)

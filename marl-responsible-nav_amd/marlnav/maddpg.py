@@ -524,7 +524,8 @@ class MADDPG:
             return (*batch, uu[:n].view(shape), uu[n:].view(shape), ci)
         return (*replay.sample(self.batch_size, generator=generator), None, None, None)
 
-    def capture(self, replay=None, warmup: int = 3, batch: tuple | None = None, actor_env=None):
+    def capture(self, replay=None, warmup: int = 3, batch: tuple | None = None, actor_env=None,
+                launches: bool = False):
         """Capture sample + learn into HIP graphs (requires capturable=True and a CUDA device).
         Later ``replay_learn()`` replays them.  ``batch`` (instead of a ReplayRing): fixed input
         tensors (states, actions, rewards, next_states, dones[, u_next, u_cur]) the graphs read
@@ -534,7 +535,12 @@ class MADDPG:
         all-reduces issued eagerly between their replays (a collective is not captured: the gloo
         backend cannot be, and RCCL's own launches stay outside the graph).
         actor_env: the env the fused actors act on; the graph then ends with the actors' workspace
-        derivation for it (one rank), so the next act_env after a replay needs no host round trip."""
+        derivation for it (one rank), so the next act_env after a replay needs no host round trip.
+        launches (one rank, the fused update sampling ``replay`` with in-kernel draws; ignored
+        otherwise): record the capture's C-ABI
+        launches (_lib.LaunchRecorder) and have replay_learn re-issue them on the current stream
+        instead of replaying the graph (the graph is kept only for its memory pool): measured
+        faster in C5 (profiles/r4_ab) -- a graph's first node and its completion cost ~10 us each."""
         if self.device.type != "cuda":
             raise RuntimeError("graph capture needs the GPU")
         if batch is not None:
@@ -554,13 +560,26 @@ class MADDPG:
         if self.world <= 1:
             g = torch.cuda.CUDAGraph()
             self._prep_env = self._prep_ws = None
+            self._launches = None
+            # launches: only where every launch of the update goes through the C ABI (the fused
+            # update sampling a ReplayRing with in-kernel draws: no torch kernel to miss); else the graph
+            launches = launches and batch is None and self._draws_in_kernel() and \
+                self.batch_size % 16 == 0 and self.K <= _lib.GW_MAX_AGENTS
             with torch.cuda.graph(g):
-                self._graph_out = self.learn(*draw())
-                if actor_env is not None:
-                    # the graph writes this workspace on every replay: hold it as long as the graph
-                    self._prep_ws = self.actors.prepare_after_update(actor_env)
-                    self._prep_env = actor_env if self._prep_ws is not None else None
+                rec = _lib.LaunchRecorder(torch.cuda.current_stream(self.device).cuda_stream) if launches else None
+                if rec is not None:
+                    rec.__enter__()
+                try:
+                    self._graph_out = self.learn(*draw())
+                    if actor_env is not None:
+                        # the graph writes this workspace on every replay: hold it as long as the graph
+                        self._prep_ws = self.actors.prepare_after_update(actor_env)
+                        self._prep_env = actor_env if self._prep_ws is not None else None
+                finally:
+                    if rec is not None:
+                        rec.__exit__()
             self._graph = g
+            self._launches = rec
             return g
         g1, g2, g3 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1):
@@ -583,6 +602,8 @@ class MADDPG:
             g2.replay()
             self._allreduce_grads("actor")
             g3.replay()
+        elif getattr(self, "_launches", None) is not None:
+            self._launches.replay(torch.cuda.current_stream(self.device).cuda_stream)
         else:
             self._graph.replay()
         for m in (self.actors, self.actor_targets):  # the replayed optimizer / soft update wrote them

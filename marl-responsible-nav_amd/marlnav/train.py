@@ -55,7 +55,7 @@ def learn_schedule(idx_step: int, ring_t: int, ring_slots: int, global_envs: int
 
 class MADDPGTrainer:
     def __init__(self, env: VecGridEnv, maddpg: MADDPG, memory_size: int = 200_000, learning_delay: int = 0,
-                 updates_per_step: int | None = None, graph: bool = True, seed: int = 0):
+                 updates_per_step: int | None = None, graph: bool | str = True, seed: int = 0):
         self.env, self.m = env, maddpg
         # data parallelism: every decision that gates a learn() (and so its two gradient
         # all-reduces) is taken from GLOBAL quantities that every rank computes alike -- the global
@@ -77,7 +77,9 @@ class MADDPGTrainer:
                                desc_ring=fusable and env.device.type == "cuda")
         self.learning_delay = learning_delay
         self.updates_per_step = updates_per_step
-        self.use_graph = graph and env.device.type == "cuda"
+        # graph="launches": the captured update re-issued as its recorded launches (MADDPG.capture)
+        self.use_graph = bool(graph) and env.device.type == "cuda"
+        self.launches = graph == "launches"
         rank = self.rollout.group_rank()
         self.gen = torch.Generator(device=env.device).manual_seed(seed + 1 + 7919 * rank)
         self.updates = 0
@@ -98,7 +100,8 @@ class MADDPGTrainer:
         if self.use_graph:
             if self.m._graph is None:
                 self.m.capture(self.rollout.replay,
-                               actor_env=self.env if self.rollout.fused and not self.rollout.patch else None)
+                               actor_env=self.env if self.rollout.fused and not self.rollout.patch else None,
+                               launches=self.launches)
             return self.m.replay_learn()
         return self.m.learn_from(self.rollout.replay, generator=self.gen)
 

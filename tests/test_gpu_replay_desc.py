@@ -108,3 +108,31 @@ def test_training_on_desc_rows_equals_dense_rows():
         env.close()
     for k in states[0]:
         assert torch.equal(states[0][k], states[1][k]), k
+
+
+def test_update_as_recorded_launches_equals_graph_replay():
+    """MADDPG.capture(launches=True): the captured update re-issued as its recorded C-ABI
+    launches (_lib.LaunchRecorder) == the HIP graph replay, every weight bit for bit (same
+    seeds, in-kernel draws), and the replayed launches really ran (the weights moved)."""
+    from marlnav.maddpg import MADDPG
+    from marlnav.train import MADDPGTrainer
+    sc = S.builtin("grid32")
+    states = []
+    for mode in ("launches", True):
+        env = VecGridEnv(sc, num_envs=256, fear=True, fear_weight=-5.0, stats=True, seed=7, max_steps=10)
+        m = MADDPG(sc.K, sc.H, sc.W, device=env.device, seed=3, capturable=True)
+        tr = MADDPGTrainer(env, m, memory_size=2048, updates_per_step=1, graph=mode, seed=3)
+        tr.reset()
+        tr.train(6)
+        assert m._graph is not None and (m._launches is not None) == (mode == "launches")
+        if mode == "launches":
+            names = [c[0] for c in m._launches.calls]
+            assert names[0] == "gw_replay_gather_desc" and "gw_actor_prepare" in names, names
+        before = m.actors.net.flat_params().clone()
+        tr.train(18)
+        torch.cuda.synchronize()
+        assert not torch.equal(before, m.actors.net.flat_params())
+        states.append({k: v.clone() for k, v in m.state_dict().items()})
+        env.close()
+    for k in states[0]:
+        assert torch.equal(states[0][k], states[1][k]), k
