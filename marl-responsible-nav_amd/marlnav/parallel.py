@@ -142,9 +142,9 @@ class ReturnGather:
     entries sent, the backlog left, an overflow flag) and up to ``cap`` returns from the FIFO's
     head -- 32 + 8 cap bytes instead of 9 bytes per env (cap = E_local / 32 by default: 16 KB at
     65,536 envs vs 576 KB).  A step with more completions than ``cap`` leaves a backlog that the
-    next steps drain; every rank sees every header, so all ranks grow ``cap`` (x1.5) at the same window
-    boundary when the backlog grew from one window to the next (a lagged host read of an already
-    finished copy: no stall; a one-off burst drains at the same cap).  Every ``window`` steps the receiver appends each rank's entries to a mirror FIFO and
+    next steps drain; every rank sees every header, so all ranks double ``cap`` at the same window
+    boundary when the last window had one (a lagged host read of an already finished copy: no
+    stall).  Every ``window`` steps the receiver appends each rank's entries to a mirror FIFO and
     emits, in (step, rank, env) order, every step whose entries have all arrived -- with
     rank-major contiguous shards that is the reference's (step, global env id) order, bit for bit
     the list of the round-3 full gather (tests/test_parallel.py, tests/test_gpu_dist.py).
@@ -370,20 +370,14 @@ class ReturnGather:
         self._compact_torch()
 
     def _adapt_from(self, ev):
-        """Grow ``cap`` (x1.5, up to the shard) when the sender backlog is growing: the window before
-        this one peaked above the window before it (completions arrive faster than ``cap`` drains
-        them), or it filled an eighth of the FIFO.  A one-off burst (episodes that started together
-        ending together) leaves a backlog that shrinks window by window and drains at the same cap.
-        Every rank reads the same gathered headers, so all ranks decide alike; the value was copied
-        a whole window ago, so the wait is normally on a long finished event."""
+        """Grow ``cap`` (x2, up to the shard) when the window before this one left a backlog on any
+        rank.  Every rank reads the same gathered headers, so all ranks decide alike; the value was
+        copied a whole window ago, so the wait is normally on a long finished event."""
         if ev is not None:
             ev.synchronize()
         prev = int(self._maxb_host[(self._nwin - 2) % 2])
-        older, self._maxb_older = getattr(self, "_maxb_older", None), prev
-        growing = older is not None and prev > older
-        if prev > 0 and (growing or 8 * prev > self.fifo_cap) and self.cap < self.emax:
-            # x1.5: the slot is sized by cap, so a smaller step lands nearer the completion rate
-            self.cap = min(max(self.cap + 1, 3 * self.cap // 2), self.emax)
+        if prev > 0 and self.cap < self.emax:
+            self.cap = min(2 * self.cap, self.emax)
             self._alloc_slots()
 
     def _compact_hip(self):
