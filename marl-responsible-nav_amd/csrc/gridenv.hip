@@ -2170,6 +2170,9 @@ struct Env {
     hipStream_t last_stream = nullptr;            // merged mode: the stream of the last gw_step
     bool obs_lazy = false;                        // gw_set_obs_async(env, 2): launch at the next step
     bool obs_hi = false;                          // GW_OBS_PRIO=hi (A/B): obs stream high priority, aux normal
+    int obs_cus = 0;                              // GW_OBS_CUS=n (A/B): obs streams confined to n CUs
+                                                  // spread over the CU ids, the rest left to the
+                                                  // caller's stream (the learner's launches in C5)
     bool obs_lo = false;                          // GW_OBS_PRIO=lo (A/B): obs streams low priority (the
                                                   // learner / actor chain on the caller's stream first)
     int obs_chunks = 1;                           // GW_OBS_CHUNKS: the obs writer as this many launches
@@ -2252,6 +2255,20 @@ gw_status create_split_stream(Env *env, hipStream_t *out, bool chain) {
     return GW_OK;
 }
 
+// an obs stream confined to env->obs_cus CUs, spread evenly over the CU ids (GW_OBS_CUS)
+gw_status create_obs_masked_stream(Env *env, hipStream_t *out) {
+    int ncu = 0;
+    HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, env->device));
+    const int n = std::max(1, std::min(env->obs_cus, ncu));
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+    for (int i = 0; i < n; ++i) {
+        const int c = (int)((int64_t)i * ncu / n);
+        mask[c / 32] |= 1u << (c % 32);
+    }
+    HIP_TRY(hipExtStreamCreateWithCUMask(out, (uint32_t)mask.size(), mask.data()));
+    return GW_OK;
+}
+
 // the second stream and n fork/join events (timing disabled), created on first use
 // n fork/join events (timing disabled), created on first use
 gw_status ensure_events(Env *env, int n) {
@@ -2292,6 +2309,8 @@ gw_status ensure_obs_stream(Env *env) {
     if (st != GW_OK) return st;
     if (!env->obs_stream && env->cu_split > 0) {
         GW_TRY(create_split_stream(env, &env->obs_stream, false));
+    } else if (!env->obs_stream && env->obs_cus > 0) {
+        GW_TRY(create_obs_masked_stream(env, &env->obs_stream));
     } else if (!env->obs_stream) {
         if (env->obs_hi || env->obs_lo) {
             int lo = 0, hi = 0;
@@ -2349,6 +2368,8 @@ gw_status flush_obs(Env *env, hipEvent_t after, hipStream_t on = nullptr) {
     if (other && !env->obs_stream2) {
         if (env->cu_split > 0) {
             GW_TRY(create_split_stream(env, &env->obs_stream2, false));
+        } else if (env->obs_cus > 0) {
+            GW_TRY(create_obs_masked_stream(env, &env->obs_stream2));
         } else if (env->obs_lo) {
             int lo = 0, hi = 0;
             HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -2913,6 +2934,8 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
         const char *op = std::getenv("GW_OBS_PRIO");
         if (op && std::strcmp(op, "hi") == 0) env->obs_hi = true;
         if (op && std::strcmp(op, "lo") == 0) env->obs_lo = true;
+        const char *ocu = std::getenv("GW_OBS_CUS");
+        if (ocu) env->obs_cus = std::max(0, std::atoi(ocu));
         const char *oc = std::getenv("GW_OBS_CHUNKS");
         if (oc) env->obs_chunks = std::max(1, std::min(64, std::atoi(oc)));
         const char *ch = std::getenv("GW_CHUNKS");
