@@ -537,10 +537,9 @@ class MADDPG:
         actor_env: the env the fused actors act on; the graph then ends with the actors' workspace
         derivation for it (one rank), so the next act_env after a replay needs no host round trip.
         launches (one rank, the fused update sampling ``replay`` with in-kernel draws; ignored
-        otherwise): record the capture's C-ABI
-        launches (_lib.LaunchRecorder) and have replay_learn re-issue them on the current stream
-        instead of replaying the graph (the graph is kept only for its memory pool): measured
-        faster in C5 (profiles/r4_ab) -- a graph's first node and its completion cost ~10 us each."""
+        otherwise): record the C-ABI launches of one more eager update (_lib.LaunchRecorder; it
+        runs) and have replay_learn re-issue them on the current stream instead of a graph
+        replay: no wait on a graph's completion before the next launch (profiles/r4_ab)."""
         if self.device.type != "cuda":
             raise RuntimeError("graph capture needs the GPU")
         if batch is not None:
@@ -551,35 +550,49 @@ class MADDPG:
         else:
             def draw():
                 return self._sample(replay)
+        # launches: only where every launch of the update goes through the C ABI (the fused update
+        # sampling a ReplayRing with in-kernel draws: no torch kernel to miss); else the graph
+        launches = launches and self.world <= 1 and batch is None and self._draws_in_kernel() and \
+            self.batch_size % 16 == 0 and self.K <= _lib.GW_MAX_AGENTS
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
-            for _ in range(warmup):  # allocator + optimizer state warm-up outside the graph
+            # allocator + optimizer state warm-up outside the graph (the recorded update below is
+            # the last warm-up update when recording launches)
+            for _ in range(max(0, warmup - 1) if launches else warmup):
                 self.learn(*draw())
         torch.cuda.current_stream(self.device).wait_stream(s)
         if self.world <= 1:
-            g = torch.cuda.CUDAGraph()
             self._prep_env = self._prep_ws = None
             self._launches = None
-            # launches: only where every launch of the update goes through the C ABI (the fused
-            # update sampling a ReplayRing with in-kernel draws: no torch kernel to miss); else the graph
-            launches = launches and batch is None and self._draws_in_kernel() and \
-                self.batch_size % 16 == 0 and self.K <= _lib.GW_MAX_AGENTS
-            with torch.cuda.graph(g):
-                rec = _lib.LaunchRecorder(torch.cuda.current_stream(self.device).cuda_stream) if launches else None
-                if rec is not None:
-                    rec.__enter__()
-                try:
-                    self._graph_out = self.learn(*draw())
+            if launches:
+                # recorded from one more eager update (it runs): its buffers come from the ordinary
+                # allocator and are held here for as long as the recording is replayed
+                rec = _lib.LaunchRecorder(torch.cuda.current_stream(self.device).cuda_stream)
+                with rec:
+                    b = draw()
+                    st, ac, rw, ns, dn, un, uc, ci = b
+                    ctx = self._learn_critic(st, ac, rw, ns, dn, un, ci)
+                    self._learn_actor(ctx, uc)
+                    self._graph_out = self._learn_finish(ctx)
                     if actor_env is not None:
-                        # the graph writes this workspace on every replay: hold it as long as the graph
                         self._prep_ws = self.actors.prepare_after_update(actor_env)
                         self._prep_env = actor_env if self._prep_ws is not None else None
-                finally:
-                    if rec is not None:
-                        rec.__exit__()
+                for m in (self.actors, self.actor_targets):
+                    m.mark_updated()
+                if self._prep_env is not None:
+                    self.actors.mark_prepared(self._prep_env)
+                self._launch_keep = (b, ctx)
+                self._graph = self._launches = rec
+                return rec
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._graph_out = self.learn(*draw())
+                if actor_env is not None:
+                    # the graph writes this workspace on every replay: hold it as long as the graph
+                    self._prep_ws = self.actors.prepare_after_update(actor_env)
+                    self._prep_env = actor_env if self._prep_ws is not None else None
             self._graph = g
-            self._launches = rec
             return g
         g1, g2, g3 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1):
