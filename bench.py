@@ -260,8 +260,10 @@ def main():
                     help="with --updates-per-step: sample the dense obs slots (waiting for the obs writer) "
                          "instead of the descriptor ring (A/B)")
     ap.add_argument("--learn-launches", action="store_true",
-                    help="with --updates-per-step: re-issue the captured update's recorded launches instead of "
-                         "replaying its HIP graph (MADDPG.capture(launches=True))")
+                    help="with --updates-per-step: re-issue the update's recorded launches (MADDPG.capture("
+                         "launches=True)); the default since late round 4")
+    ap.add_argument("--learn-graph", action="store_true",
+                    help="with --updates-per-step: replay the update as a HIP graph instead (A/B)")
     ap.add_argument("--eager-learn", action="store_true",
                     help="with --updates-per-step: issue the update eagerly instead of replaying its HIP graph (A/B)")
     ap.add_argument("--profile-steps", type=int, default=64,
@@ -457,7 +459,7 @@ def main():
                     return r
                 if learner._graph is None:
                     learner.capture(ro.replay, actor_env=env if ro.fused and not cfg.get("patch") else None,
-                                    launches=args.learn_launches)
+                                    launches=not args.learn_graph)
                 for _ in range(args.updates_per_step):
                     learner.replay_learn()
             return r

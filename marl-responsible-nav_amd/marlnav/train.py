@@ -5,8 +5,9 @@ process group exists: replicated weights, one gradient all-reduce per backward).
 Per env step (all device work, no host sync):
   actor (GumbelSoftmax sample, action mask, argmax) -> gw_step (world update, FeAR, shaped
   reward, auto-reset) -> replay ring (state slot, action probabilities, shaped reward,
-  termination) -> ``learns_per_step`` MADDPG updates (one HIP-graph replay each when
-  ``graph=True``) once the ring holds ``batch_size`` transitions.
+  termination) -> ``learns_per_step`` MADDPG updates (each the update's recorded
+  launches by default, or one HIP-graph replay with ``graph=True``) once the ring holds
+  ``batch_size`` transitions.
 
 Differences from the reference loop, all structural: episodes auto-reset per env inside the
 kernel instead of ``train()`` returning after one episode (``main_custom.py:129``), so one
@@ -55,7 +56,7 @@ def learn_schedule(idx_step: int, ring_t: int, ring_slots: int, global_envs: int
 
 class MADDPGTrainer:
     def __init__(self, env: VecGridEnv, maddpg: MADDPG, memory_size: int = 200_000, learning_delay: int = 0,
-                 updates_per_step: int | None = None, graph: bool | str = True, seed: int = 0):
+                 updates_per_step: int | None = None, graph: bool | str = "launches", seed: int = 0):
         self.env, self.m = env, maddpg
         # data parallelism: every decision that gates a learn() (and so its two gradient
         # all-reduces) is taken from GLOBAL quantities that every rank computes alike -- the global
@@ -77,7 +78,9 @@ class MADDPGTrainer:
                                desc_ring=fusable and env.device.type == "cuda")
         self.learning_delay = learning_delay
         self.updates_per_step = updates_per_step
-        # graph="launches": the captured update re-issued as its recorded launches (MADDPG.capture)
+        # graph="launches" (default): the update re-issued as its recorded launches where every
+        # launch of it goes through the C ABI (MADDPG.capture(launches=True)), else a graph replay;
+        # True: always the graph replay; False: eager
         self.use_graph = bool(graph) and env.device.type == "cuda"
         self.launches = graph == "launches"
         rank = self.rollout.group_rank()
