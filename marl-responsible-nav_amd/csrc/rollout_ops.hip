@@ -1,6 +1,8 @@
 // rollout_ops.hip — the batched rollout's per-step bookkeeping in one launch (include/rollout_ops.h).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <string>
 
@@ -267,18 +269,24 @@ constexpr int GD_CELLS = 16;  // map cells per thread prefetched (HW <= 256 * GD
 // Every load of a block is issued in two waves: (t, u, env, the apple's map value, this thread's
 // map cells), then (done, both descriptors whole, probs, reward, term); the rest is register / LDS
 // work (each dependent global round trip costs ~1-2 us).
-__global__ void __launch_bounds__(256) replay_gather_desc_kernel(
+// KB agents per block (256 threads each; GW_GATHER_KB=2: both agents of a row in one block, A/B)
+template <int KB>
+__global__ void __launch_bounds__(256 * KB) replay_gather_desc_kernel(
     DescSrc q, const uint32_t *__restrict__ desc, const float *__restrict__ probs, const double *__restrict__ reward,
     const uint8_t *__restrict__ term, const uint8_t *__restrict__ done, const int64_t *__restrict__ t_dev,
     const float *__restrict__ u, const int64_t *__restrict__ env, int64_t S, int64_t B, float *__restrict__ state,
     float *__restrict__ next_state, float *__restrict__ probs_out, double *__restrict__ reward_out,
     uint8_t *__restrict__ term_out, int64_t *__restrict__ tr_out, float *__restrict__ x_out,
     float *__restrict__ xn_out, uint64_t seed, const int32_t *__restrict__ ctr) {
-    __shared__ int s_pc[2][GW_MAX_AGENTS + 1];
-    __shared__ float s_pv[2][GW_MAX_AGENTS + 1];
-    __shared__ int s_np[2];
+    __shared__ int s_pcb[KB][2][GW_MAX_AGENTS + 1];
+    __shared__ float s_pvb[KB][2][GW_MAX_AGENTS + 1];
+    __shared__ int s_npb[KB][2];
     const int64_t b = blockIdx.x;
-    const int k = blockIdx.y, K = q.K, tid = threadIdx.x;
+    const int kb = KB > 1 ? (int)(threadIdx.x >> 8) : 0;
+    const int k = blockIdx.y * KB + kb, K = q.K, tid = threadIdx.x & 255;
+    int (*s_pc)[GW_MAX_AGENTS + 1] = s_pcb[kb];
+    float (*s_pv)[GW_MAX_AGENTS + 1] = s_pvb[kb];
+    int *s_np = s_npb[kb];
     const int64_t E = q.E, HW = q.HW;
     // wave 1
     const int64_t t = t_dev[0];
@@ -739,9 +747,15 @@ gw_status gw_replay_gather_desc(const gw_obs_source *src, const uint32_t *desc, 
     q.HW = src->H * src->W;
     q.variant = src->variant;
     q.E = src->E;
-    hipLaunchKernelGGL(replay_gather_desc_kernel, dim3((unsigned)B, (unsigned)q.K), dim3(256), 0,
-                       static_cast<hipStream_t>(stream), q, desc, probs, reward, term, done, t_dev, u, env, S, B,
-                       state, next_state, probs_out, reward_out, term_out, tr_out, x_out, xn_out, seed, ctr);
+    static const char *kb_env = std::getenv("GW_GATHER_KB");  // (measurement only: A/B)
+    if (kb_env && std::atoi(kb_env) == 2 && q.K % 2 == 0)
+        hipLaunchKernelGGL(replay_gather_desc_kernel<2>, dim3((unsigned)B, (unsigned)(q.K / 2)), dim3(512), 0,
+                           static_cast<hipStream_t>(stream), q, desc, probs, reward, term, done, t_dev, u, env, S, B,
+                           state, next_state, probs_out, reward_out, term_out, tr_out, x_out, xn_out, seed, ctr);
+    else
+        hipLaunchKernelGGL(replay_gather_desc_kernel<1>, dim3((unsigned)B, (unsigned)q.K), dim3(256), 0,
+                           static_cast<hipStream_t>(stream), q, desc, probs, reward, term, done, t_dev, u, env, S, B,
+                           state, next_state, probs_out, reward_out, term_out, tr_out, x_out, xn_out, seed, ctr);
     return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
 }
 
