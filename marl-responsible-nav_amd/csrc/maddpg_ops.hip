@@ -255,7 +255,6 @@ __device__ __forceinline__ void ln_relu_bwd(const float gy[8], const float y[8],
 constexpr int HP = HID + 4;  // padded LDS row
 template <int U = HID / 4>  // k-steps per unrolled batch (U = 32: the whole layer's loads in flight)
 __device__ __forceinline__ void gemv16(const float *s_h, const float *__restrict__ w, bool transpose, float *s_z) {
-    // wave within the caller's 4-wave group (critic_tail3 runs three groups per block)
     const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 3, lr = lane & 15, lq = lane >> 4;
     const int n0 = 32 * wave + lr, n1 = n0 + 16;
     f32x4 acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -497,127 +496,6 @@ __global__ void __launch_bounds__(256) critic_tail(TailParams p) {
     if (g == 0) {
         sv.g3[(int64_t)k * p.B + r] = dq;
         sv.aux[(int64_t)k * p.B + r] = diff * diff;
-    }
-}
-
-// a group that has no layer to run while another group of the block runs rows_gemv: the same two
-// block barriers
-__device__ __forceinline__ void rows_gemv_idle() {
-    __syncthreads();
-    __syncthreads();
-}
-
-// critic_tail with its independent chains on three 4-wave groups of one 768-thread block (same
-// arithmetic, same op order: bit for bit critic_tail).  Round-robin phase A: groups 0 and 1 the
-// target actions of agents kk = grp, grp + 2, ... (one layer each per round), group 2 the online
-// critic's forward on (s, a); phase B: group 0 the target critic on (s', a') and y; phase C: group
-// 2 the MSE gradient and the backward.  A group without work in a phase joins the block barriers
-// of the others' layer (rows_gemv_idle).  The serial chain per block drops from K + 3 layers (+
-// the LayerNorms around them) to ceil(K / 2) + 2.
-// TU: the gemv unroll (768 threads leave 168 VGPRs per lane: the full unroll would spill)
-template <int TU>
-__global__ void __launch_bounds__(768) critic_tail3(TailParams p) {
-    __shared__ __attribute__((aligned(16))) float s_in[3][RB * HP];
-    __shared__ __attribute__((aligned(16))) float s_out[3][RB * HP];
-    __shared__ float s_act[RB][NA * MAXK];
-    __shared__ float s_y[RB];
-    // group 2's forward state across phase B (in LDS, so it is not live in the other groups'
-    // registers): xh1, y1, xh2, y2 (8 each), rs1, rs2, q per thread
-    __shared__ float s_o[35][256];
-    const int k = blockIdx.y, grp = threadIdx.x >> 8, tid = threadIdx.x & 255, rl = tid >> 4, g = tid & 15;
-    const int r = blockIdx.x * RB + rl;
-    const int K = p.K, na = NA * K;
-    const int64_t Ds = (int64_t)K * p.D;
-    const Mlp mt = mlp_k(p.critic_t, k, K * p.D + na, 1);
-    const Mlp m = mlp_k(p.critic, k, K * p.D + na, 1);
-    const int rounds = (K + 1) / 2;
-    for (int rd = 0; rd < rounds; ++rd) {
-        if (grp < 2) {
-            const int kk = 2 * rd + grp;
-            if (kk < K) {
-                float pr[NA];
-                target_probs<TU>(p, kk, r, rl, g, s_in[grp], s_out[grp], pr);
-                if (g == 0) {
-#pragma unroll
-                    for (int a = 0; a < NA; ++a) s_act[rl][NA * kk + a] = pr[a];
-                    if (kk == k) {
-                        float *dst = p.x_next + (int64_t)r * p.ldx + Ds + NA * k;
-#pragma unroll
-                        for (int a = 0; a < NA; ++a) dst[a] = pr[a];
-                    }
-                }
-            } else {
-                rows_gemv_idle();
-            }
-        } else if (rd == 0) {  // online critic on (s, a): the stored actions are in the partials
-            RowFwd o;
-            float z[8];
-            z8(p.z_c, p.B, k, r, g, z);
-            ln_relu(z, m.lw1, m.lb1, g, o.xh1, o.y1, o.rs1);
-            rows_gemv<TU>(o.y1, rl, g, m.w2, false, s_in[2], s_out[2], z);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) z[i] += m.b2[8 * g + i];
-            ln_relu(z, m.lw2, m.lb2, g, o.xh2, o.y2, o.rs2);
-            float sq = 0.0f;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) sq = fmaf(o.y2[i], m.w3[8 * g + i], sq);
-            const float q = row_sum(sq) + m.b3[0];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                s_o[i][tid] = o.xh1[i];
-                s_o[8 + i][tid] = o.y1[i];
-                s_o[16 + i][tid] = o.xh2[i];
-                s_o[24 + i][tid] = o.y2[i];
-            }
-            s_o[32][tid] = o.rs1;
-            s_o[33][tid] = o.rs2;
-            s_o[34][tid] = q;
-        } else {
-            rows_gemv_idle();
-        }
-    }
-    __syncthreads();
-    if (grp == 0) {  // target critic on (s', a'), y = f32(r) + ((1 - d) * gamma) * q_next
-        RowFwd f;
-        const float q_next = critic_fwd<TU, 3>(mt, p.z_ct, p, k, r, rl, g, s_act[rl], s_in[0], s_out[0], f);
-        const float t1 = 1.0f - (float)p.done[(int64_t)r * K + k];
-        const float y = (float)p.reward[(int64_t)r * K + k] + (t1 * p.gamma) * q_next;
-        if (g == 0) s_y[rl] = y;
-    } else {
-        rows_gemv_idle();
-    }
-    __syncthreads();
-    if (grp == 2) {
-        RowFwd o;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            o.xh1[i] = s_o[i][tid];
-            o.y1[i] = s_o[8 + i][tid];
-            o.xh2[i] = s_o[16 + i][tid];
-            o.y2[i] = s_o[24 + i][tid];
-        }
-        o.rs1 = s_o[32][tid];
-        o.rs2 = s_o[33][tid];
-        const float q = s_o[34][tid];
-        const float diff = q - s_y[rl];
-        const float dq = (1.0f / (float)p.B) * (2.0f * diff);  // MSELoss backward (gw_mean_loss_bwd's order)
-        float gv1[8], dz1[8], gv2[8], dz2[8];
-        critic_bwd<TU>(m, dq, rl, g, o, s_in[2], s_out[2], gv1, dz1, gv2, dz2);
-        const Saved &sv = p.sv;
-        put8(sv.h1, K, p.B, k, r, g, o.y1);
-        put8(sv.h2, K, p.B, k, r, g, o.y2);
-        put8(sv.xh1, K, p.B, k, r, g, o.xh1);
-        put8(sv.xh2, K, p.B, k, r, g, o.xh2);
-        put8(sv.gv1, K, p.B, k, r, g, gv1);
-        put8(sv.gv2, K, p.B, k, r, g, gv2);
-        put8(sv.dz1, K, p.B, k, r, g, dz1);
-        put8(sv.dz2, K, p.B, k, r, g, dz2);
-        if (g == 0) {
-            sv.g3[(int64_t)k * p.B + r] = dq;
-            sv.aux[(int64_t)k * p.B + r] = diff * diff;
-        }
-    } else {
-        rows_gemv_idle();
     }
 }
 
@@ -1061,17 +939,7 @@ gw_status gw_maddpg_critic_grads(const gw_mlp_actors *actor_target, const gw_mlp
     tp.K = K;
     tp.B = B;
     tp.D = D;
-    // the one-group tail; GW_TAIL_PAR=8 / 4: the three-group tail with gemv unroll 8 / 4 (A/B,
-    // bit-identical but slower: 54.7 vs ~43 us, its 168-VGPR budget spills and cuts the unroll;
-    // profiles/r4_ab)
-    static const char *par_env = std::getenv("GW_TAIL_PAR");
-    const int par = par_env ? std::atoi(par_env) : 0;
-    if (par == 8)
-        hipLaunchKernelGGL(critic_tail3<8>, dim3(B / RB, K), dim3(768), 0, s, tp);
-    else if (par == 4)
-        hipLaunchKernelGGL(critic_tail3<4>, dim3(B / RB, K), dim3(768), 0, s, tp);
-    else
-        hipLaunchKernelGGL(critic_tail, dim3(B / RB, K), dim3(256), 0, s, tp);
+    hipLaunchKernelGGL(critic_tail, dim3(B / RB, K), dim3(256), 0, s, tp);
     GradParams gp{};
     gp.grad = *critic_grad;
     gp.x = batch->x;

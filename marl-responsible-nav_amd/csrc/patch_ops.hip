@@ -362,68 +362,6 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a, unsign
             const int pw = s_pw[slot * np + i];
             if (pw >= 0) a.patch[((int64_t)k * a.E + e0 + el) * PP + pw] = s_pv[slot * np + i];
         }
-    } else if (MODE == 5 && a.patch) {
-        // MODE 4's table rows, written as the store floor writes: the block's run of each agent as
-        // aligned float4 stores, each thread's V float4s' 4 V table loads all issued before its
-        // first store (no load -> store chain per window); then the patched cells, as MODE 4
-        const uint32_t m_pp = (uint32_t)((0x100000000ull + (uint64_t)PP - 1) / (uint64_t)PP);
-        constexpr int V = 4;
-        for (int k = 0; k < K; ++k) {
-            const int64_t off = ((int64_t)k * a.E + e0) * PP;
-            float *o = a.patch + off;
-            const int len = nenv * PP;
-            const int lead = min((int)((4 - (off & 3)) & 3), len);
-            const int n4 = (len - lead) / 4;
-            auto elem = [&](int i, float &v) -> bool {  // table value of run element i; false: not written
-                const int el = (int)__umulhi((uint32_t)i, m_pp), c = i - el * PP;
-                const bool w = (s_flag[el] & D_WRITE) != 0;
-                const int ctr = w ? s_ctr[el * K + k] : 0;
-                v = a.tbl[(int64_t)((ctr >> 16) * W + (ctr & 0xFFFF)) * PP + c];
-                return w;
-            };
-            for (int i = tid; i < lead; i += THREADS) {
-                float v;
-                if (elem(i, v)) o[i] = v;
-            }
-            for (int i = lead + 4 * n4 + tid; i < len; i += THREADS) {
-                float v;
-                if (elem(i, v)) o[i] = v;
-            }
-            for (int j0 = 0; j0 < n4; j0 += THREADS * V) {
-                float v[V][4];
-                uint32_t wm[V];
-#pragma unroll
-                for (int u = 0; u < V; ++u) {
-                    const int j = j0 + u * THREADS + tid;
-                    wm[u] = 0u;
-                    if (j < n4) {
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) wm[u] |= elem(lead + 4 * j + q, v[u][q]) ? (1u << q) : 0u;
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < V; ++u) {
-                    const int j = j0 + u * THREADS + tid;
-                    if (j >= n4) continue;
-                    float *dst = o + lead + 4 * j;
-                    if (wm[u] == 0xFu) {
-                        *reinterpret_cast<float4 *>(dst) = make_float4(v[u][0], v[u][1], v[u][2], v[u][3]);
-                    } else {
-#pragma unroll
-                        for (int q = 0; q < 4; ++q)
-                            if (wm[u] & (1u << q)) dst[q] = v[u][q];
-                    }
-                }
-            }
-        }
-        __builtin_amdgcn_s_waitcnt(0);
-        __syncthreads();
-        for (int t = tid; t < nenv * K * np; t += THREADS) {
-            const int slot = t / np, i = t - slot * np, el = slot / K, k = slot - el * K;
-            if (!(s_flag[el] & D_WRITE)) continue;
-            const int pw = s_pw[slot * np + i];
-            if (pw >= 0) a.patch[((int64_t)k * a.E + e0 + el) * PP + pw] = s_pv[slot * np + i];
-        }
     } else if (a.patch) {  // one thread per element (consecutive lanes: consecutive floats), overrides in registers
         // i / PP and c / P as multiply-highs (i < PB * PP; P >= 2)
         const uint32_t m_pp = (uint32_t)((0x100000000ull + (uint64_t)PP - 1) / (uint64_t)PP);
@@ -551,7 +489,7 @@ hipError_t launch_windows(const PatchArgs &args, hipStream_t s) {
         const int f = std::atoi(force);
         if (f == 1 || (f == 0 && PP <= 64 * MAXPL && base + extra[0] <= LDS_MAX) ||
             (f == 2 && a.P % 4 == 0 && np < 16 && base + extra[2] <= LDS_MAX) || (f == 3 && base + extra[3] <= LDS_MAX) ||
-            ((f == 4 || f == 5) && a.tbl && PP <= 256))
+            (f == 4 && a.tbl && PP <= 256))
             mode = f;
     }
     if (force && std::atoi(force) == 9 && a.patch) {  // measurement only: the store floor
@@ -569,7 +507,6 @@ hipError_t launch_windows(const PatchArgs &args, hipStream_t s) {
             case 2: return launch_mode<2, 64>(a, lds, s);
             case 3: return launch_mode<3, 64>(a, lds, s);
             case 4: return launch_mode<4, 64>(a, lds, s);
-            case 5: return launch_mode<5, 64>(a, lds, s);
             default: return launch_mode<1, 64>(a, lds, s);
         }
     }

@@ -269,7 +269,7 @@ constexpr int GD_CELLS = 16;  // map cells per thread prefetched (HW <= 256 * GD
 // Every load of a block is issued in two waves: (t, u, env, the apple's map value, this thread's
 // map cells), then (done, both descriptors whole, probs, reward, term); the rest is register / LDS
 // work (each dependent global round trip costs ~1-2 us).
-// KB agents per block (256 threads each; GW_GATHER_KB=2: both agents of a row in one block, A/B)
+// KB agents per block (256 threads each; one: both agents of a row in one block measured slower)
 template <int KB>
 __global__ void __launch_bounds__(256 * KB) replay_gather_desc_kernel(
     DescSrc q, const uint32_t *__restrict__ desc, const float *__restrict__ probs, const double *__restrict__ reward,
@@ -747,15 +747,9 @@ gw_status gw_replay_gather_desc(const gw_obs_source *src, const uint32_t *desc, 
     q.HW = src->H * src->W;
     q.variant = src->variant;
     q.E = src->E;
-    static const char *kb_env = std::getenv("GW_GATHER_KB");  // (measurement only: A/B)
-    if (kb_env && std::atoi(kb_env) == 2 && q.K % 2 == 0)
-        hipLaunchKernelGGL(replay_gather_desc_kernel<2>, dim3((unsigned)B, (unsigned)(q.K / 2)), dim3(512), 0,
-                           static_cast<hipStream_t>(stream), q, desc, probs, reward, term, done, t_dev, u, env, S, B,
-                           state, next_state, probs_out, reward_out, term_out, tr_out, x_out, xn_out, seed, ctr);
-    else
-        hipLaunchKernelGGL(replay_gather_desc_kernel<1>, dim3((unsigned)B, (unsigned)q.K), dim3(256), 0,
-                           static_cast<hipStream_t>(stream), q, desc, probs, reward, term, done, t_dev, u, env, S, B,
-                           state, next_state, probs_out, reward_out, term_out, tr_out, x_out, xn_out, seed, ctr);
+    hipLaunchKernelGGL(replay_gather_desc_kernel<1>, dim3((unsigned)B, (unsigned)q.K), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), q, desc, probs, reward, term, done, t_dev, u, env, S, B,
+                       state, next_state, probs_out, reward_out, term_out, tr_out, x_out, xn_out, seed, ctr);
     return hipGetLastError() == hipSuccess ? GW_OK : GW_ERR_HIP;
 }
 

@@ -54,7 +54,7 @@ def main(argv=None):
                gamma=hp["GAMMA"], tau=hp["TAU"], batch_size=hp["BATCH_SIZE"], learn_step=hp["LEARN_STEP"],
                device=env.device, seed=hp["SEED"], capturable=not args.no_graph)
     tr = MADDPGTrainer(env, m, memory_size=hp["MEMORY_SIZE"], updates_per_step=args.updates_per_step,
-                       graph=not args.no_graph, seed=hp["SEED"])
+                       graph=False if args.no_graph else "launches", seed=hp["SEED"])
     tr.reset()
     for it in range(args.iters):
         s = tr.train(hp["TRAIN_STEPS"])  # the statistics are all-reduced over the ranks

@@ -374,20 +374,60 @@ def check(status: int, what: str):
         raise GwError(f"{what} failed (status {status}): {msg}")
 
 
+class RecordingError(RuntimeError):
+    """A torch GPU kernel was launched inside a LaunchRecorder (it would be missing from replays)."""
+
+
+def _no_torch_kernels_mode():
+    import torch
+    from torch.utils._python_dispatch import TorchDispatchMode
+
+    # ops that launch no kernel: allocations and metadata queries (views are recognised by
+    # OpOverload.is_view)
+    free = {"empty", "empty_strided", "empty_like", "new_empty", "new_empty_strided", "detach", "lift_fresh",
+            "sym_size", "sym_stride", "sym_numel", "sym_storage_offset", "is_same_size", "alias"}
+
+    class Mode(TorchDispatchMode):
+        def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+            kwargs = kwargs or {}
+            name = func.overloadpacket.__name__
+            if not (getattr(func, "is_view", False) or name in free):
+                leaves = list(args) + list(kwargs.values())
+                flat = []
+                for a in leaves:
+                    flat.extend(a if isinstance(a, (list, tuple)) else (a,))
+                dev = kwargs.get("device")
+                on_gpu = any(isinstance(a, torch.Tensor) and a.is_cuda for a in flat) or \
+                    (dev is not None and torch.device(dev).type == "cuda")
+                if on_gpu:
+                    raise RecordingError(f"LaunchRecorder: torch op {func} would launch a GPU kernel that "
+                                         "replays of the recording would miss")
+            return func(*args, **kwargs)
+    return Mode()
+
+
 class LaunchRecorder:
     """Records the stream-ordered C-ABI calls made while active: every exported function whose
     last argument is ``stream`` (the handle of the stream being recorded).  ``replay(s)`` issues
     them again, in order, on stream ``s``, with the same arguments (ctypes structs passed by
     reference stay alive in the recorded tuples).  Used by MADDPG.capture(launches=True): the
-    update recorded once under a graph capture (whose private pool keeps every buffer the calls
-    point at), then re-issued as plain launches instead of a graph replay."""
+    update runs once eagerly while recorded (its buffers come from the ordinary allocator; the
+    caller keeps them alive for as long as it replays), then is re-issued as plain launches
+    instead of a graph replay.
 
-    def __init__(self, stream: int):
+    A torch operation that would launch a kernel on the GPU while recording cannot be replayed
+    (only C-ABI calls are recorded), so it raises ``RecordingError`` instead of being dropped
+    silently (``forbid_torch``, the default): views, allocations and host-side work are allowed."""
+
+    def __init__(self, stream: int, forbid_torch: bool = True):
         self.stream = int(stream)
         self.calls = []
         self._saved = {}
+        self._mode = _no_torch_kernels_mode() if forbid_torch else None
 
     def __enter__(self):
+        if self._mode is not None:
+            self._mode.__enter__()
         L = load()
         for name in EXPORTS:
             f = getattr(L, name, None)
@@ -402,6 +442,8 @@ class LaunchRecorder:
         for name, f in self._saved.items():
             setattr(L, name, f)
         self._saved = {}
+        if self._mode is not None:
+            self._mode.__exit__(*exc)
         return False
 
     def _wrap(self, name, f):

@@ -247,6 +247,24 @@ def _call(func, args):
     return Call(func, args)
 
 
+def _check_view(t: "Tensor", numel: int):
+    """Reject a tensor record whose (offset, shape, stride) would read outside its storage of
+    `numel` elements: the values come from the (untrusted) file and feed as_strided."""
+    ints = (t.offset,) + tuple(t.shape) + tuple(t.stride)
+    if not all(isinstance(v, int) and not isinstance(v, bool) for v in ints):
+        raise ValueError(f"checkpoint reader: non-integer view of storage {t.key}")
+    if len(t.shape) != len(t.stride):
+        raise ValueError(f"checkpoint reader: shape / stride rank mismatch in storage {t.key}")
+    if t.offset < 0 or any(n < 0 for n in t.shape) or any(s < 0 for s in t.stride):
+        raise ValueError(f"checkpoint reader: negative offset, size or stride in storage {t.key}")
+    if any(n == 0 for n in t.shape):
+        return  # empty view: nothing is read
+    last = t.offset + sum((n - 1) * s for n, s in zip(t.shape, t.stride))
+    if last >= numel:
+        raise ValueError(f"checkpoint reader: view of storage {t.key} reaches element {last} "
+                         f"of {numel}")
+
+
 def _attach(obj, z: zipfile.ZipFile, prefix: str, seen=None):
     """Read every Tensor record's bytes from its storage member (depth-first, shared records once)."""
     seen = set() if seen is None else seen
@@ -258,10 +276,15 @@ def _attach(obj, z: zipfile.ZipFile, prefix: str, seen=None):
         if dt is None:
             raise ValueError(f"checkpoint reader: unsupported storage type {obj.dtype}")
         raw = np.frombuffer(z.read(f"{prefix}data/{obj.key}"), dtype=np.dtype(dt).newbyteorder("<"))
+        _check_view(obj, len(raw))
         itemsize = raw.itemsize
-        view = np.lib.stride_tricks.as_strided(raw[obj.offset:], shape=obj.shape,
-                                               strides=tuple(s * itemsize for s in obj.stride)) \
-            if obj.shape else raw[obj.offset:obj.offset + 1].reshape(())
+        if any(n == 0 for n in obj.shape):
+            view = np.zeros(obj.shape, dtype=dt)
+        elif obj.shape:
+            view = np.lib.stride_tricks.as_strided(raw[obj.offset:], shape=obj.shape,
+                                                   strides=tuple(s * itemsize for s in obj.stride))
+        else:
+            view = raw[obj.offset:obj.offset + 1].reshape(())
         obj.data = np.array(view, dtype=dt)  # a contiguous copy
         return
     if isinstance(obj, dict):

@@ -542,6 +542,9 @@ class MADDPG:
         replay: no wait on a graph's completion before the next launch (profiles/r4_ab)."""
         if self.device.type != "cuda":
             raise RuntimeError("graph capture needs the GPU")
+        # which rows the captured sample reads (the descriptor ring or the dense obs slots): the
+        # caller's fence must match it, and a change of the ring's mode invalidates the capture
+        self._capture_desc = bool(getattr(replay, "use_desc", False)) if batch is None else None
         if batch is not None:
             fixed = tuple(batch) + (None,) * (8 - len(batch))
 
@@ -606,6 +609,19 @@ class MADDPG:
         self._graphs = (g1, g2, g3)
         self._graph = g3
         return g3
+
+    def invalidate_capture(self):
+        """Drop the captured update (graph, segments or recorded launches): the next learn through
+        a trainer captures again, e.g. after the replay ring switched between descriptor and dense
+        rows (Rollout.reset / resume)."""
+        self._graph = self._graphs = self._launches = None
+        self._launch_keep = self._graph_ctx = None
+        self._prep_env = self._prep_ws = None
+        self._capture_desc = None
+
+    def capture_matches(self, replay) -> bool:
+        """Whether the captured update samples the rows ``replay`` currently offers."""
+        return self._graph is not None and getattr(self, "_capture_desc", None) == bool(getattr(replay, "use_desc", False))
 
     def replay_learn(self):
         if self._graphs is not None:

@@ -144,7 +144,9 @@ class ReturnGather:
     65,536 envs vs 576 KB).  A step with more completions than ``cap`` leaves a backlog that the
     next steps drain; every rank sees every header, so all ranks double ``cap`` at the same window
     boundary when the last window had one (a lagged host read of an already finished copy: no
-    stall).  Every ``window`` steps the receiver appends each rank's entries to a mirror FIFO and
+    stall).  Window boundaries count pushes, not compactions: ``completed()`` / ``compact()`` may be
+    called on any subset of ranks at any time (e.g. rank-0-only logging) without desynchronising
+    the slot sizes.  Every ``window`` steps the receiver appends each rank's entries to a mirror FIFO and
     emits, in (step, rank, env) order, every step whose entries have all arrived -- with
     rank-major contiguous shards that is the reference's (step, global env id) order, bit for bit
     the list of the round-3 full gather (tests/test_parallel.py, tests/test_gpu_dist.py).
@@ -210,6 +212,8 @@ class ReturnGather:
             self._maxb_host = torch.zeros(2, dtype=torch.int64)
         self._maxb_ev = None
         self._nwin = 0
+        self._steps = 0          # pushes so far: window boundaries are multiples of `window` on every rank
+        self._wmax = torch.zeros(1, dtype=torch.int64, device=dev)  # max sender backlog since the last boundary
         self._alloc_slots()
 
     def _alloc_slots(self):
@@ -337,6 +341,11 @@ class ReturnGather:
             self._work[self._flip] = dist.all_gather_into_tensor(slot.view(-1), buf, group=self.group,
                                                                  async_op=True)
             self._flip ^= 1
+            self._fill += 1
+            self._steps += 1
+            if self._steps % self.window == 0:  # a boundary every rank reaches at the same push
+                self._boundary()
+            return
         self._fill += 1
         if self._fill == self.window:
             self.compact()
@@ -352,22 +361,61 @@ class ReturnGather:
         if self.distributed:
             self._unpack()
             self._fill = 0
-            # the window's max sender backlog, read by the host one window later (_adapt_from)
-            slot = self._nwin % 2
-            self._maxb_host[slot:slot + 1].copy_(self._rst[2 * self.world + 3:2 * self.world + 4],
-                                                 non_blocking=self._hip)
-            if self._hip:
-                ev = torch.cuda.Event()
-                ev.record(torch.cuda.current_stream(self.device))
-                prev_ev, self._maxb_ev = self._maxb_ev, ev
-            self._nwin += 1
-            if self._nwin >= 2:
-                self._adapt_from(prev_ev if self._hip else None)
+            # the backlog maximum over every unpack since the last boundary: the same steps' headers
+            # on every rank, however a rank split them into compactions (completed() mid-window)
+            w = 2 * self.world + 3
+            torch.maximum(self._wmax, self._rst[w:w + 1], out=self._wmax)
             return
         if self._recv.is_cuda:
             self._compact_hip()
             return
         self._compact_torch()
+
+    def drain(self, max_steps: int = 1 << 20) -> int:
+        """COLLECTIVE (every rank calls it at the same point): gather steps with no new completions
+        until no rank has a backlog, so that ``completed()`` holds every episode that ended, even in
+        a run that stopped right after a completion burst larger than ``cap``.  The loop condition is
+        read from the gathered headers, which every rank holds alike.  Returns the steps added (0
+        with one rank)."""
+        if not self.distributed:
+            return 0
+        added = 0
+        while added < max_steps:
+            buf = self._buf()
+            self._done.zero_()   # this pseudo-step completes nothing; the step's outputs were packed
+            self._pack(buf)
+            slot = self._recv[self._fill]
+            dist.all_gather_into_tensor(slot.view(-1), buf, group=self.group)
+            backlog = int(slot[:, :32].view(torch.int64)[:, 2].max())  # header: count, sent, backlog, ovf
+            self._flip ^= 1
+            self._fill += 1
+            self._steps += 1
+            added += 1
+            if self._steps % self.window == 0:
+                self._boundary()
+            if backlog == 0:
+                break
+        self.compact()
+        return added
+
+    def _boundary(self):
+        """Every ``window`` pushes (the same pushes on every rank, whatever compact() / completed()
+        calls a rank made in between): fold the received steps in, copy the window's maximum sender
+        backlog to the host (read one window later: no stall) and adapt ``cap`` from the window
+        before.  The decision depends only on gathered headers and the push count, so every rank
+        resizes its slots at the same step."""
+        self.compact()
+        slot = self._nwin % 2
+        self._maxb_host[slot:slot + 1].copy_(self._wmax, non_blocking=self._hip)
+        self._wmax.zero_()
+        prev_ev = None
+        if self._hip:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            prev_ev, self._maxb_ev = self._maxb_ev, ev
+        self._nwin += 1
+        if self._nwin >= 2:
+            self._adapt_from(prev_ev)
 
     def _adapt_from(self, ev):
         """Grow ``cap`` (x2, up to the shard) when the window before this one left a backlog on any

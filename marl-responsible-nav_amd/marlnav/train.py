@@ -99,6 +99,11 @@ class MADDPGTrainer:
         self.rollout.reset()
 
     def _learn(self):
+        rp = self.rollout.replay
+        if self.use_graph and self.m._graph is not None and not self.m.capture_matches(rp):
+            # the ring switched between descriptor and dense rows since the capture (reset after
+            # load_checkpoint): the captured sample would read the other rows than the fence orders
+            self.m.invalidate_capture()
         self.rollout.learn_fence()  # what the sampled transitions read (descriptor or obs slots)
         if self.use_graph:
             if self.m._graph is None:
@@ -178,7 +183,7 @@ class MADDPGTrainer:
             # the fused actor's Gumbel-noise Philox counter continues where the saved run stopped
             # (restarting it at 0 would replay the original run's exploration noise)
             self.rollout.resume(calls=int(calls[0]) if calls is not None else None)
-            self.m._graph = None  # the ring's rows now come from its dense slots: capture again
+            self.m.invalidate_capture()  # the ring's rows now come from its dense slots: capture again
         with open(os.path.join(path, "steps.txt")) as f:
             self.total_steps = int(f.read()) // self.global_envs * self.env.E
 

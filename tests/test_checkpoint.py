@@ -59,6 +59,50 @@ def test_reader_runs_nothing(tmp_path):
     assert not marker.exists()
 
 
+class _Storage:
+    """A storage marker the crafted pickler below writes as a persistent id."""
+
+
+def _crafted_checkpoint(path, numel, offset, size, stride):
+    """A torch-zip checkpoint whose one tensor is `_rebuild_tensor_v2(storage of numel floats,
+    offset, size, stride)` with the given (possibly hostile) view arguments."""
+    import pickle
+    st = _Storage()
+
+    class P(pickle.Pickler):
+        def persistent_id(self, obj):
+            return ("storage", torch.FloatStorage, "0", "cpu", numel) if obj is st else None
+
+    class T:
+        def __reduce__(self):
+            return torch._utils._rebuild_tensor_v2, (st, offset, size, stride, False, collections.OrderedDict())
+
+    buf = io.BytesIO()
+    P(buf, protocol=2).dump({"t": T()})
+    with zipfile.ZipFile(path, "w") as z:
+        z.writestr("ck/data.pkl", buf.getvalue())
+        z.writestr("ck/data/0", np.arange(numel, dtype="<f4").tobytes())
+
+
+def test_reader_rejects_out_of_bounds_views(tmp_path):
+    path = str(tmp_path / "ok.pt")
+    _crafted_checkpoint(path, 12, 2, (2, 3), (4, 1))  # in bounds: elements 2..8
+    r = ck.read_checkpoint(path)
+    np.testing.assert_array_equal(r["t"].data, np.array([[2, 3, 4], [6, 7, 8]], np.float32))
+    bad = {"offset past the end": (12, (1,), (1,)), "oversized shape": (0, (4, 4), (4, 1)),
+           "oversized stride": (0, (2, 3), (40, 1)), "negative stride": (5, (3,), (-1,)),
+           "negative offset": (-1, (2,), (1,)), "negative size": (0, (-2, 3), (3, 1))}
+    for what, (off, size, stride) in bad.items():
+        p = str(tmp_path / "bad.pt")
+        _crafted_checkpoint(p, 12, off, size, stride)
+        with pytest.raises(ValueError):
+            ck.read_checkpoint(p)
+            pytest.fail(what)
+    # an empty view reads nothing and is accepted
+    _crafted_checkpoint(path, 12, 0, (0, 5), (5, 1))
+    assert ck.read_checkpoint(path)["t"].data.shape == (0, 5)
+
+
 @pytest.mark.skipif(not os.path.isdir(REF_MODELS), reason="reference checkpoints not present (GPU box)")
 def test_shipped_checkpoints_match_fixture():
     z = np.load(os.path.join(GOLD, "ckpt_actors.npz"))

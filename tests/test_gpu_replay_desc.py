@@ -136,3 +136,43 @@ def test_update_as_recorded_launches_equals_graph_replay():
         env.close()
     for k in states[0]:
         assert torch.equal(states[0][k], states[1][k]), k
+
+
+def test_capture_follows_the_rings_row_mode():
+    """a capture made while the ring served dense rows (after resume) must not be
+    replayed once a reset switched the ring back to descriptor rows (its fence would then skip the
+    obs writer the captured dense gather reads): the trainer re-captures on the new mode."""
+    from marlnav.maddpg import MADDPG
+    from marlnav.train import MADDPGTrainer
+    sc = S.builtin("grid32")
+    env = VecGridEnv(sc, num_envs=256, fear=True, fear_weight=-5.0, stats=True, seed=7, max_steps=10)
+    m = MADDPG(sc.K, sc.H, sc.W, device=env.device, seed=3, capturable=True)
+    tr = MADDPGTrainer(env, m, memory_size=2048, updates_per_step=1, graph="launches", seed=3)
+    tr.reset()
+    tr.train(4)
+    tr.rollout.resume()
+    assert not tr.rollout.replay.use_desc
+    tr.train(3)
+    assert m._graph is not None and m._capture_desc is False
+    names = [c[0] for c in m._launches.calls]
+    assert names[0] == "gw_replay_gather", names
+    tr.reset()
+    assert tr.rollout.replay.use_desc and not m.capture_matches(tr.rollout.replay)
+    tr.train(3)
+    assert m._capture_desc is True and m.capture_matches(tr.rollout.replay)
+    assert [c[0] for c in m._launches.calls][0] == "gw_replay_gather_desc"
+    env.close()
+
+
+def test_launch_recorder_refuses_torch_kernels():
+    """A torch op that launches a GPU kernel inside a recording would be missing from every
+    replay: LaunchRecorder raises instead (views and allocations pass)."""
+    from marlnav import _lib
+    x = torch.zeros(8, device="cuda")
+    rec = _lib.LaunchRecorder(torch.cuda.current_stream().cuda_stream)
+    with rec:
+        x.view(2, 4)[1]
+        torch.empty(16, device="cuda")
+    with pytest.raises(_lib.RecordingError):
+        with _lib.LaunchRecorder(torch.cuda.current_stream().cuda_stream):
+            x.add_(1)

@@ -134,6 +134,68 @@ def test_gloo_world2_matches_single_process(G):
     assert ref[1] > 0                                          # some episodes completed
 
 
+def _burst_series(G, steps, seed=3):
+    """Synthetic per-step (returns [G] f64, done [G] u8) of G global envs: a low completion rate,
+    a burst where every env ends at once (step 4: episodes that started together), and a final
+    step where every env ends (the run stops right after a burst)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for t in range(steps):
+        ret = rng.normal(size=G)
+        done = rng.random(G) < 0.03
+        if t == 4 or t == steps - 1:
+            done[:] = True
+        out.append((ret, done.astype(np.uint8)))
+    return out
+
+
+def _gather_worker(rank, world, port, G, steps, outdir, mid_window_reader):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    off, cnt = shard(G, rank, world)
+    gat = ReturnGather(G, rank, world, "cpu", window=4, cap=3)  # cap far below the bursts
+    caps, mid = [], None
+    for t, (ret, done) in enumerate(_burst_series(G, steps)):
+        gat.push(torch.from_numpy(ret[off: off + cnt]), torch.from_numpy(done[off: off + cnt]))
+        caps.append(gat.cap)
+        if rank == 0 and mid_window_reader and t in (5, 9, 10):
+            # rank-0-only logging mid-window (ADVICE r4): compacts on this rank alone
+            mid = gat.completed()
+    added = gat.drain()  # collective: every rank, same point
+    np.save(os.path.join(outdir, f"done{rank}.npy"), gat.completed())
+    np.save(os.path.join(outdir, f"caps{rank}.npy"), np.array(caps + [gat.cap]))
+    np.save(os.path.join(outdir, f"added{rank}.npy"), np.array([added, gat.slot_bytes]))
+    if mid is not None:
+        np.save(os.path.join(outdir, "mid.npy"), mid)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,G,reader", [(4, 203, False), (4, 203, True), (2, 64, True)])
+def test_gloo_return_gather_bursts_match_single_process(world, G, reader):
+    """world 4 (203 envs: ragged shards 51/51/51/50) and 2: completion bursts far above ``cap``
+    (3) force backlogs and cap doubling, the run ends right after a burst, and (reader) rank 0
+    alone calls completed() mid-window.  After the collective drain() every rank holds the one-
+    process list (step, then global env id) bit for bit, and every rank resized its slots at the
+    same steps."""
+    steps = 13
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_gather_worker, args=(world, _free_port(), G, steps, d, reader), nprocs=world, join=True)
+        got = [np.load(os.path.join(d, f"done{r}.npy")) for r in range(world)]
+        caps = [np.load(os.path.join(d, f"caps{r}.npy")) for r in range(world)]
+        added = [np.load(os.path.join(d, f"added{r}.npy")) for r in range(world)]
+        mid = np.load(os.path.join(d, "mid.npy")) if reader else None
+    want = np.concatenate([ret[done != 0] for ret, done in _burst_series(G, steps)])
+    for r in range(world):
+        np.testing.assert_array_equal(got[r], want)
+        np.testing.assert_array_equal(caps[r], caps[0])
+        np.testing.assert_array_equal(added[r], added[0])
+    assert caps[0][0] == 3 and caps[0][-1] > 3       # the bursts grew the cap
+    assert added[0][0] > 0                           # the final burst needed the drain
+    if reader:  # a mid-window read is a prefix of the full list
+        np.testing.assert_array_equal(mid, want[: len(mid)])
+
+
 def test_return_gather_single_process_order_and_rings():
     """World size 1 (no process group): the compacted list == the per-step done envs' returns in
     env order, across receive-ring wraps (window 3) and a score ring smaller than the total."""
