@@ -88,7 +88,7 @@ def algorithmic_bytes(N: int, K: int, HW: int, obs_bytes: int = 4):
 
 # gw_profile span kinds (include/gridenv.h GW_SPAN_*) -> the kernel names of bench lines / rocprofv3
 SPAN_KINDS = {0: "step_kernel", 1: "obs_kernel", 2: "fear_kernel", 3: "act_kernel", 4: "cnn_l1_kernel",
-              5: "cnn_list_kernels", 6: "cnn_rare_kernel", 7: "window_kernel"}
+              5: "cnn_list_kernels", 6: "cnn_rare_kernel", 7: "window_kernel", 8: "learn_update"}
 F32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: dense f32 MFMA (v_mfma_f32_16x16x4_f32), no xf32 on gfx950
 HID, N_ACT = 128, 9        # the fused actors' hidden width and actions (configs/mlp.yaml, configs/cnn.yaml)
 

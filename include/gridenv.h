@@ -152,14 +152,15 @@ gw_status gw_copy_state(void *env, const gw_state *buf, int to_env, void *stream
  * handle: GW_SPAN_ACT the fused actors' MLP kernel (act_kernel of gw_actor_act,
  * gw_patch_actor_act, gw_cnn_act, gw_patch_cnn_act), GW_SPAN_CNN_L1 the CNN heads' layer-1
  * listing kernel, GW_SPAN_CNN_LIST their bucket scan + unit plan and scatter (two launches), GW_SPAN_CNN_RARE
- * their recompute of the listed conv positions, GW_SPAN_WINDOW the window writer (gw_obs_patch).
+ * their recompute of the listed conv positions, GW_SPAN_WINDOW the window writer (gw_obs_patch),
+ * GW_SPAN_LEARN one whole descriptor-learner update (gw_maddpg_desc_update's four launches).
  * enable > 1 also makes sure `enable` timing events exist now (creating them inside a profiled
  * step would put their host cost between its launches).  gw_profile_read synchronises on those
  * events, returns the summed elapsed milliseconds of the first three kinds and the number of
  * gw_step calls timed, and clears every span.  Used by bench.py for the live roofline. */
 enum {
     GW_SPAN_STEP = 0, GW_SPAN_OBS = 1, GW_SPAN_FEAR = 2, GW_SPAN_ACT = 3, GW_SPAN_CNN_L1 = 4,
-    GW_SPAN_CNN_LIST = 5, GW_SPAN_CNN_RARE = 6, GW_SPAN_WINDOW = 7
+    GW_SPAN_CNN_LIST = 5, GW_SPAN_CNN_RARE = 6, GW_SPAN_WINDOW = 7, GW_SPAN_LEARN = 8
 };
 gw_status gw_profile(void *env, int enable);
 gw_status gw_profile_read(void *env, double out_ms[3], int64_t *n_steps);

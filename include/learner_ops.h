@@ -120,7 +120,7 @@ int64_t gw_maddpg_workspace_floats(int32_t K, int32_t B, int32_t D);
  * critic_target_k(x_next); critic_grad = d/dtheta of mean_b (critic_k(x) - y)^2 per agent;
  * loss [K] the MSE values.  adam_step (may be NULL): the critic optimizer's step count
  * (gw_adam_step's int32 [2]), advanced by one in this call's last launch, so the Adam step that
- * follows runs with advanced = 1. 
+ * follows runs with advanced = 1. */
 gw_status gw_maddpg_critic_grads(const gw_mlp_actors *actor_target, const gw_mlp_actors *critic_target,
                                  const gw_mlp_actors *critic, const gw_mlp_actors *critic_grad,
                                  const gw_maddpg_batch *batch, float gamma, float *ws, float *loss,
@@ -134,6 +134,53 @@ gw_status gw_maddpg_actor_grads(const gw_mlp_actors *actor, const gw_mlp_actors 
                                 const gw_mlp_actors *actor_grad, const gw_maddpg_batch *batch, float *ws, float *loss,
                                 float *probs, int32_t *adam_step, void *stream);
 
+/* ---- the descriptor learner (csrc/maddpg_ops.hip, round 5) ----------------------------------
+ * The same MADDPG update on a replay ring of obs DESCRIPTORS (Rollout(desc_ring=True): per slot the
+ * 48-byte descriptors gw_obs_desc_copy stores, plus probs / rewards / terminations / dones), with
+ * the sample drawn inside (gw_replay_gather_desc's Philox draws keyed by `seed` and the critic's
+ * step count) and both Adam steps and the soft target updates inside: FOUR launches per update,
+ * one rank (the data-parallel learner all-reduces between the gradients and Adam: the two calls
+ * above).  Layer 1 is the map part c1 = b1 + map . W1 (kept in the workspace as 64-row partial
+ * sums, refreshed by the launch that changes W1) plus the <= N + 1 patched cells of each obs, and
+ * the W1 gradient is map (x) colsum(dZ1) plus the patched cells' terms: no layer-1 GEMM and no
+ * dense rows.  Differs from the dense update (gw_maddpg_critic_grads / _actor_grads + gw_adam_step
+ * + gw_soft_update2) by f32 summation order only. */
+typedef struct gw_adam_buf {
+    float *param;            /* the network's flat parameter buffer (its gw_mlp_actors point into it) */
+    float *grad;             /* the flat gradient buffer (same layout): the update's gradients, written */
+    float *exp_avg, *exp_avg_sq;
+    int32_t *step;           /* int32 [2], gw_adam_step's count: [0] advanced by the update, [1] untouched */
+    int64_t n;               /* elements */
+    double lr, beta1, beta2, eps;
+} gw_adam_buf;
+typedef struct gw_desc_ring {
+    const uint32_t *desc;    /* [S][E][12] every slot's obs descriptors (gw_obs_desc_copy)           */
+    const float *probs;      /* [S][K][E][9] stored action probabilities                            */
+    const double *reward;    /* [S][E][K] shaped rewards                                            */
+    const uint8_t *term;     /* [S][E][K] terminations                                              */
+    const uint8_t *done;     /* [S][E] env done (the next state is then the terminal obs)           */
+    const int64_t *t_dev;    /* transitions stored (device)                                         */
+    int64_t S;               /* slots                                                               */
+} gw_desc_ring;
+/* Workspace floats of a batch of B rows (16 <= B <= 256, B % 16 == 0); -1 on bad arguments. */
+int64_t gw_maddpg_desc_workspace_floats(int32_t K, int32_t B, int32_t H, int32_t W);
+/* (Re)derive the c1 partial sums of all four networks from their current W1 into ws: before the
+ * first update and after any change of the weights other than gw_maddpg_desc_update's own. */
+gw_status gw_maddpg_desc_prime(const gw_obs_source *src, const gw_mlp_actors *actor, const gw_mlp_actors *actor_target,
+                               const gw_mlp_actors *critic, const gw_mlp_actors *critic_target, int32_t B, float *ws,
+                               void *stream);
+/* One whole update: sample B rows, critic gradients + Adam, actor gradients + Adam, the soft
+ * updates of both targets (their flat buffers share the online layout), losses [K] f32.  The
+ * optimizers' counts advance by one each (opt_critic's also keys the draws); gradients are left
+ * in the grad buffers; ws keeps the rows' records (layout: csrc/maddpg_ops.hip dws_layout).
+ * prof_env (may be NULL): a gw_create handle whose gw_profile spans take the update's four
+ * launches as one GW_SPAN_LEARN span while it profiles. */
+gw_status gw_maddpg_desc_update(const gw_obs_source *src, const gw_desc_ring *ring, const gw_mlp_actors *actor,
+                                const gw_mlp_actors *actor_target, const gw_mlp_actors *critic,
+                                const gw_mlp_actors *critic_target, const gw_adam_buf *opt_actor,
+                                const gw_adam_buf *opt_critic, float *actor_target_flat, float *critic_target_flat,
+                                float gamma, float tau, int32_t B, uint64_t seed, float *ws, float *actor_loss,
+                                float *critic_loss, void *prof_env, void *stream);
 #ifdef __cplusplus
 }
 #endif

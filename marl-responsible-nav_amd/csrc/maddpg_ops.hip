@@ -32,6 +32,7 @@
 
 #include "learner_ops.h"
 #include "philox.h"
+#include "prof.h"
 
 namespace {
 
@@ -799,6 +800,1057 @@ __global__ void __launch_bounds__(256) grads_kernel(GradParams p) {
     }
 }
 
+// =================================================================================================
+// The descriptor learner (round 5): one MADDPG update on the replay ring of obs descriptors
+// (Rollout(desc_ring=True)) as FOUR launches, the sample drawn inside them.  Layer 1 never runs
+// as a GEMM: an obs is the static map (0 road, -1 inactive) plus <= N + 1 patched cells
+// (ma_customenv.py:197-209, :303-322), so for every network with obs inputs
+//     x . W1 + b1 = c1 + sum over patched cells c of (obs[c] - map[c]) * W1[c, :],
+//     c1 = b1 + map . W1   (kept as partial sums over 64-row groups of W1, refreshed in the
+//                           launch that changes W1: the Adam step or the soft update),
+// and the W1 gradient X^T dZ1 = map (x) colsum(dZ1) + the patched cells' terms.  So the update
+// reads 48-byte descriptors instead of 2 x 8 KB dense rows per sample, and needs no layer-1 GEMM,
+// no chunk reduction and no gather launch:
+//   dcritic_tail   per (agent k, 16 rows), two 4-wave groups: draws the rows (Philox, the
+//                  gather's formula), decodes their descriptors, runs the K target actors two at a
+//                  time, then the target critic beside the online critic, the TD target and the
+//                  critic backward (its 128 x 128 layer on all 8 waves); records the rows for the
+//                  launches below
+//   dgrads_adam    the critic's parameter gradients (W1 from the patched cells + the column sums
+//                  of dZ1), each element's Adam step in the thread that formed its gradient, the
+//                  new critic's c1 partials
+//   dactor_tail    the actor forward, GumbelSoftmax, the stepped critic on the mixed actions and
+//                  both backwards (each 128 x 128 layer on all 8 waves)
+//   dgrads_adam    the actor's gradients + Adam, both soft target updates, the c1 partials of the
+//                  actor and both targets
+// f32 with fixed summation orders (deterministic; graph / recorded replays equal eager launches).
+// Against the dense formulation it differs by summation order in layer 1 and in the W1 gradient.
+constexpr int NPM = GW_MAX_AGENTS + 1;  // patch slots per (row, agent obs): the apple + N agents
+constexpr int CG = 64;                  // W1 input rows per c1 partial / W1-gradient block
+constexpr int DT = 512;                 // tail threads: two 4-wave groups
+constexpr int NDW = 12;                 // descriptor words (gridenv.hip NDESC)
+constexpr uint32_t DF_RESET = 1u;
+constexpr int DMAXB = 256;              // rows per update the W1 blocks' LDS lists are sized for
+
+struct DQ {  // the descriptor ring and the env's obs source
+    const uint32_t *desc;
+    const float *probs;
+    const double *reward;
+    const uint8_t *term, *done;
+    const int64_t *t_dev;
+    int64_t S, E;
+    const float *base;
+    int apples[MAXK];
+    int N, K, HW, variant;
+};
+
+struct DWs {
+    int32_t *idx;      // [B][2] (transition slot, env) of every row
+    int32_t *pc;       // [2][K][B][NPM] patched cells of (state | next state, agent obs, row)
+    float *pd;         // [2][K][B][NPM] their obs - map deltas (overridden patches dropped)
+    int32_t *np;       // [2][K][B]
+    float *act;        // [B][9K] stored action probabilities
+    float *tact;       // [B][9K] target actions a'
+    float *u;          // [2][K][B][9] Gumbel uniforms (0: target actions, 1: the actor's sample)
+    float *probs;      // [K][B][9] the actor phase's fresh probabilities
+    float *rw, *t1;    // [K][B] f32(reward), 1 - termination
+    Saved sv;          // per-row activations and gradients (critic phase, then the actor's)
+    float *spart;      // [K][B / 16][128] column sums of dZ1 per 16-row tile
+    float *cpart[4];   // c1 partials: actor [K][NG][128], actor target, critic [K][K NG][128], critic target
+    int32_t *snap;     // [4] the Adam step counts of this update (critic, actor)
+};
+
+inline int64_t rnd4(int64_t n) { return (n + 3) & ~(int64_t)3; }
+inline int d_ng(int HW) { return (HW + CG - 1) / CG; }
+inline DWs dws_layout(float *w, int K, int B, int HW) {
+    DWs d;
+    const int NG = d_ng(HW);
+    auto take = [&](int64_t n) { float *q = w; w += rnd4(n); return q; };
+    d.idx = reinterpret_cast<int32_t *>(take(2LL * B));
+    d.pc = reinterpret_cast<int32_t *>(take(2LL * K * B * NPM));
+    d.pd = take(2LL * K * B * NPM);
+    d.np = reinterpret_cast<int32_t *>(take(2LL * K * B));
+    d.act = take((int64_t)B * NA * K);
+    d.tact = take((int64_t)B * NA * K);
+    d.u = take(2LL * K * B * NA);
+    d.probs = take((int64_t)K * B * NA);
+    d.rw = take((int64_t)K * B);
+    d.t1 = take((int64_t)K * B);
+    float **f[8] = {&d.sv.h1, &d.sv.h2, &d.sv.xh1, &d.sv.xh2, &d.sv.gv1, &d.sv.gv2, &d.sv.dz1, &d.sv.dz2};
+    for (float **q : f) *q = take((int64_t)K * B * HID);
+    d.sv.g3 = take((int64_t)K * B * NA);
+    d.sv.aux = take((int64_t)K * B);
+    d.spart = take((int64_t)K * (B / RB) * HID);
+    d.cpart[0] = take((int64_t)K * NG * HID);
+    d.cpart[1] = take((int64_t)K * NG * HID);
+    d.cpart[2] = take((int64_t)K * K * NG * HID);
+    d.cpart[3] = take((int64_t)K * K * NG * HID);
+    d.snap = reinterpret_cast<int32_t *>(take(4));
+    return d;
+}
+int64_t dws_floats(int K, int B, int HW) {
+    float *z = nullptr;
+    const DWs d = dws_layout(z, K, B, HW);
+    return (int64_t)(reinterpret_cast<float *>(d.snap) - z) + 4;
+}
+
+// obs value of agent n in RL agent k's observation (the obs writer's rule, gridenv.hip agent_value)
+__device__ __forceinline__ float d_agent_value(bool reset, int n, int k, bool on_apple, int variant) {
+    if (reset) return on_apple ? 9.5f : 0.5f;
+    if (on_apple) return (float)(n + 1 + 9);
+    if (variant == 1) return (float)(n + 1);
+    int v = n + 1;
+    if (v >= 1 && v <= 4 && v != k + 1) v = 5;
+    if (v == k + 1) v = 1;
+    return (float)v;
+}
+
+// the patched cells of agent k's obs from descriptor words d (wsel 0: the obs, 1: the terminal
+// obs, words 8-11), in the obs writer's order (the own apple, then agents 0 .. N-1; a later
+// patch of the same cell overrides an earlier one), reduced to the surviving cells, as deltas
+// against the map.  Returns the count.
+__device__ __forceinline__ int d_patches(const DQ &q, const uint32_t (&d)[NDW], int wsel, int k, float apple_map,
+                                         int *oc, float *od) {
+    const uint32_t f = d[4];
+    const bool reset = wsel == 0 && (f & DF_RESET);
+    const uint32_t apples = wsel == 0 ? (f >> 8) & 0xFFu : (f >> 16) & 0xFFu;
+    const int ac = ((apples >> k) & 1u) ? q.apples[k] : -1;
+    int pc[NPM];
+    float pv[NPM];
+    int np = 0;
+    if (ac >= 0) {
+        float av = apple_map + 9.0f;
+        if (!reset && av == (float)(k + 1)) av = 1.0f;
+        pc[np] = ac;
+        pv[np] = av;
+        ++np;
+    }
+    for (int n = 0; n < q.N; ++n) {
+        const uint32_t w = wsel == 0 ? d[n >> 1] : d[8 + (n >> 1)];
+        const int c = (int)((w >> (16 * (n & 1))) & 0xFFFFu);
+        pc[np] = c;
+        pv[np] = d_agent_value(reset, n, k, c == ac, q.variant);
+        ++np;
+    }
+    float bv[NPM];
+    for (int i = 0; i < np; ++i) bv[i] = q.base[pc[i]];  // the loads in flight together
+    int m = 0;
+    for (int i = 0; i < np; ++i) {
+        bool keep = true;
+        for (int j = i + 1; j < np; ++j) keep = keep && pc[j] != pc[i];
+        if (keep) {
+            oc[m] = pc[i];
+            od[m] = pv[i] - bv[i];
+            ++m;
+        }
+    }
+    return m;
+}
+
+// row b of the sample: transition slot tr and env e (gw_replay_gather_desc's in-kernel draws)
+__device__ __forceinline__ void d_draw(const DQ &q, uint64_t seed, uint32_t c, int b, int64_t &tr, int64_t &e) {
+    const int64_t t = q.t_dev[0];
+    const uint4 r = gwrng::philox((uint32_t)b, c, gwrng::TAG_SAMPLE, 0u, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const float ub = gwrng::unit(r.x);
+    e = (int64_t)(((uint64_t)r.y * (uint64_t)q.E) >> 32);
+    const int64_t n = t < 1 ? 1 : (t > q.S - 1 ? q.S - 1 : t);
+    int64_t step = (int64_t)(ub * (float)n);
+    if (step > n - 1) step = n - 1;
+    tr = (t - 1 - step) % q.S;
+    if (tr < 0) tr += q.S;
+}
+
+// sum over n partials p[g * HID] in g order (16 loads in flight)
+__device__ __forceinline__ float d_sum_parts(const float *p, int n) {
+    float acc = 0.0f;
+    int g = 0;
+    for (; g + 16 <= n; g += 16) {
+        float v[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = p[(int64_t)(g + i) * HID];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc += v[i];
+    }
+    for (; g < n; ++g) acc += p[(int64_t)g * HID];
+    return acc;
+}
+
+// Gumbel uniforms of (agent kk, row r) in phase ph: Philox(seed; r, c, 'GUM' + ph, 4 kk + j)
+__device__ __forceinline__ void d_gumbel_u(uint64_t seed, uint32_t c, int ph, int kk, int r, float ur[NA]) {
+#pragma unroll
+    for (int j = 0; j < (NA + 3) / 4; ++j) {
+        const uint4 d = gwrng::philox((uint32_t)r, c, gwrng::TAG_GUMBEL + (uint32_t)ph, (uint32_t)(4 * kk + j),
+                                      (uint32_t)seed, (uint32_t)(seed >> 32));
+        const uint32_t w[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (4 * j + i < NA) ur[4 * j + i] = gwrng::unit(w[i]);
+    }
+}
+
+// GumbelSoftmax (tau 1) of logits with uniforms ur: gw_gumbel_softmax's op order
+__device__ __forceinline__ void d_gumbel(const float lg[NA], const float ur[NA], float pr[NA]) {
+    float mx = -INFINITY;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        pr[a] = (lg[a] - logf(-logf(ur[a] + G_EPS) + G_EPS)) / 1.0f;
+        mx = fmaxf(mx, pr[a]);
+    }
+    float sum = 0.0f;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        pr[a] = expf(pr[a] - mx);
+        sum += pr[a];
+    }
+#pragma unroll
+    for (int a = 0; a < NA; ++a) pr[a] = pr[a] / sum;
+}
+
+// z (lane g's 8 features) += the patched cells' terms: W1 rows row0 + cell
+__device__ __forceinline__ void d_add_patches(float z[8], const float *w1, int64_t row0, const int16_t *pc,
+                                              const float *pd, int np, int g) {
+#pragma unroll 3
+    for (int i = 0; i < np; ++i) {
+        const float dv = pd[i];
+        const float *wr = w1 + (row0 + pc[i]) * HID + 8 * g;
+        const float4 a = *reinterpret_cast<const float4 *>(wr), b = *reinterpret_cast<const float4 *>(wr + 4);
+        z[0] = fmaf(dv, a.x, z[0]); z[1] = fmaf(dv, a.y, z[1]); z[2] = fmaf(dv, a.z, z[2]); z[3] = fmaf(dv, a.w, z[3]);
+        z[4] = fmaf(dv, b.x, z[4]); z[5] = fmaf(dv, b.y, z[5]); z[6] = fmaf(dv, b.z, z[6]); z[7] = fmaf(dv, b.w, z[7]);
+    }
+}
+
+// z += the action inputs' terms (na values, W1 rows row0 ..), in input order
+__device__ __forceinline__ void d_add_actions(float z[8], const float *w1, int64_t row0, const float *av, int na,
+                                              int g) {
+#pragma unroll 9
+    for (int a = 0; a < na; ++a) {
+        const float v = av[a];
+        const float *wr = w1 + (row0 + a) * HID + 8 * g;
+        const float4 w0 = *reinterpret_cast<const float4 *>(wr), w1v = *reinterpret_cast<const float4 *>(wr + 4);
+        z[0] = fmaf(v, w0.x, z[0]); z[1] = fmaf(v, w0.y, z[1]); z[2] = fmaf(v, w0.z, z[2]); z[3] = fmaf(v, w0.w, z[3]);
+        z[4] = fmaf(v, w1v.x, z[4]); z[5] = fmaf(v, w1v.y, z[5]); z[6] = fmaf(v, w1v.z, z[6]); z[7] = fmaf(v, w1v.w, z[7]);
+    }
+}
+
+// the block's 16 rows through a 128 x 128 layer on all 8 waves of a 512-thread block (wave w:
+// columns 16 w .. 16 w + 15; each output the k-ordered f32 fma chain over c = 0 .. 127 from 0, the
+// same values as gemv16); every thread calls it, s_z [16][HP] receives z
+__device__ __forceinline__ void gemv_all(const float *s_h, const float *__restrict__ w, bool transpose, float *s_z) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, lr = lane & 15, lq = lane >> 4;
+    const int n0 = 16 * wave + lr;
+    f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int kk = 0; kk < HID / 4; ++kk) {
+        const int c = 4 * kk + lq;
+        const float a = s_h[lr * HP + c];
+        const float b = transpose ? w[n0 * HID + c] : w[c * HID + n0];
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s_z[(4 * lq + i) * HP + n0] = acc[i];
+}
+
+// rows_gemv on all 8 waves: the `own` threads (the row layout's owners) write v and read out
+__device__ __forceinline__ void rows_gemv_all(bool own, const float v[8], int rl, int g, const float *w, bool transpose,
+                                              float *s_in, float *s_out, float out[8]) {
+    if (own) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s_in[rl * HP + 8 * g + i] = v[i];
+    }
+    __syncthreads();
+    gemv_all(s_in, w, transpose, s_out);
+    __syncthreads();
+    if (own) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) out[i] = s_out[rl * HP + 8 * g + i];
+    }
+}
+
+// after layer 1: LN -> ReLU -> the 128 x 128 layer (this group's 4 waves) -> LN -> ReLU -> nout outputs
+__device__ __forceinline__ void d_fwd_rest(float z[8], const Mlp &m, int nout, int rl, int g, float *s_in,
+                                           float *s_out, RowFwd &f, float out[NA]) {
+    ln_relu(z, m.lw1, m.lb1, g, f.xh1, f.y1, f.rs1);
+    rows_gemv(f.y1, rl, g, m.w2, false, s_in, s_out, z);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) z[i] += m.b2[8 * g + i];
+    ln_relu(z, m.lw2, m.lb2, g, f.xh2, f.y2, f.rs2);
+    for (int a = 0; a < nout; ++a) {
+        float s = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s = fmaf(f.y2[i], m.w3[(8 * g + i) * nout + a], s);
+        out[a] = row_sum(s) + m.b3[a];
+    }
+}
+
+struct DTail {
+    DQ q;
+    DWs w;
+    gw_mlp_actors at, ct, c, a;  // actor target, critic target, critic, actor
+    uint64_t seed;
+    const int32_t *ctr;          // the draws' counter: the critic optimizer's step count
+    const int32_t *count;        // the optimizer count this phase snapshots (critic / actor)
+    float gamma;
+    int K, B, NG;
+};
+
+__global__ void __launch_bounds__(DT) dcritic_tail(DTail p) {
+    __shared__ __attribute__((aligned(16))) float s_in[2][RB * HP];
+    __shared__ __attribute__((aligned(16))) float s_out[2][RB * HP];
+    __shared__ int16_t s_pc[2][RB][MAXK][NPM];
+    __shared__ float s_pd[2][RB][MAXK][NPM];
+    __shared__ int s_np[2][RB][MAXK];
+    __shared__ float s_act[RB][NA * MAXK], s_tact[RB][NA * MAXK];
+    __shared__ float s_c1[MAXK + 2][HID];
+    __shared__ float s_y[RB], s_rw[RB], s_t1[RB];
+    const int k = blockIdx.y, tid = threadIdx.x, grp = tid >> 8, lt = tid & 255, rl = lt >> 4, g = lt & 15;
+    const int K = p.K, B = p.B, HW = p.q.HW, r0 = blockIdx.x * RB, r = r0 + rl;
+    const int64_t E = p.q.E;
+    const uint32_t c = (uint32_t)p.ctr[0];
+    const bool rec = k == 0;  // the k = 0 blocks record the rows for the later launches
+    // c1 of the networks this block runs: the K target actors, critic target k, critic k
+    for (int o = tid; o < (K + 2) * HID; o += DT) {
+        const int net = o / HID, j = o % HID;
+        float v;
+        if (net < K)
+            v = p.at.b1[net * HID + j] + d_sum_parts(p.w.cpart[1] + (int64_t)net * p.NG * HID + j, p.NG);
+        else if (net == K)
+            v = p.ct.b1[k * HID + j] + d_sum_parts(p.w.cpart[3] + (int64_t)k * K * p.NG * HID + j, K * p.NG);
+        else
+            v = p.c.b1[k * HID + j] + d_sum_parts(p.w.cpart[2] + (int64_t)k * K * p.NG * HID + j, K * p.NG);
+        s_c1[net][j] = v;
+    }
+    // the rows' descriptors -> patched cells: one thread per (row, state | next state, agent obs)
+    if (tid < RB * 2 * K) {
+        const int rr = tid / (2 * K), which = (tid / K) & 1, kk = tid % K;
+        int64_t tr, e;
+        d_draw(p.q, p.seed, c, r0 + rr, tr, e);
+        const int64_t nx = (tr + 1) % p.q.S;
+        const bool dn = p.q.done[tr * E + e] != 0;
+        const uint4 *d4 = reinterpret_cast<const uint4 *>(p.q.desc + ((which == 0 ? tr : nx) * E + e) * NDW);
+        const uint4 a0 = d4[0], a1 = d4[1], a2 = d4[2];
+        const uint32_t d[NDW] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w};
+        const float apple_map = p.q.apples[kk] >= 0 ? p.q.base[p.q.apples[kk]] : 0.0f;
+        int oc[NPM];
+        float od[NPM];
+        const int m = d_patches(p.q, d, which == 0 ? 0 : (dn ? 1 : 0), kk, apple_map, oc, od);
+        s_np[which][rr][kk] = m;
+        const int64_t ro = ((int64_t)(which * K + kk) * B + r0 + rr);
+        for (int i = 0; i < m; ++i) {
+            s_pc[which][rr][kk][i] = (int16_t)oc[i];
+            s_pd[which][rr][kk][i] = od[i];
+            if (rec) {
+                p.w.pc[ro * NPM + i] = oc[i];
+                p.w.pd[ro * NPM + i] = od[i];
+            }
+        }
+        if (rec) {
+            p.w.np[ro] = m;
+            if (which == 0 && kk == 0) {
+                p.w.idx[2 * (r0 + rr)] = (int32_t)tr;
+                p.w.idx[2 * (r0 + rr) + 1] = (int32_t)e;
+            }
+        }
+    }
+    // the stored action probabilities of every agent (the critic's action inputs)
+    for (int o = tid; o < RB * NA * K; o += DT) {
+        const int rr = o / (NA * K), a = o % (NA * K), kk = a / NA;
+        int64_t tr, e;
+        d_draw(p.q, p.seed, c, r0 + rr, tr, e);
+        const float v = p.q.probs[((tr * K + kk) * E + e) * NA + a % NA];
+        s_act[rr][a] = v;
+        if (rec) p.w.act[(int64_t)(r0 + rr) * NA * K + a] = v;
+    }
+    // agent k's reward and termination (the TD target)
+    if (tid >= DT - RB) {
+        const int rr = tid - (DT - RB);
+        int64_t tr, e;
+        d_draw(p.q, p.seed, c, r0 + rr, tr, e);
+        const float rw = (float)p.q.reward[(tr * E + e) * K + k];
+        const float t1 = 1.0f - (float)p.q.term[(tr * E + e) * K + k];
+        s_rw[rr] = rw;
+        s_t1[rr] = t1;
+        p.w.rw[(int64_t)k * B + r0 + rr] = rw;
+        p.w.t1[(int64_t)k * B + r0 + rr] = t1;
+    }
+    if (blockIdx.x == 0 && k == 0 && tid == 0) p.w.snap[0] = p.count[0] + 1;
+    __syncthreads();
+    // the target actions a'_kk = GumbelSoftmax(actor_target_kk(s'_kk)), two agents at a time (a
+    // group without an agent in the last round recomputes agent K - 1 and discards it)
+    for (int rd = 0; rd < (K + 1) / 2; ++rd) {
+        const int kk = 2 * rd + grp, kx = kk < K ? kk : K - 1;
+        const Mlp m = mlp_k(p.at, kx, HW, NA);
+        float z[8], out[NA];
+        RowFwd f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) z[i] = s_c1[kx][8 * g + i];
+        d_add_patches(z, m.w1, 0, s_pc[1][rl][kx], s_pd[1][rl][kx], s_np[1][rl][kx], g);
+        d_fwd_rest(z, m, NA, rl, g, s_in[grp], s_out[grp], f, out);
+        if (kk < K) {
+            float ur[NA], pr[NA];
+            d_gumbel_u(p.seed, c, 0, kk, r, ur);
+            d_gumbel(out, ur, pr);
+            if (g == 0) {
+#pragma unroll
+                for (int a = 0; a < NA; ++a) s_tact[rl][NA * kk + a] = pr[a];
+                if (rec) {
+#pragma unroll
+                    for (int a = 0; a < NA; ++a) {
+                        p.w.tact[(int64_t)r * NA * K + NA * kk + a] = pr[a];
+                        p.w.u[((int64_t)kk * B + r) * NA + a] = ur[a];
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // group 0: the target critic on (s', a'); group 1: the online critic on (s, a)
+    const int in_c = K * HW + NA * K;
+    RowFwd f;
+    float out[NA];
+    {
+        const bool tgt = grp == 0;
+        const Mlp m = mlp_k(tgt ? p.ct : p.c, k, in_c, 1);
+        const int which = tgt ? 1 : 0;
+        float z[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) z[i] = s_c1[tgt ? K : K + 1][8 * g + i];
+        for (int kk = 0; kk < K; ++kk)
+            d_add_patches(z, m.w1, (int64_t)kk * HW, s_pc[which][rl][kk], s_pd[which][rl][kk], s_np[which][rl][kk], g);
+        d_add_actions(z, m.w1, (int64_t)K * HW, tgt ? s_tact[rl] : s_act[rl], NA * K, g);
+        d_fwd_rest(z, m, 1, rl, g, s_in[grp], s_out[grp], f, out);
+    }
+    // y = f32(r) + ((1 - d) * gamma) * q_next (gw_td_target's op order)
+    if (grp == 0 && g == 0) s_y[rl] = s_rw[rl] + (s_t1[rl] * p.gamma) * out[0];
+    __syncthreads();
+    const Mlp m = mlp_k(p.c, k, in_c, 1);
+    float gy[8], gv1[8], dz1[8], gv2[8], dz2[8], dq = 0.0f, diff = 0.0f;
+    if (grp == 1) {
+        diff = out[0] - s_y[rl];
+        dq = (1.0f / (float)B) * (2.0f * diff);  // MSELoss backward (gw_mean_loss_bwd's order)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) gy[i] = dq * m.w3[8 * g + i];
+        ln_relu_bwd(gy, f.y2, f.xh2, f.rs2, m.lw2, g, gv2, dz2);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s_in[1][rl * HP + 8 * g + i] = dz2[i];
+    }
+    __syncthreads();
+    gemv_all(s_in[1], m.w2, true, s_out[1]);
+    __syncthreads();
+    if (grp == 1) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) gy[i] = s_out[1][rl * HP + 8 * g + i];
+        ln_relu_bwd(gy, f.y1, f.xh1, f.rs1, m.lw1, g, gv1, dz1);
+        const Saved &sv = p.w.sv;
+        put8(sv.h1, K, B, k, r, g, f.y1);
+        put8(sv.h2, K, B, k, r, g, f.y2);
+        put8(sv.xh1, K, B, k, r, g, f.xh1);
+        put8(sv.xh2, K, B, k, r, g, f.xh2);
+        put8(sv.gv1, K, B, k, r, g, gv1);
+        put8(sv.gv2, K, B, k, r, g, gv2);
+        put8(sv.dz1, K, B, k, r, g, dz1);
+        put8(sv.dz2, K, B, k, r, g, dz2);
+        if (g == 0) {
+            sv.g3[(int64_t)k * B + r] = dq;
+            sv.aux[(int64_t)k * B + r] = diff * diff;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s_in[1][rl * HP + 8 * g + i] = dz1[i];
+    }
+    __syncthreads();
+    if (tid < HID) {  // the tile's column sums of dZ1, rows in order
+        float acc = 0.0f;
+        for (int rr = 0; rr < RB; ++rr) acc += s_in[1][rr * HP + tid];
+        p.w.spart[((int64_t)k * (B / RB) + blockIdx.x) * HID + tid] = acc;
+    }
+}
+
+__global__ void __launch_bounds__(DT) dactor_tail(DTail p) {
+    __shared__ __attribute__((aligned(16))) float s_in[RB * HP];
+    __shared__ __attribute__((aligned(16))) float s_out[RB * HP];
+    __shared__ int16_t s_pc[RB][MAXK][NPM];
+    __shared__ float s_pd[RB][MAXK][NPM];
+    __shared__ int s_np[RB][MAXK];
+    __shared__ float s_act[RB][NA * MAXK];
+    __shared__ float s_c1[2][HID];
+    const int k = blockIdx.y, tid = threadIdx.x, grp = tid >> 8, lt = tid & 255, rl = lt >> 4, g = lt & 15;
+    const int K = p.K, B = p.B, HW = p.q.HW, r0 = blockIdx.x * RB, r = r0 + rl;
+    const bool own = grp == 0;  // the row layout's owners; group 1 joins the 128 x 128 layers
+    const uint32_t c = (uint32_t)p.ctr[0];  // the critic's count, advanced by the critic's step
+    if (tid < 2 * HID) {
+        const int net = tid / HID, j = tid % HID;
+        s_c1[net][j] = net == 0 ? p.a.b1[k * HID + j] + d_sum_parts(p.w.cpart[0] + (int64_t)k * p.NG * HID + j, p.NG)
+                                : p.c.b1[k * HID + j] +
+                                      d_sum_parts(p.w.cpart[2] + (int64_t)k * K * p.NG * HID + j, K * p.NG);
+    }
+    for (int o = tid; o < RB * K * NPM; o += DT) {  // the rows' states (recorded by the critic tail)
+        const int rr = o / (K * NPM), kk = (o / NPM) % K, i = o % NPM;
+        const int64_t ro = (int64_t)kk * B + r0 + rr;
+        const int n = p.w.np[ro];
+        if (i == 0) s_np[rr][kk] = n;
+        if (i < n) {
+            s_pc[rr][kk][i] = (int16_t)p.w.pc[ro * NPM + i];
+            s_pd[rr][kk][i] = p.w.pd[ro * NPM + i];
+        }
+    }
+    for (int o = tid; o < RB * NA * K; o += DT) s_act[o / (NA * K)][o % (NA * K)] = p.w.act[(int64_t)r0 * NA * K + o];
+    if (blockIdx.x == 0 && k == 0 && tid == 0) p.w.snap[1] = p.count[0] + 1;
+    __syncthreads();
+    const int in_c = K * HW + NA * K;
+    const Mlp ma = mlp_k(p.a, k, HW, NA);
+    const Mlp mc = mlp_k(p.c, k, in_c, 1);
+    RowFwd fa, fc;
+    float z[8], pr[NA];
+    // the actor's forward and its GumbelSoftmax sample
+    if (own) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) z[i] = s_c1[0][8 * g + i];
+        d_add_patches(z, ma.w1, 0, s_pc[rl][k], s_pd[rl][k], s_np[rl][k], g);
+        ln_relu(z, ma.lw1, ma.lb1, g, fa.xh1, fa.y1, fa.rs1);
+    }
+    rows_gemv_all(own, fa.y1, rl, g, ma.w2, false, s_in, s_out, z);
+    if (own) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) z[i] += ma.b2[8 * g + i];
+        ln_relu(z, ma.lw2, ma.lb2, g, fa.xh2, fa.y2, fa.rs2);
+        float lg[NA], ur[NA];
+#pragma unroll
+        for (int a = 0; a < NA; ++a) {
+            float s = 0.0f;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) s = fmaf(fa.y2[i], ma.w3[(8 * g + i) * NA + a], s);
+            lg[a] = row_sum(s) + ma.b3[a];
+        }
+        d_gumbel_u(p.seed, c, 1, k, r, ur);
+        d_gumbel(lg, ur, pr);
+        if (g == 0) {
+#pragma unroll
+            for (int a = 0; a < NA; ++a) {
+                p.w.probs[((int64_t)k * B + r) * NA + a] = pr[a];
+                p.w.u[((int64_t)(K + k) * B + r) * NA + a] = ur[a];
+                s_act[rl][NA * k + a] = pr[a];  // the row's 16 lanes are one wave: LDS in order
+            }
+        }
+        // the stepped critic k on the mixed actions
+#pragma unroll
+        for (int i = 0; i < 8; ++i) z[i] = s_c1[1][8 * g + i];
+        for (int kk = 0; kk < K; ++kk)
+            d_add_patches(z, mc.w1, (int64_t)kk * HW, s_pc[rl][kk], s_pd[rl][kk], s_np[rl][kk], g);
+        d_add_actions(z, mc.w1, (int64_t)K * HW, s_act[rl], NA * K, g);
+        ln_relu(z, mc.lw1, mc.lb1, g, fc.xh1, fc.y1, fc.rs1);
+    }
+    rows_gemv_all(own, fc.y1, rl, g, mc.w2, false, s_in, s_out, z);
+    float q = 0.0f, gy[8], gv1[8], dz1[8], gv2[8], dz2[8];
+    const float dq = -(1.0f / (float)B);  // -mean Q backward (gw_mean_loss_bwd mode 1)
+    if (own) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) z[i] += mc.b2[8 * g + i];
+        ln_relu(z, mc.lw2, mc.lb2, g, fc.xh2, fc.y2, fc.rs2);
+        float s = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s = fmaf(fc.y2[i], mc.w3[8 * g + i], s);
+        q = row_sum(s) + mc.b3[0];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) gy[i] = dq * mc.w3[8 * g + i];
+        ln_relu_bwd(gy, fc.y2, fc.xh2, fc.rs2, mc.lw2, g, gv2, dz2);
+    }
+    rows_gemv_all(own, dz2, rl, g, mc.w2, true, s_in, s_out, gy);
+    float dl[NA];
+    if (own) {
+        ln_relu_bwd(gy, fc.y1, fc.xh1, fc.rs1, mc.lw1, g, gv1, dz1);
+        // d probs_k = dz1 . W1[the agent's action rows]^T, then the softmax backward (tau 1)
+        float dp[NA];
+#pragma unroll
+        for (int a = 0; a < NA; ++a) {
+            const float *wr = mc.w1 + ((int64_t)K * HW + NA * k + a) * HID + 8 * g;
+            float s = 0.0f;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) s = fmaf(dz1[i], wr[i], s);
+            dp[a] = row_sum(s);
+        }
+        float dot = 0.0f;
+#pragma unroll
+        for (int a = 0; a < NA; ++a) dot = fmaf(pr[a], dp[a], dot);
+#pragma unroll
+        for (int a = 0; a < NA; ++a) dl[a] = pr[a] * (dp[a] - dot);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            float s = 0.0f;
+#pragma unroll
+            for (int a = 0; a < NA; ++a) s = fmaf(dl[a], ma.w3[(8 * g + i) * NA + a], s);
+            gy[i] = s;
+        }
+        ln_relu_bwd(gy, fa.y2, fa.xh2, fa.rs2, ma.lw2, g, gv2, dz2);
+    }
+    rows_gemv_all(own, dz2, rl, g, ma.w2, true, s_in, s_out, gy);
+    if (own) {
+        ln_relu_bwd(gy, fa.y1, fa.xh1, fa.rs1, ma.lw1, g, gv1, dz1);
+        const Saved &sv = p.w.sv;
+        put8(sv.h1, K, B, k, r, g, fa.y1);
+        put8(sv.h2, K, B, k, r, g, fa.y2);
+        put8(sv.xh1, K, B, k, r, g, fa.xh1);
+        put8(sv.xh2, K, B, k, r, g, fa.xh2);
+        put8(sv.gv1, K, B, k, r, g, gv1);
+        put8(sv.gv2, K, B, k, r, g, gv2);
+        put8(sv.dz1, K, B, k, r, g, dz1);
+        put8(sv.dz2, K, B, k, r, g, dz2);
+        if (g == 0) {
+#pragma unroll
+            for (int a = 0; a < NA; ++a) sv.g3[((int64_t)k * B + r) * NA + a] = dl[a];
+            sv.aux[(int64_t)k * B + r] = q;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s_in[rl * HP + 8 * g + i] = dz1[i];
+    }
+    __syncthreads();
+    if (tid < HID) {
+        float acc = 0.0f;
+        for (int rr = 0; rr < RB; ++rr) acc += s_in[rr * HP + tid];
+        p.w.spart[((int64_t)k * (B / RB) + blockIdx.x) * HID + tid] = acc;
+    }
+}
+
+// ---- the parameter gradients with each element's Adam step ------------------------------------
+struct DGrad {
+    DWs w;
+    const float *base;
+    gw_mlp_actors net;           // the network stepped (critic: phase 0, actor: phase 1)
+    float *p0, *g0, *m0, *v0;    // its flat parameter / gradient / exp_avg / exp_avg_sq buffers
+    float *t0;                   // phase 1: the actor target's flat buffer (soft update)
+    gw_mlp_actors cnet;          // phase 1: the (stepped) critic, for the critic target's soft update
+    const float *cp0;
+    float *ct0;                  //   its flat buffer and the critic target's
+    int64_t cn;                  //   their length
+    double lr, beta1, beta2, eps;
+    float tau;
+    int32_t *count;              // the optimizer's step count (written: this step's)
+    float *loss;                 // [K]
+    int phase, K, B, HW, NG, nobs, in_dim, out, nrest;
+    int start[8];                // first block of each block type (7 types)
+};
+
+struct AdamSc {
+    float step_size, bc2, w1, b2, w2, e;
+};
+
+__device__ __forceinline__ float adam_el(const DGrad &p, const AdamSc &a, int64_t off, float gi) {
+    p.g0[off] = gi;
+    const float mo = p.m0[off], vo = p.v0[off], po = p.p0[off];
+    const float mi = __fmaf_rn(a.w1, gi - mo, mo);         // exp_avg.lerp_(grad, 1 - beta1)
+    const float vi = __fmaf_rn(a.w2 * gi, gi, vo * a.b2);  // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
+    p.m0[off] = mi;
+    p.v0[off] = vi;
+    const float denom = sqrtf(vi) / a.bc2 + a.e;            // (exp_avg_sq.sqrt() / bc2_sqrt).add_(eps)
+    const float pi = __fmaf_rn(-a.step_size, mi / denom, po);  // param.addcdiv_(exp_avg, denom, -step_size)
+    p.p0[off] = pi;
+    return pi;
+}
+
+// phase 1: the actor target at the same offset, t = tau p + (1 - tau) t (agilerl soft_update)
+__device__ __forceinline__ float soft_el(float *t, int64_t off, float pi, float tau) {
+    const float ti = tau * pi + (1.0f - tau) * t[off];
+    t[off] = ti;
+    return ti;
+}
+
+// block exclusive prefix (thread order) of v over 256 threads; total returned in `total`
+__device__ __forceinline__ int d_excl_scan256(int v, int *red, int &total) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int incl = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    __syncthreads();
+    if (lane == 63) red[wave] = incl;
+    __syncthreads();
+    int before = 0;
+    total = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const int x = red[w];
+        if (w < wave) before += x;
+        total += x;
+    }
+    return before + incl - v;
+}
+
+__global__ void __launch_bounds__(256) dgrads_adam(DGrad p) {
+    __shared__ float s_S[HID], s_base[CG], s_pp[2][2][HID];
+    __shared__ int s_cnt[CG + 1], s_red[4];
+    __shared__ float s_sc[2];
+    __shared__ __attribute__((aligned(16))) float smem[GRG * HID * NA + GRG * (NA + 1) > RB * (TILE_R + 4) + TILE_R * HID
+                                                        ? GRG * HID * NA + GRG * (NA + 1)
+                                                        : RB * (TILE_R + 4) + TILE_R * HID];
+    static_assert(4 * DMAXB * NPM <= GRG * HID * NA, "the W1 blocks' entry lists fit the shared buffer");
+    // the W1 blocks' entry lists (cell, row, delta) and per-cell buckets, in the shared buffer
+    int *s_ec = reinterpret_cast<int *>(smem), *s_er = s_ec + DMAXB * NPM, *s_bk = s_er + DMAXB * NPM;
+    float *s_ed = reinterpret_cast<float *>(s_bk + DMAXB * NPM);
+    const int tid = threadIdx.x, K = p.K, B = p.B, HW = p.HW, NG = p.NG;
+    int b = blockIdx.x, type = 0;
+    while (type < 6 && b >= p.start[type + 1]) ++type;
+    b -= p.start[type];
+    // this step's Adam scalars (the count the tail snapshotted; torch forms them in double)
+    if (tid == 0) {
+        const double s = (double)p.w.snap[p.phase];
+        s_sc[0] = (float)(p.lr / (1.0 - pow(p.beta1, s)));
+        s_sc[1] = (float)sqrt(1.0 - pow(p.beta2, s));
+        if (blockIdx.x == 0) p.count[0] = p.w.snap[p.phase];
+    }
+    __syncthreads();
+    AdamSc sc;
+    sc.step_size = s_sc[0];
+    sc.bc2 = s_sc[1];
+    sc.w1 = (float)(1.0 - p.beta1);
+    sc.b2 = (float)p.beta2;
+    sc.w2 = (float)(1.0 - p.beta2);
+    sc.e = (float)p.eps;
+    const bool soft = p.phase == 1;
+    if (type == 0 || type == 5) {
+        // W1 rows of one 64-cell group of one agent obs: type 0 the stepped network (gradient +
+        // Adam [+ the actor target's soft update]), type 5 the critic target's soft update; both
+        // leave the group's c1 partials
+        const int nob = type == 0 ? p.nobs : K;
+        const int k = b / (nob * NG), ob = (b / NG) % nob, grp = b % NG;
+        const int c0 = grp * CG, ncell = min(CG, HW - c0);
+        const int j = tid & (HID - 1), h = tid >> 7;
+        const bool critic = type == 5 || p.phase == 0;
+        const int in_dim = type == 5 ? K * HW + NA * K : p.in_dim;
+        const int64_t row0 = critic ? (int64_t)ob * HW + c0 : c0;  // W1 input row of cell c0
+        if (tid < ncell) s_base[tid] = p.base[c0 + tid];
+        if (type == 5) {
+            __syncthreads();
+            float tp = 0.0f;
+            const float *cw = p.cnet.w1 + ((int64_t)k * in_dim + row0) * HID + j;
+            for (int cc = h; cc < ncell; cc += 2) {
+                const int64_t off = (cw + (int64_t)cc * HID) - p.cp0;
+                const float ti = soft_el(p.ct0, off, p.cp0[off], p.tau);
+                tp = fmaf(s_base[cc], ti, tp);
+            }
+            s_pp[1][h][j] = tp;
+            __syncthreads();
+            if (tid < HID)
+                p.w.cpart[3][((int64_t)k * K * NG + ob * NG + grp) * HID + tid] = s_pp[1][0][tid] + s_pp[1][1][tid];
+            return;
+        }
+        if (tid < HID) {  // the column sums of dZ1 over the tiles in order
+            float acc = 0.0f;
+            for (int t = 0; t < B / RB; ++t) acc += p.w.spart[((int64_t)k * (B / RB) + t) * HID + tid];
+            s_S[tid] = acc;
+        }
+        // the patched cells of the rows' obs `obk` inside this group, in (row, slot) order
+        const int obk = p.phase == 0 ? ob : k;
+        const int NE = B * NPM, per = (NE + 255) / 256, t0 = tid * per;
+        int cnt = 0;
+        for (int i = 0; i < per; ++i) {
+            const int t = t0 + i;
+            if (t >= NE) break;
+            const int rr = t / NPM, pi = t % NPM;
+            const int64_t ro = (int64_t)obk * B + rr;
+            if (pi < p.w.np[ro]) {
+                const int cl = p.w.pc[ro * NPM + pi] - c0;
+                cnt += (cl >= 0 && cl < ncell) ? 1 : 0;
+            }
+        }
+        int total = 0;
+        int at = d_excl_scan256(cnt, s_red, total);
+        for (int i = 0; i < per; ++i) {
+            const int t = t0 + i;
+            if (t >= NE) break;
+            const int rr = t / NPM, pi = t % NPM;
+            const int64_t ro = (int64_t)obk * B + rr;
+            if (pi < p.w.np[ro]) {
+                const int cl = p.w.pc[ro * NPM + pi] - c0;
+                if (cl >= 0 && cl < ncell) {
+                    s_ec[at] = cl;
+                    s_er[at] = rr;
+                    s_ed[at] = p.w.pd[ro * NPM + pi];
+                    ++at;
+                }
+            }
+        }
+        __syncthreads();
+        // per-cell buckets, entries in list order (stable)
+        if (tid < CG) {
+            int n = 0;
+            for (int e = 0; e < total; ++e) n += s_ec[e] == tid ? 1 : 0;
+            int incl = n;  // wave 0: an inclusive scan over the 64 cells
+            for (int o = 1; o < 64; o <<= 1) {
+                const int t = __shfl_up(incl, o, 64);
+                if ((tid & 63) >= o) incl += t;
+            }
+            s_cnt[tid + 1] = incl;
+            if (tid == 0) s_cnt[0] = 0;
+            int pos = incl - n;
+            for (int e = 0; e < total; ++e)
+                if (s_ec[e] == tid) s_bk[pos++] = e;
+        }
+        __syncthreads();
+        // gradient = map * colsum(dZ1) + the cell's patched rows' terms (row order); Adam
+        const float *wk = p.net.w1 + ((int64_t)k * in_dim + row0) * HID + j;
+        const float *dz1 = p.w.sv.dz1 + (int64_t)k * B * HID + j;
+        float pp = 0.0f, tp = 0.0f;
+        for (int cc = h; cc < ncell; cc += 2) {
+            float gi = s_base[cc] * s_S[j];
+            for (int e = s_cnt[cc]; e < s_cnt[cc + 1]; ++e) {
+                const int ei = s_bk[e];
+                gi = fmaf(s_ed[ei], dz1[(int64_t)s_er[ei] * HID], gi);
+            }
+            const int64_t off = (wk + (int64_t)cc * HID) - p.p0;
+            const float pi = adam_el(p, sc, off, gi);
+            pp = fmaf(s_base[cc], pi, pp);
+            if (soft) tp = fmaf(s_base[cc], soft_el(p.t0, off, pi, p.tau), tp);
+        }
+        s_pp[0][h][j] = pp;
+        s_pp[1][h][j] = tp;
+        __syncthreads();
+        if (tid < HID) {
+            const int64_t gi = p.phase == 0 ? ((int64_t)k * K * NG + ob * NG + grp) : ((int64_t)k * NG + grp);
+            p.w.cpart[p.phase == 0 ? 2 : 0][gi * HID + tid] = s_pp[0][0][tid] + s_pp[0][1][tid];
+            if (soft) p.w.cpart[1][gi * HID + tid] = s_pp[1][0][tid] + s_pp[1][1][tid];
+        }
+        return;
+    }
+    if (type == 1) {  // the critic's action rows: dense, sum over the rows in order
+        const int k = b, na = NA * K;
+        const int j = tid & (HID - 1), h = tid >> 7;
+        const float *dz1 = p.w.sv.dz1 + (int64_t)k * B * HID + j;
+        for (int a0 = h; a0 < na; a0 += 16) {  // 8 action rows of this thread per pass
+            float acc[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc[u] = 0.0f;
+            for (int rr = 0; rr < B; ++rr) {
+                const float d = dz1[(int64_t)rr * HID];
+                const float *av = p.w.act + (int64_t)rr * na;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int a = a0 + 2 * u;
+                    if (a < na) acc[u] = fmaf(av[a], d, acc[u]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int a = a0 + 2 * u;
+                if (a < na) {
+                    const int64_t off = (p.net.w1 + ((int64_t)k * p.in_dim + (int64_t)K * HW + a) * HID + j) - p.p0;
+                    adam_el(p, sc, off, acc[u]);
+                }
+            }
+        }
+        return;
+    }
+    if (type == 2) {  // W2 = h1^T dz2 (v_mfma_f32_16x16x4_f32, rows in order), 16 inputs per block
+        const int k = b / (HID / RB), d0 = (b % (HID / RB)) * RB;
+        float (*s_x)[TILE_R + 4] = reinterpret_cast<float (*)[TILE_R + 4]>(smem);      // [input][row]
+        float (*s_dz)[HID] = reinterpret_cast<float (*)[HID]>(smem + RB * (TILE_R + 4));  // [row][feature]
+        const int lane = tid & 63, wave = tid >> 6, lr = lane & 15, lq = lane >> 4;
+        f32x4 acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = {0.0f, 0.0f, 0.0f, 0.0f};
+        const int n0 = 32 * wave + lr, n1 = n0 + 16;
+        for (int r0 = 0; r0 < B; r0 += TILE_R) {
+            const int nr = min(TILE_R, B - r0);
+            __syncthreads();
+            constexpr int XN = RB * TILE_R / 256, ZN = TILE_R * HID / 4 / 256;
+            float xv[XN];
+            float4 zv[ZN];
+#pragma unroll
+            for (int t = 0; t < XN; ++t) {
+                const int i = tid + 256 * t, rr = i / RB, d = i % RB;
+                xv[t] = rr < nr ? p.w.sv.h1[((int64_t)k * B + r0 + rr) * HID + d0 + d] : 0.0f;
+            }
+#pragma unroll
+            for (int t = 0; t < ZN; ++t) {
+                const int i = tid + 256 * t, rr = i / (HID / 4), cq = i % (HID / 4);
+                zv[t] = rr < nr ? reinterpret_cast<const float4 *>(p.w.sv.dz2 + ((int64_t)k * B + r0 + rr) * HID)[cq]
+                                : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            }
+#pragma unroll
+            for (int t = 0; t < XN; ++t) {
+                const int i = tid + 256 * t;
+                if (i / RB < nr) s_x[i % RB][i / RB] = xv[t];
+            }
+#pragma unroll
+            for (int t = 0; t < ZN; ++t) {
+                const int i = tid + 256 * t;
+                if (i / (HID / 4) < nr) *reinterpret_cast<float4 *>(&s_dz[i / (HID / 4)][4 * (i % (HID / 4))]) = zv[t];
+            }
+            __syncthreads();
+            for (int kk = 0; kk < nr / 4; ++kk) {
+                const int rr = 4 * kk + lq;
+                const float a = s_x[lr][rr];
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, s_dz[rr][n0], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, s_dz[rr][n1], acc1, 0, 0, 0);
+            }
+        }
+        const float *w2 = p.net.w2 + (int64_t)k * HID * HID;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int d = d0 + 4 * lq + i;
+            const int64_t o0 = (w2 + (int64_t)d * HID + n0) - p.p0, o1 = (w2 + (int64_t)d * HID + n1) - p.p0;
+            const float q0 = adam_el(p, sc, o0, acc0[i]), q1 = adam_el(p, sc, o1, acc1[i]);
+            if (soft) {
+                soft_el(p.t0, o0, q0, p.tau);
+                soft_el(p.t0, o1, q1, p.tau);
+            }
+        }
+        return;
+    }
+    const int rg = tid >> 4, g = tid & 15;
+    if (type == 3) {  // b1, ln1 affine, b2, ln2 affine: 16 row groups, combined in group order
+        const int k = b;
+        const int64_t base = (int64_t)k * B * HID;
+        float acc[6][8];
+#pragma unroll
+        for (int v = 0; v < 6; ++v)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) acc[v][i] = 0.0f;
+#pragma unroll 2
+        for (int r = rg; r < B; r += GRG) {
+            const int64_t o = base + (int64_t)r * HID + 8 * g;
+            const float *src[6] = {p.w.sv.dz1 + o, p.w.sv.gv1 + o, p.w.sv.xh1 + o, p.w.sv.dz2 + o, p.w.sv.gv2 + o,
+                                   p.w.sv.xh2 + o};
+            float4 q[6][2];
+#pragma unroll
+            for (int v = 0; v < 6; ++v) {
+                q[v][0] = *reinterpret_cast<const float4 *>(src[v]);
+                q[v][1] = *reinterpret_cast<const float4 *>(src[v] + 4);
+            }
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+                const int o2 = 3 * hh;
+                const float dzv[8] = {q[o2][0].x, q[o2][0].y, q[o2][0].z, q[o2][0].w,
+                                      q[o2][1].x, q[o2][1].y, q[o2][1].z, q[o2][1].w};
+                const float gvv[8] = {q[o2 + 1][0].x, q[o2 + 1][0].y, q[o2 + 1][0].z, q[o2 + 1][0].w,
+                                      q[o2 + 1][1].x, q[o2 + 1][1].y, q[o2 + 1][1].z, q[o2 + 1][1].w};
+                const float xhv[8] = {q[o2 + 2][0].x, q[o2 + 2][0].y, q[o2 + 2][0].z, q[o2 + 2][0].w,
+                                      q[o2 + 2][1].x, q[o2 + 2][1].y, q[o2 + 2][1].z, q[o2 + 2][1].w};
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    acc[o2][i] += dzv[i];
+                    acc[o2 + 1][i] = fmaf(gvv[i], xhv[i], acc[o2 + 1][i]);
+                    acc[o2 + 2][i] += gvv[i];
+                }
+            }
+        }
+        float (*part)[6][HID] = reinterpret_cast<float (*)[6][HID]>(smem);
+#pragma unroll
+        for (int v = 0; v < 6; ++v)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) part[rg][v][8 * g + i] = acc[v][i];
+        __syncthreads();
+        const float *dst[6] = {p.net.b1, p.net.ln1_w, p.net.ln1_b, p.net.b2, p.net.ln2_w, p.net.ln2_b};
+        for (int t = tid; t < 6 * HID; t += 256) {
+            const int v = t / HID, j = t % HID;
+            float sum = 0.0f;
+            for (int qq = 0; qq < GRG; ++qq) sum += part[qq][v][j];
+            const int64_t off = (dst[v] + k * HID + j) - p.p0;
+            const float pi = adam_el(p, sc, off, sum);
+            if (soft) soft_el(p.t0, off, pi, p.tau);
+        }
+        return;
+    }
+    if (type == 4) {  // W3 = h2^T g3, b3, the loss
+        const int k = b, out = p.out;
+        const int64_t base = (int64_t)k * B * HID;
+        float acc[8][NA];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int a = 0; a < NA; ++a) acc[i][a] = 0.0f;
+        float bacc[NA], lacc = 0.0f;
+#pragma unroll
+        for (int a = 0; a < NA; ++a) bacc[a] = 0.0f;
+#pragma unroll 4
+        for (int r = rg; r < B; r += GRG) {
+            const float *hs = p.w.sv.h2 + base + (int64_t)r * HID + 8 * g;
+            const float4 h0 = *reinterpret_cast<const float4 *>(hs), h1 = *reinterpret_cast<const float4 *>(hs + 4);
+            const float hv[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+            const float *gs = p.w.sv.g3 + ((int64_t)k * B + r) * out;
+            float gv[NA];
+#pragma unroll
+            for (int a = 0; a < NA; ++a) gv[a] = a < out ? gs[a] : 0.0f;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int a = 0; a < NA; ++a) acc[i][a] = fmaf(hv[i], gv[a], acc[i][a]);
+#pragma unroll
+            for (int a = 0; a < NA; ++a) bacc[a] += gv[a];
+            lacc += p.w.sv.aux[(int64_t)k * B + r];
+        }
+        float (*part)[HID][NA] = reinterpret_cast<float (*)[HID][NA]>(smem);
+        float (*pb)[NA + 1] = reinterpret_cast<float (*)[NA + 1]>(smem + GRG * HID * NA);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int a = 0; a < NA; ++a) part[rg][8 * g + i][a] = acc[i][a];
+        if (g == 0) {
+#pragma unroll
+            for (int a = 0; a < NA; ++a) pb[rg][a] = bacc[a];
+            pb[rg][NA] = lacc;
+        }
+        __syncthreads();
+        for (int t = tid; t < HID * out; t += 256) {
+            const int j = t / out, a = t % out;
+            float sum = 0.0f;
+            for (int qq = 0; qq < GRG; ++qq) sum += part[qq][j][a];
+            const int64_t off = (p.net.w3 + ((int64_t)k * HID + j) * out + a) - p.p0;
+            const float pi = adam_el(p, sc, off, sum);
+            if (soft) soft_el(p.t0, off, pi, p.tau);
+        }
+        if (tid < out) {
+            float sum = 0.0f;
+            for (int qq = 0; qq < GRG; ++qq) sum += pb[qq][tid];
+            const int64_t off = (p.net.b3 + k * out + tid) - p.p0;
+            const float pi = adam_el(p, sc, off, sum);
+            if (soft) soft_el(p.t0, off, pi, p.tau);
+        } else if (tid == 64) {
+            float sum = 0.0f;
+            for (int qq = 0; qq < GRG; ++qq) sum += pb[qq][NA];
+            p.loss[k] = p.phase == 0 ? sum / (float)B : -(sum / (float)B);
+        }
+        return;
+    }
+    // type 6: the critic target's soft update outside its W1 state rows (grid-stride)
+    const int in_c = K * HW + NA * K;
+    const int64_t w1off = p.cnet.w1 - p.cp0;
+    for (int64_t i = (int64_t)b * 256 + tid; i < p.cn; i += (int64_t)p.nrest * 256) {
+        const int64_t rel = i - w1off;
+        if (rel >= 0 && rel < (int64_t)K * in_c * HID && (rel / HID) % in_c < (int64_t)K * HW) continue;
+        p.ct0[i] = p.tau * p.cp0[i] + (1.0f - p.tau) * p.ct0[i];
+    }
+}
+
+// the c1 partials of one network from its current W1 (the update's own launches refresh them;
+// this primes them, e.g. after a load): blocks (network, agent, obs, 64-cell group)
+struct DPrime {
+    gw_mlp_actors net[4];  // actor, actor target, critic, critic target
+    DWs w;
+    const float *base;
+    int K, HW, NG;
+    int start[5];
+};
+__global__ void __launch_bounds__(256) dprime(DPrime p) {
+    __shared__ float s_base[CG], s_pp[2][HID];
+    int b = blockIdx.x, net = 0;
+    while (net < 3 && b >= p.start[net + 1]) ++net;
+    b -= p.start[net];
+    const int K = p.K, HW = p.HW, NG = p.NG, tid = threadIdx.x;
+    const bool critic = net >= 2;
+    const int nob = critic ? K : 1;
+    const int k = b / (nob * NG), ob = (b / NG) % nob, grp = b % NG;
+    const int c0 = grp * CG, ncell = min(CG, HW - c0), j = tid & (HID - 1), h = tid >> 7;
+    const int in_dim = critic ? K * HW + NA * K : HW;
+    if (tid < ncell) s_base[tid] = p.base[c0 + tid];
+    __syncthreads();
+    const float *wk = p.net[net].w1 + ((int64_t)k * in_dim + (int64_t)ob * HW + c0) * HID + j;
+    float pp = 0.0f;
+    for (int cc = h; cc < ncell; cc += 2) pp = fmaf(s_base[cc], wk[(int64_t)cc * HID], pp);
+    s_pp[h][j] = pp;
+    __syncthreads();
+    if (tid < HID) {
+        const int64_t gi = critic ? ((int64_t)k * K * NG + ob * NG + grp) : ((int64_t)k * NG + grp);
+        p.w.cpart[net][gi * HID + tid] = s_pp[0][tid] + s_pp[1][tid];
+    }
+}
+
 // ---- workspace ---------------------------------------------------------------------------------
 struct Ws {
     float *part_a, *part_ct, *part_c;
@@ -1019,6 +2071,190 @@ gw_status gw_maddpg_actor_grads(const gw_mlp_actors *actor, const gw_mlp_actors 
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(GW_ERR_HIP, who + ": " + hipGetErrorString(e));
     return GW_OK;
+}
+
+}  // extern "C"
+
+// ---- the descriptor learner's entry points ------------------------------------------------------
+namespace {
+
+gw_status dnet_ok(const gw_mlp_actors *n, int K, int in_dim, int out, const gw_adam_buf *opt, const char *who) {
+    if (!n) return fail(GW_ERR_ARG, std::string(who) + ": null network");
+    gw_status st = check_net(*n, K, in_dim, out, who);
+    if (st != GW_OK || !opt) return st;
+    const float *ps[10] = {n->w1, n->b1, n->ln1_w, n->ln1_b, n->w2, n->b2, n->ln2_w, n->ln2_b, n->w3, n->b3};
+    for (const float *q : ps)
+        if (q < opt->param || q >= opt->param + opt->n)
+            return fail(GW_ERR_ARG, std::string(who) + ": a parameter outside the optimizer's flat buffer");
+    if (!opt->grad || !opt->exp_avg || !opt->exp_avg_sq || !opt->step)
+        return fail(GW_ERR_ARG, std::string(who) + ": null optimizer buffer");
+    return GW_OK;
+}
+
+gw_status dsrc_ok(const gw_obs_source *src, int B, const float *ws, const char *who) {
+    if (!src || !src->base || !ws) return fail(GW_ERR_ARG, std::string(who) + ": null argument");
+    if (src->K < 1 || src->K > MAXK || src->N < src->K || src->N > MAXK)
+        return fail(GW_ERR_ARG, std::string(who) + ": K / N out of range");
+    if ((int64_t)src->H * src->W < 1 || (int64_t)src->H * src->W > 32767)
+        return fail(GW_ERR_ARG, std::string(who) + ": grid size out of range");
+    if (B < RB || B % RB || B > DMAXB) return fail(GW_ERR_ARG, std::string(who) + ": B must be a multiple of 16 in [16, 256]");
+    if (reinterpret_cast<uintptr_t>(ws) & 15u) return fail(GW_ERR_ARG, std::string(who) + ": ws must be 16-byte aligned");
+    return GW_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t gw_maddpg_desc_workspace_floats(int32_t K, int32_t B, int32_t H, int32_t W) {
+    if (K < 1 || K > MAXK || B < RB || B % RB || H < 1 || W < 1) return -1;
+    return dws_floats(K, B, H * W);
+}
+
+gw_status gw_maddpg_desc_prime(const gw_obs_source *src, const gw_mlp_actors *actor, const gw_mlp_actors *actor_target,
+                               const gw_mlp_actors *critic, const gw_mlp_actors *critic_target, int32_t B, float *ws,
+                               void *stream) {
+    const char *who = "gw_maddpg_desc_prime";
+    gw_status st = dsrc_ok(src, B, ws, who);
+    if (st != GW_OK) return st;
+    const int K = src->K, HW = src->H * src->W, in_c = K * HW + NA * K;
+    if ((st = dnet_ok(actor, K, HW, NA, nullptr, who)) != GW_OK || (st = dnet_ok(actor_target, K, HW, NA, nullptr, who)) != GW_OK ||
+        (st = dnet_ok(critic, K, in_c, 1, nullptr, who)) != GW_OK || (st = dnet_ok(critic_target, K, in_c, 1, nullptr, who)) != GW_OK)
+        return st;
+    DPrime p{};
+    p.net[0] = *actor;
+    p.net[1] = *actor_target;
+    p.net[2] = *critic;
+    p.net[3] = *critic_target;
+    p.w = dws_layout(ws, K, B, HW);
+    p.base = src->base;
+    p.K = K;
+    p.HW = HW;
+    p.NG = d_ng(HW);
+    p.start[0] = 0;
+    p.start[1] = K * p.NG;
+    p.start[2] = 2 * K * p.NG;
+    p.start[3] = p.start[2] + K * K * p.NG;
+    p.start[4] = p.start[3] + K * K * p.NG;
+    hipLaunchKernelGGL(dprime, dim3(p.start[4]), dim3(256), 0, static_cast<hipStream_t>(stream), p);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? GW_OK : fail(GW_ERR_HIP, std::string(who) + ": " + hipGetErrorString(e));
+}
+
+gw_status gw_maddpg_desc_update(const gw_obs_source *src, const gw_desc_ring *ring, const gw_mlp_actors *actor,
+                                const gw_mlp_actors *actor_target, const gw_mlp_actors *critic,
+                                const gw_mlp_actors *critic_target, const gw_adam_buf *opt_actor,
+                                const gw_adam_buf *opt_critic, float *actor_target_flat, float *critic_target_flat,
+                                float gamma, float tau, int32_t B, uint64_t seed, float *ws, float *actor_loss,
+                                float *critic_loss, void *prof_env, void *stream) {
+    const char *who = "gw_maddpg_desc_update";
+    gw_status st = dsrc_ok(src, B, ws, who);
+    if (st != GW_OK) return st;
+    if (!ring || !ring->desc || !ring->probs || !ring->reward || !ring->term || !ring->done || !ring->t_dev ||
+        ring->S < 2 || !opt_actor || !opt_critic || !actor_target_flat || !critic_target_flat || !actor_loss ||
+        !critic_loss || src->E < 1)
+        return fail(GW_ERR_ARG, std::string(who) + ": null argument");
+    const int K = src->K, HW = src->H * src->W, in_c = K * HW + NA * K, NG = d_ng(HW);
+    if ((st = dnet_ok(actor, K, HW, NA, opt_actor, who)) != GW_OK || (st = dnet_ok(actor_target, K, HW, NA, nullptr, who)) != GW_OK ||
+        (st = dnet_ok(critic, K, in_c, 1, opt_critic, who)) != GW_OK ||
+        (st = dnet_ok(critic_target, K, in_c, 1, nullptr, who)) != GW_OK)
+        return st;
+    if (actor_target->w1 - actor_target_flat != actor->w1 - opt_actor->param ||
+        critic_target->w1 - critic_target_flat != critic->w1 - opt_critic->param)
+        return fail(GW_ERR_ARG, std::string(who) + ": target flat buffers must share the online layout");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    // the four launches are one GW_SPAN_LEARN span of prof_env's gw_profile (when it profiles)
+    gwprof::Span span(prof_env, GW_SPAN_LEARN);
+    DQ q{};
+    q.desc = ring->desc;
+    q.probs = ring->probs;
+    q.reward = ring->reward;
+    q.term = ring->term;
+    q.done = ring->done;
+    q.t_dev = ring->t_dev;
+    q.S = ring->S;
+    q.E = src->E;
+    q.base = src->base;
+    for (int k = 0; k < MAXK; ++k) q.apples[k] = src->apples[k];
+    q.N = src->N;
+    q.K = K;
+    q.HW = HW;
+    q.variant = src->variant;
+    DTail t{};
+    t.q = q;
+    t.w = dws_layout(ws, K, B, HW);
+    t.at = *actor_target;
+    t.ct = *critic_target;
+    t.c = *critic;
+    t.a = *actor;
+    t.seed = seed;
+    t.ctr = opt_critic->step;
+    t.count = opt_critic->step;
+    t.gamma = gamma;
+    t.K = K;
+    t.B = B;
+    t.NG = NG;
+    gwprof::launch(dcritic_tail, dim3(B / RB, K), dim3(DT), 0, s, t);
+    DGrad g{};
+    g.w = t.w;
+    g.base = src->base;
+    g.net = *critic;
+    g.p0 = opt_critic->param;
+    g.g0 = opt_critic->grad;
+    g.m0 = opt_critic->exp_avg;
+    g.v0 = opt_critic->exp_avg_sq;
+    g.lr = opt_critic->lr;
+    g.beta1 = opt_critic->beta1;
+    g.beta2 = opt_critic->beta2;
+    g.eps = opt_critic->eps;
+    g.tau = tau;
+    g.count = opt_critic->step;
+    g.loss = critic_loss;
+    g.phase = 0;
+    g.K = K;
+    g.B = B;
+    g.HW = HW;
+    g.NG = NG;
+    g.nobs = K;
+    g.in_dim = in_c;
+    g.out = 1;
+    {
+        const int n[7] = {K * K * NG, K, K * (HID / RB), K, K, 0, 0};
+        g.start[0] = 0;
+        for (int i = 0; i < 7; ++i) g.start[i + 1] = g.start[i] + n[i];
+    }
+    gwprof::launch(dgrads_adam, dim3(g.start[7]), dim3(256), 0, s, g);
+    t.count = opt_actor->step;
+    gwprof::launch(dactor_tail, dim3(B / RB, K), dim3(DT), 0, s, t);
+    g.net = *actor;
+    g.p0 = opt_actor->param;
+    g.g0 = opt_actor->grad;
+    g.m0 = opt_actor->exp_avg;
+    g.v0 = opt_actor->exp_avg_sq;
+    g.lr = opt_actor->lr;
+    g.beta1 = opt_actor->beta1;
+    g.beta2 = opt_actor->beta2;
+    g.eps = opt_actor->eps;
+    g.t0 = actor_target_flat;
+    g.cnet = *critic;
+    g.cp0 = opt_critic->param;
+    g.ct0 = critic_target_flat;
+    g.cn = opt_critic->n;
+    g.count = opt_actor->step;
+    g.loss = actor_loss;
+    g.phase = 1;
+    g.nobs = 1;
+    g.in_dim = HW;
+    g.out = NA;
+    g.nrest = 64;
+    {
+        const int n[7] = {K * NG, 0, K * (HID / RB), K, K, K * K * NG, g.nrest};
+        g.start[0] = 0;
+        for (int i = 0; i < 7; ++i) g.start[i + 1] = g.start[i] + n[i];
+    }
+    gwprof::launch(dgrads_adam, dim3(g.start[7]), dim3(256), 0, s, g);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? GW_OK : fail(GW_ERR_HIP, std::string(who) + ": " + hipGetErrorString(e));
 }
 
 }  // extern "C"

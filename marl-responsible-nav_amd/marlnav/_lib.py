@@ -179,7 +179,8 @@ EXPORTS = ["gw_create", "gw_reset", "gw_step", "gw_state_view", "gw_copy_state",
            "gw_maddpg_workspace_floats", "gw_maddpg_critic_grads", "gw_maddpg_actor_grads",
            "gw_pipeline_state_bytes", "gw_pipeline_save", "gw_pipeline_load",
            "gw_gather_pack_scratch", "gw_gather_pack", "gw_gather_unpack_plan_cap", "gw_gather_unpack",
-           "gw_adam_soft_step", "gw_obs_desc_copy", "gw_replay_gather_desc"]
+           "gw_adam_soft_step", "gw_obs_desc_copy", "gw_replay_gather_desc",
+           "gw_maddpg_desc_workspace_floats", "gw_maddpg_desc_prime", "gw_maddpg_desc_update"]
 
 
 class GwObsSource(C.Structure):
@@ -210,8 +211,27 @@ class GwMaddpgBatch(C.Structure):
                 ("ctr", C.c_void_p)]
 
 
+class GwAdamBuf(C.Structure):
+    _fields_ = [("param", C.c_void_p), ("grad", C.c_void_p), ("exp_avg", C.c_void_p), ("exp_avg_sq", C.c_void_p),
+                ("step", C.c_void_p), ("n", C.c_int64), ("lr", C.c_double), ("beta1", C.c_double),
+                ("beta2", C.c_double), ("eps", C.c_double)]
+
+
+class GwDescRing(C.Structure):
+    _fields_ = [("desc", C.c_void_p), ("probs", C.c_void_p), ("reward", C.c_void_p), ("term", C.c_void_p),
+                ("done", C.c_void_p), ("t_dev", C.c_void_p), ("S", C.c_int64)]
+
+
 def _declare(L):
     p = C.c_void_p
+    L.gw_maddpg_desc_workspace_floats.argtypes = [C.c_int32] * 4
+    L.gw_maddpg_desc_workspace_floats.restype = C.c_int64
+    L.gw_maddpg_desc_prime.argtypes = [C.POINTER(GwObsSource)] + [C.POINTER(GwMlpActors)] * 4 + [C.c_int32, p, p]
+    L.gw_maddpg_desc_prime.restype = C.c_int
+    L.gw_maddpg_desc_update.argtypes = [C.POINTER(GwObsSource), C.POINTER(GwDescRing)] + \
+        [C.POINTER(GwMlpActors)] * 4 + [C.POINTER(GwAdamBuf)] * 2 + [p, p, C.c_float, C.c_float, C.c_int32,
+                                                                     C.c_uint64, p, p, p, p, p]
+    L.gw_maddpg_desc_update.restype = C.c_int
     L.gw_maddpg_workspace_floats.argtypes = [C.c_int32, C.c_int32, C.c_int32]
     L.gw_maddpg_workspace_floats.restype = C.c_int64
     L.gw_maddpg_critic_grads.argtypes = [C.POINTER(GwMlpActors)] * 4 + [C.POINTER(GwMaddpgBatch), C.c_float, p, p, p, p]

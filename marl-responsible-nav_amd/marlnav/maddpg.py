@@ -229,6 +229,8 @@ class MADDPG:
                       and all(_fusable_net(n) for n in (self.actors.net, self.actor_targets.net, self.critics,
                                                        self.critic_targets)))
         self._fws = {}
+        self._desc = {}           # the descriptor learner's per-ring state (workspace, ABI structs)
+        self._desc_stale = True   # its c1 partial sums need gw_maddpg_desc_prime before the next update
         # the key of the fused update's in-kernel draws (replay sample rows, Gumbel uniforms):
         # Philox(key; row, the critic optimizer's step count, tag), one key per rank (each rank
         # samples its own batch); the step count makes every update's draws new
@@ -266,6 +268,7 @@ class MADDPG:
         self.actor_targets.mark_updated()
         for m in (self.critics, self.critic_targets):
             m.epoch += 1
+        self._desc_stale = True
 
     @torch.no_grad()
     def _allreduce_grads(self, which: str):
@@ -308,7 +311,94 @@ class MADDPG:
         self._allreduce_grads("critic")
         self._learn_actor(ctx, u_cur)
         self._allreduce_grads("actor")
+        self._desc_stale = True  # weights changed outside the descriptor learner
         return self._learn_finish(ctx)
+
+    # ---- the descriptor learner (csrc/maddpg_ops.hip gw_maddpg_desc_update) -------------------
+    def desc_capable(self, replay, generator=None) -> bool:
+        """Whether an update on ``replay`` can run as the descriptor learner: one rank, the fused
+        flat networks with in-kernel draws, a ReplayRing currently serving descriptor rows, a batch
+        of 16..256 rows in 16-row tiles (GW_DESC_LEARN=0: never)."""
+        import os
+        return (generator is None and self.device.type == "cuda" and self.world <= 1 and self._draws_in_kernel()
+                and getattr(replay, "use_desc", False) and 16 <= self.batch_size <= 256
+                and self.batch_size % 16 == 0 and self.K <= _lib.GW_MAX_AGENTS and replay.K == self.K
+                and tuple(replay.obs.shape[-2:]) == (self.H, self.W) and os.environ.get("GW_DESC_LEARN", "1") != "0")
+
+    def _desc_setup(self, replay) -> dict:
+        """The descriptor learner's buffers and ABI structs for ``replay`` (built once per ring)."""
+        d = self._desc.get(id(replay))
+        if d is not None and d["replay"] is replay:
+            return d
+        L = _lib.load()
+        B = self.batch_size
+        n = int(L.gw_maddpg_desc_workspace_floats(self.K, B, self.H, self.W))
+        if n < 0:
+            raise ValueError("gw_maddpg_desc_workspace_floats: bad shape")
+        ring = _lib.GwDescRing(replay.desc.data_ptr(), replay.probs.data_ptr(), replay.reward.data_ptr(),
+                               replay.term.data_ptr(), replay.done.data_ptr(), replay.t_dev.data_ptr(), replay.S)
+
+        def adam(opt: FlatAdam):
+            return _lib.GwAdamBuf(opt.flat.data_ptr(), opt.flat.grad.data_ptr(), opt.m.data_ptr(), opt.v.data_ptr(),
+                                  opt.count.data_ptr(), opt.flat.numel(), opt.lr, opt.betas[0], opt.betas[1], opt.eps)
+        d = dict(replay=replay, ws=torch.zeros(n, dtype=torch.float32, device=self.device), ring=ring,
+                 specs=(_mlp_spec(self.actors.net), _mlp_spec(self.actor_targets.net), _mlp_spec(self.critics),
+                        _mlp_spec(self.critic_targets)),
+                 adam=(adam(self.opt_actor), adam(self.opt_critic)),
+                 loss=(torch.zeros(self.K, dtype=torch.float32, device=self.device),
+                       torch.zeros(self.K, dtype=torch.float32, device=self.device)))
+        self._desc = {id(replay): d}
+        self._desc_stale = True
+        return d
+
+    def desc_prime(self, replay):
+        """Derive the descriptor learner's c1 partial sums from the current weights (enqueued)."""
+        import ctypes as C
+        d = self._desc_setup(replay)
+        a, at, c, ct = d["specs"]
+        _lib.check(_lib.load().gw_maddpg_desc_prime(C.byref(replay._src), C.byref(a), C.byref(at), C.byref(c),
+                                                     C.byref(ct), self.batch_size, d["ws"].data_ptr(),
+                                                     torch.cuda.current_stream(self.device).cuda_stream),
+                   "gw_maddpg_desc_prime")
+        self._desc_stale = False
+
+    def learn_desc(self, replay):
+        """One whole MADDPG update sampling the descriptor ring ``replay`` in four launches
+        (gw_maddpg_desc_update): the sample, both gradients with their Adam steps and both soft
+        target updates.  Returns (actor_loss [K], critic_loss [K]) device tensors."""
+        import ctypes as C
+        d = self._desc_setup(replay)
+        if self._desc_stale:
+            self.desc_prime(replay)
+        a, at, c, ct = d["specs"]
+        oa, oc = d["adam"]
+        la, lc = d["loss"]
+        _lib.check(_lib.load().gw_maddpg_desc_update(
+            C.byref(replay._src), C.byref(d["ring"]), C.byref(a), C.byref(at), C.byref(c), C.byref(ct), C.byref(oa),
+            C.byref(oc), self.actor_targets.net.flat_params().data_ptr(), self.critic_targets.flat_params().data_ptr(),
+            float(self.gamma), float(self.tau), self.batch_size, self._draw_key, d["ws"].data_ptr(), la.data_ptr(),
+            lc.data_ptr(), getattr(replay, "env_handle", None), torch.cuda.current_stream(self.device).cuda_stream),
+            "gw_maddpg_desc_update")
+        for net in (self.actors.net, self.critics, self.actor_targets.net, self.critic_targets):
+            net.epoch += 1
+        return la, lc
+
+    def desc_records(self, replay) -> dict:
+        """The last descriptor update's rows as the workspace holds them (tests): ``idx`` [B, 2]
+        (transition slot, env), the Gumbel uniforms ``u_next`` / ``u_cur`` [K, B, 9], the target
+        actions ``a_next`` [B, 9K] (synchronises)."""
+        d = self._desc_setup(replay)
+        ws, K, B = d["ws"], self.K, self.batch_size
+        r4 = lambda n: (n + 3) // 4 * 4  # noqa: E731  (csrc dws_layout's 16-byte rounding)
+        npm = _lib.GW_MAX_AGENTS + 1     # patch slots per (row, agent obs)
+        o = 0
+        idx = ws[o:o + 2 * B].view(torch.int32).reshape(B, 2)
+        o += r4(2 * B) + 2 * r4(2 * K * B * npm) + r4(2 * K * B)
+        o += r4(B * 9 * K)  # act
+        tact = ws[o:o + B * 9 * K].reshape(B, 9 * K)
+        o += r4(B * 9 * K)
+        u = ws[o:o + 2 * K * B * 9].reshape(2, K, B, 9)
+        return {"idx": idx.clone(), "u_next": u[0].clone(), "u_cur": u[1].clone(), "a_next": tact.clone()}
 
     def _fused_batch(self, x, x_next, rewards, dones, u):
         """u None: the kernels draw the Gumbel uniforms (Philox keyed by _draw_key and the critic
@@ -503,7 +593,10 @@ class MADDPG:
 
     # ---------------------------------------------------------------------------------------
     def learn_from(self, replay, generator: torch.Generator | None = None):
-        """Sample ``batch_size`` transitions from a ReplayRing and learn (eager)."""
+        """Sample ``batch_size`` transitions from a ReplayRing and learn (eager): the descriptor
+        learner where it applies (desc_capable), else the sample launch + ``learn``."""
+        if self.desc_capable(replay, generator):
+            return self.learn_desc(replay)
         return self.learn(*self._sample(replay, generator))
 
     def _sample(self, replay, generator=None):
@@ -545,6 +638,9 @@ class MADDPG:
         # which rows the captured sample reads (the descriptor ring or the dense obs slots): the
         # caller's fence must match it, and a change of the ring's mode invalidates the capture
         self._capture_desc = bool(getattr(replay, "use_desc", False)) if batch is None else None
+        desc = batch is None and self.desc_capable(replay)
+        if desc:
+            return self._capture_desc_learner(replay, warmup, actor_env, launches)
         if batch is not None:
             fixed = tuple(batch) + (None,) * (8 - len(batch))
 
@@ -610,6 +706,42 @@ class MADDPG:
         self._graph = g3
         return g3
 
+    def _capture_desc_learner(self, replay, warmup: int, actor_env, launches: bool):
+        """capture() for the descriptor learner: its update is ONE C-ABI call (four launches),
+        recorded (launches) or captured into a HIP graph, after the same warm-up updates."""
+        for _ in range(max(0, warmup - 1) if launches else warmup):
+            self.learn_desc(replay)
+        if self._desc_stale:
+            self.desc_prime(replay)  # outside the recording: replays then never prime
+        self._prep_env = self._prep_ws = None
+        self._launches = None
+        if launches:
+            rec = _lib.LaunchRecorder(torch.cuda.current_stream(self.device).cuda_stream)
+            with rec:
+                self._graph_out = self.learn_desc(replay)
+                if actor_env is not None:
+                    self._prep_ws = self.actors.prepare_after_update(actor_env)
+                    self._prep_env = actor_env if self._prep_ws is not None else None
+            for m in (self.actors, self.actor_targets):
+                m.mark_updated()
+            if self._prep_env is not None:
+                self.actors.mark_prepared(self._prep_env)
+            self._launch_keep = None
+            self._graph = self._launches = rec
+            return rec
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g):
+                self._graph_out = self.learn_desc(replay)
+                if actor_env is not None:
+                    self._prep_ws = self.actors.prepare_after_update(actor_env)
+                    self._prep_env = actor_env if self._prep_ws is not None else None
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        self._graph = g
+        return g
+
     def invalidate_capture(self):
         """Drop the captured update (graph, segments or recorded launches): the next learn through
         a trainer captures again, e.g. after the replay ring switched between descriptor and dense
@@ -624,6 +756,10 @@ class MADDPG:
         return self._graph is not None and getattr(self, "_capture_desc", None) == bool(getattr(replay, "use_desc", False))
 
     def replay_learn(self):
+        desc = getattr(self, "_capture_desc", None) and self._desc
+        if desc and self._desc_stale:
+            # weights changed since the capture (a load, a dense update): re-derive the partial sums
+            self.desc_prime(next(iter(self._desc.values()))["replay"])
         if self._graphs is not None:
             g1, g2, g3 = self._graphs
             g1.replay()
@@ -639,6 +775,8 @@ class MADDPG:
             m.mark_updated()
         if self._graphs is None and getattr(self, "_prep_env", None) is not None:
             self.actors.mark_prepared(self._prep_env)  # the graph ended with the workspace derivation
+        if not desc:
+            self._desc_stale = True
         return self._graph_out
 
     # ---------------------------------------------------------------------------------------
@@ -656,6 +794,7 @@ class MADDPG:
                         ("critic_target", self.critic_targets)):
             sub = {k[len(name) + 1:]: v for k, v in sd.items() if k.startswith(name + ".")}
             m.load_state_dict(sub)
+        self._desc_stale = True
 
     def optim_state_dict(self) -> dict:
         """The two optimizers' state as flat tensors (agilerl's save_checkpoint keeps the optimizer

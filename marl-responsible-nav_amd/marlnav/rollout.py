@@ -61,6 +61,7 @@ class ReplayRing:
             self.desc = torch.zeros((self.S, E, 12), dtype=torch.int32, device=dev)
             self._src = _lib.GwObsSource()
             _lib.check(_lib.load().gw_obs_view(env.handle, C.byref(self._src)), "gw_obs_view")
+            self.env_handle = env.handle  # the env whose gw_profile spans the descriptor learner joins
 
     def __len__(self):
         return min(self.t, self.S - 1) * self.E
