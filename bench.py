@@ -90,21 +90,30 @@ def algorithmic_bytes(N: int, K: int, HW: int, obs_bytes: int = 4):
 SPAN_KINDS = {0: "step_kernel", 1: "obs_kernel", 2: "fear_kernel", 3: "act_kernel", 4: "cnn_l1_kernel",
               5: "cnn_list_kernels", 6: "cnn_rare_kernel", 7: "window_kernel", 8: "learn_update"}
 F32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: dense f32 MFMA (v_mfma_f32_16x16x4_f32), no xf32 on gfx950
+# VALU issue peak (MI355X_MICROARCH.md "Execution model"): each of 256 CUs x 4 SIMD-32 issues one
+# wave64 vector instruction per 2 cycles at the 2.4 GHz max clock = 1.2288e12 wave-instructions/s
+VALU_PEAK_GIPS = 256 * 4 * 2.4e9 / 2 / 1e9
 HID, N_ACT = 128, 9        # the fused actors' hidden width and actions (configs/mlp.yaml, configs/cnn.yaml)
 
 
-def kernel_work(kind: int, N: int, K: int, HW: int, E: int, obs_bytes: int = 4, patch: int = 0):
+def kernel_work(kind: int, N: int, K: int, HW: int, E: int, obs_bytes: int = 4, patch: int = 0, valu=None):
     """(bound, algorithmic work per step of one GW_SPAN kind, unit) for the roofline:
     HBM bytes for the env / writer kernels, f32 MFMA flops for the fused
     actors' MLP kernel (DESIGN.md §5.4: layers 2-3, 2 * (128 * 128 + 128 * 9) per (env, agent);
     its layer 1 is a gather of table rows, not a GEMM).  None where the work is data-dependent
     (the CNN recompute: a few positions per step)."""
     step_b, obs_b = algorithmic_bytes(N, K, HW, obs_bytes)
+    valu = valu or {}
+    if kind in (0, 2) and valu.get(kind):
+        # the world update and the FeAR counterfactuals are integer-VALU / latency chains (SURVEY
+        # §8d): their work is the vector instructions per step, from the committed rocprofv3
+        # SQ_INSTS_VALU pass of the same config (profiles/latest.json), against the VALU issue peak
+        return "valu", valu[kind], "inst"
     if kind == 0:
         return "hbm", step_b * E, "B"
     if kind == 1:
         return "hbm", obs_b * E, "B"
-    if kind == 2:  # FearRec 16 read, score / fear_score read + written, fear / shaped, ep_return / ep_fear
+    if kind == 2:  # FeAR: integer-VALU bound; without a VALU pass, its state / output bytes
         return "hbm", (16 + 32 + 16 * K + 16) * E, "B"
     if kind == 3:
         return "mfma", 2 * E * K * (HID * HID + HID * N_ACT), "flop"
@@ -112,6 +121,11 @@ def kernel_work(kind: int, N: int, K: int, HW: int, E: int, obs_bytes: int = 4, 
         return "hbm", (48 + 4 * K) * E, "B"
     if kind == 7:  # the windows written (f32) + the 48-byte descriptors read
         return "hbm", (4 * K * patch * patch + 48) * E, "B"
+    if kind == 8:  # one descriptor-learner update: its 128 x 128 layers on f32 MFMA --
+        # critic tail: K target actors + target critic + critic forward + critic backward, actor
+        # tail: actor / critic forward, critic / actor backward, and the two W2 gradients, per agent
+        # and row: (4 + 4 + 2) K B (2 * 128 * 128) flops with B = 128 (layer 1 is a table gather)
+        return "mfma", 10 * K * 128 * 2 * HID * HID, "flop"
     return "mfma", None, "flop"
 
 
@@ -543,9 +557,13 @@ def main():
     gc.enable()
     gpu_ms = ev0.elapsed_time(ev1)
     spans = None
+    sims = None
     if n_prof:
         # the kernel spans: n_prof eager steps right after the timed region (same env, same
         # kernels and pipeline, untimed; HIP timing events cannot be recorded inside a graph)
+        sim_ctr = torch.zeros(1, dtype=torch.int64, device=env.device) if cfg["fear"] else None
+        if sim_ctr is not None:
+            env.count_sims(sim_ctr)  # the FeAR kernels' counterfactual world updates (gw_count_sims)
         env.profile(True)
         for i in range(n_prof):
             one_step(args.steps + i)
@@ -554,6 +572,9 @@ def main():
         env.obs_fence()  # the last profiled step's writer
         torch.cuda.synchronize()
         env.profile(False)
+        if sim_ctr is not None:
+            env.count_sims(None)
+            sims = int(sim_ctr.item()) / n_prof  # de-duplicated sims per step (this rank)
         spans = env.profile_spans()
     (ms_step, ms_obs, ms_fear), nprof = env.profile_read()
 
@@ -584,6 +605,19 @@ def main():
         fused = env.fused
         merged = env.kernel_path == "merged" and bool(obs_mode)
         obs_bytes = 2 if args.obs_dtype == "bf16" else 4
+        # the VALU instructions per step of the integer-VALU kernels (world update, FeAR) from the
+        # committed rocprofv3 SQ_INSTS_VALU pass of this config (tools/gpu_profile.sh)
+        valu = {}
+        try:
+            with open(os.path.join(REPO, "profiles", "latest.json")) as f:
+                pk = json.load(f).get("configs", {}).get(args.config, {}).get("kernels", {})
+            if not args.envs and args.fear < 0 and args.obs_dtype == "f32":
+                for kd, nm in ((0, "step_kernel"), (2, "fear_kernel")):
+                    v = pk.get(nm, {}).get("valu_insts_per_step")
+                    if v:
+                        valu[kd] = v
+        except (OSError, ValueError, AttributeError):
+            pass
         # every kernel kind's busy time per profiled step (the union of its launches' intervals /
         # steps: overlapping launches of one kind count once) and its roofline
         per_kind = {}
@@ -591,18 +625,28 @@ def main():
             tot, n = busy[k]
             if not n:
                 continue
-            bound, work, unit = kernel_work(k, N, K, HW, E, obs_bytes, cfg.get("patch", 0))
+            bound, work, unit = kernel_work(k, N, K, HW, E, obs_bytes, cfg.get("patch", 0), valu)
             ms = tot / max(nprof, 1)
-            peak = F32_MFMA_PEAK_TFS * 1e3 if bound == "mfma" else HBM_PEAK_GBS
-            rate = work / (ms * 1e-3) / 1e9 if (work and ms > 0) else None  # GB/s or GFLOP/s
+            if k == 8:  # the learner's span is one update; a step may run several
+                work = work * (n / max(nprof, 1)) if work else work
+            peak = {"mfma": F32_MFMA_PEAK_TFS * 1e3, "valu": VALU_PEAK_GIPS}.get(bound, HBM_PEAK_GBS)
+            rate = work / (ms * 1e-3) / 1e9 if (work and ms > 0) else None  # GB/s, GFLOP/s or G inst/s
             per_kind[name] = {"busy_ms_per_step": ms, "launches_per_step": n / max(nprof, 1), "bound": bound,
                               "work_per_step": work, "work_unit": unit,
                               "achieved": rate / 1e3 if (rate and bound == "mfma") else rate,
+                              "achieved_unit": {"mfma": "TFLOP/s", "valu": "G inst/s"}.get(bound, "GB/s"),
                               "frac": rate / peak if rate else None}
         if fused:  # one launch per step moves every byte of the step
             dom, bytes_per_launch, span, dur = "step_fused", (step_b + obs_b) * E, avg_step_ms, busy_step_ms
         elif merged:  # step_obs: step t + the obs writer of step t-1 in one launch (its spans: kind 1)
             dom, bytes_per_launch, span, dur = "step_obs", (step_b + obs_b) * E, avg_obs_ms, busy_obs_ms
+        elif "learn_update" in per_kind:  # with updates the learner chain is the step's critical path
+            # (the obs writer overlaps it on its own stream): the line names the update
+            dom = "learn_update"
+            _, bytes_per_launch, _ = kernel_work(8, N, K, HW, E, obs_bytes, cfg.get("patch", 0))
+            launches = busy[8][1] / max(nprof, 1)
+            dur = per_kind[dom]["busy_ms_per_step"] / max(launches, 1e-9)
+            span = dur
         else:  # the kernel kind with the largest busy time per step
             dom = max(per_kind, key=lambda n: per_kind[n]["busy_ms_per_step"]) if per_kind else "obs_kernel"
             kd = next(k for k, n in SPAN_KINDS.items() if n == dom)
@@ -700,6 +744,16 @@ def main():
                          "mean_len": stats[6] / max(stats[1], 1.0)},
             # completed-episode returns all-gathered every step (warmup + timed steps, all ranks)
             "return_gather": gathered,
+            # FeAR's integer work: the counterfactual world updates the FeAR kernels ran
+            # per step (gw_count_sims over the profiled steps, after the exact de-duplication of
+            # DESIGN §5) and the reference's nominal K (N - 1) 18 per env-step, per second at the
+            # timed step time, all ranks
+            "fear_sims": None if sims is None else {
+                "per_step": sims, "per_s": world * sims / (t_max / args.steps),
+                "ref_equiv_per_step": E * K * (N - 1) * 18,
+                "ref_equiv_per_s": world * E * K * (N - 1) * 18 / (t_max / args.steps),
+                "dedup_factor": E * K * (N - 1) * 18 / sims if sims else None,
+                "unit": "world updates (custom/Responsibility.py:16-54 UpdateGWorld counterfactuals)"},
         }
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)

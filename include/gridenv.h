@@ -229,6 +229,13 @@ gw_status gw_obs_view(void *env, gw_obs_source *out);
  * include/rollout_ops.h). */
 gw_status gw_obs_desc_copy(void *env, uint32_t *dst, void *stream);
 
+/* Count the FeAR counterfactual world updates (custom/Responsibility.py:16-54's sims, after the
+ * exact de-duplication of DESIGN §5: one base sim per (actor, variant) and the 8 other actions of
+ * each close affected agent per variant) the env's FeAR kernels run from now on: every block adds
+ * its task count to *counter (device uint64, one atomic per block per step).  counter NULL: stop
+ * counting (the default).  bench.py reports sims/s from it beside the VALU roofline. */
+gw_status gw_count_sims(void *env, uint64_t *counter);
+
 /* Egocentric local patches of the env's last observation (an opt-in input format; the
  * reference observes the whole grid, ma_customenv.py:303-322): for every env and RL agent k the
  * P x P window of that agent's obs centred on its own cell (rows / cols -P/2 .. P-1-P/2), cells

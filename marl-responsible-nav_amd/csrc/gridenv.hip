@@ -99,6 +99,7 @@ struct Params {
     int64_t stats_row0;       // first gw_step_out.stats row this launch writes
     int variant;              // 0 CustomMAEnv, 1 single-agent CustomEnv (custom/customenv.py)
     int apples[MAXN];
+    unsigned long long *sims;  // gw_count_sims: FeAR counterfactual world updates run (null: not counted)
 };
 
 // ---------------------------------------------------------------------------------------
@@ -1688,6 +1689,7 @@ __device__ __forceinline__ void step_v2_block(const Params &p, int64_t bid, V2Sh
         __syncthreads();
         // ---- B ----
         const int nb_end = BE + sh.nbase, ntask = nb_end + 16 * sh.ngroup;
+        if (tid == 0 && p.sims && ntask > BE) atomicAdd(p.sims, (unsigned long long)(ntask - BE));
         for (int ti = tid; ti < ntask; ti += T) {
             if (ti < BE && ti >= nenv) continue;
             const uint32_t tk = fear_task_at(sh, ti, nb_end);
@@ -1958,6 +1960,7 @@ __global__ void __launch_bounds__(128) fear_v2(Params p) {
     __syncthreads();
     // ---- B ----
     const int nb_end = sh.nbase, ntask = nb_end + 16 * sh.ngroup;
+    if (tid == 0 && p.sims && ntask) atomicAdd(p.sims, (unsigned long long)ntask);
     for (int ti = tid; ti < ntask; ti += T) fear_task<N, KMAX>(p, sh, fear_task_at(sh, ti, nb_end), okv);
     __syncthreads();
     // ---- C ----
@@ -2207,6 +2210,7 @@ struct Env {
     int32_t *pos = nullptr, *t = nullptr, *prev = nullptr;
     uint32_t *flags = nullptr, *episode = nullptr, *desc = nullptr;
     uint4 *fwork = nullptr;  // deferred-FeAR records (mode 3 with FeAR on)
+    unsigned long long *sims = nullptr;  // gw_count_sims counter (device), or null
     // gw_obs_patch's per-P tables of the map part of every window centre (patch_ops.hip MODE 4)
     std::vector<std::pair<int, float *>> ptbls;
     double *score = nullptr, *fscore = nullptr;
@@ -2469,6 +2473,7 @@ gw::Params make_params(const Env *env) {
     p.e_begin = 0;
     p.e_end = env->E;
     p.fwork = env->fwork;
+    p.sims = env->sims;
     p.stats_row0 = 0;
     p.variant = env->variant;
     p.tb.roadbits = env->roadbits;
@@ -3417,6 +3422,12 @@ gw_status gw_obs_patch(void *handle, int32_t P, float *patch, float *final_patch
     }
     gwprof::Span span(env, GW_SPAN_WINDOW);
     HIP_TRY(gw::launch_windows(a, s));
+    return GW_OK;
+}
+
+gw_status gw_count_sims(void *handle, uint64_t *counter) {
+    if (!handle) return fail(GW_ERR_ARG, "gw_count_sims: null env");
+    static_cast<Env *>(handle)->sims = reinterpret_cast<unsigned long long *>(counter);
     return GW_OK;
 }
 

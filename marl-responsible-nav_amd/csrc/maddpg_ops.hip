@@ -948,8 +948,8 @@ __device__ __forceinline__ int d_patches(const DQ &q, const uint32_t (&d)[NDW], 
 }
 
 // row b of the sample: transition slot tr and env e (gw_replay_gather_desc's in-kernel draws)
-__device__ __forceinline__ void d_draw(const DQ &q, uint64_t seed, uint32_t c, int b, int64_t &tr, int64_t &e) {
-    const int64_t t = q.t_dev[0];
+__device__ __forceinline__ void d_draw(const DQ &q, int64_t t, uint64_t seed, uint32_t c, int b, int64_t &tr,
+                                       int64_t &e) {
     const uint4 r = gwrng::philox((uint32_t)b, c, gwrng::TAG_SAMPLE, 0u, (uint32_t)seed, (uint32_t)(seed >> 32));
     const float ub = gwrng::unit(r.x);
     e = (int64_t)(((uint64_t)r.y * (uint64_t)q.E) >> 32);
@@ -1082,6 +1082,32 @@ __device__ __forceinline__ void d_fwd_rest(float z[8], const Mlp &m, int nout, i
     }
 }
 
+// a network's small parameters staged in LDS (one slot per network of a tail block): ln1 w / b,
+// b2, ln2 w / b, W3, b3 -- loaded once at the block's start, under the prologue's descriptor round
+// trips, instead of a dependent global round trip at every LayerNorm and head
+constexpr int PSLOT = 5 * HID + HID * NA + NA + 3;  // floats per slot (rounded to 16 bytes)
+__device__ __forceinline__ int stage_size(int out) { return 5 * HID + HID * out + out; }
+__device__ __forceinline__ float stage_src(const Mlp &m, int out, int o) {
+    if (o < 5 * HID) {
+        const int v = o / HID, j = o % HID;
+        const float *src = v == 0 ? m.lw1 : v == 1 ? m.lb1 : v == 2 ? m.b2 : v == 3 ? m.lw2 : m.lb2;
+        return src[j];
+    }
+    o -= 5 * HID;
+    return o < HID * out ? m.w3[o] : m.b3[o - HID * out];
+}
+// m with its small parameters read from slot sp (W1 and W2 stay in global memory)
+__device__ __forceinline__ Mlp staged(Mlp m, const float *sp, int out) {
+    m.lw1 = sp;
+    m.lb1 = sp + HID;
+    m.b2 = sp + 2 * HID;
+    m.lw2 = sp + 3 * HID;
+    m.lb2 = sp + 4 * HID;
+    m.w3 = sp + 5 * HID;
+    m.b3 = sp + 5 * HID + HID * out;
+    return m;
+}
+
 struct DTail {
     DQ q;
     DWs w;
@@ -1102,83 +1128,115 @@ __global__ void __launch_bounds__(DT) dcritic_tail(DTail p) {
     __shared__ float s_act[RB][NA * MAXK], s_tact[RB][NA * MAXK];
     __shared__ float s_c1[MAXK + 2][HID];
     __shared__ float s_y[RB], s_rw[RB], s_t1[RB];
+    __shared__ __attribute__((aligned(16))) float s_par[MAXK + 2][PSLOT];  // target actors, critic target, critic
     const int k = blockIdx.y, tid = threadIdx.x, grp = tid >> 8, lt = tid & 255, rl = lt >> 4, g = lt & 15;
     const int K = p.K, B = p.B, HW = p.q.HW, r0 = blockIdx.x * RB, r = r0 + rl;
     const int64_t E = p.q.E;
-    const uint32_t c = (uint32_t)p.ctr[0];
+    const int in_c = K * HW + NA * K;
     const bool rec = k == 0;  // the k = 0 blocks record the rows for the later launches
-    // c1 of the networks this block runs: the K target actors, critic target k, critic k
-    for (int o = tid; o < (K + 2) * HID; o += DT) {
-        const int net = o / HID, j = o % HID;
-        float v;
-        if (net < K)
-            v = p.at.b1[net * HID + j] + d_sum_parts(p.w.cpart[1] + (int64_t)net * p.NG * HID + j, p.NG);
-        else if (net == K)
-            v = p.ct.b1[k * HID + j] + d_sum_parts(p.w.cpart[3] + (int64_t)k * K * p.NG * HID + j, K * p.NG);
-        else
-            v = p.c.b1[k * HID + j] + d_sum_parts(p.w.cpart[2] + (int64_t)k * K * p.NG * HID + j, K * p.NG);
-        s_c1[net][j] = v;
+    // prologue: every independent load first (the ring's step count, this thread's share of the
+    // small parameters), then the roles -- waves 0-3 the rows' descriptors, waves 4-7 the stored
+    // probabilities, rewards and c1 sums -- whose round trips overlap; the parameters reach LDS last
+    const int64_t t_now = p.q.t_dev[0];
+    const uint32_t c = (uint32_t)p.ctr[0];
+    const int na_ = stage_size(NA), nc_ = stage_size(1), tot = K * na_ + 2 * nc_;
+    auto par_src = [&](int o) -> float {
+        if (o < K * na_) return stage_src(mlp_k(p.at, o / na_, HW, NA), NA, o % na_);
+        const int q = o - K * na_;
+        return stage_src(mlp_k(q < nc_ ? p.ct : p.c, k, in_c, 1), 1, q % nc_);
+    };
+    auto par_dst = [&](int o) -> float * {
+        return o < K * na_ ? &s_par[o / na_][o % na_] : &s_par[K + (o - K * na_) / nc_][(o - K * na_) % nc_];
+    };
+    constexpr int NSV = 16;
+    float sv[NSV];
+#pragma unroll
+    for (int u = 0; u < NSV; ++u) {
+        const int o = tid + u * DT;
+        sv[u] = o < tot ? par_src(o) : 0.0f;
     }
-    // the rows' descriptors -> patched cells: one thread per (row, state | next state, agent obs)
-    if (tid < RB * 2 * K) {
-        const int rr = tid / (2 * K), which = (tid / K) & 1, kk = tid % K;
-        int64_t tr, e;
-        d_draw(p.q, p.seed, c, r0 + rr, tr, e);
-        const int64_t nx = (tr + 1) % p.q.S;
-        const bool dn = p.q.done[tr * E + e] != 0;
-        const uint4 *d4 = reinterpret_cast<const uint4 *>(p.q.desc + ((which == 0 ? tr : nx) * E + e) * NDW);
-        const uint4 a0 = d4[0], a1 = d4[1], a2 = d4[2];
-        const uint32_t d[NDW] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w};
-        const float apple_map = p.q.apples[kk] >= 0 ? p.q.base[p.q.apples[kk]] : 0.0f;
-        int oc[NPM];
-        float od[NPM];
-        const int m = d_patches(p.q, d, which == 0 ? 0 : (dn ? 1 : 0), kk, apple_map, oc, od);
-        s_np[which][rr][kk] = m;
-        const int64_t ro = ((int64_t)(which * K + kk) * B + r0 + rr);
-        for (int i = 0; i < m; ++i) {
-            s_pc[which][rr][kk][i] = (int16_t)oc[i];
-            s_pd[which][rr][kk][i] = od[i];
+    if (tid < 256) {
+        // the rows' descriptors -> patched cells: one thread per (row, state | next state, agent obs)
+        if (tid < RB * 2 * K) {
+            const int rr = tid / (2 * K), which = (tid / K) & 1, kk = tid % K;
+            int64_t tr, e;
+            d_draw(p.q, t_now, p.seed, c, r0 + rr, tr, e);
+            const int64_t nx = (tr + 1) % p.q.S;
+            const bool dn = p.q.done[tr * E + e] != 0;
+            const uint4 *d4 = reinterpret_cast<const uint4 *>(p.q.desc + ((which == 0 ? tr : nx) * E + e) * NDW);
+            const uint4 a0 = d4[0], a1 = d4[1], a2 = d4[2];
+            const uint32_t d[NDW] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w};
+            const float apple_map = p.q.apples[kk] >= 0 ? p.q.base[p.q.apples[kk]] : 0.0f;
+            int oc[NPM];
+            float od[NPM];
+            const int m = d_patches(p.q, d, which == 0 ? 0 : (dn ? 1 : 0), kk, apple_map, oc, od);
+            s_np[which][rr][kk] = m;
+            const int64_t ro = ((int64_t)(which * K + kk) * B + r0 + rr);
+            for (int i = 0; i < m; ++i) {
+                s_pc[which][rr][kk][i] = (int16_t)oc[i];
+                s_pd[which][rr][kk][i] = od[i];
+                if (rec) {
+                    p.w.pc[ro * NPM + i] = oc[i];
+                    p.w.pd[ro * NPM + i] = od[i];
+                }
+            }
             if (rec) {
-                p.w.pc[ro * NPM + i] = oc[i];
-                p.w.pd[ro * NPM + i] = od[i];
+                p.w.np[ro] = m;
+                if (which == 0 && kk == 0) {
+                    p.w.idx[2 * (r0 + rr)] = (int32_t)tr;
+                    p.w.idx[2 * (r0 + rr) + 1] = (int32_t)e;
+                }
             }
         }
-        if (rec) {
-            p.w.np[ro] = m;
-            if (which == 0 && kk == 0) {
-                p.w.idx[2 * (r0 + rr)] = (int32_t)tr;
-                p.w.idx[2 * (r0 + rr) + 1] = (int32_t)e;
-            }
+    } else {
+        const int t2 = tid - 256;
+        // c1 of the networks this block runs: the K target actors, critic target k, critic k
+        for (int o = t2; o < (K + 2) * HID; o += 256) {
+            const int net = o / HID, j = o % HID;
+            float v;
+            if (net < K)
+                v = p.at.b1[net * HID + j] + d_sum_parts(p.w.cpart[1] + (int64_t)net * p.NG * HID + j, p.NG);
+            else if (net == K)
+                v = p.ct.b1[k * HID + j] + d_sum_parts(p.w.cpart[3] + (int64_t)k * K * p.NG * HID + j, K * p.NG);
+            else
+                v = p.c.b1[k * HID + j] + d_sum_parts(p.w.cpart[2] + (int64_t)k * K * p.NG * HID + j, K * p.NG);
+            s_c1[net][j] = v;
+        }
+        // the stored action probabilities of every agent (the critic's action inputs)
+        for (int o = t2; o < RB * NA * K; o += 256) {
+            const int rr = o / (NA * K), a = o % (NA * K), kk = a / NA;
+            int64_t tr, e;
+            d_draw(p.q, t_now, p.seed, c, r0 + rr, tr, e);
+            const float v = p.q.probs[((tr * K + kk) * E + e) * NA + a % NA];
+            s_act[rr][a] = v;
+            if (rec) p.w.act[(int64_t)(r0 + rr) * NA * K + a] = v;
+        }
+        // agent k's reward and termination (the TD target)
+        if (t2 >= 256 - RB) {
+            const int rr = t2 - (256 - RB);
+            int64_t tr, e;
+            d_draw(p.q, t_now, p.seed, c, r0 + rr, tr, e);
+            const float rw = (float)p.q.reward[(tr * E + e) * K + k];
+            const float t1 = 1.0f - (float)p.q.term[(tr * E + e) * K + k];
+            s_rw[rr] = rw;
+            s_t1[rr] = t1;
+            p.w.rw[(int64_t)k * B + r0 + rr] = rw;
+            p.w.t1[(int64_t)k * B + r0 + rr] = t1;
         }
     }
-    // the stored action probabilities of every agent (the critic's action inputs)
-    for (int o = tid; o < RB * NA * K; o += DT) {
-        const int rr = o / (NA * K), a = o % (NA * K), kk = a / NA;
-        int64_t tr, e;
-        d_draw(p.q, p.seed, c, r0 + rr, tr, e);
-        const float v = p.q.probs[((tr * K + kk) * E + e) * NA + a % NA];
-        s_act[rr][a] = v;
-        if (rec) p.w.act[(int64_t)(r0 + rr) * NA * K + a] = v;
+#pragma unroll
+    for (int u = 0; u < NSV; ++u) {
+        const int o = tid + u * DT;
+        if (o < tot) *par_dst(o) = sv[u];
     }
-    // agent k's reward and termination (the TD target)
-    if (tid >= DT - RB) {
-        const int rr = tid - (DT - RB);
-        int64_t tr, e;
-        d_draw(p.q, p.seed, c, r0 + rr, tr, e);
-        const float rw = (float)p.q.reward[(tr * E + e) * K + k];
-        const float t1 = 1.0f - (float)p.q.term[(tr * E + e) * K + k];
-        s_rw[rr] = rw;
-        s_t1[rr] = t1;
-        p.w.rw[(int64_t)k * B + r0 + rr] = rw;
-        p.w.t1[(int64_t)k * B + r0 + rr] = t1;
-    }
+    for (int o = tid + NSV * DT; o < tot; o += DT) *par_dst(o) = par_src(o);
     if (blockIdx.x == 0 && k == 0 && tid == 0) p.w.snap[0] = p.count[0] + 1;
     __syncthreads();
     // the target actions a'_kk = GumbelSoftmax(actor_target_kk(s'_kk)), two agents at a time (a
     // group without an agent in the last round recomputes agent K - 1 and discards it)
     for (int rd = 0; rd < (K + 1) / 2; ++rd) {
         const int kk = 2 * rd + grp, kx = kk < K ? kk : K - 1;
-        const Mlp m = mlp_k(p.at, kx, HW, NA);
+        const Mlp m = staged(mlp_k(p.at, kx, HW, NA), s_par[kx], NA);
         float z[8], out[NA];
         RowFwd f;
 #pragma unroll
@@ -1204,12 +1262,11 @@ __global__ void __launch_bounds__(DT) dcritic_tail(DTail p) {
     }
     __syncthreads();
     // group 0: the target critic on (s', a'); group 1: the online critic on (s, a)
-    const int in_c = K * HW + NA * K;
     RowFwd f;
     float out[NA];
     {
         const bool tgt = grp == 0;
-        const Mlp m = mlp_k(tgt ? p.ct : p.c, k, in_c, 1);
+        const Mlp m = staged(mlp_k(tgt ? p.ct : p.c, k, in_c, 1), s_par[tgt ? K : K + 1], 1);
         const int which = tgt ? 1 : 0;
         float z[8];
 #pragma unroll
@@ -1222,7 +1279,7 @@ __global__ void __launch_bounds__(DT) dcritic_tail(DTail p) {
     // y = f32(r) + ((1 - d) * gamma) * q_next (gw_td_target's op order)
     if (grp == 0 && g == 0) s_y[rl] = s_rw[rl] + (s_t1[rl] * p.gamma) * out[0];
     __syncthreads();
-    const Mlp m = mlp_k(p.c, k, in_c, 1);
+    const Mlp m = staged(mlp_k(p.c, k, in_c, 1), s_par[K + 1], 1);
     float gy[8], gv1[8], dz1[8], gv2[8], dz2[8], dq = 0.0f, diff = 0.0f;
     if (grp == 1) {
         diff = out[0] - s_y[rl];
@@ -1272,32 +1329,61 @@ __global__ void __launch_bounds__(DT) dactor_tail(DTail p) {
     __shared__ int s_np[RB][MAXK];
     __shared__ float s_act[RB][NA * MAXK];
     __shared__ float s_c1[2][HID];
+    __shared__ __attribute__((aligned(16))) float s_par[2][PSLOT];  // actor k, critic k
+    __shared__ __attribute__((aligned(16))) float s_wa[NA][HID];    // critic k's W1 rows of agent k's actions
     const int k = blockIdx.y, tid = threadIdx.x, grp = tid >> 8, lt = tid & 255, rl = lt >> 4, g = lt & 15;
     const int K = p.K, B = p.B, HW = p.q.HW, r0 = blockIdx.x * RB, r = r0 + rl;
+    const int in_c = K * HW + NA * K;
     const bool own = grp == 0;  // the row layout's owners; group 1 joins the 128 x 128 layers
+    // prologue: this thread's share of the small parameters (loads issued first), the c1 sums and
+    // the recorded rows (their round trips overlap), then the parameters into LDS
+    const int na_ = stage_size(NA), nc_ = stage_size(1), tot = na_ + nc_ + NA * HID;
+    const float *wa = p.c.w1 + ((int64_t)k * in_c + (int64_t)K * HW + NA * k) * HID;
+    auto par_src = [&](int o) -> float {
+        return o < na_ ? stage_src(mlp_k(p.a, k, HW, NA), NA, o)
+               : o < na_ + nc_ ? stage_src(mlp_k(p.c, k, in_c, 1), 1, o - na_) : wa[o - na_ - nc_];
+    };
+    auto par_dst = [&](int o) -> float * {
+        return o < na_ ? &s_par[0][o] : o < na_ + nc_ ? &s_par[1][o - na_] : &s_wa[(o - na_ - nc_) / HID][(o - na_ - nc_) % HID];
+    };
+    constexpr int NSV = 8;
+    float sv[NSV];
+#pragma unroll
+    for (int u = 0; u < NSV; ++u) {
+        const int o = tid + u * DT;
+        sv[u] = o < tot ? par_src(o) : 0.0f;
+    }
     const uint32_t c = (uint32_t)p.ctr[0];  // the critic's count, advanced by the critic's step
     if (tid < 2 * HID) {
         const int net = tid / HID, j = tid % HID;
         s_c1[net][j] = net == 0 ? p.a.b1[k * HID + j] + d_sum_parts(p.w.cpart[0] + (int64_t)k * p.NG * HID + j, p.NG)
                                 : p.c.b1[k * HID + j] +
                                       d_sum_parts(p.w.cpart[2] + (int64_t)k * K * p.NG * HID + j, K * p.NG);
-    }
-    for (int o = tid; o < RB * K * NPM; o += DT) {  // the rows' states (recorded by the critic tail)
-        const int rr = o / (K * NPM), kk = (o / NPM) % K, i = o % NPM;
-        const int64_t ro = (int64_t)kk * B + r0 + rr;
-        const int n = p.w.np[ro];
-        if (i == 0) s_np[rr][kk] = n;
-        if (i < n) {
-            s_pc[rr][kk][i] = (int16_t)p.w.pc[ro * NPM + i];
-            s_pd[rr][kk][i] = p.w.pd[ro * NPM + i];
+    } else {
+        const int t2 = tid - 2 * HID;
+        for (int o = t2; o < RB * K * NPM; o += DT - 2 * HID) {  // the rows' states (recorded by the critic tail)
+            const int rr = o / (K * NPM), kk = (o / NPM) % K, i = o % NPM;
+            const int64_t ro = (int64_t)kk * B + r0 + rr;
+            const int n = p.w.np[ro];
+            if (i == 0) s_np[rr][kk] = n;
+            if (i < n) {
+                s_pc[rr][kk][i] = (int16_t)p.w.pc[ro * NPM + i];
+                s_pd[rr][kk][i] = p.w.pd[ro * NPM + i];
+            }
         }
+        for (int o = t2; o < RB * NA * K; o += DT - 2 * HID)
+            s_act[o / (NA * K)][o % (NA * K)] = p.w.act[(int64_t)r0 * NA * K + o];
     }
-    for (int o = tid; o < RB * NA * K; o += DT) s_act[o / (NA * K)][o % (NA * K)] = p.w.act[(int64_t)r0 * NA * K + o];
+#pragma unroll
+    for (int u = 0; u < NSV; ++u) {
+        const int o = tid + u * DT;
+        if (o < tot) *par_dst(o) = sv[u];
+    }
+    for (int o = tid + NSV * DT; o < tot; o += DT) *par_dst(o) = par_src(o);
     if (blockIdx.x == 0 && k == 0 && tid == 0) p.w.snap[1] = p.count[0] + 1;
     __syncthreads();
-    const int in_c = K * HW + NA * K;
-    const Mlp ma = mlp_k(p.a, k, HW, NA);
-    const Mlp mc = mlp_k(p.c, k, in_c, 1);
+    const Mlp ma = staged(mlp_k(p.a, k, HW, NA), s_par[0], NA);
+    const Mlp mc = staged(mlp_k(p.c, k, in_c, 1), s_par[1], 1);
     RowFwd fa, fc;
     float z[8], pr[NA];
     // the actor's forward and its GumbelSoftmax sample
@@ -1361,7 +1447,7 @@ __global__ void __launch_bounds__(DT) dactor_tail(DTail p) {
         float dp[NA];
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
-            const float *wr = mc.w1 + ((int64_t)K * HW + NA * k + a) * HID + 8 * g;
+            const float *wr = s_wa[a] + 8 * g;
             float s = 0.0f;
 #pragma unroll
             for (int i = 0; i < 8; ++i) s = fmaf(dz1[i], wr[i], s);
@@ -1432,24 +1518,49 @@ struct AdamSc {
     float step_size, bc2, w1, b2, w2, e;
 };
 
-__device__ __forceinline__ float adam_el(const DGrad &p, const AdamSc &a, int64_t off, float gi) {
-    p.g0[off] = gi;
-    const float mo = p.m0[off], vo = p.v0[off], po = p.p0[off];
-    const float mi = __fmaf_rn(a.w1, gi - mo, mo);         // exp_avg.lerp_(grad, 1 - beta1)
-    const float vi = __fmaf_rn(a.w2 * gi, gi, vo * a.b2);  // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
-    p.m0[off] = mi;
-    p.v0[off] = vi;
-    const float denom = sqrtf(vi) / a.bc2 + a.e;            // (exp_avg_sq.sqrt() / bc2_sqrt).add_(eps)
-    const float pi = __fmaf_rn(-a.step_size, mi / denom, po);  // param.addcdiv_(exp_avg, denom, -step_size)
-    p.p0[off] = pi;
-    return pi;
-}
-
-// phase 1: the actor target at the same offset, t = tau p + (1 - tau) t (agilerl soft_update)
-__device__ __forceinline__ float soft_el(float *t, int64_t off, float pi, float tau) {
-    const float ti = tau * pi + (1.0f - tau) * t[off];
-    t[off] = ti;
-    return ti;
+// NB elements' Adam steps with every load issued before the first store (a loop of element-wise
+// steps would serialise: its stores may alias the next element's loads); the first nv entries are valid.
+// soft: also the actor target's soft update at the same offsets (ti = the new target values)
+template <int NB>
+__device__ __forceinline__ void adam_n(const DGrad &p, const AdamSc &a, const int64_t (&off)[NB], const float (&gi)[NB],
+                                       int nv, bool soft, float (&pi)[NB], float (&ti)[NB]) {
+    float *__restrict__ P = p.p0;
+    float *__restrict__ G = p.g0;
+    float *__restrict__ M = p.m0;
+    float *__restrict__ V = p.v0;
+    float *__restrict__ T = p.t0;
+    float mo[NB], vo[NB], po[NB], to[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        if (i < nv) {
+            mo[i] = M[off[i]];
+            vo[i] = V[off[i]];
+            po[i] = P[off[i]];
+            to[i] = soft ? T[off[i]] : 0.0f;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        if (i < nv) {
+            const float mi = __fmaf_rn(a.w1, gi[i] - mo[i], mo[i]);
+            const float vi = __fmaf_rn(a.w2 * gi[i], gi[i], vo[i] * a.b2);
+            const float denom = sqrtf(vi) / a.bc2 + a.e;
+            pi[i] = __fmaf_rn(-a.step_size, mi / denom, po[i]);
+            mo[i] = mi;
+            vo[i] = vi;
+            if (soft) ti[i] = p.tau * pi[i] + (1.0f - p.tau) * to[i];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        if (i < nv) {
+            G[off[i]] = gi[i];
+            M[off[i]] = mo[i];
+            V[off[i]] = vo[i];
+            P[off[i]] = pi[i];
+            if (soft) T[off[i]] = ti[i];
+        }
+    }
 }
 
 // block exclusive prefix (thread order) of v over 256 threads; total returned in `total`
@@ -1521,10 +1632,29 @@ __global__ void __launch_bounds__(256) dgrads_adam(DGrad p) {
             __syncthreads();
             float tp = 0.0f;
             const float *cw = p.cnet.w1 + ((int64_t)k * in_dim + row0) * HID + j;
-            for (int cc = h; cc < ncell; cc += 2) {
-                const int64_t off = (cw + (int64_t)cc * HID) - p.cp0;
-                const float ti = soft_el(p.ct0, off, p.cp0[off], p.tau);
-                tp = fmaf(s_base[cc], ti, tp);
+            const float *__restrict__ CP = p.cp0;
+            float *__restrict__ CT = p.ct0;
+            for (int u0 = 0; u0 < CG / 2; u0 += 16) {  // 16 cells' loads in flight, then the stores
+                float pv[16], tv[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    const int cc = h + 2 * (u0 + u);
+                    if (cc < ncell) {
+                        const int64_t off = (cw + (int64_t)cc * HID) - p.cp0;
+                        pv[u] = CP[off];
+                        tv[u] = CT[off];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    const int cc = h + 2 * (u0 + u);
+                    if (cc < ncell) {
+                        const int64_t off = (cw + (int64_t)cc * HID) - p.cp0;
+                        const float ti = p.tau * pv[u] + (1.0f - p.tau) * tv[u];
+                        CT[off] = ti;
+                        tp = fmaf(s_base[cc], ti, tp);
+                    }
+                }
             }
             s_pp[1][h][j] = tp;
             __syncthreads();
@@ -1540,32 +1670,36 @@ __global__ void __launch_bounds__(256) dgrads_adam(DGrad p) {
         // the patched cells of the rows' obs `obk` inside this group, in (row, slot) order
         const int obk = p.phase == 0 ? ob : k;
         const int NE = B * NPM, per = (NE + 255) / 256, t0 = tid * per;
-        int cnt = 0;
-        for (int i = 0; i < per; ++i) {
+        constexpr int PER = (DMAXB * NPM + 255) / 256;
+        int cl[PER];  // this thread's items: the cell offset in the group, or -1 (loads batched)
+        int npv[PER];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
             const int t = t0 + i;
-            if (t >= NE) break;
-            const int rr = t / NPM, pi = t % NPM;
-            const int64_t ro = (int64_t)obk * B + rr;
-            if (pi < p.w.np[ro]) {
-                const int cl = p.w.pc[ro * NPM + pi] - c0;
-                cnt += (cl >= 0 && cl < ncell) ? 1 : 0;
+            npv[i] = (i < per && t < NE) ? p.w.np[(int64_t)obk * B + t / NPM] : 0;
+        }
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int t = t0 + i;
+            cl[i] = -1;
+            if (i < per && t < NE && t % NPM < npv[i]) {
+                const int c = p.w.pc[((int64_t)obk * B + t / NPM) * NPM + t % NPM] - c0;
+                cl[i] = (c >= 0 && c < ncell) ? c : -1;
             }
         }
+        int cnt = 0;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) cnt += cl[i] >= 0 ? 1 : 0;
         int total = 0;
         int at = d_excl_scan256(cnt, s_red, total);
-        for (int i = 0; i < per; ++i) {
-            const int t = t0 + i;
-            if (t >= NE) break;
-            const int rr = t / NPM, pi = t % NPM;
-            const int64_t ro = (int64_t)obk * B + rr;
-            if (pi < p.w.np[ro]) {
-                const int cl = p.w.pc[ro * NPM + pi] - c0;
-                if (cl >= 0 && cl < ncell) {
-                    s_ec[at] = cl;
-                    s_er[at] = rr;
-                    s_ed[at] = p.w.pd[ro * NPM + pi];
-                    ++at;
-                }
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            if (cl[i] >= 0) {
+                const int t = t0 + i;
+                s_ec[at] = cl[i];
+                s_er[at] = t / NPM;
+                s_ed[at] = p.w.pd[((int64_t)obk * B + t / NPM) * NPM + t % NPM];
+                ++at;
             }
         }
         __syncthreads();
@@ -1589,16 +1723,33 @@ __global__ void __launch_bounds__(256) dgrads_adam(DGrad p) {
         const float *wk = p.net.w1 + ((int64_t)k * in_dim + row0) * HID + j;
         const float *dz1 = p.w.sv.dz1 + (int64_t)k * B * HID + j;
         float pp = 0.0f, tp = 0.0f;
-        for (int cc = h; cc < ncell; cc += 2) {
-            float gi = s_base[cc] * s_S[j];
-            for (int e = s_cnt[cc]; e < s_cnt[cc + 1]; ++e) {
-                const int ei = s_bk[e];
-                gi = fmaf(s_ed[ei], dz1[(int64_t)s_er[ei] * HID], gi);
+        for (int u0 = 0; u0 < CG / 2; u0 += 16) {  // 16 cells per pass (h, h + 2, ...)
+            int64_t off[16];
+            float gv[16], pv[16], tv[16];
+            int nv = 0;
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int cc = h + 2 * (u0 + u);
+                if (cc < ncell) {
+                    float gi = s_base[cc] * s_S[j];
+                    for (int e = s_cnt[cc]; e < s_cnt[cc + 1]; ++e) {
+                        const int ei = s_bk[e];
+                        gi = fmaf(s_ed[ei], dz1[(int64_t)s_er[ei] * HID], gi);
+                    }
+                    gv[u] = gi;
+                    off[u] = (wk + (int64_t)cc * HID) - p.p0;
+                    nv = u + 1;
+                }
             }
-            const int64_t off = (wk + (int64_t)cc * HID) - p.p0;
-            const float pi = adam_el(p, sc, off, gi);
-            pp = fmaf(s_base[cc], pi, pp);
-            if (soft) tp = fmaf(s_base[cc], soft_el(p.t0, off, pi, p.tau), tp);
+            adam_n<16>(p, sc, off, gv, nv, soft, pv, tv);
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int cc = h + 2 * (u0 + u);
+                if (u < nv) {
+                    pp = fmaf(s_base[cc], pv[u], pp);
+                    if (soft) tp = fmaf(s_base[cc], tv[u], tp);
+                }
+            }
         }
         s_pp[0][h][j] = pp;
         s_pp[1][h][j] = tp;
@@ -1618,6 +1769,7 @@ __global__ void __launch_bounds__(256) dgrads_adam(DGrad p) {
             float acc[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) acc[u] = 0.0f;
+#pragma unroll 8
             for (int rr = 0; rr < B; ++rr) {
                 const float d = dz1[(int64_t)rr * HID];
                 const float *av = p.w.act + (int64_t)rr * na;
@@ -1627,14 +1779,18 @@ __global__ void __launch_bounds__(256) dgrads_adam(DGrad p) {
                     if (a < na) acc[u] = fmaf(av[a], d, acc[u]);
                 }
             }
+            int64_t off[8];
+            float pv[8], tv[8];
+            int nv = 0;
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const int a = a0 + 2 * u;
                 if (a < na) {
-                    const int64_t off = (p.net.w1 + ((int64_t)k * p.in_dim + (int64_t)K * HW + a) * HID + j) - p.p0;
-                    adam_el(p, sc, off, acc[u]);
+                    off[u] = (p.net.w1 + ((int64_t)k * p.in_dim + (int64_t)K * HW + a) * HID + j) - p.p0;
+                    nv = u + 1;
                 }
             }
+            adam_n<8>(p, sc, off, acc, nv, false, pv, tv);
         }
         return;
     }
@@ -1681,16 +1837,17 @@ __global__ void __launch_bounds__(256) dgrads_adam(DGrad p) {
             }
         }
         const float *w2 = p.net.w2 + (int64_t)k * HID * HID;
+        int64_t off[8];
+        float gv[8], pv[8], tv[8];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int d = d0 + 4 * lq + i;
-            const int64_t o0 = (w2 + (int64_t)d * HID + n0) - p.p0, o1 = (w2 + (int64_t)d * HID + n1) - p.p0;
-            const float q0 = adam_el(p, sc, o0, acc0[i]), q1 = adam_el(p, sc, o1, acc1[i]);
-            if (soft) {
-                soft_el(p.t0, o0, q0, p.tau);
-                soft_el(p.t0, o1, q1, p.tau);
-            }
+            off[2 * i] = (w2 + (int64_t)d * HID + n0) - p.p0;
+            off[2 * i + 1] = (w2 + (int64_t)d * HID + n1) - p.p0;
+            gv[2 * i] = acc0[i];
+            gv[2 * i + 1] = acc1[i];
         }
+        adam_n<8>(p, sc, off, gv, 8, soft, pv, tv);
         return;
     }
     const int rg = tid >> 4, g = tid & 15;
@@ -1737,14 +1894,17 @@ __global__ void __launch_bounds__(256) dgrads_adam(DGrad p) {
             for (int i = 0; i < 8; ++i) part[rg][v][8 * g + i] = acc[v][i];
         __syncthreads();
         const float *dst[6] = {p.net.b1, p.net.ln1_w, p.net.ln1_b, p.net.b2, p.net.ln2_w, p.net.ln2_b};
-        for (int t = tid; t < 6 * HID; t += 256) {
-            const int v = t / HID, j = t % HID;
+        int64_t off[3];
+        float gv[3], pv[3], tv[3];
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {  // 6 * 128 = 3 * 256 elements
+            const int t = tid + 256 * u, v = t / HID, j = t % HID;
             float sum = 0.0f;
             for (int qq = 0; qq < GRG; ++qq) sum += part[qq][v][j];
-            const int64_t off = (dst[v] + k * HID + j) - p.p0;
-            const float pi = adam_el(p, sc, off, sum);
-            if (soft) soft_el(p.t0, off, pi, p.tau);
+            gv[u] = sum;
+            off[u] = (dst[v] + k * HID + j) - p.p0;
         }
+        adam_n<3>(p, sc, off, gv, 3, soft, pv, tv);
         return;
     }
     if (type == 4) {  // W3 = h2^T g3, b3, the loss
@@ -1787,21 +1947,33 @@ __global__ void __launch_bounds__(256) dgrads_adam(DGrad p) {
             pb[rg][NA] = lacc;
         }
         __syncthreads();
-        for (int t = tid; t < HID * out; t += 256) {
-            const int j = t / out, a = t % out;
-            float sum = 0.0f;
-            for (int qq = 0; qq < GRG; ++qq) sum += part[qq][j][a];
-            const int64_t off = (p.net.w3 + ((int64_t)k * HID + j) * out + a) - p.p0;
-            const float pi = adam_el(p, sc, off, sum);
-            if (soft) soft_el(p.t0, off, pi, p.tau);
+        {
+            constexpr int NW3 = (HID * NA + 255) / 256 + 1;  // this thread's W3 elements + its b3 element
+            int64_t off[NW3];
+            float gv[NW3], pv[NW3], tv[NW3];
+            int nv = 0;
+#pragma unroll
+            for (int u = 0; u < NW3 - 1; ++u) {
+                const int t = tid + 256 * u;
+                if (t < HID * out) {
+                    const int j = t / out, a = t % out;
+                    float sum = 0.0f;
+                    for (int qq = 0; qq < GRG; ++qq) sum += part[qq][j][a];
+                    gv[nv] = sum;
+                    off[nv] = (p.net.w3 + ((int64_t)k * HID + j) * out + a) - p.p0;
+                    ++nv;
+                }
+            }
+            if (tid < out) {
+                float sum = 0.0f;
+                for (int qq = 0; qq < GRG; ++qq) sum += pb[qq][tid];
+                gv[nv] = sum;
+                off[nv] = (p.net.b3 + k * out + tid) - p.p0;
+                ++nv;
+            }
+            adam_n<NW3>(p, sc, off, gv, nv, soft, pv, tv);
         }
-        if (tid < out) {
-            float sum = 0.0f;
-            for (int qq = 0; qq < GRG; ++qq) sum += pb[qq][tid];
-            const int64_t off = (p.net.b3 + k * out + tid) - p.p0;
-            const float pi = adam_el(p, sc, off, sum);
-            if (soft) soft_el(p.t0, off, pi, p.tau);
-        } else if (tid == 64) {
+        if (tid == 64) {
             float sum = 0.0f;
             for (int qq = 0; qq < GRG; ++qq) sum += pb[qq][NA];
             p.loss[k] = p.phase == 0 ? sum / (float)B : -(sum / (float)B);
@@ -1811,10 +1983,24 @@ __global__ void __launch_bounds__(256) dgrads_adam(DGrad p) {
     // type 6: the critic target's soft update outside its W1 state rows (grid-stride)
     const int in_c = K * HW + NA * K;
     const int64_t w1off = p.cnet.w1 - p.cp0;
-    for (int64_t i = (int64_t)b * 256 + tid; i < p.cn; i += (int64_t)p.nrest * 256) {
-        const int64_t rel = i - w1off;
-        if (rel >= 0 && rel < (int64_t)K * in_c * HID && (rel / HID) % in_c < (int64_t)K * HW) continue;
-        p.ct0[i] = p.tau * p.cp0[i] + (1.0f - p.tau) * p.ct0[i];
+    const float *__restrict__ CP = p.cp0;
+    float *__restrict__ CT = p.ct0;
+    const int64_t stride = (int64_t)p.nrest * 256;
+    for (int64_t i0 = (int64_t)b * 256 + tid; i0 < p.cn; i0 += 8 * stride) {  // 8 elements' loads in flight
+        float pv[8], tv[8];
+        bool on[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t i = i0 + u * stride, rel = i - w1off;
+            on[u] = i < p.cn && !(rel >= 0 && rel < (int64_t)K * in_c * HID && (rel / HID) % in_c < (int64_t)K * HW);
+            if (on[u]) {
+                pv[u] = CP[i];
+                tv[u] = CT[i];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (on[u]) CT[i0 + u * stride] = p.tau * pv[u] + (1.0f - p.tau) * tv[u];
     }
 }
 
@@ -2246,7 +2432,7 @@ gw_status gw_maddpg_desc_update(const gw_obs_source *src, const gw_desc_ring *ri
     g.nobs = 1;
     g.in_dim = HW;
     g.out = NA;
-    g.nrest = 64;
+    g.nrest = 256;
     {
         const int n[7] = {K * NG, 0, K * (HID / RB), K, K, K * K * NG, g.nrest};
         g.start[0] = 0;

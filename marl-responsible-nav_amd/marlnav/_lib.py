@@ -180,7 +180,7 @@ EXPORTS = ["gw_create", "gw_reset", "gw_step", "gw_state_view", "gw_copy_state",
            "gw_pipeline_state_bytes", "gw_pipeline_save", "gw_pipeline_load",
            "gw_gather_pack_scratch", "gw_gather_pack", "gw_gather_unpack_plan_cap", "gw_gather_unpack",
            "gw_adam_soft_step", "gw_obs_desc_copy", "gw_replay_gather_desc",
-           "gw_maddpg_desc_workspace_floats", "gw_maddpg_desc_prime", "gw_maddpg_desc_update"]
+           "gw_maddpg_desc_workspace_floats", "gw_maddpg_desc_prime", "gw_maddpg_desc_update", "gw_count_sims"]
 
 
 class GwObsSource(C.Structure):
@@ -323,6 +323,8 @@ def _declare(L):
     L.gw_replay_gather_desc.argtypes = [C.POINTER(GwObsSource)] + [p] * 8 + [C.c_int64, C.c_int64] + [p] * 8 + \
         [C.c_uint64, p, p]
     L.gw_replay_gather_desc.restype = C.c_int
+    L.gw_count_sims.argtypes = [p, p]
+    L.gw_count_sims.restype = C.c_int
     L.gw_obs_desc_copy.argtypes = [p, p, p]
     L.gw_obs_desc_copy.restype = C.c_int
     L.gw_obs_view.argtypes = [p, C.POINTER(GwObsSource)]

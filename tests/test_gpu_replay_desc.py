@@ -85,9 +85,12 @@ def test_resume_falls_back_to_dense_rows():
     env.close()
 
 
-def test_training_on_desc_rows_equals_dense_rows():
+def test_training_on_desc_rows_equals_dense_rows(monkeypatch):
     """Two trainers from the same seeds, one sampling the descriptor ring (the default with the
-    fused actor), one the dense slots: after 24 env steps with updates every weight is equal."""
+    fused actor), one the dense slots, both with the dense-row learner (GW_DESC_LEARN=0; the
+    descriptor learner has its own tests, tests/test_gpu_desc_learner.py): after 24 env steps with
+    updates every weight is equal."""
+    monkeypatch.setenv("GW_DESC_LEARN", "0")
     from marlnav.maddpg import MADDPG
     from marlnav.train import MADDPGTrainer
     sc = S.builtin("grid32")
@@ -110,10 +113,14 @@ def test_training_on_desc_rows_equals_dense_rows():
         assert torch.equal(states[0][k], states[1][k]), k
 
 
-def test_update_as_recorded_launches_equals_graph_replay():
+@pytest.mark.parametrize("desc_learner", ["1", "0"])
+def test_update_as_recorded_launches_equals_graph_replay(monkeypatch, desc_learner):
     """MADDPG.capture(launches=True): the captured update re-issued as its recorded C-ABI
     launches (_lib.LaunchRecorder) == the HIP graph replay, every weight bit for bit (same
-    seeds, in-kernel draws), and the replayed launches really ran (the weights moved)."""
+    seeds, in-kernel draws), and the replayed launches really ran (the weights moved); with the
+    descriptor learner (one gw_maddpg_desc_update call) and with the dense-row update."""
+    monkeypatch.setenv("GW_DESC_LEARN", desc_learner)
+    first = "gw_maddpg_desc_update" if desc_learner == "1" else "gw_replay_gather_desc"
     from marlnav.maddpg import MADDPG
     from marlnav.train import MADDPGTrainer
     sc = S.builtin("grid32")
@@ -127,7 +134,7 @@ def test_update_as_recorded_launches_equals_graph_replay():
         assert m._graph is not None and (m._launches is not None) == (mode == "launches")
         if mode == "launches":
             names = [c[0] for c in m._launches.calls]
-            assert names[0] == "gw_replay_gather_desc" and "gw_actor_prepare" in names, names
+            assert names[0] == first and "gw_actor_prepare" in names, names
         before = m.actors.net.flat_params().clone()
         tr.train(18)
         torch.cuda.synchronize()
@@ -160,7 +167,7 @@ def test_capture_follows_the_rings_row_mode():
     assert tr.rollout.replay.use_desc and not m.capture_matches(tr.rollout.replay)
     tr.train(3)
     assert m._capture_desc is True and m.capture_matches(tr.rollout.replay)
-    assert [c[0] for c in m._launches.calls][0] == "gw_replay_gather_desc"
+    assert [c[0] for c in m._launches.calls][0] == "gw_maddpg_desc_update"
     env.close()
 
 

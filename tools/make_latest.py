@@ -23,7 +23,7 @@ def main(tag, config, cmd=None):
     kernels = {}
     for name, v in s.items():
         kind = KIND.get(name.split("<")[0].strip())
-        if kind and (v.get("hbm_mb") is not None or v.get("busy_us")):
+        if kind and (v.get("hbm_mb") is not None or v.get("busy_us") or v.get("valu_insts")):
             k = {"avg_us": v["avg_us"], "calls": v.get("calls")}
             if v.get("hbm_mb") is not None:
                 k["hbm_bytes_per_launch"] = v["hbm_mb"] * 1e6
@@ -35,6 +35,10 @@ def main(tag, config, cmd=None):
                     k["busy_us_per_step"] = v["busy_us"] * v["calls"] / steps
                 if v.get("hbm_mb") is not None:
                     k["hbm_bytes_per_step"] = v["hbm_mb"] * 1e6 * v["calls"] / steps
+            if v.get("valu_insts"):
+                k["valu_insts_per_launch"] = v["valu_insts"]
+                if steps:
+                    k["valu_insts_per_step"] = v["valu_insts"] * v["calls"] / steps
             kernels[kind] = k
     cmd = cmd or f"python bench.py --config {config}"
     path = os.path.join(ROOT, "profiles", "latest.json")
@@ -46,7 +50,7 @@ def main(tag, config, cmd=None):
         old = {k: out[k] for k in ("source", "config", "kernels") if k in out}
         out = {"configs": {old["config"]: {"source": old["source"], "kernels": old["kernels"]}} if old else {}}
     out["configs"][config] = {
-        "source": f"profiles/{tag} (rocprofv3 --kernel-trace --stats and --pmc FETCH_SIZE / WRITE_SIZE passes of "
+        "source": f"profiles/{tag} (rocprofv3 --kernel-trace --stats, --pmc FETCH_SIZE / WRITE_SIZE and SQ_INSTS_VALU passes of "
                   f"`{cmd}`; FETCH_SIZE x2 per MI355X_MICROARCH.md; busy_us = the union of the launches' "
                   f"intervals in the kernel trace / launches)",
         "kernels": kernels}

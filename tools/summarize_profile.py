@@ -1,4 +1,5 @@
-"""Summarise a tools/gpu_profile.sh run (rocprofv3 kernel stats + FETCH_SIZE/WRITE_SIZE passes)
+"""Summarise a tools/gpu_profile.sh run (rocprofv3 kernel stats + FETCH_SIZE / WRITE_SIZE passes +
+a SQ_INSTS_VALU / SQ_WAVES / SQ_WAVE_CYCLES / GRBM_GUI_ACTIVE pass)
 into profiles/<tag>/SUMMARY.md and copy the raw CSVs next to it.
 
 gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports half the bytes of a wide
@@ -10,16 +11,26 @@ import shutil
 import sys
 
 
-def busy_per_launch(trace_csv):
+STEP_KERNELS = ("gw::step_v2", "gw::step_obs", "gw::step_kernel_fear", "gw::step_kernel_nofear")
+
+
+def busy_per_launch(trace_csv, last_steps=64):
     """kernel short name -> (launches, union of their [start, end] intervals / launches in us):
     the busy time per launch bench.py reports as avg_launch_ms (overlapping launches of one
-    kernel, e.g. obs writers of consecutive steps on two streams, counted once)."""
+    kernel, e.g. obs writers of consecutive steps on two streams, counted once).  Only the
+    launches of the last `last_steps` steps count (bench.py's profiled steps, after its timed
+    region: warmup and the pipeline's fill are outside the window bench.py measures too)."""
     iv = {}
     for r in csv.DictReader(open(trace_csv)):
         name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
         iv.setdefault(name, []).append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+    steps = sorted(b for n, v in iv.items() if n.split("<")[0].strip() in STEP_KERNELS for b, _ in v)
+    t0 = steps[-last_steps] if last_steps and len(steps) >= last_steps else None
     out = {}
     for name, v in iv.items():
+        if t0 is not None:
+            v = [x for x in v if x[0] >= t0] or v
+
         v.sort()
         total, cb, ce = 0, None, None
         for b, e in v:
@@ -40,14 +51,15 @@ def main(src, dst):
     trace = os.path.join(src, "trace", "run_kernel_trace.csv")
     busy = busy_per_launch(trace) if os.path.exists(trace) else {}
     pmc = {}
-    for which, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+    for which, ctrs in (("fetch", ("FETCH_SIZE",)), ("write", ("WRITE_SIZE",)),
+                        ("valu", ("SQ_INSTS_VALU", "SQ_WAVES", "SQ_WAVE_CYCLES", "GRBM_GUI_ACTIVE"))):
         path = os.path.join(src, which, "run_counter_collection.csv")
         if not os.path.exists(path):
             continue
         for r in csv.DictReader(open(path)):
-            if r["Counter_Name"] != ctr:
+            if r["Counter_Name"] not in ctrs:
                 continue
-            pmc.setdefault(r["Kernel_Name"], {}).setdefault(ctr, []).append(float(r["Counter_Value"]))
+            pmc.setdefault(r["Kernel_Name"], {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     lines = [f"# rocprofv3 summary ({os.path.basename(dst)})", "",
              "| kernel | calls | avg us | busy us / launch | min us | max us | % time | FETCH MB/launch (x2 corr.) | WRITE MB/launch | HBM MB/launch |",
              "|---|---|---|---|---|---|---|---|---|---|"]
@@ -69,7 +81,19 @@ def main(src, dst):
                      f"{'' if tot is None else f'{tot:.2f}'} |")
         out[short] = dict(calls=int(r["Calls"]), avg_us=float(r["AverageNs"]) / 1e3, busy_us=bz, fetch_mb=fmb,
                           write_mb=wmb, hbm_mb=tot)
-    for log in ("trace.log", "fetch.log", "write.log"):
+        vi = p.get("SQ_INSTS_VALU")
+        if vi:  # wave-level vector instructions per launch; GRBM_GUI_ACTIVE summed over the 8 XCDs
+            avg = lambda c: sum(p[c]) / len(p[c]) if p.get(c) else None  # noqa: E731
+            out[short].update(valu_insts=avg("SQ_INSTS_VALU"), waves=avg("SQ_WAVES"), wave_cycles=avg("SQ_WAVE_CYCLES"),
+                              gui_active=avg("GRBM_GUI_ACTIVE"))
+            dur = bz or float(r["AverageNs"]) / 1e3
+            rate = out[short]["valu_insts"] / (dur * 1e-6) / 1e9
+            out[short]["valu_gips"] = rate
+            out[short]["valu_frac"] = rate / (256 * 4 * 2.4e9 / 2 / 1e9)
+            lines.append(f"|   VALU | {out[short]['valu_insts']:.4g} wave-instructions per launch, {rate:.1f} G/s over "
+                         f"{dur:.2f} us = {out[short]['valu_frac']:.3f} of the 1,228.8 G/s issue peak; "
+                         f"{out[short]['waves']:.0f} waves |  |  |  |  |  |  |  |  |")
+    for log in ("trace.log", "fetch.log", "write.log", "valu.log"):
         p = os.path.join(src, log)
         if os.path.exists(p):
             for l in open(p):
@@ -79,12 +103,12 @@ def main(src, dst):
                               f"{j['ms_per_step']:.4f} ms/step, kernels_ms {j.get('kernels_ms')}"]
     open(os.path.join(dst, "SUMMARY.md"), "w").write("\n".join(lines) + "\n")
     json.dump(out, open(os.path.join(dst, "summary.json"), "w"), indent=1)
-    for sub in ("trace", "fetch", "write"):
+    for sub in ("trace", "fetch", "write", "valu"):
         for fn in ("run_kernel_stats.csv", "run_counter_collection.csv"):
             p = os.path.join(src, sub, fn)
             if os.path.exists(p):
                 shutil.copy(p, os.path.join(dst, f"{sub}_{fn}"))
-    for log in ("trace.log", "fetch.log", "write.log"):
+    for log in ("trace.log", "fetch.log", "write.log", "valu.log"):
         p = os.path.join(src, log)
         if os.path.exists(p):
             with open(p) as fi, open(os.path.join(dst, log), "w") as fo:
