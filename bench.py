@@ -401,8 +401,12 @@ def main():
         # env-only C1 / C2 lines, and the small-batch rollout (C2) with the fused MLP actor
         small_rollout = (cfg.get("rollout") and not cfg.get("patch") and not cfg.get("arch") and
                          env.kernel_path == "merged" and not args.updates_per_step)
+        # the local-window rollouts (c5patch / c4patch): the fused window actors' host enqueue is
+        # about as long as the step, so their steps replay as ring-phase graphs too
+        window_rollout = (cfg.get("rollout") and cfg.get("patch") and not args.patch_torch and
+                          not args.updates_per_step)
         graph_n = 16 if (world == 1 and (not obs_mode or env.kernel_path == "merged") and
-                         (not cfg.get("rollout") or small_rollout)) else 0
+                         (not cfg.get("rollout") or small_rollout or window_rollout)) else 0
     graph_n = min(graph_n, args.steps)
     if obs_mode and env.kernel_path == "merged":
         graph_n -= graph_n % 2  # merged async: an even number of captured steps

@@ -149,6 +149,8 @@ struct ActParams {
     uint32_t key0, key1, ctr0, ctr1;
     const int64_t *ctr_dev;   // null, or a device counter added to (ctr1:ctr0) at launch time
     int apples[MAXN];
+    int *zero_n;              // null, or counters this launch zeroes (the window CNN's bucket sizes,
+    int zero_cnt;             //   read by the rare kernel before it), zero_cnt <= 64 * WAVES
 };
 
 // GW_ACT_AB bit 3 (measurement only): wave 0 of each block stamps s_memtime at its phase
@@ -328,6 +330,7 @@ __global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
     const bool ln = p.net.layer_norm != 0;
     const int wave = tid >> 6, lane = tid & 63, el = lane & 15, q = lane >> 4;
     int tile = blockIdx.x * WAVES + wave;
+    if (p.zero_n && blockIdx.x == 0 && k == 0 && tid < p.zero_cnt) p.zero_n[tid] = 0;
     const int bid = blockIdx.y * gridDim.x + blockIdx.x;
     ACT_STAMP(0);
     Desc dn = load_desc(p, (int64_t)tile * TILE + el, k);  // first tile's descriptor, in flight
@@ -1434,6 +1437,95 @@ __global__ void __launch_bounds__(256) wcnn_l1_kernel(CnnParams p, Lists lists) 
         lists.cnt[((size_t)k * p.P + tid) * lists.nblk + blockIdx.x] = s_cnt[0][tid] + s_cnt[1][tid] + s_cnt[2][tid] + s_cnt[3][tid];
 }
 
+// wcnn_l1_kernel with the listing folded in (round 5): a block of 256 threads takes LR_ENVS envs
+// (LR_ENVS / 256 per thread), counts its items per position in LDS, claims each position's range
+// of its bucket with ONE atomic add on the bucket's counter (64 per bucket and agent at 65,536
+// envs instead of one per wave: same-address atomics serialise), and writes its items there.  An
+// item's place inside its bucket then depends on the blocks' arrival order, but no result does:
+// the rare kernel computes each item on its own and writes it to the item's (env, slot) row, which
+// act_kernel sums in slot order.  The counters are zeroed by the act_kernel launch that follows
+// (p.zero_n), after the rare kernel has read them.
+constexpr int LR_ENVS = 1024;
+template <int NP>
+__global__ void __launch_bounds__(256) wcnn_list_kernel(CnnParams p) {
+    constexpr int PER = LR_ENVS / 256;
+    __shared__ uint32_t s_road[128];
+    __shared__ int s_cnt[WNQ], s_base[WNQ];
+    const int k = blockIdx.y, tid = threadIdx.x;
+    if (tid < 128) s_road[tid] = p.ws.road[tid];
+    if (tid < WNQ) s_cnt[tid] = 0;
+    int64_t ev[PER];
+    uint4 cells[PER];
+    uint32_t flags[PER];
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {  // every descriptor load of the thread in flight together
+        ev[r] = (int64_t)blockIdx.x * LR_ENVS + r * 256 + tid;
+        const bool valid = ev[r] < p.E;
+        cells[r] = valid ? *reinterpret_cast<const uint4 *>(p.desc + ev[r] * NDESC) : make_uint4(0, 0, 0, 0);
+        flags[r] = valid ? p.desc[ev[r] * NDESC + 4] : 0u;
+    }
+    __syncthreads();
+    auto map_at = [&](int c) { return ((s_road[c >> 5] >> (c & 31)) & 1u) ? 0.0f : -1.0f; };
+    const int half = p.PW / 2;
+    const float vo = own_value(k, p.variant);
+    uint32_t qm[PER];
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        int pc[NP];
+        float pv[NP];
+        {
+            const bool reset = (flags[r] & D_RESET) != 0;
+            const int ac = ((flags[r] >> (8 + k)) & 1u) ? p.apples[k] : -1;
+            float av = (ac >= 0 ? map_at(ac) : 0.0f) + 9.0f;
+            if (!reset && av == (float)(k + 1)) av = 1.0f;
+            pc[0] = ac;
+            pv[0] = av;
+            const uint32_t dw[4] = {cells[r].x, cells[r].y, cells[r].z, cells[r].w};
+#pragma unroll
+            for (int n = 0; n < NP - 1; ++n) {
+                const int c = (int)((dw[n >> 1] >> (16 * (n & 1))) & 0xFFFFu);
+                pc[1 + n] = c;
+                pv[1 + n] = agent_value(reset, n, k, c == ac, p.variant);
+            }
+        }
+        const int ctr = (unsigned)pc[1 + k] < (unsigned)p.HW ? pc[1 + k] : 0;
+        const int cr = ctr / p.W, cc = ctr % p.W;
+        uint32_t qmask = 0;
+        bool ctr_set = false;
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+            const int c = pc[i];
+            bool live = (unsigned)c < (unsigned)p.HW;
+#pragma unroll
+            for (int q = i + 1; q < NP; ++q) live = live && pc[q] != c;  // a later slot wins
+            if (!live) continue;
+            const int wr = c / p.W - cr + half, wc = c % p.W - cc + half;
+            if ((unsigned)wr >= (unsigned)p.PW || (unsigned)wc >= (unsigned)p.PW) continue;
+            const bool centre = c == ctr;
+            ctr_set = ctr_set || centre;
+            if (centre && pv[i] == vo) continue;
+            qmask |= 1u << ((wr >> 2) * p.Wq + (wc >> 2));
+        }
+        if (!ctr_set && map_at(ctr) != vo) qmask |= 1u << ((half >> 2) * p.Wq + (half >> 2));
+        const bool valid = ev[r] < p.E;
+        if (!valid || (p.ab & 4)) qmask = 0;
+        if (valid) p.ws.rare_n[(size_t)k * p.E + ev[r]] = __popc(qmask);
+        qm[r] = qmask;
+        for (uint32_t m = qmask; m; m &= m - 1) atomicAdd(&s_cnt[__ffs(m) - 1], 1);  // LDS
+    }
+    __syncthreads();
+    if (tid < p.P && s_cnt[tid]) s_base[tid] = atomicAdd(&p.ws.bucket_n[k * p.P + tid], s_cnt[tid]);
+    if (tid < WNQ) s_cnt[tid] = 0;  // reused as the block's fill counts
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        for (uint32_t m = qm[r]; m; m &= m - 1) {
+            const int Q = __ffs(m) - 1;
+            const int pos = s_base[Q] + atomicAdd(&s_cnt[Q], 1);
+            p.ws.bucket[((size_t)k * p.P + Q) * p.E + pos] = (int)(ev[r] * RSW + __popc(qm[r] & ((1u << Q) - 1u)));
+        }
+    }
+}
 
 // one 64-thread block per bucket: the offsets of the layer-1 blocks' items in the bucket (a wave
 // scan over the blocks in order) and the bucket's size.  All of a lane's counts are loaded before
@@ -1722,7 +1814,7 @@ gw_status actor_act(const char *who, void *env, int32_t P, const gw_mlp_actors *
     if (st != GW_OK) return st;
     if ((st = check_net(src, net, who, P)) != GW_OK) return st;
     if (!(tau > 0.0f)) return err(GW_ERR_ARG, w + ": tau must be > 0");
-    ActParams p;
+    ActParams p{};
     p.net = *net;
     const Ws wl = ws_layout(const_cast<float *>(ws), src.K);
     p.c1 = wl.c1;
@@ -1948,7 +2040,7 @@ gw_status gw_cnn_act(void *env, const gw_cnn_actors *net, const float *ws, int t
         }
     }
 #undef RARE
-    ActParams p;
+    ActParams p{};
     p.net = cnn_tail(net);
     p.c1 = cp.ws.mlp.c1;
     p.w2img = cp.ws.mlp.w2;
@@ -2039,9 +2131,11 @@ gw_status gw_patch_cnn_prepare(void *env, int32_t P, const gw_cnn_actors *net, f
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(cnn_prep_wlt, dim3(2048), dim3(256), 0, s, p);
     hipLaunchKernelGGL(wcnn_prep_base, dim3((p.HW + WCG - 1) / WCG, src.K), dim3(256), 0, s, p);
-    {  // (the lists' spare counter word starts at 0)
+    {  // (the lists' spare counter word and the fused listing's bucket counters start at 0)
         const Lists l = lists_at(p.ws.unit_off, src.K * p.P, src.K, src.E, 256);
-        if (hipMemsetAsync(l.ctr, 0, sizeof(int), s) != hipSuccess) return err(GW_ERR_HIP, "gw_patch_cnn_prepare: memset");
+        if (hipMemsetAsync(l.ctr, 0, sizeof(int), s) != hipSuccess ||
+            hipMemsetAsync(p.ws.bucket_n, 0, sizeof(int) * src.K * p.P, s) != hipSuccess)
+            return err(GW_ERR_HIP, "gw_patch_cnn_prepare: memset");
     }
     PrepParams pp;  // the layer-2/3 MFMA images (c1 unused)
     pp.net = cnn_tail(net);
@@ -2068,24 +2162,42 @@ gw_status gw_patch_cnn_act(void *env, int32_t P, const gw_cnn_actors *net, const
     if (!(tau > 0.0f)) return err(GW_ERR_ARG, "gw_patch_cnn_act: tau must be > 0");
     const CnnParams cp = wcnn_params(src, P, net, const_cast<float *>(ws));
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const Lists lists = lists_at(cp.ws.unit_off, src.K * cp.P, src.K, src.E, 256);
-    const dim3 lgrid((unsigned)lists.nblk, src.K);
-    {
+    if (src.K * cp.P > RARE_MAX_NB) return err(GW_ERR_ARG, "gw_patch_cnn_act: K x window positions above the rare kernels' table");
+    // the positions to recompute, listed per (agent, position) bucket in ONE launch (round 5;
+    // GW_WCNN_LIST=scan: the round-4 chain of layer-1 counts, bucket scan and scatter, A/B)
+    static const char *list_env = std::getenv("GW_WCNN_LIST");
+    const bool fused_list = !(list_env && std::string(list_env) == "scan");
+    if (fused_list) {
         gwprof::Span span(env, GW_SPAN_CNN_L1);
+        const dim3 fgrid((unsigned)((src.E + LR_ENVS - 1) / LR_ENVS), src.K);
         switch (src.N) {
-            case 1: gwprof::launch(wcnn_l1_kernel<2>, lgrid, dim3(256), 0, s, cp, lists); break;
-            case 2: gwprof::launch(wcnn_l1_kernel<3>, lgrid, dim3(256), 0, s, cp, lists); break;
-            case 3: gwprof::launch(wcnn_l1_kernel<4>, lgrid, dim3(256), 0, s, cp, lists); break;
-            case 4: gwprof::launch(wcnn_l1_kernel<5>, lgrid, dim3(256), 0, s, cp, lists); break;
-            case 5: gwprof::launch(wcnn_l1_kernel<6>, lgrid, dim3(256), 0, s, cp, lists); break;
-            case 6: gwprof::launch(wcnn_l1_kernel<7>, lgrid, dim3(256), 0, s, cp, lists); break;
-            case 7: gwprof::launch(wcnn_l1_kernel<8>, lgrid, dim3(256), 0, s, cp, lists); break;
-            case 8: gwprof::launch(wcnn_l1_kernel<9>, lgrid, dim3(256), 0, s, cp, lists); break;
+            case 1: gwprof::launch(wcnn_list_kernel<2>, fgrid, dim3(256), 0, s, cp); break;
+            case 2: gwprof::launch(wcnn_list_kernel<3>, fgrid, dim3(256), 0, s, cp); break;
+            case 3: gwprof::launch(wcnn_list_kernel<4>, fgrid, dim3(256), 0, s, cp); break;
+            case 4: gwprof::launch(wcnn_list_kernel<5>, fgrid, dim3(256), 0, s, cp); break;
+            case 5: gwprof::launch(wcnn_list_kernel<6>, fgrid, dim3(256), 0, s, cp); break;
+            case 6: gwprof::launch(wcnn_list_kernel<7>, fgrid, dim3(256), 0, s, cp); break;
+            case 7: gwprof::launch(wcnn_list_kernel<8>, fgrid, dim3(256), 0, s, cp); break;
+            case 8: gwprof::launch(wcnn_list_kernel<9>, fgrid, dim3(256), 0, s, cp); break;
             default: return err(GW_ERR_ARG, "gw_patch_cnn_act: N out of range");
         }
-    }
-    if (src.K * cp.P > RARE_MAX_NB) return err(GW_ERR_ARG, "gw_patch_cnn_act: K x window positions above the rare kernels' table");
-    {
+    } else {
+        const Lists lists = lists_at(cp.ws.unit_off, src.K * cp.P, src.K, src.E, 256);
+        const dim3 lgrid((unsigned)lists.nblk, src.K);
+        {
+            gwprof::Span span(env, GW_SPAN_CNN_L1);
+            switch (src.N) {
+                case 1: gwprof::launch(wcnn_l1_kernel<2>, lgrid, dim3(256), 0, s, cp, lists); break;
+                case 2: gwprof::launch(wcnn_l1_kernel<3>, lgrid, dim3(256), 0, s, cp, lists); break;
+                case 3: gwprof::launch(wcnn_l1_kernel<4>, lgrid, dim3(256), 0, s, cp, lists); break;
+                case 4: gwprof::launch(wcnn_l1_kernel<5>, lgrid, dim3(256), 0, s, cp, lists); break;
+                case 5: gwprof::launch(wcnn_l1_kernel<6>, lgrid, dim3(256), 0, s, cp, lists); break;
+                case 6: gwprof::launch(wcnn_l1_kernel<7>, lgrid, dim3(256), 0, s, cp, lists); break;
+                case 7: gwprof::launch(wcnn_l1_kernel<8>, lgrid, dim3(256), 0, s, cp, lists); break;
+                case 8: gwprof::launch(wcnn_l1_kernel<9>, lgrid, dim3(256), 0, s, cp, lists); break;
+                default: return err(GW_ERR_ARG, "gw_patch_cnn_act: N out of range");
+            }
+        }
         gwprof::Span span(env, GW_SPAN_CNN_LIST);
         gwprof::launch(bucket_scan, dim3(src.K * cp.P), dim3(64), 0, s, cp, lists);
         gwprof::launch(wcnn_scatter, lgrid, dim3(256), 0, s, cp, lists);
@@ -2105,7 +2217,7 @@ gw_status gw_patch_cnn_act(void *env, int32_t P, const gw_cnn_actors *net, const
         }
     }
 #undef RARE
-    ActParams p;
+    ActParams p{};
     p.net = cnn_tail(net);
     p.c1 = cp.ws.mlp.c1;
     p.w2img = cp.ws.mlp.w2;
@@ -2130,6 +2242,8 @@ gw_status gw_patch_cnn_act(void *env, int32_t P, const gw_cnn_actors *net, const
     p.P = P;
     p.in_dim = P * P;
     p.tbl = cp.ws.table;
+    p.zero_n = cp.ws.bucket_n;  // the fused listing's bucket counters, read by the rare kernel above
+    p.zero_cnt = src.K * cp.P;
     p.variant = src.variant;
     p.training = training ? 1 : 0;
     p.tau = tau;

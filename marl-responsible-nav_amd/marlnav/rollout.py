@@ -447,13 +447,18 @@ class Rollout:
         counter from the ring's device step count, so replays draw fresh noise, and a replayed
         rollout equals the eager one bit for bit (tests/test_gpu_rollout_graph.py).
 
-        Requirements: the fused actor, a replay ring, full-grid obs, one rank, FeAR joined; the
-        env's obs synchronous, or async on the merged kernel path with n even after at least one
-        step; a ReturnGather (if any) with window == n and nothing pending.
+        Also the local-window rollouts (patch > 0: c5patch / c4patch), whose host enqueue per step
+        (the fused window actor's launches, the window writer, the env step) is about as long as
+        the step itself; with patch_async the window writer forks to its side stream inside the
+        graph and the graph's last writer joins before its end.
+
+        Requirements: the fused actor, a replay ring, one rank, FeAR joined; the env's obs
+        synchronous (or none: window rollouts), or async on the merged kernel path with n even
+        after at least one step; a ReturnGather (if any) with window == n and nothing pending.
         Nothing runs at capture: the state is untouched until the first replay."""
         env, rp = self.env, self.replay
-        if not (self.fused and rp is not None and not self.patch and not self.distributed and self._dev_counter()):
-            raise _lib.GwError("Rollout.capture: the fused actor, a replay ring, full-grid obs and one rank")
+        if not (self.fused and rp is not None and not self.distributed and self._dev_counter()):
+            raise _lib.GwError("Rollout.capture: the fused actor, a replay ring and one rank")
         if rp.S % n:
             raise _lib.GwError(f"Rollout.capture: n must divide the ring's {rp.S} slots")
         if env.obs_async and (env.kernel_path != "merged" or n % 2 or not env._obs_queued):
@@ -462,6 +467,7 @@ class Rollout:
         if g is not None and (g.window != n or g._fill != 0 or g.distributed):
             raise _lib.GwError("Rollout.capture: the gather needs window == n, no pending steps and one rank")
         self._flush()
+        self._patch_join()  # no side-stream writer from before the capture may be waited on inside it
         t0, rt0, calls0 = self.t, rp.t, self._calls
         start = env.pipeline_save()
         graphs, ends = [], []
@@ -473,6 +479,7 @@ class Rollout:
                     env.profile(False)
                     for _i in range(n):
                         self.step()
+                    self._patch_join()  # the graph's last window writer joins its stream
                 graphs.append(cg)
                 ends.append(env.pipeline_save())
         # nothing ran: the host-side state is the pre-capture one

@@ -113,3 +113,47 @@ def test_eager_rollout_matches_oracle(runs):
             np.testing.assert_array_equal(done[slot], np.array([x.done for x in o], np.uint8),
                                           err_msg=f"done at step {t}")
     np.testing.assert_array_equal(ring_obs[T % SLOTS], obs, err_msg="the last step's obs in the ring")
+
+
+@pytest.mark.parametrize("arch,scen,P,fear", [("cnn", "grid64_n8", 16, False), ("mlp", "grid32", 11, True)])
+def test_window_rollout_graph_equals_eager(arch, scen, P, fear):
+    """The local-window rollouts (bench c4patch: the configs/cnn.yaml head on 16 x 16 windows of the
+    64 x 64 / N = 8 grid, window writer on a side stream; c5patch: the MLP actors on 11 x 11
+    windows, FeAR on) replayed as ring-phase graphs == the same rollout stepped eagerly, bit for
+    bit (ring contents, env state, totals)."""
+    from marlnav.actor import MultiAgentActors
+    from marlnav.rollout import Rollout
+    En, slots, warm = 1024, 32, 3
+    steps = warm + (slots // G + 1) * G + 2
+    outs = []
+    for graph in (False, True):
+        env = VecGridEnv(scen, num_envs=En, fear=fear, fear_weight=-5.0, max_steps=40, auto_reset=True, seed=SEED,
+                         stats=True, obs=False)
+        actors = MultiAgentActors(env.K, P, P, arch=arch, device=env.device, seed=0)
+        ro = Rollout(env, actors, replay_slots=slots, training=True, seed=SEED, patch=P)
+        assert ro.fused
+        ro.reset()
+        t = 0
+        while t < steps:
+            if graph and t == warm:
+                graphs = ro.capture(G)
+            if graph and warm <= t and t + G <= steps - 2:
+                graphs.replay()
+                t += G
+                continue
+            ro.step()
+            t += 1
+        ro.fence()
+        rp = ro.replay
+        o = {n: getattr(rp, n).clone() for n in ("obs", "final_obs", "probs", "reward", "term", "done")}
+        o["state"] = env.state()
+        o["totals"] = ro.totals()
+        torch.cuda.synchronize()
+        env.close()
+        outs.append(o)
+    a, b = outs
+    for n in ("obs", "final_obs", "probs", "reward", "term", "done"):
+        assert torch.equal(a[n], b[n]), n
+    for n, v in a["state"].items():
+        assert torch.equal(v, b["state"][n]), n
+    assert a["totals"] == b["totals"]
