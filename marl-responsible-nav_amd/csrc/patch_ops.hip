@@ -405,181 +405,6 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a, unsign
     }
 }
 
-// The persistent writers (round 5; MODE 2: P % 4 == 0, MODE 4: the table copy, P * P <= 256):
-// a grid of resident blocks walks the chunks of PB envs; the NEXT chunk's descriptors are loaded
-// into registers right after this chunk's staging, so their round trip runs under this chunk's
-// stores instead of before each block's first store, and no partial second wave of short blocks
-// follows the first (profiles/r4_window: ~5-7 us of dependent staging per block, 2,048 blocks for
-// ~1,790 resident slots).  Staging, writers and terminal windows: window_kernel's, chunk by chunk.
-template <int MODE, int PB>
-__global__ void __launch_bounds__(THREADS) window_persist(gw::PatchArgs a, int nchunk) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const int tid = threadIdx.x, K = a.K, N = a.N, W = a.W, H = a.H, P = a.P;
-    const int PP = P * P, half = P / 2, np = N + 1, nroad = (a.H * a.W + 31) / 32;
-    const uint32_t a_wmagic = (uint32_t)((0x100000000ull + (uint64_t)W - 1) / (uint64_t)W);
-    uint32_t *s_road = lds;
-    uint32_t *s_flag = s_road + nroad;
-    int *s_ctr = reinterpret_cast<int *>(s_flag + PB);
-    int *s_pw = s_ctr + 2 * PB * K;
-    float *s_pv = reinterpret_cast<float *>(s_pw + 2 * PB * K * np);
-    uint16_t *s_seg = reinterpret_cast<uint16_t *>(s_pv + 2 * PB * K * np);
-    const int Q4 = PP / 4;
-    const int wave = tid >> 6, lane = tid & 63;
-    constexpr int ITEMS = (2 * PB * GW_MAX_AGENTS + THREADS - 1) / THREADS;
-    uint32_t fl[ITEMS], wd[ITEMS][4];
-    auto load = [&](int chunk) {
-        const int64_t e0 = (int64_t)chunk * PB;
-        const int nenv = (int)min((int64_t)PB, a.E - e0);
-#pragma unroll
-        for (int it = 0; it < ITEMS; ++it) {
-            const int t = tid + it * THREADS;
-            const int which = t / (PB * K), el = (t / K) % PB;
-            const bool ok = t < 2 * PB * K && el < nenv;
-            const uint32_t *d = a.desc + (e0 + (ok ? el : 0)) * NDESC;
-            fl[it] = ok ? d[4] : 0u;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) wd[it][i] = ok ? d[(which == 0 ? 0 : 8) + i] : 0u;
-        }
-    };
-    int chunk = blockIdx.x;
-    if (chunk < nchunk) load(chunk);
-    for (int w = tid; w < nroad; w += THREADS) s_road[w] = a.roadbits[w];
-    __syncthreads();
-    for (; chunk < nchunk; chunk += gridDim.x) {
-        const int64_t e0 = (int64_t)chunk * PB;
-        const int nenv = (int)min((int64_t)PB, a.E - e0);
-        int has_final = 0;
-#pragma unroll
-        for (int it = 0; it < ITEMS; ++it) {  // staging: thread = (which, env, agent)
-            const int t = tid + it * THREADS;
-            if (t >= 2 * PB * K) break;
-            const int which = t / (PB * K), el = (t / K) % PB, k = t % K;
-            const int slot = (which * PB + el) * K + k;
-            if (el < nenv) {
-                const uint32_t f = fl[it];
-                if (k == 0 && which == 0) s_flag[el] = f;
-                if (which == 1) has_final |= (f & D_FINAL) != 0;
-                if (which == 1 && !(f & D_FINAL)) continue;
-                const bool reset = which == 0 && (f & D_RESET);
-                const uint32_t apples = which == 0 ? (f >> 8) & 0xFFu : (f >> 16) & 0xFFu;
-                const int ac = ((apples >> k) & 1u) ? a.apples[k] : -1;
-                const int ctr = (int)((wd[it][k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
-                const int cr = (int)__umulhi((uint32_t)ctr, a_wmagic), cc = ctr - cr * W;
-                s_ctr[slot] = (cr << 16) | cc;
-                uint16_t *sg = s_seg + slot * Q4;
-                if (MODE == 2 && which == 0)
-                    for (int q = 0; q < Q4; q += 2) *reinterpret_cast<uint32_t *>(sg + q) = 0u;
-                int cell[MAXP];
-                float val[MAXP];
-                int u = 0;
-                if (ac >= 0) {
-                    float av = (((s_road[ac >> 5] >> (ac & 31)) & 1u) ? 0.0f : -1.0f) + 9.0f;
-                    if (!reset && av == (float)(k + 1)) av = 1.0f;
-                    cell[0] = ac;
-                    val[0] = av;
-                    u = 1;
-                }
-#pragma unroll
-                for (int n = 0; n < GW_MAX_AGENTS; ++n) {
-                    if (n >= N) break;
-                    const int c = (int)((wd[it][n >> 1] >> (16 * (n & 1))) & 0xFFFFu);
-                    cell[u] = c;
-                    val[u] = agent_value(reset, n, k, c == ac, a.variant);
-                    ++u;
-                }
-                for (int i = 0; i < np; ++i) {
-                    int pos = -1;
-                    if (i < u) {
-                        const int c = cell[i];
-                        const int rr = (int)__umulhi((uint32_t)c, a_wmagic);
-                        const int wr = rr - cr + half, wc = c - rr * W - cc + half;
-                        bool last = (unsigned)wr < (unsigned)P && (unsigned)wc < (unsigned)P;
-                        for (int j = i + 1; j < u; ++j) last = last && cell[j] != c;
-                        pos = last ? wr * P + wc : -1;
-                    }
-                    s_pw[slot * np + i] = pos;
-                    s_pv[slot * np + i] = i < u ? val[i] : 0.0f;
-                    if (MODE == 2 && which == 0 && pos >= 0) sg[pos >> 2] |= (uint16_t)((i + 1) << (4 * (pos & 3)));
-                }
-            }
-        }
-        const bool any_final = __syncthreads_or(has_final) != 0;  // (also the barrier after the staging)
-        if (chunk + (int)gridDim.x < nchunk) load(chunk + gridDim.x);  // in flight under the stores below
-        if (MODE == 2 && a.patch) {
-            const int P4 = P / 4, per_k = nenv * Q4, nroad1 = nroad - 1;
-            const uint32_t m_p4 = P4 > 1 ? (uint32_t)((0x100000000ull + (uint64_t)P4 - 1) / (uint64_t)P4) : 0u;
-            const uint32_t m_q4 = (uint32_t)((0x100000000ull + (uint64_t)Q4 - 1) / (uint64_t)Q4);
-            for (int k = 0; k < K; ++k) {
-                float4 *o4 = reinterpret_cast<float4 *>(a.patch + ((int64_t)k * a.E + e0) * PP);
-                for (int j = tid; j < per_k; j += THREADS) {
-                    const int el = (int)__umulhi((uint32_t)j, m_q4), q = j - el * Q4;
-                    if (!(s_flag[el] & D_WRITE)) continue;
-                    const int slot = el * K + k;
-                    const int ctr = s_ctr[slot];
-                    const int wr = P4 > 1 ? (int)__umulhi((uint32_t)q, m_p4) : q, wc = 4 * (q - wr * P4);
-                    const int row = (ctr >> 16) - half + wr, col0 = (ctr & 0xFFFF) - half + wc;
-                    const int cmin = max(col0, 0), cell = row * W + cmin;
-                    const bool in_row = (unsigned)row < (unsigned)H;
-                    const int w0 = in_row ? min(cell >> 5, nroad1) : 0;
-                    const uint64_t bits = (((uint64_t)s_road[min(w0 + 1, nroad1)] << 32) | s_road[w0]) >> (cell & 31);
-                    float v[4];
-#pragma unroll
-                    for (int uu = 0; uu < 4; ++uu) {
-                        const int col = col0 + uu;
-                        const bool road = in_row && (unsigned)col < (unsigned)W && ((bits >> (col - cmin)) & 1u);
-                        v[uu] = road ? 0.0f : -1.0f;
-                    }
-                    const uint32_t sgv = s_seg[slot * Q4 + q];
-                    if (sgv) {
-#pragma unroll
-                        for (int uu = 0; uu < 4; ++uu) {
-                            const uint32_t idx = (sgv >> (4 * uu)) & 0xFu;
-                            if (idx) v[uu] = s_pv[slot * np + (int)idx - 1];
-                        }
-                    }
-                    o4[j] = make_float4(v[0], v[1], v[2], v[3]);
-                }
-            }
-        } else if (MODE == 4 && a.patch) {
-            for (int k = 0; k < K; ++k) {
-                float *o = a.patch + ((int64_t)k * a.E + e0) * PP;
-                for (int el = wave; el < nenv; el += THREADS / 64) {
-                    if (!(s_flag[el] & D_WRITE)) continue;
-                    const int ctr = s_ctr[el * K + k];
-                    const float *src = a.tbl + (int64_t)((ctr >> 16) * W + (ctr & 0xFFFF)) * PP;
-                    float *dst = o + (int64_t)el * PP;
-                    for (int c = lane; c < PP; c += 64) dst[c] = src[c];
-                }
-            }
-            __builtin_amdgcn_s_waitcnt(0);
-            __syncthreads();
-            for (int t = tid; t < nenv * K * np; t += THREADS) {
-                const int slot = t / np, i = t - slot * np, el = slot / K, k = slot - el * K;
-                if (!(s_flag[el] & D_WRITE)) continue;
-                const int pw = s_pw[slot * np + i];
-                if (pw >= 0) a.patch[((int64_t)k * a.E + e0 + el) * PP + pw] = s_pv[slot * np + i];
-            }
-        }
-        if (a.final_patch && any_final) {
-            for (int wi = wave; wi < nenv * K; wi += THREADS / 64) {
-                const int el = wi / K, k = wi - el * K;
-                if (!(s_flag[el] & D_FINAL)) continue;
-                const int slot = (PB + el) * K + k;
-                const int ctr = s_ctr[slot], cr = ctr >> 16, cc = ctr & 0xFFFF;
-                float *o = a.final_patch + ((int64_t)k * a.E + e0 + el) * PP;
-                const float *trow = a.tbl ? a.tbl + (int64_t)(cr * W + cc) * PP : nullptr;
-                for (int c = lane; c < PP; c += 64) {
-                    float v = trow ? trow[c] : map_value(s_road, H, W, cr + c / P - half, cc + c % P - half);
-                    for (int u = 0; u < np; ++u)
-                        if (s_pw[slot * np + u] == c) v = s_pv[slot * np + u];
-                    o[c] = v;
-                }
-            }
-        }
-        __syncthreads();  // the chunk's LDS tables are read before the next chunk's staging
-    }
-}
-
 // MODE 4's table: tbl[c][o] = the map value under window position o of the window centred on
 // cell c (-1 outside the grid); built once per (env, P)
 __global__ void __launch_bounds__(256) window_table_kernel(gw::PatchArgs a, float *tbl) {
@@ -631,24 +456,6 @@ hipError_t launch_mode(const PatchArgs &a, size_t lds, hipStream_t s) {
         granted = lds;
     }
     const unsigned grid = (unsigned)((a.E + PB - 1) / PB);
-    // MODE 2 / 4 as persistent blocks (window_persist) of `per_cu` blocks per CU (GW_PATCH_PERSIST=n;
-    // 0: one block per chunk, the round-4 launch)
-    static const char *pe = std::getenv("GW_PATCH_PERSIST");
-    static const int per_cu = pe ? std::max(0, std::atoi(pe)) : 4;
-    if ((MODE == 2 || MODE == 4) && per_cu > 0 && !g_patch_dbg && a.probe == 0) {
-        static int ncu = 0;
-        if (!ncu && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) ncu = 256;
-        static size_t granted_p = 64 * 1024;
-        if (lds > granted_p) {
-            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&window_persist<MODE, PB>),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            if (e != hipSuccess) return e;
-            granted_p = lds;
-        }
-        const unsigned pgrid = std::min<unsigned>(grid, (unsigned)(per_cu * ncu));
-        gwprof::launch(window_persist<MODE, PB>, dim3(pgrid), dim3(THREADS), lds, s, a, (int)grid);
-        return hipGetLastError();
-    }
     gwprof::launch(window_kernel<MODE, PB>, dim3(grid), dim3(THREADS), lds, s, a, g_patch_dbg);
     return hipGetLastError();
 }
@@ -708,6 +515,7 @@ hipError_t launch_windows(const PatchArgs &args, hipStream_t s) {
         case 2: return launch_mode<2, 32>(a, lds, s);
         case 3: return launch_mode<3, 32>(a, lds, s);
         case 4: return launch_mode<4, 32>(a, lds, s);
+        case 5: return launch_mode<5, 32>(a, lds, s);
         default: return launch_mode<1, 32>(a, lds, s);
     }
 }
