@@ -1593,6 +1593,10 @@ __global__ void __launch_bounds__(256) dgrads_adam(DGrad p) {
                                                         ? GRG * HID * NA + GRG * (NA + 1)
                                                         : RB * (TILE_R + 4) + TILE_R * HID];
     static_assert(4 * DMAXB * NPM <= GRG * HID * NA, "the W1 blocks' entry lists fit the shared buffer");
+    // the W1 blocks' dZ1 rows of the agent (B <= DZR; beyond: read from global memory): a bucket of
+    // a cell every row patches (the own apple) walks all B rows, one dependent load each
+    constexpr int DZR = 128;
+    __shared__ __attribute__((aligned(16))) float s_dzr[DZR * HID];
     // the W1 blocks' entry lists (cell, row, delta) and per-cell buckets, in the shared buffer
     int *s_ec = reinterpret_cast<int *>(smem), *s_er = s_ec + DMAXB * NPM, *s_bk = s_er + DMAXB * NPM;
     float *s_ed = reinterpret_cast<float *>(s_bk + DMAXB * NPM);
@@ -1667,6 +1671,12 @@ __global__ void __launch_bounds__(256) dgrads_adam(DGrad p) {
             for (int t = 0; t < B / RB; ++t) acc += p.w.spart[((int64_t)k * (B / RB) + t) * HID + tid];
             s_S[tid] = acc;
         }
+        if (B <= DZR) {  // the agent's dZ1 rows into LDS (16 float4 loads per thread in flight)
+            const float4 *src = reinterpret_cast<const float4 *>(p.w.sv.dz1 + (int64_t)k * B * HID);
+            float4 *dst = reinterpret_cast<float4 *>(s_dzr);
+#pragma unroll 16
+            for (int i = tid; i < B * HID / 4; i += 256) dst[i] = src[i];
+        }
         // the patched cells of the rows' obs `obk` inside this group, in (row, slot) order
         const int obk = p.phase == 0 ? ob : k;
         const int NE = B * NPM, per = (NE + 255) / 256, t0 = tid * per;
@@ -1721,7 +1731,7 @@ __global__ void __launch_bounds__(256) dgrads_adam(DGrad p) {
         __syncthreads();
         // gradient = map * colsum(dZ1) + the cell's patched rows' terms (row order); Adam
         const float *wk = p.net.w1 + ((int64_t)k * in_dim + row0) * HID + j;
-        const float *dz1 = p.w.sv.dz1 + (int64_t)k * B * HID + j;
+        const float *dz1 = (B <= DZR ? s_dzr : p.w.sv.dz1 + (int64_t)k * B * HID) + j;
         float pp = 0.0f, tp = 0.0f;
         for (int u0 = 0; u0 < CG / 2; u0 += 16) {  // 16 cells per pass (h, h + 2, ...)
             int64_t off[16];
@@ -1764,7 +1774,16 @@ __global__ void __launch_bounds__(256) dgrads_adam(DGrad p) {
     if (type == 1) {  // the critic's action rows: dense, sum over the rows in order
         const int k = b, na = NA * K;
         const int j = tid & (HID - 1), h = tid >> 7;
-        const float *dz1 = p.w.sv.dz1 + (int64_t)k * B * HID + j;
+        if (B <= DZR) {
+            const float4 *src = reinterpret_cast<const float4 *>(p.w.sv.dz1 + (int64_t)k * B * HID);
+            float4 *dst = reinterpret_cast<float4 *>(s_dzr);
+#pragma unroll 16
+            for (int i = tid; i < B * HID / 4; i += 256) dst[i] = src[i];
+        }
+        float *s_a = smem;  // the rows' stored actions [B][9K] (<= 256 x 72 floats)
+        for (int i = tid; i < B * na; i += 256) s_a[i] = p.w.act[i];
+        __syncthreads();
+        const float *dz1 = (B <= DZR ? s_dzr : p.w.sv.dz1 + (int64_t)k * B * HID) + j;
         for (int a0 = h; a0 < na; a0 += 16) {  // 8 action rows of this thread per pass
             float acc[8];
 #pragma unroll
@@ -1772,7 +1791,7 @@ __global__ void __launch_bounds__(256) dgrads_adam(DGrad p) {
 #pragma unroll 8
             for (int rr = 0; rr < B; ++rr) {
                 const float d = dz1[(int64_t)rr * HID];
-                const float *av = p.w.act + (int64_t)rr * na;
+                const float *av = s_a + rr * na;
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
                     const int a = a0 + 2 * u;

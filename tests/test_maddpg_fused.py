@@ -9,7 +9,8 @@ autograd's (measured: 2e-7 .. 6e-7, profiles/r3_learner), the losses within 1e-4
 target actions (x_next's slots) within 2e-6.  The bound is that tight because no ReLU input of
 the batch lies within 1e-5 of zero (asserted from a float64 forward of every network the update
 evaluates): a ReLU at the f32 rounding edge of its LayerNorm could take the other side in one of
-the two and move one row's contribution by far more than rounding.  A negative check shows the
+the two and move one row's contribution by far more than rounding; such rows are masked (replaced
+by a copy of a clean row of the batch, at most 2 of 128) before the comparison.  A negative check shows the
 bound bites: scaling any single gradient tensor by (1 + 1e-4) fails it.  (2) Four updates
 against the per-agent loop: losses within 1e-4 relative, every parameter tensor within 1e-5
 relative L2 (measured worst 3.2e-7).  (3) A HIP-graph replay of the fused update equals the eager
@@ -70,9 +71,10 @@ EDGE = 1e-5      # a ReLU input this close to 0 could flip between two f32 summa
 
 def _relu_margin(net, x):
     """min |ReLU input| over the hidden layers of ``net`` on inputs x [K, B, in] (float64 forward:
-    Linear -> LayerNorm(eps 1e-5) -> affine), and how many inputs lie within EDGE of zero."""
+    Linear -> LayerNorm(eps 1e-5) -> affine), and the rows [B] (bool) with an input within EDGE
+    of zero."""
     h = x.double()
-    lo, near = float("inf"), 0
+    lo, rows = float("inf"), torch.zeros(x.shape[1], dtype=torch.bool, device=x.device)
     with torch.no_grad():
         for i in range(net.n_layers - 1):
             z = torch.baddbmm(net.biases[i].double(), h, net.weights[i].double())
@@ -80,9 +82,31 @@ def _relu_margin(net, x):
             a = (z - mu) / torch.sqrt(((z - mu) ** 2).mean(-1, keepdim=True) + 1e-5) * net.ln_w[i].double() + \
                 net.ln_b[i].double()
             lo = min(lo, float(a.abs().min()))
-            near += int((a.abs() < EDGE).sum())
+            rows |= (a.abs() < EDGE).any(-1).any(0)
             h = torch.relu(a)
-    return lo, near
+    return lo, rows
+
+
+def _edge_rows(ref, st, ac, ns, un, uc, critic_after=None):
+    """Rows of the batch where a network the update evaluates has a ReLU input within EDGE of zero:
+    autograd's target actors, target critic, critic and actor before the update, and the critic
+    after its Adam step (``critic_after``: the actor phase evaluates it on the mixed actions)."""
+    from marlnav.maddpg import gumbel_softmax
+    x = ref._critic_in(st, ac)
+    with torch.no_grad():
+        xt = ref._critic_in(ns, gumbel_softmax(ref.actor_targets(ns), un))
+        probs = gumbel_softmax(ref.actors(st), uc)
+        xmix = x.unsqueeze(0).repeat(K, 1, 1)
+        for k in range(K):
+            xmix[k, :, K * H * W + 9 * k: K * H * W + 9 * (k + 1)] = probs[k]
+    checks = [(ref.actor_targets.net, ns.reshape(K, B, -1)), (ref.critic_targets, xt.unsqueeze(0).expand(K, -1, -1)),
+              (ref.critics, x.unsqueeze(0).expand(K, -1, -1)), (ref.actors.net, st.reshape(K, B, -1)),
+              (critic_after if critic_after is not None else ref.critics, xmix)]
+    res = [_relu_margin(net, xi) for net, xi in checks]
+    rows = torch.zeros(B, dtype=torch.bool, device=st.device)
+    for _, r in res:
+        rows |= r
+    return rows, [m for m, _ in res]
 
 
 def _grad_failures(got, want):
@@ -90,41 +114,52 @@ def _grad_failures(got, want):
     return [i for i, (a, b) in enumerate(zip(got, want)) if _rel(a, b) >= GRAD_TOL]
 
 
-def test_fused_gradients_match_autograd():
+def _run_update(batch):
+    """One update of a fresh (fused, autograd) pair on `batch`; the gradients and losses of both."""
+    st, ac, rw, ns, dn, un, uc = batch
     ms = _pair()
-    g = torch.Generator(device="cuda").manual_seed(7)
-    st, ac, rw, ns, dn, un, uc = _batch(g)
     x = ms[1]._critic_in(st, ac).contiguous()
     xn = [ms[1]._critic_in(ns, torch.zeros_like(ac)).contiguous() for _ in range(2)]
-    # every ReLU input the update evaluates (autograd's networks before the update, float64): none
-    # within EDGE of zero, so no row can flip between the two summation orders
-    from marlnav.maddpg import gumbel_softmax
-    ref = ms[1]
-    with torch.no_grad():
-        xt = xn[1].clone()
-        xt[:, K * H * W:] = gumbel_softmax(ref.actor_targets(ns), un).permute(1, 0, 2).reshape(B, -1)
-        probs = gumbel_softmax(ref.actors(st), uc)
-        xmix = x.unsqueeze(0).repeat(K, 1, 1)
-        for k in range(K):
-            xmix[k, :, K * H * W + 9 * k: K * H * W + 9 * (k + 1)] = probs[k]
-    checks = [(ref.actor_targets.net, ns.reshape(K, B, -1)), (ref.critic_targets, xt.unsqueeze(0).expand(K, -1, -1)),
-              (ref.critics, x.unsqueeze(0).expand(K, -1, -1)), (ref.actors.net, st.reshape(K, B, -1)),
-              (ref.critics, xmix)]
-    near = [_relu_margin(net, xi) for net, xi in checks]
-    print("ReLU input margins (min |a|, near-edge count):", near)
-    assert sum(n for _, n in near) == 0, near
     ctx = [m._learn_critic(st, ac, rw, ns, dn, un, (x.clone(), xn[i])) for i, m in enumerate(ms)]
+    gc = (_grads(ms[0].critics), _grads(ms[1].critics))
+    for i, m in enumerate(ms):
+        m._learn_actor(ctx[i], uc)
+    ga = (_grads(ms[0].actors.net), _grads(ms[1].actors.net))
+    return ms, ctx, xn, gc, ga
+
+
+def test_fused_gradients_match_autograd():
+    g = torch.Generator(device="cuda").manual_seed(7)
+    batch = list(_batch(g))
+    st, ac, rw, ns, dn, un, uc = batch
+    # every ReLU input the update evaluates (autograd's networks, float64): rows with one within
+    # EDGE of zero could flip between the two summation orders -- mask them (a copy of a clean row;
+    # the critic's Adam step depends on every row, so the check repeats after a mask) and require
+    # that they are few
+    masked = []
+    for _ in range(4):
+        ms, ctx, xn, gc, ga = _run_update(batch)
+        st, ac, rw, ns, dn, un, uc = batch
+        rows, margins = _edge_rows(_pair()[1], st, ac, ns, un, uc, critic_after=ms[1].critics)
+        print("ReLU input margins per network:", margins, "edge rows:", rows.nonzero().flatten().tolist())
+        if not rows.any():
+            break
+        clean = int((~rows).nonzero()[0])
+        batch = [t.clone() for t in batch]
+        st, ac, rw, ns, dn, un, uc = batch
+        for b in rows.nonzero().flatten().tolist():
+            masked.append(b)
+            for t in (st, ac, ns, un, uc):
+                t[:, b] = t[:, clean]
+            rw[b], dn[b] = rw[clean], dn[clean]
+    assert not rows.any() and len(masked) <= 3, masked
     D = K * H * W
     torch.testing.assert_close(xn[0][:, D:], xn[1][:, D:], rtol=0, atol=2e-6)       # target actions
     torch.testing.assert_close(ctx[0]["critic_loss"], ctx[1]["critic_loss"], rtol=1e-4, atol=1e-6)
-    gc = (_grads(ms[0].critics), _grads(ms[1].critics))
-    print("critic grad rel L2:", ["%.1e" % _rel(a, b) for a, b in zip(*gc)])
-    assert not _grad_failures(*gc)
-    for i, m in enumerate(ms):
-        m._learn_actor(ctx[i], uc)
     torch.testing.assert_close(ctx[0]["actor_loss"], ctx[1]["actor_loss"], rtol=1e-4, atol=1e-6)
-    ga = (_grads(ms[0].actors.net), _grads(ms[1].actors.net))
+    print("critic grad rel L2:", ["%.1e" % _rel(a, b) for a, b in zip(*gc)])
     print("actor grad rel L2:", ["%.1e" % _rel(a, b) for a, b in zip(*ga)])
+    assert not _grad_failures(*gc)
     assert not _grad_failures(*ga)
     # the bound bites: any single tensor perturbed by 1e-4 relative fails it
     for got, want in (gc, ga):
