@@ -29,6 +29,8 @@
 #include <cstdlib>
 #include <initializer_list>
 #include <string>
+#include <vector>
+#include <cstdio>
 
 #include "learner_ops.h"
 #include "philox.h"
@@ -184,11 +186,19 @@ __global__ void __launch_bounds__(256) l1_reduce(ReduceParams p) {
 }
 
 // ---- per-row helpers (a row = 16 lanes, lane g holds features 8 g .. 8 g + 7) ---------------------
-__device__ __forceinline__ float row_sum(float v) {  // over the row's 16 lanes
-    v += __shfl_xor(v, 1, 64);
-    v += __shfl_xor(v, 2, 64);
-    v += __shfl_xor(v, 4, 64);
-    v += __shfl_xor(v, 8, 64);
+// v from the lane the DPP control names (within the lane's 16-lane row)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+// over the row's 16 lanes, a butterfly on DPP lane moves (VALU, no LDS round trip): pairs (xor 1),
+// quads (xor 2), half rows (mirror within 8) and rows (mirror within 16); every lane ends with the
+// same sum (each step adds two equal-valued partials in either order), the xor butterfly's values
+__device__ __forceinline__ float row_sum(float v) {
+    v += dpp_f<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+    v += dpp_f<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+    v += dpp_f<0x141>(v);  // row_half_mirror
+    v += dpp_f<0x140>(v);  // row_mirror
     return v;
 }
 
@@ -1006,16 +1016,29 @@ __device__ __forceinline__ void d_gumbel(const float lg[NA], const float ur[NA],
     for (int a = 0; a < NA; ++a) pr[a] = pr[a] / sum;
 }
 
-// z (lane g's 8 features) += the patched cells' terms: W1 rows row0 + cell
+// z (lane g's 8 features) += the patched cells' terms (in list order): W1 rows row0 + cell.  The
+// NPM slots' loads are all issued at once (slots past np re-read slot 0's row and are skipped):
+// one round trip, not one per slot
 __device__ __forceinline__ void d_add_patches(float z[8], const float *w1, int64_t row0, const int16_t *pc,
                                               const float *pd, int np, int g) {
-#pragma unroll 3
-    for (int i = 0; i < np; ++i) {
-        const float dv = pd[i];
-        const float *wr = w1 + (row0 + pc[i]) * HID + 8 * g;
-        const float4 a = *reinterpret_cast<const float4 *>(wr), b = *reinterpret_cast<const float4 *>(wr + 4);
-        z[0] = fmaf(dv, a.x, z[0]); z[1] = fmaf(dv, a.y, z[1]); z[2] = fmaf(dv, a.z, z[2]); z[3] = fmaf(dv, a.w, z[3]);
-        z[4] = fmaf(dv, b.x, z[4]); z[5] = fmaf(dv, b.y, z[5]); z[6] = fmaf(dv, b.z, z[6]); z[7] = fmaf(dv, b.w, z[7]);
+    float4 a[NPM], b[NPM];
+    float dv[NPM];
+#pragma unroll
+    for (int i = 0; i < NPM; ++i) {
+        const int ii = i < np ? i : 0;
+        dv[i] = pd[ii];
+        const float *wr = w1 + (row0 + pc[ii]) * HID + 8 * g;
+        a[i] = *reinterpret_cast<const float4 *>(wr);
+        b[i] = *reinterpret_cast<const float4 *>(wr + 4);
+    }
+#pragma unroll
+    for (int i = 0; i < NPM; ++i) {
+        if (i < np) {
+            z[0] = fmaf(dv[i], a[i].x, z[0]); z[1] = fmaf(dv[i], a[i].y, z[1]);
+            z[2] = fmaf(dv[i], a[i].z, z[2]); z[3] = fmaf(dv[i], a[i].w, z[3]);
+            z[4] = fmaf(dv[i], b[i].x, z[4]); z[5] = fmaf(dv[i], b[i].y, z[5]);
+            z[6] = fmaf(dv[i], b[i].z, z[6]); z[7] = fmaf(dv[i], b[i].w, z[7]);
+        }
     }
 }
 
@@ -1108,7 +1131,17 @@ __device__ __forceinline__ Mlp staged(Mlp m, const float *sp, int out) {
     return m;
 }
 
+// GW_LEARN_STAMP=<file> (diagnostics): each block's thread 0 writes wall_clock64() stamps at its
+// phase boundaries into slots [block][0..14] (slot 15: the block type); the host appends them to <file>
+constexpr int NSTAMP = 16;
+#define DSTAMP(P, i)                                                                                   \
+    do {                                                                                               \
+        if ((P).stamp && threadIdx.x == 0)                                                             \
+            (P).stamp[(int64_t)(blockIdx.y * gridDim.x + blockIdx.x) * NSTAMP + (i)] = wall_clock64(); \
+    } while (0)
+
 struct DTail {
+    unsigned long long *stamp;
     DQ q;
     DWs w;
     gw_mlp_actors at, ct, c, a;  // actor target, critic target, critic, actor
@@ -1134,6 +1167,7 @@ __global__ void __launch_bounds__(DT) dcritic_tail(DTail p) {
     const int64_t E = p.q.E;
     const int in_c = K * HW + NA * K;
     const bool rec = k == 0;  // the k = 0 blocks record the rows for the later launches
+    DSTAMP(p, 0);
     // prologue: every independent load first (the ring's step count, this thread's share of the
     // small parameters), then the roles -- waves 0-3 the rows' descriptors, waves 4-7 the stored
     // probabilities, rewards and c1 sums -- whose round trips overlap; the parameters reach LDS last
@@ -1232,6 +1266,7 @@ __global__ void __launch_bounds__(DT) dcritic_tail(DTail p) {
     for (int o = tid + NSV * DT; o < tot; o += DT) *par_dst(o) = par_src(o);
     if (blockIdx.x == 0 && k == 0 && tid == 0) p.w.snap[0] = p.count[0] + 1;
     __syncthreads();
+    DSTAMP(p, 1);
     // the target actions a'_kk = GumbelSoftmax(actor_target_kk(s'_kk)), two agents at a time (a
     // group without an agent in the last round recomputes agent K - 1 and discards it)
     for (int rd = 0; rd < (K + 1) / 2; ++rd) {
@@ -1261,6 +1296,7 @@ __global__ void __launch_bounds__(DT) dcritic_tail(DTail p) {
         }
     }
     __syncthreads();
+    DSTAMP(p, 2);
     // group 0: the target critic on (s', a'); group 1: the online critic on (s, a)
     RowFwd f;
     float out[NA];
@@ -1279,6 +1315,7 @@ __global__ void __launch_bounds__(DT) dcritic_tail(DTail p) {
     // y = f32(r) + ((1 - d) * gamma) * q_next (gw_td_target's op order)
     if (grp == 0 && g == 0) s_y[rl] = s_rw[rl] + (s_t1[rl] * p.gamma) * out[0];
     __syncthreads();
+    DSTAMP(p, 3);
     const Mlp m = staged(mlp_k(p.c, k, in_c, 1), s_par[K + 1], 1);
     float gy[8], gv1[8], dz1[8], gv2[8], dz2[8], dq = 0.0f, diff = 0.0f;
     if (grp == 1) {
@@ -1293,6 +1330,7 @@ __global__ void __launch_bounds__(DT) dcritic_tail(DTail p) {
     __syncthreads();
     gemv_all(s_in[1], m.w2, true, s_out[1]);
     __syncthreads();
+    DSTAMP(p, 4);
     if (grp == 1) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) gy[i] = s_out[1][rl * HP + 8 * g + i];
@@ -1319,6 +1357,7 @@ __global__ void __launch_bounds__(DT) dcritic_tail(DTail p) {
         for (int rr = 0; rr < RB; ++rr) acc += s_in[1][rr * HP + tid];
         p.w.spart[((int64_t)k * (B / RB) + blockIdx.x) * HID + tid] = acc;
     }
+    DSTAMP(p, 5);
 }
 
 __global__ void __launch_bounds__(DT) dactor_tail(DTail p) {
@@ -1335,6 +1374,7 @@ __global__ void __launch_bounds__(DT) dactor_tail(DTail p) {
     const int K = p.K, B = p.B, HW = p.q.HW, r0 = blockIdx.x * RB, r = r0 + rl;
     const int in_c = K * HW + NA * K;
     const bool own = grp == 0;  // the row layout's owners; group 1 joins the 128 x 128 layers
+    DSTAMP(p, 0);
     // prologue: this thread's share of the small parameters (loads issued first), the c1 sums and
     // the recorded rows (their round trips overlap), then the parameters into LDS
     const int na_ = stage_size(NA), nc_ = stage_size(1), tot = na_ + nc_ + NA * HID;
@@ -1382,6 +1422,7 @@ __global__ void __launch_bounds__(DT) dactor_tail(DTail p) {
     for (int o = tid + NSV * DT; o < tot; o += DT) *par_dst(o) = par_src(o);
     if (blockIdx.x == 0 && k == 0 && tid == 0) p.w.snap[1] = p.count[0] + 1;
     __syncthreads();
+    DSTAMP(p, 1);
     const Mlp ma = staged(mlp_k(p.a, k, HW, NA), s_par[0], NA);
     const Mlp mc = staged(mlp_k(p.c, k, in_c, 1), s_par[1], 1);
     RowFwd fa, fc;
@@ -1394,6 +1435,7 @@ __global__ void __launch_bounds__(DT) dactor_tail(DTail p) {
         ln_relu(z, ma.lw1, ma.lb1, g, fa.xh1, fa.y1, fa.rs1);
     }
     rows_gemv_all(own, fa.y1, rl, g, ma.w2, false, s_in, s_out, z);
+    DSTAMP(p, 2);
     if (own) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) z[i] += ma.b2[8 * g + i];
@@ -1406,8 +1448,10 @@ __global__ void __launch_bounds__(DT) dactor_tail(DTail p) {
             for (int i = 0; i < 8; ++i) s = fmaf(fa.y2[i], ma.w3[(8 * g + i) * NA + a], s);
             lg[a] = row_sum(s) + ma.b3[a];
         }
+        DSTAMP(p, 6);
         d_gumbel_u(p.seed, c, 1, k, r, ur);
         d_gumbel(lg, ur, pr);
+        DSTAMP(p, 7);
         if (g == 0) {
 #pragma unroll
             for (int a = 0; a < NA; ++a) {
@@ -1421,10 +1465,13 @@ __global__ void __launch_bounds__(DT) dactor_tail(DTail p) {
         for (int i = 0; i < 8; ++i) z[i] = s_c1[1][8 * g + i];
         for (int kk = 0; kk < K; ++kk)
             d_add_patches(z, mc.w1, (int64_t)kk * HW, s_pc[rl][kk], s_pd[rl][kk], s_np[rl][kk], g);
+        DSTAMP(p, 8);
         d_add_actions(z, mc.w1, (int64_t)K * HW, s_act[rl], NA * K, g);
+        DSTAMP(p, 9);
         ln_relu(z, mc.lw1, mc.lb1, g, fc.xh1, fc.y1, fc.rs1);
     }
     rows_gemv_all(own, fc.y1, rl, g, mc.w2, false, s_in, s_out, z);
+    DSTAMP(p, 3);
     float q = 0.0f, gy[8], gv1[8], dz1[8], gv2[8], dz2[8];
     const float dq = -(1.0f / (float)B);  // -mean Q backward (gw_mean_loss_bwd mode 1)
     if (own) {
@@ -1439,7 +1486,9 @@ __global__ void __launch_bounds__(DT) dactor_tail(DTail p) {
         for (int i = 0; i < 8; ++i) gy[i] = dq * mc.w3[8 * g + i];
         ln_relu_bwd(gy, fc.y2, fc.xh2, fc.rs2, mc.lw2, g, gv2, dz2);
     }
+    DSTAMP(p, 10);
     rows_gemv_all(own, dz2, rl, g, mc.w2, true, s_in, s_out, gy);
+    DSTAMP(p, 11);
     float dl[NA];
     if (own) {
         ln_relu_bwd(gy, fc.y1, fc.xh1, fc.rs1, mc.lw1, g, gv1, dz1);
@@ -1467,6 +1516,7 @@ __global__ void __launch_bounds__(DT) dactor_tail(DTail p) {
         }
         ln_relu_bwd(gy, fa.y2, fa.xh2, fa.rs2, ma.lw2, g, gv2, dz2);
     }
+    DSTAMP(p, 4);
     rows_gemv_all(own, dz2, rl, g, ma.w2, true, s_in, s_out, gy);
     if (own) {
         ln_relu_bwd(gy, fa.y1, fa.xh1, fa.rs1, ma.lw1, g, gv1, dz1);
@@ -1493,10 +1543,12 @@ __global__ void __launch_bounds__(DT) dactor_tail(DTail p) {
         for (int rr = 0; rr < RB; ++rr) acc += s_in[rr * HP + tid];
         p.w.spart[((int64_t)k * (B / RB) + blockIdx.x) * HID + tid] = acc;
     }
+    DSTAMP(p, 5);
 }
 
 // ---- the parameter gradients with each element's Adam step ------------------------------------
 struct DGrad {
+    unsigned long long *stamp;
     DWs w;
     const float *base;
     gw_mlp_actors net;           // the network stepped (critic: phase 0, actor: phase 1)
@@ -1519,37 +1571,41 @@ struct AdamSc {
 };
 
 // NB elements' Adam steps with every load issued before the first store (a loop of element-wise
-// steps would serialise: its stores may alias the next element's loads); the first nv entries are valid.
-// soft: also the actor target's soft update at the same offsets (ti = the new target values)
+// steps would serialise: its stores may alias the next element's loads).  Every offset must be a
+// valid element (callers point unused entries at a used one): the loads are unconditional, only
+// the first nv entries are computed into the stores.  soft: also the actor target's soft update at
+// the same offsets (ti = the new target values).  adam_load may run well before adam_store (the
+// operands do not depend on the gradient).
 template <int NB>
-__device__ __forceinline__ void adam_n(const DGrad &p, const AdamSc &a, const int64_t (&off)[NB], const float (&gi)[NB],
-                                       int nv, bool soft, float (&pi)[NB], float (&ti)[NB]) {
+struct AdamIn {
+    float m[NB], v[NB], p[NB], t[NB];
+};
+template <int NB>
+__device__ __forceinline__ void adam_load(const DGrad &p, const int64_t (&off)[NB], bool soft, AdamIn<NB> &in) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        in.m[i] = p.m0[off[i]];
+        in.v[i] = p.v0[off[i]];
+        in.p[i] = p.p0[off[i]];
+        in.t[i] = soft ? p.t0[off[i]] : 0.0f;
+    }
+}
+template <int NB>
+__device__ __forceinline__ void adam_store(const DGrad &p, const AdamSc &a, const int64_t (&off)[NB], const float (&gi)[NB],
+                                           int nv, bool soft, const AdamIn<NB> &in, float (&pi)[NB], float (&ti)[NB]) {
     float *__restrict__ P = p.p0;
     float *__restrict__ G = p.g0;
     float *__restrict__ M = p.m0;
     float *__restrict__ V = p.v0;
     float *__restrict__ T = p.t0;
-    float mo[NB], vo[NB], po[NB], to[NB];
+    float mo[NB], vo[NB];
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-        if (i < nv) {
-            mo[i] = M[off[i]];
-            vo[i] = V[off[i]];
-            po[i] = P[off[i]];
-            to[i] = soft ? T[off[i]] : 0.0f;
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-        if (i < nv) {
-            const float mi = __fmaf_rn(a.w1, gi[i] - mo[i], mo[i]);
-            const float vi = __fmaf_rn(a.w2 * gi[i], gi[i], vo[i] * a.b2);
-            const float denom = sqrtf(vi) / a.bc2 + a.e;
-            pi[i] = __fmaf_rn(-a.step_size, mi / denom, po[i]);
-            mo[i] = mi;
-            vo[i] = vi;
-            if (soft) ti[i] = p.tau * pi[i] + (1.0f - p.tau) * to[i];
-        }
+        mo[i] = __fmaf_rn(a.w1, gi[i] - in.m[i], in.m[i]);
+        vo[i] = __fmaf_rn(a.w2 * gi[i], gi[i], in.v[i] * a.b2);
+        const float denom = sqrtf(vo[i]) / a.bc2 + a.e;
+        pi[i] = __fmaf_rn(-a.step_size, mo[i] / denom, in.p[i]);
+        ti[i] = soft ? p.tau * pi[i] + (1.0f - p.tau) * in.t[i] : 0.0f;
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
@@ -1562,48 +1618,56 @@ __device__ __forceinline__ void adam_n(const DGrad &p, const AdamSc &a, const in
         }
     }
 }
-
-// block exclusive prefix (thread order) of v over 256 threads; total returned in `total`
-__device__ __forceinline__ int d_excl_scan256(int v, int *red, int &total) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    int incl = v;
-    for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += t;
-    }
-    __syncthreads();
-    if (lane == 63) red[wave] = incl;
-    __syncthreads();
-    int before = 0;
-    total = 0;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        const int x = red[w];
-        if (w < wave) before += x;
-        total += x;
-    }
-    return before + incl - v;
+template <int NB>
+__device__ __forceinline__ void adam_n(const DGrad &p, const AdamSc &a, const int64_t (&off)[NB], const float (&gi)[NB],
+                                       int nv, bool soft, float (&pi)[NB], float (&ti)[NB]) {
+    AdamIn<NB> in;
+    adam_load(p, off, soft, in);
+    adam_store(p, a, off, gi, nv, soft, in, pi, ti);
 }
 
-__global__ void __launch_bounds__(256) dgrads_adam(DGrad p) {
-    __shared__ float s_S[HID], s_base[CG], s_pp[2][2][HID];
-    __shared__ int s_cnt[CG + 1], s_red[4];
+// n4 (<= 16 x 256) float4 of global HID-float rows into LDS rows of HID + 4 floats (bank-spread
+// row starts): every load in flight before the first store (d_stage_load may run well before
+// d_stage_store)
+__device__ __forceinline__ void d_stage_load(float4 (&v)[16], const float *src, int n4) {
+    const float4 *s4 = reinterpret_cast<const float4 *>(src);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        const int i = threadIdx.x + u * 256;
+        v[u] = s4[i < n4 ? i : 0];  // a clamped index, not a predicated load: v stays in registers
+    }
+}
+__device__ __forceinline__ void d_stage_store(float *dst, const float4 (&v)[16], int n4) {
+    float4 *d4 = reinterpret_cast<float4 *>(dst);
+    constexpr int R4 = HID / 4;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        const int i = threadIdx.x + u * 256;
+        if (i < n4) d4[(i / R4) * (R4 + 1) + i % R4] = v[u];
+    }
+}
+__device__ __forceinline__ void d_stage_rows(float *dst, const float *src, int n4) {
+    float4 v[16];
+    d_stage_load(v, src, n4);
+    d_stage_store(dst, v, n4);
+}
+
+__device__ __forceinline__ void dgrads_body(const DGrad &p) {
+    __shared__ float s_base[CG], s_pp[2][2][HID];
     __shared__ float s_sc[2];
     __shared__ __attribute__((aligned(16))) float smem[GRG * HID * NA + GRG * (NA + 1) > RB * (TILE_R + 4) + TILE_R * HID
                                                         ? GRG * HID * NA + GRG * (NA + 1)
                                                         : RB * (TILE_R + 4) + TILE_R * HID];
-    static_assert(4 * DMAXB * NPM <= GRG * HID * NA, "the W1 blocks' entry lists fit the shared buffer");
-    // the W1 blocks' dZ1 rows of the agent (B <= DZR; beyond: read from global memory): a bucket of
-    // a cell every row patches (the own apple) walks all B rows, one dependent load each
-    constexpr int DZR = 128;
-    __shared__ __attribute__((aligned(16))) float s_dzr[DZR * HID];
-    // the W1 blocks' entry lists (cell, row, delta) and per-cell buckets, in the shared buffer
-    int *s_ec = reinterpret_cast<int *>(smem), *s_er = s_ec + DMAXB * NPM, *s_bk = s_er + DMAXB * NPM;
-    float *s_ed = reinterpret_cast<float *>(s_bk + DMAXB * NPM);
+    // the W1 and action-row blocks: dZ1 of the agent in chunks of DZR rows [DZR][DZP] (the W1
+    // blocks' G [CG][HID] replaces it), X [B][XP] / the stored actions [B][9K] in the shared buffer
+    constexpr int DZR = 128, XP = CG + 4, DZP = HID + 4;
+    __shared__ __attribute__((aligned(16))) float s_dzr[DZR * DZP];
+    static_assert(DMAXB * XP <= sizeof(smem) / sizeof(float), "X fits the shared buffer");
     const int tid = threadIdx.x, K = p.K, B = p.B, HW = p.HW, NG = p.NG;
     int b = blockIdx.x, type = 0;
     while (type < 6 && b >= p.start[type + 1]) ++type;
     b -= p.start[type];
+    if (p.stamp && tid == 0) p.stamp[(int64_t)blockIdx.x * NSTAMP + NSTAMP - 1] = (unsigned long long)type;
     // this step's Adam scalars (the count the tail snapshotted; torch forms them in double)
     if (tid == 0) {
         const double s = (double)p.w.snap[p.phase];
@@ -1632,134 +1696,142 @@ __global__ void __launch_bounds__(256) dgrads_adam(DGrad p) {
         const int in_dim = type == 5 ? K * HW + NA * K : p.in_dim;
         const int64_t row0 = critic ? (int64_t)ob * HW + c0 : c0;  // W1 input row of cell c0
         if (tid < ncell) s_base[tid] = p.base[c0 + tid];
+        // this thread's cells h + 2 u (u < 32), two passes of 16: nvp[ps] exist in pass ps; the
+        // others are clamped to the group's last cell (their loads valid, their results unused)
+        const int ncl = ncell > h ? (ncell - h + 1) / 2 : 0;
+        const int nvp0 = min(ncl, 16), nvp1 = max(0, min(ncl - 16, 16));
+        auto cell = [&](int ps, int u) { return min(h + 2 * (16 * ps + u), ncell - 1); };
         if (type == 5) {
-            __syncthreads();
-            float tp = 0.0f;
             const float *cw = p.cnet.w1 + ((int64_t)k * in_dim + row0) * HID + j;
             const float *__restrict__ CP = p.cp0;
             float *__restrict__ CT = p.ct0;
-            for (int u0 = 0; u0 < CG / 2; u0 += 16) {  // 16 cells' loads in flight, then the stores
-                float pv[16], tv[16];
+            float pv[2][16], tv[2][16];  // both passes' loads in flight, then the stores
+#pragma unroll
+            for (int ps = 0; ps < 2; ++ps)
 #pragma unroll
                 for (int u = 0; u < 16; ++u) {
-                    const int cc = h + 2 * (u0 + u);
-                    if (cc < ncell) {
-                        const int64_t off = (cw + (int64_t)cc * HID) - p.cp0;
-                        pv[u] = CP[off];
-                        tv[u] = CT[off];
-                    }
+                    const int64_t off = (cw + (int64_t)cell(ps, u) * HID) - p.cp0;
+                    pv[ps][u] = CP[off];
+                    tv[ps][u] = CT[off];
                 }
+            __syncthreads();  // s_base
+            float tp = 0.0f;
+#pragma unroll
+            for (int ps = 0; ps < 2; ++ps)
 #pragma unroll
                 for (int u = 0; u < 16; ++u) {
-                    const int cc = h + 2 * (u0 + u);
-                    if (cc < ncell) {
-                        const int64_t off = (cw + (int64_t)cc * HID) - p.cp0;
-                        const float ti = p.tau * pv[u] + (1.0f - p.tau) * tv[u];
-                        CT[off] = ti;
+                    const int cc = cell(ps, u);
+                    const float ti = p.tau * pv[ps][u] + (1.0f - p.tau) * tv[ps][u];
+                    if (u < (ps ? nvp1 : nvp0)) {
+                        CT[(cw + (int64_t)cc * HID) - p.cp0] = ti;
                         tp = fmaf(s_base[cc], ti, tp);
                     }
                 }
-            }
             s_pp[1][h][j] = tp;
             __syncthreads();
             if (tid < HID)
                 p.w.cpart[3][((int64_t)k * K * NG + ob * NG + grp) * HID + tid] = s_pp[1][0][tid] + s_pp[1][1][tid];
             return;
         }
-        if (tid < HID) {  // the column sums of dZ1 over the tiles in order
-            float acc = 0.0f;
-            for (int t = 0; t < B / RB; ++t) acc += p.w.spart[((int64_t)k * (B / RB) + t) * HID + tid];
-            s_S[tid] = acc;
-        }
-        if (B <= DZR) {  // the agent's dZ1 rows into LDS (16 float4 loads per thread in flight)
-            const float4 *src = reinterpret_cast<const float4 *>(p.w.sv.dz1 + (int64_t)k * B * HID);
-            float4 *dst = reinterpret_cast<float4 *>(s_dzr);
-#pragma unroll 16
-            for (int i = tid; i < B * HID / 4; i += 256) dst[i] = src[i];
-        }
-        // the patched cells of the rows' obs `obk` inside this group, in (row, slot) order
-        const int obk = p.phase == 0 ? ob : k;
-        const int NE = B * NPM, per = (NE + 255) / 256, t0 = tid * per;
-        constexpr int PER = (DMAXB * NPM + 255) / 256;
-        int cl[PER];  // this thread's items: the cell offset in the group, or -1 (loads batched)
-        int npv[PER];
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int t = t0 + i;
-            npv[i] = (i < per && t < NE) ? p.w.np[(int64_t)obk * B + t / NPM] : 0;
-        }
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int t = t0 + i;
-            cl[i] = -1;
-            if (i < per && t < NE && t % NPM < npv[i]) {
-                const int c = p.w.pc[((int64_t)obk * B + t / NPM) * NPM + t % NPM] - c0;
-                cl[i] = (c >= 0 && c < ncell) ? c : -1;
-            }
-        }
-        int cnt = 0;
-#pragma unroll
-        for (int i = 0; i < PER; ++i) cnt += cl[i] >= 0 ? 1 : 0;
-        int total = 0;
-        int at = d_excl_scan256(cnt, s_red, total);
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            if (cl[i] >= 0) {
-                const int t = t0 + i;
-                s_ec[at] = cl[i];
-                s_er[at] = t / NPM;
-                s_ed[at] = p.w.pd[((int64_t)obk * B + t / NPM) * NPM + t % NPM];
-                ++at;
-            }
-        }
-        __syncthreads();
-        // per-cell buckets, entries in list order (stable)
-        if (tid < CG) {
-            int n = 0;
-            for (int e = 0; e < total; ++e) n += s_ec[e] == tid ? 1 : 0;
-            int incl = n;  // wave 0: an inclusive scan over the 64 cells
-            for (int o = 1; o < 64; o <<= 1) {
-                const int t = __shfl_up(incl, o, 64);
-                if ((tid & 63) >= o) incl += t;
-            }
-            s_cnt[tid + 1] = incl;
-            if (tid == 0) s_cnt[0] = 0;
-            int pos = incl - n;
-            for (int e = 0; e < total; ++e)
-                if (s_ec[e] == tid) s_bk[pos++] = e;
-        }
-        __syncthreads();
-        // gradient = map * colsum(dZ1) + the cell's patched rows' terms (row order); Adam
+        // X [B][XP]: the rows' obs values of the group's cells -- the map, then the patched cells
+        // (a row's patched cells are distinct: d_patches) -- and G [CG][HID] = X^T dZ1 over the
+        // rows in order on v_mfma_f32_16x16x4_f32 (dZ1 in 128-row chunks through LDS): dense and
+        // balanced whatever the cells' patch counts (a cell every row patches -- the own apple, the
+        // spawn cells -- walks all B rows like any other).  Issued first, their round trips
+        // overlapping: dZ1's first chunk, the first Adam pass's operands, the rows' patch lists.
         const float *wk = p.net.w1 + ((int64_t)k * in_dim + row0) * HID + j;
-        const float *dz1 = (B <= DZR ? s_dzr : p.w.sv.dz1 + (int64_t)k * B * HID) + j;
+        int64_t off0[16], off1[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            off0[u] = (wk + (int64_t)cell(0, u) * HID) - p.p0;
+            off1[u] = (wk + (int64_t)cell(1, u) * HID) - p.p0;
+        }
+        AdamIn<16> ain0;
+        adam_load(p, off0, soft, ain0);
+        const int obk = p.phase == 0 ? ob : k;
+        const int NE = B * NPM;
+        constexpr int PI = (DMAXB * NPM + 255) / 256;  // this thread's items t = tid + 256 i
+        int npv[PI], pcv[PI];
+        float dv[PI];
+#pragma unroll
+        for (int i = 0; i < PI; ++i) {
+            const int t = min(tid + 256 * i, NE - 1);
+            const int64_t ro = (int64_t)obk * B + t / NPM;
+            npv[i] = p.w.np[ro];
+            pcv[i] = p.w.pc[ro * NPM + t % NPM];
+            dv[i] = p.w.pd[ro * NPM + t % NPM];
+        }
+        d_stage_rows(s_dzr, p.w.sv.dz1 + (int64_t)k * B * HID, min(B, DZR) * HID / 4);
+        float *s_X = smem;
+        __syncthreads();  // s_base
+        {
+            const int c = tid % CG;  // 256 = 4 x CG: a thread's map column is fixed
+            const float v = c < ncell ? s_base[c] : 0.0f;
+            for (int r = tid / CG; r < B; r += 256 / CG) s_X[r * XP + c] = v;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < PI; ++i) {
+            const int t = tid + 256 * i, c = pcv[i] - c0;
+            if (t < NE && t % NPM < npv[i] && c >= 0 && c < ncell) s_X[(t / NPM) * XP + c] = s_base[c] + dv[i];
+        }
+        DSTAMP(p, 3);
+        const int lane = tid & 63, wave = tid >> 6, lr = lane & 15, lq = lane >> 4;
+        f32x4 acc[4][2];
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct)
+            acc[ct][0] = acc[ct][1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        for (int rc = 0; rc < B; rc += DZR) {
+            const int nr = min(DZR, B - rc);
+            __syncthreads();  // X written / the previous chunk read
+            if (rc > 0) {
+                d_stage_rows(s_dzr, p.w.sv.dz1 + ((int64_t)k * B + rc) * HID, nr * HID / 4);
+                __syncthreads();
+            }
+            const float *xa = s_X + (int64_t)rc * XP + lr, *zb = s_dzr + 32 * wave + lr;
+            for (int k0 = 0; k0 < nr / 4; k0 += 4)  // nr: a multiple of 16
+#pragma unroll
+            for (int kk = k0; kk < k0 + 4; ++kk) {
+                const int r = 4 * kk + lq;
+                const float b0 = zb[r * DZP], b1 = zb[r * DZP + 16];
+#pragma unroll
+                for (int ct = 0; ct < 4; ++ct) {
+                    const float av = xa[r * XP + 16 * ct];
+                    acc[ct][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b0, acc[ct][0], 0, 0, 0);
+                    acc[ct][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b1, acc[ct][1], 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();  // dZ1 read: G replaces it
+        float *s_G = s_dzr;
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) s_G[(16 * ct + 4 * lq + i) * HID + 32 * wave + 16 * t + lr] = acc[ct][t][i];
+        AdamIn<16> ain1;  // the second pass's operands under the first pass's step
+        adam_load(p, off1, soft, ain1);
+        __syncthreads();
+        DSTAMP(p, 1);
+        // Adam over the group's W1 rows; the c1 partials from the new values
         float pp = 0.0f, tp = 0.0f;
-        for (int u0 = 0; u0 < CG / 2; u0 += 16) {  // 16 cells per pass (h, h + 2, ...)
-            int64_t off[16];
+#pragma unroll
+        for (int ps = 0; ps < 2; ++ps) {
             float gv[16], pv[16], tv[16];
-            int nv = 0;
+#pragma unroll
+            for (int u = 0; u < 16; ++u) gv[u] = s_G[cell(ps, u) * HID + j];
+            const int nv = ps ? nvp1 : nvp0;
+            adam_store(p, sc, ps ? off1 : off0, gv, nv, soft, ps ? ain1 : ain0, pv, tv);
 #pragma unroll
             for (int u = 0; u < 16; ++u) {
-                const int cc = h + 2 * (u0 + u);
-                if (cc < ncell) {
-                    float gi = s_base[cc] * s_S[j];
-                    for (int e = s_cnt[cc]; e < s_cnt[cc + 1]; ++e) {
-                        const int ei = s_bk[e];
-                        gi = fmaf(s_ed[ei], dz1[(int64_t)s_er[ei] * HID], gi);
-                    }
-                    gv[u] = gi;
-                    off[u] = (wk + (int64_t)cc * HID) - p.p0;
-                    nv = u + 1;
-                }
-            }
-            adam_n<16>(p, sc, off, gv, nv, soft, pv, tv);
-#pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                const int cc = h + 2 * (u0 + u);
+                const float bs = s_base[cell(ps, u)];
                 if (u < nv) {
-                    pp = fmaf(s_base[cc], pv[u], pp);
-                    if (soft) tp = fmaf(s_base[cc], tv[u], tp);
+                    pp = fmaf(bs, pv[u], pp);
+                    if (soft) tp = fmaf(bs, tv[u], tp);
                 }
             }
+            if (ps == 0) DSTAMP(p, 4);
         }
         s_pp[0][h][j] = pp;
         s_pp[1][h][j] = tp;
@@ -1771,46 +1843,62 @@ __global__ void __launch_bounds__(256) dgrads_adam(DGrad p) {
         }
         return;
     }
-    if (type == 1) {  // the critic's action rows: dense, sum over the rows in order
-        const int k = b, na = NA * K;
+    if (type == 1) {  // the critic's action rows: blocks (agent, 8 rows); sum over the batch rows in order
+        const int na = NA * K, QB = (na + 7) / 8, k = b / QB, q = b % QB;
         const int j = tid & (HID - 1), h = tid >> 7;
-        if (B <= DZR) {
-            const float4 *src = reinterpret_cast<const float4 *>(p.w.sv.dz1 + (int64_t)k * B * HID);
-            float4 *dst = reinterpret_cast<float4 *>(s_dzr);
-#pragma unroll 16
-            for (int i = tid; i < B * HID / 4; i += 256) dst[i] = src[i];
+        const int a0 = 8 * q + h;  // this thread's rows a0, a0 + 2, a0 + 4, a0 + 6 (< na; others clamped)
+        int ar[4];
+        int64_t off[4];
+        int nv = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            ar[u] = min(a0 + 2 * u, na - 1);
+            off[u] = (p.net.w1 + ((int64_t)k * p.in_dim + (int64_t)K * HW + ar[u]) * HID + j) - p.p0;
+            nv += a0 + 2 * u < na ? 1 : 0;
         }
+        float4 zst[16];
+        const int n4 = min(B, DZR) * HID / 4;
+        d_stage_load(zst, p.w.sv.dz1 + (int64_t)k * B * HID, n4);
+        AdamIn<4> ain;
+        adam_load(p, off, false, ain);
         float *s_a = smem;  // the rows' stored actions [B][9K] (<= 256 x 72 floats)
-        for (int i = tid; i < B * na; i += 256) s_a[i] = p.w.act[i];
-        __syncthreads();
-        const float *dz1 = (B <= DZR ? s_dzr : p.w.sv.dz1 + (int64_t)k * B * HID) + j;
-        for (int a0 = h; a0 < na; a0 += 16) {  // 8 action rows of this thread per pass
-            float acc[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) acc[u] = 0.0f;
-#pragma unroll 8
-            for (int rr = 0; rr < B; ++rr) {
-                const float d = dz1[(int64_t)rr * HID];
-                const float *av = s_a + rr * na;
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int a = a0 + 2 * u;
-                    if (a < na) acc[u] = fmaf(av[a], d, acc[u]);
-                }
-            }
-            int64_t off[8];
-            float pv[8], tv[8];
-            int nv = 0;
+        for (int i0 = 0; i0 < B * na; i0 += 8 * 256) {  // 8 loads in flight, then the stores
+            float v[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
-                const int a = a0 + 2 * u;
-                if (a < na) {
-                    off[u] = (p.net.w1 + ((int64_t)k * p.in_dim + (int64_t)K * HW + a) * HID + j) - p.p0;
-                    nv = u + 1;
-                }
+                const int i = i0 + u * 256 + tid;
+                v[u] = p.w.act[i < B * na ? i : 0];
             }
-            adam_n<8>(p, sc, off, acc, nv, false, pv, tv);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = i0 + u * 256 + tid;
+                if (i < B * na) s_a[i] = v[u];
+            }
         }
+        d_stage_store(s_dzr, zst, n4);
+        DSTAMP(p, 3);
+        float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        for (int rc = 0; rc < B; rc += DZR) {
+            const int nr = min(DZR, B - rc);
+            if (rc > 0) {
+                __syncthreads();  // the previous chunk read
+                d_stage_rows(s_dzr, p.w.sv.dz1 + ((int64_t)k * B + rc) * HID, nr * HID / 4);
+            }
+            __syncthreads();
+            DSTAMP(p, 4);
+            const float *dz = s_dzr + j;
+            for (int r0 = 0; r0 < nr; r0 += 8)
+#pragma unroll
+            for (int rr = r0; rr < r0 + 8; ++rr) {
+                const float d = dz[rr * DZP];
+                const float *av = s_a + (rc + rr) * na;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) acc[u] = fmaf(av[ar[u]], d, acc[u]);
+            }
+        }
+        DSTAMP(p, 5);
+        float pv[4], tv[4];
+        adam_store(p, sc, off, acc, nv, false, ain, pv, tv);
         return;
     }
     if (type == 2) {  // W2 = h1^T dz2 (v_mfma_f32_16x16x4_f32, rows in order), 16 inputs per block
@@ -1945,7 +2033,10 @@ __global__ void __launch_bounds__(256) dgrads_adam(DGrad p) {
             const float *gs = p.w.sv.g3 + ((int64_t)k * B + r) * out;
             float gv[NA];
 #pragma unroll
-            for (int a = 0; a < NA; ++a) gv[a] = a < out ? gs[a] : 0.0f;
+            for (int a = 0; a < NA; ++a) {
+                const float x = gs[a < out ? a : 0];  // clamped, not predicated: the loads batch
+                gv[a] = a < out ? x : 0.0f;
+            }
 #pragma unroll
             for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -1971,6 +2062,11 @@ __global__ void __launch_bounds__(256) dgrads_adam(DGrad p) {
             int64_t off[NW3];
             float gv[NW3], pv[NW3], tv[NW3];
             int nv = 0;
+#pragma unroll
+            for (int u = 0; u < NW3; ++u) {  // unused entries: a valid element (b3[0] of agent k)
+                off[u] = (p.net.b3 + k * out) - p.p0;
+                gv[u] = 0.0f;
+            }
 #pragma unroll
             for (int u = 0; u < NW3 - 1; ++u) {
                 const int t = tid + 256 * u;
@@ -2021,6 +2117,12 @@ __global__ void __launch_bounds__(256) dgrads_adam(DGrad p) {
         for (int u = 0; u < 8; ++u)
             if (on[u]) CT[i0 + u * stride] = p.tau * pv[u] + (1.0f - p.tau) * tv[u];
     }
+}
+
+__global__ void __launch_bounds__(256) dgrads_adam(DGrad p) {
+    DSTAMP(p, 0);
+    dgrads_body(p);
+    DSTAMP(p, 2);
 }
 
 // the c1 partials of one network from its current W1 (the update's own launches refresh them;
@@ -2296,6 +2398,31 @@ gw_status dnet_ok(const gw_mlp_actors *n, int K, int in_dim, int out, const gw_a
     return GW_OK;
 }
 
+// GW_LEARN_STAMP=<file>: the four launches' block stamps (DSTAMP), appended to <file> after each
+// update as records {int32 launch, int32 blocks, blocks x NSTAMP uint64} (a synchronising diagnostic)
+constexpr int STAMP_BLOCKS = 8192;
+unsigned long long *stamp_buf() {
+    static const char *path = std::getenv("GW_LEARN_STAMP");
+    static unsigned long long *buf = nullptr;
+    if (path && *path && !buf && hipMalloc(&buf, sizeof(unsigned long long) * 4 * STAMP_BLOCKS * NSTAMP) != hipSuccess)
+        buf = nullptr;
+    return buf;
+}
+void stamp_dump(hipStream_t s, const int (&nb)[4]) {
+    unsigned long long *buf = stamp_buf();
+    if (!buf || hipStreamSynchronize(s) != hipSuccess) return;
+    static std::vector<unsigned long long> h(4 * STAMP_BLOCKS * NSTAMP);
+    if (hipMemcpy(h.data(), buf, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost) != hipSuccess) return;
+    FILE *f = std::fopen(std::getenv("GW_LEARN_STAMP"), "ab");
+    if (!f) return;
+    for (int l = 0; l < 4; ++l) {
+        const int32_t hd[2] = {l, nb[l]};
+        std::fwrite(hd, sizeof(hd), 1, f);
+        std::fwrite(h.data() + (size_t)l * STAMP_BLOCKS * NSTAMP, sizeof(unsigned long long), (size_t)nb[l] * NSTAMP, f);
+    }
+    std::fclose(f);
+}
+
 gw_status dsrc_ok(const gw_obs_source *src, int B, const float *ws, const char *who) {
     if (!src || !src->base || !ws) return fail(GW_ERR_ARG, std::string(who) + ": null argument");
     if (src->K < 1 || src->K > MAXK || src->N < src->K || src->N > MAXK)
@@ -2399,6 +2526,8 @@ gw_status gw_maddpg_desc_update(const gw_obs_source *src, const gw_desc_ring *ri
     t.K = K;
     t.B = B;
     t.NG = NG;
+    unsigned long long *const sb = stamp_buf();
+    t.stamp = sb;
     gwprof::launch(dcritic_tail, dim3(B / RB, K), dim3(DT), 0, s, t);
     DGrad g{};
     g.w = t.w;
@@ -2423,13 +2552,15 @@ gw_status gw_maddpg_desc_update(const gw_obs_source *src, const gw_desc_ring *ri
     g.nobs = K;
     g.in_dim = in_c;
     g.out = 1;
+    g.stamp = sb ? sb + STAMP_BLOCKS * NSTAMP : nullptr;
     {
-        const int n[7] = {K * K * NG, K, K * (HID / RB), K, K, 0, 0};
+        const int n[7] = {K * K * NG, K * ((NA * K + 7) / 8), K * (HID / RB), K, K, 0, 0};
         g.start[0] = 0;
         for (int i = 0; i < 7; ++i) g.start[i + 1] = g.start[i] + n[i];
     }
     gwprof::launch(dgrads_adam, dim3(g.start[7]), dim3(256), 0, s, g);
     t.count = opt_actor->step;
+    t.stamp = sb ? sb + 2 * STAMP_BLOCKS * NSTAMP : nullptr;
     gwprof::launch(dactor_tail, dim3(B / RB, K), dim3(DT), 0, s, t);
     g.net = *actor;
     g.p0 = opt_actor->param;
@@ -2452,12 +2583,15 @@ gw_status gw_maddpg_desc_update(const gw_obs_source *src, const gw_desc_ring *ri
     g.in_dim = HW;
     g.out = NA;
     g.nrest = 256;
+    g.stamp = sb ? sb + 3 * STAMP_BLOCKS * NSTAMP : nullptr;
+    const int g0blocks = g.start[7];
     {
         const int n[7] = {K * NG, 0, K * (HID / RB), K, K, K * K * NG, g.nrest};
         g.start[0] = 0;
         for (int i = 0; i < 7; ++i) g.start[i + 1] = g.start[i] + n[i];
     }
     gwprof::launch(dgrads_adam, dim3(g.start[7]), dim3(256), 0, s, g);
+    if (sb) stamp_dump(s, {B / RB * K, g0blocks, B / RB * K, g.start[7]});
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? GW_OK : fail(GW_ERR_HIP, std::string(who) + ": " + hipGetErrorString(e));
 }

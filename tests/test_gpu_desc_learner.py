@@ -63,11 +63,15 @@ def _per_tensor(net, flat_a, flat_b):
     return out
 
 
-@pytest.mark.parametrize("scen,E,fear", [("grid32", 512, True), ("level3", 300, False), ("grid64_n8", 256, True)])
-def test_desc_update_equals_dense_fused_update(scen, E, fear):
+@pytest.mark.parametrize("scen,E,fear,B", [("grid32", 512, True, 128), ("level3", 300, False, 128),
+                                           ("grid64_n8", 256, True, 128),
+                                           # dZ1 rows beyond the W1 blocks' LDS copy (B > 128); a small batch
+                                           ("grid32", 512, True, 256), ("grid64_n8", 256, True, 48)])
+def test_desc_update_equals_dense_fused_update(scen, E, fear, B):
     sc, env, m, ro = _setup(E=E, fear=fear, scen=scen)
     from marlnav.maddpg import MADDPG
-    m2 = MADDPG(sc.K, sc.H, sc.W, device=env.device, seed=3, capturable=True)
+    m.batch_size = B
+    m2 = MADDPG(sc.K, sc.H, sc.W, device=env.device, seed=3, capturable=True, batch_size=B)
     assert torch.equal(m2.critics.flat_params(), m.critics.flat_params())
     rp = ro.replay
     assert m.desc_capable(rp)
