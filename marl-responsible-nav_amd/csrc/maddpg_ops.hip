@@ -263,12 +263,44 @@ __device__ __forceinline__ void ln_relu_bwd(const float gy[8], const float y[8],
 // 31; each output is the k-ordered f32 fma chain over c = 0 .. 127 from 0 (the per-row VALU
 // GEMV it replaced, bit for bit).  All threads call it; s_z [16][HP] receives z (the caller syncs
 // before reading it).
+// gemv_t4 (round 5): the transposed layer (W^T, the backward) feeds k-step 4 t + s with input
+// c = 16 t + 4 lq + s, so a lane's four values of a step group are ONE float4 of its W row (and of
+// its LDS row): 8 instead of 32 loads per column, each a contiguous 16 bytes (the strided c = 4 kk
+// + lq order touched 16 rows' lines per load instruction: ~7 us per layer on freshly updated
+// weights vs ~1.7 us forward).  The k order differs from the VALU loop's, so the backward layers
+// are deterministic but no longer the loop's bits (the parity tests bound them against torch).
 constexpr int HP = HID + 4;  // padded LDS row
 template <int U = HID / 4>  // k-steps per unrolled batch (U = 32: the whole layer's loads in flight)
 __device__ __forceinline__ void gemv16(const float *s_h, const float *__restrict__ w, bool transpose, float *s_z) {
     const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 3, lr = lane & 15, lq = lane >> 4;
     const int n0 = 32 * wave + lr, n1 = n0 + 16;
     f32x4 acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (transpose) {  // W^T: k-step 4 t + s takes c = 16 t + 4 lq + s (gemv_t4)
+        float4 w0[HID / 16], w1[HID / 16];
+#pragma unroll
+        for (int t = 0; t < HID / 16; ++t) {
+            w0[t] = *reinterpret_cast<const float4 *>(w + n0 * HID + 16 * t + 4 * lq);
+            w1[t] = *reinterpret_cast<const float4 *>(w + n1 * HID + 16 * t + 4 * lq);
+        }
+#pragma unroll
+        for (int t = 0; t < HID / 16; ++t) {
+            const float4 a = *reinterpret_cast<const float4 *>(s_h + lr * HP + 16 * t + 4 * lq);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, w0[t].x, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, w1[t].x, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, w0[t].y, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, w1[t].y, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, w0[t].z, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, w1[t].z, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, w0[t].w, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, w1[t].w, acc1, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            s_z[(4 * lq + i) * HP + n0] = acc0[i];
+            s_z[(4 * lq + i) * HP + n1] = acc1[i];
+        }
+        return;
+    }
     // fully unrolled: the 64 weight loads of a lane are all in flight before the first MFMA
     // needs one (one L2 round trip per layer instead of one per 8 k-steps)
 #pragma unroll U
@@ -970,18 +1002,18 @@ __device__ __forceinline__ void d_draw(const DQ &q, int64_t t, uint64_t seed, ui
     if (tr < 0) tr += q.S;
 }
 
-// sum over n partials p[g * HID] in g order (16 loads in flight)
+// sum over n partials p[g * HID] in g order (32 loads in flight: one round trip up to n = 32;
+// batches past n re-read partial 0 and skip it)
 __device__ __forceinline__ float d_sum_parts(const float *p, int n) {
     float acc = 0.0f;
-    int g = 0;
-    for (; g + 16 <= n; g += 16) {
-        float v[16];
+    for (int g = 0; g < n; g += 32) {
+        float v[32];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) v[i] = p[(int64_t)(g + i) * HID];
+        for (int i = 0; i < 32; ++i) v[i] = p[(int64_t)(g + i < n ? g + i : 0) * HID];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) acc += v[i];
+        for (int i = 0; i < 32; ++i)
+            if (g + i < n) acc += v[i];
     }
-    for (; g < n; ++g) acc += p[(int64_t)g * HID];
     return acc;
 }
 
@@ -1042,16 +1074,50 @@ __device__ __forceinline__ void d_add_patches(float z[8], const float *w1, int64
     }
 }
 
-// z += the action inputs' terms (na values, W1 rows row0 ..), in input order
-__device__ __forceinline__ void d_add_actions(float z[8], const float *w1, int64_t row0, const float *av, int na,
-                                              int g) {
-#pragma unroll 9
-    for (int a = 0; a < na; ++a) {
-        const float v = av[a];
-        const float *wr = w1 + (row0 + a) * HID + 8 * g;
-        const float4 w0 = *reinterpret_cast<const float4 *>(wr), w1v = *reinterpret_cast<const float4 *>(wr + 4);
-        z[0] = fmaf(v, w0.x, z[0]); z[1] = fmaf(v, w0.y, z[1]); z[2] = fmaf(v, w0.z, z[2]); z[3] = fmaf(v, w0.w, z[3]);
-        z[4] = fmaf(v, w1v.x, z[4]); z[5] = fmaf(v, w1v.y, z[5]); z[6] = fmaf(v, w1v.z, z[6]); z[7] = fmaf(v, w1v.w, z[7]);
+// z += a critic's layer-1 input terms of one row, in order: agent kk = 0 .. K - 1's patched cells
+// (W1 rows kk HW + cell, the deltas; d_add_patches per agent), then the 9K action inputs (W1 rows
+// K HW + a; round 4's d_add_actions): the same fma order, but NB entries' loads in flight per batch, so ~2
+// round trips instead of one per agent plus one per 9 actions (entries past the end re-read a
+// valid row and are skipped)
+template <int NB>
+__device__ __forceinline__ void d_add_critic_in(float z[8], const float *w1, int HW, int K, const int16_t (*pc)[NPM],
+                                                const float (*pd)[NPM], const int *np, const float *av, int g) {
+    const int na = NA * K;
+    int tot = na;
+    for (int kk = 0; kk < K; ++kk) tot += np[kk];
+    int kk = 0, i = 0;
+    for (int e0 = 0; e0 < tot; e0 += NB) {
+        float4 a[NB], b[NB];
+        float dv[NB];
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            int64_t row;
+            if (kk < K) {
+                row = (int64_t)kk * HW + pc[kk][i];
+                dv[u] = pd[kk][i];
+            } else {
+                const int ia = min(i, na - 1);
+                row = (int64_t)K * HW + ia;
+                dv[u] = av[ia];
+            }
+            const float *wr = w1 + row * HID + 8 * g;
+            a[u] = *reinterpret_cast<const float4 *>(wr);
+            b[u] = *reinterpret_cast<const float4 *>(wr + 4);
+            ++i;
+            if (kk < K && i >= np[kk]) {
+                ++kk;
+                i = 0;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            if (e0 + u < tot) {
+                z[0] = fmaf(dv[u], a[u].x, z[0]); z[1] = fmaf(dv[u], a[u].y, z[1]);
+                z[2] = fmaf(dv[u], a[u].z, z[2]); z[3] = fmaf(dv[u], a[u].w, z[3]);
+                z[4] = fmaf(dv[u], b[u].x, z[4]); z[5] = fmaf(dv[u], b[u].y, z[5]);
+                z[6] = fmaf(dv[u], b[u].z, z[6]); z[7] = fmaf(dv[u], b[u].w, z[7]);
+            }
+        }
     }
 }
 
@@ -1062,6 +1128,22 @@ __device__ __forceinline__ void gemv_all(const float *s_h, const float *__restri
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, lr = lane & 15, lq = lane >> 4;
     const int n0 = 16 * wave + lr;
     f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (transpose) {  // W^T: k-step 4 t + s takes c = 16 t + 4 lq + s (gemv_t4)
+        float4 wv[HID / 16];
+#pragma unroll
+        for (int t = 0; t < HID / 16; ++t) wv[t] = *reinterpret_cast<const float4 *>(w + n0 * HID + 16 * t + 4 * lq);
+#pragma unroll
+        for (int t = 0; t < HID / 16; ++t) {
+            const float4 a = *reinterpret_cast<const float4 *>(s_h + lr * HP + 16 * t + 4 * lq);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, wv[t].x, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, wv[t].y, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, wv[t].z, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, wv[t].w, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s_z[(4 * lq + i) * HP + n0] = acc[i];
+        return;
+    }
 #pragma unroll
     for (int kk = 0; kk < HID / 4; ++kk) {
         const int c = 4 * kk + lq;
@@ -1134,11 +1216,12 @@ __device__ __forceinline__ Mlp staged(Mlp m, const float *sp, int out) {
 // GW_LEARN_STAMP=<file> (diagnostics): each block's thread 0 writes wall_clock64() stamps at its
 // phase boundaries into slots [block][0..14] (slot 15: the block type); the host appends them to <file>
 constexpr int NSTAMP = 16;
-#define DSTAMP(P, i)                                                                                   \
+#define DSTAMP_T(P, i, T)                                                                              \
     do {                                                                                               \
-        if ((P).stamp && threadIdx.x == 0)                                                             \
+        if ((P).stamp && threadIdx.x == (T))                                                           \
             (P).stamp[(int64_t)(blockIdx.y * gridDim.x + blockIdx.x) * NSTAMP + (i)] = wall_clock64(); \
     } while (0)
+#define DSTAMP(P, i) DSTAMP_T(P, i, 0)
 
 struct DTail {
     unsigned long long *stamp;
@@ -1222,6 +1305,7 @@ __global__ void __launch_bounds__(DT) dcritic_tail(DTail p) {
                 }
             }
         }
+        DSTAMP(p, 11);
     } else {
         const int t2 = tid - 256;
         // c1 of the networks this block runs: the K target actors, critic target k, critic k
@@ -1236,27 +1320,40 @@ __global__ void __launch_bounds__(DT) dcritic_tail(DTail p) {
                 v = p.c.b1[k * HID + j] + d_sum_parts(p.w.cpart[2] + (int64_t)k * K * p.NG * HID + j, K * p.NG);
             s_c1[net][j] = v;
         }
-        // the stored action probabilities of every agent (the critic's action inputs)
-        for (int o = t2; o < RB * NA * K; o += 256) {
-            const int rr = o / (NA * K), a = o % (NA * K), kk = a / NA;
+        DSTAMP_T(p, 12, 256);
+        // the stored action probabilities of every agent (the critic's action inputs) and agent k's
+        // reward and termination (the TD target): every draw, then every load, then the stores
+        constexpr int NPR = (RB * NA * MAXK + 255) / 256;
+        const int npr = RB * NA * K;
+        float pv[NPR];
+#pragma unroll
+        for (int u = 0; u < NPR; ++u) {
+            const int o = min(t2 + 256 * u, npr - 1), rr = o / (NA * K), a = o % (NA * K);
             int64_t tr, e;
-            d_draw(p.q, t_now, p.seed, c, r0 + rr, tr, e);
-            const float v = p.q.probs[((tr * K + kk) * E + e) * NA + a % NA];
-            s_act[rr][a] = v;
-            if (rec) p.w.act[(int64_t)(r0 + rr) * NA * K + a] = v;
+            if (t2 + 256 * u < npr || u == 0) d_draw(p.q, t_now, p.seed, c, r0 + rr, tr, e);
+            else tr = e = 0;
+            pv[u] = p.q.probs[((tr * K + a / NA) * E + e) * NA + a % NA];
         }
-        // agent k's reward and termination (the TD target)
+        const int rrw = max(t2 - (256 - RB), 0);
+        int64_t trw, ew;
+        d_draw(p.q, t_now, p.seed, c, r0 + rrw, trw, ew);
+        const float rw = (float)p.q.reward[(trw * E + ew) * K + k];
+        const float t1 = 1.0f - (float)p.q.term[(trw * E + ew) * K + k];
+#pragma unroll
+        for (int u = 0; u < NPR; ++u) {
+            const int o = t2 + 256 * u;
+            if (o < npr) {
+                s_act[o / (NA * K)][o % (NA * K)] = pv[u];
+                if (rec) p.w.act[(int64_t)(r0 + o / (NA * K)) * NA * K + o % (NA * K)] = pv[u];
+            }
+        }
         if (t2 >= 256 - RB) {
-            const int rr = t2 - (256 - RB);
-            int64_t tr, e;
-            d_draw(p.q, t_now, p.seed, c, r0 + rr, tr, e);
-            const float rw = (float)p.q.reward[(tr * E + e) * K + k];
-            const float t1 = 1.0f - (float)p.q.term[(tr * E + e) * K + k];
-            s_rw[rr] = rw;
-            s_t1[rr] = t1;
-            p.w.rw[(int64_t)k * B + r0 + rr] = rw;
-            p.w.t1[(int64_t)k * B + r0 + rr] = t1;
+            s_rw[rrw] = rw;
+            s_t1[rrw] = t1;
+            p.w.rw[(int64_t)k * B + r0 + rrw] = rw;
+            p.w.t1[(int64_t)k * B + r0 + rrw] = t1;
         }
+        DSTAMP_T(p, 13, 256);
     }
 #pragma unroll
     for (int u = 0; u < NSV; ++u) {
@@ -1264,6 +1361,7 @@ __global__ void __launch_bounds__(DT) dcritic_tail(DTail p) {
         if (o < tot) *par_dst(o) = sv[u];
     }
     for (int o = tid + NSV * DT; o < tot; o += DT) *par_dst(o) = par_src(o);
+    DSTAMP(p, 14);
     if (blockIdx.x == 0 && k == 0 && tid == 0) p.w.snap[0] = p.count[0] + 1;
     __syncthreads();
     DSTAMP(p, 1);
@@ -1277,11 +1375,14 @@ __global__ void __launch_bounds__(DT) dcritic_tail(DTail p) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) z[i] = s_c1[kx][8 * g + i];
         d_add_patches(z, m.w1, 0, s_pc[1][rl][kx], s_pd[1][rl][kx], s_np[1][rl][kx], g);
+        if (rd == 0) DSTAMP(p, 6);
         d_fwd_rest(z, m, NA, rl, g, s_in[grp], s_out[grp], f, out);
+        if (rd == 0) DSTAMP(p, 7);
         if (kk < K) {
             float ur[NA], pr[NA];
             d_gumbel_u(p.seed, c, 0, kk, r, ur);
             d_gumbel(out, ur, pr);
+            if (rd == 0) DSTAMP(p, 8);
             if (g == 0) {
 #pragma unroll
                 for (int a = 0; a < NA; ++a) s_tact[rl][NA * kk + a] = pr[a];
@@ -1307,10 +1408,10 @@ __global__ void __launch_bounds__(DT) dcritic_tail(DTail p) {
         float z[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) z[i] = s_c1[tgt ? K : K + 1][8 * g + i];
-        for (int kk = 0; kk < K; ++kk)
-            d_add_patches(z, m.w1, (int64_t)kk * HW, s_pc[which][rl][kk], s_pd[which][rl][kk], s_np[which][rl][kk], g);
-        d_add_actions(z, m.w1, (int64_t)K * HW, tgt ? s_tact[rl] : s_act[rl], NA * K, g);
+        d_add_critic_in<16>(z, m.w1, HW, K, s_pc[which][rl], s_pd[which][rl], s_np[which][rl], tgt ? s_tact[rl] : s_act[rl], g);
+        DSTAMP(p, 9);
         d_fwd_rest(z, m, 1, rl, g, s_in[grp], s_out[grp], f, out);
+        DSTAMP(p, 10);
     }
     // y = f32(r) + ((1 - d) * gamma) * q_next (gw_td_target's op order)
     if (grp == 0 && g == 0) s_y[rl] = s_rw[rl] + (s_t1[rl] * p.gamma) * out[0];
@@ -1463,10 +1564,8 @@ __global__ void __launch_bounds__(DT) dactor_tail(DTail p) {
         // the stepped critic k on the mixed actions
 #pragma unroll
         for (int i = 0; i < 8; ++i) z[i] = s_c1[1][8 * g + i];
-        for (int kk = 0; kk < K; ++kk)
-            d_add_patches(z, mc.w1, (int64_t)kk * HW, s_pc[rl][kk], s_pd[rl][kk], s_np[rl][kk], g);
         DSTAMP(p, 8);
-        d_add_actions(z, mc.w1, (int64_t)K * HW, s_act[rl], NA * K, g);
+        d_add_critic_in<16>(z, mc.w1, HW, K, s_pc[rl], s_pd[rl], s_np[rl], s_act[rl], g);
         DSTAMP(p, 9);
         ln_relu(z, mc.lw1, mc.lb1, g, fc.xh1, fc.y1, fc.rs1);
     }
@@ -1591,8 +1690,8 @@ __device__ __forceinline__ void adam_load(const DGrad &p, const int64_t (&off)[N
     }
 }
 template <int NB>
-__device__ __forceinline__ void adam_store(const DGrad &p, const AdamSc &a, const int64_t (&off)[NB], const float (&gi)[NB],
-                                           int nv, bool soft, const AdamIn<NB> &in, float (&pi)[NB], float (&ti)[NB]) {
+__device__ __forceinline__ void adam_store_m(const DGrad &p, const AdamSc &a, const int64_t (&off)[NB], const float (&gi)[NB],
+                                             uint32_t valid, bool soft, const AdamIn<NB> &in, float (&pi)[NB], float (&ti)[NB]) {
     float *__restrict__ P = p.p0;
     float *__restrict__ G = p.g0;
     float *__restrict__ M = p.m0;
@@ -1609,7 +1708,7 @@ __device__ __forceinline__ void adam_store(const DGrad &p, const AdamSc &a, cons
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-        if (i < nv) {
+        if ((valid >> i) & 1u) {
             G[off[i]] = gi[i];
             M[off[i]] = mo[i];
             V[off[i]] = vo[i];
@@ -1617,6 +1716,12 @@ __device__ __forceinline__ void adam_store(const DGrad &p, const AdamSc &a, cons
             if (soft) T[off[i]] = ti[i];
         }
     }
+}
+// the first nv entries valid
+template <int NB>
+__device__ __forceinline__ void adam_store(const DGrad &p, const AdamSc &a, const int64_t (&off)[NB], const float (&gi)[NB],
+                                           int nv, bool soft, const AdamIn<NB> &in, float (&pi)[NB], float (&ti)[NB]) {
+    adam_store_m(p, a, off, gi, nv >= 32 ? 0xFFFFFFFFu : (1u << nv) - 1u, soft, in, pi, ti);
 }
 template <int NB>
 __device__ __forceinline__ void adam_n(const DGrad &p, const AdamSc &a, const int64_t (&off)[NB], const float (&gi)[NB],
@@ -1653,7 +1758,7 @@ __device__ __forceinline__ void d_stage_rows(float *dst, const float *src, int n
 }
 
 __device__ __forceinline__ void dgrads_body(const DGrad &p) {
-    __shared__ float s_base[CG], s_pp[2][2][HID];
+    __shared__ float s_base[CG], s_pp[2][4][HID];
     __shared__ float s_sc[2];
     __shared__ __attribute__((aligned(16))) float smem[GRG * HID * NA + GRG * (NA + 1) > RB * (TILE_R + 4) + TILE_R * HID
                                                         ? GRG * HID * NA + GRG * (NA + 1)
@@ -1668,86 +1773,99 @@ __device__ __forceinline__ void dgrads_body(const DGrad &p) {
     while (type < 6 && b >= p.start[type + 1]) ++type;
     b -= p.start[type];
     if (p.stamp && tid == 0) p.stamp[(int64_t)blockIdx.x * NSTAMP + NSTAMP - 1] = (unsigned long long)type;
-    // this step's Adam scalars (the count the tail snapshotted; torch forms them in double)
-    if (tid == 0) {
-        const double s = (double)p.w.snap[p.phase];
-        s_sc[0] = (float)(p.lr / (1.0 - pow(p.beta1, s)));
-        s_sc[1] = (float)sqrt(1.0 - pow(p.beta2, s));
-        if (blockIdx.x == 0) p.count[0] = p.w.snap[p.phase];
-    }
-    __syncthreads();
-    AdamSc sc;
-    sc.step_size = s_sc[0];
-    sc.bc2 = s_sc[1];
-    sc.w1 = (float)(1.0 - p.beta1);
-    sc.b2 = (float)p.beta2;
-    sc.w2 = (float)(1.0 - p.beta2);
-    sc.e = (float)p.eps;
+    // this step's Adam scalars (the count the tail snapshotted; torch forms them in double):
+    // thread 0 forms them (set_sc; block 0, a W1 block, also publishes the count) and the threads
+    // read them after a later barrier (get_sc) -- not a barrier of its own in front of every
+    // block's first load
+    auto set_sc = [&]() {
+        if (tid == 0) {
+            const double s = (double)p.w.snap[p.phase];
+            s_sc[0] = (float)(p.lr / (1.0 - pow(p.beta1, s)));
+            s_sc[1] = (float)sqrt(1.0 - pow(p.beta2, s));
+            if (blockIdx.x == 0) p.count[0] = p.w.snap[p.phase];
+        }
+    };
+    auto get_sc = [&]() {
+        AdamSc sc;
+        sc.step_size = s_sc[0];
+        sc.bc2 = s_sc[1];
+        sc.w1 = (float)(1.0 - p.beta1);
+        sc.b2 = (float)p.beta2;
+        sc.w2 = (float)(1.0 - p.beta2);
+        sc.e = (float)p.eps;
+        return sc;
+    };
     const bool soft = p.phase == 1;
+    if (type <= 4) set_sc();  // wave 0's other loads wait behind it; the other waves' do not
     if (type == 0 || type == 5) {
         // W1 rows of one 64-cell group of one agent obs: type 0 the stepped network (gradient +
-        // Adam [+ the actor target's soft update]), type 5 the critic target's soft update; both
-        // leave the group's c1 partials
+        // Adam [+ the actor target's soft update]) for one half of the features (blocks (group,
+        // half)), type 5 the critic target's soft update; both leave the group's c1 partials, the
+        // cells in four chains (cells q, q + 4, ..) summed in q order (dprime's order)
         const int nob = type == 0 ? p.nobs : K;
+        const int jh = type == 0 ? (b & 1) : 0;
+        if (type == 0) b >>= 1;
         const int k = b / (nob * NG), ob = (b / NG) % nob, grp = b % NG;
         const int c0 = grp * CG, ncell = min(CG, HW - c0);
-        const int j = tid & (HID - 1), h = tid >> 7;
         const bool critic = type == 5 || p.phase == 0;
         const int in_dim = type == 5 ? K * HW + NA * K : p.in_dim;
         const int64_t row0 = critic ? (int64_t)ob * HW + c0 : c0;  // W1 input row of cell c0
         if (tid < ncell) s_base[tid] = p.base[c0 + tid];
-        // this thread's cells h + 2 u (u < 32), two passes of 16: nvp[ps] exist in pass ps; the
-        // others are clamped to the group's last cell (their loads valid, their results unused)
-        const int ncl = ncell > h ? (ncell - h + 1) / 2 : 0;
-        const int nvp0 = min(ncl, 16), nvp1 = max(0, min(ncl - 16, 16));
-        auto cell = [&](int ps, int u) { return min(h + 2 * (16 * ps + u), ncell - 1); };
-        if (type == 5) {
+        // chain q's cells q + 4 u (u < 16): the first ncq(q) exist, the others are clamped to the
+        // group's last cell (their loads valid, their results unused)
+        auto ncq = [&](int q) { return ncell > q ? (ncell - q + 3) / 4 : 0; };
+        auto cell = [&](int q, int u) { return min(q + 4 * u, ncell - 1); };
+        auto cpart_out = [&](int which, int64_t gi, int j0, int nj, int v) {
+            if (tid < nj)
+                p.w.cpart[which][gi * HID + j0 + tid] =
+                    ((s_pp[v][0][j0 + tid] + s_pp[v][1][j0 + tid]) + s_pp[v][2][j0 + tid]) + s_pp[v][3][j0 + tid];
+        };
+        if (type == 5) {  // thread (h, j): chains h and h + 2
+            const int j = tid & (HID - 1), h = tid >> 7;
             const float *cw = p.cnet.w1 + ((int64_t)k * in_dim + row0) * HID + j;
             const float *__restrict__ CP = p.cp0;
             float *__restrict__ CT = p.ct0;
-            float pv[2][16], tv[2][16];  // both passes' loads in flight, then the stores
+            float pv[2][16], tv[2][16];  // both chains' loads in flight, then the stores
 #pragma unroll
             for (int ps = 0; ps < 2; ++ps)
 #pragma unroll
                 for (int u = 0; u < 16; ++u) {
-                    const int64_t off = (cw + (int64_t)cell(ps, u) * HID) - p.cp0;
+                    const int64_t off = (cw + (int64_t)cell(h + 2 * ps, u) * HID) - p.cp0;
                     pv[ps][u] = CP[off];
                     tv[ps][u] = CT[off];
                 }
             __syncthreads();  // s_base
-            float tp = 0.0f;
 #pragma unroll
-            for (int ps = 0; ps < 2; ++ps)
+            for (int ps = 0; ps < 2; ++ps) {
+                const int q = h + 2 * ps, nq = ncq(q);
+                float tp = 0.0f;
 #pragma unroll
                 for (int u = 0; u < 16; ++u) {
-                    const int cc = cell(ps, u);
+                    const int cc = cell(q, u);
                     const float ti = p.tau * pv[ps][u] + (1.0f - p.tau) * tv[ps][u];
-                    if (u < (ps ? nvp1 : nvp0)) {
+                    if (u < nq) {
                         CT[(cw + (int64_t)cc * HID) - p.cp0] = ti;
                         tp = fmaf(s_base[cc], ti, tp);
                     }
                 }
-            s_pp[1][h][j] = tp;
+                s_pp[1][q][j] = tp;
+            }
             __syncthreads();
-            if (tid < HID)
-                p.w.cpart[3][((int64_t)k * K * NG + ob * NG + grp) * HID + tid] = s_pp[1][0][tid] + s_pp[1][1][tid];
+            cpart_out(3, (int64_t)k * K * NG + ob * NG + grp, 0, HID, 1);
             return;
         }
         // X [B][XP]: the rows' obs values of the group's cells -- the map, then the patched cells
-        // (a row's patched cells are distinct: d_patches) -- and G [CG][HID] = X^T dZ1 over the
-        // rows in order on v_mfma_f32_16x16x4_f32 (dZ1 in 128-row chunks through LDS): dense and
-        // balanced whatever the cells' patch counts (a cell every row patches -- the own apple, the
-        // spawn cells -- walks all B rows like any other).  Issued first, their round trips
-        // overlapping: dZ1's first chunk, the first Adam pass's operands, the rows' patch lists.
+        // (a row's patched cells are distinct: d_patches) -- and G [CG][64] = X^T dZ1 over the rows
+        // in order on v_mfma_f32_16x16x4_f32 for this block's 64 features (dZ1 in 128-row chunks
+        // through LDS): dense and balanced whatever the cells' patch counts (a cell every row
+        // patches -- the own apple, the spawn cells -- walks all B rows like any other).  Issued
+        // first, their round trips overlapping: the Adam operands, the rows' patch lists, dZ1.
+        const int jl = tid & 63, q = tid >> 6, j = 64 * jh + jl;  // thread: feature j, chain q
+        const int nq = ncq(q);
         const float *wk = p.net.w1 + ((int64_t)k * in_dim + row0) * HID + j;
-        int64_t off0[16], off1[16];
+        int64_t off[16];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            off0[u] = (wk + (int64_t)cell(0, u) * HID) - p.p0;
-            off1[u] = (wk + (int64_t)cell(1, u) * HID) - p.p0;
-        }
-        AdamIn<16> ain0;
-        adam_load(p, off0, soft, ain0);
+        for (int u = 0; u < 16; ++u) off[u] = (wk + (int64_t)cell(q, u) * HID) - p.p0;
         const int obk = p.phase == 0 ? ob : k;
         const int NE = B * NPM;
         constexpr int PI = (DMAXB * NPM + 255) / 256;  // this thread's items t = tid + 256 i
@@ -1761,9 +1879,16 @@ __device__ __forceinline__ void dgrads_body(const DGrad &p) {
             pcv[i] = p.w.pc[ro * NPM + t % NPM];
             dv[i] = p.w.pd[ro * NPM + t % NPM];
         }
-        d_stage_rows(s_dzr, p.w.sv.dz1 + (int64_t)k * B * HID, min(B, DZR) * HID / 4);
+        const int n4 = min(B, DZR) * HID / 4;
+        float4 zst[16];
+        d_stage_load(zst, p.w.sv.dz1 + (int64_t)k * B * HID, n4);
+        AdamIn<16> ain;  // issued last: the staging below does not wait for them
+        adam_load(p, off, soft, ain);
+        d_stage_store(s_dzr, zst, n4);
+        DSTAMP(p, 5);
         float *s_X = smem;
         __syncthreads();  // s_base
+        DSTAMP(p, 6);
         {
             const int c = tid % CG;  // 256 = 4 x CG: a thread's map column is fixed
             const float v = c < ncell ? s_base[c] : 0.0f;
@@ -1777,10 +1902,9 @@ __device__ __forceinline__ void dgrads_body(const DGrad &p) {
         }
         DSTAMP(p, 3);
         const int lane = tid & 63, wave = tid >> 6, lr = lane & 15, lq = lane >> 4;
-        f32x4 acc[4][2];
+        f32x4 acc[4];
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct)
-            acc[ct][0] = acc[ct][1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        for (int ct = 0; ct < 4; ++ct) acc[ct] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
         for (int rc = 0; rc < B; rc += DZR) {
             const int nr = min(DZR, B - rc);
             __syncthreads();  // X written / the previous chunk read
@@ -1788,18 +1912,15 @@ __device__ __forceinline__ void dgrads_body(const DGrad &p) {
                 d_stage_rows(s_dzr, p.w.sv.dz1 + ((int64_t)k * B + rc) * HID, nr * HID / 4);
                 __syncthreads();
             }
-            const float *xa = s_X + (int64_t)rc * XP + lr, *zb = s_dzr + 32 * wave + lr;
+            const float *xa = s_X + (int64_t)rc * XP + lr, *zb = s_dzr + 64 * jh + 16 * wave + lr;
             for (int k0 = 0; k0 < nr / 4; k0 += 4)  // nr: a multiple of 16
 #pragma unroll
             for (int kk = k0; kk < k0 + 4; ++kk) {
                 const int r = 4 * kk + lq;
-                const float b0 = zb[r * DZP], b1 = zb[r * DZP + 16];
+                const float bv = zb[r * DZP];
 #pragma unroll
-                for (int ct = 0; ct < 4; ++ct) {
-                    const float av = xa[r * XP + 16 * ct];
-                    acc[ct][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b0, acc[ct][0], 0, 0, 0);
-                    acc[ct][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b1, acc[ct][1], 0, 0, 0);
-                }
+                for (int ct = 0; ct < 4; ++ct)
+                    acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[r * XP + 16 * ct], bv, acc[ct], 0, 0, 0);
             }
         }
         __syncthreads();  // dZ1 read: G replaces it
@@ -1807,40 +1928,31 @@ __device__ __forceinline__ void dgrads_body(const DGrad &p) {
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) s_G[(16 * ct + 4 * lq + i) * HID + 32 * wave + 16 * t + lr] = acc[ct][t][i];
-        AdamIn<16> ain1;  // the second pass's operands under the first pass's step
-        adam_load(p, off1, soft, ain1);
+            for (int i = 0; i < 4; ++i) s_G[(16 * ct + 4 * lq + i) * HID + 64 * jh + 16 * wave + lr] = acc[ct][i];
         __syncthreads();
         DSTAMP(p, 1);
-        // Adam over the group's W1 rows; the c1 partials from the new values
-        float pp = 0.0f, tp = 0.0f;
-#pragma unroll
-        for (int ps = 0; ps < 2; ++ps) {
+        // Adam over the chain's W1 rows; the c1 partials from the new values
+        {
             float gv[16], pv[16], tv[16];
 #pragma unroll
-            for (int u = 0; u < 16; ++u) gv[u] = s_G[cell(ps, u) * HID + j];
-            const int nv = ps ? nvp1 : nvp0;
-            adam_store(p, sc, ps ? off1 : off0, gv, nv, soft, ps ? ain1 : ain0, pv, tv);
+            for (int u = 0; u < 16; ++u) gv[u] = s_G[cell(q, u) * HID + j];
+            adam_store(p, get_sc(), off, gv, nq, soft, ain, pv, tv);
+            float pp = 0.0f, tp = 0.0f;
 #pragma unroll
             for (int u = 0; u < 16; ++u) {
-                const float bs = s_base[cell(ps, u)];
-                if (u < nv) {
+                const float bs = s_base[cell(q, u)];
+                if (u < nq) {
                     pp = fmaf(bs, pv[u], pp);
                     if (soft) tp = fmaf(bs, tv[u], tp);
                 }
             }
-            if (ps == 0) DSTAMP(p, 4);
+            s_pp[0][q][j] = pp;
+            s_pp[1][q][j] = tp;
         }
-        s_pp[0][h][j] = pp;
-        s_pp[1][h][j] = tp;
         __syncthreads();
-        if (tid < HID) {
-            const int64_t gi = p.phase == 0 ? ((int64_t)k * K * NG + ob * NG + grp) : ((int64_t)k * NG + grp);
-            p.w.cpart[p.phase == 0 ? 2 : 0][gi * HID + tid] = s_pp[0][0][tid] + s_pp[0][1][tid];
-            if (soft) p.w.cpart[1][gi * HID + tid] = s_pp[1][0][tid] + s_pp[1][1][tid];
-        }
+        const int64_t gi = p.phase == 0 ? ((int64_t)k * K * NG + ob * NG + grp) : ((int64_t)k * NG + grp);
+        cpart_out(p.phase == 0 ? 2 : 0, gi, 64 * jh, 64, 0);
+        if (soft) cpart_out(1, gi, 64 * jh, 64, 1);
         return;
     }
     if (type == 1) {  // the critic's action rows: blocks (agent, 8 rows); sum over the batch rows in order
@@ -1898,7 +2010,7 @@ __device__ __forceinline__ void dgrads_body(const DGrad &p) {
         }
         DSTAMP(p, 5);
         float pv[4], tv[4];
-        adam_store(p, sc, off, acc, nv, false, ain, pv, tv);
+        adam_store(p, get_sc(), off, acc, nv, false, ain, pv, tv);
         return;
     }
     if (type == 2) {  // W2 = h1^T dz2 (v_mfma_f32_16x16x4_f32, rows in order), 16 inputs per block
@@ -1908,6 +2020,16 @@ __device__ __forceinline__ void dgrads_body(const DGrad &p) {
         const int lane = tid & 63, wave = tid >> 6, lr = lane & 15, lq = lane >> 4;
         f32x4 acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = {0.0f, 0.0f, 0.0f, 0.0f};
         const int n0 = 32 * wave + lr, n1 = n0 + 16;
+        const float *w2 = p.net.w2 + (int64_t)k * HID * HID;
+        int64_t off[8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int d = d0 + 4 * lq + i;
+            off[2 * i] = (w2 + (int64_t)d * HID + n0) - p.p0;
+            off[2 * i + 1] = (w2 + (int64_t)d * HID + n1) - p.p0;
+        }
+        AdamIn<8> ain;  // the Adam operands' round trip under the tiles' staging
+        adam_load(p, off, soft, ain);
         for (int r0 = 0; r0 < B; r0 += TILE_R) {
             const int nr = min(TILE_R, B - r0);
             __syncthreads();
@@ -1943,24 +2065,28 @@ __device__ __forceinline__ void dgrads_body(const DGrad &p) {
                 acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, s_dz[rr][n1], acc1, 0, 0, 0);
             }
         }
-        const float *w2 = p.net.w2 + (int64_t)k * HID * HID;
-        int64_t off[8];
         float gv[8], pv[8], tv[8];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int d = d0 + 4 * lq + i;
-            off[2 * i] = (w2 + (int64_t)d * HID + n0) - p.p0;
-            off[2 * i + 1] = (w2 + (int64_t)d * HID + n1) - p.p0;
             gv[2 * i] = acc0[i];
             gv[2 * i + 1] = acc1[i];
         }
-        adam_n<8>(p, sc, off, gv, 8, soft, pv, tv);
+        adam_store(p, get_sc(), off, gv, 8, soft, ain, pv, tv);
         return;
     }
     const int rg = tid >> 4, g = tid & 15;
     if (type == 3) {  // b1, ln1 affine, b2, ln2 affine: 16 row groups, combined in group order
         const int k = b;
         const int64_t base = (int64_t)k * B * HID;
+        const float *dst[6] = {p.net.b1, p.net.ln1_w, p.net.ln1_b, p.net.b2, p.net.ln2_w, p.net.ln2_b};
+        int64_t off[3];
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {  // 6 * 128 = 3 * 256 elements
+            const int t = tid + 256 * u;
+            off[u] = (dst[t / HID] + k * HID + t % HID) - p.p0;
+        }
+        AdamIn<3> ain;
+        adam_load(p, off, soft, ain);
         float acc[6][8];
 #pragma unroll
         for (int v = 0; v < 6; ++v)
@@ -2000,23 +2126,41 @@ __device__ __forceinline__ void dgrads_body(const DGrad &p) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) part[rg][v][8 * g + i] = acc[v][i];
         __syncthreads();
-        const float *dst[6] = {p.net.b1, p.net.ln1_w, p.net.ln1_b, p.net.b2, p.net.ln2_w, p.net.ln2_b};
-        int64_t off[3];
         float gv[3], pv[3], tv[3];
 #pragma unroll
-        for (int u = 0; u < 3; ++u) {  // 6 * 128 = 3 * 256 elements
+        for (int u = 0; u < 3; ++u) {
             const int t = tid + 256 * u, v = t / HID, j = t % HID;
             float sum = 0.0f;
+#pragma unroll
             for (int qq = 0; qq < GRG; ++qq) sum += part[qq][v][j];
             gv[u] = sum;
-            off[u] = (dst[v] + k * HID + j) - p.p0;
         }
-        adam_n<3>(p, sc, off, gv, 3, soft, pv, tv);
+        adam_store(p, get_sc(), off, gv, 3, soft, ain, pv, tv);
         return;
     }
     if (type == 4) {  // W3 = h2^T g3, b3, the loss
         const int k = b, out = p.out;
         const int64_t base = (int64_t)k * B * HID;
+        // slot u < NW3 - 1: W3 element tid + 256 u (when < HID * out); the last slot: b3[tid] (tid < out);
+        // unused slots point at b3[0] of agent k
+        constexpr int NW3 = (HID * NA + 255) / 256 + 1;
+        int64_t off[NW3];
+        uint32_t valid = 0;
+#pragma unroll
+        for (int u = 0; u < NW3; ++u) {
+            const int t = tid + 256 * u;
+            off[u] = (p.net.b3 + k * out) - p.p0;
+            if (u < NW3 - 1 && t < HID * out) {
+                off[u] = (p.net.w3 + ((int64_t)k * HID + t / out) * out + t % out) - p.p0;
+                valid |= 1u << u;
+            }
+        }
+        if (tid < out) {
+            off[NW3 - 1] = (p.net.b3 + k * out + tid) - p.p0;
+            valid |= 1u << (NW3 - 1);
+        }
+        AdamIn<NW3> ain;
+        adam_load(p, off, soft, ain);
         float acc[8][NA];
 #pragma unroll
         for (int i = 0; i < 8; ++i)
@@ -2058,35 +2202,22 @@ __device__ __forceinline__ void dgrads_body(const DGrad &p) {
         }
         __syncthreads();
         {
-            constexpr int NW3 = (HID * NA + 255) / 256 + 1;  // this thread's W3 elements + its b3 element
-            int64_t off[NW3];
             float gv[NW3], pv[NW3], tv[NW3];
-            int nv = 0;
-#pragma unroll
-            for (int u = 0; u < NW3; ++u) {  // unused entries: a valid element (b3[0] of agent k)
-                off[u] = (p.net.b3 + k * out) - p.p0;
-                gv[u] = 0.0f;
-            }
 #pragma unroll
             for (int u = 0; u < NW3 - 1; ++u) {
-                const int t = tid + 256 * u;
-                if (t < HID * out) {
-                    const int j = t / out, a = t % out;
-                    float sum = 0.0f;
-                    for (int qq = 0; qq < GRG; ++qq) sum += part[qq][j][a];
-                    gv[nv] = sum;
-                    off[nv] = (p.net.w3 + ((int64_t)k * HID + j) * out + a) - p.p0;
-                    ++nv;
-                }
-            }
-            if (tid < out) {
+                const int t = min(tid + 256 * u, HID * out - 1);
                 float sum = 0.0f;
-                for (int qq = 0; qq < GRG; ++qq) sum += pb[qq][tid];
-                gv[nv] = sum;
-                off[nv] = (p.net.b3 + k * out + tid) - p.p0;
-                ++nv;
+#pragma unroll
+                for (int qq = 0; qq < GRG; ++qq) sum += part[qq][t / out][t % out];
+                gv[u] = sum;
             }
-            adam_n<NW3>(p, sc, off, gv, nv, soft, pv, tv);
+            {
+                float sum = 0.0f;
+#pragma unroll
+                for (int qq = 0; qq < GRG; ++qq) sum += pb[qq][min(tid, out - 1)];
+                gv[NW3 - 1] = sum;
+            }
+            adam_store_m(p, get_sc(), off, gv, valid, soft, ain, pv, tv);
         }
         if (tid == 64) {
             float sum = 0.0f;
@@ -2135,7 +2266,7 @@ struct DPrime {
     int start[5];
 };
 __global__ void __launch_bounds__(256) dprime(DPrime p) {
-    __shared__ float s_base[CG], s_pp[2][HID];
+    __shared__ float s_base[CG], s_pp[4][HID];
     int b = blockIdx.x, net = 0;
     while (net < 3 && b >= p.start[net + 1]) ++net;
     b -= p.start[net];
@@ -2148,13 +2279,15 @@ __global__ void __launch_bounds__(256) dprime(DPrime p) {
     if (tid < ncell) s_base[tid] = p.base[c0 + tid];
     __syncthreads();
     const float *wk = p.net[net].w1 + ((int64_t)k * in_dim + (int64_t)ob * HW + c0) * HID + j;
-    float pp = 0.0f;
-    for (int cc = h; cc < ncell; cc += 2) pp = fmaf(s_base[cc], wk[(int64_t)cc * HID], pp);
-    s_pp[h][j] = pp;
+    for (int q = h; q < 4; q += 2) {  // chains q: cells q, q + 4, .. (the update's order)
+        float pp = 0.0f;
+        for (int cc = q; cc < ncell; cc += 4) pp = fmaf(s_base[cc], wk[(int64_t)cc * HID], pp);
+        s_pp[q][j] = pp;
+    }
     __syncthreads();
     if (tid < HID) {
         const int64_t gi = critic ? ((int64_t)k * K * NG + ob * NG + grp) : ((int64_t)k * NG + grp);
-        p.w.cpart[net][gi * HID + tid] = s_pp[0][tid] + s_pp[1][tid];
+        p.w.cpart[net][gi * HID + tid] = ((s_pp[0][tid] + s_pp[1][tid]) + s_pp[2][tid]) + s_pp[3][tid];
     }
 }
 
@@ -2554,7 +2687,7 @@ gw_status gw_maddpg_desc_update(const gw_obs_source *src, const gw_desc_ring *ri
     g.out = 1;
     g.stamp = sb ? sb + STAMP_BLOCKS * NSTAMP : nullptr;
     {
-        const int n[7] = {K * K * NG, K * ((NA * K + 7) / 8), K * (HID / RB), K, K, 0, 0};
+        const int n[7] = {2 * K * K * NG, K * ((NA * K + 7) / 8), K * (HID / RB), K, K, 0, 0};
         g.start[0] = 0;
         for (int i = 0; i < 7; ++i) g.start[i + 1] = g.start[i] + n[i];
     }
@@ -2586,7 +2719,7 @@ gw_status gw_maddpg_desc_update(const gw_obs_source *src, const gw_desc_ring *ri
     g.stamp = sb ? sb + 3 * STAMP_BLOCKS * NSTAMP : nullptr;
     const int g0blocks = g.start[7];
     {
-        const int n[7] = {K * NG, 0, K * (HID / RB), K, K, K * K * NG, g.nrest};
+        const int n[7] = {2 * K * NG, 0, K * (HID / RB), K, K, K * K * NG, g.nrest};
         g.start[0] = 0;
         for (int i = 0; i < 7; ++i) g.start[i + 1] = g.start[i] + n[i];
     }

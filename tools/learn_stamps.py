@@ -13,7 +13,7 @@ import numpy as np
 NAMES = ["dcritic_tail", "dgrads_adam(critic)", "dactor_tail", "dgrads_adam(actor)"]
 TICK_US = 0.01
 NS = 16  # stamps per block (slot 15: the block type)
-TAIL_ORDER = {0: [0, 1, 2, 3, 4, 5], 2: [0, 1, 2, 6, 7, 8, 9, 3, 10, 11, 4, 5]}
+TAIL_ORDER = {0: [0, 11, 14, 12, 13, 1, 6, 7, 8, 2, 9, 10, 3, 4, 5], 2: [0, 1, 2, 6, 7, 8, 9, 3, 10, 11, 4, 5]}
 
 
 def read(path):
@@ -56,7 +56,7 @@ def main():
             types = np.zeros(len(a), dtype=np.int64) if tail else a[:, 15]
             for ty in np.unique(types):
                 sel = a[types == ty]
-                slots = TAIL_ORDER[l] if tail else ([0, 3, 1, 4, 2] if ty == 0 else [0, 3, 4, 5, 2] if ty == 1 else [0, 2])
+                slots = TAIL_ORDER[l] if tail else ([0, 5, 6, 3, 1, 2] if ty == 0 else [0, 3, 4, 5, 2] if ty == 1 else [0, 2])
                 per[int(ty)].append([np.median((sel[:, s] - t0)) * TICK_US for s in slots] +
                                     [np.max(sel[:, end_slot] - t0) * TICK_US, len(sel)])
         print(f"{NAMES[l]}: span {np.median(span):.2f} us")
@@ -69,7 +69,7 @@ def main():
         end_slot = 5 if tail else 2
         i = int(np.argmax(a[:, end_slot]))
         t0 = a[:, 0].min()
-        order = TAIL_ORDER[l] if tail else [0, 3, 1, 4, 2]
+        order = TAIL_ORDER[l] if tail else [0, 5, 6, 3, 1, 2]
         print(f"   slowest block {i} (type {a[i, 15] if not tail else 0}): " +
               " ".join(f"{(a[i, s] - t0) * TICK_US:.2f}" for s in order))
 
