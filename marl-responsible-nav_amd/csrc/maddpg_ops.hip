@@ -897,9 +897,9 @@ struct DWs {
     float *probs;      // [K][B][9] the actor phase's fresh probabilities
     float *rw, *t1;    // [K][B] f32(reward), 1 - termination
     Saved sv;          // per-row activations and gradients (critic phase, then the actor's)
-    float *spart;      // [K][B / 16][128] column sums of dZ1 per 16-row tile
     float *cpart[4];   // c1 partials: actor [K][NG][128], actor target, critic [K][K NG][128], critic target
     int32_t *snap;     // [4] the Adam step counts of this update (critic, actor)
+    float *adsc;       // [4] this update's Adam scalars (step size, sqrt(bias correction 2)): critic, actor
 };
 
 inline int64_t rnd4(int64_t n) { return (n + 3) & ~(int64_t)3; }
@@ -922,18 +922,18 @@ inline DWs dws_layout(float *w, int K, int B, int HW) {
     for (float **q : f) *q = take((int64_t)K * B * HID);
     d.sv.g3 = take((int64_t)K * B * NA);
     d.sv.aux = take((int64_t)K * B);
-    d.spart = take((int64_t)K * (B / RB) * HID);
     d.cpart[0] = take((int64_t)K * NG * HID);
     d.cpart[1] = take((int64_t)K * NG * HID);
     d.cpart[2] = take((int64_t)K * K * NG * HID);
     d.cpart[3] = take((int64_t)K * K * NG * HID);
     d.snap = reinterpret_cast<int32_t *>(take(4));
+    d.adsc = take(4);
     return d;
 }
 int64_t dws_floats(int K, int B, int HW) {
     float *z = nullptr;
     const DWs d = dws_layout(z, K, B, HW);
-    return (int64_t)(reinterpret_cast<float *>(d.snap) - z) + 4;
+    return (int64_t)(d.adsc - z) + 4;
 }
 
 // obs value of agent n in RL agent k's observation (the obs writer's rule, gridenv.hip agent_value)
@@ -1015,6 +1015,24 @@ __device__ __forceinline__ float d_sum_parts(const float *p, int n) {
             if (g + i < n) acc += v[i];
     }
     return acc;
+}
+
+// two such sums (p1 over n1 partials, p2 over n2), every load of a 32-partial batch of both in flight
+__device__ __forceinline__ void d_sum_parts2(const float *p1, int n1, const float *p2, int n2, float &s1, float &s2) {
+    s1 = s2 = 0.0f;
+    for (int g = 0; g < max(n1, n2); g += 32) {
+        float v1[32], v2[32];
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+            v1[i] = p1[(int64_t)(g + i < n1 ? g + i : 0) * HID];
+            v2[i] = p2[(int64_t)(g + i < n2 ? g + i : 0) * HID];
+        }
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+            if (g + i < n1) s1 += v1[i];
+            if (g + i < n2) s2 += v2[i];
+        }
+    }
 }
 
 // Gumbel uniforms of (agent kk, row r) in phase ph: Philox(seed; r, c, 'GUM' + ph, 4 kk + j)
@@ -1213,6 +1231,17 @@ __device__ __forceinline__ Mlp staged(Mlp m, const float *sp, int out) {
     return m;
 }
 
+// a network's small parameters as segments of 32 float4 (segment s < 5: ln1 w, ln1 b, b2, ln2 w,
+// ln2 b; 5 .. 5 + out - 1: W3's 128-float rows of 4-output groups... i.e. W3 in 128-float pieces)
+// into its slot at s * 128 (b3 apart: stage_b3).  Every source piece is 16-byte aligned (the flat
+// buffer's [K][128] and [K][128][out] views).
+__device__ __forceinline__ int stage_segs(int out) { return 5 + out; }
+__device__ __forceinline__ const float4 *stage_seg_src(const Mlp &m, int sg, int lane) {
+    const float *src = sg == 0 ? m.lw1 : sg == 1 ? m.lb1 : sg == 2 ? m.b2 : sg == 3 ? m.lw2 : sg == 4 ? m.lb2
+                                                                              : m.w3 + (sg - 5) * HID;
+    return reinterpret_cast<const float4 *>(src) + lane;
+}
+
 // GW_LEARN_STAMP=<file> (diagnostics): each block's thread 0 writes wall_clock64() stamps at its
 // phase boundaries into slots [block][0..14] (slot 15: the block type); the host appends them to <file>
 constexpr int NSTAMP = 16;
@@ -1231,9 +1260,20 @@ struct DTail {
     uint64_t seed;
     const int32_t *ctr;          // the draws' counter: the critic optimizer's step count
     const int32_t *count;        // the optimizer count this phase snapshots (critic / actor)
+    double lr, beta1, beta2;     //   and that optimizer's hyper-parameters (its Adam scalars)
     float gamma;
     int K, B, NG;
 };
+
+// this update's step count of the phase's optimizer and its Adam scalars in torch's double forms
+// (lr / (1 - beta1^s), sqrt(1 - beta2^s)), once per update for every gradient block (one thread
+// of a tail block, on a wave the prologue leaves light)
+__device__ __forceinline__ void d_snapshot(const DTail &p, int phase) {
+    const int32_t s = p.count[0] + 1;
+    p.w.snap[phase] = s;
+    p.w.adsc[2 * phase] = (float)(p.lr / (1.0 - pow(p.beta1, (double)s)));
+    p.w.adsc[2 * phase + 1] = (float)sqrt(1.0 - pow(p.beta2, (double)s));
+}
 
 __global__ void __launch_bounds__(DT) dcritic_tail(DTail p) {
     __shared__ __attribute__((aligned(16))) float s_in[2][RB * HP];
@@ -1256,21 +1296,44 @@ __global__ void __launch_bounds__(DT) dcritic_tail(DTail p) {
     // probabilities, rewards and c1 sums -- whose round trips overlap; the parameters reach LDS last
     const int64_t t_now = p.q.t_dev[0];
     const uint32_t c = (uint32_t)p.ctr[0];
-    const int na_ = stage_size(NA), nc_ = stage_size(1), tot = K * na_ + 2 * nc_;
-    auto par_src = [&](int o) -> float {
-        if (o < K * na_) return stage_src(mlp_k(p.at, o / na_, HW, NA), NA, o % na_);
-        const int q = o - K * na_;
-        return stage_src(mlp_k(q < nc_ ? p.ct : p.c, k, in_c, 1), 1, q % nc_);
+    // the small parameters: float4 units of 32-unit segments (stage_segs), K target actors then
+    // the critic target and the critic, by the threads past the descriptor decoders' waves (whose
+    // chain is the prologue's longest); loads first, stores at the end of the prologue
+    const int sa = stage_segs(NA), sc1 = stage_segs(1), nseg = K * sa + 2 * sc1, nunit = 32 * nseg;
+    auto unit_net = [&](int v, int &net, int &sg) {
+        const int g = v >> 5;
+        if (g < K * sa) {
+            net = g / sa;
+            sg = g - net * sa;
+        } else {
+            net = K + (g - K * sa) / sc1;
+            sg = (g - K * sa) - (net - K) * sc1;
+        }
     };
-    auto par_dst = [&](int o) -> float * {
-        return o < K * na_ ? &s_par[o / na_][o % na_] : &s_par[K + (o - K * na_) / nc_][(o - K * na_) % nc_];
+    auto unit_src = [&](int v) -> const float4 * {
+        int net, sg;
+        unit_net(v, net, sg);
+        const Mlp m = net < K ? mlp_k(p.at, net, HW, NA) : mlp_k(net == K ? p.ct : p.c, k, in_c, 1);
+        return stage_seg_src(m, sg, v & 31);
     };
-    constexpr int NSV = 16;
-    float sv[NSV];
+    auto unit_dst = [&](int v) -> float4 * {
+        int net, sg;
+        unit_net(v, net, sg);
+        return reinterpret_cast<float4 *>(&s_par[net][sg * HID]) + (v & 31);
+    };
+    const int nsd = (RB * 2 * K + 63) / 64 * 64, sid = tid - nsd, sstride = DT - nsd;
+    constexpr int NSV = 4;
+    float4 sv[NSV];
 #pragma unroll
     for (int u = 0; u < NSV; ++u) {
-        const int o = tid + u * DT;
-        sv[u] = o < tot ? par_src(o) : 0.0f;
+        const int v = sid + u * sstride;
+        sv[u] = (sid >= 0 && v < nunit) ? *unit_src(v) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+    // b3 (out floats per network, not 16-byte aligned): the last threads
+    float b3v = 0.0f;
+    const int nb3 = K * NA + 2, tb3 = tid - (DT - nb3);
+    if (tb3 >= 0) {
+        b3v = tb3 < K * NA ? p.at.b3[(tb3 / NA) * NA + tb3 % NA] : (tb3 == K * NA ? p.ct.b3[k] : p.c.b3[k]);
     }
     if (tid < 256) {
         // the rows' descriptors -> patched cells: one thread per (row, state | next state, agent obs)
@@ -1309,16 +1372,30 @@ __global__ void __launch_bounds__(DT) dcritic_tail(DTail p) {
     } else {
         const int t2 = tid - 256;
         // c1 of the networks this block runs: the K target actors, critic target k, critic k
-        for (int o = t2; o < (K + 2) * HID; o += 256) {
+        // (two sums per pass: both sums' partial loads in flight together)
+        auto c1_src = [&](int o, const float *&pp, int &n, float &b) {
             const int net = o / HID, j = o % HID;
-            float v;
-            if (net < K)
-                v = p.at.b1[net * HID + j] + d_sum_parts(p.w.cpart[1] + (int64_t)net * p.NG * HID + j, p.NG);
-            else if (net == K)
-                v = p.ct.b1[k * HID + j] + d_sum_parts(p.w.cpart[3] + (int64_t)k * K * p.NG * HID + j, K * p.NG);
-            else
-                v = p.c.b1[k * HID + j] + d_sum_parts(p.w.cpart[2] + (int64_t)k * K * p.NG * HID + j, K * p.NG);
-            s_c1[net][j] = v;
+            if (net < K) {
+                pp = p.w.cpart[1] + (int64_t)net * p.NG * HID + j;
+                n = p.NG;
+                b = p.at.b1[net * HID + j];
+            } else {
+                pp = p.w.cpart[net == K ? 3 : 2] + (int64_t)k * K * p.NG * HID + j;
+                n = K * p.NG;
+                b = (net == K ? p.ct.b1 : p.c.b1)[k * HID + j];
+            }
+        };
+        for (int o = t2; o < (K + 2) * HID; o += 512) {
+            const int o2 = o + 256, ok2 = o2 < (K + 2) * HID;
+            const float *p1, *p2;
+            int n1, n2;
+            float b1v, b2v;
+            c1_src(o, p1, n1, b1v);
+            c1_src(ok2 ? o2 : o, p2, n2, b2v);
+            float v1, v2;
+            d_sum_parts2(p1, n1, p2, n2, v1, v2);
+            s_c1[o / HID][o % HID] = b1v + v1;
+            if (ok2) s_c1[o2 / HID][o2 % HID] = b2v + v2;
         }
         DSTAMP_T(p, 12, 256);
         // the stored action probabilities of every agent (the critic's action inputs) and agent k's
@@ -1357,12 +1434,19 @@ __global__ void __launch_bounds__(DT) dcritic_tail(DTail p) {
     }
 #pragma unroll
     for (int u = 0; u < NSV; ++u) {
-        const int o = tid + u * DT;
-        if (o < tot) *par_dst(o) = sv[u];
+        const int v = sid + u * sstride;
+        if (sid >= 0 && v < nunit) *unit_dst(v) = sv[u];
     }
-    for (int o = tid + NSV * DT; o < tot; o += DT) *par_dst(o) = par_src(o);
+    if (sid >= 0)
+        for (int v = sid + NSV * sstride; v < nunit; v += sstride) *unit_dst(v) = *unit_src(v);
+    if (tb3 >= 0) {
+        if (tb3 < K * NA)
+            s_par[tb3 / NA][5 * HID + HID * NA + tb3 % NA] = b3v;
+        else
+            s_par[K + (tb3 - K * NA)][5 * HID + HID] = b3v;
+    }
     DSTAMP(p, 14);
-    if (blockIdx.x == 0 && k == 0 && tid == 0) p.w.snap[0] = p.count[0] + 1;
+    if (blockIdx.x == 0 && k == 0 && tid == 255) d_snapshot(p, 0);
     __syncthreads();
     DSTAMP(p, 1);
     // the target actions a'_kk = GumbelSoftmax(actor_target_kk(s'_kk)), two agents at a time (a
@@ -1452,12 +1536,6 @@ __global__ void __launch_bounds__(DT) dcritic_tail(DTail p) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) s_in[1][rl * HP + 8 * g + i] = dz1[i];
     }
-    __syncthreads();
-    if (tid < HID) {  // the tile's column sums of dZ1, rows in order
-        float acc = 0.0f;
-        for (int rr = 0; rr < RB; ++rr) acc += s_in[1][rr * HP + tid];
-        p.w.spart[((int64_t)k * (B / RB) + blockIdx.x) * HID + tid] = acc;
-    }
     DSTAMP(p, 5);
 }
 
@@ -1521,7 +1599,7 @@ __global__ void __launch_bounds__(DT) dactor_tail(DTail p) {
         if (o < tot) *par_dst(o) = sv[u];
     }
     for (int o = tid + NSV * DT; o < tot; o += DT) *par_dst(o) = par_src(o);
-    if (blockIdx.x == 0 && k == 0 && tid == 0) p.w.snap[1] = p.count[0] + 1;
+    if (blockIdx.x == 0 && k == 0 && tid == DT - 1) d_snapshot(p, 1);
     __syncthreads();
     DSTAMP(p, 1);
     const Mlp ma = staged(mlp_k(p.a, k, HW, NA), s_par[0], NA);
@@ -1635,12 +1713,6 @@ __global__ void __launch_bounds__(DT) dactor_tail(DTail p) {
         }
 #pragma unroll
         for (int i = 0; i < 8; ++i) s_in[rl * HP + 8 * g + i] = dz1[i];
-    }
-    __syncthreads();
-    if (tid < HID) {
-        float acc = 0.0f;
-        for (int rr = 0; rr < RB; ++rr) acc += s_in[rr * HP + tid];
-        p.w.spart[((int64_t)k * (B / RB) + blockIdx.x) * HID + tid] = acc;
     }
     DSTAMP(p, 5);
 }
@@ -1759,7 +1831,6 @@ __device__ __forceinline__ void d_stage_rows(float *dst, const float *src, int n
 
 __device__ __forceinline__ void dgrads_body(const DGrad &p) {
     __shared__ float s_base[CG], s_pp[2][4][HID];
-    __shared__ float s_sc[2];
     __shared__ __attribute__((aligned(16))) float smem[GRG * HID * NA + GRG * (NA + 1) > RB * (TILE_R + 4) + TILE_R * HID
                                                         ? GRG * HID * NA + GRG * (NA + 1)
                                                         : RB * (TILE_R + 4) + TILE_R * HID];
@@ -1773,22 +1844,13 @@ __device__ __forceinline__ void dgrads_body(const DGrad &p) {
     while (type < 6 && b >= p.start[type + 1]) ++type;
     b -= p.start[type];
     if (p.stamp && tid == 0) p.stamp[(int64_t)blockIdx.x * NSTAMP + NSTAMP - 1] = (unsigned long long)type;
-    // this step's Adam scalars (the count the tail snapshotted; torch forms them in double):
-    // thread 0 forms them (set_sc; block 0, a W1 block, also publishes the count) and the threads
-    // read them after a later barrier (get_sc) -- not a barrier of its own in front of every
-    // block's first load
-    auto set_sc = [&]() {
-        if (tid == 0) {
-            const double s = (double)p.w.snap[p.phase];
-            s_sc[0] = (float)(p.lr / (1.0 - pow(p.beta1, s)));
-            s_sc[1] = (float)sqrt(1.0 - pow(p.beta2, s));
-            if (blockIdx.x == 0) p.count[0] = p.w.snap[p.phase];
-        }
-    };
+    // this step's Adam scalars and count, as the tail snapshotted them (d_snapshot)
+    const float sc_step = p.w.adsc[2 * p.phase], sc_bc2 = p.w.adsc[2 * p.phase + 1];
+    if (blockIdx.x == 0 && tid == 0) p.count[0] = p.w.snap[p.phase];
     auto get_sc = [&]() {
         AdamSc sc;
-        sc.step_size = s_sc[0];
-        sc.bc2 = s_sc[1];
+        sc.step_size = sc_step;
+        sc.bc2 = sc_bc2;
         sc.w1 = (float)(1.0 - p.beta1);
         sc.b2 = (float)p.beta2;
         sc.w2 = (float)(1.0 - p.beta2);
@@ -1796,7 +1858,6 @@ __device__ __forceinline__ void dgrads_body(const DGrad &p) {
         return sc;
     };
     const bool soft = p.phase == 1;
-    if (type <= 4) set_sc();  // wave 0's other loads wait behind it; the other waves' do not
     if (type == 0 || type == 5) {
         // W1 rows of one 64-cell group of one agent obs: type 0 the stepped network (gradient +
         // Adam [+ the actor target's soft update]) for one half of the features (blocks (group,
@@ -1875,17 +1936,18 @@ __device__ __forceinline__ void dgrads_body(const DGrad &p) {
         for (int i = 0; i < PI; ++i) {
             const int t = min(tid + 256 * i, NE - 1);
             const int64_t ro = (int64_t)obk * B + t / NPM;
-            npv[i] = p.w.np[ro];
-            pcv[i] = p.w.pc[ro * NPM + t % NPM];
-            dv[i] = p.w.pd[ro * NPM + t % NPM];
+            npv[i] = pcv[i] = 0;
+            dv[i] = 0.0f;
+            if (tid + 256 * i < NE) {  // (block-uniform but for the last pass: no wasted loads)
+                npv[i] = p.w.np[ro];
+                pcv[i] = p.w.pc[ro * NPM + t % NPM];
+                dv[i] = p.w.pd[ro * NPM + t % NPM];
+            }
         }
-        const int n4 = min(B, DZR) * HID / 4;
-        float4 zst[16];
-        d_stage_load(zst, p.w.sv.dz1 + (int64_t)k * B * HID, n4);
-        AdamIn<16> ain;  // issued last: the staging below does not wait for them
-        adam_load(p, off, soft, ain);
-        d_stage_store(s_dzr, zst, n4);
+        d_stage_rows(s_dzr, p.w.sv.dz1 + (int64_t)k * B * HID, min(B, DZR) * HID / 4);
         DSTAMP(p, 5);
+        AdamIn<16> ain;  // in flight under the X build and the MFMA
+        adam_load(p, off, soft, ain);
         float *s_X = smem;
         __syncthreads();  // s_base
         DSTAMP(p, 6);
@@ -1971,8 +2033,6 @@ __device__ __forceinline__ void dgrads_body(const DGrad &p) {
         float4 zst[16];
         const int n4 = min(B, DZR) * HID / 4;
         d_stage_load(zst, p.w.sv.dz1 + (int64_t)k * B * HID, n4);
-        AdamIn<4> ain;
-        adam_load(p, off, false, ain);
         float *s_a = smem;  // the rows' stored actions [B][9K] (<= 256 x 72 floats)
         for (int i0 = 0; i0 < B * na; i0 += 8 * 256) {  // 8 loads in flight, then the stores
             float v[8];
@@ -1989,6 +2049,8 @@ __device__ __forceinline__ void dgrads_body(const DGrad &p) {
         }
         d_stage_store(s_dzr, zst, n4);
         DSTAMP(p, 3);
+        AdamIn<4> ain;  // in flight under the row loop
+        adam_load(p, off, false, ain);
         float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
         for (int rc = 0; rc < B; rc += DZR) {
             const int nr = min(DZR, B - rc);
@@ -2655,6 +2717,9 @@ gw_status gw_maddpg_desc_update(const gw_obs_source *src, const gw_desc_ring *ri
     t.seed = seed;
     t.ctr = opt_critic->step;
     t.count = opt_critic->step;
+    t.lr = opt_critic->lr;
+    t.beta1 = opt_critic->beta1;
+    t.beta2 = opt_critic->beta2;
     t.gamma = gamma;
     t.K = K;
     t.B = B;
@@ -2693,6 +2758,9 @@ gw_status gw_maddpg_desc_update(const gw_obs_source *src, const gw_desc_ring *ri
     }
     gwprof::launch(dgrads_adam, dim3(g.start[7]), dim3(256), 0, s, g);
     t.count = opt_actor->step;
+    t.lr = opt_actor->lr;
+    t.beta1 = opt_actor->beta1;
+    t.beta2 = opt_actor->beta2;
     t.stamp = sb ? sb + 2 * STAMP_BLOCKS * NSTAMP : nullptr;
     gwprof::launch(dactor_tail, dim3(B / RB, K), dim3(DT), 0, s, t);
     g.net = *actor;
