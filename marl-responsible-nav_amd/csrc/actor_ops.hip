@@ -38,7 +38,9 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
+#include <cstdio>
 #include <string>
+#include <vector>
 
 #include "actor_ops.h"
 #include "prof.h"
@@ -1072,13 +1074,14 @@ constexpr int RARE_WAVES = 8, RARE_ITEMS = 16 * RARE_WAVES, RARE_BLOCKS = 256;
 // s_uo[b] = the units (RARE_ITEMS items each) before bucket b, s_uo[nb] = all units: a block scan
 // of the bucket sizes in bucket order (every rare block computes the same table)
 constexpr int RARE_MAX_NB = 2048;  // K x positions (8 agents x 16 x 16 conv-2 positions)
+template <int WAVES = RARE_WAVES, int ITEMS = RARE_ITEMS>
 __device__ __forceinline__ void block_unit_offsets(const int *bucket_n, int nb, int *s_uo, int *s_wt) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     int base = 0;
-    for (int c0 = 0; c0 < nb; c0 += 64 * RARE_WAVES) {
+    for (int c0 = 0; c0 < nb; c0 += 64 * WAVES) {
         const int i = c0 + tid;
         const int n = i < nb ? bucket_n[i] : 0;
-        const int u = (n + RARE_ITEMS - 1) / RARE_ITEMS;
+        const int u = (n + ITEMS - 1) / ITEMS;
         int incl = u;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -1089,7 +1092,7 @@ __device__ __forceinline__ void block_unit_offsets(const int *bucket_n, int nb, 
         __syncthreads();
         int before = base, tot = 0;
 #pragma unroll
-        for (int w = 0; w < RARE_WAVES; ++w) {
+        for (int w = 0; w < WAVES; ++w) {
             before += w < wave ? s_wt[w] : 0;
             tot += s_wt[w];
         }
@@ -1590,8 +1593,12 @@ __global__ void __launch_bounds__(256) wcnn_scatter(CnnParams p, Lists lists) {
 // cnn_rare_kernel over window positions: per unit (agent k, position Q) the Linear-1 block in LDS;
 // lane (item it, quarter q) rebuilds conv-1 window q of Q from the item's descriptor (map under
 // the window, -1 outside, the patched cells); rare_mfma against the base window's activations a2b.
+// (round 5) units of 64 items on 4-wave blocks, two blocks per CU: ~500 units at c4patch's ~33k
+// items for 512 resident blocks, where 128-item units on 256 eight-wave blocks left ~10 % of the
+// blocks two units (the kernel's span: two units' staging + compute)
+constexpr int WR_WAVES = 4, WR_ITEMS = 16 * WR_WAVES, WR_BLOCKS = 512;
 template <int NP>
-__global__ void __launch_bounds__(64 * RARE_WAVES) wcnn_rare_kernel(CnnParams p) {
+__global__ void __launch_bounds__(64 * WR_WAVES) wcnn_rare_kernel(CnnParams p) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int it = lane & 15, q = lane >> 4;
     const int nb = p.K * p.P, half = p.PW / 2;
@@ -1599,9 +1606,9 @@ __global__ void __launch_bounds__(64 * RARE_WAVES) wcnn_rare_kernel(CnnParams p)
     __shared__ __attribute__((aligned(16))) float s_wl[RARE_LDS_WL];   // 34 KB
     __shared__ float s_w1[C1][4], s_b1[C1], s_b2[C2];
     __shared__ uint32_t s_road[128];
-    __shared__ int s_uo[RARE_MAX_NB + 1], s_wt[RARE_WAVES];
+    __shared__ int s_uo[RARE_MAX_NB + 1], s_wt[WR_WAVES];
     if (tid < 128) s_road[tid] = p.ws.road[tid];
-    block_unit_offsets(p.ws.bucket_n, nb, s_uo, s_wt);
+    block_unit_offsets<WR_WAVES, WR_ITEMS>(p.ws.bucket_n, nb, s_uo, s_wt);
     const int nunits = s_uo[nb];
     int staged_k = -1, staged_Q = -1;
     for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
@@ -1612,15 +1619,15 @@ __global__ void __launch_bounds__(64 * RARE_WAVES) wcnn_rare_kernel(CnnParams p)
         }
         const int k = lo / p.P, Q = lo % p.P;
         const int n = p.ws.bucket_n[lo];
-        const int i_begin = (u - s_uo[lo]) * RARE_ITEMS, i_end = min(n, i_begin + RARE_ITEMS);
+        const int i_begin = (u - s_uo[lo]) * WR_ITEMS, i_end = min(n, i_begin + WR_ITEMS);
         __syncthreads();  // the previous unit is done with the LDS images
         if (k != staged_k) {
-            stage_w2(s_w2, p.ws.w2t + (size_t)k * 4 * C2 * C1, tid, 64 * RARE_WAVES);
+            stage_w2(s_w2, p.ws.w2t + (size_t)k * 4 * C2 * C1, tid, 64 * WR_WAVES);
             if (tid < C1 * 4) (&s_w1[0][0])[tid] = p.net.conv1_w[k * C1 * 4 + tid];
             if (tid < C1) s_b1[tid] = p.net.conv1_b[k * C1 + tid];
             if (tid < C2) s_b2[tid] = p.net.conv2_b[k * C2 + tid];
         }
-        if (k != staged_k || Q != staged_Q) stage_wl(s_wl, p.ws.wlt + ((size_t)k * p.P + Q) * C2 * HID, tid, 64 * RARE_WAVES);
+        if (k != staged_k || Q != staged_Q) stage_wl(s_wl, p.ws.wlt + ((size_t)k * p.P + Q) * C2 * HID, tid, 64 * WR_WAVES);
         staged_k = k;
         staged_Q = Q;
         __syncthreads();
@@ -2202,7 +2209,25 @@ gw_status gw_patch_cnn_act(void *env, int32_t P, const gw_cnn_actors *net, const
         gwprof::launch(bucket_scan, dim3(src.K * cp.P), dim3(64), 0, s, cp, lists);
         gwprof::launch(wcnn_scatter, lgrid, dim3(256), 0, s, cp, lists);
     }
-#define RARE(NP) gwprof::launch(wcnn_rare_kernel<NP>, dim3(RARE_BLOCKS), dim3(64 * RARE_WAVES), 0, s, cp)
+    static const char *stat_env = std::getenv("GW_WCNN_STAT");  // diagnostics: the buckets' sizes (synchronises)
+    if (stat_env && *stat_env && fused_list) {
+        std::vector<int> bn((size_t)src.K * cp.P);
+        if (hipStreamSynchronize(s) == hipSuccess &&
+            hipMemcpy(bn.data(), cp.ws.bucket_n, sizeof(int) * bn.size(), hipMemcpyDeviceToHost) == hipSuccess) {
+            long tot = 0, units = 0;
+            int mx = 0;
+            for (int v : bn) {
+                tot += v;
+                units += (v + WR_ITEMS - 1) / WR_ITEMS;
+                mx = std::max(mx, v);
+            }
+            std::fprintf(stderr, "wcnn buckets: %ld items (%.3f per env-agent), %ld units, max bucket %d:", tot,
+                         (double)tot / ((double)src.E * src.K), units, mx);
+            for (int b = 0; b < (int)bn.size(); ++b) std::fprintf(stderr, " %d", bn[b]);
+            std::fprintf(stderr, "\n");
+        }
+    }
+#define RARE(NP) gwprof::launch(wcnn_rare_kernel<NP>, dim3(WR_BLOCKS), dim3(64 * WR_WAVES), 0, s, cp)
     {
         gwprof::Span span(env, GW_SPAN_CNN_RARE);
         switch (src.N) {
