@@ -701,6 +701,7 @@ constexpr int C1 = 32, C2 = 64, NV = 19;  // NV: obs values of a patched cell (c
 struct CnnWs {
     Ws mlp;           // layer-2/3 MFMA images (and an unused c1)
     float *wlt;       // [K][P][64][128]  Linear-1 weight, transposed per position
+    float *wlj;       // [K][P][128][64]  (windows) the same per position, feature-major: staged as float4
     float *a2map;     // [K][P][64]       conv-2 activations of the static map
     float *pre2map;   // [K][P][64]       ... before the ReLU
     float *a1map;     // [K][P][4][32]    conv-1 activations of the map, per window
@@ -786,7 +787,12 @@ struct CnnParams {
     int ab;                   // GW_CNN_AB (measurement only): bit 0 skip the recomputed positions,
                               // bit 1 skip the table rows; windows: bit 2 list no positions
     int apples[MAXN];
+    unsigned long long *stamp = nullptr;  // GW_RARE_STAMP (diagnostics): per block [8] wall clocks
 };
+#define RSTAMP(P, i)                                                                               \
+    do {                                                                                           \
+        if ((P).stamp && threadIdx.x == 0) (P).stamp[(int64_t)blockIdx.x * 8 + (i)] = wall_clock64(); \
+    } while (0)
 
 // Linear-1 weight, transposed: wlt[k][P][o][j] = lin1_w[k][j][o P_n + P]
 __global__ void __launch_bounds__(256) cnn_prep_wlt(CnnParams p) {
@@ -796,6 +802,17 @@ __global__ void __launch_bounds__(256) cnn_prep_wlt(CnnParams p) {
         const int64_t r = i / HID;
         const int o = (int)(r % C2), P = (int)((r / C2) % p.P), k = (int)(r / (C2 * (int64_t)p.P));
         p.ws.wlt[i] = p.net.lin1_w[((int64_t)k * HID + j) * F + (int64_t)o * p.P + P];
+    }
+}
+
+// (windows) wlj[k][Q][j][o] = lin1_w[k][j][o P_n + Q]
+__global__ void __launch_bounds__(256) wcnn_prep_wlj(CnnParams p) {
+    const int64_t F = (int64_t)C2 * p.P, n = (int64_t)p.K * F * HID;
+    for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const int o = (int)(i % C2);
+        const int64_t r = i / C2;
+        const int j = (int)(r % HID), Q = (int)((r / HID) % p.P), k = (int)(r / (HID * (int64_t)p.P));
+        p.ws.wlj[i] = p.net.lin1_w[((int64_t)k * HID + j) * F + (int64_t)o * p.P + Q];
     }
 }
 
@@ -1070,6 +1087,7 @@ __global__ void __launch_bounds__(L1_ENVS) cnn_scatter(CnnParams p, Lists lists)
 // Units of work over the buckets: bucket b (= k P_n + P) holds ceil(n_b / RARE_ITEMS) units;
 // unit_off[b] = the units before bucket b (block_unit_offsets, in each rare block's LDS).
 constexpr int RARE_WAVES = 8, RARE_ITEMS = 16 * RARE_WAVES, RARE_BLOCKS = 256;
+constexpr int WR_WAVES_C = 4;  // the window rare kernel's waves per block (WR_WAVES)
 
 // s_uo[b] = the units (RARE_ITEMS items each) before bucket b, s_uo[nb] = all units: a block scan
 // of the bucket sizes in bucket order (every rare block computes the same table)
@@ -1119,6 +1137,20 @@ __device__ __forceinline__ void stage_w2(float *s_w2, const float *w2t, int tid,
     for (int i = tid; i < 4 * C2 * C1 / 4; i += nthreads) {
         const int row = i / (C1 / 4), c4 = i % (C1 / 4);
         *reinterpret_cast<float4 *>(s_w2 + row * W2R + 4 * c4) = src[i];
+    }
+}
+// ... a position's Linear-1 block from its feature-major image (wlj[j][o] -> [j][WLR]): float4
+// copies, every load of the thread in flight before its stores
+__device__ __forceinline__ void stage_wl4(float *s_wl, const float *wlj, int tid) {
+    constexpr int N4 = C2 * HID / 4, PER = N4 / (64 * WR_WAVES_C);
+    const float4 *src = reinterpret_cast<const float4 *>(wlj);
+    float4 v[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) v[u] = src[tid + u * 64 * WR_WAVES_C];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const int i = tid + u * 64 * WR_WAVES_C;
+        *reinterpret_cast<float4 *>(s_wl + (i / (C2 / 4)) * WLR + 4 * (i % (C2 / 4))) = v[u];
     }
 }
 // ... and a position's Linear-1 block (wlt[o][j] -> [j][WLR])
@@ -1282,6 +1314,7 @@ inline CnnWs wcnn_ws_layout(float *base, int K, int NQ, int HW, int64_t E) {
     w.mlp = ws_layout(base, K);
     float *f = base + cnn_mlp_floats(K);
     w.wlt = f;        f += (int64_t)K * NQ * C2 * HID;
+    w.wlj = f;        f += (int64_t)K * NQ * C2 * HID;
     w.a2map = f;      f += (int64_t)K * HW * NQ * C2;     // a2b [K][HW][NQ][64]
     w.table = f;      f += (int64_t)K * HW * HID;         // tbl [K][HW][128]
     w.w2t = f;        f += (int64_t)K * 4 * C2 * C1;
@@ -1596,9 +1629,13 @@ __global__ void __launch_bounds__(256) wcnn_scatter(CnnParams p, Lists lists) {
 // (round 5) units of 64 items on 4-wave blocks, two blocks per CU: ~500 units at c4patch's ~33k
 // items for 512 resident blocks, where 128-item units on 256 eight-wave blocks left ~10 % of the
 // blocks two units (the kernel's span: two units' staging + compute)
-constexpr int WR_WAVES = 4, WR_ITEMS = 16 * WR_WAVES, WR_BLOCKS = 512;
+constexpr int WR_WAVES = WR_WAVES_C, WR_ITEMS = 16 * WR_WAVES, WR_BLOCKS = 512;
+// buckets (agent, window position): K <= 8 x P <= 16.  The unit table sized for these (not the
+// full-grid kernel's 2,048) keeps a block at ~73 KB of LDS: two blocks per CU (at 81 KB only one
+// fitted, and half the grid waited for the first half: block starts p50 6.7 us, p75 14 us)
+constexpr int WR_MAX_NB = GW_MAX_AGENTS * 16;
 template <int NP>
-__global__ void __launch_bounds__(64 * WR_WAVES) wcnn_rare_kernel(CnnParams p) {
+__global__ void __launch_bounds__(64 * WR_WAVES, 2) wcnn_rare_kernel(CnnParams p) {  // (<= 256 VGPRs: two blocks per CU)
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int it = lane & 15, q = lane >> 4;
     const int nb = p.K * p.P, half = p.PW / 2;
@@ -1606,12 +1643,15 @@ __global__ void __launch_bounds__(64 * WR_WAVES) wcnn_rare_kernel(CnnParams p) {
     __shared__ __attribute__((aligned(16))) float s_wl[RARE_LDS_WL];   // 34 KB
     __shared__ float s_w1[C1][4], s_b1[C1], s_b2[C2];
     __shared__ uint32_t s_road[128];
-    __shared__ int s_uo[RARE_MAX_NB + 1], s_wt[WR_WAVES];
+    __shared__ int s_uo[WR_MAX_NB + 1], s_wt[WR_WAVES];
+    RSTAMP(p, 0);
     if (tid < 128) s_road[tid] = p.ws.road[tid];
     block_unit_offsets<WR_WAVES, WR_ITEMS>(p.ws.bucket_n, nb, s_uo, s_wt);
     const int nunits = s_uo[nb];
+    RSTAMP(p, 1);
+    int nu = 0;
     int staged_k = -1, staged_Q = -1;
-    for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
+    for (int u = blockIdx.x; u < nunits; u += gridDim.x, ++nu) {
         int lo = 0, hi = nb;  // the bucket holding unit u: unit_off[lo] <= u < unit_off[lo + 1]
         while (hi - lo > 1) {
             const int mid = (lo + hi) >> 1;
@@ -1627,10 +1667,11 @@ __global__ void __launch_bounds__(64 * WR_WAVES) wcnn_rare_kernel(CnnParams p) {
             if (tid < C1) s_b1[tid] = p.net.conv1_b[k * C1 + tid];
             if (tid < C2) s_b2[tid] = p.net.conv2_b[k * C2 + tid];
         }
-        if (k != staged_k || Q != staged_Q) stage_wl(s_wl, p.ws.wlt + ((size_t)k * p.P + Q) * C2 * HID, tid, 64 * WR_WAVES);
+        if (k != staged_k || Q != staged_Q) stage_wl4(s_wl, p.ws.wlj + ((size_t)k * p.P + Q) * C2 * HID, tid);
         staged_k = k;
         staged_Q = Q;
         __syncthreads();
+        if (nu == 0) RSTAMP(p, 2);
         auto map_at = [&](int c) { return ((s_road[c >> 5] >> (c & 31)) & 1u) ? 0.0f : -1.0f; };
         const int Y = Q / p.Wq, X = Q % p.Wq;
         const int b = i_begin + 16 * wave;
@@ -1688,14 +1729,18 @@ __global__ void __launch_bounds__(64 * WR_WAVES) wcnn_rare_kernel(CnnParams p) {
             base[4 * t + 2] = bq[t].z;
             base[4 * t + 3] = bq[t].w;
         }
+        if (nu == 0) RSTAMP(p, 3);
         float4 z[8];
         rare_mfma(a1, s_w2, s_wl, s_b2, base, lane, z);
+        if (nu == 0) RSTAMP(p, 4);
         if (ok) {
             float4 *zo = reinterpret_cast<float4 *>(p.ws.rare_z + ((size_t)k * p.E * RSW + item) * HID);
 #pragma unroll
             for (int j = 0; j < 8; ++j) zo[4 * j + q] = z[j];
         }
     }
+    if (p.stamp && tid == 0) p.stamp[(int64_t)blockIdx.x * 8 + 6] = (unsigned long long)nu;
+    RSTAMP(p, 5);
 }
 
 gw_status err(gw_status s, const std::string &msg) {
@@ -2137,6 +2182,7 @@ gw_status gw_patch_cnn_prepare(void *env, int32_t P, const gw_cnn_actors *net, f
     const CnnParams p = wcnn_params(src, P, net, ws);
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(cnn_prep_wlt, dim3(2048), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(wcnn_prep_wlj, dim3(2048), dim3(256), 0, s, p);
     hipLaunchKernelGGL(wcnn_prep_base, dim3((p.HW + WCG - 1) / WCG, src.K), dim3(256), 0, s, p);
     {  // (the lists' spare counter word and the fused listing's bucket counters start at 0)
         const Lists l = lists_at(p.ws.unit_off, src.K * p.P, src.K, src.E, 256);
@@ -2169,7 +2215,7 @@ gw_status gw_patch_cnn_act(void *env, int32_t P, const gw_cnn_actors *net, const
     if (!(tau > 0.0f)) return err(GW_ERR_ARG, "gw_patch_cnn_act: tau must be > 0");
     const CnnParams cp = wcnn_params(src, P, net, const_cast<float *>(ws));
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (src.K * cp.P > RARE_MAX_NB) return err(GW_ERR_ARG, "gw_patch_cnn_act: K x window positions above the rare kernels' table");
+    if (src.K * cp.P > WR_MAX_NB) return err(GW_ERR_ARG, "gw_patch_cnn_act: K x window positions above the rare kernel's table");
     // the positions to recompute, listed per (agent, position) bucket in ONE launch (round 5;
     // GW_WCNN_LIST=scan: the round-4 chain of layer-1 counts, bucket scan and scatter, A/B)
     static const char *list_env = std::getenv("GW_WCNN_LIST");
@@ -2227,7 +2273,13 @@ gw_status gw_patch_cnn_act(void *env, int32_t P, const gw_cnn_actors *net, const
             std::fprintf(stderr, "\n");
         }
     }
-#define RARE(NP) gwprof::launch(wcnn_rare_kernel<NP>, dim3(WR_BLOCKS), dim3(64 * WR_WAVES), 0, s, cp)
+    static const char *rstamp_env = std::getenv("GW_RARE_STAMP");  // diagnostics: block stamps (synchronises)
+    static unsigned long long *rstamp = nullptr;
+    if (rstamp_env && *rstamp_env && !rstamp && hipMalloc(&rstamp, sizeof(unsigned long long) * WR_BLOCKS * 8) != hipSuccess)
+        rstamp = nullptr;
+    CnnParams cps = cp;
+    cps.stamp = rstamp;
+#define RARE(NP) gwprof::launch(wcnn_rare_kernel<NP>, dim3(WR_BLOCKS), dim3(64 * WR_WAVES), 0, s, cps)
     {
         gwprof::Span span(env, GW_SPAN_CNN_RARE);
         switch (src.N) {
@@ -2242,6 +2294,16 @@ gw_status gw_patch_cnn_act(void *env, int32_t P, const gw_cnn_actors *net, const
         }
     }
 #undef RARE
+    if (rstamp) {
+        std::vector<unsigned long long> h((size_t)WR_BLOCKS * 8);
+        if (hipStreamSynchronize(s) == hipSuccess &&
+            hipMemcpy(h.data(), rstamp, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost) == hipSuccess) {
+            if (FILE *f = std::fopen(rstamp_env, "ab")) {
+                std::fwrite(h.data(), sizeof(unsigned long long), h.size(), f);
+                std::fclose(f);
+            }
+        }
+    }
     ActParams p{};
     p.net = cnn_tail(net);
     p.c1 = cp.ws.mlp.c1;

@@ -223,11 +223,13 @@ class Rollout:
         # descriptors, not the windows, so the window writer of step t overlaps actor t+1; the
         # world update of step t+1 (which rewrites the descriptors) waits for it, and fence()
         # orders the ring slots for readers (GW_PATCH_ASYNC=0: on the caller's stream)
-        if patch_async is None:  # default: the CNN head (several short kernels the writer fits
-            # beside: c4patch 203 -> 184 us per step); the MLP head's one-block-per-CU actor loses
-            # more CUs to the writer than the overlap hides (c5patch 142 -> 148), profiles/r3_s2
+        if patch_async is None:  # default: on the caller's stream.  Round 3 put the CNN head's writer
+            # beside it (c4patch 203 -> 184 us per step, profiles/r3_s2); since the round-5 row writer
+            # (29 us alone at c4patch) the side stream costs more than it hides: its blocks take the
+            # CU slots the rare kernel's two-blocks-per-CU grid needs (c4patch 156.7 beside vs 150.2
+            # serial, profiles/r5_window); the MLP head's one-block-per-CU actor never gained from it
             env_pa = os.environ.get("GW_PATCH_ASYNC")
-            patch_async = (env_pa != "0") if env_pa is not None else getattr(actors, "arch", "") == "cnn"
+            patch_async = env_pa is not None and env_pa != "0"
         self.patch_async = (bool(patch_async) and bool(self.patch) and self.fused and self.replay is not None
                             and env.device.type == "cuda")
         if self.patch_async:
