@@ -415,9 +415,11 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a, unsign
 // ~6 us per block on a dependent staging phase with none of that block's stores in flight, and at
 // c4patch ran at ~3 TB/s alone (45 us; the launch shape's store floor, GW_PATCH_MODE=9: 18 us).
 // Terminal windows (D_FINAL) take the same path from the descriptor's terminal words.
-constexpr int WR_RUNS = 4;  // runs of 64 rows per wave
+// WR_RUNS runs of 64 rows per wave (1 or 2 measured slower: 36.3 / 30.5 vs 29.4 us at c4patch's
+// shape; the body needs ~100 VGPRs at any run count, so fewer runs only lose the batched loads)
+constexpr int WR_RUNS = 4;
 template <int NP>
-__global__ void __launch_bounds__(256) window_rows_kernel(gw::PatchArgs a) {
+__global__ void __launch_bounds__(256, 4) window_rows_kernel(gw::PatchArgs a) {
     constexpr int MAXW = 16;  // P <= 16
     __shared__ __attribute__((aligned(16))) float4 s_rows[4][64 * (MAXW / 4)];  // per wave: 64 rows
     const int P = a.P, W = a.W, H = a.H, half = P / 2, k = blockIdx.y, P4 = P / 4, N4 = 16 * P;  // N4: the run's float4

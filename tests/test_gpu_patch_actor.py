@@ -99,7 +99,7 @@ def test_fused_patch_rollout_matches_torch_rollout_without_noise():
     for t in range(25):
         r0, r1 = ros[0].step(), ros[1].step()
         assert torch.equal(r0.shaped, r1.shaped) and torch.equal(r0.done, r1.done), t
-        ros[0].fence()  # the fused rollout writes its windows on a side stream (patch_async)
+        ros[0].fence()  # (orders the window writer for the readers below)
         assert torch.equal(ros[0].replay.obs, ros[1].replay.obs), t
         torch.testing.assert_close(ros[0].replay.probs, ros[1].replay.probs, rtol=0, atol=2e-5)
     for e in envs:
@@ -108,7 +108,7 @@ def test_fused_patch_rollout_matches_torch_rollout_without_noise():
 
 @pytest.mark.parametrize("scenario,P", [("grid32", 11), ("grid64_n8", 16)])
 def test_async_window_writer_equals_sync(scenario, P):
-    """Rollout(patch=P) with the window writer on a side stream (patch_async, the default) ==
+    """Rollout(patch=P) with the window writer on a side stream (patch_async=True; GW_PATCH_ASYNC=1) ==
     the same rollout with the writer on the caller's stream: every ring slot (windows, terminal
     windows, probs, rewards, dones) after fence(), training mode (Philox noise), a ragged E."""
     from marlnav.rollout import Rollout

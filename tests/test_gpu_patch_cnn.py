@@ -123,7 +123,7 @@ def test_fused_patch_cnn_rollout_matches_torch_rollout_without_noise():
     for t in range(25):
         r0, r1 = ros[0].step(), ros[1].step()
         assert torch.equal(r0.shaped, r1.shaped) and torch.equal(r0.done, r1.done), t
-        ros[0].fence()  # the fused rollout writes its windows on a side stream (patch_async)
+        ros[0].fence()  # (orders the window writer for the readers below)
         assert torch.equal(ros[0].replay.obs, ros[1].replay.obs), t
         torch.testing.assert_close(ros[0].replay.probs, ros[1].replay.probs, rtol=0, atol=5e-5)
     for e in envs:
