@@ -10,7 +10,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KIND = {"gw::obs_kernel": "obs_kernel", "gw::step_v2": "step_kernel", "gw::fear_v2": "fear_kernel",
         "gw::step_obs": "step_obs", "act_kernel": "act_kernel", "window_kernel": "window_kernel",
         "wcnn_rare_kernel": "cnn_rare_kernel", "cnn_rare_kernel": "cnn_rare_kernel",
-        "wcnn_l1_kernel": "cnn_l1_kernel", "cnn_l1_kernel": "cnn_l1_kernel"}
+        "wcnn_l1_kernel": "cnn_l1_kernel", "cnn_l1_kernel": "cnn_l1_kernel",
+        "window_rows_kernel": "window_kernel", "wcnn_list_kernel": "cnn_l1_kernel",
+        # the descriptor learner: one update = dcritic_tail + dgrads_adam x 2 + dactor_tail
+        "dcritic_tail": "learn_update", "dactor_tail": "learn_update", "dgrads_adam": "learn_update"}
+# kinds made of several kernels: per launch of the first kernel (one per update), the kernels' time summed
+MULTI = {"learn_update": "dcritic_tail"}
 
 
 STEP_KERNELS = ("gw::step_v2", "gw::step_obs", "gw::step_kernel_fear", "gw::step_kernel_nofear")
@@ -21,8 +26,19 @@ def main(tag, config, cmd=None):
     # steps in the traced run: the world-update kernel runs once per step
     steps = max((v["calls"] for n, v in s.items() if n.split("<")[0].strip() in STEP_KERNELS), default=0) or None
     kernels = {}
+    for kind, lead in MULTI.items():
+        parts = {n: v for n, v in s.items() if KIND.get(n.split("<")[0].strip()) == kind}
+        lv = next((v for n, v in parts.items() if lead in n), None)
+        if lv and lv.get("calls"):
+            tot_us = sum(v["avg_us"] * v["calls"] for v in parts.values())
+            busy = sum((v.get("busy_us") or v["avg_us"]) * v["calls"] for v in parts.values())
+            k = {"avg_us": tot_us / lv["calls"], "calls": lv["calls"], "busy_us": busy / lv["calls"],
+                 "kernels": sorted(parts)}
+            kernels[kind] = k
     for name, v in s.items():
         kind = KIND.get(name.split("<")[0].strip())
+        if kind in MULTI:
+            continue
         if kind and (v.get("hbm_mb") is not None or v.get("busy_us") or v.get("valu_insts")):
             k = {"avg_us": v["avg_us"], "calls": v.get("calls")}
             if v.get("hbm_mb") is not None:
