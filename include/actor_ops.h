@@ -53,6 +53,20 @@ int64_t gw_actor_workspace_floats(int32_t in_dim, int32_t K);
  * it again after every change of the parameters (optimizer step, load); ws 16-byte aligned. */
 gw_status gw_actor_prepare(void *env, const gw_mlp_actors *net, float *ws, void *stream);
 
+/* The parts of a gw_actor_prepare workspace a learner may write directly after its actor update
+ * (gw_maddpg_desc_update_img), instead of a gw_actor_prepare launch pair: the map . W1 row slices
+ * (slice sl = rows [32 sl, 32 sl + 32), an f32 fma chain in row order from 0 -- gw_actor_act sums
+ * them in slice order onto b1) and the MFMA-operand images of W2 (f32 and bf16x3) and W3. */
+typedef struct {
+    float *part;     /* [K][nslices][128] */
+    int32_t nslices; /* ceil(in_dim / 32) */
+    float *w2img;    /* [K][128 * 128] */
+    void *w2bimg;    /* [K][3 * 8 * 4 * 64 * 4] u32: the bf16x3 image */
+    float *w3img;    /* [K][8 * 4 * 9 * 4] */
+} gw_actor_images;
+/* ws: a gw_actor_workspace_floats(in_dim, K) workspace. */
+gw_status gw_actor_images_view(float *ws, int32_t in_dim, int32_t K, gw_actor_images *out);
+
 /* For every env e and RL agent k, on the observation the env last wrote:
  *   logits = actor_k(obs_k);  training: logits -= log(-log(u + 1e-20) + 1e-20)  (Gumbel noise;
  *   u = uniform[k][e][a] if `uniform` is given, else Philox(seed; global env id, c, k) with

@@ -181,6 +181,16 @@ gw_status gw_maddpg_desc_update(const gw_obs_source *src, const gw_desc_ring *ri
                                 const gw_adam_buf *opt_critic, float *actor_target_flat, float *critic_target_flat,
                                 float gamma, float tau, int32_t B, uint64_t seed, float *ws, float *actor_loss,
                                 float *critic_loss, void *prof_env, void *stream);
+/* gw_maddpg_desc_update that also leaves the stepped actor's gw_actor_act workspace parts (img,
+ * from gw_actor_images_view of the workspace gw_actor_act reads; NULL = none): the row slices from
+ * the actor W1 blocks, the W2 / W3 images from the blocks that step those layers -- the values
+ * gw_actor_prepare would derive, bit for bit, without its two launches after the update. */
+gw_status gw_maddpg_desc_update_img(const gw_obs_source *src, const gw_desc_ring *ring, const gw_mlp_actors *actor,
+                                    const gw_mlp_actors *actor_target, const gw_mlp_actors *critic,
+                                    const gw_mlp_actors *critic_target, const gw_adam_buf *opt_actor,
+                                    const gw_adam_buf *opt_critic, float *actor_target_flat, float *critic_target_flat,
+                                    float gamma, float tau, int32_t B, uint64_t seed, float *ws, float *actor_loss,
+                                    float *critic_loss, const gw_actor_images *img, void *prof_env, void *stream);
 #ifdef __cplusplus
 }
 #endif

@@ -153,6 +153,8 @@ struct ActParams {
     int apples[MAXN];
     int *zero_n;              // null, or counters this launch zeroes (the window CNN's bucket sizes,
     int zero_cnt;             //   read by the rare kernel before it), zero_cnt <= 64 * WAVES
+    const float *c1_part;     // non-null: c1 = b1 + these [K][c1_nslices][128] slices in slice order
+    int c1_nslices;           //   (prep_images' sum; a learner may leave the slices, not c1)
 };
 
 // GW_ACT_AB bit 3 (measurement only): wave 0 of each block stamps s_memtime at its phase
@@ -347,7 +349,22 @@ __global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
         for (int i = 0; i < R; ++i) s_w2[i * THREADS + tid] = r[i];
         for (int i = tid; i < W3IMG / 4; i += THREADS) s_w3[i] = p.w3img[(size_t)k * (W3IMG / 4) + i];
         if (tid < HID) {
-            s_vec[0][tid] = p.c1[k * HID + tid];
+            if (p.c1_part) {  // prep_images' c1: b1 + the slices, 8 loads in flight, added in order
+                float part = 0.0f;
+                const float *ps = p.c1_part + (size_t)k * p.c1_nslices * HID + tid;
+                int sl = 0;
+                for (; sl + 8 <= p.c1_nslices; sl += 8) {
+                    float v[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) v[i] = ps[(size_t)(sl + i) * HID];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) part += v[i];
+                }
+                for (; sl < p.c1_nslices; ++sl) part += ps[(size_t)sl * HID];
+                s_vec[0][tid] = p.net.b1[k * HID + tid] + part;
+            } else {
+                s_vec[0][tid] = p.c1[k * HID + tid];
+            }
             s_vec[1][tid] = ln ? p.net.ln1_w[k * HID + tid] : 1.0f;
             s_vec[2][tid] = ln ? p.net.ln1_b[k * HID + tid] : 0.0f;
             s_vec[3][tid] = p.net.b2[k * HID + tid];
@@ -1850,6 +1867,17 @@ gw_status gw_actor_prepare(void *env, const gw_mlp_actors *net, float *ws, void 
     return GW_OK;
 }
 
+gw_status gw_actor_images_view(float *ws, int32_t in_dim, int32_t K, gw_actor_images *out) {
+    if (!ws || !out || in_dim < 1 || K < 1 || K > MAXN) return err(GW_ERR_ARG, "gw_actor_images_view: bad argument");
+    const Ws wl = ws_layout(ws, K);
+    out->part = wl.part;
+    out->nslices = (in_dim + 31) / 32;
+    out->w2img = reinterpret_cast<float *>(wl.w2);
+    out->w2bimg = reinterpret_cast<void *>(wl.w2b);
+    out->w3img = reinterpret_cast<float *>(wl.w3);
+    return GW_OK;
+}
+
 }  // extern "C"
 
 namespace {
@@ -1873,6 +1901,10 @@ gw_status actor_act(const char *who, void *env, int32_t P, const gw_mlp_actors *
     p.w2img = wl.w2;
     p.w3img = wl.w3;
     p.w2bimg = wl.w2b;
+    if (P == 0) {  // c1 from the row slices (gw_actor_prepare's or a learner's: gw_actor_images)
+        p.c1_part = wl.part;
+        p.c1_nslices = (src.H * src.W + 31) / 32;
+    }
     p.desc = src.desc;
     p.base = src.base;
     p.mask = mask;

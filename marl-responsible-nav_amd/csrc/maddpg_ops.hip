@@ -1735,7 +1735,40 @@ struct DGrad {
     float *loss;                 // [K]
     int phase, K, B, HW, NG, nobs, in_dim, out, nrest;
     int start[8];                // first block of each block type (7 types)
+    gw_actor_images img;         // phase 1, img.part non-null: the fused actor's workspace parts
 };
+
+// ---- the fused actor's workspace parts (actor_ops.hip prep_slices / prep_images layouts) ----------
+constexpr int AW2B_U16 = 3 * 8 * 4 * 64 * 8;  // the bf16x3 W2 image per agent, 16-bit halves
+constexpr int AW3IMG = 8 * 4 * NA * 4;        // the W3 image per agent (floats)
+__device__ __forceinline__ uint32_t a_bf16_bits(float x) {  // round to nearest even (actor_ops bf16_rn_bits)
+    const uint32_t u = __float_as_uint(x);
+    return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
+// W2 element (row, col) of agent k: its f32 image entry (w2_slot) and its three bf16x3 halves
+// (w2b_slot; the row's place in the K-block order kperm inverted)
+__device__ __forceinline__ void a_img_w2(const gw_actor_images &im, int k, int row, int col, float w) {
+    const int slot = (((col >> 4) * 8 + (row >> 4)) * 4 + ((row >> 2) & 3)) * 16 + (col & 15);
+    im.w2img[(size_t)k * HID * HID + 4 * slot + (row & 3)] = w;
+    const int kb = row >> 5, rem = row & 31, qq = (rem & 15) >> 2, j = (rem & 3) + (rem >= 16 ? 4 : 0);
+    const int lane = (qq << 4) | (col & 15), m = col >> 4, jp = j >> 1, h = j & 1;
+    const uint32_t hi = a_bf16_bits(w);
+    float r = w - __uint_as_float(hi << 16);
+    const uint32_t mi = a_bf16_bits(r);
+    r = r - __uint_as_float(mi << 16);
+    const uint32_t lo = a_bf16_bits(r);
+    uint16_t *b = static_cast<uint16_t *>(im.w2bimg) + (size_t)k * AW2B_U16;
+    const uint32_t bits[3] = {hi, mi, lo};
+#pragma unroll
+    for (int part = 0; part < 3; ++part) {
+        const int wd = jp | (lane << 2) | (kb << 8) | (m << 10) | (part << 13);
+        b[2 * wd + h] = (uint16_t)bits[part];
+    }
+}
+// W3 element (j, el) of agent k: its image entry (w3_slot, element j & 3)
+__device__ __forceinline__ void a_img_w3(const gw_actor_images &im, int k, int j, int el, float w) {
+    im.w3img[(size_t)k * AW3IMG + 4 * (((j >> 4) * 4 + ((j >> 2) & 3)) * NA + el) + (j & 3)] = w;
+}
 
 struct AdamSc {
     float step_size, bc2, w1, b2, w2, e;
@@ -1858,6 +1891,7 @@ __device__ __forceinline__ void dgrads_body(const DGrad &p) {
         return sc;
     };
     const bool soft = p.phase == 1;
+    const bool img = p.phase == 1 && p.img.part != nullptr;  // (the actor's workspace parts)
     if (type == 0 || type == 5) {
         // W1 rows of one 64-cell group of one agent obs: type 0 the stepped network (gradient +
         // Adam [+ the actor target's soft update]) for one half of the features (blocks (group,
@@ -2010,11 +2044,27 @@ __device__ __forceinline__ void dgrads_body(const DGrad &p) {
             }
             s_pp[0][q][j] = pp;
             s_pp[1][q][j] = tp;
+            if (img) {  // the new rows, for the actor workspace's row slices below
+#pragma unroll
+                for (int u = 0; u < 16; ++u)
+                    if (u < nq) s_G[cell(q, u) * HID + j] = pv[u];
+            }
         }
         __syncthreads();
         const int64_t gi = p.phase == 0 ? ((int64_t)k * K * NG + ob * NG + grp) : ((int64_t)k * NG + grp);
         cpart_out(p.phase == 0 ? 2 : 0, gi, 64 * jh, 64, 0);
         if (soft) cpart_out(1, gi, 64 * jh, 64, 1);
+        if (img && tid < 128) {  // slices 2 grp, 2 grp + 1: prep_slices' fma chain in row order
+            const int sl = tid >> 6, j2 = 64 * jh + (tid & 63);
+            if (32 * sl < ncell) {
+                float acc = 0.0f;
+                for (int i = 0; i < 32; ++i) {
+                    const int c = 32 * sl + i;
+                    if (c < ncell) acc = fmaf(s_base[c], s_G[c * HID + j2], acc);
+                }
+                p.img.part[((int64_t)k * p.img.nslices + 2 * grp + sl) * HID + j2] = acc;
+            }
+        }
         return;
     }
     if (type == 1) {  // the critic's action rows: blocks (agent, 8 rows); sum over the batch rows in order
@@ -2134,6 +2184,10 @@ __device__ __forceinline__ void dgrads_body(const DGrad &p) {
             gv[2 * i + 1] = acc1[i];
         }
         adam_store(p, get_sc(), off, gv, 8, soft, ain, pv, tv);
+        if (img) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) a_img_w2(p.img, k, d0 + 4 * lq + (i >> 1), (i & 1) ? n1 : n0, pv[i]);
+        }
         return;
     }
     const int rg = tid >> 4, g = tid & 15;
@@ -2280,6 +2334,13 @@ __device__ __forceinline__ void dgrads_body(const DGrad &p) {
                 gv[NW3 - 1] = sum;
             }
             adam_store_m(p, get_sc(), off, gv, valid, soft, ain, pv, tv);
+            if (img) {
+#pragma unroll
+                for (int u = 0; u < NW3 - 1; ++u) {
+                    const int t = tid + 256 * u;
+                    if (t < HID * out) a_img_w3(p.img, k, t / out, t % out, pv[u]);
+                }
+            }
         }
         if (tid == 64) {
             float sum = 0.0f;
@@ -2674,7 +2735,21 @@ gw_status gw_maddpg_desc_update(const gw_obs_source *src, const gw_desc_ring *ri
                                 const gw_adam_buf *opt_critic, float *actor_target_flat, float *critic_target_flat,
                                 float gamma, float tau, int32_t B, uint64_t seed, float *ws, float *actor_loss,
                                 float *critic_loss, void *prof_env, void *stream) {
+    return gw_maddpg_desc_update_img(src, ring, actor, actor_target, critic, critic_target, opt_actor, opt_critic,
+                                     actor_target_flat, critic_target_flat, gamma, tau, B, seed, ws, actor_loss,
+                                     critic_loss, nullptr, prof_env, stream);
+}
+
+gw_status gw_maddpg_desc_update_img(const gw_obs_source *src, const gw_desc_ring *ring, const gw_mlp_actors *actor,
+                                    const gw_mlp_actors *actor_target, const gw_mlp_actors *critic,
+                                    const gw_mlp_actors *critic_target, const gw_adam_buf *opt_actor,
+                                    const gw_adam_buf *opt_critic, float *actor_target_flat, float *critic_target_flat,
+                                    float gamma, float tau, int32_t B, uint64_t seed, float *ws, float *actor_loss,
+                                    float *critic_loss, const gw_actor_images *img, void *prof_env, void *stream) {
     const char *who = "gw_maddpg_desc_update";
+    if (img && (!img->part || !img->w2img || !img->w2bimg || !img->w3img || img->nslices != (src ? (src->H * src->W + 31) / 32 : -1) ||
+                (reinterpret_cast<uintptr_t>(img->w2bimg) & 3u)))
+        return fail(GW_ERR_ARG, std::string(who) + ": actor images do not match the source's grid");
     gw_status st = dsrc_ok(src, B, ws, who);
     if (st != GW_OK) return st;
     if (!ring || !ring->desc || !ring->probs || !ring->reward || !ring->term || !ring->done || !ring->t_dev ||
@@ -2784,6 +2859,7 @@ gw_status gw_maddpg_desc_update(const gw_obs_source *src, const gw_desc_ring *ri
     g.in_dim = HW;
     g.out = NA;
     g.nrest = 256;
+    if (img) g.img = *img;
     g.stamp = sb ? sb + 3 * STAMP_BLOCKS * NSTAMP : nullptr;
     const int g0blocks = g.start[7];
     {

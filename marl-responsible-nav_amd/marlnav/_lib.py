@@ -180,7 +180,8 @@ EXPORTS = ["gw_create", "gw_reset", "gw_step", "gw_state_view", "gw_copy_state",
            "gw_pipeline_state_bytes", "gw_pipeline_save", "gw_pipeline_load",
            "gw_gather_pack_scratch", "gw_gather_pack", "gw_gather_unpack_plan_cap", "gw_gather_unpack",
            "gw_adam_soft_step", "gw_obs_desc_copy", "gw_replay_gather_desc",
-           "gw_maddpg_desc_workspace_floats", "gw_maddpg_desc_prime", "gw_maddpg_desc_update", "gw_count_sims"]
+           "gw_maddpg_desc_workspace_floats", "gw_maddpg_desc_prime", "gw_maddpg_desc_update", "gw_count_sims",
+           "gw_actor_images_view", "gw_maddpg_desc_update_img"]
 
 
 class GwObsSource(C.Structure):
@@ -217,6 +218,11 @@ class GwAdamBuf(C.Structure):
                 ("beta2", C.c_double), ("eps", C.c_double)]
 
 
+class GwActorImages(C.Structure):
+    _fields_ = [("part", C.c_void_p), ("nslices", C.c_int32), ("w2img", C.c_void_p), ("w2bimg", C.c_void_p),
+                ("w3img", C.c_void_p)]
+
+
 class GwDescRing(C.Structure):
     _fields_ = [("desc", C.c_void_p), ("probs", C.c_void_p), ("reward", C.c_void_p), ("term", C.c_void_p),
                 ("done", C.c_void_p), ("t_dev", C.c_void_p), ("S", C.c_int64)]
@@ -232,6 +238,12 @@ def _declare(L):
         [C.POINTER(GwMlpActors)] * 4 + [C.POINTER(GwAdamBuf)] * 2 + [p, p, C.c_float, C.c_float, C.c_int32,
                                                                      C.c_uint64, p, p, p, p, p]
     L.gw_maddpg_desc_update.restype = C.c_int
+    L.gw_maddpg_desc_update_img.argtypes = [C.POINTER(GwObsSource), C.POINTER(GwDescRing)] + \
+        [C.POINTER(GwMlpActors)] * 4 + [C.POINTER(GwAdamBuf)] * 2 + [p, p, C.c_float, C.c_float, C.c_int32,
+                                                                     C.c_uint64, p, p, p, C.POINTER(GwActorImages), p, p]
+    L.gw_maddpg_desc_update_img.restype = C.c_int
+    L.gw_actor_images_view.argtypes = [p, C.c_int32, C.c_int32, C.POINTER(GwActorImages)]
+    L.gw_actor_images_view.restype = C.c_int
     L.gw_maddpg_workspace_floats.argtypes = [C.c_int32, C.c_int32, C.c_int32]
     L.gw_maddpg_workspace_floats.restype = C.c_int64
     L.gw_maddpg_critic_grads.argtypes = [C.POINTER(GwMlpActors)] * 4 + [C.POINTER(GwMaddpgBatch), C.c_float, p, p, p, p]

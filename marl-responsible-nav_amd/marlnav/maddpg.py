@@ -362,10 +362,30 @@ class MADDPG:
                    "gw_maddpg_desc_prime")
         self._desc_stale = False
 
-    def learn_desc(self, replay):
+    def _actor_images(self, env):
+        """The fused actor's workspace parts for ``env`` (gw_actor_images_view) when its fused MLP
+        path already acts on ``env`` (full-grid input), else None."""
+        import ctypes as C
+        st = getattr(self.actors, "_fast", None)
+        if (env is None or self.actors.arch != "mlp" or st is None or st.get("env") is not env or st.get("patch", 0)
+                or st.get("spec") is None):
+            return None
+        ws = st["ws"]
+        key = (ws.data_ptr(), env.H * env.W, self.K)
+        cached = getattr(self, "_img_view", None)
+        if cached is None or cached[0] != key:
+            im = _lib.GwActorImages()
+            _lib.check(_lib.load().gw_actor_images_view(ws.data_ptr(), env.H * env.W, self.K, C.byref(im)),
+                       "gw_actor_images_view")
+            self._img_view = cached = (key, im, ws)
+        return cached[1]
+
+    def learn_desc(self, replay, actor_env=None):
         """One whole MADDPG update sampling the descriptor ring ``replay`` in four launches
         (gw_maddpg_desc_update): the sample, both gradients with their Adam steps and both soft
-        target updates.  Returns (actor_loss [K], critic_loss [K]) device tensors."""
+        target updates.  actor_env: an env the fused MLP actor acts on; the update then also leaves
+        that actor's workspace parts (gw_maddpg_desc_update_img: row slices, W2 / W3 images), so
+        the next act_env needs no gw_actor_prepare.  Returns (actor_loss [K], critic_loss [K])."""
         import ctypes as C
         d = self._desc_setup(replay)
         if self._desc_stale:
@@ -373,14 +393,18 @@ class MADDPG:
         a, at, c, ct = d["specs"]
         oa, oc = d["adam"]
         la, lc = d["loss"]
-        _lib.check(_lib.load().gw_maddpg_desc_update(
+        im = self._actor_images(actor_env)
+        _lib.check(_lib.load().gw_maddpg_desc_update_img(
             C.byref(replay._src), C.byref(d["ring"]), C.byref(a), C.byref(at), C.byref(c), C.byref(ct), C.byref(oa),
             C.byref(oc), self.actor_targets.net.flat_params().data_ptr(), self.critic_targets.flat_params().data_ptr(),
             float(self.gamma), float(self.tau), self.batch_size, self._draw_key, d["ws"].data_ptr(), la.data_ptr(),
-            lc.data_ptr(), getattr(replay, "env_handle", None), torch.cuda.current_stream(self.device).cuda_stream),
-            "gw_maddpg_desc_update")
+            lc.data_ptr(), C.byref(im) if im is not None else None, getattr(replay, "env_handle", None),
+            torch.cuda.current_stream(self.device).cuda_stream), "gw_maddpg_desc_update")
         for net in (self.actors.net, self.critics, self.actor_targets.net, self.critic_targets):
             net.epoch += 1
+        if im is not None and not torch.cuda.is_current_stream_capturing():
+            # (inside a graph capture nothing ran yet: replay_learn marks each replay's workspace)
+            self.actors.mark_prepared(actor_env)
         return la, lc
 
     def desc_records(self, replay) -> dict:
@@ -715,11 +739,14 @@ class MADDPG:
             self.desc_prime(replay)  # outside the recording: replays then never prime
         self._prep_env = self._prep_ws = None
         self._launches = None
+        fused_prep = self._actor_images(actor_env) is not None  # the update leaves the actor's workspace
         if launches:
             rec = _lib.LaunchRecorder(torch.cuda.current_stream(self.device).cuda_stream)
             with rec:
-                self._graph_out = self.learn_desc(replay)
-                if actor_env is not None:
+                self._graph_out = self.learn_desc(replay, actor_env=actor_env)
+                if fused_prep:
+                    self._prep_ws, self._prep_env = self.actors._fast["ws"], actor_env
+                elif actor_env is not None:
                     self._prep_ws = self.actors.prepare_after_update(actor_env)
                     self._prep_env = actor_env if self._prep_ws is not None else None
             for m in (self.actors, self.actor_targets):
@@ -734,8 +761,10 @@ class MADDPG:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.stream(s):
             with torch.cuda.graph(g):
-                self._graph_out = self.learn_desc(replay)
-                if actor_env is not None:
+                self._graph_out = self.learn_desc(replay, actor_env=actor_env)
+                if fused_prep:
+                    self._prep_ws, self._prep_env = self.actors._fast["ws"], actor_env
+                elif actor_env is not None:
                     self._prep_ws = self.actors.prepare_after_update(actor_env)
                     self._prep_env = actor_env if self._prep_ws is not None else None
         torch.cuda.current_stream(self.device).wait_stream(s)

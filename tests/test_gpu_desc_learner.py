@@ -147,7 +147,9 @@ def test_desc_update_replays_bit_for_bit():
                     m.replay_learn()
         torch.cuda.synchronize()
         if mode == "launches":
-            assert [c[0] for c in m._launches.calls][0] == "gw_maddpg_desc_update"
+            calls = [c[0] for c in m._launches.calls]
+            # one call; the fused actor's workspace comes from the update itself (no prepare launches)
+            assert calls == ["gw_maddpg_desc_update_img"], calls
         states.append({k: v.clone() for k, v in m.state_dict().items()})
         env.close()
     for s in states[1:]:
@@ -174,4 +176,27 @@ def test_desc_learner_primes_after_a_load():
     torch.cuda.synchronize()
     for a, b in ((m.critics, m2.critics), (m.actors.net, m2.actors.net)):
         assert torch.equal(a.flat_params(), b.flat_params())
+    env.close()
+
+
+def test_desc_update_leaves_the_fused_actor_workspace():
+    """gw_maddpg_desc_update_img (learn_desc with the env the fused actor acts on) leaves the fused
+    actor's row slices and W2 / W3 operand images bit for bit as gw_actor_prepare derives them
+    from the updated weights, and act_env then runs without a prepare."""
+    sc, env, m, ro = _setup()
+    rp = ro.replay
+    st = m.actors._fast
+    assert st is not None and st["env"] is env
+    m.learn_desc(rp, actor_env=env)
+    assert st["key"] == m.actors._ws_key()  # marked prepared: the next act_env derives nothing
+    torch.cuda.synchronize()
+    ws_learner = st["ws"].clone()
+    m.actors._prepare(env, st)
+    torch.cuda.synchronize()
+    K, HW, HID = sc.K, sc.H * sc.W, 128
+    w2img, w3img, w2bimg = HID * HID, 8 * 4 * 9 * 4, 3 * 8 * 4 * 64 * 4
+    o_w2 = K * HID                      # (c1 first: the learner leaves it, gw_actor_act sums the slices)
+    o_end = K * (HID + w2img + w3img + w2bimg) + K * ((HW + 31) // 32) * HID
+    a, b = ws_learner[o_w2:o_end].view(torch.int32), st["ws"][o_w2:o_end].view(torch.int32)
+    assert torch.equal(a, b), int((a != b).sum())
     env.close()

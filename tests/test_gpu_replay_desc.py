@@ -118,9 +118,10 @@ def test_update_as_recorded_launches_equals_graph_replay(monkeypatch, desc_learn
     """MADDPG.capture(launches=True): the captured update re-issued as its recorded C-ABI
     launches (_lib.LaunchRecorder) == the HIP graph replay, every weight bit for bit (same
     seeds, in-kernel draws), and the replayed launches really ran (the weights moved); with the
-    descriptor learner (one gw_maddpg_desc_update call) and with the dense-row update."""
+    descriptor learner (one gw_maddpg_desc_update_img call, which also leaves the fused actor's
+    workspace: no gw_actor_prepare) and with the dense-row update."""
     monkeypatch.setenv("GW_DESC_LEARN", desc_learner)
-    first = "gw_maddpg_desc_update" if desc_learner == "1" else "gw_replay_gather_desc"
+    first = "gw_maddpg_desc_update_img" if desc_learner == "1" else "gw_replay_gather_desc"
     from marlnav.maddpg import MADDPG
     from marlnav.train import MADDPGTrainer
     sc = S.builtin("grid32")
@@ -134,7 +135,7 @@ def test_update_as_recorded_launches_equals_graph_replay(monkeypatch, desc_learn
         assert m._graph is not None and (m._launches is not None) == (mode == "launches")
         if mode == "launches":
             names = [c[0] for c in m._launches.calls]
-            assert names[0] == first and "gw_actor_prepare" in names, names
+            assert names[0] == first and ("gw_actor_prepare" in names) == (desc_learner == "0"), names
         before = m.actors.net.flat_params().clone()
         tr.train(18)
         torch.cuda.synchronize()
@@ -167,7 +168,7 @@ def test_capture_follows_the_rings_row_mode():
     assert tr.rollout.replay.use_desc and not m.capture_matches(tr.rollout.replay)
     tr.train(3)
     assert m._capture_desc is True and m.capture_matches(tr.rollout.replay)
-    assert [c[0] for c in m._launches.calls][0] == "gw_maddpg_desc_update"
+    assert [c[0] for c in m._launches.calls][0] == "gw_maddpg_desc_update_img"
     env.close()
 
 
