@@ -349,18 +349,17 @@ __global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
         for (int i = 0; i < R; ++i) s_w2[i * THREADS + tid] = r[i];
         for (int i = tid; i < W3IMG / 4; i += THREADS) s_w3[i] = p.w3img[(size_t)k * (W3IMG / 4) + i];
         if (tid < HID) {
-            if (p.c1_part) {  // prep_images' c1: b1 + the slices, 8 loads in flight, added in order
+            if (p.c1_part) {  // prep_images' c1: b1 + the slices added in slice order (32 loads in flight)
                 float part = 0.0f;
                 const float *ps = p.c1_part + (size_t)k * p.c1_nslices * HID + tid;
-                int sl = 0;
-                for (; sl + 8 <= p.c1_nslices; sl += 8) {
-                    float v[8];
+                for (int s0 = 0; s0 < p.c1_nslices; s0 += 32) {
+                    float v[32];
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) v[i] = ps[(size_t)(sl + i) * HID];
+                    for (int i = 0; i < 32; ++i) v[i] = ps[(size_t)min(s0 + i, p.c1_nslices - 1) * HID];
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) part += v[i];
+                    for (int i = 0; i < 32; ++i)
+                        if (s0 + i < p.c1_nslices) part += v[i];
                 }
-                for (; sl < p.c1_nslices; ++sl) part += ps[(size_t)sl * HID];
                 s_vec[0][tid] = p.net.b1[k * HID + tid] + part;
             } else {
                 s_vec[0][tid] = p.c1[k * HID + tid];
