@@ -1497,7 +1497,9 @@ __global__ void __launch_bounds__(256) wcnn_l1_kernel(CnnParams p, Lists lists) 
 // the rare kernel computes each item on its own and writes it to the item's (env, slot) row, which
 // act_kernel sums in slot order.  The counters are zeroed by the act_kernel launch that follows
 // (p.zero_n), after the rare kernel has read them.
-constexpr int LR_ENVS = 1024;
+// (512 envs per block: 8.2 us per launch at c4patch; 1024: 11.8, 256: 8.6 -- fewer envs per thread
+// shorten the decode chain until the blocks' same-address bucket claims take over)
+constexpr int LR_ENVS = 512;
 template <int NP>
 __global__ void __launch_bounds__(256) wcnn_list_kernel(CnnParams p) {
     constexpr int PER = LR_ENVS / 256;
