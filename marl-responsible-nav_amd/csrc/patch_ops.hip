@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdlib>
+#include <type_traits>
 
 #include "patch_ops.h"
 #include "prof.h"
@@ -415,12 +416,12 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a, unsign
 // ~6 us per block on a dependent staging phase with none of that block's stores in flight, and at
 // c4patch ran at ~3 TB/s alone (45 us; the launch shape's store floor, GW_PATCH_MODE=9: 18 us).
 // Terminal windows (D_FINAL) take the same path from the descriptor's terminal words.
-// WR_RUNS runs of 64 rows per wave (1 or 2 measured slower: 36.3 / 30.5 vs 29.4 us at c4patch's
-// shape; the body needs ~100 VGPRs at any run count, so fewer runs only lose the batched loads)
-constexpr int WR_RUNS = 4;
-template <int NP>
+// WR_RUNS = 2 runs of 64 rows per wave, the row's map written four columns at a time and the
+// terminal descriptor words loaded only by waves with a terminal window (80 VGPRs at P <= 12:
+// six waves per SIMD).  Alone at c4patch's / c5patch's shapes: 1 run 36.1 / 22.7 us, 2 runs
+// 29.9 / 18.4, 4 runs 31.0 / 18.9, 8 runs 38.8 / 21.7 (the preloaded descriptors' registers)
+template <int NP, int MAXW, int WR_RUNS = 2>  // MAXW: 8, 12 or 16 >= P (the row's registers)
 __global__ void __launch_bounds__(256, 4) window_rows_kernel(gw::PatchArgs a) {
-    constexpr int MAXW = 16;  // P <= 16
     __shared__ __attribute__((aligned(16))) float4 s_rows[4][64 * (MAXW / 4)];  // per wave: 64 rows
     const int P = a.P, W = a.W, H = a.H, half = P / 2, k = blockIdx.y, P4 = P / 4, N4 = 16 * P;  // N4: the run's float4
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -431,14 +432,13 @@ __global__ void __launch_bounds__(256, 4) window_rows_kernel(gw::PatchArgs a) {
     // before the first run's stores (one round trip per wave, not one per 64 rows)
     const uint32_t run0 = (blockIdx.x * 4u + (uint32_t)wave) * WR_RUNS;
     uint32_t fr[WR_RUNS];
-    uint4 wsr[WR_RUNS], wfr[WR_RUNS];
+    uint4 wsr[WR_RUNS];  // (the terminal words: loaded by the few waves that need them)
 #pragma unroll
     for (int j = 0; j < WR_RUNS; ++j) {
         const uint32_t t = (run0 + j) * 64u + lane, tc = t < nrows ? t : nrows - 1;
         const uint32_t *d = a.desc + (int64_t)__umulhi(tc, m_p) * NDESC;
         fr[j] = d[4];
         wsr[j] = *reinterpret_cast<const uint4 *>(d);
-        wfr[j] = *reinterpret_cast<const uint4 *>(d + 8);
     }
 #pragma unroll
     for (int j = 0; j < WR_RUNS; ++j) {
@@ -450,7 +450,8 @@ __global__ void __launch_bounds__(256, 4) window_rows_kernel(gw::PatchArgs a) {
     const int wr = (int)(tc - e * (uint32_t)P);
     const uint32_t f = fr[j];
     const bool step = live && (f & D_WRITE) && a.patch, fin = live && (f & D_FINAL) && a.final_patch;
-    const uint4 ws = wsr[j], wf = wfr[j];
+    const uint4 ws = wsr[j];
+    const uint32_t *dj = a.desc + (int64_t)e * NDESC;
     auto road = [&](int cell) { return (a.roadbits[cell >> 5] >> (cell & 31)) & 1u; };
     // the wave's 64 rows are one contiguous run of 64 P floats: each lane parks its row's map values
     // in the wave's LDS slice, then stores the patched cells that lie on its row over them (scalar
@@ -462,7 +463,7 @@ __global__ void __launch_bounds__(256, 4) window_rows_kernel(gw::PatchArgs a) {
     auto emit = [&](int which, bool mine, float *dst) {
         const uint64_t mask = __ballot(mine);
         if (!mask) return;  // wave-uniform
-        const uint4 w4 = which == 0 ? ws : wf;
+        const uint4 w4 = which == 0 ? ws : *reinterpret_cast<const uint4 *>(dj + 8);
         const uint32_t wd[4] = {w4.x, w4.y, w4.z, w4.w};
         const bool reset = which == 0 && (f & D_RESET);
         const uint32_t apples = which == 0 ? (f >> 8) & 0xFFu : (f >> 16) & 0xFFu;
@@ -475,20 +476,21 @@ __global__ void __launch_bounds__(256, 4) window_rows_kernel(gw::PatchArgs a) {
             const int cmin = max(gc0, 0), cell = (in_row ? grow : 0) * W + cmin;
             const int nroad1 = (H * W + 31) / 32 - 1, w0 = min(cell >> 5, nroad1);
             const uint64_t bits = (((uint64_t)a.roadbits[min(w0 + 1, nroad1)] << 32) | a.roadbits[w0]) >> (cell & 31);
-            float v[MAXW];
 #pragma unroll
-            for (int c = 0; c < MAXW; ++c) {
-                const int col = gc0 + c;
-                v[c] = (in_row && (unsigned)col < (unsigned)W && ((bits >> (col - cmin)) & 1u)) ? 0.0f : -1.0f;
-            }
-            if ((P & 3) == 0) {
+            for (int q = 0; q < MAXW / 4; ++q) {  // four columns at a time: no row array in registers
+                float v[4];
 #pragma unroll
-                for (int q = 0; q < MAXW / 4; ++q)
-                    if (q < P4) sw[lane * P4 + q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-            } else {  // rows not 16-byte aligned in LDS: scalar stores
+                for (int u = 0; u < 4; ++u) {
+                    const int col = gc0 + 4 * q + u;
+                    v[u] = (in_row && (unsigned)col < (unsigned)W && ((bits >> (col - cmin)) & 1u)) ? 0.0f : -1.0f;
+                }
+                if ((P & 3) == 0) {
+                    if (q < P4) sw[lane * P4 + q] = make_float4(v[0], v[1], v[2], v[3]);
+                } else {  // rows not 16-byte aligned in LDS: scalar stores
 #pragma unroll
-                for (int c = 0; c < MAXW; ++c)
-                    if (c < P) swf[c] = v[c];
+                    for (int u = 0; u < 4; ++u)
+                        if (4 * q + u < P) swf[4 * q + u] = v[u];
+                }
             }
         }
         auto patch = [&](int cell, float val) {  // the cell's value, if it lies on this row
@@ -625,16 +627,22 @@ hipError_t launch_windows(const PatchArgs &args, hipStream_t s) {
     const bool rows_ok = a.P >= 2 && a.P <= 16 && a.E % 4 == 0 && a.N >= 1 && a.N <= GW_MAX_AGENTS &&
                          a.E * a.P < (1LL << 32);
     if (rows_ok && (!force || std::atoi(force) == 6)) {
-        const dim3 grid((unsigned)((a.E * a.P + 256 * WR_RUNS - 1) / (256 * WR_RUNS)), a.K);
+        const dim3 grid((unsigned)((a.E * a.P + 512 - 1) / 512), a.K);  // 4 waves x 2 runs of 64 rows
+        auto go = [&](auto np_c) {
+            constexpr int NPv = decltype(np_c)::value;
+            if (a.P <= 8) gwprof::launch(window_rows_kernel<NPv, 8>, grid, dim3(256), 0, s, a);
+            else if (a.P <= 12) gwprof::launch(window_rows_kernel<NPv, 12>, grid, dim3(256), 0, s, a);
+            else gwprof::launch(window_rows_kernel<NPv, 16>, grid, dim3(256), 0, s, a);
+        };
         switch (a.N) {
-            case 1: gwprof::launch(window_rows_kernel<2>, grid, dim3(256), 0, s, a); break;
-            case 2: gwprof::launch(window_rows_kernel<3>, grid, dim3(256), 0, s, a); break;
-            case 3: gwprof::launch(window_rows_kernel<4>, grid, dim3(256), 0, s, a); break;
-            case 4: gwprof::launch(window_rows_kernel<5>, grid, dim3(256), 0, s, a); break;
-            case 5: gwprof::launch(window_rows_kernel<6>, grid, dim3(256), 0, s, a); break;
-            case 6: gwprof::launch(window_rows_kernel<7>, grid, dim3(256), 0, s, a); break;
-            case 7: gwprof::launch(window_rows_kernel<8>, grid, dim3(256), 0, s, a); break;
-            default: gwprof::launch(window_rows_kernel<9>, grid, dim3(256), 0, s, a); break;
+            case 1: go(std::integral_constant<int, 2>{}); break;
+            case 2: go(std::integral_constant<int, 3>{}); break;
+            case 3: go(std::integral_constant<int, 4>{}); break;
+            case 4: go(std::integral_constant<int, 5>{}); break;
+            case 5: go(std::integral_constant<int, 6>{}); break;
+            case 6: go(std::integral_constant<int, 7>{}); break;
+            case 7: go(std::integral_constant<int, 8>{}); break;
+            default: go(std::integral_constant<int, 9>{}); break;
         }
         return hipGetLastError();
     }
