@@ -1097,11 +1097,14 @@ __device__ __forceinline__ void d_add_patches(float z[8], const float *w1, int64
 // K HW + a; round 4's d_add_actions): the same fma order, but NB entries' loads in flight per batch, so ~2
 // round trips instead of one per agent plus one per 9 actions (entries past the end re-read a
 // valid row and are skipped)
+// (sa non-null: the 9K action rows are staged in LDS at sa [9K][HID], so the global batches hold
+// only the patched cells and the actions follow from LDS, the same order)
 template <int NB>
 __device__ __forceinline__ void d_add_critic_in(float z[8], const float *w1, int HW, int K, const int16_t (*pc)[NPM],
-                                                const float (*pd)[NPM], const int *np, const float *av, int g) {
+                                                const float (*pd)[NPM], const int *np, const float *av, int g,
+                                                const float *sa = nullptr) {
     const int na = NA * K;
-    int tot = na;
+    int tot = sa ? 0 : na;
     for (int kk = 0; kk < K; ++kk) tot += np[kk];
     int kk = 0, i = 0;
     for (int e0 = 0; e0 < tot; e0 += NB) {
@@ -1135,6 +1138,17 @@ __device__ __forceinline__ void d_add_critic_in(float z[8], const float *w1, int
                 z[4] = fmaf(dv[u], b[u].x, z[4]); z[5] = fmaf(dv[u], b[u].y, z[5]);
                 z[6] = fmaf(dv[u], b[u].z, z[6]); z[7] = fmaf(dv[u], b[u].w, z[7]);
             }
+        }
+    }
+    if (sa) {
+        for (int a = 0; a < na; ++a) {
+            const float4 x = *reinterpret_cast<const float4 *>(sa + a * HID + 8 * g);
+            const float4 y = *reinterpret_cast<const float4 *>(sa + a * HID + 8 * g + 4);
+            const float dv = av[a];
+            z[0] = fmaf(dv, x.x, z[0]); z[1] = fmaf(dv, x.y, z[1]);
+            z[2] = fmaf(dv, x.z, z[2]); z[3] = fmaf(dv, x.w, z[3]);
+            z[4] = fmaf(dv, y.x, z[4]); z[5] = fmaf(dv, y.y, z[5]);
+            z[6] = fmaf(dv, y.z, z[6]); z[7] = fmaf(dv, y.w, z[7]);
         }
     }
 }
@@ -1299,7 +1313,13 @@ __global__ void __launch_bounds__(DT) dcritic_tail(DTail p) {
     // the small parameters: float4 units of 32-unit segments (stage_segs), K target actors then
     // the critic target and the critic, by the threads past the descriptor decoders' waves (whose
     // chain is the prologue's longest); loads first, stores at the end of the prologue
-    const int sa = stage_segs(NA), sc1 = stage_segs(1), nseg = K * sa + 2 * sc1, nunit = 32 * nseg;
+    // when they fit in the slots K + 2 .. MAXK + 1 (K <= 3), the two critics' 9K action rows of W1
+    // follow as segments too (critic target then critic, [9K][HID] each), so the critics' layer-1
+    // sums read only the patched cells from global memory
+    const int sa = stage_segs(NA), sc1 = stage_segs(1), nseg_net = K * sa + 2 * sc1;
+    const bool arow = 2 * NA * K * HID <= (MAXK - K) * PSLOT;
+    const int nseg = nseg_net + (arow ? 2 * NA * K : 0), nunit = 32 * nseg;
+    float *const s_arow = &s_par[0][0] + (size_t)(K + 2) * PSLOT;
     auto unit_net = [&](int v, int &net, int &sg) {
         const int g = v >> 5;
         if (g < K * sa) {
@@ -1311,18 +1331,26 @@ __global__ void __launch_bounds__(DT) dcritic_tail(DTail p) {
         }
     };
     auto unit_src = [&](int v) -> const float4 * {
+        const int gs = v >> 5;
+        if (gs >= nseg_net) {  // action row a of critic target (ar < 9K) or critic
+            const int ar = gs - nseg_net, a = ar % (NA * K);
+            const float *w1 = (ar < NA * K ? p.ct : p.c).w1 + ((int64_t)k * in_c + (int64_t)K * HW + a) * HID;
+            return reinterpret_cast<const float4 *>(w1) + (v & 31);
+        }
         int net, sg;
         unit_net(v, net, sg);
         const Mlp m = net < K ? mlp_k(p.at, net, HW, NA) : mlp_k(net == K ? p.ct : p.c, k, in_c, 1);
         return stage_seg_src(m, sg, v & 31);
     };
     auto unit_dst = [&](int v) -> float4 * {
+        const int gs = v >> 5;
+        if (gs >= nseg_net) return reinterpret_cast<float4 *>(s_arow + (gs - nseg_net) * HID) + (v & 31);
         int net, sg;
         unit_net(v, net, sg);
         return reinterpret_cast<float4 *>(&s_par[net][sg * HID]) + (v & 31);
     };
     const int nsd = (RB * 2 * K + 63) / 64 * 64, sid = tid - nsd, sstride = DT - nsd;
-    constexpr int NSV = 4;
+    constexpr int NSV = 6;
     float4 sv[NSV];
 #pragma unroll
     for (int u = 0; u < NSV; ++u) {
@@ -1492,7 +1520,8 @@ __global__ void __launch_bounds__(DT) dcritic_tail(DTail p) {
         float z[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) z[i] = s_c1[tgt ? K : K + 1][8 * g + i];
-        d_add_critic_in<16>(z, m.w1, HW, K, s_pc[which][rl], s_pd[which][rl], s_np[which][rl], tgt ? s_tact[rl] : s_act[rl], g);
+        d_add_critic_in<16>(z, m.w1, HW, K, s_pc[which][rl], s_pd[which][rl], s_np[which][rl], tgt ? s_tact[rl] : s_act[rl], g,
+                            arow ? s_arow + (tgt ? 0 : NA * K * HID) : nullptr);
         DSTAMP(p, 9);
         d_fwd_rest(z, m, 1, rl, g, s_in[grp], s_out[grp], f, out);
         DSTAMP(p, 10);
@@ -1548,7 +1577,7 @@ __global__ void __launch_bounds__(DT) dactor_tail(DTail p) {
     __shared__ float s_act[RB][NA * MAXK];
     __shared__ float s_c1[2][HID];
     __shared__ __attribute__((aligned(16))) float s_par[2][PSLOT];  // actor k, critic k
-    __shared__ __attribute__((aligned(16))) float s_wa[NA][HID];    // critic k's W1 rows of agent k's actions
+    __shared__ __attribute__((aligned(16))) float s_wa[NA * MAXK][HID];  // critic k's W1 action rows (all agents)
     const int k = blockIdx.y, tid = threadIdx.x, grp = tid >> 8, lt = tid & 255, rl = lt >> 4, g = lt & 15;
     const int K = p.K, B = p.B, HW = p.q.HW, r0 = blockIdx.x * RB, r = r0 + rl;
     const int in_c = K * HW + NA * K;
@@ -1556,15 +1585,18 @@ __global__ void __launch_bounds__(DT) dactor_tail(DTail p) {
     DSTAMP(p, 0);
     // prologue: this thread's share of the small parameters (loads issued first), the c1 sums and
     // the recorded rows (their round trips overlap), then the parameters into LDS
-    const int na_ = stage_size(NA), nc_ = stage_size(1), tot = na_ + nc_ + NA * HID;
-    const float *wa = p.c.w1 + ((int64_t)k * in_c + (int64_t)K * HW + NA * k) * HID;
+    const int na_ = stage_size(NA), nc_ = stage_size(1), tot = na_ + nc_;
+    // the 9K action rows (contiguous, 16-byte aligned: HID | 4), as float4s, loads first
+    const float4 *wa = reinterpret_cast<const float4 *>(p.c.w1 + ((int64_t)k * in_c + (int64_t)K * HW) * HID);
+    const int nwa = NA * K * HID / 4;
+    constexpr int NWA = (NA * MAXK * HID / 4 + DT - 1) / DT;
+    float4 wv[NWA];
+#pragma unroll
+    for (int u = 0; u < NWA; ++u) wv[u] = wa[min(tid + u * DT, nwa - 1)];
     auto par_src = [&](int o) -> float {
-        return o < na_ ? stage_src(mlp_k(p.a, k, HW, NA), NA, o)
-               : o < na_ + nc_ ? stage_src(mlp_k(p.c, k, in_c, 1), 1, o - na_) : wa[o - na_ - nc_];
+        return o < na_ ? stage_src(mlp_k(p.a, k, HW, NA), NA, o) : stage_src(mlp_k(p.c, k, in_c, 1), 1, o - na_);
     };
-    auto par_dst = [&](int o) -> float * {
-        return o < na_ ? &s_par[0][o] : o < na_ + nc_ ? &s_par[1][o - na_] : &s_wa[(o - na_ - nc_) / HID][(o - na_ - nc_) % HID];
-    };
+    auto par_dst = [&](int o) -> float * { return o < na_ ? &s_par[0][o] : &s_par[1][o - na_]; };
     constexpr int NSV = 8;
     float sv[NSV];
 #pragma unroll
@@ -1599,6 +1631,9 @@ __global__ void __launch_bounds__(DT) dactor_tail(DTail p) {
         if (o < tot) *par_dst(o) = sv[u];
     }
     for (int o = tid + NSV * DT; o < tot; o += DT) *par_dst(o) = par_src(o);
+#pragma unroll
+    for (int u = 0; u < NWA; ++u)
+        if (tid + u * DT < nwa) reinterpret_cast<float4 *>(&s_wa[0][0])[tid + u * DT] = wv[u];
     if (blockIdx.x == 0 && k == 0 && tid == DT - 1) d_snapshot(p, 1);
     __syncthreads();
     DSTAMP(p, 1);
@@ -1643,7 +1678,7 @@ __global__ void __launch_bounds__(DT) dactor_tail(DTail p) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) z[i] = s_c1[1][8 * g + i];
         DSTAMP(p, 8);
-        d_add_critic_in<16>(z, mc.w1, HW, K, s_pc[rl], s_pd[rl], s_np[rl], s_act[rl], g);
+        d_add_critic_in<16>(z, mc.w1, HW, K, s_pc[rl], s_pd[rl], s_np[rl], s_act[rl], g, &s_wa[0][0]);
         DSTAMP(p, 9);
         ln_relu(z, mc.lw1, mc.lb1, g, fc.xh1, fc.y1, fc.rs1);
     }
@@ -1673,7 +1708,7 @@ __global__ void __launch_bounds__(DT) dactor_tail(DTail p) {
         float dp[NA];
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
-            const float *wr = s_wa[a] + 8 * g;
+            const float *wr = s_wa[NA * k + a] + 8 * g;
             float s = 0.0f;
 #pragma unroll
             for (int i = 0; i < 8; ++i) s = fmaf(dz1[i], wr[i], s);
