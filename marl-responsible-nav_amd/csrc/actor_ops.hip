@@ -343,13 +343,15 @@ __global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
                                : p.w2img + (size_t)k * (W2IMG / 4);
         constexpr int R = NW2 / THREADS;
         float4 r[R];
+        if (!(p.ab & 32)) {  // GW_ACT_AB bit 5 (measurement only): no W2 staging
 #pragma unroll
         for (int i = 0; i < R; ++i) r[i] = w2[i * THREADS + tid];
 #pragma unroll
         for (int i = 0; i < R; ++i) s_w2[i * THREADS + tid] = r[i];
+        }
         for (int i = tid; i < W3IMG / 4; i += THREADS) s_w3[i] = p.w3img[(size_t)k * (W3IMG / 4) + i];
         if (tid < HID) {
-            if (p.c1_part) {  // prep_images' c1: b1 + the slices added in slice order (32 loads in flight)
+            if (p.c1_part && !(p.ab & 64)) {  // prep_images' c1 (GW_ACT_AB bit 6, measurement: skipped): b1 + the slices added in slice order (32 loads in flight)
                 float part = 0.0f;
                 const float *ps = p.c1_part + (size_t)k * p.c1_nslices * HID + tid;
                 for (int s0 = 0; s0 < p.c1_nslices; s0 += 32) {

@@ -420,6 +420,7 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a, unsign
 // terminal descriptor words loaded only by waves with a terminal window (80 VGPRs at P <= 12:
 // six waves per SIMD).  Alone at c4patch's / c5patch's shapes: 1 run 36.1 / 22.7 us, 2 runs
 // 29.9 / 18.4, 4 runs 31.0 / 18.9, 8 runs 38.8 / 21.7 (the preloaded descriptors' registers)
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 template <int NP, int MAXW, int WR_RUNS = 2>  // MAXW: 8, 12 or 16 >= P (the row's registers)
 __global__ void __launch_bounds__(256, 4) window_rows_kernel(gw::PatchArgs a) {
     __shared__ __attribute__((aligned(16))) float4 s_rows[4][64 * (MAXW / 4)];  // per wave: 64 rows
@@ -520,13 +521,15 @@ __global__ void __launch_bounds__(256, 4) window_rows_kernel(gw::PatchArgs a) {
                 // unwritten row (or past the last row) goes out as its written floats alone
                 const int r0 = (int)__umulhi((uint32_t)(4 * i), m_p), r1 = (int)__umulhi((uint32_t)(4 * i + 3), m_p);
                 const bool w0 = (mask >> r0) & 1u, w1 = (mask >> r1) & 1u;
+                // nontemporal (streamed past the caches, as the obs writer's): alone 18.5 -> 17.7 us at
+                // c5patch's shape, 30.3 -> 28.8 us at c4patch's (tools/gpu_r5_nt.sh)
                 if (w0 && w1) {
-                    o4[i] = sw[i];
+                    __builtin_nontemporal_store(*reinterpret_cast<const f32x4 *>(&sw[i]), reinterpret_cast<f32x4 *>(&o4[i]));
                 } else if (w0 || w1) {
                     const float *src = reinterpret_cast<const float *>(sw) + 4 * i;
 #pragma unroll
                     for (int c = 0; c < 4; ++c)
-                        if ((mask >> __umulhi((uint32_t)(4 * i + c), m_p)) & 1u) run[4 * i + c] = src[c];
+                        if ((mask >> __umulhi((uint32_t)(4 * i + c), m_p)) & 1u) __builtin_nontemporal_store(src[c], &run[4 * i + c]);
                 }
             }
         }

@@ -29,7 +29,7 @@ def main():
     mask = env.out["mask"]
     a = torch.empty((E, env.K), dtype=torch.int32, device="cuda")
     pr = torch.empty((env.K, E, 9), dtype=torch.float32, device="cuda")
-    for ab in [0, 1, 2, 4, 3, 7, 6, 5, 16, 23]:
+    for ab in [int(x) for x in os.environ.get("ACT_AB_LIST", "0,1,2,4,3,7,6,5,16,23").split(",")]:
         os.environ["GW_ACT_AB"] = str(ab)
         actors.act_env(env, mask, True, seed=1, counter=0, actions_out=a, probs_out=pr)  # prepare outside
         torch.cuda.synchronize()
