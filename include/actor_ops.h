@@ -160,6 +160,22 @@ gw_status gw_patch_cnn_act(void *env, int32_t P, const gw_cnn_actors *net, const
                            uint64_t seed, uint64_t counter, const int64_t *counter_dev, const float *uniform,
                            const uint16_t *mask,
                            int32_t *actions, float *probs, float *logits, void *stream);
+/* A rollout's step in fewer launches: gw_patch_cnn_write_list writes the env's windows exactly as
+ * gw_obs_patch(env, P, patch, final_patch) does (the row writer; E % 4 == 0) and, in the SAME launch,
+ * lists the positions the next act recomputes for those descriptors (the first part of
+ * gw_patch_cnn_act); gw_patch_cnn_act_listed is the rest of gw_patch_cnn_act on that listing
+ * (ordered after it, no env step or reset in between, the same workspace derivation).  Together
+ * they equal gw_obs_patch + gw_patch_cnn_act bit for bit (tests/test_gpu_patch_cnn.py).  The
+ * listing adds into bucket counters that the act kernel zeroes once the rare kernel has read them:
+ * between two gw_patch_cnn_write_list calls there must be an act (either form; gw_patch_cnn_act
+ * also zeroes them before its own listing, so a listing followed by an env reset and a
+ * gw_patch_cnn_act is fine). */
+gw_status gw_patch_cnn_write_list(void *env, int32_t P, const gw_cnn_actors *net, const float *ws, float *patch,
+                                  float *final_patch, void *stream);
+gw_status gw_patch_cnn_act_listed(void *env, int32_t P, const gw_cnn_actors *net, const float *ws, int training,
+                                  float tau, uint64_t seed, uint64_t counter, const int64_t *counter_dev,
+                                  const float *uniform, const uint16_t *mask, int32_t *actions, float *probs,
+                                  float *logits, void *stream);
 
 #ifdef __cplusplus
 }

@@ -44,6 +44,7 @@
 
 #include "actor_ops.h"
 #include "prof.h"
+#include "window_rows.h"
 
 namespace {
 
@@ -1503,11 +1504,11 @@ __global__ void __launch_bounds__(256) wcnn_l1_kernel(CnnParams p, Lists lists) 
 // shorten the decode chain until the blocks' same-address bucket claims take over)
 constexpr int LR_ENVS = 512;
 template <int NP>
-__global__ void __launch_bounds__(256) wcnn_list_kernel(CnnParams p) {
+__device__ __forceinline__ void list_block(const CnnParams &p, int bx, int k) {
     constexpr int PER = LR_ENVS / 256;
     __shared__ uint32_t s_road[128];
     __shared__ int s_cnt[WNQ], s_base[WNQ];
-    const int k = blockIdx.y, tid = threadIdx.x;
+    const int tid = threadIdx.x;
     if (tid < 128) s_road[tid] = p.ws.road[tid];
     if (tid < WNQ) s_cnt[tid] = 0;
     int64_t ev[PER];
@@ -1515,7 +1516,7 @@ __global__ void __launch_bounds__(256) wcnn_list_kernel(CnnParams p) {
     uint32_t flags[PER];
 #pragma unroll
     for (int r = 0; r < PER; ++r) {  // every descriptor load of the thread in flight together
-        ev[r] = (int64_t)blockIdx.x * LR_ENVS + r * 256 + tid;
+        ev[r] = (int64_t)bx * LR_ENVS + r * 256 + tid;
         const bool valid = ev[r] < p.E;
         cells[r] = valid ? *reinterpret_cast<const uint4 *>(p.desc + ev[r] * NDESC) : make_uint4(0, 0, 0, 0);
         flags[r] = valid ? p.desc[ev[r] * NDESC + 4] : 0u;
@@ -1581,6 +1582,23 @@ __global__ void __launch_bounds__(256) wcnn_list_kernel(CnnParams p) {
             p.ws.bucket[((size_t)k * p.P + Q) * p.E + pos] = (int)(ev[r] * RSW + __popc(qm[r] & ((1u << Q) - 1u)));
         }
     }
+}
+template <int NP>
+__global__ void __launch_bounds__(256) wcnn_list_kernel(CnnParams p) {
+    list_block<NP>(p, blockIdx.x, blockIdx.y);
+}
+
+// gw_patch_cnn_write_list: the step's windows (the row writer's blocks, window_rows.h) and the
+// listing of the next act's recomputed positions in ONE launch -- both read only the step's
+// descriptors; the listing's blocks first (a short chain), the writer's HBM stream beside them
+template <int NP, int MAXW>
+__global__ void __launch_bounds__(256, 4) rows_list_kernel(gw::PatchArgs a, CnnParams p, uint32_t nlist) {
+    __shared__ __attribute__((aligned(16))) float4 s_rows[4][64 * (MAXW / 4)];
+    if (blockIdx.x < nlist) {
+        list_block<NP>(p, blockIdx.x, blockIdx.y);
+        return;
+    }
+    gwrows::rows_block<NP, MAXW, 2>(a, blockIdx.x - nlist, blockIdx.y, s_rows);
 }
 
 // one 64-thread block per bucket: the offsets of the layer-1 blocks' items in the bucket (a wave
@@ -2237,26 +2255,18 @@ gw_status gw_patch_cnn_prepare(void *env, int32_t P, const gw_cnn_actors *net, f
     return GW_OK;
 }
 
-gw_status gw_patch_cnn_act(void *env, int32_t P, const gw_cnn_actors *net, const float *ws, int training, float tau,
-                           uint64_t seed, uint64_t counter, const int64_t *counter_dev, const float *uniform,
-                           const uint16_t *mask,
-                           int32_t *actions, float *probs, float *logits, void *stream) {
-    if (!env || !net || !ws || !actions || !probs) return err(GW_ERR_ARG, "gw_patch_cnn_act: null argument");
-    if (reinterpret_cast<uintptr_t>(ws) & 15u) return err(GW_ERR_ARG, "gw_patch_cnn_act: ws must be 16-byte aligned");
-    gw_obs_source src;
-    gw_status st = gw_obs_view(env, &src);
-    if (st != GW_OK) return st;
-    if ((st = check_patch_cnn(src, P, net, "gw_patch_cnn_act")) != GW_OK) return st;
-    if (!(tau > 0.0f)) return err(GW_ERR_ARG, "gw_patch_cnn_act: tau must be > 0");
-    const CnnParams cp = wcnn_params(src, P, net, const_cast<float *>(ws));
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    if (src.K * cp.P > WR_MAX_NB) return err(GW_ERR_ARG, "gw_patch_cnn_act: K x window positions above the rare kernel's table");
-    // the positions to recompute, listed per (agent, position) bucket in ONE launch (round 5;
-    // GW_WCNN_LIST=scan: the round-4 chain of layer-1 counts, bucket scan and scatter, A/B)
+// the positions the act recomputes for the env's current descriptors, listed per (agent, position)
+// bucket in ONE launch (round 5; GW_WCNN_LIST=scan: the round-4 chain of layer-1 counts, bucket
+// scan and scatter, A/B).  The bucket counters start from zero: the act kernel zeroes them after
+// the rare kernel read them, and this call (zero = true) zeroes them itself, so a listing that no
+// act consumed (gw_patch_cnn_write_list before an env reset) leaves no counts behind.
+static gw_status patch_cnn_list(void *env, const gw_obs_source &src, const CnnParams &cp, hipStream_t s) {
     static const char *list_env = std::getenv("GW_WCNN_LIST");
     const bool fused_list = !(list_env && std::string(list_env) == "scan");
     if (fused_list) {
         gwprof::Span span(env, GW_SPAN_CNN_L1);
+        if (hipMemsetAsync(cp.ws.bucket_n, 0, sizeof(int) * src.K * cp.P, s) != hipSuccess)
+            return err(GW_ERR_HIP, "gw_patch_cnn_act: memset");
         const dim3 fgrid((unsigned)((src.E + LR_ENVS - 1) / LR_ENVS), src.K);
         switch (src.N) {
             case 1: gwprof::launch(wcnn_list_kernel<2>, fgrid, dim3(256), 0, s, cp); break;
@@ -2290,6 +2300,30 @@ gw_status gw_patch_cnn_act(void *env, int32_t P, const gw_cnn_actors *net, const
         gwprof::launch(bucket_scan, dim3(src.K * cp.P), dim3(64), 0, s, cp, lists);
         gwprof::launch(wcnn_scatter, lgrid, dim3(256), 0, s, cp, lists);
     }
+    return GW_OK;
+}
+
+static gw_status patch_cnn_check(void *env, int32_t P, const gw_cnn_actors *net, const float *ws, gw_obs_source &src,
+                                 const char *who) {
+    const std::string w(who);
+    if (!env || !net || !ws) return err(GW_ERR_ARG, w + ": null argument");
+    if (reinterpret_cast<uintptr_t>(ws) & 15u) return err(GW_ERR_ARG, w + ": ws must be 16-byte aligned");
+    gw_status st = gw_obs_view(env, &src);
+    if (st != GW_OK) return st;
+    if ((st = check_patch_cnn(src, P, net, who)) != GW_OK) return st;
+    if (src.K * (P / 4) * (P / 4) > WR_MAX_NB) return err(GW_ERR_ARG, w + ": K x window positions above the rare kernel's table");
+    return GW_OK;
+}
+
+// the rare kernel and the actor over the listed positions
+static gw_status patch_cnn_rest(void *env, const gw_obs_source &src, const CnnParams &cp, int32_t P,
+                                const gw_cnn_actors *net, int training, float tau, uint64_t seed, uint64_t counter,
+                                const int64_t *counter_dev, const float *uniform, const uint16_t *mask,
+                                int32_t *actions, float *probs, float *logits, hipStream_t s) {
+    if (!actions || !probs) return err(GW_ERR_ARG, "gw_patch_cnn_act: null argument");
+    if (!(tau > 0.0f)) return err(GW_ERR_ARG, "gw_patch_cnn_act: tau must be > 0");
+    static const char *list_env = std::getenv("GW_WCNN_LIST");
+    const bool fused_list = !(list_env && std::string(list_env) == "scan");
     static const char *stat_env = std::getenv("GW_WCNN_STAT");  // diagnostics: the buckets' sizes (synchronises)
     if (stat_env && *stat_env && fused_list) {
         std::vector<int> bn((size_t)src.K * cp.P);
@@ -2395,6 +2429,83 @@ gw_status gw_patch_cnn_act(void *env, int32_t P, const gw_cnn_actors *net, const
 #undef ACTW
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return err(GW_ERR_HIP, std::string("gw_patch_cnn_act: ") + hipGetErrorString(e));
+    return GW_OK;
+}
+
+gw_status gw_patch_cnn_act(void *env, int32_t P, const gw_cnn_actors *net, const float *ws, int training, float tau,
+                           uint64_t seed, uint64_t counter, const int64_t *counter_dev, const float *uniform,
+                           const uint16_t *mask,
+                           int32_t *actions, float *probs, float *logits, void *stream) {
+    gw_obs_source src;
+    gw_status st = patch_cnn_check(env, P, net, ws, src, "gw_patch_cnn_act");
+    if (st != GW_OK) return st;
+    const CnnParams cp = wcnn_params(src, P, net, const_cast<float *>(ws));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if ((st = patch_cnn_list(env, src, cp, s)) != GW_OK) return st;
+    return patch_cnn_rest(env, src, cp, P, net, training, tau, seed, counter, counter_dev, uniform, mask, actions,
+                          probs, logits, s);
+}
+
+gw_status gw_patch_cnn_act_listed(void *env, int32_t P, const gw_cnn_actors *net, const float *ws, int training,
+                                  float tau, uint64_t seed, uint64_t counter, const int64_t *counter_dev,
+                                  const float *uniform, const uint16_t *mask, int32_t *actions, float *probs,
+                                  float *logits, void *stream) {
+    gw_obs_source src;
+    gw_status st = patch_cnn_check(env, P, net, ws, src, "gw_patch_cnn_act_listed");
+    if (st != GW_OK) return st;
+    const CnnParams cp = wcnn_params(src, P, net, const_cast<float *>(ws));
+    return patch_cnn_rest(env, src, cp, P, net, training, tau, seed, counter, counter_dev, uniform, mask, actions,
+                          probs, logits, static_cast<hipStream_t>(stream));
+}
+
+gw_status gw_patch_cnn_write_list(void *env, int32_t P, const gw_cnn_actors *net, const float *ws, float *patch,
+                                  float *final_patch, void *stream) {
+    gw_obs_source src;
+    gw_status st = patch_cnn_check(env, P, net, ws, src, "gw_patch_cnn_write_list");
+    if (st != GW_OK) return st;
+    if (!patch) return err(GW_ERR_ARG, "gw_patch_cnn_write_list: null patch");
+    if (src.E % 4 != 0 || (uint64_t)src.E * (uint64_t)P >= (1ull << 32))
+        return err(GW_ERR_ARG, "gw_patch_cnn_write_list: needs E % 4 == 0 (the row writer's runs)");
+    const CnnParams cp = wcnn_params(src, P, net, const_cast<float *>(ws));
+    gw::PatchArgs a;
+    a.desc = src.desc;
+    a.roadbits = cp.ws.road;  // the workspace's copy of the env's road bits (gw_patch_cnn_prepare)
+    a.base = src.base;
+    a.patch = patch;
+    a.final_patch = final_patch;
+    a.E = src.E;
+    a.H = src.H;
+    a.W = src.W;
+    a.N = src.N;
+    a.K = src.K;
+    a.P = P;
+    a.variant = src.variant;
+    for (int k = 0; k < GW_MAX_AGENTS; ++k) a.apples[k] = src.apples[k];
+    const uint32_t nlist = (uint32_t)((src.E + LR_ENVS - 1) / LR_ENVS);
+    const uint32_t nrows = (uint32_t)((src.E * P + 511) / 512);
+    const dim3 grid(nlist + nrows, src.K);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    gwprof::Span span(env, GW_SPAN_WINDOW);
+#define RL(NP)                                                                                      \
+    do {                                                                                            \
+        if (P <= 8) gwprof::launch(rows_list_kernel<NP, 8>, grid, dim3(256), 0, s, a, cp, nlist);  \
+        else if (P <= 12) gwprof::launch(rows_list_kernel<NP, 12>, grid, dim3(256), 0, s, a, cp, nlist); \
+        else gwprof::launch(rows_list_kernel<NP, 16>, grid, dim3(256), 0, s, a, cp, nlist);           \
+    } while (0)
+    switch (src.N) {
+        case 1: RL(2); break;
+        case 2: RL(3); break;
+        case 3: RL(4); break;
+        case 4: RL(5); break;
+        case 5: RL(6); break;
+        case 6: RL(7); break;
+        case 7: RL(8); break;
+        case 8: RL(9); break;
+        default: return err(GW_ERR_ARG, "gw_patch_cnn_write_list: N out of range");
+    }
+#undef RL
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return err(GW_ERR_HIP, std::string("gw_patch_cnn_write_list: ") + hipGetErrorString(e));
     return GW_OK;
 }
 

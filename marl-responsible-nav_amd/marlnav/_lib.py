@@ -24,7 +24,7 @@ HIP_SOURCES = [os.path.join(CSRC, "gridenv.hip"), os.path.join(CSRC, "learner_op
                os.path.join(CSRC, "maddpg_ops.hip"), os.path.join(CSRC, "patch_ops.hip")]
 HEADERS = [os.path.join(INCLUDE, "gridenv.h"), os.path.join(INCLUDE, "learner_ops.h"),
            os.path.join(INCLUDE, "actor_ops.h"), os.path.join(INCLUDE, "rollout_ops.h")]
-SOURCES = HIP_SOURCES + HEADERS + [os.path.join(CSRC, "patch_ops.h"), os.path.join(CSRC, "prof.h"),
+SOURCES = HIP_SOURCES + HEADERS + [os.path.join(CSRC, "patch_ops.h"), os.path.join(CSRC, "window_rows.h"), os.path.join(CSRC, "prof.h"),
                                    os.path.join(CSRC, "philox.h")]
 OBJ_DIR = os.path.join(CSRC, "build")
 ARCH = os.environ.get("MARLNAV_OFFLOAD_ARCH", "gfx950")
@@ -175,7 +175,7 @@ EXPORTS = ["gw_create", "gw_reset", "gw_step", "gw_state_view", "gw_copy_state",
            "gw_replay_gather", "gw_affine_relu_fwd", "gw_affine_relu_bwd",
            "gw_soft_update2", "gw_td_target", "gw_mean_loss_fwd", "gw_mean_loss_bwd",
            "gw_eval_accum", "gw_profile_spans", "gw_patch_actor_workspace_floats", "gw_patch_actor_prepare",
-           "gw_patch_actor_act", "gw_patch_cnn_workspace_floats", "gw_patch_cnn_prepare", "gw_patch_cnn_act",
+           "gw_patch_actor_act", "gw_patch_cnn_workspace_floats", "gw_patch_cnn_prepare", "gw_patch_cnn_act", "gw_patch_cnn_write_list", "gw_patch_cnn_act_listed",
            "gw_maddpg_workspace_floats", "gw_maddpg_critic_grads", "gw_maddpg_actor_grads",
            "gw_pipeline_state_bytes", "gw_pipeline_save", "gw_pipeline_load",
            "gw_gather_pack_scratch", "gw_gather_pack", "gw_gather_unpack_plan_cap", "gw_gather_unpack",
@@ -360,6 +360,10 @@ def _declare(L):
     L.gw_patch_cnn_act.argtypes = [p, C.c_int32, C.POINTER(GwCnnActors), p, C.c_int, C.c_float, C.c_uint64,
                                    C.c_uint64, p, p, p, p, p, p, p]
     L.gw_patch_cnn_act.restype = C.c_int
+    L.gw_patch_cnn_act_listed.argtypes = L.gw_patch_cnn_act.argtypes
+    L.gw_patch_cnn_act_listed.restype = C.c_int
+    L.gw_patch_cnn_write_list.argtypes = [p, C.c_int32, C.POINTER(GwCnnActors), p, p, p, p]
+    L.gw_patch_cnn_write_list.restype = C.c_int
     L.gw_actor_workspace_floats.argtypes = [C.c_int32, C.c_int32]
     L.gw_actor_workspace_floats.restype = C.c_int64
     L.gw_actor_prepare.argtypes = [p, C.POINTER(GwMlpActors), p, p]

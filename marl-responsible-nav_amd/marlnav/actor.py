@@ -495,7 +495,8 @@ class MultiAgentActors(nn.Module):
     def act_env(self, env, mask: torch.Tensor | None = None, training: bool = True, tau: float = 1.0,
                 seed: int = 0, counter: int = 0, uniform: torch.Tensor | None = None,
                 actions_out: torch.Tensor | None = None, probs_out: torch.Tensor | None = None,
-                logits_out: torch.Tensor | None = None, patch: int = 0, counter_dev: torch.Tensor | None = None):
+                logits_out: torch.Tensor | None = None, patch: int = 0, counter_dev: torch.Tensor | None = None,
+                listed: bool = False):
         """``act`` on the observation ``env`` last wrote, as ONE fused HIP kernel (gw_actor_act):
         the first layer from the env's obs descriptors (map + patched cells, no obs read back),
         layers 2-3 on f32 MFMA, Gumbel noise from Philox(seed; env, counter, k) or ``uniform``
@@ -504,11 +505,14 @@ class MultiAgentActors(nn.Module):
         ring's step count: a captured graph's replays then draw fresh noise).
         patch = P > 0: actors built for P x P inputs act on each agent's egocentric window
         (gw_patch_actor_act; the windows VecGridEnv.obs_patch(P) would write).
+        listed (the CNN head on windows): ``patch_cnn_write_list`` already listed the positions to
+        recompute for the env's current descriptors on this stream (gw_patch_cnn_act_listed);
+        ignored, and listed here again, when the workspace had to be re-derived first.
         Raises if the library or a GPU is missing (no fallback)."""
         from . import _lib
         if self.arch == "cnn":
             return self._act_env_cnn(env, mask, training, tau, seed, counter, uniform, actions_out, probs_out,
-                                     logits_out, int(patch), counter_dev)
+                                     logits_out, int(patch), counter_dev, listed)
         net, K, E, dev = self.net, self.K, env.E, env.device
         patch = int(patch)
         st = self._fast
@@ -548,8 +552,36 @@ class MultiAgentActors(nn.Module):
             _lib.check(st["lib"].gw_actor_act(env.handle, *args), "gw_actor_act")
         return actions_out, probs_out
 
+    def patch_cnn_write_list(self, env, patch: int, out: torch.Tensor, final_out: torch.Tensor | None) -> bool:
+        """``env.obs_patch(patch, final=True, out=out, final_out=final_out)`` and, in the same launch,
+        the listing of the positions the next ``act_env(..., patch=P, listed=True)`` recomputes
+        (gw_patch_cnn_write_list).  False (nothing launched: the caller writes the windows itself)
+        while the fused workspace is not derived for the current weights, E % 4 != 0, or a listing
+        is still pending (no act since the last one: a second listing would add to its bucket
+        counts, which only the act resets)."""
+        from . import _lib
+        st = self._fast
+        if st is None or st["env"] is not env or st.get("patch", 0) != patch or env.E % 4 or st.get("pending"):
+            return False
+        params = [p for n in self.nets for p in n.parameters()]
+        key = (tuple(p._version for p in params), tuple(p.data_ptr() for p in params), getattr(self, "_epoch", 0))
+        if st["key"] != key:
+            return False
+        K, E, P = self.K, env.E, patch
+        for t in (out, final_out):
+            if t is not None and (t.dtype != torch.float32 or t.numel() != K * E * P * P or not t.is_contiguous()):
+                raise ValueError(f"patch_cnn_write_list: need contiguous float32 [K, E, {P}, {P}] buffers")
+        with torch.cuda.device(env.device):
+            _lib.check(st["lib"].gw_patch_cnn_write_list(env.handle, patch, C.byref(st["spec"]), st["ws"].data_ptr(),
+                                                         out.data_ptr(),
+                                                         final_out.data_ptr() if final_out is not None else None,
+                                                         torch.cuda.current_stream(env.device).cuda_stream),
+                       "gw_patch_cnn_write_list")
+        st["pending"] = True
+        return True
+
     def _act_env_cnn(self, env, mask, training, tau, seed, counter, uniform, actions_out, probs_out, logits_out,
-                     patch=0, counter_dev=None):
+                     patch=0, counter_dev=None, listed=False):
         """act_env for the CNN head: gw_cnn_act (layer 1 from the obs descriptors through the
         per-position delta table, include/actor_ops.h), then the same fused layers 2-3 + noise +
         softmax + mask + argmax as the MLP path.  patch = P: the head built for P x P inputs on each
@@ -594,6 +626,7 @@ class MultiAgentActors(nn.Module):
                     _lib.check(st["lib"].gw_cnn_prepare(env.handle, C.byref(st["spec"]), st["ws"].data_ptr(), stream),
                                "gw_cnn_prepare")
             st["key"] = key
+            listed = False  # a listing made before the workspace was re-derived is not used
         if actions_out is None:
             actions_out = torch.empty((E, K), dtype=torch.int32, device=dev)
         if probs_out is None:
@@ -611,7 +644,10 @@ class MultiAgentActors(nn.Module):
                 uniform.contiguous().data_ptr() if uniform is not None else None,
                 mask.data_ptr() if mask is not None else None, actions_out.data_ptr(), probs_out.data_ptr(),
                 logits_out.data_ptr() if logits_out is not None else None, torch.cuda.current_stream(dev).cuda_stream)
-        if patch:
+        st["pending"] = False  # either act leaves the bucket counters zeroed for the next listing
+        if patch and listed:
+            _lib.check(st["lib"].gw_patch_cnn_act_listed(env.handle, patch, *args), "gw_patch_cnn_act_listed")
+        elif patch:
             _lib.check(st["lib"].gw_patch_cnn_act(env.handle, patch, *args), "gw_patch_cnn_act")
         else:
             _lib.check(st["lib"].gw_cnn_act(env.handle, *args), "gw_cnn_act")

@@ -236,6 +236,13 @@ class Rollout:
             self._pstream = torch.cuda.Stream(device=env.device)
             self._pev = torch.cuda.Event()
         self._pev_live = False
+        # the CNN head on windows: the step's windows and the listing of the positions the next act
+        # recomputes in ONE launch (gw_patch_cnn_write_list), then the act without its listing
+        # (gw_patch_cnn_act_listed).  GW_CNN_WRITE_LIST=0: the separate writer and act (A/B)
+        self._cnn_list = (self.fused and bool(self.patch) and getattr(actors, "arch", "") == "cnn" and
+                          not self.patch_async and self.replay is not None and env.device.type == "cuda" and
+                          env.E % 4 == 0 and os.environ.get("GW_CNN_WRITE_LIST", "1") != "0")
+        self._lists_ready = False  # a listing for the env's current descriptors was launched
         self.distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
         rank = dist.get_rank(group) if self.distributed else 0
         # the PyTorch actor's Gumbel noise: one stream per rank (the fused actor's Philox noise is
@@ -311,6 +318,7 @@ class Rollout:
         # count restarts, so t_dev never runs ahead of the transitions written
         self._patch_join()
         self._flush()
+        self._lists_ready = False  # new descriptors: the next act lists itself
         if self.replay is not None:
             obs, mask = self.env.reset()
             if self.patch:
@@ -341,6 +349,7 @@ class Rollout:
             return
         self._patch_join()
         self._flush()
+        self._lists_ready = False
         t, S = rp.t, rp.S
         cur, prev = t % S, (t - 1) % S
         if t > 0:
@@ -374,10 +383,12 @@ class Rollout:
             if self._dev_counter():  # counter = _noise_base + t_dev (== _calls), read on the device
                 actions, probs = self.actors.act_env(env, mask, self.training, seed=self.seed, counter=self._noise_base,
                                                      counter_dev=self.replay.t_dev, actions_out=self._actions,
-                                                     probs_out=probs_out, patch=self.patch)
+                                                     probs_out=probs_out, patch=self.patch, listed=self._lists_ready)
             else:
                 actions, probs = self.actors.act_env(env, mask, self.training, seed=self.seed, counter=self._calls,
-                                                     actions_out=self._actions, probs_out=probs_out, patch=self.patch)
+                                                     actions_out=self._actions, probs_out=probs_out, patch=self.patch,
+                                                     listed=self._lists_ready)
+            self._lists_ready = False
             self._calls += 1
         elif self.actors is not None:
             if not self.patch:
@@ -413,7 +424,11 @@ class Rollout:
                 self._pev.record(self._pstream)
                 self._pev_live = True
             elif self.patch:  # the step's obs / terminal obs as patches, straight into the ring
-                env.obs_patch(self.patch, final=True, out=rp.obs[nxt], final_out=rp.final_obs[cur])
+                if not (self._cnn_list and not env.fear_async and
+                        self.actors.patch_cnn_write_list(env, self.patch, rp.obs[nxt], rp.final_obs[cur])):
+                    env.obs_patch(self.patch, final=True, out=rp.obs[nxt], final_out=rp.final_obs[cur])
+                else:
+                    self._lists_ready = True
             if probs is not None and probs.data_ptr() != rp.probs[cur].data_ptr():
                 rp.probs[cur].copy_(probs)
             rp.t = self.t + 1

@@ -128,3 +128,76 @@ def test_fused_patch_cnn_rollout_matches_torch_rollout_without_noise():
         torch.testing.assert_close(ros[0].replay.probs, ros[1].replay.probs, rtol=0, atol=5e-5)
     for e in envs:
         e.close()
+
+
+def test_write_list_equals_obs_patch_and_act():
+    """gw_patch_cnn_write_list == gw_obs_patch (windows and terminal windows, bit for bit) and,
+    with gw_patch_cnn_act_listed, == gw_patch_cnn_act (actions and probabilities bit for bit),
+    over a rollout with auto-resets; a refused second listing while one is pending, a listing
+    consumed by the self-listing act, and a weight change after the listing (the act then
+    re-derives and lists itself), included."""
+    sc = S.builtin("grid64_n8")
+    P, E = 16, 3000
+    env = VecGridEnv(sc, num_envs=E, fear=False, seed=4, max_steps=12, obs=False)
+    actors = _actors(sc.K, P, seed=6)
+    env.reset()
+    actors.act_env(env, env.out["mask"], True, seed=2, counter=0, patch=P)  # derives the workspace
+    K = sc.K
+    outs = [torch.full((K, E, P, P), float("nan"), device="cuda") for _ in range(4)]
+    for t in range(30):
+        assert actors.patch_cnn_write_list(env, P, outs[0], outs[1])
+        if t % 7 == 3:  # no second listing while one is pending (its counts would add up)
+            assert not actors.patch_cnn_write_list(env, P, outs[0], outs[1])
+        env.obs_patch(P, final=True, out=outs[2], final_out=outs[3])
+        assert torch.equal(outs[0], outs[2]), t
+        assert torch.equal(torch.nan_to_num(outs[1], nan=7.0), torch.nan_to_num(outs[3], nan=7.0)), t
+        if t == 17:  # a weight change after the listing: act_env re-derives and lists itself
+            with torch.no_grad():
+                actors.nets[1].mlp[0].bias.add_(0.01)
+        if t % 5 == 4:  # the listing consumed by the self-listing act (gw_patch_cnn_act zeroes first)
+            a1, p1 = [x.clone() for x in actors.act_env(env, env.out["mask"], True, seed=2, counter=t, patch=P)]
+        else:
+            a1, p1 = [x.clone() for x in actors.act_env(env, env.out["mask"], True, seed=2, counter=t, patch=P,
+                                                         listed=True)]
+        a0, p0 = actors.act_env(env, env.out["mask"], True, seed=2, counter=t, patch=P)
+        assert torch.equal(a0, a1) and torch.equal(p0, p1), t
+        env.step(a0)
+    env.close()
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_rollout_write_list_equals_separate_writer_and_act(graph, monkeypatch):
+    """Rollout with the CNN head on windows (default: the windows and the next act's listing in one
+    launch) == the separate writer and act (GW_CNN_WRITE_LIST=0): identical ring contents over a
+    training rollout with auto-resets and a Rollout.reset in between, eager and as ring-phase
+    graphs."""
+    from marlnav.rollout import Rollout
+    sc = S.builtin("grid64_n8")
+    E, P, n = 2048, 16, 4
+    actors = _actors(sc.K, P, seed=7)
+    rings = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("GW_CNN_WRITE_LIST", fused)
+        env = VecGridEnv(sc, num_envs=E, fear=False, seed=9, max_steps=12, obs=False)
+        ro = Rollout(env, actors, replay_slots=8, training=True, seed=3, patch=P)
+        assert ro._cnn_list == (fused == "1")
+        ro.reset()
+        for _ in range(5):
+            ro.step()
+        ro.reset()  # a listing left by the last step is not used after the reset
+        for _ in range(3):
+            ro.step()
+        if graph:
+            g = ro.capture(n)
+            for _ in range(3):
+                g.replay()
+        else:
+            for _ in range(3 * n):
+                ro.step()
+        ro.fence()
+        torch.cuda.synchronize()
+        rings.append((ro.replay.obs.clone(), ro.replay.probs.clone(), ro.replay.reward.clone(),
+                      ro.replay.done.clone(), torch.nan_to_num(ro.replay.final_obs, nan=7.0)))
+        env.close()
+    for x, y in zip(*rings):
+        assert torch.equal(x, y)
