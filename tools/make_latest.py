@@ -11,7 +11,7 @@ KIND = {"gw::obs_kernel": "obs_kernel", "gw::step_v2": "step_kernel", "gw::fear_
         "gw::step_obs": "step_obs", "act_kernel": "act_kernel", "window_kernel": "window_kernel",
         "wcnn_rare_kernel": "cnn_rare_kernel", "cnn_rare_kernel": "cnn_rare_kernel",
         "wcnn_l1_kernel": "cnn_l1_kernel", "cnn_l1_kernel": "cnn_l1_kernel",
-        "window_rows_kernel": "window_kernel", "wcnn_list_kernel": "cnn_l1_kernel",
+        "window_rows_kernel": "window_kernel", "rows_list_kernel": "window_kernel", "wcnn_list_kernel": "cnn_l1_kernel",
         # the descriptor learner: one update = dcritic_tail + dgrads_adam x 2 + dactor_tail
         "dcritic_tail": "learn_update", "dactor_tail": "learn_update", "dgrads_adam": "learn_update"}
 # kinds made of several kernels: per launch of the first kernel (one per update), the kernels' time summed
@@ -39,6 +39,8 @@ def main(tag, config, cmd=None):
         kind = KIND.get(name.split("<")[0].strip())
         if kind in MULTI:
             continue
+        if kind in kernels and (kernels[kind].get("calls") or 0) >= (v.get("calls") or 0):
+            continue  # a kind with several kernels (a few launches of another form): the most called
         if kind and (v.get("hbm_mb") is not None or v.get("busy_us") or v.get("valu_insts")):
             k = {"avg_us": v["avg_us"], "calls": v.get("calls")}
             if v.get("hbm_mb") is not None:
