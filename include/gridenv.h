@@ -244,6 +244,11 @@ gw_status gw_count_sims(void *env, uint64_t *counter);
  * the terminal cell); either may be NULL.  Works from the descriptors, so it needs no full obs
  * (gw_step_out.obs may be NULL).  Enqueued on stream, after the step on the same stream. */
 gw_status gw_obs_patch(void *env, int32_t P, float *patch, float *final_patch, void *stream);
+/* Arm the NEXT gw_step to also write its P x P windows exactly as gw_obs_patch(env, P, patch,
+ * final_patch) right after it would: with FeAR on (joined) and the row writer's conditions
+ * (2 <= P <= 16, E % 4 == 0) inside the FeAR launch (both read only the world update's outputs),
+ * else as that gw_obs_patch on the step's stream.  One request per step (cleared by gw_step). */
+gw_status gw_step_patch_next(void *env, int32_t P, float *patch, float *final_patch);
 
 /* Async observation writes (a software pipeline across steps; default off).  While enabled,
  * gw_step enqueues the world update (+ FeAR) on an internal stream that waits for the caller's

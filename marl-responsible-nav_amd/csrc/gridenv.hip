@@ -32,6 +32,7 @@
 #include "patch_ops.h"
 #include "gridenv.h"
 #include "prof.h"
+#include "window_rows.h"
 
 namespace gw {
 
@@ -1916,7 +1917,7 @@ __global__ void __launch_bounds__(128) step_obs(Params p, Params q, float *__res
 // without the env's own update.  Dynamic LDS: [cell table][Resp 100 f64] (no CDFs).
 // ---------------------------------------------------------------------------------------
 template <int N, int KMAX, bool WIDE>
-__global__ void __launch_bounds__(128) fear_v2(Params p) {
+__device__ __forceinline__ void fear_block(const Params &p, uint32_t bid) {
     using Cfg = V2Cfg<N, KMAX, true, WIDE>;
     using Sh = V2Shared<N, KMAX, true, false, WIDE>;
     constexpr int BE = Cfg::BE, T = Cfg::THREADS;
@@ -1926,8 +1927,8 @@ __global__ void __launch_bounds__(128) fear_v2(Params p) {
     double *resp_s = reinterpret_cast<double *>(dyn + p.resp_off);
 
     const int tid = threadIdx.x;
-    if (p.e_begin + (int64_t)blockIdx.x * BE >= p.e_end) return;  // uniform per block
-    const int64_t e0 = p.e_begin + (int64_t)blockIdx.x * BE;
+    if (p.e_begin + (int64_t)bid * BE >= p.e_end) return;  // uniform per block
+    const int64_t e0 = p.e_begin + (int64_t)bid * BE;
     const int nenv = (int)min((int64_t)BE, p.e_end - e0);
     const int K = p.K;
     int pos[N], act[N], rew[MAXN];
@@ -1999,6 +2000,27 @@ __global__ void __launch_bounds__(128) fear_v2(Params p) {
         ct.v[5] = np_sum_small(shaped, K);
     }
     block_stats<T, ST_F64_FEAR, 0u>(p, ct, sh.red, tid, p.stats_row0 + e0 / BE);
+}
+
+template <int N, int KMAX, bool WIDE>
+__global__ void __launch_bounds__(128) fear_v2(Params p) {
+    fear_block<N, KMAX, WIDE>(p, blockIdx.x);
+}
+
+// fear_v2 and the step's P x P windows (gw_step_patch_next; the row writer of csrc/window_rows.h on
+// two waves per block) in ONE launch: both read only the world update's outputs, and the writer's
+// HBM stream fills the CU slots the latency-bound FeAR blocks leave
+template <int N, int KMAX, bool WIDE>
+__global__ void __launch_bounds__(128) fear_rows_kernel(Params p, PatchArgs a, uint32_t nfear, uint32_t nrx) {
+    if (blockIdx.x < nfear) {
+        fear_block<N, KMAX, WIDE>(p, blockIdx.x);
+        return;
+    }
+    // the rows' LDS slices in the dynamic region the FeAR blocks use for their tables (the launch
+    // sizes it for both), so the writer adds no LDS to the FeAR blocks' footprint
+    extern __shared__ __attribute__((aligned(16))) uint8_t dynr[];
+    const uint32_t r = blockIdx.x - nfear;
+    gwrows::rows_block<N + 1, 16, 2, 2>(a, r % nrx, (int)(r / nrx), reinterpret_cast<float4 (*)[64 * 4]>(dynr));
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2174,6 +2196,13 @@ struct Env {
     bool obs_lazy = false;                        // gw_set_obs_async(env, 2): launch at the next step
     bool obs_hi = false;                          // GW_OBS_PRIO=hi (A/B): obs stream high priority, aux normal
     int obs_chunks = 1;                           // GW_OBS_CHUNKS: the obs writer as this many launches
+    // gw_step_patch_next: the next gw_step also writes the step's P x P windows (in the FeAR launch
+    // where it can: fear_rows_kernel; else as gw_obs_patch right after the step)
+    struct PatchReq {
+        bool armed = false, done = false;
+        int P = 0;
+        float *patch = nullptr, *final_patch = nullptr;
+    } patch_req;
     // one obs stream: a second one alternating with the descriptor buffer (so obs_kernel(t+1)
     // could start while obs_kernel(t) drains) measured 2.1x slower at C3 (more streams than the
     // process's hardware queues, GPU_MAX_HW_QUEUES = 4; profiles/r1_async)
@@ -2557,6 +2586,63 @@ template <int N>
 int fear_be(const Env *env) {
     if (env->fear_wide) return env->K <= 2 ? gw::V2Cfg<N, 2, true, true>::BE : gw::V2Cfg<N, N, true, true>::BE;
     return env->K <= 2 ? gw::V2Cfg<N, 2, true>::BE : gw::V2Cfg<N, N, true>::BE;
+}
+
+// the windows' writer args for the env's current descriptors (gw_obs_patch's, without its table)
+gw::PatchArgs patch_args(const Env *env, int P, float *patch, float *final_patch) {
+    gw::PatchArgs a;
+    a.desc = env->desc;
+    a.roadbits = env->roadbits;
+    a.base = env->base;
+    a.patch = patch;
+    a.final_patch = final_patch;
+    a.E = env->E;
+    a.H = env->H;
+    a.W = env->W;
+    a.N = env->N;
+    a.K = env->K;
+    a.P = P;
+    a.variant = env->variant;
+    for (int k = 0; k < GW_MAX_AGENTS; ++k) a.apples[k] = k < env->K ? env->apples[k] : -1;
+    return a;
+}
+
+template <int N, int KMAX, bool WIDE>
+hipError_t launch_fear_rows_k(const Env *env, const gw::Params &p0, const gw::PatchArgs &a, hipStream_t s) {
+    constexpr int BE = gw::V2Cfg<N, KMAX, true, WIDE>::BE;
+    gw::Params p = p0;
+    p.lds_cdf = 0;
+    p.ctab_off = 0;
+    p.resp_off = ((env->HW * 4 + 15) / 16) * 16;
+    p.stats_row0 = defer_step_rows<N>(env);
+    const int64_t n = p.e_end - p.e_begin;
+    const unsigned nfear = (unsigned)((n + BE - 1) / BE);
+    const unsigned nrx = (unsigned)((a.E * a.P + 255) / 256);  // 2 waves x 2 runs x 64 rows per block
+    const size_t dyn = std::max((size_t)p.resp_off + 100 * sizeof(double), sizeof(float4) * 2 * 64 * 4);
+    gw_launch((gw::fear_rows_kernel<N, KMAX, WIDE>), dim3(nfear + nrx * (unsigned)a.K), dim3(128), dyn, s, p, a,
+              nfear, nrx);
+    return hipGetLastError();
+}
+
+template <int N>
+hipError_t launch_fear_rows(const Env *env, const gw::Params &p, const gw::PatchArgs &a, hipStream_t s) {
+    if (env->fear_wide)
+        return env->K <= 2 ? launch_fear_rows_k<N, 2, true>(env, p, a, s) : launch_fear_rows_k<N, N, true>(env, p, a, s);
+    return env->K <= 2 ? launch_fear_rows_k<N, 2, false>(env, p, a, s) : launch_fear_rows_k<N, N, false>(env, p, a, s);
+}
+
+hipError_t dispatch_fear_rows(const Env *env, const gw::Params &p, const gw::PatchArgs &a, hipStream_t s) {
+    switch (env->N) {
+        case 1: return launch_fear_rows<1>(env, p, a, s);
+        case 2: return launch_fear_rows<2>(env, p, a, s);
+        case 3: return launch_fear_rows<3>(env, p, a, s);
+        case 4: return launch_fear_rows<4>(env, p, a, s);
+        case 5: return launch_fear_rows<5>(env, p, a, s);
+        case 6: return launch_fear_rows<6>(env, p, a, s);
+        case 7: return launch_fear_rows<7>(env, p, a, s);
+        case 8: return launch_fear_rows<8>(env, p, a, s);
+    }
+    return hipErrorInvalidValue;
 }
 
 hipError_t dispatch_fear(const Env *env, const gw::Params &p, hipStream_t s) {
@@ -2947,8 +3033,38 @@ gw_status gw_reset(void *handle, const uint8_t *env_mask, const int32_t *spawn_c
     return GW_OK;
 }
 
+static gw_status obs_patch_launch(Env *env, int32_t P, float *patch, float *final_patch, hipStream_t s);
+
+static gw_status gw_step_body(void *handle, const int32_t *rl_actions, const int32_t *scripted,
+                              const int32_t *spawn, const gw_step_out *out, void *stream);
+
 gw_status gw_step(void *handle, const int32_t *rl_actions, const int32_t *scripted,
                   const int32_t *spawn, const gw_step_out *out, void *stream) {
+    Env *env = static_cast<Env *>(handle);
+    if (!env) return fail(GW_ERR_ARG, "null env");
+    const gw_status st = gw_step_body(handle, rl_actions, scripted, spawn, out, stream);
+    Env::PatchReq rq = env->patch_req;
+    env->patch_req = Env::PatchReq{};
+    if (st != GW_OK || !rq.armed || rq.done) return st;
+    // the requested windows, not written inside the step's launches: as gw_obs_patch right after
+    return obs_patch_launch(env, rq.P, rq.patch, rq.final_patch, static_cast<hipStream_t>(stream));
+}
+
+gw_status gw_step_patch_next(void *handle, int32_t P, float *patch, float *final_patch) {
+    Env *env = static_cast<Env *>(handle);
+    if (!env) return fail(GW_ERR_ARG, "null env");
+    if (P < 1 || P > 129) return fail(GW_ERR_ARG, "gw_step_patch_next: need 1 <= P <= 129");
+    env->patch_req = Env::PatchReq{};
+    if (!patch && !final_patch) return GW_OK;
+    env->patch_req.armed = true;
+    env->patch_req.P = P;
+    env->patch_req.patch = patch;
+    env->patch_req.final_patch = final_patch;
+    return GW_OK;
+}
+
+static gw_status gw_step_body(void *handle, const int32_t *rl_actions, const int32_t *scripted,
+                              const int32_t *spawn, const gw_step_out *out, void *stream) {
     Env *env = static_cast<Env *>(handle);
     if (!env) return fail(GW_ERR_ARG, "null env");
     if (!env->initialized) return fail(GW_ERR_STATE, "gw_step before gw_reset");
@@ -3065,8 +3181,22 @@ gw_status gw_step(void *handle, const int32_t *rl_actions, const int32_t *script
         HIP_TRY(dispatch_step(env, p, s));
         GW_TRY(span_end(s, b, 0));
         if (!want_obs || env->defer_order == 0) {
+            Env::PatchReq &rq = env->patch_req;
+            const int P = rq.P;
+            // the requested windows inside the FeAR launch: the row writer's conditions, whole range
+            const bool rows = rq.armed && !want_obs && rq.patch && P >= 2 && P <= 16 && env->E % 4 == 0 &&
+                              env->N >= 1 && env->N <= 8 && (uint64_t)env->E * (uint64_t)P < (1ull << 32) &&
+                              p.e_begin == 0 && p.e_end == env->E;
             GW_TRY(span_begin(s, b));
-            HIP_TRY(dispatch_fear(env, p, s));
+            if (rows) {
+                // (the world update just wrote env->desc: p.desc is that buffer)
+                gw::PatchArgs a = patch_args(env, P, rq.patch, rq.final_patch);
+                a.desc = p.desc;
+                HIP_TRY(dispatch_fear_rows(env, p, a, s));
+                rq.done = true;
+            } else {
+                HIP_TRY(dispatch_fear(env, p, s));
+            }
             GW_TRY(span_end(s, b, 2));
             if (want_obs) {
                 GW_TRY(span_begin(s, b));
@@ -3384,7 +3514,10 @@ gw_status gw_obs_patch(void *handle, int32_t P, float *patch, float *final_patch
     if (!env) return fail(GW_ERR_ARG, "null env");
     if (P < 1 || P > 129) return fail(GW_ERR_ARG, "gw_obs_patch: need 1 <= P <= 129");
     if (!patch && !final_patch) return GW_OK;
-    hipStream_t s = static_cast<hipStream_t>(stream);
+    return obs_patch_launch(env, P, patch, final_patch, static_cast<hipStream_t>(stream));
+}
+
+static gw_status obs_patch_launch(Env *env, int32_t P, float *patch, float *final_patch, hipStream_t s) {
     GW_TRY(wait_fear(env, s));  // async FeAR: the descriptors are written by the world update (joined)
     gw::PatchArgs a;
     a.desc = env->desc;

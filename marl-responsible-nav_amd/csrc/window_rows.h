@@ -29,8 +29,10 @@ __device__ __forceinline__ float agent_value(bool reset, int n, int k, bool on_a
 }
 
 // block bx of agent k (grid ((E P + 511) / 512, K), 256 threads); s_rows: the block's LDS,
-// [4 waves][64 rows x MAXW / 4 float4]
-template <int NP, int MAXW, int WR_RUNS = 2>  // MAXW: 8, 12 or 16 >= P (the row's registers)
+// [WAVES][64 rows x MAXW / 4 float4]
+// (WAVES = 2: the 128-thread blocks of a launch shared with gridenv.hip's FeAR kernel; the grid
+// then has (E P + 64 WAVES WR_RUNS - 1) / (64 WAVES WR_RUNS) blocks per agent)
+template <int NP, int MAXW, int WR_RUNS = 2, int WAVES = 4>  // MAXW: 8, 12 or 16 >= P (the row's registers)
 __device__ __forceinline__ void rows_block(const gw::PatchArgs &a, uint32_t bx, int k,
                                            float4 (*s_rows)[64 * (MAXW / 4)]) {
 
@@ -41,7 +43,7 @@ __device__ __forceinline__ void rows_block(const gw::PatchArgs &a, uint32_t bx, 
     const uint32_t m_w = (uint32_t)((0x100000000ull + (uint64_t)W - 1) / (uint64_t)W);
     // a wave takes WR_RUNS consecutive runs of 64 rows; every run's descriptor loads are issued
     // before the first run's stores (one round trip per wave, not one per 64 rows)
-    const uint32_t run0 = (bx * 4u + (uint32_t)wave) * WR_RUNS;
+    const uint32_t run0 = (bx * (uint32_t)WAVES + (uint32_t)wave) * WR_RUNS;
     uint32_t fr[WR_RUNS];
     uint4 wsr[WR_RUNS];  // (the terminal words: loaded by the few waves that need them)
 #pragma unroll

@@ -170,7 +170,7 @@ EXPORTS = ["gw_create", "gw_reset", "gw_step", "gw_state_view", "gw_copy_state",
            "gw_adam_step", "gw_soft_update", "gw_obs_view", "gw_set_last_error", "gw_actor_act",
            "gw_actor_workspace_floats", "gw_actor_prepare", "gw_rollout_tick", "gw_set_obs_async",
            "gw_obs_fence", "gw_fear_fence", "gw_set_obs_dtype", "gw_cnn_workspace_floats", "gw_cnn_prepare",
-           "gw_cnn_act", "gw_return_compact", "gw_return_compact_scratch", "gw_kernel_path", "gw_graph_replayed", "gw_obs_patch",
+           "gw_cnn_act", "gw_return_compact", "gw_return_compact_scratch", "gw_kernel_path", "gw_graph_replayed", "gw_obs_patch", "gw_step_patch_next",
            "gw_ln_relu_fwd", "gw_ln_relu_bwd", "gw_gumbel_softmax",
            "gw_replay_gather", "gw_affine_relu_fwd", "gw_affine_relu_bwd",
            "gw_soft_update2", "gw_td_target", "gw_mean_loss_fwd", "gw_mean_loss_bwd",
@@ -275,6 +275,8 @@ def _declare(L):
     L.gw_profile_spans.restype = C.c_int
     L.gw_obs_patch.argtypes = [p, C.c_int32, p, p, p]
     L.gw_obs_patch.restype = C.c_int
+    L.gw_step_patch_next.argtypes = [p, C.c_int32, p, p]
+    L.gw_step_patch_next.restype = C.c_int
     L.gw_gather_pack_scratch.argtypes = [C.c_int64]
     L.gw_gather_pack_scratch.restype = C.c_int64
     L.gw_gather_pack.argtypes = [p, p, C.c_int64, C.c_int64, p, C.c_int64, p, p, p, p]

@@ -415,6 +415,13 @@ class Rollout:
                 # done goes to the ring slot and, from the same kernel, to the gather's send buffer
                 into["done_copy"] = g["done"]
             self._patch_join()  # the previous window writer has read the descriptors
+            # the step's windows inside its FeAR launch (gw_step_patch_next; FeAR on and joined):
+            # the MLP head's rollout, where no listing shares the writer's launch
+            step_patch = (self.patch and not self.patch_async and not self._cnn_list and env.fear_enabled and
+                          not env.fear_async and env.device.type == "cuda" and
+                          os.environ.get("GW_FEAR_PATCH", "1") != "0")
+            if step_patch:
+                env.patch_next(self.patch, rp.obs[nxt], rp.final_obs[cur])
             r = env.step(actions, into=into)
             if self.patch_async:  # the step's windows, beside the next step's actor
                 main = torch.cuda.current_stream(env.device)
@@ -423,6 +430,8 @@ class Rollout:
                     env.obs_patch(self.patch, final=True, out=rp.obs[nxt], final_out=rp.final_obs[cur])
                 self._pev.record(self._pstream)
                 self._pev_live = True
+            elif self.patch and step_patch:
+                pass  # written by the step (gw_step_patch_next)
             elif self.patch:  # the step's obs / terminal obs as patches, straight into the ring
                 if not (self._cnn_list and not env.fear_async and
                         self.actors.patch_cnn_write_list(env, self.patch, rp.obs[nxt], rp.final_obs[cur])):

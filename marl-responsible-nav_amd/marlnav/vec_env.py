@@ -376,6 +376,16 @@ class VecGridEnv:
                                              self._stream()), "gw_obs_patch")
         return (out, final_out) if final else out
 
+    def patch_next(self, size: int, out: torch.Tensor, final_out: torch.Tensor | None = None):
+        """Have the next ``step`` write its P x P windows into ``out`` / ``final_out`` exactly as
+        ``obs_patch(size, final=True, out=out, final_out=final_out)`` right after it would
+        (gw_step_patch_next): with FeAR on, inside the FeAR launch where the row writer applies."""
+        K, E, P = self.K, self.E, int(size)
+        for t in (out, final_out):
+            if t is not None and (t.dtype != torch.float32 or t.numel() != K * E * P * P or not t.is_contiguous()):
+                raise ValueError(f"patch_next: need contiguous float32 [K, E, {P}, {P}] buffers")
+        _lib.check(self.lib.gw_step_patch_next(self.handle, P, _ptr(out), _ptr(final_out)), "gw_step_patch_next")
+
     def set_obs_async(self, enable: bool | str = True, fear_async: bool = False):
         """Pipeline the obs writer of step t with the world update of step t+1 (gw_set_obs_async).
         While on, ``step``'s obs / final_obs are ready on the current stream only after

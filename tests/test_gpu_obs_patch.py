@@ -162,3 +162,66 @@ def test_patch_rollout_feeds_the_actor_and_the_ring():
     assert state.shape == (2, 256, P, P) and nxt.shape == (2, 256, P, P)
     env_p.close()
     env_f.close()
+
+
+@pytest.mark.parametrize("scen,E,P,fear", [("grid32", 4096, 11, True), ("grid64_n8", 2048, 16, True),
+                                           ("grid32", 1024, 8, True), ("level3", 64, 4, True),
+                                           ("grid32", 1000, 11, False), ("grid32", 1022, 11, True)])
+def test_step_patch_next_equals_obs_patch_after_the_step(scen, E, P, fear):
+    """gw_step_patch_next + gw_step == gw_step + gw_obs_patch: the windows and terminal windows bit
+    for bit, and every step output unchanged, over auto-resets.  FeAR on with E % 4 == 0: the
+    windows come from the FeAR launch (fear_rows_kernel); FeAR off or E % 4 != 0: the fallback
+    writer after the step."""
+    envs = [VecGridEnv(scen, num_envs=E, fear=fear, fear_weight=-5.0, seed=21, max_steps=9, obs=False)
+            for _ in range(2)]
+    K = envs[0].K
+    bufs = [[torch.full((K, E, P, P), float("nan"), device="cuda") for _ in range(2)] for _ in range(2)]
+    for env in envs:
+        env.reset()
+    for t in range(25):
+        envs[0].patch_next(P, bufs[0][0], bufs[0][1])
+        r0 = envs[0].step()
+        r1 = envs[1].step()
+        envs[1].obs_patch(P, final=True, out=bufs[1][0], final_out=bufs[1][1])
+        assert torch.equal(bufs[0][0], bufs[1][0]), t
+        assert torch.equal(torch.nan_to_num(bufs[0][1], nan=7.0), torch.nan_to_num(bufs[1][1], nan=7.0)), t
+        for name in ("reward", "done", "shaped", "fear"):
+            x, y = getattr(r0, name), getattr(r1, name)
+            if x is not None:
+                assert torch.equal(x, y), (t, name)
+    for env in envs:
+        env.close()
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_rollout_windows_from_the_fear_launch(graph, monkeypatch):
+    """Rollout(patch=P) with the fused MLP window actor and FeAR on writes each step's windows from
+    the FeAR launch (default) == the writer after the step (GW_FEAR_PATCH=0): identical ring
+    contents, eager and as ring-phase graphs."""
+    from marlnav.actor import MultiAgentActors
+    from marlnav.rollout import Rollout
+    E, P, n = 2048, 11, 4
+    actors = MultiAgentActors(2, P, P, "mlp", device="cuda", seed=4)
+    rings = []
+    for on in ("1", "0"):
+        monkeypatch.setenv("GW_FEAR_PATCH", on)
+        env = VecGridEnv("grid32", num_envs=E, fear=True, fear_weight=-5.0, seed=13, max_steps=10, obs=False)
+        ro = Rollout(env, actors, replay_slots=8, training=True, seed=6, patch=P)
+        assert ro.fused
+        ro.reset()
+        for _ in range(3):
+            ro.step()
+        if graph:
+            g = ro.capture(n)
+            for _ in range(3):
+                g.replay()
+        else:
+            for _ in range(3 * n):
+                ro.step()
+        ro.fence()
+        torch.cuda.synchronize()
+        rings.append((ro.replay.obs.clone(), ro.replay.probs.clone(), ro.replay.reward.clone(),
+                      ro.replay.done.clone(), torch.nan_to_num(ro.replay.final_obs, nan=7.0)))
+        env.close()
+    for x, y in zip(*rings):
+        assert torch.equal(x, y)
