@@ -7,7 +7,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # rocprofv3 kernel name (namespace stripped, before the template arguments) -> bench.py's SPAN_KINDS name
-KIND = {"gw::obs_kernel": "obs_kernel", "gw::step_v2": "step_kernel", "gw::fear_v2": "fear_kernel",
+KIND = {"gw::obs_kernel": "obs_kernel", "gw::step_v2": "step_kernel", "gw::fear_v2": "fear_kernel", "gw::fear_rows_kernel": "fear_kernel",
         "gw::step_obs": "step_obs", "act_kernel": "act_kernel", "window_kernel": "window_kernel",
         "wcnn_rare_kernel": "cnn_rare_kernel", "cnn_rare_kernel": "cnn_rare_kernel",
         "wcnn_l1_kernel": "cnn_l1_kernel", "cnn_l1_kernel": "cnn_l1_kernel",
