@@ -759,6 +759,14 @@ def main():
                 "dedup_factor": E * K * (N - 1) * 18 / sims if sims else None,
                 "unit": "world updates (custom/Responsibility.py:16-54 UpdateGWorld counterfactuals)"},
         }
+        rf = line["roofline"]
+        if dom_bound == "valu" and dom in per_kind and per_kind[dom].get("achieved"):
+            # an integer-VALU kernel leads (c5patch: FeAR with the windows in its launch): its
+            # instruction rate against the VALU issue peak, as in roofline.kernels
+            pk = per_kind[dom]
+            rf.update(achieved=pk["achieved"], peak=VALU_PEAK_GIPS, unit="G inst/s", frac=pk["frac"],
+                      bytes_per_launch=None, frac_rocprof=None, frac_per_launch_span=None,
+                      achieved_per_period=None, frac_per_period=None)
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
         print(json.dumps(line), flush=True)
