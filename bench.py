@@ -90,9 +90,15 @@ def algorithmic_bytes(N: int, K: int, HW: int, obs_bytes: int = 4):
 SPAN_KINDS = {0: "step_kernel", 1: "obs_kernel", 2: "fear_kernel", 3: "act_kernel", 4: "cnn_l1_kernel",
               5: "cnn_list_kernels", 6: "cnn_rare_kernel", 7: "window_kernel", 8: "learn_update"}
 F32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: dense f32 MFMA (v_mfma_f32_16x16x4_f32), no xf32 on gfx950
-# VALU issue peak (MI355X_MICROARCH.md "Execution model"): each of 256 CUs x 4 SIMD-32 issues one
-# wave64 vector instruction per 2 cycles at the 2.4 GHz max clock = 1.2288e12 wave-instructions/s
+# VALU issue peak (MI355X_MICROARCH.md "Execution model": "A wave (64 lanes) is assigned to one SIMD
+# and issues each VALU instruction over 2 cycles (32 lanes/cycle x 2)"): each of 256 CUs x 4 SIMD-32
+# issues one wave64 vector instruction per 2 cycles at the 2.4 GHz max clock = 1.2288e12
+# wave-instructions/s = 64 lanes x 4 SIMDs / 2 = 128 lane-ops per CU per clock.  Against the
+# one-wave64-per-CU-per-clock figure sometimes quoted for CDNA (64 lane-ops per CU per clock) every
+# VALU fraction would be 2x; the line states the basis (VALU_PEAK_BASIS)
 VALU_PEAK_GIPS = 256 * 4 * 2.4e9 / 2 / 1e9
+VALU_PEAK_BASIS = ("256 CUs x 4 SIMD-32 x 2.4 GHz / 2 cycles per wave64 VALU instruction (MI355X_MICROARCH.md "
+                   "'Execution model'); at 1 wave64 per CU per clock the fractions would double")
 HID, N_ACT = 128, 9        # the fused actors' hidden width and actions (configs/mlp.yaml, configs/cnn.yaml)
 
 
@@ -663,6 +669,16 @@ def main():
         dom_bound = per_kind.get(dom, {}).get("bound", "hbm")
         mfma = dom_bound == "mfma"
         peak_u = F32_MFMA_PEAK_TFS if mfma else HBM_PEAK_GBS
+        # the busy time comes from profiled steps after the timed region (their
+        # events cost a few us per step), so it can exceed the timed step.  A kernel's busy time per
+        # step cannot exceed the step it ran in: the time per launch used below is capped at the
+        # timed ms_per_step / launches per step, and the uncapped profiled figure is kept beside it
+        timed_ms = t_max * 1e3 / args.steps
+        dom_lps = per_kind.get(dom, {}).get("launches_per_step") or 1.0
+        dur_profiled = dur
+        dur_cap = timed_ms / max(dom_lps, 1e-9)
+        if dur > dur_cap:
+            dur = dur_cap
         # achieved: GB/s (hbm) or TFLOP/s (mfma) of the dominant kernel's algorithmic work per launch
         # over its busy time per launch
         achieved = (bytes_per_launch / (dur * 1e-3) / (1e12 if mfma else 1e9)) if (dur > 0 and bytes_per_launch) else None
@@ -682,7 +698,9 @@ def main():
                 if pk.get("hbm_bytes_per_step") is not None:
                     traffic = pk["hbm_bytes_per_step"] / live_lps
                 if bytes_per_launch and pk.get("busy_us_per_step"):
-                    prof_frac = bytes_per_launch * live_lps / (pk["busy_us_per_step"] * 1e-6) / \
+                    # the trace's busy time per step, capped at the timed step like `dur`
+                    busy_us = min(pk["busy_us_per_step"], timed_ms * 1e3)
+                    prof_frac = bytes_per_launch * live_lps / (busy_us * 1e-6) / \
                         (1e12 if mfma else 1e9) / peak_u
         except (OSError, KeyError, ValueError, TypeError):
             pass
@@ -717,6 +735,13 @@ def main():
                          # duration, which overlapping writers stretch (the per-span figure beside it
                          # is the lower, per-launch view)
                          "avg_launch_ms": dur, "avg_launch_span_ms": span,
+                         # the busy time per launch as profiled (uncapped) and the cap applied to it
+                         "avg_launch_busy_profiled_ms": dur_profiled, "avg_launch_cap_timed_ms": dur_cap,
+                         "busy_capped_by_timed_step": dur_profiled > dur_cap,
+                         # the dominant kernel's work per step over the whole timed step: a lower
+                         # bound of its rate (its busy time per step is at most the step)
+                         "frac_timed_step_bound": (bytes_per_launch * dom_lps / (timed_ms * 1e-3) /
+                                                   (1e12 if mfma else 1e9) / peak_u) if bytes_per_launch else None,
                          "frac_per_launch_span": (bytes_per_launch / (span * 1e-3) / (1e12 if mfma else 1e9) / peak_u
                                                   if (span and span > 0 and bytes_per_launch) else None),
                          "launches_profiled": busy[1 if dom in ("obs_kernel", "step_obs") else
@@ -738,7 +763,6 @@ def main():
             "kernels_ms": {"profiled_steps": nprof, "step_kernel": avg_step_ms, "obs_kernel": avg_obs_ms, "fear_kernel": avg_fear_ms,
                            "kernel_path": env.kernel_path,
                            "stream_ms_per_step": gpu_ms / args.steps,
-                           "pipeline_chunks": int(os.environ.get("GW_CHUNKS", "1")) if not env.fused else 1,
                            "obs_async": obs_mode, "fear_async": env.fear_async,
                            "graph_steps": graph_n, "obs_ring": n_ring,
                            "host_enqueue_ms_per_step": t_enq * 1e3 / args.steps,
@@ -765,6 +789,7 @@ def main():
             # instruction rate against the VALU issue peak, as in roofline.kernels
             pk = per_kind[dom]
             rf.update(achieved=pk["achieved"], peak=VALU_PEAK_GIPS, unit="G inst/s", frac=pk["frac"],
+                      peak_basis=VALU_PEAK_BASIS,
                       bytes_per_launch=None, frac_rocprof=None, frac_per_launch_span=None,
                       achieved_per_period=None, frac_per_period=None)
         if not args.no_cpu_baseline and world == 1:

@@ -187,10 +187,11 @@ gw_status gw_fear_matrix(void *env, int64_t n, const int32_t *cells, const int32
  * kernel's rows then fear_v2's rows, each kernel filling the fields it owns, zeros elsewhere). */
 int64_t gw_stats_rows(void *env);
 
-/* The kernel path gw_create chose: 0 "v1", 1 "split", 2 "fused", 3 "defer", 4 "merged".
- * GW_KERNEL selects it; unset: "merged" when a step's obs is at most GW_MERGE_BYTES (default
- * 160 MiB: small batches, bound by the step's latency chain, gain from one step_obs launch per
- * pipelined step), else "defer".  -1 on a null handle. */
+/* The kernel path gw_create chose: 3 "defer", 4 "merged" (values 0-2 named the round-1..5 A/B
+ * paths "v1", "split", "fused", removed in round 6).  "merged" when a step's obs is at most
+ * GW_MERGE_BYTES (default 160 MiB: small batches, bound by the step's latency chain, gain from
+ * one step_obs launch per pipelined step), else "defer"; GW_KERNEL=defer|merged forces one (both
+ * produce the same results).  -1 on a null handle. */
 int64_t gw_kernel_path(void *env);
 
 /* After replaying (on `stream`) a HIP graph of captured gw_step calls: the env's host-side
@@ -266,13 +267,13 @@ gw_status gw_step_patch_next(void *env, int32_t P, float *patch, float *final_pa
  * stream and overlaps the caller's next work (an actor that needs only the descriptors and
  * masks); those outputs are ready on `stream` after gw_fear_fence (gw_reset, gw_copy_state
  * and the next gw_step order themselves).
- * Only the split / defer kernel paths pipeline; the others stay synchronous. */
+ * Both kernel paths pipeline (defer: the writer on its own streams; merged: one step_obs launch). */
 gw_status gw_set_obs_async(void *env, int enable);
 
 /* Observation element type of every obs / final_obs buffer the env writes (gw_reset, gw_step):
  * GW_OBS_F32 (default; the reference's values as float32) or GW_OBS_BF16 (the same values as
  * bfloat16 bits, [K][E][H*W] uint16: every value the env produces is exact in bf16, so this is
- * lossless and halves the obs bytes; needs H*W % 8 == 0 and the split / defer kernel paths).
+ * lossless and halves the obs bytes; needs H*W % 8 == 0).
  * The float* obs pointers then address bf16 buffers.  Called before the first gw_reset it may
  * also change gw_stats_rows (the FeAR kernel's envs per block follow the format's best choice):
  * size the stats buffer after it. */

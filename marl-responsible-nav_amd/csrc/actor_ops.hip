@@ -44,6 +44,7 @@
 
 #include "actor_ops.h"
 #include "prof.h"
+#include "measure.h"
 #include "window_rows.h"
 
 namespace {
@@ -163,7 +164,7 @@ struct ActParams {
 __device__ unsigned long long g_act_clk[1024][16];
 #define ACT_STAMP(slot)                                                                  \
     do {                                                                                 \
-        if ((p.ab & 8) && tid == 0 && bid < 1024 && (slot) < 16) g_act_clk[bid][slot] = clock64(); \
+        if ((GW_AB(p.ab, 8)) && tid == 0 && bid < 1024 && (slot) < 16) g_act_clk[bid][slot] = clock64(); \
     } while (0)
 
 // Philox4x32-10, the same generator as gridenv.hip (keyed draws, graph- and shard-invariant)
@@ -344,7 +345,7 @@ __global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
                                : p.w2img + (size_t)k * (W2IMG / 4);
         constexpr int R = NW2 / THREADS;
         float4 r[R];
-        if (!(p.ab & 32)) {  // GW_ACT_AB bit 5 (measurement only): no W2 staging
+        if (!(GW_AB(p.ab, 32))) {  // GW_ACT_AB bit 5 (measurement only): no W2 staging
 #pragma unroll
         for (int i = 0; i < R; ++i) r[i] = w2[i * THREADS + tid];
 #pragma unroll
@@ -352,7 +353,7 @@ __global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
         }
         for (int i = tid; i < W3IMG / 4; i += THREADS) s_w3[i] = p.w3img[(size_t)k * (W3IMG / 4) + i];
         if (tid < HID) {
-            if (p.c1_part && !(p.ab & 64)) {  // prep_images' c1 (GW_ACT_AB bit 6, measurement: skipped): b1 + the slices added in slice order (32 loads in flight)
+            if (p.c1_part && !(GW_AB(p.ab, 64))) {  // prep_images' c1 (GW_ACT_AB bit 6, measurement: skipped): b1 + the slices added in slice order (32 loads in flight)
                 float part = 0.0f;
                 const float *ps = p.c1_part + (size_t)k * p.c1_nslices * HID + tid;
                 for (int s0 = 0; s0 < p.c1_nslices; s0 += 32) {
@@ -494,8 +495,8 @@ __global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
                 last = last && in;
                 row = in ? wr * p.P + wc : 0;
             }
-            dlt[i] = (last && !(p.ab & 1)) ? pv[i] - map : 0.0f;
-            rowc[i] = (p.ab & 16) ? q : row * (HID / 4) + q;  // float4 index of features 4q .. 4q + 3 of row
+            dlt[i] = (last && !(GW_AB(p.ab, 1))) ? pv[i] - map : 0.0f;
+            rowc[i] = (GW_AB(p.ab, 16)) ? q : row * (HID / 4) + q;  // float4 index of features 4q .. 4q + 3 of row
         }
         const float4 *w1v = reinterpret_cast<const float4 *>(w1);
 #pragma unroll
@@ -540,7 +541,7 @@ __global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
         f32x4 acc[8];
 #pragma unroll
         for (int m = 0; m < 8; ++m) acc[m] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        if (BF3 && !(p.ab & 2)) {
+        if (BF3 && !(GW_AB(p.ab, 2))) {
 #pragma unroll
             for (int kb = 0; kb < 4; ++kb) {
                 // B fragments: registers 8kb .. 8kb + 7 = features 32kb + 4q + j (j < 4) and
@@ -571,7 +572,7 @@ __global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
                     acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bh, acc[m], 0, 0, 0);
                 }
             }
-        } else if (!(p.ab & 2)) {
+        } else if (!(GW_AB(p.ab, 2))) {
 #pragma unroll
             for (int s4 = 0; s4 < 8; ++s4) {
 #pragma unroll
@@ -631,7 +632,7 @@ __global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
             for (int r = 0; r < 4; ++r) o3[m & 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[r], acc[m][r], o3[m & 1], 0, 0, 0);
         }
         const f32x4 out = o3[0] + o3[1];
-        if (p.ab & 4) {
+        if (GW_AB(p.ab, 4)) {
             ACT_STAMP(6 + 5 * it);
             continue;
         }
@@ -1024,8 +1025,8 @@ __global__ void __launch_bounds__(64 * L1_WAVES, 4) cnn_l1_kernel(CnnParams p, L
             s_rows[wave][nrow++][lane] = (((k * p.P + pos[i]) * 16 + 4 * (y & 3) + (x & 3)) * NV + vidx[i]) * (HID / 4);
         }
     }
-    if (p.ab & 2) nrow = 0;
-    if (p.ab & 1) rare = 0;
+    if (GW_AB(p.ab, 2)) nrow = 0;
+    if (GW_AB(p.ab, 1)) rare = 0;
     {
         float a[32];
         const float4 *z = reinterpret_cast<const float4 *>(p.ws.zmap + k * HID);
@@ -1475,7 +1476,7 @@ __global__ void __launch_bounds__(256) wcnn_l1_kernel(CnnParams p, Lists lists) 
         qmask |= 1u << ((wr >> 2) * p.Wq + (wc >> 2));
     }
     if (!ctr_set && map_at(ctr) != vo) qmask |= 1u << ((half >> 2) * p.Wq + (half >> 2));
-    if (!valid || (p.ab & 4)) qmask = 0;  // (bit 2, measurement only: decode, list nothing)
+    if (!valid || (GW_AB(p.ab, 4))) qmask = 0;  // (bit 2, measurement only: decode, list nothing)
     if (valid) {
         p.ws.rare_n[(size_t)k * p.E + e] = __popc(qmask);
         lists.item[(size_t)k * p.E + e] = (int)qmask;
@@ -1565,7 +1566,7 @@ __device__ __forceinline__ void list_block(const CnnParams &p, int bx, int k) {
         }
         if (!ctr_set && map_at(ctr) != vo) qmask |= 1u << ((half >> 2) * p.Wq + (half >> 2));
         const bool valid = ev[r] < p.E;
-        if (!valid || (p.ab & 4)) qmask = 0;
+        if (!valid || (GW_AB(p.ab, 4))) qmask = 0;
         if (valid) p.ws.rare_n[(size_t)k * p.E + ev[r]] = __popc(qmask);
         qm[r] = qmask;
         for (uint32_t m = qmask; m; m &= m - 1) atomicAdd(&s_cnt[__ffs(m) - 1], 1);  // LDS
@@ -1832,7 +1833,7 @@ CnnParams cnn_params(const gw_obs_source &src, const gw_cnn_actors *net, float *
     p.variant = src.variant;
     p.PW = 0;
     for (int k = 0; k < MAXN; ++k) p.apples[k] = src.apples[k];
-    const char *ab = std::getenv("GW_CNN_AB");
+    const char *ab = GW_MEASURE_ENV("GW_CNN_AB");
     p.ab = ab ? std::atoi(ab) : 0;
     return p;
 }
@@ -1954,7 +1955,7 @@ gw_status actor_act(const char *who, void *env, int32_t P, const gw_mlp_actors *
     p.ctr1 = (uint32_t)(counter >> 32);
     p.ctr_dev = counter_dev;
     for (int k = 0; k < MAXN; ++k) p.apples[k] = src.apples[k];
-    const char *ab = std::getenv("GW_ACT_AB");
+    const char *ab = GW_MEASURE_ENV("GW_ACT_AB");
     p.ab = ab ? std::atoi(ab) : 0;
     const int64_t tiles = (src.E + TILE - 1) / TILE;
     p.tiles = (int)tiles;
@@ -1964,11 +1965,13 @@ gw_status actor_act(const char *who, void *env, int32_t P, const gw_mlp_actors *
     const int v = P > 0 ? 4 : (av ? std::atoi(av) : 4);
     // small env counts (C2: 4,096 envs = 256 tiles per agent): 16-wave blocks would leave most
     // CUs idle with 4 waves per SIMD each doing one tile; 4-wave blocks spread the same tiles over
-    // 4x the CUs (one wave per SIMD).  GW_ACT_WAVES=16|4 forces either (A/B).
+    // 4x the CUs (one wave per SIMD).  GW_ACT_WAVES=16|12|8|4 forces the block's waves
+    // (result-neutral, tests/test_actor_ops.py): 12 / 8 leave a quarter / half of each SIMD's
+    // VGPRs to co-resident kernels (the rollout's obs writer)
     const char *aw = std::getenv("GW_ACT_WAVES");
-    const bool small = P == 0 && v == 4 &&
-                       (aw ? std::atoi(aw) == 4 : (tiles + 15) / 16 < std::max(1, 256 / src.K) / 2);
-    const int waves = v == 0 ? 8 : small ? 4 : 16;
+    const int awv = aw ? std::atoi(aw) : 0;
+    const bool small = P == 0 && v == 4 && (aw ? awv == 4 : (tiles + 15) / 16 < std::max(1, 256 / src.K) / 2);
+    const int waves = v == 0 ? 8 : small ? 4 : (P == 0 && v == 4 && (awv == 12 || awv == 8)) ? awv : 16;
     const int resident = v == 0 ? 512 : 256;
     const int64_t want = (tiles + waves - 1) / waves;
     const int per_agent = (int)std::max<int64_t>(1, std::min<int64_t>(want, std::max(1, resident / src.K)));
@@ -1983,6 +1986,10 @@ gw_status actor_act(const char *who, void *env, int32_t P, const gw_mlp_actors *
             gwprof::launch(act_kernel<NP, 8>, grid, block, 0, s, p);                     \
         else if (v == 4 && small)                                                        \
             gwprof::launch(act_kernel<NP, 4, true>, grid, block, 0, s, p);               \
+        else if (v == 4 && waves == 12)                                                  \
+            gwprof::launch(act_kernel<NP, 12, true>, grid, block, 0, s, p);              \
+        else if (v == 4 && waves == 8)                                                   \
+            gwprof::launch(act_kernel<NP, 8, true>, grid, block, 0, s, p);               \
         else if (v == 4)                                                                 \
             gwprof::launch(act_kernel<NP, 16, true>, grid, block, 0, s, p);              \
         else                                                                             \
@@ -2324,7 +2331,7 @@ static gw_status patch_cnn_rest(void *env, const gw_obs_source &src, const CnnPa
     if (!(tau > 0.0f)) return err(GW_ERR_ARG, "gw_patch_cnn_act: tau must be > 0");
     static const char *list_env = std::getenv("GW_WCNN_LIST");
     const bool fused_list = !(list_env && std::string(list_env) == "scan");
-    static const char *stat_env = std::getenv("GW_WCNN_STAT");  // diagnostics: the buckets' sizes (synchronises)
+    static const char *stat_env = GW_MEASURE_ENV("GW_WCNN_STAT");  // diagnostics: the buckets' sizes (synchronises)
     if (stat_env && *stat_env && fused_list) {
         std::vector<int> bn((size_t)src.K * cp.P);
         if (hipStreamSynchronize(s) == hipSuccess &&
@@ -2342,7 +2349,7 @@ static gw_status patch_cnn_rest(void *env, const gw_obs_source &src, const CnnPa
             std::fprintf(stderr, "\n");
         }
     }
-    static const char *rstamp_env = std::getenv("GW_RARE_STAMP");  // diagnostics: block stamps (synchronises)
+    static const char *rstamp_env = GW_MEASURE_ENV("GW_RARE_STAMP");  // diagnostics: block stamps (synchronises)
     static unsigned long long *rstamp = nullptr;
     if (rstamp_env && *rstamp_env && !rstamp && hipMalloc(&rstamp, sizeof(unsigned long long) * WR_BLOCKS * 8) != hipSuccess)
         rstamp = nullptr;

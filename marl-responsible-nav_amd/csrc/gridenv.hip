@@ -145,12 +145,7 @@ template <> struct SubStep<1> { static constexpr int f1 = 0, c1 = 1, f2 = 1, c2 
 template <> struct SubStep<2> { static constexpr int f1 = 0, c1 = 1, f2 = 1, c2 = 2, ohf1 = 1, ohc1 = 3, ohf2 = 2, ohc2 = 2; };
 template <> struct SubStep<3> { static constexpr int f1 = 1, c1 = 1, f2 = 2, c2 = 2, ohf1 = 0, ohc1 = 0, ohf2 = 0, ohc2 = 0; };
 
-// unit-move bit tables seen by the world update: a byte table (v1 kernels) or the u32 cell
-// table of step_v2 (bits CT_OK..CT_OK+3)
-struct ByteOk {
-    const uint8_t *t;
-    __device__ __forceinline__ uint32_t operator()(int c) const { return t[c]; }
-};
+// unit-move bits seen by the world update: the u32 cell table of step_v2 (bits CT_OK..CT_OK+3)
 struct CtabOk {
     const uint32_t *t;
     __device__ __forceinline__ uint32_t operator()(int c) const { return t[c] >> 21; }
@@ -454,43 +449,6 @@ __device__ __forceinline__ double np_sum_small(const double (&a)[MAXN], int n) {
 // ---------------------------------------------------------------------------------------
 // per-env helpers
 // ---------------------------------------------------------------------------------------
-template <int N>
-__device__ __forceinline__ void load_state(const Params &p, int64_t e, int (&pos)[N]) {
-#pragma unroll
-    for (int n = 0; n < N; ++n) pos[n] = p.st.pos[(int64_t)n * p.E + e];
-}
-
-// setup_step (ma_customenv.py:432-452) + the RL override (:239-242)
-template <int N>
-__device__ __forceinline__ void select_actions(const Params &p, int64_t e, uint32_t episode, int t,
-                                               const int (&pos)[N], int (&act)[N]) {
-    const uint32_t gid = (uint32_t)(p.env_offset + e);
-#pragma unroll
-    for (int n = 0; n < N; ++n) {
-        if (n < p.K) {
-            if (p.rl) {
-                act[n] = p.rl[e * p.K + n];
-            } else {
-                const uint4 r = philox(gid, episode, (uint32_t)t, (2u << 24) | (uint32_t)n, p.key0, p.key1);
-                act[n] = (int)(((uint64_t)r.x * 9u) >> 32);
-            }
-        } else if (p.scripted) {
-            act[n] = p.scripted[e * (p.N - p.K) + (n - p.K)];
-        } else {
-            const uint4 r = philox(gid, episode, (uint32_t)t, (1u << 24) | (uint32_t)n, p.key0, p.key1);
-            const int uni = r.x < 0x40000000u;  // random.random() < 0.25 (:441)
-            const double u = ((double)(r.y >> 5) * 67108864.0 + (double)(r.z >> 6)) * (1.0 / 9007199254740992.0);
-            const double *cdf = p.tb.cdf + ((int)p.tb.policy[pos[n]] * 2 + uni) * NA;
-            int a = NA - 1;
-#pragma unroll
-            for (int q = NA - 2; q >= 0; --q)
-                if (u < cdf[q]) a = q;  // searchsorted(cdf, u, 'right')
-            act[n] = a;
-        }
-        act[n] = ((unsigned)act[n] < (unsigned)NA) ? act[n] : 0;
-    }
-}
-
 template <int N>
 __device__ __forceinline__ void spawn_cells(const Params &p, int64_t e, uint32_t episode, int (&pos)[N]) {
     if (p.spawn) {
@@ -854,265 +812,6 @@ __device__ __forceinline__ void finish_env(const Params &p, int64_t e, const Env
     }
 }
 
-// ---------------------------------------------------------------------------------------
-// step kernel, fear off: one thread per env
-// ---------------------------------------------------------------------------------------
-template <int N>
-__device__ __forceinline__ void step_env_nofear(const Params &p, int64_t e, const uint8_t *s_ok, Contrib &ct) {
-    int pos[N], act[N], mdr[N], fin[N];
-    EnvState<N> es;
-    load_env<N>(p, e, es);
-#pragma unroll
-    for (int n = 0; n < N; ++n) pos[n] = es.pos[n];
-    select_actions<N>(p, e, es.episode, es.t, pos, act);
-#pragma unroll
-    for (int n = 0; n < N; ++n) mdr[n] = p.tb.mdr[pos[n]];
-    const uint32_t flags = es.flags;
-    int apple[MAXN];
-#pragma unroll
-    for (int k = 0; k < MAXN; ++k) apple[k] = (k < p.K && ((flags >> k) & 1u)) ? p.apples[k] : -1;
-    World<N> w;
-    w.init(pos, act, p.W, p.w_magic);
-    uint32_t caught;
-    simulate<N, true>(w, ByteOk{s_ok}, p.K, apple, caught, fin);
-    double fear[MAXN];
-#pragma unroll
-    for (int k = 0; k < MAXN; ++k) fear[k] = 0.0;
-    ObsInfo<N> oi;
-    finish_env<N>(p, e, es, act, mdr, fear, w.crash, w.restr, fin, caught, ct, oi);
-    store_desc<N>(p, e, oi);
-}
-
-template <int N>
-__global__ void __launch_bounds__(256) step_kernel_nofear(Params p) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t s_ok[];
-    for (int c = threadIdx.x; c < p.HW; c += blockDim.x) s_ok[c] = p.tb.okmask[c];
-    __syncthreads();
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    Contrib ct;
-    contrib_zero(ct);
-    if (e < p.E) step_env_nofear<N>(p, e, s_ok, ct);
-    if (blockIdx.x == 0 && threadIdx.x == 0) step_tick(p.out);
-    if (p.out.stats || p.out.stats_acc) {
-        __shared__ double s_red[4][GW_STATS];
-        wave_sum(ct);
-        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-        if (lane == 0)
-            for (int i = 0; i < GW_STATS; ++i) s_red[wv][i] = ct.v[i];
-        __syncthreads();
-        if (threadIdx.x < GW_STATS) {
-            const int i = threadIdx.x;
-            stats_put(p.out, (int64_t)blockIdx.x * GW_STATS + i,
-                      __dadd_rn(__dadd_rn(s_red[0][i], s_red[1][i]), __dadd_rn(s_red[2][i], s_red[3][i])));
-        }
-    }
-}
-
-
-// ---------------------------------------------------------------------------------------
-// step kernel, fear on: BE envs per 256-thread block, counterfactual sims as LDS tasks.
-//   FeAR_4_one_actor(actor k): for every affected j != k,
-//     V_x(j) = #{b : sim(joint_x with a_j := b if j close else a_j = stay).valid(j)}
-//   x in {MdR_k, a_k}.  Far j (not in close_agents) ignore b, so all 9 sims equal the
-//   "base" sim of x (j stays) -> one sim serves every far j.  For close j the b = a_j sim is
-//   the base sim too.  Tasks per (env, k) with a_k != MdR_k: 2 base + 2*8 per close j;
-//   a_k == MdR_k gives V_mdr == V_act -> Resp = 0 exactly, no task.
-// ---------------------------------------------------------------------------------------
-template <int N, int KMAX> struct FearCfg {
-    // envs per block, sized so that the task list + sim results stay under ~48 KB of LDS
-    static constexpr int BE = KMAX <= 2 ? (N <= 4 ? 64 : 32) : (N <= 4 ? 32 : 8);
-    static constexpr int MAXT = BE * (1 + KMAX * (2 + 16 * (N - 1)));
-};
-
-enum : uint32_t { T_MAIN = 0, T_BASE = 1, T_CJ = 2 };
-
-__device__ __forceinline__ uint32_t enc(uint32_t e, uint32_t k, uint32_t j, uint32_t var, uint32_t b, uint32_t kind) {
-    return e | (k << 6) | (j << 9) | (var << 12) | (b << 13) | (kind << 17);
-}
-
-template <int N, int KMAX>
-__global__ void __launch_bounds__(256) step_kernel_fear(Params p) {
-    constexpr int BE = FearCfg<N, KMAX>::BE;
-    constexpr int MAXT = FearCfg<N, KMAX>::MAXT;
-    __shared__ __attribute__((aligned(16))) uint8_t s_ok[4096];
-    __shared__ int s_pos[BE][N];
-    __shared__ int8_t s_act[BE][N];
-    __shared__ int8_t s_mdr[BE][N];
-    __shared__ uint8_t s_close[BE][KMAX];
-    __shared__ uint32_t s_tasks[MAXT];
-    __shared__ uint8_t s_base[BE][KMAX][2];
-    __shared__ uint8_t s_cj[BE][KMAX][N][2][NA];
-    __shared__ int s_fin[BE][N];
-    __shared__ uint32_t s_bits[BE];  // crash | restr << 8 | caught << 16
-    __shared__ int s_apple[BE][KMAX];
-    __shared__ int s_ntask;
-
-    const int tid = threadIdx.x;
-    for (int c = tid; c < p.HW; c += blockDim.x) s_ok[c] = p.tb.okmask[c];
-    if (tid == 0) s_ntask = BE;
-    __syncthreads();
-
-    const int64_t e0 = (int64_t)blockIdx.x * BE;
-    const int nenv = (int)min((int64_t)BE, p.E - e0);
-    const int K = p.K;
-
-    // ---- phase A: per env: actions, MdR, close sets, task list ----
-    if (tid < nenv) {
-        const int64_t e = e0 + tid;
-        int pos[N], act[N];
-        load_state<N>(p, e, pos);
-        select_actions<N>(p, e, p.st.episode[e], p.st.t[e], pos, act);
-        const uint32_t flags = p.st.flags[e];
-#pragma unroll
-        for (int n = 0; n < N; ++n) {
-            s_pos[tid][n] = pos[n];
-            s_act[tid][n] = (int8_t)act[n];
-            s_mdr[tid][n] = (int8_t)p.tb.mdr[pos[n]];
-        }
-        int ntask = 0;
-        uint32_t close[KMAX];
-#pragma unroll
-        for (int k = 0; k < KMAX; ++k) {
-            close[k] = 0;
-            s_apple[tid][k] = (k < K && ((flags >> k) & 1u)) ? p.apples[k] : -1;
-            if (k >= K) continue;
-#pragma unroll
-            for (int n = 0; n < N; ++n)
-                if (n == k || manhattan(p, pos[k], pos[n]) <= 5) close[k] |= 1u << n;  // :456-464
-            s_close[tid][k] = (uint8_t)close[k];
-            if (act[k] != (int)p.tb.mdr[pos[k]]) ntask += 2 + 16 * (__popc(close[k]) - 1);
-        }
-        s_tasks[tid] = enc(tid, 0, 0, 0, 0, T_MAIN);
-        if (ntask) {
-            int slot = atomicAdd(&s_ntask, ntask);
-#pragma unroll
-            for (int k = 0; k < KMAX; ++k) {
-                if (k >= K || act[k] == (int)p.tb.mdr[pos[k]]) continue;
-                s_tasks[slot++] = enc(tid, k, 0, 0, 15, T_BASE);
-                s_tasks[slot++] = enc(tid, k, 0, 1, 15, T_BASE);
-#pragma unroll
-                for (int j = 0; j < N; ++j) {
-                    if (j == k || !((close[k] >> j) & 1u)) continue;
-#pragma unroll
-                    for (int var = 0; var < 2; ++var)
-                        for (int b = 0; b < NA; ++b)
-                            if (b != act[j]) s_tasks[slot++] = enc(tid, k, j, var, b, T_CJ);
-                }
-            }
-        }
-    }
-    __syncthreads();
-
-    // ---- phase B: every lane runs one world update per task ----
-    const int ntask = s_ntask;
-    for (int ti = tid; ti < ntask; ti += blockDim.x) {
-        if (ti < BE && ti >= nenv) continue;  // main-sim slot of a missing env
-        const uint32_t tk = s_tasks[ti];
-        const int el = tk & 63, k = (tk >> 6) & 7, j = (tk >> 9) & 7, var = (tk >> 12) & 1,
-                  b = (tk >> 13) & 15, kind = (tk >> 17) & 3;
-        int pos[N], joint[N], fin[N];
-#pragma unroll
-        for (int n = 0; n < N; ++n) pos[n] = s_pos[el][n];
-        if (kind == T_MAIN) {
-#pragma unroll
-            for (int n = 0; n < N; ++n) joint[n] = s_act[el][n];
-            int apple[MAXN];
-#pragma unroll
-            for (int q = 0; q < MAXN; ++q) apple[q] = -1;
-#pragma unroll
-            for (int q = 0; q < KMAX; ++q) apple[q] = s_apple[el][q];
-            World<N> w;
-            w.init(pos, joint, p.W, p.w_magic);
-            uint32_t caught;
-            simulate<N, true>(w, ByteOk{s_ok}, K, apple, caught, fin);
-#pragma unroll
-            for (int n = 0; n < N; ++n) s_fin[el][n] = fin[n];
-            s_bits[el] = w.crash | (w.restr << 8) | (caught << 16);
-        } else {
-            const uint32_t cl = s_close[el][k];
-#pragma unroll
-            for (int n = 0; n < N; ++n) joint[n] = ((cl >> n) & 1u) ? (int)s_act[el][n] : 0;
-#pragma unroll
-            for (int n = 0; n < N; ++n)
-                if (n == k && var == 0) joint[n] = s_mdr[el][n];
-            if (kind == T_CJ) {
-#pragma unroll
-                for (int n = 0; n < N; ++n)
-                    if (n == j) joint[n] = b;
-            }
-            World<N> w;
-            w.init(pos, joint, p.W, p.w_magic);
-            uint32_t caught;
-            int no_apple[MAXN];
-#pragma unroll
-            for (int q = 0; q < MAXN; ++q) no_apple[q] = -1;
-            simulate<N, true>(w, ByteOk{s_ok}, 0, no_apple, caught, fin);  // one sim body in the loop
-            const uint32_t valid = ~(w.crash | w.restr) & ((1u << N) - 1u);
-            if (kind == T_BASE) {
-                s_base[el][k][var] = (uint8_t)valid;
-            } else {
-                s_cj[el][k][j][var][b] = (uint8_t)((valid >> j) & 1u);
-            }
-        }
-    }
-    __syncthreads();
-
-    // ---- phase C: FeAR sums, rewards, outputs ----
-    Contrib ct;
-    contrib_zero(ct);
-    if (tid < nenv) {
-        const int64_t e = e0 + tid;
-        int pos[N], act[N], mdr[N], fin[N];
-#pragma unroll
-        for (int n = 0; n < N; ++n) {
-            pos[n] = s_pos[tid][n];
-            act[n] = s_act[tid][n];
-            mdr[n] = s_mdr[tid][n];
-            fin[n] = s_fin[tid][n];
-        }
-        double fear[MAXN];
-#pragma unroll
-        for (int k = 0; k < MAXN; ++k) fear[k] = 0.0;
-#pragma unroll
-        for (int k = 0; k < KMAX; ++k) {
-            if (k >= K || act[k] == mdr[k]) continue;
-            const uint32_t cl = s_close[tid][k];
-            const uint32_t b0 = s_base[tid][k][0], b1 = s_base[tid][k][1];
-            double resp[N];
-#pragma unroll
-            for (int jj = 0; jj < N; ++jj) {
-                resp[jj] = 0.0;
-                if (jj == k) continue;
-                int vm, va;
-                if ((cl >> jj) & 1u) {
-                    vm = 0;
-                    va = 0;
-                    for (int b = 0; b < NA; ++b) {
-                        vm += (b == act[jj]) ? (int)((b0 >> jj) & 1u) : (int)s_cj[tid][k][jj][0][b];
-                        va += (b == act[jj]) ? (int)((b1 >> jj) & 1u) : (int)s_cj[tid][k][jj][1][b];
-                    }
-                } else {
-                    vm = 9 * (int)((b0 >> jj) & 1u);
-                    va = 9 * (int)((b1 >> jj) & 1u);
-                }
-                resp[jj] = p.tb.resp[vm * 10 + va];
-            }
-            fear[k] = np_sum_row<N>(resp, k);
-        }
-        const uint32_t bits = s_bits[tid];
-        EnvState<N> es;
-        load_env<N>(p, e, es);
-        ObsInfo<N> oi;
-        finish_env<N>(p, e, es, act, mdr, fear, bits & 0xFFu, (bits >> 8) & 0xFFu, fin, bits >> 16, ct, oi);
-        store_desc<N>(p, e, oi);
-    }
-    if (blockIdx.x == 0 && tid == 0) step_tick(p.out);
-    if ((p.out.stats || p.out.stats_acc) && tid < 64) {  // BE <= 64: every env of the block sits in wave 0
-        wave_sum(ct);
-        if (tid < GW_STATS) stats_put(p.out, (int64_t)blockIdx.x * GW_STATS + tid, ct.v[tid]);
-    }
-}
-
 // a plain 16-byte-per-lane copy (gw_obs_desc_copy)
 __global__ void __launch_bounds__(256) copy16_kernel(const uint4 *__restrict__ src, uint4 *__restrict__ dst, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) dst[i] = src[i];
@@ -1161,6 +860,109 @@ __device__ __forceinline__ float agent_value(bool reset, int n, int k, bool on_a
 // bf16 bits of an obs value: every value the env writes (-1, 0, 0.5, 1, 5..13, 9.5) is exact in
 // bf16, so the compact format is lossless (the low 16 bits of the f32 are zero)
 __device__ __forceinline__ uint32_t bf16_bits(float v) { return __float_as_uint(v) >> 16; }
+
+// The f32 writer's patch tables (round 6).  Per (which, env, agent) the float4s
+// its <= N + 1 patches touch are built ONCE in LDS (the map float4 with every patch of that float4
+// applied in slot order) and a byte per float4 of the obs names its entry (0 = map only), so a
+// 16-byte store costs one byte lookup instead of N + 1 compares and selects.  Used where the byte
+// tables fit (obs_tab_bytes <= OBS_TAB_MAX); else the compare loop.
+constexpr int OBS_TAB_MAX = 16384;
+__host__ __device__ __forceinline__ int obs_tab_stride(int HW) { return ((HW >> 2) + 15) & ~15; }
+__host__ __device__ __forceinline__ int obs_tab_bytes(int HW, int obs_be, int K) {
+    return 2 * obs_be * K * obs_tab_stride(HW);
+}
+__host__ __device__ __forceinline__ bool obs_tab_ok(int HW, int obs_be, int K) {
+    return HW % 4 == 0 && obs_tab_bytes(HW, obs_be, K) <= OBS_TAB_MAX;
+}
+// offset (bytes) of the float4 entries in obs_lds: after road bits, flags, patch cells + values
+__host__ __device__ __forceinline__ int obs_ent_off(int HW, int obs_be, int K, int npatch) {
+    const int words = (HW + 31) / 32 + OBS_BE + 2 * 2 * obs_be * K * npatch;
+    return ((words * 4) + 15) & ~15;
+}
+
+// The f32 writer's store loop over the patch tables.  J = H*W / 4 / T > 0: each thread owns the
+// same J float4 columns of every env, their map values in registers (J is a template parameter,
+// so they stay in VGPRs), and the env loop is uniform; J = 0: any shape, one float4 per iteration.
+template <int T, int J, bool NT>
+__device__ __forceinline__ void obs_store_cols(const Params &p, float *__restrict__ obs, float *__restrict__ final_obs,
+                                               int64_t e0, int nenv, int npatch, int tstride, const uint32_t *s_road,
+                                               const uint32_t *s_flag, const float4 *s_ent, const uint8_t *s_tab) {
+    const int tid = threadIdx.x, HW = p.HW, HW4 = HW >> 2, K = p.K;
+    auto map4 = [&](int c4) {
+        const int c0 = c4 << 2;
+        const uint32_t rb = s_road[c0 >> 5] >> (c0 & 31);
+        float4 v;
+        v.x = (rb & 1u) ? 0.0f : -1.0f;
+        v.y = (rb & 2u) ? 0.0f : -1.0f;
+        v.z = (rb & 4u) ? 0.0f : -1.0f;
+        v.w = (rb & 8u) ? 0.0f : -1.0f;
+        return v;
+    };
+    if constexpr (J > 0) {
+        float4 mapv[J];
+#pragma unroll
+        for (int j = 0; j < J; ++j) mapv[j] = map4(j * T + tid);
+        for (int which = 0; which < 2; ++which) {
+            float *dst = which == 0 ? obs : final_obs;
+            if (!dst) continue;
+            const uint32_t need = which == 0 ? D_WRITE : D_FINAL;
+            for (int k = 0; k < K; ++k) {
+                float4 *out4 = reinterpret_cast<float4 *>(dst + ((int64_t)k * p.E + e0) * HW);
+                for (int el = 0; el < nenv; ++el) {
+                    if (!(s_flag[el] & need)) continue;
+                    const int own = (which * p.obs_be + el) * K + k;
+                    const uint8_t *tb = s_tab + own * tstride;
+                    const float4 *ent = s_ent + own * npatch - 1;
+#pragma unroll
+                    for (int j = 0; j < J; ++j) {
+                        const int c4 = j * T + tid;
+                        const int en = tb[c4];
+                        // both operands read, then a value select: a select of the two addresses
+                        // would put mapv in scratch behind a flat load (ent[0] is readable LDS:
+                        // the previous owner's last entry, or the patch values before s_ent)
+                        const float4 ev = ent[en];
+                        float4 v;
+                        v.x = en ? ev.x : mapv[j].x;
+                        v.y = en ? ev.y : mapv[j].y;
+                        v.z = en ? ev.z : mapv[j].z;
+                        v.w = en ? ev.w : mapv[j].w;
+                        if (NT)
+                            store_nt(&out4[el * HW4 + c4], v);
+                        else
+                            out4[el * HW4 + c4] = v;
+                    }
+                }
+            }
+        }
+    } else {
+        const int total4 = nenv * HW4;
+        for (int which = 0; which < 2; ++which) {
+            float *dst = which == 0 ? obs : final_obs;
+            if (!dst) continue;
+            const uint32_t need = which == 0 ? D_WRITE : D_FINAL;
+            for (int k = 0; k < K; ++k) {
+                float4 *out4 = reinterpret_cast<float4 *>(dst + ((int64_t)k * p.E + e0) * HW);
+                for (int i4 = tid; i4 < total4; i4 += T) {
+                    const int el = HW4 == 1 ? i4 : (int)__umulhi((uint32_t)i4, p.hw4_magic);
+                    if (!(s_flag[el] & need)) continue;
+                    const int c4 = i4 - el * HW4;
+                    const int own = (which * p.obs_be + el) * K + k;
+                    const int en = s_tab[own * tstride + c4];
+                    const float4 ev = s_ent[own * npatch + en - 1], mv = map4(c4);  // value select, as above
+                    float4 v;
+                    v.x = en ? ev.x : mv.x;
+                    v.y = en ? ev.y : mv.y;
+                    v.z = en ? ev.z : mv.z;
+                    v.w = en ? ev.w : mv.w;
+                    if (NT)
+                        store_nt(&out4[i4], v);
+                    else
+                        out4[i4] = v;
+                }
+            }
+        }
+    }
+}
 
 // One obs block (T threads): the envs [e_begin + bid * obs_be, + obs_be) of the launch.
 // obs_lds: road bitmask, flags, then per (which, env, k) N + 1 patch cells and values, sized to
@@ -1211,7 +1013,66 @@ __device__ __forceinline__ void obs_block(const Params &p, float *__restrict__ o
         }
     }
     if (tid < OBS_BE && tid >= nenv) s_flag[tid] = 0;
+    const bool tab = VEC4 && !BF16 && obs_tab_ok(HW, p.obs_be, K);
+    float4 *s_ent = reinterpret_cast<float4 *>(reinterpret_cast<uint8_t *>(obs_lds) + obs_ent_off(HW, p.obs_be, K, npatch));
+    uint8_t *s_tab = reinterpret_cast<uint8_t *>(s_ent + 2 * p.obs_be * K * npatch);
+    const int tstride = obs_tab_stride(HW);
+    if (tab) {  // zero the byte tables (16 B per thread and pass)
+        const int n16 = obs_tab_bytes(HW, p.obs_be, K) >> 4;
+        for (int i = tid; i < n16; i += T) reinterpret_cast<uint4 *>(s_tab)[i] = make_uint4(0, 0, 0, 0);
+    }
     __syncthreads();
+    for (int t = tid; tab && t < 2 * p.obs_be * K * npatch; t += T) {
+        // one thread per patch slot q of (which, env, agent): the first slot touching a float4
+        // builds its entry (the map float4 with every slot of that float4 applied in slot order:
+        // a later slot overrides, the obs writer's rule) and names it in the byte table
+        const int own = t / npatch, q = t - own * npatch;
+        const int which = own / (p.obs_be * K), el = (own / K) % p.obs_be, k = own % K;
+        const int slot = own * npatch;  // == ((which * obs_be + el) * K + k) * npatch
+        const int c = s_pc[slot + q];
+        if (el < nenv && (s_flag[el] & (which == 0 ? D_WRITE : D_FINAL)) && c >= 0 && c < HW) {
+            bool first = true;
+            for (int q2 = 0; q2 < q; ++q2) {
+                const int c2 = s_pc[slot + q2];
+                first = first && (c2 < 0 || (c2 >> 2) != (c >> 2));
+            }
+            if (first) {
+                const int c0 = c & ~3;
+                const uint32_t rb = s_road[c0 >> 5] >> (c0 & 31);
+                float4 v;
+                v.x = (rb & 1u) ? 0.0f : -1.0f;
+                v.y = (rb & 2u) ? 0.0f : -1.0f;
+                v.z = (rb & 4u) ? 0.0f : -1.0f;
+                v.w = (rb & 8u) ? 0.0f : -1.0f;
+                for (int q2 = q; q2 < npatch; ++q2) {
+                    const int dd = s_pc[slot + q2] - c0;
+                    if ((unsigned)dd < 4u) {
+                        const float pv = s_pv[slot + q2];
+                        v.x = dd == 0 ? pv : v.x;
+                        v.y = dd == 1 ? pv : v.y;
+                        v.z = dd == 2 ? pv : v.z;
+                        v.w = dd == 3 ? pv : v.w;
+                    }
+                }
+                s_ent[slot + q] = v;
+                s_tab[own * tstride + (c >> 2)] = (uint8_t)(q + 1);
+            }
+        }
+    }
+    if (tab) {
+        __syncthreads();
+        const int HW4 = HW >> 2;
+        const int J = HW4 % T == 0 ? HW4 / T : 0;
+        if (J == 1)
+            obs_store_cols<T, 1, NT>(p, obs, final_obs, e0, nenv, npatch, tstride, s_road, s_flag, s_ent, s_tab);
+        else if (J == 2)
+            obs_store_cols<T, 2, NT>(p, obs, final_obs, e0, nenv, npatch, tstride, s_road, s_flag, s_ent, s_tab);
+        else if (J == 4)
+            obs_store_cols<T, 4, NT>(p, obs, final_obs, e0, nenv, npatch, tstride, s_road, s_flag, s_ent, s_tab);
+        else
+            obs_store_cols<T, 0, NT>(p, obs, final_obs, e0, nenv, npatch, tstride, s_road, s_flag, s_ent, s_tab);
+        return;
+    }
 
     for (int which = 0; which < 2; ++which) {
         float *dst = which == 0 ? obs : final_obs;
@@ -1312,7 +1173,6 @@ __global__ void __launch_bounds__(OBS_THREADS) obs_kernel(Params p, float *__res
 //      MdR, close sets, and the de-duplicated FeAR task list (see FeAR note above)
 //   B  every lane: one world update per task (the env's real update = the first BE slots)
 //   C  per env: FeAR sums in numpy order, rewards, dones, state, outputs, obs descriptor
-//   D  (OBS = true, GW_KERNEL=fused) the block's float32 obs, 16-byte coalesced stores
 // All per-cell tables live in one u32 LDS table (policy | MdR | action mask | unit moves |
 // road), the policy CDFs in LDS too, so no lane walks a dependent chain of global loads.
 // Small blocks (2 waves) keep ~9 blocks per CU resident so their latency-bound phases overlap.
@@ -1352,10 +1212,10 @@ template <int N, int KMAX, bool FEAR, bool WIDE = false, bool DEF = false> struc
     }
 };
 
-template <int N, int KMAX, bool FEAR, bool OBS, bool WIDE = false, bool DEF = false>
+template <int N, int KMAX, bool FEAR, bool WIDE = false, bool DEF = false>
 struct alignas(16) V2Shared {
     using Cfg = V2Cfg<N, KMAX, FEAR, WIDE, DEF>;
-    static constexpr int BE = Cfg::BE, FB = FEAR ? BE : 1, OB = OBS ? BE : 1, NP = N + 1;
+    static constexpr int BE = Cfg::BE, FB = FEAR ? BE : 1;
     double red[Cfg::THREADS / 64][GW_STATS];
     typename Cfg::Task tasks[Cfg::MAXB];
     typename Cfg::Task groups[Cfg::MAXG];
@@ -1368,9 +1228,6 @@ struct alignas(16) V2Shared {
     uint8_t close[FB][KMAX];
     uint8_t base[FB][KMAX][2];
     uint8_t cj[FB][KMAX][FEAR ? N : 1][2][NA];
-    uint16_t pc[2][OB][KMAX][NP];
-    float pv[2][OB][KMAX][NP];
-    uint32_t eflag[OB];
     uint2 wl[(N >= GW_LIST_MIN_N) ? Cfg::THREADS * N : 1];  // World<N, true> rows (one per thread)
     int8_t xact[Cfg::XDRAW ? BE : 1][N];   // FeAR off: the (env, agent) threads' action draws and MdRs
     int8_t xmdr[Cfg::XDRAW ? BE : 1][N];
@@ -1410,35 +1267,6 @@ __device__ __forceinline__ void select_actions_v2(const Params &p, int64_t e, co
                                                   const uint32_t *ctab, const double *cdf_s, int (&act)[N]) {
 #pragma unroll
     for (int n = 0; n < N; ++n) act[n] = draw_action(p, e, n, es.episode, es.t, es.pos[n], ctab, cdf_s);
-}
-
-template <int N, int WH, int OB, int KMAX, int NP>
-__device__ __forceinline__ void v2_patches(const Params &p, int el, const ObsInfo<N> &oi, const uint32_t *ctab,
-                                           uint16_t (&pc)[2][OB][KMAX][NP], float (&pv)[2][OB][KMAX][NP]) {
-    const uint32_t f = oi.flags;
-    const bool reset = (WH == 0) && (f & D_RESET);
-    const uint32_t apples = WH == 0 ? (f >> 8) & 0xFFu : (f >> 16) & 0xFFu;
-#pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-        if (k >= p.K) continue;
-        const int ac = ((apples >> k) & 1u) ? p.apples[k] : -1;
-        int np = 0;
-        if (ac >= 0) {  // own apple first; an agent standing on it overrides this patch
-            float av = ((ctab[ac] >> CT_ROAD) & 1u) ? 9.0f : 8.0f;
-            if (!reset && av == (float)(k + 1)) av = 1.0f;  // relabel of :321 (apple on a wall, K = 8)
-            pc[WH][el][k][np] = (uint16_t)ac;
-            pv[WH][el][k][np] = av;
-            ++np;
-        }
-#pragma unroll
-        for (int n = 0; n < N; ++n) {
-            const int c = WH == 0 ? oi.pos[n] : oi.fpos[n];
-            pc[WH][el][k][np] = (uint16_t)c;
-            pv[WH][el][k][np] = agent_value(reset, n, k, c == ac, p.variant);
-            ++np;
-        }
-        for (; np < NP; ++np) pc[WH][el][k][np] = 0xFFFFu;
-    }
 }
 
 // Copy n 32-bit words global -> LDS with 16-byte accesses, all loads of a lane issued before
@@ -1611,12 +1439,11 @@ __device__ unsigned long long g_step_clk[64][16];
     } while (0)
 #endif
 
-template <int N, int KMAX, bool FEAR, bool OBS, bool DEFER>
-__device__ __forceinline__ void step_v2_block(const Params &p, int64_t bid, V2Shared<N, KMAX, FEAR, OBS, false, DEFER> &sh,
+template <int N, int KMAX, bool FEAR, bool DEFER>
+__device__ __forceinline__ void step_v2_block(const Params &p, int64_t bid, V2Shared<N, KMAX, FEAR, false, DEFER> &sh,
                                               uint8_t *dyn) {  // dyn: [cdf P*18 f64][cell table HW u32][Resp]
     using Cfg = V2Cfg<N, KMAX, FEAR, false, DEFER>;
-    using Sh = V2Shared<N, KMAX, FEAR, OBS, false, DEFER>;
-    constexpr int BE = Cfg::BE, T = Cfg::THREADS, NP = N + 1, OB = Sh::OB;
+    constexpr int BE = Cfg::BE, T = Cfg::THREADS;
     const double *cdf_s = p.lds_cdf ? reinterpret_cast<const double *>(dyn) : nullptr;
     uint32_t *ctab = reinterpret_cast<uint32_t *>(dyn + p.ctab_off);
     double *resp_s = reinterpret_cast<double *>(dyn + p.resp_off);  // [10][10] Resp table
@@ -1755,13 +1582,7 @@ __device__ __forceinline__ void step_v2_block(const Params &p, int64_t bid, V2Sh
             const uint32_t bits = sh.bits[tid];
             ObsInfo<N> oi;
             finish_env<N>(p, e, es, act, mdr, fear, bits & 0xFFu, (bits >> 8) & 0xFFu, fin, bits >> 16, ct, oi, ctab);
-            if constexpr (OBS) {
-                v2_patches<N, 0, OB, KMAX, NP>(p, tid, oi, ctab, sh.pc, sh.pv);
-                if (oi.flags & D_FINAL) v2_patches<N, 1, OB, KMAX, NP>(p, tid, oi, ctab, sh.pc, sh.pv);
-                sh.eflag[tid] = oi.flags;
-            } else {
-                store_desc<N>(p, e, oi);
-            }
+            store_desc<N>(p, e, oi);
         }
     } else {
         if constexpr (XDRAW) {  // the action draws and MdRs, one thread per (env, agent)
@@ -1814,17 +1635,8 @@ __device__ __forceinline__ void step_v2_block(const Params &p, int64_t bid, V2Sh
             ObsInfo<N> oi;
             finish_env<N, DEFER>(p, e, es, act, mdr, fear, w.crash, w.restr, fin, caught, ct, oi, ctab);
             STEP_STAMP(4);
-            if constexpr (OBS) {
-                v2_patches<N, 0, OB, KMAX, NP>(p, cel, oi, ctab, sh.pc, sh.pv);
-                if (oi.flags & D_FINAL) v2_patches<N, 1, OB, KMAX, NP>(p, cel, oi, ctab, sh.pc, sh.pv);
-                sh.eflag[cel] = oi.flags;
-            } else {
-                store_desc<N>(p, e, oi);
-            }
+            store_desc<N>(p, e, oi);
         }
-    }
-    if constexpr (OBS) {
-        if (tid < BE && tid >= nenv) sh.eflag[tid] = 0;
     }
 
     // ---- block statistics (deterministic tree) ----
@@ -1833,51 +1645,13 @@ __device__ __forceinline__ void step_v2_block(const Params &p, int64_t bid, V2Sh
     STEP_STAMP(5);
     block_stats<T, FM, ST_INT>(p, ct, sh.red, tid, p.stats_row0 + e0 / BE);
     STEP_STAMP(6);
-
-    if constexpr (OBS) {
-        // ---- D: obs of the block's envs, 16-byte coalesced stores ----
-        const int HW4 = p.HW >> 2;
-        const int total4 = nenv * HW4;
-#pragma unroll
-        for (int wh = 0; wh < 2; ++wh) {
-            float *dst = wh == 0 ? p.out.obs : p.out.final_obs;
-            if (!dst) continue;
-            const uint32_t need = wh == 0 ? D_WRITE : D_FINAL;
-            for (int k = 0; k < K; ++k) {
-                float4 *out4 = reinterpret_cast<float4 *>(dst + ((int64_t)k * p.E + e0) * p.HW);
-                for (int i4 = tid; i4 < total4; i4 += T) {
-                    const int el = HW4 == 1 ? i4 : (int)__umulhi((uint32_t)i4, p.hw4_magic);
-                    if (!(sh.eflag[el] & need)) continue;
-                    const int c0 = (i4 - el * HW4) << 2;
-                    const uint4 cw = *reinterpret_cast<const uint4 *>(&ctab[c0]);
-                    float4 v;
-                    v.x = ((cw.x >> CT_ROAD) & 1u) ? 0.0f : -1.0f;
-                    v.y = ((cw.y >> CT_ROAD) & 1u) ? 0.0f : -1.0f;
-                    v.z = ((cw.z >> CT_ROAD) & 1u) ? 0.0f : -1.0f;
-                    v.w = ((cw.w >> CT_ROAD) & 1u) ? 0.0f : -1.0f;
-#pragma unroll
-                    for (int q = 0; q < NP; ++q) {
-                        const int dd = (int)sh.pc[wh][el][k][q] - c0;
-                        if ((unsigned)dd < 4u) {
-                            const float pvq = sh.pv[wh][el][k][q];
-                            v.x = dd == 0 ? pvq : v.x;
-                            v.y = dd == 1 ? pvq : v.y;
-                            v.z = dd == 2 ? pvq : v.z;
-                            v.w = dd == 3 ? pvq : v.w;
-                        }
-                    }
-                    store_nt(&out4[i4], v);
-                }
-            }
-        }
-    }
 }
 
-template <int N, int KMAX, bool FEAR, bool OBS, bool DEFER = false>
+template <int N, int KMAX, bool FEAR, bool DEFER = false>
 __global__ void __launch_bounds__(128) step_v2(Params p) {
-    __shared__ V2Shared<N, KMAX, FEAR, OBS, false, DEFER> sh;
+    __shared__ V2Shared<N, KMAX, FEAR, false, DEFER> sh;
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
-    step_v2_block<N, KMAX, FEAR, OBS, DEFER>(p, blockIdx.x, sh, dyn);
+    step_v2_block<N, KMAX, FEAR, DEFER>(p, blockIdx.x, sh, dyn);
 }
 
 // gw_obs_patch (egocentric P x P windows of the env's last observation, -1 outside the grid,
@@ -1892,16 +1666,14 @@ __global__ void __launch_bounds__(128) step_v2(Params p) {
 // ---------------------------------------------------------------------------------------
 template <int N, int KMAX, bool FEAR>
 __global__ void __launch_bounds__(128) step_obs(Params p, Params q, float *__restrict__ obs,
-                                                float *__restrict__ final_obs, uint32_t nstep, uint32_t order) {
-    __shared__ V2Shared<N, KMAX, FEAR, false> sh;
+                                                float *__restrict__ final_obs, uint32_t nstep) {
+    __shared__ V2Shared<N, KMAX, FEAR> sh;
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
-    const uint32_t nobs = gridDim.x - nstep;
-    // order 0: step blocks first (the long latency chains start first); 1: obs blocks first
-    const bool is_step = order == 0 ? blockIdx.x < nstep : blockIdx.x >= nobs;
-    const uint32_t rb = order == 0 ? (is_step ? blockIdx.x : blockIdx.x - nstep)
-                                   : (is_step ? blockIdx.x - nobs : blockIdx.x);
+    // the step blocks first: their long latency chains start first
+    const bool is_step = blockIdx.x < nstep;
+    const uint32_t rb = is_step ? blockIdx.x : blockIdx.x - nstep;
     if (is_step)
-        step_v2_block<N, KMAX, FEAR, false, false>(p, rb, sh, dyn);
+        step_v2_block<N, KMAX, FEAR, false>(p, rb, sh, dyn);
     else if (q.obs_bf16)
         obs_block<128, true, true, true>(q, obs, final_obs, rb, reinterpret_cast<uint32_t *>(dyn));
     else
@@ -1919,7 +1691,7 @@ __global__ void __launch_bounds__(128) step_obs(Params p, Params q, float *__res
 template <int N, int KMAX, bool WIDE>
 __device__ __forceinline__ void fear_block(const Params &p, uint32_t bid) {
     using Cfg = V2Cfg<N, KMAX, true, WIDE>;
-    using Sh = V2Shared<N, KMAX, true, false, WIDE>;
+    using Sh = V2Shared<N, KMAX, true, WIDE>;
     constexpr int BE = Cfg::BE, T = Cfg::THREADS;
     __shared__ Sh sh;
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
@@ -2016,8 +1788,10 @@ __global__ void __launch_bounds__(128) fear_rows_kernel(Params p, PatchArgs a, u
         fear_block<N, KMAX, WIDE>(p, blockIdx.x);
         return;
     }
-    // the rows' LDS slices in the dynamic region the FeAR blocks use for their tables (the launch
-    // sizes it for both), so the writer adds no LDS to the FeAR blocks' footprint
+    // the rows' LDS slices in the dynamic region the FeAR blocks use for their tables.  One launch
+    // has one footprint: the dynamic region is max(FeAR tables, 8 KB of row slices), so on small
+    // grids (32x32: ~4.9 KB of tables) the FeAR blocks reserve 8 KB, and the row blocks also
+    // reserve fear_block's static shared state; both stay far below the 160 KB per CU
     extern __shared__ __attribute__((aligned(16))) uint8_t dynr[];
     const uint32_t r = blockIdx.x - nfear;
     gwrows::rows_block<N + 1, 16, 2, 2>(a, r % nrx, (int)(r / nrx), reinterpret_cast<float4 (*)[64 * 4]>(dynr));
@@ -2165,36 +1939,29 @@ struct Env {
     uint64_t seed = 0;
     int apples[GW_MAX_AGENTS] = {0};
     bool initialized = false;
-    int mode = 3;        // GW_KERNEL: 0 "v1" (first kernels), 1 "split" step_v2 (FeAR inline) + obs_kernel,
-                         // 2 "fused", 3 "defer" (default; FeAR on: step_v2 <DEFER>, then fear_v2 || obs_kernel),
-                         // 4 "merged" (as split; with async obs one step_obs launch per step)
-    int obs_be = 2;      // GW_OBS_BE: envs per obs_kernel block (default: see gw_create)
-    bool obs_nt = true;  // GW_OBS_NT=0: plain instead of nontemporal obs stores
+    int mode = 3;        // kernel path (gw_create picks by batch size; GW_KERNEL=defer|merged forces):
+                         // 3 "defer" (FeAR on: step_v2 <DEFER>, then fear_v2 || obs_kernel; FeAR off:
+                         // step_v2, then obs_kernel), 4 "merged" (synchronous as defer with FeAR
+                         // inline; with async obs one step_obs launch per step)
+    int obs_be = 2;      // envs per obs_kernel block (default: see gw_create)
     bool obs_bf16 = false;  // gw_set_obs_dtype(env, GW_OBS_BF16): obs buffers hold bf16 (lossless)
-    bool obs_be_fixed = false;  // GW_OBS_BE given
     int obs_be_f32 = 2;         // the float32 writer's default
     uint32_t *celltab = nullptr;
     uint32_t *roadbits = nullptr;
-    int defer_order = 3;            // GW_DEFER (A/B): 0 fear then obs on one stream; 1 fear on a second
-                                    // stream || obs; 3 (default) as 1 with the second stream at high priority
     // fear_v2 with 2x envs per block (default since the obs writers overlap: C3 93.8 -> 92.1 us,
     // C5 175 -> 166, C4f 368 -> 358 per step; the bf16 line loses 2 %: profiles/r2_events);
     // GW_FEAR_BE=narrow: 1x (A/B)
     bool fear_wide = true;
     bool fear_wide_fixed = false;   // GW_FEAR_BE given (else the obs format picks, before any reset)
-    int chunks = 1;                 // GW_CHUNKS: step/obs pipeline depth (split path; 1 = off, measured best)
-    hipStream_t aux = nullptr;      // second stream of the pipeline (created on first use)
-    hipStream_t aux2 = nullptr;     // third stream: obs_kernel of the chunked defer pipeline
+    hipStream_t aux = nullptr;      // second (high-priority) stream: fear_v2 beside the writer
     std::vector<hipEvent_t> sync_ev;  // fork/chunk/join events (timing disabled)
     // async obs (gw_set_obs_async): obs_kernel of step t runs on obs_stream while the world update
     // of step t+1 runs; the descriptor is double-buffered (desc_buf[dcur] = the latest step's)
     // (launched lazily: at the start of gw_step t+1, behind the caller's work between the steps,
     // e.g. the fused actor, so the writer never competes with it for the CUs; or at a fence)
     bool obs_async = false;
-    int merge_order = 0;                          // GW_MERGE_ORDER (A/B): step_obs role order
     hipStream_t last_stream = nullptr;            // merged mode: the stream of the last gw_step
     bool obs_lazy = false;                        // gw_set_obs_async(env, 2): launch at the next step
-    bool obs_hi = false;                          // GW_OBS_PRIO=hi (A/B): obs stream high priority, aux normal
     int obs_chunks = 1;                           // GW_OBS_CHUNKS: the obs writer as this many launches
     // gw_step_patch_next: the next gw_step also writes the step's P x P windows (in the FeAR launch
     // where it can: fear_rows_kernel; else as gw_obs_patch right after the step)
@@ -2221,7 +1988,6 @@ struct Env {
     // shaped reward, returns, FeAR stats rows) finishes on the aux stream, ordered by gw_fear_fence
     bool fear_async = false;
     bool fear_pending = false;
-    bool async_aux = false;                       // GW_ASYNC_AUX=1 (A/B): world + FeAR on the aux stream
     hipEvent_t fear_ev = nullptr;
     bool obs_queued = false;                      // an obs_kernel launch waits in qobs
     bool qobs_prof = false;                       // profiling state of the step that queued it
@@ -2255,12 +2021,10 @@ struct Env {
     // kernel already ends with an agent-scope release), so by default they skip the
     // system-scope fence (L2 write-back + invalidate) that a plain event record / wait costs at
     // every use: 5 us per record and 11-18 us between consecutive obs writers at C3 with it.
-    // GW_EVENT_FENCE=system restores the plain events (A/B).
     unsigned sync_flags = hipEventDisableTiming | hipEventDisableSystemFence;
     unsigned prof_flags = hipEventDisableSystemFence;  // timing events of gw_profile
-    // obs_done / world_ev bound to the kernel launch they follow (hipExtLaunchKernelGGL stop
-    // event) instead of a marker packet after it; GW_BIND_EVENTS=0 records them (A/B)
-    bool bind_events = true;
+    // obs_done / world_ev are bound to the kernel launch they follow (hipExtLaunchKernelGGL stop
+    // event) instead of a marker packet after it (+0.5 %, profiles/HISTORY.md)
 };
 
 // the second stream and n fork/join events (timing disabled), created on first use
@@ -2274,40 +2038,23 @@ gw_status ensure_events(Env *env, int n) {
     return GW_OK;
 }
 
-// the second stream (+ the third, aux2, for the chunked defer pipeline only) and n events.
-// Streams are created only where a path uses them: a process has few hardware queues
-// (GPU_MAX_HW_QUEUES = 4 on the box) and every extra stream competes for them.
-gw_status ensure_aux(Env *env, int n, bool need_aux2 = false) {
+// the second stream (high priority: fear_v2's workgroups are dispatched ahead of the writer's)
+// and n events.  Streams are created only where a path uses them: a process has few hardware
+// queues (GPU_MAX_HW_QUEUES = 4 on the box) and every extra stream competes for them.
+gw_status ensure_aux(Env *env, int n) {
     if (!env->aux) {
-        if (env->mode == 3 && env->defer_order == 3 && !env->obs_hi) {
-            int lo = 0, hi = 0;
-            HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-            HIP_TRY(hipStreamCreateWithPriority(&env->aux, hipStreamNonBlocking, hi));
-        } else {
-            HIP_TRY(hipStreamCreateWithFlags(&env->aux, hipStreamNonBlocking));
-        }
+        int lo = 0, hi = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIP_TRY(hipStreamCreateWithPriority(&env->aux, hipStreamNonBlocking, hi));
     }
-    {
-        const gw_status st = ensure_events(env, n);
-        if (st != GW_OK) return st;
-    }
-    if (need_aux2 && !env->aux2) HIP_TRY(hipStreamCreateWithFlags(&env->aux2, hipStreamNonBlocking));
-    return GW_OK;
+    return ensure_events(env, n);
 }
 
 // the async-obs stream and its per-descriptor-buffer completion events, created on first use
 gw_status ensure_obs_stream(Env *env) {
     const gw_status st = ensure_events(env, 3);
     if (st != GW_OK) return st;
-    if (!env->obs_stream) {
-        if (env->obs_hi) {
-            int lo = 0, hi = 0;
-            HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-            HIP_TRY(hipStreamCreateWithPriority(&env->obs_stream, hipStreamNonBlocking, hi));
-        } else {
-            HIP_TRY(hipStreamCreateWithFlags(&env->obs_stream, hipStreamNonBlocking));
-        }
-    }
+    if (!env->obs_stream) HIP_TRY(hipStreamCreateWithFlags(&env->obs_stream, hipStreamNonBlocking));
     for (hipEvent_t &e : env->obs_done)
         if (!e) HIP_TRY(hipEventCreateWithFlags(&e, env->sync_flags));
     if (!env->world_ev) HIP_TRY(hipEventCreateWithFlags(&env->world_ev, env->sync_flags));
@@ -2363,7 +2110,7 @@ gw_status flush_obs(Env *env, hipEvent_t after, hipStream_t on = nullptr) {
     const bool prof = env->qobs_prof;  // timed iff the step that queued it was
     size_t b = 0;
     if (prof && prof_span_begin(env, b) != GW_OK) return GW_ERR_HIP;
-    const bool bind = env->bind_events && !prof;  // obs_done carried by the writer's launch
+    const bool bind = !prof;  // obs_done carried by the writer's launch
     if (bind) t_bind_stop = env->obs_done[env->qobs_buf];
     const hipError_t le = launch_obs(env, env->qobs, env->qobs.out.obs, env->qobs.out.final_obs, os);
     t_bind_stop = nullptr;
@@ -2538,7 +2285,7 @@ gw::Params make_params(const Env *env) {
     return p;
 }
 
-template <int N, int KMAX, bool FEAR, bool OBS, bool DEFER = false>
+template <int N, int KMAX, bool FEAR, bool DEFER = false>
 hipError_t launch_v2(const Env *env, const gw::Params &p, hipStream_t s) {
     constexpr int BE = gw::V2Cfg<N, KMAX, FEAR, false, DEFER>::BE;
     const int64_t n = p.e_end - p.e_begin;  // this launch's env range (a pipeline chunk or all)
@@ -2547,7 +2294,7 @@ hipError_t launch_v2(const Env *env, const gw::Params &p, hipStream_t s) {
     // dynamic LDS [cdf][cell table][Resp (FeAR)].  (Staging the free-cell list there too for the
     // auto-reset's spawn made C2's step kernel slower: 11.4 -> 12.2 us, profiles/r3_c2.)
     const size_t dyn = (size_t)p.resp_off + (FEAR ? 100 * sizeof(double) : 0);
-    gw_launch((gw::step_v2<N, KMAX, FEAR, OBS, DEFER>), dim3(grid), dim3(gw::V2Cfg<N, KMAX, FEAR, false, DEFER>::THREADS),
+    gw_launch((gw::step_v2<N, KMAX, FEAR, DEFER>), dim3(grid), dim3(gw::V2Cfg<N, KMAX, FEAR, false, DEFER>::THREADS),
               dyn, s, p);
     return hipGetLastError();
 }
@@ -2618,6 +2365,7 @@ hipError_t launch_fear_rows_k(const Env *env, const gw::Params &p0, const gw::Pa
     const int64_t n = p.e_end - p.e_begin;
     const unsigned nfear = (unsigned)((n + BE - 1) / BE);
     const unsigned nrx = (unsigned)((a.E * a.P + 255) / 256);  // 2 waves x 2 runs x 64 rows per block
+    // one footprint for both roles: the FeAR tables or the row writer's 2 x 64 x 4 float4 slices
     const size_t dyn = std::max((size_t)p.resp_off + 100 * sizeof(double), sizeof(float4) * 2 * 64 * 4);
     gw_launch((gw::fear_rows_kernel<N, KMAX, WIDE>), dim3(nfear + nrx * (unsigned)a.K), dim3(128), dyn, s, p, a,
               nfear, nrx);
@@ -2659,34 +2407,13 @@ hipError_t dispatch_fear(const Env *env, const gw::Params &p, hipStream_t s) {
     return hipErrorInvalidValue;
 }
 
-template <int N, bool OBS>
-hipError_t launch_v2_k(const Env *env, const gw::Params &p, hipStream_t s) {
-    if (env->mode == 3 && env->fear && !OBS)  // deferred FeAR: the world update only, + FearRec
-        return env->K <= 2 ? launch_v2<N, 2, false, false, true>(env, p, s) : launch_v2<N, N, false, false, true>(env, p, s);
-    if (env->fear)
-        return env->K <= 2 ? launch_v2<N, 2, true, OBS>(env, p, s) : launch_v2<N, N, true, OBS>(env, p, s);
-    return env->K <= 2 ? launch_v2<N, 2, false, OBS>(env, p, s) : launch_v2<N, N, false, OBS>(env, p, s);
-}
-
 template <int N>
 hipError_t launch_step(const Env *env, const gw::Params &p, hipStream_t s) {
-    if (env->mode == 2) return launch_v2_k<N, true>(env, p, s);
-    if (env->mode == 1 || env->mode == 3 || env->mode == 4) return launch_v2_k<N, false>(env, p, s);
-    if (env->fear) {
-        if (env->K <= 2) {
-            constexpr int BE = gw::FearCfg<N, 2>::BE;
-            const unsigned grid = (unsigned)((env->E + BE - 1) / BE);
-            gw_launch((gw::step_kernel_fear<N, 2>), dim3(grid), dim3(256), 0, s, p);
-        } else {
-            constexpr int BE = gw::FearCfg<N, N>::BE;
-            const unsigned grid = (unsigned)((env->E + BE - 1) / BE);
-            gw_launch((gw::step_kernel_fear<N, N>), dim3(grid), dim3(256), 0, s, p);
-        }
-    } else {
-        const unsigned grid = (unsigned)((env->E + 255) / 256);
-        gw_launch((gw::step_kernel_nofear<N>), dim3(grid), dim3(256), env->HW, s, p);
-    }
-    return hipGetLastError();
+    if (env->mode == 3 && env->fear)  // deferred FeAR: the world update only, + FearRec
+        return env->K <= 2 ? launch_v2<N, 2, false, true>(env, p, s) : launch_v2<N, N, false, true>(env, p, s);
+    if (env->fear)  // FeAR inline (the merged path's step role, its synchronous steps)
+        return env->K <= 2 ? launch_v2<N, 2, true>(env, p, s) : launch_v2<N, N, true>(env, p, s);
+    return env->K <= 2 ? launch_v2<N, 2, false>(env, p, s) : launch_v2<N, N, false>(env, p, s);
 }
 
 template <int N>
@@ -2727,9 +2454,14 @@ hipError_t dispatch_reset(const Env *env, const gw::Params &p, hipStream_t s) {
 hipError_t launch_obs_range(const Env *env, const gw::Params &p, float *obs, float *final_obs, hipStream_t s);
 
 // obs_kernel's LDS: road bitmask, OBS_BE flags, [2][obs_be][K][N + 1] patch cells + values
+// (+ with the f32 patch tables: [2][obs_be][K][N + 1] float4 entries and the byte tables)
 size_t obs_lds_bytes(const Env *env) {
-    return sizeof(uint32_t) * ((env->HW + 31) / 32 + gw::OBS_BE) +
-           (size_t)2 * 2 * env->obs_be * env->K * (env->N + 1) * sizeof(uint32_t);
+    const size_t base = sizeof(uint32_t) * ((env->HW + 31) / 32 + gw::OBS_BE) +
+                        (size_t)2 * 2 * env->obs_be * env->K * (env->N + 1) * sizeof(uint32_t);
+    if (env->obs_bf16 || !gw::obs_tab_ok(env->HW, env->obs_be, env->K)) return base;
+    return (size_t)gw::obs_ent_off(env->HW, env->obs_be, env->K, env->N + 1) +
+           (size_t)2 * env->obs_be * env->K * (env->N + 1) * sizeof(float4) +
+           (size_t)gw::obs_tab_bytes(env->HW, env->obs_be, env->K);
 }
 
 template <int N, int KMAX, bool FEAR>
@@ -2741,7 +2473,7 @@ hipError_t launch_step_obs_k(const Env *env, const gw::Params &p, const gw::Para
     const size_t step_dyn = (size_t)p.resp_off + (FEAR ? 100 * sizeof(double) : 0);
     const size_t dyn = std::max(step_dyn, obs_lds_bytes(env));
     gw_launch((gw::step_obs<N, KMAX, FEAR>), dim3(nstep + nobs), dim3(128), dyn, s, p, q, q.out.obs, q.out.final_obs,
-              nstep, (uint32_t)env->merge_order);
+              nstep);
     return hipGetLastError();
 }
 
@@ -2796,10 +2528,7 @@ hipError_t launch_obs_range(const Env *env, const gw::Params &p, float *obs, flo
     if (env->obs_bf16) {  // gw_set_obs_dtype checked HW % 8 == 0
         gw_launch((gw::obs_kernel<true, true, true>), dim3(grid), dim3(gw::OBS_THREADS), lds, s, p, obs, final_obs);
     } else if (env->HW % 4 == 0) {
-        if (env->obs_nt)
-            gw_launch((gw::obs_kernel<true, true>), dim3(grid), dim3(gw::OBS_THREADS), lds, s, p, obs, final_obs);
-        else
-            gw_launch((gw::obs_kernel<true, false>), dim3(grid), dim3(gw::OBS_THREADS), lds, s, p, obs, final_obs);
+        gw_launch((gw::obs_kernel<true, true>), dim3(grid), dim3(gw::OBS_THREADS), lds, s, p, obs, final_obs);
     } else {
         gw_launch((gw::obs_kernel<false, false>), dim3(grid), dim3(gw::OBS_THREADS), lds, s, p, obs, final_obs);
     }
@@ -2816,14 +2545,8 @@ int64_t stats_rows_n(const Env *env) {
         const int bf = fear_be<N>(env);
         return defer_step_rows<N>(env) + (env->E + bf - 1) / bf;
     }
-    if (env->mode >= 1) {
-        if (env->fear) be = env->K <= 2 ? gw::V2Cfg<N, 2, true>::BE : gw::V2Cfg<N, N, true>::BE;
-        else be = env->K <= 2 ? gw::V2Cfg<N, 2, false>::BE : gw::V2Cfg<N, N, false>::BE;
-    } else if (!env->fear) {
-        be = 256;
-    } else {
-        be = env->K <= 2 ? gw::FearCfg<N, 2>::BE : gw::FearCfg<N, N>::BE;
-    }
+    if (env->fear) be = env->K <= 2 ? gw::V2Cfg<N, 2, true>::BE : gw::V2Cfg<N, N, true>::BE;
+    else be = env->K <= 2 ? gw::V2Cfg<N, 2, false>::BE : gw::V2Cfg<N, N, false>::BE;
     return (env->E + be - 1) / be;
 }
 }  // namespace
@@ -2922,57 +2645,37 @@ gw_status gw_create(const gw_scenario *sc, const gw_config *cfg, int device, voi
     env->seed = cfg->seed;
     for (int k = 0; k < K; ++k) env->apples[k] = sc->apples[k];
     {
-        const char *kv = std::getenv("GW_KERNEL");  // kernel path for A/B measurements
+        // the kernel path: merged for small batches, defer above GW_MERGE_BYTES of obs per step
+        // (crossover at C3's shape with the obs ring's overlapping writers: merged wins up to
+        // 16,384 envs = 128 MiB, defer from 24,576 = 192 MiB; profiles/HISTORY.md);
+        // GW_KERNEL=defer|merged forces one of the two (result-neutral: both are pinned to the
+        // oracle by tests/test_gpu_parity.py)
+        const char *kv = std::getenv("GW_KERNEL");
         env->mode = 3;
-        if (!kv && HW % 4 == 0) {  // small batches: the merged pipeline (profiles/r2_merged)
+        if (HW % 4 == 0) {
             const char *mb = std::getenv("GW_MERGE_BYTES");
-            // crossover at C3's shape (defer with the obs ring's overlapping writers): merged
-            // wins up to 16,384 envs (128 MiB of obs per step), defer from 24,576 (192 MiB)
             const int64_t lim = mb ? std::atoll(mb) : ((int64_t)160 << 20);
             if (cfg->num_envs * (int64_t)K * HW * 4 <= lim) env->mode = 4;
+            if (kv && std::strcmp(kv, "merged") == 0) env->mode = 4;
         }
-        if (kv && std::strcmp(kv, "split") == 0) env->mode = 1;
-        if (kv && std::strcmp(kv, "v1") == 0) env->mode = 0;
-        if (kv && std::strcmp(kv, "fused") == 0 && HW % 4 == 0) env->mode = 2;
         if (kv && std::strcmp(kv, "defer") == 0) env->mode = 3;
-        if (kv && std::strcmp(kv, "merged") == 0 && HW % 4 == 0) env->mode = 4;
-        const char *mo = std::getenv("GW_MERGE_ORDER");
-        if (mo) env->merge_order = std::atoi(mo) ? 1 : 0;
-        const char *dv = std::getenv("GW_DEFER");
-        if (dv) env->defer_order = std::atoi(dv) == 0 ? 0 : (std::atoi(dv) == 3 ? 3 : 1);
+        // fear_v2 block size (result-neutral): wide (default) or narrow (the bf16 obs default)
         const char *fb = std::getenv("GW_FEAR_BE");
         if (fb && std::strcmp(fb, "wide") == 0) env->fear_wide = true;
         if (fb && std::strcmp(fb, "narrow") == 0) env->fear_wide = false;
         env->fear_wide_fixed = fb != nullptr;
-        // obs_kernel block size (tools/gpu_ab2.sh): 4 float4 stores per thread when the writer
+        // obs_kernel block size (profiles/HISTORY.md): 4 float4 stores per thread when the writer
         // runs alone (32x32 K=2 -> 2 envs, 64x64 -> 1), 8 while fear_v2 shares the CUs (32x32 ->
         // 4 envs: 2.5 % faster step at C3)
         int be_def = std::max(1, 4096 / std::max(1, K * HW));
         if (env->mode == 3 && env->fear) be_def *= 2;
         env->obs_be = std::max(1, std::min(8, be_def));  // f32 default <= 8 envs per block
-        const char *be = std::getenv("GW_OBS_BE");
-        if (be) env->obs_be = std::max(1, std::min(gw::OBS_BE, std::atoi(be)));
-        env->obs_be_fixed = be != nullptr;
         env->obs_be_f32 = env->obs_be;
-        const char *nt = std::getenv("GW_OBS_NT");
-        if (nt) env->obs_nt = std::atoi(nt) != 0;
-        const char *aa = std::getenv("GW_ASYNC_AUX");
-        if (aa) env->async_aux = std::atoi(aa) != 0;
-        const char *op = std::getenv("GW_OBS_PRIO");
-        if (op && std::strcmp(op, "hi") == 0) env->obs_hi = true;
+        // scheduling of the async writer (result-neutral): c launches per step, one or two streams
         const char *oc = std::getenv("GW_OBS_CHUNKS");
         if (oc) env->obs_chunks = std::max(1, std::min(64, std::atoi(oc)));
-        const char *ch = std::getenv("GW_CHUNKS");
-        if (ch) env->chunks = std::max(1, std::min(16, std::atoi(ch)));
-        const char *bev = std::getenv("GW_BIND_EVENTS");
-        if (bev) env->bind_events = std::atoi(bev) != 0;
         const char *osn = std::getenv("GW_OBS_STREAMS");
         if (osn) env->obs_streams = std::atoi(osn) > 1 ? 2 : 1;
-        const char *ef = std::getenv("GW_EVENT_FENCE");
-        if (ef && std::strcmp(ef, "system") == 0) {
-            env->sync_flags = hipEventDisableTiming;
-            env->prof_flags = hipEventDefault;
-        }
     }
 
     auto cleanup = [&](gw_status s) {
@@ -3021,6 +2724,7 @@ gw_status gw_reset(void *handle, const uint8_t *env_mask, const int32_t *spawn_c
                    uint16_t *mask, void *stream) {
     Env *env = static_cast<Env *>(handle);
     if (!env) return fail(GW_ERR_ARG, "null env");
+    env->patch_req = Env::PatchReq{};  // a window request armed before the reset is dropped
     gw::Params p = make_params(env);
     p.rmask = env_mask;
     p.spawn = spawn_cells;
@@ -3083,11 +2787,7 @@ static gw_status gw_step_body(void *handle, const int32_t *rl_actions, const int
     auto span_end = [&](hipStream_t, size_t b, int kind) -> gw_status {
         return env->profiling ? prof_span_end(env, b, kind) : GW_OK;
     };
-    // chunk size: a multiple of every block size in play (v2 BE, obs_be) so blocks never straddle
-    const int64_t unit = 128;  // multiple of every step_v2 BE (<= 128) and obs_be (<= 8)
     const bool defer = env->mode == 3 && env->fear;
-    const int nch = ((env->mode == 1 || defer) && want_obs && env->chunks > 1 && env->E >= unit * env->chunks)
-                        ? env->chunks : 1;
     if (env->obs_async && want_obs && env->mode == 4) {
         // Merged pipeline: ONE launch per step on the caller's stream: this step's world update
         // + FeAR (writing descriptor buffer nb) and the obs writer of the previous step (reading
@@ -3112,7 +2812,7 @@ static gw_status gw_step_body(void *handle, const int32_t *rl_actions, const int
         env->desc = env->desc_buf[nb];
         return GW_OK;
     }
-    if (env->obs_async && want_obs && nch == 1 && (env->mode == 1 || env->mode == 3)) {
+    if (env->obs_async && want_obs && env->mode == 3) {
         // Software pipeline over steps.  The world update (and FeAR) of step t runs on s
         // (rewards, dones, masks, state, stats: stream-ordered as usual).  The obs writer of
         // step t runs on obs_stream right after the world update (eager), or is queued and
@@ -3122,9 +2822,8 @@ static gw_status gw_step_body(void *handle, const int32_t *rl_actions, const int
         // that buffer, so the world update waits for it.
         GW_TRY(ensure_obs_stream(env));
         // the world update + FeAR chain runs on the caller's stream itself (no fork / join hops
-        // between consecutive steps); only with the unjoined FeAR (| 4) or GW_ASYNC_AUX=1 (A/B)
-        // does it go to the aux stream
-        const bool on_aux = (defer && env->fear_async) || env->async_aux;
+        // between consecutive steps); only with the unjoined FeAR (| 4) does it go to the aux stream
+        const bool on_aux = defer && env->fear_async;
         if (on_aux) GW_TRY(ensure_aux(env, 3));
         hipStream_t ws = on_aux ? env->aux : s;
         if (on_aux || env->obs_queued) HIP_TRY(hipEventRecord(env->sync_ev[0], s));  // the caller's prior work
@@ -3135,7 +2834,7 @@ static gw_status gw_step_body(void *handle, const int32_t *rl_actions, const int
         if (on_aux) HIP_TRY(hipStreamWaitEvent(ws, env->sync_ev[0], 0));
         if (env->obs_pending[nb]) HIP_TRY(hipStreamWaitEvent(ws, env->obs_done[nb], 0));
         GW_TRY(span_begin(ws, b));
-        const bool bind = env->bind_events && !env->profiling;  // world_ev carried by the launch
+        const bool bind = !env->profiling;  // world_ev carried by the launch
         if (bind) t_bind_stop = env->world_ev;
         const hipError_t se = dispatch_step(env, p, ws);
         t_bind_stop = nullptr;
@@ -3174,17 +2873,17 @@ static gw_status gw_step_body(void *handle, const int32_t *rl_actions, const int
     // every other path writes the current descriptor buffer in place: an async obs_kernel still
     // reading it (a step without obs outputs, or a non-pipelining kernel path) must finish first
     if (env->obs_async || env->fear_pending) GW_TRY(wait_obs(env, s));
-    if (defer && (nch == 1 || env->defer_order == 0)) {
+    if (defer) {
         // world update; then fear_v2 on the aux stream || obs_kernel on s; join
         size_t b;
         GW_TRY(span_begin(s, b));
         HIP_TRY(dispatch_step(env, p, s));
         GW_TRY(span_end(s, b, 0));
-        if (!want_obs || env->defer_order == 0) {
+        if (!want_obs) {
             Env::PatchReq &rq = env->patch_req;
             const int P = rq.P;
             // the requested windows inside the FeAR launch: the row writer's conditions, whole range
-            const bool rows = rq.armed && !want_obs && rq.patch && P >= 2 && P <= 16 && env->E % 4 == 0 &&
+            const bool rows = rq.armed && rq.patch && P >= 2 && P <= 16 && env->E % 4 == 0 &&
                               env->N >= 1 && env->N <= 8 && (uint64_t)env->E * (uint64_t)P < (1ull << 32) &&
                               p.e_begin == 0 && p.e_end == env->E;
             GW_TRY(span_begin(s, b));
@@ -3198,11 +2897,6 @@ static gw_status gw_step_body(void *handle, const int32_t *rl_actions, const int
                 HIP_TRY(dispatch_fear(env, p, s));
             }
             GW_TRY(span_end(s, b, 2));
-            if (want_obs) {
-                GW_TRY(span_begin(s, b));
-                HIP_TRY(launch_obs(env, p, p.out.obs, p.out.final_obs, s));
-                GW_TRY(span_end(s, b, 1));
-            }
             return GW_OK;
         }
         GW_TRY(ensure_aux(env, 2));
@@ -3218,71 +2912,15 @@ static gw_status gw_step_body(void *handle, const int32_t *rl_actions, const int
         HIP_TRY(hipStreamWaitEvent(s, env->sync_ev[1], 0));
         return GW_OK;
     }
-    if (defer) {
-        // env chunks: world update of chunk c on s, then its fear_v2 (aux) and obs_kernel (aux2)
-        // while s moves on to chunk c + 1; s joins both streams at the end
-        GW_TRY(ensure_aux(env, nch + 2, true));
-        const int64_t per = ((env->E / nch + unit - 1) / unit) * unit;
-        for (int c = 0; c < nch; ++c) {
-            gw::Params q = p;
-            q.e_begin = std::min<int64_t>(env->E, c * per);
-            q.e_end = std::min<int64_t>(env->E, (c + 1) * per);
-            if (q.e_begin >= q.e_end) break;
-            size_t b;
-            GW_TRY(span_begin(s, b));
-            HIP_TRY(dispatch_step(env, q, s));
-            GW_TRY(span_end(s, b, 0));
-            HIP_TRY(hipEventRecord(env->sync_ev[c], s));
-            HIP_TRY(hipStreamWaitEvent(env->aux, env->sync_ev[c], 0));
-            HIP_TRY(hipStreamWaitEvent(env->aux2, env->sync_ev[c], 0));
-            GW_TRY(span_begin(env->aux, b));
-            HIP_TRY(dispatch_fear(env, q, env->aux));
-            GW_TRY(span_end(env->aux, b, 2));
-            GW_TRY(span_begin(env->aux2, b));
-            HIP_TRY(launch_obs(env, q, q.out.obs, q.out.final_obs, env->aux2));
-            GW_TRY(span_end(env->aux2, b, 1));
-        }
-        HIP_TRY(hipEventRecord(env->sync_ev[nch], env->aux));
-        HIP_TRY(hipEventRecord(env->sync_ev[nch + 1], env->aux2));
-        HIP_TRY(hipStreamWaitEvent(s, env->sync_ev[nch], 0));
-        HIP_TRY(hipStreamWaitEvent(s, env->sync_ev[nch + 1], 0));
-        return GW_OK;
-    }
-    if (nch == 1) {
-        size_t b;
+    size_t b;
+    GW_TRY(span_begin(s, b));
+    HIP_TRY(dispatch_step(env, p, s));
+    GW_TRY(span_end(s, b, 0));
+    if (want_obs) {
         GW_TRY(span_begin(s, b));
-        HIP_TRY(dispatch_step(env, p, s));
-        GW_TRY(span_end(s, b, 0));
-        if (env->mode != 2 && want_obs) {
-            GW_TRY(span_begin(s, b));
-            HIP_TRY(launch_obs(env, p, p.out.obs, p.out.final_obs, s));
-            GW_TRY(span_end(s, b, 1));
-        }
-        return GW_OK;
+        HIP_TRY(launch_obs(env, p, p.out.obs, p.out.final_obs, s));
+        GW_TRY(span_end(s, b, 1));
     }
-    // Pipeline over env chunks: step_v2(chunk c) on `s`, obs_kernel(chunk c) on the aux stream
-    // after an event; VALU-bound step chunks run concurrently with HBM-bound obs chunks.
-    GW_TRY(ensure_aux(env, nch + 2));
-    HIP_TRY(hipEventRecord(env->sync_ev[0], s));           // fork: aux waits for prior work on s
-    HIP_TRY(hipStreamWaitEvent(env->aux, env->sync_ev[0], 0));
-    const int64_t per = ((env->E / nch + unit - 1) / unit) * unit;
-    for (int c = 0; c < nch; ++c) {
-        gw::Params q = p;
-        q.e_begin = std::min<int64_t>(env->E, c * per);
-        q.e_end = std::min<int64_t>(env->E, (c + 1) * per);
-        if (q.e_begin >= q.e_end) break;
-        size_t b;
-        GW_TRY(span_begin(s, b));
-        HIP_TRY(dispatch_step(env, q, s));
-        GW_TRY(span_end(s, b, 0));
-        HIP_TRY(hipEventRecord(env->sync_ev[1 + c], s));
-        HIP_TRY(hipStreamWaitEvent(env->aux, env->sync_ev[1 + c], 0));
-        GW_TRY(span_begin(env->aux, b));
-        HIP_TRY(launch_obs(env, q, q.out.obs, q.out.final_obs, env->aux));
-        GW_TRY(span_end(env->aux, b, 1));
-    }
-    HIP_TRY(hipEventRecord(env->sync_ev[nch + 1], env->aux));  // join
-    HIP_TRY(hipStreamWaitEvent(s, env->sync_ev[nch + 1], 0));
     return GW_OK;
 }
 
@@ -3322,8 +2960,8 @@ gw_status gw_set_obs_dtype(void *handle, int dtype) {
     Env *env = static_cast<Env *>(handle);
     if (!env) return fail(GW_ERR_ARG, "null env");
     if (dtype != GW_OBS_F32 && dtype != GW_OBS_BF16) return fail(GW_ERR_ARG, "gw_set_obs_dtype: unknown dtype");
-    if (dtype == GW_OBS_BF16 && (env->HW % 8 != 0 || env->mode == 0 || env->mode == 2))
-        return fail(GW_ERR_ARG, "gw_set_obs_dtype: bf16 obs needs H*W % 8 == 0 and the split / defer kernel paths");
+    if (dtype == GW_OBS_BF16 && env->HW % 8 != 0)
+        return fail(GW_ERR_ARG, "gw_set_obs_dtype: bf16 obs needs H*W % 8 == 0");
     const bool bf = dtype == GW_OBS_BF16;
     if (bf != env->obs_bf16 && env->mode == 4 && env->obs_queued) {  // merged: the queued writer
         hipStream_t ls = env->last_stream;
@@ -3338,9 +2976,8 @@ gw_status gw_set_obs_dtype(void *handle, int dtype) {
     }
     // bf16 writer: ~64 KB of obs per block (C3: 16 envs, 4.3 TB/s; 4 envs 3.4, 8 envs 4.2;
     // C4: 4 envs; profiles/r1_bf16); f32: the create-time default
-    if (!env->obs_be_fixed)
-        env->obs_be = bf ? std::max(1, std::min(gw::OBS_BE, 32768 / std::max(1, env->K * env->HW)))
-                         : env->obs_be_f32;
+    env->obs_be = bf ? std::max(1, std::min(gw::OBS_BE, 32768 / std::max(1, env->K * env->HW)))
+                 : env->obs_be_f32;
     env->obs_bf16 = bf;
     // the bf16 step is bound by the world update + FeAR chain, where 32 envs per fear block is
     // 2 % faster; the stats rows depend on it, so only before the first reset
@@ -3535,10 +3172,8 @@ static gw_status obs_patch_launch(Env *env, int32_t P, float *patch, float *fina
     for (int k = 0; k < GW_MAX_AGENTS; ++k) a.apples[k] = k < env->K ? env->apples[k] : -1;
     // the map part of each window (P <= 16) comes from a table of every centre's window (built on
     // first use of this P; 0.5 MB at 32 x 32 and P = 11, 4 MB at 64 x 64 and P = 16);
-    // GW_PATCH_TABLE=0: the table-free writers (A/B)
-    static const char *tbl_env = std::getenv("GW_PATCH_TABLE");
     const size_t tb = gw::window_table_bytes(env->H, env->W, P);
-    if (P * P <= 256 && tb <= (size_t)64 << 20 && !(tbl_env && tbl_env[0] == '0')) {
+    if (P * P <= 256 && tb <= (size_t)64 << 20) {
         float *t = nullptr;
         for (auto &pt : env->ptbls)
             if (pt.first == P) t = pt.second;
@@ -3668,7 +3303,6 @@ void gw_destroy(void *handle) {
     for (hipEvent_t e : env->ev_pool) (void)hipEventDestroy(e);
     for (hipEvent_t e : env->sync_ev) (void)hipEventDestroy(e);
     if (env->aux) (void)hipStreamDestroy(env->aux);
-    if (env->aux2) (void)hipStreamDestroy(env->aux2);
     if (env->obs_stream) (void)hipStreamDestroy(env->obs_stream);
     if (env->obs_stream2) (void)hipStreamDestroy(env->obs_stream2);
     for (hipEvent_t e : env->obs_done)

@@ -35,6 +35,7 @@
 #include "learner_ops.h"
 #include "philox.h"
 #include "prof.h"
+#include "measure.h"
 
 namespace {
 
@@ -2693,7 +2694,7 @@ gw_status dnet_ok(const gw_mlp_actors *n, int K, int in_dim, int out, const gw_a
 // update as records {int32 launch, int32 blocks, blocks x NSTAMP uint64} (a synchronising diagnostic)
 constexpr int STAMP_BLOCKS = 8192;
 unsigned long long *stamp_buf() {
-    static const char *path = std::getenv("GW_LEARN_STAMP");
+    static const char *path = GW_MEASURE_ENV("GW_LEARN_STAMP");
     static unsigned long long *buf = nullptr;
     if (path && *path && !buf && hipMalloc(&buf, sizeof(unsigned long long) * 4 * STAMP_BLOCKS * NSTAMP) != hipSuccess)
         buf = nullptr;
@@ -2704,7 +2705,7 @@ void stamp_dump(hipStream_t s, const int (&nb)[4]) {
     if (!buf || hipStreamSynchronize(s) != hipSuccess) return;
     static std::vector<unsigned long long> h(4 * STAMP_BLOCKS * NSTAMP);
     if (hipMemcpy(h.data(), buf, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost) != hipSuccess) return;
-    FILE *f = std::fopen(std::getenv("GW_LEARN_STAMP"), "ab");
+    FILE *f = std::fopen(GW_MEASURE_ENV("GW_LEARN_STAMP"), "ab");
     if (!f) return;
     for (int l = 0; l < 4; ++l) {
         const int32_t hd[2] = {l, nb[l]};

@@ -23,6 +23,7 @@
 
 #include "patch_ops.h"
 #include "prof.h"
+#include "measure.h"
 #include "window_rows.h"
 
 namespace {
@@ -250,7 +251,7 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a, unsign
         const int len = nenv * PP;
         const uint32_t m_pp = (uint32_t)((0x100000000ull + (uint64_t)PP - 1) / (uint64_t)PP);
         const uint32_t m_p = (uint32_t)((0x100000000ull + (uint64_t)P - 1) / (uint64_t)P);
-        if (a.probe == 2) {  // measurement only: staging, then zeros
+        if ((GW_MEASURE_ON && a.probe == 2)) {  // measurement only: staging, then zeros
             for (int k = 0; k < K; ++k) {
                 const int64_t off = ((int64_t)k * a.E + e0) * PP;
                 float *o = a.patch + off;
@@ -301,7 +302,7 @@ __global__ void __launch_bounds__(THREADS) window_kernel(gw::PatchArgs a, unsign
             const int n4 = (len - lead) / 4;
             float4 *o4 = reinterpret_cast<float4 *>(o + lead);
             for (int j = tid; j < n4; j += THREADS) {
-                if (a.probe == 1) {  // measurement only: the table was built, zeros stored
+                if ((GW_MEASURE_ON && a.probe == 1)) {  // measurement only: the table was built, zeros stored
                     reinterpret_cast<float4 *>(o + lead)[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
                     continue;
                 }
@@ -486,9 +487,9 @@ hipError_t launch_windows(const PatchArgs &args, hipStream_t s) {
     PatchArgs a = args;
     const int np = a.N + 1, PP = a.P * a.P;
     // envs per block: 32, or 64 (GW_PATCH_PB=64, measurement only for now)
-    static const char *probe_env = std::getenv("GW_PATCH_PROBE");  // (measurement only)
+    static const char *probe_env = GW_MEASURE_ENV("GW_PATCH_PROBE");  // (measurement only)
     if (probe_env) a.probe = std::atoi(probe_env);
-    static const char *pb_env = std::getenv("GW_PATCH_PB");
+    static const char *pb_env = GW_MEASURE_ENV("GW_PATCH_PB");
     const int PB = (pb_env && std::atoi(pb_env) == 64) ? 64 : 32;
     // LDS: road bitmask, flags, centres, patch cells + values, and per mode: MODE 0 one agent's
     // window run (PP <= 256), MODE 2 the nibble table (PB * K * P * P / 4 u16, patch indices
@@ -506,7 +507,7 @@ hipError_t launch_windows(const PatchArgs &args, hipStream_t s) {
     int mode = (a.P % 4 == 0 && np < 16 && base + extra[2] <= LDS_MAX) ? 2
                : (a.tbl && PP <= 256) ? 4
                : (np < 256 && base + extra[3] <= LDS_MAX) ? 3 : 1;
-    static const char *force = std::getenv("GW_PATCH_MODE");  // (measurement only: A/B of the writers)
+    static const char *force = GW_MEASURE_ENV("GW_PATCH_MODE");  // (measurement only: A/B of the writers)
     if (force) {
         const int f = std::atoi(force);
         if (f == 1 || (f == 0 && PP <= 64 * MAXPL && base + extra[0] <= LDS_MAX) ||

@@ -18,20 +18,24 @@ PKG_ROOT = os.path.dirname(HERE)
 REPO_ROOT = os.path.dirname(PKG_ROOT)
 CSRC = os.path.join(PKG_ROOT, "csrc")
 INCLUDE = os.path.join(REPO_ROOT, "include")
-LIB_PATH = os.path.join(CSRC, "libgridenv.so")
+# MARLNAV_MEASURE=1: the measurement build (-DGW_MEASURE, csrc/measure.h: the kernels' A/B, probe
+# and block-stamp switches read from the environment), a separate library and object cache; the
+# release library (the product, the default) compiles those switches out
+MEASURE = os.environ.get("MARLNAV_MEASURE", "0") == "1"
+LIB_PATH = os.path.join(CSRC, "libgridenv_measure.so" if MEASURE else "libgridenv.so")
 HIP_SOURCES = [os.path.join(CSRC, "gridenv.hip"), os.path.join(CSRC, "learner_ops.hip"),
                os.path.join(CSRC, "actor_ops.hip"), os.path.join(CSRC, "rollout_ops.hip"),
                os.path.join(CSRC, "maddpg_ops.hip"), os.path.join(CSRC, "patch_ops.hip")]
 HEADERS = [os.path.join(INCLUDE, "gridenv.h"), os.path.join(INCLUDE, "learner_ops.h"),
            os.path.join(INCLUDE, "actor_ops.h"), os.path.join(INCLUDE, "rollout_ops.h")]
 SOURCES = HIP_SOURCES + HEADERS + [os.path.join(CSRC, "patch_ops.h"), os.path.join(CSRC, "window_rows.h"), os.path.join(CSRC, "prof.h"),
-                                   os.path.join(CSRC, "philox.h")]
-OBJ_DIR = os.path.join(CSRC, "build")
+                                   os.path.join(CSRC, "philox.h"), os.path.join(CSRC, "measure.h")]
+OBJ_DIR = os.path.join(CSRC, "build_measure" if MEASURE else "build")
 ARCH = os.environ.get("MARLNAV_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 HIPCC_FLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared",
-               "-ffp-contract=off", "-fno-fast-math", "-Wall"]
+               "-ffp-contract=off", "-fno-fast-math", "-Wall"] + (["-DGW_MEASURE"] if MEASURE else [])
 COMPILE_FLAGS = [f for f in HIPCC_FLAGS if f != "-shared"]
 
 GW_MAX_AGENTS = 8

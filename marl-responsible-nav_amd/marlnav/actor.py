@@ -491,6 +491,37 @@ class MultiAgentActors(nn.Module):
         else:
             self._epoch = getattr(self, "_epoch", 0) + 1
 
+    def _mlp_workspace(self, env, patch: int):
+        """The fused MLP path's per-(actors, env) state, its workspace derived for the current
+        parameters (enqueued on the current stream when they changed)."""
+        from . import _lib
+        st = self._fast
+        if st is None or st["env"] is not env or st.get("patch", 0) != patch:  # per-(actors, env) constants
+            if not self.fusable(env, patch):
+                raise _lib.GwError("act_env: actor not fusable (needs the f32 MLP 128-128-9 over the env's H*W obs, "
+                                   "or over P x P windows with patch=P)")
+            lib = _lib.load()
+            ws_n = int(lib.gw_patch_actor_workspace_floats(patch, env.H, env.W, self.K) if patch
+                       else lib.gw_actor_workspace_floats(self.net.in_dim, self.K))
+            st = self._fast = dict(env=env, lib=lib, ws=torch.empty(ws_n, dtype=torch.float32, device=env.device),
+                                   key=None, spec=None, actions=None, probs=None, patch=patch)
+        key = self._ws_key()
+        if key != st["key"]:
+            self._prepare(env, st)
+            st["key"] = key
+        return st
+
+    @torch.no_grad()
+    def ensure_workspace(self, env, patch: int = 0):
+        """Create and derive the fused path's workspace for ``env`` now, on the current stream.
+        Rollout.capture calls it before capturing: a derivation (and the workspace's allocation)
+        made inside a captured graph would run only in that graph's replays, so eager steps before
+        the first replay would act on an underived workspace."""
+        if self.arch == "cnn":
+            self._cnn_workspace(env, int(patch))
+        else:
+            self._mlp_workspace(env, int(patch))
+
     @torch.no_grad()
     def act_env(self, env, mask: torch.Tensor | None = None, training: bool = True, tau: float = 1.0,
                 seed: int = 0, counter: int = 0, uniform: torch.Tensor | None = None,
@@ -515,20 +546,7 @@ class MultiAgentActors(nn.Module):
                                      logits_out, int(patch), counter_dev, listed)
         net, K, E, dev = self.net, self.K, env.E, env.device
         patch = int(patch)
-        st = self._fast
-        if st is None or st["env"] is not env or st.get("patch", 0) != patch:  # per-(actors, env) constants
-            if not self.fusable(env, patch):
-                raise _lib.GwError("act_env: actor not fusable (needs the f32 MLP 128-128-9 over the env's H*W obs, "
-                                   "or over P x P windows with patch=P)")
-            lib = _lib.load()
-            ws_n = int(lib.gw_patch_actor_workspace_floats(patch, env.H, env.W, K) if patch
-                       else lib.gw_actor_workspace_floats(net.in_dim, K))
-            st = self._fast = dict(env=env, lib=lib, ws=torch.empty(ws_n, dtype=torch.float32, device=dev), key=None,
-                                   spec=None, actions=None, probs=None, patch=patch)
-        key = self._ws_key()
-        if key != st["key"]:
-            self._prepare(env, st)
-            st["key"] = key
+        st = self._mlp_workspace(env, patch)
         if actions_out is None:
             actions_out = torch.empty((E, K), dtype=torch.int32, device=dev)
         if probs_out is None:
@@ -580,14 +598,12 @@ class MultiAgentActors(nn.Module):
         st["pending"] = True
         return True
 
-    def _act_env_cnn(self, env, mask, training, tau, seed, counter, uniform, actions_out, probs_out, logits_out,
-                     patch=0, counter_dev=None, listed=False):
-        """act_env for the CNN head: gw_cnn_act (layer 1 from the obs descriptors through the
-        per-position delta table, include/actor_ops.h), then the same fused layers 2-3 + noise +
-        softmax + mask + argmax as the MLP path.  patch = P: the head built for P x P inputs on each
-        agent's window (gw_patch_cnn_act: per-centre tables + the recomputed positions)."""
+    def _cnn_workspace(self, env, patch: int):
+        """The fused CNN path's per-(actors, env) state, its workspace (gw_cnn_prepare /
+        gw_patch_cnn_prepare) derived for the current parameters; -> (state, derived now)."""
         from . import _lib
         K, E, dev = self.K, env.E, env.device
+        derived = False
         st = self._fast
         if st is None or st["env"] is not env or st.get("patch", 0) != patch:
             if not self.fusable(env, patch):
@@ -626,6 +642,19 @@ class MultiAgentActors(nn.Module):
                     _lib.check(st["lib"].gw_cnn_prepare(env.handle, C.byref(st["spec"]), st["ws"].data_ptr(), stream),
                                "gw_cnn_prepare")
             st["key"] = key
+            derived = True
+        return st, derived
+
+    def _act_env_cnn(self, env, mask, training, tau, seed, counter, uniform, actions_out, probs_out, logits_out,
+                     patch=0, counter_dev=None, listed=False):
+        """act_env for the CNN head: gw_cnn_act (layer 1 from the obs descriptors through the
+        per-position delta table, include/actor_ops.h), then the same fused layers 2-3 + noise +
+        softmax + mask + argmax as the MLP path.  patch = P: the head built for P x P inputs on each
+        agent's window (gw_patch_cnn_act: per-centre tables + the recomputed positions)."""
+        from . import _lib
+        K, E, dev = self.K, env.E, env.device
+        st, derived = self._cnn_workspace(env, patch)
+        if derived:
             listed = False  # a listing made before the workspace was re-derived is not used
         if actions_out is None:
             actions_out = torch.empty((E, K), dtype=torch.int32, device=dev)

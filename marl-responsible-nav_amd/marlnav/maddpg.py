@@ -663,6 +663,9 @@ class MADDPG:
         # caller's fence must match it, and a change of the ring's mode invalidates the capture
         self._capture_desc = bool(getattr(replay, "use_desc", False)) if batch is None else None
         desc = batch is None and self.desc_capable(replay)
+        # which learner the capture holds: replay_learn primes / marks staleness only for the
+        # descriptor learner's capture, not whenever _desc happens to be populated
+        self._capture_is_desc = bool(desc)
         if desc:
             return self._capture_desc_learner(replay, warmup, actor_env, launches)
         if batch is not None:
@@ -779,13 +782,14 @@ class MADDPG:
         self._launch_keep = self._graph_ctx = None
         self._prep_env = self._prep_ws = None
         self._capture_desc = None
+        self._capture_is_desc = False
 
     def capture_matches(self, replay) -> bool:
         """Whether the captured update samples the rows ``replay`` currently offers."""
         return self._graph is not None and getattr(self, "_capture_desc", None) == bool(getattr(replay, "use_desc", False))
 
     def replay_learn(self):
-        desc = getattr(self, "_capture_desc", None) and self._desc
+        desc = getattr(self, "_capture_is_desc", False) and self._desc
         if desc and self._desc_stale:
             # weights changed since the capture (a load, a dense update): re-derive the partial sums
             self.desc_prime(next(iter(self._desc.values()))["replay"])

@@ -243,6 +243,7 @@ class Rollout:
                           not self.patch_async and self.replay is not None and env.device.type == "cuda" and
                           env.E % 4 == 0 and os.environ.get("GW_CNN_WRITE_LIST", "1") != "0")
         self._lists_ready = False  # a listing for the env's current descriptors was launched
+        self._no_list = False  # capture(): this step writes its windows without the listing
         self.distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
         rank = dist.get_rank(group) if self.distributed else 0
         # the PyTorch actor's Gumbel noise: one stream per rank (the fused actor's Philox noise is
@@ -422,7 +423,12 @@ class Rollout:
                           os.environ.get("GW_FEAR_PATCH", "1") != "0")
             if step_patch:
                 env.patch_next(self.patch, rp.obs[nxt], rp.final_obs[cur])
-            r = env.step(actions, into=into)
+            try:
+                r = env.step(actions, into=into)
+            except BaseException:
+                if step_patch:  # disarm: a later gw_step must not write through these pointers
+                    env.patch_next(self.patch, None, None)
+                raise
             if self.patch_async:  # the step's windows, beside the next step's actor
                 main = torch.cuda.current_stream(env.device)
                 self._pstream.wait_stream(main)
@@ -433,7 +439,7 @@ class Rollout:
             elif self.patch and step_patch:
                 pass  # written by the step (gw_step_patch_next)
             elif self.patch:  # the step's obs / terminal obs as patches, straight into the ring
-                if not (self._cnn_list and not env.fear_async and
+                if not (self._cnn_list and not env.fear_async and not self._no_list and
                         self.actors.patch_cnn_write_list(env, self.patch, rp.obs[nxt], rp.final_obs[cur])):
                     env.obs_patch(self.patch, final=True, out=rp.obs[nxt], final_out=rp.final_obs[cur])
                 else:
@@ -494,22 +500,40 @@ class Rollout:
             raise _lib.GwError("Rollout.capture: the gather needs window == n, no pending steps and one rank")
         self._flush()
         self._patch_join()  # no side-stream writer from before the capture may be waited on inside it
+        # the fused actor's workspace exists and matches the weights before the capture (a
+        # derivation captured into a graph would not run for eager steps before its replay)
+        self.actors.ensure_workspace(env, self.patch)
         t0, rt0, calls0 = self.t, rp.t, self._calls
+        fast = getattr(self.actors, "_fast", None)
+        lists0, pend0 = self._lists_ready, (fast or {}).get("pending")
         start = env.pipeline_save()
         graphs, ends = [], []
-        with torch.cuda.device(env.device):
-            torch.cuda.synchronize(env.device)
-            for _ in range(rp.S // n):
-                cg = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(cg):
-                    env.profile(False)
-                    for _i in range(n):
-                        self.step()
-                    self._patch_join()  # the graph's last window writer joins its stream
-                graphs.append(cg)
-                ends.append(env.pipeline_save())
-        # nothing ran: the host-side state is the pre-capture one
-        self.t, rp.t, self._calls = t0, rt0, calls0
+        try:
+            with torch.cuda.device(env.device):
+                torch.cuda.synchronize(env.device)
+                for _ in range(rp.S // n):
+                    cg = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(cg):
+                        env.profile(False)
+                        for _i in range(n):
+                            # the CNN listing (gw_patch_cnn_write_list) never crosses a graph
+                            # boundary: a graph's first act lists for itself and its last step
+                            # writes the windows alone, so every graph replays correctly after
+                            # any other graph, after eager steps and right after reset()
+                            if _i == 0:
+                                self._lists_ready = False
+                            self._no_list = _i == n - 1
+                            self.step()
+                        self._patch_join()  # the graph's last window writer joins its stream
+                    graphs.append(cg)
+                    ends.append(env.pipeline_save())
+        finally:
+            # nothing ran: the host-side state is the pre-capture one
+            self._no_list = False
+            self.t, rp.t, self._calls = t0, rt0, calls0
+            self._lists_ready = lists0
+            if fast is not None:
+                fast["pending"] = pend0
         env.pipeline_load(start)
         self._graphs = RolloutGraphs(self, n, graphs, ends, t0 % rp.S)
         return self._graphs
@@ -553,6 +577,11 @@ class RolloutGraphs:
         g = off // self.n
         self.graphs[g].replay()
         ro.env.pipeline_load(self.ends[g])
+        # a graph's last step lists nothing and its acts leave the bucket counters zeroed (capture)
+        ro._lists_ready = False
+        fast = getattr(ro.actors, "_fast", None)
+        if fast is not None:
+            fast["pending"] = False
         ro.t += self.n
         rp.t = ro.t
         ro._calls += self.n

@@ -19,17 +19,16 @@ OUTS = ("reward", "fear", "shaped", "term", "trunc", "done", "mask", "ep_return"
 
 @pytest.mark.parametrize("path,fear,name,mode,E", [
     ("defer", True, "grid32", True, 4096), ("defer", False, "grid32", True, 4096),
-    ("split", True, "grid32", True, 4096), ("defer", True, "grid64_n8", True, 1024),
-    ("defer", True, "grid32", "lazy", 4096), ("split", False, "grid32", "lazy", 4096),
+    ("defer", True, "grid64_n8", True, 1024), ("defer", True, "grid32", "lazy", 4096),
+    ("defer", False, "grid32", "lazy", 4096), ("defer", False, "grid64_n8", True, 1024),
     ("defer", True, "level3", True, 1), ("defer", True, "level3", "lazy", 333),   # ragged env counts
-    ("fused", True, "grid32", True, 515), ("v1", True, "grid32", True, 257),       # non-pipelining paths
+    ("defer", True, "grid32", True, 515), ("defer", False, "grid32", True, 257),
     # merged: one step_obs launch per step (step t + the obs writer of step t-1), one stream
     ("merged", True, "grid32", True, 4096), ("merged", False, "grid32", True, 4099),
     ("merged", True, "grid64_n8", "lazy", 1024), ("merged", True, "level3", True, 1),
     ("merged", False, "level3", True, 333)])
 def test_async_obs_matches_sync(path, fear, name, mode, E, monkeypatch):
     monkeypatch.setenv("GW_KERNEL", path)
-    monkeypatch.setenv("GW_CHUNKS", "1")
     sc = S.builtin(name)
     T = 12 if name == "grid64_n8" else 24
     mk = lambda: VecGridEnv(sc, num_envs=E, fear=fear, fear_weight=-5.0, seed=5, final_obs=True, debug=True,

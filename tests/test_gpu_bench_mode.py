@@ -37,7 +37,6 @@ def _bench_env():
 def bench_run(request):
     mp = pytest.MonkeyPatch()
     mp.delenv("GW_KERNEL", raising=False)  # the default path (defer) as in bench.py
-    mp.delenv("GW_CHUNKS", raising=False)
     try:
         # pass 1: which envs hit the cap (first episode cut at step 150)
         env = _bench_env()

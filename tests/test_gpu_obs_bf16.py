@@ -46,10 +46,11 @@ def test_bf16_obs_equals_f32(name, fear, mode, E):
     b.close()
 
 
-def test_bf16_obs_rejected_on_the_fused_path(monkeypatch):
-    monkeypatch.setenv("GW_KERNEL", "fused")
+def test_bf16_obs_rejected_without_hw_multiple_of_8():
+    # level3 is 10 x 16 = 160 cells (a multiple of 8): a 10 x 15 map is not
+    sc = S.compile_scenario(S.level3_like(10, 15, 4, 2))
     with pytest.raises(_lib.GwError):
-        VecGridEnv("grid32", num_envs=64, obs_dtype=torch.bfloat16)
+        VecGridEnv(sc, num_envs=64, obs_dtype=torch.bfloat16)
 
 
 def test_bf16_rollout_matches_f32():

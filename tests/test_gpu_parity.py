@@ -140,17 +140,11 @@ def _compare_native(sc, E, fear, steps, nthreads=16, offset=0, seed=7, weight=-5
 
 
 KERNEL_PATHS = {
-    "split": {"GW_KERNEL": "split", "GW_CHUNKS": "2"},       # FeAR inline in step_v2, chunked 2-stream pipeline
-    "split1": {"GW_KERNEL": "split", "GW_CHUNKS": "1"},       # step_v2 then obs_kernel, one stream
-    "split_plain": {"GW_KERNEL": "split", "GW_OBS_NT": "0", "GW_OBS_BE": "8"},
-    "fused": {"GW_KERNEL": "fused"},                          # obs stores inside step_v2
-    "defer": {"GW_KERNEL": "defer"},                          # default: fear_v2 on a 2nd stream || obs_kernel
-    "defer_serial": {"GW_KERNEL": "defer", "GW_DEFER": "0"},  # step_v2 <DEFER>, fear_v2, obs_kernel, one stream
-    "defer_wide": {"GW_KERNEL": "defer", "GW_FEAR_BE": "wide"},  # fear_v2 with 2x envs per block (default)
-    "defer_narrow": {"GW_KERNEL": "defer", "GW_FEAR_BE": "narrow"},  # fear_v2 with 1x
-    "defer_chunks": {"GW_KERNEL": "defer", "GW_CHUNKS": "2"},  # 2 env chunks over 3 streams
-    "v1": {"GW_KERNEL": "v1"},                                # the first kernels
-    "merged": {"GW_KERNEL": "merged"},                        # synchronous: as split1 (async: step_obs)
+    # the two kernel paths gw_create picks (round 6: the A/B-only paths v1 / split / fused and
+    # the env-chunk pipelines were deleted)
+    "defer": {"GW_KERNEL": "defer"},   # FeAR on: step_v2 <DEFER>, fear_v2 on a 2nd stream || obs_kernel
+    "defer_narrow": {"GW_KERNEL": "defer", "GW_FEAR_BE": "narrow"},  # fear_v2 blocks of the bf16 obs default
+    "merged": {"GW_KERNEL": "merged"},  # synchronous: step_v2 with FeAR inline, then obs_kernel
 }
 
 
@@ -222,8 +216,6 @@ def test_sharding_is_invariant():
 @pytest.mark.parametrize("name,E", [("grid32", 65536), ("grid64_n8", 65536)])
 def test_full_size_properties(name, E, kernel_path):
     """BASELINE sizes: size-independent invariants on every env + a bit-exact slice vs the oracle."""
-    if kernel_path in ("v1", "split_plain"):
-        pytest.skip("full-size run only for the default and fused paths")
     sc = S.builtin(name)
     env = VecGridEnv(sc, num_envs=E, fear=True, fear_weight=-5.0, seed=9, stats=True, debug=True)
     sl0, sl = 4096 + 128, 256  # a slice that straddles pipeline chunks and blocks

@@ -157,3 +157,49 @@ def test_window_rollout_graph_equals_eager(arch, scen, P, fear):
     for n, v in a["state"].items():
         assert torch.equal(v, b["state"][n]), n
     assert a["totals"] == b["totals"]
+
+
+@pytest.mark.parametrize("arch,scen,P,fear", [("cnn", "grid64_n8", 16, False)])
+def test_window_graph_captured_right_after_reset(arch, scen, P, fear):
+    """a capture taken right after reset() (no listing pending) followed by EAGER steps
+    before the first replay, then replays, then eager steps again: == the eager rollout bit for bit.
+    The CNN head's listing never crosses a graph boundary (Rollout.capture), and the capture leaves
+    the host's listing state (_lists_ready, the actor's pending flag) as it found it."""
+    from marlnav.actor import MultiAgentActors
+    from marlnav.rollout import Rollout
+    En, slots = 1024, 32
+    plan = ["capture"] + ["e"] * G + ["g", "g"] + ["e"] * 3
+    outs = []
+    for graph in (False, True):
+        env = VecGridEnv(scen, num_envs=En, fear=fear, fear_weight=-5.0, max_steps=40, auto_reset=True, seed=SEED,
+                         stats=True, obs=False)
+        actors = MultiAgentActors(env.K, P, P, arch=arch, device=env.device, seed=0)
+        ro = Rollout(env, actors, replay_slots=slots, training=True, seed=SEED, patch=P)
+        assert ro.fused and ro._cnn_list
+        ro.reset()
+        for op in plan:
+            if op == "capture":
+                if graph:
+                    graphs = ro.capture(G)
+                    assert ro._lists_ready is False and not actors._fast.get("pending")
+            elif op == "g" and graph:
+                graphs.replay()
+            elif op == "g":
+                for _ in range(G):
+                    ro.step()
+            else:
+                ro.step()
+        ro.fence()
+        rp = ro.replay
+        o = {n: getattr(rp, n).clone() for n in ("obs", "final_obs", "probs", "reward", "term", "done")}
+        o["state"] = env.state()
+        o["totals"] = ro.totals()
+        torch.cuda.synchronize()
+        env.close()
+        outs.append(o)
+    a, b = outs
+    for n in ("obs", "final_obs", "probs", "reward", "term", "done"):
+        assert torch.equal(a[n], b[n]), n
+    for n, v in a["state"].items():
+        assert torch.equal(v, b["state"][n]), n
+    assert a["totals"] == b["totals"]

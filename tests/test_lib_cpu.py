@@ -41,6 +41,35 @@ def test_library_targets_gfx950():
     assert b"amdgcn-amd-amdhsa--gfx950" in blob
 
 
+MEASURE_SWITCHES = ("GW_ACT_AB", "GW_CNN_AB", "GW_PATCH_PROBE", "GW_PATCH_PB", "GW_PATCH_MODE", "GW_WCNN_STAT",
+                    "GW_RARE_STAMP", "GW_LEARN_STAMP")
+
+
+def test_release_library_ignores_measurement_switches():
+    """the kernels' work-skipping A/B and probe switches (GW_ACT_AB drops layer 2,
+    GW_PATCH_PROBE stores zeros, ...) exist only in the -DGW_MEASURE build (csrc/measure.h).  The
+    release library never reads them: their names are not even in the binary, so no stale export
+    can change what the product computes.  The env knobs it does read are result-neutral
+    scheduling choices or the tested precision variant."""
+    assert not _lib.MEASURE
+    blob = open(_lib.build(), "rb").read()
+    for name in MEASURE_SWITCHES:
+        assert name.encode() not in blob, f"{name} is read by the release library"
+    # the sources read every one of them only through GW_MEASURE_ENV
+    csrc = os.path.join(REPO, "marl-responsible-nav_amd", "csrc")
+    for fn in os.listdir(csrc):
+        if fn.endswith((".hip", ".h")):
+            text = open(os.path.join(csrc, fn)).read()
+            for name in MEASURE_SWITCHES:
+                assert f'getenv("{name}")' not in text.replace("GW_MEASURE_ENV", ""), (fn, name)
+    known = {"GW_KERNEL", "GW_MERGE_BYTES", "GW_FEAR_BE", "GW_OBS_CHUNKS", "GW_OBS_STREAMS", "GW_ACT_V",
+             "GW_ACT_WAVES", "GW_WCNN_LIST"}
+    for fn in os.listdir(csrc):
+        if fn.endswith((".hip", ".h")):
+            for name in re.findall(r'std::getenv\("(\w+)"\)', open(os.path.join(csrc, fn)).read()):
+                assert name in known, (fn, name)
+
+
 STRUCTS = {
     "gw_scenario": (_lib.GwScenario, ["H", "W", "region", "policy_id", "n_policies", "policy_cdf", "mdr", "apples"]),
     "gw_config": (_lib.GwConfig, ["N", "K", "num_envs", "env_offset", "fear", "fear_weight", "max_steps",

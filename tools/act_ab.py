@@ -4,6 +4,9 @@ stamps of wave 0 of every block.  Run on the GPU box:
     python tools/act_ab.py [scenario] [envs] [iters]"""
 import ctypes as C
 import os
+
+# the A/B and probe switches exist only in the measurement build (csrc/measure.h)
+os.environ.setdefault("MARLNAV_MEASURE", "1")
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

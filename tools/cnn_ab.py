@@ -3,6 +3,9 @@ with phases switched off through GW_CNN_AB (bit 0: the recomputed positions, bit
 rows).  Eager launches timed with events around `iters` calls on an otherwise idle GPU.
 Run on the GPU box:  python tools/cnn_ab.py [scenario] [envs] [iters]"""
 import os
+
+# the A/B and probe switches exist only in the measurement build (csrc/measure.h)
+os.environ.setdefault("MARLNAV_MEASURE", "1")
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -5,7 +5,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$T; mkdir -p $O
 for pr in 0 0; do
   for sh in "65536 11 grid32" "65536 16 grid64_n8"; do
-    GW_PATCH_PROBE=$pr timeout -k 10 120 python tools/patch_probe.py $sh > $O/p.log 2>&1 || { tail -5 $O/p.log; exit 1; }
+    MARLNAV_MEASURE=1 GW_PATCH_PROBE=$pr timeout -k 10 120 python tools/patch_probe.py $sh > $O/p.log 2>&1 || { tail -5 $O/p.log; exit 1; }
     echo "probe=$pr $(grep GB/s $O/p.log)"
   done
 done

@@ -1,5 +1,8 @@
 """Time gw_obs_patch alone (HIP events) over E and P: where does the patch writer's time go."""
 import os
+
+# the A/B and probe switches exist only in the measurement build (csrc/measure.h)
+os.environ.setdefault("MARLNAV_MEASURE", "1")
 import sys
 import time
 

@@ -3,6 +3,9 @@ gw_cnn_act at c4cnn's), CALLS act calls on a fixed env state (run under rocprofv
 --stats; GW_CNN_AB selects the A/B variants of the layer-1 kernels, csrc/actor_ops.hip).
 Usage: wcnn_probe.py [CALLS] [full]"""
 import os
+
+# the A/B and probe switches exist only in the measurement build (csrc/measure.h)
+os.environ.setdefault("MARLNAV_MEASURE", "1")
 import sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "marl-responsible-nav_amd"))
