@@ -118,6 +118,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     one object per source (cached by content hash), the sources compiled in parallel."""
     if not force and not needs_build():
         return LIB_PATH
+    stamp = source_hash()  # of the sources as compiled (an edit during the build leaves it stale)
     if force and os.path.isdir(OBJ_DIR):
         for old in os.listdir(OBJ_DIR):
             os.remove(os.path.join(OBJ_DIR, old))
@@ -133,7 +134,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         raise GwError(f"hipcc link failed ({r.returncode}):\n{r.stderr[-4000:]}")
     os.replace(tmp, LIB_PATH)
     with open(STAMP_PATH, "w") as f:
-        f.write(source_hash())
+        f.write(stamp)
     return LIB_PATH
 
 

@@ -222,22 +222,30 @@ def test_fused_act_layer2_precision(variant, monkeypatch):
     env.close()
 
 
-@pytest.mark.parametrize("E", [4096, 777])
+@pytest.mark.parametrize("E", [4096, 777, 20000])
 def test_fused_act_block_shape_does_not_change_results(E, monkeypatch):
-    """Small env counts launch 4-wave blocks (one wave per SIMD on 4x the CUs) instead of one
-    16-wave block per CU; each wave still evaluates whole 16-env tiles in the same order, so
-    logits, probabilities and actions (Philox noise) are bit for bit those of 16-wave blocks."""
+    """The actor's block shape (4 / 8 / 12 / 16 waves: GW_ACT_WAVES) does not change the results:
+    each wave evaluates whole 16-env tiles, so logits, probabilities and actions (Philox noise)
+    are bit for bit the same, and every launch writes every output (sentinel-filled buffers)."""
     sc = S.builtin("grid32")
     env = VecGridEnv(sc, num_envs=E, fear=False, seed=12)
     actors = _actors(sc, seed=13)
     env.reset()
     env.step()
     out = {}
-    for w in ("4", "16"):
-        monkeypatch.setenv("GW_ACT_WAVES", w)
-        lk = torch.empty((sc.K, E, N_ACTIONS), device="cuda")
-        a, p = actors.act_env(env, env.out["mask"], True, seed=5, counter=9, logits_out=lk)
-        out[w] = (a.clone(), p.clone(), lk)
-    for x, y in zip(out["4"], out["16"]):
-        assert torch.equal(x, y)
+    for sched in ("static",):
+        for w in ("4", "8", "12", "16"):
+            monkeypatch.setenv("GW_ACT_WAVES", w)
+            for rep in range(2):
+                lk = torch.full((sc.K, E, N_ACTIONS), float("nan"), device="cuda")
+                a = torch.full((E, sc.K), -7, dtype=torch.int32, device="cuda")
+                pr = torch.full((sc.K, E, N_ACTIONS), float("nan"), device="cuda")
+                actors.act_env(env, env.out["mask"], True, seed=5, counter=9, logits_out=lk, actions_out=a,
+                               probs_out=pr)
+                assert not torch.isnan(lk).any() and not torch.isnan(pr).any() and bool((a >= 0).all())
+                out[(sched, w, rep)] = (a, pr, lk)
+    ref = out[("static", "16", 0)]
+    for key, v in out.items():
+        for x, y in zip(v, ref):
+            assert torch.equal(x, y), key
     env.close()
