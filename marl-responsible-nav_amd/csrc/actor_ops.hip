@@ -323,7 +323,7 @@ __device__ __forceinline__ Desc load_desc(const ActParams &p, int64_t e, int k) 
 // H1 && PW: the window CNN head (gw_patch_cnn_act): layer 1 = the centre's table row + the
 //     recomputed positions' terms (RSX slots per (env, agent))
 template <int NP, int WAVES, bool BF3 = false, bool H1 = false, bool PW = false, int RSX = RS>  // NP = patch slots per (env, agent) = N + 1
-__global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
+__device__ __forceinline__ void act_body(const ActParams &p) {
     constexpr int THREADS = 64 * WAVES;
     constexpr int NW2 = BF3 ? W2B_U4 : W2IMG / 4;
     __shared__ float4 s_w2[NW2];             // W2 image (w2_slot, 64 KB; BF3: w2b_slot, 96 KB)
@@ -712,6 +712,22 @@ __global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
     }
 }
 
+
+template <int NP, int WAVES, bool BF3 = false, bool H1 = false, bool PW = false, int RSX = RS>
+__global__ void __launch_bounds__(64 * WAVES, 4) act_kernel(ActParams p) {
+    act_body<NP, WAVES, BF3, H1, PW, RSX>(p);
+}
+
+// GW_ACT_WAVES=12|8 (A/B, result-neutral): 12- or 8-wave blocks held to the 16-wave block's 128
+// VGPRs per lane, so that a quarter or half of each SIMD's register file stays free for the
+// kernels beside the actor (the rollout's obs writer).  Left to itself the compiler spends the
+// smaller block's whole budget (8 waves: 243 VGPRs): its LDS allows one block per CU, so it
+// ignores waves-per-EU requests; declaring the 16-wave block size (launched with fewer threads)
+// is what holds the allocation to 128
+template <int NP, int WAVES>
+__global__ void __launch_bounds__(1024) act_kernel_lean(ActParams p) {
+    act_body<NP, WAVES, true>(p);
+}
 
 // ---- the configs/cnn.yaml head (gw_cnn_prepare / gw_cnn_act; include/actor_ops.h) -------------
 // Geometry: conv-2 position P = (Y, X) (P = Y (W/4) + X) sees obs cells (4Y + ry, 4X + rx); the
@@ -1987,9 +2003,9 @@ gw_status actor_act(const char *who, void *env, int32_t P, const gw_mlp_actors *
         else if (v == 4 && small)                                                        \
             gwprof::launch(act_kernel<NP, 4, true>, grid, block, 0, s, p);               \
         else if (v == 4 && waves == 12)                                                  \
-            gwprof::launch(act_kernel<NP, 12, true>, grid, block, 0, s, p);              \
+            gwprof::launch(act_kernel_lean<NP, 12>, grid, block, 0, s, p);               \
         else if (v == 4 && waves == 8)                                                   \
-            gwprof::launch(act_kernel<NP, 8, true>, grid, block, 0, s, p);               \
+            gwprof::launch(act_kernel_lean<NP, 8>, grid, block, 0, s, p);                \
         else if (v == 4)                                                                 \
             gwprof::launch(act_kernel<NP, 16, true>, grid, block, 0, s, p);              \
         else                                                                             \
