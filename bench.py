@@ -104,8 +104,8 @@ HID, N_ACT = 128, 9        # the fused actors' hidden width and actions (configs
 
 def kernel_work(kind: int, N: int, K: int, HW: int, E: int, obs_bytes: int = 4, patch: int = 0, valu=None):
     """(bound, algorithmic work per step of one GW_SPAN kind, unit) for the roofline:
-    HBM bytes for the env / writer kernels (DESIGN.md §4, §5.10), f32 MFMA flops for the fused
-    actors' MLP kernel (DESIGN.md §5.4: layers 2-3, 2 * (128 * 128 + 128 * 9) per (env, agent);
+    HBM bytes for the env / writer kernels (DESIGN.md §4, §5.6), f32 MFMA flops for the fused
+    actors' MLP kernel (DESIGN.md §5.5: layers 2-3, 2 * (128 * 128 + 128 * 9) per (env, agent);
     its layer 1 is a gather of table rows, not a GEMM).  None where the work is data-dependent
     (the CNN recompute: a few positions per step)."""
     step_b, obs_b = algorithmic_bytes(N, K, HW, obs_bytes)
@@ -127,7 +127,7 @@ def kernel_work(kind: int, N: int, K: int, HW: int, E: int, obs_bytes: int = 4, 
         return "hbm", (48 + 4 * K) * E, "B"
     if kind == 7:  # the windows written (f32) + the 48-byte descriptors read
         return "hbm", (4 * K * patch * patch + 48) * E, "B"
-    if kind == 8:  # one descriptor-learner update (DESIGN §5.11b): its 128 x 128 layers on f32 MFMA --
+    if kind == 8:  # one descriptor-learner update (DESIGN §5.8): its 128 x 128 layers on f32 MFMA --
         # critic tail: K target actors + target critic + critic forward + critic backward, actor
         # tail: actor / critic forward, critic / actor backward, and the two W2 gradients, per agent
         # and row: (4 + 4 + 2) K B (2 * 128 * 128) flops with B = 128 (layer 1 is a table gather)
@@ -608,7 +608,7 @@ def main():
         avg_fear_ms = ms_fear / max(nprof, 1)
         # busy time per launch: the union of the launches' intervals / launches.  Equal to the
         # mean launch duration when launches do not overlap; with the obs writers of consecutive
-        # steps overlapping on two streams (DESIGN §5.8) a launch's own span covers part of its
+        # steps overlapping on two streams (DESIGN §5.4) a launch's own span covers part of its
         # neighbours' work, and the busy time is what a launch costs the timeline
         busy = {k: busy_ms(spans, k) if spans is not None and len(spans) else (0.0, 0) for k in SPAN_KINDS}
         busy_step_ms, busy_obs_ms = (busy[k][0] / max(busy[k][1], 1) for k in (0, 1))
@@ -750,7 +750,7 @@ def main():
                          # per step: what the pipelined steps sustain end to end
                          "step_level_GBps": (step_b + obs_b) * E / (t_max / args.steps) / 1e9,
                          # with an obs ring the writers of consecutive steps overlap on two streams
-                         # (DESIGN §5.8), so a launch's duration spans two writers' shared bandwidth:
+                         # (DESIGN §5.4), so a launch's duration spans two writers' shared bandwidth:
                          # the dominant kernel's bytes per launch over the launch PERIOD (= the
                          # stream time per step) is its sustained rate
                          "writers_overlap": n_ring > 1 and bool(obs_mode) and env.kernel_path == "defer",
@@ -774,7 +774,7 @@ def main():
             "return_gather": gathered,
             # FeAR's integer work: the counterfactual world updates the FeAR kernels ran
             # per step (gw_count_sims over the profiled steps, after the exact de-duplication of
-            # DESIGN §5) and the reference's nominal K (N - 1) 18 per env-step, per second at the
+            # DESIGN §5.2) and the reference's nominal K (N - 1) 18 per env-step, per second at the
             # timed step time, all ranks
             "fear_sims": None if sims is None else {
                 "per_step": sims, "per_s": world * sims / (t_max / args.steps),

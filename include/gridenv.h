@@ -231,7 +231,7 @@ gw_status gw_obs_view(void *env, gw_obs_source *out);
 gw_status gw_obs_desc_copy(void *env, uint32_t *dst, void *stream);
 
 /* Count the FeAR counterfactual world updates (custom/Responsibility.py:16-54's sims, after the
- * exact de-duplication of DESIGN §5: one base sim per (actor, variant) and the 8 other actions of
+ * exact de-duplication of DESIGN §5.2: one base sim per (actor, variant) and the 8 other actions of
  * each close affected agent per variant) the env's FeAR kernels run from now on: every block adds
  * its task count to *counter (device uint64, one atomic per block per step).  counter NULL: stop
  * counting (the default).  bench.py reports sims/s from it beside the VALU roofline. */

@@ -1,4 +1,4 @@
-// window_rows.h -- the row window writer's block (gw_obs_patch MODE 6, DESIGN §5.10), shared by
+// window_rows.h -- the row window writer's block (gw_obs_patch MODE 6, DESIGN §5.6), shared by
 // patch_ops.hip (its own launch) and actor_ops.hip (the same blocks in the launch that also lists
 // the window CNN head's recomputed positions).  One thread per window ROW of the [K][E][P*P] layout;
 // a wave's 64 rows leave as one contiguous run of consecutive nontemporal 16-byte stores.
