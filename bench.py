@@ -61,13 +61,15 @@ CONFIGS = {
                              "reference format, reported separately): no dense obs, the MADDPG MLP actors on "
                              "121 inputs (fused gw_patch_actor_act), patch replay ring, FeAR on"),
     "c4patch": dict(scenario="grid64_n8", envs=65536, fear=False, fear_weight=-5.0, rollout=True, arch="cnn", patch=16,
-                    workload="BASELINE config 4's CNN head (configs/cnn.yaml: conv 32-64 k2 s2, 128-128, f32) on "
+                    workload="BASELINE config 4's CNN head (configs/cnn.yaml: conv 32-64 k2 s2, 128-128; f32 weights, layer 2 "
+                             "as bf16x3 MFMA products) on "
                              "egocentric 16x16 local windows (gw_obs_patch; not a reference format, reported "
                              "separately): 8-agent 64x64 grid, 65536 envs, no dense obs, the fused CNN head "
                              "(gw_patch_cnn_act: per-centre tables + recomputed positions), patch replay ring"),
     "c4cnn": dict(scenario="grid64_n8", envs=65536, fear=False, fear_weight=-5.0, rollout=True, arch="cnn",
                   workload="BASELINE config 4 as a rollout: 8-agent 64x64 grid, 65536 envs, the configs/cnn.yaml "
-                           "actor head (conv 32-64, k2 s2, 128-128, f32; fused gw_cnn_act from the obs "
+                           "actor head (conv 32-64, k2 s2, 128-128; f32 weights, layer 2 as bf16x3 MFMA products; fused "
+                           "gw_cnn_act from the obs "
                            "descriptors), env step, replay ring"),
 }
 
@@ -100,6 +102,11 @@ VALU_PEAK_GIPS = 256 * 4 * 2.4e9 / 2 / 1e9
 VALU_PEAK_BASIS = ("256 CUs x 4 SIMD-32 x 2.4 GHz / 2 cycles per wave64 VALU instruction (MI355X_MICROARCH.md "
                    "'Execution model'); at 1 wave64 per CU per clock the fractions would double")
 HID, N_ACT = 128, 9        # the fused actors' hidden width and actions (configs/mlp.yaml, configs/cnn.yaml)
+# what the fused actors compute in: f32 weights and activations, layer 2 as bf16x3 products
+# (hi / mid / lo bf16 parts, the 6 largest of the 9 part products on v_mfma_f32_16x16x32_bf16, f32
+# accumulation: ~2^-23 relative per product), layer 3 on f32 MFMA; their roofline counts the f32-equivalent
+# flops against the f32 MFMA peak
+ACT_PRECISION = "f32 weights; layer 2 as bf16x3 MFMA products (f32-equivalent flops vs the f32 MFMA peak); layer 3 f32 MFMA"
 
 
 def kernel_work(kind: int, N: int, K: int, HW: int, E: int, obs_bytes: int = 4, patch: int = 0, valu=None):
@@ -642,6 +649,7 @@ def main():
             peak = {"mfma": F32_MFMA_PEAK_TFS * 1e3, "valu": VALU_PEAK_GIPS}.get(bound, HBM_PEAK_GBS)
             rate = work / (ms * 1e-3) / 1e9 if (work and ms > 0) else None  # GB/s, GFLOP/s or G inst/s
             per_kind[name] = {"busy_ms_per_step": ms, "launches_per_step": n / max(nprof, 1), "bound": bound,
+                              **({"precision": ACT_PRECISION} if k == 3 else {}),
                               "work_per_step": work, "work_unit": unit,
                               "achieved": rate / 1e3 if (rate and bound == "mfma") else rate,
                               "achieved_unit": {"mfma": "TFLOP/s", "valu": "G inst/s"}.get(bound, "GB/s"),
@@ -784,6 +792,8 @@ def main():
                 "unit": "world updates (custom/Responsibility.py:16-54 UpdateGWorld counterfactuals)"},
         }
         rf = line["roofline"]
+        if dom == "act_kernel":
+            rf["precision"] = ACT_PRECISION
         if dom_bound == "valu" and dom in per_kind and per_kind[dom].get("achieved"):
             # an integer-VALU kernel leads (c5patch: FeAR with the windows in its launch): its
             # instruction rate against the VALU issue peak, as in roofline.kernels
