@@ -622,12 +622,15 @@ def main():
         fused = env.fused
         merged = env.kernel_path == "merged" and bool(obs_mode)
         obs_bytes = 2 if args.obs_dtype == "bf16" else 4
+        # the committed rocprofv3 evidence of this workload: profiles/latest.json["configs"][prof_key]
+        # (C5 with n MADDPG updates per env step: "c5u<n>")
+        prof_key = args.config + (f"u{args.updates_per_step}" if args.updates_per_step else "")
         # the VALU instructions per step of the integer-VALU kernels (world update, FeAR) from the
         # committed rocprofv3 SQ_INSTS_VALU pass of this config (tools/gpu_profile.sh)
         valu = {}
         try:
             with open(os.path.join(REPO, "profiles", "latest.json")) as f:
-                pk = json.load(f).get("configs", {}).get(args.config, {}).get("kernels", {})
+                pk = json.load(f).get("configs", {}).get(prof_key, {}).get("kernels", {})
             if not args.envs and args.fear < 0 and args.obs_dtype == "f32":
                 for kd, nm in ((0, "step_kernel"), (2, "fear_kernel")):
                     v = pk.get(nm, {}).get("valu_insts_per_step")
@@ -694,7 +697,7 @@ def main():
         try:  # HBM bytes measured by the PMC passes committed under profiles/ for this workload
             with open(os.path.join(REPO, "profiles", "latest.json")) as f:
                 prof = json.load(f)
-            pc = prof.get("configs", {}).get(args.config)
+            pc = prof.get("configs", {}).get(prof_key)
             if pc and not args.envs and args.fear < 0 and not fused and dom in pc["kernels"] \
                     and args.obs_dtype == "f32":
                 pk = pc["kernels"][dom]
