@@ -861,15 +861,17 @@ __device__ __forceinline__ float agent_value(bool reset, int n, int k, bool on_a
 // bf16, so the compact format is lossless (the low 16 bits of the f32 are zero)
 __device__ __forceinline__ uint32_t bf16_bits(float v) { return __float_as_uint(v) >> 16; }
 
-// The f32 writer's patch tables (round 6).  Per (which, env, agent) the float4s
-// its <= N + 1 patches touch are built ONCE in LDS (the map float4 with every patch of that float4
+// The f32 writer's patch tables (round 6).  Per (env, agent) the float4s its
+// <= N + 1 patches touch are built ONCE in LDS (the map float4 with every patch of that float4
 // applied in slot order) and a byte per float4 of the obs names its entry (0 = map only), so a
 // 16-byte store costs one byte lookup instead of N + 1 compares and selects.  Used where the byte
-// tables fit (obs_tab_bytes <= OBS_TAB_MAX); else the compare loop.
+// tables fit (obs_tab_bytes <= OBS_TAB_MAX); else the compare loop.  The terminal obs of the few
+// envs that ended (final_obs) keep the compare loop: tables for them would double the block's LDS,
+// which decides whether the rollout's large-LDS kernels (the learner's tails) fit beside writer blocks.
 constexpr int OBS_TAB_MAX = 16384;
 __host__ __device__ __forceinline__ int obs_tab_stride(int HW) { return ((HW >> 2) + 15) & ~15; }
 __host__ __device__ __forceinline__ int obs_tab_bytes(int HW, int obs_be, int K) {
-    return 2 * obs_be * K * obs_tab_stride(HW);
+    return obs_be * K * obs_tab_stride(HW);
 }
 __host__ __device__ __forceinline__ bool obs_tab_ok(int HW, int obs_be, int K) {
     return HW % 4 == 0 && obs_tab_bytes(HW, obs_be, K) <= OBS_TAB_MAX;
@@ -902,15 +904,15 @@ __device__ __forceinline__ void obs_store_cols(const Params &p, float *__restric
         float4 mapv[J];
 #pragma unroll
         for (int j = 0; j < J; ++j) mapv[j] = map4(j * T + tid);
-        for (int which = 0; which < 2; ++which) {
-            float *dst = which == 0 ? obs : final_obs;
-            if (!dst) continue;
-            const uint32_t need = which == 0 ? D_WRITE : D_FINAL;
+        {
+            float *dst = obs;
+            if (!dst) return;
+            const uint32_t need = D_WRITE;
             for (int k = 0; k < K; ++k) {
                 float4 *out4 = reinterpret_cast<float4 *>(dst + ((int64_t)k * p.E + e0) * HW);
                 for (int el = 0; el < nenv; ++el) {
                     if (!(s_flag[el] & need)) continue;
-                    const int own = (which * p.obs_be + el) * K + k;
+                    const int own = el * K + k;
                     const uint8_t *tb = s_tab + own * tstride;
                     const float4 *ent = s_ent + own * npatch - 1;
 #pragma unroll
@@ -936,17 +938,17 @@ __device__ __forceinline__ void obs_store_cols(const Params &p, float *__restric
         }
     } else {
         const int total4 = nenv * HW4;
-        for (int which = 0; which < 2; ++which) {
-            float *dst = which == 0 ? obs : final_obs;
-            if (!dst) continue;
-            const uint32_t need = which == 0 ? D_WRITE : D_FINAL;
+        {
+            float *dst = obs;
+            if (!dst) return;
+            const uint32_t need = D_WRITE;
             for (int k = 0; k < K; ++k) {
                 float4 *out4 = reinterpret_cast<float4 *>(dst + ((int64_t)k * p.E + e0) * HW);
                 for (int i4 = tid; i4 < total4; i4 += T) {
                     const int el = HW4 == 1 ? i4 : (int)__umulhi((uint32_t)i4, p.hw4_magic);
                     if (!(s_flag[el] & need)) continue;
                     const int c4 = i4 - el * HW4;
-                    const int own = (which * p.obs_be + el) * K + k;
+                    const int own = el * K + k;
                     const int en = s_tab[own * tstride + c4];
                     const float4 ev = s_ent[own * npatch + en - 1], mv = map4(c4);  // value select, as above
                     float4 v;
@@ -1015,22 +1017,22 @@ __device__ __forceinline__ void obs_block(const Params &p, float *__restrict__ o
     if (tid < OBS_BE && tid >= nenv) s_flag[tid] = 0;
     const bool tab = VEC4 && !BF16 && obs_tab_ok(HW, p.obs_be, K);
     float4 *s_ent = reinterpret_cast<float4 *>(reinterpret_cast<uint8_t *>(obs_lds) + obs_ent_off(HW, p.obs_be, K, npatch));
-    uint8_t *s_tab = reinterpret_cast<uint8_t *>(s_ent + 2 * p.obs_be * K * npatch);
+    uint8_t *s_tab = reinterpret_cast<uint8_t *>(s_ent + p.obs_be * K * npatch);
     const int tstride = obs_tab_stride(HW);
     if (tab) {  // zero the byte tables (16 B per thread and pass)
         const int n16 = obs_tab_bytes(HW, p.obs_be, K) >> 4;
         for (int i = tid; i < n16; i += T) reinterpret_cast<uint4 *>(s_tab)[i] = make_uint4(0, 0, 0, 0);
     }
     __syncthreads();
-    for (int t = tid; tab && t < 2 * p.obs_be * K * npatch; t += T) {
-        // one thread per patch slot q of (which, env, agent): the first slot touching a float4
-        // builds its entry (the map float4 with every slot of that float4 applied in slot order:
-        // a later slot overrides, the obs writer's rule) and names it in the byte table
+    for (int t = tid; tab && t < p.obs_be * K * npatch; t += T) {
+        // one thread per patch slot q of (env, agent) of the step obs: the first slot touching a
+        // float4 builds its entry (the map float4 with every slot of that float4 applied in slot
+        // order: a later slot overrides, the obs writer's rule) and names it in the byte table
         const int own = t / npatch, q = t - own * npatch;
-        const int which = own / (p.obs_be * K), el = (own / K) % p.obs_be, k = own % K;
-        const int slot = own * npatch;  // == ((which * obs_be + el) * K + k) * npatch
+        const int el = own / K;
+        const int slot = own * npatch;  // == ((0 * obs_be + el) * K + k) * npatch: the step obs' slots
         const int c = s_pc[slot + q];
-        if (el < nenv && (s_flag[el] & (which == 0 ? D_WRITE : D_FINAL)) && c >= 0 && c < HW) {
+        if (el < nenv && (s_flag[el] & D_WRITE) && c >= 0 && c < HW) {
             bool first = true;
             for (int q2 = 0; q2 < q; ++q2) {
                 const int c2 = s_pc[slot + q2];
@@ -1071,10 +1073,11 @@ __device__ __forceinline__ void obs_block(const Params &p, float *__restrict__ o
             obs_store_cols<T, 4, NT>(p, obs, final_obs, e0, nenv, npatch, tstride, s_road, s_flag, s_ent, s_tab);
         else
             obs_store_cols<T, 0, NT>(p, obs, final_obs, e0, nenv, npatch, tstride, s_road, s_flag, s_ent, s_tab);
-        return;
     }
 
-    for (int which = 0; which < 2; ++which) {
+    // the terminal obs with the tables (the step obs without them, every obs of the bf16 / odd-HW
+    // formats): per float4 the N + 1 patch compares
+    for (int which = tab ? 1 : 0; which < 2; ++which) {
         float *dst = which == 0 ? obs : final_obs;
         if (!dst) continue;
         const uint32_t need = which == 0 ? D_WRITE : D_FINAL;
@@ -2460,7 +2463,7 @@ size_t obs_lds_bytes(const Env *env) {
                         (size_t)2 * 2 * env->obs_be * env->K * (env->N + 1) * sizeof(uint32_t);
     if (env->obs_bf16 || !gw::obs_tab_ok(env->HW, env->obs_be, env->K)) return base;
     return (size_t)gw::obs_ent_off(env->HW, env->obs_be, env->K, env->N + 1) +
-           (size_t)2 * env->obs_be * env->K * (env->N + 1) * sizeof(float4) +
+           (size_t)env->obs_be * env->K * (env->N + 1) * sizeof(float4) +
            (size_t)gw::obs_tab_bytes(env->HW, env->obs_be, env->K);
 }
 
