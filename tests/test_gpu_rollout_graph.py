@@ -10,7 +10,7 @@ device step count).
    ring-phase graph replayed (graph 0 twice: the cycle closes) and eager steps after them.
 2. The eager rollout == the C oracle fed the actions the actor chose (``vec_step(rl_act=...)``):
    every step's shaped rewards (the ring's reward slots), terminations and dones for all 4,096
-   envs, and the observations in the ring at the end.
+   envs, and the observations of every ring slot written in the last SLOTS steps.
 """
 import numpy as np
 import pytest
@@ -101,9 +101,15 @@ def test_eager_rollout_matches_oracle(runs):
     reward = a["reward"].cpu().numpy()
     term = a["term"].cpu().numpy()
     done = a["done"].cpu().numpy()
+    fin = a["final_obs"].cpu().numpy().reshape(SLOTS, K, E, -1)
     for t, act in acts:
-        orc.vec_step(act.cpu().numpy(), obs=obs, outs=outs, nthreads=16)
+        fobs = np.zeros_like(obs)
+        orc.vec_step(act.cpu().numpy(), obs=obs, final_obs=fobs, outs=outs, nthreads=16)
         slot = t % SLOTS
+        if t >= T - SLOTS:  # obs_{t+1} in slot t + 1 (written by the next step_obs or the fence)
+            np.testing.assert_array_equal(ring_obs[(t + 1) % SLOTS], obs, err_msg=f"ring obs after step {t}")
+            dn = np.array([outs[e].done for e in range(E)], bool)
+            np.testing.assert_array_equal(fin[slot][:, dn], fobs[:, dn], err_msg=f"terminal obs of step {t}")
         if t >= T - SLOTS + 1:  # the ring slots not overwritten since
             o = [outs[e] for e in range(E)]
             np.testing.assert_array_equal(reward[slot], np.array([list(x.shaped)[:K] for x in o]),
