@@ -279,6 +279,13 @@ gw_status gw_set_obs_async(void *env, int enable);
  * size the stats buffer after it. */
 enum { GW_OBS_F32 = 0, GW_OBS_BF16 = 1 };
 gw_status gw_set_obs_dtype(void *env, int dtype);
+
+/* The FeAR kernel's envs per block, before the first gw_reset (it fixes gw_stats_rows: size the
+ * stats buffer after it): wide = 1 (the default: half the resident waves, best beside the full-obs
+ * writer), 0 = narrow (twice the waves, best where FeAR is on the critical path: an env that writes
+ * no full obs, e.g. the local-window rollouts; c5patch 115 -> 111-112 us per step).
+ * GW_FEAR_BE=wide|narrow in the environment overrides it.  GW_ERR_STATE after gw_reset. */
+gw_status gw_set_fear_blocks(void *env, int wide);
 gw_status gw_obs_fence(void *env, void *stream);
 gw_status gw_fear_fence(void *env, void *stream);
 /* Set the thread-local error text returned by gw_last_error (for the library's other

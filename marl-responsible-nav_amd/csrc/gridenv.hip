@@ -2988,6 +2988,14 @@ gw_status gw_set_obs_dtype(void *handle, int dtype) {
     return GW_OK;
 }
 
+gw_status gw_set_fear_blocks(void *handle, int wide) {
+    Env *env = static_cast<Env *>(handle);
+    if (!env) return fail(GW_ERR_ARG, "null env");
+    if (env->initialized) return fail(GW_ERR_STATE, "gw_set_fear_blocks after gw_reset (the stats rows follow it)");
+    if (!env->fear_wide_fixed) env->fear_wide = wide != 0;
+    return GW_OK;
+}
+
 gw_status gw_fear_fence(void *handle, void *stream) {
     Env *env = static_cast<Env *>(handle);
     if (!env) return fail(GW_ERR_ARG, "null env");

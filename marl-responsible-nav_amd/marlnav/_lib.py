@@ -174,7 +174,7 @@ EXPORTS = ["gw_create", "gw_reset", "gw_step", "gw_state_view", "gw_copy_state",
            "gw_profile_read", "gw_stats_rows", "gw_dims", "gw_last_error", "gw_destroy", "gw_fear_matrix",
            "gw_adam_step", "gw_soft_update", "gw_obs_view", "gw_set_last_error", "gw_actor_act",
            "gw_actor_workspace_floats", "gw_actor_prepare", "gw_rollout_tick", "gw_set_obs_async",
-           "gw_obs_fence", "gw_fear_fence", "gw_set_obs_dtype", "gw_cnn_workspace_floats", "gw_cnn_prepare",
+           "gw_obs_fence", "gw_fear_fence", "gw_set_obs_dtype", "gw_set_fear_blocks", "gw_cnn_workspace_floats", "gw_cnn_prepare",
            "gw_cnn_act", "gw_return_compact", "gw_return_compact_scratch", "gw_kernel_path", "gw_graph_replayed", "gw_obs_patch", "gw_step_patch_next",
            "gw_ln_relu_fwd", "gw_ln_relu_bwd", "gw_gumbel_softmax",
            "gw_replay_gather", "gw_affine_relu_fwd", "gw_affine_relu_bwd",
@@ -389,6 +389,8 @@ def _declare(L):
     L.gw_fear_fence.restype = C.c_int
     L.gw_set_obs_dtype.argtypes = [p, C.c_int]
     L.gw_set_obs_dtype.restype = C.c_int
+    L.gw_set_fear_blocks.argtypes = [p, C.c_int]
+    L.gw_set_fear_blocks.restype = C.c_int
     L.gw_destroy.argtypes = [p]
     L.gw_destroy.restype = None
     return L

@@ -118,6 +118,10 @@ class VecGridEnv:
         self.obs_dtype = obs_dtype
         if obs_dtype == torch.bfloat16:  # lossless: every obs value is exact in bf16
             _lib.check(self.lib.gw_set_obs_dtype(self.handle, 1), "gw_set_obs_dtype")
+        if not obs and self.fear_enabled:
+            # no full-obs writer to overlap: FeAR is on the step's critical path, where twice the
+            # resident waves (32-env blocks) are faster (the local-window rollouts, profiles/r6_ab)
+            _lib.check(self.lib.gw_set_fear_blocks(self.handle, 0), "gw_set_fear_blocks")
 
         dev, E, K, N = self.device, self.E, self.K, self.N
         f64 = dict(dtype=torch.float64, device=dev)
