@@ -12,7 +12,7 @@ O=$C/build_ab/$REV$TAG
 mkdir -p $O
 if [ "$REV" = wt ]; then cp $C/gridenv.hip $O/gridenv.hip
 else git -C $R show $REV:marl-responsible-nav_amd/csrc/gridenv.hip > $O/gridenv.hip; fi
-cp $C/patch_ops.h $O/
+cp $C/*.h $O/
 F="-O3 --offload-arch=gfx950 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -I$R/include"
 /opt/rocm/bin/hipcc $F $XF -c $O/gridenv.hip -o $O/gridenv.o
 objs=""
